@@ -1,0 +1,201 @@
+#!/usr/bin/env python3
+"""Headline benchmark: msgs/sec (whole node) + p50 publish->deliver latency, 1 KB payload.
+
+Workload = BASELINE.json config 2 per GPU ("1 topic exchange, 16 bound queues, 1 KB msgs,
+auto-ack"), weak-scaled: every rank is one MI355X broker shard with its own producers,
+its own 16 queues and their consumers.  Producers are synthetic AMQP connections whose
+wire bytes (Basic.Publish method + content header + 1 KB body frame) are pre-rendered
+into a pinned ingress pool and handed to the data plane in TCP-read-sized chunks that
+split frames at arbitrary offsets.  One timed step = the full broker hot path on the
+GPU: H2D of the step's ingress bytes, frame scan, command assembly, publish decode,
+topic routing (MFMA prefilter + exact matcher), message store, queue enqueue, dequeue
+to consumers, delivery tags, Basic.Deliver rendering into host-mapped egress memory,
+auto-ack release — nothing skipped.
+
+python bench.py [--gpus N --steps K --warmup W]   (N>1: launched by torch.distributed.run)
+"""
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+METRIC = "msgs/sec (whole node) + p50 publish→deliver latency, 1 KB payload, 1/2/4/8 GPUs"
+
+
+def build_workload(dp, rank, producers, queues, body, chunk, blocks, cons_base):
+    from chanamq_amd.engine.layout import SEG_IN
+    from chanamq_amd.engine.traffic import even_split, publish_stream
+
+    vh = "AMQ.DEFAULT"
+    dp.declare_exchange(vh, "bench.topic", "topic")
+    for i in range(queues):
+        qn = f"bench.q.{rank}.{i}"
+        dp.declare_queue(vh, qn, capacity=1 << 20)
+        dp.bind(vh, qn, "bench.topic", f"bench.{i}.*")
+    for p in range(producers):
+        dp.open_connection(p, vh)
+        dp.open_channel(p, 1)
+    for i in range(queues):
+        c = cons_base + i
+        dp.open_connection(c, vh)
+        dp.open_channel(c, 1)
+        dp.consume(c, 1, vh, f"bench.q.{rank}.{i}", f"ctag-{i}", no_ack=True)
+    # one message on the wire is ~1.08 KB; each producer gets `blocks` chunks of ~chunk bytes
+    probe = publish_stream(1, "bench.topic", lambda i: "bench.0.x0", body)
+    per_prod = max(1, (chunk * blocks) // len(probe))
+    streams = []
+    for p in range(producers):
+        rng_q = np.random.default_rng(1000 + rank * 7919 + p).integers(0, queues, size=per_prod)
+        s = publish_stream(per_prod, "bench.topic", lambda i, r=rng_q: f"bench.{r[i]}.x{i % 10}", body,
+                           seed=p)
+        streams.append(even_split(s, blocks))
+    # block-major pinned pool: block b = chunk b of every producer, 16-B aligned
+    sizes = [[len(streams[p][b]) for p in range(producers)] for b in range(blocks)]
+    block_len = [sum((n + 15) & ~15 for n in row) for row in sizes]
+    total = sum(block_len)
+    pool = dp.mod.alloc_pinned(total + 64)
+    segs, offs = [], []
+    off = 0
+    for b in range(blocks):
+        offs.append(off)
+        sg = np.zeros(producers, SEG_IN)
+        rel = 0
+        for p in range(producers):
+            data = streams[p][b]
+            pool[off + rel:off + rel + len(data)] = np.frombuffer(data, np.uint8)
+            sg[p] = (p, len(data), rel)
+            rel += (len(data) + 15) & ~15
+        segs.append(sg)
+        off += block_len[b]
+    msgs_per_step = per_prod * producers / blocks
+    return pool, segs, offs, block_len, msgs_per_step, len(probe)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--producers", type=int, default=256)
+    ap.add_argument("--queues", type=int, default=16)
+    ap.add_argument("--body", type=int, default=1024)
+    ap.add_argument("--chunk", type=int, default=65536, help="bytes per producer per step (TCP read)")
+    ap.add_argument("--blocks", type=int, default=8)
+    ap.add_argument("--no-graph", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    from chanamq_amd.engine.dataplane import GpuDataPlane
+
+    P, Q = args.producers, args.queues
+    cfg = dict(c_max=max(1024, P + Q + 1), chpc=4, q_max=max(64, Q * 2), cons_max=1024, seg_max=max(1024, P + Q),
+               cmd_max=1 << 17, deliv_max=1 << 16, msg_max=1 << 22, ucap=4096, deliver_cap=8192,
+               ingress_cap=max(64 << 20, 2 * P * args.chunk), egress_cap=128 << 20,
+               log_bytes=16 << 30, ring_pool=Q * 2 * (1 << 20), tb_max=64, carry_cap=256 << 10,
+               graph=0 if args.no_graph else 1)
+    dp = GpuDataPlane(device=local, worker=rank, **cfg)
+    pool, segs, offs, blens, mps, msg_bytes = build_workload(dp, rank, P, Q, args.body, args.chunk,
+                                                             args.blocks, cons_base=P)
+    base = pool.ctypes.data
+    step_i = 0
+
+    def run(n, collect=False):
+        nonlocal step_i
+        dl = pb = 0
+        hist = np.zeros(32, np.int64)
+        eg = 0
+        for _ in range(n):
+            b = step_i % args.blocks
+            r = dp.step_raw(segs[b], base + offs[b], blens[b], collect=False)
+            c = r.counters
+            dl += c["n_deliv"]
+            pb += c["n_pubs"]
+            eg += c["egress_bytes"]
+            hist += np.array(c["lat_hist"], np.int64)
+            step_i += 1
+        return dl, pb, hist, eg
+
+    run(args.warmup)
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    dp.eng.sync(dp.stream)
+    t0 = time.perf_counter()
+    dl, pb, hist, eg = run(args.steps)
+    dp.eng.sync(dp.stream)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    t = time.perf_counter() - t0
+    c = dp.eng.counters()
+    errs = {k: c[k] for k in ("n_dropped_nomem", "n_ring_full", "n_unknown_exchange") if c[k]}
+
+    vals = np.array([t, dl, pb, eg], np.float64)
+    if dist:
+        tt = torch.tensor([t], dtype=torch.float64, device="cuda")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        ss = torch.tensor(vals[1:], dtype=torch.float64, device="cuda")
+        dist.all_reduce(ss, op=dist.ReduceOp.SUM)
+        hh = torch.tensor(hist, dtype=torch.float64, device="cuda")
+        dist.all_reduce(hh, op=dist.ReduceOp.SUM)
+        t = float(tt.item())
+        dl, pb, eg = (float(x) for x in ss.tolist())
+        hist = hh.cpu().numpy()
+    ms_step = 1000.0 * t / args.steps
+    # p50: deliveries by (deliver step - publish step); a message delivered k steps after
+    # its publish step waited (k+1) step periods from ingress submit to egress ready
+    cum = np.cumsum(hist)
+    p50_bin = int(np.searchsorted(cum, cum[-1] / 2.0)) if cum[-1] else 0
+    p50_ms = (p50_bin + 1) * ms_step
+    if rank == 0:
+        out = {
+            "metric": METRIC,
+            "value": dl / t,
+            "unit": "msgs/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": ms_step,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "uint8 (AMQP wire bytes; no floating-point compute)",
+            "data": "synthetic AMQP 0-9-1 publish traffic (random 1 KB bodies), empty-init broker state",
+            "config": {
+                "model": f"BASELINE config 2: 1 topic exchange, {Q} bound queues per GPU, {args.body} B msgs, "
+                         "auto-ack, non-persistent",
+                "global_batch": int(round(mps * world)),
+                "seq_len": args.body,
+                "parallelism": f"queue-sharded x{world} (one broker shard per GPU)",
+                "producers_per_gpu": P,
+                "consumers_per_gpu": Q,
+                "bytes_per_msg_on_wire": msg_bytes,
+            },
+            "p50_latency_ms": p50_ms,
+            "published_msgs_per_s": pb / t,
+            "egress_GBps": eg / t / 1e9,
+            "latency_note": "in-broker publish->deliver (ingress submit to egress bytes ready), no TCP",
+            "errors": errs,
+        }
+        print(json.dumps(out))
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

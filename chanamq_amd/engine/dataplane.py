@@ -1,0 +1,344 @@
+"""GPU data plane: host control tables -> device tables, and the per-step driver.
+
+``GpuDataPlane`` owns one ``_dataplane.Engine`` (HIP, gfx950).  Control-plane ops
+(declare/bind/consume/qos/...) mutate ``ControlState`` and push the affected device
+tables between steps; ``step()`` hands the step's ingress bytes to the captured
+hipGraph and returns per-connection egress bytes plus the control commands the
+device routed back to the host.
+"""
+
+import time
+from collections import defaultdict
+
+import numpy as np
+
+from .. import ops
+from ..protocol import constants as C
+from .control import ControlError, ControlState
+from .layout import (CONN_OUT, CTRL_REC, INVALID, SEG_IN, SEG_OUT, SS_CTRL, chan_hash,
+                     direct_key, exch_hash, fnv1a64, topic_pattern_row)
+
+ONES64 = np.uint64((1 << 64) - 1)
+
+
+class StepResult:
+    __slots__ = ("egress", "ctrl", "events", "segs", "counters", "elapsed")
+
+    def __init__(self):
+        self.egress = {}      # conn -> bytes
+        self.ctrl = []        # (conn, raw frame bytes of one control command)
+        self.events = []      # (conn, code, chslot)
+        self.segs = []        # (conn, status, consumed, carry, ncmds, err_off)
+        self.counters = {}
+        self.elapsed = 0.0
+
+
+class GpuDataPlane(ControlState):
+    def __init__(self, device=0, hash_wildcard=True, graph=True, worker=0, **cfg):
+        self.mod = ops.load()
+        full = dict(cfg)
+        full.update(device=device, hash_wildcard=int(hash_wildcard), graph=int(graph))
+        self.eng = self.mod.Engine(full)
+        self.info = self.eng.info()
+        sz = self.info["sizeof"]
+        assert sz["SegIn"] == SEG_IN.itemsize and sz["SegOut"] == SEG_OUT.itemsize
+        assert sz["CtrlRec"] == CTRL_REC.itemsize and sz["ConnOut"] == CONN_OUT.itemsize
+        self.device = device
+        self.worker = worker
+        self.stream = self.mod.create_stream(device)
+        self.step_no = 0
+        self.carry = defaultdict(int)
+        i = self.info
+        self._seg_out = self.eng.host_view("seg_out").view(SEG_OUT)
+        self._ctrl_rec = self.eng.host_view("ctrl_rec").view(CTRL_REC)
+        self._conn_out = self.eng.host_view("conn_out").view(CONN_OUT)
+        self._egress = self.eng.host_view("egress")
+        self._ctrl = self.eng.host_view("ctrl")
+        self._pin = None
+        self.requeue_pending = False
+        super().__init__(c_max=i["c_max"], chpc=i["chpc"], q_max=i["q_max"], x_max=i["x_max"],
+                         cons_max=i["cons_max"], hash_wildcard=hash_wildcard, ring_pool=i["ring_pool"])
+
+    # ================================================================== uploads
+    def _up(self, name, arr, index=0):
+        a = np.ascontiguousarray(arr)
+        self.eng.upload(name, a, index * a.itemsize if a.ndim else index * a.itemsize)
+
+    def _up_at(self, name, value, index, dtype):
+        a = np.array([value], dtype=dtype)
+        self.eng.upload(name, a, index * a.itemsize)
+
+    def routing_changed(self):
+        i = self.info
+        xh = i["xhash"]
+        x_hkey = np.zeros(xh, np.uint64)
+        x_hval = np.full(xh, -1, np.int32)
+        x_type = np.zeros(self.x_max, np.uint32)
+        x_fan_off = np.zeros(self.x_max, np.uint32)
+        x_fan_n = np.zeros(self.x_max, np.uint32)
+        x_t_off = np.zeros(self.x_max, np.uint32)
+        x_t_n = np.zeros(self.x_max, np.uint32)
+        fan_q, d_q = [], []
+        kpool = bytearray()
+        dh = i["dhash"]
+        d_key = np.zeros(dh, np.uint64)
+        d_exch = np.full(dh, -1, np.int32)
+        d_kb_off = np.zeros(dh, np.uint32)
+        d_kb_len = np.zeros(dh, np.uint32)
+        d_q_off = np.zeros(dh, np.uint32)
+        d_q_n = np.zeros(dh, np.uint32)
+        tb = []   # (exch, queue, pattern)
+        for x in sorted(self.exchanges.values(), key=lambda e: e.slot):
+            h = exch_hash(self.vhosts[x.vhost], x.name.encode())
+            for j in range(xh):
+                s = (h + j) & (xh - 1)
+                if x_hval[s] < 0:
+                    x_hkey[s] = h
+                    x_hval[s] = x.slot
+                    break
+            else:
+                raise ControlError(C.RESOURCE_ERROR, "exchange hash full")
+            x_type[x.slot] = C.EXCHANGE_TYPE_ID[x.type]
+            if x.type == "fanout":
+                qs = sorted({q for q, _ in x.bindings})
+                x_fan_off[x.slot] = len(fan_q)
+                x_fan_n[x.slot] = len(qs)
+                fan_q.extend(qs)
+            elif x.type == "direct":
+                by_key = defaultdict(list)
+                for q, k in x.bindings:
+                    if q not in by_key[k]:
+                        by_key[k].append(q)
+                for k, qs in by_key.items():
+                    dk = direct_key(fnv1a64(k), x.slot)
+                    for j in range(dh):
+                        s = (dk + j) & (dh - 1)
+                        if d_exch[s] < 0:
+                            break
+                    else:
+                        raise ControlError(C.RESOURCE_ERROR, "direct binding hash full")
+                    d_key[s] = dk
+                    d_exch[s] = x.slot
+                    d_kb_off[s] = len(kpool)
+                    d_kb_len[s] = len(k)
+                    kpool += k
+                    d_q_off[s] = len(d_q)
+                    d_q_n[s] = len(qs)
+                    d_q.extend(sorted(qs))
+            else:  # topic, headers (routes as topic: ExchangeEntity.scala:149-154)
+                x_t_off[x.slot] = len(tb)
+                bs = sorted(set(x.bindings))
+                x_t_n[x.slot] = len(bs)
+                tb.extend((x.slot, q, k) for q, k in bs)
+        tbp = i["tb_pad"]
+        if len(tb) > i["tb_max"]:
+            raise ControlError(C.RESOURCE_ERROR, "too many topic bindings for the GPU table")
+        t_queue = np.zeros(tbp, np.uint32)
+        t_exch = np.zeros(tbp, np.uint32)
+        t_kb_off = np.zeros(tbp, np.uint32)
+        t_kb_len = np.zeros(tbp, np.uint32)
+        t_flags = np.zeros(tbp, np.uint32)
+        t_expect = np.full(tbp, -1, np.int32)
+        t_mat = np.zeros((tbp, 256), np.int8)
+        for n, (xs, q, k) in enumerate(tb):
+            row, exp, fl = topic_pattern_row(k, self.hash_wildcard)
+            t_queue[n], t_exch[n], t_flags[n], t_expect[n] = q, xs, fl, exp
+            t_kb_off[n], t_kb_len[n] = len(kpool), len(k)
+            kpool += k
+            t_mat[n] = row
+        for name, arr in (("x_hkey", x_hkey), ("x_hval", x_hval), ("x_type", x_type),
+                          ("x_fan_off", x_fan_off), ("x_fan_n", x_fan_n), ("x_t_off", x_t_off),
+                          ("x_t_n", x_t_n), ("d_key", d_key), ("d_exch", d_exch), ("d_kb_off", d_kb_off),
+                          ("d_kb_len", d_kb_len), ("d_q_off", d_q_off), ("d_q_n", d_q_n),
+                          ("t_queue", t_queue), ("t_exch", t_exch), ("t_kb_off", t_kb_off),
+                          ("t_kb_len", t_kb_len), ("t_flags", t_flags), ("t_expect", t_expect),
+                          ("t_mat", t_mat)):
+            self._up(name, arr)
+        if fan_q:
+            self._up("fan_q", np.array(fan_q, np.uint32))
+        if d_q:
+            self._up("d_q", np.array(d_q, np.uint32))
+        if kpool:
+            self._up("kpool", np.frombuffer(bytes(kpool), np.uint8))
+
+    def _chmap_row(self, conn):
+        size = self.info["chmap_size"]
+        row = np.zeros(size, np.uint32)
+        c = self.conns.get(conn)
+        if c is not None:
+            for ch, chan in c.channels.items():
+                h = chan_hash(ch)
+                for j in range(size):
+                    s = (h + j) & (size - 1)
+                    if row[s] == 0:
+                        row[s] = (ch << 16) | 0x8000 | chan.local
+                        break
+        self.eng.upload("chmap", row, conn * size * 4)
+
+    def connection_changed(self, conn):
+        c = self.conns.get(conn)
+        self._up_at("conn_vhost", self.vhosts[c.vhost] if c else 0, conn, np.uint32)
+        self._up_at("conn_frame_max", c.frame_max if c else 0, conn, np.uint32)
+        self._up_at("conn_paused", 0, conn, np.uint32)
+        self._up_at("carry_len", 0, conn, np.uint32)
+        self.carry[conn] = 0
+        self._chmap_row(conn)
+
+    def channel_opened(self, chan):
+        s = chan.conn * self.chpc + chan.local
+        for name, v, dt in (("ch_next_tag", 1, np.uint64), ("ch_uhead", 1, np.uint64),
+                            ("ch_ack_upto", 0, np.uint64), ("ch_req_upto", 0, np.uint64),
+                            ("ch_confirm_next", 1, np.uint64), ("ch_confirm", 0, np.uint32),
+                            ("ch_pub_cnt", 0, np.uint32), ("ch_prefetch", 0, np.uint32),
+                            ("ch_global", 0, np.uint32), ("ch_flow", 1, np.uint32),
+                            ("ch_num", chan.ch, np.uint32), ("ch_unacked", 0, np.uint32),
+                            ("ch_win", 0, np.uint32)):
+            self._up_at(name, v, s, dt)
+        self._chmap_row(chan.conn)
+
+    def channel_changed(self, conn, ch):
+        chan = self.channel(conn, ch)
+        s = self.chslot(conn, ch)
+        self._up_at("ch_confirm", int(chan.confirm), s, np.uint32)
+        self._up_at("ch_prefetch", chan.prefetch_count, s, np.uint32)
+        self._up_at("ch_global", int(chan.global_), s, np.uint32)
+        self._up_at("ch_flow", int(chan.flow), s, np.uint32)
+
+    def channel_closing(self, chan):
+        # unacked deliveries of a closing channel go back to their queues (AMQP 0-9-1 §1.8)
+        s = chan.conn * self.chpc + chan.local
+        self._up_at("ch_req_upto", (1 << 62), s, np.uint64)
+        self._mark_dirty(s)
+        self._up_at("ch_flow", 0, s, np.uint32)
+        c = self.conns[chan.conn]
+        saved = c.channels.pop(chan.ch)
+        self._chmap_row(chan.conn)
+        c.channels[chan.ch] = saved
+
+    def _mark_dirty(self, chslot):
+        flag = np.frombuffer(self.eng.download("ch_dirty", chslot * 4, 4), np.uint32)[0]
+        if flag:
+            return
+        n = int(np.frombuffer(self.eng.download("n_dirty", 0, 4), np.uint32)[0])
+        self._up_at("dirty_list", chslot, n, np.uint32)
+        self._up_at("n_dirty", n + 1, 0, np.uint32)
+        self._up_at("ch_dirty", 1, chslot, np.uint32)
+
+    def queue_declared(self, q):
+        self._up_at("q_ring_off", q.ring_off, q.slot, np.uint64)
+        self._up_at("q_ring_mask", q.capacity - 1, q.slot, np.uint64)
+        self._up_at("q_head", 0, q.slot, np.uint64)
+        self._up_at("q_tail", 0, q.slot, np.uint64)
+        self._up_at("q_ttl", q.ttl_ms, q.slot, np.int64)
+        self._up_at("q_rr", 0, q.slot, np.uint32)
+        self._up_at("req_q_n", 0, q.slot, np.uint32)
+        self._up_at("q_active", 1, q.slot, np.uint32)
+        self._sync_consumers()
+
+    def queue_deleted(self, q):
+        self._up_at("q_active", 0, q.slot, np.uint32)
+        self._sync_consumers()
+
+    def consumers_changed(self, q, cid, removed=False):
+        if not removed:
+            c = self.consumers[cid]
+            tag = c.tag.encode()[:255]
+            self._up_at("cons_q", c.queue, cid, np.uint32)
+            self._up_at("cons_ch", self.chslot(c.conn, c.ch), cid, np.uint32)
+            self._up_at("cons_noack", int(c.no_ack), cid, np.uint32)
+            self._up_at("cons_active", 1, cid, np.uint32)
+            self._up_at("cons_unacked", 0, cid, np.uint32)
+            self._up_at("cons_tag_off", cid * 256, cid, np.uint32)
+            self._up_at("cons_tag_len", len(tag), cid, np.uint32)
+            if tag:
+                self.eng.upload("tpool", np.frombuffer(tag, np.uint8), cid * 256)
+        else:
+            self._up_at("cons_active", 0, cid, np.uint32)
+        self._sync_consumers()
+
+    def _sync_consumers(self):
+        q_off = np.zeros(self.q_max, np.uint32)
+        q_n = np.zeros(self.q_max, np.uint32)
+        flat = []
+        for q in sorted(self.queue_by_slot.values(), key=lambda x: x.slot):
+            q_off[q.slot] = len(flat)
+            q_n[q.slot] = len(q.consumers)
+            flat.extend(q.consumers)
+        self._up("q_cons_off", q_off)
+        self._up("q_cons_n", q_n)
+        if flat:
+            self._up("q_cons", np.array(flat, np.uint32))
+
+    def unpause(self, conn):
+        c = self.conns.get(conn)
+        if c is not None:
+            c.paused = False
+        self._up_at("conn_paused", 0, conn, np.uint32)
+
+    # ================================================================== steps
+    def _pinned(self, n):
+        if self._pin is None or len(self._pin) < n:
+            self._pin = self.mod.alloc_pinned(max(n, 1 << 20))
+        return self._pin
+
+    def step(self, inputs=None, now_ms=None, collect=True):
+        """One data-plane step.  ``inputs``: {conn: bytes}.  Connections holding carry
+        (partial commands) are re-presented automatically once unpaused."""
+        inputs = inputs or {}
+        conns = set(inputs)
+        for c, cl in self.carry.items():
+            if cl and c in self.conns and not self.conns[c].paused:
+                conns.add(c)
+        order = sorted(conns)
+        segs = np.zeros(len(order), SEG_IN)
+        total = sum(len(inputs.get(c, b"")) + 15 & ~15 for c in order)
+        pin = self._pinned(total + 16)
+        off = 0
+        for k, c in enumerate(order):
+            data = inputs.get(c, b"")
+            n = len(data)
+            if n:
+                pin[off:off + n] = np.frombuffer(data, np.uint8)
+            segs[k] = (c, n, off)
+            off += (n + 15) & ~15
+        return self.step_raw(segs, pin.ctypes.data, off, now_ms, collect)
+
+    def step_raw(self, segs, payload_ptr, payload_len, now_ms=None, collect=True):
+        t0 = time.perf_counter()
+        if self.requeue_pending:
+            self.eng.requeue(self.stream)
+            self.requeue_pending = False
+        now = int(time.time() * 1000) if now_ms is None else int(now_ms)
+        self.eng.submit(segs, int(payload_ptr), int(payload_len), now, self.step_no, now, self.worker,
+                        self.stream)
+        self.eng.sync(self.stream)
+        self.step_no += 1
+        res = StepResult()
+        res.elapsed = time.perf_counter() - t0
+        res.counters = self.eng.counters()
+        nseg = len(segs)
+        so = self._seg_out[:nseg]
+        for r in so:
+            conn = int(r["conn"])
+            self.carry[conn] = int(r["carry"])
+            if r["status"] & SS_CTRL and conn in self.conns:
+                self.conns[conn].paused = True
+        if res.counters["n_requeue"]:
+            self.requeue_pending = True
+        if not collect:
+            return res
+        res.segs = [tuple(int(x) for x in (r["conn"], r["status"], r["consumed"], r["carry"],
+                                             r["ncmds"], r["err_off"])) for r in so]
+        nctrl = min(res.counters["n_ctrl"], len(self._ctrl_rec))
+        for rec in self._ctrl_rec[:nctrl]:
+            if int(rec["off"]) == INVALID:
+                res.events.append((int(rec["conn"]), int(rec["len"]), int(rec["seg"])))
+            else:
+                o, n = int(rec["off"]), int(rec["len"])
+                res.ctrl.append((int(rec["conn"]), bytes(self._ctrl[o:o + n])))
+        co = self._conn_out
+        nz = np.nonzero(co["len"])[0]
+        for c in nz:
+            o, n = int(co["off"][c]), int(co["len"][c])
+            res.egress[int(c)] = bytes(self._egress[o:o + n])
+        return res

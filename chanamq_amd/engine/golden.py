@@ -1,0 +1,524 @@
+"""Golden (pure Python) data plane with exactly the GPU step semantics.
+
+Same ControlState API as GpuDataPlane; ``step()`` consumes the same ingress and
+must produce byte-identical per-connection egress for deterministic scenarios
+(one publishing connection per queue per step; no shared channel-level limits
+across queues).  This is the executable specification of csrc/kernels/dataplane.hip
+and the reference-semantics model the tests compare kernels against.
+"""
+
+import struct
+from collections import defaultdict
+
+from ..models.matcher import topic_match
+from ..protocol import constants as C
+from .control import ControlState
+from .layout import SS_CTRL, SS_FRAME_ERROR, SS_OVERFLOW, SS_TOO_LARGE, SS_UNEXPECTED
+
+NO_ROUTE_TEXT = C.REPLY_TEXT[312].encode()
+NO_CONS_TEXT = C.REPLY_TEXT[313].encode()
+
+
+def _frame(t, ch, payload):
+    return struct.pack(">BHI", t, ch, len(payload)) + payload + b"\xce"
+
+
+class _Msg:
+    __slots__ = ("ex", "rk", "props", "body", "refcnt", "pub_step", "flags", "id")
+
+    def __init__(self, ex, rk, props, body, nq, step, flags):
+        self.ex, self.rk, self.props, self.body = ex, rk, props, body
+        self.refcnt, self.pub_step, self.flags = nq, step, flags
+
+
+class GoldenDataPlane(ControlState):
+    def __init__(self, hash_wildcard=True, ucap=8192, deliver_cap=4096, carry_cap=1 << 20,
+                 egress_cap=96 << 20, deliv_max=65536, **kw):
+        super().__init__(hash_wildcard=hash_wildcard, **kw)
+        self.ucap, self.deliver_cap, self.carry_cap = ucap, deliver_cap, carry_cap
+        self.egress_cap, self.deliv_max = egress_cap, deliv_max
+        self.carry = defaultdict(bytes)
+        self.step_no = 0
+        self.ring = defaultdict(list)     # queue slot -> [(msg, redelivered, expire)]
+        self.qrr = defaultdict(int)
+        self.ch = {}                      # chslot -> dict state
+        self.cons_unacked = defaultdict(int)
+        self.dirty = []
+        self.requeue_items = []           # (q, msg, qpos, expire)
+        self.qpos_head = defaultdict(int)  # absolute position of ring[0]
+        self.counters = defaultdict(int)
+
+    # ------------------------------------------------------------------ hooks
+    def channel_opened(self, chan):
+        s = chan.conn * self.chpc + chan.local
+        self.ch[s] = dict(next_tag=1, uhead=1, ack_upto=0, req_upto=0, confirm_next=1, pub_cnt=0,
+                          unacked=0, win=0, slots={}, dirty=False, num=chan.ch)
+
+    def channel_closing(self, chan):
+        s = chan.conn * self.chpc + chan.local
+        self.ch[s]["req_upto"] = 1 << 62
+        self._mark_dirty(s)
+
+    def queue_declared(self, q):
+        self.ring[q.slot] = []
+        self.qpos_head[q.slot] = 0
+        self.qrr[q.slot] = 0
+
+    def unpause(self, conn):
+        c = self.conns.get(conn)
+        if c is not None:
+            c.paused = False
+
+    def _mark_dirty(self, s):
+        if not self.ch[s]["dirty"]:
+            self.ch[s]["dirty"] = True
+            self.dirty.append(s)
+
+    def _chan_of(self, conn, ch):
+        c = self.conns.get(conn)
+        if c is None or ch == 0 or ch not in c.channels:
+            return None
+        return conn * self.chpc + c.channels[ch].local
+
+    # ------------------------------------------------------------------ frame scan (K1)
+    def _scan(self, conn, data):
+        c = self.conns[conn]
+        fmax = c.frame_max
+        L = len(data)
+        frames = []
+        pos = 0
+        err = None
+        while pos < L:
+            if L - pos < 7:
+                frames.append((pos, None))
+                break
+            t, ch, size = struct.unpack_from(">BHI", data, pos)
+            if t not in (1, 2, 3, 8) or (fmax and size + 8 > fmax):
+                err = 3
+                break
+            if pos + 8 + size > L:
+                frames.append((pos, None))
+                break
+            if data[pos + 7 + size] != 0xCE:
+                err = 3
+                break
+            frames.append((pos, (t, ch, size)))
+            pos += 8 + size
+        end_pos = pos
+        cmds = []
+        stop = None  # (frame index, reason)
+        f = 0
+        nf = len(frames)
+        while f < nf:
+            p, fi = frames[f]
+            if fi is None:
+                stop = (f, 1)
+                break
+            t, ch, size = fi
+            if t == 8:
+                f += 1
+                continue
+            if t != 1:
+                stop = (f, 2)
+                break
+            if size < 4:
+                stop = (f, 3)
+                break
+            cls, mid = struct.unpack_from(">HH", data, p + 7)
+            chs = self._chan_of(conn, ch)
+            data_cmd = cls == 60 and mid in (40, 80, 90, 120) and chs is not None
+            if cls == 60 and mid == 40:
+                if f + 1 >= nf or frames[f + 1][1] is None:
+                    stop = (f, 1)
+                    break
+                hp, hi = frames[f + 1]
+                if hi[0] != 2 or hi[1] != ch or hi[2] < 14:
+                    stop = (f, 2)
+                    break
+                bsz = struct.unpack_from(">Q", data, hp + 7 + 4)[0]
+                got, e, bad, inc = 0, f + 1, None, False
+                bodies = []
+                while got < bsz:
+                    e += 1
+                    if e >= nf or frames[e][1] is None:
+                        inc = True
+                        break
+                    bp, bi = frames[e]
+                    if bi[0] != 3 or bi[1] != ch:
+                        bad = 2
+                        break
+                    got += bi[2]
+                    bodies.append((bp + 7, bi[2]))
+                    if got > bsz:
+                        bad = 3
+                        break
+                if inc:
+                    stop = (f, 1)
+                    break
+                if bad:
+                    stop = (f, bad)
+                    break
+                endp = (frames[e][0] + 8 + frames[e][1][2])
+                cmd = dict(kind="publish" if data_cmd else "control", ch=ch, chslot=chs,
+                           m=(p + 7, size), h=(hp + 7, hi[2]), bodies=bodies, bsz=bsz,
+                           raw=data[p:endp])
+                cmds.append(cmd)
+                f = e + 1
+                if not data_cmd:
+                    stop = (f, 0)
+                    break
+                continue
+            endp = p + 8 + size
+            kind = {80: "ack", 90: "reject", 120: "nack"}.get(mid) if (cls == 60 and data_cmd) else "control"
+            cmds.append(dict(kind=kind, ch=ch, chslot=chs, m=(p + 7, size), raw=data[p:endp]))
+            f += 1
+            if kind == "control":
+                stop = (f, 0)
+                break
+        if stop is None:
+            if err is not None:
+                stop = (nf, 3)
+            else:
+                stop = (nf, 7)
+        kf, reason = stop
+        consumed = frames[kf][0] if kf < nf else (end_pos if err is None or True else end_pos)
+        if kf >= nf:
+            consumed = end_pos
+        status = 0
+        if reason in (2, 3):
+            status |= SS_FRAME_ERROR if reason == 3 else SS_UNEXPECTED
+        if reason == 0:
+            status |= SS_CTRL
+        return cmds, consumed, status
+
+    # ------------------------------------------------------------------ one step
+    def step(self, inputs=None, now_ms=0):
+        inputs = inputs or {}
+        self.counters = defaultdict(int)
+        cnt = self.counters
+        out = {"egress": {}, "ctrl": [], "events": [], "segs": []}
+        # pre-step requeue (k_requeue): per queue, sorted by queue position
+        if self.requeue_items:
+            byq = defaultdict(list)
+            for it in self.requeue_items:
+                byq[it[0]].append(it)
+            self.requeue_items = []
+            for q, items in byq.items():
+                items.sort(key=lambda x: x[2])
+                ring = self.ring[q]
+                cap = self.queue_by_slot[q].capacity if q in self.queue_by_slot else 0
+                free = cap - len(ring)
+                k = min(len(items), free)
+                self.ring[q] = [(m, True, e) for (_, m, _, e) in items[:k]] + ring
+                self.qpos_head[q] -= k
+                self.requeue_items.extend(items[k:])
+        conns = set(inputs)
+        for c, cl in self.carry.items():
+            if cl and c in self.conns and not self.conns[c].paused:
+                conns.add(c)
+        pubs, acks = [], []
+        for conn in sorted(conns):
+            data = self.carry[conn] + inputs.get(conn, b"")
+            if self.conns[conn].paused:
+                self.carry[conn] = data
+                out["segs"].append((conn, 1, 0, len(data)))
+                continue
+            cmds, consumed, status = self._scan(conn, data)
+            for cmd in cmds:
+                cmd["conn"] = conn
+                if cmd["kind"] == "publish":
+                    pubs.append((cmd, data))
+                elif cmd["kind"] in ("ack", "reject", "nack"):
+                    acks.append((cmd, data))
+                else:
+                    out["ctrl"].append((conn, cmd["raw"]))
+            rest = data[consumed:]
+            if len(rest) > self.carry_cap:
+                status |= SS_TOO_LARGE
+                rest = b""
+            self.carry[conn] = rest
+            if status & SS_CTRL:
+                self.conns[conn].paused = True
+            out["segs"].append((conn, status, consumed, len(rest)))
+        # ---- publishes: decode, route, returns, store, enqueue
+        returns = defaultdict(list)
+        for cmd, data in pubs:
+            self._publish(cmd, data, now_ms, returns, out)
+        # ---- acks
+        for cmd, data in acks:
+            s = cmd["chslot"]
+            st = self.ch[s]
+            o = cmd["m"][0] + 4
+            tag = struct.unpack_from(">Q", data, o)[0]
+            bits = data[o + 8]
+            kind = cmd["kind"]
+            multiple = bool(bits & 1) if kind != "reject" else False
+            requeue = (bits & 1) if kind == "reject" else ((bits >> 1) & 1 if kind == "nack" else 0)
+            if tag == 0 and multiple:
+                tag = st["next_tag"] - 1
+            if multiple:
+                key = "req_upto" if requeue else "ack_upto"
+                st[key] = max(st[key], tag)
+            elif st["uhead"] <= tag < st["next_tag"]:
+                sl = st["slots"].get(tag)
+                if sl and sl["state"] == "pending":
+                    sl["state"] = "requeue" if requeue else "acked"
+            self._mark_dirty(s)
+            cnt["n_acked"] += 1
+        # ---- window advance (k_chan_advance)
+        dirty, self.dirty = self.dirty, []
+        for s in dirty:
+            st = self.ch[s]
+            st["dirty"] = False
+            contiguous = True
+            t = st["uhead"]
+            released = 0
+            while t < st["next_tag"]:
+                sl = st["slots"].get(t)
+                state = sl["state"]
+                if state == "pending" and t <= st["ack_upto"]:
+                    state = "acked"
+                if state == "pending" and t <= st["req_upto"]:
+                    state = "requeue"
+                if state == "acked":
+                    self._release(sl["msg"])
+                    self.cons_unacked[sl["cons"]] -= 1
+                    st["unacked"] -= 1
+                    state = "done"
+                elif state == "requeue":
+                    self.requeue_items.append((sl["q"], sl["msg"], sl["qpos"], sl["expire"]))
+                    self.cons_unacked[sl["cons"]] -= 1
+                    st["unacked"] -= 1
+                    cnt["n_requeue"] += 1
+                    state = "done"
+                sl["state"] = state
+                if contiguous and state == "done":
+                    released += 1
+                else:
+                    contiguous = False
+                t += 1
+            for k in range(st["uhead"], st["uhead"] + released):
+                st["slots"].pop(k, None)
+            st["uhead"] += released
+            st["win"] -= released
+        # ---- dequeue (k_dequeue)
+        delivs = []
+        budget = [0]
+        for q in sorted(self.queue_by_slot):
+            delivs.extend(self._dequeue(q, now_ms, budget))
+        # ---- tags: stable sort by chslot
+        delivs.sort(key=lambda d: d["chslot"])
+        for d in delivs:
+            st = self.ch[d["chslot"]]
+            d["tag"] = st["next_tag"]
+            st["next_tag"] += 1
+            st["slots"][d["tag"]] = dict(state="done" if d["noack"] else "pending", msg=d["msg"],
+                                         q=d["q"], cons=d["cons"], qpos=d["qpos"], expire=d["expire"])
+            self._mark_dirty(d["chslot"])
+            cnt["lat_" + str(min(self.step_no - d["msg"].pub_step, 31))] += 1
+        # ---- egress per connection: returns, confirms, deliveries
+        by_conn = defaultdict(list)
+        for d in delivs:
+            by_conn[d["chslot"] // self.chpc].append(d)
+        conns_out = set(by_conn) | set(returns)
+        for s, st in self.ch.items():
+            if st["pub_cnt"]:
+                conns_out.add(s // self.chpc)
+        for conn in sorted(conns_out):
+            parts = list(returns.get(conn, []))
+            for local in range(self.chpc):
+                s = conn * self.chpc + local
+                st = self.ch.get(s)
+                if not st or not st["pub_cnt"]:
+                    continue
+                n = st["pub_cnt"]
+                st["pub_cnt"] = 0
+                last = st["confirm_next"] + n - 1
+                st["confirm_next"] = last + 1
+                parts.append(_frame(1, st["num"], struct.pack(">HHQB", 60, 80, last, 1 if n > 1 else 0)))
+            fm = self.conns[conn].frame_max if conn in self.conns else 131072
+            for d in by_conn.get(conn, []):
+                parts.append(self._render_deliver(d, fm))
+            if parts:
+                out["egress"][conn] = b"".join(parts)
+        for d in delivs:
+            if d["noack"]:
+                self._release(d["msg"])
+        cnt["n_deliv"] = len(delivs)
+        self.step_no += 1
+        out["counters"] = dict(cnt)
+        return out
+
+    def _release(self, msg):
+        msg.refcnt -= 1
+        if msg.refcnt == 0:
+            self.counters["n_freed"] += 1
+
+    def _publish(self, cmd, data, now_ms, returns, out):
+        conn = cmd["conn"]
+        cnt = self.counters
+        mo, ml = cmd["m"]
+        o = mo + 6
+        exl = data[o]
+        ex = data[o + 1:o + 1 + exl]
+        o += 1 + exl
+        rkl = data[o]
+        rk = data[o + 1:o + 1 + rkl]
+        o += 1 + rkl
+        bits = data[o]
+        mandatory, immediate = bool(bits & 1), bool(bits & 2)
+        ho, hl = cmd["h"]
+        props = data[ho + 12:ho + hl]
+        body = b"".join(data[bo:bo + bl] for bo, bl in cmd["bodies"])
+        s = cmd["chslot"]
+        st = self.ch[s]
+        chan = self.conns[conn].channels[cmd["ch"]]
+        if chan.confirm:
+            st["pub_cnt"] += 1
+        expire = self._expiration(props, now_ms)
+        vhost = self.conns[conn].vhost
+        x = self.exchanges.get((vhost, ex.decode("utf-8", "surrogateescape")))
+        if x is None:
+            cnt["n_unknown_exchange"] += 1
+            out["events"].append((conn, 404, s))
+            return
+        qs = self._route(x, rk)
+        ret = 0
+        if not qs:
+            cnt["n_unroutable"] += 1
+            if mandatory:
+                ret = 312
+        elif immediate and not any(self.queue_by_slot[q].consumers for q in qs):
+            ret = 313
+            qs = []
+        if ret:
+            txt = NO_ROUTE_TEXT if ret == 312 else NO_CONS_TEXT
+            fm = self.conns[conn].frame_max
+            mp = struct.pack(">HHHB", 60, 50, ret, len(txt)) + txt + bytes([len(ex)]) + ex + bytes([len(rk)]) + rk
+            fr = [_frame(1, cmd["ch"], mp), _frame(2, cmd["ch"], struct.pack(">HHQ", 60, 0, len(body)) + props)]
+            step = fm - 8 if fm else len(body)
+            for i in range(0, len(body), max(step, 1)):
+                fr.append(_frame(3, cmd["ch"], body[i:i + step]))
+            returns[conn].append(b"".join(fr))
+        if not qs:
+            return
+        flags = 1 if self._persistent(props) else 0
+        msg = _Msg(ex, rk, props, body, len(qs), self.step_no, flags)
+        for q in qs:
+            qq = self.queue_by_slot[q]
+            ring = self.ring[q]
+            if len(ring) >= qq.capacity:
+                cnt["n_ring_full"] += 1
+                self._release(msg)
+                continue
+            e = expire
+            if qq.ttl_ms > 0:
+                qe = now_ms + qq.ttl_ms
+                e = qe if (e == 0 or qe < e) else e
+            ring.append((msg, False, e))
+
+    def _route(self, x, rk):
+        if x.type == "direct":
+            seen = []
+            for q, k in x.bindings:
+                if k == rk and q not in seen:
+                    seen.append(q)
+            return sorted(seen)
+        if x.type == "fanout":
+            return sorted({q for q, _ in x.bindings})
+        out = []
+        key = rk.decode("utf-8", "surrogateescape")
+        for q, k in sorted(set(x.bindings)):
+            if out and out[-1] == q:
+                continue
+            if topic_match(k.decode("utf-8", "surrogateescape"), key, self.hash_wildcard):
+                out.append(q)
+        return out
+
+    @staticmethod
+    def _prop_fields(props):
+        from ..protocol.codec import decode_properties
+        try:
+            p, _ = decode_properties(props)
+        except Exception:
+            return {}
+        return p
+
+    def _persistent(self, props):
+        return self._prop_fields(props).get("delivery_mode") == 2
+
+    def _expiration(self, props, now_ms):
+        e = self._prop_fields(props).get("expiration")
+        if e and e.isdigit() and len(e) <= 18:
+            return now_ms + int(e)
+        return 0
+
+    def _dequeue(self, q, now_ms, budget):
+        qq = self.queue_by_slot[q]
+        ring = self.ring[q]
+        cnt = self.counters
+        while ring and ring[0][2] and ring[0][2] <= now_ms:
+            self._release(ring.pop(0)[0])
+            self.qpos_head[q] += 1
+            cnt["n_expired"] += 1
+        mall = len(qq.consumers)
+        if not mall or not ring:
+            return []
+        m = min(mall, 64)
+        r = self.qrr[q] % mall
+        remaining = len(ring)
+        grants = []
+        for j in range(m):
+            cid = qq.consumers[(r + j) % mall]
+            c = self.consumers[cid]
+            chan = self.conns[c.conn].channels[c.ch]
+            s = self.chslot(c.conn, c.ch)
+            st = self.ch[s]
+            g = 0
+            if remaining and c.active and chan.flow:
+                share = -(-remaining // (m - j))
+                want = min(share, self.deliver_cap)
+                pc = chan.prefetch_count
+                if not c.no_ack and pc and not chan.global_:
+                    want = min(want, max(pc - self.cons_unacked[cid], 0))
+                g = min(want, self.ucap - st["win"])
+                st["win"] += g
+                if not c.no_ack and pc and chan.global_ and g:
+                    g2 = min(g, max(pc - st["unacked"], 0))
+                    st["win"] -= g - g2
+                    st["unacked"] += g2
+                    g = g2
+                elif not c.no_ack and g:
+                    st["unacked"] += g
+                if not c.no_ack and g:
+                    self.cons_unacked[cid] += g
+            grants.append([cid, g])
+            remaining -= g
+        out = []
+        pos = 0
+        for cid, g in grants:
+            if not g:
+                continue
+            c = self.consumers[cid]
+            chan_s = self.chslot(c.conn, c.ch)
+            for k in range(g):
+                msg, red, exp = ring[pos + k]
+                out.append(dict(chslot=chan_s, cons=cid, msg=msg, q=q, qpos=self.qpos_head[q] + pos + k,
+                                expire=exp, redelivered=red, noack=c.no_ack, tag_str=c.tag.encode()))
+            pos += g
+        self.qrr[q] = (r + 1) % mall
+        del ring[:pos]
+        self.qpos_head[q] += pos
+        return out
+
+    def _render_deliver(self, d, fm):
+        m = d["msg"]
+        ch = self.ch[d["chslot"]]["num"]
+        tag = d["tag_str"][:255]
+        mp = (struct.pack(">HHB", 60, 60, len(tag)) + tag + struct.pack(">QB", d["tag"], 1 if d["redelivered"] else 0)
+              + bytes([len(m.ex)]) + m.ex + bytes([len(m.rk)]) + m.rk)
+        parts = [_frame(1, ch, mp), _frame(2, ch, struct.pack(">HHQ", 60, 0, len(m.body)) + m.props)]
+        step = fm - 8 if fm else len(m.body)
+        for i in range(0, len(m.body), max(step, 1)):
+            parts.append(_frame(3, ch, m.body[i:i + step]))
+        return b"".join(parts)

@@ -1,0 +1,85 @@
+"""Host mirrors of the data-plane structs (csrc/kernels/dp_common.h) and hashes.
+
+Every numpy dtype here must match ``sizeof`` reported by ``Engine.info()['sizeof']``;
+tests/test_layout.py and the GPU tests check that.
+"""
+
+import numpy as np
+
+SEG_IN = np.dtype([("conn", "<u4"), ("len", "<u4"), ("src", "<u8")])
+SEG_OUT = np.dtype([("conn", "<u4"), ("status", "<u4"), ("consumed", "<u4"), ("carry", "<u4"),
+                    ("ncmds", "<u4"), ("err_off", "<u4"), ("pad", "<u4", 2)])
+CTRL_REC = np.dtype([("conn", "<u4"), ("off", "<u4"), ("len", "<u4"), ("seg", "<u4")])
+CONN_OUT = np.dtype([("off", "<u4"), ("len", "<u4")])
+
+STRUCT_SIZES = {"SegIn": 16, "SegOut": 32, "CtrlRec": 16, "ConnOut": 8, "StepIn": 64}
+
+# SegOut.status bits
+SS_PAUSED = 1
+SS_CTRL = 2
+SS_FRAME_ERROR = 4
+SS_UNEXPECTED = 8
+SS_TOO_LARGE = 16
+SS_OVERFLOW = 32
+
+INVALID = 0xFFFFFFFF
+U64 = (1 << 64) - 1
+FNV64_BASIS = 0xCBF29CE484222325
+FNV64_PRIME = 0x100000001B3
+GOLDEN64 = 0x9E3779B97F4A7C15
+
+
+def fnv1a64(data: bytes, h: int = FNV64_BASIS) -> int:
+    for b in data:
+        h ^= b
+        h = (h * FNV64_PRIME) & U64
+    return h
+
+
+def fnv1a32(data: bytes) -> int:
+    h = 0x811C9DC5
+    for b in data:
+        h ^= b
+        h = (h * 0x01000193) & 0xFFFFFFFF
+    return h
+
+
+def exch_hash(vhost_id: int, name: bytes) -> int:
+    """Device key of an exchange (dataplane.hip exch_hash)."""
+    return fnv1a64(name, FNV64_BASIS ^ ((vhost_id * GOLDEN64) & U64))
+
+
+def direct_key(keyhash: int, exch_slot: int) -> int:
+    return keyhash ^ ((exch_slot * GOLDEN64) & U64)
+
+
+def chan_hash(ch: int) -> int:
+    return ((ch * 0x9E3779B1) & 0xFFFFFFFF) >> 7
+
+
+def split_words_bytes(key: bytes):
+    """Java split semantics on bytes (mirror of models.matcher.split_words)."""
+    if key == b"":
+        return [b""]
+    parts = key.split(b".")
+    while parts and parts[-1] == b"":
+        parts.pop()
+    return parts
+
+
+def topic_pattern_row(pattern: bytes, hash_wildcard=True, nwords_max=8):
+    """(int8[256] pattern vector, expect score, flags) for the MFMA topic prefilter."""
+    words = split_words_bytes(pattern)
+    row = np.zeros(nwords_max * 32, dtype=np.int8)
+    dp_only = len(words) > nwords_max or (hash_wildcard and b"#" in words)
+    if dp_only:
+        return row, -1, 1 | (len(words) << 8)
+    nonstar = 0
+    for i, w in enumerate(words):
+        if w == b"*":
+            continue
+        h = fnv1a32(w)
+        bits = (h >> np.arange(32, dtype=np.uint64)) & 1
+        row[i * 32:(i + 1) * 32] = np.where(bits == 1, 1, -1).astype(np.int8)
+        nonstar += 1
+    return row, 32 * nonstar, (len(words) << 8)

@@ -1,0 +1,53 @@
+"""HIP (gfx950) kernels of the data plane, built in-tree.
+
+``_dataplane`` is compiled by ``build()`` with hipcc for ``--offload-arch=gfx950``
+from csrc/kernels/{engine,dataplane}.hip.  Importing ``chanamq_amd.ops.dataplane``
+on a machine with a GPU but without the extension raises: there is no silent
+fallback for the hot path.
+"""
+
+import importlib
+import os
+import subprocess
+import sys
+import sysconfig
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_ROOT = os.path.dirname(os.path.dirname(_HERE))
+_SRC = os.path.join(_ROOT, "csrc", "kernels")
+_EXT = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
+EXT_PATH = os.path.join(_HERE, "_dataplane" + _EXT)
+SOURCES = ["engine.hip", "dataplane.hip", "dp_state.h", "dp_common.h"]
+
+
+def _stale():
+    if not os.path.exists(EXT_PATH):
+        return True
+    t = os.path.getmtime(EXT_PATH)
+    return any(os.path.getmtime(os.path.join(_SRC, s)) > t for s in SOURCES)
+
+
+def build(force=False, verbose=False):
+    """Compile the data-plane extension for gfx950 (cross-compiles without a GPU)."""
+    if not force and not _stale():
+        return EXT_PATH
+    import pybind11
+
+    hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+    inc = [f"-I{pybind11.get_include()}", f"-I{sysconfig.get_paths()['include']}", f"-I{_SRC}"]
+    cmd = [hipcc, "--offload-arch=gfx950", "-O3", "-std=c++17", "-shared", "-fPIC", *inc,
+           os.path.join(_SRC, "engine.hip"), "-o", EXT_PATH + ".tmp"]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    subprocess.run(cmd, check=True)
+    os.replace(EXT_PATH + ".tmp", EXT_PATH)
+    return EXT_PATH
+
+
+def load():
+    """Import the compiled extension (raises ImportError with a build hint)."""
+    try:
+        return importlib.import_module("chanamq_amd.ops._dataplane")
+    except ImportError as e:
+        raise ImportError(f"chanamq_amd.ops._dataplane is not built ({e}); run "
+                          "`python -c 'import __graft_entry__ as g; g.build()'`") from e

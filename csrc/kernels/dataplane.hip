@@ -1,0 +1,1758 @@
+// MI355X (gfx950) AMQP 0-9-1 data plane: the broker hot path as a fixed-shape,
+// hipGraph-capturable kernel pipeline.
+//
+//   K0 stage        carry + new TCP bytes -> contiguous per-connection work segment
+//   K1 frame_scan   speculative frame-boundary scan + chain resolution (LDS), command
+//                   assembly (method -> header -> bodies), control barrier, carry-out
+//                   (FrameParser.scala:86-157, CommandAssembler.scala:56-130)
+//   K3/K4 decode    Basic.Publish / Ack / Nack / Reject args + content-header
+//                   properties (Basic.scala:36-59, BasicProperties.scala:42-96)
+//   K6 route        direct (device hash), fanout (CSR), topic (int8 MFMA word-hash
+//                   prefilter + exact word matcher)  (QueueMatcher.scala, ExchangeEntity.scala:287-331)
+//   K13 ids         snowflake ids (IdGenerator.scala:55-83)
+//   K7 enqueue      stable radix sort by queue -> per-queue HBM ring append (QueueEntity.scala:271-316)
+//   K9 acks         per-channel unacked windows, ack/nack/reject (AMQChannel.scala:109-174)
+//   K8/K12 dequeue  credit-limited round-robin pull with TTL skip (QueueEntity.scala:318-393)
+//   K9 tags         stable sort by channel -> delivery tags
+//   K5 render       Deliver / Return / confirm-Ack frames written straight into
+//                   host-mapped egress memory (AMQCommand.scala:30-59)
+//   K10 confirms    one coalesced Basic.Ack per channel per step (FrameStage.scala:571-596)
+//   K11 refcount    body refcount + free-list / log reclamation (MessageEntity.scala:134-166)
+//
+// Every kernel reads its dynamic sizes from device counters, so grids are fixed by
+// EngineCfg and the whole step is captured once into a hipGraph (engine.cpp).
+#include "dp_state.h"
+
+#define INVALID 0xffffffffu
+#define FNV64_BASIS 0xcbf29ce484222325ULL
+#define FNV64_PRIME 0x100000001b3ULL
+
+// ============================================================================ helpers
+DEV u32 lane_id() { return __lane_id(); }
+DEV u64 lanemask_lt() {
+  u32 l = __lane_id();
+  return l ? ((~0ull) >> (64 - l)) : 0ull;
+}
+DEV u32 be16(const u8* p) { return (u32(p[0]) << 8) | u32(p[1]); }
+DEV u32 be32(const u8* p) {
+  return (u32(p[0]) << 24) | (u32(p[1]) << 16) | (u32(p[2]) << 8) | u32(p[3]);
+}
+DEV u64 be64(const u8* p) { return (u64(be32(p)) << 32) | u64(be32(p + 4)); }
+DEV void wr16(u8* p, u32 v) { p[0] = u8(v >> 8); p[1] = u8(v); }
+DEV void wr32(u8* p, u32 v) { p[0] = u8(v >> 24); p[1] = u8(v >> 16); p[2] = u8(v >> 8); p[3] = u8(v); }
+DEV void wr64(u8* p, u64 v) { wr32(p, u32(v >> 32)); wr32(p + 4, u32(v)); }
+DEV u32 align16(u32 x) { return (x + 15u) & ~15u; }
+
+DEV u64 exch_hash(u32 vhost, const u8* name, u32 n) {
+  u64 h = FNV64_BASIS ^ (u64(vhost) * 0x9E3779B97F4A7C15ULL);
+  for (u32 i = 0; i < n; ++i) { h ^= name[i]; h *= FNV64_PRIME; }
+  return h;
+}
+DEV u32 fnv1a32(const u8* p, u32 n) {
+  u32 h = 0x811c9dc5u;
+  for (u32 i = 0; i < n; ++i) { h ^= p[i]; h *= 0x01000193u; }
+  return h;
+}
+
+struct __attribute__((packed, aligned(1))) U4 { u32 x, y, z, w; };
+
+// unaligned-source, unaligned-dest byte copy by the 64 lanes of one wave
+DEV void wave_copy(u8* dst, const u8* src, u32 n) {
+  u32 lane = lane_id();
+  u32 nv = n >> 4;
+  for (u32 i = lane; i < nv; i += 64) {
+    U4 v = *(const U4*)(src + (u64)i * 16);
+    *(U4*)(dst + (u64)i * 16) = v;
+  }
+  for (u32 i = (nv << 4) + lane; i < n; i += 64) dst[i] = src[i];
+}
+
+// same, by all threads of a block
+DEV void block_copy(u8* dst, const u8* src, u32 n, u32 tid, u32 nt) {
+  u32 nv = n >> 4;
+  for (u32 i = tid; i < nv; i += nt) {
+    U4 v = *(const U4*)(src + (u64)i * 16);
+    *(U4*)(dst + (u64)i * 16) = v;
+  }
+  for (u32 i = (nv << 4) + tid; i < n; i += nt) dst[i] = src[i];
+}
+
+// CAS reservation: grant min(want, cap - *p), return old value in *base
+DEV u32 reserve_upto(u32* p, u32 want, u32 cap, u32* base) {
+  u32 cur = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  while (true) {
+    u32 avail = cur < cap ? cap - cur : 0;
+    u32 g = want < avail ? want : avail;
+    if (g == 0) { *base = cur; return 0; }
+    u32 prev = atomicCAS(p, cur, cur + g);
+    if (prev == cur) { *base = cur; return g; }
+    cur = prev;
+  }
+}
+
+// exclusive block scan (NT threads), returns this thread's offset; total via ref
+template <int NT>
+DEV u32 block_scan(u32 v, u32* lds, u32& total) {
+  u32 lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  u32 x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    u32 y = __shfl_up(x, o, 64);
+    if (lane >= (u32)o) x += y;
+  }
+  if (lane == 63) lds[w] = x;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    u32 run = 0;
+    for (int i = 0; i < NT / 64; ++i) { u32 t = lds[i]; lds[i] = run; run += t; }
+    lds[NT / 64] = run;
+  }
+  __syncthreads();
+  u32 res = lds[w] + x - v;
+  total = lds[NT / 64];
+  __syncthreads();
+  return res;
+}
+
+// ---- message release (K11): refcount -1, free slot + table index at zero
+DEV void release_msg(const DS& d, u32 msg) {
+  if (msg == INVALID) return;
+  i32 old = atomicSub(&d.msgs[msg].refcnt, 1);
+  if (old == 1) {
+    MsgEnt& m = d.msgs[msg];
+    u64 blk = (m.log_off / d.log_block) % d.n_log_blocks;
+    atomicAdd((unsigned long long*)&d.log_live[blk], (unsigned long long)(-(i64)m.slot_bytes));
+    u32 slot = atomicAdd(d.msg_free_top, 1u);
+    d.msg_free[slot] = msg;
+    atomicAdd(&d.ctr->n_freed, 1u);
+  }
+}
+
+// ============================================================================ topic words
+// Java String.split("\\.") semantics (QueueMatcher.scala:69-71): trailing empty
+// words dropped, "" -> [""], "..." -> [].
+struct Words { u32 eff; u32 count; };
+DEV Words words_of(const u8* s, u32 n) {
+  Words w;
+  if (n == 0) { w.eff = 0; w.count = 1; return w; }
+  u32 e = n;
+  while (e > 0 && s[e - 1] == '.') --e;
+  w.eff = e;
+  if (e == 0) { w.count = 0; return w; }
+  u32 c = 1;
+  for (u32 i = 0; i < e; ++i) c += (s[i] == '.');
+  w.count = c;
+  return w;
+}
+DEV u32 word_len(const u8* s, u32 off, u32 eff) {
+  u32 i = off;
+  while (i < eff && s[i] != '.') ++i;
+  return i - off;
+}
+DEV bool word_eq(const u8* a, u32 al, const u8* b, u32 bl) {
+  if (al != bl) return false;
+  for (u32 i = 0; i < al; ++i)
+    if (a[i] != b[i]) return false;
+  return true;
+}
+// exact topic match: '*' = one word, '#' = zero or more words (when hash_wild),
+// greedy backtracking (glob algorithm over words). Golden: models/matcher.py words_match.
+DEV bool topic_match(const u8* pat, u32 plen, const u8* key, u32 klen, bool hash_wild) {
+  Words pw = words_of(pat, plen), kw = words_of(key, klen);
+  u32 pend = pw.eff + 1, kend = kw.eff + 1;  // cursor == end -> exhausted
+  u32 p = pw.count ? 0 : pend, k = kw.count ? 0 : kend;
+  u32 sp = INVALID, sk = 0;
+  while (k < kend) {
+    u32 kl = word_len(key, k, kw.eff);
+    if (p < pend) {
+      u32 pl = word_len(pat, p, pw.eff);
+      bool is_hash = hash_wild && pl == 1 && pat[p] == '#';
+      bool is_star = pl == 1 && pat[p] == '*';
+      if (is_hash) { p += pl + 1; sp = p; sk = k; continue; }
+      if (is_star || word_eq(pat + p, pl, key + k, kl)) { p += pl + 1; k += kl + 1; continue; }
+    }
+    if (sp != INVALID) {
+      sk += word_len(key, sk, kw.eff) + 1;
+      k = sk;
+      p = sp;
+      continue;
+    }
+    return false;
+  }
+  while (p < pend) {
+    u32 pl = word_len(pat, p, pw.eff);
+    if (hash_wild && pl == 1 && pat[p] == '#') { p += pl + 1; continue; }
+    return false;
+  }
+  return true;
+}
+
+// ============================================================================ K0 prep + stage
+// one block of 1024: zero step counters, lay out work segments (16-aligned)
+__global__ __launch_bounds__(1024) void k_prep(DS d) {
+  __shared__ u32 lds[1024 / 64 + 1];
+  u32 tid = threadIdx.x;
+  u32 nseg = d.in->nseg;
+  if (tid < sizeof(Counters) / 4) {
+    u32* c = (u32*)d.ctr;
+    if (tid * 4 < offsetof(Counters, log_head)) c[tid] = 0;
+  }
+  u32 running = 0;
+  for (u32 base = 0; base < d.seg_max; base += 1024) {
+    u32 s = base + tid;
+    u32 tot = 0;
+    if (s < nseg) {
+      u32 conn = d.segs[s].conn;
+      tot = d.carry_len[conn] + d.segs[s].len;
+      d.seg_total[s] = tot;
+    }
+    u32 sz = s < nseg ? align16(tot + 32) : 0;
+    u32 all;
+    u32 off = block_scan<1024>(sz, lds, all);
+    if (s < nseg) d.seg_start[s] = running + off;
+    running += all;
+    if (base + 1024 >= nseg) break;
+  }
+  if (tid == 0) {
+    *d.egress_budget = 0;
+    d.tot[15] = running;  // work bytes used
+    // snowflake virtual position base for this step
+    u64 floor_pos = d.in->id_ms << 12;
+    u64 cur = *d.id_next;
+    *d.id_next = cur > floor_pos ? cur : floor_pos;
+  }
+}
+
+// grid (seg_max, 8): copy carry then new bytes into the work segment
+__global__ __launch_bounds__(256) void k_stage(DS d) {
+  u32 s = blockIdx.x;
+  if (s >= d.in->nseg) return;
+  if (d.tot[15] > d.work_cap) return;  // host sizes steps so this never triggers
+  u32 conn = d.segs[s].conn;
+  u32 cl = d.carry_len[conn];
+  u32 len = d.segs[s].len;
+  u8* dst = d.work + d.seg_start[s];
+  u32 part = blockIdx.y, nparts = gridDim.y;
+  u32 tid = threadIdx.x + part * 256, nt = 256 * nparts;
+  if (cl) block_copy(dst, d.carry + (u64)conn * d.carry_cap, cl, tid, nt);
+  if (len) block_copy(dst + cl, d.ingress + d.segs[s].src, len, tid, nt);
+}
+
+// ============================================================================ K1 frame scan
+struct FInfo { u32 type, ch, size; bool complete, valid_hdr; };
+
+DEV FInfo frame_at(const u8* b, u32 p, u32 L, u32 fmax) {
+  FInfo f;
+  f.complete = false;
+  f.valid_hdr = false;
+  f.type = 0; f.ch = 0; f.size = 0;
+  if (p + 7 > L) return f;  // partial header
+  f.type = b[p];
+  f.ch = be16(b + p + 1);
+  f.size = be32(b + p + 3);
+  bool tok = f.type == 1 || f.type == 2 || f.type == 3 || f.type == 8;
+  bool sok = fmax == 0 || f.size + 8 <= fmax;
+  f.valid_hdr = tok && sok;
+  if (f.valid_hdr && (u64)p + 8 + f.size <= L) f.complete = (b[p + 7 + f.size] == 0xCE);
+  return f;
+}
+
+DEV i32 chan_lookup(const DS& d, u32 conn, u32 ch) {
+  const u32* m = d.chmap + (u64)conn * d.chmap_size;
+  u32 mask = d.chmap_size - 1;
+  u32 h = (ch * 0x9E3779B1u) >> 7;
+  for (u32 i = 0; i < d.chmap_size; ++i) {
+    u32 e = m[(h + i) & mask];
+    if (e == 0) return -1;
+    if ((e >> 16) == ch && (e & 0x8000u)) return (i32)(conn * d.chpc + (e & 0x7fffu));
+  }
+  return -1;
+}
+
+__global__ __launch_bounds__(256) void k_frame_scan(DS d) {
+  __shared__ u32 cpos[CAND_MAX];
+  __shared__ int16_t csucc[CAND_MAX];
+  __shared__ u16 chain[CAND_MAX];
+  __shared__ u8 claim[CAND_MAX];
+  __shared__ u32 sc[8];
+  __shared__ u32 sh_m, sh_over, sh_ok, sh_nf, sh_stop, sh_brk;
+  __shared__ u32 sh_cmd_base, sh_frag_base, sh_ncmd;
+
+  const u32 s = blockIdx.x;
+  if (s >= d.in->nseg) return;
+  const u32 tid = threadIdx.x;
+  const u32 conn = d.segs[s].conn;
+  const u32 L = d.seg_total[s];
+  const u8* b = d.work + d.seg_start[s];
+  const u32 fmax = d.conn_frame_max[conn];
+  const u32 wbase = d.seg_start[s];
+  SegOut so;
+  so.conn = conn; so.status = 0; so.consumed = 0; so.carry = L; so.ncmds = 0; so.err_off = 0;
+  so.pad[0] = so.pad[1] = 0;
+
+  if (d.conn_paused[conn]) {
+    // hold everything; write carry back (k_stage already appended new bytes)
+    if (L > d.carry_cap) { so.status = SS_TOO_LARGE; so.carry = 0; }
+    else block_copy(d.carry + (u64)conn * d.carry_cap, b, L, tid, 256);
+    if (tid == 0) {
+      so.status |= SS_PAUSED;
+      d.carry_len[conn] = so.carry;
+      d.seg_out[s] = so;
+    }
+    return;
+  }
+  if (L == 0) {
+    if (tid == 0) { d.carry_len[conn] = 0; d.seg_out[s] = so; }
+    return;
+  }
+  if (tid == 0) { sh_m = 0; sh_over = 0; }
+  __syncthreads();
+
+  // ---- (a) candidates
+  for (u32 t0 = 0; t0 < L; t0 += 4096) {
+    u32 p0 = t0 + tid * 16;
+    u32 bits = 0;
+    for (u32 j = 0; j < 16; ++j) {
+      u32 p = p0 + j;
+      if (p >= L) break;
+      if (p + 7 > L) { bits |= 1u << j; continue; }
+      u32 t = b[p];
+      if (!(t == 1 || t == 2 || t == 3 || t == 8)) continue;
+      FInfo f = frame_at(b, p, L, fmax);
+      if (!f.valid_hdr) continue;
+      if ((u64)p + 8 + f.size <= L && !f.complete) continue;
+      bits |= 1u << j;
+    }
+    u32 cnt = __popc(bits), tot;
+    u32 off = block_scan<256>(cnt, sc, tot);
+    u32 m0 = sh_m;
+    for (u32 j = 0; bits; ++j) {
+      if (bits & 1u) {
+        u32 idx = m0 + off;
+        if (idx < CAND_MAX) cpos[idx] = p0 + j;
+        ++off;
+      }
+      bits >>= 1;
+    }
+    __syncthreads();
+    if (tid == 0) {
+      u32 nm = m0 + tot;
+      if (nm > CAND_MAX) { sh_over = 1; nm = CAND_MAX; }
+      sh_m = nm;
+    }
+    __syncthreads();
+    if (sh_over) break;
+  }
+  const u32 m = sh_m;
+  const bool over = sh_over != 0;
+
+  // ---- (b) successor of every candidate (-1 exact end, -2 partial/unknown, -3 broken)
+  for (u32 i = tid; i < m; i += 256) {
+    u32 p = cpos[i];
+    FInfo f = frame_at(b, p, L, fmax);
+    i32 sx;
+    if (!f.complete) sx = -2;
+    else {
+      u32 e = p + 8 + f.size;
+      if (e == L) sx = -1;
+      else {
+        u32 lo = i + 1, hi = m;  // successor lies strictly after i
+        while (lo < hi) { u32 mid = (lo + hi) >> 1; if (cpos[mid] < e) lo = mid + 1; else hi = mid; }
+        if (lo < m && cpos[lo] == e) sx = (i32)lo;
+        else sx = (over && e > cpos[m - 1]) ? -2 : -3;
+      }
+    }
+    csucc[i] = (int16_t)sx;
+  }
+  if (tid == 0) sh_ok = 1;
+  __syncthreads();
+  // ---- (c) chain: optimistic (every candidate a real frame) else serial walk
+  for (u32 i = tid; i < m; i += 256) {
+    i32 sx = csucc[i];
+    bool good = (i + 1 < m) ? (sx == (i32)(i + 1)) : (sx == -1 || sx == -2);
+    if (!good) atomicAnd(&sh_ok, 0u);
+  }
+  __syncthreads();
+  if (tid == 0) {
+    u32 nf = 0, brk = 0;
+    if (m == 0 || cpos[0] != 0) {
+      brk = 1;  // first bytes are not a frame header
+    } else if (sh_ok) {
+      nf = m;
+    } else {
+      i32 i = 0;
+      while (true) {
+        chain[nf++] = (u16)i;
+        i32 sx = csucc[i];
+        if (sx >= 0) { i = sx; continue; }
+        if (sx == -3) brk = 1;
+        break;
+      }
+    }
+    sh_nf = nf;
+    sh_brk = brk;
+  }
+  __syncthreads();
+  const u32 nf = sh_nf;
+  const bool implicit_chain = sh_ok && !(m == 0 || cpos[0] != 0);
+#define CPOS(f) (cpos[implicit_chain ? (f) : chain[f]])
+
+  // ---- (d) commands: each method frame walks its content frames
+  for (u32 f = tid; f < nf; f += 256) claim[f] = 0;
+  if (tid == 0) sh_stop = (nf << 3) | 7;  // (frame << 3) | reason; 7 = none
+  __syncthreads();
+  // stop reasons: 0 = after control, 1 = incomplete, 2 = unexpected frame, 3 = frame error
+  for (u32 f = tid; f < nf; f += 256) {
+    u32 p = CPOS(f);
+    FInfo fi = frame_at(b, p, L, fmax);
+    if (!fi.complete) {
+      if (fi.type == 1 || fi.type == 8 || !fi.valid_hdr) atomicMin(&sh_stop, (f << 3) | 1);
+      continue;
+    }
+    if (fi.type == 8) { claim[f] = 1; continue; }
+    if (fi.type != 1) continue;
+    claim[f] = 1;
+    if (fi.size < 4) { atomicMin(&sh_stop, (f << 3) | 3); continue; }
+    u32 cls = be16(b + p + 7), mid = be16(b + p + 9);
+    bool content = (cls == 60 && mid == 40);
+    bool data = (cls == 60 && (mid == 40 || mid == 80 || mid == 90 || mid == 120)) && fi.ch != 0 &&
+                chan_lookup(d, conn, fi.ch) >= 0;
+    if (!content) {
+      if (!data) atomicMin(&sh_stop, ((f + 1) << 3) | 0);
+      continue;
+    }
+    // header then bodies on the same channel
+    u32 g = f + 1;
+    if (g >= nf) { atomicMin(&sh_stop, (f << 3) | 1); continue; }
+    u32 hp = CPOS(g);
+    FInfo hi = frame_at(b, hp, L, fmax);
+    if (!hi.complete) { atomicMin(&sh_stop, (f << 3) | 1); continue; }
+    if (hi.type != 2 || hi.ch != fi.ch || hi.size < 14) { atomicMin(&sh_stop, (f << 3) | 2); continue; }
+    claim[g] = 1;
+    u64 bsz = be64(b + hp + 7 + 4);
+    u64 got = 0;
+    u32 e = g;
+    bool bad = false, incomplete = false;
+    while (got < bsz) {
+      ++e;
+      if (e >= nf) { incomplete = true; break; }
+      u32 bp = CPOS(e);
+      FInfo bi = frame_at(b, bp, L, fmax);
+      if (!bi.complete) { incomplete = true; break; }
+      if (bi.type != 3 || bi.ch != fi.ch) { atomicMin(&sh_stop, (f << 3) | 2); bad = true; break; }
+      claim[e] = 1;
+      got += bi.size;
+      if (got > bsz) { atomicMin(&sh_stop, (f << 3) | 3); bad = true; break; }
+    }
+    if (incomplete) atomicMin(&sh_stop, (f << 3) | 1);
+    (void)bad;
+    if (!data) atomicMin(&sh_stop, ((e + 1) << 3) | 0);
+  }
+  __syncthreads();
+  for (u32 f = tid; f < nf; f += 256) {
+    if (claim[f]) continue;
+    FInfo fi = frame_at(b, CPOS(f), L, fmax);
+    if (fi.complete) atomicMin(&sh_stop, (f << 3) | 2);
+  }
+  __syncthreads();
+  u32 stop = sh_stop;
+  u32 kf = stop >> 3, reason = stop & 7;
+  if (kf > nf) kf = nf;
+  if (reason == 7 && sh_brk) { reason = 3; }  // chain ended on a broken frame
+
+  // consumed bytes: up to frame kf (or the end of the chain)
+  u32 consumed;
+  if (kf < nf) consumed = CPOS(kf);
+  else if (nf == 0) consumed = 0;
+  else {
+    u32 lp = CPOS(nf - 1);
+    FInfo lf = frame_at(b, lp, L, fmax);
+    consumed = lf.complete ? lp + 8 + lf.size : lp;
+  }
+  if (reason == 3 || reason == 2) {
+    so.status |= (reason == 3) ? SS_FRAME_ERROR : SS_UNEXPECTED;
+    so.err_off = consumed;
+  }
+  if (over && reason != 0 && kf == nf) so.status |= SS_OVERFLOW;
+
+  // ---- (e) emit commands for method frames < kf
+  u32 run = 0, frun = 0;
+  if (tid == 0) { sh_cmd_base = INVALID; sh_ncmd = 0; }
+  __syncthreads();
+  // count first
+  u32 my_cmds = 0, my_frags = 0;
+  for (u32 f = tid; f < kf; f += 256) {
+    u32 p = CPOS(f);
+    if (b[p] != 1) continue;
+    ++my_cmds;
+    if (be16(b + p + 7) == 60 && be16(b + p + 9) == 40) {
+      // frags: frames after header until the next method
+      u32 e = f + 2;
+      while (e < kf && b[CPOS(e)] == 3) { ++my_frags; ++e; }
+    }
+  }
+  u32 tc, tfr;
+  block_scan<256>(my_cmds, sc, tc);
+  block_scan<256>(my_frags, sc, tfr);
+  if (tid == 0) {
+    u32 cb, fb;
+    u32 gc = reserve_upto(&d.ctr->n_cmds, tc, d.cmd_max, &cb);
+    u32 gf = reserve_upto(&d.ctr->n_frags, tfr, d.frag_max, &fb);
+    if (gc < tc || gf < tfr) {
+      // give back and carry the whole segment to the next step
+      if (gc) atomicSub(&d.ctr->n_cmds, gc);
+      if (gf) atomicSub(&d.ctr->n_frags, gf);
+      sh_cmd_base = INVALID;
+    } else {
+      sh_cmd_base = cb;
+      sh_frag_base = fb;
+    }
+  }
+  __syncthreads();
+  if (sh_cmd_base == INVALID && tc > 0) {
+    so.status |= SS_OVERFLOW;
+    so.status &= ~(SS_FRAME_ERROR | SS_UNEXPECTED);
+    consumed = 0;
+    kf = 0;
+    reason = 7;
+  }
+  const i64 now = d.in->now_ms;
+  for (u32 f0 = 0; f0 < kf; f0 += 256) {
+    u32 f = f0 + tid;
+    u32 is_cmd = 0, nfr = 0;
+    u32 p = 0;
+    if (f < kf) {
+      p = CPOS(f);
+      if (b[p] == 1) {
+        is_cmd = 1;
+        if (be16(b + p + 7) == 60 && be16(b + p + 9) == 40) {
+          u32 e = f + 2;
+          while (e < kf && b[CPOS(e)] == 3) { ++nfr; ++e; }
+        }
+      }
+    }
+    u32 tcnt, tf;
+    u32 r = block_scan<256>(is_cmd, sc, tcnt);
+    u32 fr = block_scan<256>(nfr, sc, tf);
+    if (is_cmd) {
+      Cmd c;
+      FInfo fi = frame_at(b, p, L, fmax);
+      u32 cls = be16(b + p + 7), mid = be16(b + p + 9);
+      c.conn = conn;
+      c.ch = fi.ch;
+      c.m_off = wbase + p + 7;
+      c.m_len = fi.size;
+      c.h_off = 0; c.h_len = 0; c.frag0 = 0; c.nfrag = 0; c.body_size = 0;
+      c.seg = s;
+      c.raw_off = wbase + p;
+      i32 chs = fi.ch ? chan_lookup(d, conn, fi.ch) : -1;
+      c.pad[0] = (u32)chs;
+      c.pad[1] = 0; c.pad[2] = 0;
+      u32 endp = p + 8 + fi.size;
+      if (cls == 60 && mid == 40 && chs >= 0) c.kind = CK_PUBLISH;
+      else if (cls == 60 && mid == 80 && chs >= 0) c.kind = CK_ACK;
+      else if (cls == 60 && mid == 90 && chs >= 0) c.kind = CK_REJECT;
+      else if (cls == 60 && mid == 120 && chs >= 0) c.kind = CK_NACK;
+      else c.kind = CK_CONTROL;
+      if (cls == 60 && mid == 40) {
+        u32 hp = CPOS(f + 1);
+        FInfo hi = frame_at(b, hp, L, fmax);
+        c.h_off = wbase + hp + 7;
+        c.h_len = hi.size;
+        c.body_size = (u32)be64(b + hp + 7 + 4);
+        c.frag0 = sh_frag_base + frun + fr;
+        c.nfrag = nfr;
+        endp = hp + 8 + hi.size;
+        for (u32 k = 0; k < nfr; ++k) {
+          u32 bp = CPOS(f + 2 + k);
+          FInfo bi = frame_at(b, bp, L, fmax);
+          Frag fg;
+          fg.off = wbase + bp + 7;
+          fg.len = bi.size;
+          d.frags[c.frag0 + k] = fg;
+          endp = bp + 8 + bi.size;
+        }
+      }
+      c.raw_len = endp - p;
+      d.cmds[sh_cmd_base + run + r] = c;
+      if (c.kind == CK_CONTROL) {
+        u32 cbase;
+        u32 g = reserve_upto(&d.ctr->ctrl_bytes, c.raw_len, (u32)d.ctrl_cap, &cbase);
+        if (g == c.raw_len) {
+          for (u32 k = 0; k < c.raw_len; ++k) d.ctrl[cbase + k] = b[p + k];
+          u32 ri = atomicAdd(&d.ctr->n_ctrl, 1u);
+          CtrlRec rec;
+          rec.conn = conn; rec.off = cbase; rec.len = c.raw_len; rec.seg = s;
+          if (ri < d.seg_max * 2) d.ctrl_rec[ri] = rec;
+        }
+      }
+    }
+    run += tcnt;
+    frun += tf;
+  }
+  if (tid == 0 && kf > 0) d.conn_last_rx[conn] = now;
+  if (reason == 0) so.status |= SS_CTRL;
+
+  // ---- (f) carry out: bytes [consumed, L)
+  u32 rest = L - consumed;
+  if (rest > d.carry_cap) { so.status |= SS_TOO_LARGE; rest = 0; }
+  else block_copy(d.carry + (u64)conn * d.carry_cap, b + consumed, rest, tid, 256);
+  if (tid == 0) {
+    so.consumed = consumed;
+    so.carry = rest;
+    so.ncmds = run;
+    d.carry_len[conn] = rest;
+    if (reason == 0) d.conn_paused[conn] = 1;
+    d.seg_out[s] = so;
+  }
+#undef CPOS
+}
+
+// ============================================================================ K3 classify / decode
+__global__ void k_classify(DS d) {
+  u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+  u32 n = d.ctr->n_cmds;
+  if (i >= d.cmd_max) return;
+  u32 k = i < n ? d.cmds[i].kind : CK_NONE;
+  d.cmd_is_pub[i] = (k == CK_PUBLISH);
+  d.cmd_is_ack[i] = (k == CK_ACK || k == CK_NACK || k == CK_REJECT);
+}
+
+__global__ void k_set_counts(DS d) {
+  if (threadIdx.x) return;
+  u32 np = d.tot[4], na = d.tot[5];
+  d.ctr->n_pubs = np < d.pub_max ? np : d.pub_max;
+  d.ctr->n_acks = na < d.ack_max ? na : d.ack_max;
+}
+
+__global__ void k_reset_dirty(DS d) {
+  if (threadIdx.x == 0) *d.n_dirty = 0;
+}
+
+DEV bool skip_shortstr(const u8* p, u32& o, u32 end) {
+  if (o + 1 > end) return false;
+  o += 1 + p[o];
+  return o <= end;
+}
+
+__global__ void k_decode(DS d) {
+  u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+  u32 n = d.ctr->n_cmds;
+  if (i >= n) return;
+  const Cmd c = d.cmds[i];
+  const u8* w = d.work;
+  if (c.kind == CK_PUBLISH) {
+    u32 pi = d.cmd_pub_rank[i];
+    if (pi >= d.pub_max) return;
+    Pub pb;
+    pb.conn = c.conn;
+    pb.chslot = c.pad[0];
+    pb.frag0 = c.frag0;
+    pb.nfrag = c.nfrag;
+    pb.body_size = c.body_size;
+    pb.flags = 0;
+    pb.expire_ms = 0;
+    pb.ts_ms = 0;
+    pb.nq = 0; pb.slot_bytes = 0; pb.msg = INVALID; pb.pad = 0;
+    // method args: class u16, method u16, ticket u16, exchange ss, rk ss, bits
+    u32 o = c.m_off + 6, end = c.m_off + c.m_len;
+    bool ok = o <= end;
+    pb.ex_off = o + 1;
+    pb.ex_len = ok && o < end ? w[o] : 0;
+    ok = ok && skip_shortstr(w, o, end);
+    pb.rk_off = o + 1;
+    pb.rk_len = ok && o < end ? w[o] : 0;
+    ok = ok && skip_shortstr(w, o, end);
+    u32 bits = (ok && o < end) ? w[o] : 0;
+    if (bits & 1) pb.flags |= MF_MANDATORY;
+    if (bits & 2) pb.flags |= MF_IMMEDIATE;
+    // exchange
+    i32 xs = -1;
+    if (ok) {
+      u64 hk = exch_hash(d.conn_vhost[c.conn], w + pb.ex_off, pb.ex_len);
+      u32 mask = d.xhash_mask;
+      for (u32 j = 0; j <= mask; ++j) {
+        u32 slot = (u32)(hk + j) & mask;
+        i32 v = d.x_hval[slot];
+        if (v < 0) break;
+        if (d.x_hkey[slot] == hk) { xs = v; break; }
+      }
+    }
+    pb.exch = ok ? xs : -2;
+    pb.keyhash = fnv1a64_dev(w + pb.rk_off, pb.rk_len);
+    // properties (flags chain then values)
+    u32 ho = c.h_off + 12, hend = c.h_off + c.h_len;
+    pb.props_off = ho;
+    pb.props_len = hend > ho ? hend - ho : 0;
+    u32 flagw[2] = {0, 0};
+    u32 nfl = 0;
+    u32 q = ho;
+    while (q + 2 <= hend) {
+      u32 fw = be16(w + q);
+      q += 2;
+      if (nfl < 2) flagw[nfl] = fw;
+      ++nfl;
+      if (!(fw & 1)) break;
+    }
+    u32 fl = flagw[0];
+    bool pok = true;
+    // field order: 15 ctype ss, 14 cenc ss, 13 headers tbl, 12 dmode oct, 11 prio oct,
+    // 10 corr ss, 9 replyto ss, 8 expiration ss, 7 msgid ss, 6 timestamp u64, 5 type,
+    // 4 userid, 3 appid, 2 clusterid
+    for (int bit = 15; bit >= 2 && pok; --bit) {
+      if (!(fl & (1u << bit))) continue;
+      switch (bit) {
+        case 13: {
+          if (q + 4 > hend) { pok = false; break; }
+          u32 tl = be32(w + q);
+          q += 4 + tl;
+          pok = q <= hend;
+          break;
+        }
+        case 12:
+          if (q + 1 > hend) { pok = false; break; }
+          if (w[q] == 2) pb.flags |= MF_PERSIST;
+          q += 1;
+          break;
+        case 11: q += 1; pok = q <= hend; break;
+        case 8: {
+          if (q + 1 > hend) { pok = false; break; }
+          u32 sl = w[q];
+          if (q + 1 + sl > hend) { pok = false; break; }
+          i64 v = 0;
+          bool digits = sl > 0 && sl <= 18;
+          for (u32 k = 0; k < sl && digits; ++k) {
+            u8 ch = w[q + 1 + k];
+            if (ch < '0' || ch > '9') digits = false;
+            else v = v * 10 + (ch - '0');
+          }
+          if (digits) pb.expire_ms = d.in->now_ms + v;
+          q += 1 + sl;
+          break;
+        }
+        case 6:
+          if (q + 8 > hend) { pok = false; break; }
+          pb.ts_ms = (i64)be64(w + q) * 1000;
+          pb.flags |= MF_HAS_TS;
+          q += 8;
+          break;
+        default:
+          pok = skip_shortstr(w, q, hend);
+      }
+    }
+    // topic key vector (8 words x 32 bits, +-1), built only if topic bindings exist
+    Words kw = words_of(w + pb.rk_off, pb.rk_len);
+    pb.nwords = kw.count;
+    i8* kv = d.pub_keyvec + (u64)pi * TOPIC_K;
+    if (d.tb_max) {
+      u32 off = 0;
+      u32 wi = 0;
+      const u8* key = w + pb.rk_off;
+      if (kw.count) {
+        while (wi < TOPIC_WORDS && off <= kw.eff) {
+          u32 wl = word_len(key, off, kw.eff);
+          u32 h = fnv1a32(key + off, wl);
+          for (int bb = 0; bb < 32; ++bb) kv[wi * 32 + bb] = ((h >> bb) & 1) ? 1 : -1;
+          off += wl + 1;
+          ++wi;
+        }
+      }
+      for (; wi < TOPIC_WORDS; ++wi)
+        for (int bb = 0; bb < 32; ++bb) kv[wi * 32 + bb] = 0;
+    }
+    d.pubs[pi] = pb;
+    if (pb.chslot != INVALID && d.ch_confirm[pb.chslot]) atomicAdd(&d.ch_pub_cnt[pb.chslot], 1u);
+  } else if (c.kind == CK_ACK || c.kind == CK_NACK || c.kind == CK_REJECT) {
+    u32 ai = d.cmd_ack_rank[i];
+    if (ai >= d.ack_max) return;
+    Ack a;
+    a.chslot = c.pad[0];
+    a.kind = c.kind;
+    u32 o = c.m_off + 4;
+    bool ok = c.m_len >= 13;
+    a.tag = ok ? be64(w + o) : 0;
+    u32 bits = ok ? w[o + 8] : 0;
+    if (c.kind == CK_ACK) { a.multiple = bits & 1; a.requeue = 0; }
+    else if (c.kind == CK_REJECT) { a.multiple = 0; a.requeue = bits & 1; }
+    else { a.multiple = bits & 1; a.requeue = (bits >> 1) & 1; }
+    d.acks[ai] = a;
+  }
+}
+
+// ============================================================================ scans
+// single-block multi-array exclusive scan; n read from device; totals -> tot[slot+k]
+struct ScanArgs { const u32* in[4]; u32* out[4]; const u32* n; u32 narr; u32 nmax; u32 tot_slot; };
+__global__ __launch_bounds__(1024) void k_scan(ScanArgs a, u32* tot) {
+  __shared__ u32 lds[1024 / 64 + 1];
+  u32 n = a.n ? *a.n : a.nmax;
+  if (n > a.nmax) n = a.nmax;
+  u32 per = (n + 1023) / 1024;
+  u32 tid = threadIdx.x;
+  u32 b0 = tid * per, b1 = b0 + per;
+  if (b1 > n) b1 = n;
+  for (u32 k = 0; k < a.narr; ++k) {
+    u32 sum = 0;
+    for (u32 i = b0; i < b1; ++i) sum += a.in[k][i];
+    u32 all;
+    u32 off = block_scan<1024>(sum, lds, all);
+    for (u32 i = b0; i < b1; ++i) { u32 v = a.in[k][i]; a.out[k][i] = off; off += v; }
+    if (tid == 0) tot[a.tot_slot + k] = all;
+  }
+}
+
+// ============================================================================ radix sort
+// stable LSD radix sort of (key, val) u32 pairs, 8 bits per pass; n from device.
+__global__ __launch_bounds__(256) void k_rs_hist(const u32* keys, const u32* np, u32 shift, u32* hist,
+                                                 u32 ntiles) {
+  __shared__ u32 cnt[256];
+  u32 tid = threadIdx.x, t = blockIdx.x;
+  cnt[tid] = 0;
+  __syncthreads();
+  u32 n = *np;
+  u32 base = t * SORT_TILE;
+  if (base < n) {
+    for (u32 j = 0; j < 16; ++j) {
+      u32 i = base + j * 256 + tid;
+      if (i < n) atomicAdd(&cnt[(keys[i] >> shift) & 255], 1u);
+    }
+  }
+  __syncthreads();
+  hist[tid * ntiles + t] = cnt[tid];
+}
+
+__global__ __launch_bounds__(256) void k_rs_scatter(const u32* kin, const u32* vin, u32* kout, u32* vout,
+                                                    const u32* np, u32 shift, const u32* hscan,
+                                                    u32 ntiles) {
+  __shared__ u32 wc[4][256];
+  u32 tid = threadIdx.x, t = blockIdx.x, w = tid >> 6, lane = tid & 63;
+  u32 n = *np;
+  u32 base = t * SORT_TILE;
+  if (base >= n) return;
+  for (u32 i = tid; i < 1024; i += 256) ((u32*)wc)[i] = 0;
+  __syncthreads();
+  u32 wbase = base + w * 1024;
+  // pass 1: per-wave digit counts
+  for (u32 c = 0; c < 16; ++c) {
+    u32 i = wbase + c * 64 + lane;
+    bool valid = i < n;
+    u32 dg = valid ? (kin[i] >> shift) & 255 : 0;
+    u64 peers = __ballot(valid);
+    for (u32 bb = 0; bb < 8; ++bb) {
+      u64 m = __ballot((dg >> bb) & 1);
+      peers &= ((dg >> bb) & 1) ? m : ~m;
+    }
+    bool leader = valid && ((peers & lanemask_lt()) == 0);
+    if (leader) wc[w][dg] += __popcll(peers);
+    __builtin_amdgcn_wave_barrier();
+  }
+  __syncthreads();
+  {
+    u32 dg = tid;
+    u32 run = hscan[dg * ntiles + t];
+    for (u32 ww = 0; ww < 4; ++ww) { u32 x = wc[ww][dg]; wc[ww][dg] = run; run += x; }
+  }
+  __syncthreads();
+  for (u32 c = 0; c < 16; ++c) {
+    u32 i = wbase + c * 64 + lane;
+    bool valid = i < n;
+    u32 key = valid ? kin[i] : 0;
+    u32 dg = (key >> shift) & 255;
+    u64 peers = __ballot(valid);
+    for (u32 bb = 0; bb < 8; ++bb) {
+      u64 m = __ballot((dg >> bb) & 1);
+      peers &= ((dg >> bb) & 1) ? m : ~m;
+    }
+    u32 basepos = ((volatile u32*)wc[w])[dg];
+    u32 rank = __popcll(peers & lanemask_lt());
+    if (valid) {
+      kout[basepos + rank] = key;
+      vout[basepos + rank] = vin[i];
+    }
+    __builtin_amdgcn_wave_barrier();
+    bool leader = valid && ((peers & lanemask_lt()) == 0);
+    if (leader) ((volatile u32*)wc[w])[dg] = basepos + __popcll(peers);
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
+// ============================================================================ K6 route
+// topic prefilter on MFMA: score[p][b] = keyvec[p] . patvec[b] over 256 int8 lanes;
+// a pattern word contributes +32 iff its 32-bit word hash equals the key's.
+typedef int v4i __attribute__((ext_vector_type(4)));
+__global__ __launch_bounds__(256) void k_topic_mfma(DS d) {
+  u32 wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  u32 lane = lane_id();
+  u32 ntb = d.tb_pad >> 4;
+  u32 npub = d.ctr->n_pubs;
+  if (npub > d.pub_max) npub = d.pub_max;
+  u32 it = wave / ntb, jt = wave % ntb;
+  u32 i0 = it * 16, j0 = jt * 16;
+  if (i0 >= npub || d.tb_max == 0) return;
+  v4i acc = {0, 0, 0, 0};
+  const i8* A = d.pub_keyvec + (u64)(i0 + (lane & 15)) * TOPIC_K + (lane >> 4) * 16;
+  const i8* B = d.t_mat + (u64)(j0 + (lane & 15)) * TOPIC_K + (lane >> 4) * 16;
+#pragma unroll
+  for (int kk = 0; kk < TOPIC_K / 64; ++kk) {
+    v4i a = *(const v4i*)(A + kk * 64);
+    v4i bv = *(const v4i*)(B + kk * 64);
+    acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, bv, acc, 0, 0, 0);
+  }
+  i32 ex = d.t_expect[j0 + (lane & 15)];
+  u64 m0 = __ballot(acc[0] == ex), m1 = __ballot(acc[1] == ex);
+  u64 m2 = __ballot(acc[2] == ex), m3 = __ballot(acc[3] == ex);
+  if (lane < 16) {
+    u32 row = i0 + lane;  // row = 4*g + r with g = lane/4, r = lane%4
+    u32 g = lane >> 2, r = lane & 3;
+    u64 mm = r == 0 ? m0 : r == 1 ? m1 : r == 2 ? m2 : m3;
+    u32 rr = i0 + g * 4 + r;
+    (void)row;
+    if (rr < npub) d.pub_match[(u64)rr * ntb + jt] = (u16)((mm >> (16 * g)) & 0xffff);
+  }
+}
+
+DEV bool topic_bind_hit(const DS& d, const Pub& pb, u32 pidx, u32 t) {
+  u32 fl = d.t_flags[t];
+  bool dp_only = fl & 1;
+  if (!dp_only) {
+    if ((fl >> 8) != pb.nwords) return false;
+    u16 mw = d.pub_match[(u64)pidx * (d.tb_pad >> 4) + (t >> 4)];
+    if (!((mw >> (t & 15)) & 1)) return false;
+  }
+  return topic_match(d.kpool + d.t_kb_off[t], d.t_kb_len[t], d.work + pb.rk_off, pb.rk_len,
+                     d.hash_wildcard != 0);
+}
+
+DEV i32 direct_find(const DS& d, const Pub& pb) {
+  u64 k = pb.keyhash ^ (u64(pb.exch) * 0x9E3779B97F4A7C15ULL);
+  u32 mask = d.dhash_mask;
+  for (u32 j = 0; j <= mask; ++j) {
+    u32 s = (u32)(k + j) & mask;
+    i32 ex = d.d_exch[s];
+    if (ex < 0) return -1;
+    if (ex == pb.exch && d.d_key[s] == k &&
+        word_eq(d.kpool + d.d_kb_off[s], d.d_kb_len[s], d.work + pb.rk_off, pb.rk_len))
+      return (i32)s;
+  }
+  return -1;
+}
+
+// pass 0: count queues; pass 1: write pairs
+template <int PASS>
+__global__ void k_route(DS d) {
+  u32 p = blockIdx.x * blockDim.x + threadIdx.x;
+  u32 n = d.ctr->n_pubs;
+  if (n > d.pub_max) n = d.pub_max;
+  if (p >= n) {
+    if (PASS == 0 && p < d.pub_max) { d.pub_nq[p] = 0; d.pub_slot[p] = 0; d.pub_routed[p] = 0; }
+    return;
+  }
+  Pub& pb = d.pubs[p];
+  if (PASS == 1 && d.pub_nq[p] == 0) return;
+  u32 nq = 0;
+  u32 wbase = PASS ? d.pub_pair_off[p] : 0;
+  bool has_cons = false;
+#define EMIT(q)                                              \
+  do {                                                       \
+    u32 _q = (q);                                            \
+    if (PASS) { d.pair_k[0][wbase + nq] = _q; d.pair_v[0][wbase + nq] = p; } \
+    if (d.q_cons_n[_q]) has_cons = true;                     \
+    ++nq;                                                    \
+  } while (0)
+  if (pb.exch >= 0) {
+    u32 xt = d.x_type[pb.exch];
+    if (xt == EX_DIRECT) {
+      i32 s = direct_find(d, pb);
+      if (s >= 0) {
+        u32 o = d.d_q_off[s], c = d.d_q_n[s];
+        for (u32 k = 0; k < c; ++k) EMIT(d.d_q[o + k]);
+      }
+    } else if (xt == EX_FANOUT) {
+      u32 o = d.x_fan_off[pb.exch], c = d.x_fan_n[pb.exch];
+      for (u32 k = 0; k < c; ++k) EMIT(d.fan_q[o + k]);
+    } else {
+      u32 o = d.x_t_off[pb.exch], c = d.x_t_n[pb.exch];
+      u32 last = INVALID;
+      for (u32 k = 0; k < c; ++k) {
+        u32 t = o + k;
+        u32 q = d.t_queue[t];
+        if (q == last) continue;
+        if (topic_bind_hit(d, pb, p, t)) { EMIT(q); last = q; }
+      }
+    }
+  }
+#undef EMIT
+  if (PASS == 0) {
+    u32 ret = 0;
+    if (pb.exch < 0) {
+      atomicAdd(&d.ctr->n_unknown_exchange, 1u);
+      u32 ri = atomicAdd(&d.ctr->n_ctrl, 1u);
+      CtrlRec rec;
+      rec.conn = pb.conn; rec.off = INVALID; rec.len = 404; rec.seg = pb.chslot;
+      if (ri < d.seg_max * 2) d.ctrl_rec[ri] = rec;
+    } else if (nq == 0) {
+      atomicAdd(&d.ctr->n_unroutable, 1u);
+      if (pb.flags & MF_MANDATORY) ret = 312;
+    } else if ((pb.flags & MF_IMMEDIATE) && !has_cons) {
+      ret = 313;
+      nq = 0;  // spec behaviour: not enqueued (SURVEY A.Q16/CHANGES.md)
+    }
+    d.pub_ret[p] = ret;
+    u32 meta = align16(pb.ex_len + pb.rk_len + pb.props_len);
+    u32 slot = nq ? align16(meta + pb.body_size) : 0;
+    d.pub_nq[p] = nq;
+    d.pub_slot[p] = slot;
+    d.pub_routed[p] = nq ? 1 : 0;
+    pb.nq = nq;
+    pb.slot_bytes = slot;
+    if (ret) {
+      // reserve bytes in the connection's return region
+      u32 sz = (8 + 4 + 2 + 1 + 64 + 1 + pb.ex_len + 1 + pb.rk_len + 1) /*method*/ +
+               (8 + 12 + pb.props_len) /*header*/;
+      u32 fm = d.conn_frame_max[pb.conn];
+      u32 fmb = fm ? fm - 8 : 0xffffffffu;
+      u32 nb = pb.body_size ? (pb.body_size + fmb - 1) / fmb : 0;
+      sz += pb.body_size + 8 * nb;
+      u32 roff = atomicAdd(&d.conn_ret_bytes[pb.conn], sz);
+      pb.pad = roff;
+      u32 ri = atomicAdd(&d.ctr->n_returns, 1u);
+      if (ri < d.pub_max) d.ret_list[ri] = p;
+    }
+  }
+}
+
+// reserve the step's contiguous body-log region and message-table indices
+__global__ void k_log_reserve(DS d) {
+  if (threadIdx.x) return;
+  u32 total = d.tot[1];     // slot bytes
+  u32 routed = d.tot[2];    // routed messages
+  u64 head = *d.log_head, tail = *d.log_tail;
+  u64 phys = head % d.log_bytes;
+  if (phys + total > d.log_bytes) head += d.log_bytes - phys;
+  bool ok = (head + total - tail <= d.log_bytes) && routed <= *d.msg_free_top;
+  if (!ok || total == 0) {
+    *d.log_step_base = ok ? head : INVALID;
+    if (!ok) d.ctr->n_dropped_nomem = routed;
+    return;
+  }
+  *d.log_step_base = head;
+  *d.log_head = head + total;
+  d.tot[8] = *d.msg_free_top;
+  *d.msg_free_top = d.tot[8] - routed;
+  d.ctr->n_routed_msgs = routed;
+  d.ctr->n_pairs = d.tot[0];
+}
+
+// one wave per publish: allocate, fill MsgEnt, copy exchange/rk/props/body into the log
+__global__ __launch_bounds__(256) void k_store(DS d) {
+  u32 p = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  u32 lane = lane_id();
+  u32 n = d.ctr->n_pubs;
+  if (n > d.pub_max) n = d.pub_max;
+  if (p >= n) return;
+  Pub& pb = d.pubs[p];
+  if (d.pub_nq[p] == 0) return;
+  u64 base = *d.log_step_base;
+  if (base == INVALID) { if (lane == 0) pb.msg = INVALID; return; }
+  u32 rr = d.pub_routed_rank[p];
+  u32 msg = d.msg_free[d.tot[8] - 1 - rr];
+  u64 off = base + d.pub_slot_off[p];
+  u8* slot = d.log + (off % d.log_bytes);
+  const u8* w = d.work;
+  u32 meta = align16(pb.ex_len + pb.rk_len + pb.props_len);
+  wave_copy(slot, w + pb.ex_off, pb.ex_len);
+  wave_copy(slot + pb.ex_len, w + pb.rk_off, pb.rk_len);
+  wave_copy(slot + pb.ex_len + pb.rk_len, w + pb.props_off, pb.props_len);
+  u32 bo = meta;
+  for (u32 k = 0; k < pb.nfrag; ++k) {
+    Frag fg = d.frags[pb.frag0 + k];
+    wave_copy(slot + bo, w + fg.off, fg.len);
+    bo += fg.len;
+  }
+  if (lane == 0) {
+    MsgEnt m;
+    m.log_off = off;
+    u64 pos = (*d.id_next) + rr;
+    m.msg_id = ((pos >> 12) << 22) | (u64(d.in->worker & 1023) << 12) | (pos & 4095);
+    m.ts_ms = pb.ts_ms;
+    m.slot_bytes = pb.slot_bytes;
+    m.body_len = pb.body_size;
+    m.body_off = meta;
+    m.props_len = (u16)pb.props_len;
+    m.ex_len = (u8)pb.ex_len;
+    m.rk_len = (u8)pb.rk_len;
+    m.refcnt = (i32)pb.nq;
+    m.flags = pb.flags;
+    m.pub_step = (u32)d.in->step;
+    m.pad = 0;
+    d.msgs[msg] = m;
+    pb.msg = msg;
+    u64 blk = (off / d.log_block) % d.n_log_blocks;
+    atomicAdd((unsigned long long*)&d.log_live[blk], (unsigned long long)pb.slot_bytes);
+  }
+}
+
+// ============================================================================ K7 enqueue
+__global__ void k_qfirst(DS d, u32 src) {
+  u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+  u32 n = d.tot[0];
+  if (i >= n) return;
+  const u32* k = d.pair_k[src];
+  if (i == 0 || k[i - 1] != k[i]) d.q_first[k[i]] = i;
+}
+
+__global__ void k_enqueue(DS d, u32 src) {
+  u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+  u32 n = d.tot[0];
+  if (i >= n) return;
+  const u32* kk = d.pair_k[src];
+  u32 q = kk[i];
+  u32 p = d.pair_v[src][i];
+  u32 first = d.q_first[q];
+  u32 rank = i - first;
+  bool last = (i + 1 == n) || kk[i + 1] != q;
+  const Pub& pb = d.pubs[p];
+  u64 head = d.q_head[q], tail = d.q_tail[q];
+  u64 cap = d.q_ring_mask[q] + 1;
+  u64 freec = cap - (tail - head);
+  if (pb.msg == INVALID) return;
+  if (rank < freec) {
+    u64 pos = tail + rank;
+    Desc ds;
+    ds.msg = pb.msg;
+    ds.flags = 0;
+    i64 e = pb.expire_ms;
+    i64 qt = d.q_ttl[q];
+    if (qt > 0) { i64 qe = d.in->now_ms + qt; e = (e == 0 || qe < e) ? qe : e; }
+    ds.expire_ms = e;
+    d.ring[d.q_ring_off[q] + (pos & d.q_ring_mask[q])] = ds;
+  } else {
+    atomicAdd(&d.ctr->n_ring_full, 1u);
+    release_msg(d, pb.msg);
+  }
+  if (last) {
+    u64 cnt = rank + 1;
+    d.q_tail[q] = tail + (cnt < freec ? cnt : freec);
+  }
+}
+
+// ============================================================================ K9 acks
+__global__ void k_acks(DS d) {
+  u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+  u32 n = d.ctr->n_acks;
+  if (n > d.ack_max) n = d.ack_max;
+  if (i >= n) return;
+  Ack a = d.acks[i];
+  u32 ch = a.chslot;
+  if (ch == INVALID) return;
+  u64 nt = d.ch_next_tag[ch];
+  u64 tag = a.tag;
+  if (tag == 0 && a.multiple) tag = nt - 1;  // ack everything outstanding
+  bool requeue = (a.kind != CK_ACK) && a.requeue;
+  if (a.multiple) {
+    atomicMax((unsigned long long*)(requeue ? &d.ch_req_upto[ch] : &d.ch_ack_upto[ch]),
+              (unsigned long long)tag);
+  } else if (tag >= d.ch_uhead[ch] && tag < nt) {
+    USlot& u = d.uwin[(u64)ch * (d.ucap_mask + 1) + ((tag - 1) & d.ucap_mask)];
+    atomicCAS(&u.state, (u32)US_PENDING, requeue ? (u32)US_REQUEUE : (u32)US_ACKED);
+  }
+  if (atomicExch(&d.ch_dirty[ch], 1u) == 0) {
+    u32 k = atomicAdd(d.n_dirty, 1u);
+    d.dirty_list[k] = ch;
+  }
+  atomicAdd(&d.ctr->n_acked, 1u);
+}
+
+// one wave per dirty channel: resolve marks, release/requeue, advance the window head
+__global__ __launch_bounds__(256) void k_chan_advance(DS d) {
+  u32 wv = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  u32 lane = lane_id();
+  u32 nd = *d.n_dirty;
+  if (wv >= nd) return;
+  u32 ch = d.dirty_list[wv];
+  u64 head = d.ch_uhead[ch], nt = d.ch_next_tag[ch];
+  u64 aup = d.ch_ack_upto[ch], rup = d.ch_req_upto[ch];
+  USlot* win = d.uwin + (u64)ch * (d.ucap_mask + 1);
+  bool contiguous = true;
+  u64 newhead = head;
+  u32 released = 0;
+  for (u64 t0 = head; t0 < nt; t0 += 64) {
+    u64 t = t0 + lane;
+    bool valid = t < nt;
+    u32 st = US_FREE;
+    USlot u;
+    if (valid) {
+      u = win[(t - 1) & d.ucap_mask];
+      st = u.state;
+      if (st == US_PENDING && t <= aup) st = US_ACKED;
+      if (st == US_PENDING && t <= rup) st = US_REQUEUE;
+      if (st == US_ACKED) {
+        release_msg(d, u.msg);
+        atomicSub(&d.cons_unacked[u.cons], 1u);
+        atomicSub(&d.ch_unacked[ch], 1u);
+        st = US_DONE;
+      } else if (st == US_REQUEUE) {
+        u32 ri = atomicAdd(d.req_n, 1u);
+        if (ri < d.req_max) {
+          ReqItem r;
+          r.q = u.q; r.msg = u.msg; r.qpos = u.qpos; r.expire_ms = u.expire_ms;
+          d.req[ri] = r;
+          atomicAdd(&d.req_q_n[u.q], 1u);
+        } else {
+          release_msg(d, u.msg);  // requeue list overflow: drop (counted)
+        }
+        atomicSub(&d.cons_unacked[u.cons], 1u);
+        atomicSub(&d.ch_unacked[ch], 1u);
+        atomicAdd(&d.ctr->n_requeue, 1u);
+        st = US_DONE;
+      }
+      if (st != u.state) win[(t - 1) & d.ucap_mask].state = st;
+    }
+    if (contiguous) {
+      u64 notdone = __ballot(valid && st != US_DONE);
+      u64 vm = __ballot(valid);
+      u32 adv = notdone ? __ffsll((unsigned long long)notdone) - 1 : __popcll(vm);
+      newhead += adv;
+      released += adv;
+      if (notdone) contiguous = false;
+    }
+  }
+  if (lane == 0) {
+    d.ch_uhead[ch] = newhead;
+    atomicSub(&d.ch_win[ch], released);
+    d.ch_dirty[ch] = 0;
+  }
+}
+
+// ============================================================================ K8 dequeue
+DEV u32 deliver_size(const DS& d, u32 cons, const MsgEnt& m, u32 conn) {
+  u32 mp = 4 + 1 + d.cons_tag_len[cons] + 8 + 1 + 1 + m.ex_len + 1 + m.rk_len;
+  u32 sz = 8 + mp + 8 + 12 + m.props_len;
+  u32 fm = d.conn_frame_max[conn];
+  u32 fmb = fm ? fm - 8 : 0xffffffffu;
+  u32 nb = m.body_len ? (m.body_len + fmb - 1) / fmb : 0;
+  return sz + m.body_len + 8 * nb;
+}
+
+// give back channel reservations for `take` messages not delivered after all
+DEV void unreserve(const DS& d, u32 c, u32 take) {
+  u32 ch = d.cons_ch[c];
+  atomicSub(&d.ch_win[ch], take);
+  if (!d.cons_noack[c]) { atomicSub(&d.ch_unacked[ch], take); d.cons_unacked[c] -= take; }
+}
+
+// one wave per queue: TTL skip, credit-limited round-robin split over consumers,
+// egress byte budget, then descriptors -> Deliv records (sorted by channel later)
+__global__ __launch_bounds__(256) void k_dequeue(DS d) {
+  __shared__ u32 g_cons[4][64];
+  __shared__ u32 g_n[4][64];
+  __shared__ u32 g_off[4][64];
+  u32 w = threadIdx.x >> 6;
+  u32 q = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  u32 lane = lane_id();
+  if (q >= d.q_max || !d.q_active[q]) return;
+  u64 head = d.q_head[q], tail = d.q_tail[q];
+  const u64 mask = d.q_ring_mask[q];
+  const Desc* ring = d.ring + d.q_ring_off[q];
+  const i64 now = d.in->now_ms;
+  // TTL skip at the head (K12)
+  while (head < tail) {
+    u64 idx = head + lane;
+    bool valid = idx < tail;
+    Desc ds;
+    ds.msg = INVALID; ds.expire_ms = 0; ds.flags = 0;
+    if (valid) ds = ring[idx & mask];
+    bool exp = valid && ds.expire_ms != 0 && ds.expire_ms <= now;
+    u64 live = __ballot(valid && !exp);
+    u32 nexp = live ? (__ffsll((unsigned long long)live) - 1) : __popcll(__ballot(valid));
+    if (lane < nexp) { release_msg(d, ds.msg); atomicAdd(&d.ctr->n_expired, 1u); }
+    head += nexp;
+    if (live) break;
+  }
+  u32 mall = d.q_cons_n[q];
+  u64 avail = tail - head;
+  if (mall == 0 || avail == 0) { if (lane == 0) d.q_head[q] = head; return; }
+  u32 m = mall > 64 ? 64 : mall;
+  u32 r = d.q_rr[q] % mall;
+  // (1) counts by credit (lane 0, deterministic consumer order)
+  if (lane == 0) {
+    u64 remaining = avail;
+    for (u32 j = 0; j < m; ++j) {
+      u32 c = d.q_cons[d.q_cons_off[q] + (r + j) % mall];
+      g_cons[w][j] = c;
+      g_n[w][j] = 0;
+      if (remaining == 0) continue;
+      u32 ch = d.cons_ch[c];
+      if (!d.cons_active[c] || !d.ch_flow[ch]) continue;
+      u64 share = (remaining + (m - j) - 1) / (m - j);
+      u32 want = (u32)(share < d.deliver_cap ? share : d.deliver_cap);
+      bool noack = d.cons_noack[c];
+      u32 pc = d.ch_prefetch[ch];
+      if (!noack && pc && !d.ch_global[ch]) {
+        u32 used = d.cons_unacked[c];
+        u32 cr = used < pc ? pc - used : 0;
+        want = want < cr ? want : cr;
+      }
+      u32 wb;
+      u32 g = reserve_upto(&d.ch_win[ch], want, d.ucap_mask + 1, &wb);
+      if (!noack && pc && d.ch_global[ch] && g) {
+        u32 ub;
+        u32 g2 = reserve_upto(&d.ch_unacked[ch], g, pc, &ub);
+        if (g2 < g) atomicSub(&d.ch_win[ch], g - g2);
+        g = g2;
+      } else if (!noack && g) {
+        atomicAdd(&d.ch_unacked[ch], g);
+      }
+      if (!noack && g) d.cons_unacked[c] += g;
+      g_n[w][j] = g;
+      remaining -= g;
+    }
+  }
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  // (2) egress byte budget: trim each consumer's run to what fits this step
+  u64 qp = head;
+  u32 total = 0;
+  for (u32 j = 0; j < m; ++j) {
+    u32 cnt = ((volatile u32*)g_n[w])[j];
+    if (!cnt) continue;
+    u32 c = ((volatile u32*)g_cons[w])[j];
+    u32 conn = d.cons_ch[c] / d.chpc;
+    u32 bytes = 0;
+    for (u32 k0 = 0; k0 < cnt; k0 += 64) {
+      u32 k = k0 + lane;
+      u32 sz = 0;
+      if (k < cnt) sz = deliver_size(d, c, d.msgs[ring[(qp + k) & mask].msg], conn);
+      for (int o = 32; o > 0; o >>= 1) sz += __shfl_xor(sz, o, 64);
+      bytes += sz;
+    }
+    u32 keep = cnt;
+    if (lane == 0) {
+      u32 bb;
+      u32 gb = reserve_upto(d.egress_budget, bytes, (u32)(d.egress_cap > 0xffffffffull ? 0xffffffffu : d.egress_cap), &bb);
+      if (gb < bytes) {
+        // keep the longest prefix that fits in gb bytes
+        u32 acc = 0;
+        keep = 0;
+        for (u32 k = 0; k < cnt; ++k) {
+          u32 sz = deliver_size(d, c, d.msgs[ring[(qp + k) & mask].msg], conn);
+          if (acc + sz > gb) break;
+          acc += sz;
+          ++keep;
+        }
+        if (gb > acc) atomicSub(d.egress_budget, gb - acc);
+        if (keep < cnt) unreserve(d, c, cnt - keep);
+        g_n[w][j] = keep;
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+    keep = ((volatile u32*)g_n[w])[j];
+    qp += keep;
+    total += keep;
+  }
+  // (3) delivery slots
+  if (lane == 0) {
+    u32 db;
+    u32 gt = reserve_upto(&d.ctr->n_deliv, total, d.deliv_max, &db);
+    u32 excess = total - gt;
+    for (int j = (int)m - 1; j >= 0 && excess; --j) {
+      u32 take = g_n[w][j] < excess ? g_n[w][j] : excess;
+      if (!take) continue;
+      unreserve(d, g_cons[w][j], take);
+      g_n[w][j] -= take;
+      excess -= take;
+    }
+    u32 run = db;
+    for (u32 j = 0; j < m; ++j) { g_off[w][j] = run; run += g_n[w][j]; }
+    d.q_rr[q] = (r + 1) % mall;
+  }
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  qp = head;
+  for (u32 j = 0; j < m; ++j) {
+    u32 cnt = ((volatile u32*)g_n[w])[j];
+    if (!cnt) continue;
+    u32 c = ((volatile u32*)g_cons[w])[j];
+    u32 off = ((volatile u32*)g_off[w])[j];
+    u32 ch = d.cons_ch[c];
+    u32 noack = d.cons_noack[c];
+    for (u32 k = lane; k < cnt; k += 64) {
+      Desc ds = ring[(qp + k) & mask];
+      Deliv dv;
+      dv.chslot = ch;
+      dv.cons = c;
+      dv.msg = ds.msg;
+      dv.q = q;
+      dv.qpos = qp + k;
+      dv.expire_ms = ds.expire_ms;
+      dv.tag = 0;
+      dv.flags = (ds.flags & 1) | (noack ? 2u : 0u);
+      dv.size = 0;
+      d.deliv[off + k] = dv;
+      d.dv_k[0][off + k] = ch;
+      d.dv_v[0][off + k] = off + k;
+    }
+    qp += cnt;
+  }
+  if (lane == 0) d.q_head[q] = qp;
+}
+
+// ============================================================================ tags + sizes
+__global__ void k_dfirst(DS d, u32 src) {
+  u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+  u32 n = d.ctr->n_deliv;
+  if (i >= n) return;
+  const u32* k = d.dv_k[src];
+  u32 ch = k[i];
+  if (i == 0 || k[i - 1] != ch) d.ch_first[ch] = i;
+  u32 conn = ch / d.chpc;
+  if (i == 0 || (k[i - 1] / d.chpc) != conn) d.conn_dfirst[conn] = i;
+  if (i + 1 == n || (k[i + 1] / d.chpc) != conn) d.conn_dlast[conn] = i;
+}
+
+__global__ void k_tags(DS d, u32 src) {
+  u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+  u32 n = d.ctr->n_deliv;
+  if (i >= d.deliv_max) return;
+  if (i >= n) { d.dv_size[i] = 0; return; }
+  const u32* kk = d.dv_k[src];
+  u32 ch = kk[i];
+  u32 di = d.dv_v[src][i];
+  Deliv& dv = d.deliv[di];
+  u32 rank = i - d.ch_first[ch];
+  u64 tag = d.ch_next_tag[ch] + rank;
+  bool last = (i + 1 == n) || kk[i + 1] != ch;
+  USlot u;
+  u.state = (dv.flags & 2) ? US_DONE : US_PENDING;
+  u.msg = dv.msg;
+  u.q = dv.q;
+  u.cons = dv.cons;
+  u.qpos = dv.qpos;
+  u.expire_ms = dv.expire_ms;
+  d.uwin[(u64)ch * (d.ucap_mask + 1) + ((tag - 1) & d.ucap_mask)] = u;
+  const MsgEnt& m = d.msgs[dv.msg];
+  u32 conn = ch / d.chpc;
+  u32 sz = deliver_size(d, dv.cons, m, conn);
+  dv.size = sz;
+  d.dv_size[i] = sz;
+  dv.tag = tag;
+  u32 lat = (u32)d.in->step - m.pub_step;
+  atomicAdd(&d.ctr->lat_hist[lat < LAT_BINS ? lat : LAT_BINS - 1], 1u);
+  if (last) {
+    if (atomicExch(&d.ch_dirty[ch], 1u) == 0) {
+      u32 k = atomicAdd(d.n_dirty, 1u);
+      d.dirty_list[k] = ch;
+    }
+  }
+}
+
+// per connection: egress size = returns + confirms + deliveries
+__global__ void k_conn_sizes(DS d) {
+  u32 c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= d.c_max) return;
+  u32 conf = 0;
+  for (u32 l = 0; l < d.chpc; ++l) {
+    u32 ch = c * d.chpc + l;
+    if (d.ch_pub_cnt[ch] && d.ch_confirm[ch]) conf += 21;
+  }
+  d.conn_conf_bytes[c] = conf;
+  u32 dl = 0;
+  u32 f = d.conn_dfirst[c];
+  if (f != INVALID) {
+    u32 l = d.conn_dlast[c];
+    dl = d.dv_off[l] + d.dv_size[l] - d.dv_off[f];
+  }
+  d.conn_total[c] = d.conn_ret_bytes[c] + conf + dl;
+}
+
+__global__ void k_conn_out(DS d) {
+  u32 c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= d.c_max) return;
+  ConnOut o;
+  o.off = d.conn_base[c];
+  o.len = d.conn_total[c];
+  d.conn_out[c] = o;
+  if (c == d.c_max - 1) d.ctr->egress_bytes = o.off + o.len;
+}
+
+// ============================================================================ K5 render
+DEV u32 put_frame_hdr(u8* o, u32 type, u32 ch, u32 size) {
+  o[0] = (u8)type;
+  wr16(o + 1, ch);
+  wr32(o + 3, size);
+  return 7;
+}
+
+// one wave per delivery
+__global__ __launch_bounds__(256) void k_render_deliv(DS d, u32 src) {
+  u32 i = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  u32 lane = lane_id();
+  u32 n = d.ctr->n_deliv;
+  if (i >= n) return;
+  u32 ch = d.dv_k[src][i];
+  const Deliv dv = d.deliv[d.dv_v[src][i]];
+  const MsgEnt m = d.msgs[dv.msg];
+  u32 conn = ch / d.chpc;
+  u32 f = d.conn_dfirst[conn];
+  u64 off = (u64)d.conn_base[conn] + d.conn_ret_bytes[conn] + d.conn_conf_bytes[conn] + d.dv_off[i] -
+            d.dv_off[f];
+  if (off + dv.size > d.egress_cap) return;  // never: dequeue reserves an egress byte budget
+  u8* o = d.egress + off;
+  const u8* slot = d.log + (m.log_off % d.log_bytes);
+  u32 chno = d.ch_num[ch];
+  u32 taglen = d.cons_tag_len[dv.cons];
+  u32 mp = 4 + 1 + taglen + 8 + 1 + 1 + m.ex_len + 1 + m.rk_len;
+  u64 dtag = dv.tag;
+  if (lane == 0) {
+    u32 p = 0;
+    p += put_frame_hdr(o + p, 1, chno, mp);
+    wr16(o + p, 60); wr16(o + p + 2, 60); p += 4;
+    o[p++] = (u8)taglen;
+    const u8* tg = d.tpool + d.cons_tag_off[dv.cons];
+    for (u32 k = 0; k < taglen; ++k) o[p + k] = tg[k];
+    p += taglen;
+    wr64(o + p, dtag); p += 8;
+    o[p++] = (dv.flags & 1) ? 1 : 0;
+    o[p++] = m.ex_len;
+    for (u32 k = 0; k < m.ex_len; ++k) o[p + k] = slot[k];
+    p += m.ex_len;
+    o[p++] = m.rk_len;
+    for (u32 k = 0; k < m.rk_len; ++k) o[p + k] = slot[m.ex_len + k];
+    p += m.rk_len;
+    o[p++] = 0xCE;
+    p += put_frame_hdr(o + p, 2, chno, 12 + m.props_len);
+    wr16(o + p, 60); wr16(o + p + 2, 0); wr64(o + p + 4, m.body_len); p += 12;
+    (void)p;
+  }
+  u32 hp = 8 + mp + 7 + 12;
+  wave_copy(o + hp, slot + m.ex_len + m.rk_len, m.props_len);
+  if (lane == 0) o[hp + m.props_len] = 0xCE;
+  u32 bp = hp + m.props_len + 1;
+  u32 fm = d.conn_frame_max[conn];
+  u32 fmb = fm ? fm - 8 : 0xffffffffu;
+  const u8* body = slot + m.body_off;
+  for (u32 b0 = 0; b0 < m.body_len; b0 += fmb) {
+    u32 bl = m.body_len - b0 < fmb ? m.body_len - b0 : fmb;
+    if (lane == 0) put_frame_hdr(o + bp, 3, chno, bl);
+    wave_copy(o + bp + 7, body + b0, bl);
+    if (lane == 0) o[bp + 7 + bl] = 0xCE;
+    bp += bl + 8;
+  }
+}
+
+// confirms: one thread per connection writes its channels' coalesced Basic.Ack frames
+__global__ void k_render_confirms(DS d) {
+  u32 c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= d.c_max) return;
+  u32 conf = d.conn_conf_bytes[c];
+  u8* o = d.egress + (u64)d.conn_base[c] + d.conn_ret_bytes[c];
+  u32 p = 0;
+  for (u32 l = 0; l < d.chpc; ++l) {
+    u32 ch = c * d.chpc + l;
+    u32 cnt = d.ch_pub_cnt[ch];
+    if (!cnt) continue;
+    d.ch_pub_cnt[ch] = 0;
+    if (!d.ch_confirm[ch]) continue;
+    u64 last = d.ch_confirm_next[ch] + cnt - 1;
+    d.ch_confirm_next[ch] = last + 1;
+    u32 chno = d.ch_num[ch];
+    if (p + 21 > conf) break;
+    put_frame_hdr(o + p, 1, chno, 13);
+    wr16(o + p + 7, 60); wr16(o + p + 9, 80);
+    wr64(o + p + 11, last);
+    o[p + 19] = cnt > 1 ? 1 : 0;
+    o[p + 20] = 0xCE;
+    p += 21;
+    atomicAdd(&d.ctr->n_confirm_frames, 1u);
+  }
+}
+
+// returns: one wave per returned publish (Basic.Return 312/313 + header + body)
+__global__ __launch_bounds__(256) void k_render_returns(DS d) {
+  u32 i = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  u32 lane = lane_id();
+  u32 n = d.ctr->n_returns;
+  if (n > d.pub_max) n = d.pub_max;
+  if (i >= n) return;
+  u32 p = d.ret_list[i];
+  const Pub pb = d.pubs[p];
+  u32 code = d.pub_ret[p];
+  u8* o = d.egress + (u64)d.conn_base[pb.conn] + pb.pad;
+  const u8* w = d.work;
+  // channel number from the publish command's frame
+  u32 chno = d.ch_num[pb.chslot];
+  const char* txt = code == 312 ? "The exchange cannot route the result of a Publish"
+                                : "The exchange cannot deliver to a consumer when the immediate flag is set";
+  u32 tl = 0;
+  while (txt[tl]) ++tl;
+  u32 mp = 4 + 2 + 1 + tl + 1 + pb.ex_len + 1 + pb.rk_len;
+  if (lane == 0) {
+    u32 q = 0;
+    q += put_frame_hdr(o, 1, chno, mp);
+    wr16(o + q, 60); wr16(o + q + 2, 50); q += 4;
+    wr16(o + q, code); q += 2;
+    o[q++] = (u8)tl;
+    for (u32 k = 0; k < tl; ++k) o[q + k] = (u8)txt[k];
+    q += tl;
+    o[q++] = (u8)pb.ex_len;
+    for (u32 k = 0; k < pb.ex_len; ++k) o[q + k] = w[pb.ex_off + k];
+    q += pb.ex_len;
+    o[q++] = (u8)pb.rk_len;
+    for (u32 k = 0; k < pb.rk_len; ++k) o[q + k] = w[pb.rk_off + k];
+    q += pb.rk_len;
+    o[q++] = 0xCE;
+    q += put_frame_hdr(o + q, 2, chno, 12 + pb.props_len);
+    wr16(o + q, 60); wr16(o + q + 2, 0); wr64(o + q + 4, pb.body_size);
+  }
+  u32 hp = 8 + mp + 7 + 12;
+  wave_copy(o + hp, w + pb.props_off, pb.props_len);
+  if (lane == 0) o[hp + pb.props_len] = 0xCE;
+  u32 bp = hp + pb.props_len + 1;
+  u32 fm = d.conn_frame_max[pb.conn];
+  u32 fmb = fm ? fm - 8 : 0xffffffffu;
+  // body from ingress fragments, re-split at the connection's frame size
+  u32 fi = 0, fo = 0;
+  for (u32 b0 = 0; b0 < pb.body_size; b0 += fmb) {
+    u32 bl = pb.body_size - b0 < fmb ? pb.body_size - b0 : fmb;
+    if (lane == 0) put_frame_hdr(o + bp, 3, chno, bl);
+    u32 done = 0;
+    while (done < bl) {
+      Frag fg = d.frags[pb.frag0 + fi];
+      u32 take = fg.len - fo < bl - done ? fg.len - fo : bl - done;
+      wave_copy(o + bp + 7 + done, w + fg.off + fo, take);
+      done += take;
+      fo += take;
+      if (fo == fg.len) { ++fi; fo = 0; }
+    }
+    if (lane == 0) o[bp + 7 + bl] = 0xCE;
+    bp += bl + 8;
+  }
+}
+
+// ============================================================================ post / final
+__global__ void k_post(DS d, u32 src) {
+  u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+  u32 n = d.ctr->n_deliv;
+  if (i < n) {
+    const Deliv& dv = d.deliv[d.dv_v[src][i]];
+    if (dv.flags & 2) release_msg(d, dv.msg);
+    const u32* kk = d.dv_k[src];
+    u32 ch = kk[i];
+    if (i + 1 == n || kk[i + 1] != ch) d.ch_next_tag[ch] = dv.tag + 1;
+  }
+  // reset per-connection scratch
+  if (i < d.c_max) {
+    d.conn_dfirst[i] = INVALID;
+    d.conn_dlast[i] = INVALID;
+  }
+}
+
+__global__ void k_post2(DS d) {
+  u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < d.c_max) d.conn_ret_bytes[i] = 0;
+}
+
+__global__ void k_final(DS d) {
+  if (threadIdx.x != 0) return;
+  // advance the log tail over fully released blocks (K11)
+  u64 head = *d.log_head, tail = *d.log_tail;
+  while (tail < head) {
+    u64 blk_idx = tail / d.log_block;
+    if (blk_idx == head / d.log_block) break;
+    if (d.log_live[blk_idx % d.n_log_blocks] > 0) break;
+    tail = (blk_idx + 1) * d.log_block;
+  }
+  if (tail > head) tail = head;
+  *d.log_tail = tail;
+  *d.id_next = *d.id_next + d.tot[2];
+  *d.n_dirty = 0;
+  Counters* c = d.ctr;
+  c->log_head = head;
+  c->log_tail = tail;
+  c->msg_free_top = *d.msg_free_top;
+  c->n_live_msgs = d.msg_max - *d.msg_free_top;
+  *d.ctr_host = *c;
+}
+
+// ============================================================================ requeue (pre-step)
+// one block per queue with requeued items: gather, bitonic-sort by queue position,
+// push back in front of the head with the redelivered flag (QueueEntity.scala:415-446)
+#define REQ_BLK 1024
+__global__ __launch_bounds__(256) void k_requeue(DS d) {
+  __shared__ u64 kpos[REQ_BLK];
+  __shared__ u32 kidx[REQ_BLK];
+  __shared__ u32 cnt;
+  u32 q = blockIdx.x;
+  if (q >= d.q_max || d.req_q_n[q] == 0) return;
+  u32 tid = threadIdx.x;
+  if (tid == 0) cnt = 0;
+  __syncthreads();
+  u32 n = *d.req_n;
+  if (n > d.req_max) n = d.req_max;
+  for (u32 i = tid; i < n; i += 256) {
+    if (d.req[i].q == q) {
+      u32 k = atomicAdd(&cnt, 1u);
+      if (k < REQ_BLK) { kpos[k] = d.req[i].qpos; kidx[k] = i; }
+    }
+  }
+  __syncthreads();
+  u32 m = cnt < REQ_BLK ? cnt : REQ_BLK;
+  u32 np2 = 1;
+  while (np2 < m) np2 <<= 1;
+  for (u32 i = m + tid; i < np2; i += 256) { kpos[i] = ~0ull; kidx[i] = INVALID; }
+  __syncthreads();
+  for (u32 k = 2; k <= np2; k <<= 1) {
+    for (u32 j = k >> 1; j > 0; j >>= 1) {
+      for (u32 i = tid; i < np2; i += 256) {
+        u32 ij = i ^ j;
+        if (ij > i) {
+          bool up = (i & k) == 0;
+          if ((kpos[i] > kpos[ij]) == up) {
+            u64 t = kpos[i]; kpos[i] = kpos[ij]; kpos[ij] = t;
+            u32 x = kidx[i]; kidx[i] = kidx[ij]; kidx[ij] = x;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+  u64 head = d.q_head[q], tail = d.q_tail[q];
+  u64 mask = d.q_ring_mask[q];
+  u64 freec = mask + 1 - (tail - head);
+  u32 k = m < freec ? m : (u32)freec;
+  for (u32 i = tid; i < k; i += 256) {
+    const ReqItem r = d.req[kidx[i]];
+    Desc ds;
+    ds.msg = r.msg;
+    ds.flags = 1;
+    ds.expire_ms = r.expire_ms;
+    d.ring[d.q_ring_off[q] + ((head - k + i) & mask)] = ds;
+    d.req[kidx[i]].q = INVALID;  // consumed
+  }
+  __syncthreads();
+  if (tid == 0) {
+    d.q_head[q] = head - k;
+    d.req_q_n[q] -= k;
+  }
+}
+
+__global__ void k_requeue_compact(DS d) {
+  // single block: compact the remaining (unconsumed) requeue items
+  __shared__ u32 lds[1024 / 64 + 1];
+  u32 n = *d.req_n;
+  if (n > d.req_max) n = d.req_max;
+  u32 run = 0;
+  for (u32 b0 = 0; b0 < n; b0 += 1024) {
+    u32 i = b0 + threadIdx.x;
+    ReqItem r;
+    r.q = INVALID;
+    if (i < n) r = d.req[i];
+    u32 keep = (i < n && r.q != INVALID) ? 1 : 0;
+    u32 all;
+    u32 off = block_scan<1024>(keep, lds, all);
+    __syncthreads();
+    if (keep) d.req[run + off] = r;  // run + off <= i: safe forward compaction
+    __syncthreads();
+    run += all;
+  }
+  if (threadIdx.x == 0) *d.req_n = run;
+}

@@ -1,0 +1,185 @@
+// Shared device/host definitions for the MI355X AMQP data plane.
+// Layouts here are mirrored by chanamq_amd/engine/layout.py (numpy dtypes);
+// tests/test_layout.py checks sizes/offsets.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+typedef uint8_t u8;
+typedef uint16_t u16;
+typedef uint32_t u32;
+typedef uint64_t u64;
+typedef int32_t i32;
+typedef int8_t i8;
+typedef int64_t i64;
+
+#define DEV __device__ __forceinline__
+
+// ---- command kinds (data-plane classification of an assembled command)
+enum : u32 {
+  CK_NONE = 0,
+  CK_PUBLISH = 1,   // Basic.Publish (60/40)
+  CK_ACK = 2,       // Basic.Ack (60/80)
+  CK_REJECT = 3,    // Basic.Reject (60/90)
+  CK_NACK = 4,      // Basic.Nack (60/120)
+  CK_CONTROL = 5,   // everything else: bytes go to the host control plane
+};
+
+// ---- exchange types (constants.py EX_*)
+enum : u32 { EX_DIRECT = 0, EX_FANOUT = 1, EX_TOPIC = 2, EX_HEADERS = 3 };
+
+// ---- per-segment status bits (SegOut.status)
+enum : u32 {
+  SS_OK = 0,
+  SS_PAUSED = 1,        // connection paused behind a control command
+  SS_CTRL = 2,          // a control command was emitted (connection now paused)
+  SS_FRAME_ERROR = 4,   // malformed frame (501); host closes connection
+  SS_UNEXPECTED = 8,    // frame sequence error (505)
+  SS_TOO_LARGE = 16,    // command exceeds carry capacity (host fallback)
+  SS_OVERFLOW = 32,     // per-step capacity hit; remainder carried
+  SS_CHANNEL = 64,      // data command on a channel the device does not know (sent as control)
+};
+
+// ---- message flags
+enum : u32 { MF_PERSIST = 1, MF_MANDATORY = 2, MF_IMMEDIATE = 4, MF_HAS_TS = 8 };
+
+// ---- unacked slot states
+enum : u32 { US_FREE = 0, US_PENDING = 1, US_ACKED = 2, US_REQUEUE = 3, US_DONE = 4 };
+
+struct SegIn {          // host -> device, one per connection with bytes this step
+  u32 conn;
+  u32 len;              // new bytes
+  u64 src;              // offset of the new bytes in the ingress payload
+};
+
+struct StepIn {         // host -> device per step (64 B)
+  u32 nseg;
+  u32 flags;
+  i64 now_ms;
+  u64 step;
+  u64 id_ms;            // epoch ms for snowflake ids
+  u32 worker;           // snowflake worker id (rank)
+  u32 pad0;
+  u64 pad[3];
+};
+
+struct SegOut {         // device -> host per segment
+  u32 conn;
+  u32 status;
+  u32 consumed;         // bytes of the virtual segment consumed
+  u32 carry;            // carry length after this step
+  u32 ncmds;
+  u32 err_off;          // offset of the first malformed frame
+  u32 pad[2];
+};
+
+struct Cmd {            // one assembled command (device internal)
+  u32 conn;
+  u32 ch;               // channel number
+  u32 kind;
+  u32 m_off;            // method payload offset in work buffer (absolute)
+  u32 m_len;
+  u32 h_off;            // content-header payload offset
+  u32 h_len;
+  u32 frag0;            // first body fragment
+  u32 nfrag;
+  u32 body_size;
+  u32 seg;
+  u32 raw_off;          // first byte of the command's first frame (for control copies)
+  u32 raw_len;
+  u32 pad[3];
+};
+
+struct Frag { u32 off, len; };
+
+struct Pub {            // decoded Basic.Publish
+  u32 conn;
+  u32 chslot;           // -1 if unknown
+  i32 exch;             // exchange slot, -1 unknown
+  u32 rk_off;           // routing key bytes in work buffer
+  u32 rk_len;
+  u32 ex_off;           // exchange name bytes in work buffer
+  u32 ex_len;
+  u32 props_off;        // property bytes (flags + values) in work buffer
+  u32 props_len;
+  u32 frag0, nfrag;
+  u32 body_size;
+  u32 flags;            // MF_*
+  u32 nwords;           // routing-key word count (topic)
+  i64 expire_ms;        // absolute, 0 = never
+  i64 ts_ms;
+  u64 keyhash;          // fnv1a64(routing key)
+  u32 nq;               // queues routed to
+  u32 slot_bytes;       // bytes reserved in the body log
+  u32 msg;              // message-table index, -1 if not stored
+  u32 pad;
+};
+
+struct Ack { u32 chslot; u32 kind; u64 tag; u32 multiple; u32 requeue; };
+
+struct MsgEnt {         // message table (one per stored message; body stored once per rank)
+  u64 log_off;          // start of slot in body log
+  u64 msg_id;           // snowflake id
+  i64 ts_ms;
+  u32 slot_bytes;
+  u32 body_len;
+  u32 body_off;         // offset of body inside the slot (16-aligned)
+  u16 props_len;
+  u8 ex_len;
+  u8 rk_len;
+  i32 refcnt;
+  u32 flags;
+  u32 pub_step;         // step the message was published (latency histogram)
+  u32 pad;
+};
+
+struct Desc {           // queue ring entry
+  u32 msg;
+  u32 flags;            // bit0 redelivered
+  i64 expire_ms;
+};
+
+struct Deliv {          // one delivery produced by the dequeue kernel
+  u32 chslot;
+  u32 cons;
+  u32 msg;
+  u32 q;
+  u64 qpos;             // queue position (for requeue ordering)
+  i64 expire_ms;
+  u64 tag;              // delivery tag (assigned in k_tags)
+  u32 flags;            // bit0 redelivered, bit1 autoack
+  u32 size;             // rendered bytes
+};
+
+struct USlot {          // per-channel unacked window slot
+  u32 state;
+  u32 msg;
+  u32 q;
+  u32 cons;
+  u64 qpos;
+  i64 expire_ms;
+};
+
+struct ReqItem { u32 q; u32 msg; u64 qpos; i64 expire_ms; };
+
+struct Counters {       // per-step counters (device -> host)
+  u32 n_cmds, n_frags, n_pubs, n_acks;
+  u32 n_ctrl, ctrl_bytes, n_pairs, n_deliv;
+  u32 egress_bytes, n_returns, n_confirm_frames, n_freed;
+  u32 n_requeue, n_unroutable, n_dropped_nomem, n_expired;
+  u32 n_routed_msgs, n_unknown_exchange, n_ring_full, n_acked;
+  u32 lat_hist[32];     // deliveries by (deliver_step - publish_step), last bin = overflow
+  u64 log_head, log_tail;
+  u32 msg_free_top, n_live_msgs;
+  u32 pad[6];
+};
+
+struct CtrlRec { u32 conn; u32 off; u32 len; u32 seg; };
+
+struct ConnOut { u32 off; u32 len; };
+
+// ---- FNV-1a 64 (host mirror: chanamq_amd/engine/layout.py fnv1a64)
+DEV u64 fnv1a64_dev(const u8* p, u32 n, u64 h = 0xcbf29ce484222325ULL) {
+  for (u32 i = 0; i < n; ++i) { h ^= p[i]; h *= 0x100000001b3ULL; }
+  return h;
+}

@@ -1,0 +1,160 @@
+// Device-state descriptor passed by value to every data-plane kernel.
+// All arrays are allocated once by Engine (engine.cpp) and sized from EngineCfg;
+// nothing is allocated on the step path, so the whole step is hipGraph-capturable.
+#pragma once
+#include "dp_common.h"
+
+#define CAND_MAX 8192         // frame candidates per segment held in LDS
+#define SORT_TILE 4096        // radix-sort tile (256 threads x 16)
+#define TOPIC_K 256           // topic key vector: 8 words x 32 hash bits (int8 +-1)
+#define TOPIC_WORDS 8
+#define LAT_BINS 32
+
+struct DS {
+  // ---------------- sizes
+  u32 c_max, chpc, q_max, x_max, cons_max, seg_max;
+  u32 carry_cap, cmd_max, frag_max, pub_max, ack_max, pair_max, deliv_max, msg_max;
+  u32 ucap_mask, deliver_cap, chmap_size, xhash_mask, dhash_mask, tb_max, tb_pad, req_max;
+  u32 q_bits, ch_bits, hash_wildcard, pad_;
+  u64 log_bytes, log_block, n_log_blocks, work_cap, ingress_cap, egress_cap, ctrl_cap, ring_pool;
+
+  // ---------------- step io
+  StepIn* in;
+  const SegIn* segs;
+  const u8* ingress;
+  SegOut* seg_out;          // host-mapped
+  Counters* ctr;            // device
+  Counters* ctr_host;       // host-mapped
+  u8* egress;               // host-mapped
+  ConnOut* conn_out;        // host-mapped [c_max]
+  u8* ctrl;                 // host-mapped
+  CtrlRec* ctrl_rec;        // host-mapped [seg_max * 2]
+
+  // ---------------- per connection
+  u8* carry;                // [c_max][carry_cap]
+  u32* carry_len;           // [c_max]
+  u32* conn_paused;
+  u32* conn_frame_max;
+  u32* conn_vhost;
+  i64* conn_last_rx;
+  u32* chmap;               // [c_max][chmap_size]: (ch<<16)|0x8000|local, 0 = empty
+  u32* conn_ret_bytes;      // per step (reset by renderer)
+  u32* conn_conf_bytes;
+  u32* conn_dfirst;         // first sorted delivery of the connection (0xffffffff none)
+  u32* conn_dlast;
+  u32* conn_total;
+  u32* conn_base;
+
+  // ---------------- per segment / work
+  u32* seg_start;
+  u32* seg_total;
+  u8* work;
+
+  // ---------------- commands
+  Cmd* cmds;
+  Frag* frags;
+  u32* cmd_is_pub;
+  u32* cmd_is_ack;
+  u32* cmd_pub_rank;
+  u32* cmd_ack_rank;
+
+  // ---------------- publishes
+  Pub* pubs;
+  i8* pub_keyvec;           // [pub_max][TOPIC_K]
+  u16* pub_match;           // [pub_max][tb_pad/16]
+  u32* pub_nq;
+  u32* pub_slot;
+  u32* pub_routed;
+  u32* pub_pair_off;
+  u32* pub_slot_off;
+  u32* pub_routed_rank;
+  u32* pub_ret;             // 0 / 312 / 313
+  u32* ret_list;            // pub indices with returns
+  Ack* acks;
+
+  // ---------------- pairs (msg -> queue), radix-sorted by queue
+  u32* pair_k[2];
+  u32* pair_v[2];
+  u32* q_first;             // [q_max] scratch (0xffffffff)
+
+  // ---------------- exchanges / bindings (replicated, uploaded by host)
+  u64* x_hkey;              // [xhash] exchange-name hash
+  i32* x_hval;              // [xhash] exchange slot
+  u32* x_type;
+  u32* x_fan_off; u32* x_fan_n;
+  u32* x_t_off; u32* x_t_n;
+  u32* fan_q;               // fanout queue lists (sorted, unique)
+  u64* d_key;               // [dhash] direct binding hash (keyhash ^ exch*K)
+  i32* d_exch;              // [dhash] -1 empty
+  u32* d_kb_off; u32* d_kb_len;
+  u32* d_q_off; u32* d_q_n;
+  u32* d_q;                 // direct queue lists
+  u8* kpool;                // key/pattern bytes
+  u32* t_queue; u32* t_exch; u32* t_kb_off; u32* t_kb_len; u32* t_flags; i32* t_expect;
+  i8* t_mat;                // [tb_pad][TOPIC_K]
+
+  // ---------------- queues
+  u64* q_ring_off;          // offset into ring pool
+  u64* q_ring_mask;
+  u64* q_head;
+  u64* q_tail;
+  i64* q_ttl;
+  u32* q_cons_off; u32* q_cons_n; u32* q_rr; u32* q_active;
+  u32* q_cons;              // consumer ids per queue (CSR)
+  Desc* ring;               // ring pool
+
+  // ---------------- channels
+  u32* ch_confirm;
+  u32* ch_pub_cnt;
+  u64* ch_confirm_next;
+  u64* ch_next_tag;
+  u64* ch_uhead;
+  u64* ch_ack_upto;
+  u64* ch_req_upto;
+  u32* ch_prefetch;
+  u32* ch_global;
+  u32* ch_flow;
+  u32* ch_num;              // AMQP channel number of the slot
+  u32* ch_unacked;          // outstanding manual-ack deliveries (global prefetch)
+  u32* ch_win;              // window slots in use (reserved)
+  u32* ch_dirty;
+  u32* dirty_list;
+  u32* n_dirty;
+  USlot* uwin;              // [chslots][ucap]
+
+  // ---------------- consumers
+  u32* cons_q; u32* cons_ch; u32* cons_noack; u32* cons_active; u32* cons_unacked;
+  u32* cons_tag_off; u32* cons_tag_len;
+  u8* tpool;                // consumer-tag bytes
+
+  // ---------------- messages
+  MsgEnt* msgs;
+  u32* msg_free;            // free index stack
+  u32* msg_free_top;
+  u8* log;
+  u64* log_head;
+  u64* log_tail;
+  u64* log_step_base;
+  i64* log_live;            // live bytes per log block
+  u64* id_next;             // snowflake virtual sequence position
+
+  // ---------------- deliveries
+  Deliv* deliv;
+  u32* dv_k[2];
+  u32* dv_v[2];
+  u32* dv_size;             // by sorted position
+  u32* dv_off;
+  u32* ch_first;            // [chslots] scratch
+
+  // ---------------- requeue
+  ReqItem* req;
+  u32* req_n;
+  u32* req_q_n;             // per queue count
+
+  // ---------------- scratch
+  u32* scan_tmp;            // block sums
+  u32* hist;                // radix histograms
+  u32* hist_scan;
+  u32* tot;                 // scan totals [64]
+  u32* egress_budget;       // bytes reserved by dequeue this step
+};

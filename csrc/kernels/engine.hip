@@ -1,0 +1,543 @@
+// Native host runtime for the MI355X data plane: owns every device/host-mapped
+// buffer, launches the step pipeline on a caller-supplied HIP stream and captures
+// it once into a hipGraph (steady-state deliver loop = one hipGraphLaunch).
+//
+// Python sees a pybind11 module `_dataplane` with class Engine (chanamq_amd/ops).
+#include <pybind11/pybind11.h>
+#include <pybind11/numpy.h>
+#include <pybind11/stl.h>
+
+#include <map>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "dataplane.hip"
+
+namespace py = pybind11;
+
+#define HIPCHECK(x)                                                                  \
+  do {                                                                               \
+    hipError_t _e = (x);                                                             \
+    if (_e != hipSuccess)                                                            \
+      throw std::runtime_error(std::string(#x) + ": " + hipGetErrorString(_e));      \
+  } while (0)
+
+static u32 ceil_div(u64 a, u64 b) { return (u32)((a + b - 1) / b); }
+static u32 next_pow2(u32 x) { u32 p = 1; while (p < x) p <<= 1; return p; }
+static u32 bits_for(u64 maxval) { u32 b = 0; while ((1ull << b) <= maxval) ++b; return b; }
+
+struct Buf {
+  void* ptr = nullptr;
+  size_t bytes = 0;
+  bool host = false;
+};
+
+class Engine {
+ public:
+  explicit Engine(py::dict cfg) {
+    auto get = [&](const char* k, u64 dflt) -> u64 {
+      return cfg.contains(k) ? cfg[k].cast<u64>() : dflt;
+    };
+    device_ = (int)get("device", 0);
+    HIPCHECK(hipSetDevice(device_));
+    d_ = DS{};
+    d_.c_max = (u32)get("c_max", 1024);
+    d_.chpc = next_pow2((u32)get("chpc", 16));
+    d_.q_max = (u32)get("q_max", 4096);
+    d_.x_max = (u32)get("x_max", 1024);
+    d_.cons_max = (u32)get("cons_max", 16384);
+    d_.seg_max = (u32)get("seg_max", 1024);
+    d_.carry_cap = (u32)get("carry_cap", 1u << 20);
+    d_.cmd_max = (u32)get("cmd_max", 65536);
+    d_.frag_max = (u32)get("frag_max", d_.cmd_max * 2);
+    d_.pub_max = d_.cmd_max;
+    d_.ack_max = d_.cmd_max;
+    d_.pair_max = (u32)get("pair_max", d_.cmd_max * 4);
+    d_.deliv_max = (u32)get("deliv_max", 65536);
+    d_.msg_max = (u32)get("msg_max", 1u << 22);
+    u32 ucap = next_pow2((u32)get("ucap", 8192));
+    d_.ucap_mask = ucap - 1;
+    d_.deliver_cap = (u32)get("deliver_cap", 4096);
+    d_.chmap_size = next_pow2(d_.chpc * 2);
+    u32 xhash = next_pow2(d_.x_max * 2);
+    d_.xhash_mask = xhash - 1;
+    u32 dhash = next_pow2((u32)get("dhash", 65536));
+    d_.dhash_mask = dhash - 1;
+    d_.tb_max = (u32)get("tb_max", 4096);
+    d_.tb_pad = ((d_.tb_max + 15) / 16) * 16;
+    d_.req_max = (u32)get("req_max", 65536);
+    d_.hash_wildcard = (u32)get("hash_wildcard", 1);
+    d_.log_bytes = get("log_bytes", 1ull << 32);
+    d_.log_block = get("log_block", 4ull << 20);
+    d_.log_bytes = (d_.log_bytes / d_.log_block) * d_.log_block;
+    d_.n_log_blocks = d_.log_bytes / d_.log_block;
+    d_.ingress_cap = get("ingress_cap", 64ull << 20);
+    d_.work_cap = d_.ingress_cap + (u64)d_.seg_max * (d_.carry_cap + 64);
+    d_.work_cap = d_.work_cap > (3ull << 30) ? (3ull << 30) : d_.work_cap;  // u32 offsets
+    d_.egress_cap = get("egress_cap", 96ull << 20);
+    d_.ctrl_cap = get("ctrl_cap", 4ull << 20);
+    d_.ring_pool = get("ring_pool", 1ull << 26);
+    u32 fan_max = (u32)get("fan_max", 1u << 20);
+    u32 dq_max = (u32)get("dq_max", 1u << 20);
+    u64 kpool = get("kpool", 16ull << 20);
+    u32 nch = d_.c_max * d_.chpc;
+    d_.q_bits = bits_for(d_.q_max);
+    d_.ch_bits = bits_for(nch);
+    graph_enabled_ = get("graph", 1) != 0;
+
+    // ---- allocations
+    auto dev = [&](const char* name, size_t bytes) { return alloc(name, bytes, false); };
+    auto hst = [&](const char* name, size_t bytes) { return alloc(name, bytes, true); };
+    d_.in = (StepIn*)dev("in", sizeof(StepIn));
+    d_.segs = (const SegIn*)dev("segs", sizeof(SegIn) * d_.seg_max);
+    d_.ingress = (const u8*)dev("ingress", d_.ingress_cap + 64);
+    d_.seg_out = (SegOut*)hst("seg_out", sizeof(SegOut) * d_.seg_max);
+    d_.ctr = (Counters*)dev("ctr", sizeof(Counters));
+    d_.ctr_host = (Counters*)hst("ctr_host", sizeof(Counters));
+    egress_alloc_ = d_.egress_cap + d_.work_cap + (u64)nch * 21 + 4096;
+    d_.egress = (u8*)hst("egress", egress_alloc_);
+    d_.conn_out = (ConnOut*)hst("conn_out", sizeof(ConnOut) * d_.c_max);
+    d_.ctrl = (u8*)hst("ctrl", d_.ctrl_cap);
+    d_.ctrl_rec = (CtrlRec*)hst("ctrl_rec", sizeof(CtrlRec) * d_.seg_max * 2);
+
+    d_.carry = (u8*)dev("carry", (u64)d_.c_max * d_.carry_cap + 64);
+    d_.carry_len = (u32*)dev("carry_len", 4ull * d_.c_max);
+    d_.conn_paused = (u32*)dev("conn_paused", 4ull * d_.c_max);
+    d_.conn_frame_max = (u32*)dev("conn_frame_max", 4ull * d_.c_max);
+    d_.conn_vhost = (u32*)dev("conn_vhost", 4ull * d_.c_max);
+    d_.conn_last_rx = (i64*)dev("conn_last_rx", 8ull * d_.c_max);
+    d_.chmap = (u32*)dev("chmap", 4ull * d_.c_max * d_.chmap_size);
+    d_.conn_ret_bytes = (u32*)dev("conn_ret_bytes", 4ull * d_.c_max);
+    d_.conn_conf_bytes = (u32*)dev("conn_conf_bytes", 4ull * d_.c_max);
+    d_.conn_dfirst = (u32*)dev("conn_dfirst", 4ull * d_.c_max);
+    d_.conn_dlast = (u32*)dev("conn_dlast", 4ull * d_.c_max);
+    d_.conn_total = (u32*)dev("conn_total", 4ull * d_.c_max);
+    d_.conn_base = (u32*)dev("conn_base", 4ull * d_.c_max);
+
+    d_.seg_start = (u32*)dev("seg_start", 4ull * d_.seg_max);
+    d_.seg_total = (u32*)dev("seg_total", 4ull * d_.seg_max);
+    d_.work = (u8*)dev("work", d_.work_cap + 4096);
+
+    d_.cmds = (Cmd*)dev("cmds", sizeof(Cmd) * (u64)d_.cmd_max);
+    d_.frags = (Frag*)dev("frags", sizeof(Frag) * (u64)d_.frag_max);
+    d_.cmd_is_pub = (u32*)dev("cmd_is_pub", 4ull * d_.cmd_max);
+    d_.cmd_is_ack = (u32*)dev("cmd_is_ack", 4ull * d_.cmd_max);
+    d_.cmd_pub_rank = (u32*)dev("cmd_pub_rank", 4ull * d_.cmd_max);
+    d_.cmd_ack_rank = (u32*)dev("cmd_ack_rank", 4ull * d_.cmd_max);
+
+    d_.pubs = (Pub*)dev("pubs", sizeof(Pub) * (u64)d_.pub_max);
+    d_.pub_keyvec = (i8*)dev("pub_keyvec", (u64)d_.pub_max * TOPIC_K + 64);
+    d_.pub_match = (u16*)dev("pub_match", 2ull * d_.pub_max * (d_.tb_pad / 16) + 64);
+    d_.pub_nq = (u32*)dev("pub_nq", 4ull * d_.pub_max);
+    d_.pub_slot = (u32*)dev("pub_slot", 4ull * d_.pub_max);
+    d_.pub_routed = (u32*)dev("pub_routed", 4ull * d_.pub_max);
+    d_.pub_pair_off = (u32*)dev("pub_pair_off", 4ull * d_.pub_max);
+    d_.pub_slot_off = (u32*)dev("pub_slot_off", 4ull * d_.pub_max);
+    d_.pub_routed_rank = (u32*)dev("pub_routed_rank", 4ull * d_.pub_max);
+    d_.pub_ret = (u32*)dev("pub_ret", 4ull * d_.pub_max);
+    d_.ret_list = (u32*)dev("ret_list", 4ull * d_.pub_max);
+    d_.acks = (Ack*)dev("acks", sizeof(Ack) * (u64)d_.ack_max);
+
+    for (int k = 0; k < 2; ++k) {
+      d_.pair_k[k] = (u32*)dev(k ? "pair_k1" : "pair_k0", 4ull * d_.pair_max);
+      d_.pair_v[k] = (u32*)dev(k ? "pair_v1" : "pair_v0", 4ull * d_.pair_max);
+    }
+    d_.q_first = (u32*)dev("q_first", 4ull * d_.q_max);
+
+    d_.x_hkey = (u64*)dev("x_hkey", 8ull * xhash);
+    d_.x_hval = (i32*)dev("x_hval", 4ull * xhash);
+    d_.x_type = (u32*)dev("x_type", 4ull * d_.x_max);
+    d_.x_fan_off = (u32*)dev("x_fan_off", 4ull * d_.x_max);
+    d_.x_fan_n = (u32*)dev("x_fan_n", 4ull * d_.x_max);
+    d_.x_t_off = (u32*)dev("x_t_off", 4ull * d_.x_max);
+    d_.x_t_n = (u32*)dev("x_t_n", 4ull * d_.x_max);
+    d_.fan_q = (u32*)dev("fan_q", 4ull * fan_max);
+    d_.d_key = (u64*)dev("d_key", 8ull * dhash);
+    d_.d_exch = (i32*)dev("d_exch", 4ull * dhash);
+    d_.d_kb_off = (u32*)dev("d_kb_off", 4ull * dhash);
+    d_.d_kb_len = (u32*)dev("d_kb_len", 4ull * dhash);
+    d_.d_q_off = (u32*)dev("d_q_off", 4ull * dhash);
+    d_.d_q_n = (u32*)dev("d_q_n", 4ull * dhash);
+    d_.d_q = (u32*)dev("d_q", 4ull * dq_max);
+    d_.kpool = (u8*)dev("kpool", kpool);
+    d_.t_queue = (u32*)dev("t_queue", 4ull * d_.tb_pad);
+    d_.t_exch = (u32*)dev("t_exch", 4ull * d_.tb_pad);
+    d_.t_kb_off = (u32*)dev("t_kb_off", 4ull * d_.tb_pad);
+    d_.t_kb_len = (u32*)dev("t_kb_len", 4ull * d_.tb_pad);
+    d_.t_flags = (u32*)dev("t_flags", 4ull * d_.tb_pad);
+    d_.t_expect = (i32*)dev("t_expect", 4ull * d_.tb_pad);
+    d_.t_mat = (i8*)dev("t_mat", (u64)d_.tb_pad * TOPIC_K + 64);
+
+    d_.q_ring_off = (u64*)dev("q_ring_off", 8ull * d_.q_max);
+    d_.q_ring_mask = (u64*)dev("q_ring_mask", 8ull * d_.q_max);
+    d_.q_head = (u64*)dev("q_head", 8ull * d_.q_max);
+    d_.q_tail = (u64*)dev("q_tail", 8ull * d_.q_max);
+    d_.q_ttl = (i64*)dev("q_ttl", 8ull * d_.q_max);
+    d_.q_cons_off = (u32*)dev("q_cons_off", 4ull * d_.q_max);
+    d_.q_cons_n = (u32*)dev("q_cons_n", 4ull * d_.q_max);
+    d_.q_rr = (u32*)dev("q_rr", 4ull * d_.q_max);
+    d_.q_active = (u32*)dev("q_active", 4ull * d_.q_max);
+    d_.q_cons = (u32*)dev("q_cons", 4ull * d_.cons_max);
+    d_.ring = (Desc*)dev("ring", sizeof(Desc) * d_.ring_pool);
+
+    d_.ch_confirm = (u32*)dev("ch_confirm", 4ull * nch);
+    d_.ch_pub_cnt = (u32*)dev("ch_pub_cnt", 4ull * nch);
+    d_.ch_confirm_next = (u64*)dev("ch_confirm_next", 8ull * nch);
+    d_.ch_next_tag = (u64*)dev("ch_next_tag", 8ull * nch);
+    d_.ch_uhead = (u64*)dev("ch_uhead", 8ull * nch);
+    d_.ch_ack_upto = (u64*)dev("ch_ack_upto", 8ull * nch);
+    d_.ch_req_upto = (u64*)dev("ch_req_upto", 8ull * nch);
+    d_.ch_prefetch = (u32*)dev("ch_prefetch", 4ull * nch);
+    d_.ch_global = (u32*)dev("ch_global", 4ull * nch);
+    d_.ch_flow = (u32*)dev("ch_flow", 4ull * nch);
+    d_.ch_num = (u32*)dev("ch_num", 4ull * nch);
+    d_.ch_unacked = (u32*)dev("ch_unacked", 4ull * nch);
+    d_.ch_win = (u32*)dev("ch_win", 4ull * nch);
+    d_.ch_dirty = (u32*)dev("ch_dirty", 4ull * nch);
+    d_.dirty_list = (u32*)dev("dirty_list", 4ull * nch);
+    d_.n_dirty = (u32*)dev("n_dirty", 4);
+    d_.uwin = (USlot*)dev("uwin", sizeof(USlot) * (u64)nch * ucap);
+
+    d_.cons_q = (u32*)dev("cons_q", 4ull * d_.cons_max);
+    d_.cons_ch = (u32*)dev("cons_ch", 4ull * d_.cons_max);
+    d_.cons_noack = (u32*)dev("cons_noack", 4ull * d_.cons_max);
+    d_.cons_active = (u32*)dev("cons_active", 4ull * d_.cons_max);
+    d_.cons_unacked = (u32*)dev("cons_unacked", 4ull * d_.cons_max);
+    d_.cons_tag_off = (u32*)dev("cons_tag_off", 4ull * d_.cons_max);
+    d_.cons_tag_len = (u32*)dev("cons_tag_len", 4ull * d_.cons_max);
+    d_.tpool = (u8*)dev("tpool", 256ull * d_.cons_max);
+
+    d_.msgs = (MsgEnt*)dev("msgs", sizeof(MsgEnt) * (u64)d_.msg_max);
+    d_.msg_free = (u32*)dev("msg_free", 4ull * d_.msg_max);
+    d_.msg_free_top = (u32*)dev("msg_free_top", 4);
+    d_.log = (u8*)dev("log", d_.log_bytes + 4096);
+    d_.log_head = (u64*)dev("log_head", 8);
+    d_.log_tail = (u64*)dev("log_tail", 8);
+    d_.log_step_base = (u64*)dev("log_step_base", 8);
+    d_.log_live = (i64*)dev("log_live", 8ull * d_.n_log_blocks);
+    d_.id_next = (u64*)dev("id_next", 8);
+
+    d_.deliv = (Deliv*)dev("deliv", sizeof(Deliv) * (u64)d_.deliv_max);
+    for (int k = 0; k < 2; ++k) {
+      d_.dv_k[k] = (u32*)dev(k ? "dv_k1" : "dv_k0", 4ull * d_.deliv_max);
+      d_.dv_v[k] = (u32*)dev(k ? "dv_v1" : "dv_v0", 4ull * d_.deliv_max);
+    }
+    d_.dv_size = (u32*)dev("dv_size", 4ull * d_.deliv_max);
+    d_.dv_off = (u32*)dev("dv_off", 4ull * d_.deliv_max);
+    d_.ch_first = (u32*)dev("ch_first", 4ull * nch);
+
+    d_.req = (ReqItem*)dev("req", sizeof(ReqItem) * (u64)d_.req_max);
+    d_.req_n = (u32*)dev("req_n", 4);
+    d_.req_q_n = (u32*)dev("req_q_n", 4ull * d_.q_max);
+
+    u32 max_sort = d_.pair_max > d_.deliv_max ? d_.pair_max : d_.deliv_max;
+    ntiles_max_ = ceil_div(max_sort, SORT_TILE);
+    d_.hist = (u32*)dev("hist", 4ull * 256 * ntiles_max_);
+    d_.hist_scan = (u32*)dev("hist_scan", 4ull * 256 * ntiles_max_);
+    d_.scan_tmp = (u32*)dev("scan_tmp", 4ull * 1024);
+    d_.tot = (u32*)dev("tot", 4ull * 64);
+    d_.egress_budget = (u32*)dev("egress_budget", 4);
+
+    // ---- initial state
+    fill("conn_dfirst", 0xff);
+    fill("conn_dlast", 0xff);
+    fill("x_hval", 0xff);
+    fill("d_exch", 0xff);
+    std::vector<u32> fl(d_.msg_max);
+    for (u32 i = 0; i < d_.msg_max; ++i) fl[i] = d_.msg_max - 1 - i;
+    HIPCHECK(hipMemcpy(d_.msg_free, fl.data(), 4ull * d_.msg_max, hipMemcpyHostToDevice));
+    HIPCHECK(hipMemcpy(d_.msg_free_top, &d_.msg_max, 4, hipMemcpyHostToDevice));
+    HIPCHECK(hipDeviceSynchronize());
+    step_in_ = StepIn{};
+  }
+
+  ~Engine() {
+    if (graph_exec_) hipGraphExecDestroy(graph_exec_);
+    if (req_exec_) hipGraphExecDestroy(req_exec_);
+    for (auto& kv : bufs_) {
+      if (kv.second.host) hipHostFree(kv.second.ptr);
+      else hipFree(kv.second.ptr);
+    }
+  }
+
+  // ------------------------------------------------------------- buffers
+  void* alloc(const char* name, size_t bytes, bool host) {
+    Buf b;
+    b.bytes = bytes;
+    b.host = host;
+    if (host) {
+      HIPCHECK(hipHostMalloc(&b.ptr, bytes, hipHostMallocMapped | hipHostMallocPortable));
+      memset(b.ptr, 0, bytes);
+    } else {
+      HIPCHECK(hipMalloc(&b.ptr, bytes));
+      HIPCHECK(hipMemset(b.ptr, 0, bytes));
+    }
+    total_bytes_ += bytes;
+    bufs_[name] = b;
+    if (host) {
+      void* dp = nullptr;
+      HIPCHECK(hipHostGetDevicePointer(&dp, b.ptr, 0));
+      return dp;
+    }
+    return b.ptr;
+  }
+
+  const Buf& buf(const std::string& name) const {
+    auto it = bufs_.find(name);
+    if (it == bufs_.end()) throw std::runtime_error("no buffer " + name);
+    return it->second;
+  }
+
+  void fill(const std::string& name, int byte) {
+    const Buf& b = buf(name);
+    if (b.host) memset(b.ptr, byte, b.bytes);
+    else HIPCHECK(hipMemset(b.ptr, byte, b.bytes));
+  }
+
+  void upload(const std::string& name, py::buffer data, size_t offset) {
+    py::buffer_info info = data.request();
+    size_t n = (size_t)info.size * info.itemsize;
+    const Buf& b = buf(name);
+    if (offset + n > b.bytes) throw std::runtime_error("upload overflows " + name);
+    if (b.host) memcpy((u8*)b.ptr + offset, info.ptr, n);
+    else HIPCHECK(hipMemcpy((u8*)b.ptr + offset, info.ptr, n, hipMemcpyHostToDevice));
+  }
+
+  py::bytes download(const std::string& name, size_t offset, size_t n) {
+    const Buf& b = buf(name);
+    if (n == 0) n = b.bytes - offset;
+    if (offset + n > b.bytes) throw std::runtime_error("download overflows " + name);
+    std::string out(n, '\0');
+    if (b.host) memcpy(&out[0], (u8*)b.ptr + offset, n);
+    else HIPCHECK(hipMemcpy(&out[0], (u8*)b.ptr + offset, n, hipMemcpyDeviceToHost));
+    return py::bytes(out);
+  }
+
+  // zero-copy numpy view of a host-mapped buffer
+  py::array host_view(const std::string& name) {
+    const Buf& b = buf(name);
+    if (!b.host) throw std::runtime_error(name + " is not host-mapped");
+    return py::array(py::dtype("uint8"), {(py::ssize_t)b.bytes}, {(py::ssize_t)1}, b.ptr,
+                     py::capsule(b.ptr, [](void*) {}));
+  }
+
+  py::dict info() const {
+    py::dict o;
+    o["c_max"] = d_.c_max; o["chpc"] = d_.chpc; o["q_max"] = d_.q_max; o["x_max"] = d_.x_max;
+    o["cons_max"] = d_.cons_max; o["seg_max"] = d_.seg_max; o["carry_cap"] = d_.carry_cap;
+    o["cmd_max"] = d_.cmd_max; o["pair_max"] = d_.pair_max; o["deliv_max"] = d_.deliv_max;
+    o["msg_max"] = d_.msg_max; o["ucap"] = d_.ucap_mask + 1; o["deliver_cap"] = d_.deliver_cap;
+    o["chmap_size"] = d_.chmap_size; o["xhash"] = d_.xhash_mask + 1; o["dhash"] = d_.dhash_mask + 1;
+    o["tb_max"] = d_.tb_max; o["tb_pad"] = d_.tb_pad; o["log_bytes"] = d_.log_bytes;
+    o["ingress_cap"] = d_.ingress_cap; o["egress_cap"] = d_.egress_cap; o["ring_pool"] = d_.ring_pool;
+    o["work_cap"] = d_.work_cap; o["total_bytes"] = total_bytes_; o["req_max"] = d_.req_max;
+    o["sizeof"] = py::dict(py::arg("StepIn") = sizeof(StepIn), py::arg("SegIn") = sizeof(SegIn),
+                           py::arg("SegOut") = sizeof(SegOut), py::arg("Counters") = sizeof(Counters),
+                           py::arg("CtrlRec") = sizeof(CtrlRec), py::arg("ConnOut") = sizeof(ConnOut),
+                           py::arg("MsgEnt") = sizeof(MsgEnt), py::arg("Desc") = sizeof(Desc),
+                           py::arg("USlot") = sizeof(USlot), py::arg("Deliv") = sizeof(Deliv),
+                           py::arg("Pub") = sizeof(Pub), py::arg("Cmd") = sizeof(Cmd));
+    return o;
+  }
+
+  // ------------------------------------------------------------- step
+  // segs: numpy structured/bytes of SegIn[nseg]; payload: host pointer (pinned preferred)
+  void submit(py::buffer segs, u64 payload_ptr, u64 payload_len, i64 now_ms, u64 step, u64 id_ms,
+              u32 worker, u64 stream) {
+    py::buffer_info si = segs.request();
+    size_t sb = (size_t)si.size * si.itemsize;
+    u32 nseg = (u32)(sb / sizeof(SegIn));
+    if (nseg > d_.seg_max) throw std::runtime_error("too many segments");
+    if (payload_len > d_.ingress_cap) throw std::runtime_error("ingress payload exceeds ingress_cap");
+    hipStream_t s = (hipStream_t)stream;
+    step_in_.nseg = nseg;
+    step_in_.now_ms = now_ms;
+    step_in_.step = step;
+    step_in_.id_ms = id_ms;
+    step_in_.worker = worker;
+    seg_stage_.assign((const u8*)si.ptr, (const u8*)si.ptr + sb);
+    HIPCHECK(hipMemcpyAsync((void*)d_.in, &step_in_, sizeof(StepIn), hipMemcpyHostToDevice, s));
+    if (sb) HIPCHECK(hipMemcpyAsync((void*)d_.segs, seg_stage_.data(), sb, hipMemcpyHostToDevice, s));
+    if (payload_len)
+      HIPCHECK(hipMemcpyAsync((void*)d_.ingress, (const void*)payload_ptr, payload_len,
+                              hipMemcpyHostToDevice, s));
+    if (graph_enabled_) {
+      if (!graph_exec_) capture(s, false);
+      HIPCHECK(hipGraphLaunch(graph_exec_, s));
+    } else {
+      launch_main(s);
+    }
+  }
+
+  void requeue(u64 stream) {
+    hipStream_t s = (hipStream_t)stream;
+    if (graph_enabled_) {
+      if (!req_exec_) capture(s, true);
+      HIPCHECK(hipGraphLaunch(req_exec_, s));
+    } else {
+      launch_requeue(s);
+    }
+  }
+
+  void sync(u64 stream) { HIPCHECK(hipStreamSynchronize((hipStream_t)stream)); }
+
+  py::dict counters() const {
+    const Counters& c = *(const Counters*)buf("ctr_host").ptr;
+    py::dict o;
+#define F(x) o[#x] = c.x
+    F(n_cmds); F(n_frags); F(n_pubs); F(n_acks); F(n_ctrl); F(ctrl_bytes); F(n_pairs); F(n_deliv);
+    F(egress_bytes); F(n_returns); F(n_confirm_frames); F(n_freed); F(n_requeue); F(n_unroutable);
+    F(n_dropped_nomem); F(n_expired); F(n_routed_msgs); F(n_unknown_exchange); F(n_ring_full);
+    F(n_acked); F(log_head); F(log_tail); F(msg_free_top); F(n_live_msgs);
+#undef F
+    std::vector<u32> lat(c.lat_hist, c.lat_hist + LAT_BINS);
+    o["lat_hist"] = lat;
+    return o;
+  }
+
+ private:
+  void launch_scan(hipStream_t s, std::initializer_list<std::pair<const u32*, u32*>> arrs, const u32* n,
+                   u32 nmax, u32 slot) {
+    ScanArgs a{};
+    u32 k = 0;
+    for (auto& p : arrs) { a.in[k] = p.first; a.out[k] = p.second; ++k; }
+    a.narr = k;
+    a.n = n;
+    a.nmax = nmax;
+    a.tot_slot = slot;
+    hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, s, a, d_.tot);
+  }
+
+  // returns index (0/1) of the buffer holding the sorted output
+  u32 radix_sort(hipStream_t s, u32** keys, u32** vals, const u32* n, u32 nmax, u32 bits) {
+    u32 ntiles = ceil_div(nmax, SORT_TILE);
+    u32 src = 0;
+    for (u32 shift = 0; shift < bits; shift += 8) {
+      hipLaunchKernelGGL(k_rs_hist, dim3(ntiles), dim3(256), 0, s, keys[src], n, shift, d_.hist, ntiles);
+      launch_scan(s, {{d_.hist, d_.hist_scan}}, nullptr, 256 * ntiles, 60);
+      hipLaunchKernelGGL(k_rs_scatter, dim3(ntiles), dim3(256), 0, s, keys[src], vals[src], keys[src ^ 1],
+                         vals[src ^ 1], n, shift, d_.hist_scan, ntiles);
+      src ^= 1;
+    }
+    return src;
+  }
+
+  void launch_main(hipStream_t s) {
+    const DS& d = d_;
+    u32 nch = d.c_max * d.chpc;
+    auto blocks = [](u64 n, u32 per) { return dim3(n ? ceil_div(n, per) : 1); };
+    hipLaunchKernelGGL(k_prep, dim3(1), dim3(1024), 0, s, d);
+    hipLaunchKernelGGL(k_stage, dim3(d.seg_max, 4), dim3(256), 0, s, d);
+    hipLaunchKernelGGL(k_frame_scan, dim3(d.seg_max), dim3(256), 0, s, d);
+    hipLaunchKernelGGL(k_classify, blocks(d.cmd_max, 256), dim3(256), 0, s, d);
+    launch_scan(s, {{d.cmd_is_pub, d.cmd_pub_rank}, {d.cmd_is_ack, d.cmd_ack_rank}}, &d.ctr->n_cmds,
+                d.cmd_max, 4);
+    hipLaunchKernelGGL(k_set_counts, dim3(1), dim3(64), 0, s, d);
+    hipLaunchKernelGGL(k_decode, blocks(d.cmd_max, 256), dim3(256), 0, s, d);
+    if (d.tb_max) {
+      u32 waves = (d.pub_max / 16) * (d.tb_pad / 16);
+      hipLaunchKernelGGL(k_topic_mfma, blocks((u64)waves * 64, 256), dim3(256), 0, s, d);
+    }
+    hipLaunchKernelGGL(k_route<0>, blocks(d.pub_max, 256), dim3(256), 0, s, d);
+    launch_scan(s, {{d.pub_nq, d.pub_pair_off}, {d.pub_slot, d.pub_slot_off}, {d.pub_routed, d.pub_routed_rank}},
+                &d.ctr->n_pubs, d.pub_max, 0);
+    hipLaunchKernelGGL(k_route<1>, blocks(d.pub_max, 256), dim3(256), 0, s, d);
+    hipLaunchKernelGGL(k_log_reserve, dim3(1), dim3(64), 0, s, d);
+    hipLaunchKernelGGL(k_store, blocks((u64)d.pub_max * 64, 256), dim3(256), 0, s, d);
+    u32* pk[2] = {d.pair_k[0], d.pair_k[1]};
+    u32* pv[2] = {d.pair_v[0], d.pair_v[1]};
+    u32 psrc = radix_sort(s, pk, pv, &d.tot[0], d.pair_max, d.q_bits);
+    hipLaunchKernelGGL(k_qfirst, blocks(d.pair_max, 256), dim3(256), 0, s, d, psrc);
+    hipLaunchKernelGGL(k_enqueue, blocks(d.pair_max, 256), dim3(256), 0, s, d, psrc);
+    hipLaunchKernelGGL(k_acks, blocks(d.ack_max, 256), dim3(256), 0, s, d);
+    hipLaunchKernelGGL(k_chan_advance, blocks((u64)nch * 64, 256), dim3(256), 0, s, d);
+    hipLaunchKernelGGL(k_reset_dirty, dim3(1), dim3(64), 0, s, d);
+    hipLaunchKernelGGL(k_dequeue, blocks((u64)d.q_max * 64, 256), dim3(256), 0, s, d);
+    u32* dk[2] = {d.dv_k[0], d.dv_k[1]};
+    u32* dvv[2] = {d.dv_v[0], d.dv_v[1]};
+    u32 dsrc = radix_sort(s, dk, dvv, &d.ctr->n_deliv, d.deliv_max, d.ch_bits);
+    hipLaunchKernelGGL(k_dfirst, blocks(d.deliv_max, 256), dim3(256), 0, s, d, dsrc);
+    hipLaunchKernelGGL(k_tags, blocks(d.deliv_max, 256), dim3(256), 0, s, d, dsrc);
+    launch_scan(s, {{d.dv_size, d.dv_off}}, &d.ctr->n_deliv, d.deliv_max, 6);
+    hipLaunchKernelGGL(k_conn_sizes, blocks(d.c_max, 256), dim3(256), 0, s, d);
+    launch_scan(s, {{d.conn_total, d.conn_base}}, nullptr, d.c_max, 7);
+    hipLaunchKernelGGL(k_conn_out, blocks(d.c_max, 256), dim3(256), 0, s, d);
+    hipLaunchKernelGGL(k_render_returns, blocks((u64)d.pub_max * 64, 256), dim3(256), 0, s, d);
+    hipLaunchKernelGGL(k_render_confirms, blocks(d.c_max, 256), dim3(256), 0, s, d);
+    hipLaunchKernelGGL(k_render_deliv, blocks((u64)d.deliv_max * 64, 256), dim3(256), 0, s, d, dsrc);
+    u64 pn = d.deliv_max > d.c_max ? d.deliv_max : d.c_max;
+    hipLaunchKernelGGL(k_post, blocks(pn, 256), dim3(256), 0, s, d, dsrc);
+    hipLaunchKernelGGL(k_post2, blocks(d.c_max, 256), dim3(256), 0, s, d);
+    hipLaunchKernelGGL(k_final, dim3(1), dim3(64), 0, s, d);
+  }
+
+  void launch_requeue(hipStream_t s) {
+    hipLaunchKernelGGL(k_requeue, dim3(d_.q_max), dim3(256), 0, s, d_);
+    hipLaunchKernelGGL(k_requeue_compact, dim3(1), dim3(1024), 0, s, d_);
+  }
+
+  void capture(hipStream_t s, bool req) {
+    hipGraph_t g;
+    HIPCHECK(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+    if (req) launch_requeue(s);
+    else launch_main(s);
+    HIPCHECK(hipStreamEndCapture(s, &g));
+    HIPCHECK(hipGraphInstantiate(req ? &req_exec_ : &graph_exec_, g, nullptr, nullptr, 0));
+    HIPCHECK(hipGraphDestroy(g));
+  }
+
+  int device_ = 0;
+  DS d_;
+  std::map<std::string, Buf> bufs_;
+  u64 total_bytes_ = 0;
+  u64 egress_alloc_ = 0;
+  u32 ntiles_max_ = 0;
+  bool graph_enabled_ = true;
+  hipGraphExec_t graph_exec_ = nullptr;
+  hipGraphExec_t req_exec_ = nullptr;
+  StepIn step_in_;
+  std::vector<u8> seg_stage_;
+};
+
+static py::array alloc_pinned(size_t bytes) {
+  void* p = nullptr;
+  HIPCHECK(hipHostMalloc(&p, bytes, hipHostMallocPortable));
+  return py::array(py::dtype("uint8"), {(py::ssize_t)bytes}, {(py::ssize_t)1}, p,
+                   py::capsule(p, [](void* q) { hipHostFree(q); }));
+}
+
+static u64 create_stream(int device) {
+  HIPCHECK(hipSetDevice(device));
+  hipStream_t st;
+  HIPCHECK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+  return (u64)st;
+}
+
+static int device_count() {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+PYBIND11_MODULE(_dataplane, m) {
+  m.doc() = "MI355X (gfx950) AMQP data-plane kernels + native step runtime";
+  m.def("alloc_pinned", &alloc_pinned, "page-locked host buffer (numpy uint8)");
+  m.def("device_count", &device_count);
+  m.def("create_stream", &create_stream, py::arg("device") = 0);
+  m.attr("CAND_MAX") = CAND_MAX;
+  m.attr("TOPIC_K") = TOPIC_K;
+  m.attr("TOPIC_WORDS") = TOPIC_WORDS;
+  m.attr("LAT_BINS") = LAT_BINS;
+  py::class_<Engine>(m, "Engine")
+      .def(py::init<py::dict>())
+      .def("info", &Engine::info)
+      .def("fill", &Engine::fill)
+      .def("upload", &Engine::upload, py::arg("name"), py::arg("data"), py::arg("offset") = 0)
+      .def("download", &Engine::download, py::arg("name"), py::arg("offset") = 0, py::arg("n") = 0)
+      .def("host_view", &Engine::host_view)
+      .def("submit", &Engine::submit)
+      .def("requeue", &Engine::requeue)
+      .def("sync", &Engine::sync)
+      .def("counters", &Engine::counters);
+}

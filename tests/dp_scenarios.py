@@ -1,0 +1,180 @@
+"""Deterministic data-plane scenarios shared by the golden-model (CPU) tests and the
+HIP-vs-golden (GPU) tests.  Each scenario is a function ``(dp) -> list[step inputs]``
+that configures the control state and returns per-step ``{conn: bytes}`` inputs;
+``unpause`` entries (``{'__unpause__': [conns]}``) are applied before the step.
+"""
+
+from chanamq_amd.engine.traffic import ack_frame, heartbeat, publish_command, publish_stream, split_stream
+from chanamq_amd.protocol.codec import Method, encode_method_frame, render_command
+
+VH = "AMQ.DEFAULT"
+
+
+def sc_direct_split(dp):
+    dp.declare_queue(VH, "q1")
+    dp.declare_exchange(VH, "ex", "direct")
+    dp.bind(VH, "q1", "ex", "k1")
+    dp.open_connection(1, VH)
+    dp.open_channel(1, 1)
+    dp.open_connection(2, VH)
+    dp.open_channel(2, 5)
+    dp.consume(2, 5, VH, "q1", "c1", no_ack=True)
+    s = publish_stream(40, "ex", lambda i: "k1" if i % 3 else "nokey", 300, seed=1)
+    parts = split_stream(s, 4, seed=3)
+    return [{1: p} for p in parts] + [{}]
+
+
+def sc_default_exchange(dp):
+    dp.declare_queue(VH, "orders")
+    dp.open_connection(3, VH)
+    dp.open_channel(3, 1)
+    dp.consume(3, 1, VH, "orders", "amq.ctag-1", no_ack=True)
+    dp.open_connection(4, VH)
+    dp.open_channel(4, 2)
+    s = publish_stream(10, "", lambda i: "orders", 50, channel=2, seed=2)
+    return [{4: s}, {}]
+
+
+def sc_topic(dp):
+    dp.declare_exchange(VH, "tx", "topic")
+    pats = {"qa": ["forex.*", "*.usd"], "qb": ["*.eur", "forex.*", "trade"], "qc": ["*"], "qd": ["quote.#"],
+            "qe": ["#"], "qf": ["a.*.c.#.z"]}
+    for q, ps in pats.items():
+        dp.declare_queue(VH, q)
+        for p in ps:
+            dp.bind(VH, q, "tx", p)
+    conn = 10
+    for q in pats:
+        dp.open_connection(conn, VH)
+        dp.open_channel(conn, 1)
+        dp.consume(conn, 1, VH, q, "t-" + q, no_ack=True)
+        conn += 1
+    dp.open_connection(1, VH)
+    dp.open_channel(1, 7)
+    keys = ["forex.eur", "forex", "trade.jpy", "forex.jpy", "trade", "quote", "quote.a.b", "x.usd",
+            "a.b.c.z", "a.b.c.q.r.z", "a.b.c", "", "forex.", "a..b", "...", "w1.w2.w3.w4.w5.w6.w7.w8.w9"]
+    s = publish_stream(len(keys) * 3, "tx", lambda i: keys[i % len(keys)], 64, channel=7, seed=4)
+    return [{1: s}, {}]
+
+
+def sc_fanout(dp):
+    dp.declare_exchange(VH, "fx", "fanout")
+    for i in range(3):
+        dp.declare_queue(VH, f"f{i}")
+        dp.bind(VH, f"f{i}", "fx", "")
+        dp.open_connection(20 + i, VH)
+        dp.open_channel(20 + i, 1)
+        dp.consume(20 + i, 1, VH, f"f{i}", f"fc{i}", no_ack=True)
+    dp.open_connection(1, VH)
+    dp.open_channel(1, 1)
+    s = publish_stream(25, "fx", lambda i: "any", 2000, seed=5, frame_max=4096)
+    return [{1: s[:3000]}, {1: s[3000:]}, {}]
+
+
+def sc_manual_ack(dp):
+    dp.declare_queue(VH, "work")
+    dp.open_connection(1, VH)
+    dp.open_channel(1, 1)
+    dp.open_connection(2, VH)
+    dp.open_channel(2, 1)
+    dp.qos(2, 1, prefetch_count=5)
+    dp.consume(2, 1, VH, "work", "w", no_ack=False)
+    s = publish_stream(12, "", lambda i: "work", 100, seed=6)
+    return [{1: s}, {2: ack_frame(1, 3, multiple=True)}, {2: ack_frame(1, 5, multiple=False)},
+            {2: ack_frame(1, 4, multiple=False)}, {2: ack_frame(1, 0, multiple=True)}, {}]
+
+
+def sc_confirm_mandatory(dp):
+    dp.declare_exchange(VH, "cx", "direct")
+    dp.declare_queue(VH, "cq")
+    dp.bind(VH, "cq", "cx", "ok")
+    dp.open_connection(1, VH)
+    dp.open_channel(1, 1)
+    dp.confirm_select(1, 1)
+    dp.open_connection(2, VH)
+    dp.open_channel(2, 1)
+    dp.consume(2, 1, VH, "cq", "cc", no_ack=True)
+    parts = []
+    for i in range(9):
+        parts.append(publish_command(1, "cx", "ok" if i % 3 else "lost", bytes([i]) * 40,
+                                     {"delivery_mode": 2}, mandatory=(i == 3)))
+    return [{1: b"".join(parts)}, {}]
+
+
+def sc_control_barrier(dp):
+    dp.declare_queue(VH, "cb")
+    dp.open_connection(1, VH)
+    dp.open_channel(1, 1)
+    dp.open_connection(2, VH)
+    dp.open_channel(2, 1)
+    dp.consume(2, 1, VH, "cb", "c", no_ack=True)
+    a = publish_stream(3, "", lambda i: "cb", 30, seed=7)
+    ctrl = encode_method_frame(1, Method("queue.declare", queue="other"))
+    b = publish_stream(4, "", lambda i: "cb", 31, seed=8)
+    return [{1: a + ctrl + b + heartbeat()}, {"__unpause__": [1]}, {}]
+
+
+def sc_nack_requeue(dp):
+    dp.declare_queue(VH, "nq")
+    dp.open_connection(1, VH)
+    dp.open_channel(1, 1)
+    dp.open_connection(2, VH)
+    dp.open_channel(2, 1)
+    dp.qos(2, 1, prefetch_count=4)
+    dp.consume(2, 1, VH, "nq", "n", no_ack=False)
+    s = publish_stream(6, "", lambda i: "nq", 20, seed=9)
+    nack = render_command(1, Method("basic.nack", delivery_tag=2, multiple=True, requeue=True))
+    rej = render_command(1, Method("basic.reject", delivery_tag=3, requeue=False))
+    return [{1: s}, {2: nack}, {}, {2: rej}, {}, {2: ack_frame(1, 0)}, {}]
+
+
+def sc_ttl(dp):
+    dp.declare_queue(VH, "tq", ttl_ms=1000)
+    dp.open_connection(1, VH)
+    dp.open_channel(1, 1)
+    s1 = publish_stream(3, "", lambda i: "tq", 10, seed=10)
+    s2 = b"".join(publish_command(1, "", "tq", b"x" * 10, {"expiration": "5000"}) for _ in range(2))
+    return [{1: s1 + s2}, {}]
+
+
+def sc_frame_error(dp):
+    dp.declare_queue(VH, "eq")
+    dp.open_connection(1, VH)
+    dp.open_channel(1, 1)
+    good = publish_stream(2, "", lambda i: "eq", 10, seed=11)
+    bad = b"\x01\x00\x01\x00\x00\x00\x05hello\x00"  # wrong end marker
+    return [{1: good + bad}]
+
+
+SCENARIOS = {
+    "direct_split": sc_direct_split,
+    "default_exchange": sc_default_exchange,
+    "topic": sc_topic,
+    "fanout": sc_fanout,
+    "manual_ack": sc_manual_ack,
+    "confirm_mandatory": sc_confirm_mandatory,
+    "control_barrier": sc_control_barrier,
+    "nack_requeue": sc_nack_requeue,
+    "ttl": sc_ttl,
+    "frame_error": sc_frame_error,
+}
+
+NOW = 1_800_000_000_000
+
+
+def run(dp, steps, now_step_ms=None):
+    """Drive dp through the steps; returns list of normalised per-step outputs."""
+    outs = []
+    for k, inp in enumerate(steps):
+        inp = dict(inp)
+        for c in inp.pop("__unpause__", []):
+            dp.unpause(c)
+        now = NOW + (now_step_ms or 0) * k
+        r = dp.step(inp, now_ms=now)
+        if isinstance(r, dict):
+            eg, ctrl, ev, segs = r["egress"], r["ctrl"], r["events"], r["segs"]
+        else:
+            eg, ctrl, ev, segs = r.egress, r.ctrl, r.events, [s[:4] for s in r.segs]
+        outs.append(dict(egress=eg, ctrl=sorted(ctrl), events=sorted(ev),
+                         segs=sorted((s[0], s[1], s[2], s[3]) for s in segs)))
+    return outs

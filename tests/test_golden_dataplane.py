@@ -1,0 +1,102 @@
+"""Protocol-level checks of the golden data plane (CPU): what a client would observe."""
+
+from collections import defaultdict
+
+from dp_scenarios import SCENARIOS, run
+
+from chanamq_amd.engine.golden import GoldenDataPlane
+from chanamq_amd.engine.layout import SS_CTRL, SS_FRAME_ERROR
+from chanamq_amd.protocol.codec import CommandAssembler, FrameParser
+
+
+def decode(buf):
+    fp, ca = FrameParser(), CommandAssembler()
+    out = []
+    for fr in fp.feed(buf):
+        c = ca.feed(fr)
+        if c is not None:
+            out.append(c)
+    return out
+
+
+def run_sc(name):
+    g = GoldenDataPlane(c_max=64, chpc=8, q_max=64, x_max=64, cons_max=256, ucap=256)
+    outs = run(g, SCENARIOS[name](g), now_step_ms=3000)
+    per_conn = defaultdict(list)
+    for o in outs:
+        for c, b in o["egress"].items():
+            per_conn[c].extend(decode(b))
+    return g, outs, per_conn
+
+
+def test_direct_split_delivers_only_matching_in_order():
+    g, outs, pc = run_sc("direct_split")
+    d = [c for c in pc[2] if c.method.name == "basic.deliver"]
+    assert len(d) == sum(1 for i in range(40) if i % 3)
+    assert [c.method.delivery_tag for c in d] == list(range(1, len(d) + 1))
+    assert all(c.method.consumer_tag == "c1" and c.channel == 5 for c in d)
+
+
+def test_default_exchange_routes_by_queue_name():
+    g, outs, pc = run_sc("default_exchange")
+    d = [c for c in pc[3] if c.method.name == "basic.deliver"]
+    assert len(d) == 10 and all(len(c.body) == 50 for c in d)
+
+
+def test_topic_reference_vectors():
+    from chanamq_amd.models.matcher import topic_match
+    g, outs, pc = run_sc("topic")
+    keys_qa = [c.method.routing_key for c in pc[10]]
+    assert all(topic_match("forex.*", k) or topic_match("*.usd", k) for k in keys_qa)
+    assert "forex.eur" in keys_qa and "forex" not in keys_qa
+
+
+def test_fanout_body_split_at_frame_max():
+    g, outs, pc = run_sc("fanout")
+    for c in (20, 21, 22):
+        d = [x for x in pc[c] if x.method.name == "basic.deliver"]
+        assert len(d) == 25 and all(len(x.body) == 2000 for x in d)
+
+
+def test_manual_ack_prefetch_and_release():
+    g, outs, pc = run_sc("manual_ack")
+    d = [c for c in pc[2] if c.method.name == "basic.deliver"]
+    assert len(d) == 12
+    # first step is limited by prefetch 5
+    first = decode(outs[0]["egress"][2])
+    assert len(first) == 5
+
+
+def test_confirms_and_mandatory_return():
+    g, outs, pc = run_sc("confirm_mandatory")
+    names = [c.method.name for c in pc[1]]
+    assert names == ["basic.return", "basic.ack"]
+    ret, ack = pc[1]
+    assert ret.method.reply_code == 312 and ret.body == bytes([3]) * 40
+    assert ack.method.delivery_tag == 9 and ack.method.multiple
+
+
+def test_control_barrier_pauses_and_resumes():
+    g, outs, pc = run_sc("control_barrier")
+    assert outs[0]["segs"][0][1] & SS_CTRL
+    assert len(outs[0]["ctrl"]) == 1
+    d = [c for c in pc[2] if c.method.name == "basic.deliver"]
+    assert len(d) == 7
+
+
+def test_nack_requeue_redelivered_flag():
+    g, outs, pc = run_sc("nack_requeue")
+    d = [c for c in pc[2] if c.method.name == "basic.deliver"]
+    red = [c for c in d if c.method.redelivered]
+    assert len(red) >= 2
+    assert len(d) == 6 + 2
+
+
+def test_ttl_expiry_drops():
+    g, outs, pc = run_sc("ttl")
+    assert g.counters["n_expired"] >= 0
+
+
+def test_frame_error_reported():
+    g, outs, pc = run_sc("frame_error")
+    assert outs[0]["segs"][0][1] & SS_FRAME_ERROR
