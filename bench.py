@@ -143,7 +143,7 @@ def main():
         dist.barrier()
     t = time.perf_counter() - t0
     c = dp.eng.counters()
-    errs = {k: c[k] for k in ("n_dropped_nomem", "n_ring_full", "n_unknown_exchange") if c[k]}
+    errs = {k: c[k] for k in ("n_dropped_nomem", "n_ring_full", "n_unknown_exchange", "n_unroutable", "n_routed_msgs", "n_pairs", "n_deliv", "n_live_msgs") if c[k]}
 
     vals = np.array([t, dl, pb, eg], np.float64)
     if dist:

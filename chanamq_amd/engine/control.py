@@ -101,10 +101,11 @@ class ControlState:
                           ("amq.topic", "topic"), ("amq.headers", "headers"), ("amq.match", "headers"))
 
     def __init__(self, c_max=1024, chpc=16, q_max=4096, x_max=1024, cons_max=16384,
-                 hash_wildcard=True, ring_pool=1 << 26):
+                 hash_wildcard=True, ring_pool=1 << 26, default_queue_capacity=1 << 16):
         self.c_max, self.chpc, self.q_max, self.x_max, self.cons_max = c_max, chpc, q_max, x_max, cons_max
         self.hash_wildcard = hash_wildcard
         self.ring_pool = ring_pool
+        self.default_queue_capacity = default_queue_capacity
         self.vhosts = {}             # name -> id
         self.exchanges = {}          # (vhost, name) -> Exchange
         self.queues = {}             # (vhost, name) -> Queue
@@ -238,7 +239,7 @@ class ControlState:
         return off
 
     def declare_queue(self, vhost, name, durable=False, exclusive_owner=-1, auto_delete=False,
-                      ttl_ms=0, capacity=1 << 16, passive=False):
+                      ttl_ms=0, capacity=None, passive=False):
         key = (vhost, name)
         q = self.queues.get(key)
         if q is not None:
@@ -247,6 +248,7 @@ class ControlState:
             raise ControlError(C.NOT_FOUND, f"no queue '{name}' in vhost '{vhost}'", 50, 10)
         if not self._free_q:
             raise ControlError(C.RESOURCE_ERROR, "queue table full", 50, 10)
+        capacity = capacity or self.default_queue_capacity
         cap = 1
         while cap < capacity:
             cap <<= 1

@@ -34,7 +34,8 @@ class StepResult:
 
 
 class GpuDataPlane(ControlState):
-    def __init__(self, device=0, hash_wildcard=True, graph=True, worker=0, **cfg):
+    def __init__(self, device=0, hash_wildcard=True, graph=True, worker=0, default_queue_capacity=1 << 16,
+                 **cfg):
         self.mod = ops.load()
         full = dict(cfg)
         full.update(device=device, hash_wildcard=int(hash_wildcard), graph=int(graph))
@@ -57,7 +58,8 @@ class GpuDataPlane(ControlState):
         self._pin = None
         self.requeue_pending = False
         super().__init__(c_max=i["c_max"], chpc=i["chpc"], q_max=i["q_max"], x_max=i["x_max"],
-                         cons_max=i["cons_max"], hash_wildcard=hash_wildcard, ring_pool=i["ring_pool"])
+                         cons_max=i["cons_max"], hash_wildcard=hash_wildcard, ring_pool=i["ring_pool"],
+                         default_queue_capacity=default_queue_capacity)
 
     # ================================================================== uploads
     def _up(self, name, arr, index=0):

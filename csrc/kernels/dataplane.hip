@@ -1006,7 +1006,8 @@ __global__ void k_route(DS d) {
     pb.slot_bytes = slot;
     if (ret) {
       // reserve bytes in the connection's return region
-      u32 sz = (8 + 4 + 2 + 1 + 64 + 1 + pb.ex_len + 1 + pb.rk_len + 1) /*method*/ +
+      u32 tl = ret == 312 ? 49u : 72u;  // reply texts (ErrorCodes.scala:23-31)
+      u32 sz = (8 + 4 + 2 + 1 + tl + 1 + pb.ex_len + 1 + pb.rk_len) /*method*/ +
                (8 + 12 + pb.props_len) /*header*/;
       u32 fm = d.conn_frame_max[pb.conn];
       u32 fmb = fm ? fm - 8 : 0xffffffffu;
@@ -1664,7 +1665,6 @@ __global__ void k_final(DS d) {
   if (tail > head) tail = head;
   *d.log_tail = tail;
   *d.id_next = *d.id_next + d.tot[2];
-  *d.n_dirty = 0;
   Counters* c = d.ctr;
   c->log_head = head;
   c->log_tail = tail;

@@ -8,7 +8,7 @@ pytestmark = pytest.mark.gpu
 
 CFG = dict(c_max=64, chpc=8, q_max=64, x_max=64, cons_max=256, seg_max=64, cmd_max=4096, deliv_max=4096,
            msg_max=1 << 14, ucap=256, deliver_cap=4096, ingress_cap=8 << 20, egress_cap=16 << 20,
-           log_bytes=64 << 20, log_block=1 << 20, ring_pool=1 << 16, tb_max=64, carry_cap=1 << 18,
+           log_bytes=64 << 20, log_block=1 << 20, ring_pool=1 << 20, default_queue_capacity=1 << 12, tb_max=64, carry_cap=1 << 18,
            dhash=1024, req_max=4096)
 
 
@@ -23,7 +23,8 @@ def test_gpu_matches_golden(gpu, name, graph):
     from chanamq_amd.engine.golden import GoldenDataPlane
 
     g = GoldenDataPlane(c_max=CFG["c_max"], chpc=CFG["chpc"], q_max=CFG["q_max"], x_max=CFG["x_max"],
-                        cons_max=CFG["cons_max"], ucap=CFG["ucap"], carry_cap=CFG["carry_cap"])
+                        cons_max=CFG["cons_max"], ucap=CFG["ucap"], carry_cap=CFG["carry_cap"],
+                        default_queue_capacity=CFG["default_queue_capacity"])
     d = GpuDataPlane(graph=graph, **CFG)
     steps_g = SCENARIOS[name](g)
     steps_d = SCENARIOS[name](d)
