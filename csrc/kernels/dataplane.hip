@@ -114,6 +114,68 @@ DEV u32 block_scan(u32 v, u32* lds, u32& total) {
   return res;
 }
 
+DEV u64 shfl64(u64 v, u32 src) {
+  u32 lo = __shfl((u32)v, src, 64), hi = __shfl((u32)(v >> 32), src, 64);
+  return (u64(hi) << 32) | lo;
+}
+DEV i64 wave_sum64(i64 v) {
+  u64 x = (u64)v;
+  for (int o = 32; o > 0; o >>= 1) {
+    u32 lo = __shfl_xor((u32)x, o, 64), hi = __shfl_xor((u32)(x >> 32), o, 64);
+    x += (u64(hi) << 32) | lo;
+  }
+  return (i64)x;
+}
+// all 64 lanes must call these (wave-uniform control flow); one atomic per distinct index
+DEV void wave_add_u32(u32* arr, u32 idx, u32 v, bool valid) {
+  u64 pend = __ballot(valid);
+  while (pend) {
+    u32 leader = __ffsll((unsigned long long)pend) - 1;
+    u32 b = __shfl(idx, leader, 64);
+    bool mine = valid && idx == b && ((pend >> lane_id()) & 1);
+    u32 x = mine ? v : 0;
+    for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
+    if (lane_id() == leader) atomicAdd(&arr[b], x);
+    pend &= ~__ballot(mine);
+  }
+}
+DEV void wave_sub_u32(u32* arr, u32 idx, u32 v, bool valid) {
+  u64 pend = __ballot(valid);
+  while (pend) {
+    u32 leader = __ffsll((unsigned long long)pend) - 1;
+    u32 b = __shfl(idx, leader, 64);
+    bool mine = valid && idx == b && ((pend >> lane_id()) & 1);
+    u32 x = mine ? v : 0;
+    for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
+    if (lane_id() == leader) atomicSub(&arr[b], x);
+    pend &= ~__ballot(mine);
+  }
+}
+DEV void wave_add_i64(i64* arr, u64 idx, i64 v, bool valid) {
+  u64 pend = __ballot(valid);
+  while (pend) {
+    u32 leader = __ffsll((unsigned long long)pend) - 1;
+    u64 b = shfl64(idx, leader);
+    bool mine = valid && idx == b && ((pend >> lane_id()) & 1);
+    i64 x = wave_sum64(mine ? v : 0);
+    if (lane_id() == leader) atomicAdd((unsigned long long*)&arr[b], (unsigned long long)x);
+    pend &= ~__ballot(mine);
+  }
+}
+// wave-uniform reservation of `cnt` (per lane) slots from one counter: returns lane's base
+DEV u32 wave_reserve(u32* ctr, bool want, u32* total_out = nullptr) {
+  u64 m = __ballot(want);
+  u32 n = __popcll(m);
+  u32 base = 0;
+  if (n) {
+    u32 leader = __ffsll((unsigned long long)m) - 1;
+    if (lane_id() == leader) base = atomicAdd(ctr, n);
+    base = __shfl(base, leader, 64);
+  }
+  if (total_out) *total_out = n;
+  return base + __popcll(m & lanemask_lt());
+}
+
 // ---- message release (K11): refcount -1, free slot + table index at zero
 DEV void release_msg(const DS& d, u32 msg) {
   if (msg == INVALID) return;
@@ -126,6 +188,29 @@ DEV void release_msg(const DS& d, u32 msg) {
     d.msg_free[slot] = msg;
     atomicAdd(&d.ctr->n_freed, 1u);
   }
+}
+
+// wave-uniform release: refcount atomics per lane, one free-list reservation and one
+// live-bytes atomic per distinct log block per wave (avoids serialising on hot words)
+DEV void wave_release(const DS& d, u32 msg, bool valid) {
+  bool freed = false;
+  u64 blk = 0;
+  i64 sb = 0;
+  if (valid && msg != INVALID) {
+    i32 old = atomicSub(&d.msgs[msg].refcnt, 1);
+    if (old == 1) {
+      freed = true;
+      blk = (d.msgs[msg].log_off / d.log_block) % d.n_log_blocks;
+      sb = d.msgs[msg].slot_bytes;
+    }
+  }
+  u64 fm = __ballot(freed);
+  if (!fm) return;
+  u32 nf;
+  u32 pos = wave_reserve(d.msg_free_top, freed, &nf);
+  if (freed) d.msg_free[pos] = msg;
+  if (lane_id() == __ffsll((unsigned long long)fm) - 1) atomicAdd(&d.ctr->n_freed, nf);
+  wave_add_i64(d.log_live, blk, -sb, freed);
 }
 
 // ============================================================================ topic words
@@ -269,6 +354,32 @@ DEV i32 chan_lookup(const DS& d, u32 conn, u32 ch) {
   return -1;
 }
 
+// chip-wide candidate screen: one u16 mask per 16 work bytes; bit j set when byte j
+// looks like a frame header (type 1/2/3/8, size within the broker frame-max)
+__global__ __launch_bounds__(256) void k_cand(DS d) {
+  const u64 used = d.tot[15];
+  const u64 nch = (used + 15) >> 4;
+  const u32 fm = d.frame_max_global;
+  for (u64 c = (u64)blockIdx.x * 256 + threadIdx.x; c < nch; c += (u64)gridDim.x * 256) {
+    const uint4* q = (const uint4*)(d.work + c * 16);
+    uint4 A = q[0], B = q[1];
+    u32 w[8] = {A.x, A.y, A.z, A.w, B.x, B.y, B.z, B.w};
+    u32 m = 0;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+#define BYTE(k) ((w[(k) >> 2] >> (8 * ((k) & 3))) & 255u)
+      u32 t = BYTE(j);
+      u32 sz = (BYTE(j + 3) << 24) | (BYTE(j + 4) << 16) | (BYTE(j + 5) << 8) | BYTE(j + 6);
+#undef BYTE
+      bool ok = (t == 1 || t == 2 || t == 3 || t == 8) && (fm == 0 || sz <= fm - 8);
+      m |= (ok ? 1u : 0u) << j;
+    }
+    d.cmask[c] = (u16)m;
+  }
+}
+
+#define FS_MARK(k) \
+  do { if (tid == 0 && d.dbg) d.dbg[(u64)s * 16 + (k)] = __builtin_amdgcn_s_memrealtime(); } while (0)
 __global__ __launch_bounds__(256) void k_frame_scan(DS d) {
   __shared__ u32 cpos[CAND_MAX];
   __shared__ int16_t csucc[CAND_MAX];
@@ -308,41 +419,58 @@ __global__ __launch_bounds__(256) void k_frame_scan(DS d) {
   if (tid == 0) { sh_m = 0; sh_over = 0; }
   __syncthreads();
 
-  // ---- (a) candidates
-  for (u32 t0 = 0; t0 < L; t0 += 4096) {
-    u32 p0 = t0 + tid * 16;
-    u32 bits = 0;
-    for (u32 j = 0; j < 16; ++j) {
-      u32 p = p0 + j;
-      if (p >= L) break;
-      if (p + 7 > L) { bits |= 1u << j; continue; }
-      u32 t = b[p];
-      if (!(t == 1 || t == 2 || t == 3 || t == 8)) continue;
-      FInfo f = frame_at(b, p, L, fmax);
-      if (!f.valid_hdr) continue;
-      if ((u64)p + 8 + f.size <= L && !f.complete) continue;
-      bits |= 1u << j;
-    }
-    u32 cnt = __popc(bits), tot;
-    u32 off = block_scan<256>(cnt, sc, tot);
-    u32 m0 = sh_m;
-    for (u32 j = 0; bits; ++j) {
-      if (bits & 1u) {
-        u32 idx = m0 + off;
-        if (idx < CAND_MAX) cpos[idx] = p0 + j;
-        ++off;
+  FS_MARK(0);
+  // ---- (a) candidates: compact the chip-wide candidate mask (k_cand) of this segment,
+  // validate against the connection's frame-max / end marker, append the trailing
+  // positions that can only hold a partial header
+  {
+    const u32 m0 = d.seg_start[s] >> 4;
+    const u32 nm = (L + 15) >> 4;
+    const u32 per = (nm + 255) >> 8;
+    const u32 c0 = tid * per;
+    const u32 c1 = c0 + per < nm ? c0 + per : nm;
+    const u32 lim = L >= 7 ? L - 6 : 0;   // full-header positions are p < lim
+    u32 cnt = 0;
+    for (u32 c = c0; c < c1; ++c) {
+      u32 mk = d.cmask[m0 + c];
+      while (mk) {
+        u32 j = __ffs(mk) - 1;
+        mk &= mk - 1;
+        u32 p = c * 16 + j;
+        if (p >= lim) break;
+        FInfo f = frame_at(b, p, L, fmax);
+        if (f.valid_hdr && (f.complete || (u64)p + 8 + f.size > L)) ++cnt;
       }
-      bits >>= 1;
+    }
+    u32 tot;
+    u32 off = block_scan<256>(cnt, sc, tot);
+    for (u32 c = c0; c < c1; ++c) {
+      u32 mk = d.cmask[m0 + c];
+      while (mk) {
+        u32 j = __ffs(mk) - 1;
+        mk &= mk - 1;
+        u32 p = c * 16 + j;
+        if (p >= lim) break;
+        FInfo f = frame_at(b, p, L, fmax);
+        if (f.valid_hdr && (f.complete || (u64)p + 8 + f.size > L)) {
+          if (off < CAND_MAX) cpos[off] = p;
+          ++off;
+        }
+      }
     }
     __syncthreads();
     if (tid == 0) {
-      u32 nm = m0 + tot;
-      if (nm > CAND_MAX) { sh_over = 1; nm = CAND_MAX; }
-      sh_m = nm;
+      u32 nmc = tot;
+      for (u32 p = lim; p < L; ++p) {
+        if (nmc < CAND_MAX) cpos[nmc] = p;
+        ++nmc;
+      }
+      if (nmc > CAND_MAX) { sh_over = 1; nmc = CAND_MAX; }
+      sh_m = nmc;
     }
     __syncthreads();
-    if (sh_over) break;
   }
+  FS_MARK(1);
   const u32 m = sh_m;
   const bool over = sh_over != 0;
 
@@ -364,6 +492,7 @@ __global__ __launch_bounds__(256) void k_frame_scan(DS d) {
     }
     csucc[i] = (int16_t)sx;
   }
+  FS_MARK(2);
   if (tid == 0) sh_ok = 1;
   __syncthreads();
   // ---- (c) chain: optimistic (every candidate a real frame) else serial walk
@@ -393,6 +522,7 @@ __global__ __launch_bounds__(256) void k_frame_scan(DS d) {
     sh_brk = brk;
   }
   __syncthreads();
+  FS_MARK(3);
   const u32 nf = sh_nf;
   const bool implicit_chain = sh_ok && !(m == 0 || cpos[0] != 0);
 #define CPOS(f) (cpos[implicit_chain ? (f) : chain[f]])
@@ -455,6 +585,7 @@ __global__ __launch_bounds__(256) void k_frame_scan(DS d) {
     if (fi.complete) atomicMin(&sh_stop, (f << 3) | 2);
   }
   __syncthreads();
+  FS_MARK(4);
   u32 stop = sh_stop;
   u32 kf = stop >> 3, reason = stop & 7;
   if (kf > nf) kf = nf;
@@ -475,6 +606,7 @@ __global__ __launch_bounds__(256) void k_frame_scan(DS d) {
   }
   if (over && reason != 0 && kf == nf) so.status |= SS_OVERFLOW;
 
+  FS_MARK(5);
   // ---- (e) emit commands for method frames < kf
   u32 run = 0, frun = 0;
   if (tid == 0) { sh_cmd_base = INVALID; sh_ncmd = 0; }
@@ -494,21 +626,23 @@ __global__ __launch_bounds__(256) void k_frame_scan(DS d) {
   u32 tc, tfr;
   block_scan<256>(my_cmds, sc, tc);
   block_scan<256>(my_frags, sc, tfr);
+  // one uncontended atomicAdd per block (a CAS loop here serialises all blocks);
+  // on overflow the reserved in-range slots are filled with CK_NONE and the whole
+  // segment is carried to the next step
   if (tid == 0) {
-    u32 cb, fb;
-    u32 gc = reserve_upto(&d.ctr->n_cmds, tc, d.cmd_max, &cb);
-    u32 gf = reserve_upto(&d.ctr->n_frags, tfr, d.frag_max, &fb);
-    if (gc < tc || gf < tfr) {
-      // give back and carry the whole segment to the next step
-      if (gc) atomicSub(&d.ctr->n_cmds, gc);
-      if (gf) atomicSub(&d.ctr->n_frags, gf);
-      sh_cmd_base = INVALID;
-    } else {
-      sh_cmd_base = cb;
-      sh_frag_base = fb;
-    }
+    u32 cb = tc ? atomicAdd(&d.ctr->n_cmds, tc) : 0;
+    u32 fb = tfr ? atomicAdd(&d.ctr->n_frags, tfr) : 0;
+    sh_frag_base = fb;
+    sh_cmd_base = cb;
+    sh_ncmd = (cb + tc > d.cmd_max || fb + tfr > d.frag_max) ? 1u : 0u;
   }
   __syncthreads();
+  if (sh_ncmd && tc > 0) {
+    u32 cb = sh_cmd_base;
+    for (u32 i = cb + tid; i < cb + tc && i < d.cmd_max; i += 256) d.cmds[i].kind = CK_NONE;
+    if (tid == 0) sh_cmd_base = INVALID;
+    __syncthreads();
+  }
   if (sh_cmd_base == INVALID && tc > 0) {
     so.status |= SS_OVERFLOW;
     so.status &= ~(SS_FRAME_ERROR | SS_UNEXPECTED);
@@ -516,6 +650,7 @@ __global__ __launch_bounds__(256) void k_frame_scan(DS d) {
     kf = 0;
     reason = 7;
   }
+  FS_MARK(6);
   const i64 now = d.in->now_ms;
   for (u32 f0 = 0; f0 < kf; f0 += 256) {
     u32 f = f0 + tid;
@@ -593,10 +728,12 @@ __global__ __launch_bounds__(256) void k_frame_scan(DS d) {
   if (tid == 0 && kf > 0) d.conn_last_rx[conn] = now;
   if (reason == 0) so.status |= SS_CTRL;
 
+  FS_MARK(7);
   // ---- (f) carry out: bytes [consumed, L)
   u32 rest = L - consumed;
   if (rest > d.carry_cap) { so.status |= SS_TOO_LARGE; rest = 0; }
   else block_copy(d.carry + (u64)conn * d.carry_cap, b + consumed, rest, tid, 256);
+  FS_MARK(8);
   if (tid == 0) {
     so.consumed = consumed;
     so.carry = rest;
@@ -612,6 +749,7 @@ __global__ __launch_bounds__(256) void k_frame_scan(DS d) {
 __global__ void k_classify(DS d) {
   u32 i = blockIdx.x * blockDim.x + threadIdx.x;
   u32 n = d.ctr->n_cmds;
+  if (n > d.cmd_max) n = d.cmd_max;
   if (i >= d.cmd_max) return;
   u32 k = i < n ? d.cmds[i].kind : CK_NONE;
   d.cmd_is_pub[i] = (k == CK_PUBLISH);
@@ -638,6 +776,7 @@ DEV bool skip_shortstr(const u8* p, u32& o, u32 end) {
 __global__ void k_decode(DS d) {
   u32 i = blockIdx.x * blockDim.x + threadIdx.x;
   u32 n = d.ctr->n_cmds;
+  if (n > d.cmd_max) n = d.cmd_max;
   if (i >= n) return;
   const Cmd c = d.cmds[i];
   const u8* w = d.work;
@@ -782,22 +921,42 @@ __global__ void k_decode(DS d) {
 // ============================================================================ scans
 // single-block multi-array exclusive scan; n read from device; totals -> tot[slot+k]
 struct ScanArgs { const u32* in[4]; u32* out[4]; const u32* n; u32 narr; u32 nmax; u32 tot_slot; };
+// single-block exclusive scan over up to 4 arrays; tiles of 4096 with 16-B loads/stores
 __global__ __launch_bounds__(1024) void k_scan(ScanArgs a, u32* tot) {
   __shared__ u32 lds[1024 / 64 + 1];
   u32 n = a.n ? *a.n : a.nmax;
   if (n > a.nmax) n = a.nmax;
-  u32 per = (n + 1023) / 1024;
-  u32 tid = threadIdx.x;
-  u32 b0 = tid * per, b1 = b0 + per;
-  if (b1 > n) b1 = n;
-  for (u32 k = 0; k < a.narr; ++k) {
-    u32 sum = 0;
-    for (u32 i = b0; i < b1; ++i) sum += a.in[k][i];
-    u32 all;
-    u32 off = block_scan<1024>(sum, lds, all);
-    for (u32 i = b0; i < b1; ++i) { u32 v = a.in[k][i]; a.out[k][i] = off; off += v; }
-    if (tid == 0) tot[a.tot_slot + k] = all;
+  const u32 tid = threadIdx.x;
+  u32 run[4] = {0, 0, 0, 0};
+  for (u32 base = 0; base < n; base += 4096) {
+    const u32 i = base + tid * 4;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      if ((u32)k >= a.narr) break;
+      u32 v0 = 0, v1 = 0, v2 = 0, v3 = 0;
+      if (i + 3 < n) {
+        uint4 v = *(const uint4*)(a.in[k] + i);
+        v0 = v.x; v1 = v.y; v2 = v.z; v3 = v.w;
+      } else {
+        if (i < n) v0 = a.in[k][i];
+        if (i + 1 < n) v1 = a.in[k][i + 1];
+        if (i + 2 < n) v2 = a.in[k][i + 2];
+      }
+      u32 sum = v0 + v1 + v2 + v3, all;
+      u32 off = run[k] + block_scan<1024>(sum, lds, all);
+      uint4 o;
+      o.x = off; o.y = off + v0; o.z = o.y + v1; o.w = o.z + v2;
+      if (i + 3 < n) *(uint4*)(a.out[k] + i) = o;
+      else {
+        if (i < n) a.out[k][i] = o.x;
+        if (i + 1 < n) a.out[k][i + 1] = o.y;
+        if (i + 2 < n) a.out[k][i + 2] = o.z;
+      }
+      run[k] += all;
+    }
   }
+  if (tid == 0)
+    for (u32 k = 0; k < a.narr; ++k) tot[a.tot_slot + k] = run[k];
 }
 
 // ============================================================================ radix sort
@@ -818,6 +977,24 @@ __global__ __launch_bounds__(256) void k_rs_hist(const u32* keys, const u32* np,
   }
   __syncthreads();
   hist[tid * ntiles + t] = cnt[tid];
+}
+
+// digit-major offsets for the occupied tiles only: one thread per digit
+__global__ __launch_bounds__(256) void k_rs_offsets(const u32* hist, u32* hscan, const u32* np, u32 ntiles) {
+  __shared__ u32 lds[256 / 64 + 1];
+  u32 n = *np;
+  u32 T = (n + SORT_TILE - 1) / SORT_TILE;
+  if (T > ntiles) T = ntiles;
+  u32 dg = threadIdx.x;
+  u32 sum = 0;
+  for (u32 t = 0; t < T; ++t) sum += hist[dg * ntiles + t];
+  u32 all;
+  u32 run = block_scan<256>(sum, lds, all);
+  for (u32 t = 0; t < T; ++t) {
+    u32 h = hist[dg * ntiles + t];
+    hscan[dg * ntiles + t] = run;
+    run += h;
+  }
 }
 
 __global__ __launch_bounds__(256) void k_rs_scatter(const u32* kin, const u32* vin, u32* kout, u32* vout,
@@ -947,14 +1124,22 @@ __global__ void k_route(DS d) {
     return;
   }
   Pub& pb = d.pubs[p];
-  if (PASS == 1 && d.pub_nq[p] == 0) return;
-  u32 nq = 0;
   u32 wbase = PASS ? d.pub_pair_off[p] : 0;
+  if (PASS == 1) {
+    u32 nq0 = d.pub_nq[p];
+    if (nq0 == 0) return;
+    if (nq0 <= 8) {  // routing result cached by pass 0
+      for (u32 k = 0; k < nq0; ++k) { d.pair_k[0][wbase + k] = d.pub_qc[(u64)p * 8 + k]; d.pair_v[0][wbase + k] = p; }
+      return;
+    }
+  }
+  u32 nq = 0;
   bool has_cons = false;
 #define EMIT(q)                                              \
   do {                                                       \
     u32 _q = (q);                                            \
     if (PASS) { d.pair_k[0][wbase + nq] = _q; d.pair_v[0][wbase + nq] = p; } \
+    else if (nq < 8) d.pub_qc[(u64)p * 8 + nq] = _q;         \
     if (d.q_cons_n[_q]) has_cons = true;                     \
     ++nq;                                                    \
   } while (0)
@@ -1087,9 +1272,24 @@ __global__ __launch_bounds__(256) void k_store(DS d) {
     m.pad = 0;
     d.msgs[msg] = m;
     pb.msg = msg;
-    u64 blk = (off / d.log_block) % d.n_log_blocks;
-    atomicAdd((unsigned long long*)&d.log_live[blk], (unsigned long long)pb.slot_bytes);
   }
+}
+
+// thread per publish: account stored bytes per log block (one atomic per block per wave)
+__global__ void k_live_add(DS d) {
+  u32 p = blockIdx.x * blockDim.x + threadIdx.x;
+  u32 n = d.ctr->n_pubs;
+  if (n > d.pub_max) n = d.pub_max;
+  u64 base = *d.log_step_base;
+  bool valid = p < n && base != INVALID && d.pub_nq[p] > 0;
+  u64 blk = 0;
+  i64 sb = 0;
+  if (valid) {
+    u64 off = base + d.pub_slot_off[p];
+    blk = (off / d.log_block) % d.n_log_blocks;
+    sb = d.pub_slot[p];
+  }
+  wave_add_i64(d.log_live, blk, sb, valid);
 }
 
 // ============================================================================ K7 enqueue
@@ -1101,10 +1301,7 @@ __global__ void k_qfirst(DS d, u32 src) {
   if (i == 0 || k[i - 1] != k[i]) d.q_first[k[i]] = i;
 }
 
-__global__ void k_enqueue(DS d, u32 src) {
-  u32 i = blockIdx.x * blockDim.x + threadIdx.x;
-  u32 n = d.tot[0];
-  if (i >= n) return;
+DEV u32 enqueue_one(const DS& d, u32 src, u32 i, u32 n) {
   const u32* kk = d.pair_k[src];
   u32 q = kk[i];
   u32 p = d.pair_v[src][i];
@@ -1115,7 +1312,8 @@ __global__ void k_enqueue(DS d, u32 src) {
   u64 head = d.q_head[q], tail = d.q_tail[q];
   u64 cap = d.q_ring_mask[q] + 1;
   u64 freec = cap - (tail - head);
-  if (pb.msg == INVALID) return;
+  u32 drop = INVALID;
+  if (pb.msg == INVALID) return INVALID;
   if (rank < freec) {
     u64 pos = tail + rank;
     Desc ds;
@@ -1127,14 +1325,23 @@ __global__ void k_enqueue(DS d, u32 src) {
     ds.expire_ms = e;
     d.ring[d.q_ring_off[q] + (pos & d.q_ring_mask[q])] = ds;
   } else {
-    atomicAdd(&d.ctr->n_ring_full, 1u);
-    release_msg(d, pb.msg);
+    drop = pb.msg;
   }
   if (last) {
     u64 cnt = rank + 1;
     d.q_tail[q] = tail + (cnt < freec ? cnt : freec);
   }
+  return drop;
 }
+
+__global__ void k_enqueue(DS d, u32 src) {
+  u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+  u32 n = d.tot[0];
+  u32 drop = i < n ? enqueue_one(d, src, i, n) : INVALID;
+  wave_release(d, drop, drop != INVALID);
+  if (drop != INVALID) atomicAdd(&d.ctr->n_ring_full, 1u);
+}
+
 
 // ============================================================================ K9 acks
 __global__ void k_acks(DS d) {
@@ -1175,39 +1382,37 @@ __global__ __launch_bounds__(256) void k_chan_advance(DS d) {
   USlot* win = d.uwin + (u64)ch * (d.ucap_mask + 1);
   bool contiguous = true;
   u64 newhead = head;
-  u32 released = 0;
+  u32 released = 0, manual_done = 0;
   for (u64 t0 = head; t0 < nt; t0 += 64) {
     u64 t = t0 + lane;
     bool valid = t < nt;
     u32 st = US_FREE;
     USlot u;
+    u.state = US_FREE; u.msg = INVALID; u.q = 0; u.cons = 0; u.qpos = 0; u.expire_ms = 0;
     if (valid) {
       u = win[(t - 1) & d.ucap_mask];
       st = u.state;
       if (st == US_PENDING && t <= aup) st = US_ACKED;
       if (st == US_PENDING && t <= rup) st = US_REQUEUE;
-      if (st == US_ACKED) {
-        release_msg(d, u.msg);
-        atomicSub(&d.cons_unacked[u.cons], 1u);
-        atomicSub(&d.ch_unacked[ch], 1u);
-        st = US_DONE;
-      } else if (st == US_REQUEUE) {
-        u32 ri = atomicAdd(d.req_n, 1u);
-        if (ri < d.req_max) {
-          ReqItem r;
-          r.q = u.q; r.msg = u.msg; r.qpos = u.qpos; r.expire_ms = u.expire_ms;
-          d.req[ri] = r;
-          atomicAdd(&d.req_q_n[u.q], 1u);
-        } else {
-          release_msg(d, u.msg);  // requeue list overflow: drop (counted)
-        }
-        atomicSub(&d.cons_unacked[u.cons], 1u);
-        atomicSub(&d.ch_unacked[ch], 1u);
-        atomicAdd(&d.ctr->n_requeue, 1u);
-        st = US_DONE;
-      }
-      if (st != u.state) win[(t - 1) & d.ucap_mask].state = st;
     }
+    bool acked = valid && st == US_ACKED;
+    bool req = valid && st == US_REQUEUE;
+    // requeue list (one reservation per wave)
+    u32 rtot;
+    u32 ri = wave_reserve(d.req_n, req, &rtot);
+    bool req_ok = req && ri < d.req_max;
+    if (req_ok) {
+      ReqItem r;
+      r.q = u.q; r.msg = u.msg; r.qpos = u.qpos; r.expire_ms = u.expire_ms;
+      d.req[ri] = r;
+    }
+    wave_add_u32(d.req_q_n, u.q, 1u, req_ok);
+    wave_release(d, u.msg, acked || (req && !req_ok));
+    wave_sub_u32(d.cons_unacked, u.cons, 1u, acked || req);
+    manual_done += __popcll(__ballot(acked || req));
+    if (lane == 0 && rtot) atomicAdd(&d.ctr->n_requeue, rtot);
+    if (acked || req) st = US_DONE;
+    if (valid && st != u.state) win[(t - 1) & d.ucap_mask].state = st;
     if (contiguous) {
       u64 notdone = __ballot(valid && st != US_DONE);
       u64 vm = __ballot(valid);
@@ -1220,6 +1425,7 @@ __global__ __launch_bounds__(256) void k_chan_advance(DS d) {
   if (lane == 0) {
     d.ch_uhead[ch] = newhead;
     atomicSub(&d.ch_win[ch], released);
+    if (manual_done) atomicSub(&d.ch_unacked[ch], manual_done);
     d.ch_dirty[ch] = 0;
   }
 }
@@ -1265,7 +1471,8 @@ __global__ __launch_bounds__(256) void k_dequeue(DS d) {
     bool exp = valid && ds.expire_ms != 0 && ds.expire_ms <= now;
     u64 live = __ballot(valid && !exp);
     u32 nexp = live ? (__ffsll((unsigned long long)live) - 1) : __popcll(__ballot(valid));
-    if (lane < nexp) { release_msg(d, ds.msg); atomicAdd(&d.ctr->n_expired, 1u); }
+    wave_release(d, ds.msg, lane < nexp);
+    if (lane == 0 && nexp) atomicAdd(&d.ctr->n_expired, nexp);
     head += nexp;
     if (live) break;
   }
@@ -1410,11 +1617,7 @@ __global__ void k_dfirst(DS d, u32 src) {
   if (i + 1 == n || (k[i + 1] / d.chpc) != conn) d.conn_dlast[conn] = i;
 }
 
-__global__ void k_tags(DS d, u32 src) {
-  u32 i = blockIdx.x * blockDim.x + threadIdx.x;
-  u32 n = d.ctr->n_deliv;
-  if (i >= d.deliv_max) return;
-  if (i >= n) { d.dv_size[i] = 0; return; }
+DEV u32 tag_one(const DS& d, u32 src, u32 i, u32 n) {
   const u32* kk = d.dv_k[src];
   u32 ch = kk[i];
   u32 di = d.dv_v[src][i];
@@ -1437,14 +1640,25 @@ __global__ void k_tags(DS d, u32 src) {
   d.dv_size[i] = sz;
   dv.tag = tag;
   u32 lat = (u32)d.in->step - m.pub_step;
-  atomicAdd(&d.ctr->lat_hist[lat < LAT_BINS ? lat : LAT_BINS - 1], 1u);
   if (last) {
     if (atomicExch(&d.ch_dirty[ch], 1u) == 0) {
       u32 k = atomicAdd(d.n_dirty, 1u);
       d.dirty_list[k] = ch;
     }
   }
+  return lat;
 }
+
+__global__ void k_tags(DS d, u32 src) {
+  u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+  u32 n = d.ctr->n_deliv;
+  bool valid = i < n;
+  u32 lat = 0;
+  if (valid) lat = tag_one(d, src, i, n);
+  else if (i < d.deliv_max) d.dv_size[i] = 0;
+  wave_add_u32(d.ctr->lat_hist, lat < LAT_BINS ? lat : LAT_BINS - 1, 1u, valid);
+}
+
 
 // per connection: egress size = returns + confirms + deliveries
 __global__ void k_conn_sizes(DS d) {
@@ -1633,13 +1847,17 @@ __global__ __launch_bounds__(256) void k_render_returns(DS d) {
 __global__ void k_post(DS d, u32 src) {
   u32 i = blockIdx.x * blockDim.x + threadIdx.x;
   u32 n = d.ctr->n_deliv;
+  u32 msg = INVALID;
+  bool aa = false;
   if (i < n) {
     const Deliv& dv = d.deliv[d.dv_v[src][i]];
-    if (dv.flags & 2) release_msg(d, dv.msg);
+    aa = dv.flags & 2;
+    msg = dv.msg;
     const u32* kk = d.dv_k[src];
     u32 ch = kk[i];
     if (i + 1 == n || kk[i + 1] != ch) d.ch_next_tag[ch] = dv.tag + 1;
   }
+  wave_release(d, msg, aa);
   // reset per-connection scratch
   if (i < d.c_max) {
     d.conn_dfirst[i] = INVALID;

@@ -15,7 +15,7 @@ struct DS {
   u32 c_max, chpc, q_max, x_max, cons_max, seg_max;
   u32 carry_cap, cmd_max, frag_max, pub_max, ack_max, pair_max, deliv_max, msg_max;
   u32 ucap_mask, deliver_cap, chmap_size, xhash_mask, dhash_mask, tb_max, tb_pad, req_max;
-  u32 q_bits, ch_bits, hash_wildcard, pad_;
+  u32 q_bits, ch_bits, hash_wildcard, frame_max_global;
   u64 log_bytes, log_block, n_log_blocks, work_cap, ingress_cap, egress_cap, ctrl_cap, ring_pool;
 
   // ---------------- step io
@@ -49,6 +49,7 @@ struct DS {
   u32* seg_start;
   u32* seg_total;
   u8* work;
+  u16* cmask;               // candidate bitmask, one u16 per 16 work bytes
 
   // ---------------- commands
   Cmd* cmds;
@@ -63,6 +64,7 @@ struct DS {
   i8* pub_keyvec;           // [pub_max][TOPIC_K]
   u16* pub_match;           // [pub_max][tb_pad/16]
   u32* pub_nq;
+  u32* pub_qc;              // [pub_max][8] routed queues cached by route pass 0
   u32* pub_slot;
   u32* pub_routed;
   u32* pub_pair_off;
@@ -157,4 +159,5 @@ struct DS {
   u32* hist_scan;
   u32* tot;                 // scan totals [64]
   u32* egress_budget;       // bytes reserved by dequeue this step
+  u64* dbg;                 // per-segment phase timestamps (s_memrealtime, 100 MHz)
 };

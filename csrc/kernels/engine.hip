@@ -68,6 +68,7 @@ class Engine {
     d_.tb_pad = ((d_.tb_max + 15) / 16) * 16;
     d_.req_max = (u32)get("req_max", 65536);
     d_.hash_wildcard = (u32)get("hash_wildcard", 1);
+    d_.frame_max_global = (u32)get("frame_max", 131072);
     d_.log_bytes = get("log_bytes", 1ull << 32);
     d_.log_block = get("log_block", 4ull << 20);
     d_.log_bytes = (d_.log_bytes / d_.log_block) * d_.log_block;
@@ -118,6 +119,7 @@ class Engine {
     d_.seg_start = (u32*)dev("seg_start", 4ull * d_.seg_max);
     d_.seg_total = (u32*)dev("seg_total", 4ull * d_.seg_max);
     d_.work = (u8*)dev("work", d_.work_cap + 4096);
+    d_.cmask = (u16*)dev("cmask", 2ull * ((d_.work_cap + 4096) / 16 + 1));
 
     d_.cmds = (Cmd*)dev("cmds", sizeof(Cmd) * (u64)d_.cmd_max);
     d_.frags = (Frag*)dev("frags", sizeof(Frag) * (u64)d_.frag_max);
@@ -130,6 +132,7 @@ class Engine {
     d_.pub_keyvec = (i8*)dev("pub_keyvec", (u64)d_.pub_max * TOPIC_K + 64);
     d_.pub_match = (u16*)dev("pub_match", 2ull * d_.pub_max * (d_.tb_pad / 16) + 64);
     d_.pub_nq = (u32*)dev("pub_nq", 4ull * d_.pub_max);
+    d_.pub_qc = (u32*)dev("pub_qc", 32ull * d_.pub_max);
     d_.pub_slot = (u32*)dev("pub_slot", 4ull * d_.pub_max);
     d_.pub_routed = (u32*)dev("pub_routed", 4ull * d_.pub_max);
     d_.pub_pair_off = (u32*)dev("pub_pair_off", 4ull * d_.pub_max);
@@ -238,6 +241,7 @@ class Engine {
     d_.scan_tmp = (u32*)dev("scan_tmp", 4ull * 1024);
     d_.tot = (u32*)dev("tot", 4ull * 64);
     d_.egress_budget = (u32*)dev("egress_budget", 4);
+    d_.dbg = (u64*)dev("dbg", 8ull * 16 * d_.seg_max);
 
     // ---- initial state
     fill("conn_dfirst", 0xff);
@@ -415,7 +419,7 @@ class Engine {
     u32 src = 0;
     for (u32 shift = 0; shift < bits; shift += 8) {
       hipLaunchKernelGGL(k_rs_hist, dim3(ntiles), dim3(256), 0, s, keys[src], n, shift, d_.hist, ntiles);
-      launch_scan(s, {{d_.hist, d_.hist_scan}}, nullptr, 256 * ntiles, 60);
+      hipLaunchKernelGGL(k_rs_offsets, dim3(1), dim3(256), 0, s, d_.hist, d_.hist_scan, n, ntiles);
       hipLaunchKernelGGL(k_rs_scatter, dim3(ntiles), dim3(256), 0, s, keys[src], vals[src], keys[src ^ 1],
                          vals[src ^ 1], n, shift, d_.hist_scan, ntiles);
       src ^= 1;
@@ -429,6 +433,7 @@ class Engine {
     auto blocks = [](u64 n, u32 per) { return dim3(n ? ceil_div(n, per) : 1); };
     hipLaunchKernelGGL(k_prep, dim3(1), dim3(1024), 0, s, d);
     hipLaunchKernelGGL(k_stage, dim3(d.seg_max, 4), dim3(256), 0, s, d);
+    hipLaunchKernelGGL(k_cand, dim3(2048), dim3(256), 0, s, d);
     hipLaunchKernelGGL(k_frame_scan, dim3(d.seg_max), dim3(256), 0, s, d);
     hipLaunchKernelGGL(k_classify, blocks(d.cmd_max, 256), dim3(256), 0, s, d);
     launch_scan(s, {{d.cmd_is_pub, d.cmd_pub_rank}, {d.cmd_is_ack, d.cmd_ack_rank}}, &d.ctr->n_cmds,
@@ -445,6 +450,7 @@ class Engine {
     hipLaunchKernelGGL(k_route<1>, blocks(d.pub_max, 256), dim3(256), 0, s, d);
     hipLaunchKernelGGL(k_log_reserve, dim3(1), dim3(64), 0, s, d);
     hipLaunchKernelGGL(k_store, blocks((u64)d.pub_max * 64, 256), dim3(256), 0, s, d);
+    hipLaunchKernelGGL(k_live_add, blocks(d.pub_max, 256), dim3(256), 0, s, d);
     u32* pk[2] = {d.pair_k[0], d.pair_k[1]};
     u32* pv[2] = {d.pair_v[0], d.pair_v[1]};
     u32 psrc = radix_sort(s, pk, pv, &d.tot[0], d.pair_max, d.q_bits);
