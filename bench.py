@@ -114,35 +114,53 @@ def main():
     base = pool.ctypes.data
     step_i = 0
 
-    def run(n, collect=False):
+    def run(n):
+        # software pipeline, 3 steps in flight: H2D(t+1) || kernels(t) || D2H(t-1);
+        # the host consumes step t-1's results/egress while the GPU runs step t
         nonlocal step_i
         dl = pb = 0
         hist = np.zeros(32, np.int64)
         eg = 0
-        for _ in range(n):
-            b = step_i % args.blocks
-            r = dp.step_raw(segs[b], base + offs[b], blens[b], collect=False)
+        pending = []
+        done = []
+
+        def account(r):
+            nonlocal dl, pb, eg
             c = r.counters
             dl += c["n_deliv"]
             pb += c["n_pubs"]
             eg += c["egress_bytes"]
-            hist += np.array(c["lat_hist"], np.int64)
+            hist[:] += np.array(c["lat_hist"], np.int64)
+
+        for _ in range(n):
+            b = step_i % args.blocks
+            pending.append(dp.submit_raw(segs[b], base + offs[b], blens[b]))
             step_i += 1
+            if len(pending) > 1:
+                t = pending.pop(0)
+                account(dp.finish(t, collect=False, wait_egress=False))
+                if done:
+                    dp.egress_wait(done.pop(0))
+                done.append(t)
+        for t in pending:
+            account(dp.finish(t, collect=False, wait_egress=True))
+        for t in done:
+            dp.egress_wait(t)
         return dl, pb, hist, eg
 
     run(args.warmup)
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
-    dp.eng.sync(dp.stream)
+    dp.eng.sync()
     t0 = time.perf_counter()
     dl, pb, hist, eg = run(args.steps)
-    dp.eng.sync(dp.stream)
+    dp.eng.sync()
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
     t = time.perf_counter() - t0
-    c = dp.eng.counters()
+    c = dp.eng.counters((step_i - 1) & 1)
     errs = {k: c[k] for k in ("n_dropped_nomem", "n_ring_full", "n_unknown_exchange", "n_unroutable", "n_routed_msgs", "n_pairs", "n_deliv", "n_live_msgs") if c[k]}
 
     vals = np.array([t, dl, pb, eg], np.float64)
@@ -157,11 +175,12 @@ def main():
         dl, pb, eg = (float(x) for x in ss.tolist())
         hist = hh.cpu().numpy()
     ms_step = 1000.0 * t / args.steps
-    # p50: deliveries by (deliver step - publish step); a message delivered k steps after
-    # its publish step waited (k+1) step periods from ingress submit to egress ready
+    # p50: deliveries by (deliver step - publish step).  With the 3-deep pipeline a message
+    # submitted in step s is in host memory ~3 step periods later (H2D, kernels, D2H), plus
+    # k more periods if it waited k steps in its queue
     cum = np.cumsum(hist)
     p50_bin = int(np.searchsorted(cum, cum[-1] / 2.0)) if cum[-1] else 0
-    p50_ms = (p50_bin + 1) * ms_step
+    p50_ms = (p50_bin + 3) * ms_step
     if rank == 0:
         out = {
             "metric": METRIC,

@@ -46,16 +46,15 @@ class GpuDataPlane(ControlState):
         assert sz["CtrlRec"] == CTRL_REC.itemsize and sz["ConnOut"] == CONN_OUT.itemsize
         self.device = device
         self.worker = worker
-        self.stream = self.mod.create_stream(device)
         self.step_no = 0
-        self.carry = defaultdict(int)
         i = self.info
-        self._seg_out = self.eng.host_view("seg_out").view(SEG_OUT)
-        self._ctrl_rec = self.eng.host_view("ctrl_rec").view(CTRL_REC)
-        self._conn_out = self.eng.host_view("conn_out").view(CONN_OUT)
-        self._egress = self.eng.host_view("egress")
-        self._ctrl = self.eng.host_view("ctrl")
-        self._pin = None
+        self.carry = np.zeros(i["c_max"], np.int64)
+        self._io = [dict(seg_out=self.eng.host_view(f"seg_out{p}").view(SEG_OUT),
+                         ctrl_rec=self.eng.host_view(f"ctrl_rec{p}").view(CTRL_REC),
+                         conn_out=self.eng.host_view(f"conn_out{p}").view(CONN_OUT),
+                         ctrl=self.eng.host_view(f"ctrl{p}"),
+                         egress=self.eng.host_view(f"egress_host{p}")) for p in (0, 1)]
+        self._pin = [None, None]
         self.requeue_pending = False
         super().__init__(c_max=i["c_max"], chpc=i["chpc"], q_max=i["q_max"], x_max=i["x_max"],
                          cons_max=i["cons_max"], hash_wildcard=hash_wildcard, ring_pool=i["ring_pool"],
@@ -184,6 +183,8 @@ class GpuDataPlane(ControlState):
         self._up_at("conn_paused", 0, conn, np.uint32)
         self._up_at("carry_len", 0, conn, np.uint32)
         self.carry[conn] = 0
+        if c is None:
+            self._up_at("conn_paused", 0, conn, np.uint32)
         self._chmap_row(conn)
 
     def channel_opened(self, chan):
@@ -278,23 +279,25 @@ class GpuDataPlane(ControlState):
         self._up_at("conn_paused", 0, conn, np.uint32)
 
     # ================================================================== steps
-    def _pinned(self, n):
-        if self._pin is None or len(self._pin) < n:
-            self._pin = self.mod.alloc_pinned(max(n, 1 << 20))
-        return self._pin
+    def _pinned(self, n, parity):
+        pin = self._pin[parity]
+        if pin is None or len(pin) < n:
+            pin = self._pin[parity] = self.mod.alloc_pinned(max(n, 1 << 20))
+        return pin
 
     def step(self, inputs=None, now_ms=None, collect=True):
-        """One data-plane step.  ``inputs``: {conn: bytes}.  Connections holding carry
-        (partial commands) are re-presented automatically once unpaused."""
+        """One synchronous data-plane step.  ``inputs``: {conn: bytes}.  Connections
+        holding carry (partial commands) are re-presented once unpaused."""
         inputs = inputs or {}
         conns = set(inputs)
-        for c, cl in self.carry.items():
-            if cl and c in self.conns and not self.conns[c].paused:
+        for c in np.nonzero(self.carry)[0]:
+            c = int(c)
+            if c in self.conns and not self.conns[c].paused:
                 conns.add(c)
         order = sorted(conns)
         segs = np.zeros(len(order), SEG_IN)
-        total = sum(len(inputs.get(c, b"")) + 15 & ~15 for c in order)
-        pin = self._pinned(total + 16)
+        total = sum((len(inputs.get(c, b"")) + 15) & ~15 for c in order)
+        pin = self._pinned(total + 16, self.step_no & 1)
         off = 0
         for k, c in enumerate(order):
             data = inputs.get(c, b"")
@@ -306,41 +309,55 @@ class GpuDataPlane(ControlState):
         return self.step_raw(segs, pin.ctypes.data, off, now_ms, collect)
 
     def step_raw(self, segs, payload_ptr, payload_len, now_ms=None, collect=True):
-        t0 = time.perf_counter()
-        if self.requeue_pending:
-            self.eng.requeue(self.stream)
-            self.requeue_pending = False
+        t = self.submit_raw(segs, payload_ptr, payload_len, now_ms)
+        return self.finish(t, collect=collect)
+
+    def submit_raw(self, segs, payload_ptr, payload_len, now_ms=None):
+        """Asynchronous half of a step: returns a ticket for ``finish``.  At most two
+        steps may be outstanding (double-buffered step IO)."""
         now = int(time.time() * 1000) if now_ms is None else int(now_ms)
-        self.eng.submit(segs, int(payload_ptr), int(payload_len), now, self.step_no, now, self.worker,
-                        self.stream)
-        self.eng.sync(self.stream)
+        t0 = time.perf_counter()
+        p = self.eng.submit(segs, int(payload_ptr), int(payload_len), now, self.step_no, now, self.worker)
         self.step_no += 1
+        return (p, len(segs), t0)
+
+    def finish(self, ticket, collect=True, wait_egress=True):
+        p, nseg, t0 = ticket
+        self.eng.wait_results(p)
         res = StepResult()
+        res.counters = c = self.eng.counters(p)
+        io = self._io[p]
+        so = io["seg_out"][:nseg]
+        self.carry[so["conn"]] = so["carry"]
+        paused = (so["status"] & SS_CTRL) != 0
+        if paused.any():
+            for conn in so["conn"][paused]:
+                cc = self.conns.get(int(conn))
+                if cc is not None:
+                    cc.paused = True
+        if c["n_requeue"]:
+            self.eng.request_requeue()
+        self.eng.egress_copy(p)
+        if collect:
+            res.segs = [tuple(int(x) for x in (r["conn"], r["status"], r["consumed"], r["carry"],
+                                                 r["ncmds"], r["err_off"])) for r in so]
+            nctrl = min(c["n_ctrl"], len(io["ctrl_rec"]))
+            for rec in io["ctrl_rec"][:nctrl]:
+                if int(rec["off"]) == INVALID:
+                    res.events.append((int(rec["conn"]), int(rec["len"]), int(rec["seg"])))
+                else:
+                    o, n = int(rec["off"]), int(rec["len"])
+                    res.ctrl.append((int(rec["conn"]), bytes(io["ctrl"][o:o + n])))
+        if wait_egress or collect:
+            self.eng.egress_wait(p)
+        if collect:
+            co = io["conn_out"]
+            eg = io["egress"]
+            for conn in np.nonzero(co["len"])[0]:
+                o, n = int(co["off"][conn]), int(co["len"][conn])
+                res.egress[int(conn)] = bytes(eg[o:o + n])
         res.elapsed = time.perf_counter() - t0
-        res.counters = self.eng.counters()
-        nseg = len(segs)
-        so = self._seg_out[:nseg]
-        for r in so:
-            conn = int(r["conn"])
-            self.carry[conn] = int(r["carry"])
-            if r["status"] & SS_CTRL and conn in self.conns:
-                self.conns[conn].paused = True
-        if res.counters["n_requeue"]:
-            self.requeue_pending = True
-        if not collect:
-            return res
-        res.segs = [tuple(int(x) for x in (r["conn"], r["status"], r["consumed"], r["carry"],
-                                             r["ncmds"], r["err_off"])) for r in so]
-        nctrl = min(res.counters["n_ctrl"], len(self._ctrl_rec))
-        for rec in self._ctrl_rec[:nctrl]:
-            if int(rec["off"]) == INVALID:
-                res.events.append((int(rec["conn"]), int(rec["len"]), int(rec["seg"])))
-            else:
-                o, n = int(rec["off"]), int(rec["len"])
-                res.ctrl.append((int(rec["conn"]), bytes(self._ctrl[o:o + n])))
-        co = self._conn_out
-        nz = np.nonzero(co["len"])[0]
-        for c in nz:
-            o, n = int(co["off"][c]), int(co["len"][c])
-            res.egress[int(c)] = bytes(self._egress[o:o + n])
         return res
+
+    def egress_wait(self, ticket):
+        self.eng.egress_wait(ticket[0])

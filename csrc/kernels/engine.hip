@@ -90,17 +90,26 @@ class Engine {
     // ---- allocations
     auto dev = [&](const char* name, size_t bytes) { return alloc(name, bytes, false); };
     auto hst = [&](const char* name, size_t bytes) { return alloc(name, bytes, true); };
-    d_.in = (StepIn*)dev("in", sizeof(StepIn));
-    d_.segs = (const SegIn*)dev("segs", sizeof(SegIn) * d_.seg_max);
-    d_.ingress = (const u8*)dev("ingress", d_.ingress_cap + 64);
-    d_.seg_out = (SegOut*)hst("seg_out", sizeof(SegOut) * d_.seg_max);
     d_.ctr = (Counters*)dev("ctr", sizeof(Counters));
-    d_.ctr_host = (Counters*)hst("ctr_host", sizeof(Counters));
     egress_alloc_ = d_.egress_cap + d_.work_cap + (u64)nch * 21 + 4096;
-    d_.egress = (u8*)hst("egress", egress_alloc_);
-    d_.conn_out = (ConnOut*)hst("conn_out", sizeof(ConnOut) * d_.c_max);
-    d_.ctrl = (u8*)hst("ctrl", d_.ctrl_cap);
-    d_.ctrl_rec = (CtrlRec*)hst("ctrl_rec", sizeof(CtrlRec) * d_.seg_max * 2);
+    // per-parity step IO: step t uses set t&1, so step t+1's H2D and step t-1's D2H
+    // overlap step t's kernels (double buffering; the graph of each parity is captured once)
+    for (int p = 0; p < 2; ++p) {
+      std::string sfx = std::to_string(p);
+      DS& io = io_[p];
+      io.in = (StepIn*)dev(("in" + sfx).c_str(), sizeof(StepIn));
+      io.segs = (const SegIn*)dev(("segs" + sfx).c_str(), sizeof(SegIn) * d_.seg_max);
+      io.ingress = (const u8*)dev(("ingress" + sfx).c_str(), d_.ingress_cap + 64);
+      io.seg_out = (SegOut*)hst(("seg_out" + sfx).c_str(), sizeof(SegOut) * d_.seg_max);
+      io.ctr_host = (Counters*)hst(("ctr_host" + sfx).c_str(), sizeof(Counters));
+      io.egress = (u8*)dev(("egress" + sfx).c_str(), egress_alloc_);
+      io.conn_out = (ConnOut*)hst(("conn_out" + sfx).c_str(), sizeof(ConnOut) * d_.c_max);
+      io.ctrl = (u8*)hst(("ctrl" + sfx).c_str(), d_.ctrl_cap);
+      io.ctrl_rec = (CtrlRec*)hst(("ctrl_rec" + sfx).c_str(), sizeof(CtrlRec) * d_.seg_max * 2);
+      egress_host_[p] = (u8*)pinned(("egress_host" + sfx).c_str(), egress_alloc_);
+      stage_in_[p] = (StepIn*)pinned(("stage_in" + sfx).c_str(), sizeof(StepIn));
+      stage_segs_[p] = (SegIn*)pinned(("stage_segs" + sfx).c_str(), sizeof(SegIn) * d_.seg_max);
+    }
 
     d_.carry = (u8*)dev("carry", (u64)d_.c_max * d_.carry_cap + 64);
     d_.carry_len = (u32*)dev("carry_len", 4ull * d_.c_max);
@@ -243,6 +252,21 @@ class Engine {
     d_.egress_budget = (u32*)dev("egress_budget", 4);
     d_.dbg = (u64*)dev("dbg", 8ull * 16 * d_.seg_max);
 
+    for (int p = 0; p < 2; ++p) {
+      DS io = d_;
+      io.in = io_[p].in; io.segs = io_[p].segs; io.ingress = io_[p].ingress; io.seg_out = io_[p].seg_out;
+      io.ctr_host = io_[p].ctr_host; io.egress = io_[p].egress; io.conn_out = io_[p].conn_out;
+      io.ctrl = io_[p].ctrl; io.ctrl_rec = io_[p].ctrl_rec;
+      io_[p] = io;
+    }
+    HIPCHECK(hipStreamCreateWithFlags(&s_comp_, hipStreamNonBlocking));
+    HIPCHECK(hipStreamCreateWithFlags(&s_h2d_, hipStreamNonBlocking));
+    HIPCHECK(hipStreamCreateWithFlags(&s_d2h_, hipStreamNonBlocking));
+    for (int p = 0; p < 2; ++p) {
+      HIPCHECK(hipEventCreateWithFlags(&ev_h2d_[p], hipEventDisableTiming));
+      HIPCHECK(hipEventCreateWithFlags(&ev_done_[p], hipEventDisableTiming));
+      HIPCHECK(hipEventCreateWithFlags(&ev_d2h_[p], hipEventDisableTiming));
+    }
     // ---- initial state
     fill("conn_dfirst", 0xff);
     fill("conn_dlast", 0xff);
@@ -253,16 +277,38 @@ class Engine {
     HIPCHECK(hipMemcpy(d_.msg_free, fl.data(), 4ull * d_.msg_max, hipMemcpyHostToDevice));
     HIPCHECK(hipMemcpy(d_.msg_free_top, &d_.msg_max, 4, hipMemcpyHostToDevice));
     HIPCHECK(hipDeviceSynchronize());
-    step_in_ = StepIn{};
   }
 
   ~Engine() {
-    if (graph_exec_) hipGraphExecDestroy(graph_exec_);
-    if (req_exec_) hipGraphExecDestroy(req_exec_);
-    for (auto& kv : bufs_) {
-      if (kv.second.host) hipHostFree(kv.second.ptr);
-      else hipFree(kv.second.ptr);
+    hipStreamSynchronize(s_comp_);
+    hipStreamSynchronize(s_h2d_);
+    hipStreamSynchronize(s_d2h_);
+    for (int p = 0; p < 2; ++p) {
+      if (graph_exec_[p]) (void)hipGraphExecDestroy(graph_exec_[p]);
+      (void)hipEventDestroy(ev_h2d_[p]);
+      (void)hipEventDestroy(ev_done_[p]);
+      (void)hipEventDestroy(ev_d2h_[p]);
     }
+    if (req_exec_) (void)hipGraphExecDestroy(req_exec_);
+    (void)hipStreamDestroy(s_comp_);
+    (void)hipStreamDestroy(s_h2d_);
+    (void)hipStreamDestroy(s_d2h_);
+    for (auto& kv : bufs_) {
+      if (kv.second.host) (void)hipHostFree(kv.second.ptr);
+      else (void)hipFree(kv.second.ptr);
+    }
+  }
+
+  // page-locked (not mapped into kernels) host buffer: DMA target/source
+  void* pinned(const char* name, size_t bytes) {
+    Buf b;
+    b.bytes = bytes;
+    b.host = true;
+    HIPCHECK(hipHostMalloc(&b.ptr, bytes, hipHostMallocPortable));
+    memset(b.ptr, 0, bytes);
+    total_bytes_ += bytes;
+    bufs_[name] = b;
+    return b.ptr;
   }
 
   // ------------------------------------------------------------- buffers
@@ -345,49 +391,85 @@ class Engine {
     return o;
   }
 
-  // ------------------------------------------------------------- step
-  // segs: numpy structured/bytes of SegIn[nseg]; payload: host pointer (pinned preferred)
-  void submit(py::buffer segs, u64 payload_ptr, u64 payload_len, i64 now_ms, u64 step, u64 id_ms,
-              u32 worker, u64 stream) {
+  // ------------------------------------------------------------- step (pipelined)
+  // submit(): stage step t's ingress on the H2D stream and launch parity t&1's graph on
+  // the compute stream behind it.  wait_results(p) -> host-mapped SegOut/Counters/ConnOut
+  // are valid; egress_copy(p) DMAs exactly the rendered bytes on the D2H stream;
+  // egress_wait(p) -> egress_host(p) is valid.
+  int submit(py::buffer segs, u64 payload_ptr, u64 payload_len, i64 now_ms, u64 step, u64 id_ms,
+             u32 worker) {
     py::buffer_info si = segs.request();
     size_t sb = (size_t)si.size * si.itemsize;
     u32 nseg = (u32)(sb / sizeof(SegIn));
     if (nseg > d_.seg_max) throw std::runtime_error("too many segments");
     if (payload_len > d_.ingress_cap) throw std::runtime_error("ingress payload exceeds ingress_cap");
-    hipStream_t s = (hipStream_t)stream;
-    step_in_.nseg = nseg;
-    step_in_.now_ms = now_ms;
-    step_in_.step = step;
-    step_in_.id_ms = id_ms;
-    step_in_.worker = worker;
-    seg_stage_.assign((const u8*)si.ptr, (const u8*)si.ptr + sb);
-    HIPCHECK(hipMemcpyAsync((void*)d_.in, &step_in_, sizeof(StepIn), hipMemcpyHostToDevice, s));
-    if (sb) HIPCHECK(hipMemcpyAsync((void*)d_.segs, seg_stage_.data(), sb, hipMemcpyHostToDevice, s));
+    int p = (int)(seq_ & 1);
+    if (inflight_[p]) throw std::runtime_error("submit: results of the previous step of this parity not collected");
+    HIPCHECK(hipEventSynchronize(ev_h2d_[p]));  // staging buffers of step t-2 are free
+    StepIn* in = stage_in_[p];
+    *in = StepIn{};
+    in->nseg = nseg;
+    in->now_ms = now_ms;
+    in->step = step;
+    in->id_ms = id_ms;
+    in->worker = worker;
+    memcpy(stage_segs_[p], si.ptr, sb);
+    HIPCHECK(hipMemcpyAsync((void*)io_[p].in, in, sizeof(StepIn), hipMemcpyHostToDevice, s_h2d_));
+    if (sb) HIPCHECK(hipMemcpyAsync((void*)io_[p].segs, stage_segs_[p], sb, hipMemcpyHostToDevice, s_h2d_));
     if (payload_len)
-      HIPCHECK(hipMemcpyAsync((void*)d_.ingress, (const void*)payload_ptr, payload_len,
-                              hipMemcpyHostToDevice, s));
-    if (graph_enabled_) {
-      if (!graph_exec_) capture(s, false);
-      HIPCHECK(hipGraphLaunch(graph_exec_, s));
-    } else {
-      launch_main(s);
+      HIPCHECK(hipMemcpyAsync((void*)io_[p].ingress, (const void*)payload_ptr, payload_len,
+                              hipMemcpyHostToDevice, s_h2d_));
+    HIPCHECK(hipEventRecord(ev_h2d_[p], s_h2d_));
+    HIPCHECK(hipStreamWaitEvent(s_comp_, ev_h2d_[p], 0));
+    if (d2h_issued_[p]) HIPCHECK(hipStreamWaitEvent(s_comp_, ev_d2h_[p], 0));  // egress[p] drained
+    if (req_pending_) {
+      if (graph_enabled_) {
+        if (!req_exec_) capture_req();
+        HIPCHECK(hipGraphLaunch(req_exec_, s_comp_));
+      } else {
+        launch_requeue(s_comp_);
+      }
+      req_pending_ = false;
     }
+    if (graph_enabled_) {
+      if (!graph_exec_[p]) capture_main(p);
+      HIPCHECK(hipGraphLaunch(graph_exec_[p], s_comp_));
+    } else {
+      launch_main(s_comp_, io_[p]);
+    }
+    HIPCHECK(hipEventRecord(ev_done_[p], s_comp_));
+    inflight_[p] = true;
+    ++seq_;
+    return p;
   }
 
-  void requeue(u64 stream) {
-    hipStream_t s = (hipStream_t)stream;
-    if (graph_enabled_) {
-      if (!req_exec_) capture(s, true);
-      HIPCHECK(hipGraphLaunch(req_exec_, s));
-    } else {
-      launch_requeue(s);
-    }
+  void wait_results(int p) {
+    HIPCHECK(hipEventSynchronize(ev_done_[p]));
+    inflight_[p] = false;
   }
 
-  void sync(u64 stream) { HIPCHECK(hipStreamSynchronize((hipStream_t)stream)); }
+  u64 egress_copy(int p) {
+    const Counters* c = (const Counters*)buf("ctr_host" + std::to_string(p)).ptr;
+    u64 n = c->egress_bytes;
+    HIPCHECK(hipStreamWaitEvent(s_d2h_, ev_done_[p], 0));
+    if (n) HIPCHECK(hipMemcpyAsync(egress_host_[p], io_[p].egress, n, hipMemcpyDeviceToHost, s_d2h_));
+    HIPCHECK(hipEventRecord(ev_d2h_[p], s_d2h_));
+    d2h_issued_[p] = true;
+    return n;
+  }
 
-  py::dict counters() const {
-    const Counters& c = *(const Counters*)buf("ctr_host").ptr;
+  void egress_wait(int p) { HIPCHECK(hipEventSynchronize(ev_d2h_[p])); }
+
+  void request_requeue() { req_pending_ = true; }
+
+  void sync() {
+    HIPCHECK(hipStreamSynchronize(s_h2d_));
+    HIPCHECK(hipStreamSynchronize(s_comp_));
+    HIPCHECK(hipStreamSynchronize(s_d2h_));
+  }
+
+  py::dict counters(int p) const {
+    const Counters& c = *(const Counters*)buf("ctr_host" + std::to_string(p)).ptr;
     py::dict o;
 #define F(x) o[#x] = c.x
     F(n_cmds); F(n_frags); F(n_pubs); F(n_acks); F(n_ctrl); F(ctrl_bytes); F(n_pairs); F(n_deliv);
@@ -427,8 +509,7 @@ class Engine {
     return src;
   }
 
-  void launch_main(hipStream_t s) {
-    const DS& d = d_;
+  void launch_main(hipStream_t s, const DS& d) {
     u32 nch = d.c_max * d.chpc;
     auto blocks = [](u64 n, u32 per) { return dim3(n ? ceil_div(n, per) : 1); };
     hipLaunchKernelGGL(k_prep, dim3(1), dim3(1024), 0, s, d);
@@ -478,18 +559,26 @@ class Engine {
     hipLaunchKernelGGL(k_final, dim3(1), dim3(64), 0, s, d);
   }
 
-  void launch_requeue(hipStream_t s) {
+  void launch_requeue(hipStream_t s) {  // state-only kernels: IO pointers unused
     hipLaunchKernelGGL(k_requeue, dim3(d_.q_max), dim3(256), 0, s, d_);
     hipLaunchKernelGGL(k_requeue_compact, dim3(1), dim3(1024), 0, s, d_);
   }
 
-  void capture(hipStream_t s, bool req) {
+  void capture_main(int p) {
     hipGraph_t g;
-    HIPCHECK(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
-    if (req) launch_requeue(s);
-    else launch_main(s);
-    HIPCHECK(hipStreamEndCapture(s, &g));
-    HIPCHECK(hipGraphInstantiate(req ? &req_exec_ : &graph_exec_, g, nullptr, nullptr, 0));
+    HIPCHECK(hipStreamBeginCapture(s_comp_, hipStreamCaptureModeThreadLocal));
+    launch_main(s_comp_, io_[p]);
+    HIPCHECK(hipStreamEndCapture(s_comp_, &g));
+    HIPCHECK(hipGraphInstantiate(&graph_exec_[p], g, nullptr, nullptr, 0));
+    HIPCHECK(hipGraphDestroy(g));
+  }
+
+  void capture_req() {
+    hipGraph_t g;
+    HIPCHECK(hipStreamBeginCapture(s_comp_, hipStreamCaptureModeThreadLocal));
+    launch_requeue(s_comp_);
+    HIPCHECK(hipStreamEndCapture(s_comp_, &g));
+    HIPCHECK(hipGraphInstantiate(&req_exec_, g, nullptr, nullptr, 0));
     HIPCHECK(hipGraphDestroy(g));
   }
 
@@ -500,10 +589,18 @@ class Engine {
   u64 egress_alloc_ = 0;
   u32 ntiles_max_ = 0;
   bool graph_enabled_ = true;
-  hipGraphExec_t graph_exec_ = nullptr;
+  hipGraphExec_t graph_exec_[2] = {nullptr, nullptr};
   hipGraphExec_t req_exec_ = nullptr;
-  StepIn step_in_;
-  std::vector<u8> seg_stage_;
+  DS io_[2];
+  u8* egress_host_[2] = {nullptr, nullptr};
+  StepIn* stage_in_[2] = {nullptr, nullptr};
+  SegIn* stage_segs_[2] = {nullptr, nullptr};
+  hipStream_t s_comp_ = nullptr, s_h2d_ = nullptr, s_d2h_ = nullptr;
+  hipEvent_t ev_h2d_[2], ev_done_[2], ev_d2h_[2];
+  bool inflight_[2] = {false, false};
+  bool d2h_issued_[2] = {false, false};
+  bool req_pending_ = false;
+  u64 seq_ = 0;
 };
 
 static py::array alloc_pinned(size_t bytes) {
@@ -543,7 +640,10 @@ PYBIND11_MODULE(_dataplane, m) {
       .def("download", &Engine::download, py::arg("name"), py::arg("offset") = 0, py::arg("n") = 0)
       .def("host_view", &Engine::host_view)
       .def("submit", &Engine::submit)
-      .def("requeue", &Engine::requeue)
+      .def("wait_results", &Engine::wait_results)
+      .def("egress_copy", &Engine::egress_copy)
+      .def("egress_wait", &Engine::egress_wait)
+      .def("request_requeue", &Engine::request_requeue)
       .def("sync", &Engine::sync)
       .def("counters", &Engine::counters);
 }
