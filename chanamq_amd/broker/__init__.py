@@ -1,1 +1,51 @@
-"""chanamq_amd.broker"""
+"""Native broker core (C++): AMQP codec, connection engine, control plane, CPU data path,
+embedded Cassandra-schema store.  Built in-tree by ``build()`` with g++ (+OpenSSL)."""
+
+import importlib
+import os
+import subprocess
+import sys
+import sysconfig
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_ROOT = os.path.dirname(os.path.dirname(_HERE))
+_SRC = os.path.join(_ROOT, "csrc", "core")
+_EXT = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
+EXT_PATH = os.path.join(_HERE, "_core" + _EXT)
+SOURCES = ["codec.cpp", "store.cpp", "broker.cpp", "bindings.cpp"]
+HEADERS = ["codec.hpp", "store.hpp", "broker.hpp"]
+
+
+def _stale():
+    if not os.path.exists(EXT_PATH):
+        return True
+    t = os.path.getmtime(EXT_PATH)
+    return any(os.path.getmtime(os.path.join(_SRC, s)) > t for s in SOURCES + HEADERS)
+
+
+def build(force=False, verbose=False, sanitize=None):
+    """g++ -O2 shared library; ``sanitize='address'|'thread'`` builds an instrumented
+    copy for host-side race/memory checks."""
+    if not force and not sanitize and not _stale():
+        return EXT_PATH
+    import pybind11
+
+    cxx = os.environ.get("CXX", "g++")
+    out = EXT_PATH if not sanitize else EXT_PATH.replace("_core", f"_core_{sanitize}")
+    flags = ["-O2", "-g", "-std=c++17", "-shared", "-fPIC", "-Wall", "-Wno-unused-result"]
+    if sanitize:
+        flags += [f"-fsanitize={sanitize}", "-fno-omit-frame-pointer"]
+    cmd = [cxx, *flags, f"-I{pybind11.get_include()}", f"-I{sysconfig.get_paths()['include']}",
+           *[os.path.join(_SRC, s) for s in SOURCES], "-o", out + ".tmp", "-lssl", "-lcrypto", "-lpthread"]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    subprocess.run(cmd, check=True)
+    os.replace(out + ".tmp", out)
+    return out
+
+
+def load():
+    try:
+        return importlib.import_module("chanamq_amd.broker._core")
+    except ImportError as e:
+        raise ImportError(f"chanamq_amd.broker._core is not built ({e}); run __graft_entry__.build()") from e

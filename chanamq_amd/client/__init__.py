@@ -1,1 +1,2 @@
-"""chanamq_amd.client"""
+"""AMQP 0-9-1 test client + load generators."""
+from .amqp_client import ChannelClosed, Connection, ConnectionClosed, Delivery

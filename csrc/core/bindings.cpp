@@ -1,0 +1,151 @@
+// pybind11 module `_core`: the native broker, store and codec for Python.
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <condition_variable>
+
+#include "broker.hpp"
+#include "codec.hpp"
+#include "store.hpp"
+
+namespace py = pybind11;
+using namespace cmq;
+
+static BrokerConfig config_from(py::dict d) {
+  BrokerConfig c;
+#define S(k, f) if (d.contains(k)) c.f = d[k].cast<decltype(c.f)>()
+  S("host", host); S("port", port); S("amqp_enable", amqp_enable); S("tls_port", tls_port);
+  S("tls_enable", tls_enable); S("tls_cert", tls_cert); S("tls_key", tls_key); S("tls_p12", tls_p12);
+  S("tls_p12_password", tls_p12_password); S("channel_max", channel_max); S("frame_max", frame_max);
+  S("frame_min", frame_min); S("heartbeat", heartbeat); S("default_vhost", default_vhost);
+  S("data_dir", data_dir); S("fsync", fsync); S("worker_id", worker_id);
+  S("mem_high_watermark", mem_high_watermark); S("mem_low_watermark", mem_low_watermark);
+  S("flow_channel", flow_channel); S("max_connections", max_connections); S("hash_wildcard", hash_wildcard);
+#undef S
+  return c;
+}
+
+static py::tuple decode(py::bytes payload) {
+  std::string s = payload;
+  Method m = decode_method((const u8*)s.data(), s.size());
+  py::list args;
+  for (size_t k = 0; k < m.spec->fields.size(); ++k) {
+    switch (m.spec->fields[k].second) {
+      case A_SHORTSTR: args.append(py::bytes(m.args[k].s)); break;
+      case A_LONGSTR: args.append(py::bytes(m.args[k].s)); break;
+      case A_TABLE: {
+        py::dict t;
+        for (auto& kv : m.args[k].t) t[py::str(kv.first)] = py::str(kv.second.tag == 'S' ? kv.second.s : std::to_string(kv.second.i));
+        args.append(t);
+        break;
+      }
+      default: args.append(m.args[k].i);
+    }
+  }
+  return py::make_tuple(m.cls(), m.mid(), std::string(m.spec->name), args);
+}
+
+static py::bytes reencode(py::bytes payload) {
+  std::string s = payload;
+  Method m = decode_method((const u8*)s.data(), s.size());
+  return py::bytes(encode_method_payload(m));
+}
+
+PYBIND11_MODULE(_core, m) {
+  m.doc() = "chanamq native broker core (C++): AMQP codec, control plane, CPU data path, store";
+  py::class_<Broker>(m, "Broker")
+      .def(py::init([](py::dict d) { return new Broker(config_from(d)); }))
+      .def("start", &Broker::start, py::call_guard<py::gil_scoped_release>())
+      .def("stop", &Broker::stop, py::call_guard<py::gil_scoped_release>())
+      .def_property_readonly("port", &Broker::listen_port)
+      .def_property_readonly("tls_port", &Broker::listen_tls_port)
+      .def_property_readonly("running", &Broker::running)
+      .def("create_vhost", &Broker::create_vhost, py::call_guard<py::gil_scoped_release>())
+      .def("delete_vhost", &Broker::delete_vhost, py::call_guard<py::gil_scoped_release>())
+      .def("stats_json", &Broker::stats_json, py::call_guard<py::gil_scoped_release>())
+      .def("queues_json", &Broker::queues_json, py::call_guard<py::gil_scoped_release>());
+
+  py::class_<Store>(m, "Store")
+      .def(py::init<>())
+      .def("open", &Store::open, py::arg("dir"), py::arg("fsync") = true)
+      .def("close", &Store::close)
+      .def("sync", &Store::sync)
+      .def("compact", &Store::compact)
+      .def("row_count", &Store::rowCount)
+      .def("queue_ids", &Store::queueIds)
+      .def("exchange_ids", &Store::exchangeIds)
+      .def("vhost_ids", &Store::vhostIds)
+      .def("insert_vhost", &Store::insertVhost)
+      .def("delete_vhost", &Store::deleteVhost)
+      .def("insert_message", [](Store& s, int64_t id, int64_t tstamp, py::bytes header, py::bytes body,
+                                std::string ex, std::string rk, bool durable, int32_t refer, int64_t ttl_ms) {
+             MsgRow r;
+             r.id = id; r.tstamp = tstamp; r.header = header; r.body = body; r.exchange = ex; r.routing = rk;
+             r.durable = durable; r.refer = refer;
+             s.insertMessage(r, ttl_ms);
+           })
+      .def("select_message", [](Store& s, int64_t id) -> py::object {
+             MsgRow r;
+             if (!s.selectMessage(id, &r)) return py::none();
+             return py::make_tuple(r.id, r.tstamp, py::bytes(r.header), py::bytes(r.body), r.exchange, r.routing,
+                                   r.durable, r.refer);
+           })
+      .def("delete_message", &Store::deleteMessage)
+      .def("update_message_refer_count", &Store::updateMessageReferCount)
+      .def("insert_queue_meta", &Store::insertQueueMeta)
+      .def("insert_queue_msg", &Store::insertQueueMsg)
+      .def("insert_last_consumed", &Store::insertLastConsumed)
+      .def("consumed_queue_messages", [](Store& s, std::string q, int64_t l, std::vector<std::tuple<int64_t, int64_t, int32_t>> u) {
+             std::vector<QueueMsgRow> rows;
+             for (auto& t : u) { QueueMsgRow r; r.offset = std::get<0>(t); r.msgid = std::get<1>(t); r.size = std::get<2>(t); rows.push_back(r); }
+             s.consumedQueueMessages(q, l, rows);
+           })
+      .def("select_queue", [](Store& s, std::string q) -> py::object {
+             QueueMetaRow meta;
+             std::vector<QueueMsgRow> msgs, unacks;
+             if (!s.selectQueue(q, &meta, &msgs, &unacks)) return py::none();
+             py::list ml, ul;
+             for (auto& r : msgs) ml.append(py::make_tuple(r.offset, r.msgid, r.size));
+             for (auto& r : unacks) ul.append(py::make_tuple(r.offset, r.msgid, r.size));
+             return py::make_tuple(py::make_tuple(meta.lconsumed, meta.consumers, meta.durable, meta.ttl), ml, ul);
+           })
+      .def("force_delete_queue", &Store::forceDeleteQueue)
+      .def("pending_delete_queue", &Store::pendingDeleteQueue)
+      .def("delete_consumed_queue_msgs", &Store::deleteConsumedQueueMsgs)
+      .def("insert_queue_unack", &Store::insertQueueUnack)
+      .def("delete_queue_unack", &Store::deleteQueueUnack)
+      .def("insert_exchange", [](Store& s, std::string id, std::string tpe, bool durable, bool autodel, bool internal,
+                                 std::map<std::string, std::string> args) {
+             ExchangeRow x; x.tpe = tpe; x.durable = durable; x.autodel = autodel; x.internal = internal; x.args = args;
+             s.insertExchange(id, x);
+           })
+      .def("insert_bind", &Store::insertBind)
+      .def("select_exchange", [](Store& s, std::string id) -> py::object {
+             ExchangeRow x;
+             std::vector<BindRow> b;
+             if (!s.selectExchange(id, &x, &b)) return py::none();
+             py::list bl;
+             for (auto& r : b) bl.append(py::make_tuple(r.queue, r.key, r.args));
+             return py::make_tuple(py::make_tuple(x.tpe, x.durable, x.autodel, x.internal, x.args), bl);
+           })
+      .def("delete_bind", &Store::deleteBind)
+      .def("delete_binds_of_queue", &Store::deleteBindsOfQueue)
+      .def("delete_exchange", &Store::deleteExchange)
+      .def("select_vhost", [](Store& s, std::string id) -> py::object {
+             bool a;
+             if (!s.selectVhost(id, &a)) return py::none();
+             return py::bool_(a);
+           });
+
+  m.def("decode_method", &decode);
+  m.def("reencode_method", &reencode);
+  m.def("method_table", [] {
+    py::list out;
+    for (auto& s : method_table()) {
+      py::list f;
+      for (auto& x : s.fields) f.append(py::make_tuple(std::string(x.first), (int)x.second));
+      out.append(py::make_tuple(s.cls, s.mid, std::string(s.name), f, s.content));
+    }
+    return out;
+  });
+}

@@ -1,0 +1,452 @@
+// Embedded Cassandra-schema store with a CRC-checked write-ahead log (see store.hpp).
+#include "store.hpp"
+
+#include <fcntl.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <chrono>
+#include <cstring>
+#include <stdexcept>
+
+#include "codec.hpp"
+
+namespace cmq {
+
+namespace {
+enum Op : uint8_t {
+  OP_MSG_INS = 1, OP_MSG_REFER, OP_MSG_DEL, OP_QMETA_INS, OP_QMSG_INS, OP_QLAST, OP_QCONSUMED, OP_QFORCE_DEL,
+  OP_QPENDING_DEL, OP_QDEL_CONSUMED, OP_QUNACK_INS, OP_QUNACK_DEL, OP_X_INS, OP_BIND_INS, OP_BIND_DEL,
+  OP_BIND_DEL_Q, OP_X_DEL, OP_VH_INS, OP_VH_DEL, OP_QMSG_DEL
+};
+
+uint32_t crc32(const std::string& s) {
+  static uint32_t T[256];
+  static bool init = false;
+  if (!init) {
+    for (uint32_t i = 0; i < 256; ++i) {
+      uint32_t c = i;
+      for (int k = 0; k < 8; ++k) c = c & 1 ? 0xEDB88320u ^ (c >> 1) : c >> 1;
+      T[i] = c;
+    }
+    init = true;
+  }
+  uint32_t c = 0xFFFFFFFFu;
+  for (unsigned char b : s) c = T[(c ^ b) & 255] ^ (c >> 8);
+  return c ^ 0xFFFFFFFFu;
+}
+
+void w_map(Writer& w, const std::map<std::string, std::string>& m) {
+  w.lng((u32)m.size());
+  for (auto& kv : m) { w.longstr(kv.first); w.longstr(kv.second); }
+}
+std::map<std::string, std::string> r_map(Reader& r) {
+  std::map<std::string, std::string> m;
+  u32 n = r.lng();
+  for (u32 i = 0; i < n; ++i) { std::string k = r.longstr(); m[k] = r.longstr(); }
+  return m;
+}
+}  // namespace
+
+Store::~Store() { close(); }
+
+int64_t Store::now_ms() const {
+  return std::chrono::duration_cast<std::chrono::milliseconds>(
+             std::chrono::system_clock::now().time_since_epoch()).count();
+}
+
+void Store::open(const std::string& dir, bool fsync_enabled) {
+  std::lock_guard<std::recursive_mutex> g(mu_);
+  fsync_ = fsync_enabled;
+  if (dir.empty()) return;
+  ::mkdir(dir.c_str(), 0755);
+  path_ = dir + "/chanamq.wal";
+  fd_ = ::open(path_.c_str(), O_RDWR | O_CREAT | O_APPEND, 0644);
+  if (fd_ < 0) throw std::runtime_error("store: cannot open " + path_);
+  replay();
+}
+
+void Store::close() {
+  std::lock_guard<std::recursive_mutex> g(mu_);
+  if (fd_ >= 0) {
+    sync();
+    ::close(fd_);
+    fd_ = -1;
+  }
+}
+
+void Store::write_all(const std::string& rec) {
+  const char* p = rec.data();
+  size_t n = rec.size();
+  while (n) {
+    ssize_t k = ::write(fd_, p, n);
+    if (k < 0) throw std::runtime_error("store: WAL write failed");
+    p += k;
+    n -= (size_t)k;
+  }
+  wal_bytes_ += rec.size();
+}
+
+void Store::append(uint8_t op, const std::string& payload) {
+  apply(op, payload);
+  if (fd_ < 0 || replaying_) return;
+  std::string rec;
+  u32 len = (u32)payload.size() + 1;
+  for (int s = 24; s >= 0; s -= 8) rec.push_back((char)(len >> s));
+  rec.push_back((char)op);
+  rec += payload;
+  u32 c = crc32(rec.substr(4));
+  for (int s = 24; s >= 0; s -= 8) rec.push_back((char)(c >> s));
+  write_all(rec);
+  dirty_ = true;
+}
+
+void Store::sync() {
+  std::lock_guard<std::recursive_mutex> g(mu_);
+  if (fd_ >= 0 && dirty_) {
+    if (fsync_) ::fdatasync(fd_);
+    dirty_ = false;
+  }
+}
+
+void Store::replay() {
+  replaying_ = true;
+  std::string data;
+  ::lseek(fd_, 0, SEEK_SET);
+  char buf[1 << 16];
+  ssize_t k;
+  while ((k = ::read(fd_, buf, sizeof buf)) > 0) data.append(buf, (size_t)k);
+  size_t pos = 0, good = 0;
+  while (pos + 9 <= data.size()) {
+    const u8* p = (const u8*)data.data() + pos;
+    u32 len = (u32(p[0]) << 24) | (u32(p[1]) << 16) | (u32(p[2]) << 8) | p[3];
+    if (len == 0 || pos + 4 + len + 4 > data.size()) break;
+    std::string body = data.substr(pos + 4, len);
+    const u8* q = p + 4 + len;
+    u32 crc = (u32(q[0]) << 24) | (u32(q[1]) << 16) | (u32(q[2]) << 8) | q[3];
+    if (crc != crc32(body)) break;  // torn tail: stop at the last good record
+    apply((uint8_t)body[0], body.substr(1));
+    pos += 8 + len;
+    good = pos;
+  }
+  if (good < data.size()) (void)::ftruncate(fd_, (off_t)good);
+  wal_bytes_ = good;
+  ::lseek(fd_, 0, SEEK_END);
+  replaying_ = false;
+}
+
+void Store::compact() {
+  std::lock_guard<std::recursive_mutex> g(mu_);
+  if (fd_ < 0) return;
+  std::string tmp = path_ + ".tmp";
+  int nfd = ::open(tmp.c_str(), O_RDWR | O_CREAT | O_TRUNC, 0644);
+  if (nfd < 0) throw std::runtime_error("store: compact open failed");
+  int old = fd_;
+  fd_ = nfd;
+  wal_bytes_ = 0;
+  // re-emit live rows (replaying_ stays false so records are written, apply is idempotent)
+  auto vh = vhosts_;
+  auto xs = exchanges_;
+  auto bs = binds_;
+  auto qm = queue_metas_;
+  auto qs = queues_;
+  auto qu = queue_unacks_;
+  auto ms = msgs_;
+  for (auto& kv : vh) insertVhost(kv.first, kv.second);
+  for (auto& kv : xs) insertExchange(kv.first, kv.second);
+  for (auto& kv : bs)
+    for (auto& b : kv.second) insertBind(kv.first, b.second.queue, b.second.key, b.second.args);
+  for (auto& kv : qm) insertQueueMeta(kv.first, kv.second.lconsumed, kv.second.consumers, kv.second.durable, kv.second.ttl);
+  int64_t now = now_ms();
+  for (auto& kv : qs)
+    for (auto& r : kv.second)
+      insertQueueMsg(kv.first, r.second.offset, r.second.msgid, r.second.size,
+                     r.second.expire_at ? std::max<int64_t>(1, r.second.expire_at - now) : 0);
+  for (auto& kv : qu)
+    for (auto& r : kv.second) insertQueueUnack(kv.first, r.second.offset, r.second.msgid, r.second.size);
+  for (auto& kv : ms)
+    insertMessage(kv.second, kv.second.expire_at ? std::max<int64_t>(1, kv.second.expire_at - now) : 0);
+  if (fsync_) ::fdatasync(fd_);
+  ::rename(tmp.c_str(), path_.c_str());
+  ::close(old);
+  dirty_ = false;
+}
+
+// ------------------------------------------------------------------ apply (row semantics)
+void Store::apply(uint8_t op, const std::string& pl) {
+  Reader r((const u8*)pl.data(), pl.size());
+  int64_t now = now_ms();
+  switch (op) {
+    case OP_MSG_INS: {
+      MsgRow m;
+      m.id = (int64_t)r.llng(); m.tstamp = (int64_t)r.llng(); m.header = r.longstr(); m.body = r.longstr();
+      m.exchange = r.longstr(); m.routing = r.longstr(); m.durable = r.octet(); m.refer = (int32_t)r.lng();
+      int64_t ttl = (int64_t)r.llng();
+      int64_t at = (int64_t)r.llng();
+      m.expire_at = ttl > 0 ? at + ttl : 0;
+      msgs_[m.id] = m;
+      break;
+    }
+    case OP_MSG_REFER: { int64_t id = (int64_t)r.llng(); int32_t ref = (int32_t)r.lng();
+      auto it = msgs_.find(id); if (it != msgs_.end()) it->second.refer = ref; break; }
+    case OP_MSG_DEL: msgs_.erase((int64_t)r.llng()); break;
+    case OP_QMETA_INS: {
+      std::string q = r.longstr();
+      QueueMetaRow m;
+      m.lconsumed = (int64_t)r.llng();
+      u32 n = r.lng();
+      for (u32 i = 0; i < n; ++i) m.consumers.insert(r.longstr());
+      m.durable = r.octet(); m.ttl = (int64_t)r.llng();
+      queue_metas_[q] = m;
+      break;
+    }
+    case OP_QMSG_INS: {
+      std::string q = r.longstr();
+      QueueMsgRow m;
+      m.offset = (int64_t)r.llng(); m.msgid = (int64_t)r.llng(); m.size = (int32_t)r.lng();
+      int64_t ttl = (int64_t)r.llng(), at = (int64_t)r.llng();
+      m.expire_at = ttl > 0 ? at + ttl : 0;
+      queues_[q][m.offset] = m;
+      break;
+    }
+    case OP_QMSG_DEL: { std::string q = r.longstr(); queues_[q].erase((int64_t)r.llng()); break; }
+    case OP_QLAST: { std::string q = r.longstr(); queue_metas_[q].lconsumed = (int64_t)r.llng(); break; }
+    case OP_QCONSUMED: {
+      // lconsumed := L; rows with offset <= L removed; unacks inserted (correct columns: A.Q21)
+      std::string q = r.longstr();
+      int64_t L = (int64_t)r.llng();
+      queue_metas_[q].lconsumed = L;
+      auto& rows = queues_[q];
+      rows.erase(rows.begin(), rows.upper_bound(L));
+      u32 n = r.lng();
+      for (u32 i = 0; i < n; ++i) {
+        QueueMsgRow u;
+        u.offset = (int64_t)r.llng(); u.msgid = (int64_t)r.llng(); u.size = (int32_t)r.lng();
+        queue_unacks_[q][u.msgid] = u;
+      }
+      break;
+    }
+    case OP_QFORCE_DEL: {
+      std::string q = r.longstr();
+      queues_.erase(q); queue_metas_.erase(q); queue_unacks_.erase(q);
+      break;
+    }
+    case OP_QPENDING_DEL: {  // copy to *_deleted tables, then delete (CassandraOpService.scala:561-604)
+      std::string q = r.longstr();
+      auto mi = queue_metas_.find(q);
+      if (mi != queue_metas_.end()) {
+        QueueMetaDeletedRow d;
+        d.lconsumed = mi->second.lconsumed; d.nconsumer = (int32_t)mi->second.consumers.size();
+        d.durable = mi->second.durable;
+        queue_metas_deleted_[q] = d;
+      }
+      for (auto& kv : queues_[q]) queues_deleted_[q][kv.first] = kv.second;
+      for (auto& kv : queue_unacks_[q]) queue_unacks_deleted_[q][kv.first] = kv.second;
+      queues_.erase(q); queue_metas_.erase(q); queue_unacks_.erase(q);
+      break;
+    }
+    case OP_QDEL_CONSUMED: {
+      std::string q = r.longstr();
+      int64_t L = (int64_t)r.llng();
+      auto& rows = queues_[q];
+      rows.erase(rows.begin(), rows.upper_bound(L));
+      break;
+    }
+    case OP_QUNACK_INS: {
+      std::string q = r.longstr();
+      QueueMsgRow u;
+      u.offset = (int64_t)r.llng(); u.msgid = (int64_t)r.llng(); u.size = (int32_t)r.lng();
+      queue_unacks_[q][u.msgid] = u;
+      break;
+    }
+    case OP_QUNACK_DEL: { std::string q = r.longstr(); queue_unacks_[q].erase((int64_t)r.llng()); break; }
+    case OP_X_INS: {
+      std::string id = r.longstr();
+      ExchangeRow x;
+      x.tpe = r.longstr(); x.durable = r.octet(); x.autodel = r.octet(); x.internal = r.octet();
+      x.args = r_map(r);
+      exchanges_[id] = x;
+      break;
+    }
+    case OP_BIND_INS: {
+      std::string id = r.longstr();
+      BindRow b;
+      b.queue = r.longstr(); b.key = r.longstr(); b.args = r_map(r);
+      binds_[id][{b.queue, b.key}] = b;
+      break;
+    }
+    case OP_BIND_DEL: {
+      std::string id = r.longstr(), q = r.longstr(), k = r.longstr();
+      binds_[id].erase({q, k});
+      break;
+    }
+    case OP_BIND_DEL_Q: {
+      std::string q = r.longstr();
+      for (auto& kv : binds_)
+        for (auto it = kv.second.begin(); it != kv.second.end();)
+          it = it->first.first == q ? kv.second.erase(it) : std::next(it);
+      break;
+    }
+    case OP_X_DEL: { std::string id = r.longstr(); exchanges_.erase(id); binds_.erase(id); break; }
+    case OP_VH_INS: { std::string id = r.longstr(); vhosts_[id] = r.octet(); break; }
+    case OP_VH_DEL: vhosts_.erase(r.longstr()); break;
+    default: break;
+  }
+  (void)now;
+}
+
+// ------------------------------------------------------------------ operations
+#define LOCK std::lock_guard<std::recursive_mutex> g(mu_)
+
+void Store::insertMessage(const MsgRow& m, int64_t ttl_ms) {
+  LOCK;
+  Writer w;
+  w.llng((u64)m.id); w.llng((u64)m.tstamp); w.longstr(m.header); w.longstr(m.body); w.longstr(m.exchange);
+  w.longstr(m.routing); w.octet(m.durable); w.lng((u32)m.refer);
+  // Cassandra TTL is whole seconds (CassandraOpService.scala:157-159); keep ms precision internally
+  w.llng((u64)ttl_ms); w.llng((u64)now_ms());
+  append(OP_MSG_INS, w.done());
+}
+void Store::updateMessageReferCount(int64_t id, int32_t refer) {
+  LOCK; Writer w; w.llng((u64)id); w.lng((u32)refer); append(OP_MSG_REFER, w.done());
+}
+bool Store::selectMessage(int64_t id, MsgRow* out) {
+  LOCK;
+  auto it = msgs_.find(id);
+  if (it == msgs_.end()) return false;
+  if (it->second.expire_at && it->second.expire_at <= now_ms()) return false;
+  *out = it->second;
+  return true;
+}
+void Store::deleteMessage(int64_t id) { LOCK; Writer w; w.llng((u64)id); append(OP_MSG_DEL, w.done()); }
+
+void Store::insertQueueMeta(const std::string& q, int64_t lconsumed, const std::set<std::string>& consumers,
+                            bool durable, int64_t ttl) {
+  LOCK;
+  Writer w;
+  w.longstr(q); w.llng((u64)lconsumed); w.lng((u32)consumers.size());
+  for (auto& c : consumers) w.longstr(c);
+  w.octet(durable); w.llng((u64)ttl);
+  append(OP_QMETA_INS, w.done());
+}
+void Store::insertQueueMsg(const std::string& q, int64_t offset, int64_t msgid, int32_t size, int64_t ttl_ms) {
+  LOCK;
+  Writer w;
+  w.longstr(q); w.llng((u64)offset); w.llng((u64)msgid); w.lng((u32)size); w.llng((u64)ttl_ms);
+  w.llng((u64)now_ms());
+  append(OP_QMSG_INS, w.done());
+}
+void Store::deleteQueueMsg(const std::string& q, int64_t offset) {
+  LOCK; Writer w; w.longstr(q); w.llng((u64)offset); append(OP_QMSG_DEL, w.done());
+}
+void Store::insertLastConsumed(const std::string& q, int64_t l) {
+  LOCK; Writer w; w.longstr(q); w.llng((u64)l); append(OP_QLAST, w.done());
+}
+void Store::consumedQueueMessages(const std::string& q, int64_t l, const std::vector<QueueMsgRow>& unacks) {
+  LOCK;
+  Writer w;
+  w.longstr(q); w.llng((u64)l); w.lng((u32)unacks.size());
+  for (auto& u : unacks) { w.llng((u64)u.offset); w.llng((u64)u.msgid); w.lng((u32)u.size); }
+  append(OP_QCONSUMED, w.done());
+}
+bool Store::selectQueue(const std::string& q, QueueMetaRow* meta, std::vector<QueueMsgRow>* msgs,
+                        std::vector<QueueMsgRow>* unacks) {
+  LOCK;
+  auto mi = queue_metas_.find(q);
+  if (mi == queue_metas_.end()) return false;
+  if (meta) *meta = mi->second;
+  int64_t now = now_ms();
+  if (msgs) {
+    msgs->clear();
+    auto qi = queues_.find(q);
+    if (qi != queues_.end())
+      for (auto it = qi->second.upper_bound(mi->second.lconsumed); it != qi->second.end(); ++it)
+        if (!it->second.expire_at || it->second.expire_at > now) msgs->push_back(it->second);
+  }
+  if (unacks) {
+    unacks->clear();
+    auto ui = queue_unacks_.find(q);
+    if (ui != queue_unacks_.end())
+      for (auto& kv : ui->second) unacks->push_back(kv.second);
+  }
+  return true;
+}
+void Store::forceDeleteQueue(const std::string& q) { LOCK; Writer w; w.longstr(q); append(OP_QFORCE_DEL, w.done()); }
+void Store::pendingDeleteQueue(const std::string& q) { LOCK; Writer w; w.longstr(q); append(OP_QPENDING_DEL, w.done()); }
+void Store::deleteConsumedQueueMsgs(const std::string& q, int64_t upto) {
+  LOCK; Writer w; w.longstr(q); w.llng((u64)upto); append(OP_QDEL_CONSUMED, w.done());
+}
+void Store::insertQueueUnack(const std::string& q, int64_t offset, int64_t msgid, int32_t size) {
+  LOCK; Writer w; w.longstr(q); w.llng((u64)offset); w.llng((u64)msgid); w.lng((u32)size);
+  append(OP_QUNACK_INS, w.done());
+}
+void Store::deleteQueueUnack(const std::string& q, int64_t msgid) {
+  LOCK; Writer w; w.longstr(q); w.llng((u64)msgid); append(OP_QUNACK_DEL, w.done());
+}
+void Store::insertExchange(const std::string& id, const ExchangeRow& x) {
+  LOCK; Writer w; w.longstr(id); w.longstr(x.tpe); w.octet(x.durable); w.octet(x.autodel); w.octet(x.internal);
+  w_map(w, x.args); append(OP_X_INS, w.done());
+}
+void Store::insertBind(const std::string& id, const std::string& queue, const std::string& key,
+                       const std::map<std::string, std::string>& args) {
+  LOCK; Writer w; w.longstr(id); w.longstr(queue); w.longstr(key); w_map(w, args); append(OP_BIND_INS, w.done());
+}
+bool Store::selectExchange(const std::string& id, ExchangeRow* x, std::vector<BindRow>* binds) {
+  LOCK;
+  auto it = exchanges_.find(id);
+  if (it == exchanges_.end()) return false;
+  if (x) *x = it->second;
+  if (binds) {
+    binds->clear();
+    auto bi = binds_.find(id);
+    if (bi != binds_.end())
+      for (auto& kv : bi->second) binds->push_back(kv.second);
+  }
+  return true;
+}
+void Store::deleteBind(const std::string& id, const std::string& queue, const std::string& key) {
+  LOCK; Writer w; w.longstr(id); w.longstr(queue); w.longstr(key); append(OP_BIND_DEL, w.done());
+}
+void Store::deleteBindsOfQueue(const std::string& queue) {
+  LOCK; Writer w; w.longstr(queue); append(OP_BIND_DEL_Q, w.done());
+}
+void Store::deleteExchange(const std::string& id) { LOCK; Writer w; w.longstr(id); append(OP_X_DEL, w.done()); }
+void Store::insertVhost(const std::string& id, bool active) {
+  LOCK; Writer w; w.longstr(id); w.octet(active); append(OP_VH_INS, w.done());
+}
+bool Store::selectVhost(const std::string& id, bool* active) {
+  LOCK;
+  auto it = vhosts_.find(id);
+  if (it == vhosts_.end()) return false;
+  if (active) *active = it->second;
+  return true;
+}
+void Store::deleteVhost(const std::string& id) { LOCK; Writer w; w.longstr(id); append(OP_VH_DEL, w.done()); }
+
+std::vector<std::string> Store::vhostIds() {
+  LOCK; std::vector<std::string> v; for (auto& kv : vhosts_) v.push_back(kv.first); return v;
+}
+std::vector<std::string> Store::exchangeIds() {
+  LOCK; std::vector<std::string> v; for (auto& kv : exchanges_) v.push_back(kv.first); return v;
+}
+std::vector<std::string> Store::queueIds() {
+  LOCK; std::vector<std::string> v; for (auto& kv : queue_metas_) v.push_back(kv.first); return v;
+}
+size_t Store::rowCount(const std::string& t) {
+  LOCK;
+  auto count2 = [](const std::map<std::string, std::map<int64_t, QueueMsgRow>>& m) {
+    size_t n = 0; for (auto& kv : m) n += kv.second.size(); return n; };
+  if (t == "msgs") return msgs_.size();
+  if (t == "queues") return count2(queues_);
+  if (t == "queues_deleted") return count2(queues_deleted_);
+  if (t == "queue_unacks") return count2(queue_unacks_);
+  if (t == "queue_unacks_deleted") return count2(queue_unacks_deleted_);
+  if (t == "queue_metas") return queue_metas_.size();
+  if (t == "queue_metas_deleted") return queue_metas_deleted_.size();
+  if (t == "exchanges") return exchanges_.size();
+  if (t == "binds") { size_t n = 0; for (auto& kv : binds_) n += kv.second.size(); return n; }
+  if (t == "vhosts") return vhosts_.size();
+  throw std::runtime_error("unknown table " + t);
+}
+
+}  // namespace cmq
