@@ -1,0 +1,55 @@
+"""``python -m chanamq_amd.server`` — the broker launcher (AMQPServer.scala:39-133).
+
+  --config FILE        HOCON file layered over conf/reference.conf (like -Dconfig.file)
+  --set key=value      override one key (repeatable)
+  --stats-interval S   log the "published msgs" / "delivered msgs" counters every S seconds
+                       (the lines chana-mq-test/perf/sum-published.sh scrapes)
+"""
+
+import argparse
+import json
+import logging
+import signal
+import sys
+import threading
+
+from ..broker import load
+from ..utils.config import Config
+from .admin import AdminServer
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser(prog="chanamq_amd.server")
+    ap.add_argument("--config", action="append", default=[])
+    ap.add_argument("--set", action="append", default=[], metavar="KEY=VALUE")
+    ap.add_argument("--stats-interval", type=float, default=10.0)
+    ap.add_argument("--log-level", default="INFO")
+    args = ap.parse_args(argv)
+    logging.basicConfig(level=args.log_level, format="%(asctime)s:%(levelname)s %(threadName)s - %(message)s")
+    log = logging.getLogger("chanamq")
+    overrides = dict(kv.split("=", 1) for kv in args.set)
+    cfg = Config.load(args.config, overrides)
+    bc = cfg.broker_config()
+    core = load()
+    broker = core.Broker(bc)
+    broker.start()
+    log.info("AMQP listening on %s:%s%s", bc["host"], broker.port,
+             f", AMQPS on {broker.tls_port}" if bc["tls_enable"] else "")
+    admin = AdminServer(broker, int(cfg.get("chana.mq.amqp.admin.port"))).start()
+    log.info("admin REST on 127.0.0.1:%d", admin.port)
+    stop = threading.Event()
+    for sig in (signal.SIGINT, signal.SIGTERM):
+        signal.signal(sig, lambda *a: stop.set())
+    last = {}
+    while not stop.wait(args.stats_interval):
+        s = json.loads(broker.stats_json())
+        log.info("server published msgs: %d", s["published"] - last.get("published", 0))
+        log.info("server delivered msgs: %d", s["delivered"] - last.get("delivered", 0))
+        last = s
+    admin.stop()
+    broker.stop()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

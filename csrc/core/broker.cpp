@@ -910,7 +910,10 @@ void Broker::persist_queue_meta(Queue* q) {
   std::set<std::string> cons;
   for (Consumer* c : q->consumers)   // AMQConsumer.globalId = "$connId-$chanId-$tag"
     cons.insert(std::to_string(c->conn->id) + "-" + std::to_string(c->ch) + "-" + c->tag);
-  store_.insertQueueMeta(q->id, q->next_offset - 1 - (i64)q->ready.size(), cons, true, q->ttl);
+  // rows with offset > lconsumed are live; requeued messages sit at the front with their
+  // original (smallest) offsets, so lconsumed = front offset - 1
+  i64 lconsumed = q->ready.empty() ? q->next_offset - 1 : q->ready.front().offset - 1;
+  store_.insertQueueMeta(q->id, lconsumed, cons, true, q->ttl);
 }
 
 void Broker::on_exchange(Conn* c, Channel& ch, Method& m) {
@@ -1599,6 +1602,7 @@ void Broker::requeue_unacked(Conn* c, Channel& ch, std::vector<u64> tags) {
     auto& v = kv.second;
     std::sort(v.begin(), v.end(), [](const QEntry& a, const QEntry& b) { return a.offset < b.offset; });
     for (auto it = v.rbegin(); it != v.rend(); ++it) kv.first->ready.push_front(std::move(*it));
+    persist_queue_meta(kv.first);
     mark_dirty(kv.first);
   }
 }
