@@ -6,6 +6,7 @@
 
 #include "broker.hpp"
 #include "codec.hpp"
+#include "loadgen.hpp"
 #include "store.hpp"
 
 namespace py = pybind11;
@@ -137,6 +138,25 @@ PYBIND11_MODULE(_core, m) {
              return py::bool_(a);
            });
 
+  m.def("run_load", [](py::dict d) {
+    LoadSpec s;
+#define S(k, f) if (d.contains(k)) s.f = d[k].cast<decltype(s.f)>()
+    S("host", host); S("port", port); S("vhost", vhost); S("producers", producers); S("consumers", consumers);
+    S("msg_size", msg_size); S("seconds", seconds); S("exchange", exchange); S("exchange_type", exchange_type);
+    S("routing_key", routing_key); S("queue", queue); S("queues", queues); S("auto_ack", auto_ack);
+    S("prefetch", prefetch); S("persistent", persistent); S("durable", durable); S("confirm", confirm);
+    S("rate", rate);
+#undef S
+    LoadResult r;
+    {
+      py::gil_scoped_release nogil;
+      r = run_load(s);
+    }
+    py::dict o;
+    o["sent"] = r.sent; o["received"] = r.received; o["elapsed"] = r.elapsed; o["p50_us"] = r.p50_us;
+    o["p95_us"] = r.p95_us; o["p99_us"] = r.p99_us; o["error"] = r.error;
+    return o;
+  });
   m.def("decode_method", &decode);
   m.def("reencode_method", &reencode);
   m.def("method_table", [] {

@@ -1,0 +1,30 @@
+// PerfTest-shaped native load generator (see loadgen.cpp).
+#pragma once
+#include <string>
+
+namespace cmq {
+
+struct LoadSpec {
+  std::string host = "127.0.0.1";
+  int port = 5672;
+  std::string vhost = "/";
+  int producers = 1, consumers = 1;
+  int msg_size = 256;
+  double seconds = 5;
+  std::string exchange = "lg.direct", exchange_type = "direct", routing_key = "lg", queue = "lg.q";
+  int queues = 1;
+  bool auto_ack = true;
+  int prefetch = 5000;
+  bool persistent = false, durable = false, confirm = false;
+  double rate = 0;   // msgs/s per producer, 0 = unthrottled
+};
+
+struct LoadResult {
+  unsigned long long sent = 0, received = 0;
+  double elapsed = 0, p50_us = 0, p95_us = 0, p99_us = 0;
+  std::string error;
+};
+
+LoadResult run_load(const LoadSpec& s);
+
+}  // namespace cmq
