@@ -2,8 +2,13 @@
 """Headline benchmark: msgs/sec (whole node) + p50 publish->deliver latency, 1 KB payload.
 
 Workload = BASELINE.json config 2 per GPU ("1 topic exchange, 16 bound queues, 1 KB msgs,
-auto-ack"), weak-scaled: every rank is one MI355X broker shard with its own producers,
-its own 16 queues and their consumers.  Producers are synthetic AMQP connections whose
+auto-ack"), weak-scaled: each rank (one MI355X) owns 16 queues and their consumers and
+serves 256 producer connections.  With N>1 the ranks form ONE sharded broker: exchanges
+and bindings are replicated, every producer publishes uniformly over all 16*N queues of
+the node, so (N-1)/N of the messages are routed on the ingress GPU and shipped to the
+owning GPU by the per-step RCCL all-to-all (parallel/exchange.py) before they are
+enqueued and delivered there (``--mode independent`` = N unconnected shards).
+Producers are synthetic AMQP connections whose
 wire bytes (Basic.Publish method + content header + 1 KB body frame) are pre-rendered
 into a pinned ingress pool and handed to the data plane in TCP-read-sized chunks that
 split frames at arbitrary offsets.  One timed step = the full broker hot path on the
@@ -28,16 +33,22 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 METRIC = "msgs/sec (whole node) + p50 publish→deliver latency, 1 KB payload, 1/2/4/8 GPUs"
 
 
-def build_workload(dp, rank, producers, queues, body, chunk, blocks, cons_base):
+def build_workload(dp, rank, producers, queues, body, chunk, blocks, cons_base, shards=1):
+    """``shards`` > 1: the replicated topology of a sharded broker (every rank declares
+    every queue; queue bench.q.{r}.{i} is placed on rank r and consumed there)."""
     from chanamq_amd.engine.layout import SEG_IN
     from chanamq_amd.engine.traffic import even_split, publish_stream
 
     vh = "AMQ.DEFAULT"
     dp.declare_exchange(vh, "bench.topic", "topic")
-    for i in range(queues):
-        qn = f"bench.q.{rank}.{i}"
-        dp.declare_queue(vh, qn, capacity=1 << 20)
-        dp.bind(vh, qn, "bench.topic", f"bench.{i}.*")
+    owners = range(shards) if shards > 1 else [rank]
+    for r in owners:
+        for i in range(queues):
+            qn = f"bench.q.{r}.{i}"
+            if shards > 1:
+                dp.shard_map.place(vh, qn, r)
+            dp.declare_queue(vh, qn, capacity=1 << 20)
+            dp.bind(vh, qn, "bench.topic", f"bench.{r}.{i}.*")
     for p in range(producers):
         dp.open_connection(p, vh)
         dp.open_channel(p, 1)
@@ -47,12 +58,14 @@ def build_workload(dp, rank, producers, queues, body, chunk, blocks, cons_base):
         dp.open_channel(c, 1)
         dp.consume(c, 1, vh, f"bench.q.{rank}.{i}", f"ctag-{i}", no_ack=True)
     # one message on the wire is ~1.08 KB; each producer gets `blocks` chunks of ~chunk bytes
-    probe = publish_stream(1, "bench.topic", lambda i: "bench.0.x0", body)
+    probe = publish_stream(1, "bench.topic", lambda i: f"bench.{rank}.0.x0", body)
     per_prod = max(1, (chunk * blocks) // len(probe))
     streams = []
+    nq = queues * len(owners)
     for p in range(producers):
-        rng_q = np.random.default_rng(1000 + rank * 7919 + p).integers(0, queues, size=per_prod)
-        s = publish_stream(per_prod, "bench.topic", lambda i, r=rng_q: f"bench.{r[i]}.x{i % 10}", body,
+        rng_q = np.random.default_rng(1000 + rank * 7919 + p).integers(0, nq, size=per_prod)
+        s = publish_stream(per_prod, "bench.topic",
+                           lambda i, r=rng_q: f"bench.{owners[r[i] // queues]}.{r[i] % queues}.x{i % 10}", body,
                            seed=p)
         streams.append(even_split(s, blocks))
     # block-major pinned pool: block b = chunk b of every producer, 16-B aligned
@@ -88,6 +101,8 @@ def main():
     ap.add_argument("--chunk", type=int, default=65536, help="bytes per producer per step (TCP read)")
     ap.add_argument("--blocks", type=int, default=8)
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--mode", choices=["sharded", "independent"], default="sharded",
+                    help="N>1: one sharded broker (cross-GPU routing over RCCL) or N unconnected shards")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -103,14 +118,20 @@ def main():
     from chanamq_amd.engine.dataplane import GpuDataPlane
 
     P, Q = args.producers, args.queues
-    cfg = dict(c_max=max(1024, P + Q + 1), chpc=4, q_max=max(64, Q * 2), cons_max=1024, seg_max=max(1024, P + Q),
-               cmd_max=1 << 17, deliv_max=1 << 16, msg_max=1 << 22, ucap=4096, deliver_cap=8192,
-               ingress_cap=max(64 << 20, 2 * P * args.chunk), egress_cap=128 << 20,
-               log_bytes=16 << 30, ring_pool=Q * 2 * (1 << 20), tb_max=64, carry_cap=256 << 10,
+    shards = world if (world > 1 and args.mode == "sharded") else 1
+    qtot = Q * shards
+    cfg = dict(c_max=max(1024, P + Q + 1), chpc=4, q_max=max(64, qtot * 2), cons_max=1024,
+               seg_max=max(1024, P + Q), cmd_max=1 << 17, deliv_max=1 << 16, msg_max=1 << 22, ucap=4096,
+               deliver_cap=8192, ingress_cap=max(32 << 20, P * args.chunk + (4 << 20)), egress_cap=128 << 20,
+               log_bytes=16 << 30, ring_pool=Q * (1 << 20) + qtot + 1024, tb_max=max(64, qtot), carry_cap=256 << 10,
                graph=0 if args.no_graph else 1)
-    dp = GpuDataPlane(device=local, worker=rank, **cfg)
+    if shards > 1:
+        from chanamq_amd.parallel.exchange import Exchanger
+        dp = GpuDataPlane(device=local, worker=rank, world=world, rank=rank, exchanger=Exchanger(), **cfg)
+    else:
+        dp = GpuDataPlane(device=local, worker=rank, **cfg)
     pool, segs, offs, blens, mps, msg_bytes = build_workload(dp, rank, P, Q, args.body, args.chunk,
-                                                             args.blocks, cons_base=P)
+                                                             args.blocks, cons_base=P, shards=shards)
     base = pool.ctypes.data
     step_i = 0
 
@@ -153,6 +174,8 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     dp.eng.sync()
+    if shards > 1:
+        dp.exchanger.bytes_sent = 0
     t0 = time.perf_counter()
     dl, pb, hist, eg = run(args.steps)
     dp.eng.sync()
@@ -200,7 +223,9 @@ def main():
                          "auto-ack, non-persistent",
                 "global_batch": int(round(mps * world)),
                 "seq_len": args.body,
-                "parallelism": f"queue-sharded x{world} (one broker shard per GPU)",
+                "parallelism": (f"queue-sharded x{world}: one broker, cross-GPU routing by RCCL all-to-all"
+                                if shards > 1 else
+                                (f"x{world} independent broker shards" if world > 1 else "single GPU")),
                 "producers_per_gpu": P,
                 "consumers_per_gpu": Q,
                 "bytes_per_msg_on_wire": msg_bytes,
@@ -210,6 +235,7 @@ def main():
             "egress_GBps": eg / t / 1e9,
             "latency_note": "in-broker publish->deliver (ingress submit to egress bytes ready), no TCP",
             "errors": errs,
+            "cross_gpu_bytes_per_s": (dp.exchanger.bytes_sent * world / t) if shards > 1 else 0.0,
         }
         print(json.dumps(out))
     if dist:

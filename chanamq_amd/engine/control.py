@@ -55,6 +55,7 @@ class Queue:
     capacity: int = 1 << 16
     ring_off: int = 0
     consumers: list = field(default_factory=list)  # consumer ids, in registration order
+    owner: int = 0                                  # owning rank (sharded data plane)
 
 
 @dataclass
@@ -101,8 +102,17 @@ class ControlState:
                           ("amq.topic", "topic"), ("amq.headers", "headers"), ("amq.match", "headers"))
 
     def __init__(self, c_max=1024, chpc=16, q_max=4096, x_max=1024, cons_max=16384,
-                 hash_wildcard=True, ring_pool=1 << 26, default_queue_capacity=1 << 16):
+                 hash_wildcard=True, ring_pool=1 << 26, default_queue_capacity=1 << 16,
+                 world=1, rank=0, shard_map=None):
         self.c_max, self.chpc, self.q_max, self.x_max, self.cons_max = c_max, chpc, q_max, x_max, cons_max
+        # sharded data plane: every rank holds the same exchanges/bindings/queue slots
+        # (control ops are applied on all ranks in the same order); a queue's ring,
+        # consumers and deliveries live only on its owner (parallel/shard.py)
+        self.world, self.rank = world, rank
+        if world > 1 and shard_map is None:
+            from ..parallel.shard import ShardMap
+            shard_map = ShardMap(world)
+        self.shard_map = shard_map
         self.hash_wildcard = hash_wildcard
         self.ring_pool = ring_pool
         self.default_queue_capacity = default_queue_capacity
@@ -249,12 +259,13 @@ class ControlState:
         if not self._free_q:
             raise ControlError(C.RESOURCE_ERROR, "queue table full", 50, 10)
         capacity = capacity or self.default_queue_capacity
+        owner = self.shard_map.owner(vhost, name) if self.world > 1 else self.rank
         cap = 1
-        while cap < capacity:
+        while cap < capacity and owner == self.rank:   # remote queues hold no ring here
             cap <<= 1
         slot = self._free_q.pop()
         q = Queue(slot, vhost, name, durable, exclusive_owner, auto_delete, ttl_ms, cap,
-                  self._ring_alloc(cap))
+                  self._ring_alloc(cap), owner=owner)
         self.queues[key] = q
         self.queue_by_slot[slot] = q
         dx = self.exchanges.get((vhost, ""))
@@ -311,6 +322,9 @@ class ControlState:
         q = self.queues.get((queue_vhost, queue))
         if q is None:
             raise ControlError(C.NOT_FOUND, f"no queue '{queue}'", 60, 20)
+        if q.owner != self.rank:
+            # consumers attach on the owning rank (the front end places the connection there)
+            raise ControlError(C.NOT_ALLOWED, f"queue '{queue}' is served by rank {q.owner}", 60, 20)
         chan = self.channel(conn, ch)
         if tag in chan.consumers:
             raise ControlError(C.NOT_ALLOWED, f"consumer tag '{tag}' in use", 60, 20)

@@ -15,7 +15,7 @@ import numpy as np
 from .. import ops
 from ..protocol import constants as C
 from .control import ControlError, ControlState
-from .layout import (CONN_OUT, CTRL_REC, INVALID, SEG_IN, SEG_OUT, SS_CTRL, chan_hash,
+from .layout import (CONN_OUT, CTRL_REC, INVALID, RDESC, SEG_IN, SEG_OUT, SS_CTRL, chan_hash,
                      direct_key, exch_hash, fnv1a64, topic_pattern_row)
 
 ONES64 = np.uint64((1 << 64) - 1)
@@ -35,10 +35,10 @@ class StepResult:
 
 class GpuDataPlane(ControlState):
     def __init__(self, device=0, hash_wildcard=True, graph=True, worker=0, default_queue_capacity=1 << 16,
-                 **cfg):
+                 world=1, rank=0, shard_map=None, exchanger=None, **cfg):
         self.mod = ops.load()
         full = dict(cfg)
-        full.update(device=device, hash_wildcard=int(hash_wildcard), graph=int(graph))
+        full.update(device=device, hash_wildcard=int(hash_wildcard), graph=int(graph), world=world, rank=rank)
         self.eng = self.mod.Engine(full)
         self.info = self.eng.info()
         sz = self.info["sizeof"]
@@ -56,9 +56,23 @@ class GpuDataPlane(ControlState):
                          egress=self.eng.host_view(f"egress_host{p}")) for p in (0, 1)]
         self._pin = [None, None]
         self.requeue_pending = False
+        self.exchanger = exchanger
+        self._pending = None
+        if world > 1:
+            # exchange operands live in torch's allocator so RCCL can use them directly
+            import torch
+            dev = torch.device("cuda", device)
+            u8 = torch.uint8
+            self._xs_desc = torch.empty(i["xfer_desc_max"] * RDESC.itemsize, dtype=u8, device=dev)
+            self._xs_pay = torch.empty(i["xfer_bytes"], dtype=u8, device=dev)
+            self._xr_desc = torch.empty(i["import_max"] * RDESC.itemsize, dtype=u8, device=dev)
+            self._xr_pay = torch.empty(i["xfer_bytes"], dtype=u8, device=dev)
+            self.eng.set_xfer_buffers(self._xs_desc.data_ptr(), self._xs_pay.data_ptr(),
+                                      self._xr_desc.data_ptr(), self._xr_pay.data_ptr())
         super().__init__(c_max=i["c_max"], chpc=i["chpc"], q_max=i["q_max"], x_max=i["x_max"],
                          cons_max=i["cons_max"], hash_wildcard=hash_wildcard, ring_pool=i["ring_pool"],
-                         default_queue_capacity=default_queue_capacity)
+                         default_queue_capacity=default_queue_capacity, world=world, rank=rank,
+                         shard_map=shard_map)
 
     # ================================================================== uploads
     def _up(self, name, arr, index=0):
@@ -228,6 +242,7 @@ class GpuDataPlane(ControlState):
         self._up_at("ch_dirty", 1, chslot, np.uint32)
 
     def queue_declared(self, q):
+        self._up_at("q_owner", q.owner, q.slot, np.uint32)
         self._up_at("q_ring_off", q.ring_off, q.slot, np.uint64)
         self._up_at("q_ring_mask", q.capacity - 1, q.slot, np.uint64)
         self._up_at("q_head", 0, q.slot, np.uint64)
@@ -288,6 +303,11 @@ class GpuDataPlane(ControlState):
     def step(self, inputs=None, now_ms=None, collect=True):
         """One synchronous data-plane step.  ``inputs``: {conn: bytes}.  Connections
         holding carry (partial commands) are re-presented once unpaused."""
+        segs, ptr, n = self.stage(inputs)
+        return self.step_raw(segs, ptr, n, now_ms, collect)
+
+    def stage(self, inputs):
+        """{conn: bytes} (+ connections holding carry) -> (SegIn[], pinned ptr, bytes)."""
         inputs = inputs or {}
         conns = set(inputs)
         for c in np.nonzero(self.carry)[0]:
@@ -306,7 +326,7 @@ class GpuDataPlane(ControlState):
                 pin[off:off + n] = np.frombuffer(data, np.uint8)
             segs[k] = (c, n, off)
             off += (n + 15) & ~15
-        return self.step_raw(segs, pin.ctypes.data, off, now_ms, collect)
+        return segs, pin.ctypes.data, off
 
     def step_raw(self, segs, payload_ptr, payload_len, now_ms=None, collect=True):
         t = self.submit_raw(segs, payload_ptr, payload_len, now_ms)
@@ -319,7 +339,39 @@ class GpuDataPlane(ControlState):
         t0 = time.perf_counter()
         p = self.eng.submit(segs, int(payload_ptr), int(payload_len), now, self.step_no, now, self.worker)
         self.step_no += 1
+        if self.world > 1:
+            self._pending = p
+            cnt = self.eng.send_counts(p)
+            if cnt[-1]:
+                raise RuntimeError("cross-rank send buffers overflowed (xfer_desc_max / xfer_bytes)")
+            self._send_counts = cnt[:-1]
+            if self.exchanger is not None:   # one process per rank: collective now
+                recv = self.exchanger.exchange(self._send_counts, self._xs_desc, self._xs_pay,
+                                               self._xr_desc, self._xr_pay)
+                self.submit_b(recv)
         return (p, len(segs), t0)
+
+    # ---- sharded step, phase B (LocalCluster drives it after its in-process exchange)
+    def pending_send_counts(self):
+        return self._send_counts
+
+    def xfer_send_desc(self):
+        return self._xs_desc
+
+    def xfer_send_pay(self):
+        return self._xs_pay
+
+    def xfer_recv_desc(self):
+        return self._xr_desc
+
+    def xfer_recv_pay(self):
+        return self._xr_pay
+
+    def submit_b(self, recv):
+        import torch
+        stream = torch.cuda.current_stream(self.device).cuda_stream
+        self.eng.submit_b(self._pending, [int(x) for x in recv], int(stream))
+        self._pending = None
 
     def finish(self, ticket, collect=True, wait_egress=True):
         p, nseg, t0 = ticket

@@ -10,10 +10,13 @@ and the reference-semantics model the tests compare kernels against.
 import struct
 from collections import defaultdict
 
+import numpy as np
+
 from ..models.matcher import topic_match
 from ..protocol import constants as C
 from .control import ControlState
-from .layout import SS_CTRL, SS_FRAME_ERROR, SS_OVERFLOW, SS_TOO_LARGE, SS_UNEXPECTED
+from .layout import (MF_HAS_TS, MF_PERSIST, RDESC, SS_CTRL, SS_FRAME_ERROR, SS_OVERFLOW, SS_TOO_LARGE,
+                     SS_UNEXPECTED)
 
 NO_ROUTE_TEXT = C.REPLY_TEXT[312].encode()
 NO_CONS_TEXT = C.REPLY_TEXT[313].encode()
@@ -33,8 +36,19 @@ class _Msg:
 
 class GoldenDataPlane(ControlState):
     def __init__(self, hash_wildcard=True, ucap=8192, deliver_cap=4096, carry_cap=1 << 20,
-                 egress_cap=96 << 20, deliv_max=65536, **kw):
+                 egress_cap=96 << 20, deliv_max=65536, exchanger=None, xfer_desc_max=1 << 15,
+                 xfer_bytes=1 << 24, **kw):
         super().__init__(hash_wildcard=hash_wildcard, **kw)
+        self.exchanger = exchanger
+        self._outbox = defaultdict(list)  # dest rank -> [(RDesc fields, payload)]
+        self._deferred = []                # this rank's routed publishes awaiting step_b
+        self._pend = None
+        if self.world > 1:
+            import torch
+            self._xs_desc = torch.zeros(xfer_desc_max * RDESC.itemsize, dtype=torch.uint8)
+            self._xs_pay = torch.zeros(xfer_bytes, dtype=torch.uint8)
+            self._xr_desc = torch.zeros(xfer_desc_max * RDESC.itemsize, dtype=torch.uint8)
+            self._xr_pay = torch.zeros(xfer_bytes, dtype=torch.uint8)
         self.ucap, self.deliver_cap, self.carry_cap = ucap, deliver_cap, carry_cap
         self.egress_cap, self.deliv_max = egress_cap, deliv_max
         self.carry = defaultdict(bytes)
@@ -193,6 +207,101 @@ class GoldenDataPlane(ControlState):
 
     # ------------------------------------------------------------------ one step
     def step(self, inputs=None, now_ms=0):
+        """One step.  Sharded (world > 1): phase A, the all-to-all through ``exchanger``,
+        phase B — ``LocalCluster`` drives the phases itself for in-process clusters."""
+        self.step_a(inputs, now_ms)
+        if self.world > 1:
+            if self.exchanger is None:
+                raise RuntimeError("sharded golden plane needs an exchanger (or a LocalCluster)")
+            recv = self.exchanger.exchange(self.pending_send_counts(), self._xs_desc, self._xs_pay,
+                                           self._xr_desc, self._xr_pay)
+            return self.step_b(recv)
+        return self.step_b(None)
+
+    # exchange operands (parallel/exchange.py)
+    def xfer_send_desc(self):
+        return self._xs_desc
+
+    def xfer_send_pay(self):
+        return self._xs_pay
+
+    def xfer_recv_desc(self):
+        return self._xr_desc
+
+    def xfer_recv_pay(self):
+        return self._xr_pay
+
+    def pending_send_counts(self):
+        return self._pend["send_counts"]
+
+    def _pack(self):
+        """Serialise the outbox destination-major (same layout as k_pack)."""
+        W = self.world
+        n, b = [0] * W, [0] * W
+        recs = []
+        for r in range(W):
+            for fields, payload in self._outbox.get(r, []):
+                recs.append((r, fields, payload))
+        desc = np.zeros(len(recs), RDESC)
+        pay = bytearray()
+        for r in range(W):
+            rel = 0
+            for fields, payload in self._outbox.get(r, []):
+                k = sum(n)
+                f = dict(fields)
+                f["pay_off"] = rel
+                for key, v in f.items():
+                    desc[k][key] = v
+                padded = payload + b"\0" * ((-len(payload)) % 16)
+                pay += padded
+                rel += len(padded)
+                n[r] += 1
+                b[r] += len(padded)
+        self._outbox = defaultdict(list)
+        if desc.nbytes > self._xs_desc.numel() or len(pay) > self._xs_pay.numel():
+            raise RuntimeError("golden exchange buffers too small")
+        import torch
+        if len(desc):
+            self._xs_desc[:desc.nbytes] = torch.from_numpy(desc.view(np.uint8).copy())
+        if pay:
+            self._xs_pay[:len(pay)] = torch.frombuffer(bytearray(pay), dtype=torch.uint8)
+        return n + b
+
+    def _import(self, recv, now_ms):
+        """Enqueue the step's messages in (source rank, connection, publish) order: this
+        rank's own publishes at its rank position, records from rank s at s's — the
+        order the GPU pair sort produces with its (queue, source rank) keys."""
+        W = self.world
+        rn, rb = recv[:W], recv[W:2 * W]
+        tot = sum(rn)
+        desc = self._xr_desc[:tot * RDESC.itemsize].numpy().view(RDESC) if tot else None
+        pay = self._xr_pay[:sum(rb)].numpy().tobytes() if tot else b""
+        pbase = [sum(rb[:s]) for s in range(W)]
+        i = 0
+        for s in range(W):
+            if s == self.rank:
+                for msg, qs, expire in self._deferred:
+                    self._enqueue(msg, qs, expire, now_ms)
+                self._deferred = []
+            for _ in range(rn[s]):
+                d = desc[i]
+                i += 1
+                o = pbase[s] + int(d["pay_off"])
+                exl, rkl, pl, bl = int(d["ex_len"]), int(d["rk_len"]), int(d["props_len"]), int(d["body_len"])
+                ex = pay[o:o + exl]
+                rk = pay[o + exl:o + exl + rkl]
+                props = pay[o + exl + rkl:o + exl + rkl + pl]
+                body = pay[o + exl + rkl + pl:o + exl + rkl + pl + bl]
+                x = self.exch_by_slot.get(int(d["exch"]))
+                if x is None:
+                    continue
+                qs = [q for q in self._route(x, rk) if self.queue_by_slot[q].owner == self.rank]
+                if not qs:
+                    continue
+                msg = _Msg(ex, rk, props, body, len(qs), self.step_no, int(d["flags"]) & MF_PERSIST)
+                self._enqueue(msg, qs, int(d["expire_ms"]), now_ms)
+
+    def step_a(self, inputs=None, now_ms=0):
         inputs = inputs or {}
         self.counters = defaultdict(int)
         cnt = self.counters
@@ -244,6 +353,15 @@ class GoldenDataPlane(ControlState):
         returns = defaultdict(list)
         for cmd, data in pubs:
             self._publish(cmd, data, now_ms, returns, out)
+        self._pend = dict(out=out, returns=returns, acks=acks, now_ms=now_ms,
+                          send_counts=self._pack() if self.world > 1 else None)
+
+    def step_b(self, recv=None):
+        st, self._pend = self._pend, None
+        out, returns, acks, now_ms = st["out"], st["returns"], st["acks"], st["now_ms"]
+        cnt = self.counters
+        if recv is not None:
+            self._import(recv, now_ms)
         # ---- acks
         for cmd, data in acks:
             s = cmd["chslot"]
@@ -383,14 +501,24 @@ class GoldenDataPlane(ControlState):
             out["events"].append((conn, 404, s))
             return
         qs = self._route(x, rk)
+        remote = sorted({self.queue_by_slot[q].owner for q in qs} - {self.rank}) if self.world > 1 else []
         ret = 0
         if not qs:
             cnt["n_unroutable"] += 1
             if mandatory:
                 ret = 312
-        elif immediate and not any(self.queue_by_slot[q].consumers for q in qs):
+        elif immediate and not remote and not any(self.queue_by_slot[q].consumers for q in qs):
             ret = 313
             qs = []
+        if remote and not ret:
+            fl = (MF_PERSIST if self._persistent(props) else 0)
+            if self._prop_fields(props).get("timestamp") is not None:
+                fl |= MF_HAS_TS
+            fields = dict(body_len=len(body), props_len=len(props), exch=x.slot, flags=fl, ex_len=len(ex),
+                          rk_len=len(rk), expire_ms=expire, ts_ms=0)
+            for r in remote:
+                self._outbox[r].append((fields, ex + rk + props + body))
+            qs = [q for q in qs if self.queue_by_slot[q].owner == self.rank]
         if ret:
             txt = NO_ROUTE_TEXT if ret == 312 else NO_CONS_TEXT
             fm = self.conns[conn].frame_max
@@ -404,6 +532,13 @@ class GoldenDataPlane(ControlState):
             return
         flags = 1 if self._persistent(props) else 0
         msg = _Msg(ex, rk, props, body, len(qs), self.step_no, flags)
+        if self.world > 1:   # enqueued in step_b, ordered by source rank (see _import)
+            self._deferred.append((msg, qs, expire))
+        else:
+            self._enqueue(msg, qs, expire, now_ms)
+
+    def _enqueue(self, msg, qs, expire, now_ms):
+        cnt = self.counters
         for q in qs:
             qq = self.queue_by_slot[q]
             ring = self.ring[q]

@@ -11,8 +11,14 @@ SEG_OUT = np.dtype([("conn", "<u4"), ("status", "<u4"), ("consumed", "<u4"), ("c
                     ("ncmds", "<u4"), ("err_off", "<u4"), ("pad", "<u4", 2)])
 CTRL_REC = np.dtype([("conn", "<u4"), ("off", "<u4"), ("len", "<u4"), ("seg", "<u4")])
 CONN_OUT = np.dtype([("off", "<u4"), ("len", "<u4")])
+# cross-rank publish record (dp_common.h RDesc); payload = [exchange][routing key][props][body]
+RDESC = np.dtype([("pay_off", "<u4"), ("body_len", "<u4"), ("props_len", "<u4"), ("exch", "<i4"),
+                  ("flags", "<u4"), ("ex_len", "u1"), ("rk_len", "u1"), ("pad0", "<u2"),
+                  ("expire_ms", "<i8"), ("ts_ms", "<i8"), ("pad", "<u4", 6)])
+MF_PERSIST, MF_MANDATORY, MF_IMMEDIATE, MF_HAS_TS, MF_IMPORTED = 1, 2, 4, 8, 16
 
-STRUCT_SIZES = {"SegIn": 16, "SegOut": 32, "CtrlRec": 16, "ConnOut": 8, "StepIn": 64}
+STRUCT_SIZES = {"SegIn": 16, "SegOut": 32, "CtrlRec": 16, "ConnOut": 8, "StepIn": 64, "RDesc": 64}
+assert RDESC.itemsize == 64
 
 # SegOut.status bits
 SS_PAUSED = 1

@@ -1,0 +1,48 @@
+"""In-process sharded cluster: W data planes (GPU or golden) stepped in lockstep, the
+cross-rank exchange done by local copies.  Used by tests on one device and as the
+reference for the one-process-per-GPU deployment (each rank then owns one plane and an
+``Exchanger`` over RCCL).  Control operations are replicated to every plane in the same
+order so queue/exchange slots agree across ranks."""
+
+from .exchange import local_exchange
+from .shard import ShardMap
+
+
+class LocalCluster:
+    def __init__(self, make_plane, world, shard_map=None):
+        self.world = world
+        self.shard_map = shard_map or ShardMap(world)
+        self.planes = [make_plane(rank=r, world=world, shard_map=self.shard_map) for r in range(world)]
+
+    def __getitem__(self, r):
+        return self.planes[r]
+
+    def replicate(self, fn, *args, **kw):
+        """Apply a control-plane op (declare/bind/delete ...) on every rank."""
+        return [getattr(p, fn)(*args, **kw) for p in self.planes]
+
+    def step(self, inputs_by_rank, now_ms=0):
+        """``inputs_by_rank``: [ {conn: bytes} per rank ] -> [StepResult/dict per rank]."""
+        gpu = hasattr(self.planes[0], "eng")
+        tickets = []
+        for r, p in enumerate(self.planes):
+            inp = inputs_by_rank[r] if r < len(inputs_by_rank) else {}
+            if gpu:
+                tickets.append(_gpu_submit(p, inp, now_ms))
+            else:
+                p.step_a(inp, now_ms)
+        recv = local_exchange(self.planes)
+        out = []
+        for r, p in enumerate(self.planes):
+            if gpu:
+                p.submit_b(recv[r])
+                out.append(p.finish(tickets[r]))
+            else:
+                out.append(p.step_b(recv[r]))
+        return out
+
+
+def _gpu_submit(plane, inputs, now_ms):
+    """GpuDataPlane.step() without the collective: stage ingress and run phase A."""
+    segs, ptr, n = plane.stage(inputs)
+    return plane.submit_raw(segs, ptr, n, now_ms)

@@ -761,6 +761,12 @@ __global__ void k_set_counts(DS d) {
   u32 np = d.tot[4], na = d.tot[5];
   d.ctr->n_pubs = np < d.pub_max ? np : d.pub_max;
   d.ctr->n_acks = na < d.ack_max ? na : d.ack_max;
+  // routing phase 0: the step's own publishes
+  d.tot[TS_RANGE_LO] = 0;
+  d.tot[TS_RANGE_HI] = d.ctr->n_pubs;
+  d.tot[TS_PAIR_BASE] = 0;
+  d.tot[TS_PAIR_N] = 0;
+  d.tot[TS_NIMPORT] = 0;
 }
 
 __global__ void k_reset_dirty(DS d) {
@@ -771,6 +777,28 @@ DEV bool skip_shortstr(const u8* p, u32& o, u32 end) {
   if (o + 1 > end) return false;
   o += 1 + p[o];
   return o <= end;
+}
+
+// topic key vector (8 words x 32 bits, +-1), built only if topic bindings exist
+DEV u32 build_keyvec(const DS& d, const u8* key, u32 len, u32 pi) {
+  Words kw = words_of(key, len);
+  if (d.tb_max) {
+    i8* kv = d.pub_keyvec + (u64)pi * TOPIC_K;
+    u32 off = 0;
+    u32 wi = 0;
+    if (kw.count) {
+      while (wi < TOPIC_WORDS && off <= kw.eff) {
+        u32 wl = word_len(key, off, kw.eff);
+        u32 h = fnv1a32(key + off, wl);
+        for (int bb = 0; bb < 32; ++bb) kv[wi * 32 + bb] = ((h >> bb) & 1) ? 1 : -1;
+        off += wl + 1;
+        ++wi;
+      }
+    }
+    for (; wi < TOPIC_WORDS; ++wi)
+      for (int bb = 0; bb < 32; ++bb) kv[wi * 32 + bb] = 0;
+  }
+  return kw.count;
 }
 
 __global__ void k_decode(DS d) {
@@ -879,26 +907,7 @@ __global__ void k_decode(DS d) {
           pok = skip_shortstr(w, q, hend);
       }
     }
-    // topic key vector (8 words x 32 bits, +-1), built only if topic bindings exist
-    Words kw = words_of(w + pb.rk_off, pb.rk_len);
-    pb.nwords = kw.count;
-    i8* kv = d.pub_keyvec + (u64)pi * TOPIC_K;
-    if (d.tb_max) {
-      u32 off = 0;
-      u32 wi = 0;
-      const u8* key = w + pb.rk_off;
-      if (kw.count) {
-        while (wi < TOPIC_WORDS && off <= kw.eff) {
-          u32 wl = word_len(key, off, kw.eff);
-          u32 h = fnv1a32(key + off, wl);
-          for (int bb = 0; bb < 32; ++bb) kv[wi * 32 + bb] = ((h >> bb) & 1) ? 1 : -1;
-          off += wl + 1;
-          ++wi;
-        }
-      }
-      for (; wi < TOPIC_WORDS; ++wi)
-        for (int bb = 0; bb < 32; ++bb) kv[wi * 32 + bb] = 0;
-    }
+    pb.nwords = build_keyvec(d, w + pb.rk_off, pb.rk_len, pi);
     d.pubs[pi] = pb;
     if (pb.chslot != INVALID && d.ch_confirm[pb.chslot]) atomicAdd(&d.ch_pub_cnt[pb.chslot], 1u);
   } else if (c.kind == CK_ACK || c.kind == CK_NACK || c.kind == CK_REJECT) {
@@ -920,12 +929,18 @@ __global__ void k_decode(DS d) {
 
 // ============================================================================ scans
 // single-block multi-array exclusive scan; n read from device; totals -> tot[slot+k]
-struct ScanArgs { const u32* in[4]; u32* out[4]; const u32* n; u32 narr; u32 nmax; u32 tot_slot; };
+// lo != null: scan elements [*lo, *n) (absolute indices), else [0, *n)
+struct ScanArgs { const u32* in[4]; u32* out[4]; const u32* n; const u32* lo; u32 narr; u32 nmax; u32 tot_slot; };
 // single-block exclusive scan over up to 4 arrays; tiles of 4096 with 16-B loads/stores
 __global__ __launch_bounds__(1024) void k_scan(ScanArgs a, u32* tot) {
   __shared__ u32 lds[1024 / 64 + 1];
   u32 n = a.n ? *a.n : a.nmax;
   if (n > a.nmax) n = a.nmax;
+  if (a.lo) {
+    u32 lo = *a.lo;
+    n = n > lo ? n - lo : 0;
+    for (u32 k = 0; k < a.narr; ++k) { a.in[k] += lo; a.out[k] += lo; }
+  }
   const u32 tid = threadIdx.x;
   u32 run[4] = {0, 0, 0, 0};
   for (u32 base = 0; base < n; base += 4096) {
@@ -934,23 +949,25 @@ __global__ __launch_bounds__(1024) void k_scan(ScanArgs a, u32* tot) {
     for (int k = 0; k < 4; ++k) {
       if ((u32)k >= a.narr) break;
       u32 v0 = 0, v1 = 0, v2 = 0, v3 = 0;
-      if (i + 3 < n) {
+      if (i + 3 < n && !(((uintptr_t)(a.in[k] + i)) & 15)) {
         uint4 v = *(const uint4*)(a.in[k] + i);
         v0 = v.x; v1 = v.y; v2 = v.z; v3 = v.w;
       } else {
         if (i < n) v0 = a.in[k][i];
         if (i + 1 < n) v1 = a.in[k][i + 1];
         if (i + 2 < n) v2 = a.in[k][i + 2];
+        if (i + 3 < n) v3 = a.in[k][i + 3];
       }
       u32 sum = v0 + v1 + v2 + v3, all;
       u32 off = run[k] + block_scan<1024>(sum, lds, all);
       uint4 o;
       o.x = off; o.y = off + v0; o.z = o.y + v1; o.w = o.z + v2;
-      if (i + 3 < n) *(uint4*)(a.out[k] + i) = o;
+      if (i + 3 < n && !(((uintptr_t)(a.out[k] + i)) & 15)) *(uint4*)(a.out[k] + i) = o;
       else {
         if (i < n) a.out[k][i] = o.x;
         if (i + 1 < n) a.out[k][i + 1] = o.y;
         if (i + 2 < n) a.out[k][i + 2] = o.z;
+        if (i + 3 < n) a.out[k][i + 3] = o.w;
       }
       run[k] += all;
     }
@@ -1056,15 +1073,7 @@ __global__ __launch_bounds__(256) void k_rs_scatter(const u32* kin, const u32* v
 // topic prefilter on MFMA: score[p][b] = keyvec[p] . patvec[b] over 256 int8 lanes;
 // a pattern word contributes +32 iff its 32-bit word hash equals the key's.
 typedef int v4i __attribute__((ext_vector_type(4)));
-__global__ __launch_bounds__(256) void k_topic_mfma(DS d) {
-  u32 wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  u32 lane = lane_id();
-  u32 ntb = d.tb_pad >> 4;
-  u32 npub = d.ctr->n_pubs;
-  if (npub > d.pub_max) npub = d.pub_max;
-  u32 it = wave / ntb, jt = wave % ntb;
-  u32 i0 = it * 16, j0 = jt * 16;
-  if (i0 >= npub || d.tb_max == 0) return;
+DEV void topic_tile(const DS& d, u32 i0, u32 j0, u32 jt, u32 ntb, u32 npub, u32 lane) {
   v4i acc = {0, 0, 0, 0};
   const i8* A = d.pub_keyvec + (u64)(i0 + (lane & 15)) * TOPIC_K + (lane >> 4) * 16;
   const i8* B = d.t_mat + (u64)(j0 + (lane & 15)) * TOPIC_K + (lane >> 4) * 16;
@@ -1077,13 +1086,26 @@ __global__ __launch_bounds__(256) void k_topic_mfma(DS d) {
   i32 ex = d.t_expect[j0 + (lane & 15)];
   u64 m0 = __ballot(acc[0] == ex), m1 = __ballot(acc[1] == ex);
   u64 m2 = __ballot(acc[2] == ex), m3 = __ballot(acc[3] == ex);
-  if (lane < 16) {
-    u32 row = i0 + lane;  // row = 4*g + r with g = lane/4, r = lane%4
+  if (lane < 16) {  // row = i0 + 4*g + r with g = lane/4, r = lane%4
     u32 g = lane >> 2, r = lane & 3;
     u64 mm = r == 0 ? m0 : r == 1 ? m1 : r == 2 ? m2 : m3;
     u32 rr = i0 + g * 4 + r;
-    (void)row;
     if (rr < npub) d.pub_match[(u64)rr * ntb + jt] = (u16)((mm >> (16 * g)) & 0xffff);
+  }
+}
+
+// grid-stride over 16x16 (publish x binding) tiles of the current phase range
+__global__ __launch_bounds__(256) void k_topic_mfma(DS d) {
+  if (d.tb_max == 0) return;
+  u32 lane = lane_id();
+  u32 ntb = d.tb_pad >> 4;
+  u32 lo = d.tot[TS_RANGE_LO], npub = d.tot[TS_RANGE_HI];
+  if (npub > d.pub_cap) npub = d.pub_cap;
+  u32 ntiles = (npub > lo ? (npub - lo + 15) / 16 : 0) * ntb;
+  const u32 nw = (gridDim.x * blockDim.x) >> 6;
+  for (u32 wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6; wave < ntiles; wave += nw) {
+    u32 it = wave / ntb, jt = wave % ntb;
+    topic_tile(d, lo + it * 16, jt * 16, jt, ntb, npub, lane);
   }
 }
 
@@ -1114,31 +1136,43 @@ DEV i32 direct_find(const DS& d, const Pub& pb) {
 }
 
 // pass 0: count queues; pass 1: write pairs
+// Publishes [tot[RANGE_LO], tot[RANGE_HI]): phase 0 = the step's own, phase 1 = records
+// imported from other ranks (sharded queues; only locally owned queues are emitted).
 template <int PASS>
 __global__ void k_route(DS d) {
-  u32 p = blockIdx.x * blockDim.x + threadIdx.x;
-  u32 n = d.ctr->n_pubs;
-  if (n > d.pub_max) n = d.pub_max;
-  if (p >= n) {
-    if (PASS == 0 && p < d.pub_max) { d.pub_nq[p] = 0; d.pub_slot[p] = 0; d.pub_routed[p] = 0; }
-    return;
-  }
+  u32 p = d.tot[TS_RANGE_LO] + blockIdx.x * blockDim.x + threadIdx.x;
+  u32 n = d.tot[TS_RANGE_HI];
+  if (n > d.pub_cap) n = d.pub_cap;
+  if (p >= n) return;
   Pub& pb = d.pubs[p];
-  u32 wbase = PASS ? d.pub_pair_off[p] : 0;
+  u32 wbase = PASS ? d.tot[TS_PAIR_BASE] + d.pub_pair_off[p] : 0;
+  // pair key = queue << rank_bits | source rank: a queue's messages are ordered by
+  // (source rank, connection, publish order) whichever rank owns it
+  const u32 rb = d.rank_bits;
+  const u32 srank = (pb.flags & MF_IMPORTED) ? pb.pad : d.my_rank;
   if (PASS == 1) {
     u32 nq0 = d.pub_nq[p];
     if (nq0 == 0) return;
+    if (wbase + nq0 > d.pair_max) return;  // capacity: k_log_reserve clamps the pair count
     if (nq0 <= 8) {  // routing result cached by pass 0
-      for (u32 k = 0; k < nq0; ++k) { d.pair_k[0][wbase + k] = d.pub_qc[(u64)p * 8 + k]; d.pair_v[0][wbase + k] = p; }
+      for (u32 k = 0; k < nq0; ++k) {
+        d.pair_k[0][wbase + k] = (d.pub_qc[(u64)p * 8 + k] << rb) | srank;
+        d.pair_v[0][wbase + k] = p;
+      }
       return;
     }
   }
-  u32 nq = 0;
+  u32 nq = 0, nq_all = 0, rmask = 0;
   bool has_cons = false;
+  const u32 me = d.my_rank;
+  const bool sharded = d.world > 1;
 #define EMIT(q)                                              \
   do {                                                       \
     u32 _q = (q);                                            \
-    if (PASS) { d.pair_k[0][wbase + nq] = _q; d.pair_v[0][wbase + nq] = p; } \
+    ++nq_all;                                                \
+    u32 _o = sharded ? d.q_owner[_q] : me;                   \
+    if (_o != me) { rmask |= 1u << _o; has_cons = true; break; } \
+    if (PASS) { d.pair_k[0][wbase + nq] = (_q << rb) | srank; d.pair_v[0][wbase + nq] = p; } \
     else if (nq < 8) d.pub_qc[(u64)p * 8 + nq] = _q;         \
     if (d.q_cons_n[_q]) has_cons = true;                     \
     ++nq;                                                    \
@@ -1168,13 +1202,15 @@ __global__ void k_route(DS d) {
 #undef EMIT
   if (PASS == 0) {
     u32 ret = 0;
-    if (pb.exch < 0) {
+    if (pb.flags & MF_IMPORTED) {
+      rmask = 0;  // imported records are never forwarded again
+    } else if (pb.exch < 0) {
       atomicAdd(&d.ctr->n_unknown_exchange, 1u);
       u32 ri = atomicAdd(&d.ctr->n_ctrl, 1u);
       CtrlRec rec;
       rec.conn = pb.conn; rec.off = INVALID; rec.len = 404; rec.seg = pb.chslot;
       if (ri < d.seg_max * 2) d.ctrl_rec[ri] = rec;
-    } else if (nq == 0) {
+    } else if (nq_all == 0) {
       atomicAdd(&d.ctr->n_unroutable, 1u);
       if (pb.flags & MF_MANDATORY) ret = 312;
     } else if ((pb.flags & MF_IMMEDIATE) && !has_cons) {
@@ -1182,6 +1218,7 @@ __global__ void k_route(DS d) {
       nq = 0;  // spec behaviour: not enqueued (SURVEY A.Q16/CHANGES.md)
     }
     d.pub_ret[p] = ret;
+    if (sharded) d.pub_rmask[p] = ret ? 0 : rmask;
     u32 meta = align16(pb.ex_len + pb.rk_len + pb.props_len);
     u32 slot = nq ? align16(meta + pb.body_size) : 0;
     d.pub_nq[p] = nq;
@@ -1211,30 +1248,39 @@ __global__ void k_log_reserve(DS d) {
   if (threadIdx.x) return;
   u32 total = d.tot[1];     // slot bytes
   u32 routed = d.tot[2];    // routed messages
+  u32 np = d.tot[TS_PAIR_BASE] + d.tot[0];
+  d.tot[TS_PAIR_N] = np < d.pair_max ? np : d.pair_max;
+  d.ctr->n_pairs = d.tot[TS_PAIR_N];
+  *d.id_base = *d.id_next;
+  *d.id_next = *d.id_next + routed;
   u64 head = *d.log_head, tail = *d.log_tail;
   u64 phys = head % d.log_bytes;
   if (phys + total > d.log_bytes) head += d.log_bytes - phys;
   bool ok = (head + total - tail <= d.log_bytes) && routed <= *d.msg_free_top;
   if (!ok || total == 0) {
     *d.log_step_base = ok ? head : INVALID;
-    if (!ok) d.ctr->n_dropped_nomem = routed;
+    if (!ok) d.ctr->n_dropped_nomem += routed;
     return;
   }
   *d.log_step_base = head;
   *d.log_head = head + total;
   d.tot[8] = *d.msg_free_top;
   *d.msg_free_top = d.tot[8] - routed;
-  d.ctr->n_routed_msgs = routed;
-  d.ctr->n_pairs = d.tot[0];
+  d.ctr->n_routed_msgs += routed;
 }
 
 // one wave per publish: allocate, fill MsgEnt, copy exchange/rk/props/body into the log
+DEV void store_one(const DS& d, u32 p, u32 lane);
 __global__ __launch_bounds__(256) void k_store(DS d) {
-  u32 p = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   u32 lane = lane_id();
-  u32 n = d.ctr->n_pubs;
-  if (n > d.pub_max) n = d.pub_max;
-  if (p >= n) return;
+  u32 n = d.tot[TS_RANGE_HI];
+  if (n > d.pub_cap) n = d.pub_cap;
+  const u32 nw = (gridDim.x * blockDim.x) >> 6;
+  for (u32 p = d.tot[TS_RANGE_LO] + ((blockIdx.x * blockDim.x + threadIdx.x) >> 6); p < n; p += nw)
+    store_one(d, p, lane);
+}
+
+DEV void store_one(const DS& d, u32 p, u32 lane) {
   Pub& pb = d.pubs[p];
   if (d.pub_nq[p] == 0) return;
   u64 base = *d.log_step_base;
@@ -1257,7 +1303,7 @@ __global__ __launch_bounds__(256) void k_store(DS d) {
   if (lane == 0) {
     MsgEnt m;
     m.log_off = off;
-    u64 pos = (*d.id_next) + rr;
+    u64 pos = (*d.id_base) + rr;
     m.msg_id = ((pos >> 12) << 22) | (u64(d.in->worker & 1023) << 12) | (pos & 4095);
     m.ts_ms = pb.ts_ms;
     m.slot_bytes = pb.slot_bytes;
@@ -1277,9 +1323,9 @@ __global__ __launch_bounds__(256) void k_store(DS d) {
 
 // thread per publish: account stored bytes per log block (one atomic per block per wave)
 __global__ void k_live_add(DS d) {
-  u32 p = blockIdx.x * blockDim.x + threadIdx.x;
-  u32 n = d.ctr->n_pubs;
-  if (n > d.pub_max) n = d.pub_max;
+  u32 p = d.tot[TS_RANGE_LO] + blockIdx.x * blockDim.x + threadIdx.x;
+  u32 n = d.tot[TS_RANGE_HI];
+  if (n > d.pub_cap) n = d.pub_cap;
   u64 base = *d.log_step_base;
   bool valid = p < n && base != INVALID && d.pub_nq[p] > 0;
   u64 blk = 0;
@@ -1292,22 +1338,179 @@ __global__ void k_live_add(DS d) {
   wave_add_i64(d.log_live, blk, sb, valid);
 }
 
+// ============================================================================ sharded queues
+// Cross-rank exchange of publishes (SURVEY §3.4 / BASELINE config 3).  Each queue has one
+// owning rank; bindings are replicated.  Phase A (the step's own publishes) emits pairs for
+// local queues and marks remote owners in pub_rmask; the packers below serialise each such
+// publish once per destination rank into [RDesc][payload] send buffers, laid out
+// destination-major so one RCCL all_to_all_single moves them.  Phase B imports the
+// received records as publishes and routes them against local queues only.
+
+// thread per local publish: record / payload bytes per destination rank
+__global__ void k_pack_count(DS d) {
+  u32 p = blockIdx.x * blockDim.x + threadIdx.x;
+  u32 n = d.ctr->n_pubs;
+  if (p >= d.pub_max) return;
+  u32 m = 0, sz = 0;
+  if (p < n) {
+    m = d.pub_rmask[p];
+    const Pub& pb = d.pubs[p];
+    sz = align16(pb.ex_len + pb.rk_len + pb.props_len + pb.body_size);
+  }
+  for (u32 r = 0; r < d.world; ++r) {
+    u32 b = (m >> r) & 1;
+    d.xp_cnt[(u64)r * d.pub_cap + p] = b;
+    d.xp_byt[(u64)r * d.pub_cap + p] = b ? sz : 0;
+  }
+}
+
+// destination bases (exclusive scans over ranks) + host-visible send counts
+__global__ void k_pack_bases(DS d) {
+  if (threadIdx.x) return;
+  u32 dsum = 0, psum = 0;
+  for (u32 r = 0; r < d.world; ++r) {
+    u32 c = d.tot[TS_XSCAN + 2 * r], b = d.tot[TS_XSCAN + 2 * r + 1];
+    d.xs_base[r] = dsum;
+    d.xs_base[WORLD_MAX + r] = psum;
+    d.xchg[r] = c;
+    d.xchg[WORLD_MAX + r] = b;
+    dsum += c;
+    psum += b;
+  }
+  d.xchg[4 * WORLD_MAX] = (dsum > d.xfer_desc_max || psum > d.xfer_bytes) ? 1u : 0u;
+}
+
+// one wave per local publish with remote owners: write one record per destination
+__global__ __launch_bounds__(256) void k_pack(DS d) {
+  u32 p = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  u32 n = d.ctr->n_pubs;
+  if (p >= n) return;
+  u32 m = d.pub_rmask[p];
+  if (!m) return;
+  u32 lane = lane_id();
+  const Pub pb = d.pubs[p];
+  const u8* w = d.work;
+  while (m) {
+    u32 r = __builtin_ctz(m);
+    m &= m - 1;
+    u32 di = d.xs_base[r] + d.xp_cnt_off[(u64)r * d.pub_cap + p];
+    u32 rel = d.xp_byt_off[(u64)r * d.pub_cap + p];
+    u64 po = (u64)d.xs_base[WORLD_MAX + r] + rel;
+    u32 sz = align16(pb.ex_len + pb.rk_len + pb.props_len + pb.body_size);
+    if (di >= d.xfer_desc_max || po + sz > d.xfer_bytes) continue;  // overflow flagged by k_pack_bases
+    u8* o = d.send_pay + po;
+    wave_copy(o, w + pb.ex_off, pb.ex_len);
+    o += pb.ex_len;
+    wave_copy(o, w + pb.rk_off, pb.rk_len);
+    o += pb.rk_len;
+    wave_copy(o, w + pb.props_off, pb.props_len);
+    o += pb.props_len;
+    for (u32 k = 0; k < pb.nfrag; ++k) {
+      Frag fg = d.frags[pb.frag0 + k];
+      wave_copy(o, w + fg.off, fg.len);
+      o += fg.len;
+    }
+    if (lane == 0) {
+      RDesc rd{};
+      rd.pay_off = rel;
+      rd.body_len = pb.body_size;
+      rd.props_len = pb.props_len;
+      rd.exch = pb.exch;
+      rd.flags = pb.flags & (MF_PERSIST | MF_HAS_TS);
+      rd.ex_len = (u8)pb.ex_len;
+      rd.rk_len = (u8)pb.rk_len;
+      rd.expire_ms = pb.expire_ms;
+      rd.ts_ms = pb.ts_ms;
+      d.send_desc[di] = rd;
+    }
+  }
+}
+
+// phase B set-up: source bases from the received counts (host-mapped xchg), import range
+__global__ void k_import_prep(DS d) {
+  if (threadIdx.x) return;
+  u32 dsum = 0, psum = 0;
+  for (u32 r = 0; r < d.world; ++r) {
+    d.xr_base[r] = dsum;
+    d.xr_base[WORLD_MAX + r] = psum;
+    dsum += d.xchg[2 * WORLD_MAX + r];
+    psum += d.xchg[3 * WORLD_MAX + r];
+  }
+  u32 base = align16(d.tot[15]) + 64;
+  bool fits = dsum <= d.import_max && (u64)base + psum <= d.work_cap + d.xfer_bytes;
+  u32 ni = fits ? dsum : 0;
+  if (!fits) d.ctr->n_dropped_nomem += dsum;
+  d.tot[TS_NIMPORT] = ni;
+  d.tot[TS_IMPORT_BASE] = base;
+  d.tot[TS_RANGE_LO] = d.ctr->n_pubs;
+  d.tot[TS_RANGE_HI] = d.ctr->n_pubs + ni;
+  d.tot[TS_PAIR_BASE] = d.tot[TS_PAIR_N];
+}
+
+// one wave per received record: payload -> work buffer, record -> imported Publish
+DEV void import_one(const DS& d, u32 i, u32 lane);
+__global__ __launch_bounds__(256) void k_import(DS d) {
+  u32 lane = lane_id();
+  const u32 nw = (gridDim.x * blockDim.x) >> 6;
+  const u32 n = d.tot[TS_NIMPORT];
+  for (u32 i = (blockIdx.x * blockDim.x + threadIdx.x) >> 6; i < n; i += nw) import_one(d, i, lane);
+}
+
+DEV void import_one(const DS& d, u32 i, u32 lane) {
+  u32 src = 0;
+  for (u32 r = 1; r < d.world; ++r)
+    if (d.xr_base[r] <= i) src = r;
+  const RDesc rd = d.recv_desc[i];
+  u32 roff = d.xr_base[WORLD_MAX + src] + rd.pay_off;
+  u32 len = rd.ex_len + rd.rk_len + rd.props_len + rd.body_len;
+  u32 wo = d.tot[TS_IMPORT_BASE] + roff;
+  wave_copy(d.work + wo, d.recv_pay + roff, len);
+  if (lane) return;
+  u32 pi = d.ctr->n_pubs + i;
+  Pub pb;
+  pb.conn = INVALID;
+  pb.chslot = INVALID;
+  pb.exch = rd.exch;
+  pb.ex_off = wo;
+  pb.ex_len = rd.ex_len;
+  pb.rk_off = wo + rd.ex_len;
+  pb.rk_len = rd.rk_len;
+  pb.props_off = pb.rk_off + rd.rk_len;
+  pb.props_len = rd.props_len;
+  u32 fi = d.frag_max + i;  // imported bodies live past the step's own fragments
+  d.frags[fi] = Frag{pb.props_off + rd.props_len, rd.body_len};
+  pb.frag0 = fi;
+  pb.nfrag = rd.body_len ? 1 : 0;
+  pb.body_size = rd.body_len;
+  pb.flags = rd.flags | MF_IMPORTED;
+  pb.expire_ms = rd.expire_ms;
+  pb.ts_ms = rd.ts_ms;
+  const u8* key = d.recv_pay + roff + rd.ex_len;  // read from the source: same wave wrote work
+  pb.keyhash = fnv1a64_dev(key, rd.rk_len);
+  pb.nwords = build_keyvec(d, key, rd.rk_len, pi);
+  pb.nq = 0; pb.slot_bytes = 0; pb.msg = INVALID;
+  pb.pad = src;  // source rank (pair ordering)
+  d.pubs[pi] = pb;
+}
+
 // ============================================================================ K7 enqueue
 __global__ void k_qfirst(DS d, u32 src) {
   u32 i = blockIdx.x * blockDim.x + threadIdx.x;
-  u32 n = d.tot[0];
+  u32 n = d.tot[TS_PAIR_N];
   if (i >= n) return;
   const u32* k = d.pair_k[src];
-  if (i == 0 || k[i - 1] != k[i]) d.q_first[k[i]] = i;
+  const u32 rb = d.rank_bits;
+  if (i == 0 || (k[i - 1] >> rb) != (k[i] >> rb)) d.q_first[k[i] >> rb] = i;
 }
 
 DEV u32 enqueue_one(const DS& d, u32 src, u32 i, u32 n) {
   const u32* kk = d.pair_k[src];
-  u32 q = kk[i];
+  const u32 rb = d.rank_bits;
+  u32 q = kk[i] >> rb;
   u32 p = d.pair_v[src][i];
   u32 first = d.q_first[q];
   u32 rank = i - first;
-  bool last = (i + 1 == n) || kk[i + 1] != q;
+  bool last = (i + 1 == n) || (kk[i + 1] >> rb) != q;
   const Pub& pb = d.pubs[p];
   u64 head = d.q_head[q], tail = d.q_tail[q];
   u64 cap = d.q_ring_mask[q] + 1;
@@ -1336,7 +1539,7 @@ DEV u32 enqueue_one(const DS& d, u32 src, u32 i, u32 n) {
 
 __global__ void k_enqueue(DS d, u32 src) {
   u32 i = blockIdx.x * blockDim.x + threadIdx.x;
-  u32 n = d.tot[0];
+  u32 n = d.tot[TS_PAIR_N];
   u32 drop = i < n ? enqueue_one(d, src, i, n) : INVALID;
   wave_release(d, drop, drop != INVALID);
   if (drop != INVALID) atomicAdd(&d.ctr->n_ring_full, 1u);
@@ -1882,7 +2085,6 @@ __global__ void k_final(DS d) {
   }
   if (tail > head) tail = head;
   *d.log_tail = tail;
-  *d.id_next = *d.id_next + d.tot[2];
   Counters* c = d.ctr;
   c->log_head = head;
   c->log_tail = tail;

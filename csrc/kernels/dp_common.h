@@ -41,7 +41,7 @@ enum : u32 {
 };
 
 // ---- message flags
-enum : u32 { MF_PERSIST = 1, MF_MANDATORY = 2, MF_IMMEDIATE = 4, MF_HAS_TS = 8 };
+enum : u32 { MF_PERSIST = 1, MF_MANDATORY = 2, MF_IMMEDIATE = 4, MF_HAS_TS = 8, MF_IMPORTED = 16 };
 
 // ---- unacked slot states
 enum : u32 { US_FREE = 0, US_PENDING = 1, US_ACKED = 2, US_REQUEUE = 3, US_DONE = 4 };
@@ -114,6 +114,23 @@ struct Pub {            // decoded Basic.Publish
   u32 msg;              // message-table index, -1 if not stored
   u32 pad;
 };
+
+// cross-rank publish record (sharded queues): the ingress rank ships each publish once
+// per destination rank that owns >= 1 of its queues; the owner re-routes it against its
+// replicated binding tables restricted to local queues.  Payload = [ex][rk][props][body].
+struct RDesc {
+  u32 pay_off;          // payload offset within the sender's region for this destination
+  u32 body_len;
+  u32 props_len;
+  i32 exch;             // exchange slot (identical on every rank: replicated control plane)
+  u32 flags;            // MF_* of the original publish
+  u8 ex_len, rk_len;
+  u16 pad0;
+  i64 expire_ms;
+  i64 ts_ms;
+  u32 pad[6];
+};
+static_assert(sizeof(RDesc) == 64, "RDesc layout");
 
 struct Ack { u32 chslot; u32 kind; u64 tag; u32 multiple; u32 requeue; };
 

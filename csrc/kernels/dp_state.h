@@ -9,6 +9,15 @@
 #define TOPIC_K 256           // topic key vector: 8 words x 32 hash bits (int8 +-1)
 #define TOPIC_WORDS 8
 #define LAT_BINS 32
+#define WORLD_MAX 16          // ranks of one sharded broker (one node: 8 GPUs)
+
+// tot[] scratch slots (scan totals and phase bookkeeping)
+enum : u32 {
+  TS_RANGE_LO = 20, TS_RANGE_HI = 21,   // publish index range of the current routing phase
+  TS_PAIR_BASE = 22, TS_PAIR_N = 23,    // pair base of the phase / pairs so far
+  TS_NIMPORT = 24, TS_IMPORT_BASE = 25, // imported records / their work-buffer base
+  TS_XSCAN = 32                         // + 2*r: per-destination record / byte totals
+};
 
 struct DS {
   // ---------------- sizes
@@ -160,4 +169,23 @@ struct DS {
   u32* tot;                 // scan totals [64]
   u32* egress_budget;       // bytes reserved by dequeue this step
   u64* dbg;                 // per-segment phase timestamps (s_memrealtime, 100 MHz)
+
+  // ---------------- sharding (cross-rank publish exchange; world == 1: unused)
+  u32 world, my_rank, rank_bits, pub_cap, import_max;
+  u32 xfer_desc_max;        // records per step, all destinations
+  u64 xfer_bytes;           // payload bytes per step, all destinations
+  u32* q_owner;             // [q_max] owning rank
+  u32* pub_rmask;           // [pub_cap] remote ranks owning >= 1 routed queue
+  u32* xp_cnt;              // [world][pub_cap] record for rank r?
+  u32* xp_cnt_off;
+  u32* xp_byt;              // [world][pub_cap] payload bytes for rank r
+  u32* xp_byt_off;
+  u32* xs_base;             // [2*WORLD_MAX] send record / byte bases per destination
+  u32* xr_base;             // [2*WORLD_MAX] recv record / byte bases per source
+  u32* xchg;                // host-mapped [4*WORLD_MAX+4]: send counts/bytes (out), recv counts/bytes (in), overflow
+  RDesc* send_desc;         // caller-provided (torch tensors: RCCL all-to-all operands)
+  u8* send_pay;
+  const RDesc* recv_desc;
+  const u8* recv_pay;
+  u64* id_base;             // snowflake position base of the current routing phase
 };

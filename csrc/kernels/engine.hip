@@ -53,6 +53,16 @@ class Engine {
     d_.frag_max = (u32)get("frag_max", d_.cmd_max * 2);
     d_.pub_max = d_.cmd_max;
     d_.ack_max = d_.cmd_max;
+    // sharded queues (world > 1): records imported from other ranks per step
+    d_.world = (u32)get("world", 1);
+    d_.my_rank = (u32)get("rank", 0);
+    if (d_.world < 1 || d_.world > WORLD_MAX || d_.my_rank >= d_.world)
+      throw std::runtime_error("world must be 1..16 and rank < world");
+    // Each publish is shipped at most once per other rank and its record payload never
+    // exceeds its wire bytes, so these defaults cannot overflow (records / bytes per step).
+    d_.import_max = d_.world > 1 ? (u32)get("import_max", (d_.world - 1) * d_.pub_max) : 0;
+    d_.pub_cap = ((d_.pub_max + d_.import_max + 63) / 64) * 64;
+    d_.xfer_desc_max = d_.world > 1 ? (u32)get("xfer_desc_max", (d_.world - 1) * d_.pub_max) : 0;
     d_.pair_max = (u32)get("pair_max", d_.cmd_max * 4);
     d_.deliv_max = (u32)get("deliv_max", 65536);
     d_.msg_max = (u32)get("msg_max", 1u << 22);
@@ -74,8 +84,11 @@ class Engine {
     d_.log_bytes = (d_.log_bytes / d_.log_block) * d_.log_block;
     d_.n_log_blocks = d_.log_bytes / d_.log_block;
     d_.ingress_cap = get("ingress_cap", 64ull << 20);
+    d_.xfer_bytes = d_.world > 1 ? get("xfer_bytes", (d_.world - 1) * (d_.ingress_cap + 64)) : 0;
     d_.work_cap = d_.ingress_cap + (u64)d_.seg_max * (d_.carry_cap + 64);
     d_.work_cap = d_.work_cap > (3ull << 30) ? (3ull << 30) : d_.work_cap;  // u32 offsets
+    if (d_.work_cap + d_.xfer_bytes + 8192 > (4ull << 30))
+      throw std::runtime_error("work buffer + imported bytes must stay below 4 GiB (u32 offsets): lower ingress_cap");
     d_.egress_cap = get("egress_cap", 96ull << 20);
     d_.ctrl_cap = get("ctrl_cap", 4ull << 20);
     d_.ring_pool = get("ring_pool", 1ull << 26);
@@ -83,7 +96,9 @@ class Engine {
     u32 dq_max = (u32)get("dq_max", 1u << 20);
     u64 kpool = get("kpool", 16ull << 20);
     u32 nch = d_.c_max * d_.chpc;
+    d_.rank_bits = d_.world > 1 ? bits_for(d_.world - 1) : 0;
     d_.q_bits = bits_for(d_.q_max);
+    if (d_.q_bits + d_.rank_bits > 32) throw std::runtime_error("q_max too large for sharded pair keys");
     d_.ch_bits = bits_for(nch);
     graph_enabled_ = get("graph", 1) != 0;
 
@@ -106,6 +121,7 @@ class Engine {
       io.conn_out = (ConnOut*)hst(("conn_out" + sfx).c_str(), sizeof(ConnOut) * d_.c_max);
       io.ctrl = (u8*)hst(("ctrl" + sfx).c_str(), d_.ctrl_cap);
       io.ctrl_rec = (CtrlRec*)hst(("ctrl_rec" + sfx).c_str(), sizeof(CtrlRec) * d_.seg_max * 2);
+      io.xchg = (u32*)hst(("xchg" + sfx).c_str(), 4ull * (4 * WORLD_MAX + 4));
       egress_host_[p] = (u8*)pinned(("egress_host" + sfx).c_str(), egress_alloc_);
       stage_in_[p] = (StepIn*)pinned(("stage_in" + sfx).c_str(), sizeof(StepIn));
       stage_segs_[p] = (SegIn*)pinned(("stage_segs" + sfx).c_str(), sizeof(SegIn) * d_.seg_max);
@@ -127,28 +143,38 @@ class Engine {
 
     d_.seg_start = (u32*)dev("seg_start", 4ull * d_.seg_max);
     d_.seg_total = (u32*)dev("seg_total", 4ull * d_.seg_max);
-    d_.work = (u8*)dev("work", d_.work_cap + 4096);
+    d_.work = (u8*)dev("work", d_.work_cap + 4096 + (d_.world > 1 ? d_.xfer_bytes + 128 : 0));
     d_.cmask = (u16*)dev("cmask", 2ull * ((d_.work_cap + 4096) / 16 + 1));
 
     d_.cmds = (Cmd*)dev("cmds", sizeof(Cmd) * (u64)d_.cmd_max);
-    d_.frags = (Frag*)dev("frags", sizeof(Frag) * (u64)d_.frag_max);
+    d_.frags = (Frag*)dev("frags", sizeof(Frag) * ((u64)d_.frag_max + d_.import_max));
     d_.cmd_is_pub = (u32*)dev("cmd_is_pub", 4ull * d_.cmd_max);
     d_.cmd_is_ack = (u32*)dev("cmd_is_ack", 4ull * d_.cmd_max);
     d_.cmd_pub_rank = (u32*)dev("cmd_pub_rank", 4ull * d_.cmd_max);
     d_.cmd_ack_rank = (u32*)dev("cmd_ack_rank", 4ull * d_.cmd_max);
 
-    d_.pubs = (Pub*)dev("pubs", sizeof(Pub) * (u64)d_.pub_max);
-    d_.pub_keyvec = (i8*)dev("pub_keyvec", (u64)d_.pub_max * TOPIC_K + 64);
-    d_.pub_match = (u16*)dev("pub_match", 2ull * d_.pub_max * (d_.tb_pad / 16) + 64);
-    d_.pub_nq = (u32*)dev("pub_nq", 4ull * d_.pub_max);
-    d_.pub_qc = (u32*)dev("pub_qc", 32ull * d_.pub_max);
-    d_.pub_slot = (u32*)dev("pub_slot", 4ull * d_.pub_max);
-    d_.pub_routed = (u32*)dev("pub_routed", 4ull * d_.pub_max);
-    d_.pub_pair_off = (u32*)dev("pub_pair_off", 4ull * d_.pub_max);
-    d_.pub_slot_off = (u32*)dev("pub_slot_off", 4ull * d_.pub_max);
-    d_.pub_routed_rank = (u32*)dev("pub_routed_rank", 4ull * d_.pub_max);
-    d_.pub_ret = (u32*)dev("pub_ret", 4ull * d_.pub_max);
-    d_.ret_list = (u32*)dev("ret_list", 4ull * d_.pub_max);
+    d_.pubs = (Pub*)dev("pubs", sizeof(Pub) * (u64)d_.pub_cap);
+    d_.pub_keyvec = (i8*)dev("pub_keyvec", (u64)d_.pub_cap * TOPIC_K + 64);
+    d_.pub_match = (u16*)dev("pub_match", 2ull * d_.pub_cap * (d_.tb_pad / 16) + 64);
+    d_.pub_nq = (u32*)dev("pub_nq", 4ull * d_.pub_cap);
+    d_.pub_qc = (u32*)dev("pub_qc", 32ull * d_.pub_cap);
+    d_.pub_slot = (u32*)dev("pub_slot", 4ull * d_.pub_cap);
+    d_.pub_routed = (u32*)dev("pub_routed", 4ull * d_.pub_cap);
+    d_.pub_pair_off = (u32*)dev("pub_pair_off", 4ull * d_.pub_cap);
+    d_.pub_slot_off = (u32*)dev("pub_slot_off", 4ull * d_.pub_cap);
+    d_.pub_routed_rank = (u32*)dev("pub_routed_rank", 4ull * d_.pub_cap);
+    d_.pub_ret = (u32*)dev("pub_ret", 4ull * d_.pub_cap);
+    d_.ret_list = (u32*)dev("ret_list", 4ull * d_.pub_cap);
+    u64 xw = d_.world > 1 ? (u64)d_.world * d_.pub_cap : 64;
+    d_.q_owner = (u32*)dev("q_owner", 4ull * d_.q_max);
+    d_.pub_rmask = (u32*)dev("pub_rmask", 4ull * d_.pub_cap);
+    d_.xp_cnt = (u32*)dev("xp_cnt", 4 * xw);
+    d_.xp_cnt_off = (u32*)dev("xp_cnt_off", 4 * xw);
+    d_.xp_byt = (u32*)dev("xp_byt", 4 * xw);
+    d_.xp_byt_off = (u32*)dev("xp_byt_off", 4 * xw);
+    d_.xs_base = (u32*)dev("xs_base", 8ull * WORLD_MAX);
+    d_.xr_base = (u32*)dev("xr_base", 8ull * WORLD_MAX);
+    d_.id_base = (u64*)dev("id_base", 8);
     d_.acks = (Ack*)dev("acks", sizeof(Ack) * (u64)d_.ack_max);
 
     for (int k = 0; k < 2; ++k) {
@@ -248,7 +274,7 @@ class Engine {
     d_.hist = (u32*)dev("hist", 4ull * 256 * ntiles_max_);
     d_.hist_scan = (u32*)dev("hist_scan", 4ull * 256 * ntiles_max_);
     d_.scan_tmp = (u32*)dev("scan_tmp", 4ull * 1024);
-    d_.tot = (u32*)dev("tot", 4ull * 64);
+    d_.tot = (u32*)dev("tot", 4ull * 128);
     d_.egress_budget = (u32*)dev("egress_budget", 4);
     d_.dbg = (u64*)dev("dbg", 8ull * 16 * d_.seg_max);
 
@@ -256,7 +282,7 @@ class Engine {
       DS io = d_;
       io.in = io_[p].in; io.segs = io_[p].segs; io.ingress = io_[p].ingress; io.seg_out = io_[p].seg_out;
       io.ctr_host = io_[p].ctr_host; io.egress = io_[p].egress; io.conn_out = io_[p].conn_out;
-      io.ctrl = io_[p].ctrl; io.ctrl_rec = io_[p].ctrl_rec;
+      io.ctrl = io_[p].ctrl; io.ctrl_rec = io_[p].ctrl_rec; io.xchg = io_[p].xchg;
       io_[p] = io;
     }
     HIPCHECK(hipStreamCreateWithFlags(&s_comp_, hipStreamNonBlocking));
@@ -266,6 +292,8 @@ class Engine {
       HIPCHECK(hipEventCreateWithFlags(&ev_h2d_[p], hipEventDisableTiming));
       HIPCHECK(hipEventCreateWithFlags(&ev_done_[p], hipEventDisableTiming));
       HIPCHECK(hipEventCreateWithFlags(&ev_d2h_[p], hipEventDisableTiming));
+      HIPCHECK(hipEventCreateWithFlags(&ev_a_[p], hipEventDisableTiming));
+      HIPCHECK(hipEventCreateWithFlags(&ev_ext_[p], hipEventDisableTiming));
     }
     // ---- initial state
     fill("conn_dfirst", 0xff);
@@ -280,11 +308,14 @@ class Engine {
   }
 
   ~Engine() {
-    hipStreamSynchronize(s_comp_);
-    hipStreamSynchronize(s_h2d_);
-    hipStreamSynchronize(s_d2h_);
+    (void)hipStreamSynchronize(s_comp_);
+    (void)hipStreamSynchronize(s_h2d_);
+    (void)hipStreamSynchronize(s_d2h_);
     for (int p = 0; p < 2; ++p) {
       if (graph_exec_[p]) (void)hipGraphExecDestroy(graph_exec_[p]);
+      if (graph_b_[p]) (void)hipGraphExecDestroy(graph_b_[p]);
+      (void)hipEventDestroy(ev_a_[p]);
+      (void)hipEventDestroy(ev_ext_[p]);
       (void)hipEventDestroy(ev_h2d_[p]);
       (void)hipEventDestroy(ev_done_[p]);
       (void)hipEventDestroy(ev_d2h_[p]);
@@ -382,12 +413,15 @@ class Engine {
     o["tb_max"] = d_.tb_max; o["tb_pad"] = d_.tb_pad; o["log_bytes"] = d_.log_bytes;
     o["ingress_cap"] = d_.ingress_cap; o["egress_cap"] = d_.egress_cap; o["ring_pool"] = d_.ring_pool;
     o["work_cap"] = d_.work_cap; o["total_bytes"] = total_bytes_; o["req_max"] = d_.req_max;
+    o["world"] = d_.world; o["rank"] = d_.my_rank; o["import_max"] = d_.import_max; o["pub_cap"] = d_.pub_cap;
+    o["xfer_desc_max"] = d_.xfer_desc_max; o["xfer_bytes"] = d_.xfer_bytes; o["world_max"] = WORLD_MAX;
     o["sizeof"] = py::dict(py::arg("StepIn") = sizeof(StepIn), py::arg("SegIn") = sizeof(SegIn),
                            py::arg("SegOut") = sizeof(SegOut), py::arg("Counters") = sizeof(Counters),
                            py::arg("CtrlRec") = sizeof(CtrlRec), py::arg("ConnOut") = sizeof(ConnOut),
                            py::arg("MsgEnt") = sizeof(MsgEnt), py::arg("Desc") = sizeof(Desc),
                            py::arg("USlot") = sizeof(USlot), py::arg("Deliv") = sizeof(Deliv),
-                           py::arg("Pub") = sizeof(Pub), py::arg("Cmd") = sizeof(Cmd));
+                           py::arg("Pub") = sizeof(Pub), py::arg("Cmd") = sizeof(Cmd),
+                           py::arg("RDesc") = sizeof(RDesc));
     return o;
   }
 
@@ -431,19 +465,76 @@ class Engine {
       }
       req_pending_ = false;
     }
+    if (d_.world > 1 && !xfer_set_) throw std::runtime_error("set_xfer_buffers() before the first sharded step");
     if (graph_enabled_) {
       if (!graph_exec_[p]) capture_main(p);
       HIPCHECK(hipGraphLaunch(graph_exec_[p], s_comp_));
     } else {
       launch_main(s_comp_, io_[p]);
     }
-    HIPCHECK(hipEventRecord(ev_done_[p], s_comp_));
+    if (d_.world > 1) {
+      HIPCHECK(hipEventRecord(ev_a_[p], s_comp_));
+      phase_a_[p] = true;
+    } else {
+      HIPCHECK(hipEventRecord(ev_done_[p], s_comp_));
+    }
     inflight_[p] = true;
     ++seq_;
     return p;
   }
 
+  // sharded step, after submit(): wait for phase A and return the per-destination send
+  // counts [records x world, bytes x world, overflow]
+  std::vector<u32> send_counts(int p) {
+    if (!phase_a_[p]) throw std::runtime_error("send_counts: no phase-A step in flight for this parity");
+    HIPCHECK(hipEventSynchronize(ev_a_[p]));
+    const u32* x = (const u32*)buf("xchg" + std::to_string(p)).ptr;
+    std::vector<u32> o;
+    for (u32 r = 0; r < d_.world; ++r) o.push_back(x[r]);
+    for (u32 r = 0; r < d_.world; ++r) o.push_back(x[WORLD_MAX + r]);
+    o.push_back(x[4 * WORLD_MAX]);
+    return o;
+  }
+
+  // sharded step: received [records x world, bytes x world]; the exchange ran on
+  // `stream` (0 = already complete); launches phase B behind it
+  void submit_b(int p, std::vector<u32> recv, u64 stream) {
+    if (!phase_a_[p]) throw std::runtime_error("submit_b: no phase-A step in flight for this parity");
+    if (recv.size() != 2 * d_.world) throw std::runtime_error("submit_b: need 2*world counts");
+    u32* x = (u32*)buf("xchg" + std::to_string(p)).ptr;
+    for (u32 r = 0; r < d_.world; ++r) {
+      x[2 * WORLD_MAX + r] = recv[r];
+      x[3 * WORLD_MAX + r] = recv[d_.world + r];
+    }
+    if (stream) {
+      HIPCHECK(hipEventRecord(ev_ext_[p], (hipStream_t)stream));
+      HIPCHECK(hipStreamWaitEvent(s_comp_, ev_ext_[p], 0));
+    }
+    if (graph_enabled_) {
+      if (!graph_b_[p]) capture_b(p);
+      HIPCHECK(hipGraphLaunch(graph_b_[p], s_comp_));
+    } else {
+      launch_phase_b(s_comp_, io_[p]);
+    }
+    HIPCHECK(hipEventRecord(ev_done_[p], s_comp_));
+    phase_a_[p] = false;
+  }
+
+  // caller-owned exchange operands (device pointers, e.g. torch tensors used by RCCL)
+  void set_xfer_buffers(u64 send_desc, u64 send_pay, u64 recv_desc, u64 recv_pay) {
+    d_.send_desc = (RDesc*)send_desc; d_.send_pay = (u8*)send_pay;
+    d_.recv_desc = (const RDesc*)recv_desc; d_.recv_pay = (const u8*)recv_pay;
+    for (int p = 0; p < 2; ++p) {
+      io_[p].send_desc = d_.send_desc; io_[p].send_pay = d_.send_pay;
+      io_[p].recv_desc = d_.recv_desc; io_[p].recv_pay = d_.recv_pay;
+      if (graph_exec_[p]) { HIPCHECK(hipGraphExecDestroy(graph_exec_[p])); graph_exec_[p] = nullptr; }
+      if (graph_b_[p]) { HIPCHECK(hipGraphExecDestroy(graph_b_[p])); graph_b_[p] = nullptr; }
+    }
+    xfer_set_ = true;
+  }
+
   void wait_results(int p) {
+    if (phase_a_[p]) throw std::runtime_error("wait_results: phase B of this sharded step not submitted");
     HIPCHECK(hipEventSynchronize(ev_done_[p]));
     inflight_[p] = false;
   }
@@ -484,8 +575,9 @@ class Engine {
 
  private:
   void launch_scan(hipStream_t s, std::initializer_list<std::pair<const u32*, u32*>> arrs, const u32* n,
-                   u32 nmax, u32 slot) {
+                   u32 nmax, u32 slot, const u32* lo = nullptr) {
     ScanArgs a{};
+    a.lo = lo;
     u32 k = 0;
     for (auto& p : arrs) { a.in[k] = p.first; a.out[k] = p.second; ++k; }
     a.narr = k;
@@ -509,9 +601,12 @@ class Engine {
     return src;
   }
 
-  void launch_main(hipStream_t s, const DS& d) {
-    u32 nch = d.c_max * d.chpc;
-    auto blocks = [](u64 n, u32 per) { return dim3(n ? ceil_div(n, per) : 1); };
+  static dim3 blocks(u64 n, u32 per) { return dim3(n ? ceil_div(n, per) : 1); }
+  // wave-per-item grid-stride kernels: 4 waves per block, at most 8192 blocks
+  static dim3 wave_blocks(u64 n) { u64 b = n ? ceil_div(n, 4) : 1; return dim3(b > 8192 ? 8192 : (u32)b); }
+
+  // frame scan, command assembly, decode (K1-K5)
+  void launch_ingest(hipStream_t s, const DS& d) {
     hipLaunchKernelGGL(k_prep, dim3(1), dim3(1024), 0, s, d);
     hipLaunchKernelGGL(k_stage, dim3(d.seg_max, 4), dim3(256), 0, s, d);
     hipLaunchKernelGGL(k_cand, dim3(2048), dim3(256), 0, s, d);
@@ -521,20 +616,46 @@ class Engine {
                 d.cmd_max, 4);
     hipLaunchKernelGGL(k_set_counts, dim3(1), dim3(64), 0, s, d);
     hipLaunchKernelGGL(k_decode, blocks(d.cmd_max, 256), dim3(256), 0, s, d);
+  }
+
+  // route + store the publishes of the current phase range (K6); nmax = range capacity
+  void launch_route(hipStream_t s, const DS& d, u32 nmax) {
     if (d.tb_max) {
-      u32 waves = (d.pub_max / 16) * (d.tb_pad / 16);
-      hipLaunchKernelGGL(k_topic_mfma, blocks((u64)waves * 64, 256), dim3(256), 0, s, d);
+      u64 waves = (u64)((nmax + 15) / 16) * (d.tb_pad / 16);
+      hipLaunchKernelGGL(k_topic_mfma, wave_blocks(waves), dim3(256), 0, s, d);
     }
-    hipLaunchKernelGGL(k_route<0>, blocks(d.pub_max, 256), dim3(256), 0, s, d);
+    hipLaunchKernelGGL(k_route<0>, blocks(nmax, 256), dim3(256), 0, s, d);
     launch_scan(s, {{d.pub_nq, d.pub_pair_off}, {d.pub_slot, d.pub_slot_off}, {d.pub_routed, d.pub_routed_rank}},
-                &d.ctr->n_pubs, d.pub_max, 0);
-    hipLaunchKernelGGL(k_route<1>, blocks(d.pub_max, 256), dim3(256), 0, s, d);
+                &d.tot[TS_RANGE_HI], d.pub_cap, 0, &d.tot[TS_RANGE_LO]);
+    hipLaunchKernelGGL(k_route<1>, blocks(nmax, 256), dim3(256), 0, s, d);
     hipLaunchKernelGGL(k_log_reserve, dim3(1), dim3(64), 0, s, d);
-    hipLaunchKernelGGL(k_store, blocks((u64)d.pub_max * 64, 256), dim3(256), 0, s, d);
-    hipLaunchKernelGGL(k_live_add, blocks(d.pub_max, 256), dim3(256), 0, s, d);
+    hipLaunchKernelGGL(k_store, wave_blocks(nmax), dim3(256), 0, s, d);
+    hipLaunchKernelGGL(k_live_add, blocks(nmax, 256), dim3(256), 0, s, d);
+  }
+
+  // serialise publishes with remote owners into the per-destination send buffers
+  void launch_pack(hipStream_t s, const DS& d) {
+    hipLaunchKernelGGL(k_pack_count, blocks(d.pub_max, 256), dim3(256), 0, s, d);
+    for (u32 r = 0; r < d.world; r += 2) {
+      u64 a = (u64)r * d.pub_cap, b = (u64)(r + 1) * d.pub_cap;
+      if (r + 1 < d.world)
+        launch_scan(s, {{d.xp_cnt + a, d.xp_cnt_off + a}, {d.xp_byt + a, d.xp_byt_off + a},
+                        {d.xp_cnt + b, d.xp_cnt_off + b}, {d.xp_byt + b, d.xp_byt_off + b}},
+                    &d.ctr->n_pubs, d.pub_max, TS_XSCAN + 2 * r);
+      else
+        launch_scan(s, {{d.xp_cnt + a, d.xp_cnt_off + a}, {d.xp_byt + a, d.xp_byt_off + a}}, &d.ctr->n_pubs,
+                    d.pub_max, TS_XSCAN + 2 * r);
+    }
+    hipLaunchKernelGGL(k_pack_bases, dim3(1), dim3(64), 0, s, d);
+    hipLaunchKernelGGL(k_pack, blocks((u64)d.pub_max * 64, 256), dim3(256), 0, s, d);
+  }
+
+  // enqueue, acks, dispatch, render (K7-K11)
+  void launch_tail(hipStream_t s, const DS& d) {
+    u32 nch = d.c_max * d.chpc;
     u32* pk[2] = {d.pair_k[0], d.pair_k[1]};
     u32* pv[2] = {d.pair_v[0], d.pair_v[1]};
-    u32 psrc = radix_sort(s, pk, pv, &d.tot[0], d.pair_max, d.q_bits);
+    u32 psrc = radix_sort(s, pk, pv, &d.tot[TS_PAIR_N], d.pair_max, d.q_bits + d.rank_bits);
     hipLaunchKernelGGL(k_qfirst, blocks(d.pair_max, 256), dim3(256), 0, s, d, psrc);
     hipLaunchKernelGGL(k_enqueue, blocks(d.pair_max, 256), dim3(256), 0, s, d, psrc);
     hipLaunchKernelGGL(k_acks, blocks(d.ack_max, 256), dim3(256), 0, s, d);
@@ -559,6 +680,22 @@ class Engine {
     hipLaunchKernelGGL(k_final, dim3(1), dim3(64), 0, s, d);
   }
 
+  // world == 1: the whole step; world > 1: phase A (ingest, local route, pack)
+  void launch_main(hipStream_t s, const DS& d) {
+    launch_ingest(s, d);
+    launch_route(s, d, d.pub_max);
+    if (d.world > 1) launch_pack(s, d);
+    else launch_tail(s, d);
+  }
+
+  // world > 1, after the all-to-all: import, route against local queues, rest of the step
+  void launch_phase_b(hipStream_t s, const DS& d) {
+    hipLaunchKernelGGL(k_import_prep, dim3(1), dim3(64), 0, s, d);
+    hipLaunchKernelGGL(k_import, wave_blocks(d.import_max), dim3(256), 0, s, d);
+    launch_route(s, d, d.import_max);
+    launch_tail(s, d);
+  }
+
   void launch_requeue(hipStream_t s) {  // state-only kernels: IO pointers unused
     hipLaunchKernelGGL(k_requeue, dim3(d_.q_max), dim3(256), 0, s, d_);
     hipLaunchKernelGGL(k_requeue_compact, dim3(1), dim3(1024), 0, s, d_);
@@ -570,6 +707,15 @@ class Engine {
     launch_main(s_comp_, io_[p]);
     HIPCHECK(hipStreamEndCapture(s_comp_, &g));
     HIPCHECK(hipGraphInstantiate(&graph_exec_[p], g, nullptr, nullptr, 0));
+    HIPCHECK(hipGraphDestroy(g));
+  }
+
+  void capture_b(int p) {
+    hipGraph_t g;
+    HIPCHECK(hipStreamBeginCapture(s_comp_, hipStreamCaptureModeThreadLocal));
+    launch_phase_b(s_comp_, io_[p]);
+    HIPCHECK(hipStreamEndCapture(s_comp_, &g));
+    HIPCHECK(hipGraphInstantiate(&graph_b_[p], g, nullptr, nullptr, 0));
     HIPCHECK(hipGraphDestroy(g));
   }
 
@@ -591,6 +737,10 @@ class Engine {
   bool graph_enabled_ = true;
   hipGraphExec_t graph_exec_[2] = {nullptr, nullptr};
   hipGraphExec_t req_exec_ = nullptr;
+  hipGraphExec_t graph_b_[2] = {nullptr, nullptr};
+  hipEvent_t ev_a_[2], ev_ext_[2];
+  bool phase_a_[2] = {false, false};
+  bool xfer_set_ = false;
   DS io_[2];
   u8* egress_host_[2] = {nullptr, nullptr};
   StepIn* stage_in_[2] = {nullptr, nullptr};
@@ -607,7 +757,7 @@ static py::array alloc_pinned(size_t bytes) {
   void* p = nullptr;
   HIPCHECK(hipHostMalloc(&p, bytes, hipHostMallocPortable));
   return py::array(py::dtype("uint8"), {(py::ssize_t)bytes}, {(py::ssize_t)1}, p,
-                   py::capsule(p, [](void* q) { hipHostFree(q); }));
+                   py::capsule(p, [](void* q) { (void)hipHostFree(q); }));
 }
 
 static u64 create_stream(int device) {
@@ -640,6 +790,9 @@ PYBIND11_MODULE(_dataplane, m) {
       .def("download", &Engine::download, py::arg("name"), py::arg("offset") = 0, py::arg("n") = 0)
       .def("host_view", &Engine::host_view)
       .def("submit", &Engine::submit)
+      .def("send_counts", &Engine::send_counts)
+      .def("submit_b", &Engine::submit_b, py::arg("parity"), py::arg("recv"), py::arg("stream") = 0)
+      .def("set_xfer_buffers", &Engine::set_xfer_buffers)
       .def("wait_results", &Engine::wait_results)
       .def("egress_copy", &Engine::egress_copy)
       .def("egress_wait", &Engine::egress_wait)
