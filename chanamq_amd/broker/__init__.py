@@ -16,11 +16,21 @@ SOURCES = ["codec.cpp", "store.cpp", "broker.cpp", "loadgen.cpp", "bindings.cpp"
 HEADERS = ["codec.hpp", "store.hpp", "broker.hpp", "loadgen.hpp"]
 
 
+def _src_hash():
+    import hashlib
+    h = hashlib.sha256()
+    for s in SOURCES + HEADERS:
+        with open(os.path.join(_SRC, s), "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()
+
+
 def _stale():
-    if not os.path.exists(EXT_PATH):
+    """Content-based (mtimes do not survive copies to the GPU box)."""
+    if not os.path.exists(EXT_PATH) or not os.path.exists(EXT_PATH + ".srchash"):
         return True
-    t = os.path.getmtime(EXT_PATH)
-    return any(os.path.getmtime(os.path.join(_SRC, s)) > t for s in SOURCES + HEADERS)
+    with open(EXT_PATH + ".srchash") as f:
+        return f.read().strip() != _src_hash()
 
 
 def build(force=False, verbose=False, sanitize=None):
@@ -41,10 +51,15 @@ def build(force=False, verbose=False, sanitize=None):
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)
     os.replace(out + ".tmp", out)
+    if not sanitize:
+        with open(out + ".srchash", "w") as f:
+            f.write(_src_hash())
     return out
 
 
 def load():
+    if _stale():
+        build()
     try:
         return importlib.import_module("chanamq_amd.broker._core")
     except ImportError as e:

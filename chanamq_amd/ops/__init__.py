@@ -20,11 +20,21 @@ EXT_PATH = os.path.join(_HERE, "_dataplane" + _EXT)
 SOURCES = ["engine.hip", "dataplane.hip", "dp_state.h", "dp_common.h"]
 
 
+def _src_hash():
+    import hashlib
+    h = hashlib.sha256()
+    for s in SOURCES:
+        with open(os.path.join(_SRC, s), "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()
+
+
 def _stale():
-    if not os.path.exists(EXT_PATH):
+    """Content-based (mtimes do not survive copies to the GPU box)."""
+    if not os.path.exists(EXT_PATH) or not os.path.exists(EXT_PATH + ".srchash"):
         return True
-    t = os.path.getmtime(EXT_PATH)
-    return any(os.path.getmtime(os.path.join(_SRC, s)) > t for s in SOURCES)
+    with open(EXT_PATH + ".srchash") as f:
+        return f.read().strip() != _src_hash()
 
 
 def build(force=False, verbose=False):
@@ -41,11 +51,16 @@ def build(force=False, verbose=False):
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)
     os.replace(EXT_PATH + ".tmp", EXT_PATH)
+    with open(EXT_PATH + ".srchash", "w") as f:
+        f.write(_src_hash())
     return EXT_PATH
 
 
 def load():
-    """Import the compiled extension (raises ImportError with a build hint)."""
+    """Import the compiled extension, rebuilding it first if the sources changed
+    (raises ImportError with a build hint if it cannot be built)."""
+    if _stale():
+        build()
     try:
         return importlib.import_module("chanamq_amd.ops._dataplane")
     except ImportError as e:
