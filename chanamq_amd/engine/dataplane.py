@@ -55,7 +55,6 @@ class GpuDataPlane(ControlState):
                          ctrl=self.eng.host_view(f"ctrl{p}"),
                          egress=self.eng.host_view(f"egress_host{p}")) for p in (0, 1)]
         self._pin = [None, None]
-        self.requeue_pending = False
         self.exchanger = exchanger
         self._pending = None
         if world > 1:
@@ -287,6 +286,44 @@ class GpuDataPlane(ControlState):
         if flat:
             self._up("q_cons", np.array(flat, np.uint32))
 
+    # ---- host-side queue/channel ops between steps (the plane is idle: step() is synchronous)
+    def _u64(self, name, idx):
+        return int(np.frombuffer(self.eng.download(name, idx * 8, 8), np.uint64)[0])
+
+    def message_count(self, q):
+        """Ready messages of queue slot ``q`` (AMQP Queue.DeclareOk message-count)."""
+        return self._u64("q_tail", q) - self._u64("q_head", q)
+
+    def purge(self, q):
+        """Queue.Purge: mark every ready entry expired; the next step's dequeue (K12 TTL
+        skip) releases them and their body-log bytes.  Returns the purged count."""
+        head, tail = self._u64("q_head", q), self._u64("q_tail", q)
+        n = tail - head
+        if n <= 0:
+            return 0
+        qq = self.queue_by_slot[q]
+        mask = qq.capacity - 1
+        base = qq.ring_off * 16
+        for lo in range(head, tail, mask + 1):
+            k = min(tail - lo, mask + 1)
+            i0 = lo & mask
+            first = min(k, mask + 1 - i0)
+            for start, cnt in ((i0, first), (0, k - first)):
+                if cnt <= 0:
+                    continue
+                raw = np.frombuffer(self.eng.download("ring", base + start * 16, cnt * 16), np.uint8).copy()
+                ent = raw.view(np.int64).reshape(cnt, 2)
+                ent[:, 1] = 1   # expire_ms = 1 ms after the epoch
+                self.eng.upload("ring", raw, base + start * 16)
+        return n
+
+    def recover(self, conn, ch):
+        """Basic.Recover(requeue): requeue every outstanding delivery of the channel."""
+        s = self.chslot(conn, ch)
+        upto = max(self._u64("ch_req_upto", s), self._u64("ch_next_tag", s) - 1)
+        self._up_at("ch_req_upto", upto, s, np.uint64)
+        self._mark_dirty(s)
+
     def unpause(self, conn):
         c = self.conns.get(conn)
         if c is not None:
@@ -387,8 +424,6 @@ class GpuDataPlane(ControlState):
                 cc = self.conns.get(int(conn))
                 if cc is not None:
                     cc.paused = True
-        if c["n_requeue"]:
-            self.eng.request_requeue()
         self.eng.egress_copy(p)
         if collect:
             res.segs = [tuple(int(x) for x in (r["conn"], r["status"], r["consumed"], r["carry"],

@@ -78,6 +78,20 @@ class GoldenDataPlane(ControlState):
         self.qpos_head[q.slot] = 0
         self.qrr[q.slot] = 0
 
+    def message_count(self, q):
+        return len(self.ring[q])
+
+    def purge(self, q):
+        ring = self.ring[q]
+        self.ring[q] = [(m, red, 1) for (m, red, _) in ring]   # released by the next dequeue
+        return len(ring)
+
+    def recover(self, conn, ch):
+        s = self.chslot(conn, ch)
+        st = self.ch[s]
+        st["req_upto"] = max(st["req_upto"], st["next_tag"] - 1)
+        self._mark_dirty(s)
+
     def unpause(self, conn):
         c = self.conns.get(conn)
         if c is not None:
@@ -306,21 +320,6 @@ class GoldenDataPlane(ControlState):
         self.counters = defaultdict(int)
         cnt = self.counters
         out = {"egress": {}, "ctrl": [], "events": [], "segs": []}
-        # pre-step requeue (k_requeue): per queue, sorted by queue position
-        if self.requeue_items:
-            byq = defaultdict(list)
-            for it in self.requeue_items:
-                byq[it[0]].append(it)
-            self.requeue_items = []
-            for q, items in byq.items():
-                items.sort(key=lambda x: x[2])
-                ring = self.ring[q]
-                cap = self.queue_by_slot[q].capacity if q in self.queue_by_slot else 0
-                free = cap - len(ring)
-                k = min(len(items), free)
-                self.ring[q] = [(m, True, e) for (_, m, _, e) in items[:k]] + ring
-                self.qpos_head[q] -= k
-                self.requeue_items.extend(items[k:])
         conns = set(inputs)
         for c, cl in self.carry.items():
             if cl and c in self.conns and not self.conns[c].paused:
@@ -419,6 +418,22 @@ class GoldenDataPlane(ControlState):
                 st["slots"].pop(k, None)
             st["uhead"] += released
             st["win"] -= released
+        # requeue (k_requeue): back in front of the heads, per queue in queue-position order,
+        # before this step's dispatch
+        if self.requeue_items:
+            byq = defaultdict(list)
+            for it in self.requeue_items:
+                byq[it[0]].append(it)
+            self.requeue_items = []
+            for q, items in byq.items():
+                items.sort(key=lambda x: x[2])
+                ring = self.ring[q]
+                cap = self.queue_by_slot[q].capacity if q in self.queue_by_slot else 0
+                free = cap - len(ring)
+                k = min(len(items), free)
+                self.ring[q] = [(m, True, e) for (_, m, _, e) in items[:k]] + ring
+                self.qpos_head[q] -= k
+                self.requeue_items.extend(items[k:])
         # ---- dequeue (k_dequeue)
         delivs = []
         budget = [0]

@@ -4,6 +4,8 @@
   --set key=value      override one key (repeatable)
   --stats-interval S   log the "published msgs" / "delivered msgs" counters every S seconds
                        (the lines chana-mq-test/perf/sum-published.sh scrapes)
+  --data-plane host|gpu  host = native C++ broker (CPU data path, store, TLS);
+                       gpu = the HIP data plane on --device behind server/gpu_broker.py
 """
 
 import argparse
@@ -24,12 +26,16 @@ def main(argv=None):
     ap.add_argument("--set", action="append", default=[], metavar="KEY=VALUE")
     ap.add_argument("--stats-interval", type=float, default=10.0)
     ap.add_argument("--log-level", default="INFO")
+    ap.add_argument("--data-plane", choices=["host", "gpu"], default="host")
+    ap.add_argument("--device", type=int, default=0)
     args = ap.parse_args(argv)
     logging.basicConfig(level=args.log_level, format="%(asctime)s:%(levelname)s %(threadName)s - %(message)s")
     log = logging.getLogger("chanamq")
     overrides = dict(kv.split("=", 1) for kv in args.set)
     cfg = Config.load(args.config, overrides)
     bc = cfg.broker_config()
+    if args.data_plane == "gpu":
+        return _main_gpu(args, bc, log)
     core = load()
     broker = core.Broker(bc)
     broker.start()
@@ -47,6 +53,26 @@ def main(argv=None):
         log.info("server delivered msgs: %d", s["delivered"] - last.get("delivered", 0))
         last = s
     admin.stop()
+    broker.stop()
+    return 0
+
+
+def _main_gpu(args, bc, log):
+    from ..engine.dataplane import GpuDataPlane
+    from .gpu_broker import GpuBroker
+    plane = GpuDataPlane(device=args.device, hash_wildcard=bc["hash_wildcard"], frame_max=bc["frame_max"])
+    broker = GpuBroker(plane, host=bc["host"], port=bc["port"], heartbeat=bc["heartbeat"],
+                       frame_max=bc["frame_max"], channel_max=bc["channel_max"] or 2047).start()
+    log.info("AMQP (GPU data plane, device %d) listening on %s:%s", args.device, bc["host"], broker.port)
+    stop = threading.Event()
+    for sig in (signal.SIGINT, signal.SIGTERM):
+        signal.signal(sig, lambda *a: stop.set())
+    last = {}
+    while not stop.wait(args.stats_interval):
+        s = dict(broker.stats)
+        log.info("server published msgs: %d", s["published"] - last.get("published", 0))
+        log.info("server delivered msgs: %d", s["delivered"] - last.get("delivered", 0))
+        last = s
     broker.stop()
     return 0
 

@@ -1,0 +1,541 @@
+"""AMQP 0-9-1 server whose data path is the GPU data plane.
+
+Sockets, the connection handshake and control methods are handled on the host; once a
+connection is open every byte it sends goes into the next data-plane step, which scans
+frames, routes/stores/enqueues publishes, processes acks, dispatches deliveries and
+renders the egress bytes (csrc/kernels/dataplane.hip).  The device pauses a connection
+at its first control command and hands the raw command back; this module executes it
+against ``ControlState`` (which pushes the changed tables to the device), writes the
+reply, and unpauses the connection, so per-connection ordering is exactly the wire order
+(the reference's FrameStage does the same per connection: chana-mq-server/src/main/
+scala/chana/mq/amqp/server/engine/FrameStage.scala:319-500).
+
+The plane can be a ``GpuDataPlane`` (HIP) or a ``GoldenDataPlane`` (CPU executable
+spec, used by the CPU tests of this server).
+
+Not on the GPU path yet (answered with 540 NOT_IMPLEMENTED; the host-path broker in
+csrc/core serves them): Basic.Get, Tx.*, Exchange.Bind/Unbind.
+"""
+
+import os
+import selectors
+import socket
+import struct
+import threading
+import time
+import uuid
+
+from ..engine.control import ControlError, normalize_vhost
+from ..engine.layout import SS_FRAME_ERROR, SS_OVERFLOW, SS_TOO_LARGE, SS_UNEXPECTED
+from ..protocol import constants as C
+from ..protocol.codec import Method, decode_method, encode_method_frame, encode_table
+
+HEARTBEAT = C.HEARTBEAT_FRAME
+
+
+class _Conn:
+    __slots__ = ("sock", "id", "state", "inbuf", "out", "frame_max", "heartbeat", "last_rx", "last_tx",
+                 "closing_channels", "last_queue", "peer", "user")
+
+    def __init__(self, sock, cid, peer):
+        self.sock, self.id, self.peer = sock, cid, peer
+        self.state = "header"   # header -> start -> tune -> open -> closing -> closed
+        self.inbuf = bytearray()
+        self.out = bytearray()
+        self.frame_max = 131072
+        self.heartbeat = 0
+        self.last_rx = self.last_tx = time.monotonic()
+        self.closing_channels = set()
+        self.last_queue = {}    # channel -> last declared queue name (AMQP empty-name rule)
+        self.user = ""
+
+
+class _Hard(Exception):
+    """Connection-level error: Connection.Close(code, text, class, method)."""
+
+    def __init__(self, code, text, cls=0, mid=0):
+        super().__init__(text)
+        self.code, self.text, self.cls, self.mid = code, text, cls, mid
+
+
+def _frames(buf):
+    """Complete frames at the front of ``buf`` -> [(type, channel, payload)], consumed."""
+    out, pos = [], 0
+    while len(buf) - pos >= 7:
+        t, ch, size = struct.unpack_from(">BHI", buf, pos)
+        if len(buf) - pos < 8 + size:
+            break
+        if buf[pos + 7 + size] != C.FRAME_END:
+            raise _Hard(C.FRAME_ERROR, "bad frame end")
+        out.append((t, ch, bytes(buf[pos + 7:pos + 7 + size])))
+        pos += 8 + size
+    return out, pos
+
+
+class GpuBroker:
+    def __init__(self, plane, host="127.0.0.1", port=0, heartbeat=0, frame_max=131072, channel_max=2047,
+                 idle_step_ms=2.0, product="chanamq-amd", version="0.1.0"):
+        self.plane = plane
+        self.host, self.port = host, port
+        self.heartbeat, self.frame_max, self.channel_max = heartbeat, frame_max, channel_max
+        self.idle_step_s = idle_step_ms / 1000.0
+        self.product, self.version = product, version
+        self.conns = {}
+        self._free = list(range(plane.c_max - 1, 0, -1))   # slot 0 unused
+        self._sel = selectors.DefaultSelector()
+        self._lsock = None
+        self._thread = None
+        self._running = False
+        self._wake_r, self._wake_w = os.pipe()
+        self.stats = dict(steps=0, published=0, delivered=0, connections=0)
+        self.lock = threading.RLock()
+
+    # ------------------------------------------------------------------ lifecycle
+    def start(self):
+        ls = socket.socket(socket.AF_INET, socket.SOCK_STREAM)
+        ls.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
+        ls.bind((self.host, self.port))
+        ls.listen(1024)
+        ls.setblocking(False)
+        self.port = ls.getsockname()[1]
+        self._lsock = ls
+        self._sel.register(ls, selectors.EVENT_READ, "listen")
+        self._sel.register(self._wake_r, selectors.EVENT_READ, "wake")
+        self._running = True
+        self._thread = threading.Thread(target=self._loop, name="gpu-broker", daemon=True)
+        self._thread.start()
+        return self
+
+    def stop(self):
+        self._running = False
+        os.write(self._wake_w, b"x")
+        if self._thread:
+            self._thread.join(timeout=10)
+        for c in list(self.conns.values()):
+            self._drop(c)
+        self._sel.close()
+        self._lsock.close()
+        os.close(self._wake_r)
+        os.close(self._wake_w)
+
+    # ------------------------------------------------------------------ loop
+    def _loop(self):
+        last_step = 0.0
+        busy = False
+        while self._running:
+            timeout = 0 if busy else self.idle_step_s
+            inputs = {}
+            for key, _ in self._sel.select(timeout):
+                if key.data == "listen":
+                    self._accept()
+                elif key.data == "wake":
+                    os.read(self._wake_r, 64)
+                else:
+                    self._read(key.data, inputs)
+            now = time.monotonic()
+            open_conns = any(c.state == "open" for c in self.conns.values())
+            if open_conns and (inputs or busy or now - last_step >= self.idle_step_s):
+                with self.lock:
+                    busy = self._step(inputs)
+                last_step = now
+            else:
+                busy = False
+            self._heartbeats(now)
+            self._flush_all()
+
+    def _accept(self):
+        try:
+            s, peer = self._lsock.accept()
+        except BlockingIOError:
+            return
+        if not self._free:
+            s.close()
+            return
+        s.setblocking(False)
+        s.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
+        c = _Conn(s, self._free.pop(), peer)
+        self.conns[c.id] = c
+        self._sel.register(s, selectors.EVENT_READ, c)
+        self.stats["connections"] += 1
+
+    def _read(self, c, inputs):
+        try:
+            data = c.sock.recv(1 << 18)
+        except (BlockingIOError, InterruptedError):
+            return
+        except OSError:
+            data = b""
+        if not data:
+            self._drop(c)
+            return
+        c.last_rx = time.monotonic()
+        if c.state == "open":
+            inputs[c.id] = inputs.get(c.id, b"") + data
+        elif c.state in ("header", "start", "tune"):
+            c.inbuf += data
+            try:
+                rest = self._handshake(c)
+            except _Hard as e:
+                self._conn_close(c, e.code, e.text, e.cls, e.mid)
+                return
+            except ControlError as e:
+                self._conn_close(c, e.code, e.text, e.class_id, e.method_id)
+                return
+            if rest:
+                inputs[c.id] = rest
+        elif c.state == "closing":
+            c.inbuf += data
+            frames, used = _frames(c.inbuf)
+            del c.inbuf[:used]
+            for t, ch, payload in frames:
+                if t == C.FRAME_METHOD and ch == 0:
+                    m = decode_method(payload)
+                    if m.name in ("connection.close_ok", "connection.close"):
+                        if m.name == "connection.close":
+                            self._send(c, 0, Method("connection.close_ok"))
+                        self._flush(c)
+                        self._drop(c)
+                        return
+
+    # ------------------------------------------------------------------ handshake (host)
+    def _handshake(self, c):
+        if c.state == "header":
+            if len(c.inbuf) < 8:
+                return b""
+            if bytes(c.inbuf[:8]) != C.PROTOCOL_HEADER:
+                c.out += C.PROTOCOL_HEADER
+                self._flush(c)
+                self._drop(c)
+                return b""
+            del c.inbuf[:8]
+            caps = {"publisher_confirms": True, "exchange_exchange_bindings": False, "basic.nack": True,
+                    "consumer_cancel_notify": True, "connection.blocked": False}
+            self._send(c, 0, Method("connection.start", version_major=0, version_minor=9,
+                                    server_properties={"product": self.product, "version": self.version,
+                                                       "capabilities": caps},
+                                    mechanisms=b"PLAIN AMQPLAIN EXTERNAL", locales=b"en_US"))
+            c.state = "start"
+        frames, used = _frames(c.inbuf)
+        consumed = 0
+        for k, (t, ch, payload) in enumerate(frames):
+            if t == C.FRAME_HEARTBEAT:
+                continue
+            if t != C.FRAME_METHOD or ch != 0:
+                raise _Hard(C.UNEXPECTED_FRAME, "unexpected frame during handshake")
+            m = decode_method(payload)
+            if m.name == "connection.start_ok" and c.state == "start":
+                mech = m.mechanism
+                if mech not in ("PLAIN", "AMQPLAIN", "EXTERNAL"):
+                    raise _Hard(C.ACCESS_REFUSED, f"unsupported SASL mechanism {mech}", 10, 11)
+                if mech == "PLAIN":
+                    parts = bytes(m.response).split(b"\0")
+                    c.user = parts[1].decode("utf-8", "replace") if len(parts) > 1 else ""
+                self._send(c, 0, Method("connection.tune", channel_max=self.channel_max,
+                                        frame_max=self.frame_max, heartbeat=self.heartbeat))
+                c.state = "tune"
+            elif m.name == "connection.tune_ok" and c.state == "tune":
+                fm = m.frame_max or self.frame_max
+                if fm > self.frame_max or fm < 4096:
+                    raise _Hard(C.SYNTAX_ERROR, f"frame-max {fm} outside negotiated range", 10, 31)
+                c.frame_max = fm
+                c.heartbeat = m.heartbeat
+            elif m.name == "connection.open" and c.state == "tune":
+                vh = normalize_vhost(m.virtual_host)
+                if vh not in self.plane.vhosts:
+                    raise _Hard(C.NOT_FOUND, f"no vhost '{vh}'", 10, 40)
+                with self.lock:
+                    self.plane.open_connection(c.id, vh, c.frame_max)
+                self._send(c, 0, Method("connection.open_ok"))
+                c.state = "open"
+                # bytes after Connection.Open belong to the data plane
+                rest = bytes(c.inbuf[self._frame_end(c.inbuf, k)[0]:])
+                c.inbuf.clear()
+                return rest
+            else:
+                raise _Hard(C.COMMAND_INVALID, f"unexpected {m.name} during handshake", m.class_id, m.method_id)
+            consumed = used
+        del c.inbuf[:used]
+        return b""
+
+    @staticmethod
+    def _frame_end(buf, k):
+        pos = 0
+        for _ in range(k + 1):
+            size = struct.unpack_from(">I", buf, pos + 3)[0]
+            pos += 8 + size
+        return pos, None
+
+    # ------------------------------------------------------------------ data-plane step
+    def _step(self, inputs):
+        res = self.plane.step(inputs, now_ms=int(time.time() * 1000))
+        if isinstance(res, dict):   # golden plane
+            egress, ctrl, events, segs, cnt = res["egress"], res["ctrl"], res["events"], res["segs"], \
+                res.get("counters", {})
+            seg_status = [(s[0], s[1]) for s in segs]
+        else:
+            egress, ctrl, events, cnt = res.egress, res.ctrl, res.events, res.counters
+            seg_status = [(s[0], s[1]) for s in res.segs]
+        self.stats["steps"] += 1
+        self.stats["published"] += cnt.get("n_pubs", 0)
+        self.stats["delivered"] += cnt.get("n_deliv", 0)
+        for conn, data in egress.items():
+            c = self.conns.get(conn)
+            if c is not None and c.state == "open":
+                c.out += data
+        for conn, code, chslot in events:
+            c = self.conns.get(conn)
+            if c is None or c.state != "open":
+                continue
+            ch = self._chan_of_slot(conn, chslot)
+            if code == 404 and ch is not None:
+                self._chan_close(c, ch, C.NOT_FOUND, "no exchange", 60, 40)
+        for conn, status in seg_status:
+            c = self.conns.get(conn)
+            if c is None or c.state != "open":
+                continue
+            if status & SS_FRAME_ERROR:
+                self._conn_close(c, C.FRAME_ERROR, "malformed frame")
+            elif status & SS_UNEXPECTED:
+                self._conn_close(c, C.UNEXPECTED_FRAME, "unexpected frame")
+            elif status & (SS_TOO_LARGE | SS_OVERFLOW):
+                self._conn_close(c, C.FRAME_ERROR, "command exceeds the server's limits")
+        for conn, raw in ctrl:
+            c = self.conns.get(conn)
+            if c is None:
+                continue
+            if c.state == "open":
+                try:
+                    self._control(c, raw)
+                except _Hard as e:
+                    self._conn_close(c, e.code, e.text, e.cls, e.mid)
+            if c.state == "open":
+                self.plane.unpause(conn)
+        return bool(inputs) or bool(egress) or bool(ctrl) or cnt.get("n_deliv", 0) > 0
+
+    def _chan_of_slot(self, conn, chslot):
+        cc = self.plane.conns.get(conn)
+        if cc is None:
+            return None
+        for ch, chan in cc.channels.items():
+            if conn * self.plane.chpc + chan.local == chslot:
+                return ch
+        return None
+
+    # ------------------------------------------------------------------ control methods
+    def _control(self, c, raw):
+        t, ch, size = struct.unpack_from(">BHI", raw, 0)
+        if t != C.FRAME_METHOD:
+            raise _Hard(C.UNEXPECTED_FRAME, "content frame without a method")
+        m = decode_method(raw[7:7 + size])
+        if ch in c.closing_channels:
+            if m.name == "channel.close_ok":
+                c.closing_channels.discard(ch)
+            elif m.name == "channel.close":
+                self._send(c, ch, Method("channel.close_ok"))
+            return
+        if ch == 0:
+            return self._connection_method(c, m)
+        p = self.plane
+        chans = p.conns[c.id].channels
+        if m.name == "channel.open":
+            if ch in chans:
+                raise _Hard(C.CHANNEL_ERROR, f"channel {ch} already open", 20, 10)
+            if ch > self.channel_max:
+                raise _Hard(C.CHANNEL_ERROR, f"channel {ch} above channel-max", 20, 10)
+            try:
+                p.open_channel(c.id, ch)
+            except ControlError as e:
+                raise _Hard(e.code, e.text, 20, 10)
+            return self._send(c, ch, Method("channel.open_ok"))
+        if ch not in chans:
+            raise _Hard(C.CHANNEL_ERROR, f"channel {ch} is not open", m.class_id, m.method_id)
+        try:
+            self._channel_method(c, ch, m)
+        except ControlError as e:
+            if e.code >= 500 or e.code in (C.CONNECTION_FORCED, C.INVALID_PATH):
+                raise _Hard(e.code, e.text, e.class_id or m.class_id, e.method_id or m.method_id)
+            self._chan_close(c, ch, e.code, e.text, m.class_id, m.method_id)
+
+    def _connection_method(self, c, m):
+        if m.name == "connection.close":
+            self._send(c, 0, Method("connection.close_ok"))
+            self._flush(c)
+            self._drop(c)
+        elif m.name == "connection.close_ok":
+            self._drop(c)
+        else:
+            raise _Hard(C.COMMAND_INVALID, f"unexpected {m.name}", m.class_id, m.method_id)
+
+    def _channel_method(self, c, ch, m):
+        p = self.plane
+        vh = p.conns[c.id].vhost
+        n = m.name
+        if n == "channel.close":
+            p.close_channel(c.id, ch)
+            self._send(c, ch, Method("channel.close_ok"))
+        elif n == "channel.close_ok":
+            pass
+        elif n == "channel.flow":
+            p.flow(c.id, ch, m.active)
+            self._send(c, ch, Method("channel.flow_ok", active=m.active))
+        elif n == "channel.flow_ok":
+            pass
+        elif n == "access.request":
+            self._send(c, ch, Method("access.request_ok", ticket=1))
+        elif n == "exchange.declare":
+            if m.exchange.startswith("amq.") and not m.passive and (vh, m.exchange) not in p.exchanges:
+                raise ControlError(C.ACCESS_REFUSED, f"exchange name '{m.exchange}' is reserved", 40, 10)
+            x = p.exchanges.get((vh, m.exchange))
+            if x is not None and not m.passive and x.type != m.type:
+                raise ControlError(C.PRECONDITION_FAILED, f"exchange '{m.exchange}' declared as {x.type}", 40, 10)
+            p.declare_exchange(vh, m.exchange, m.type or "direct", durable=m.durable, auto_delete=m.auto_delete,
+                               internal=m.internal, arguments=m.arguments, passive=m.passive)
+            if not m.nowait:
+                self._send(c, ch, Method("exchange.declare_ok"))
+        elif n == "exchange.delete":
+            p.delete_exchange(vh, m.exchange, if_unused=m.if_unused)
+            if not m.nowait:
+                self._send(c, ch, Method("exchange.delete_ok"))
+        elif n == "queue.declare":
+            name = m.queue or ("tmp." + uuid.uuid4().hex)
+            args = m.arguments or {}
+            ttl = int(args.get("x-message-ttl", 0) or 0)
+            q = p.queues.get((vh, name))
+            if q is not None and q.exclusive_owner not in (-1, c.id):
+                raise ControlError(C.RESOURCE_LOCKED, f"queue '{name}' is exclusive to another connection", 50, 10)
+            slot = p.declare_queue(vh, name, durable=m.durable, exclusive_owner=c.id if m.exclusive else -1,
+                                   auto_delete=m.auto_delete, ttl_ms=ttl, passive=m.passive)
+            c.last_queue[ch] = name
+            if not m.nowait:
+                qq = p.queue_by_slot[slot]
+                self._send(c, ch, Method("queue.declare_ok", queue=name, message_count=p.message_count(slot),
+                                         consumer_count=len(qq.consumers)))
+        elif n == "queue.bind":
+            qn = m.queue or c.last_queue.get(ch, "")
+            p.bind(vh, qn, m.exchange, m.routing_key)
+            if not m.nowait:
+                self._send(c, ch, Method("queue.bind_ok"))
+        elif n == "queue.unbind":
+            qn = m.queue or c.last_queue.get(ch, "")
+            p.unbind(vh, qn, m.exchange, m.routing_key)
+            self._send(c, ch, Method("queue.unbind_ok"))
+        elif n == "queue.purge":
+            q = self._queue(vh, m.queue or c.last_queue.get(ch, ""), 50, 30)
+            cnt = p.purge(q.slot)
+            if not m.nowait:
+                self._send(c, ch, Method("queue.purge_ok", message_count=cnt))
+        elif n == "queue.delete":
+            q = self._queue(vh, m.queue or c.last_queue.get(ch, ""), 50, 40)
+            if m.if_unused and q.consumers:
+                raise ControlError(C.PRECONDITION_FAILED, f"queue '{q.name}' in use", 50, 40)
+            cnt = p.message_count(q.slot)
+            if m.if_empty and cnt:
+                raise ControlError(C.PRECONDITION_FAILED, f"queue '{q.name}' not empty", 50, 40)
+            p.purge(q.slot)
+            p.step({}, now_ms=int(time.time() * 1000))   # releases the purged messages
+            p.delete_queue(vh, q.name)
+            if not m.nowait:
+                self._send(c, ch, Method("queue.delete_ok", message_count=cnt))
+        elif n == "basic.qos":
+            p.qos(c.id, ch, m.prefetch_count, m.prefetch_size, m.global_)
+            self._send(c, ch, Method("basic.qos_ok"))
+        elif n == "basic.consume":
+            qn = m.queue or c.last_queue.get(ch, "")
+            self._queue(vh, qn, 60, 20)
+            tag = m.consumer_tag or ("amq.ctag-" + uuid.uuid4().hex)
+            p.consume(c.id, ch, vh, qn, tag, no_ack=m.no_ack)
+            if not m.nowait:
+                self._send(c, ch, Method("basic.consume_ok", consumer_tag=tag))
+        elif n == "basic.cancel":
+            p.cancel(c.id, ch, m.consumer_tag)
+            if not m.nowait:
+                self._send(c, ch, Method("basic.cancel_ok", consumer_tag=m.consumer_tag))
+        elif n in ("basic.recover", "basic.recover_async"):
+            p.recover(c.id, ch)   # requeue=false is treated as requeue (RabbitMQ behaviour)
+            if n == "basic.recover":
+                self._send(c, ch, Method("basic.recover_ok"))
+        elif n == "confirm.select":
+            p.confirm_select(c.id, ch)
+            if not m.nowait:
+                self._send(c, ch, Method("confirm.select_ok"))
+        elif n in ("basic.get", "tx.select", "tx.commit", "tx.rollback", "exchange.bind", "exchange.unbind"):
+            raise ControlError(C.NOT_IMPLEMENTED, f"{n} is not served by the GPU data path", m.class_id,
+                               m.method_id)
+        elif n == "basic.publish":   # publish on a channel the device did not know (closing race)
+            raise ControlError(C.CHANNEL_ERROR, "publish on a closed channel", 60, 40)
+        else:
+            raise _Hard(C.COMMAND_INVALID, f"unexpected {n}", m.class_id, m.method_id)
+
+    def _queue(self, vh, name, cls, mid):
+        q = self.plane.queues.get((vh, name))
+        if q is None:
+            raise ControlError(C.NOT_FOUND, f"no queue '{name}' in vhost '{vh}'", cls, mid)
+        return q
+
+    # ------------------------------------------------------------------ output
+    def _send(self, c, ch, m):
+        c.out += encode_method_frame(ch, m)
+
+    def _chan_close(self, c, ch, code, text, cls, mid):
+        self.plane.close_channel(c.id, ch)
+        c.closing_channels.add(ch)
+        self._send(c, ch, Method("channel.close", reply_code=code, reply_text=text[:255], class_id=cls,
+                                 method_id=mid))
+
+    def _conn_close(self, c, code, text, cls=0, mid=0):
+        if c.state in ("closing", "closed"):
+            return
+        self._send(c, 0, Method("connection.close", reply_code=code, reply_text=text[:255], class_id=cls,
+                                method_id=mid))
+        with self.lock:
+            self.plane.close_connection(c.id)
+        c.state = "closing"
+
+    def _flush(self, c):
+        if not c.out or c.state == "closed":
+            return
+        try:
+            n = c.sock.send(c.out)
+        except (BlockingIOError, InterruptedError):
+            return
+        except OSError:
+            self._drop(c)
+            return
+        del c.out[:n]
+        c.last_tx = time.monotonic()
+
+    def _flush_all(self):
+        for c in list(self.conns.values()):
+            if c.out:
+                self._flush(c)
+
+    def _heartbeats(self, now):
+        for c in list(self.conns.values()):
+            if c.state != "open" or not c.heartbeat:
+                continue
+            if now - c.last_tx >= c.heartbeat / 2 and not c.out:
+                c.out += HEARTBEAT
+            if now - c.last_rx > 2 * c.heartbeat:   # missed two heartbeats: peer is gone
+                self._drop(c)
+
+    def _drop(self, c):
+        if c.state == "closed":
+            return
+        prev = c.state
+        c.state = "closed"
+        try:
+            self._sel.unregister(c.sock)
+        except (KeyError, ValueError):
+            pass
+        try:
+            c.sock.close()
+        except OSError:
+            pass
+        if prev in ("open",) or c.id in self.plane.conns:
+            with self.lock:
+                self.plane.close_connection(c.id)
+        self.conns.pop(c.id, None)
+        self._free.append(c.id)
+
+
+__all__ = ["GpuBroker", "encode_table"]

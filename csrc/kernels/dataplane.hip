@@ -2159,6 +2159,7 @@ __global__ void k_requeue_compact(DS d) {
   // single block: compact the remaining (unconsumed) requeue items
   __shared__ u32 lds[1024 / 64 + 1];
   u32 n = *d.req_n;
+  if (n == 0) return;
   if (n > d.req_max) n = d.req_max;
   u32 run = 0;
   for (u32 b0 = 0; b0 < n; b0 += 1024) {

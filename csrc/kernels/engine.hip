@@ -320,7 +320,6 @@ class Engine {
       (void)hipEventDestroy(ev_done_[p]);
       (void)hipEventDestroy(ev_d2h_[p]);
     }
-    if (req_exec_) (void)hipGraphExecDestroy(req_exec_);
     (void)hipStreamDestroy(s_comp_);
     (void)hipStreamDestroy(s_h2d_);
     (void)hipStreamDestroy(s_d2h_);
@@ -456,15 +455,6 @@ class Engine {
     HIPCHECK(hipEventRecord(ev_h2d_[p], s_h2d_));
     HIPCHECK(hipStreamWaitEvent(s_comp_, ev_h2d_[p], 0));
     if (d2h_issued_[p]) HIPCHECK(hipStreamWaitEvent(s_comp_, ev_d2h_[p], 0));  // egress[p] drained
-    if (req_pending_) {
-      if (graph_enabled_) {
-        if (!req_exec_) capture_req();
-        HIPCHECK(hipGraphLaunch(req_exec_, s_comp_));
-      } else {
-        launch_requeue(s_comp_);
-      }
-      req_pending_ = false;
-    }
     if (d_.world > 1 && !xfer_set_) throw std::runtime_error("set_xfer_buffers() before the first sharded step");
     if (graph_enabled_) {
       if (!graph_exec_[p]) capture_main(p);
@@ -550,8 +540,6 @@ class Engine {
   }
 
   void egress_wait(int p) { HIPCHECK(hipEventSynchronize(ev_d2h_[p])); }
-
-  void request_requeue() { req_pending_ = true; }
 
   void sync() {
     HIPCHECK(hipStreamSynchronize(s_h2d_));
@@ -661,6 +649,10 @@ class Engine {
     hipLaunchKernelGGL(k_acks, blocks(d.ack_max, 256), dim3(256), 0, s, d);
     hipLaunchKernelGGL(k_chan_advance, blocks((u64)nch * 64, 256), dim3(256), 0, s, d);
     hipLaunchKernelGGL(k_reset_dirty, dim3(1), dim3(64), 0, s, d);
+    // requeued deliveries go back in front of their queues' heads before this step's
+    // dispatch, in queue-offset order (QueueEntity.scala:415-446)
+    hipLaunchKernelGGL(k_requeue, dim3(d.q_max), dim3(256), 0, s, d);
+    hipLaunchKernelGGL(k_requeue_compact, dim3(1), dim3(1024), 0, s, d);
     hipLaunchKernelGGL(k_dequeue, blocks((u64)d.q_max * 64, 256), dim3(256), 0, s, d);
     u32* dk[2] = {d.dv_k[0], d.dv_k[1]};
     u32* dvv[2] = {d.dv_v[0], d.dv_v[1]};
@@ -696,11 +688,6 @@ class Engine {
     launch_tail(s, d);
   }
 
-  void launch_requeue(hipStream_t s) {  // state-only kernels: IO pointers unused
-    hipLaunchKernelGGL(k_requeue, dim3(d_.q_max), dim3(256), 0, s, d_);
-    hipLaunchKernelGGL(k_requeue_compact, dim3(1), dim3(1024), 0, s, d_);
-  }
-
   void capture_main(int p) {
     hipGraph_t g;
     HIPCHECK(hipStreamBeginCapture(s_comp_, hipStreamCaptureModeThreadLocal));
@@ -719,15 +706,6 @@ class Engine {
     HIPCHECK(hipGraphDestroy(g));
   }
 
-  void capture_req() {
-    hipGraph_t g;
-    HIPCHECK(hipStreamBeginCapture(s_comp_, hipStreamCaptureModeThreadLocal));
-    launch_requeue(s_comp_);
-    HIPCHECK(hipStreamEndCapture(s_comp_, &g));
-    HIPCHECK(hipGraphInstantiate(&req_exec_, g, nullptr, nullptr, 0));
-    HIPCHECK(hipGraphDestroy(g));
-  }
-
   int device_ = 0;
   DS d_;
   std::map<std::string, Buf> bufs_;
@@ -736,7 +714,6 @@ class Engine {
   u32 ntiles_max_ = 0;
   bool graph_enabled_ = true;
   hipGraphExec_t graph_exec_[2] = {nullptr, nullptr};
-  hipGraphExec_t req_exec_ = nullptr;
   hipGraphExec_t graph_b_[2] = {nullptr, nullptr};
   hipEvent_t ev_a_[2], ev_ext_[2];
   bool phase_a_[2] = {false, false};
@@ -749,7 +726,6 @@ class Engine {
   hipEvent_t ev_h2d_[2], ev_done_[2], ev_d2h_[2];
   bool inflight_[2] = {false, false};
   bool d2h_issued_[2] = {false, false};
-  bool req_pending_ = false;
   u64 seq_ = 0;
 };
 
@@ -796,7 +772,6 @@ PYBIND11_MODULE(_dataplane, m) {
       .def("wait_results", &Engine::wait_results)
       .def("egress_copy", &Engine::egress_copy)
       .def("egress_wait", &Engine::egress_wait)
-      .def("request_requeue", &Engine::request_requeue)
       .def("sync", &Engine::sync)
       .def("counters", &Engine::counters);
 }

@@ -1,0 +1,143 @@
+"""AMQP conversations against the GPU-data-path server (server/gpu_broker.py), with the
+plane = golden model (CPU, always) and = HIP data plane (GPU box, marked gpu)."""
+
+import pytest
+
+from chanamq_amd.client import ChannelClosed, Connection, ConnectionClosed
+
+SMALL = dict(c_max=64, chpc=8, q_max=64, x_max=64, cons_max=256, ucap=256, deliver_cap=4096)
+GPU_CFG = dict(SMALL, seg_max=64, cmd_max=4096, deliv_max=4096, msg_max=1 << 14, ingress_cap=8 << 20,
+               egress_cap=16 << 20, log_bytes=64 << 20, log_block=1 << 20, ring_pool=1 << 20, tb_max=64,
+               carry_cap=1 << 18, dhash=1024, req_max=4096)
+
+
+def make_plane(kind):
+    if kind == "golden":
+        from chanamq_amd.engine.golden import GoldenDataPlane
+        return GoldenDataPlane(default_queue_capacity=1 << 12, ring_pool=1 << 20, **SMALL)
+    import torch
+    if not torch.cuda.is_available():
+        pytest.fail("GPU test scheduled on a machine without a GPU")
+    from chanamq_amd.engine.dataplane import GpuDataPlane
+    return GpuDataPlane(default_queue_capacity=1 << 12, **GPU_CFG)
+
+
+@pytest.fixture(params=["golden", pytest.param("gpu", marks=pytest.mark.gpu)])
+def broker(request):
+    from chanamq_amd.server.gpu_broker import GpuBroker
+    b = GpuBroker(make_plane(request.param), idle_step_ms=1.0).start()
+    yield b
+    b.stop()
+
+
+def conn(b, **kw):
+    return Connection(port=b.port, vhost="/", **kw)
+
+
+def test_publish_consume_topic(broker):
+    p = conn(broker)
+    ch = p.channel()
+    ch.exchange_declare("tx", "topic")
+    for q, pat in (("qa", "a.*"), ("qb", "*.b"), ("qall", "#")):
+        ch.queue_declare(q)
+        ch.queue_bind(q, "tx", pat)
+    c = conn(broker)
+    cc = c.channel()
+    for q in ("qa", "qb", "qall"):
+        cc.basic_consume(q, "t-" + q, no_ack=True)
+    keys = ["a.x", "y.b", "a.b", "zzz"]
+    for i, k in enumerate(keys):
+        ch.basic_publish("tx", k, f"m{i}".encode(), {"content_type": "text/plain"})
+    got = cc.consume_n(1 + 1 + 4 + 2)   # a.x->qa,qall; y.b->qb,qall; a.b->all 3; zzz->qall
+    by_tag = {}
+    for d in got:
+        by_tag.setdefault(d.method.consumer_tag, []).append(d.body)
+    assert by_tag["t-qa"] == [b"m0", b"m2"]
+    assert by_tag["t-qb"] == [b"m1", b"m2"]
+    assert by_tag["t-qall"] == [b"m0", b"m1", b"m2", b"m3"]
+    assert got[0].props.get("content_type") in ("text/plain", b"text/plain")
+    p.close()
+    c.close()
+
+
+def test_default_exchange_and_declare_counts(broker):
+    p = conn(broker)
+    ch = p.channel()
+    ok = ch.queue_declare("")          # server-named
+    name = ok.queue
+    assert name.startswith("tmp.")
+    for i in range(5):
+        ch.basic_publish("", name, b"x%d" % i)
+    p.process(0.2)
+    ok2 = ch.queue_declare(name, passive=True)
+    assert ok2.message_count == 5 and ok2.consumer_count == 0
+    assert ch.queue_purge(name) == 5
+    p.process(0.1)
+    assert ch.queue_declare(name, passive=True).message_count == 0
+    ch.basic_publish("", name, b"after")
+    p.process(0.1)
+    assert ch.queue_delete(name) == 1
+    with pytest.raises(ChannelClosed) as e:
+        ch.queue_declare(name, passive=True)
+    assert e.value.code == 404
+    p.close()
+
+
+def test_manual_ack_prefetch_and_redelivery(broker):
+    p = conn(broker)
+    ch = p.channel()
+    ch.queue_declare("work")
+    for i in range(10):
+        ch.basic_publish("", "work", b"w%d" % i)
+    c = conn(broker)
+    cc = c.channel()
+    cc.basic_qos(prefetch_count=3)
+    cc.basic_consume("work", "wc")
+    first = cc.consume_n(3)
+    assert [d.body for d in first] == [b"w0", b"w1", b"w2"]
+    c.process(0.2)
+    assert len(cc.deliveries) == 0           # prefetch window full
+    cc.basic_nack(first[1].delivery_tag, requeue=True)
+    cc.basic_ack(first[2].delivery_tag)
+    nxt = cc.consume_n(2)
+    assert nxt[0].body == b"w1" and nxt[0].method.redelivered
+    cc.basic_recover()
+    again = cc.consume_n(3)
+    assert sorted(d.body for d in again) == sorted([b"w0", nxt[0].body, nxt[1].body])
+    assert all(d.method.redelivered for d in again)
+    p.close()
+    c.close()
+
+
+def test_confirms_and_mandatory_return(broker):
+    p = conn(broker)
+    ch = p.channel()
+    ch.exchange_declare("dx", "direct")
+    ch.queue_declare("dq")
+    ch.queue_bind("dq", "dx", "k")
+    ch.confirm_select()
+    ch.basic_publish("dx", "k", b"ok")
+    ch.basic_publish("dx", "nokey", b"lost", mandatory=True)
+    assert ch.wait_for_confirms()
+    p._wait(lambda: ch.returns or None, ch)
+    r = ch.returns[0]
+    assert r.method.reply_code == 312 and r.body == b"lost"
+    p.close()
+
+
+def test_errors_unknown_exchange_and_unsupported(broker):
+    p = conn(broker)
+    ch = p.channel()
+    ch.basic_publish("nope", "k", b"x")
+    with pytest.raises(ChannelClosed) as e:
+        p._wait(lambda: None, ch, timeout=3)
+    assert e.value.code == 404
+    ch2 = p.channel()
+    ch2.queue_declare("g")
+    with pytest.raises(ConnectionClosed) as e:    # 540 is a connection exception (AMQP 0-9-1)
+        ch2.basic_get("g")
+    assert e.value.code == 540
+    p.close()
+    q = conn(broker)
+    q.channel().queue_declare("g", passive=True)   # broker still serving
+    q.close()
