@@ -56,6 +56,7 @@ class Queue:
     ring_off: int = 0
     consumers: list = field(default_factory=list)  # consumer ids, in registration order
     owner: int = 0                                  # owning rank (sharded data plane)
+    requested: int = 0                              # requested ring capacity (for re-homing)
 
 
 @dataclass
@@ -265,7 +266,7 @@ class ControlState:
             cap <<= 1
         slot = self._free_q.pop()
         q = Queue(slot, vhost, name, durable, exclusive_owner, auto_delete, ttl_ms, cap,
-                  self._ring_alloc(cap), owner=owner)
+                  self._ring_alloc(cap), owner=owner, requested=capacity)
         self.queues[key] = q
         self.queue_by_slot[slot] = q
         dx = self.exchanges.get((vhost, ""))
@@ -292,6 +293,36 @@ class ControlState:
         self._ring_free.setdefault(q.capacity, []).append(q.ring_off)
         self.queue_deleted(q)
         self.routing_changed()
+
+    def set_queue_owner(self, slot, owner):
+        """Move queue ``slot`` to rank ``owner`` (failover re-homing, placement).  The new
+        owner allocates a fresh ring; the old owner's ring is released (it must be the
+        dead rank's, or empty).  Applied identically on every rank (control log)."""
+        q = self.queue_by_slot[slot]
+        if q.owner == owner:
+            return owner
+        if q.owner == self.rank:
+            for cid in list(q.consumers):
+                c = self.consumers[cid]
+                self.channel(c.conn, c.ch).consumers.pop(c.tag, None)
+                self._drop_consumer(cid)
+        self._ring_free.setdefault(q.capacity, []).append(q.ring_off)
+        cap = 1
+        while cap < (q.requested or self.default_queue_capacity) and owner == self.rank:
+            cap <<= 1
+        q.owner, q.capacity, q.ring_off = owner, cap, self._ring_alloc(cap)
+        self.queue_declared(q)
+        self.routing_changed()
+        return owner
+
+    def rehome(self, dead):
+        """Re-home every queue owned by the ``dead`` ranks (ShardMap already updated)."""
+        moved = []
+        for q in sorted(self.queue_by_slot.values(), key=lambda x: x.slot):
+            if q.owner in dead:
+                self.set_queue_owner(q.slot, self.shard_map.owner(q.vhost, q.name))
+                moved.append(q.name)
+        return moved
 
     def bind(self, vhost, queue, exchange, key):
         x = self.exchanges.get((vhost, exchange))

@@ -1,0 +1,72 @@
+"""Replicated control plane (the role of the reference's DistributedPubSub broadcasts
+and entity messages for exchange/queue/binding changes).
+
+Control operations issued on any rank are appended to that rank's outbox; ``sync()``
+all-gathers the outboxes once per step and every rank applies the union in the same
+order (logical rank, then sequence), so the replicated tables (exchanges, bindings,
+queue slots, ownership) stay identical everywhere.  Connection-scoped state (channels,
+consumers) stays local and is not logged.  Ops are JSON: nothing executable crosses
+ranks.
+"""
+
+from ..protocol import constants as C
+from .comm import Comm
+
+REPLICATED = {"declare_exchange", "delete_exchange", "declare_queue", "delete_queue", "bind", "unbind",
+              "place_queue", "ensure_vhost"}
+
+
+class ControlLog:
+    def __init__(self, plane, comm: Comm):
+        self.plane, self.comm = plane, comm
+        self.outbox = []
+        self.applied = 0
+        self.results = {}     # local seq -> result or ControlError tuple
+
+    def submit(self, op, *args, **kw):
+        if op not in REPLICATED:
+            raise ValueError(f"{op} is not a replicated control op")
+        seq = len(self.outbox)
+        self.outbox.append([op, list(args), kw])
+        return seq
+
+    def sync(self):
+        """All-gather and apply.  Returns {local seq: result} for this rank's ops."""
+        from ..engine.control import ControlError
+        got = self.comm.allgather_json(self.outbox)
+        mine = {}
+        for r in sorted(got):
+            for seq, (op, args, kw) in enumerate(got[r]):
+                try:
+                    res = self._apply(op, args, kw)
+                except ControlError as e:
+                    res = ("error", e.code, e.text, e.class_id, e.method_id)
+                self.applied += 1
+                if r == self.comm.rank:
+                    mine[seq] = res
+        self.outbox = []
+        return mine
+
+    def _apply(self, op, args, kw):
+        p = self.plane
+        if op == "place_queue":
+            vhost, name, rank = args
+            q = p.queues.get((vhost, name))
+            if q is None:
+                p.shard_map.place(vhost, name, rank)
+                return None
+            p.shard_map.place(vhost, name, rank)
+            return p.set_queue_owner(q.slot, rank)
+        if op == "ensure_vhost":
+            return p.ensure_vhost(*args)
+        return getattr(p, op)(*args, **kw)
+
+
+def error_of(res):
+    """(code, text, class, method) if ``res`` is a logged ControlError, else None."""
+    if isinstance(res, (list, tuple)) and res and res[0] == "error":
+        return tuple(res[1:])
+    return None
+
+
+__all__ = ["ControlLog", "error_of", "REPLICATED", "C"]

@@ -19,7 +19,6 @@ step's whole cross-rank traffic is one bulk collective.
 """
 
 import torch
-import torch.distributed as dist
 
 from ..engine.layout import RDESC
 
@@ -27,34 +26,42 @@ REC = RDESC.itemsize
 
 
 class Exchanger:
-    def __init__(self, world=None, rank=None, group=None, stage_cpu=None):
-        self.group = group
-        self.world = dist.get_world_size(group) if world is None else world
-        self.rank = dist.get_rank(group) if rank is None else rank
-        backend = dist.get_backend(group)
-        self.device_ok = backend == "nccl"
+    def __init__(self, comm=None, stage_cpu=None):
+        from .comm import Comm
+        self.comm = comm or Comm()
+        self.device_ok = self.comm.backend == "nccl"
         self.stage_cpu = (not self.device_ok) if stage_cpu is None else stage_cpu
         self.bytes_sent = 0
         self.calls = 0
 
+    @property
+    def world(self):
+        return self.comm.world
+
+    @property
+    def rank(self):
+        return self.comm.rank
+
     def _a2a(self, out, inp, out_splits, in_splits):
         if self.stage_cpu and inp.is_cuda:
             ci, co = inp.cpu(), torch.empty(out.numel(), dtype=out.dtype)
-            dist.all_to_all_single(co, ci, out_splits, in_splits, group=self.group)
+            self.comm.alltoall(co, ci, out_splits, in_splits)
             out.copy_(co)
         else:
-            dist.all_to_all_single(out, inp, out_splits, in_splits, group=self.group)
+            self.comm.alltoall(out, inp, out_splits, in_splits)
 
     def exchange(self, send_counts, send_desc, send_pay, recv_desc, recv_pay):
-        """``send_counts`` = [n_0..n_{W-1}, b_0..b_{W-1}] -> received [n.., b..] by source.
-        Tensors are flat uint8 (records: 64 bytes each)."""
+        """``send_counts`` = [n_0..n_{W-1}, b_0..b_{W-1}] (logical ranks) -> received
+        [n.., b..] by source.  Tensors are flat uint8 (records: 64 bytes each).  Traffic
+        for ranks that left the group is dropped (its owner is gone; at-most-once)."""
         W = self.world
-        n, b = list(send_counts[:W]), list(send_counts[W:2 * W])
-        dev = send_desc.device if (self.device_ok and send_desc.is_cuda) else torch.device("cpu")
-        cnt = torch.tensor([v for r in range(W) for v in (n[r], b[r])], dtype=torch.int64, device=dev)
-        out = torch.empty_like(cnt)
-        dist.all_to_all_single(out, cnt, group=self.group)
-        rc = out.view(W, 2).cpu().tolist()
+        live = set(self.comm.members)
+        n = [send_counts[r] if r in live else 0 for r in range(W)]
+        b = [send_counts[W + r] if r in live else 0 for r in range(W)]
+        if n != list(send_counts[:W]):
+            # repack without the departed destinations (records are destination-major)
+            n, b, send_desc, send_pay = _drop_dead(send_counts, send_desc, send_pay, live, W)
+        rc = self.comm.alltoall_counts([[n[r], b[r]] for r in range(W)])
         rn, rb = [x[0] for x in rc], [x[1] for x in rc]
         if sum(rn) * REC > recv_desc.numel() or sum(rb) > recv_pay.numel():
             raise RuntimeError(f"rank {self.rank}: received {sum(rn)} records / {sum(rb)} bytes "
@@ -65,6 +72,24 @@ class Exchanger:
         self.bytes_sent += sd + sum(b)
         self.calls += 1
         return rn + rb
+
+
+def _drop_dead(send_counts, send_desc, send_pay, live, W):
+    n0, b0 = list(send_counts[:W]), list(send_counts[W:2 * W])
+    descs, pays, n, b = [], [], [], []
+    do = po = 0
+    for r in range(W):
+        if r in live:
+            descs.append(send_desc[do:do + n0[r] * REC])
+            pays.append(send_pay[po:po + b0[r]])
+            n.append(n0[r])
+            b.append(b0[r])
+        else:
+            n.append(0)
+            b.append(0)
+        do += n0[r] * REC
+        po += b0[r]
+    return n, b, torch.cat(descs) if descs else send_desc[:0], torch.cat(pays) if pays else send_pay[:0]
 
 
 def local_exchange(planes):

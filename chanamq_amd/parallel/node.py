@@ -1,0 +1,89 @@
+"""One rank of a sharded broker: data plane + communicator + replicated control log +
+failure detector, stepped in lockstep with its peers.
+
+  step(inputs):  control-log sync (all-gather, apply everywhere)
+                 -> data-plane step (phase A, all-to-all of cross-rank publishes, phase B)
+  on a failed collective:  wait for the failure detector, agree on the dead set, rebuild
+                 the communicator over the survivors, re-home the dead ranks' queues
+                 (rendezvous hashing moves only those), retry the step.
+
+This is the reference's cluster behaviour (Akka cluster sharding re-homes entities of a
+downed node) for the per-step collective design.  Messages held only by the
+dead GPU are lost unless persistent on durable queues (reloaded from the store by the
+new owner).
+"""
+
+import logging
+
+from .comm import Comm
+from .control_log import ControlLog
+from .exchange import Exchanger
+from .membership import Membership
+
+log = logging.getLogger("chanamq.node")
+
+
+class ShardedNode:
+    def __init__(self, plane, comm: Comm = None, membership: Membership = None, hb_timeout_s=2.0):
+        self.plane = plane
+        self.comm = comm or Comm()
+        self.exchanger = Exchanger(self.comm)
+        plane.exchanger = None   # the node drives the exchange (and retries it on failover)
+        self.log = ControlLog(plane, self.comm)
+        self.members = membership or Membership(self.comm.store, self.comm.rank, self.comm.world,
+                                                timeout_s=hb_timeout_s)
+        self.failovers = []
+
+    @property
+    def rank(self):
+        return self.comm.rank
+
+    def submit(self, op, *args, **kw):
+        return self.log.submit(op, *args, **kw)
+
+    def step(self, inputs=None, now_ms=0, retries=3):
+        """One lockstep step -> (plane step result, {seq: result} of this rank's ops)."""
+        results = self._retry(self.log.sync, retries)
+        return self._data_step(inputs or {}, now_ms, retries), results
+
+    def _retry(self, fn, retries):
+        for attempt in range(retries + 1):
+            try:
+                return fn()
+            except RuntimeError as e:   # a peer vanished mid-collective
+                if attempt == retries:
+                    raise
+                log.warning("rank %d: collective failed (%s); checking membership", self.rank, e)
+                self.handle_failure()
+
+    def _data_step(self, inputs, now_ms, retries):
+        p = self.plane
+        gpu = hasattr(p, "eng")
+        if gpu:
+            segs, ptr, n = p.stage(inputs)
+            ticket = p.submit_raw(segs, ptr, n, now_ms)     # phase A (no exchanger on the plane)
+        else:
+            p.step_a(inputs, now_ms)
+        recv = self._retry(lambda: self.exchanger.exchange(p.pending_send_counts(), p.xfer_send_desc(),
+                                                           p.xfer_send_pay(), p.xfer_recv_desc(),
+                                                           p.xfer_recv_pay()), retries)
+        if gpu:
+            p.submit_b(recv)
+            return p.finish(ticket)
+        return p.step_b(recv)
+
+    def handle_failure(self, suspects=None):
+        suspects = suspects if suspects is not None else self.members.wait_suspects()
+        if not suspects:
+            raise RuntimeError("collective failed but no peer is suspected")
+        dead = self.members.agree_dead(suspects, epoch=self.comm.epoch + 1)
+        self.comm.rebuild(self.members.live)
+        for r in dead:
+            self.plane.shard_map.fail(r)
+        moved = self.plane.rehome(dead)
+        self.failovers.append((sorted(dead), moved))
+        log.warning("rank %d: ranks %s left; re-homed %d queues", self.rank, sorted(dead), len(moved))
+        return dead, moved
+
+    def close(self):
+        self.members.stop()
