@@ -111,10 +111,17 @@ def main():
     import torch
 
     dist = None
+    # CHANAMQ_BENCH_BACKEND=gloo rehearses the multi-rank path on fewer GPUs (ranks share
+    # devices, exchange staged through the host); the real run uses RCCL ("nccl")
+    backend = os.environ.get("CHANAMQ_BENCH_BACKEND", "nccl")
     if world > 1:
         import torch.distributed as dist
+        local = local % max(1, torch.cuda.device_count())
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     from chanamq_amd.engine.dataplane import GpuDataPlane
 
     P, Q = args.producers, args.queues
@@ -184,15 +191,17 @@ def main():
         dist.barrier()
     t = time.perf_counter() - t0
     c = dp.eng.counters((step_i - 1) & 1)
-    errs = {k: c[k] for k in ("n_dropped_nomem", "n_ring_full", "n_unknown_exchange", "n_unroutable", "n_routed_msgs", "n_pairs", "n_deliv", "n_live_msgs") if c[k]}
+    errs = {k: c[k] for k in ("n_dropped_nomem", "n_ring_full", "n_unknown_exchange", "n_unroutable",
+                              "n_routed_msgs", "n_pairs", "n_deliv", "n_live_msgs") if c[k]}
 
     vals = np.array([t, dl, pb, eg], np.float64)
     if dist:
-        tt = torch.tensor([t], dtype=torch.float64, device="cuda")
+        rdev = "cuda" if backend == "nccl" else "cpu"
+        tt = torch.tensor([t], dtype=torch.float64, device=rdev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        ss = torch.tensor(vals[1:], dtype=torch.float64, device="cuda")
+        ss = torch.tensor(vals[1:], dtype=torch.float64, device=rdev)
         dist.all_reduce(ss, op=dist.ReduceOp.SUM)
-        hh = torch.tensor(hist, dtype=torch.float64, device="cuda")
+        hh = torch.tensor(hist, dtype=torch.float64, device=rdev)
         dist.all_reduce(hh, op=dist.ReduceOp.SUM)
         t = float(tt.item())
         dl, pb, eg = (float(x) for x in ss.tolist())
@@ -234,7 +243,7 @@ def main():
             "published_msgs_per_s": pb / t,
             "egress_GBps": eg / t / 1e9,
             "latency_note": "in-broker publish->deliver (ingress submit to egress bytes ready), no TCP",
-            "errors": errs,
+            "diag": errs,
             "cross_gpu_bytes_per_s": (dp.exchanger.bytes_sent * world / t) if shards > 1 else 0.0,
         }
         print(json.dumps(out))

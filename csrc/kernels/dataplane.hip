@@ -756,8 +756,7 @@ __global__ void k_classify(DS d) {
   d.cmd_is_ack[i] = (k == CK_ACK || k == CK_NACK || k == CK_REJECT);
 }
 
-__global__ void k_set_counts(DS d) {
-  if (threadIdx.x) return;
+DEV void set_counts(const DS& d) {
   u32 np = d.tot[4], na = d.tot[5];
   d.ctr->n_pubs = np < d.pub_max ? np : d.pub_max;
   d.ctr->n_acks = na < d.ack_max ? na : d.ack_max;
@@ -768,6 +767,7 @@ __global__ void k_set_counts(DS d) {
   d.tot[TS_PAIR_N] = 0;
   d.tot[TS_NIMPORT] = 0;
 }
+__global__ void k_set_counts(DS d) { if (threadIdx.x == 0) set_counts(d); }
 
 __global__ void k_reset_dirty(DS d) {
   if (threadIdx.x == 0) *d.n_dirty = 0;
@@ -802,6 +802,7 @@ DEV u32 build_keyvec(const DS& d, const u8* key, u32 len, u32 pi) {
 }
 
 __global__ void k_decode(DS d) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) set_counts(d);  // fused: counts + phase-0 range
   u32 i = blockIdx.x * blockDim.x + threadIdx.x;
   u32 n = d.ctr->n_cmds;
   if (n > d.cmd_max) n = d.cmd_max;
@@ -931,9 +932,25 @@ __global__ void k_decode(DS d) {
 // single-block multi-array exclusive scan; n read from device; totals -> tot[slot+k]
 // lo != null: scan elements [*lo, *n) (absolute indices), else [0, *n)
 struct ScanArgs { const u32* in[4]; u32* out[4]; const u32* n; const u32* lo; u32 narr; u32 nmax; u32 tot_slot; };
-// single-block exclusive scan over up to 4 arrays; tiles of 4096 with 16-B loads/stores
-__global__ __launch_bounds__(1024) void k_scan(ScanArgs a, u32* tot) {
+// Single-pass exclusive scan over up to 4 arrays, one 4096-element tile per block, tiles
+// chained by decoupled look-back: each tile publishes its aggregate, then its inclusive
+// prefix, in a per-(array, tile) status word tagged with the launch epoch, so the status
+// array never needs clearing.  Tickets (not blockIdx) order the tiles, so a tile only
+// ever waits on tiles whose blocks are already running.
+//   status word = epoch << 34 | flag << 32 | value   (flag 1 = aggregate, 2 = inclusive)
+#define SCAN_TILE 4096
+__global__ __launch_bounds__(1024) void k_scan(ScanArgs a, u32* tot, u64* status, u32* ctl, u32 smax) {
   __shared__ u32 lds[1024 / 64 + 1];
+  __shared__ u32 s_tile, s_epoch;
+  __shared__ u32 s_excl[4];
+  const u32 tid = threadIdx.x;
+  if (tid == 0) {
+    s_epoch = atomicAdd(&ctl[1], 0u);
+    s_tile = atomicAdd(&ctl[0], 1u);
+  }
+  __syncthreads();
+  const u32 tile = s_tile, epoch = s_epoch & 0x3fffffffu;
+  const bool last_block = tile == gridDim.x - 1;
   u32 n = a.n ? *a.n : a.nmax;
   if (n > a.nmax) n = a.nmax;
   if (a.lo) {
@@ -941,27 +958,56 @@ __global__ __launch_bounds__(1024) void k_scan(ScanArgs a, u32* tot) {
     n = n > lo ? n - lo : 0;
     for (u32 k = 0; k < a.narr; ++k) { a.in[k] += lo; a.out[k] += lo; }
   }
-  const u32 tid = threadIdx.x;
-  u32 run[4] = {0, 0, 0, 0};
-  for (u32 base = 0; base < n; base += 4096) {
+  const u32 base = tile * SCAN_TILE;
+  if (base < n || (tile == 0)) {
     const u32 i = base + tid * 4;
+    u32 v[4][4], off[4], agg[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       if ((u32)k >= a.narr) break;
-      u32 v0 = 0, v1 = 0, v2 = 0, v3 = 0;
+      v[k][0] = v[k][1] = v[k][2] = v[k][3] = 0;
       if (i + 3 < n && !(((uintptr_t)(a.in[k] + i)) & 15)) {
-        uint4 v = *(const uint4*)(a.in[k] + i);
-        v0 = v.x; v1 = v.y; v2 = v.z; v3 = v.w;
+        uint4 x = *(const uint4*)(a.in[k] + i);
+        v[k][0] = x.x; v[k][1] = x.y; v[k][2] = x.z; v[k][3] = x.w;
       } else {
-        if (i < n) v0 = a.in[k][i];
-        if (i + 1 < n) v1 = a.in[k][i + 1];
-        if (i + 2 < n) v2 = a.in[k][i + 2];
-        if (i + 3 < n) v3 = a.in[k][i + 3];
+        for (u32 e = 0; e < 4; ++e)
+          if (i + e < n) v[k][e] = a.in[k][i + e];
       }
-      u32 sum = v0 + v1 + v2 + v3, all;
-      u32 off = run[k] + block_scan<1024>(sum, lds, all);
+      u32 sum = v[k][0] + v[k][1] + v[k][2] + v[k][3], all;
+      off[k] = block_scan<1024>(sum, lds, all);
+      agg[k] = all;
+      __syncthreads();
+    }
+    if (tid < a.narr) {
+      const u32 k = tid;
+      u32 A = tid == 0 ? agg[0] : tid == 1 ? agg[1] : tid == 2 ? agg[2] : agg[3];
+      // agent-scope acquire/release: the tiles run on different XCDs (separate L2s)
+      u64* st = status + (u64)k * smax;
+      const u64 tag = (u64)epoch << 34;
+      u32 excl = 0;
+      if (tile > 0) {
+        __hip_atomic_store(&st[tile], tag | (1ull << 32) | A, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        for (u32 j = tile; j > 0;) {
+          --j;
+          u64 w;
+          do {
+            w = __hip_atomic_load(&st[j], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+          } while ((w >> 34) != epoch || ((w >> 32) & 3) == 0);
+          excl += (u32)w;
+          if (((w >> 32) & 3) == 2) break;
+        }
+      }
+      __hip_atomic_store(&st[tile], tag | (2ull << 32) | (excl + A), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      s_excl[k] = excl;
+      if (base + SCAN_TILE >= n) tot[a.tot_slot + k] = excl + A;   // the last data tile
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      if ((u32)k >= a.narr) break;
+      u32 o0 = s_excl[k] + off[k];
       uint4 o;
-      o.x = off; o.y = off + v0; o.z = o.y + v1; o.w = o.z + v2;
+      o.x = o0; o.y = o0 + v[k][0]; o.z = o.y + v[k][1]; o.w = o.z + v[k][2];
       if (i + 3 < n && !(((uintptr_t)(a.out[k] + i)) & 15)) *(uint4*)(a.out[k] + i) = o;
       else {
         if (i < n) a.out[k][i] = o.x;
@@ -969,11 +1015,12 @@ __global__ __launch_bounds__(1024) void k_scan(ScanArgs a, u32* tot) {
         if (i + 2 < n) a.out[k][i + 2] = o.z;
         if (i + 3 < n) a.out[k][i + 3] = o.w;
       }
-      run[k] += all;
     }
   }
-  if (tid == 0)
-    for (u32 k = 0; k < a.narr; ++k) tot[a.tot_slot + k] = run[k];
+  if (last_block && tid == 0) {   // every block has its ticket: reset for the next launch
+    atomicExch(&ctl[0], 0u);
+    atomicExch(&ctl[1], epoch + 1);
+  }
 }
 
 // ============================================================================ radix sort
@@ -1138,87 +1185,124 @@ DEV i32 direct_find(const DS& d, const Pub& pb) {
 // pass 0: count queues; pass 1: write pairs
 // Publishes [tot[RANGE_LO], tot[RANGE_HI]): phase 0 = the step's own, phase 1 = records
 // imported from other ranks (sharded queues; only locally owned queues are emitted).
+// One wave per publish: the lanes walk the exchange's candidate list (direct queue list,
+// fanout list, or topic bindings with their MFMA prefilter bits) 64 entries at a time, so
+// a publish costs a few dependent loads instead of one serial chain per binding.
+DEV u32 wave_or(u32 v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v |= __shfl_xor(v, o);
+  return v;
+}
+
 template <int PASS>
-__global__ void k_route(DS d) {
-  u32 p = d.tot[TS_RANGE_LO] + blockIdx.x * blockDim.x + threadIdx.x;
-  u32 n = d.tot[TS_RANGE_HI];
-  if (n > d.pub_cap) n = d.pub_cap;
-  if (p >= n) return;
+struct RouteAcc {
+  u32 nq = 0, nq_all = 0, rmask = 0;
+  bool has_cons = false;
+};
+
+// emit one candidate queue per lane (valid lanes), preserving lane order
+template <int PASS>
+DEV void route_emit(const DS& d, RouteAcc<PASS>& a, u32 p, u32 wbase, u32 srank, u32 q, bool valid, u32 lane) {
+  const u32 me = d.my_rank;
+  u32 owner = (valid && d.world > 1) ? d.q_owner[q] : me;
+  bool remote = valid && owner != me;
+  bool local = valid && !remote;
+  a.rmask |= wave_or(remote ? (1u << owner) : 0u);
+  u64 lm = __ballot(local);
+  bool cons = local && d.q_cons_n[q] != 0;
+  if (__ballot(cons || remote)) a.has_cons = true;
+  u32 pos = a.nq + (u32)__popcll(lm & lanemask_lt());
+  if (local) {
+    if (PASS) {
+      d.pair_k[0][wbase + pos] = (q << d.rank_bits) | srank;
+      d.pair_v[0][wbase + pos] = p;
+    } else if (pos < 8) {
+      d.pub_qc[(u64)p * 8 + pos] = q;
+    }
+  }
+  a.nq += (u32)__popcll(lm);
+  a.nq_all += (u32)__popcll(__ballot(valid));
+}
+
+template <int PASS>
+DEV void route_one(const DS& d, u32 p, u32 lane) {
   Pub& pb = d.pubs[p];
-  u32 wbase = PASS ? d.tot[TS_PAIR_BASE] + d.pub_pair_off[p] : 0;
+  const u32 wbase = PASS ? d.tot[TS_PAIR_BASE] + d.pub_pair_off[p] : 0;
   // pair key = queue << rank_bits | source rank: a queue's messages are ordered by
   // (source rank, connection, publish order) whichever rank owns it
-  const u32 rb = d.rank_bits;
   const u32 srank = (pb.flags & MF_IMPORTED) ? pb.pad : d.my_rank;
   if (PASS == 1) {
     u32 nq0 = d.pub_nq[p];
     if (nq0 == 0) return;
     if (wbase + nq0 > d.pair_max) return;  // capacity: k_log_reserve clamps the pair count
     if (nq0 <= 8) {  // routing result cached by pass 0
-      for (u32 k = 0; k < nq0; ++k) {
-        d.pair_k[0][wbase + k] = (d.pub_qc[(u64)p * 8 + k] << rb) | srank;
-        d.pair_v[0][wbase + k] = p;
+      if (lane < nq0) {
+        d.pair_k[0][wbase + lane] = (d.pub_qc[(u64)p * 8 + lane] << d.rank_bits) | srank;
+        d.pair_v[0][wbase + lane] = p;
       }
       return;
     }
   }
-  u32 nq = 0, nq_all = 0, rmask = 0;
-  bool has_cons = false;
-  const u32 me = d.my_rank;
-  const bool sharded = d.world > 1;
-#define EMIT(q)                                              \
-  do {                                                       \
-    u32 _q = (q);                                            \
-    ++nq_all;                                                \
-    u32 _o = sharded ? d.q_owner[_q] : me;                   \
-    if (_o != me) { rmask |= 1u << _o; has_cons = true; break; } \
-    if (PASS) { d.pair_k[0][wbase + nq] = (_q << rb) | srank; d.pair_v[0][wbase + nq] = p; } \
-    else if (nq < 8) d.pub_qc[(u64)p * 8 + nq] = _q;         \
-    if (d.q_cons_n[_q]) has_cons = true;                     \
-    ++nq;                                                    \
-  } while (0)
-  if (pb.exch >= 0) {
-    u32 xt = d.x_type[pb.exch];
-    if (xt == EX_DIRECT) {
-      i32 s = direct_find(d, pb);
-      if (s >= 0) {
-        u32 o = d.d_q_off[s], c = d.d_q_n[s];
-        for (u32 k = 0; k < c; ++k) EMIT(d.d_q[o + k]);
+  RouteAcc<PASS> a;
+  const i32 ex = pb.exch;
+  if (ex >= 0) {
+    u32 xt = d.x_type[ex];
+    if (xt == EX_DIRECT || xt == EX_FANOUT) {
+      u32 o = 0, c = 0;
+      const u32* list;
+      if (xt == EX_DIRECT) {
+        i32 s = lane == 0 ? direct_find(d, pb) : 0;
+        s = __shfl(s, 0);
+        if (s >= 0) { o = d.d_q_off[s]; c = d.d_q_n[s]; }
+        list = d.d_q;
+      } else {
+        o = d.x_fan_off[ex]; c = d.x_fan_n[ex];
+        list = d.fan_q;
       }
-    } else if (xt == EX_FANOUT) {
-      u32 o = d.x_fan_off[pb.exch], c = d.x_fan_n[pb.exch];
-      for (u32 k = 0; k < c; ++k) EMIT(d.fan_q[o + k]);
+      for (u32 k0 = 0; k0 < c; k0 += 64) {
+        bool v = k0 + lane < c;
+        u32 q = v ? list[o + k0 + lane] : 0;
+        route_emit<PASS>(d, a, p, wbase, srank, q, v, lane);
+      }
     } else {
-      u32 o = d.x_t_off[pb.exch], c = d.x_t_n[pb.exch];
-      u32 last = INVALID;
-      for (u32 k = 0; k < c; ++k) {
-        u32 t = o + k;
-        u32 q = d.t_queue[t];
-        if (q == last) continue;
-        if (topic_bind_hit(d, pb, p, t)) { EMIT(q); last = q; }
+      u32 o = d.x_t_off[ex], c = d.x_t_n[ex];
+      u32 lastq = INVALID;
+      for (u32 k0 = 0; k0 < c; k0 += 64) {
+        u32 t = o + k0 + lane;
+        bool v = k0 + lane < c;
+        u32 q = v ? d.t_queue[t] : INVALID;
+        bool hit = v && topic_bind_hit(d, pb, p, t);
+        // bindings are sorted by queue: a queue is emitted once, by its first hit
+        u64 hm = __ballot(hit);
+        u64 below = hm & lanemask_lt();
+        u32 qb = (u32)__shfl((int)q, below ? 63 - __clzll(below) : 0);  // nearest lower hit
+        u32 qtop = (u32)__shfl((int)q, hm ? 63 - __clzll(hm) : 0);     // highest hit
+        bool emit = hit && (below ? qb : lastq) != q;
+        route_emit<PASS>(d, a, p, wbase, srank, q, emit, lane);
+        if (hm) lastq = qtop;
       }
     }
   }
-#undef EMIT
-  if (PASS == 0) {
+  if (PASS == 0 && lane == 0) {
+    u32 nq = a.nq, rmask = a.rmask;
     u32 ret = 0;
     if (pb.flags & MF_IMPORTED) {
       rmask = 0;  // imported records are never forwarded again
-    } else if (pb.exch < 0) {
+    } else if (ex < 0) {
       atomicAdd(&d.ctr->n_unknown_exchange, 1u);
       u32 ri = atomicAdd(&d.ctr->n_ctrl, 1u);
       CtrlRec rec;
       rec.conn = pb.conn; rec.off = INVALID; rec.len = 404; rec.seg = pb.chslot;
       if (ri < d.seg_max * 2) d.ctrl_rec[ri] = rec;
-    } else if (nq_all == 0) {
+    } else if (a.nq_all == 0) {
       atomicAdd(&d.ctr->n_unroutable, 1u);
       if (pb.flags & MF_MANDATORY) ret = 312;
-    } else if ((pb.flags & MF_IMMEDIATE) && !has_cons) {
+    } else if ((pb.flags & MF_IMMEDIATE) && !a.has_cons) {
       ret = 313;
       nq = 0;  // spec behaviour: not enqueued (SURVEY A.Q16/CHANGES.md)
     }
     d.pub_ret[p] = ret;
-    if (sharded) d.pub_rmask[p] = ret ? 0 : rmask;
+    if (d.world > 1) d.pub_rmask[p] = ret ? 0 : rmask;
     u32 meta = align16(pb.ex_len + pb.rk_len + pb.props_len);
     u32 slot = nq ? align16(meta + pb.body_size) : 0;
     d.pub_nq[p] = nq;
@@ -1243,9 +1327,21 @@ __global__ void k_route(DS d) {
   }
 }
 
+DEV void log_reserve(const DS& d);
+template <int PASS>
+__global__ __launch_bounds__(256) void k_route(DS d) {
+  // pass 1 also reserves the phase's body-log region (consumed by k_store, next kernel)
+  if (PASS == 1 && blockIdx.x == 0 && threadIdx.x == 0) log_reserve(d);
+  const u32 lane = lane_id();
+  const u32 nw = (gridDim.x * blockDim.x) >> 6;
+  u32 n = d.tot[TS_RANGE_HI];
+  if (n > d.pub_cap) n = d.pub_cap;
+  for (u32 p = d.tot[TS_RANGE_LO] + ((blockIdx.x * blockDim.x + threadIdx.x) >> 6); p < n; p += nw)
+    route_one<PASS>(d, p, lane);
+}
+
 // reserve the step's contiguous body-log region and message-table indices
-__global__ void k_log_reserve(DS d) {
-  if (threadIdx.x) return;
+DEV void log_reserve(const DS& d) {
   u32 total = d.tot[1];     // slot bytes
   u32 routed = d.tot[2];    // routed messages
   u32 np = d.tot[TS_PAIR_BASE] + d.tot[0];
@@ -1268,6 +1364,7 @@ __global__ void k_log_reserve(DS d) {
   *d.msg_free_top = d.tot[8] - routed;
   d.ctr->n_routed_msgs += routed;
 }
+__global__ void k_log_reserve(DS d) { if (threadIdx.x == 0) log_reserve(d); }
 
 // one wave per publish: allocate, fill MsgEnt, copy exchange/rk/props/body into the log
 DEV void store_one(const DS& d, u32 p, u32 lane);
@@ -2073,8 +2170,7 @@ __global__ void k_post2(DS d) {
   if (i < d.c_max) d.conn_ret_bytes[i] = 0;
 }
 
-__global__ void k_final(DS d) {
-  if (threadIdx.x != 0) return;
+DEV void final_step(const DS& d) {
   // advance the log tail over fully released blocks (K11)
   u64 head = *d.log_head, tail = *d.log_tail;
   while (tail < head) {
@@ -2092,6 +2188,30 @@ __global__ void k_final(DS d) {
   c->n_live_msgs = d.msg_max - *d.msg_free_top;
   *d.ctr_host = *c;
 }
+__global__ void k_final(DS d) { if (threadIdx.x == 0) final_step(d); }
+
+// copy the step's small host-visible results to their host-mapped mirrors in one pass
+// (16-B stores, grid-stride) once the whole step has run
+DEV void copy16(u8* dst, const u8* src, u64 n, u64 gtid, u64 gsz) {
+  u64 nv = n >> 4;
+  for (u64 i = gtid; i < nv; i += gsz) ((uint4*)dst)[i] = ((const uint4*)src)[i];
+  for (u64 i = (nv << 4) + gtid; i < n; i += gsz) dst[i] = src[i];
+}
+
+DEV void final_step(const DS& d);
+__global__ __launch_bounds__(256) void k_host_out(DS d) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) final_step(d);   // log tail, counters -> host
+  const u64 gtid = blockIdx.x * blockDim.x + threadIdx.x, gsz = (u64)gridDim.x * blockDim.x;
+  u32 nseg = d.in->nseg;
+  copy16((u8*)d.seg_out_h, (const u8*)d.seg_out, (u64)nseg * sizeof(SegOut), gtid, gsz);
+  copy16((u8*)d.conn_out_h, (const u8*)d.conn_out, (u64)d.c_max * sizeof(ConnOut), gtid, gsz);
+  u32 nc = d.ctr->n_ctrl;
+  if (nc > d.seg_max * 2) nc = d.seg_max * 2;
+  copy16((u8*)d.ctrl_rec_h, (const u8*)d.ctrl_rec, (u64)nc * sizeof(CtrlRec), gtid, gsz);
+  u64 cb = d.ctr->ctrl_bytes;
+  if (cb > d.ctrl_cap) cb = d.ctrl_cap;
+  copy16(d.ctrl_h, d.ctrl, cb, gtid, gsz);
+}
 
 // ============================================================================ requeue (pre-step)
 // one block per queue with requeued items: gather, bitonic-sort by queue position,
@@ -2102,6 +2222,7 @@ __global__ __launch_bounds__(256) void k_requeue(DS d) {
   __shared__ u32 kidx[REQ_BLK];
   __shared__ u32 cnt;
   u32 q = blockIdx.x;
+  if (q == 0 && threadIdx.x == 0) *d.n_dirty = 0;   // fused k_reset_dirty (after k_chan_advance)
   if (q >= d.q_max || d.req_q_n[q] == 0) return;
   u32 tid = threadIdx.x;
   if (tid == 0) cnt = 0;

@@ -31,13 +31,19 @@ struct DS {
   StepIn* in;
   const SegIn* segs;
   const u8* ingress;
-  SegOut* seg_out;          // host-mapped
+  SegOut* seg_out;          // device; published to seg_out_h at the end of the step
   Counters* ctr;            // device
   Counters* ctr_host;       // host-mapped
-  u8* egress;               // host-mapped
-  ConnOut* conn_out;        // host-mapped [c_max]
-  u8* ctrl;                 // host-mapped
-  CtrlRec* ctrl_rec;        // host-mapped [seg_max * 2]
+  u8* egress;               // device (D2H DMA by the host)
+  ConnOut* conn_out;        // device [c_max]
+  u8* ctrl;                 // device
+  CtrlRec* ctrl_rec;        // device [seg_max * 2]
+  // host-mapped mirrors, written once by k_host_out after every other kernel: mid-step
+  // stores over PCIe would queue behind the previous step's egress DMA
+  SegOut* seg_out_h;
+  ConnOut* conn_out_h;
+  u8* ctrl_h;
+  CtrlRec* ctrl_rec_h;
 
   // ---------------- per connection
   u8* carry;                // [c_max][carry_cap]

@@ -115,12 +115,16 @@ class Engine {
       io.in = (StepIn*)dev(("in" + sfx).c_str(), sizeof(StepIn));
       io.segs = (const SegIn*)dev(("segs" + sfx).c_str(), sizeof(SegIn) * d_.seg_max);
       io.ingress = (const u8*)dev(("ingress" + sfx).c_str(), d_.ingress_cap + 64);
-      io.seg_out = (SegOut*)hst(("seg_out" + sfx).c_str(), sizeof(SegOut) * d_.seg_max);
+      io.seg_out = (SegOut*)dev(("seg_out_d" + sfx).c_str(), sizeof(SegOut) * d_.seg_max);
+      io.seg_out_h = (SegOut*)hst(("seg_out" + sfx).c_str(), sizeof(SegOut) * d_.seg_max);
       io.ctr_host = (Counters*)hst(("ctr_host" + sfx).c_str(), sizeof(Counters));
       io.egress = (u8*)dev(("egress" + sfx).c_str(), egress_alloc_);
-      io.conn_out = (ConnOut*)hst(("conn_out" + sfx).c_str(), sizeof(ConnOut) * d_.c_max);
-      io.ctrl = (u8*)hst(("ctrl" + sfx).c_str(), d_.ctrl_cap);
-      io.ctrl_rec = (CtrlRec*)hst(("ctrl_rec" + sfx).c_str(), sizeof(CtrlRec) * d_.seg_max * 2);
+      io.conn_out = (ConnOut*)dev(("conn_out_d" + sfx).c_str(), sizeof(ConnOut) * d_.c_max);
+      io.conn_out_h = (ConnOut*)hst(("conn_out" + sfx).c_str(), sizeof(ConnOut) * d_.c_max);
+      io.ctrl = (u8*)dev(("ctrl_d" + sfx).c_str(), d_.ctrl_cap);
+      io.ctrl_h = (u8*)hst(("ctrl" + sfx).c_str(), d_.ctrl_cap);
+      io.ctrl_rec = (CtrlRec*)dev(("ctrl_rec_d" + sfx).c_str(), sizeof(CtrlRec) * d_.seg_max * 2);
+      io.ctrl_rec_h = (CtrlRec*)hst(("ctrl_rec" + sfx).c_str(), sizeof(CtrlRec) * d_.seg_max * 2);
       io.xchg = (u32*)hst(("xchg" + sfx).c_str(), 4ull * (4 * WORLD_MAX + 4));
       egress_host_[p] = (u8*)pinned(("egress_host" + sfx).c_str(), egress_alloc_);
       stage_in_[p] = (StepIn*)pinned(("stage_in" + sfx).c_str(), sizeof(StepIn));
@@ -274,6 +278,14 @@ class Engine {
     d_.hist = (u32*)dev("hist", 4ull * 256 * ntiles_max_);
     d_.hist_scan = (u32*)dev("hist_scan", 4ull * 256 * ntiles_max_);
     d_.scan_tmp = (u32*)dev("scan_tmp", 4ull * 1024);
+    {   // look-back scan state: status words for the largest scan, ticket/epoch
+      u64 big = d_.pub_cap > d_.cmd_max ? d_.pub_cap : d_.cmd_max;
+      big = big > d_.deliv_max ? big : d_.deliv_max;
+      big = big > d_.c_max ? big : d_.c_max;
+      scan_smax_ = ceil_div(big, SCAN_TILE) + 1;
+      scan_status_ = (u64*)dev("scan_status", 8ull * 4 * scan_smax_);
+      scan_ctl_ = (u32*)dev("scan_ctl", 64);
+    }
     d_.tot = (u32*)dev("tot", 4ull * 128);
     d_.egress_budget = (u32*)dev("egress_budget", 4);
     d_.dbg = (u64*)dev("dbg", 8ull * 16 * d_.seg_max);
@@ -283,6 +295,8 @@ class Engine {
       io.in = io_[p].in; io.segs = io_[p].segs; io.ingress = io_[p].ingress; io.seg_out = io_[p].seg_out;
       io.ctr_host = io_[p].ctr_host; io.egress = io_[p].egress; io.conn_out = io_[p].conn_out;
       io.ctrl = io_[p].ctrl; io.ctrl_rec = io_[p].ctrl_rec; io.xchg = io_[p].xchg;
+      io.seg_out_h = io_[p].seg_out_h; io.conn_out_h = io_[p].conn_out_h; io.ctrl_h = io_[p].ctrl_h;
+      io.ctrl_rec_h = io_[p].ctrl_rec_h;
       io_[p] = io;
     }
     HIPCHECK(hipStreamCreateWithFlags(&s_comp_, hipStreamNonBlocking));
@@ -572,7 +586,8 @@ class Engine {
     a.n = n;
     a.nmax = nmax;
     a.tot_slot = slot;
-    hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, s, a, d_.tot);
+    u32 nb = ceil_div(nmax ? nmax : 1, SCAN_TILE);
+    hipLaunchKernelGGL(k_scan, dim3(nb), dim3(1024), 0, s, a, d_.tot, scan_status_, scan_ctl_, scan_smax_);
   }
 
   // returns index (0/1) of the buffer holding the sorted output
@@ -602,7 +617,6 @@ class Engine {
     hipLaunchKernelGGL(k_classify, blocks(d.cmd_max, 256), dim3(256), 0, s, d);
     launch_scan(s, {{d.cmd_is_pub, d.cmd_pub_rank}, {d.cmd_is_ack, d.cmd_ack_rank}}, &d.ctr->n_cmds,
                 d.cmd_max, 4);
-    hipLaunchKernelGGL(k_set_counts, dim3(1), dim3(64), 0, s, d);
     hipLaunchKernelGGL(k_decode, blocks(d.cmd_max, 256), dim3(256), 0, s, d);
   }
 
@@ -612,11 +626,10 @@ class Engine {
       u64 waves = (u64)((nmax + 15) / 16) * (d.tb_pad / 16);
       hipLaunchKernelGGL(k_topic_mfma, wave_blocks(waves), dim3(256), 0, s, d);
     }
-    hipLaunchKernelGGL(k_route<0>, blocks(nmax, 256), dim3(256), 0, s, d);
+    hipLaunchKernelGGL(k_route<0>, wave_blocks(nmax), dim3(256), 0, s, d);
     launch_scan(s, {{d.pub_nq, d.pub_pair_off}, {d.pub_slot, d.pub_slot_off}, {d.pub_routed, d.pub_routed_rank}},
                 &d.tot[TS_RANGE_HI], d.pub_cap, 0, &d.tot[TS_RANGE_LO]);
-    hipLaunchKernelGGL(k_route<1>, blocks(nmax, 256), dim3(256), 0, s, d);
-    hipLaunchKernelGGL(k_log_reserve, dim3(1), dim3(64), 0, s, d);
+    hipLaunchKernelGGL(k_route<1>, wave_blocks(nmax), dim3(256), 0, s, d);
     hipLaunchKernelGGL(k_store, wave_blocks(nmax), dim3(256), 0, s, d);
     hipLaunchKernelGGL(k_live_add, blocks(nmax, 256), dim3(256), 0, s, d);
   }
@@ -648,7 +661,6 @@ class Engine {
     hipLaunchKernelGGL(k_enqueue, blocks(d.pair_max, 256), dim3(256), 0, s, d, psrc);
     hipLaunchKernelGGL(k_acks, blocks(d.ack_max, 256), dim3(256), 0, s, d);
     hipLaunchKernelGGL(k_chan_advance, blocks((u64)nch * 64, 256), dim3(256), 0, s, d);
-    hipLaunchKernelGGL(k_reset_dirty, dim3(1), dim3(64), 0, s, d);
     // requeued deliveries go back in front of their queues' heads before this step's
     // dispatch, in queue-offset order (QueueEntity.scala:415-446)
     hipLaunchKernelGGL(k_requeue, dim3(d.q_max), dim3(256), 0, s, d);
@@ -669,7 +681,7 @@ class Engine {
     u64 pn = d.deliv_max > d.c_max ? d.deliv_max : d.c_max;
     hipLaunchKernelGGL(k_post, blocks(pn, 256), dim3(256), 0, s, d, dsrc);
     hipLaunchKernelGGL(k_post2, blocks(d.c_max, 256), dim3(256), 0, s, d);
-    hipLaunchKernelGGL(k_final, dim3(1), dim3(64), 0, s, d);
+    hipLaunchKernelGGL(k_host_out, dim3(64), dim3(256), 0, s, d);
   }
 
   // world == 1: the whole step; world > 1: phase A (ingest, local route, pack)
@@ -712,6 +724,9 @@ class Engine {
   u64 total_bytes_ = 0;
   u64 egress_alloc_ = 0;
   u32 ntiles_max_ = 0;
+  u64* scan_status_ = nullptr;
+  u32* scan_ctl_ = nullptr;
+  u32 scan_smax_ = 0;
   bool graph_enabled_ = true;
   hipGraphExec_t graph_exec_[2] = {nullptr, nullptr};
   hipGraphExec_t graph_b_[2] = {nullptr, nullptr};
