@@ -33,22 +33,25 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 METRIC = "msgs/sec (whole node) + p50 publish→deliver latency, 1 KB payload, 1/2/4/8 GPUs"
 
 
-def build_workload(dp, rank, producers, queues, body, chunk, blocks, cons_base, shards=1):
+def build_workload(dp, rank, producers, queues, body, chunk, blocks, cons_base, shards=1, kind="topic"):
     """``shards`` > 1: the replicated topology of a sharded broker (every rank declares
-    every queue; queue bench.q.{r}.{i} is placed on rank r and consumed there)."""
+    every queue; queue bench.q.{r}.{i} is placed on rank r and consumed there).
+    kind "topic" = config 2 (``queues`` per rank, one key pattern each); "fanout" =
+    config 3 (every publish goes to every queue of the node)."""
     from chanamq_amd.engine.layout import SEG_IN
     from chanamq_amd.engine.traffic import even_split, publish_stream
 
     vh = "AMQ.DEFAULT"
-    dp.declare_exchange(vh, "bench.topic", "topic")
+    xname = "bench.topic" if kind == "topic" else "bench.fanout"
+    dp.declare_exchange(vh, xname, kind)
     owners = range(shards) if shards > 1 else [rank]
     for r in owners:
         for i in range(queues):
             qn = f"bench.q.{r}.{i}"
             if shards > 1:
                 dp.shard_map.place(vh, qn, r)
-            dp.declare_queue(vh, qn, capacity=1 << 20)
-            dp.bind(vh, qn, "bench.topic", f"bench.{r}.{i}.*")
+            dp.declare_queue(vh, qn, capacity=1 << 20 if kind == "topic" else 1 << 14)
+            dp.bind(vh, qn, xname, f"bench.{r}.{i}.*" if kind == "topic" else "")
     for p in range(producers):
         dp.open_connection(p, vh)
         dp.open_channel(p, 1)
@@ -58,13 +61,13 @@ def build_workload(dp, rank, producers, queues, body, chunk, blocks, cons_base, 
         dp.open_channel(c, 1)
         dp.consume(c, 1, vh, f"bench.q.{rank}.{i}", f"ctag-{i}", no_ack=True)
     # one message on the wire is ~1.08 KB; each producer gets `blocks` chunks of ~chunk bytes
-    probe = publish_stream(1, "bench.topic", lambda i: f"bench.{rank}.0.x0", body)
+    probe = publish_stream(1, xname, lambda i: f"bench.{rank}.0.x0", body)
     per_prod = max(1, (chunk * blocks) // len(probe))
     streams = []
     nq = queues * len(owners)
     for p in range(producers):
         rng_q = np.random.default_rng(1000 + rank * 7919 + p).integers(0, nq, size=per_prod)
-        s = publish_stream(per_prod, "bench.topic",
+        s = publish_stream(per_prod, xname,
                            lambda i, r=rng_q: f"bench.{owners[r[i] // queues]}.{r[i] % queues}.x{i % 10}", body,
                            seed=p)
         streams.append(even_split(s, blocks))
@@ -101,6 +104,11 @@ def main():
     ap.add_argument("--chunk", type=int, default=65536, help="bytes per producer per step (TCP read)")
     ap.add_argument("--blocks", type=int, default=8)
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--copy-engine", choices=["sdma", "blit"], default="sdma",
+                    help="step IO copies on the SDMA engines (default) or runtime blit kernels")
+    ap.add_argument("--workload", choices=["topic", "fanout"], default="topic",
+                    help="topic = BASELINE config 2 (default, the headline); fanout = config 3 "
+                         "(--queues is then the node total, default 1024, with small publish batches)")
     ap.add_argument("--mode", choices=["sharded", "independent"], default="sharded",
                     help="N>1: one sharded broker (cross-GPU routing over RCCL) or N unconnected shards")
     args = ap.parse_args()
@@ -124,21 +132,32 @@ def main():
             dist.init_process_group(backend)
     from chanamq_amd.engine.dataplane import GpuDataPlane
 
-    P, Q = args.producers, args.queues
+    fan = args.workload == "fanout"
+    if fan and args.queues == 16:
+        args.queues = 1024
+    if fan and args.producers == 256:
+        args.producers, args.chunk = 16, 4096
     shards = world if (world > 1 and args.mode == "sharded") else 1
+    P = args.producers
+    Q = max(1, args.queues // shards) if fan else args.queues    # queues per rank
     qtot = Q * shards
-    cfg = dict(c_max=max(1024, P + Q + 1), chpc=4, q_max=max(64, qtot * 2), cons_max=1024,
-               seg_max=max(1024, P + Q), cmd_max=1 << 17, deliv_max=1 << 16, msg_max=1 << 22, ucap=4096,
-               deliver_cap=8192, ingress_cap=max(32 << 20, P * args.chunk + (4 << 20)), egress_cap=128 << 20,
-               log_bytes=16 << 30, ring_pool=Q * (1 << 20) + qtot + 1024, tb_max=max(64, qtot), carry_cap=256 << 10,
-               graph=0 if args.no_graph else 1)
+    qcap = (1 << 20) if not fan else (1 << 14)
+    cfg = dict(c_max=max(1024, P + Q + 1), chpc=4, q_max=max(64, qtot * 2), cons_max=max(1024, Q + 16),
+               seg_max=max(1024, P + Q), cmd_max=1 << 17, deliv_max=(1 << 16) if not fan else (1 << 18),
+               msg_max=1 << 22, ucap=4096, deliver_cap=8192,
+               ingress_cap=max(32 << 20, P * args.chunk + (4 << 20)),
+               egress_cap=(128 << 20) if not fan else (320 << 20),
+               log_bytes=16 << 30, ring_pool=Q * qcap + qtot + 1024, tb_max=max(64, qtot) if not fan else 64,
+               fan_max=max(1 << 20, qtot * 2), carry_cap=256 << 10, graph=0 if args.no_graph else 1,
+               copy_engine=1 if args.copy_engine == "sdma" else 0)
     if shards > 1:
         from chanamq_amd.parallel.exchange import Exchanger
         dp = GpuDataPlane(device=local, worker=rank, world=world, rank=rank, exchanger=Exchanger(), **cfg)
     else:
         dp = GpuDataPlane(device=local, worker=rank, **cfg)
     pool, segs, offs, blens, mps, msg_bytes = build_workload(dp, rank, P, Q, args.body, args.chunk,
-                                                             args.blocks, cons_base=P, shards=shards)
+                                                             args.blocks, cons_base=P, shards=shards,
+                                                             kind=args.workload)
     base = pool.ctypes.data
     step_i = 0
 
@@ -228,8 +247,10 @@ def main():
             "dtype": "uint8 (AMQP wire bytes; no floating-point compute)",
             "data": "synthetic AMQP 0-9-1 publish traffic (random 1 KB bodies), empty-init broker state",
             "config": {
-                "model": f"BASELINE config 2: 1 topic exchange, {Q} bound queues per GPU, {args.body} B msgs, "
-                         "auto-ack, non-persistent",
+                "model": (f"BASELINE config 2: 1 topic exchange, {Q} bound queues per GPU, {args.body} B msgs, "
+                          "auto-ack, non-persistent") if not fan else
+                         (f"BASELINE config 3: fanout exchange -> {qtot} queues ({Q} per GPU), {args.body} B msgs, "
+                          "auto-ack, non-persistent; value = deliveries/s"),
                 "global_batch": int(round(mps * world)),
                 "seq_len": args.body,
                 "parallelism": (f"queue-sharded x{world}: one broker, cross-GPU routing by RCCL all-to-all"

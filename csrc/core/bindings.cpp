@@ -6,6 +6,7 @@
 
 #include "broker.hpp"
 #include "codec.hpp"
+#include "gateway.hpp"
 #include "loadgen.hpp"
 #include "store.hpp"
 
@@ -137,6 +138,42 @@ PYBIND11_MODULE(_core, m) {
              if (!s.selectVhost(id, &a)) return py::none();
              return py::bool_(a);
            });
+
+  py::class_<Gateway>(m, "Gateway")
+      .def(py::init<const std::string&, int, uint32_t, bool>(), py::arg("host") = "127.0.0.1", py::arg("port") = 0,
+           py::arg("max_conns") = 1024, py::arg("reuseport") = false)
+      .def_property_readonly("port", &Gateway::port)
+      .def_readonly("rx_bytes", &Gateway::rx_bytes)
+      .def_readonly("tx_bytes", &Gateway::tx_bytes)
+      .def("poll", [](Gateway& g, int timeout_ms, py::buffer buf, uint64_t offset, uint64_t per_conn_cap) {
+             py::buffer_info bi = buf.request(true);
+             uint64_t cap = (uint64_t)bi.size * bi.itemsize;
+             if (offset > cap) throw std::runtime_error("offset beyond buffer");
+             GwPoll r;
+             {
+               py::gil_scoped_release nogil;
+               r = g.poll(timeout_ms, (uint8_t*)bi.ptr + offset, cap - offset, per_conn_cap);
+             }
+             for (auto& s : r.segs) s.src += offset;
+             py::bytes segs((const char*)r.segs.data(), r.segs.size() * sizeof(GwSeg));
+             py::list hs;
+             for (auto& h : r.handshake) hs.append(py::make_tuple(h.first, py::bytes(h.second)));
+             return py::make_tuple(segs, r.used + offset, hs, r.opened, r.closed);
+           }, py::arg("timeout_ms"), py::arg("buf"), py::arg("offset") = 0, py::arg("per_conn_cap") = 1 << 20)
+      .def("send", [](Gateway& g, uint32_t conn, py::bytes b) {
+             std::string s = b;
+             g.send(conn, s.data(), s.size());
+           })
+      .def("send_egress", [](Gateway& g, py::buffer egress, py::buffer conn_out, uint32_t n_slots) {
+             py::buffer_info e = egress.request(), c = conn_out.request();
+             if ((uint64_t)c.size * c.itemsize < 8ull * n_slots) throw std::runtime_error("conn_out too small");
+             py::gil_scoped_release nogil;
+             return g.send_egress((const uint8_t*)e.ptr, (const uint32_t*)c.ptr, n_slots);
+           })
+      .def("flush", &Gateway::flush, py::call_guard<py::gil_scoped_release>())
+      .def("set_data_mode", &Gateway::set_data_mode)
+      .def("close", &Gateway::close)
+      .def("pending_bytes", &Gateway::pending_bytes);
 
   m.def("run_load", [](py::dict d) {
     LoadSpec s;

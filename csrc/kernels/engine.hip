@@ -101,6 +101,10 @@ class Engine {
     if (d_.q_bits + d_.rank_bits > 32) throw std::runtime_error("q_max too large for sharded pair keys");
     d_.ch_bits = bits_for(nch);
     graph_enabled_ = get("graph", 1) != 0;
+    // step IO copies on the SDMA engines (hipMemcpyDeviceToDeviceNoCU): a blit-kernel copy
+    // of a step's egress occupies CUs for the whole PCIe transfer and stalls the next
+    // step's kernels; copy_engine=0 keeps the runtime's default (blit) path
+    sdma_ = get("copy_engine", 1) != 0;
 
     // ---- allocations
     auto dev = [&](const char* name, size_t bytes) { return alloc(name, bytes, false); };
@@ -427,6 +431,7 @@ class Engine {
     o["ingress_cap"] = d_.ingress_cap; o["egress_cap"] = d_.egress_cap; o["ring_pool"] = d_.ring_pool;
     o["work_cap"] = d_.work_cap; o["total_bytes"] = total_bytes_; o["req_max"] = d_.req_max;
     o["world"] = d_.world; o["rank"] = d_.my_rank; o["import_max"] = d_.import_max; o["pub_cap"] = d_.pub_cap;
+    o["copy_engine"] = sdma_ ? "sdma" : "blit";
     o["xfer_desc_max"] = d_.xfer_desc_max; o["xfer_bytes"] = d_.xfer_bytes; o["world_max"] = WORLD_MAX;
     o["sizeof"] = py::dict(py::arg("StepIn") = sizeof(StepIn), py::arg("SegIn") = sizeof(SegIn),
                            py::arg("SegOut") = sizeof(SegOut), py::arg("Counters") = sizeof(Counters),
@@ -465,7 +470,7 @@ class Engine {
     if (sb) HIPCHECK(hipMemcpyAsync((void*)io_[p].segs, stage_segs_[p], sb, hipMemcpyHostToDevice, s_h2d_));
     if (payload_len)
       HIPCHECK(hipMemcpyAsync((void*)io_[p].ingress, (const void*)payload_ptr, payload_len,
-                              hipMemcpyHostToDevice, s_h2d_));
+                              sdma_ ? hipMemcpyDeviceToDeviceNoCU : hipMemcpyHostToDevice, s_h2d_));
     HIPCHECK(hipEventRecord(ev_h2d_[p], s_h2d_));
     HIPCHECK(hipStreamWaitEvent(s_comp_, ev_h2d_[p], 0));
     if (d2h_issued_[p]) HIPCHECK(hipStreamWaitEvent(s_comp_, ev_d2h_[p], 0));  // egress[p] drained
@@ -547,7 +552,9 @@ class Engine {
     const Counters* c = (const Counters*)buf("ctr_host" + std::to_string(p)).ptr;
     u64 n = c->egress_bytes;
     HIPCHECK(hipStreamWaitEvent(s_d2h_, ev_done_[p], 0));
-    if (n) HIPCHECK(hipMemcpyAsync(egress_host_[p], io_[p].egress, n, hipMemcpyDeviceToHost, s_d2h_));
+    if (n)
+      HIPCHECK(hipMemcpyAsync(egress_host_[p], io_[p].egress, n,
+                              sdma_ ? hipMemcpyDeviceToDeviceNoCU : hipMemcpyDeviceToHost, s_d2h_));
     HIPCHECK(hipEventRecord(ev_d2h_[p], s_d2h_));
     d2h_issued_[p] = true;
     return n;
@@ -728,6 +735,7 @@ class Engine {
   u32* scan_ctl_ = nullptr;
   u32 scan_smax_ = 0;
   bool graph_enabled_ = true;
+  bool sdma_ = true;
   hipGraphExec_t graph_exec_[2] = {nullptr, nullptr};
   hipGraphExec_t graph_b_[2] = {nullptr, nullptr};
   hipEvent_t ev_a_[2], ev_ext_[2];
