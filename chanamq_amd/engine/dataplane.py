@@ -410,7 +410,7 @@ class GpuDataPlane(ControlState):
         self.eng.submit_b(self._pending, [int(x) for x in recv], int(stream))
         self._pending = None
 
-    def finish(self, ticket, collect=True, wait_egress=True):
+    def finish(self, ticket, collect=True, wait_egress=True, collect_egress=True):
         p, nseg, t0 = ticket
         self.eng.wait_results(p)
         res = StepResult()
@@ -437,7 +437,7 @@ class GpuDataPlane(ControlState):
                     res.ctrl.append((int(rec["conn"]), bytes(io["ctrl"][o:o + n])))
         if wait_egress or collect:
             self.eng.egress_wait(p)
-        if collect:
+        if collect and collect_egress:
             co = io["conn_out"]
             eg = io["egress"]
             for conn in np.nonzero(co["len"])[0]:
@@ -445,6 +445,11 @@ class GpuDataPlane(ControlState):
                 res.egress[int(conn)] = bytes(eg[o:o + n])
         res.elapsed = time.perf_counter() - t0
         return res
+
+    def host_egress(self, ticket):
+        """(egress bytes view, ConnOut view) of a finished step, for zero-copy socket writes."""
+        io = self._io[ticket[0]]
+        return io["egress"], io["conn_out"]
 
     def egress_wait(self, ticket):
         self.eng.egress_wait(ticket[0])

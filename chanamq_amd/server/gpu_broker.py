@@ -25,6 +25,8 @@ import threading
 import time
 import uuid
 
+import numpy as np
+
 from ..engine.control import ControlError, normalize_vhost
 from ..engine.layout import SS_FRAME_ERROR, SS_OVERFLOW, SS_TOO_LARGE, SS_UNEXPECTED
 from ..protocol import constants as C
@@ -74,8 +76,14 @@ def _frames(buf):
 
 class GpuBroker:
     def __init__(self, plane, host="127.0.0.1", port=0, heartbeat=0, frame_max=131072, channel_max=2047,
-                 idle_step_ms=2.0, product="chanamq-amd", version="0.1.0"):
+                 idle_step_ms=2.0, product="chanamq-amd", version="0.1.0", io="native",
+                 ingress_bytes=64 << 20, per_conn_read=1 << 20):
+        """``io``: "native" = C++ batched gateway (csrc/core/gateway.cpp), "python" =
+        selectors loop (portable fallback)."""
         self.plane = plane
+        self.io = io
+        self.gw = None
+        self.ingress_bytes, self.per_conn_read = ingress_bytes, per_conn_read
         self.host, self.port = host, port
         self.heartbeat, self.frame_max, self.channel_max = heartbeat, frame_max, channel_max
         self.idle_step_s = idle_step_ms / 1000.0
@@ -92,6 +100,19 @@ class GpuBroker:
 
     # ------------------------------------------------------------------ lifecycle
     def start(self):
+        if self.io == "native":
+            from ..broker import load
+            self.gw = load().Gateway(self.host, self.port, self.plane.c_max, False)
+            self.port = self.gw.port
+            if hasattr(self.plane, "mod"):
+                self._pin = self.plane.mod.alloc_pinned(self.ingress_bytes)
+            else:
+                import numpy as np
+                self._pin = np.zeros(self.ingress_bytes, np.uint8)
+            self._running = True
+            self._thread = threading.Thread(target=self._loop_native, name="gpu-broker", daemon=True)
+            self._thread.start()
+            return self
         ls = socket.socket(socket.AF_INET, socket.SOCK_STREAM)
         ls.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
         ls.bind((self.host, self.port))
@@ -114,9 +135,85 @@ class GpuBroker:
         for c in list(self.conns.values()):
             self._drop(c)
         self._sel.close()
-        self._lsock.close()
+        if self._lsock is not None:
+            self._lsock.close()
+        self.gw = None
         os.close(self._wake_r)
         os.close(self._wake_w)
+
+    # ------------------------------------------------------------------ native loop
+    def _loop_native(self):
+        import numpy as np
+
+        from ..engine.layout import SEG_IN
+        gw, pin = self.gw, self._pin
+        gpu = hasattr(self.plane, "eng")
+        last_step = 0.0
+        busy = False
+        while self._running:
+            timeout_ms = 0 if busy else max(1, int(self.idle_step_s * 1000))
+            segs_b, used, hs, opened, closed = gw.poll(timeout_ms, pin, 0, self.per_conn_read)
+            now = time.monotonic()
+            for cid in opened:
+                self.conns[cid] = _Conn(None, cid, None)
+                self.stats["connections"] += 1
+            for cid in closed:
+                c = self.conns.get(cid)
+                if c is not None:
+                    c.state = "gone"
+                    self._drop(c)
+            segs = np.frombuffer(segs_b, SEG_IN).copy()
+            extra = []
+            for cid, data in hs:
+                c = self.conns.get(cid)
+                if c is None:
+                    continue
+                c.last_rx = now
+                rest = self._host_bytes(c, data)
+                if c.state == "open":
+                    gw.set_data_mode(cid, True)
+                if rest:
+                    extra.append((cid, rest))
+            for cid in segs["conn"]:
+                c = self.conns.get(int(cid))
+                if c is not None:
+                    c.last_rx = now
+            if extra:
+                rows = []
+                for cid, data in extra:
+                    off = (used + 15) & ~15
+                    pin[off:off + len(data)] = np.frombuffer(data, np.uint8)
+                    rows.append((cid, len(data), off))
+                    used = off + len(data)
+                segs = np.concatenate([segs, np.array(rows, SEG_IN)])
+            if gpu:
+                have = set(int(x) for x in segs["conn"])
+                add = [(int(cc), 0, 0) for cc in np.nonzero(self.plane.carry)[0]
+                       if int(cc) not in have and int(cc) in self.plane.conns and not self.plane.conns[int(cc)].paused]
+                if add:
+                    segs = np.concatenate([segs, np.array(add, SEG_IN)])
+            open_conns = any(c.state == "open" for c in self.conns.values())
+            if open_conns and (len(segs) or busy or now - last_step >= self.idle_step_s):
+                with self.lock:
+                    busy = self._step_native(segs, used, gpu)
+                last_step = now
+            else:
+                busy = False
+            self._heartbeats(now)
+            self._flush_all()
+            gw.flush()
+
+    def _step_native(self, segs, used, gpu):
+        if not gpu:   # golden plane: bytes per connection
+            inputs = {int(r["conn"]): bytes(self._pin[int(r["src"]):int(r["src"]) + int(r["len"])]) for r in segs}
+            return self._step(inputs)
+        p = self.plane
+        t = p.submit_raw(segs, self._pin.ctypes.data, used, int(time.time() * 1000))
+        res = p.finish(t, collect=True, collect_egress=False)
+        eg, co = p.host_egress(t)
+        self.gw.send_egress(eg, co.view(np.uint32), p.c_max)
+        return self._after_step(res.ctrl, res.events, [(s[0], s[1]) for s in res.segs], res.counters,
+                                bool(len(segs)), bool(co["len"].any()))
 
     # ------------------------------------------------------------------ loop
     def _loop(self):
@@ -171,19 +268,24 @@ class GpuBroker:
         c.last_rx = time.monotonic()
         if c.state == "open":
             inputs[c.id] = inputs.get(c.id, b"") + data
-        elif c.state in ("header", "start", "tune"):
+            return
+        rest = self._host_bytes(c, data)
+        if rest:
+            inputs[c.id] = rest
+
+    def _host_bytes(self, c, data):
+        """Bytes of a connection that is not (yet / any more) on the data plane:
+        handshake, or waiting for Connection.CloseOk.  Returns data-plane leftovers."""
+        if c.state in ("header", "start", "tune"):
             c.inbuf += data
             try:
-                rest = self._handshake(c)
+                return self._handshake(c)
             except _Hard as e:
                 self._conn_close(c, e.code, e.text, e.cls, e.mid)
-                return
             except ControlError as e:
                 self._conn_close(c, e.code, e.text, e.class_id, e.method_id)
-                return
-            if rest:
-                inputs[c.id] = rest
-        elif c.state == "closing":
+            return b""
+        if c.state == "closing":
             c.inbuf += data
             frames, used = _frames(c.inbuf)
             del c.inbuf[:used]
@@ -195,7 +297,8 @@ class GpuBroker:
                             self._send(c, 0, Method("connection.close_ok"))
                         self._flush(c)
                         self._drop(c)
-                        return
+                        return b""
+        return b""
 
     # ------------------------------------------------------------------ handshake (host)
     def _handshake(self, c):
@@ -275,13 +378,19 @@ class GpuBroker:
         else:
             egress, ctrl, events, cnt = res.egress, res.ctrl, res.events, res.counters
             seg_status = [(s[0], s[1]) for s in res.segs]
-        self.stats["steps"] += 1
-        self.stats["published"] += cnt.get("n_pubs", 0)
-        self.stats["delivered"] += cnt.get("n_deliv", 0)
         for conn, data in egress.items():
             c = self.conns.get(conn)
             if c is not None and c.state == "open":
-                c.out += data
+                if self.gw is not None:
+                    self.gw.send(conn, data)
+                else:
+                    c.out += data
+        return self._after_step(ctrl, events, seg_status, cnt, bool(inputs), bool(egress))
+
+    def _after_step(self, ctrl, events, seg_status, cnt, had_input, had_egress):
+        self.stats["steps"] += 1
+        self.stats["published"] += cnt.get("n_pubs", 0)
+        self.stats["delivered"] += cnt.get("n_deliv", 0)
         for conn, code, chslot in events:
             c = self.conns.get(conn)
             if c is None or c.state != "open":
@@ -310,7 +419,7 @@ class GpuBroker:
                     self._conn_close(c, e.code, e.text, e.cls, e.mid)
             if c.state == "open":
                 self.plane.unpause(conn)
-        return bool(inputs) or bool(egress) or bool(ctrl) or cnt.get("n_deliv", 0) > 0
+        return had_input or had_egress or bool(ctrl) or cnt.get("n_deliv", 0) > 0
 
     def _chan_of_slot(self, conn, chslot):
         cc = self.plane.conns.get(conn)
@@ -494,6 +603,11 @@ class GpuBroker:
     def _flush(self, c):
         if not c.out or c.state == "closed":
             return
+        if self.gw is not None:
+            self.gw.send(c.id, bytes(c.out))
+            c.out.clear()
+            c.last_tx = time.monotonic()
+            return
         try:
             n = c.sock.send(c.out)
         except (BlockingIOError, InterruptedError):
@@ -523,19 +637,26 @@ class GpuBroker:
             return
         prev = c.state
         c.state = "closed"
-        try:
-            self._sel.unregister(c.sock)
-        except (KeyError, ValueError):
-            pass
-        try:
-            c.sock.close()
-        except OSError:
-            pass
+        if self.gw is not None:
+            if prev != "gone":
+                self._flush(c)
+                self.gw.flush()
+                self.gw.close(c.id)
+        else:
+            try:
+                self._sel.unregister(c.sock)
+            except (KeyError, ValueError):
+                pass
+            try:
+                c.sock.close()
+            except OSError:
+                pass
         if prev in ("open",) or c.id in self.plane.conns:
             with self.lock:
                 self.plane.close_connection(c.id)
         self.conns.pop(c.id, None)
-        self._free.append(c.id)
+        if self.gw is None:
+            self._free.append(c.id)
 
 
 __all__ = ["GpuBroker", "encode_table"]

@@ -1232,6 +1232,7 @@ DEV void route_one(const DS& d, u32 p, u32 lane) {
   // (source rank, connection, publish order) whichever rank owns it
   const u32 srank = (pb.flags & MF_IMPORTED) ? pb.pad : d.my_rank;
   if (PASS == 1) {
+    if (lane == 0 && d.pub_ret_sz[p]) atomicMin(&d.conn_ret_min[pb.conn], d.pub_ret_off[p]);
     u32 nq0 = d.pub_nq[p];
     if (nq0 == 0) return;
     if (wbase + nq0 > d.pair_max) return;  // capacity: k_log_reserve clamps the pair count
@@ -1310,8 +1311,10 @@ DEV void route_one(const DS& d, u32 p, u32 lane) {
     d.pub_routed[p] = nq ? 1 : 0;
     pb.nq = nq;
     pb.slot_bytes = slot;
+    u32 rsz = 0;
     if (ret) {
-      // reserve bytes in the connection's return region
+      // bytes in the connection's return region; the offset comes from the publish-order
+      // scan of pub_ret_sz (returns keep publish order within a connection)
       u32 tl = ret == 312 ? 49u : 72u;  // reply texts (ErrorCodes.scala:23-31)
       u32 sz = (8 + 4 + 2 + 1 + tl + 1 + pb.ex_len + 1 + pb.rk_len) /*method*/ +
                (8 + 12 + pb.props_len) /*header*/;
@@ -1319,11 +1322,12 @@ DEV void route_one(const DS& d, u32 p, u32 lane) {
       u32 fmb = fm ? fm - 8 : 0xffffffffu;
       u32 nb = pb.body_size ? (pb.body_size + fmb - 1) / fmb : 0;
       sz += pb.body_size + 8 * nb;
-      u32 roff = atomicAdd(&d.conn_ret_bytes[pb.conn], sz);
-      pb.pad = roff;
+      atomicAdd(&d.conn_ret_bytes[pb.conn], sz);
+      rsz = sz;
       u32 ri = atomicAdd(&d.ctr->n_returns, 1u);
       if (ri < d.pub_max) d.ret_list[ri] = p;
     }
+    d.pub_ret_sz[p] = rsz;
   }
 }
 
@@ -2091,7 +2095,7 @@ __global__ __launch_bounds__(256) void k_render_returns(DS d) {
   u32 p = d.ret_list[i];
   const Pub pb = d.pubs[p];
   u32 code = d.pub_ret[p];
-  u8* o = d.egress + (u64)d.conn_base[pb.conn] + pb.pad;
+  u8* o = d.egress + (u64)d.conn_base[pb.conn] + (d.pub_ret_off[p] - d.conn_ret_min[pb.conn]);
   const u8* w = d.work;
   // channel number from the publish command's frame
   u32 chno = d.ch_num[pb.chslot];
@@ -2167,7 +2171,7 @@ __global__ void k_post(DS d, u32 src) {
 
 __global__ void k_post2(DS d) {
   u32 i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < d.c_max) d.conn_ret_bytes[i] = 0;
+  if (i < d.c_max) { d.conn_ret_bytes[i] = 0; d.conn_ret_min[i] = INVALID; }
 }
 
 DEV void final_step(const DS& d) {

@@ -86,6 +86,9 @@ struct DS {
   u32* pub_slot_off;
   u32* pub_routed_rank;
   u32* pub_ret;             // 0 / 312 / 313
+  u32* pub_ret_sz;          // rendered Basic.Return bytes of the publish (0 = none)
+  u32* pub_ret_off;         // exclusive scan of pub_ret_sz (publish order)
+  u32* conn_ret_min;        // per connection: smallest pub_ret_off (0xffffffff none)
   u32* ret_list;            // pub indices with returns
   Ack* acks;
 

@@ -173,6 +173,9 @@ class Engine {
     d_.pub_routed_rank = (u32*)dev("pub_routed_rank", 4ull * d_.pub_cap);
     d_.pub_ret = (u32*)dev("pub_ret", 4ull * d_.pub_cap);
     d_.ret_list = (u32*)dev("ret_list", 4ull * d_.pub_cap);
+    d_.pub_ret_sz = (u32*)dev("pub_ret_sz", 4ull * d_.pub_cap);
+    d_.pub_ret_off = (u32*)dev("pub_ret_off", 4ull * d_.pub_cap);
+    d_.conn_ret_min = (u32*)dev("conn_ret_min", 4ull * d_.c_max);
     u64 xw = d_.world > 1 ? (u64)d_.world * d_.pub_cap : 64;
     d_.q_owner = (u32*)dev("q_owner", 4ull * d_.q_max);
     d_.pub_rmask = (u32*)dev("pub_rmask", 4ull * d_.pub_cap);
@@ -315,6 +318,7 @@ class Engine {
     }
     // ---- initial state
     fill("conn_dfirst", 0xff);
+    fill("conn_ret_min", 0xff);
     fill("conn_dlast", 0xff);
     fill("x_hval", 0xff);
     fill("d_exch", 0xff);
@@ -634,7 +638,8 @@ class Engine {
       hipLaunchKernelGGL(k_topic_mfma, wave_blocks(waves), dim3(256), 0, s, d);
     }
     hipLaunchKernelGGL(k_route<0>, wave_blocks(nmax), dim3(256), 0, s, d);
-    launch_scan(s, {{d.pub_nq, d.pub_pair_off}, {d.pub_slot, d.pub_slot_off}, {d.pub_routed, d.pub_routed_rank}},
+    launch_scan(s, {{d.pub_nq, d.pub_pair_off}, {d.pub_slot, d.pub_slot_off}, {d.pub_routed, d.pub_routed_rank},
+                    {d.pub_ret_sz, d.pub_ret_off}},
                 &d.tot[TS_RANGE_HI], d.pub_cap, 0, &d.tot[TS_RANGE_LO]);
     hipLaunchKernelGGL(k_route<1>, wave_blocks(nmax), dim3(256), 0, s, d);
     hipLaunchKernelGGL(k_store, wave_blocks(nmax), dim3(256), 0, s, d);

@@ -22,10 +22,12 @@ def make_plane(kind):
     return GpuDataPlane(default_queue_capacity=1 << 12, **GPU_CFG)
 
 
-@pytest.fixture(params=["golden", pytest.param("gpu", marks=pytest.mark.gpu)])
+@pytest.fixture(params=["golden-native", "golden-python", pytest.param("gpu-native", marks=pytest.mark.gpu),
+                        pytest.param("gpu-python", marks=pytest.mark.gpu)])
 def broker(request):
     from chanamq_amd.server.gpu_broker import GpuBroker
-    b = GpuBroker(make_plane(request.param), idle_step_ms=1.0).start()
+    kind, io = request.param.split("-")
+    b = GpuBroker(make_plane(kind), idle_step_ms=1.0, io=io, ingress_bytes=8 << 20).start()
     yield b
     b.stop()
 
