@@ -290,6 +290,11 @@ class GpuDataPlane(ControlState):
     def _u64(self, name, idx):
         return int(np.frombuffer(self.eng.download(name, idx * 8, 8), np.uint64)[0])
 
+    def memory_in_use(self):
+        """Body-log bytes held by live messages (after the last finished step)."""
+        c = getattr(self, "last_counters", None)
+        return int(c["log_head"] - c["log_tail"]) if c else 0
+
     def message_count(self, q):
         """Ready messages of queue slot ``q`` (AMQP Queue.DeclareOk message-count)."""
         return self._u64("q_tail", q) - self._u64("q_head", q)
@@ -415,6 +420,7 @@ class GpuDataPlane(ControlState):
         self.eng.wait_results(p)
         res = StepResult()
         res.counters = c = self.eng.counters(p)
+        self.last_counters = c
         io = self._io[p]
         so = io["seg_out"][:nseg]
         self.carry[so["conn"]] = so["carry"]

@@ -78,6 +78,15 @@ class GoldenDataPlane(ControlState):
         self.qpos_head[q.slot] = 0
         self.qrr[q.slot] = 0
 
+    def memory_in_use(self):
+        seen, tot = set(), 0
+        for ring in self.ring.values():
+            for m, _, _ in ring:
+                if id(m) not in seen:
+                    seen.add(id(m))
+                    tot += len(m.ex) + len(m.rk) + len(m.props) + len(m.body)
+        return tot
+
     def message_count(self, q):
         return len(self.ring[q])
 

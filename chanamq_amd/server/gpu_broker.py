@@ -37,7 +37,7 @@ HEARTBEAT = C.HEARTBEAT_FRAME
 
 class _Conn:
     __slots__ = ("sock", "id", "state", "inbuf", "out", "frame_max", "heartbeat", "last_rx", "last_tx",
-                 "closing_channels", "last_queue", "peer", "user")
+                 "closing_channels", "last_queue", "peer", "user", "cap_blocked")
 
     def __init__(self, sock, cid, peer):
         self.sock, self.id, self.peer = sock, cid, peer
@@ -50,6 +50,7 @@ class _Conn:
         self.closing_channels = set()
         self.last_queue = {}    # channel -> last declared queue name (AMQP empty-name rule)
         self.user = ""
+        self.cap_blocked = False
 
 
 class _Hard(Exception):
@@ -77,13 +78,18 @@ def _frames(buf):
 class GpuBroker:
     def __init__(self, plane, host="127.0.0.1", port=0, heartbeat=0, frame_max=131072, channel_max=2047,
                  idle_step_ms=2.0, product="chanamq-amd", version="0.1.0", io="native",
-                 ingress_bytes=64 << 20, per_conn_read=1 << 20):
+                 ingress_bytes=64 << 20, per_conn_read=1 << 20, mem_high_watermark=0, mem_low_watermark=0):
         """``io``: "native" = C++ batched gateway (csrc/core/gateway.cpp), "python" =
         selectors loop (portable fallback)."""
         self.plane = plane
         self.io = io
         self.gw = None
         self.ingress_bytes, self.per_conn_read = ingress_bytes, per_conn_read
+        # back-pressure (SURVEY A.Q17 / config 5): above the high watermark of stored
+        # message bytes publishers get Connection.Blocked (if they announced the
+        # capability) or Channel.Flow(active=false); released below the low watermark
+        self.mem_high, self.mem_low = mem_high_watermark, mem_low_watermark or mem_high_watermark // 2
+        self.blocked = False
         self.host, self.port = host, port
         self.heartbeat, self.frame_max, self.channel_max = heartbeat, frame_max, channel_max
         self.idle_step_s = idle_step_ms / 1000.0
@@ -327,6 +333,8 @@ class GpuBroker:
                 raise _Hard(C.UNEXPECTED_FRAME, "unexpected frame during handshake")
             m = decode_method(payload)
             if m.name == "connection.start_ok" and c.state == "start":
+                caps = (m.client_properties or {}).get("capabilities") or {}
+                c.cap_blocked = bool(caps.get("connection.blocked", False)) if isinstance(caps, dict) else False
                 mech = m.mechanism
                 if mech not in ("PLAIN", "AMQPLAIN", "EXTERNAL"):
                     raise _Hard(C.ACCESS_REFUSED, f"unsupported SASL mechanism {mech}", 10, 11)
@@ -388,6 +396,7 @@ class GpuBroker:
         return self._after_step(ctrl, events, seg_status, cnt, bool(inputs), bool(egress))
 
     def _after_step(self, ctrl, events, seg_status, cnt, had_input, had_egress):
+        self._watermarks()
         self.stats["steps"] += 1
         self.stats["published"] += cnt.get("n_pubs", 0)
         self.stats["delivered"] += cnt.get("n_deliv", 0)
@@ -622,6 +631,32 @@ class GpuBroker:
         for c in list(self.conns.values()):
             if c.out:
                 self._flush(c)
+
+    def _watermarks(self):
+        if not self.mem_high:
+            return
+        used = self.plane.memory_in_use()
+        if not self.blocked and used >= self.mem_high:
+            self.blocked = True
+            self._set_flow(False)
+        elif self.blocked and used <= self.mem_low:
+            self.blocked = False
+            self._set_flow(True)
+
+    def _set_flow(self, active):
+        for c in list(self.conns.values()):
+            if c.state != "open":
+                continue
+            if c.cap_blocked:
+                if active:
+                    self._send(c, 0, Method("connection.unblocked"))
+                else:
+                    self._send(c, 0, Method("connection.blocked", reason="low on memory"))
+            else:
+                pc = self.plane.conns.get(c.id)
+                for ch in (list(pc.channels) if pc else []):
+                    if ch not in c.closing_channels:
+                        self._send(c, ch, Method("channel.flow", active=active))
 
     def _heartbeats(self, now):
         for c in list(self.conns.values()):

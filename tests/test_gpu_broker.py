@@ -143,3 +143,34 @@ def test_errors_unknown_exchange_and_unsupported(broker):
     q = conn(broker)
     q.channel().queue_declare("g", passive=True)   # broker still serving
     q.close()
+
+
+@pytest.fixture(params=["golden", pytest.param("gpu", marks=pytest.mark.gpu)])
+def wm_broker(request):
+    from chanamq_amd.server.gpu_broker import GpuBroker
+    b = GpuBroker(make_plane(request.param), idle_step_ms=1.0, ingress_bytes=8 << 20,
+                  mem_high_watermark=40_000, mem_low_watermark=10_000).start()
+    yield b
+    b.stop()
+
+
+def test_memory_watermark_blocks_and_unblocks(wm_broker):
+    p = conn(wm_broker)
+    ch = p.channel()
+    ch.queue_declare("wm")
+    for i in range(60):
+        ch.basic_publish("", "wm", bytes(1000))
+    p._wait(lambda: True if p.blocked else None, timeout=5)
+    c = conn(wm_broker)
+    cc = c.channel()
+    cc.basic_consume("wm", "wmc", no_ack=True)
+    assert len(cc.consume_n(60)) == 60
+    p._wait(lambda: True if not p.blocked else None, timeout=5)
+    # a client without the connection.blocked capability gets Channel.Flow instead
+    q = conn(wm_broker, capabilities={"publisher_confirms": True})
+    qc = q.channel()
+    qc.queue_declare("wm2")            # no consumer: the bytes stay
+    for i in range(60):
+        qc.basic_publish("", "wm2", bytes(1000))
+    q._wait(lambda: True if qc.flow_active is False else None, timeout=5)
+    p.close(); c.close(); q.close()
