@@ -15,8 +15,9 @@ import numpy as np
 from .. import ops
 from ..protocol import constants as C
 from .control import ControlError, ControlState
-from .layout import (CONN_OUT, CTRL_REC, INVALID, RDESC, SEG_IN, SEG_OUT, SS_CTRL, chan_hash,
-                     direct_key, exch_hash, fnv1a64, topic_pattern_row)
+from .layout import (CONN_OUT, CONSUMED_REC, CTRL_REC, INVALID, MF_PERSIST, MF_REDELIVERED, MF_RESTORE, PERSIST_HDR,
+                     RDESC, SEG_IN, SEG_OUT, SS_CTRL, chan_hash, direct_key, exch_hash, fnv1a64,
+                     topic_pattern_row)
 
 ONES64 = np.uint64((1 << 64) - 1)
 
@@ -242,6 +243,7 @@ class GpuDataPlane(ControlState):
 
     def queue_declared(self, q):
         self._up_at("q_owner", q.owner, q.slot, np.uint32)
+        self._up_at("q_durable", int(q.durable), q.slot, np.uint32)
         self._up_at("q_ring_off", q.ring_off, q.slot, np.uint64)
         self._up_at("q_ring_mask", q.capacity - 1, q.slot, np.uint64)
         self._up_at("q_head", 0, q.slot, np.uint64)
@@ -289,6 +291,60 @@ class GpuDataPlane(ControlState):
     # ---- host-side queue/channel ops between steps (the plane is idle: step() is synchronous)
     def _u64(self, name, idx):
         return int(np.frombuffer(self.eng.download(name, idx * 8, 8), np.uint64)[0])
+
+    # ---- persistence (engine built with persist=1)
+    def take_persist(self):
+        """Persist records of the last finished step: [(msg_id, ts_ms, q, qpos, expire_ms,
+        ex, rk, props, body)] — durable queue x persistent message, one per enqueue."""
+        c = self.last_counters
+        n = min(c["n_persist"], self.info["persist_max"])
+        if not n:
+            return []
+        if c["n_persist_overflow"] or c["n_persist"] > self.info["persist_max"]:
+            raise RuntimeError("persist buffer overflow: raise persist_max / persist_bytes")
+        raw = self.eng.host_view(f"persist{self._last_parity}")[:c["persist_used"]]
+        out, off = [], 0
+        for _ in range(n):
+            h = raw[off:off + PERSIST_HDR.itemsize].view(PERSIST_HDR)[0]
+            b = off + PERSIST_HDR.itemsize
+            el, rl, pl, bl = int(h["ex_len"]), int(h["rk_len"]), int(h["props_len"]), int(h["body_len"])
+            data = bytes(raw[b:b + el + rl + pl + bl])
+            out.append((int(h["msg_id"]), int(h["ts_ms"]), int(h["q"]), int(h["qpos"]), int(h["expire_ms"]),
+                        data[:el], data[el:el + rl], data[el + rl:el + rl + pl], data[el + rl + pl:]))
+            off += int(h["size"])
+        return out
+
+    def take_consumed(self):
+        """[(msg_id, q, qpos, kind)] of persistent messages that left durable queues."""
+        c = self.last_counters
+        n = min(c["n_consumed"], self.info["persist_max"])
+        if not n:
+            return []
+        recs = self.eng.host_view(f"consumed{self._last_parity}")[:n * CONSUMED_REC.itemsize].view(CONSUMED_REC)
+        return [(int(r["msg_id"]), int(r["q"]), int(r["qpos"]), int(r["kind"])) for r in recs]
+
+    def restore(self, items, now_ms=None):
+        """Recovery: enqueue stored messages into their queues in the given order.
+        items: [(q_slot, msg_id, ts_ms, expire_ms, ex, rk, props, body, persistent, redelivered)]."""
+        now = int(time.time() * 1000) if now_ms is None else int(now_ms)
+        cap = self.info["restore_max"]
+        total = 0
+        for k0 in range(0, len(items), max(1, cap)):
+            chunk = items[k0:k0 + cap]
+            desc = np.zeros(len(chunk), RDESC)
+            pay = bytearray()
+            for i, (q, mid, ts, exp, ex, rk, props, body, persistent, red) in enumerate(chunk):
+                d = desc[i]
+                d["pay_off"] = len(pay)
+                d["body_len"], d["props_len"], d["exch"] = len(body), len(props), -1
+                d["flags"] = MF_RESTORE | (MF_PERSIST if persistent else 0) | (MF_REDELIVERED if red else 0)
+                d["ex_len"], d["rk_len"] = len(ex), len(rk)
+                d["expire_ms"], d["ts_ms"], d["xid"], d["tq"] = exp, ts, mid, q
+                rec = ex + rk + props + body
+                pay += rec + b"\0" * ((-len(rec)) % 16)
+            total += self.eng.restore(desc.view(np.uint8), np.frombuffer(bytes(pay) or b"\0", np.uint8)[:len(pay)],
+                                      now)
+        return total
 
     def memory_in_use(self):
         """Body-log bytes held by live messages (after the last finished step)."""
@@ -418,6 +474,7 @@ class GpuDataPlane(ControlState):
     def finish(self, ticket, collect=True, wait_egress=True, collect_egress=True):
         p, nseg, t0 = ticket
         self.eng.wait_results(p)
+        self._last_parity = p
         res = StepResult()
         res.counters = c = self.eng.counters(p)
         self.last_counters = c

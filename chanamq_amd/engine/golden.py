@@ -27,18 +27,24 @@ def _frame(t, ch, payload):
 
 
 class _Msg:
-    __slots__ = ("ex", "rk", "props", "body", "refcnt", "pub_step", "flags", "id")
+    __slots__ = ("ex", "rk", "props", "body", "refcnt", "pub_step", "flags", "id", "ts", "restored")
+    _next = 1
 
-    def __init__(self, ex, rk, props, body, nq, step, flags):
+    def __init__(self, ex, rk, props, body, nq, step, flags, mid=None, ts=0):
         self.ex, self.rk, self.props, self.body = ex, rk, props, body
         self.refcnt, self.pub_step, self.flags = nq, step, flags
+        if mid is None:
+            mid, _Msg._next = _Msg._next, _Msg._next + 1
+        self.id, self.ts, self.restored = mid, ts, False
 
 
 class GoldenDataPlane(ControlState):
     def __init__(self, hash_wildcard=True, ucap=8192, deliver_cap=4096, carry_cap=1 << 20,
                  egress_cap=96 << 20, deliv_max=65536, exchanger=None, xfer_desc_max=1 << 15,
-                 xfer_bytes=1 << 24, **kw):
+                 xfer_bytes=1 << 24, persist=False, **kw):
         super().__init__(hash_wildcard=hash_wildcard, **kw)
+        self.persist = persist
+        self._persist_out, self._consumed_out = [], []
         self.exchanger = exchanger
         self._outbox = defaultdict(list)  # dest rank -> [(RDesc fields, payload)]
         self._deferred = []                # this rank's routed publishes awaiting step_b
@@ -77,6 +83,33 @@ class GoldenDataPlane(ControlState):
         self.ring[q.slot] = []
         self.qpos_head[q.slot] = 0
         self.qrr[q.slot] = 0
+
+    # ---- persistence (same records as the GPU plane's take_persist / take_consumed)
+    def _consumed(self, msg, q, qpos, kind):
+        qq = self.queue_by_slot.get(q)
+        if self.persist and qq is not None and qq.durable and (msg.flags & MF_PERSIST):
+            self._consumed_out.append((msg.id, q, qpos, kind))
+
+    def take_persist(self):
+        out, self._persist_out = self._persist_out, []
+        return out
+
+    def take_consumed(self):
+        out, self._consumed_out = self._consumed_out, []
+        return out
+
+    def restore(self, items, now_ms=0):
+        n = 0
+        for q, mid, ts, exp, ex, rk, props, body, persistent, red in items:
+            qq = self.queue_by_slot[q]
+            ring = self.ring[q]
+            if len(ring) >= qq.capacity:
+                continue
+            msg = _Msg(ex, rk, props, body, 1, self.step_no, MF_PERSIST if persistent else 0, mid=mid, ts=ts)
+            msg.restored = True
+            ring.append((msg, bool(red), exp))
+            n += 1
+        return n
 
     def memory_in_use(self):
         seen, tot = set(), 0
@@ -407,11 +440,13 @@ class GoldenDataPlane(ControlState):
                 if state == "pending" and t <= st["req_upto"]:
                     state = "requeue"
                 if state == "acked":
+                    self._consumed(sl["msg"], sl["q"], sl["qpos"], 0)
                     self._release(sl["msg"])
                     self.cons_unacked[sl["cons"]] -= 1
                     st["unacked"] -= 1
                     state = "done"
                 elif state == "requeue":
+                    self._consumed(sl["msg"], sl["q"], sl["qpos"], 4)
                     self.requeue_items.append((sl["q"], sl["msg"], sl["qpos"], sl["expire"]))
                     self.cons_unacked[sl["cons"]] -= 1
                     st["unacked"] -= 1
@@ -456,6 +491,8 @@ class GoldenDataPlane(ControlState):
             st["next_tag"] += 1
             st["slots"][d["tag"]] = dict(state="done" if d["noack"] else "pending", msg=d["msg"],
                                          q=d["q"], cons=d["cons"], qpos=d["qpos"], expire=d["expire"])
+            if not d["noack"]:
+                self._consumed(d["msg"], d["q"], d["qpos"], 3)
             self._mark_dirty(d["chslot"])
             cnt["lat_" + str(min(self.step_no - d["msg"].pub_step, 31))] += 1
         # ---- egress per connection: returns, confirms, deliveries
@@ -485,6 +522,7 @@ class GoldenDataPlane(ControlState):
                 out["egress"][conn] = b"".join(parts)
         for d in delivs:
             if d["noack"]:
+                self._consumed(d["msg"], d["q"], d["qpos"], 0)
                 self._release(d["msg"])
         cnt["n_deliv"] = len(delivs)
         self.step_no += 1
@@ -555,7 +593,8 @@ class GoldenDataPlane(ControlState):
         if not qs:
             return
         flags = 1 if self._persistent(props) else 0
-        msg = _Msg(ex, rk, props, body, len(qs), self.step_no, flags)
+        tsp = self._prop_fields(props).get("timestamp")
+        msg = _Msg(ex, rk, props, body, len(qs), self.step_no, flags, ts=int(tsp) * 1000 if tsp else 0)
         if self.world > 1:   # enqueued in step_b, ordered by source rank (see _import)
             self._deferred.append((msg, qs, expire))
         else:
@@ -574,6 +613,9 @@ class GoldenDataPlane(ControlState):
             if qq.ttl_ms > 0:
                 qe = now_ms + qq.ttl_ms
                 e = qe if (e == 0 or qe < e) else e
+            if self.persist and qq.durable and (msg.flags & MF_PERSIST) and not msg.restored:
+                self._persist_out.append((msg.id, msg.ts, q, self.qpos_head[q] + len(ring), e, msg.ex, msg.rk,
+                                          msg.props, msg.body))
             ring.append((msg, False, e))
 
     def _route(self, x, rk):
@@ -617,6 +659,7 @@ class GoldenDataPlane(ControlState):
         ring = self.ring[q]
         cnt = self.counters
         while ring and ring[0][2] and ring[0][2] <= now_ms:
+            self._consumed(ring[0][0], q, self.qpos_head[q], 1)
             self._release(ring.pop(0)[0])
             self.qpos_head[q] += 1
             cnt["n_expired"] += 1

@@ -14,8 +14,15 @@ CONN_OUT = np.dtype([("off", "<u4"), ("len", "<u4")])
 # cross-rank publish record (dp_common.h RDesc); payload = [exchange][routing key][props][body]
 RDESC = np.dtype([("pay_off", "<u4"), ("body_len", "<u4"), ("props_len", "<u4"), ("exch", "<i4"),
                   ("flags", "<u4"), ("ex_len", "u1"), ("rk_len", "u1"), ("pad0", "<u2"),
-                  ("expire_ms", "<i8"), ("ts_ms", "<i8"), ("pad", "<u4", 6)])
+                  ("expire_ms", "<i8"), ("ts_ms", "<i8"), ("xid", "<u8"), ("tq", "<u4"), ("pad", "<u4", 3)])
 MF_PERSIST, MF_MANDATORY, MF_IMMEDIATE, MF_HAS_TS, MF_IMPORTED = 1, 2, 4, 8, 16
+MF_RESTORE, MF_REDELIVERED = 32, 64
+# persistence records (dp_common.h PersistHdr / ConsumedRec)
+PERSIST_HDR = np.dtype([("msg_id", "<i8"), ("ts_ms", "<i8"), ("qpos", "<u8"), ("expire_ms", "<i8"), ("q", "<u4"),
+                        ("body_len", "<u4"), ("props_len", "<u2"), ("ex_len", "u1"), ("rk_len", "u1"),
+                        ("size", "<u4")])
+CONSUMED_REC = np.dtype([("msg_id", "<i8"), ("qpos", "<u8"), ("q", "<u4"), ("kind", "<u4"), ("pad", "<u4", 2)])
+assert PERSIST_HDR.itemsize == 48 and CONSUMED_REC.itemsize == 32
 
 STRUCT_SIZES = {"SegIn": 16, "SegOut": 32, "CtrlRec": 16, "ConnOut": 8, "StepIn": 64, "RDesc": 64}
 assert RDESC.itemsize == 64

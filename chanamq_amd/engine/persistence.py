@@ -1,0 +1,199 @@
+"""Write-behind persistence for the GPU data plane (SURVEY §3.3, P7 / BASELINE config 4).
+
+Each step the device emits (a) one persist record per enqueue of a persistent message
+into a durable queue, packed with the message bytes, and (b) one consumed record per
+persistent message that leaves a durable queue (acked, auto-acked, expired).  ``after_step``
+turns them into rows of the Cassandra-schema store (csrc/core/store.cpp, same tables
+as the reference's create-cassantra.cql):
+
+  msgs(id, tstamp, header, body, exchange, routing, durable, refer)   once per message
+  queues(queue, offset, msgid, size)                                   per durable queue
+  -> deleted when consumed; the message row when its refer count drops to zero
+
+and the server calls ``commit()`` (one fsync, group commit) before it releases the
+step's egress, so a publisher confirm is never sent before its message is durable.
+
+``recover`` rebuilds durable vhosts/exchanges/queues/bindings from the store and feeds
+the stored messages back through the device import path (``restore``) — unacked ones
+first, flagged redelivered (reference QueueEntity.scala:117 never requeued them: A.Q31).
+Queue offsets restart at 0 on the device, so recovery rewrites the queue rows to the new
+offsets in the same commit.
+"""
+
+import struct
+
+from .control import entity_id
+
+
+def _split_eid(eid):
+    if "-_." in eid:
+        v, n = eid.split("-_.", 1)
+        return v, n
+    return "", eid
+
+
+class GpuPersistence:
+    def __init__(self, plane, store):
+        self.plane, self.store = plane, store
+        self.refs = {}            # msg id -> durable queue rows referencing it
+        self.rows = {}            # (queue id, msg id) -> [stored offset, size, is_unack]
+        self.rows_written = 0
+        self.dirty = False
+
+    def _qid(self, slot):
+        q = self.plane.queue_by_slot.get(slot)
+        return entity_id(q.vhost, q.name) if q is not None else None
+
+    # ------------------------------------------------------------------ step records
+    def after_step(self):
+        """Apply the step's records.  Device queue positions change on requeue, so rows
+        are addressed by (queue, message id) -> the offset they were stored at."""
+        st = self.store
+        persisted = self.plane.take_persist()
+        consumed = self.plane.take_consumed()
+        for mid, ts, q, qpos, exp, ex, rk, props, body in persisted:
+            qid = self._qid(q)
+            if qid is None:
+                continue
+            n = self.refs.get(mid, 0)
+            self.refs[mid] = n + 1
+            if n == 0:
+                header = b"\0\0" + struct.pack(">Q", len(body)) + props
+                st.insert_message(mid, ts, header, body, ex.decode("utf-8", "replace"),
+                                  rk.decode("utf-8", "replace"), True, 1, 0)
+            else:
+                st.update_message_refer_count(mid, n + 1)
+            st.insert_queue_msg(qid, qpos, mid, len(body), 0)
+            self.rows[(qid, mid)] = [qpos, len(body), False]
+            self.rows_written += 1
+        for mid, q, qpos, kind in consumed:
+            qid = self._qid(q)
+            row = self.rows.get((qid, mid)) if qid is not None else None
+            if row is None:
+                continue
+            off, size, unack = row
+            if kind == 3:                 # delivered, awaiting ack: queues -> queue_unacks
+                if not unack:
+                    st.insert_queue_unack(qid, off, mid, size)
+                    st.delete_queue_msg(qid, off)
+                    row[2] = True
+                continue
+            if kind == 4:                 # requeued: back to queues (redelivered on recovery
+                if unack:                 # is implied by the unack history; RabbitMQ-like)
+                    st.delete_queue_unack(qid, mid)
+                    st.insert_queue_msg(qid, off, mid, size, 0)
+                    row[2] = False
+                continue
+            # consumed / expired / dropped: the row goes, the message when unreferenced
+            if unack:
+                st.delete_queue_unack(qid, mid)
+            else:
+                st.delete_queue_msg(qid, off)
+            del self.rows[(qid, mid)]
+            n = self.refs.get(mid, 1) - 1
+            if n <= 0:
+                self.refs.pop(mid, None)
+                st.delete_message(mid)
+            else:
+                self.refs[mid] = n
+                st.update_message_refer_count(mid, n)
+        if persisted or consumed:
+            self.dirty = True
+        return bool(persisted)
+
+    def commit(self):
+        if self.dirty:
+            self.store.sync()
+            self.dirty = False
+
+    # ------------------------------------------------------------------ control rows
+    def vhost(self, name):
+        self.store.insert_vhost(name, True)
+
+    def exchange(self, x):
+        if x.durable and x.name and not x.name.startswith("amq."):
+            self.store.insert_exchange(entity_id(x.vhost, x.name), x.type, True, x.auto_delete, x.internal,
+                                       {k: str(v) for k, v in (x.arguments or {}).items()})
+
+    def exchange_deleted(self, vhost, name):
+        self.store.delete_exchange(entity_id(vhost, name))
+
+    def queue(self, q):
+        if q.durable:
+            self.store.insert_queue_meta(entity_id(q.vhost, q.name), -1, set(), True, q.ttl_ms)
+
+    def queue_deleted(self, vhost, name):
+        qid = entity_id(vhost, name)
+        self.store.force_delete_queue(qid)
+        self.store.delete_binds_of_queue(qid)
+
+    def bind(self, vhost, queue, exchange, key):
+        x = self.plane.exchanges.get((vhost, exchange))
+        q = self.plane.queues.get((vhost, queue))
+        if x is not None and q is not None and x.durable and q.durable and exchange and \
+                not exchange.startswith("amq."):
+            self.store.insert_bind(entity_id(vhost, exchange), entity_id(vhost, queue), key, {})
+
+    def unbind(self, vhost, queue, exchange, key):
+        self.store.delete_bind(entity_id(vhost, exchange), entity_id(vhost, queue), key)
+
+    # ------------------------------------------------------------------ recovery
+    def recover(self, now_ms=0):
+        """Durable topology + messages from the store into the plane.  Returns the number
+        of messages restored."""
+        p, st = self.plane, self.store
+        for v in st.vhost_ids():
+            p.ensure_vhost(v)
+        binds = []
+        for xid in st.exchange_ids():
+            r = st.select_exchange(xid)
+            if r is None:
+                continue
+            (tpe, durable, autodel, internal, args), bl = r
+            v, name = _split_eid(xid)
+            v = v or "AMQ.DEFAULT"
+            p.ensure_vhost(v)
+            p.declare_exchange(v, name, tpe, durable=durable, auto_delete=autodel, internal=internal,
+                               arguments=args)
+            binds += [(v, _split_eid(qid)[1], name, key) for qid, key, _ in bl]
+        items, rewrite = [], []
+        for qid in st.queue_ids():
+            r = st.select_queue(qid)
+            if r is None:
+                continue
+            (lconsumed, consumers, durable, ttl), msgs, unacks = r
+            if not durable:
+                continue
+            v, name = _split_eid(qid)
+            v = v or "AMQ.DEFAULT"
+            p.ensure_vhost(v)
+            slot = p.declare_queue(v, name, durable=True, ttl_ms=int(ttl or 0))
+            order = [(off, mid, True) for off, mid, _ in sorted(unacks)] + \
+                    [(off, mid, False) for off, mid, _ in sorted(msgs) if off > lconsumed]
+            new_off = 0
+            for off, mid, red in order:
+                m = st.select_message(mid)
+                if m is None:
+                    continue
+                _, ts, header, body, ex, rk, _, _ = m
+                props = header[10:]
+                items.append((slot, mid, ts, 0, ex.encode(), rk.encode(), props, body, True, red))
+                rewrite.append((qid, off, new_off, mid, len(body), red))
+                self.refs[mid] = self.refs.get(mid, 0) + 1
+                new_off += 1
+        for v, q, x, key in binds:
+            if (v, q) in p.queues:
+                p.bind(v, q, x, key)
+        n = p.restore(items, now_ms) if items else 0
+        # device offsets restart at 0: move the rows to them
+        for qid, off, new_off, mid, size, red in rewrite:
+            if red:
+                st.delete_queue_unack(qid, mid)
+            else:
+                st.delete_queue_msg(qid, off)
+        for qid, off, new_off, mid, size, red in rewrite:
+            st.insert_queue_msg(qid, new_off, mid, size, 0)
+            st.insert_last_consumed(qid, -1)
+            self.rows[(qid, mid)] = [new_off, size, False]
+        st.sync()
+        return n

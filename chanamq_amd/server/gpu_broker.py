@@ -78,7 +78,8 @@ def _frames(buf):
 class GpuBroker:
     def __init__(self, plane, host="127.0.0.1", port=0, heartbeat=0, frame_max=131072, channel_max=2047,
                  idle_step_ms=2.0, product="chanamq-amd", version="0.1.0", io="native",
-                 ingress_bytes=64 << 20, per_conn_read=1 << 20, mem_high_watermark=0, mem_low_watermark=0):
+                 ingress_bytes=64 << 20, per_conn_read=1 << 20, mem_high_watermark=0, mem_low_watermark=0,
+                 store=None):
         """``io``: "native" = C++ batched gateway (csrc/core/gateway.cpp), "python" =
         selectors loop (portable fallback)."""
         self.plane = plane
@@ -90,6 +91,13 @@ class GpuBroker:
         # capability) or Channel.Flow(active=false); released below the low watermark
         self.mem_high, self.mem_low = mem_high_watermark, mem_low_watermark or mem_high_watermark // 2
         self.blocked = False
+        # durable queues x persistent messages -> store (write-behind, confirm gating)
+        self.persistence = None
+        self.recovered = 0
+        if store is not None:
+            from ..engine.persistence import GpuPersistence
+            self.persistence = GpuPersistence(plane, store)
+            self.recovered = self.persistence.recover(int(time.time() * 1000))
         self.host, self.port = host, port
         self.heartbeat, self.frame_max, self.channel_max = heartbeat, frame_max, channel_max
         self.idle_step_s = idle_step_ms / 1000.0
@@ -216,6 +224,7 @@ class GpuBroker:
         p = self.plane
         t = p.submit_raw(segs, self._pin.ctypes.data, used, int(time.time() * 1000))
         res = p.finish(t, collect=True, collect_egress=False)
+        self._persist_step()
         eg, co = p.host_egress(t)
         self.gw.send_egress(eg, co.view(np.uint32), p.c_max)
         return self._after_step(res.ctrl, res.events, [(s[0], s[1]) for s in res.segs], res.counters,
@@ -379,6 +388,7 @@ class GpuBroker:
     # ------------------------------------------------------------------ data-plane step
     def _step(self, inputs):
         res = self.plane.step(inputs, now_ms=int(time.time() * 1000))
+        self._persist_step()
         if isinstance(res, dict):   # golden plane
             egress, ctrl, events, segs, cnt = res["egress"], res["ctrl"], res["events"], res["segs"], \
                 res.get("counters", {})
@@ -429,6 +439,13 @@ class GpuBroker:
             if c.state == "open":
                 self.plane.unpause(conn)
         return had_input or had_egress or bool(ctrl) or cnt.get("n_deliv", 0) > 0
+
+    def _persist_step(self):
+        """Store rows of this step, committed (fsync) before the step's egress — which
+        carries its publisher confirms — leaves the broker."""
+        if self.persistence is not None:
+            self.persistence.after_step()
+            self.persistence.commit()
 
     def _chan_of_slot(self, conn, chslot):
         cc = self.plane.conns.get(conn)
@@ -508,10 +525,14 @@ class GpuBroker:
                 raise ControlError(C.PRECONDITION_FAILED, f"exchange '{m.exchange}' declared as {x.type}", 40, 10)
             p.declare_exchange(vh, m.exchange, m.type or "direct", durable=m.durable, auto_delete=m.auto_delete,
                                internal=m.internal, arguments=m.arguments, passive=m.passive)
+            if self.persistence is not None and not m.passive:
+                self.persistence.exchange(p.exchanges[(vh, m.exchange)])
             if not m.nowait:
                 self._send(c, ch, Method("exchange.declare_ok"))
         elif n == "exchange.delete":
             p.delete_exchange(vh, m.exchange, if_unused=m.if_unused)
+            if self.persistence is not None:
+                self.persistence.exchange_deleted(vh, m.exchange)
             if not m.nowait:
                 self._send(c, ch, Method("exchange.delete_ok"))
         elif n == "queue.declare":
@@ -524,6 +545,8 @@ class GpuBroker:
             slot = p.declare_queue(vh, name, durable=m.durable, exclusive_owner=c.id if m.exclusive else -1,
                                    auto_delete=m.auto_delete, ttl_ms=ttl, passive=m.passive)
             c.last_queue[ch] = name
+            if self.persistence is not None and q is None and not m.passive:
+                self.persistence.queue(p.queue_by_slot[slot])
             if not m.nowait:
                 qq = p.queue_by_slot[slot]
                 self._send(c, ch, Method("queue.declare_ok", queue=name, message_count=p.message_count(slot),
@@ -531,11 +554,15 @@ class GpuBroker:
         elif n == "queue.bind":
             qn = m.queue or c.last_queue.get(ch, "")
             p.bind(vh, qn, m.exchange, m.routing_key)
+            if self.persistence is not None:
+                self.persistence.bind(vh, qn, m.exchange, m.routing_key)
             if not m.nowait:
                 self._send(c, ch, Method("queue.bind_ok"))
         elif n == "queue.unbind":
             qn = m.queue or c.last_queue.get(ch, "")
             p.unbind(vh, qn, m.exchange, m.routing_key)
+            if self.persistence is not None:
+                self.persistence.unbind(vh, qn, m.exchange, m.routing_key)
             self._send(c, ch, Method("queue.unbind_ok"))
         elif n == "queue.purge":
             q = self._queue(vh, m.queue or c.last_queue.get(ch, ""), 50, 30)
@@ -551,7 +578,10 @@ class GpuBroker:
                 raise ControlError(C.PRECONDITION_FAILED, f"queue '{q.name}' not empty", 50, 40)
             p.purge(q.slot)
             p.step({}, now_ms=int(time.time() * 1000))   # releases the purged messages
+            self._persist_step()
             p.delete_queue(vh, q.name)
+            if self.persistence is not None:
+                self.persistence.queue_deleted(vh, q.name)
             if not m.nowait:
                 self._send(c, ch, Method("queue.delete_ok", message_count=cnt))
         elif n == "basic.qos":

@@ -116,6 +116,7 @@ PYBIND11_MODULE(_core, m) {
       .def("delete_consumed_queue_msgs", &Store::deleteConsumedQueueMsgs)
       .def("insert_queue_unack", &Store::insertQueueUnack)
       .def("delete_queue_unack", &Store::deleteQueueUnack)
+      .def("delete_queue_msg", &Store::deleteQueueMsg)
       .def("insert_exchange", [](Store& s, std::string id, std::string tpe, bool durable, bool autodel, bool internal,
                                  std::map<std::string, std::string> args) {
              ExchangeRow x; x.tpe = tpe; x.durable = durable; x.autodel = autodel; x.internal = internal; x.args = args;

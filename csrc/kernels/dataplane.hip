@@ -821,7 +821,7 @@ __global__ void k_decode(DS d) {
     pb.flags = 0;
     pb.expire_ms = 0;
     pb.ts_ms = 0;
-    pb.nq = 0; pb.slot_bytes = 0; pb.msg = INVALID; pb.pad = 0;
+    pb.nq = 0; pb.slot_bytes = 0; pb.msg = INVALID; pb.pad = 0; pb.xid = 0;
     // method args: class u16, method u16, ticket u16, exchange ss, rk ss, bits
     u32 o = c.m_off + 6, end = c.m_off + c.m_len;
     bool ok = o <= end;
@@ -1246,7 +1246,9 @@ DEV void route_one(const DS& d, u32 p, u32 lane) {
   }
   RouteAcc<PASS> a;
   const i32 ex = pb.exch;
-  if (ex >= 0) {
+  if (pb.flags & MF_RESTORE) {   // recovered message: exactly its queue
+    route_emit<PASS>(d, a, p, wbase, srank, (u32)pb.keyhash, lane == 0, lane);
+  } else if (ex >= 0) {
     u32 xt = d.x_type[ex];
     if (xt == EX_DIRECT || xt == EX_FANOUT) {
       u32 o = 0, c = 0;
@@ -1289,7 +1291,7 @@ DEV void route_one(const DS& d, u32 p, u32 lane) {
     u32 ret = 0;
     if (pb.flags & MF_IMPORTED) {
       rmask = 0;  // imported records are never forwarded again
-    } else if (ex < 0) {
+    } else if (ex < 0 && !(pb.flags & MF_RESTORE)) {
       atomicAdd(&d.ctr->n_unknown_exchange, 1u);
       u32 ri = atomicAdd(&d.ctr->n_ctrl, 1u);
       CtrlRec rec;
@@ -1405,7 +1407,7 @@ DEV void store_one(const DS& d, u32 p, u32 lane) {
     MsgEnt m;
     m.log_off = off;
     u64 pos = (*d.id_base) + rr;
-    m.msg_id = ((pos >> 12) << 22) | (u64(d.in->worker & 1023) << 12) | (pos & 4095);
+    m.msg_id = (pb.flags & MF_RESTORE) ? pb.xid : ((pos >> 12) << 22) | (u64(d.in->worker & 1023) << 12) | (pos & 4095);
     m.ts_ms = pb.ts_ms;
     m.slot_bytes = pb.slot_bytes;
     m.body_len = pb.body_size;
@@ -1587,9 +1589,9 @@ DEV void import_one(const DS& d, u32 i, u32 lane) {
   pb.expire_ms = rd.expire_ms;
   pb.ts_ms = rd.ts_ms;
   const u8* key = d.recv_pay + roff + rd.ex_len;  // read from the source: same wave wrote work
-  pb.keyhash = fnv1a64_dev(key, rd.rk_len);
+  pb.keyhash = (rd.flags & MF_RESTORE) ? (u64)rd.tq : fnv1a64_dev(key, rd.rk_len);
   pb.nwords = build_keyvec(d, key, rd.rk_len, pi);
-  pb.nq = 0; pb.slot_bytes = 0; pb.msg = INVALID;
+  pb.nq = 0; pb.slot_bytes = 0; pb.msg = INVALID; pb.xid = rd.xid;
   pb.pad = src;  // source rank (pair ordering)
   d.pubs[pi] = pb;
 }
@@ -1604,7 +1606,7 @@ __global__ void k_qfirst(DS d, u32 src) {
   if (i == 0 || (k[i - 1] >> rb) != (k[i] >> rb)) d.q_first[k[i] >> rb] = i;
 }
 
-DEV u32 enqueue_one(const DS& d, u32 src, u32 i, u32 n) {
+DEV u32 enqueue_one(const DS& d, u32 src, u32 i, u32 n, PersistRec* pr) {
   const u32* kk = d.pair_k[src];
   const u32 rb = d.rank_bits;
   u32 q = kk[i] >> rb;
@@ -1622,12 +1624,15 @@ DEV u32 enqueue_one(const DS& d, u32 src, u32 i, u32 n) {
     u64 pos = tail + rank;
     Desc ds;
     ds.msg = pb.msg;
-    ds.flags = 0;
+    ds.flags = (pb.flags & MF_REDELIVERED) ? 1u : 0u;
     i64 e = pb.expire_ms;
     i64 qt = d.q_ttl[q];
     if (qt > 0) { i64 qe = d.in->now_ms + qt; e = (e == 0 || qe < e) ? qe : e; }
     ds.expire_ms = e;
     d.ring[d.q_ring_off[q] + (pos & d.q_ring_mask[q])] = ds;
+    if (d.persist && d.q_durable[q] && (pb.flags & MF_PERSIST) && !(pb.flags & MF_RESTORE)) {
+      pr->msg = pb.msg; pr->q = q; pr->qpos = pos; pr->expire_ms = e;
+    }
   } else {
     drop = pb.msg;
   }
@@ -1641,9 +1646,33 @@ DEV u32 enqueue_one(const DS& d, u32 src, u32 i, u32 n) {
 __global__ void k_enqueue(DS d, u32 src) {
   u32 i = blockIdx.x * blockDim.x + threadIdx.x;
   u32 n = d.tot[TS_PAIR_N];
-  u32 drop = i < n ? enqueue_one(d, src, i, n) : INVALID;
+  PersistRec pr;
+  pr.msg = INVALID;
+  u32 drop = i < n ? enqueue_one(d, src, i, n, &pr) : INVALID;
   wave_release(d, drop, drop != INVALID);
   if (drop != INVALID) atomicAdd(&d.ctr->n_ring_full, 1u);
+  if (d.persist) {
+    bool want = pr.msg != INVALID;
+    u32 k = wave_reserve(&d.ctr->n_persist, want);
+    if (want && k < d.persist_max) d.prec[k] = pr;
+  }
+}
+
+// a persistent message changed state in a durable queue: record it for the store
+// (kind 0 consumed/acked, 1 expired, 2 dropped, 3 delivered awaiting ack, 4 requeued)
+DEV void wave_consumed(const DS& d, u32 msg, u32 q, u64 qpos, u32 kind, bool valid) {
+  if (!d.persist) return;
+  bool want = valid && msg != INVALID && d.q_durable[q] && (d.msgs[msg].flags & MF_PERSIST);
+  u32 k = wave_reserve(&d.ctr->n_consumed, want);
+  if (want && k < d.persist_max) {
+    ConsumedRec r;
+    r.msg_id = (i64)d.msgs[msg].msg_id;
+    r.qpos = qpos;
+    r.q = q;
+    r.kind = kind;
+    r.pad[0] = r.pad[1] = 0;
+    d.crec[k] = r;
+  }
 }
 
 
@@ -1711,6 +1740,7 @@ __global__ __launch_bounds__(256) void k_chan_advance(DS d) {
       d.req[ri] = r;
     }
     wave_add_u32(d.req_q_n, u.q, 1u, req_ok);
+    wave_consumed(d, u.msg, u.q, u.qpos, acked ? 0u : (req_ok ? 4u : 2u), acked || req);
     wave_release(d, u.msg, acked || (req && !req_ok));
     wave_sub_u32(d.cons_unacked, u.cons, 1u, acked || req);
     manual_done += __popcll(__ballot(acked || req));
@@ -1775,6 +1805,7 @@ __global__ __launch_bounds__(256) void k_dequeue(DS d) {
     bool exp = valid && ds.expire_ms != 0 && ds.expire_ms <= now;
     u64 live = __ballot(valid && !exp);
     u32 nexp = live ? (__ffsll((unsigned long long)live) - 1) : __popcll(__ballot(valid));
+    wave_consumed(d, ds.msg, q, idx, 1u, lane < nexp);
     wave_release(d, ds.msg, lane < nexp);
     if (lane == 0 && nexp) atomicAdd(&d.ctr->n_expired, nexp);
     head += nexp;
@@ -1921,6 +1952,7 @@ __global__ void k_dfirst(DS d, u32 src) {
   if (i + 1 == n || (k[i + 1] / d.chpc) != conn) d.conn_dlast[conn] = i;
 }
 
+DEV void wave_consumed(const DS& d, u32 msg, u32 q, u64 qpos, u32 kind, bool valid);
 DEV u32 tag_one(const DS& d, u32 src, u32 i, u32 n) {
   const u32* kk = d.dv_k[src];
   u32 ch = kk[i];
@@ -1960,6 +1992,10 @@ __global__ void k_tags(DS d, u32 src) {
   u32 lat = 0;
   if (valid) lat = tag_one(d, src, i, n);
   else if (i < d.deliv_max) d.dv_size[i] = 0;
+  if (d.persist) {   // manual-ack delivery of a persistent message: its row becomes an unack
+    const Deliv* dv = valid ? &d.deliv[d.dv_v[src][i]] : nullptr;
+    wave_consumed(d, dv ? dv->msg : INVALID, dv ? dv->q : 0, dv ? dv->qpos : 0, 3u, valid && !(dv->flags & 2));
+  }
   wave_add_u32(d.ctr->lat_hist, lat < LAT_BINS ? lat : LAT_BINS - 1, 1u, valid);
 }
 
@@ -2151,16 +2187,20 @@ __global__ __launch_bounds__(256) void k_render_returns(DS d) {
 __global__ void k_post(DS d, u32 src) {
   u32 i = blockIdx.x * blockDim.x + threadIdx.x;
   u32 n = d.ctr->n_deliv;
-  u32 msg = INVALID;
+  u32 msg = INVALID, q = 0;
+  u64 qpos = 0;
   bool aa = false;
   if (i < n) {
     const Deliv& dv = d.deliv[d.dv_v[src][i]];
     aa = dv.flags & 2;
     msg = dv.msg;
+    q = dv.q;
+    qpos = dv.qpos;
     const u32* kk = d.dv_k[src];
     u32 ch = kk[i];
     if (i + 1 == n || kk[i + 1] != ch) d.ch_next_tag[ch] = dv.tag + 1;
   }
+  wave_consumed(d, msg, q, qpos, 0u, aa);
   wave_release(d, msg, aa);
   // reset per-connection scratch
   if (i < d.c_max) {
@@ -2194,6 +2234,51 @@ DEV void final_step(const DS& d) {
 }
 __global__ void k_final(DS d) { if (threadIdx.x == 0) final_step(d); }
 
+// persistence: size + pack the step's persist records (header + message bytes) into the
+// host-mapped persist buffer; the host writes them to the store before it releases the
+// step's publisher confirms (write-behind with confirm gating)
+__global__ void k_persist_size(DS d) {
+  u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+  u32 n = d.ctr->n_persist;
+  if (n > d.persist_max) n = d.persist_max;
+  if (i >= n) return;
+  const MsgEnt& m = d.msgs[d.prec[i].msg];
+  d.ps_size[i] = (u32)sizeof(PersistHdr) + ((m.ex_len + m.rk_len + m.props_len + m.body_len + 7u) & ~7u);
+}
+
+__global__ __launch_bounds__(256) void k_persist_pack(DS d) {
+  u32 lane = lane_id();
+  u32 n = d.ctr->n_persist;
+  if (n > d.persist_max) n = d.persist_max;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    u64 used = d.tot[TS_PERSIST];
+    d.ctr->persist_used = (u32)(used < d.persist_bytes ? used : d.persist_bytes);
+  }
+  const u32 nw = (gridDim.x * blockDim.x) >> 6;
+  for (u32 i = (blockIdx.x * blockDim.x + threadIdx.x) >> 6; i < n; i += nw) {
+    const PersistRec r = d.prec[i];
+    const MsgEnt m = d.msgs[r.msg];
+    u64 off = d.ps_off[i];
+    u32 sz = d.ps_size[i];
+    if (off + sz > d.persist_bytes) {
+      if (lane == 0) atomicAdd(&d.ctr->n_persist_overflow, 1u);
+      continue;
+    }
+    u8* o = d.persist_h + off;
+    const u8* slot = d.log + (m.log_off % d.log_bytes);
+    if (lane == 0) {
+      PersistHdr h;
+      h.msg_id = (i64)m.msg_id; h.ts_ms = m.ts_ms; h.qpos = r.qpos; h.expire_ms = r.expire_ms;
+      h.q = r.q; h.body_len = m.body_len; h.props_len = m.props_len; h.ex_len = m.ex_len; h.rk_len = m.rk_len;
+      h.size = sz;
+      *(PersistHdr*)o = h;
+    }
+    u32 meta = m.ex_len + m.rk_len + m.props_len;
+    wave_copy(o + sizeof(PersistHdr), slot, meta);
+    wave_copy(o + sizeof(PersistHdr) + meta, slot + m.body_off, m.body_len);
+  }
+}
+
 // copy the step's small host-visible results to their host-mapped mirrors in one pass
 // (16-B stores, grid-stride) once the whole step has run
 DEV void copy16(u8* dst, const u8* src, u64 n, u64 gtid, u64 gsz) {
@@ -2215,6 +2300,11 @@ __global__ __launch_bounds__(256) void k_host_out(DS d) {
   u64 cb = d.ctr->ctrl_bytes;
   if (cb > d.ctrl_cap) cb = d.ctrl_cap;
   copy16(d.ctrl_h, d.ctrl, cb, gtid, gsz);
+  if (d.persist) {
+    u32 nr = d.ctr->n_consumed;
+    if (nr > d.persist_max) nr = d.persist_max;
+    copy16((u8*)d.crec_h, (const u8*)d.crec, (u64)nr * sizeof(ConsumedRec), gtid, gsz);
+  }
 }
 
 // ============================================================================ requeue (pre-step)

@@ -41,7 +41,11 @@ enum : u32 {
 };
 
 // ---- message flags
-enum : u32 { MF_PERSIST = 1, MF_MANDATORY = 2, MF_IMMEDIATE = 4, MF_HAS_TS = 8, MF_IMPORTED = 16 };
+enum : u32 {
+  MF_PERSIST = 1, MF_MANDATORY = 2, MF_IMMEDIATE = 4, MF_HAS_TS = 8, MF_IMPORTED = 16,
+  MF_RESTORE = 32,      // recovered from the store: enqueue into exactly RDesc.tq, keep RDesc.xid
+  MF_REDELIVERED = 64   // enqueue with the redelivered flag (recovered unacks)
+};
 
 // ---- unacked slot states
 enum : u32 { US_FREE = 0, US_PENDING = 1, US_ACKED = 2, US_REQUEUE = 3, US_DONE = 4 };
@@ -108,11 +112,12 @@ struct Pub {            // decoded Basic.Publish
   u32 nwords;           // routing-key word count (topic)
   i64 expire_ms;        // absolute, 0 = never
   i64 ts_ms;
-  u64 keyhash;          // fnv1a64(routing key)
+  u64 keyhash;          // fnv1a64(routing key); MF_RESTORE: target queue slot
   u32 nq;               // queues routed to
   u32 slot_bytes;       // bytes reserved in the body log
   u32 msg;              // message-table index, -1 if not stored
   u32 pad;
+  u64 xid;              // MF_RESTORE: message id to keep
 };
 
 // cross-rank publish record (sharded queues): the ingress rank ships each publish once
@@ -128,9 +133,31 @@ struct RDesc {
   u16 pad0;
   i64 expire_ms;
   i64 ts_ms;
-  u32 pad[6];
+  u64 xid;              // MF_RESTORE: the message id to keep
+  u32 tq;               // MF_RESTORE: target queue slot
+  u32 pad[3];
 };
 static_assert(sizeof(RDesc) == 64, "RDesc layout");
+
+// persistence (durable queue x persistent message): one record per enqueue, packed with
+// the message bytes into the host-mapped persist buffer at the end of the step
+struct PersistRec { u32 msg; u32 q; u64 qpos; i64 expire_ms; };
+struct PersistHdr {     // host-visible header of one packed persist record (48 B)
+  i64 msg_id;
+  i64 ts_ms;
+  u64 qpos;
+  i64 expire_ms;
+  u32 q;
+  u32 body_len;
+  u16 props_len;
+  u8 ex_len, rk_len;
+  u32 size;             // bytes of this record including the header (8-aligned)
+};
+static_assert(sizeof(PersistHdr) == 48, "PersistHdr layout");
+// a persistent message changed state in a durable queue (kind 0 consumed/acked, 1 expired,
+// 2 dropped, 3 delivered awaiting ack, 4 requeued)
+struct ConsumedRec { i64 msg_id; u64 qpos; u32 q; u32 kind; u32 pad[2]; };
+static_assert(sizeof(ConsumedRec) == 32, "ConsumedRec layout");
 
 struct Ack { u32 chslot; u32 kind; u64 tag; u32 multiple; u32 requeue; };
 
@@ -185,6 +212,7 @@ struct Counters {       // per-step counters (device -> host)
   u32 egress_bytes, n_returns, n_confirm_frames, n_freed;
   u32 n_requeue, n_unroutable, n_dropped_nomem, n_expired;
   u32 n_routed_msgs, n_unknown_exchange, n_ring_full, n_acked;
+  u32 n_persist, n_consumed, persist_used, n_persist_overflow;
   u32 lat_hist[32];     // deliveries by (deliver_step - publish_step), last bin = overflow
   u64 log_head, log_tail;
   u32 msg_free_top, n_live_msgs;

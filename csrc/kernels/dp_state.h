@@ -16,6 +16,7 @@ enum : u32 {
   TS_RANGE_LO = 20, TS_RANGE_HI = 21,   // publish index range of the current routing phase
   TS_PAIR_BASE = 22, TS_PAIR_N = 23,    // pair base of the phase / pairs so far
   TS_NIMPORT = 24, TS_IMPORT_BASE = 25, // imported records / their work-buffer base
+  TS_PERSIST = 26,                      // packed persist bytes
   TS_XSCAN = 32                         // + 2*r: per-destination record / byte totals
 };
 
@@ -197,4 +198,15 @@ struct DS {
   const RDesc* recv_desc;
   const u8* recv_pay;
   u64* id_base;             // snowflake position base of the current routing phase
+
+  // ---------------- persistence (persist == 0: unused)
+  u32 persist, persist_max;
+  u64 persist_bytes;
+  u32* q_durable;           // [q_max]
+  PersistRec* prec;         // [persist_max]
+  ConsumedRec* crec;        // [persist_max]
+  u32* ps_size;             // [persist_max]
+  u32* ps_off;
+  u8* persist_h;            // host-mapped [persist_bytes]
+  ConsumedRec* crec_h;      // host-mapped [persist_max]
 };

@@ -63,6 +63,15 @@ class Engine {
     d_.import_max = d_.world > 1 ? (u32)get("import_max", (d_.world - 1) * d_.pub_max) : 0;
     d_.pub_cap = ((d_.pub_max + d_.import_max + 63) / 64) * 64;
     d_.xfer_desc_max = d_.world > 1 ? (u32)get("xfer_desc_max", (d_.world - 1) * d_.pub_max) : 0;
+    // persistence + recovery: restore batches reuse the import path (world == 1: own buffers)
+    d_.persist = (u32)get("persist", 0);
+    d_.persist_max = d_.persist ? (u32)get("persist_max", d_.cmd_max) : 0;
+    d_.persist_bytes = d_.persist ? get("persist_bytes", 64ull << 20) : 0;
+    restore_max_ = (u32)get("restore_max", d_.persist ? (1u << 14) : 0);
+    if (d_.world == 1 && restore_max_) {
+      d_.import_max = restore_max_;
+      d_.pub_cap = ((d_.pub_max + d_.import_max + 63) / 64) * 64;
+    }
     d_.pair_max = (u32)get("pair_max", d_.cmd_max * 4);
     d_.deliv_max = (u32)get("deliv_max", 65536);
     d_.msg_max = (u32)get("msg_max", 1u << 22);
@@ -84,7 +93,8 @@ class Engine {
     d_.log_bytes = (d_.log_bytes / d_.log_block) * d_.log_block;
     d_.n_log_blocks = d_.log_bytes / d_.log_block;
     d_.ingress_cap = get("ingress_cap", 64ull << 20);
-    d_.xfer_bytes = d_.world > 1 ? get("xfer_bytes", (d_.world - 1) * (d_.ingress_cap + 64)) : 0;
+    d_.xfer_bytes = d_.world > 1 ? get("xfer_bytes", (d_.world - 1) * (d_.ingress_cap + 64))
+                                 : (restore_max_ ? get("restore_bytes", 64ull << 20) : 0);
     d_.work_cap = d_.ingress_cap + (u64)d_.seg_max * (d_.carry_cap + 64);
     d_.work_cap = d_.work_cap > (3ull << 30) ? (3ull << 30) : d_.work_cap;  // u32 offsets
     if (d_.work_cap + d_.xfer_bytes + 8192 > (4ull << 30))
@@ -130,6 +140,10 @@ class Engine {
       io.ctrl_rec = (CtrlRec*)dev(("ctrl_rec_d" + sfx).c_str(), sizeof(CtrlRec) * d_.seg_max * 2);
       io.ctrl_rec_h = (CtrlRec*)hst(("ctrl_rec" + sfx).c_str(), sizeof(CtrlRec) * d_.seg_max * 2);
       io.xchg = (u32*)hst(("xchg" + sfx).c_str(), 4ull * (4 * WORLD_MAX + 4));
+      if (d_.persist) {
+        io.persist_h = (u8*)hst(("persist" + sfx).c_str(), d_.persist_bytes + 64);
+        io.crec_h = (ConsumedRec*)hst(("consumed" + sfx).c_str(), sizeof(ConsumedRec) * (u64)d_.persist_max + 64);
+      }
       egress_host_[p] = (u8*)pinned(("egress_host" + sfx).c_str(), egress_alloc_);
       stage_in_[p] = (StepIn*)pinned(("stage_in" + sfx).c_str(), sizeof(StepIn));
       stage_segs_[p] = (SegIn*)pinned(("stage_segs" + sfx).c_str(), sizeof(SegIn) * d_.seg_max);
@@ -151,7 +165,7 @@ class Engine {
 
     d_.seg_start = (u32*)dev("seg_start", 4ull * d_.seg_max);
     d_.seg_total = (u32*)dev("seg_total", 4ull * d_.seg_max);
-    d_.work = (u8*)dev("work", d_.work_cap + 4096 + (d_.world > 1 ? d_.xfer_bytes + 128 : 0));
+    d_.work = (u8*)dev("work", d_.work_cap + 4096 + (d_.xfer_bytes ? d_.xfer_bytes + 128 : 0));
     d_.cmask = (u16*)dev("cmask", 2ull * ((d_.work_cap + 4096) / 16 + 1));
 
     d_.cmds = (Cmd*)dev("cmds", sizeof(Cmd) * (u64)d_.cmd_max);
@@ -186,6 +200,17 @@ class Engine {
     d_.xs_base = (u32*)dev("xs_base", 8ull * WORLD_MAX);
     d_.xr_base = (u32*)dev("xr_base", 8ull * WORLD_MAX);
     d_.id_base = (u64*)dev("id_base", 8);
+    d_.q_durable = (u32*)dev("q_durable", 4ull * d_.q_max);
+    if (d_.persist) {
+      d_.prec = (PersistRec*)dev("prec", sizeof(PersistRec) * (u64)d_.persist_max);
+      d_.crec = (ConsumedRec*)dev("crec", sizeof(ConsumedRec) * (u64)d_.persist_max);
+      d_.ps_size = (u32*)dev("ps_size", 4ull * d_.persist_max);
+      d_.ps_off = (u32*)dev("ps_off", 4ull * d_.persist_max);
+    }
+    if (d_.world == 1 && restore_max_) {
+      d_.recv_desc = (const RDesc*)dev("restore_desc", sizeof(RDesc) * (u64)restore_max_);
+      d_.recv_pay = (const u8*)dev("restore_pay", d_.xfer_bytes + 64);
+    }
     d_.acks = (Ack*)dev("acks", sizeof(Ack) * (u64)d_.ack_max);
 
     for (int k = 0; k < 2; ++k) {
@@ -304,6 +329,7 @@ class Engine {
       io.ctrl = io_[p].ctrl; io.ctrl_rec = io_[p].ctrl_rec; io.xchg = io_[p].xchg;
       io.seg_out_h = io_[p].seg_out_h; io.conn_out_h = io_[p].conn_out_h; io.ctrl_h = io_[p].ctrl_h;
       io.ctrl_rec_h = io_[p].ctrl_rec_h;
+      io.persist_h = io_[p].persist_h; io.crec_h = io_[p].crec_h;
       io_[p] = io;
     }
     HIPCHECK(hipStreamCreateWithFlags(&s_comp_, hipStreamNonBlocking));
@@ -436,6 +462,8 @@ class Engine {
     o["work_cap"] = d_.work_cap; o["total_bytes"] = total_bytes_; o["req_max"] = d_.req_max;
     o["world"] = d_.world; o["rank"] = d_.my_rank; o["import_max"] = d_.import_max; o["pub_cap"] = d_.pub_cap;
     o["copy_engine"] = sdma_ ? "sdma" : "blit";
+    o["persist"] = d_.persist; o["persist_max"] = d_.persist_max; o["persist_bytes"] = d_.persist_bytes;
+    o["restore_max"] = restore_max_;
     o["xfer_desc_max"] = d_.xfer_desc_max; o["xfer_bytes"] = d_.xfer_bytes; o["world_max"] = WORLD_MAX;
     o["sizeof"] = py::dict(py::arg("StepIn") = sizeof(StepIn), py::arg("SegIn") = sizeof(SegIn),
                            py::arg("SegOut") = sizeof(SegOut), py::arg("Counters") = sizeof(Counters),
@@ -533,6 +561,38 @@ class Engine {
     phase_a_[p] = false;
   }
 
+  // recovery: enqueue store records (RDesc with MF_RESTORE, payload [ex][rk][props][body])
+  // through the import path, between steps; returns the number of messages enqueued
+  u32 restore(py::buffer desc, py::buffer pay, i64 now_ms) {
+    py::buffer_info di = desc.request(), pi = pay.request();
+    u64 db = (u64)di.size * di.itemsize, pb = (u64)pi.size * pi.itemsize;
+    u32 n = (u32)(db / sizeof(RDesc));
+    if (!d_.recv_desc || n > d_.import_max || pb > d_.xfer_bytes)
+      throw std::runtime_error("restore batch exceeds the import buffers (restore_max / restore_bytes)");
+    if (inflight_[0] || inflight_[1]) throw std::runtime_error("restore() between steps only");
+    sync();
+    if (db) HIPCHECK(hipMemcpy((void*)d_.recv_desc, di.ptr, db, hipMemcpyHostToDevice));
+    if (pb) HIPCHECK(hipMemcpy((void*)d_.recv_pay, pi.ptr, pb, hipMemcpyHostToDevice));
+    DS& io = io_[0];
+    StepIn in{};
+    in.nseg = 0;
+    in.now_ms = now_ms;
+    in.step = seq_;
+    in.id_ms = now_ms;
+    in.worker = 0;
+    HIPCHECK(hipMemcpy((void*)io.in, &in, sizeof(StepIn), hipMemcpyHostToDevice));
+    u32* x = (u32*)buf("xchg0").ptr;
+    for (u32 r = 0; r < 2 * WORLD_MAX; ++r) x[2 * WORLD_MAX + r] = 0;
+    x[2 * WORLD_MAX + d_.my_rank] = n;
+    x[3 * WORLD_MAX + d_.my_rank] = (u32)pb;
+    launch_ingest(s_comp_, io);
+    launch_route(s_comp_, io, d_.pub_max);
+    launch_phase_b(s_comp_, io);
+    HIPCHECK(hipStreamSynchronize(s_comp_));
+    const Counters* c = (const Counters*)buf("ctr_host0").ptr;
+    return c->n_routed_msgs;
+  }
+
   // caller-owned exchange operands (device pointers, e.g. torch tensors used by RCCL)
   void set_xfer_buffers(u64 send_desc, u64 send_pay, u64 recv_desc, u64 recv_pay) {
     d_.send_desc = (RDesc*)send_desc; d_.send_pay = (u8*)send_pay;
@@ -580,6 +640,7 @@ class Engine {
     F(egress_bytes); F(n_returns); F(n_confirm_frames); F(n_freed); F(n_requeue); F(n_unroutable);
     F(n_dropped_nomem); F(n_expired); F(n_routed_msgs); F(n_unknown_exchange); F(n_ring_full);
     F(n_acked); F(log_head); F(log_tail); F(msg_free_top); F(n_live_msgs);
+    F(n_persist); F(n_consumed); F(persist_used); F(n_persist_overflow);
 #undef F
     std::vector<u32> lat(c.lat_hist, c.lat_hist + LAT_BINS);
     o["lat_hist"] = lat;
@@ -693,6 +754,11 @@ class Engine {
     u64 pn = d.deliv_max > d.c_max ? d.deliv_max : d.c_max;
     hipLaunchKernelGGL(k_post, blocks(pn, 256), dim3(256), 0, s, d, dsrc);
     hipLaunchKernelGGL(k_post2, blocks(d.c_max, 256), dim3(256), 0, s, d);
+    if (d.persist) {
+      hipLaunchKernelGGL(k_persist_size, blocks(d.persist_max, 256), dim3(256), 0, s, d);
+      launch_scan(s, {{d.ps_size, d.ps_off}}, &d.ctr->n_persist, d.persist_max, TS_PERSIST);
+      hipLaunchKernelGGL(k_persist_pack, wave_blocks(d.persist_max), dim3(256), 0, s, d);
+    }
     hipLaunchKernelGGL(k_host_out, dim3(64), dim3(256), 0, s, d);
   }
 
@@ -736,6 +802,7 @@ class Engine {
   u64 total_bytes_ = 0;
   u64 egress_alloc_ = 0;
   u32 ntiles_max_ = 0;
+  u32 restore_max_ = 0;
   u64* scan_status_ = nullptr;
   u32* scan_ctl_ = nullptr;
   u32 scan_smax_ = 0;
@@ -797,6 +864,7 @@ PYBIND11_MODULE(_dataplane, m) {
       .def("send_counts", &Engine::send_counts)
       .def("submit_b", &Engine::submit_b, py::arg("parity"), py::arg("recv"), py::arg("stream") = 0)
       .def("set_xfer_buffers", &Engine::set_xfer_buffers)
+      .def("restore", &Engine::restore, py::arg("desc"), py::arg("payload"), py::arg("now_ms"))
       .def("wait_results", &Engine::wait_results)
       .def("egress_copy", &Engine::egress_copy)
       .def("egress_wait", &Engine::egress_wait)
