@@ -11,6 +11,7 @@ import argparse
 import json
 import os
 import sys
+import tempfile
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
@@ -21,6 +22,9 @@ SPECS = {
                                    prefetch=5000, exchange_type="topic"),
     "direct_1p1c_256B": dict(producers=1, consumers=1, msg_size=256, auto_ack=True, prefetch=5000),
     "direct_4p4c_1KB_manual_ack": dict(producers=4, consumers=4, msg_size=1024, auto_ack=False, prefetch=1000),
+    # BASELINE config 4 shape: durable queue, delivery-mode 2, 4 KB, publisher confirms, manual ack
+    "config4_durable_4KB_confirms": dict(producers=1, consumers=1, msg_size=4096, auto_ack=False, prefetch=1000,
+                                         persistent=True, durable=True, confirm=True),
 }
 
 
@@ -39,16 +43,24 @@ def main():
     for name, spec in SPECS.items():
         if args.only and args.only not in name:
             continue
+        persist = bool(spec.get("persistent"))
         plane = GpuDataPlane(c_max=256, chpc=8, q_max=256, cons_max=1024, seg_max=256, cmd_max=1 << 16,
                              deliv_max=1 << 16, msg_max=1 << 20, ucap=8192, deliver_cap=8192,
                              ingress_cap=64 << 20, egress_cap=128 << 20, log_bytes=4 << 30, ring_pool=1 << 24,
-                             tb_max=256, default_queue_capacity=1 << 18)
-        b = GpuBroker(plane, idle_step_ms=0.5).start()
+                             tb_max=256, default_queue_capacity=1 << 18, persist=int(persist),
+                             persist_max=1 << 15, persist_bytes=256 << 20)
+        store = None
+        if persist:
+            store = core.Store()
+            store.open(tempfile.mkdtemp(prefix="cmq-gpu-store-"), True)
+        b = GpuBroker(plane, idle_step_ms=0.5, store=store).start()
         try:
             r = core.run_load(dict(port=b.port, seconds=args.seconds, queue=f"e2e.{name}", exchange=f"e2e.x.{name}",
                                    **spec))
         finally:
             b.stop()
+            if store is not None:
+                store.close()
         r.update(name=name, spec=spec, recv_msgs_per_s=r["received"] / r["elapsed"],
                  sent_msgs_per_s=r["sent"] / r["elapsed"], steps=b.stats["steps"])
         results[name] = r

@@ -347,9 +347,9 @@ class GpuDataPlane(ControlState):
         return total
 
     def memory_in_use(self):
-        """Body-log bytes held by live messages (after the last finished step)."""
+        """Body-log slot bytes held by live messages (after the last finished step)."""
         c = getattr(self, "last_counters", None)
-        return int(c["log_head"] - c["log_tail"]) if c else 0
+        return int(c["live_bytes"]) if c else 0
 
     def message_count(self, q):
         """Ready messages of queue slot ``q`` (AMQP Queue.DeclareOk message-count)."""

@@ -209,7 +209,11 @@ DEV void wave_release(const DS& d, u32 msg, bool valid) {
   u32 nf;
   u32 pos = wave_reserve(d.msg_free_top, freed, &nf);
   if (freed) d.msg_free[pos] = msg;
-  if (lane_id() == __ffsll((unsigned long long)fm) - 1) atomicAdd(&d.ctr->n_freed, nf);
+  i64 tot = wave_sum64(freed ? sb : 0);
+  if (lane_id() == __ffsll((unsigned long long)fm) - 1) {
+    atomicAdd(&d.ctr->n_freed, nf);
+    atomicAdd((unsigned long long*)d.live_bytes, (unsigned long long)(-tot));
+  }
   wave_add_i64(d.log_live, blk, -sb, freed);
 }
 
@@ -1439,6 +1443,8 @@ __global__ void k_live_add(DS d) {
     sb = d.pub_slot[p];
   }
   wave_add_i64(d.log_live, blk, sb, valid);
+  i64 tot = wave_sum64(valid ? sb : 0);
+  if (lane_id() == 0 && tot) atomicAdd((unsigned long long*)d.live_bytes, (unsigned long long)tot);
 }
 
 // ============================================================================ sharded queues
@@ -2230,6 +2236,7 @@ DEV void final_step(const DS& d) {
   c->log_tail = tail;
   c->msg_free_top = *d.msg_free_top;
   c->n_live_msgs = d.msg_max - *d.msg_free_top;
+  c->live_bytes = *d.live_bytes;
   *d.ctr_host = *c;
 }
 __global__ void k_final(DS d) { if (threadIdx.x == 0) final_step(d); }

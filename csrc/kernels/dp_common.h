@@ -216,7 +216,8 @@ struct Counters {       // per-step counters (device -> host)
   u32 lat_hist[32];     // deliveries by (deliver_step - publish_step), last bin = overflow
   u64 log_head, log_tail;
   u32 msg_free_top, n_live_msgs;
-  u32 pad[6];
+  i64 live_bytes;       // body-log slot bytes of live messages (exact, unlike head - tail)
+  u32 pad[4];
 };
 
 struct CtrlRec { u32 conn; u32 off; u32 len; u32 seg; };

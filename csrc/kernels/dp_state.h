@@ -157,6 +157,7 @@ struct DS {
   u64* log_tail;
   u64* log_step_base;
   i64* log_live;            // live bytes per log block
+  i64* live_bytes;          // live slot bytes, all blocks
   u64* id_next;             // snowflake virtual sequence position
 
   // ---------------- deliveries

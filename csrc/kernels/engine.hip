@@ -290,6 +290,7 @@ class Engine {
     d_.log_tail = (u64*)dev("log_tail", 8);
     d_.log_step_base = (u64*)dev("log_step_base", 8);
     d_.log_live = (i64*)dev("log_live", 8ull * d_.n_log_blocks);
+    d_.live_bytes = (i64*)dev("live_bytes", 8);
     d_.id_next = (u64*)dev("id_next", 8);
 
     d_.deliv = (Deliv*)dev("deliv", sizeof(Deliv) * (u64)d_.deliv_max);
@@ -641,6 +642,7 @@ class Engine {
     F(n_dropped_nomem); F(n_expired); F(n_routed_msgs); F(n_unknown_exchange); F(n_ring_full);
     F(n_acked); F(log_head); F(log_tail); F(msg_free_top); F(n_live_msgs);
     F(n_persist); F(n_consumed); F(persist_used); F(n_persist_overflow);
+    F(live_bytes);
 #undef F
     std::vector<u32> lat(c.lat_hist, c.lat_hist + LAT_BINS);
     o["lat_hist"] = lat;
