@@ -104,8 +104,10 @@ def main():
     ap.add_argument("--chunk", type=int, default=65536, help="bytes per producer per step (TCP read)")
     ap.add_argument("--blocks", type=int, default=8)
     ap.add_argument("--no-graph", action="store_true")
-    ap.add_argument("--copy-engine", choices=["sdma", "blit"], default="sdma",
-                    help="step IO copies on the SDMA engines (default) or runtime blit kernels")
+    ap.add_argument("--copy-engine", choices=["kernel", "nocu", "blit"], default="kernel",
+                    help="egress D2H: our copy kernel on --copy-wgs workgroups (default), the runtime's "
+                         "NoCU copy request, or the runtime blit kernel")
+    ap.add_argument("--copy-wgs", type=int, default=16)
     ap.add_argument("--workload", choices=["topic", "fanout"], default="topic",
                     help="topic = BASELINE config 2 (default, the headline); fanout = config 3 "
                          "(--queues is then the node total, default 1024, with small publish batches)")
@@ -149,7 +151,7 @@ def main():
                egress_cap=(128 << 20) if not fan else (320 << 20),
                log_bytes=16 << 30, ring_pool=Q * qcap + qtot + 1024, tb_max=max(64, qtot) if not fan else 64,
                fan_max=max(1 << 20, qtot * 2), carry_cap=256 << 10, graph=0 if args.no_graph else 1,
-               copy_engine=1 if args.copy_engine == "sdma" else 0)
+               copy_engine={"blit": 0, "nocu": 1, "kernel": 2}[args.copy_engine], copy_wgs=args.copy_wgs)
     if shards > 1:
         from chanamq_amd.parallel.exchange import Exchanger
         dp = GpuDataPlane(device=local, worker=rank, world=world, rank=rank, exchanger=Exchanger(), **cfg)

@@ -2286,6 +2286,16 @@ __global__ __launch_bounds__(256) void k_persist_pack(DS d) {
   }
 }
 
+// egress D2H on a few workgroups (copy_engine=2): 16-B loads from HBM, 16-B stores into
+// mapped pinned memory; PCIe is the limit, so a handful of CUs saturate it
+__global__ __launch_bounds__(256) void k_copy_out(u8* dst, const u8* src, u64 n) {
+  const u64 gtid = blockIdx.x * blockDim.x + threadIdx.x, gsz = (u64)gridDim.x * blockDim.x;
+  const u64 nv = n >> 4;
+  typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+  for (u64 i = gtid; i < nv; i += gsz) ((v4u*)dst)[i] = __builtin_nontemporal_load(((const v4u*)src) + i);
+  for (u64 i = (nv << 4) + gtid; i < n; i += gsz) dst[i] = src[i];
+}
+
 // copy the step's small host-visible results to their host-mapped mirrors in one pass
 // (16-B stores, grid-stride) once the whole step has run
 DEV void copy16(u8* dst, const u8* src, u64 n, u64 gtid, u64 gsz) {

@@ -111,10 +111,14 @@ class Engine {
     if (d_.q_bits + d_.rank_bits > 32) throw std::runtime_error("q_max too large for sharded pair keys");
     d_.ch_bits = bits_for(nch);
     graph_enabled_ = get("graph", 1) != 0;
-    // step IO copies on the SDMA engines (hipMemcpyDeviceToDeviceNoCU): a blit-kernel copy
-    // of a step's egress occupies CUs for the whole PCIe transfer and stalls the next
-    // step's kernels; copy_engine=0 keeps the runtime's default (blit) path
-    sdma_ = get("copy_engine", 1) != 0;
+    // step IO copies.  copy_engine: 0 = runtime default (a blit kernel that spreads over
+    // the whole GPU and, for the egress D2H, holds its CUs for the entire PCIe transfer,
+    // stalling the next step's kernels), 1 = hipMemcpyDeviceToDeviceNoCU request,
+    // 2 = our own egress copy kernel on copy_wgs workgroups only (stores straight into
+    // mapped pinned memory), leaving the rest of the CUs to the step kernels
+    copy_mode_ = (int)get("copy_engine", 2);
+    sdma_ = copy_mode_ == 1;
+    copy_wgs_ = (u32)get("copy_wgs", 16);
 
     // ---- allocations
     auto dev = [&](const char* name, size_t bytes) { return alloc(name, bytes, false); };
@@ -144,7 +148,12 @@ class Engine {
         io.persist_h = (u8*)hst(("persist" + sfx).c_str(), d_.persist_bytes + 64);
         io.crec_h = (ConsumedRec*)hst(("consumed" + sfx).c_str(), sizeof(ConsumedRec) * (u64)d_.persist_max + 64);
       }
-      egress_host_[p] = (u8*)pinned(("egress_host" + sfx).c_str(), egress_alloc_);
+      if (copy_mode_ == 2) {
+        egress_host_dev_[p] = (u8*)hst(("egress_host" + sfx).c_str(), egress_alloc_);
+        egress_host_[p] = (u8*)buf("egress_host" + sfx).ptr;
+      } else {
+        egress_host_[p] = (u8*)pinned(("egress_host" + sfx).c_str(), egress_alloc_);
+      }
       stage_in_[p] = (StepIn*)pinned(("stage_in" + sfx).c_str(), sizeof(StepIn));
       stage_segs_[p] = (SegIn*)pinned(("stage_segs" + sfx).c_str(), sizeof(SegIn) * d_.seg_max);
     }
@@ -462,7 +471,8 @@ class Engine {
     o["ingress_cap"] = d_.ingress_cap; o["egress_cap"] = d_.egress_cap; o["ring_pool"] = d_.ring_pool;
     o["work_cap"] = d_.work_cap; o["total_bytes"] = total_bytes_; o["req_max"] = d_.req_max;
     o["world"] = d_.world; o["rank"] = d_.my_rank; o["import_max"] = d_.import_max; o["pub_cap"] = d_.pub_cap;
-    o["copy_engine"] = sdma_ ? "sdma" : "blit";
+    o["copy_engine"] = copy_mode_ == 2 ? "kernel" : (sdma_ ? "nocu" : "blit");
+    o["copy_wgs"] = copy_wgs_;
     o["persist"] = d_.persist; o["persist_max"] = d_.persist_max; o["persist_bytes"] = d_.persist_bytes;
     o["restore_max"] = restore_max_;
     o["xfer_desc_max"] = d_.xfer_desc_max; o["xfer_bytes"] = d_.xfer_bytes; o["world_max"] = WORLD_MAX;
@@ -617,7 +627,10 @@ class Engine {
     const Counters* c = (const Counters*)buf("ctr_host" + std::to_string(p)).ptr;
     u64 n = c->egress_bytes;
     HIPCHECK(hipStreamWaitEvent(s_d2h_, ev_done_[p], 0));
-    if (n)
+    if (n && copy_mode_ == 2)
+      hipLaunchKernelGGL(k_copy_out, dim3(copy_wgs_), dim3(256), 0, s_d2h_, egress_host_dev_[p],
+                         (const u8*)io_[p].egress, n);
+    else if (n)
       HIPCHECK(hipMemcpyAsync(egress_host_[p], io_[p].egress, n,
                               sdma_ ? hipMemcpyDeviceToDeviceNoCU : hipMemcpyDeviceToHost, s_d2h_));
     HIPCHECK(hipEventRecord(ev_d2h_[p], s_d2h_));
@@ -817,6 +830,9 @@ class Engine {
   bool xfer_set_ = false;
   DS io_[2];
   u8* egress_host_[2] = {nullptr, nullptr};
+  u8* egress_host_dev_[2] = {nullptr, nullptr};
+  int copy_mode_ = 2;
+  u32 copy_wgs_ = 16;
   StepIn* stage_in_[2] = {nullptr, nullptr};
   SegIn* stage_segs_[2] = {nullptr, nullptr};
   hipStream_t s_comp_ = nullptr, s_h2d_ = nullptr, s_d2h_ = nullptr;
