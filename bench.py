@@ -104,9 +104,9 @@ def main():
     ap.add_argument("--chunk", type=int, default=65536, help="bytes per producer per step (TCP read)")
     ap.add_argument("--blocks", type=int, default=8)
     ap.add_argument("--no-graph", action="store_true")
-    ap.add_argument("--copy-engine", choices=["kernel", "nocu", "blit"], default="kernel",
-                    help="egress D2H: our copy kernel on --copy-wgs workgroups (default), the runtime's "
-                         "NoCU copy request, or the runtime blit kernel")
+    ap.add_argument("--copy-engine", choices=["kernel", "nocu", "blit"], default="blit",
+                    help="egress D2H: the runtime blit copy (default, fastest measured), the runtime's NoCU "
+                         "copy request, or our copy kernel on --copy-wgs workgroups")
     ap.add_argument("--copy-wgs", type=int, default=16)
     ap.add_argument("--workload", choices=["topic", "fanout"], default="topic",
                     help="topic = BASELINE config 2 (default, the headline); fanout = config 3 "

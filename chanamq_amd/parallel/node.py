@@ -46,6 +46,18 @@ class ShardedNode:
         results = self._retry(self.log.sync, retries)
         return self._data_step(inputs or {}, now_ms, retries), results
 
+    def step_raw(self, segs, ptr, nbytes, now_ms, retries=3):
+        """GPU plane, pre-staged ingress (server gateway): runs phase A, the exchange and
+        phase B; returns (ticket for plane.finish, {seq: result})."""
+        results = self._retry(self.log.sync, retries)
+        p = self.plane
+        ticket = p.submit_raw(segs, ptr, nbytes, now_ms)
+        recv = self._retry(lambda: self.exchanger.exchange(p.pending_send_counts(), p.xfer_send_desc(),
+                                                           p.xfer_send_pay(), p.xfer_recv_desc(),
+                                                           p.xfer_recv_pay()), retries)
+        p.submit_b(recv)
+        return ticket, results
+
     def _retry(self, fn, retries):
         for attempt in range(retries + 1):
             try:

@@ -33,6 +33,8 @@ from ..protocol import constants as C
 from ..protocol.codec import Method, decode_method, encode_method_frame, encode_table
 
 HEARTBEAT = C.HEARTBEAT_FRAME
+_REPLICATED_METHODS = {"exchange.declare", "exchange.delete", "queue.declare", "queue.bind", "queue.unbind",
+                       "queue.delete"}
 
 
 class _Conn:
@@ -79,7 +81,7 @@ class GpuBroker:
     def __init__(self, plane, host="127.0.0.1", port=0, heartbeat=0, frame_max=131072, channel_max=2047,
                  idle_step_ms=2.0, product="chanamq-amd", version="0.1.0", io="native",
                  ingress_bytes=64 << 20, per_conn_read=1 << 20, mem_high_watermark=0, mem_low_watermark=0,
-                 store=None):
+                 store=None, node=None, reuseport=False):
         """``io``: "native" = C++ batched gateway (csrc/core/gateway.cpp), "python" =
         selectors loop (portable fallback)."""
         self.plane = plane
@@ -94,6 +96,12 @@ class GpuBroker:
         # durable queues x persistent messages -> store (write-behind, confirm gating)
         self.persistence = None
         self.recovered = 0
+        # sharded node (parallel/node.py): every step is a lockstep collective step;
+        # replicated control ops (exchanges, queues, bindings) go through the control
+        # log and are answered in the step that applies them on every rank
+        self.node = node
+        self.reuseport = reuseport
+        self._deferred = {}     # control-log seq -> (conn, channel, reply builder)
         if store is not None:
             from ..engine.persistence import GpuPersistence
             self.persistence = GpuPersistence(plane, store)
@@ -116,7 +124,7 @@ class GpuBroker:
     def start(self):
         if self.io == "native":
             from ..broker import load
-            self.gw = load().Gateway(self.host, self.port, self.plane.c_max, False)
+            self.gw = load().Gateway(self.host, self.port, self.plane.c_max, self.reuseport)
             self.port = self.gw.port
             if hasattr(self.plane, "mod"):
                 self._pin = self.plane.mod.alloc_pinned(self.ingress_bytes)
@@ -207,7 +215,11 @@ class GpuBroker:
                 if add:
                     segs = np.concatenate([segs, np.array(add, SEG_IN)])
             open_conns = any(c.state == "open" for c in self.conns.values())
-            if open_conns and (len(segs) or busy or now - last_step >= self.idle_step_s):
+            if self.node is not None:     # lockstep: every rank steps every tick
+                with self.lock:
+                    busy = self._step_native(segs, used, gpu)
+                last_step = now
+            elif open_conns and (len(segs) or busy or now - last_step >= self.idle_step_s):
                 with self.lock:
                     busy = self._step_native(segs, used, gpu)
                 last_step = now
@@ -222,7 +234,12 @@ class GpuBroker:
             inputs = {int(r["conn"]): bytes(self._pin[int(r["src"]):int(r["src"]) + int(r["len"])]) for r in segs}
             return self._step(inputs)
         p = self.plane
-        t = p.submit_raw(segs, self._pin.ctypes.data, used, int(time.time() * 1000))
+        now = int(time.time() * 1000)
+        if self.node is not None:
+            t, results = self.node.step_raw(segs, self._pin.ctypes.data, used, now)
+            self._answer(results)
+        else:
+            t = p.submit_raw(segs, self._pin.ctypes.data, used, now)
         res = p.finish(t, collect=True, collect_egress=False)
         self._persist_step()
         eg, co = p.host_egress(t)
@@ -387,7 +404,11 @@ class GpuBroker:
 
     # ------------------------------------------------------------------ data-plane step
     def _step(self, inputs):
-        res = self.plane.step(inputs, now_ms=int(time.time() * 1000))
+        if self.node is not None:
+            res, results = self.node.step(inputs, now_ms=int(time.time() * 1000))
+            self._answer(results)
+        else:
+            res = self.plane.step(inputs, now_ms=int(time.time() * 1000))
         self._persist_step()
         if isinstance(res, dict):   # golden plane
             egress, ctrl, events, segs, cnt = res["egress"], res["ctrl"], res["events"], res["segs"], \
@@ -431,12 +452,13 @@ class GpuBroker:
             c = self.conns.get(conn)
             if c is None:
                 continue
+            deferred = False
             if c.state == "open":
                 try:
-                    self._control(c, raw)
+                    deferred = self._control(c, raw) == "deferred"
                 except _Hard as e:
                     self._conn_close(c, e.code, e.text, e.cls, e.mid)
-            if c.state == "open":
+            if c.state == "open" and not deferred:
                 self.plane.unpause(conn)
         return had_input or had_egress or bool(ctrl) or cnt.get("n_deliv", 0) > 0
 
@@ -485,6 +507,8 @@ class GpuBroker:
         if ch not in chans:
             raise _Hard(C.CHANNEL_ERROR, f"channel {ch} is not open", m.class_id, m.method_id)
         try:
+            if self.node is not None and m.name in _REPLICATED_METHODS:
+                return self._replicated(c, ch, m)
             self._channel_method(c, ch, m)
         except ControlError as e:
             if e.code >= 500 or e.code in (C.CONNECTION_FORCED, C.INVALID_PATH):
@@ -613,6 +637,86 @@ class GpuBroker:
             raise ControlError(C.CHANNEL_ERROR, "publish on a closed channel", 60, 40)
         else:
             raise _Hard(C.COMMAND_INVALID, f"unexpected {n}", m.class_id, m.method_id)
+
+    # ------------------------------------------------------------------ sharded control ops
+    def _replicated(self, c, ch, m):
+        """Submit a replicated op to the control log; the reply (and the unpause of the
+        connection) happens in the step that applies it on every rank."""
+        p, node = self.plane, self.node
+        vh = p.conns[c.id].vhost
+        n = m.name
+        if n == "exchange.declare":
+            x = p.exchanges.get((vh, m.exchange))
+            if m.passive:
+                if x is None:
+                    raise ControlError(C.NOT_FOUND, f"no exchange '{m.exchange}' in vhost '{vh}'", 40, 10)
+                return self._send(c, ch, Method("exchange.declare_ok"))
+            if m.exchange.startswith("amq.") and x is None:
+                raise ControlError(C.ACCESS_REFUSED, f"exchange name '{m.exchange}' is reserved", 40, 10)
+            if x is not None and x.type != m.type:
+                raise ControlError(C.PRECONDITION_FAILED, f"exchange '{m.exchange}' declared as {x.type}", 40, 10)
+            seq = node.submit("declare_exchange", vh, m.exchange, m.type or "direct", durable=m.durable,
+                              auto_delete=m.auto_delete, internal=m.internal, arguments=dict(m.arguments or {}))
+            reply = None if m.nowait else (lambda r: Method("exchange.declare_ok"))
+        elif n == "exchange.delete":
+            seq = node.submit("delete_exchange", vh, m.exchange, if_unused=m.if_unused)
+            reply = None if m.nowait else (lambda r: Method("exchange.delete_ok"))
+        elif n == "queue.declare":
+            name = m.queue or ("tmp." + uuid.uuid4().hex)
+            q = p.queues.get((vh, name))
+            if m.passive:
+                if q is None:
+                    raise ControlError(C.NOT_FOUND, f"no queue '{name}' in vhost '{vh}'", 50, 10)
+                c.last_queue[ch] = name
+                cnt = p.message_count(q.slot) if q.owner == p.rank else 0
+                return self._send(c, ch, Method("queue.declare_ok", queue=name, message_count=cnt,
+                                                consumer_count=len(q.consumers)))
+            if q is None:   # client-local placement: the queue lives on the declaring rank
+                node.submit("place_queue", vh, name, p.rank)
+            args = m.arguments or {}
+            seq = node.submit("declare_queue", vh, name, durable=m.durable, auto_delete=m.auto_delete,
+                              ttl_ms=int(args.get("x-message-ttl", 0) or 0))
+            c.last_queue[ch] = name
+
+            def reply(r, name=name):
+                qq = p.queues.get((vh, name))
+                return Method("queue.declare_ok", queue=name, message_count=0,
+                              consumer_count=len(qq.consumers) if qq else 0)
+            reply = None if m.nowait else reply
+        elif n in ("queue.bind", "queue.unbind"):
+            qn = m.queue or c.last_queue.get(ch, "")
+            seq = node.submit("bind" if n == "queue.bind" else "unbind", vh, qn, m.exchange, m.routing_key)
+            ok = "queue.bind_ok" if n == "queue.bind" else "queue.unbind_ok"
+            reply = None if (n == "queue.bind" and m.nowait) else (lambda r, ok=ok: Method(ok))
+        else:   # queue.delete
+            q = self._queue(vh, m.queue or c.last_queue.get(ch, ""), 50, 40)
+            if m.if_unused and q.consumers:
+                raise ControlError(C.PRECONDITION_FAILED, f"queue '{q.name}' in use", 50, 40)
+            seq = node.submit("delete_queue", vh, q.name)
+            reply = None if m.nowait else (lambda r: Method("queue.delete_ok", message_count=0))
+        self._deferred[seq] = (c.id, ch, reply, m)
+        return "deferred"
+
+    def _answer(self, results):
+        """Replies for this rank's control-log ops applied in this step."""
+        from ..parallel.control_log import error_of
+        pending, self._deferred = self._deferred, {}
+        for seq, (conn, ch, reply, m) in pending.items():
+            c = self.conns.get(conn)
+            if c is None or c.state != "open":
+                continue
+            res = results.get(seq)
+            err = error_of(res)
+            if err:
+                code, text, cls, mid = err
+                if code >= 500:
+                    self._conn_close(c, code, text, cls or m.class_id, mid or m.method_id)
+                    continue
+                self._chan_close(c, ch, code, text, m.class_id, m.method_id)
+            elif reply is not None:
+                self._send(c, ch, reply(res))
+            if c.state == "open":
+                self.plane.unpause(conn)
 
     def _queue(self, vh, name, cls, mid):
         q = self.plane.queues.get((vh, name))

@@ -1,0 +1,62 @@
+"""Two ranks of the sharded GPU server (golden planes, gloo) started by the launcher:
+clients on different ranks declare, bind, publish and consume; messages cross ranks
+through the per-step all-to-all; replicated ops are answered once applied everywhere."""
+
+import json
+import os
+import time
+
+import pytest
+
+from chanamq_amd.client import ChannelClosed, Connection
+from test_sharded_golden import _free_port
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+@pytest.fixture()
+def cluster(tmp_path):
+    from chanamq_amd.parallel.launch import Launcher
+    port = _free_port()
+    env = dict(os.environ, PYTHONPATH=os.path.dirname(HERE))
+    ln = Launcher(2, ["-m", "chanamq_amd.server.sharded", "--plane", "golden", "--port", str(port),
+                      "--info-dir", str(tmp_path)], env=env).start()
+    deadline = time.time() + 120
+    while time.time() < deadline and not all((tmp_path / f"rank{r}.json").exists() for r in range(2)):
+        assert not ln.poll(), f"rank exited early: {ln.poll()}"
+        time.sleep(0.2)
+    ports = [json.load(open(tmp_path / f"rank{r}.json"))["port"] for r in range(2)]
+    yield ports
+    ln.stop()
+
+
+@pytest.mark.timeout(300)
+def test_cross_rank_routing_and_replicated_topology(cluster):
+    c0 = Connection(port=cluster[0], vhost="/")
+    c1 = Connection(port=cluster[1], vhost="/")
+    a = c0.channel()
+    a.exchange_declare("sx", "topic")
+    a.queue_declare("qa")
+    a.queue_bind("qa", "sx", "a.*")
+    b = c1.channel()
+    b.exchange_declare("sx", "topic", passive=True)   # replicated to rank 1 already
+    b.queue_declare("qb")
+    b.queue_bind("qb", "sx", "*.b")
+    a.basic_consume("qa", "ca", no_ack=True)
+    b.basic_consume("qb", "cb", no_ack=True)
+    p = c0.channel()
+    for k in ("a.b", "a.x", "z.b"):
+        p.basic_publish("sx", k, k.encode())
+    assert [d.body for d in a.consume_n(2)] == [b"a.b", b"a.x"]
+    assert [d.body for d in b.consume_n(2)] == [b"a.b", b"z.b"]
+    # publishes from rank 1 reach rank 0's queue too
+    p1 = c1.channel()
+    p1.basic_publish("sx", "a.q", b"from-1")
+    assert a.consume_n(1)[0].body == b"from-1"
+    # consumers attach on the owning rank
+    with pytest.raises(ChannelClosed) as e:
+        c1.channel().basic_consume("qa", "remote")
+        c1.process(1.0)
+    assert e.value.code == 530
+    c0.close()
+    c1.close()
