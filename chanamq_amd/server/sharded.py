@@ -27,11 +27,16 @@ def main(argv=None):
     ap.add_argument("--info-dir", default="")
     ap.add_argument("--idle-step-ms", type=float, default=1.0)
     ap.add_argument("--c-max", type=int, default=256)
+    ap.add_argument("--backend", default="", help="default: nccl (RCCL) for --plane gpu, gloo for golden; "
+                                                  "gloo + gpu rehearses several ranks on one GPU")
     args = ap.parse_args(argv)
 
     from ..parallel.launch import join
-    backend = "nccl" if args.plane == "gpu" else "gloo"
+    backend = args.backend or ("nccl" if args.plane == "gpu" else "gloo")
     rank, world, store = join(backend)
+    if args.plane == "gpu" and backend != "nccl":
+        import torch
+        torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", rank)) % max(1, torch.cuda.device_count()))
     from ..parallel.comm import Comm
     from ..parallel.node import ShardedNode
     if args.plane == "gpu":

@@ -14,13 +14,14 @@ from test_sharded_golden import _free_port
 HERE = os.path.dirname(os.path.abspath(__file__))
 
 
-@pytest.fixture()
-def cluster(tmp_path):
+@pytest.fixture(params=["golden", pytest.param("gpu", marks=pytest.mark.gpu)])
+def cluster(request, tmp_path):
     from chanamq_amd.parallel.launch import Launcher
     port = _free_port()
     env = dict(os.environ, PYTHONPATH=os.path.dirname(HERE))
-    ln = Launcher(2, ["-m", "chanamq_amd.server.sharded", "--plane", "golden", "--port", str(port),
-                      "--info-dir", str(tmp_path)], env=env).start()
+    extra = ["--backend", "gloo"] if request.param == "gpu" else []   # 2 ranks share the one test GPU
+    ln = Launcher(2, ["-m", "chanamq_amd.server.sharded", "--plane", request.param, "--port", str(port),
+                      "--info-dir", str(tmp_path)] + extra, env=env).start()
     deadline = time.time() + 120
     while time.time() < deadline and not all((tmp_path / f"rank{r}.json").exists() for r in range(2)):
         assert not ln.poll(), f"rank exited early: {ln.poll()}"
