@@ -37,21 +37,24 @@ def build_workload(dp, rank, producers, queues, body, chunk, blocks, cons_base, 
     """``shards`` > 1: the replicated topology of a sharded broker (every rank declares
     every queue; queue bench.q.{r}.{i} is placed on rank r and consumed there).
     kind "topic" = config 2 (``queues`` per rank, one key pattern each); "fanout" =
-    config 3 (every publish goes to every queue of the node)."""
+    config 3 (every publish goes to every queue of the node); "storm" = config 5 (direct,
+    manual-ack consumers that ack everything each step and nack-requeue everything every
+    4th step)."""
     from chanamq_amd.engine.layout import SEG_IN
     from chanamq_amd.engine.traffic import even_split, publish_stream
 
     vh = "AMQ.DEFAULT"
-    xname = "bench.topic" if kind == "topic" else "bench.fanout"
-    dp.declare_exchange(vh, xname, kind)
+    xname = {"topic": "bench.topic", "fanout": "bench.fanout", "storm": "bench.direct"}[kind]
+    dp.declare_exchange(vh, xname, "direct" if kind == "storm" else kind)
     owners = range(shards) if shards > 1 else [rank]
     for r in owners:
         for i in range(queues):
             qn = f"bench.q.{r}.{i}"
             if shards > 1:
                 dp.shard_map.place(vh, qn, r)
-            dp.declare_queue(vh, qn, capacity=1 << 20 if kind == "topic" else 1 << 14)
-            dp.bind(vh, qn, xname, f"bench.{r}.{i}.*" if kind == "topic" else "")
+            dp.declare_queue(vh, qn, capacity=1 << 14 if kind == "fanout" else 1 << 20)
+            key = {"topic": f"bench.{r}.{i}.*", "fanout": "", "storm": f"bench.{r}.{i}"}[kind]
+            dp.bind(vh, qn, xname, key)
     for p in range(producers):
         dp.open_connection(p, vh)
         dp.open_channel(p, 1)
@@ -59,7 +62,9 @@ def build_workload(dp, rank, producers, queues, body, chunk, blocks, cons_base, 
         c = cons_base + i
         dp.open_connection(c, vh)
         dp.open_channel(c, 1)
-        dp.consume(c, 1, vh, f"bench.q.{rank}.{i}", f"ctag-{i}", no_ack=True)
+        if kind == "storm":
+            dp.qos(c, 1, prefetch_count=512)
+        dp.consume(c, 1, vh, f"bench.q.{rank}.{i}", f"ctag-{i}", no_ack=kind != "storm")
     # one message on the wire is ~1.08 KB; each producer gets `blocks` chunks of ~chunk bytes
     probe = publish_stream(1, xname, lambda i: f"bench.{rank}.0.x0", body)
     per_prod = max(1, (chunk * blocks) // len(probe))
@@ -67,13 +72,25 @@ def build_workload(dp, rank, producers, queues, body, chunk, blocks, cons_base, 
     nq = queues * len(owners)
     for p in range(producers):
         rng_q = np.random.default_rng(1000 + rank * 7919 + p).integers(0, nq, size=per_prod)
-        s = publish_stream(per_prod, xname,
-                           lambda i, r=rng_q: f"bench.{owners[r[i] // queues]}.{r[i] % queues}.x{i % 10}", body,
-                           seed=p)
+        if kind == "storm":
+            keyf = (lambda i, r=rng_q: f"bench.{owners[r[i] // queues]}.{r[i] % queues}")
+        else:
+            keyf = (lambda i, r=rng_q: f"bench.{owners[r[i] // queues]}.{r[i] % queues}.x{i % 10}")
+        s = publish_stream(per_prod, xname, keyf, body, seed=p)
         streams.append(even_split(s, blocks))
     # block-major pinned pool: block b = chunk b of every producer, 16-B aligned
     sizes = [[len(streams[p][b]) for p in range(producers)] for b in range(blocks)]
-    block_len = [sum((n + 15) & ~15 for n in row) for row in sizes]
+    ctl = b""
+    if kind == "storm":   # consumer frames: ack-all, nack-all-requeue (delivery-tag 0 + multiple)
+        from chanamq_amd.engine.traffic import ack_frame
+        from chanamq_amd.protocol.codec import Method, render_command
+        ack = ack_frame(1, 0, multiple=True)
+        nack = render_command(1, Method("basic.nack", delivery_tag=0, multiple=True, requeue=True))
+        ctl = ack + b"\0" * ((-len(ack)) % 16) + nack
+        ctl += b"\0" * ((-len(ctl)) % 16)
+    # each block = the producers' chunks, then the consumer control frames (storm)
+    data_len = [sum((n + 15) & ~15 for n in row) for row in sizes]
+    block_len = [n + len(ctl) for n in data_len]
     total = sum(block_len)
     pool = dp.mod.alloc_pinned(total + 64)
     segs, offs = [], []
@@ -88,9 +105,18 @@ def build_workload(dp, rank, producers, queues, body, chunk, blocks, cons_base, 
             sg[p] = (p, len(data), rel)
             rel += (len(data) + 15) & ~15
         segs.append(sg)
+        if ctl:
+            pool[off + data_len[b]:off + data_len[b] + len(ctl)] = np.frombuffer(ctl, np.uint8)
         off += block_len[b]
     msgs_per_step = per_prod * producers / blocks
-    return pool, segs, offs, block_len, msgs_per_step, len(probe)
+    extra = None
+    if kind == "storm":   # per-step consumer segments, offsets relative to each block's base
+        extra = {}
+        nack_rel = len(ack) + ((-len(ack)) % 16)
+        for name, o, ln in (("ack", 0, len(ack)), ("nack", nack_rel, len(nack))):
+            extra[name] = [np.array([(cons_base + i, ln, data_len[b] + o) for i in range(queues)], SEG_IN)
+                           for b in range(blocks)]
+    return pool, segs, offs, block_len, msgs_per_step, len(probe), extra
 
 
 def main():
@@ -108,7 +134,7 @@ def main():
                     help="egress D2H: the runtime blit copy (default, fastest measured), the runtime's NoCU "
                          "copy request, or our copy kernel on --copy-wgs workgroups")
     ap.add_argument("--copy-wgs", type=int, default=16)
-    ap.add_argument("--workload", choices=["topic", "fanout"], default="topic",
+    ap.add_argument("--workload", choices=["topic", "fanout", "storm"], default="topic",
                     help="topic = BASELINE config 2 (default, the headline); fanout = config 3 "
                          "(--queues is then the node total, default 1024, with small publish batches)")
     ap.add_argument("--mode", choices=["sharded", "independent"], default="sharded",
@@ -135,10 +161,15 @@ def main():
     from chanamq_amd.engine.dataplane import GpuDataPlane
 
     fan = args.workload == "fanout"
+    storm = args.workload == "storm"
     if fan and args.queues == 16:
         args.queues = 1024
     if fan and args.producers == 256:
         args.producers, args.chunk = 16, 4096
+    if storm and args.queues == 16:     # config 5: 64 producers x 64 manual-ack consumers per GPU
+        args.queues = 64
+    if storm and args.producers == 256:
+        args.producers, args.chunk = 64, 16384
     shards = world if (world > 1 and args.mode == "sharded") else 1
     P = args.producers
     Q = max(1, args.queues // shards) if fan else args.queues    # queues per rank
@@ -157,9 +188,11 @@ def main():
         dp = GpuDataPlane(device=local, worker=rank, world=world, rank=rank, exchanger=Exchanger(), **cfg)
     else:
         dp = GpuDataPlane(device=local, worker=rank, **cfg)
-    pool, segs, offs, blens, mps, msg_bytes = build_workload(dp, rank, P, Q, args.body, args.chunk,
-                                                             args.blocks, cons_base=P, shards=shards,
-                                                             kind=args.workload)
+    pool, segs, offs, blens, mps, msg_bytes, extra = build_workload(dp, rank, P, Q, args.body, args.chunk,
+                                                                    args.blocks, cons_base=P, shards=shards,
+                                                                    kind=args.workload)
+    flow_high = 1 << 30      # storm: producers pause (Channel.Flow) above 1 GiB of stored bodies
+    flow = {"paused": False, "paused_steps": 0, "requeued": 0}
     base = pool.ctypes.data
     step_i = 0
 
@@ -180,10 +213,22 @@ def main():
             pb += c["n_pubs"]
             eg += c["egress_bytes"]
             hist[:] += np.array(c["lat_hist"], np.int64)
+            if storm:
+                flow["requeued"] += c["n_requeue"]
+                flow["paused"] = c["live_bytes"] > flow_high
 
         for _ in range(n):
             b = step_i % args.blocks
-            pending.append(dp.submit_raw(segs[b], base + offs[b], blens[b]))
+            if storm:   # ack-all each step, nack-all-requeue every 4th: a redelivery storm
+                cs = extra["nack" if step_i % 4 == 3 else "ack"][b]
+                if flow["paused"]:
+                    flow["paused_steps"] += 1
+                    sg = cs
+                else:
+                    sg = np.concatenate([segs[b], cs])
+                pending.append(dp.submit_raw(sg, base + offs[b], blens[b]))
+            else:
+                pending.append(dp.submit_raw(segs[b], base + offs[b], blens[b]))
             step_i += 1
             if len(pending) > 1:
                 t = pending.pop(0)
@@ -249,10 +294,13 @@ def main():
             "dtype": "uint8 (AMQP wire bytes; no floating-point compute)",
             "data": "synthetic AMQP 0-9-1 publish traffic (random 1 KB bodies), empty-init broker state",
             "config": {
-                "model": (f"BASELINE config 2: 1 topic exchange, {Q} bound queues per GPU, {args.body} B msgs, "
-                          "auto-ack, non-persistent") if not fan else
-                         (f"BASELINE config 3: fanout exchange -> {qtot} queues ({Q} per GPU), {args.body} B msgs, "
-                          "auto-ack, non-persistent; value = deliveries/s"),
+                "model": (f"BASELINE config 3: fanout exchange -> {qtot} queues ({Q} per GPU), {args.body} B msgs, "
+                          "auto-ack, non-persistent; value = deliveries/s") if fan else
+                         (f"BASELINE config 5: direct exchange, {P} producers x {Q} manual-ack consumers per GPU "
+                          f"(prefetch 512), ack-all each step, nack-all-requeue every 4th step, producer flow "
+                          f"pause above 1 GiB; value = deliveries/s incl. redeliveries") if storm else
+                         (f"BASELINE config 2: 1 topic exchange, {Q} bound queues per GPU, {args.body} B msgs, "
+                          "auto-ack, non-persistent"),
                 "global_batch": int(round(mps * world)),
                 "seq_len": args.body,
                 "parallelism": (f"queue-sharded x{world}: one broker, cross-GPU routing by RCCL all-to-all"
@@ -267,6 +315,8 @@ def main():
             "egress_GBps": eg / t / 1e9,
             "latency_note": "in-broker publish->deliver (ingress submit to egress bytes ready), no TCP",
             "diag": errs,
+            "storm": ({"requeued_msgs": flow["requeued"], "flow_paused_steps": flow["paused_steps"]}
+                      if storm else None),
             "cross_gpu_bytes_per_s": (dp.exchanger.bytes_sent * world / t) if shards > 1 else 0.0,
         }
         print(json.dumps(out))

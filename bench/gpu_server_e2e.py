@@ -61,11 +61,14 @@ def main():
             b.stop()
             if store is not None:
                 store.close()
+        lc = getattr(plane, "last_counters", {}) or {}
         r.update(name=name, spec=spec, recv_msgs_per_s=r["received"] / r["elapsed"],
-                 sent_msgs_per_s=r["sent"] / r["elapsed"], steps=b.stats["steps"])
+                 sent_msgs_per_s=r["sent"] / r["elapsed"], steps=b.stats["steps"], server=dict(b.stats),
+                 last_step={k: lc.get(k) for k in ("n_pubs", "n_deliv", "n_ring_full", "n_live_msgs", "live_bytes",
+                                                   "n_dropped_nomem", "egress_bytes")})
         results[name] = r
         print(json.dumps({k: r[k] for k in ("name", "recv_msgs_per_s", "sent_msgs_per_s", "p50_us", "p99_us",
-                                            "steps", "error")}), flush=True)
+                                            "steps", "error", "server", "last_step")}), flush=True)
         del plane
     if args.out:
         with open(args.out, "w") as f:
