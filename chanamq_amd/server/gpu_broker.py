@@ -80,7 +80,7 @@ def _frames(buf):
 class GpuBroker:
     def __init__(self, plane, host="127.0.0.1", port=0, heartbeat=0, frame_max=131072, channel_max=2047,
                  idle_step_ms=2.0, product="chanamq-amd", version="0.1.0", io="native",
-                 ingress_bytes=64 << 20, per_conn_read=1 << 20, mem_high_watermark=0, mem_low_watermark=0,
+                 ingress_bytes=64 << 20, per_conn_read=256 << 10, mem_high_watermark=0, mem_low_watermark=0,
                  store=None, node=None, reuseport=False):
         """``io``: "native" = C++ batched gateway (csrc/core/gateway.cpp), "python" =
         selectors loop (portable fallback)."""
@@ -102,6 +102,7 @@ class GpuBroker:
         self.node = node
         self.reuseport = reuseport
         self._deferred = {}     # control-log seq -> (conn, channel, reply builder)
+        self._rpaused = set()
         if store is not None:
             from ..engine.persistence import GpuPersistence
             self.persistence = GpuPersistence(plane, store)
@@ -244,6 +245,7 @@ class GpuBroker:
         self._persist_step()
         eg, co = p.host_egress(t)
         self.gw.send_egress(eg, co.view(np.uint32), p.c_max)
+        self._read_backpressure(segs)
         return self._after_step(res.ctrl, res.events, [(s[0], s[1]) for s in res.segs], res.counters,
                                 bool(len(segs)), bool(co["len"].any()))
 
@@ -446,8 +448,9 @@ class GpuBroker:
                 self._conn_close(c, C.FRAME_ERROR, "malformed frame")
             elif status & SS_UNEXPECTED:
                 self._conn_close(c, C.UNEXPECTED_FRAME, "unexpected frame")
-            elif status & (SS_TOO_LARGE | SS_OVERFLOW):
+            elif status & SS_TOO_LARGE:
                 self._conn_close(c, C.FRAME_ERROR, "command exceeds the server's limits")
+            # SS_OVERFLOW is a per-step capacity limit: the rest stays in the carry
         for conn, raw in ctrl:
             c = self.conns.get(conn)
             if c is None:
@@ -461,6 +464,21 @@ class GpuBroker:
             if c.state == "open" and not deferred:
                 self.plane.unpause(conn)
         return had_input or had_egress or bool(ctrl) or cnt.get("n_deliv", 0) > 0
+
+    def _read_backpressure(self, segs):
+        """Stop reading a connection while the device still holds a large backlog of its
+        bytes (carry); resume once it drains."""
+        carry = self.plane.carry
+        for cid in segs["conn"]:
+            cid = int(cid)
+            big = carry[cid] > self.per_conn_read
+            if big != (cid in self._rpaused):
+                self.gw.set_read_paused(cid, big)
+                (self._rpaused.add if big else self._rpaused.discard)(cid)
+        for cid in list(self._rpaused):
+            if carry[cid] <= self.per_conn_read:
+                self.gw.set_read_paused(cid, False)
+                self._rpaused.discard(cid)
 
     def _persist_step(self):
         """Store rows of this step, committed (fsync) before the step's egress — which

@@ -173,6 +173,7 @@ PYBIND11_MODULE(_core, m) {
            })
       .def("flush", &Gateway::flush, py::call_guard<py::gil_scoped_release>())
       .def("set_data_mode", &Gateway::set_data_mode)
+      .def("set_read_paused", &Gateway::set_read_paused)
       .def("close", &Gateway::close)
       .def("pending_bytes", &Gateway::pending_bytes);
 

@@ -97,6 +97,7 @@ GwPoll Gateway::poll(int timeout_ms, uint8_t* buf, uint64_t cap, uint64_t per_co
     if (c.fd < 0) continue;
     if (evs[i].events & EPOLLOUT) write_some(c);
     if (!(evs[i].events & (EPOLLIN | EPOLLHUP | EPOLLERR))) continue;
+    if (c.rpause && !(evs[i].events & (EPOLLHUP | EPOLLERR))) continue;
     uint64_t start = (off + 15) & ~15ull;
     uint64_t room = cap > start ? cap - start : 0;
     if (room > per_conn_cap) room = per_conn_cap;
@@ -182,6 +183,10 @@ void Gateway::flush() {
 
 void Gateway::set_data_mode(uint32_t conn, bool on) {
   if (conn < conns_.size()) conns_[conn].data = on;
+}
+
+void Gateway::set_read_paused(uint32_t conn, bool on) {
+  if (conn < conns_.size()) conns_[conn].rpause = on;
 }
 
 void Gateway::close(uint32_t conn) {

@@ -31,6 +31,7 @@ struct GwConn {
   uint32_t id = 0;
   bool data = false;      // bytes go to the data plane (else: handshake bytes to the host)
   bool dead = false;
+  bool rpause = false;    // reads paused (ingress back-pressure: the data plane still holds a backlog)
   std::string out;        // pending egress
   size_t out_pos = 0;
 };
@@ -53,6 +54,7 @@ class Gateway {
   uint64_t send_egress(const uint8_t* egress, const uint32_t* conn_out, uint32_t n_slots);
   void flush();
   void set_data_mode(uint32_t conn, bool on);
+  void set_read_paused(uint32_t conn, bool on);
   void close(uint32_t conn);
   uint64_t pending_bytes() const;
   uint64_t rx_bytes = 0, tx_bytes = 0;
