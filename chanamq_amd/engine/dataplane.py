@@ -36,10 +36,11 @@ class StepResult:
 
 class GpuDataPlane(ControlState):
     def __init__(self, device=0, hash_wildcard=True, graph=True, worker=0, default_queue_capacity=1 << 16,
-                 world=1, rank=0, shard_map=None, exchanger=None, **cfg):
+                 world=1, rank=0, shard_map=None, exchanger=None, exchange_lag=0, **cfg):
         self.mod = ops.load()
         full = dict(cfg)
-        full.update(device=device, hash_wildcard=int(hash_wildcard), graph=int(graph), world=world, rank=rank)
+        full.update(device=device, hash_wildcard=int(hash_wildcard), graph=int(graph), world=world, rank=rank,
+                    exchange_lag=int(exchange_lag))
         self.eng = self.mod.Engine(full)
         self.info = self.eng.info()
         sz = self.info["sizeof"]
@@ -58,17 +59,25 @@ class GpuDataPlane(ControlState):
         self._pin = [None, None]
         self.exchanger = exchanger
         self._pending = None
+        self.lag = False
         if world > 1:
             # exchange operands live in torch's allocator so RCCL can use them directly
             import torch
             dev = torch.device("cuda", device)
             u8 = torch.uint8
-            self._xs_desc = torch.empty(i["xfer_desc_max"] * RDESC.itemsize, dtype=u8, device=dev)
-            self._xs_pay = torch.empty(i["xfer_bytes"], dtype=u8, device=dev)
-            self._xr_desc = torch.empty(i["import_max"] * RDESC.itemsize, dtype=u8, device=dev)
-            self._xr_pay = torch.empty(i["xfer_bytes"], dtype=u8, device=dev)
-            self.eng.set_xfer_buffers(self._xs_desc.data_ptr(), self._xs_pay.data_ptr(),
-                                      self._xr_desc.data_ptr(), self._xr_pay.data_ptr())
+            self.lag = bool(i["exchange_lag"])
+            nb = 2 if self.lag else 1
+            self._xs = [(torch.empty(i["xfer_desc_max"] * RDESC.itemsize, dtype=u8, device=dev),
+                         torch.empty(i["xfer_bytes"], dtype=u8, device=dev)) for _ in range(nb)]
+            self._xr = [(torch.empty(i["import_max"] * RDESC.itemsize, dtype=u8, device=dev),
+                         torch.empty(i["xfer_bytes"], dtype=u8, device=dev)) for _ in range(nb)]
+            if self.lag:   # parity p packs into S[p] and imports R[p^1] (the previous step's exchange)
+                for p in (0, 1):
+                    self.eng.set_xfer_parity(p, self._xs[p][0].data_ptr(), self._xs[p][1].data_ptr(),
+                                             self._xr[p ^ 1][0].data_ptr(), self._xr[p ^ 1][1].data_ptr())
+            else:
+                self.eng.set_xfer_buffers(self._xs[0][0].data_ptr(), self._xs[0][1].data_ptr(),
+                                          self._xr[0][0].data_ptr(), self._xr[0][1].data_ptr())
         super().__init__(c_max=i["c_max"], chpc=i["chpc"], q_max=i["q_max"], x_max=i["x_max"],
                          cons_max=i["cons_max"], hash_wildcard=hash_wildcard, ring_pool=i["ring_pool"],
                          default_queue_capacity=default_queue_capacity, world=world, rank=rank,
@@ -444,26 +453,40 @@ class GpuDataPlane(ControlState):
                 raise RuntimeError("cross-rank send buffers overflowed (xfer_desc_max / xfer_bytes)")
             self._send_counts = cnt[:-1]
             if self.exchanger is not None:   # one process per rank: collective now
-                recv = self.exchanger.exchange(self._send_counts, self._xs_desc, self._xs_pay,
-                                               self._xr_desc, self._xr_pay)
-                self.submit_b(recv)
+                recv = self.exchanger.exchange(self._send_counts, self.xfer_send_desc(), self.xfer_send_pay(),
+                                               self.xfer_recv_desc(), self.xfer_recv_pay())
+                if self.lag:
+                    self.set_import(recv)
+                else:
+                    self.submit_b(recv)
         return (p, len(segs), t0)
 
     # ---- sharded step, phase B (LocalCluster drives it after its in-process exchange)
     def pending_send_counts(self):
         return self._send_counts
 
+    # exchange operands of the step in flight (lag: S[p] -> R[p], imported by the next step)
+    def _xp(self):
+        return self._pending if self.lag else 0
+
     def xfer_send_desc(self):
-        return self._xs_desc
+        return self._xs[self._xp()][0]
 
     def xfer_send_pay(self):
-        return self._xs_pay
+        return self._xs[self._xp()][1]
 
     def xfer_recv_desc(self):
-        return self._xr_desc
+        return self._xr[self._xp()][0]
 
     def xfer_recv_pay(self):
-        return self._xr_pay
+        return self._xr[self._xp()][1]
+
+    def set_import(self, recv):
+        """exchange_lag: this step's exchange is complete on the current torch stream; the
+        next step's phase B imports it."""
+        import torch
+        stream = torch.cuda.current_stream(self.device).cuda_stream
+        self.eng.set_import([int(x) for x in recv], int(stream))
 
     def submit_b(self, recv):
         import torch

@@ -41,9 +41,11 @@ class _Msg:
 class GoldenDataPlane(ControlState):
     def __init__(self, hash_wildcard=True, ucap=8192, deliver_cap=4096, carry_cap=1 << 20,
                  egress_cap=96 << 20, deliv_max=65536, exchanger=None, xfer_desc_max=1 << 15,
-                 xfer_bytes=1 << 24, persist=False, **kw):
+                 xfer_bytes=1 << 24, persist=False, exchange_lag=0, **kw):
         super().__init__(hash_wildcard=hash_wildcard, **kw)
         self.persist = persist
+        self.lag = bool(exchange_lag) and self.world > 1
+        self._lag_prev = []                 # exchange_lag: records received last step
         self._persist_out, self._consumed_out = [], []
         self.exchanger = exchanger
         self._outbox = defaultdict(list)  # dest rank -> [(RDesc fields, payload)]
@@ -323,39 +325,49 @@ class GoldenDataPlane(ControlState):
             self._xs_pay[:len(pay)] = torch.frombuffer(bytearray(pay), dtype=torch.uint8)
         return n + b
 
-    def _import(self, recv, now_ms):
-        """Enqueue the step's messages in (source rank, connection, publish) order: this
-        rank's own publishes at its rank position, records from rank s at s's — the
-        order the GPU pair sort produces with its (queue, source rank) keys."""
+    def _parse_recv(self, recv):
+        """Received records -> [(source rank, exch, flags, expire, ex, rk, props, body)]."""
         W = self.world
         rn, rb = recv[:W], recv[W:2 * W]
         tot = sum(rn)
-        desc = self._xr_desc[:tot * RDESC.itemsize].numpy().view(RDESC) if tot else None
-        pay = self._xr_pay[:sum(rb)].numpy().tobytes() if tot else b""
+        if not tot:
+            return []
+        desc = self._xr_desc[:tot * RDESC.itemsize].numpy().view(RDESC)
+        pay = self._xr_pay[:sum(rb)].numpy().tobytes()
         pbase = [sum(rb[:s]) for s in range(W)]
-        i = 0
+        out, i = [], 0
         for s in range(W):
-            if s == self.rank:
-                for msg, qs, expire in self._deferred:
-                    self._enqueue(msg, qs, expire, now_ms)
-                self._deferred = []
             for _ in range(rn[s]):
                 d = desc[i]
                 i += 1
                 o = pbase[s] + int(d["pay_off"])
                 exl, rkl, pl, bl = int(d["ex_len"]), int(d["rk_len"]), int(d["props_len"]), int(d["body_len"])
-                ex = pay[o:o + exl]
-                rk = pay[o + exl:o + exl + rkl]
-                props = pay[o + exl + rkl:o + exl + rkl + pl]
-                body = pay[o + exl + rkl + pl:o + exl + rkl + pl + bl]
-                x = self.exch_by_slot.get(int(d["exch"]))
+                out.append((s, int(d["exch"]), int(d["flags"]), int(d["expire_ms"]), pay[o:o + exl],
+                            pay[o + exl:o + exl + rkl], pay[o + exl + rkl:o + exl + rkl + pl],
+                            pay[o + exl + rkl + pl:o + exl + rkl + pl + bl]))
+        return out
+
+    def _import(self, records, now_ms):
+        """Enqueue the step's messages in (source rank, connection, publish) order: this
+        rank's own publishes at its rank position, records from rank s at s's — the
+        order the GPU pair sort produces with its (queue, source rank) keys."""
+        by_src = defaultdict(list)
+        for r in records:
+            by_src[r[0]].append(r)
+        for s in range(self.world):
+            if s == self.rank:
+                for msg, qs, expire in self._deferred:
+                    self._enqueue(msg, qs, expire, now_ms)
+                self._deferred = []
+            for _, exch, flags, expire, ex, rk, props, body in by_src.get(s, []):
+                x = self.exch_by_slot.get(exch)
                 if x is None:
                     continue
                 qs = [q for q in self._route(x, rk) if self.queue_by_slot[q].owner == self.rank]
                 if not qs:
                     continue
-                msg = _Msg(ex, rk, props, body, len(qs), self.step_no, int(d["flags"]) & MF_PERSIST)
-                self._enqueue(msg, qs, int(d["expire_ms"]), now_ms)
+                msg = _Msg(ex, rk, props, body, len(qs), self.step_no, flags & MF_PERSIST)
+                self._enqueue(msg, qs, expire, now_ms)
 
     def step_a(self, inputs=None, now_ms=0):
         inputs = inputs or {}
@@ -402,7 +414,10 @@ class GoldenDataPlane(ControlState):
         out, returns, acks, now_ms = st["out"], st["returns"], st["acks"], st["now_ms"]
         cnt = self.counters
         if recv is not None:
-            self._import(recv, now_ms)
+            records = self._parse_recv(recv)
+            if self.lag:   # exchange_lag: import what arrived last step, keep this step's
+                records, self._lag_prev = self._lag_prev, records
+            self._import(records, now_ms)
         # ---- acks
         for cmd, data in acks:
             s = cmd["chslot"]

@@ -35,7 +35,10 @@ class LocalCluster:
         out = []
         for r, p in enumerate(self.planes):
             if gpu:
-                p.submit_b(recv[r])
+                if p.lag:   # phase B already ran (importing the previous exchange)
+                    p.set_import(recv[r])
+                else:
+                    p.submit_b(recv[r])
                 out.append(p.finish(tickets[r]))
             else:
                 out.append(p.step_b(recv[r]))

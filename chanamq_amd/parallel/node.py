@@ -55,7 +55,10 @@ class ShardedNode:
         recv = self._retry(lambda: self.exchanger.exchange(p.pending_send_counts(), p.xfer_send_desc(),
                                                            p.xfer_send_pay(), p.xfer_recv_desc(),
                                                            p.xfer_recv_pay()), retries)
-        p.submit_b(recv)
+        if p.lag:
+            p.set_import(recv)
+        else:
+            p.submit_b(recv)
         return ticket, results
 
     def _retry(self, fn, retries):
@@ -80,7 +83,10 @@ class ShardedNode:
                                                            p.xfer_send_pay(), p.xfer_recv_desc(),
                                                            p.xfer_recv_pay()), retries)
         if gpu:
-            p.submit_b(recv)
+            if p.lag:
+                p.set_import(recv)
+            else:
+                p.submit_b(recv)
             return p.finish(ticket)
         return p.step_b(recv)
 

@@ -61,6 +61,10 @@ class Engine {
     // Each publish is shipped at most once per other rank and its record payload never
     // exceeds its wire bytes, so these defaults cannot overflow (records / bytes per step).
     d_.import_max = d_.world > 1 ? (u32)get("import_max", (d_.world - 1) * d_.pub_max) : 0;
+    // exchange_lag = 1: step t's phase B imports the records of step t-1's all-to-all, so
+    // phases A and B launch back to back and the collective overlaps the next step's
+    // kernels (cross-GPU publishes are delivered one step later)
+    lag_ = d_.world > 1 && get("exchange_lag", 0) != 0;
     d_.pub_cap = ((d_.pub_max + d_.import_max + 63) / 64) * 64;
     d_.xfer_desc_max = d_.world > 1 ? (u32)get("xfer_desc_max", (d_.world - 1) * d_.pub_max) : 0;
     // persistence + recovery: restore batches reuse the import path (world == 1: own buffers)
@@ -470,6 +474,7 @@ class Engine {
     o["tb_max"] = d_.tb_max; o["tb_pad"] = d_.tb_pad; o["log_bytes"] = d_.log_bytes;
     o["ingress_cap"] = d_.ingress_cap; o["egress_cap"] = d_.egress_cap; o["ring_pool"] = d_.ring_pool;
     o["work_cap"] = d_.work_cap; o["total_bytes"] = total_bytes_; o["req_max"] = d_.req_max;
+    o["exchange_lag"] = lag_ ? 1 : 0;
     o["world"] = d_.world; o["rank"] = d_.my_rank; o["import_max"] = d_.import_max; o["pub_cap"] = d_.pub_cap;
     o["copy_engine"] = copy_mode_ == 2 ? "kernel" : (sdma_ ? "nocu" : "blit");
     o["copy_wgs"] = copy_wgs_;
@@ -524,9 +529,32 @@ class Engine {
     } else {
       launch_main(s_comp_, io_[p]);
     }
-    if (d_.world > 1) {
+    if (d_.world > 1 && lag_) {
+      HIPCHECK(hipEventRecord(ev_a_[p], s_comp_));
+      counts_ready_[p] = true;
+      // phase B right behind phase A: imports the previous step's exchange
+      u32* x = (u32*)buf("xchg" + std::to_string(p)).ptr;
+      for (u32 r = 0; r < d_.world; ++r) {
+        x[2 * WORLD_MAX + r] = lag_recv_.size() == 2 * d_.world ? lag_recv_[r] : 0;
+        x[3 * WORLD_MAX + r] = lag_recv_.size() == 2 * d_.world ? lag_recv_[d_.world + r] : 0;
+      }
+      lag_recv_.clear();
+      if (lag_stream_) {
+        HIPCHECK(hipEventRecord(ev_ext_[p], (hipStream_t)lag_stream_));
+        HIPCHECK(hipStreamWaitEvent(s_comp_, ev_ext_[p], 0));
+        lag_stream_ = 0;
+      }
+      if (graph_enabled_) {
+        if (!graph_b_[p]) capture_b(p);
+        HIPCHECK(hipGraphLaunch(graph_b_[p], s_comp_));
+      } else {
+        launch_phase_b(s_comp_, io_[p]);
+      }
+      HIPCHECK(hipEventRecord(ev_done_[p], s_comp_));
+    } else if (d_.world > 1) {
       HIPCHECK(hipEventRecord(ev_a_[p], s_comp_));
       phase_a_[p] = true;
+      counts_ready_[p] = true;
     } else {
       HIPCHECK(hipEventRecord(ev_done_[p], s_comp_));
     }
@@ -538,7 +566,8 @@ class Engine {
   // sharded step, after submit(): wait for phase A and return the per-destination send
   // counts [records x world, bytes x world, overflow]
   std::vector<u32> send_counts(int p) {
-    if (!phase_a_[p]) throw std::runtime_error("send_counts: no phase-A step in flight for this parity");
+    if (!counts_ready_[p]) throw std::runtime_error("send_counts: no phase-A step in flight for this parity");
+    counts_ready_[p] = false;
     HIPCHECK(hipEventSynchronize(ev_a_[p]));
     const u32* x = (const u32*)buf("xchg" + std::to_string(p)).ptr;
     std::vector<u32> o;
@@ -602,6 +631,23 @@ class Engine {
     HIPCHECK(hipStreamSynchronize(s_comp_));
     const Counters* c = (const Counters*)buf("ctr_host0").ptr;
     return c->n_routed_msgs;
+  }
+
+  // exchange_lag mode: the all-to-all of step t finished on `stream` (0 = complete) with
+  // these received counts; the next submit()'s phase B imports it
+  void set_import(std::vector<u32> recv, u64 stream) {
+    if (recv.size() != 2 * d_.world) throw std::runtime_error("set_import: need 2*world counts");
+    lag_recv_ = recv;
+    lag_stream_ = stream;
+  }
+
+  // per-parity exchange operands (exchange_lag: parity p sends from S[p] and imports R[p^1])
+  void set_xfer_parity(int p, u64 send_desc, u64 send_pay, u64 recv_desc, u64 recv_pay) {
+    io_[p].send_desc = (RDesc*)send_desc; io_[p].send_pay = (u8*)send_pay;
+    io_[p].recv_desc = (const RDesc*)recv_desc; io_[p].recv_pay = (const u8*)recv_pay;
+    if (graph_exec_[p]) { HIPCHECK(hipGraphExecDestroy(graph_exec_[p])); graph_exec_[p] = nullptr; }
+    if (graph_b_[p]) { HIPCHECK(hipGraphExecDestroy(graph_b_[p])); graph_b_[p] = nullptr; }
+    xfer_set_ = true;
   }
 
   // caller-owned exchange operands (device pointers, e.g. torch tensors used by RCCL)
@@ -827,6 +873,10 @@ class Engine {
   hipGraphExec_t graph_b_[2] = {nullptr, nullptr};
   hipEvent_t ev_a_[2], ev_ext_[2];
   bool phase_a_[2] = {false, false};
+  bool counts_ready_[2] = {false, false};
+  bool lag_ = false;
+  std::vector<u32> lag_recv_;
+  u64 lag_stream_ = 0;
   bool xfer_set_ = false;
   DS io_[2];
   u8* egress_host_[2] = {nullptr, nullptr};
@@ -882,6 +932,8 @@ PYBIND11_MODULE(_dataplane, m) {
       .def("send_counts", &Engine::send_counts)
       .def("submit_b", &Engine::submit_b, py::arg("parity"), py::arg("recv"), py::arg("stream") = 0)
       .def("set_xfer_buffers", &Engine::set_xfer_buffers)
+      .def("set_xfer_parity", &Engine::set_xfer_parity)
+      .def("set_import", &Engine::set_import, py::arg("recv"), py::arg("stream") = 0)
       .def("restore", &Engine::restore, py::arg("desc"), py::arg("payload"), py::arg("now_ms"))
       .def("wait_results", &Engine::wait_results)
       .def("egress_copy", &Engine::egress_copy)

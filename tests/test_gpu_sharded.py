@@ -12,23 +12,23 @@ import pytest
 
 from gpu_cfg import CFG
 from sharded_scenarios import SHARDED, apply, split_inputs
-from test_sharded_golden import _free_port, run_single
+from test_sharded_golden import _free_port, run_cluster_lag, run_single
 
 pytestmark = pytest.mark.gpu
 HERE = os.path.dirname(os.path.abspath(__file__))
 
 
-def run_gpu_cluster(spec, world, graph=True):
+def run_gpu_cluster(spec, world, graph=True, lag=0, extra_steps=0):
     import torch
 
     from chanamq_amd.engine.dataplane import GpuDataPlane
     from chanamq_amd.parallel.cluster import LocalCluster
     torch.cuda.set_device(0)
-    cl = LocalCluster(lambda **kw: GpuDataPlane(graph=graph, **CFG, **kw), world)
+    cl = LocalCluster(lambda **kw: GpuDataPlane(graph=graph, exchange_lag=lag, **CFG, **kw), world)
     for r in range(world):
         apply(cl[r], spec, rank=r, world=world)
     outs = []
-    for k, st in enumerate(spec.steps):
+    for k, st in enumerate(spec.steps + [{}] * extra_steps):
         res = cl.step(split_inputs(spec, st, world), now_ms=1000 + k)
         merged = {}
         for r in res:
@@ -73,3 +73,15 @@ def test_gpu_two_process_exchange(gpu):
                     for c, hx in eg.items():
                         got[k][int(c)] = bytes.fromhex(hx)
     assert single == got
+
+
+@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("name", sorted(SHARDED))
+def test_gpu_lagged_exchange_matches_golden(gpu, name, world):
+    """exchange_lag=1: the HIP cluster and the golden cluster agree byte for byte."""
+    want = run_cluster_lag(SHARDED[name](), world, extra_steps=2)
+    got = run_gpu_cluster(SHARDED[name](), world, lag=1, extra_steps=2)
+    for k, (a, b) in enumerate(zip(want, got)):
+        assert set(a) == set(b), (k, sorted(a), sorted(b))
+        for c in a:
+            assert a[c] == b[c], (k, c)
