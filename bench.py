@@ -137,6 +137,9 @@ def main():
     ap.add_argument("--workload", choices=["topic", "fanout", "storm"], default="topic",
                     help="topic = BASELINE config 2 (default, the headline); fanout = config 3 "
                          "(--queues is then the node total, default 1024, with small publish batches)")
+    ap.add_argument("--exchange-lag", type=int, choices=[0, 1], default=1,
+                    help="N>1: 1 = pipelined all-to-all (phase B imports the previous step's exchange, "
+                         "the collective overlaps the next step); 0 = synchronous")
     ap.add_argument("--mode", choices=["sharded", "independent"], default="sharded",
                     help="N>1: one sharded broker (cross-GPU routing over RCCL) or N unconnected shards")
     args = ap.parse_args()
@@ -185,7 +188,8 @@ def main():
                copy_engine={"blit": 0, "nocu": 1, "kernel": 2}[args.copy_engine], copy_wgs=args.copy_wgs)
     if shards > 1:
         from chanamq_amd.parallel.exchange import Exchanger
-        dp = GpuDataPlane(device=local, worker=rank, world=world, rank=rank, exchanger=Exchanger(), **cfg)
+        dp = GpuDataPlane(device=local, worker=rank, world=world, rank=rank, exchanger=Exchanger(),
+                          exchange_lag=args.exchange_lag, **cfg)
     else:
         dp = GpuDataPlane(device=local, worker=rank, **cfg)
     pool, segs, offs, blens, mps, msg_bytes, extra = build_workload(dp, rank, P, Q, args.body, args.chunk,
@@ -304,6 +308,7 @@ def main():
                 "global_batch": int(round(mps * world)),
                 "seq_len": args.body,
                 "parallelism": (f"queue-sharded x{world}: one broker, cross-GPU routing by RCCL all-to-all"
+                                + (" (pipelined, +1 step for cross-GPU messages)" if args.exchange_lag else "")
                                 if shards > 1 else
                                 (f"x{world} independent broker shards" if world > 1 else "single GPU")),
                 "producers_per_gpu": P,

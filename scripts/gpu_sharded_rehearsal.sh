@@ -3,7 +3,11 @@
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
 export CHANAMQ_BENCH_BACKEND=gloo
-timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
-    --master-port 29611 bench.py --gpus 2 --steps 20 --warmup 5 --producers 64 > gpurun_out/shard_rehearsal.log 2>&1
-rc=$?; echo "rehearsal exit $rc" >> gpurun_out/shard_rehearsal.log
-exit $rc
+for lag in 1 0; do
+  timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
+      --master-port 2961$lag bench.py --gpus 2 --steps 20 --warmup 5 --producers 64 --exchange-lag $lag \
+      > gpurun_out/shard_rehearsal_lag$lag.log 2>&1
+  rc=$?; echo "rehearsal lag=$lag exit $rc" >> gpurun_out/shard_rehearsal_lag$lag.log
+  [ $rc -eq 0 ] || exit $rc
+  grep '^{"metric"' gpurun_out/shard_rehearsal_lag$lag.log | cut -c1-200
+done
