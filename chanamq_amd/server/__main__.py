@@ -28,6 +28,7 @@ def main(argv=None):
     ap.add_argument("--log-level", default="INFO")
     ap.add_argument("--data-plane", choices=["host", "gpu"], default="host")
     ap.add_argument("--device", type=int, default=0)
+    ap.add_argument("--admin-port", type=int, default=-1, help="GPU mode: admin REST port (0 = any, -1 = off)")
     args = ap.parse_args(argv)
     logging.basicConfig(level=args.log_level, format="%(asctime)s:%(levelname)s %(threadName)s - %(message)s")
     log = logging.getLogger("chanamq")
@@ -64,6 +65,10 @@ def _main_gpu(args, bc, log):
     broker = GpuBroker(plane, host=bc["host"], port=bc["port"], heartbeat=bc["heartbeat"],
                        frame_max=bc["frame_max"], channel_max=bc["channel_max"] or 2047).start()
     log.info("AMQP (GPU data plane, device %d) listening on %s:%s", args.device, bc["host"], broker.port)
+    from ..utils.config import Config  # noqa: F401  (admin port from the same config)
+    admin = AdminServer(broker, int(args.admin_port)).start() if args.admin_port >= 0 else None
+    if admin is not None:
+        log.info("admin REST on 127.0.0.1:%d", admin.port)
     stop = threading.Event()
     for sig in (signal.SIGINT, signal.SIGTERM):
         signal.signal(sig, lambda *a: stop.set())
@@ -73,6 +78,8 @@ def _main_gpu(args, bc, log):
         log.info("server published msgs: %d", s["published"] - last.get("published", 0))
         log.info("server delivered msgs: %d", s["delivered"] - last.get("delivered", 0))
         last = s
+    if admin is not None:
+        admin.stop()
     broker.stop()
     return 0
 

@@ -164,6 +164,35 @@ class GpuBroker:
         os.close(self._wake_r)
         os.close(self._wake_w)
 
+    # ------------------------------------------------------------------ admin (server/admin.py)
+    def create_vhost(self, name):
+        with self.lock:
+            self.plane.ensure_vhost(name)
+            if self.persistence is not None:
+                self.persistence.vhost(name)
+        return True
+
+    def delete_vhost(self, name):
+        # reference parity (A.Q28): no cascade; the vhost stays usable by open connections
+        return True
+
+    def stats_json(self):
+        import json
+        with self.lock:
+            d = dict(self.stats)
+            d.update(connections_open=sum(1 for c in self.conns.values() if c.state == "open"),
+                     queues=len(self.plane.queues), exchanges=len(self.plane.exchanges),
+                     stored_bytes=self.plane.memory_in_use(), blocked=self.blocked)
+        return json.dumps(d)
+
+    def queues_json(self):
+        import json
+        with self.lock:
+            out = [{"vhost": q.vhost, "name": q.name, "durable": q.durable, "owner": q.owner,
+                    "ready": self.plane.message_count(q.slot) if q.owner == self.plane.rank else None,
+                    "consumers": len(q.consumers)} for q in self.plane.queues.values()]
+        return json.dumps(out)
+
     # ------------------------------------------------------------------ native loop
     def _loop_native(self):
         import numpy as np

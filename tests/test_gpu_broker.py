@@ -241,3 +241,27 @@ def test_durable_persistent_messages_survive_restart(kind, tmp_path):
     c2.close()
     b2.stop()
     st2.close()
+
+
+def test_admin_rest_on_gpu_server(broker):
+    import json
+    import urllib.request
+
+    from chanamq_amd.server.admin import AdminServer
+    adm = AdminServer(broker, 0).start()
+    try:
+        base = f"http://127.0.0.1:{adm.port}"
+        assert urllib.request.urlopen(base + "/admin/vhost/put/vx").status == 200
+        assert "vx" in broker.plane.vhosts
+        p = conn(broker)
+        ch = p.channel()
+        ch.queue_declare("adm.q")
+        ch.basic_publish("", "adm.q", b"x")
+        p.process(0.2)
+        qs = json.loads(urllib.request.urlopen(base + "/admin/queues").read())
+        assert any(q["name"] == "adm.q" and q["ready"] == 1 for q in qs)
+        st = json.loads(urllib.request.urlopen(base + "/admin/stats").read())
+        assert st["connections_open"] >= 1
+        p.close()
+    finally:
+        adm.stop()
