@@ -130,7 +130,7 @@ def main():
     ap.add_argument("--chunk", type=int, default=65536, help="bytes per producer per step (TCP read)")
     ap.add_argument("--blocks", type=int, default=8)
     ap.add_argument("--no-graph", action="store_true")
-    ap.add_argument("--copy-engine", choices=["kernel", "nocu", "blit"], default="blit",
+    ap.add_argument("--copy-engine", choices=["kernel", "nocu", "blit", "sdma"], default="blit",
                     help="egress D2H: the runtime blit copy (default, fastest measured), the runtime's NoCU "
                          "copy request, or our copy kernel on --copy-wgs workgroups")
     ap.add_argument("--copy-wgs", type=int, default=16)
@@ -185,7 +185,7 @@ def main():
                egress_cap=(128 << 20) if not fan else (320 << 20),
                log_bytes=16 << 30, ring_pool=Q * qcap + qtot + 1024, tb_max=max(64, qtot) if not fan else 64,
                fan_max=max(1 << 20, qtot * 2), carry_cap=256 << 10, graph=0 if args.no_graph else 1,
-               copy_engine={"blit": 0, "nocu": 1, "kernel": 2}[args.copy_engine], copy_wgs=args.copy_wgs)
+               copy_engine={"blit": 0, "nocu": 1, "kernel": 2, "sdma": 3}[args.copy_engine], copy_wgs=args.copy_wgs)
     if shards > 1:
         from chanamq_amd.parallel.exchange import Exchanger
         dp = GpuDataPlane(device=local, worker=rank, world=world, rank=rank, exchanger=Exchanger(),

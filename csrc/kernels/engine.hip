@@ -12,6 +12,9 @@
 #include <string>
 #include <vector>
 
+#include <hsa/hsa.h>
+#include <hsa/hsa_ext_amd.h>
+
 #include "dataplane.hip"
 
 namespace py = pybind11;
@@ -120,6 +123,7 @@ class Engine {
     // stalling the next step's kernels), 1 = hipMemcpyDeviceToDeviceNoCU request,
     // 2 = our own egress copy kernel on copy_wgs workgroups only (stores straight into
     // mapped pinned memory), leaving the rest of the CUs to the step kernels
+    // 3 = the egress D2H on an SDMA engine through HSA directly (no CUs involved)
     copy_mode_ = (int)get("copy_engine", 0);   // measured: blit 24.0 M msgs/s, kernel(16 WG) 19.1 M
     sdma_ = copy_mode_ == 1;
     copy_wgs_ = (u32)get("copy_wgs", 16);
@@ -346,6 +350,7 @@ class Engine {
       io.persist_h = io_[p].persist_h; io.crec_h = io_[p].crec_h;
       io_[p] = io;
     }
+    if (copy_mode_ == 3) init_sdma();
     HIPCHECK(hipStreamCreateWithFlags(&s_comp_, hipStreamNonBlocking));
     HIPCHECK(hipStreamCreateWithFlags(&s_h2d_, hipStreamNonBlocking));
     HIPCHECK(hipStreamCreateWithFlags(&s_d2h_, hipStreamNonBlocking));
@@ -476,7 +481,7 @@ class Engine {
     o["work_cap"] = d_.work_cap; o["total_bytes"] = total_bytes_; o["req_max"] = d_.req_max;
     o["exchange_lag"] = lag_ ? 1 : 0;
     o["world"] = d_.world; o["rank"] = d_.my_rank; o["import_max"] = d_.import_max; o["pub_cap"] = d_.pub_cap;
-    o["copy_engine"] = copy_mode_ == 2 ? "kernel" : (sdma_ ? "nocu" : "blit");
+    o["copy_engine"] = copy_mode_ == 3 ? "hsa-sdma" : copy_mode_ == 2 ? "kernel" : (sdma_ ? "nocu" : "blit");
     o["copy_wgs"] = copy_wgs_;
     o["persist"] = d_.persist; o["persist_max"] = d_.persist_max; o["persist_bytes"] = d_.persist_bytes;
     o["restore_max"] = restore_max_;
@@ -506,6 +511,7 @@ class Engine {
     int p = (int)(seq_ & 1);
     if (inflight_[p]) throw std::runtime_error("submit: results of the previous step of this parity not collected");
     HIPCHECK(hipEventSynchronize(ev_h2d_[p]));  // staging buffers of step t-2 are free
+    if (copy_mode_ == 3 && sdma_pending_[p]) sdma_wait(p);   // egress[p] of step t-2 drained
     StepIn* in = stage_in_[p];
     *in = StepIn{};
     in->nseg = nseg;
@@ -673,6 +679,15 @@ class Engine {
     const Counters* c = (const Counters*)buf("ctr_host" + std::to_string(p)).ptr;
     u64 n = c->egress_bytes;
     HIPCHECK(hipStreamWaitEvent(s_d2h_, ev_done_[p], 0));
+    if (n && copy_mode_ == 3) {
+      HIPCHECK(hipEventSynchronize(ev_done_[p]));
+      hsa_signal_store_screlease(sdma_sig_[p], 1);
+      hsa_status_t st = hsa_amd_memory_async_copy_on_engine(egress_host_[p], cpu_agent_, io_[p].egress, gpu_agent_, n,
+                                                            0, nullptr, sdma_sig_[p], sdma_engine_, true);
+      if (st != HSA_STATUS_SUCCESS) throw std::runtime_error("hsa_amd_memory_async_copy_on_engine failed");
+      sdma_pending_[p] = true;
+      return n;
+    }
     if (n && copy_mode_ == 2)
       hipLaunchKernelGGL(k_copy_out, dim3(copy_wgs_), dim3(256), 0, s_d2h_, egress_host_dev_[p],
                          (const u8*)io_[p].egress, n);
@@ -684,7 +699,39 @@ class Engine {
     return n;
   }
 
-  void egress_wait(int p) { HIPCHECK(hipEventSynchronize(ev_d2h_[p])); }
+  void egress_wait(int p) {
+    if (copy_mode_ == 3) { if (sdma_pending_[p]) sdma_wait(p); return; }
+    HIPCHECK(hipEventSynchronize(ev_d2h_[p]));
+  }
+
+  void sdma_wait(int p) {
+    hsa_signal_wait_scacquire(sdma_sig_[p], HSA_SIGNAL_CONDITION_EQ, 0, UINT64_MAX, HSA_WAIT_STATE_ACTIVE);
+    sdma_pending_[p] = false;
+  }
+
+  // HSA agents of this device and of the host, an SDMA engine for GPU -> host copies
+  void init_sdma() {
+    if (hsa_init() != HSA_STATUS_SUCCESS) throw std::runtime_error("hsa_init failed");
+    struct Ctx { std::vector<hsa_agent_t> gpus, cpus; } ctx;
+    hsa_iterate_agents([](hsa_agent_t a, void* data) {
+      hsa_device_type_t t;
+      hsa_agent_get_info(a, HSA_AGENT_INFO_DEVICE, &t);
+      auto* c = (Ctx*)data;
+      if (t == HSA_DEVICE_TYPE_GPU) c->gpus.push_back(a);
+      else if (t == HSA_DEVICE_TYPE_CPU) c->cpus.push_back(a);
+      return HSA_STATUS_SUCCESS;
+    }, &ctx);
+    if ((int)ctx.gpus.size() <= device_ || ctx.cpus.empty()) throw std::runtime_error("HSA agents not found");
+    gpu_agent_ = ctx.gpus[device_];
+    cpu_agent_ = ctx.cpus[0];
+    uint32_t mask = 0;
+    if (hsa_amd_memory_copy_engine_status(cpu_agent_, gpu_agent_, &mask) != HSA_STATUS_SUCCESS || !mask)
+      throw std::runtime_error("no SDMA engine available for device -> host copies");
+    sdma_engine_ = (hsa_amd_sdma_engine_id_t)(mask & (~mask + 1));   // lowest available engine
+    for (int p = 0; p < 2; ++p)
+      if (hsa_signal_create(0, 0, nullptr, &sdma_sig_[p]) != HSA_STATUS_SUCCESS)
+        throw std::runtime_error("hsa_signal_create failed");
+  }
 
   void sync() {
     HIPCHECK(hipStreamSynchronize(s_h2d_));
@@ -882,6 +929,10 @@ class Engine {
   u8* egress_host_[2] = {nullptr, nullptr};
   u8* egress_host_dev_[2] = {nullptr, nullptr};
   int copy_mode_ = 0;
+  hsa_agent_t gpu_agent_{}, cpu_agent_{};
+  hsa_amd_sdma_engine_id_t sdma_engine_{};
+  hsa_signal_t sdma_sig_[2] = {{0}, {0}};
+  bool sdma_pending_[2] = {false, false};
   u32 copy_wgs_ = 16;
   StepIn* stage_in_[2] = {nullptr, nullptr};
   SegIn* stage_segs_[2] = {nullptr, nullptr};

@@ -9,7 +9,7 @@ pytestmark = pytest.mark.gpu
 from gpu_cfg import CFG  # noqa: E402
 
 
-@pytest.fixture(params=[True, False], ids=["graph", "eager"])
+@pytest.fixture(params=[(True, 0), (False, 0), (True, 2), (True, 3)], ids=["graph", "eager", "copykernel", "hsa-sdma"])
 def graph(request):
     return request.param
 
@@ -22,7 +22,7 @@ def test_gpu_matches_golden(gpu, name, graph):
     g = GoldenDataPlane(c_max=CFG["c_max"], chpc=CFG["chpc"], q_max=CFG["q_max"], x_max=CFG["x_max"],
                         cons_max=CFG["cons_max"], ucap=CFG["ucap"], carry_cap=CFG["carry_cap"],
                         default_queue_capacity=CFG["default_queue_capacity"])
-    d = GpuDataPlane(graph=graph, **CFG)
+    d = GpuDataPlane(graph=graph[0], copy_engine=graph[1], **CFG)
     steps_g = SCENARIOS[name](g)
     steps_d = SCENARIOS[name](d)
     og = run(g, steps_g, now_step_ms=3000)
