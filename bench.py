@@ -130,10 +130,13 @@ def main():
     ap.add_argument("--chunk", type=int, default=65536, help="bytes per producer per step (TCP read)")
     ap.add_argument("--blocks", type=int, default=8)
     ap.add_argument("--no-graph", action="store_true")
-    ap.add_argument("--copy-engine", choices=["kernel", "nocu", "blit", "sdma"], default="blit",
-                    help="egress D2H: the runtime blit copy (default, fastest measured), the runtime's NoCU "
-                         "copy request, or our copy kernel on --copy-wgs workgroups")
+    ap.add_argument("--copy-engine", choices=["kernel", "nocu", "blit", "sdma"], default="sdma",
+                    help="egress D2H: an SDMA engine other than the ingress H2D's (default: H2D and D2H "
+                         "overlap at ~47 GB/s each, bench/pcie_probe.hip), the runtime blit kernel (holds CUs "
+                         "for the whole transfer), the runtime's NoCU request, or our copy kernel")
     ap.add_argument("--copy-wgs", type=int, default=16)
+    ap.add_argument("--sdma-engine", type=int, default=-1,
+                    help="--copy-engine sdma: SDMA engine for the egress D2H (-1 = highest available)")
     ap.add_argument("--workload", choices=["topic", "fanout", "storm"], default="topic",
                     help="topic = BASELINE config 2 (default, the headline); fanout = config 3 "
                          "(--queues is then the node total, default 1024, with small publish batches)")
@@ -185,7 +188,7 @@ def main():
                egress_cap=(128 << 20) if not fan else (320 << 20),
                log_bytes=16 << 30, ring_pool=Q * qcap + qtot + 1024, tb_max=max(64, qtot) if not fan else 64,
                fan_max=max(1 << 20, qtot * 2), carry_cap=256 << 10, graph=0 if args.no_graph else 1,
-               copy_engine={"blit": 0, "nocu": 1, "kernel": 2, "sdma": 3}[args.copy_engine], copy_wgs=args.copy_wgs)
+               copy_engine={"blit": 0, "nocu": 1, "kernel": 2, "sdma": 3}[args.copy_engine], copy_wgs=args.copy_wgs, sdma_engine=args.sdma_engine)
     if shards > 1:
         from chanamq_amd.parallel.exchange import Exchanger
         dp = GpuDataPlane(device=local, worker=rank, world=world, rank=rank, exchanger=Exchanger(),
@@ -253,6 +256,7 @@ def main():
     dp.eng.sync()
     if shards > 1:
         dp.exchanger.bytes_sent = 0
+    dp.eng.host_times(True)
     t0 = time.perf_counter()
     dl, pb, hist, eg = run(args.steps)
     dp.eng.sync()
@@ -320,6 +324,7 @@ def main():
             "egress_GBps": eg / t / 1e9,
             "latency_note": "in-broker publish->deliver (ingress submit to egress bytes ready), no TCP",
             "diag": errs,
+            "host_us_per_step": {k: round(v * 1e6 / args.steps, 1) for k, v in dp.eng.host_times(False).items()},
             "storm": ({"requeued_msgs": flow["requeued"], "flow_paused_steps": flow["paused_steps"]}
                       if storm else None),
             "cross_gpu_bytes_per_s": (dp.exchanger.bytes_sent * world / t) if shards > 1 else 0.0,

@@ -54,8 +54,9 @@ class GpuDataPlane(ControlState):
         self._io = [dict(seg_out=self.eng.host_view(f"seg_out{p}").view(SEG_OUT),
                          ctrl_rec=self.eng.host_view(f"ctrl_rec{p}").view(CTRL_REC),
                          conn_out=self.eng.host_view(f"conn_out{p}").view(CONN_OUT),
-                         ctrl=self.eng.host_view(f"ctrl{p}"),
-                         egress=self.eng.host_view(f"egress_host{p}")) for p in (0, 1)]
+                         ctrl=self.eng.host_view(f"ctrl{p}")) for p in (0, 1)]
+        # rendered egress: the engine rotates i["egress_slots"] buffers over the steps
+        self._egress = [self.eng.host_view(f"egress_host{e}") for e in range(i["egress_slots"])]
         self._pin = [None, None]
         self.exchanger = exchanger
         self._pending = None
@@ -525,7 +526,7 @@ class GpuDataPlane(ControlState):
             self.eng.egress_wait(p)
         if collect and collect_egress:
             co = io["conn_out"]
-            eg = io["egress"]
+            eg = self._egress[self.eng.egress_slot(p)]
             for conn in np.nonzero(co["len"])[0]:
                 o, n = int(co["off"][conn]), int(co["len"][conn])
                 res.egress[int(conn)] = bytes(eg[o:o + n])
@@ -535,7 +536,7 @@ class GpuDataPlane(ControlState):
     def host_egress(self, ticket):
         """(egress bytes view, ConnOut view) of a finished step, for zero-copy socket writes."""
         io = self._io[ticket[0]]
-        return io["egress"], io["conn_out"]
+        return self._egress[self.eng.egress_slot(ticket[0])], io["conn_out"]
 
     def egress_wait(self, ticket):
         self.eng.egress_wait(ticket[0])

@@ -2057,7 +2057,7 @@ __global__ __launch_bounds__(256) void k_render_deliv(DS d, u32 src) {
   u64 off = (u64)d.conn_base[conn] + d.conn_ret_bytes[conn] + d.conn_conf_bytes[conn] + d.dv_off[i] -
             d.dv_off[f];
   if (off + dv.size > d.egress_cap) return;  // never: dequeue reserves an egress byte budget
-  u8* o = d.egress + off;
+  u8* o = (u8*)d.in->egress + off;
   const u8* slot = d.log + (m.log_off % d.log_bytes);
   u32 chno = d.ch_num[ch];
   u32 taglen = d.cons_tag_len[dv.cons];
@@ -2105,7 +2105,7 @@ __global__ void k_render_confirms(DS d) {
   u32 c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= d.c_max) return;
   u32 conf = d.conn_conf_bytes[c];
-  u8* o = d.egress + (u64)d.conn_base[c] + d.conn_ret_bytes[c];
+  u8* o = (u8*)d.in->egress + (u64)d.conn_base[c] + d.conn_ret_bytes[c];
   u32 p = 0;
   for (u32 l = 0; l < d.chpc; ++l) {
     u32 ch = c * d.chpc + l;
@@ -2137,7 +2137,7 @@ __global__ __launch_bounds__(256) void k_render_returns(DS d) {
   u32 p = d.ret_list[i];
   const Pub pb = d.pubs[p];
   u32 code = d.pub_ret[p];
-  u8* o = d.egress + (u64)d.conn_base[pb.conn] + (d.pub_ret_off[p] - d.conn_ret_min[pb.conn]);
+  u8* o = (u8*)d.in->egress + (u64)d.conn_base[pb.conn] + (d.pub_ret_off[p] - d.conn_ret_min[pb.conn]);
   const u8* w = d.work;
   // channel number from the publish command's frame
   u32 chno = d.ch_num[pb.chslot];
@@ -2322,6 +2322,144 @@ __global__ __launch_bounds__(256) void k_host_out(DS d) {
     if (nr > d.persist_max) nr = d.persist_max;
     copy16((u8*)d.crec_h, (const u8*)d.crec, (u64)nr * sizeof(ConsumedRec), gtid, gsz);
   }
+}
+
+// ============================================================================ Basic.Get
+// Basic.Get (60/70) between steps, while the connection is paused behind the command
+// (FrameStage.scala:1199-1229: Pull(1) -> GetOk / GetEmpty; QueueEntity.scala:318-393).
+// One wave: TTL skip of up to 64 head entries (K12), then the head message gets the
+// channel's next delivery tag.  Manual ack: a pending window slot that Basic.Ack/Nack/
+// Reject/Recover/channel close resolve exactly like a consumer delivery (k_chan_advance);
+// no-ack: a done slot, the message is released now.  GetOk + content header + body frames
+// (split at the connection's frame-max) are rendered into `out` (host-mapped).
+// Consumer bookkeeping uses the spare consumer slot cons_max.
+__global__ __launch_bounds__(64) void k_basic_get(DS d, u32 q, u32 ch, u32 noack, i64 now, u8* out, u64 out_cap,
+                                                  GetRes* res) {
+  u32 lane = lane_id();
+  u64 head = d.q_head[q], tail = d.q_tail[q];
+  const u64 mask = d.q_ring_mask[q];
+  const Desc* ring = d.ring + d.q_ring_off[q];
+  u32 nexp = 0;
+  bool more_expired = false;
+  if (head < tail) {
+    u64 idx = head + lane;
+    bool valid = idx < tail;
+    Desc ds;
+    ds.msg = INVALID; ds.expire_ms = 0; ds.flags = 0;
+    if (valid) ds = ring[idx & mask];
+    bool exp = valid && ds.expire_ms != 0 && ds.expire_ms <= now;
+    u64 live = __ballot(valid && !exp);
+    nexp = live ? (__ffsll((unsigned long long)live) - 1) : __popcll(__ballot(valid));
+    more_expired = !live && head + nexp < tail;
+    bool mine = lane < nexp;
+    bool rec = mine && d.q_durable[q] && (d.msgs[ds.msg].flags & MF_PERSIST);
+    u64 rm = __ballot(rec);
+    if (rec) {
+      ConsumedRec r;
+      r.msg_id = (i64)d.msgs[ds.msg].msg_id;
+      r.qpos = idx;
+      r.q = q;
+      r.kind = 1;
+      r.pad[0] = r.pad[1] = 0;
+      res->exp[__popcll(rm & lanemask_lt())] = r;
+    }
+    wave_release(d, ds.msg, mine);
+    if (lane == 0) res->n_exp = __popcll(rm);
+    head += nexp;
+  } else if (lane == 0) {
+    res->n_exp = 0;
+  }
+  if (head >= tail || more_expired) {
+    if (lane == 0) {
+      d.q_head[q] = head;
+      res->status = more_expired ? GET_RETRY : GET_EMPTY;
+      res->msg_count = (u32)(tail - head);
+      res->out_len = 0;
+    }
+    return;
+  }
+  const Desc ds = ring[head & mask];
+  const MsgEnt m = d.msgs[ds.msg];
+  const u32 conn = ch / d.chpc;
+  const u32 ucap = d.ucap_mask + 1;
+  const u32 msg_count = (u32)(tail - head - 1);
+  u32 mp = 4 + 8 + 1 + 1 + m.ex_len + 1 + m.rk_len + 4;
+  u32 fm = d.conn_frame_max[conn];
+  u32 fmb = fm ? fm - 8 : 0xffffffffu;
+  u32 nb = m.body_len ? (m.body_len + fmb - 1) / fmb : 0;
+  u64 need = 8ull + mp + 8 + 12 + m.props_len + m.body_len + 8ull * nb;
+  u32 st = need > out_cap ? GET_NO_SPACE : (d.ch_win[ch] >= ucap ? GET_WINDOW_FULL : GET_OK);
+  if (st != GET_OK) {
+    if (lane == 0) {
+      d.q_head[q] = head;
+      res->status = st;
+      res->msg_count = (u32)(tail - head);
+      res->out_len = 0;
+    }
+    return;
+  }
+  const u64 tag = d.ch_next_tag[ch];
+  const bool redelivered = ds.flags & 1;
+  if (lane == 0) {
+    d.ch_next_tag[ch] = tag + 1;
+    d.ch_win[ch] += 1;
+    USlot u;
+    u.state = noack ? US_DONE : US_PENDING;
+    u.msg = ds.msg;
+    u.q = q;
+    u.cons = d.cons_max;
+    u.qpos = head;
+    u.expire_ms = ds.expire_ms;
+    d.uwin[(u64)ch * ucap + ((tag - 1) & d.ucap_mask)] = u;
+    if (!noack) { d.ch_unacked[ch] += 1; d.cons_unacked[d.cons_max] += 1; }
+    if (d.ch_dirty[ch] == 0) {   // k_chan_advance walks the window at the next step
+      d.ch_dirty[ch] = 1;
+      u32 k = *d.n_dirty;
+      d.dirty_list[k] = ch;
+      *d.n_dirty = k + 1;
+    }
+    d.q_head[q] = head + 1;
+    res->status = GET_OK;
+    res->msg_count = msg_count;
+    res->out_len = (u32)need;
+    res->tag = tag;
+    res->msg_id = (i64)m.msg_id;
+    res->qpos = head;
+    res->persist = d.q_durable[q] && (m.flags & MF_PERSIST) ? 1u : 0u;
+  }
+  // render: GetOk(tag, redelivered, exchange, routing-key, message-count) + header + body
+  const u8* slot = d.log + (m.log_off % d.log_bytes);
+  const u32 chno = d.ch_num[ch];
+  if (lane == 0) {
+    u32 p = 0;
+    p += put_frame_hdr(out + p, 1, chno, mp);
+    wr16(out + p, 60); wr16(out + p + 2, 71); p += 4;
+    wr64(out + p, tag); p += 8;
+    out[p++] = redelivered ? 1 : 0;
+    out[p++] = m.ex_len;
+    for (u32 k = 0; k < m.ex_len; ++k) out[p + k] = slot[k];
+    p += m.ex_len;
+    out[p++] = m.rk_len;
+    for (u32 k = 0; k < m.rk_len; ++k) out[p + k] = slot[m.ex_len + k];
+    p += m.rk_len;
+    wr32(out + p, msg_count); p += 4;
+    out[p++] = 0xCE;
+    p += put_frame_hdr(out + p, 2, chno, 12 + m.props_len);
+    wr16(out + p, 60); wr16(out + p + 2, 0); wr64(out + p + 4, m.body_len);
+  }
+  u32 hp = 8 + mp + 7 + 12;
+  wave_copy(out + hp, slot + m.ex_len + m.rk_len, m.props_len);
+  if (lane == 0) out[hp + m.props_len] = 0xCE;
+  u32 bp = hp + m.props_len + 1;
+  const u8* body = slot + m.body_off;
+  for (u32 b0 = 0; b0 < m.body_len; b0 += fmb) {
+    u32 bl = m.body_len - b0 < fmb ? m.body_len - b0 : fmb;
+    if (lane == 0) put_frame_hdr(out + bp, 3, chno, bl);
+    wave_copy(out + bp + 7, body + b0, bl);
+    if (lane == 0) out[bp + 7 + bl] = 0xCE;
+    bp += bl + 8;
+  }
+  wave_release(d, ds.msg, noack && lane == 0);
 }
 
 // ============================================================================ requeue (pre-step)

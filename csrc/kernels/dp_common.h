@@ -64,7 +64,8 @@ struct StepIn {         // host -> device per step (64 B)
   u64 id_ms;            // epoch ms for snowflake ids
   u32 worker;           // snowflake worker id (rank)
   u32 pad0;
-  u64 pad[3];
+  u64 egress;           // device pointer: this step's egress slot (engine rotates slots)
+  u64 pad[2];
 };
 
 struct SegOut {         // device -> host per segment
@@ -221,6 +222,23 @@ struct Counters {       // per-step counters (device -> host)
 };
 
 struct CtrlRec { u32 conn; u32 off; u32 len; u32 seg; };
+
+// Basic.Get result (k_basic_get -> host-mapped); exp[] = persistent messages of durable
+// queues dropped by the TTL skip (their store rows go, like ConsumedRec kind 1)
+#define GET_EXP_MAX 64
+enum : u32 { GET_EMPTY = 0, GET_OK = 1, GET_RETRY = 2, GET_NO_SPACE = 3, GET_WINDOW_FULL = 4 };
+struct GetRes {
+  u32 status;
+  u32 msg_count;        // ready messages left in the queue
+  u32 out_len;          // rendered GetOk + header + body bytes
+  u32 n_exp;
+  u64 tag;
+  i64 msg_id;
+  u64 qpos;
+  u32 persist;          // durable queue x persistent message
+  u32 pad;
+  ConsumedRec exp[GET_EXP_MAX];
+};
 
 struct ConnOut { u32 off; u32 len; };
 

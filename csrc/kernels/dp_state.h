@@ -10,6 +10,7 @@
 #define TOPIC_WORDS 8
 #define LAT_BINS 32
 #define WORLD_MAX 16          // ranks of one sharded broker (one node: 8 GPUs)
+#define EGRESS_SLOTS 3        // rotating egress buffers (render of step t || D2H of t-1, t-2)
 
 // tot[] scratch slots (scan totals and phase bookkeeping)
 enum : u32 {
@@ -35,7 +36,6 @@ struct DS {
   SegOut* seg_out;          // device; published to seg_out_h at the end of the step
   Counters* ctr;            // device
   Counters* ctr_host;       // host-mapped
-  u8* egress;               // device (D2H DMA by the host)
   ConnOut* conn_out;        // device [c_max]
   u8* ctrl;                 // device
   CtrlRec* ctrl_rec;        // device [seg_max * 2]

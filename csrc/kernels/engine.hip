@@ -7,6 +7,7 @@
 #include <pybind11/numpy.h>
 #include <pybind11/stl.h>
 
+#include <chrono>
 #include <map>
 #include <stdexcept>
 #include <string>
@@ -29,6 +30,14 @@ namespace py = pybind11;
 static u32 ceil_div(u64 a, u64 b) { return (u32)((a + b - 1) / b); }
 static u32 next_pow2(u32 x) { u32 p = 1; while (p < x) p <<= 1; return p; }
 static u32 bits_for(u64 maxval) { u32 b = 0; while ((1ull << b) <= maxval) ++b; return b; }
+
+// host-side time accounting of the step loop (seconds, per named phase)
+struct HostTimer {
+  double* acc;
+  std::chrono::steady_clock::time_point t0;
+  explicit HostTimer(double* a) : acc(a), t0(std::chrono::steady_clock::now()) {}
+  ~HostTimer() { *acc += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count(); }
+};
 
 struct Buf {
   void* ptr = nullptr;
@@ -127,6 +136,7 @@ class Engine {
     copy_mode_ = (int)get("copy_engine", 0);   // measured: blit 24.0 M msgs/s, kernel(16 WG) 19.1 M
     sdma_ = copy_mode_ == 1;
     copy_wgs_ = (u32)get("copy_wgs", 16);
+    sdma_pref_ = cfg.contains("sdma_engine") ? cfg["sdma_engine"].cast<int>() : -1;
 
     // ---- allocations
     auto dev = [&](const char* name, size_t bytes) { return alloc(name, bytes, false); };
@@ -144,7 +154,6 @@ class Engine {
       io.seg_out = (SegOut*)dev(("seg_out_d" + sfx).c_str(), sizeof(SegOut) * d_.seg_max);
       io.seg_out_h = (SegOut*)hst(("seg_out" + sfx).c_str(), sizeof(SegOut) * d_.seg_max);
       io.ctr_host = (Counters*)hst(("ctr_host" + sfx).c_str(), sizeof(Counters));
-      io.egress = (u8*)dev(("egress" + sfx).c_str(), egress_alloc_);
       io.conn_out = (ConnOut*)dev(("conn_out_d" + sfx).c_str(), sizeof(ConnOut) * d_.c_max);
       io.conn_out_h = (ConnOut*)hst(("conn_out" + sfx).c_str(), sizeof(ConnOut) * d_.c_max);
       io.ctrl = (u8*)dev(("ctrl_d" + sfx).c_str(), d_.ctrl_cap);
@@ -156,16 +165,23 @@ class Engine {
         io.persist_h = (u8*)hst(("persist" + sfx).c_str(), d_.persist_bytes + 64);
         io.crec_h = (ConsumedRec*)hst(("consumed" + sfx).c_str(), sizeof(ConsumedRec) * (u64)d_.persist_max + 64);
       }
-      if (copy_mode_ == 2) {
-        egress_host_dev_[p] = (u8*)hst(("egress_host" + sfx).c_str(), egress_alloc_);
-        egress_host_[p] = (u8*)buf("egress_host" + sfx).ptr;
-      } else {
-        egress_host_[p] = (u8*)pinned(("egress_host" + sfx).c_str(), egress_alloc_);
-      }
       stage_in_[p] = (StepIn*)pinned(("stage_in" + sfx).c_str(), sizeof(StepIn));
       stage_segs_[p] = (SegIn*)pinned(("stage_segs" + sfx).c_str(), sizeof(SegIn) * d_.seg_max);
     }
 
+    // egress slots rotate per step independently of the IO parity: step t renders into
+    // slot t % EGRESS_SLOTS, so its kernels only wait for the D2H of step t-3 (long done)
+    // instead of step t-2's, which is still on the copy engine
+    for (int e = 0; e < EGRESS_SLOTS; ++e) {
+      std::string sfx = std::to_string(e);
+      egress_dev_[e] = (u8*)dev(("egress" + sfx).c_str(), egress_alloc_);
+      if (copy_mode_ == 2) {
+        egress_host_dev_[e] = (u8*)hst(("egress_host" + sfx).c_str(), egress_alloc_);
+        egress_host_[e] = (u8*)buf("egress_host" + sfx).ptr;
+      } else {
+        egress_host_[e] = (u8*)pinned(("egress_host" + sfx).c_str(), egress_alloc_);
+      }
+    }
     d_.carry = (u8*)dev("carry", (u64)d_.c_max * d_.carry_cap + 64);
     d_.carry_len = (u32*)dev("carry_len", 4ull * d_.c_max);
     d_.conn_paused = (u32*)dev("conn_paused", 4ull * d_.c_max);
@@ -294,7 +310,7 @@ class Engine {
     d_.cons_ch = (u32*)dev("cons_ch", 4ull * d_.cons_max);
     d_.cons_noack = (u32*)dev("cons_noack", 4ull * d_.cons_max);
     d_.cons_active = (u32*)dev("cons_active", 4ull * d_.cons_max);
-    d_.cons_unacked = (u32*)dev("cons_unacked", 4ull * d_.cons_max);
+    d_.cons_unacked = (u32*)dev("cons_unacked", 4ull * (d_.cons_max + 1));   // [cons_max]: Basic.Get
     d_.cons_tag_off = (u32*)dev("cons_tag_off", 4ull * d_.cons_max);
     d_.cons_tag_len = (u32*)dev("cons_tag_len", 4ull * d_.cons_max);
     d_.tpool = (u8*)dev("tpool", 256ull * d_.cons_max);
@@ -338,12 +354,17 @@ class Engine {
     }
     d_.tot = (u32*)dev("tot", 4ull * 128);
     d_.egress_budget = (u32*)dev("egress_budget", 4);
+    // Basic.Get: rendered frames + result, host-mapped (a stored body never exceeds the
+    // carry, which bounds an assembled command)
+    get_cap_ = (u64)d_.carry_cap + d_.carry_cap / 64 + 4096;
+    get_out_dev_ = (u8*)hst("get_out", get_cap_);
+    get_res_dev_ = (GetRes*)hst("get_res", sizeof(GetRes));
     d_.dbg = (u64*)dev("dbg", 8ull * 16 * d_.seg_max);
 
     for (int p = 0; p < 2; ++p) {
       DS io = d_;
       io.in = io_[p].in; io.segs = io_[p].segs; io.ingress = io_[p].ingress; io.seg_out = io_[p].seg_out;
-      io.ctr_host = io_[p].ctr_host; io.egress = io_[p].egress; io.conn_out = io_[p].conn_out;
+      io.ctr_host = io_[p].ctr_host; io.conn_out = io_[p].conn_out;
       io.ctrl = io_[p].ctrl; io.ctrl_rec = io_[p].ctrl_rec; io.xchg = io_[p].xchg;
       io.seg_out_h = io_[p].seg_out_h; io.conn_out_h = io_[p].conn_out_h; io.ctrl_h = io_[p].ctrl_h;
       io.ctrl_rec_h = io_[p].ctrl_rec_h;
@@ -357,10 +378,10 @@ class Engine {
     for (int p = 0; p < 2; ++p) {
       HIPCHECK(hipEventCreateWithFlags(&ev_h2d_[p], hipEventDisableTiming));
       HIPCHECK(hipEventCreateWithFlags(&ev_done_[p], hipEventDisableTiming));
-      HIPCHECK(hipEventCreateWithFlags(&ev_d2h_[p], hipEventDisableTiming));
       HIPCHECK(hipEventCreateWithFlags(&ev_a_[p], hipEventDisableTiming));
       HIPCHECK(hipEventCreateWithFlags(&ev_ext_[p], hipEventDisableTiming));
     }
+    for (int e = 0; e < EGRESS_SLOTS; ++e) HIPCHECK(hipEventCreateWithFlags(&ev_d2h_[e], hipEventDisableTiming));
     // ---- initial state
     fill("conn_dfirst", 0xff);
     fill("conn_ret_min", 0xff);
@@ -385,8 +406,8 @@ class Engine {
       (void)hipEventDestroy(ev_ext_[p]);
       (void)hipEventDestroy(ev_h2d_[p]);
       (void)hipEventDestroy(ev_done_[p]);
-      (void)hipEventDestroy(ev_d2h_[p]);
     }
+    for (int e = 0; e < EGRESS_SLOTS; ++e) (void)hipEventDestroy(ev_d2h_[e]);
     (void)hipStreamDestroy(s_comp_);
     (void)hipStreamDestroy(s_h2d_);
     (void)hipStreamDestroy(s_d2h_);
@@ -483,6 +504,8 @@ class Engine {
     o["world"] = d_.world; o["rank"] = d_.my_rank; o["import_max"] = d_.import_max; o["pub_cap"] = d_.pub_cap;
     o["copy_engine"] = copy_mode_ == 3 ? "hsa-sdma" : copy_mode_ == 2 ? "kernel" : (sdma_ ? "nocu" : "blit");
     o["copy_wgs"] = copy_wgs_;
+    o["egress_slots"] = EGRESS_SLOTS;
+    { u32 e = 0; while (copy_mode_ == 3 && e < 32 && !(((u32)sdma_engine_ >> e) & 1u)) ++e; o["sdma_engine"] = copy_mode_ == 3 ? (int)e : -1; }
     o["persist"] = d_.persist; o["persist_max"] = d_.persist_max; o["persist_bytes"] = d_.persist_bytes;
     o["restore_max"] = restore_max_;
     o["xfer_desc_max"] = d_.xfer_desc_max; o["xfer_bytes"] = d_.xfer_bytes; o["world_max"] = WORLD_MAX;
@@ -503,6 +526,7 @@ class Engine {
   // egress_wait(p) -> egress_host(p) is valid.
   int submit(py::buffer segs, u64 payload_ptr, u64 payload_len, i64 now_ms, u64 step, u64 id_ms,
              u32 worker) {
+    HostTimer ht(&ht_[0]);
     py::buffer_info si = segs.request();
     size_t sb = (size_t)si.size * si.itemsize;
     u32 nseg = (u32)(sb / sizeof(SegIn));
@@ -511,7 +535,6 @@ class Engine {
     int p = (int)(seq_ & 1);
     if (inflight_[p]) throw std::runtime_error("submit: results of the previous step of this parity not collected");
     HIPCHECK(hipEventSynchronize(ev_h2d_[p]));  // staging buffers of step t-2 are free
-    if (copy_mode_ == 3 && sdma_pending_[p]) sdma_wait(p);   // egress[p] of step t-2 drained
     StepIn* in = stage_in_[p];
     *in = StepIn{};
     in->nseg = nseg;
@@ -519,6 +542,9 @@ class Engine {
     in->step = step;
     in->id_ms = id_ms;
     in->worker = worker;
+    const int e = (int)(seq_ % EGRESS_SLOTS);
+    in->egress = (u64)egress_dev_[e];
+    slot_of_[p] = e;
     memcpy(stage_segs_[p], si.ptr, sb);
     HIPCHECK(hipMemcpyAsync((void*)io_[p].in, in, sizeof(StepIn), hipMemcpyHostToDevice, s_h2d_));
     if (sb) HIPCHECK(hipMemcpyAsync((void*)io_[p].segs, stage_segs_[p], sb, hipMemcpyHostToDevice, s_h2d_));
@@ -526,11 +552,16 @@ class Engine {
       HIPCHECK(hipMemcpyAsync((void*)io_[p].ingress, (const void*)payload_ptr, payload_len,
                               sdma_ ? hipMemcpyDeviceToDeviceNoCU : hipMemcpyHostToDevice, s_h2d_));
     HIPCHECK(hipEventRecord(ev_h2d_[p], s_h2d_));
+    // egress slot e (last used by step t-EGRESS_SLOTS) drained before this step's kernels
+    // overwrite it; waited for only after this step's ingress H2D is queued, so the H2D
+    // and the in-flight D2H overlap on their two SDMA engines
+    if (copy_mode_ == 3 && sdma_pending_[e]) { HostTimer t(&ht_[1]); sdma_wait(e); }
     HIPCHECK(hipStreamWaitEvent(s_comp_, ev_h2d_[p], 0));
-    if (d2h_issued_[p]) HIPCHECK(hipStreamWaitEvent(s_comp_, ev_d2h_[p], 0));  // egress[p] drained
+    if (d2h_issued_[e]) HIPCHECK(hipStreamWaitEvent(s_comp_, ev_d2h_[e], 0));
     if (d_.world > 1 && !xfer_set_) throw std::runtime_error("set_xfer_buffers() before the first sharded step");
     if (graph_enabled_) {
       if (!graph_exec_[p]) capture_main(p);
+      HostTimer t(&ht_[2]);
       HIPCHECK(hipGraphLaunch(graph_exec_[p], s_comp_));
     } else {
       launch_main(s_comp_, io_[p]);
@@ -617,6 +648,7 @@ class Engine {
       throw std::runtime_error("restore batch exceeds the import buffers (restore_max / restore_bytes)");
     if (inflight_[0] || inflight_[1]) throw std::runtime_error("restore() between steps only");
     sync();
+    drain_egress();
     if (db) HIPCHECK(hipMemcpy((void*)d_.recv_desc, di.ptr, db, hipMemcpyHostToDevice));
     if (pb) HIPCHECK(hipMemcpy((void*)d_.recv_pay, pi.ptr, pb, hipMemcpyHostToDevice));
     DS& io = io_[0];
@@ -626,6 +658,7 @@ class Engine {
     in.step = seq_;
     in.id_ms = now_ms;
     in.worker = 0;
+    in.egress = (u64)egress_dev_[0];
     HIPCHECK(hipMemcpy((void*)io.in, &in, sizeof(StepIn), hipMemcpyHostToDevice));
     u32* x = (u32*)buf("xchg0").ptr;
     for (u32 r = 0; r < 2 * WORLD_MAX; ++r) x[2 * WORLD_MAX + r] = 0;
@@ -637,6 +670,24 @@ class Engine {
     HIPCHECK(hipStreamSynchronize(s_comp_));
     const Counters* c = (const Counters*)buf("ctr_host0").ptr;
     return c->n_routed_msgs;
+  }
+
+  // Basic.Get between steps: (status, message_count, frames, tag, msg_id, qpos, persist,
+  // expired [(msg_id, q, qpos)] of durable x persistent messages dropped by the TTL skip)
+  py::tuple basic_get(u32 q, u32 chslot, u32 noack, i64 now_ms) {
+    if (inflight_[0] || inflight_[1]) throw std::runtime_error("basic_get() between steps only");
+    if (q >= d_.q_max || chslot >= d_.c_max * d_.chpc) throw std::runtime_error("basic_get: bad queue / channel");
+    sync();
+    hipLaunchKernelGGL(k_basic_get, dim3(1), dim3(64), 0, s_comp_, io_[0], q, chslot, noack, now_ms, get_out_dev_,
+                       get_cap_, get_res_dev_);
+    HIPCHECK(hipGetLastError());
+    HIPCHECK(hipStreamSynchronize(s_comp_));
+    const GetRes& r = *(const GetRes*)buf("get_res").ptr;
+    py::list exp;
+    for (u32 i = 0; i < r.n_exp && i < GET_EXP_MAX; ++i)
+      exp.append(py::make_tuple(r.exp[i].msg_id, r.exp[i].q, r.exp[i].qpos));
+    py::bytes frames(r.status == GET_OK ? (const char*)buf("get_out").ptr : "", r.status == GET_OK ? r.out_len : 0);
+    return py::make_tuple(r.status, r.msg_count, frames, r.tag, r.msg_id, r.qpos, r.persist, exp);
   }
 
   // exchange_lag mode: the all-to-all of step t finished on `stream` (0 = complete) with
@@ -670,44 +721,52 @@ class Engine {
   }
 
   void wait_results(int p) {
+    HostTimer ht(&ht_[3]);
     if (phase_a_[p]) throw std::runtime_error("wait_results: phase B of this sharded step not submitted");
     HIPCHECK(hipEventSynchronize(ev_done_[p]));
     inflight_[p] = false;
   }
 
   u64 egress_copy(int p) {
+    HostTimer ht(&ht_[4]);
     const Counters* c = (const Counters*)buf("ctr_host" + std::to_string(p)).ptr;
     u64 n = c->egress_bytes;
+    const int e = slot_of_[p];
     HIPCHECK(hipStreamWaitEvent(s_d2h_, ev_done_[p], 0));
     if (n && copy_mode_ == 3) {
       HIPCHECK(hipEventSynchronize(ev_done_[p]));
-      hsa_signal_store_screlease(sdma_sig_[p], 1);
-      hsa_status_t st = hsa_amd_memory_async_copy_on_engine(egress_host_[p], cpu_agent_, io_[p].egress, gpu_agent_, n,
-                                                            0, nullptr, sdma_sig_[p], sdma_engine_, true);
+      hsa_signal_store_screlease(sdma_sig_[e], 1);
+      hsa_status_t st = hsa_amd_memory_async_copy_on_engine(egress_host_[e], cpu_agent_, egress_dev_[e], gpu_agent_, n,
+                                                            0, nullptr, sdma_sig_[e], sdma_engine_, true);
       if (st != HSA_STATUS_SUCCESS) throw std::runtime_error("hsa_amd_memory_async_copy_on_engine failed");
-      sdma_pending_[p] = true;
+      sdma_pending_[e] = true;
       return n;
     }
     if (n && copy_mode_ == 2)
-      hipLaunchKernelGGL(k_copy_out, dim3(copy_wgs_), dim3(256), 0, s_d2h_, egress_host_dev_[p],
-                         (const u8*)io_[p].egress, n);
+      hipLaunchKernelGGL(k_copy_out, dim3(copy_wgs_), dim3(256), 0, s_d2h_, egress_host_dev_[e],
+                         (const u8*)egress_dev_[e], n);
     else if (n)
-      HIPCHECK(hipMemcpyAsync(egress_host_[p], io_[p].egress, n,
+      HIPCHECK(hipMemcpyAsync(egress_host_[e], egress_dev_[e], n,
                               sdma_ ? hipMemcpyDeviceToDeviceNoCU : hipMemcpyDeviceToHost, s_d2h_));
-    HIPCHECK(hipEventRecord(ev_d2h_[p], s_d2h_));
-    d2h_issued_[p] = true;
+    HIPCHECK(hipEventRecord(ev_d2h_[e], s_d2h_));
+    d2h_issued_[e] = true;
     return n;
   }
 
   void egress_wait(int p) {
-    if (copy_mode_ == 3) { if (sdma_pending_[p]) sdma_wait(p); return; }
-    HIPCHECK(hipEventSynchronize(ev_d2h_[p]));
+    HostTimer ht(&ht_[5]);
+    const int e = slot_of_[p];
+    if (copy_mode_ == 3) { if (sdma_pending_[e]) sdma_wait(e); return; }
+    HIPCHECK(hipEventSynchronize(ev_d2h_[e]));
   }
 
-  void sdma_wait(int p) {
-    hsa_signal_wait_scacquire(sdma_sig_[p], HSA_SIGNAL_CONDITION_EQ, 0, UINT64_MAX, HSA_WAIT_STATE_ACTIVE);
-    sdma_pending_[p] = false;
+  void sdma_wait(int e) {
+    hsa_signal_wait_scacquire(sdma_sig_[e], HSA_SIGNAL_CONDITION_EQ, 0, UINT64_MAX, HSA_WAIT_STATE_ACTIVE);
+    sdma_pending_[e] = false;
   }
+
+  // egress slot (host view "egress_host<slot>") of the step last submitted with parity p
+  int egress_slot(int p) const { return slot_of_[p]; }
 
   // HSA agents of this device and of the host, an SDMA engine for GPU -> host copies
   void init_sdma() {
@@ -727,16 +786,39 @@ class Engine {
     uint32_t mask = 0;
     if (hsa_amd_memory_copy_engine_status(cpu_agent_, gpu_agent_, &mask) != HSA_STATUS_SUCCESS || !mask)
       throw std::runtime_error("no SDMA engine available for device -> host copies");
-    sdma_engine_ = (hsa_amd_sdma_engine_id_t)(mask & (~mask + 1));   // lowest available engine
-    for (int p = 0; p < 2; ++p)
-      if (hsa_signal_create(0, 0, nullptr, &sdma_sig_[p]) != HSA_STATUS_SUCCESS)
+    // not the engine of the runtime's own H2D copies: one SDMA engine serialises both
+    // directions (measured 54 GB/s total vs 94 GB/s on two engines, bench/pcie_probe.hip)
+    // (measured on MI355X: engines 0-3 reach PCIe rate, 8 and 15 a third of it)
+    u32 pick = 0;
+    if (sdma_pref_ >= 0 && (mask >> sdma_pref_) & 1u) pick = (u32)sdma_pref_;
+    else if ((mask >> 1) & 1u) pick = 1;
+    else while (!((mask >> pick) & 1u)) ++pick;
+    sdma_engine_ = (hsa_amd_sdma_engine_id_t)(1u << pick);
+    for (int e = 0; e < EGRESS_SLOTS; ++e)
+      if (hsa_signal_create(0, 0, nullptr, &sdma_sig_[e]) != HSA_STATUS_SUCCESS)
         throw std::runtime_error("hsa_signal_create failed");
+  }
+
+  void drain_egress() {
+    for (int e = 0; e < EGRESS_SLOTS; ++e) {
+      if (sdma_pending_[e]) sdma_wait(e);
+      if (d2h_issued_[e]) HIPCHECK(hipEventSynchronize(ev_d2h_[e]));
+    }
   }
 
   void sync() {
     HIPCHECK(hipStreamSynchronize(s_h2d_));
     HIPCHECK(hipStreamSynchronize(s_comp_));
     HIPCHECK(hipStreamSynchronize(s_d2h_));
+  }
+
+  // seconds spent in each host phase since the last reset
+  py::dict host_times(bool reset) {
+    static const char* names[6] = {"submit", "submit_sdma_wait", "submit_graph_launch", "wait_results",
+                                   "egress_copy", "egress_wait"};
+    py::dict o;
+    for (int i = 0; i < 6; ++i) { o[names[i]] = ht_[i]; if (reset) ht_[i] = 0; }
+    return o;
   }
 
   py::dict counters(int p) const {
@@ -911,6 +993,9 @@ class Engine {
   u64 egress_alloc_ = 0;
   u32 ntiles_max_ = 0;
   u32 restore_max_ = 0;
+  u64 get_cap_ = 0;
+  u8* get_out_dev_ = nullptr;
+  GetRes* get_res_dev_ = nullptr;
   u64* scan_status_ = nullptr;
   u32* scan_ctl_ = nullptr;
   u32 scan_smax_ = 0;
@@ -926,20 +1011,24 @@ class Engine {
   u64 lag_stream_ = 0;
   bool xfer_set_ = false;
   DS io_[2];
-  u8* egress_host_[2] = {nullptr, nullptr};
-  u8* egress_host_dev_[2] = {nullptr, nullptr};
+  u8* egress_dev_[EGRESS_SLOTS] = {};
+  u8* egress_host_[EGRESS_SLOTS] = {};
+  u8* egress_host_dev_[EGRESS_SLOTS] = {};
+  int slot_of_[2] = {0, 0};
   int copy_mode_ = 0;
   hsa_agent_t gpu_agent_{}, cpu_agent_{};
   hsa_amd_sdma_engine_id_t sdma_engine_{};
-  hsa_signal_t sdma_sig_[2] = {{0}, {0}};
-  bool sdma_pending_[2] = {false, false};
+  hsa_signal_t sdma_sig_[EGRESS_SLOTS] = {};
+  bool sdma_pending_[EGRESS_SLOTS] = {};
   u32 copy_wgs_ = 16;
+  int sdma_pref_ = -1;
+  double ht_[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   StepIn* stage_in_[2] = {nullptr, nullptr};
   SegIn* stage_segs_[2] = {nullptr, nullptr};
   hipStream_t s_comp_ = nullptr, s_h2d_ = nullptr, s_d2h_ = nullptr;
-  hipEvent_t ev_h2d_[2], ev_done_[2], ev_d2h_[2];
+  hipEvent_t ev_h2d_[2], ev_done_[2], ev_d2h_[EGRESS_SLOTS];
   bool inflight_[2] = {false, false};
-  bool d2h_issued_[2] = {false, false};
+  bool d2h_issued_[EGRESS_SLOTS] = {};
   u64 seq_ = 0;
 };
 
@@ -986,9 +1075,12 @@ PYBIND11_MODULE(_dataplane, m) {
       .def("set_xfer_parity", &Engine::set_xfer_parity)
       .def("set_import", &Engine::set_import, py::arg("recv"), py::arg("stream") = 0)
       .def("restore", &Engine::restore, py::arg("desc"), py::arg("payload"), py::arg("now_ms"))
+      .def("basic_get", &Engine::basic_get, py::arg("q"), py::arg("chslot"), py::arg("noack"), py::arg("now_ms"))
       .def("wait_results", &Engine::wait_results)
       .def("egress_copy", &Engine::egress_copy)
       .def("egress_wait", &Engine::egress_wait)
+      .def("egress_slot", &Engine::egress_slot)
       .def("sync", &Engine::sync)
-      .def("counters", &Engine::counters);
+      .def("counters", &Engine::counters)
+      .def("host_times", &Engine::host_times, py::arg("reset") = false);
 }

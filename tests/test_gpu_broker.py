@@ -11,12 +11,18 @@ GPU_CFG = dict(SMALL, seg_max=64, cmd_max=4096, deliv_max=4096, msg_max=1 << 14,
                carry_cap=1 << 18, dhash=1024, req_max=4096)
 
 
+def _gpu_present():
+    # HIP device count through the data-plane extension itself (torch's lazy CUDA init
+    # reports no device once another library initialised HIP first in this process)
+    from chanamq_amd import ops
+    return ops.load().device_count() > 0
+
+
 def make_plane(kind):
     if kind == "golden":
         from chanamq_amd.engine.golden import GoldenDataPlane
         return GoldenDataPlane(default_queue_capacity=1 << 12, ring_pool=1 << 20, **SMALL)
-    import torch
-    if not torch.cuda.is_available():
+    if not _gpu_present():
         pytest.fail("GPU test scheduled on a machine without a GPU")
     from chanamq_amd.engine.dataplane import GpuDataPlane
     return GpuDataPlane(default_queue_capacity=1 << 12, **GPU_CFG)
@@ -180,8 +186,7 @@ def make_persist_plane(kind):
     if kind == "golden":
         from chanamq_amd.engine.golden import GoldenDataPlane
         return GoldenDataPlane(default_queue_capacity=1 << 12, ring_pool=1 << 20, persist=True, **SMALL)
-    import torch
-    if not torch.cuda.is_available():
+    if not _gpu_present():
         pytest.fail("GPU test scheduled on a machine without a GPU")
     from chanamq_amd.engine.dataplane import GpuDataPlane
     return GpuDataPlane(default_queue_capacity=1 << 12, persist=1, persist_max=4096, persist_bytes=8 << 20,
