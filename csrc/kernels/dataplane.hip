@@ -1038,7 +1038,7 @@ __global__ __launch_bounds__(256) void k_rs_hist(const u32* keys, const u32* np,
   u32 n = *np;
   u32 base = t * SORT_TILE;
   if (base < n) {
-    for (u32 j = 0; j < 16; ++j) {
+    for (u32 j = 0; j < SORT_TILE / 256; ++j) {
       u32 i = base + j * 256 + tid;
       if (i < n) atomicAdd(&cnt[(keys[i] >> shift) & 255], 1u);
     }
@@ -1075,9 +1075,9 @@ __global__ __launch_bounds__(256) void k_rs_scatter(const u32* kin, const u32* v
   if (base >= n) return;
   for (u32 i = tid; i < 1024; i += 256) ((u32*)wc)[i] = 0;
   __syncthreads();
-  u32 wbase = base + w * 1024;
+  u32 wbase = base + w * (SORT_TILE / 4);
   // pass 1: per-wave digit counts
-  for (u32 c = 0; c < 16; ++c) {
+  for (u32 c = 0; c < SORT_TILE / 256; ++c) {
     u32 i = wbase + c * 64 + lane;
     bool valid = i < n;
     u32 dg = valid ? (kin[i] >> shift) & 255 : 0;
@@ -1097,7 +1097,7 @@ __global__ __launch_bounds__(256) void k_rs_scatter(const u32* kin, const u32* v
     for (u32 ww = 0; ww < 4; ++ww) { u32 x = wc[ww][dg]; wc[ww][dg] = run; run += x; }
   }
   __syncthreads();
-  for (u32 c = 0; c < 16; ++c) {
+  for (u32 c = 0; c < SORT_TILE / 256; ++c) {
     u32 i = wbase + c * 64 + lane;
     bool valid = i < n;
     u32 key = valid ? kin[i] : 0;
@@ -1787,48 +1787,62 @@ DEV void unreserve(const DS& d, u32 c, u32 take) {
   if (!d.cons_noack[c]) { atomicSub(&d.ch_unacked[ch], take); d.cons_unacked[c] -= take; }
 }
 
-// one wave per queue: TTL skip, credit-limited round-robin split over consumers,
-// egress byte budget, then descriptors -> Deliv records (sorted by channel later)
+// one block per queue: TTL skip (K12, wave 0), credit-limited round-robin split over the
+// consumers (thread 0, deterministic consumer order), egress byte budget (block-parallel
+// sizes), then one delivery run per granted consumer.  k_runs orders the runs by channel
+// and k_dv_write expands them into Deliv records at their final positions, so no sort
+// over individual deliveries is needed (QueueEntity.scala:318-393, FrameStage.scala:380-406).
 __global__ __launch_bounds__(256) void k_dequeue(DS d) {
-  __shared__ u32 g_cons[4][64];
-  __shared__ u32 g_n[4][64];
-  __shared__ u32 g_off[4][64];
-  u32 w = threadIdx.x >> 6;
-  u32 q = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  u32 lane = lane_id();
-  if (q >= d.q_max || !d.q_active[q]) return;
-  u64 head = d.q_head[q], tail = d.q_tail[q];
+  __shared__ u32 g_cons[RUNS_PER_Q];
+  __shared__ u32 g_n[RUNS_PER_Q];
+  __shared__ u64 s_head;
+  __shared__ u32 s_bytes;
+  const u32 q = blockIdx.x, tid = threadIdx.x, lane = lane_id();
+  if (q >= d.q_max) return;
+  if (!d.q_active[q]) {
+    if (tid == 0) d.q_nruns[q] = 0;
+    return;
+  }
+  u64 head = d.q_head[q];
+  const u64 tail = d.q_tail[q];
   const u64 mask = d.q_ring_mask[q];
   const Desc* ring = d.ring + d.q_ring_off[q];
   const i64 now = d.in->now_ms;
-  // TTL skip at the head (K12)
-  while (head < tail) {
-    u64 idx = head + lane;
-    bool valid = idx < tail;
-    Desc ds;
-    ds.msg = INVALID; ds.expire_ms = 0; ds.flags = 0;
-    if (valid) ds = ring[idx & mask];
-    bool exp = valid && ds.expire_ms != 0 && ds.expire_ms <= now;
-    u64 live = __ballot(valid && !exp);
-    u32 nexp = live ? (__ffsll((unsigned long long)live) - 1) : __popcll(__ballot(valid));
-    wave_consumed(d, ds.msg, q, idx, 1u, lane < nexp);
-    wave_release(d, ds.msg, lane < nexp);
-    if (lane == 0 && nexp) atomicAdd(&d.ctr->n_expired, nexp);
-    head += nexp;
-    if (live) break;
+  if (tid < 64) {   // TTL skip at the head (K12)
+    while (head < tail) {
+      u64 idx = head + lane;
+      bool valid = idx < tail;
+      Desc ds;
+      ds.msg = INVALID; ds.expire_ms = 0; ds.flags = 0;
+      if (valid) ds = ring[idx & mask];
+      bool exp = valid && ds.expire_ms != 0 && ds.expire_ms <= now;
+      u64 live = __ballot(valid && !exp);
+      u32 nexp = live ? (__ffsll((unsigned long long)live) - 1) : __popcll(__ballot(valid));
+      wave_consumed(d, ds.msg, q, idx, 1u, lane < nexp);
+      wave_release(d, ds.msg, lane < nexp);
+      if (lane == 0 && nexp) atomicAdd(&d.ctr->n_expired, nexp);
+      head += nexp;
+      if (live) break;
+    }
+    if (lane == 0) { s_head = head; s_bytes = 0; }
   }
-  u32 mall = d.q_cons_n[q];
-  u64 avail = tail - head;
-  if (mall == 0 || avail == 0) { if (lane == 0) d.q_head[q] = head; return; }
-  u32 m = mall > 64 ? 64 : mall;
-  u32 r = d.q_rr[q] % mall;
-  // (1) counts by credit (lane 0, deterministic consumer order)
-  if (lane == 0) {
+  __syncthreads();
+  head = s_head;
+  const u32 mall = d.q_cons_n[q];
+  const u64 avail = tail - head;
+  if (mall == 0 || avail == 0) {
+    if (tid == 0) { d.q_head[q] = head; d.q_nruns[q] = 0; }
+    return;
+  }
+  const u32 m = mall > RUNS_PER_Q ? RUNS_PER_Q : mall;
+  const u32 r = d.q_rr[q] % mall;
+  // (1) counts by credit
+  if (tid == 0) {
     u64 remaining = avail;
     for (u32 j = 0; j < m; ++j) {
       u32 c = d.q_cons[d.q_cons_off[q] + (r + j) % mall];
-      g_cons[w][j] = c;
-      g_n[w][j] = 0;
+      g_cons[j] = c;
+      g_n[j] = 0;
       if (remaining == 0) continue;
       u32 ch = d.cons_ch[c];
       if (!d.cons_active[c] || !d.ch_flow[ch]) continue;
@@ -1852,159 +1866,231 @@ __global__ __launch_bounds__(256) void k_dequeue(DS d) {
         atomicAdd(&d.ch_unacked[ch], g);
       }
       if (!noack && g) d.cons_unacked[c] += g;
-      g_n[w][j] = g;
+      g_n[j] = g;
       remaining -= g;
     }
   }
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-  // (2) egress byte budget: trim each consumer's run to what fits this step
-  u64 qp = head;
-  u32 total = 0;
-  for (u32 j = 0; j < m; ++j) {
-    u32 cnt = ((volatile u32*)g_n[w])[j];
-    if (!cnt) continue;
-    u32 c = ((volatile u32*)g_cons[w])[j];
-    u32 conn = d.cons_ch[c] / d.chpc;
-    u32 bytes = 0;
-    for (u32 k0 = 0; k0 < cnt; k0 += 64) {
-      u32 k = k0 + lane;
-      u32 sz = 0;
-      if (k < cnt) sz = deliver_size(d, c, d.msgs[ring[(qp + k) & mask].msg], conn);
-      for (int o = 32; o > 0; o >>= 1) sz += __shfl_xor(sz, o, 64);
-      bytes += sz;
+  __syncthreads();
+  // (2) egress bytes of every granted entry, block-parallel per consumer run
+  {
+    u32 mine = 0;
+    u64 qp = head;
+    for (u32 j = 0; j < m; ++j) {
+      const u32 cnt = g_n[j];
+      if (!cnt) continue;
+      const u32 c = g_cons[j];
+      const u32 conn = d.cons_ch[c] / d.chpc;
+      for (u32 k = tid; k < cnt; k += 256) mine += deliver_size(d, c, d.msgs[ring[(qp + k) & mask].msg], conn);
+      qp += cnt;
     }
-    u32 keep = cnt;
-    if (lane == 0) {
-      u32 bb;
-      u32 gb = reserve_upto(d.egress_budget, bytes, (u32)(d.egress_cap > 0xffffffffull ? 0xffffffffu : d.egress_cap), &bb);
-      if (gb < bytes) {
-        // keep the longest prefix that fits in gb bytes
-        u32 acc = 0;
-        keep = 0;
-        for (u32 k = 0; k < cnt; ++k) {
-          u32 sz = deliver_size(d, c, d.msgs[ring[(qp + k) & mask].msg], conn);
-          if (acc + sz > gb) break;
-          acc += sz;
-          ++keep;
+    for (int o = 32; o > 0; o >>= 1) mine += __shfl_xor(mine, o, 64);
+    if (lane == 0 && mine) atomicAdd(&s_bytes, mine);
+  }
+  __syncthreads();
+  if (tid == 0) {
+    const u32 ecap = (u32)(d.egress_cap > 0xffffffffull ? 0xffffffffu : d.egress_cap);
+    const u32 bytes = s_bytes;
+    u32 bb;
+    u32 gb = reserve_upto(d.egress_budget, bytes, ecap, &bb);
+    if (gb < bytes) {
+      // slow path (egress budget nearly spent): give it back and take, run by run, the
+      // longest prefix of each consumer's run that still fits
+      if (gb) atomicSub(d.egress_budget, gb);
+      u64 qp = head;
+      for (u32 j = 0; j < m; ++j) {
+        u32 cnt = g_n[j];
+        if (!cnt) continue;
+        u32 c = g_cons[j];
+        u32 conn = d.cons_ch[c] / d.chpc;
+        u32 rb = 0;
+        for (u32 k = 0; k < cnt; ++k) rb += deliver_size(d, c, d.msgs[ring[(qp + k) & mask].msg], conn);
+        u32 gj = reserve_upto(d.egress_budget, rb, ecap, &bb);
+        u32 keep = cnt;
+        if (gj < rb) {
+          u32 acc = 0;
+          keep = 0;
+          for (u32 k = 0; k < cnt; ++k) {
+            u32 sz = deliver_size(d, c, d.msgs[ring[(qp + k) & mask].msg], conn);
+            if (acc + sz > gj) break;
+            acc += sz;
+            ++keep;
+          }
+          if (gj > acc) atomicSub(d.egress_budget, gj - acc);
+          if (keep < cnt) unreserve(d, c, cnt - keep);
+          g_n[j] = keep;
         }
-        if (gb > acc) atomicSub(d.egress_budget, gb - acc);
-        if (keep < cnt) unreserve(d, c, cnt - keep);
-        g_n[w][j] = keep;
+        qp += keep;
       }
     }
-    __builtin_amdgcn_wave_barrier();
-    keep = ((volatile u32*)g_n[w])[j];
-    qp += keep;
-    total += keep;
-  }
-  // (3) delivery slots
-  if (lane == 0) {
+    // (3) delivery slots (capacity), trimmed from the last run backwards
+    u32 total = 0;
+    for (u32 j = 0; j < m; ++j) total += g_n[j];
     u32 db;
     u32 gt = reserve_upto(&d.ctr->n_deliv, total, d.deliv_max, &db);
     u32 excess = total - gt;
     for (int j = (int)m - 1; j >= 0 && excess; --j) {
-      u32 take = g_n[w][j] < excess ? g_n[w][j] : excess;
+      u32 take = g_n[j] < excess ? g_n[j] : excess;
       if (!take) continue;
-      unreserve(d, g_cons[w][j], take);
-      g_n[w][j] -= take;
+      unreserve(d, g_cons[j], take);
+      g_n[j] -= take;
       excess -= take;
     }
-    u32 run = db;
-    for (u32 j = 0; j < m; ++j) { g_off[w][j] = run; run += g_n[w][j]; }
+    // (4) runs, in round-robin order
+    u32 nr = 0;
+    u64 qp = head;
+    for (u32 j = 0; j < m; ++j) {
+      u32 cnt = g_n[j];
+      if (!cnt) continue;
+      u32 c = g_cons[j];
+      Run rn;
+      rn.ch = d.cons_ch[c];
+      rn.cons = c;
+      rn.cnt = cnt;
+      rn.q = q;
+      rn.qpos = qp;
+      rn.noack = d.cons_noack[c];
+      rn.pad = 0;
+      d.runs[(u64)q * RUNS_PER_Q + nr] = rn;
+      ++nr;
+      qp += cnt;
+    }
+    d.q_nruns[q] = nr;
+    d.q_head[q] = qp;
     d.q_rr[q] = (r + 1) % mall;
   }
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-  qp = head;
-  for (u32 j = 0; j < m; ++j) {
-    u32 cnt = ((volatile u32*)g_n[w])[j];
-    if (!cnt) continue;
-    u32 c = ((volatile u32*)g_cons[w])[j];
-    u32 off = ((volatile u32*)g_off[w])[j];
-    u32 ch = d.cons_ch[c];
-    u32 noack = d.cons_noack[c];
-    for (u32 k = lane; k < cnt; k += 64) {
-      Desc ds = ring[(qp + k) & mask];
-      Deliv dv;
-      dv.chslot = ch;
-      dv.cons = c;
-      dv.msg = ds.msg;
-      dv.q = q;
-      dv.qpos = qp + k;
-      dv.expire_ms = ds.expire_ms;
-      dv.tag = 0;
-      dv.flags = (ds.flags & 1) | (noack ? 2u : 0u);
-      dv.size = 0;
-      d.deliv[off + k] = dv;
-      d.dv_k[0][off + k] = ch;
-      d.dv_v[0][off + k] = off + k;
-    }
-    qp += cnt;
-  }
-  if (lane == 0) d.q_head[q] = qp;
 }
 
-// ============================================================================ tags + sizes
-__global__ void k_dfirst(DS d, u32 src) {
-  u32 i = blockIdx.x * blockDim.x + threadIdx.x;
-  u32 n = d.ctr->n_deliv;
-  if (i >= n) return;
-  const u32* k = d.dv_k[src];
-  u32 ch = k[i];
-  if (i == 0 || k[i - 1] != ch) d.ch_first[ch] = i;
-  u32 conn = ch / d.chpc;
-  if (i == 0 || (k[i - 1] / d.chpc) != conn) d.conn_dfirst[conn] = i;
-  if (i + 1 == n || (k[i + 1] / d.chpc) != conn) d.conn_dlast[conn] = i;
+// ============================================================================ runs -> deliveries
+// One block: gather the step's runs (queue order, then round-robin order), sort them by
+// channel (bitonic on (channel << 32 | run slot): ties keep queue order, the stable order
+// of the reference's per-channel delivery), lay out their deliveries contiguously, and
+// record the first delivery of every channel / first and last of every connection.
+DEV void bitonic_sort_u64(u64* k, u32 np2, u32 tid, u32 nt) {
+  for (u32 sz = 2; sz <= np2; sz <<= 1) {
+    for (u32 j = sz >> 1; j > 0; j >>= 1) {
+      for (u32 i = tid; i < np2; i += nt) {
+        u32 ij = i ^ j;
+        if (ij > i) {
+          bool up = (i & sz) == 0;
+          u64 a = k[i], b = k[ij];
+          if ((a > b) == up) { k[i] = b; k[ij] = a; }
+        }
+      }
+      __syncthreads();
+    }
+  }
+}
+
+__global__ __launch_bounds__(1024) void k_runs(DS d) {
+  __shared__ u64 key_lds[RUN_SORT_LDS];
+  __shared__ u32 lds[1024 / 64 + 1];
+  const u32 tid = threadIdx.x;
+  // pass 1: total runs
+  u32 R = 0;
+  for (u32 b0 = 0; b0 < d.q_max; b0 += 1024) {
+    u32 qq = b0 + tid;
+    u32 v = qq < d.q_max ? d.q_nruns[qq] : 0;
+    u32 all;
+    u32 off = block_scan<1024>(v, lds, all);
+    for (u32 j = 0; j < v; ++j) {
+      const u32 slot = qq * RUNS_PER_Q + j;
+      const u32 pos = R + off + j;
+      const u64 k = ((u64)d.runs[slot].ch << 32) | slot;
+      if (pos < RUN_SORT_LDS) key_lds[pos] = k;
+      d.run_key[pos] = k;
+    }
+    R += all;
+  }
+  __syncthreads();
+  u32 np2 = 1;
+  while (np2 < R) np2 <<= 1;
+  const bool in_lds = np2 <= RUN_SORT_LDS;
+  u64* key = in_lds ? key_lds : d.run_key;
+  for (u32 i = R + tid; i < np2; i += 1024) key[i] = ~0ull;
+  __syncthreads();
+  if (R > 1) bitonic_sort_u64(key, np2, tid, 1024);
+  // pass 2: delivery offsets in run order
+  u32 run = 0;
+  for (u32 b0 = 0; b0 < R; b0 += 1024) {
+    const u32 s = b0 + tid;
+    u32 cnt = 0, slot = 0;
+    if (s < R) { slot = (u32)key[s]; cnt = d.runs[slot].cnt; }
+    u32 all;
+    u32 off = block_scan<1024>(cnt, lds, all);
+    if (s < R) {
+      const u32 start = run + off;
+      d.run_order[s] = slot;
+      d.run_start[s] = start;
+      const u32 ch = (u32)(key[s] >> 32);
+      const u32 conn = ch / d.chpc;
+      const u32 pch = s > 0 ? (u32)(key[s - 1] >> 32) : INVALID;
+      const u32 nch = s + 1 < R ? (u32)(key[s + 1] >> 32) : INVALID;
+      if (pch != ch) d.ch_first[ch] = start;
+      if (pch == INVALID || pch / d.chpc != conn) d.conn_dfirst[conn] = start;
+      if (nch == INVALID || nch / d.chpc != conn) d.conn_dlast[conn] = start + cnt - 1;
+    }
+    run += all;
+  }
+  if (tid == 0) d.tot[TS_NRUNS] = R;
 }
 
 DEV void wave_consumed(const DS& d, u32 msg, u32 q, u64 qpos, u32 kind, bool valid);
-DEV u32 tag_one(const DS& d, u32 src, u32 i, u32 n) {
-  const u32* kk = d.dv_k[src];
-  u32 ch = kk[i];
-  u32 di = d.dv_v[src][i];
-  Deliv& dv = d.deliv[di];
-  u32 rank = i - d.ch_first[ch];
-  u64 tag = d.ch_next_tag[ch] + rank;
-  bool last = (i + 1 == n) || kk[i + 1] != ch;
-  USlot u;
-  u.state = (dv.flags & 2) ? US_DONE : US_PENDING;
-  u.msg = dv.msg;
-  u.q = dv.q;
-  u.cons = dv.cons;
-  u.qpos = dv.qpos;
-  u.expire_ms = dv.expire_ms;
-  d.uwin[(u64)ch * (d.ucap_mask + 1) + ((tag - 1) & d.ucap_mask)] = u;
-  const MsgEnt& m = d.msgs[dv.msg];
-  u32 conn = ch / d.chpc;
-  u32 sz = deliver_size(d, dv.cons, m, conn);
-  dv.size = sz;
-  d.dv_size[i] = sz;
-  dv.tag = tag;
-  u32 lat = (u32)d.in->step - m.pub_step;
-  if (last) {
-    if (atomicExch(&d.ch_dirty[ch], 1u) == 0) {
-      u32 k = atomicAdd(d.n_dirty, 1u);
-      d.dirty_list[k] = ch;
-    }
-  }
-  return lat;
-}
-
-__global__ void k_tags(DS d, u32 src) {
-  u32 i = blockIdx.x * blockDim.x + threadIdx.x;
-  u32 n = d.ctr->n_deliv;
-  bool valid = i < n;
+// thread per delivery: expand its run (binary search), assign the channel's next delivery
+// tag, fill the unacked window slot, size the rendered frames
+__global__ void k_dv_write(DS d) {
+  const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+  const u32 n = d.ctr->n_deliv;
+  const bool valid = i < n;
   u32 lat = 0;
-  if (valid) lat = tag_one(d, src, i, n);
-  else if (i < d.deliv_max) d.dv_size[i] = 0;
-  if (d.persist) {   // manual-ack delivery of a persistent message: its row becomes an unack
-    const Deliv* dv = valid ? &d.deliv[d.dv_v[src][i]] : nullptr;
-    wave_consumed(d, dv ? dv->msg : INVALID, dv ? dv->q : 0, dv ? dv->qpos : 0, 3u, valid && !(dv->flags & 2));
+  Deliv dv;
+  dv.msg = INVALID; dv.q = 0; dv.qpos = 0; dv.flags = 2;
+  if (valid) {
+    const u32 R = d.tot[TS_NRUNS];
+    u32 lo = 0, hi = R;   // last s with run_start[s] <= i
+    while (hi - lo > 1) {
+      u32 mid = (lo + hi) >> 1;
+      if (d.run_start[mid] <= i) lo = mid; else hi = mid;
+    }
+    const Run rn = d.runs[d.run_order[lo]];
+    const u32 k = i - d.run_start[lo];
+    const Desc ds = d.ring[d.q_ring_off[rn.q] + ((rn.qpos + k) & d.q_ring_mask[rn.q])];
+    const u32 ch = rn.ch;
+    const u64 tag = d.ch_next_tag[ch] + (i - d.ch_first[ch]);
+    dv.chslot = ch;
+    dv.cons = rn.cons;
+    dv.msg = ds.msg;
+    dv.q = rn.q;
+    dv.qpos = rn.qpos + k;
+    dv.expire_ms = ds.expire_ms;
+    dv.tag = tag;
+    dv.flags = (ds.flags & 1) | (rn.noack ? 2u : 0u);
+    USlot u;
+    u.state = rn.noack ? US_DONE : US_PENDING;
+    u.msg = ds.msg;
+    u.q = rn.q;
+    u.cons = rn.cons;
+    u.qpos = dv.qpos;
+    u.expire_ms = ds.expire_ms;
+    d.uwin[(u64)ch * (d.ucap_mask + 1) + ((tag - 1) & d.ucap_mask)] = u;
+    const MsgEnt& m = d.msgs[ds.msg];
+    const u32 sz = deliver_size(d, rn.cons, m, ch / d.chpc);
+    dv.size = sz;
+    d.dv_size[i] = sz;
+    d.deliv[i] = dv;
+    lat = (u32)d.in->step - m.pub_step;
+    // the channel's last delivery this step: the window needs a k_chan_advance pass
+    bool last = i + 1 == n || (k + 1 == rn.cnt && (lo + 1 >= R || d.runs[d.run_order[lo + 1]].ch != ch));
+    if (last && atomicExch(&d.ch_dirty[ch], 1u) == 0) {
+      u32 kk = atomicAdd(d.n_dirty, 1u);
+      d.dirty_list[kk] = ch;
+    }
+  } else if (i < d.deliv_max) {
+    d.dv_size[i] = 0;
   }
+  if (d.persist)   // manual-ack delivery of a persistent message: its row becomes an unack
+    wave_consumed(d, dv.msg, dv.q, dv.qpos, 3u, valid && !(dv.flags & 2));
   wave_add_u32(d.ctr->lat_hist, lat < LAT_BINS ? lat : LAT_BINS - 1, 1u, valid);
 }
-
 
 // per connection: egress size = returns + confirms + deliveries
 __global__ void k_conn_sizes(DS d) {
@@ -2044,13 +2130,13 @@ DEV u32 put_frame_hdr(u8* o, u32 type, u32 ch, u32 size) {
 }
 
 // one wave per delivery
-__global__ __launch_bounds__(256) void k_render_deliv(DS d, u32 src) {
+__global__ __launch_bounds__(256) void k_render_deliv(DS d) {
   u32 i = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   u32 lane = lane_id();
   u32 n = d.ctr->n_deliv;
   if (i >= n) return;
-  u32 ch = d.dv_k[src][i];
-  const Deliv dv = d.deliv[d.dv_v[src][i]];
+  const Deliv dv = d.deliv[i];
+  const u32 ch = dv.chslot;
   const MsgEnt m = d.msgs[dv.msg];
   u32 conn = ch / d.chpc;
   u32 f = d.conn_dfirst[conn];
@@ -2190,21 +2276,20 @@ __global__ __launch_bounds__(256) void k_render_returns(DS d) {
 }
 
 // ============================================================================ post / final
-__global__ void k_post(DS d, u32 src) {
+__global__ void k_post(DS d) {
   u32 i = blockIdx.x * blockDim.x + threadIdx.x;
   u32 n = d.ctr->n_deliv;
   u32 msg = INVALID, q = 0;
   u64 qpos = 0;
   bool aa = false;
   if (i < n) {
-    const Deliv& dv = d.deliv[d.dv_v[src][i]];
+    const Deliv& dv = d.deliv[i];
     aa = dv.flags & 2;
     msg = dv.msg;
     q = dv.q;
     qpos = dv.qpos;
-    const u32* kk = d.dv_k[src];
-    u32 ch = kk[i];
-    if (i + 1 == n || kk[i + 1] != ch) d.ch_next_tag[ch] = dv.tag + 1;
+    const u32 ch = dv.chslot;
+    if (i + 1 == n || d.deliv[i + 1].chslot != ch) d.ch_next_tag[ch] = dv.tag + 1;
   }
   wave_consumed(d, msg, q, qpos, 0u, aa);
   wave_release(d, msg, aa);

@@ -196,6 +196,16 @@ struct Deliv {          // one delivery produced by the dequeue kernel
   u32 size;             // rendered bytes
 };
 
+struct Run {            // consecutive queue entries granted to one consumer this step
+  u32 ch;               // channel slot
+  u32 cons;
+  u32 cnt;
+  u32 q;
+  u64 qpos;             // queue position of the first entry
+  u32 noack;
+  u32 pad;
+};
+
 struct USlot {          // per-channel unacked window slot
   u32 state;
   u32 msg;

@@ -5,12 +5,14 @@
 #include "dp_common.h"
 
 #define CAND_MAX 8192         // frame candidates per segment held in LDS
-#define SORT_TILE 4096        // radix-sort tile (256 threads x 16)
+#define SORT_TILE 1024        // radix-sort tile (256 threads x 4): more tiles, more blocks in flight
 #define TOPIC_K 256           // topic key vector: 8 words x 32 hash bits (int8 +-1)
 #define TOPIC_WORDS 8
 #define LAT_BINS 32
 #define WORLD_MAX 16          // ranks of one sharded broker (one node: 8 GPUs)
 #define EGRESS_SLOTS 3        // rotating egress buffers (render of step t || D2H of t-1, t-2)
+#define RUNS_PER_Q 64         // consumers served per queue per step (dequeue round-robin window)
+#define RUN_SORT_LDS 8192     // runs sorted in LDS by k_runs (more: global-memory sort)
 
 // tot[] scratch slots (scan totals and phase bookkeeping)
 enum : u32 {
@@ -18,6 +20,7 @@ enum : u32 {
   TS_PAIR_BASE = 22, TS_PAIR_N = 23,    // pair base of the phase / pairs so far
   TS_NIMPORT = 24, TS_IMPORT_BASE = 25, // imported records / their work-buffer base
   TS_PERSIST = 26,                      // packed persist bytes
+  TS_NRUNS = 27,                        // delivery runs of the step (k_runs)
   TS_XSCAN = 32                         // + 2*r: per-destination record / byte totals
 };
 
@@ -161,12 +164,17 @@ struct DS {
   u64* id_next;             // snowflake virtual sequence position
 
   // ---------------- deliveries
-  Deliv* deliv;
-  u32* dv_k[2];
-  u32* dv_v[2];
+  Deliv* deliv;             // in final (channel-sorted) order
   u32* dv_size;             // by sorted position
   u32* dv_off;
   u32* ch_first;            // [chslots] scratch
+  // delivery runs: k_dequeue emits one run per (queue, consumer) grant, k_runs orders
+  // them by channel, k_dv_write expands them into Deliv records at their final positions
+  Run* runs;                // [q_max * RUNS_PER_Q]
+  u32* q_nruns;             // [q_max] runs of the queue this step
+  u32* run_order;           // [q_max * RUNS_PER_Q] run slots in delivery order
+  u32* run_start;           // first delivery index of each ordered run
+  u64* run_key;             // global sort space when the runs exceed the LDS sort
 
   // ---------------- requeue
   ReqItem* req;

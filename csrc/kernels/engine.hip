@@ -327,9 +327,15 @@ class Engine {
     d_.id_next = (u64*)dev("id_next", 8);
 
     d_.deliv = (Deliv*)dev("deliv", sizeof(Deliv) * (u64)d_.deliv_max);
-    for (int k = 0; k < 2; ++k) {
-      d_.dv_k[k] = (u32*)dev(k ? "dv_k1" : "dv_k0", 4ull * d_.deliv_max);
-      d_.dv_v[k] = (u32*)dev(k ? "dv_v1" : "dv_v0", 4ull * d_.deliv_max);
+    {
+      const u64 nrun = (u64)d_.q_max * RUNS_PER_Q;
+      d_.runs = (Run*)dev("runs", sizeof(Run) * nrun);
+      d_.q_nruns = (u32*)dev("q_nruns", 4ull * d_.q_max);
+      d_.run_order = (u32*)dev("run_order", 4ull * nrun);
+      d_.run_start = (u32*)dev("run_start", 4ull * nrun);
+      u64 np2 = 1;
+      while (np2 < nrun) np2 <<= 1;
+      d_.run_key = (u64*)dev("run_key", 8ull * np2);
     }
     d_.dv_size = (u32*)dev("dv_size", 4ull * d_.deliv_max);
     d_.dv_off = (u32*)dev("dv_off", 4ull * d_.deliv_max);
@@ -339,8 +345,7 @@ class Engine {
     d_.req_n = (u32*)dev("req_n", 4);
     d_.req_q_n = (u32*)dev("req_q_n", 4ull * d_.q_max);
 
-    u32 max_sort = d_.pair_max > d_.deliv_max ? d_.pair_max : d_.deliv_max;
-    ntiles_max_ = ceil_div(max_sort, SORT_TILE);
+    ntiles_max_ = ceil_div(d_.pair_max, SORT_TILE);
     d_.hist = (u32*)dev("hist", 4ull * 256 * ntiles_max_);
     d_.hist_scan = (u32*)dev("hist_scan", 4ull * 256 * ntiles_max_);
     d_.scan_tmp = (u32*)dev("scan_tmp", 4ull * 1024);
@@ -928,21 +933,18 @@ class Engine {
     // dispatch, in queue-offset order (QueueEntity.scala:415-446)
     hipLaunchKernelGGL(k_requeue, dim3(d.q_max), dim3(256), 0, s, d);
     hipLaunchKernelGGL(k_requeue_compact, dim3(1), dim3(1024), 0, s, d);
-    hipLaunchKernelGGL(k_dequeue, blocks((u64)d.q_max * 64, 256), dim3(256), 0, s, d);
-    u32* dk[2] = {d.dv_k[0], d.dv_k[1]};
-    u32* dvv[2] = {d.dv_v[0], d.dv_v[1]};
-    u32 dsrc = radix_sort(s, dk, dvv, &d.ctr->n_deliv, d.deliv_max, d.ch_bits);
-    hipLaunchKernelGGL(k_dfirst, blocks(d.deliv_max, 256), dim3(256), 0, s, d, dsrc);
-    hipLaunchKernelGGL(k_tags, blocks(d.deliv_max, 256), dim3(256), 0, s, d, dsrc);
+    hipLaunchKernelGGL(k_dequeue, dim3(d.q_max), dim3(256), 0, s, d);
+    hipLaunchKernelGGL(k_runs, dim3(1), dim3(1024), 0, s, d);
+    hipLaunchKernelGGL(k_dv_write, blocks(d.deliv_max, 256), dim3(256), 0, s, d);
     launch_scan(s, {{d.dv_size, d.dv_off}}, &d.ctr->n_deliv, d.deliv_max, 6);
     hipLaunchKernelGGL(k_conn_sizes, blocks(d.c_max, 256), dim3(256), 0, s, d);
     launch_scan(s, {{d.conn_total, d.conn_base}}, nullptr, d.c_max, 7);
     hipLaunchKernelGGL(k_conn_out, blocks(d.c_max, 256), dim3(256), 0, s, d);
     hipLaunchKernelGGL(k_render_returns, blocks((u64)d.pub_max * 64, 256), dim3(256), 0, s, d);
     hipLaunchKernelGGL(k_render_confirms, blocks(d.c_max, 256), dim3(256), 0, s, d);
-    hipLaunchKernelGGL(k_render_deliv, blocks((u64)d.deliv_max * 64, 256), dim3(256), 0, s, d, dsrc);
+    hipLaunchKernelGGL(k_render_deliv, blocks((u64)d.deliv_max * 64, 256), dim3(256), 0, s, d);
     u64 pn = d.deliv_max > d.c_max ? d.deliv_max : d.c_max;
-    hipLaunchKernelGGL(k_post, blocks(pn, 256), dim3(256), 0, s, d, dsrc);
+    hipLaunchKernelGGL(k_post, blocks(pn, 256), dim3(256), 0, s, d);
     hipLaunchKernelGGL(k_post2, blocks(d.c_max, 256), dim3(256), 0, s, d);
     if (d.persist) {
       hipLaunchKernelGGL(k_persist_size, blocks(d.persist_max, 256), dim3(256), 0, s, d);
