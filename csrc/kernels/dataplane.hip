@@ -643,7 +643,11 @@ __global__ __launch_bounds__(256) void k_frame_scan(DS d) {
   __syncthreads();
   if (sh_ncmd && tc > 0) {
     u32 cb = sh_cmd_base;
-    for (u32 i = cb + tid; i < cb + tc && i < d.cmd_max; i += 256) d.cmds[i].kind = CK_NONE;
+    for (u32 i = cb + tid; i < cb + tc && i < d.cmd_max; i += 256) {
+      d.cmds[i].kind = CK_NONE;
+      d.cmd_is_pub[i] = 0;
+      d.cmd_is_ack[i] = 0;
+    }
     if (tid == 0) sh_cmd_base = INVALID;
     __syncthreads();
   }
@@ -713,7 +717,11 @@ __global__ __launch_bounds__(256) void k_frame_scan(DS d) {
         }
       }
       c.raw_len = endp - p;
-      d.cmds[sh_cmd_base + run + r] = c;
+      const u32 ci = sh_cmd_base + run + r;
+      d.cmds[ci] = c;
+      // classification for the publish / ack rank scans (fused k_classify)
+      d.cmd_is_pub[ci] = c.kind == CK_PUBLISH;
+      d.cmd_is_ack[ci] = c.kind == CK_ACK || c.kind == CK_NACK || c.kind == CK_REJECT;
       if (c.kind == CK_CONTROL) {
         u32 cbase;
         u32 g = reserve_upto(&d.ctr->ctrl_bytes, c.raw_len, (u32)d.ctrl_cap, &cbase);
@@ -787,22 +795,56 @@ DEV bool skip_shortstr(const u8* p, u32& o, u32 end) {
 DEV u32 build_keyvec(const DS& d, const u8* key, u32 len, u32 pi) {
   Words kw = words_of(key, len);
   if (d.tb_max) {
-    i8* kv = d.pub_keyvec + (u64)pi * TOPIC_K;
+    // 32 int8 lanes per word (+1 / -1 per hash bit), written as two 16-B stores
+    uint4* kv = (uint4*)(d.pub_keyvec + (u64)pi * TOPIC_K);
     u32 off = 0;
     u32 wi = 0;
     if (kw.count) {
       while (wi < TOPIC_WORDS && off <= kw.eff) {
         u32 wl = word_len(key, off, kw.eff);
         u32 h = fnv1a32(key + off, wl);
-        for (int bb = 0; bb < 32; ++bb) kv[wi * 32 + bb] = ((h >> bb) & 1) ? 1 : -1;
+        u32 pk[8];
+#pragma unroll
+        for (int g = 0; g < 8; ++g) {
+          u32 v = 0;
+#pragma unroll
+          for (int bb = 0; bb < 4; ++bb) v |= (((h >> (g * 4 + bb)) & 1) ? 0x01u : 0xffu) << (8 * bb);
+          pk[g] = v;
+        }
+        kv[wi * 2] = make_uint4(pk[0], pk[1], pk[2], pk[3]);
+        kv[wi * 2 + 1] = make_uint4(pk[4], pk[5], pk[6], pk[7]);
         off += wl + 1;
         ++wi;
       }
     }
-    for (; wi < TOPIC_WORDS; ++wi)
-      for (int bb = 0; bb < 32; ++bb) kv[wi * 32 + bb] = 0;
+    for (; wi < TOPIC_WORDS; ++wi) {
+      kv[wi * 2] = make_uint4(0, 0, 0, 0);
+      kv[wi * 2 + 1] = make_uint4(0, 0, 0, 0);
+    }
   }
   return kw.count;
+}
+
+// K9 ack mark (AMQChannel.scala:128-174): single tag -> its window slot; multiple -> the
+// channel's ack/requeue watermark.  Marks only depend on earlier steps' deliveries.
+DEV void apply_ack(const DS& d, const Ack& a) {
+  const u32 ch = a.chslot;
+  if (ch == INVALID) return;
+  const u64 nt = d.ch_next_tag[ch];
+  u64 tag = a.tag;
+  if (tag == 0 && a.multiple) tag = nt - 1;  // ack everything outstanding
+  const bool requeue = (a.kind != CK_ACK) && a.requeue;
+  if (a.multiple) {
+    atomicMax((unsigned long long*)(requeue ? &d.ch_req_upto[ch] : &d.ch_ack_upto[ch]), (unsigned long long)tag);
+  } else if (tag >= d.ch_uhead[ch] && tag < nt) {
+    USlot& u = d.uwin[(u64)ch * (d.ucap_mask + 1) + ((tag - 1) & d.ucap_mask)];
+    atomicCAS(&u.state, (u32)US_PENDING, requeue ? (u32)US_REQUEUE : (u32)US_ACKED);
+  }
+  if (atomicExch(&d.ch_dirty[ch], 1u) == 0) {
+    u32 k = atomicAdd(d.n_dirty, 1u);
+    d.dirty_list[k] = ch;
+  }
+  atomicAdd(&d.ctr->n_acked, 1u);
 }
 
 __global__ void k_decode(DS d) {
@@ -929,6 +971,7 @@ __global__ void k_decode(DS d) {
     else if (c.kind == CK_REJECT) { a.multiple = 0; a.requeue = bits & 1; }
     else { a.multiple = bits & 1; a.requeue = (bits >> 1) & 1; }
     d.acks[ai] = a;
+    apply_ack(d, a);   // fused K9 mark: k_chan_advance resolves the window next
   }
 }
 
@@ -1373,13 +1416,46 @@ DEV void log_reserve(const DS& d) {
   d.tot[8] = *d.msg_free_top;
   *d.msg_free_top = d.tot[8] - routed;
   d.ctr->n_routed_msgs += routed;
+  atomicAdd((unsigned long long*)d.live_bytes, (unsigned long long)total);
+}
+
+// live bytes per log block (fused k_live_add), by one wave: the phase's slots are
+// contiguous from the step base (slot p at base + pub_slot_off[p]) and a slot counts in
+// the block where it starts, as release_msg subtracts it.  Lane l owns log block b0 + l:
+// its bytes = S(end of the block) - S(start), S(x) = pub_slot_off of the first slot
+// starting at or after x (a prefix sum; binary search, all lanes in parallel).
+DEV void live_add_blocks(const DS& d, u32 lane) {
+  const u64 head = *d.log_step_base;
+  const u32 total = d.tot[1];
+  if (head == INVALID || total == 0) return;
+  const u32 lo = d.tot[TS_RANGE_LO];
+  u32 hi = d.tot[TS_RANGE_HI];
+  if (hi > d.pub_cap) hi = d.pub_cap;
+  const u64 b0 = head / d.log_block, b1 = (head + total - 1) / d.log_block;
+  for (u64 g = b0; g <= b1; g += 64) {
+    const u64 bk = g + lane;
+    u64 s_end = 0, s_beg = 0;
+    if (bk <= b1) {
+      auto S = [&](u64 x) -> u64 {
+        u32 a = lo, b = hi;
+        while (a < b) { u32 mid = (a + b) >> 1; if ((u64)d.pub_slot_off[mid] < x) a = mid + 1; else b = mid; }
+        return a < hi ? (u64)d.pub_slot_off[a] : (u64)total;
+      };
+      s_end = bk == b1 ? (u64)total : S((bk + 1) * d.log_block - head);
+      s_beg = bk == b0 ? 0 : S(bk * d.log_block - head);
+      if (s_end > s_beg)
+        atomicAdd((unsigned long long*)&d.log_live[bk % d.n_log_blocks], (unsigned long long)(s_end - s_beg));
+    }
+  }
 }
 __global__ void k_log_reserve(DS d) { if (threadIdx.x == 0) log_reserve(d); }
 
 // one wave per publish: allocate, fill MsgEnt, copy exchange/rk/props/body into the log
 DEV void store_one(const DS& d, u32 p, u32 lane);
+DEV void live_add_blocks(const DS& d, u32 lane);
 __global__ __launch_bounds__(256) void k_store(DS d) {
   u32 lane = lane_id();
+  if (blockIdx.x == 0 && threadIdx.x < 64) live_add_blocks(d, lane);
   u32 n = d.tot[TS_RANGE_HI];
   if (n > d.pub_cap) n = d.pub_cap;
   const u32 nw = (gridDim.x * blockDim.x) >> 6;
@@ -1612,12 +1688,14 @@ __global__ void k_qfirst(DS d, u32 src) {
   if (i == 0 || (k[i - 1] >> rb) != (k[i] >> rb)) d.q_first[k[i] >> rb] = i;
 }
 
-DEV u32 enqueue_one(const DS& d, u32 src, u32 i, u32 n, PersistRec* pr) {
+DEV u32 enqueue_one(const DS& d, u32 src, u32 i, u32 n, PersistRec* pr, u32 hs_ntiles) {
   const u32* kk = d.pair_k[src];
   const u32 rb = d.rank_bits;
   u32 q = kk[i] >> rb;
   u32 p = d.pair_v[src][i];
-  u32 first = d.q_first[q];
+  // single-pass sort (queue|rank key <= 8 bits): the queue's first pair is where digit
+  // (q << rank_bits) starts; otherwise k_qfirst recorded it
+  u32 first = hs_ntiles ? d.hist_scan[(q << rb) * hs_ntiles] : d.q_first[q];
   u32 rank = i - first;
   bool last = (i + 1 == n) || (kk[i + 1] >> rb) != q;
   const Pub& pb = d.pubs[p];
@@ -1649,12 +1727,12 @@ DEV u32 enqueue_one(const DS& d, u32 src, u32 i, u32 n, PersistRec* pr) {
   return drop;
 }
 
-__global__ void k_enqueue(DS d, u32 src) {
+__global__ void k_enqueue(DS d, u32 src, u32 hs_ntiles) {
   u32 i = blockIdx.x * blockDim.x + threadIdx.x;
   u32 n = d.tot[TS_PAIR_N];
   PersistRec pr;
   pr.msg = INVALID;
-  u32 drop = i < n ? enqueue_one(d, src, i, n, &pr) : INVALID;
+  u32 drop = i < n ? enqueue_one(d, src, i, n, &pr, hs_ntiles) : INVALID;
   wave_release(d, drop, drop != INVALID);
   if (drop != INVALID) atomicAdd(&d.ctr->n_ring_full, 1u);
   if (d.persist) {
@@ -2111,6 +2189,44 @@ __global__ void k_conn_sizes(DS d) {
   d.conn_total[c] = d.conn_ret_bytes[c] + conf + dl;
 }
 
+// single block (c_max <= CONN_LAYOUT_MAX): k_conn_sizes + scan of conn_total + k_conn_out
+#define CONN_LAYOUT_MAX 8192
+__global__ __launch_bounds__(1024) void k_conn_layout(DS d) {
+  __shared__ u32 lds[1024 / 64 + 1];
+  u32 run = 0;
+  for (u32 b0 = 0; b0 < d.c_max; b0 += 1024) {
+    const u32 c = b0 + threadIdx.x;
+    u32 total = 0;
+    if (c < d.c_max) {
+      u32 conf = 0;
+      for (u32 l = 0; l < d.chpc; ++l) {
+        u32 ch = c * d.chpc + l;
+        if (d.ch_pub_cnt[ch] && d.ch_confirm[ch]) conf += 21;
+      }
+      d.conn_conf_bytes[c] = conf;
+      u32 dl = 0;
+      u32 f = d.conn_dfirst[c];
+      if (f != INVALID) {
+        u32 l = d.conn_dlast[c];
+        dl = d.dv_off[l] + d.dv_size[l] - d.dv_off[f];
+      }
+      total = d.conn_ret_bytes[c] + conf + dl;
+      d.conn_total[c] = total;
+    }
+    u32 all;
+    const u32 off = block_scan<1024>(total, lds, all);
+    if (c < d.c_max) {
+      ConnOut o;
+      o.off = run + off;
+      o.len = total;
+      d.conn_base[c] = o.off;
+      d.conn_out[c] = o;
+      if (c == d.c_max - 1) d.ctr->egress_bytes = o.off + o.len;
+    }
+    run += all;
+  }
+}
+
 __global__ void k_conn_out(DS d) {
   u32 c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= d.c_max) return;
@@ -2187,9 +2303,7 @@ __global__ __launch_bounds__(256) void k_render_deliv(DS d) {
 }
 
 // confirms: one thread per connection writes its channels' coalesced Basic.Ack frames
-__global__ void k_render_confirms(DS d) {
-  u32 c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= d.c_max) return;
+DEV void render_confirms(const DS& d, u32 c) {
   u32 conf = d.conn_conf_bytes[c];
   u8* o = (u8*)d.in->egress + (u64)d.conn_base[c] + d.conn_ret_bytes[c];
   u32 p = 0;
@@ -2214,12 +2328,7 @@ __global__ void k_render_confirms(DS d) {
 }
 
 // returns: one wave per returned publish (Basic.Return 312/313 + header + body)
-__global__ __launch_bounds__(256) void k_render_returns(DS d) {
-  u32 i = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  u32 lane = lane_id();
-  u32 n = d.ctr->n_returns;
-  if (n > d.pub_max) n = d.pub_max;
-  if (i >= n) return;
+DEV void render_return(const DS& d, u32 i, u32 lane) {
   u32 p = d.ret_list[i];
   const Pub pb = d.pubs[p];
   u32 code = d.pub_ret[p];
@@ -2275,6 +2384,21 @@ __global__ __launch_bounds__(256) void k_render_returns(DS d) {
   }
 }
 
+// blocks [0, RC_RET_BLOCKS): returns, grid-stride, one wave each; the rest: confirms,
+// one thread per connection
+#define RC_RET_BLOCKS 512
+__global__ __launch_bounds__(256) void k_render_rc(DS d) {
+  if (blockIdx.x >= RC_RET_BLOCKS) {
+    u32 c = (blockIdx.x - RC_RET_BLOCKS) * blockDim.x + threadIdx.x;
+    if (c < d.c_max) render_confirms(d, c);
+    return;
+  }
+  u32 n = d.ctr->n_returns;
+  if (n > d.pub_max) n = d.pub_max;
+  const u32 lane = lane_id();
+  for (u32 i = (blockIdx.x * blockDim.x + threadIdx.x) >> 6; i < n; i += RC_RET_BLOCKS * 4) render_return(d, i, lane);
+}
+
 // ============================================================================ post / final
 __global__ void k_post(DS d) {
   u32 i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -2293,10 +2417,12 @@ __global__ void k_post(DS d) {
   }
   wave_consumed(d, msg, q, qpos, 0u, aa);
   wave_release(d, msg, aa);
-  // reset per-connection scratch
+  // reset per-connection scratch (fused k_post2)
   if (i < d.c_max) {
     d.conn_dfirst[i] = INVALID;
     d.conn_dlast[i] = INVALID;
+    d.conn_ret_bytes[i] = 0;
+    d.conn_ret_min[i] = INVALID;
   }
 }
 
@@ -2551,13 +2677,29 @@ __global__ __launch_bounds__(64) void k_basic_get(DS d, u32 q, u32 ch, u32 noack
 // one block per queue with requeued items: gather, bitonic-sort by queue position,
 // push back in front of the head with the redelivered flag (QueueEntity.scala:415-446)
 #define REQ_BLK 1024
+DEV void requeue_compact(const DS& d);
+DEV void requeue_queue(const DS& d, u32 q, u64* kpos, u32* kidx, u32* cnt_p);
 __global__ __launch_bounds__(256) void k_requeue(DS d) {
   __shared__ u64 kpos[REQ_BLK];
   __shared__ u32 kidx[REQ_BLK];
   __shared__ u32 cnt;
+  __shared__ u32 s_last;
   u32 q = blockIdx.x;
   if (q == 0 && threadIdx.x == 0) *d.n_dirty = 0;   // fused k_reset_dirty (after k_chan_advance)
-  if (q >= d.q_max || d.req_q_n[q] == 0) return;
+  if (q < d.q_max && d.req_q_n[q] != 0) requeue_queue(d, q, kpos, kidx, &cnt);
+  // the last block to finish compacts the unconsumed items (fused k_requeue_compact)
+  __threadfence();
+  __syncthreads();
+  if (threadIdx.x == 0) s_last = atomicAdd(&d.tot[TS_REQ_TICKET], 1u) == gridDim.x - 1;
+  __syncthreads();
+  if (!s_last) return;
+  __threadfence();
+  if (threadIdx.x == 0) d.tot[TS_REQ_TICKET] = 0;
+  requeue_compact(d);
+}
+
+DEV void requeue_queue(const DS& d, u32 q, u64* kpos, u32* kidx, u32* cnt_p) {
+  u32& cnt = *cnt_p;
   u32 tid = threadIdx.x;
   if (tid == 0) cnt = 0;
   __syncthreads();
@@ -2610,21 +2752,21 @@ __global__ __launch_bounds__(256) void k_requeue(DS d) {
   }
 }
 
-__global__ void k_requeue_compact(DS d) {
-  // single block: compact the remaining (unconsumed) requeue items
-  __shared__ u32 lds[1024 / 64 + 1];
+DEV void requeue_compact(const DS& d) {
+  // one block of 256: compact the remaining (unconsumed) requeue items
+  __shared__ u32 lds[256 / 64 + 1];
   u32 n = *d.req_n;
   if (n == 0) return;
   if (n > d.req_max) n = d.req_max;
   u32 run = 0;
-  for (u32 b0 = 0; b0 < n; b0 += 1024) {
+  for (u32 b0 = 0; b0 < n; b0 += 256) {
     u32 i = b0 + threadIdx.x;
     ReqItem r;
     r.q = INVALID;
     if (i < n) r = d.req[i];
     u32 keep = (i < n && r.q != INVALID) ? 1 : 0;
     u32 all;
-    u32 off = block_scan<1024>(keep, lds, all);
+    u32 off = block_scan<256>(keep, lds, all);
     __syncthreads();
     if (keep) d.req[run + off] = r;  // run + off <= i: safe forward compaction
     __syncthreads();

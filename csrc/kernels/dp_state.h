@@ -21,6 +21,8 @@ enum : u32 {
   TS_NIMPORT = 24, TS_IMPORT_BASE = 25, // imported records / their work-buffer base
   TS_PERSIST = 26,                      // packed persist bytes
   TS_NRUNS = 27,                        // delivery runs of the step (k_runs)
+  TS_REQ_TICKET = 28,                   // k_requeue finished-block ticket (last block compacts)
+  TS_RS_TICKET = 29,                    // k_rs_hist finished-block ticket (last block: offsets)
   TS_XSCAN = 32                         // + 2*r: per-destination record / byte totals
 };
 

@@ -881,7 +881,6 @@ class Engine {
     hipLaunchKernelGGL(k_stage, dim3(d.seg_max, 4), dim3(256), 0, s, d);
     hipLaunchKernelGGL(k_cand, dim3(2048), dim3(256), 0, s, d);
     hipLaunchKernelGGL(k_frame_scan, dim3(d.seg_max), dim3(256), 0, s, d);
-    hipLaunchKernelGGL(k_classify, blocks(d.cmd_max, 256), dim3(256), 0, s, d);
     launch_scan(s, {{d.cmd_is_pub, d.cmd_pub_rank}, {d.cmd_is_ack, d.cmd_ack_rank}}, &d.ctr->n_cmds,
                 d.cmd_max, 4);
     hipLaunchKernelGGL(k_decode, blocks(d.cmd_max, 256), dim3(256), 0, s, d);
@@ -899,7 +898,6 @@ class Engine {
                 &d.tot[TS_RANGE_HI], d.pub_cap, 0, &d.tot[TS_RANGE_LO]);
     hipLaunchKernelGGL(k_route<1>, wave_blocks(nmax), dim3(256), 0, s, d);
     hipLaunchKernelGGL(k_store, wave_blocks(nmax), dim3(256), 0, s, d);
-    hipLaunchKernelGGL(k_live_add, blocks(nmax, 256), dim3(256), 0, s, d);
   }
 
   // serialise publishes with remote owners into the per-destination send buffers
@@ -925,27 +923,29 @@ class Engine {
     u32* pk[2] = {d.pair_k[0], d.pair_k[1]};
     u32* pv[2] = {d.pair_v[0], d.pair_v[1]};
     u32 psrc = radix_sort(s, pk, pv, &d.tot[TS_PAIR_N], d.pair_max, d.q_bits + d.rank_bits);
-    hipLaunchKernelGGL(k_qfirst, blocks(d.pair_max, 256), dim3(256), 0, s, d, psrc);
-    hipLaunchKernelGGL(k_enqueue, blocks(d.pair_max, 256), dim3(256), 0, s, d, psrc);
-    hipLaunchKernelGGL(k_acks, blocks(d.ack_max, 256), dim3(256), 0, s, d);
+    const u32 pbits = d.q_bits + d.rank_bits;
+    const u32 hs_ntiles = pbits <= 8 ? ceil_div(d.pair_max, SORT_TILE) : 0;   // single pass: starts from hist_scan
+    if (!hs_ntiles) hipLaunchKernelGGL(k_qfirst, blocks(d.pair_max, 256), dim3(256), 0, s, d, psrc);
+    hipLaunchKernelGGL(k_enqueue, blocks(d.pair_max, 256), dim3(256), 0, s, d, psrc, hs_ntiles);
     hipLaunchKernelGGL(k_chan_advance, blocks((u64)nch * 64, 256), dim3(256), 0, s, d);
     // requeued deliveries go back in front of their queues' heads before this step's
     // dispatch, in queue-offset order (QueueEntity.scala:415-446)
     hipLaunchKernelGGL(k_requeue, dim3(d.q_max), dim3(256), 0, s, d);
-    hipLaunchKernelGGL(k_requeue_compact, dim3(1), dim3(1024), 0, s, d);
     hipLaunchKernelGGL(k_dequeue, dim3(d.q_max), dim3(256), 0, s, d);
     hipLaunchKernelGGL(k_runs, dim3(1), dim3(1024), 0, s, d);
     hipLaunchKernelGGL(k_dv_write, blocks(d.deliv_max, 256), dim3(256), 0, s, d);
     launch_scan(s, {{d.dv_size, d.dv_off}}, &d.ctr->n_deliv, d.deliv_max, 6);
-    hipLaunchKernelGGL(k_conn_sizes, blocks(d.c_max, 256), dim3(256), 0, s, d);
-    launch_scan(s, {{d.conn_total, d.conn_base}}, nullptr, d.c_max, 7);
-    hipLaunchKernelGGL(k_conn_out, blocks(d.c_max, 256), dim3(256), 0, s, d);
-    hipLaunchKernelGGL(k_render_returns, blocks((u64)d.pub_max * 64, 256), dim3(256), 0, s, d);
-    hipLaunchKernelGGL(k_render_confirms, blocks(d.c_max, 256), dim3(256), 0, s, d);
+    if (d.c_max <= CONN_LAYOUT_MAX) {
+      hipLaunchKernelGGL(k_conn_layout, dim3(1), dim3(1024), 0, s, d);
+    } else {
+      hipLaunchKernelGGL(k_conn_sizes, blocks(d.c_max, 256), dim3(256), 0, s, d);
+      launch_scan(s, {{d.conn_total, d.conn_base}}, nullptr, d.c_max, 7);
+      hipLaunchKernelGGL(k_conn_out, blocks(d.c_max, 256), dim3(256), 0, s, d);
+    }
+    hipLaunchKernelGGL(k_render_rc, dim3(RC_RET_BLOCKS + ceil_div(d.c_max, 256)), dim3(256), 0, s, d);
     hipLaunchKernelGGL(k_render_deliv, blocks((u64)d.deliv_max * 64, 256), dim3(256), 0, s, d);
     u64 pn = d.deliv_max > d.c_max ? d.deliv_max : d.c_max;
     hipLaunchKernelGGL(k_post, blocks(pn, 256), dim3(256), 0, s, d);
-    hipLaunchKernelGGL(k_post2, blocks(d.c_max, 256), dim3(256), 0, s, d);
     if (d.persist) {
       hipLaunchKernelGGL(k_persist_size, blocks(d.persist_max, 256), dim3(256), 0, s, d);
       launch_scan(s, {{d.ps_size, d.ps_off}}, &d.ctr->n_persist, d.persist_max, TS_PERSIST);
