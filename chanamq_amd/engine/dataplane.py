@@ -59,6 +59,7 @@ class GpuDataPlane(ControlState):
         self._egress = [self.eng.host_view(f"egress_host{e}") for e in range(i["egress_slots"])]
         self._pin = [None, None]
         self.exchanger = exchanger
+        self._get_consumed = []   # store records of Basic.Get, emitted with the next step's
         self._pending = None
         self.lag = False
         if world > 1:
@@ -326,12 +327,33 @@ class GpuDataPlane(ControlState):
 
     def take_consumed(self):
         """[(msg_id, q, qpos, kind)] of persistent messages that left durable queues."""
+        out, self._get_consumed = self._get_consumed, []
         c = self.last_counters
         n = min(c["n_consumed"], self.info["persist_max"])
         if not n:
-            return []
+            return out
         recs = self.eng.host_view(f"consumed{self._last_parity}")[:n * CONSUMED_REC.itemsize].view(CONSUMED_REC)
-        return [(int(r["msg_id"]), int(r["q"]), int(r["qpos"]), int(r["kind"])) for r in recs]
+        return out + [(int(r["msg_id"]), int(r["q"]), int(r["qpos"]), int(r["kind"])) for r in recs]
+
+    def basic_get(self, conn, ch, q, no_ack, now_ms=None):
+        """Basic.Get between steps (k_basic_get): the head of queue slot ``q`` after the
+        TTL skip, with the channel's next delivery tag.  Returns (GetOk + header + body
+        frames | None when empty, ready messages left).  Reference FrameStage.scala:1199-1229."""
+        now = int(time.time() * 1000) if now_ms is None else int(now_ms)
+        s = self.chslot(conn, ch)
+        while True:
+            st, cnt, frames, tag, mid, qpos, persist, exp = self.eng.basic_get(q, s, int(bool(no_ack)), now)
+            self._get_consumed.extend((int(m), int(qq), int(qp), 1) for m, qq, qp in exp)
+            if st != 2:   # GET_RETRY: 64 expired entries skipped, more at the head
+                break
+        if st == 1:
+            if persist:
+                self._get_consumed.append((int(mid), q, int(qpos), 0 if no_ack else 3))
+            return bytes(frames), int(cnt)
+        if st in (3, 4):
+            raise ControlError(C.RESOURCE_ERROR, "basic.get: " + ("message exceeds the get buffer" if st == 3
+                                                                 else "channel delivery window full"), 60, 70)
+        return None, int(cnt)
 
     def restore(self, items, now_ms=None):
         """Recovery: enqueue stored messages into their queues in the given order.

@@ -141,6 +141,44 @@ class GoldenDataPlane(ControlState):
         if c is not None:
             c.paused = False
 
+    def basic_get(self, conn, ch, q, no_ack, now_ms=0):
+        """Basic.Get between steps: spec of k_basic_get (dataplane.hip)."""
+        ring = self.ring[q]
+        while ring and ring[0][2] and ring[0][2] <= now_ms:
+            self._consumed(ring[0][0], q, self.qpos_head[q], 1)
+            self._release(ring.pop(0)[0])
+            self.qpos_head[q] += 1
+        if not ring:
+            return None, 0
+        s = self.chslot(conn, ch)
+        st = self.ch[s]
+        if st["win"] >= self.ucap:
+            from .control import ControlError
+            raise ControlError(C.RESOURCE_ERROR, "basic.get: channel delivery window full", 60, 70)
+        msg, red, exp = ring.pop(0)
+        qpos = self.qpos_head[q]
+        self.qpos_head[q] += 1
+        tag = st["next_tag"]
+        st["next_tag"] += 1
+        st["win"] += 1
+        st["slots"][tag] = dict(state="done" if no_ack else "pending", msg=msg, q=q, cons=-1, qpos=qpos, expire=exp)
+        if no_ack:
+            self._consumed(msg, q, qpos, 0)
+            self._release(msg)
+        else:
+            st["unacked"] += 1
+            self.cons_unacked[-1] += 1
+            self._consumed(msg, q, qpos, 3)
+        self._mark_dirty(s)
+        fm = self.conns[conn].frame_max
+        mp = (struct.pack(">HHQB", 60, 71, tag, 1 if red else 0) + bytes([len(msg.ex)]) + msg.ex
+              + bytes([len(msg.rk)]) + msg.rk + struct.pack(">I", len(ring)))
+        parts = [_frame(1, st["num"], mp), _frame(2, st["num"], struct.pack(">HHQ", 60, 0, len(msg.body)) + msg.props)]
+        step = fm - 8 if fm else len(msg.body)
+        for i in range(0, len(msg.body), max(step, 1)):
+            parts.append(_frame(3, st["num"], msg.body[i:i + step]))
+        return b"".join(parts), len(ring)
+
     def _mark_dirty(self, s):
         if not self.ch[s]["dirty"]:
             self.ch[s]["dirty"] = True

@@ -13,8 +13,9 @@ scala/chana/mq/amqp/server/engine/FrameStage.scala:319-500).
 The plane can be a ``GpuDataPlane`` (HIP) or a ``GoldenDataPlane`` (CPU executable
 spec, used by the CPU tests of this server).
 
-Not on the GPU path yet (answered with 540 NOT_IMPLEMENTED; the host-path broker in
-csrc/core serves them): Basic.Get, Tx.*, Exchange.Bind/Unbind.
+Basic.Get runs on the device between steps (k_basic_get).  Not on the GPU path yet
+(answered with 540 NOT_IMPLEMENTED; the host-path broker in csrc/core serves them):
+Tx.*, Exchange.Bind/Unbind.
 """
 
 import os
@@ -677,7 +678,18 @@ class GpuBroker:
             p.confirm_select(c.id, ch)
             if not m.nowait:
                 self._send(c, ch, Method("confirm.select_ok"))
-        elif n in ("basic.get", "tx.select", "tx.commit", "tx.rollback", "exchange.bind", "exchange.unbind"):
+        elif n == "basic.get":
+            q = self._queue(vh, m.queue or c.last_queue.get(ch, ""), 60, 70)
+            if q.exclusive_owner not in (-1, c.id):
+                raise ControlError(C.RESOURCE_LOCKED, f"queue '{q.name}' is exclusive to another connection", 60, 70)
+            if q.owner != p.rank:
+                raise ControlError(C.NOT_IMPLEMENTED, "basic.get on a queue owned by another GPU", 60, 70)
+            frames, _ = p.basic_get(c.id, ch, q.slot, m.no_ack, int(time.time() * 1000))
+            if frames is None:
+                self._send(c, ch, Method("basic.get_empty"))
+            else:
+                c.out += frames
+        elif n in ("tx.select", "tx.commit", "tx.rollback", "exchange.bind", "exchange.unbind"):
             raise ControlError(C.NOT_IMPLEMENTED, f"{n} is not served by the GPU data path", m.class_id,
                                m.method_id)
         elif n == "basic.publish":   # publish on a channel the device did not know (closing race)

@@ -146,7 +146,23 @@ def sc_frame_error(dp):
     return [{1: good + bad}]
 
 
+def sc_basic_get(dp):
+    dp.declare_queue(VH, "bg", ttl_ms=0)
+    dp.open_connection(1, VH)
+    dp.open_channel(1, 3)
+    dp.open_connection(2, VH)
+    dp.open_channel(2, 1)
+    s = publish_stream(5, "", lambda i: "bg", 5000, channel=3, seed=12, frame_max=4096)
+    s2 = publish_command(3, "", "bg", b"short-lived", {"expiration": "10"})
+    return [{1: s + s2}, {"__get__": [(2, 1, "bg", True), (2, 1, "bg", False), (2, 1, "bg", False)]},
+            {2: ack_frame(1, 2), "__get__": [(2, 1, "bg", False)]},
+            {2: render_command(1, Method("basic.nack", delivery_tag=3, multiple=False, requeue=True))},
+            {"__get__": [(2, 1, "bg", True), (2, 1, "bg", True), (2, 1, "bg", True), (2, 1, "bg", True)]},
+            {2: ack_frame(1, 0, multiple=True)}, {}]
+
+
 SCENARIOS = {
+    "basic_get": sc_basic_get,
     "direct_split": sc_direct_split,
     "default_exchange": sc_default_exchange,
     "topic": sc_topic,
@@ -170,11 +186,14 @@ def run(dp, steps, now_step_ms=None):
         for c in inp.pop("__unpause__", []):
             dp.unpause(c)
         now = NOW + (now_step_ms or 0) * k
+        gets = []
+        for conn, ch, qn, no_ack in inp.pop("__get__", []):   # Basic.Get between steps
+            gets.append(dp.basic_get(conn, ch, dp.queues[(VH, qn)].slot, no_ack, now_ms=now))
         r = dp.step(inp, now_ms=now)
         if isinstance(r, dict):
             eg, ctrl, ev, segs = r["egress"], r["ctrl"], r["events"], r["segs"]
         else:
             eg, ctrl, ev, segs = r.egress, r.ctrl, r.events, [s[:4] for s in r.segs]
         outs.append(dict(egress=eg, ctrl=sorted(ctrl), events=sorted(ev),
-                         segs=sorted((s[0], s[1], s[2], s[3]) for s in segs)))
+                         segs=sorted((s[0], s[1], s[2], s[3]) for s in segs), gets=gets))
     return outs

@@ -100,3 +100,21 @@ def test_ttl_expiry_drops():
 def test_frame_error_reported():
     g, outs, pc = run_sc("frame_error")
     assert outs[0]["segs"][0][1] & SS_FRAME_ERROR
+
+
+def test_basic_get_semantics():
+    """GetOk tags follow the channel's delivery tags, message-count is what is left, a
+    nacked get comes back redelivered, an expired head is skipped, an empty queue -> None."""
+    g, outs, pc = run_sc("basic_get")
+    gets = [decode(f) if f is not None else None for o in outs for f, _ in o["gets"]]
+    counts = [n for o in outs for _, n in o["gets"]]
+    oks = [x[0] for x in gets if x]
+    assert [c.method.name for c in oks] == ["basic.get_ok"] * len(oks)
+    assert [c.method.delivery_tag for c in oks] == list(range(1, len(oks) + 1))
+    assert len(oks[0].body) == 5000 and oks[0].channel == 1
+    # step 1: no-ack g0, manual g1 (tag 2), manual g2 (tag 3); step 2: ack 2, get g3 (tag 4)
+    # step 3: nack 3 -> requeued in front; step 4: g2 again (redelivered), g4, expired skip, empty
+    assert [c.method.redelivered for c in oks] == [False, False, False, False, True, False]
+    assert counts[:4] == [5, 4, 3, 2]
+    assert gets[-1] is None and gets[-2] is None
+    assert sum(1 for x in gets if x is None) == 2

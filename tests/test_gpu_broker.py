@@ -143,12 +143,46 @@ def test_errors_unknown_exchange_and_unsupported(broker):
     ch2 = p.channel()
     ch2.queue_declare("g")
     with pytest.raises(ConnectionClosed) as e:    # 540 is a connection exception (AMQP 0-9-1)
-        ch2.basic_get("g")
+        ch2.tx_select()
     assert e.value.code == 540
     p.close()
     q = conn(broker)
     q.channel().queue_declare("g", passive=True)   # broker still serving
     q.close()
+
+
+def test_basic_get_ack_nack_and_empty(broker):
+    """Basic.Get on the data path (k_basic_get): GetOk carries the remaining count and the
+    channel's delivery tags; manual-ack gets are acked / requeued like deliveries."""
+    p = conn(broker)
+    ch = p.channel()
+    ch.queue_declare("gq")
+    for i in range(4):
+        ch.basic_publish("", "gq", f"g{i}".encode(), {"delivery_mode": 1})
+    d0 = ch.basic_get("gq", no_ack=True)
+    assert d0.body == b"g0" and d0.method.message_count == 3 and not d0.method.redelivered
+    d1 = ch.basic_get("gq")
+    assert d1.body == b"g1" and d1.method.message_count == 2
+    assert d1.method.delivery_tag == d0.method.delivery_tag + 1
+    ch.basic_ack(d1.method.delivery_tag)
+    d2 = ch.basic_get("gq")
+    assert d2.body == b"g2"
+    ch.basic_nack(d2.method.delivery_tag, requeue=True)
+    d2b = ch.basic_get("gq")
+    assert d2b.body == b"g2" and d2b.method.redelivered
+    ch.basic_reject(d2b.method.delivery_tag, requeue=False)
+    d3 = ch.basic_get("gq", no_ack=True)
+    assert d3.body == b"g3" and d3.method.message_count == 0
+    assert ch.basic_get("gq") is None
+    assert ch.queue_declare("gq", passive=True).message_count == 0
+    # a consumer sees nothing left over from the gets
+    c = conn(broker)
+    cc = c.channel()
+    cc.basic_consume("gq", "after", no_ack=True)
+    ch.basic_publish("", "gq", b"tail")
+    assert [d.body for d in cc.consume_n(1)] == [b"tail"]
+    p.close()
+    c.close()
 
 
 @pytest.fixture(params=["golden", pytest.param("gpu", marks=pytest.mark.gpu)])
