@@ -69,6 +69,7 @@ class Channel:
     prefetch_size: int = 0
     global_: bool = False
     flow: bool = True
+    tx: bool = False            # Tx.Select: publishes / acks held by the host until Tx.Commit
     consumers: dict = field(default_factory=dict)  # tag -> consumer id
 
 
@@ -191,6 +192,10 @@ class ControlState:
 
     def confirm_select(self, conn, ch):
         self.channel(conn, ch).confirm = True
+        self.channel_changed(conn, ch)
+
+    def tx_select(self, conn, ch):
+        self.channel(conn, ch).tx = True
         self.channel_changed(conn, ch)
 
     def qos(self, conn, ch, prefetch_count, prefetch_size=0, global_=False):

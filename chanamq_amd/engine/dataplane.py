@@ -15,19 +15,20 @@ import numpy as np
 from .. import ops
 from ..protocol import constants as C
 from .control import ControlError, ControlState
-from .layout import (CONN_OUT, CONSUMED_REC, CTRL_REC, INVALID, MF_PERSIST, MF_REDELIVERED, MF_RESTORE, PERSIST_HDR,
-                     RDESC, SEG_IN, SEG_OUT, SS_CTRL, chan_hash, direct_key, exch_hash, fnv1a64,
-                     topic_pattern_row)
+from .layout import (CONN_OUT, CONSUMED_REC, CTRL_REC, CTRL_TXBUF, INVALID, MF_PERSIST, MF_REDELIVERED, MF_RESTORE,
+                     PERSIST_HDR, RDESC, SEG_IN, SEG_OUT, SS_CTRL, US_ACKED, US_PENDING, US_REQUEUE, USLOT,
+                     chan_hash, direct_key, exch_hash, fnv1a64, topic_pattern_row)
 
 ONES64 = np.uint64((1 << 64) - 1)
 
 
 class StepResult:
-    __slots__ = ("egress", "ctrl", "events", "segs", "counters", "elapsed")
+    __slots__ = ("egress", "ctrl", "txbuf", "events", "segs", "counters", "elapsed")
 
     def __init__(self):
         self.egress = {}      # conn -> bytes
         self.ctrl = []        # (conn, raw frame bytes of one control command)
+        self.txbuf = []       # (conn, wire position, raw bytes): data commands of Tx channels
         self.events = []      # (conn, code, chslot)
         self.segs = []        # (conn, status, consumed, carry, ncmds, err_off)
         self.counters = {}
@@ -220,7 +221,7 @@ class GpuDataPlane(ControlState):
                             ("ch_pub_cnt", 0, np.uint32), ("ch_prefetch", 0, np.uint32),
                             ("ch_global", 0, np.uint32), ("ch_flow", 1, np.uint32),
                             ("ch_num", chan.ch, np.uint32), ("ch_unacked", 0, np.uint32),
-                            ("ch_win", 0, np.uint32)):
+                            ("ch_win", 0, np.uint32), ("ch_tx", 0, np.uint32)):
             self._up_at(name, v, s, dt)
         self._chmap_row(chan.conn)
 
@@ -231,6 +232,7 @@ class GpuDataPlane(ControlState):
         self._up_at("ch_prefetch", chan.prefetch_count, s, np.uint32)
         self._up_at("ch_global", int(chan.global_), s, np.uint32)
         self._up_at("ch_flow", int(chan.flow), s, np.uint32)
+        self._up_at("ch_tx", int(chan.tx), s, np.uint32)
 
     def channel_closing(self, chan):
         # unacked deliveries of a closing channel go back to their queues (AMQP 0-9-1 §1.8)
@@ -410,6 +412,26 @@ class GpuDataPlane(ControlState):
                 self.eng.upload("ring", raw, base + start * 16)
         return n
 
+    def apply_ack(self, conn, ch, tag, multiple=False, requeue=False, kind="ack"):
+        """Basic.Ack / Nack / Reject applied between steps (Tx.Commit of a transactional
+        channel): the same marks k_decode makes; k_chan_advance resolves them next step."""
+        s = self.chslot(conn, ch)
+        nt = self._u64("ch_next_tag", s)
+        requeue = bool(requeue) and kind != "ack"
+        if tag == 0 and multiple:
+            tag = nt - 1
+        if multiple:
+            name = "ch_req_upto" if requeue else "ch_ack_upto"
+            if tag > self._u64(name, s):
+                self._up_at(name, tag, s, np.uint64)
+        elif self._u64("ch_uhead", s) <= tag < nt:
+            ucap = self.info["ucap"]
+            off = (s * ucap + ((tag - 1) & (ucap - 1))) * USLOT.itemsize
+            st = int(np.frombuffer(self.eng.download("uwin", off, 4), np.uint32)[0])
+            if st == US_PENDING:
+                self._up_at("uwin", US_REQUEUE if requeue else US_ACKED, off // 4, np.uint32)
+        self._mark_dirty(s)
+
     def recover(self, conn, ch):
         """Basic.Recover(requeue): requeue every outstanding delivery of the channel."""
         s = self.chslot(conn, ch)
@@ -542,8 +564,12 @@ class GpuDataPlane(ControlState):
                 if int(rec["off"]) == INVALID:
                     res.events.append((int(rec["conn"]), int(rec["len"]), int(rec["seg"])))
                 else:
-                    o, n = int(rec["off"]), int(rec["len"])
-                    res.ctrl.append((int(rec["conn"]), bytes(io["ctrl"][o:o + n])))
+                    o, n, sg = int(rec["off"]), int(rec["len"]), int(rec["seg"])
+                    if sg & CTRL_TXBUF:
+                        res.txbuf.append((int(rec["conn"]), sg & ~CTRL_TXBUF, bytes(io["ctrl"][o:o + n])))
+                    else:
+                        res.ctrl.append((int(rec["conn"]), bytes(io["ctrl"][o:o + n])))
+            res.txbuf.sort()
         if wait_egress or collect:
             self.eng.egress_wait(p)
         if collect and collect_egress:

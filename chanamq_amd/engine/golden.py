@@ -141,6 +141,23 @@ class GoldenDataPlane(ControlState):
         if c is not None:
             c.paused = False
 
+    def _ack_mark(self, s, tag, multiple, requeue):
+        st = self.ch[s]
+        if tag == 0 and multiple:
+            tag = st["next_tag"] - 1
+        if multiple:
+            key = "req_upto" if requeue else "ack_upto"
+            st[key] = max(st[key], tag)
+        elif st["uhead"] <= tag < st["next_tag"]:
+            sl = st["slots"].get(tag)
+            if sl and sl["state"] == "pending":
+                sl["state"] = "requeue" if requeue else "acked"
+        self._mark_dirty(s)
+
+    def apply_ack(self, conn, ch, tag, multiple=False, requeue=False, kind="ack"):
+        """Ack / Nack / Reject between steps (Tx.Commit), like GpuDataPlane.apply_ack."""
+        self._ack_mark(self.chslot(conn, ch), tag, multiple, bool(requeue) and kind != "ack")
+
     def basic_get(self, conn, ch, q, no_ack, now_ms=0):
         """Basic.Get between steps: spec of k_basic_get (dataplane.hip)."""
         ring = self.ring[q]
@@ -411,7 +428,7 @@ class GoldenDataPlane(ControlState):
         inputs = inputs or {}
         self.counters = defaultdict(int)
         cnt = self.counters
-        out = {"egress": {}, "ctrl": [], "events": [], "segs": []}
+        out = {"egress": {}, "ctrl": [], "txbuf": [], "events": [], "segs": []}
         conns = set(inputs)
         for c, cl in self.carry.items():
             if cl and c in self.conns and not self.conns[c].paused:
@@ -424,9 +441,12 @@ class GoldenDataPlane(ControlState):
                 out["segs"].append((conn, 1, 0, len(data)))
                 continue
             cmds, consumed, status = self._scan(conn, data)
+            chans = self.conns[conn].channels
             for cmd in cmds:
                 cmd["conn"] = conn
-                if cmd["kind"] == "publish":
+                if cmd["kind"] != "control" and chans[cmd["ch"]].tx:   # held until Tx.Commit
+                    out["txbuf"].append((conn, cmd["m"][0] - 7, cmd["raw"]))
+                elif cmd["kind"] == "publish":
                     pubs.append((cmd, data))
                 elif cmd["kind"] in ("ack", "reject", "nack"):
                     acks.append((cmd, data))
@@ -458,24 +478,13 @@ class GoldenDataPlane(ControlState):
             self._import(records, now_ms)
         # ---- acks
         for cmd, data in acks:
-            s = cmd["chslot"]
-            st = self.ch[s]
             o = cmd["m"][0] + 4
             tag = struct.unpack_from(">Q", data, o)[0]
             bits = data[o + 8]
             kind = cmd["kind"]
             multiple = bool(bits & 1) if kind != "reject" else False
             requeue = (bits & 1) if kind == "reject" else ((bits >> 1) & 1 if kind == "nack" else 0)
-            if tag == 0 and multiple:
-                tag = st["next_tag"] - 1
-            if multiple:
-                key = "req_upto" if requeue else "ack_upto"
-                st[key] = max(st[key], tag)
-            elif st["uhead"] <= tag < st["next_tag"]:
-                sl = st["slots"].get(tag)
-                if sl and sl["state"] == "pending":
-                    sl["state"] = "requeue" if requeue else "acked"
-            self._mark_dirty(s)
+            self._ack_mark(cmd["chslot"], tag, multiple, requeue)
             cnt["n_acked"] += 1
         # ---- window advance (k_chan_advance)
         dirty, self.dirty = self.dirty, []

@@ -24,7 +24,13 @@ PERSIST_HDR = np.dtype([("msg_id", "<i8"), ("ts_ms", "<i8"), ("qpos", "<u8"), ("
 CONSUMED_REC = np.dtype([("msg_id", "<i8"), ("qpos", "<u8"), ("q", "<u4"), ("kind", "<u4"), ("pad", "<u4", 2)])
 assert PERSIST_HDR.itemsize == 48 and CONSUMED_REC.itemsize == 32
 
-STRUCT_SIZES = {"SegIn": 16, "SegOut": 32, "CtrlRec": 16, "ConnOut": 8, "StepIn": 64, "RDesc": 64}
+# per-channel unacked window slot (dp_common.h USlot)
+USLOT = np.dtype([("state", "<u4"), ("msg", "<u4"), ("q", "<u4"), ("cons", "<u4"), ("qpos", "<u8"),
+                  ("expire_ms", "<i8")])
+US_FREE, US_PENDING, US_ACKED, US_REQUEUE, US_DONE = 0, 1, 2, 3, 4
+CTRL_TXBUF = 0x80000000     # CtrlRec.seg: data command of a transactional channel (low bits = position)
+
+STRUCT_SIZES = {"SegIn": 16, "SegOut": 32, "CtrlRec": 16, "ConnOut": 8, "StepIn": 64, "RDesc": 64, "USlot": 32}
 assert RDESC.itemsize == 64
 
 # SegOut.status bits

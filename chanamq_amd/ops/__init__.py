@@ -46,7 +46,7 @@ def build(force=False, verbose=False):
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
     inc = [f"-I{pybind11.get_include()}", f"-I{sysconfig.get_paths()['include']}", f"-I{_SRC}"]
     cmd = [hipcc, "--offload-arch=gfx950", "-O3", "-std=c++17", "-shared", "-fPIC", *inc,
-           os.path.join(_SRC, "engine.hip"), "-o", EXT_PATH + ".tmp", "-L/opt/rocm/lib", "-lhsa-runtime64"]
+           os.path.join(_SRC, "engine.hip"), "-o", EXT_PATH + ".tmp", "-L/opt/rocm/lib", "-lhsa-runtime64", "-lrocprofiler-sdk-roctx"]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)

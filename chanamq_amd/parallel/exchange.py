@@ -23,6 +23,15 @@ import torch
 from ..engine.layout import RDESC
 
 REC = RDESC.itemsize
+_RT = []
+
+
+def _roctx():
+    """The data-plane extension's roctx hooks when it is already loaded (GPU runs), else None."""
+    if not _RT:
+        import sys
+        _RT.append(sys.modules.get("chanamq_amd.ops._dataplane"))
+    return _RT[0]
 
 
 class Exchanger:
@@ -54,6 +63,16 @@ class Exchanger:
         """``send_counts`` = [n_0..n_{W-1}, b_0..b_{W-1}] (logical ranks) -> received
         [n.., b..] by source.  Tensors are flat uint8 (records: 64 bytes each).  Traffic
         for ranks that left the group is dropped (its owner is gone; at-most-once)."""
+        rt = _roctx()
+        if rt is not None:
+            rt.roctx_push("chanamq.X1.all_to_all")
+        try:
+            return self._exchange(send_counts, send_desc, send_pay, recv_desc, recv_pay)
+        finally:
+            if rt is not None:
+                rt.roctx_pop()
+
+    def _exchange(self, send_counts, send_desc, send_pay, recv_desc, recv_pay):
         W = self.world
         live = set(self.comm.members)
         n = [send_counts[r] if r in live else 0 for r in range(W)]

@@ -13,9 +13,11 @@ scala/chana/mq/amqp/server/engine/FrameStage.scala:319-500).
 The plane can be a ``GpuDataPlane`` (HIP) or a ``GoldenDataPlane`` (CPU executable
 spec, used by the CPU tests of this server).
 
-Basic.Get runs on the device between steps (k_basic_get).  Not on the GPU path yet
-(answered with 540 NOT_IMPLEMENTED; the host-path broker in csrc/core serves them):
-Tx.*, Exchange.Bind/Unbind.
+Basic.Get runs on the device between steps (k_basic_get).  Transactions: on a Tx
+channel the device hands publishes / acks to the host instead of applying them
+(CK_TXBUF); Tx.Commit applies the acks between steps and injects the publishes through a
+pseudo-connection in the next step, Tx.Rollback drops them.  Not on the GPU path yet
+(540 NOT_IMPLEMENTED; the host-path broker in csrc/core serves it): Exchange.Bind/Unbind.
 """
 
 import os
@@ -113,7 +115,12 @@ class GpuBroker:
         self.idle_step_s = idle_step_ms / 1000.0
         self.product, self.version = product, version
         self.conns = {}
-        self._free = list(range(plane.c_max - 1, 0, -1))   # slot 0 unused
+        # slot c_max-1: pseudo-connection through which committed transactions publish
+        self.txc = plane.c_max - 1
+        self._free = list(range(plane.c_max - 2, 0, -1))   # slot 0 unused
+        self._txbuf = {}        # (conn, channel) -> raw data commands held since Tx.Select / last commit
+        self._tx_pending = []   # commits waiting for their injection step: (conn, channel, bytes)
+        self._tx_active = None  # (conn, channel) injected in the current step
         self._sel = selectors.DefaultSelector()
         self._lsock = None
         self._thread = None
@@ -266,6 +273,12 @@ class GpuBroker:
             return self._step(inputs)
         p = self.plane
         now = int(time.time() * 1000)
+        inj = self._tx_begin()
+        if inj:
+            off = (used + 15) & ~15
+            self._pin[off:off + len(inj)] = np.frombuffer(inj, np.uint8)
+            segs = np.concatenate([segs, np.array([(self.txc, len(inj), off)], segs.dtype)])
+            used = off + len(inj)
         if self.node is not None:
             t, results = self.node.step_raw(segs, self._pin.ctypes.data, used, now)
             self._answer(results)
@@ -274,10 +287,15 @@ class GpuBroker:
         res = p.finish(t, collect=True, collect_egress=False)
         self._persist_step()
         eg, co = p.host_egress(t)
+        if co["len"][self.txc]:    # Basic.Return of committed publishes -> their connection
+            o, n = int(co["off"][self.txc]), int(co["len"][self.txc])
+            if self._tx_active is not None and self._tx_active[0] in self.conns:
+                self.gw.send(self._tx_active[0], bytes(eg[o:o + n]))
+            co["len"][self.txc] = 0
         self.gw.send_egress(eg, co.view(np.uint32), p.c_max)
         self._read_backpressure(segs)
         return self._after_step(res.ctrl, res.events, [(s[0], s[1]) for s in res.segs], res.counters,
-                                bool(len(segs)), bool(co["len"].any()))
+                                bool(len(segs)), bool(co["len"].any()), res.txbuf)
 
     # ------------------------------------------------------------------ loop
     def _loop(self):
@@ -436,6 +454,10 @@ class GpuBroker:
 
     # ------------------------------------------------------------------ data-plane step
     def _step(self, inputs):
+        inj = self._tx_begin()
+        if inj:
+            inputs = dict(inputs)
+            inputs[self.txc] = inj
         if self.node is not None:
             res, results = self.node.step(inputs, now_ms=int(time.time() * 1000))
             self._answer(results)
@@ -446,9 +468,16 @@ class GpuBroker:
             egress, ctrl, events, segs, cnt = res["egress"], res["ctrl"], res["events"], res["segs"], \
                 res.get("counters", {})
             seg_status = [(s[0], s[1]) for s in segs]
+            txbuf = res.get("txbuf", [])
         else:
             egress, ctrl, events, cnt = res.egress, res.ctrl, res.events, res.counters
             seg_status = [(s[0], s[1]) for s in res.segs]
+            txbuf = res.txbuf
+        egress = dict(egress)
+        if self.txc in egress:     # Basic.Return of committed publishes -> their connection
+            data = egress.pop(self.txc)
+            if self._tx_active is not None:
+                egress[self._tx_active[0]] = egress.get(self._tx_active[0], b"") + data
         for conn, data in egress.items():
             c = self.conns.get(conn)
             if c is not None and c.state == "open":
@@ -456,9 +485,69 @@ class GpuBroker:
                     self.gw.send(conn, data)
                 else:
                     c.out += data
-        return self._after_step(ctrl, events, seg_status, cnt, bool(inputs), bool(egress))
+        return self._after_step(ctrl, events, seg_status, cnt, bool(inputs), bool(egress), txbuf)
 
-    def _after_step(self, ctrl, events, seg_status, cnt, had_input, had_egress):
+    # ------------------------------------------------------------------ transactions
+    def _tx_begin(self):
+        """Bytes of the next committed transaction's publishes, injected this step through
+        the pseudo-connection ``txc`` (same vhost, channel number and frame-max as the
+        committing connection); its Tx.CommitOk goes out after the step."""
+        self._tx_active = None
+        while self._tx_pending:
+            conn, ch, data = self._tx_pending.pop(0)
+            c = self.conns.get(conn)
+            pc = self.plane.conns.get(conn)
+            if c is None or pc is None or c.state != "open":
+                continue
+            with self.lock:
+                self.plane.close_connection(self.txc)
+                self.plane.open_connection(self.txc, pc.vhost, pc.frame_max)
+                self.plane.open_channel(self.txc, ch)
+            self._tx_active = (conn, ch)
+            return data
+        return b""
+
+    def _tx_end(self):
+        """After the injection step: Tx.CommitOk, and the connection resumes."""
+        if self._tx_active is None:
+            return
+        conn, ch = self._tx_active
+        c = self.conns.get(conn)
+        if c is not None and c.state == "open":
+            self._send(c, ch, Method("tx.commit_ok"))
+            self.plane.unpause(conn)
+
+    def _tx_commit(self, c, ch):
+        """Apply the channel's held acks now (window marks between steps) and queue its
+        publishes for injection; returns "deferred" when CommitOk waits for that step."""
+        held = self._txbuf.get((c.id, ch), [])
+        self._txbuf[(c.id, ch)] = []
+        pubs = []
+        for raw in held:
+            t, _, size = struct.unpack_from(">BHI", raw, 0)
+            cls, mid = struct.unpack_from(">HH", raw, 7)
+            if (cls, mid) == (60, 40):
+                pubs.append(raw)
+                continue
+            m = decode_method(raw[7:7 + size])
+            if m.name == "basic.ack":
+                self.plane.apply_ack(c.id, ch, m.delivery_tag, m.multiple, False, "ack")
+            elif m.name == "basic.nack":
+                self.plane.apply_ack(c.id, ch, m.delivery_tag, m.multiple, m.requeue, "nack")
+            elif m.name == "basic.reject":
+                self.plane.apply_ack(c.id, ch, m.delivery_tag, False, m.requeue, "reject")
+        if not pubs:
+            self._send(c, ch, Method("tx.commit_ok"))
+            return None
+        self._tx_pending.append((c.id, ch, b"".join(pubs)))
+        return "deferred"
+
+    def _after_step(self, ctrl, events, seg_status, cnt, had_input, had_egress, txbuf=()):
+        self._tx_end()
+        for conn, _, raw in txbuf:   # data commands of transactional channels, in wire order
+            ch = struct.unpack_from(">H", raw, 1)[0]
+            if (conn, ch) in self._txbuf:
+                self._txbuf[(conn, ch)].append(raw)
         self._watermarks()
         self.stats["steps"] += 1
         self.stats["published"] += cnt.get("n_pubs", 0)
@@ -557,7 +646,7 @@ class GpuBroker:
         try:
             if self.node is not None and m.name in _REPLICATED_METHODS:
                 return self._replicated(c, ch, m)
-            self._channel_method(c, ch, m)
+            return self._channel_method(c, ch, m)
         except ControlError as e:
             if e.code >= 500 or e.code in (C.CONNECTION_FORCED, C.INVALID_PATH):
                 raise _Hard(e.code, e.text, e.class_id or m.class_id, e.method_id or m.method_id)
@@ -578,6 +667,7 @@ class GpuBroker:
         vh = p.conns[c.id].vhost
         n = m.name
         if n == "channel.close":
+            self._txbuf.pop((c.id, ch), None)
             p.close_channel(c.id, ch)
             self._send(c, ch, Method("channel.close_ok"))
         elif n == "channel.close_ok":
@@ -675,6 +765,8 @@ class GpuBroker:
             if n == "basic.recover":
                 self._send(c, ch, Method("basic.recover_ok"))
         elif n == "confirm.select":
+            if p.channel(c.id, ch).tx:
+                raise ControlError(C.PRECONDITION_FAILED, "cannot switch from tx to confirm mode", 85, 10)
             p.confirm_select(c.id, ch)
             if not m.nowait:
                 self._send(c, ch, Method("confirm.select_ok"))
@@ -689,7 +781,22 @@ class GpuBroker:
                 self._send(c, ch, Method("basic.get_empty"))
             else:
                 c.out += frames
-        elif n in ("tx.select", "tx.commit", "tx.rollback", "exchange.bind", "exchange.unbind"):
+        elif n == "tx.select":
+            if p.channel(c.id, ch).confirm:
+                raise ControlError(C.PRECONDITION_FAILED, "cannot switch from confirm to tx mode", 90, 10)
+            if not p.channel(c.id, ch).tx:
+                p.tx_select(c.id, ch)
+                self._txbuf[(c.id, ch)] = []
+            self._send(c, ch, Method("tx.select_ok"))
+        elif n in ("tx.commit", "tx.rollback"):
+            if not p.channel(c.id, ch).tx:
+                raise ControlError(C.PRECONDITION_FAILED, "channel is not transactional", 90, m.method_id)
+            if n == "tx.rollback":
+                self._txbuf[(c.id, ch)] = []
+                self._send(c, ch, Method("tx.rollback_ok"))
+            else:
+                return self._tx_commit(c, ch)
+        elif n in ("exchange.bind", "exchange.unbind"):
             raise ControlError(C.NOT_IMPLEMENTED, f"{n} is not served by the GPU data path", m.class_id,
                                m.method_id)
         elif n == "basic.publish":   # publish on a channel the device did not know (closing race)

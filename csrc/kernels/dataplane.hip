@@ -697,6 +697,7 @@ __global__ __launch_bounds__(256) void k_frame_scan(DS d) {
       else if (cls == 60 && mid == 90 && chs >= 0) c.kind = CK_REJECT;
       else if (cls == 60 && mid == 120 && chs >= 0) c.kind = CK_NACK;
       else c.kind = CK_CONTROL;
+      if (c.kind != CK_CONTROL && d.ch_tx[chs]) c.kind = CK_TXBUF;   // held by the host until Tx.Commit
       if (cls == 60 && mid == 40) {
         u32 hp = CPOS(f + 1);
         FInfo hi = frame_at(b, hp, L, fmax);
@@ -722,14 +723,15 @@ __global__ __launch_bounds__(256) void k_frame_scan(DS d) {
       // classification for the publish / ack rank scans (fused k_classify)
       d.cmd_is_pub[ci] = c.kind == CK_PUBLISH;
       d.cmd_is_ack[ci] = c.kind == CK_ACK || c.kind == CK_NACK || c.kind == CK_REJECT;
-      if (c.kind == CK_CONTROL) {
+      if (c.kind == CK_CONTROL || c.kind == CK_TXBUF) {
         u32 cbase;
         u32 g = reserve_upto(&d.ctr->ctrl_bytes, c.raw_len, (u32)d.ctrl_cap, &cbase);
         if (g == c.raw_len) {
           for (u32 k = 0; k < c.raw_len; ++k) d.ctrl[cbase + k] = b[p + k];
           u32 ri = atomicAdd(&d.ctr->n_ctrl, 1u);
           CtrlRec rec;
-          rec.conn = conn; rec.off = cbase; rec.len = c.raw_len; rec.seg = s;
+          rec.conn = conn; rec.off = cbase; rec.len = c.raw_len;
+          rec.seg = c.kind == CK_TXBUF ? (CTRL_TXBUF | p) : s;
           if (ri < d.seg_max * 2) d.ctrl_rec[ri] = rec;
         }
       }

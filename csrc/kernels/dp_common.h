@@ -23,7 +23,10 @@ enum : u32 {
   CK_REJECT = 3,    // Basic.Reject (60/90)
   CK_NACK = 4,      // Basic.Nack (60/120)
   CK_CONTROL = 5,   // everything else: bytes go to the host control plane
+  CK_TXBUF = 6,     // publish / ack / nack / reject on a transactional channel: raw bytes
+                    // to the host (buffered until Tx.Commit), connection not paused
 };
+#define CTRL_TXBUF 0x80000000u   // CtrlRec.seg flag: CK_TXBUF record, low bits = wire position
 
 // ---- exchange types (constants.py EX_*)
 enum : u32 { EX_DIRECT = 0, EX_FANOUT = 1, EX_TOPIC = 2, EX_HEADERS = 3 };

@@ -140,6 +140,7 @@ struct DS {
   u32* ch_prefetch;
   u32* ch_global;
   u32* ch_flow;
+  u32* ch_tx;               // transactional channel (Tx.Select): data commands -> CK_TXBUF
   u32* ch_num;              // AMQP channel number of the slot
   u32* ch_unacked;          // outstanding manual-ack deliveries (global prefetch)
   u32* ch_win;              // window slots in use (reserved)

@@ -15,6 +15,7 @@
 
 #include <hsa/hsa.h>
 #include <hsa/hsa_ext_amd.h>
+#include <rocprofiler-sdk-roctx/roctx.h>
 
 #include "dataplane.hip"
 
@@ -37,6 +38,12 @@ struct HostTimer {
   std::chrono::steady_clock::time_point t0;
   explicit HostTimer(double* a) : acc(a), t0(std::chrono::steady_clock::now()) {}
   ~HostTimer() { *acc += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count(); }
+};
+
+// roctx range over a host scope (rocprofv3 --marker-trace): step phases, copies, Get
+struct Range {
+  explicit Range(const char* name) { roctxRangePushA(name); }
+  ~Range() { roctxRangePop(); }
 };
 
 struct Buf {
@@ -298,6 +305,7 @@ class Engine {
     d_.ch_prefetch = (u32*)dev("ch_prefetch", 4ull * nch);
     d_.ch_global = (u32*)dev("ch_global", 4ull * nch);
     d_.ch_flow = (u32*)dev("ch_flow", 4ull * nch);
+    d_.ch_tx = (u32*)dev("ch_tx", 4ull * nch);
     d_.ch_num = (u32*)dev("ch_num", 4ull * nch);
     d_.ch_unacked = (u32*)dev("ch_unacked", 4ull * nch);
     d_.ch_win = (u32*)dev("ch_win", 4ull * nch);
@@ -532,6 +540,7 @@ class Engine {
   int submit(py::buffer segs, u64 payload_ptr, u64 payload_len, i64 now_ms, u64 step, u64 id_ms,
              u32 worker) {
     HostTimer ht(&ht_[0]);
+    Range rg("chanamq.step.submit");
     py::buffer_info si = segs.request();
     size_t sb = (size_t)si.size * si.itemsize;
     u32 nseg = (u32)(sb / sizeof(SegIn));
@@ -682,6 +691,7 @@ class Engine {
   py::tuple basic_get(u32 q, u32 chslot, u32 noack, i64 now_ms) {
     if (inflight_[0] || inflight_[1]) throw std::runtime_error("basic_get() between steps only");
     if (q >= d_.q_max || chslot >= d_.c_max * d_.chpc) throw std::runtime_error("basic_get: bad queue / channel");
+    Range rg("chanamq.basic_get");
     sync();
     hipLaunchKernelGGL(k_basic_get, dim3(1), dim3(64), 0, s_comp_, io_[0], q, chslot, noack, now_ms, get_out_dev_,
                        get_cap_, get_res_dev_);
@@ -727,6 +737,7 @@ class Engine {
 
   void wait_results(int p) {
     HostTimer ht(&ht_[3]);
+    Range rg("chanamq.step.wait_results");
     if (phase_a_[p]) throw std::runtime_error("wait_results: phase B of this sharded step not submitted");
     HIPCHECK(hipEventSynchronize(ev_done_[p]));
     inflight_[p] = false;
@@ -734,6 +745,7 @@ class Engine {
 
   u64 egress_copy(int p) {
     HostTimer ht(&ht_[4]);
+    Range rg("chanamq.K5.egress_d2h");
     const Counters* c = (const Counters*)buf("ctr_host" + std::to_string(p)).ptr;
     u64 n = c->egress_bytes;
     const int e = slot_of_[p];
@@ -877,6 +889,7 @@ class Engine {
 
   // frame scan, command assembly, decode (K1-K5)
   void launch_ingest(hipStream_t s, const DS& d) {
+    Range rg("chanamq.K1-K4.ingest");
     hipLaunchKernelGGL(k_prep, dim3(1), dim3(1024), 0, s, d);
     hipLaunchKernelGGL(k_stage, dim3(d.seg_max, 4), dim3(256), 0, s, d);
     hipLaunchKernelGGL(k_cand, dim3(2048), dim3(256), 0, s, d);
@@ -888,6 +901,7 @@ class Engine {
 
   // route + store the publishes of the current phase range (K6); nmax = range capacity
   void launch_route(hipStream_t s, const DS& d, u32 nmax) {
+    Range rg("chanamq.K6-K13.route_store");
     if (d.tb_max) {
       u64 waves = (u64)((nmax + 15) / 16) * (d.tb_pad / 16);
       hipLaunchKernelGGL(k_topic_mfma, wave_blocks(waves), dim3(256), 0, s, d);
@@ -902,6 +916,7 @@ class Engine {
 
   // serialise publishes with remote owners into the per-destination send buffers
   void launch_pack(hipStream_t s, const DS& d) {
+    Range rg("chanamq.X1.pack");
     hipLaunchKernelGGL(k_pack_count, blocks(d.pub_max, 256), dim3(256), 0, s, d);
     for (u32 r = 0; r < d.world; r += 2) {
       u64 a = (u64)r * d.pub_cap, b = (u64)(r + 1) * d.pub_cap;
@@ -919,6 +934,7 @@ class Engine {
 
   // enqueue, acks, dispatch, render (K7-K11)
   void launch_tail(hipStream_t s, const DS& d) {
+    Range rg("chanamq.K7-K11.tail");
     u32 nch = d.c_max * d.chpc;
     u32* pk[2] = {d.pair_k[0], d.pair_k[1]};
     u32* pv[2] = {d.pair_v[0], d.pair_v[1]};
@@ -964,6 +980,7 @@ class Engine {
 
   // world > 1, after the all-to-all: import, route against local queues, rest of the step
   void launch_phase_b(hipStream_t s, const DS& d) {
+    Range rg("chanamq.X1.import");
     hipLaunchKernelGGL(k_import_prep, dim3(1), dim3(64), 0, s, d);
     hipLaunchKernelGGL(k_import, wave_blocks(d.import_max), dim3(256), 0, s, d);
     launch_route(s, d, d.import_max);
@@ -1057,6 +1074,9 @@ static int device_count() {
 PYBIND11_MODULE(_dataplane, m) {
   m.doc() = "MI355X (gfx950) AMQP data-plane kernels + native step runtime";
   m.def("alloc_pinned", &alloc_pinned, "page-locked host buffer (numpy uint8)");
+  m.def("roctx_push", [](const std::string& n) { roctxRangePushA(n.c_str()); });
+  m.def("roctx_pop", []() { roctxRangePop(); });
+  m.def("roctx_mark", [](const std::string& n) { roctxMarkA(n.c_str()); });
   m.def("device_count", &device_count);
   m.def("create_stream", &create_stream, py::arg("device") = 0);
   m.attr("CAND_MAX") = CAND_MAX;

@@ -161,7 +161,26 @@ def sc_basic_get(dp):
             {2: ack_frame(1, 0, multiple=True)}, {}]
 
 
+def sc_tx_hold(dp):
+    dp.declare_queue(VH, "txh")
+    dp.open_connection(1, VH)
+    dp.open_channel(1, 1)
+    dp.open_channel(1, 2)
+    dp.tx_select(1, 2)
+    dp.open_connection(2, VH)
+    dp.open_channel(2, 1)
+    dp.consume(2, 1, VH, "txh", "c", no_ack=True)
+    held = [publish_command(2, "", "txh", bytes([i]) * 40) for i in range(3)]
+    live = [publish_command(1, "", "txh", bytes([9 - i]) * 41) for i in range(4)]
+    ack = render_command(2, Method("basic.ack", delivery_tag=1, multiple=False))
+    ctrl = encode_method_frame(2, Method("tx.commit"))
+    s1 = held[0] + live[0] + held[1]
+    s2 = held[2] + ack + live[1] + ctrl + live[2] + live[3]
+    return [{1: s1[:70]}, {1: s1[70:] + s2[:50]}, {1: s2[50:]}, {"__unpause__": [1]}, {}]
+
+
 SCENARIOS = {
+    "tx_hold": sc_tx_hold,
     "basic_get": sc_basic_get,
     "direct_split": sc_direct_split,
     "default_exchange": sc_default_exchange,
@@ -191,9 +210,9 @@ def run(dp, steps, now_step_ms=None):
             gets.append(dp.basic_get(conn, ch, dp.queues[(VH, qn)].slot, no_ack, now_ms=now))
         r = dp.step(inp, now_ms=now)
         if isinstance(r, dict):
-            eg, ctrl, ev, segs = r["egress"], r["ctrl"], r["events"], r["segs"]
+            eg, ctrl, ev, segs, tx = r["egress"], r["ctrl"], r["events"], r["segs"], r.get("txbuf", [])
         else:
-            eg, ctrl, ev, segs = r.egress, r.ctrl, r.events, [s[:4] for s in r.segs]
+            eg, ctrl, ev, segs, tx = r.egress, r.ctrl, r.events, [s[:4] for s in r.segs], r.txbuf
         outs.append(dict(egress=eg, ctrl=sorted(ctrl), events=sorted(ev),
-                         segs=sorted((s[0], s[1], s[2], s[3]) for s in segs), gets=gets))
+                         segs=sorted((s[0], s[1], s[2], s[3]) for s in segs), gets=gets, txbuf=sorted(tx)))
     return outs

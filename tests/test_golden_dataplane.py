@@ -118,3 +118,14 @@ def test_basic_get_semantics():
     assert counts[:4] == [5, 4, 3, 2]
     assert gets[-1] is None and gets[-2] is None
     assert sum(1 for x in gets if x is None) == 2
+
+
+def test_tx_channel_commands_held_not_applied():
+    g, outs, pc = run_sc("tx_hold")
+    held = [raw for o in outs for _, _, raw in o["txbuf"]]
+    assert len(held) == 4                      # 3 publishes + 1 ack of the Tx channel, wire order
+    assert [decode(r)[0].method.name for r in held] == ["basic.publish"] * 3 + ["basic.ack"]
+    d = [c for c in pc[2] if c.method.name == "basic.deliver"]
+    assert len(d) == 4                         # only the non-transactional channel's
+    assert [c.body for c in d] == [bytes([9 - i]) * 41 for i in range(4)]
+    assert any(o["ctrl"] for o in outs)        # tx.commit reached the host and paused the connection

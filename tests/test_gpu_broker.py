@@ -143,7 +143,7 @@ def test_errors_unknown_exchange_and_unsupported(broker):
     ch2 = p.channel()
     ch2.queue_declare("g")
     with pytest.raises(ConnectionClosed) as e:    # 540 is a connection exception (AMQP 0-9-1)
-        ch2.tx_select()
+        ch2.exchange_bind("amq.direct", "amq.fanout", "k")
     assert e.value.code == 540
     p.close()
     q = conn(broker)
@@ -181,6 +181,52 @@ def test_basic_get_ack_nack_and_empty(broker):
     cc.basic_consume("gq", "after", no_ack=True)
     ch.basic_publish("", "gq", b"tail")
     assert [d.body for d in cc.consume_n(1)] == [b"tail"]
+    p.close()
+    c.close()
+
+
+def test_transactions_commit_and_rollback(broker):
+    """Tx on the data path: publishes and acks of a Tx channel take effect at Tx.Commit
+    only (in order), Tx.Rollback drops them; a mandatory unroutable publish is returned
+    at commit."""
+    p = conn(broker)
+    ch = p.channel()
+    ch.queue_declare("txq")
+    c = conn(broker)
+    cc = c.channel()
+    cc.basic_consume("txq", "tc", no_ack=True)
+    ch.tx_select()
+    for i in range(3):
+        ch.basic_publish("", "txq", f"t{i}".encode())
+    ch.basic_publish("", "no-such-queue", b"lost", mandatory=True)
+    assert ch.queue_declare("txq", passive=True).message_count == 0
+    ch.tx_commit()
+    assert [d.body for d in cc.consume_n(3)] == [b"t0", b"t1", b"t2"]
+    p._wait(lambda: (True,) if ch.returns else None, ch, timeout=5)
+    assert ch.returns[0].method.reply_code == 312
+    ch.basic_publish("", "txq", b"dropped")
+    ch.tx_rollback()
+    ch.basic_publish("", "txq", b"t3")
+    ch.tx_commit()
+    assert [d.body for d in cc.consume_n(1)] == [b"t3"]
+    # acks are transactional too: a rolled-back ack leaves the message unacked
+    cc.basic_cancel("tc")
+    w = c.channel()
+    w.basic_qos(prefetch_count=10)
+    w.tx_select()
+    ch.basic_publish("", "txq", b"a0")
+    ch.basic_publish("", "txq", b"a1")
+    ch.tx_commit()
+    w.basic_consume("txq", "wc")
+    got = w.consume_n(2)
+    w.basic_ack(got[1].method.delivery_tag, multiple=True)
+    w.tx_rollback()
+    w.basic_recover(requeue=True)        # nothing was acked: both come back
+    again = w.consume_n(2)
+    assert [d.body for d in again] == [b"a0", b"a1"] and all(d.method.redelivered for d in again)
+    w.basic_ack(again[1].method.delivery_tag, multiple=True)
+    w.tx_commit()
+    assert w.queue_declare("txq", passive=True).message_count == 0
     p.close()
     c.close()
 

@@ -32,6 +32,7 @@ def test_gpu_matches_golden(gpu, name, graph):
         assert a["ctrl"] == b["ctrl"], f"step {k} ctrl"
         assert a["events"] == b["events"], f"step {k} events"
         assert a["gets"] == b["gets"], f"step {k} basic.get"
+        assert a["txbuf"] == b["txbuf"], f"step {k} tx-held commands"
         assert sorted(a["egress"]) == sorted(b["egress"]), f"step {k} egress conns"
         for c in a["egress"]:
             assert a["egress"][c] == b["egress"][c], f"step {k} conn {c} egress differs"
