@@ -17,7 +17,7 @@ from ..protocol import constants as C
 from .control import ControlError, ControlState
 from .layout import (CONN_OUT, CONSUMED_REC, CTRL_REC, CTRL_TXBUF, INVALID, MF_PERSIST, MF_REDELIVERED, MF_RESTORE,
                      PERSIST_HDR, RDESC, SEG_IN, SEG_OUT, SS_CTRL, US_ACKED, US_PENDING, US_REQUEUE, USLOT,
-                     chan_hash, direct_key, exch_hash, fnv1a64, topic_pattern_row)
+                     chan_hash, direct_key, exch_hash, fnv1a64, topic_pattern_row, topic_word_offsets)
 
 ONES64 = np.uint64((1 << 64) - 1)
 
@@ -167,9 +167,11 @@ class GpuDataPlane(ControlState):
         t_flags = np.zeros(tbp, np.uint32)
         t_expect = np.full(tbp, -1, np.int32)
         t_mat = np.zeros((tbp, 256), np.int8)
+        t_woff = np.zeros((tbp, 8), np.uint16)
         for n, (xs, q, k) in enumerate(tb):
             row, exp, fl = topic_pattern_row(k, self.hash_wildcard)
             t_queue[n], t_exch[n], t_flags[n], t_expect[n] = q, xs, fl, exp
+            t_woff[n] = topic_word_offsets(k)
             t_kb_off[n], t_kb_len[n] = len(kpool), len(k)
             kpool += k
             t_mat[n] = row
@@ -179,7 +181,7 @@ class GpuDataPlane(ControlState):
                           ("d_kb_len", d_kb_len), ("d_q_off", d_q_off), ("d_q_n", d_q_n),
                           ("t_queue", t_queue), ("t_exch", t_exch), ("t_kb_off", t_kb_off),
                           ("t_kb_len", t_kb_len), ("t_flags", t_flags), ("t_expect", t_expect),
-                          ("t_mat", t_mat)):
+                          ("t_mat", t_mat), ("t_woff", t_woff)):
             self._up(name, arr)
         if fan_q:
             self._up("fan_q", np.array(fan_q, np.uint32))

@@ -94,11 +94,24 @@ def topic_pattern_row(pattern: bytes, hash_wildcard=True, nwords_max=8):
     if dp_only:
         return row, -1, 1 | (len(words) << 8)
     nonstar = 0
+    star = 0
     for i, w in enumerate(words):
         if w == b"*":
+            star |= 1 << i
             continue
         h = fnv1a32(w)
         bits = (h >> np.arange(32, dtype=np.uint64)) & 1
         row[i * 32:(i + 1) * 32] = np.where(bits == 1, 1, -1).astype(np.int8)
         nonstar += 1
-    return row, 32 * nonstar, (len(words) << 8)
+    return row, 32 * nonstar, (len(words) << 8) | (star << 16)
+
+
+def topic_word_offsets(pattern: bytes, nwords_max=8):
+    """uint16[8]: (offset << 8 | length) of each pattern word (device exact check)."""
+    out = np.zeros(nwords_max, np.uint16)
+    words = split_words_bytes(pattern)
+    off = 0
+    for i, w in enumerate(words[:nwords_max]):
+        out[i] = (off << 8) | (len(w) & 255)
+        off += len(w) + 1
+    return out

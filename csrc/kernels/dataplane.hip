@@ -799,12 +799,14 @@ DEV u32 build_keyvec(const DS& d, const u8* key, u32 len, u32 pi) {
   if (d.tb_max) {
     // 32 int8 lanes per word (+1 / -1 per hash bit), written as two 16-B stores
     uint4* kv = (uint4*)(d.pub_keyvec + (u64)pi * TOPIC_K);
+    u16* kwo = d.pub_kwoff + (u64)pi * TOPIC_WORDS;   // (offset << 8 | length) per word
     u32 off = 0;
     u32 wi = 0;
     if (kw.count) {
       while (wi < TOPIC_WORDS && off <= kw.eff) {
         u32 wl = word_len(key, off, kw.eff);
         u32 h = fnv1a32(key + off, wl);
+        kwo[wi] = (u16)((off << 8) | (wl & 255));
         u32 pk[8];
 #pragma unroll
         for (int g = 0; g < 8; ++g) {
@@ -1205,13 +1207,42 @@ __global__ __launch_bounds__(256) void k_topic_mfma(DS d) {
   }
 }
 
+// exact check behind an MFMA prefilter hit: same word count (checked) and every non-'*'
+// pattern word byte-equal to the key word at its position.  Word offsets are precomputed
+// (host: t_woff, decode: pub_kwoff), so the compares of all words issue together instead
+// of walking both strings byte by byte.
+DEV bool topic_verify_words(const DS& d, const Pub& pb, u32 pidx, u32 t, u32 fl) {
+  const u32 nw = pb.nwords < TOPIC_WORDS ? pb.nwords : TOPIC_WORDS;
+  const u32 star = (fl >> 16) & 0xffu;
+  const u16* pw = d.t_woff + (u64)t * TOPIC_WORDS;
+  const u16* kw = d.pub_kwoff + (u64)pidx * TOPIC_WORDS;
+  const u8* pat = d.kpool + d.t_kb_off[t];
+  const u8* key = d.work + pb.rk_off;
+  u32 diff = 0;
+  for (u32 i = 0; i < nw; ++i) {
+    if ((star >> i) & 1) continue;
+    const u32 pe = pw[i], ke = kw[i];
+    const u32 len = pe & 255;
+    if (len != (ke & 255)) return false;
+    const u8* a = pat + (pe >> 8);
+    const u8* b = key + (ke >> 8);
+    for (u32 k0 = 0; k0 < len; k0 += 8) {
+#pragma unroll
+      for (u32 j = 0; j < 8; ++j)
+        if (k0 + j < len) diff |= (u32)(a[k0 + j] ^ b[k0 + j]);
+    }
+  }
+  return diff == 0;
+}
+
 DEV bool topic_bind_hit(const DS& d, const Pub& pb, u32 pidx, u32 t) {
   u32 fl = d.t_flags[t];
   bool dp_only = fl & 1;
   if (!dp_only) {
-    if ((fl >> 8) != pb.nwords) return false;
+    if (((fl >> 8) & 0xffu) != pb.nwords) return false;
     u16 mw = d.pub_match[(u64)pidx * (d.tb_pad >> 4) + (t >> 4)];
     if (!((mw >> (t & 15)) & 1)) return false;
+    return topic_verify_words(d, pb, pidx, t, fl);
   }
   return topic_match(d.kpool + d.t_kb_off[t], d.t_kb_len[t], d.work + pb.rk_off, pb.rk_len,
                      d.hash_wildcard != 0);
@@ -1789,22 +1820,28 @@ __global__ void k_acks(DS d) {
   atomicAdd(&d.ctr->n_acked, 1u);
 }
 
-// one wave per dirty channel: resolve marks, release/requeue, advance the window head
+// one block (4 waves) per dirty channel: resolve marks, release/requeue, advance the
+// window head over the contiguous run of finished slots, 256 slots per iteration
+DEV void chan_advance_one(const DS& d, u32 ch, u32 tid, u32 lane, u32 w, u32* s_first, u32* s_done);
 __global__ __launch_bounds__(256) void k_chan_advance(DS d) {
-  u32 wv = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  u32 lane = lane_id();
-  u32 nd = *d.n_dirty;
-  if (wv >= nd) return;
-  u32 ch = d.dirty_list[wv];
-  u64 head = d.ch_uhead[ch], nt = d.ch_next_tag[ch];
-  u64 aup = d.ch_ack_upto[ch], rup = d.ch_req_upto[ch];
+  __shared__ u32 s_first[4];
+  __shared__ u32 s_done[4];
+  const u32 tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
+  const u32 nd = *d.n_dirty;
+  for (u32 wv = blockIdx.x; wv < nd; wv += gridDim.x) chan_advance_one(d, d.dirty_list[wv], tid, lane, w, s_first,
+                                                                        s_done);
+}
+
+DEV void chan_advance_one(const DS& d, u32 ch, u32 tid, u32 lane, u32 w, u32* s_first, u32* s_done) {
+  const u64 head = d.ch_uhead[ch], nt = d.ch_next_tag[ch];
+  const u64 aup = d.ch_ack_upto[ch], rup = d.ch_req_upto[ch];
   USlot* win = d.uwin + (u64)ch * (d.ucap_mask + 1);
   bool contiguous = true;
   u64 newhead = head;
-  u32 released = 0, manual_done = 0;
-  for (u64 t0 = head; t0 < nt; t0 += 64) {
-    u64 t = t0 + lane;
-    bool valid = t < nt;
+  u32 manual_done = 0;
+  for (u64 t0 = head; t0 < nt; t0 += 256) {
+    const u64 t = t0 + tid;
+    const bool valid = t < nt;
     u32 st = US_FREE;
     USlot u;
     u.state = US_FREE; u.msg = INVALID; u.q = 0; u.cons = 0; u.qpos = 0; u.expire_ms = 0;
@@ -1814,8 +1851,8 @@ __global__ __launch_bounds__(256) void k_chan_advance(DS d) {
       if (st == US_PENDING && t <= aup) st = US_ACKED;
       if (st == US_PENDING && t <= rup) st = US_REQUEUE;
     }
-    bool acked = valid && st == US_ACKED;
-    bool req = valid && st == US_REQUEUE;
+    const bool acked = valid && st == US_ACKED;
+    const bool req = valid && st == US_REQUEUE;
     // requeue list (one reservation per wave)
     u32 rtot;
     u32 ri = wave_reserve(d.req_n, req, &rtot);
@@ -1833,19 +1870,30 @@ __global__ __launch_bounds__(256) void k_chan_advance(DS d) {
     if (lane == 0 && rtot) atomicAdd(&d.ctr->n_requeue, rtot);
     if (acked || req) st = US_DONE;
     if (valid && st != u.state) win[(t - 1) & d.ucap_mask].state = st;
-    if (contiguous) {
-      u64 notdone = __ballot(valid && st != US_DONE);
-      u64 vm = __ballot(valid);
-      u32 adv = notdone ? __ffsll((unsigned long long)notdone) - 1 : __popcll(vm);
+    if (contiguous) {   // block-uniform
+      // both ballots wave-wide (a ballot inside the lane-0 branch would see one lane)
+      const u64 notdone = __ballot(valid && st != US_DONE);
+      const u32 nvalid = (u32)__popcll(__ballot(valid));
+      if (lane == 0) {
+        s_first[w] = notdone ? (u32)(__ffsll((unsigned long long)notdone) - 1) : 64u;
+        s_done[w] = nvalid;
+      }
+      __syncthreads();
+      u32 adv = 0;
+      bool stop = false;
+      for (u32 k = 0; k < 4 && !stop; ++k) {
+        if (s_first[k] < 64) { adv += s_first[k]; stop = true; }
+        else adv += s_done[k];
+      }
       newhead += adv;
-      released += adv;
-      if (notdone) contiguous = false;
+      if (stop) contiguous = false;
+      __syncthreads();
     }
   }
-  if (lane == 0) {
+  if (lane == 0 && manual_done) atomicSub(&d.ch_unacked[ch], manual_done);
+  if (tid == 0) {
+    atomicSub(&d.ch_win[ch], (u32)(newhead - head));
     d.ch_uhead[ch] = newhead;
-    atomicSub(&d.ch_win[ch], released);
-    if (manual_done) atomicSub(&d.ch_unacked[ch], manual_done);
     d.ch_dirty[ch] = 0;
   }
 }
@@ -2267,27 +2315,26 @@ __global__ __launch_bounds__(256) void k_render_deliv(DS d) {
   u32 taglen = d.cons_tag_len[dv.cons];
   u32 mp = 4 + 1 + taglen + 8 + 1 + 1 + m.ex_len + 1 + m.rk_len;
   u64 dtag = dv.tag;
+  // method frame: scalar fields by lane 0, the variable-length strings (consumer tag,
+  // exchange, routing key) by all lanes in parallel (no serial byte-load chains)
+  const u32 p_tag = 7 + 4 + 1, p_ex = p_tag + taglen + 8 + 1 + 1, p_rk = p_ex + m.ex_len + 1;
   if (lane == 0) {
-    u32 p = 0;
-    p += put_frame_hdr(o + p, 1, chno, mp);
-    wr16(o + p, 60); wr16(o + p + 2, 60); p += 4;
-    o[p++] = (u8)taglen;
-    const u8* tg = d.tpool + d.cons_tag_off[dv.cons];
-    for (u32 k = 0; k < taglen; ++k) o[p + k] = tg[k];
-    p += taglen;
-    wr64(o + p, dtag); p += 8;
-    o[p++] = (dv.flags & 1) ? 1 : 0;
-    o[p++] = m.ex_len;
-    for (u32 k = 0; k < m.ex_len; ++k) o[p + k] = slot[k];
-    p += m.ex_len;
-    o[p++] = m.rk_len;
-    for (u32 k = 0; k < m.rk_len; ++k) o[p + k] = slot[m.ex_len + k];
-    p += m.rk_len;
+    put_frame_hdr(o, 1, chno, mp);
+    wr16(o + 7, 60); wr16(o + 9, 60);
+    o[11] = (u8)taglen;
+    wr64(o + p_tag + taglen, dtag);
+    o[p_tag + taglen + 8] = (dv.flags & 1) ? 1 : 0;
+    o[p_ex - 1] = m.ex_len;
+    o[p_rk - 1] = m.rk_len;
+    u32 p = p_rk + m.rk_len;
     o[p++] = 0xCE;
     p += put_frame_hdr(o + p, 2, chno, 12 + m.props_len);
-    wr16(o + p, 60); wr16(o + p + 2, 0); wr64(o + p + 4, m.body_len); p += 12;
-    (void)p;
+    wr16(o + p, 60); wr16(o + p + 2, 0); wr64(o + p + 4, m.body_len);
   }
+  const u8* tg = d.tpool + d.cons_tag_off[dv.cons];
+  for (u32 k = lane; k < taglen; k += 64) o[p_tag + k] = tg[k];
+  for (u32 k = lane; k < m.ex_len; k += 64) o[p_ex + k] = slot[k];
+  for (u32 k = lane; k < m.rk_len; k += 64) o[p_rk + k] = slot[m.ex_len + k];
   u32 hp = 8 + mp + 7 + 12;
   wave_copy(o + hp, slot + m.ex_len + m.rk_len, m.props_len);
   if (lane == 0) o[hp + m.props_len] = 0xCE;

@@ -83,6 +83,7 @@ struct DS {
   // ---------------- publishes
   Pub* pubs;
   i8* pub_keyvec;           // [pub_max][TOPIC_K]
+  u16* pub_kwoff;           // [pub_max][TOPIC_WORDS] routing-key words: offset << 8 | length
   u16* pub_match;           // [pub_max][tb_pad/16]
   u32* pub_nq;
   u32* pub_qc;              // [pub_max][8] routed queues cached by route pass 0
@@ -118,6 +119,7 @@ struct DS {
   u8* kpool;                // key/pattern bytes
   u32* t_queue; u32* t_exch; u32* t_kb_off; u32* t_kb_len; u32* t_flags; i32* t_expect;
   i8* t_mat;                // [tb_pad][TOPIC_K]
+  u16* t_woff;              // [tb_pad][TOPIC_WORDS] pattern words: offset << 8 | length
 
   // ---------------- queues
   u64* q_ring_off;          // offset into ring pool

@@ -217,6 +217,7 @@ class Engine {
 
     d_.pubs = (Pub*)dev("pubs", sizeof(Pub) * (u64)d_.pub_cap);
     d_.pub_keyvec = (i8*)dev("pub_keyvec", (u64)d_.pub_cap * TOPIC_K + 64);
+    d_.pub_kwoff = (u16*)dev("pub_kwoff", 2ull * TOPIC_WORDS * d_.pub_cap + 64);
     d_.pub_match = (u16*)dev("pub_match", 2ull * d_.pub_cap * (d_.tb_pad / 16) + 64);
     d_.pub_nq = (u32*)dev("pub_nq", 4ull * d_.pub_cap);
     d_.pub_qc = (u32*)dev("pub_qc", 32ull * d_.pub_cap);
@@ -282,6 +283,7 @@ class Engine {
     d_.t_flags = (u32*)dev("t_flags", 4ull * d_.tb_pad);
     d_.t_expect = (i32*)dev("t_expect", 4ull * d_.tb_pad);
     d_.t_mat = (i8*)dev("t_mat", (u64)d_.tb_pad * TOPIC_K + 64);
+    d_.t_woff = (u16*)dev("t_woff", 2ull * TOPIC_WORDS * d_.tb_pad + 64);
 
     d_.q_ring_off = (u64*)dev("q_ring_off", 8ull * d_.q_max);
     d_.q_ring_mask = (u64*)dev("q_ring_mask", 8ull * d_.q_max);
@@ -943,7 +945,7 @@ class Engine {
     const u32 hs_ntiles = pbits <= 8 ? ceil_div(d.pair_max, SORT_TILE) : 0;   // single pass: starts from hist_scan
     if (!hs_ntiles) hipLaunchKernelGGL(k_qfirst, blocks(d.pair_max, 256), dim3(256), 0, s, d, psrc);
     hipLaunchKernelGGL(k_enqueue, blocks(d.pair_max, 256), dim3(256), 0, s, d, psrc, hs_ntiles);
-    hipLaunchKernelGGL(k_chan_advance, blocks((u64)nch * 64, 256), dim3(256), 0, s, d);
+    hipLaunchKernelGGL(k_chan_advance, dim3(nch < 2048 ? nch : 2048), dim3(256), 0, s, d);
     // requeued deliveries go back in front of their queues' heads before this step's
     // dispatch, in queue-offset order (QueueEntity.scala:415-446)
     hipLaunchKernelGGL(k_requeue, dim3(d.q_max), dim3(256), 0, s, d);

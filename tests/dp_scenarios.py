@@ -179,7 +179,21 @@ def sc_tx_hold(dp):
     return [{1: s1[:70]}, {1: s1[70:] + s2[:50]}, {1: s2[50:]}, {"__unpause__": [1]}, {}]
 
 
+def sc_window_wrap(dp):
+    """Auto-ack deliveries over several steps total more than the channel's unacked window
+    (ucap=256 in the test config): the window head must advance over several 64-slot waves
+    per k_chan_advance pass or deliveries stall once the window wraps."""
+    dp.declare_queue(VH, "wq")
+    dp.open_connection(1, VH)
+    dp.open_channel(1, 1)
+    dp.open_connection(2, VH)
+    dp.open_channel(2, 3)
+    dp.consume(2, 3, VH, "wq", "wc", no_ack=True)
+    return [{1: publish_stream(200, "", lambda i: "wq", 16, seed=10 + k)} for k in range(4)] + [{}]
+
+
 SCENARIOS = {
+    "window_wrap": sc_window_wrap,
     "tx_hold": sc_tx_hold,
     "basic_get": sc_basic_get,
     "direct_split": sc_direct_split,
