@@ -948,7 +948,7 @@ class Engine {
     hipLaunchKernelGGL(k_chan_advance, dim3(nch < 2048 ? nch : 2048), dim3(256), 0, s, d);
     // requeued deliveries go back in front of their queues' heads before this step's
     // dispatch, in queue-offset order (QueueEntity.scala:415-446)
-    hipLaunchKernelGGL(k_requeue, dim3(d.q_max), dim3(256), 0, s, d);
+    hipLaunchKernelGGL(k_requeue, dim3(d.q_max < 256 ? d.q_max : 256), dim3(256), 0, s, d);
     hipLaunchKernelGGL(k_dequeue, dim3(d.q_max), dim3(256), 0, s, d);
     hipLaunchKernelGGL(k_runs, dim3(1), dim3(1024), 0, s, d);
     hipLaunchKernelGGL(k_dv_write, blocks(d.deliv_max, 256), dim3(256), 0, s, d);
