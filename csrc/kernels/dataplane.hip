@@ -391,11 +391,13 @@ __global__ __launch_bounds__(256) void k_cand(DS d) {
 
 #define FS_MARK(k) \
   do { if (tid == 0 && d.dbg) d.dbg[(u64)s * 16 + (k)] = __builtin_amdgcn_s_memrealtime(); } while (0)
+constexpr u32 FS_AM_MAX = 8192;  // 128 KB segment; 16 KB of LDS
 __global__ __launch_bounds__(256) void k_frame_scan(DS d) {
   __shared__ u32 cpos[CAND_MAX];
   __shared__ int16_t csucc[CAND_MAX];
   __shared__ u16 chain[CAND_MAX];
   __shared__ u8 claim[CAND_MAX];
+  __shared__ u16 amask[FS_AM_MAX];
   __shared__ u32 sc[8];
   __shared__ u32 sh_m, sh_over, sh_ok, sh_nf, sh_stop, sh_brk;
   __shared__ u32 sh_cmd_base, sh_frag_base, sh_ncmd;
@@ -441,29 +443,39 @@ __global__ __launch_bounds__(256) void k_frame_scan(DS d) {
     const u32 c0 = tid * per;
     const u32 c1 = c0 + per < nm ? c0 + per : nm;
     const u32 lim = L >= 7 ? L - 6 : 0;   // full-header positions are p < lim
+    // pass 1 validates each candidate once and keeps the accepted bits in LDS (amask), so
+    // pass 2 only emits positions instead of re-reading every frame header from HBM;
+    // segments longer than FS_AM_MAX mask words fall back to re-validating
+    const bool use_am = nm <= FS_AM_MAX;
     u32 cnt = 0;
     for (u32 c = c0; c < c1; ++c) {
       u32 mk = d.cmask[m0 + c];
+      u32 acc = 0;
       while (mk) {
         u32 j = __ffs(mk) - 1;
         mk &= mk - 1;
         u32 p = c * 16 + j;
         if (p >= lim) break;
         FInfo f = frame_at(b, p, L, fmax);
-        if (f.valid_hdr && (f.complete || (u64)p + 8 + f.size > L)) ++cnt;
+        if (f.valid_hdr && (f.complete || (u64)p + 8 + f.size > L)) { ++cnt; acc |= 1u << j; }
       }
+      if (use_am) amask[c] = (u16)acc;
     }
     u32 tot;
     u32 off = block_scan<256>(cnt, sc, tot);
     for (u32 c = c0; c < c1; ++c) {
-      u32 mk = d.cmask[m0 + c];
+      u32 mk = use_am ? (u32)amask[c] : (u32)d.cmask[m0 + c];
       while (mk) {
         u32 j = __ffs(mk) - 1;
         mk &= mk - 1;
         u32 p = c * 16 + j;
         if (p >= lim) break;
-        FInfo f = frame_at(b, p, L, fmax);
-        if (f.valid_hdr && (f.complete || (u64)p + 8 + f.size > L)) {
+        bool acc = use_am;
+        if (!use_am) {
+          FInfo f = frame_at(b, p, L, fmax);
+          acc = f.valid_hdr && (f.complete || (u64)p + 8 + f.size > L);
+        }
+        if (acc) {
           if (off < CAND_MAX) cpos[off] = p;
           ++off;
         }
