@@ -411,8 +411,8 @@ class GoldenDataPlane(ControlState):
             by_src[r[0]].append(r)
         for s in range(self.world):
             if s == self.rank:
-                for msg, qs, expire in self._deferred:
-                    self._enqueue(msg, qs, expire, now_ms)
+                for msg, qs, expire, chslot in self._deferred:
+                    self._enqueue(msg, qs, expire, now_ms, chslot)
                 self._deferred = []
             for _, exch, flags, expire, ex, rk, props, body in by_src.get(s, []):
                 x = self.exch_by_slot.get(exch)
@@ -576,7 +576,8 @@ class GoldenDataPlane(ControlState):
                 st["pub_cnt"] = 0
                 last = st["confirm_next"] + n - 1
                 st["confirm_next"] = last + 1
-                parts.append(_frame(1, st["num"], struct.pack(">HHQB", 60, 80, last, 1 if n > 1 else 0)))
+                mid = 120 if st.pop("pub_fail", False) else 80
+                parts.append(_frame(1, st["num"], struct.pack(">HHQB", 60, mid, last, 1 if n > 1 else 0)))
             fm = self.conns[conn].frame_max if conn in self.conns else 131072
             for d in by_conn.get(conn, []):
                 parts.append(self._render_deliver(d, fm))
@@ -658,11 +659,11 @@ class GoldenDataPlane(ControlState):
         tsp = self._prop_fields(props).get("timestamp")
         msg = _Msg(ex, rk, props, body, len(qs), self.step_no, flags, ts=int(tsp) * 1000 if tsp else 0)
         if self.world > 1:   # enqueued in step_b, ordered by source rank (see _import)
-            self._deferred.append((msg, qs, expire))
+            self._deferred.append((msg, qs, expire, s))
         else:
-            self._enqueue(msg, qs, expire, now_ms)
+            self._enqueue(msg, qs, expire, now_ms, s)
 
-    def _enqueue(self, msg, qs, expire, now_ms):
+    def _enqueue(self, msg, qs, expire, now_ms, chslot=None):
         cnt = self.counters
         for q in qs:
             qq = self.queue_by_slot[q]
@@ -670,6 +671,8 @@ class GoldenDataPlane(ControlState):
             if len(ring) >= qq.capacity:
                 cnt["n_ring_full"] += 1
                 self._release(msg)
+                if chslot is not None:   # the publisher gets Basic.Nack for this step's range
+                    self.ch[chslot]["pub_fail"] = True
                 continue
             e = expire
             if qq.ttl_ms > 0:

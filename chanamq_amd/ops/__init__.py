@@ -17,7 +17,7 @@ _ROOT = os.path.dirname(os.path.dirname(_HERE))
 _SRC = os.path.join(_ROOT, "csrc", "kernels")
 _EXT = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
 EXT_PATH = os.path.join(_HERE, "_dataplane" + _EXT)
-SOURCES = ["engine.hip", "dataplane.hip", "dp_state.h", "dp_common.h"]
+SOURCES = ["engine.hip", "dataplane.hip", "dp_state.h", "dp_common.h", "step_abi.h"]
 
 
 def _src_hash():

@@ -1,0 +1,212 @@
+// Native pipelined front end of the GPU broker: sockets -> data-plane steps -> sockets
+// with no Python on the per-step path.
+//
+//   * N IO threads, each with its own edge-triggered epoll set of connections (thread 0
+//     also owns the listener).  Per step they gather, in parallel, every readable data
+//     connection straight from its socket into one pinned ingress arena (FIONREAD-sized
+//     reservations from a shared atomic cursor: one dense buffer, one H2D copy), and
+//     scatter the previous step's rendered egress from the host egress slot to the
+//     sockets (zero-copy unless a socket is full).
+//   * One stepper thread runs the same software pipeline as bench.py: two steps in
+//     flight on the GPU (H2D(t+1) || kernels(t) || D2H(t-1)), the IO phase of step t+1
+//     overlapping the kernels of step t.  It drives the HIP engine through the C table of
+//     step_abi.h (CmqEngineApi), converts step outputs (control commands, tx-held
+//     commands, status errors, persistence records) into events for the control plane.
+//   * The control plane (Python, server/gpu_broker.py) blocks in poll_events(); before it
+//     touches device tables it calls pause(): the stepper finishes the steps in flight,
+//     writes their egress and parks, so control replies are ordered after every earlier
+//     delivery of the connection.
+//   * Persistence write-behind: a step that produced store records is "held": its egress
+//     (with the publisher confirms) waits until the control plane has committed the
+//     records and calls release(); steps keep running meanwhile.
+//
+// Per-connection byte budget: at most carry_cap - device_carry - bytes_in_flight is
+// gathered for a connection, so a paused connection's backlog never overflows the
+// device carry (TCP back-pressure does the rest).
+//
+// Reference counterpart: the per-connection Akka stream of the reference (Amqp.scala:74-111
+// bind, ServerBluePrint.scala:27-43 tick-driven FrameStage), here batched over all
+// connections per step.
+#pragma once
+#include <atomic>
+#include <condition_variable>
+#include <deque>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../kernels/step_abi.h"
+
+namespace cmq {
+
+enum FeEventKind : int {
+  FE_OPEN = 1,      // conn accepted (host mode: its bytes go to the control plane)
+  FE_CLOSED = 2,    // peer closed / socket error / heartbeat timeout; call close() to free the slot
+  FE_HOST = 3,      // host-mode bytes available: take()
+  FE_CTRL = 4,      // control command (raw frames); the device paused the connection
+  FE_TXBUF = 5,     // data command of a transactional channel: a = wire position
+  FE_EVENT = 6,     // device event: a = code (404 unknown exchange, 506 control overflow), b = channel slot
+  FE_STATUS = 7,    // segment error status (SS_FRAME_ERROR / SS_UNEXPECTED / SS_TOO_LARGE): a = status
+  FE_PERSIST = 8,   // store records of step a (data = packed PersistHdr records, data2 = ConsumedRec[]);
+                    // that step's egress is held until release(a)
+  FE_ERROR = 9,     // engine failure (data = message); the stepper stopped
+};
+
+struct FeEvent {
+  int kind = 0;
+  u32 conn = 0;
+  u64 a = 0, b = 0;
+  std::string data, data2;
+};
+
+struct FrontendCfg {
+  std::string host = "127.0.0.1";
+  int port = 0;
+  int io_threads = 4;
+  u64 per_conn_read = 256 << 10;   // max bytes gathered per connection per step
+  double idle_step_ms = 2.0;       // step period with open data connections and no traffic
+  u32 worker = 0;                  // snowflake worker id
+  u32 max_slot = 0;                // connection slots 1..max_slot (default c_max - 2)
+  bool reuseport = false;
+  int sndbuf = 4 << 20, rcvbuf = 4 << 20;
+};
+
+struct FeStats {
+  u64 steps = 0, published = 0, delivered = 0, rx_bytes = 0, tx_bytes = 0, egress_bytes = 0;
+  u64 held_steps = 0, idle_steps = 0, gather_segs = 0;
+  i64 live_bytes = 0;
+  u64 lat_hist[32] = {};
+  double io_phase_s = 0, wait_s = 0, submit_s = 0;
+};
+
+struct FeConn;
+struct FeIo;
+
+class Frontend {
+ public:
+  Frontend(const FrontendCfg& cfg, const CmqEngineApi* api);
+  ~Frontend();
+  int port() const { return port_; }
+  void start();
+  void stop();
+
+  // ---- control-plane API (thread-safe; the bindings release the GIL)
+  std::vector<FeEvent> poll_events(int timeout_ms);
+  std::string take(u32 conn);                           // host-mode bytes received so far
+  void send(u32 conn, const char* data, size_t n);      // append to the connection's output
+  void send_egress(const u8* egress, const ConnOut* co, u32 n_slots);   // a host-run step's egress
+  void set_data_mode(u32 conn, const std::string& leftover);   // bytes now go to the GPU
+  void set_host_mode(u32 conn);                          // bytes go to the control plane again
+  void set_heartbeat(u32 conn, u32 seconds);
+  void close(u32 conn);                                  // flush, close the socket, free the slot
+  void kick(u32 conn);                                   // unpaused: re-present its device carry
+  void pause();                                          // exclusive device access (nests)
+  void resume();
+  void release(u64 step);                                // store commit of steps <= step landed
+  FeStats stats();
+  u64 pending_out() const;
+
+ private:
+  friend struct FeIo;
+  struct Inflight { int p; u64 step; std::vector<std::pair<u32, u32>> segs; };
+  struct Scatter {   // one step's rendered egress, ready to write
+    const u8* egress = nullptr;
+    std::vector<ConnOut> co;
+    std::string own;         // held copy (persistence) or host-run step
+  };
+  struct Held { u64 step; bool needs_commit; Scatter sc; };
+
+  void stepper();
+  void io_loop(int i);
+  void io_phase(std::vector<Scatter*>& scat, bool gather);
+  void finish_oldest(std::deque<Inflight>& inflight);
+  void post(FeEvent&& e);
+  void wake_stepper();
+  void accept_all(FeIo& io);
+  void drop(FeConn& c, bool notify);
+  bool write_some(FeConn& c);   // mu held
+  void scatter_conn(FeConn& c, const u8* data, u32 n);
+  void gather_conn(FeIo& io, FeConn& c, u8* arena, u64 cap);
+  bool check(int rc);
+
+  FrontendCfg cfg_;
+  const CmqEngineApi* api_;
+  int lfd_ = -1, port_ = 0;
+  u32 c_max_ = 0;
+  std::vector<std::unique_ptr<FeConn>> conns_;
+  std::vector<std::unique_ptr<FeIo>> io_;
+  std::mutex free_mu_;
+  std::vector<u32> free_;
+  std::thread stepper_;
+  std::atomic<bool> running_{false};
+
+  // pinned ingress arenas (3: the H2D of step t is done before step t+3 gathers)
+  u8* arena_[3] = {nullptr, nullptr, nullptr};
+  int arena_i_ = 0;
+
+  // IO phase
+  std::mutex ph_mu_;
+  std::condition_variable ph_cv_;
+  std::atomic<u64> ph_id_{0};
+  std::atomic<int> ph_left_{0};
+  std::vector<Scatter*>* ph_scat_ = nullptr;
+  bool ph_gather_ = false;
+  u8* ph_arena_ = nullptr;
+  u64 ph_cap_ = 0;
+  std::atomic<u64> ph_used_{0};
+  std::atomic<u32> ph_nseg_{0};
+
+  // stepper wake-up / pause
+  std::mutex st_mu_;
+  std::condition_variable st_cv_, pause_cv_;
+  bool wake_ = false;
+  int pause_req_ = 0;
+  bool paused_ = false;
+
+  // events to the control plane
+  std::mutex ev_mu_;
+  std::condition_variable ev_cv_;
+  std::deque<FeEvent> events_;
+
+  // persistence write-behind
+  std::deque<Held> held_;
+  std::atomic<u64> released_{0};
+  bool have_released_ = false;
+
+  std::mutex stats_mu_;
+  FeStats stats_;
+  std::atomic<u64> rx_bytes_{0}, tx_bytes_{0};
+  u64 step_no_ = 0;
+  bool failed_ = false;
+};
+
+// CPU stand-in for the HIP engine (tests without a GPU): every segment's bytes come back
+// to the same connection as egress one step later; a segment containing "CTRL" is
+// reported as a control command and pauses the connection like the device does.
+class EchoEngine {
+ public:
+  EchoEngine(u32 c_max, u32 seg_max, u64 ingress_cap, u32 carry_cap);
+  u64 c_api() { return (u64)&api_; }
+  u64 steps = 0;
+
+ private:
+  struct Io {
+    Counters ctr{};
+    std::vector<SegOut> so;
+    std::vector<ConnOut> co;
+    std::vector<CtrlRec> cr;
+    std::string ctrl;
+    std::string egress;
+  };
+  CmqEngineApi api_{};
+  Io io_[2];
+  std::string slot_[3];
+  int slot_of_[2] = {0, 0};
+  std::vector<u8> paused_;
+  u64 seq_ = 0;
+  std::string err_;
+};
+
+}  // namespace cmq

@@ -77,16 +77,29 @@ DEV void block_copy(u8* dst, const u8* src, u32 n, u32 tid, u32 nt) {
   for (u32 i = (nv << 4) + tid; i < n; i += nt) dst[i] = src[i];
 }
 
-// CAS reservation: grant min(want, cap - *p), return old value in *base
+// Saturating reservation for counters that restart at 0 every step (control bytes,
+// delivery slots, egress budget): one atomicAdd and no give-back.  The caller owns
+// [cur, cur + want) and is granted its part below cap, so granted ranges never overlap
+// and the total granted is exactly min(sum of requests, cap) whatever the arrival order.
+// The counter itself may end above cap: every reader clamps.  (A CAS loop serialises
+// ~1000 queue blocks on one L2 line — 2.9 ms per step at 1024 fan-out queues — and an
+// add-then-give-back fast path lets a transient overshoot inflate other threads' bases.)
+DEV u32 reserve_sat(u32* p, u32 want, u32 cap, u32* base) {
+  u32 cur = want ? atomicAdd(p, want) : __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  *base = cur;
+  if (cur >= cap) return 0;
+  return want < cap - cur ? want : cap - cur;
+}
+DEV u64 reserve_sat64(u64* p, u64 want, u64 cap) {
+  u64 cur = atomicAdd((unsigned long long*)p, (unsigned long long)want);
+  if (cur >= cap) return 0;
+  return want < cap - cur ? want : cap - cur;
+}
+
+// exact CAS reservation for counters that persist across steps and are also decremented
+// (per-channel delivery windows): grant min(want, cap - *p).  Contention is per channel.
 DEV u32 reserve_upto(u32* p, u32 want, u32 cap, u32* base) {
-  if (want == 0) { *base = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); return 0; }
-  // fast path: one atomicAdd when the whole request fits.  A CAS loop alone serialises
-  // when ~1000 queue blocks reserve from the same counter (egress budget, delivery
-  // slots): N contenders cost O(N^2) CAS attempts on one L2 line (2.9 ms per step at
-  // 1024 fan-out queues).  An overshoot is given back and retried exactly by CAS.
-  u32 cur = atomicAdd(p, want);
-  if (cur <= cap && want <= cap - cur) { *base = cur; return want; }
-  cur = atomicSub(p, want) - want;
+  u32 cur = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   while (true) {
     u32 avail = cur < cap ? cap - cur : 0;
     u32 g = want < avail ? want : avail;
@@ -395,9 +408,12 @@ constexpr u32 FS_AM_MAX = 8192;  // 128 KB segment; 16 KB of LDS
 __global__ __launch_bounds__(256) void k_frame_scan(DS d) {
   __shared__ u32 cpos[CAND_MAX];
   __shared__ int16_t csucc[CAND_MAX];
-  __shared__ u16 chain[CAND_MAX];
+  // chain (first written in phase c) aliases amask (used only in phase a, which ends on
+  // a __syncthreads): 16 KB less LDS per block, two blocks fit on a CU
+  __shared__ u16 chain_am[CAND_MAX > FS_AM_MAX ? CAND_MAX : FS_AM_MAX];
+  u16* const chain = chain_am;
+  u16* const amask = chain_am;
   __shared__ u8 claim[CAND_MAX];
-  __shared__ u16 amask[FS_AM_MAX];
   __shared__ u32 sc[8];
   __shared__ u32 sh_m, sh_over, sh_ok, sh_nf, sh_stop, sh_brk;
   __shared__ u32 sh_cmd_base, sh_frag_base, sh_ncmd;
@@ -744,15 +760,18 @@ __global__ __launch_bounds__(256) void k_frame_scan(DS d) {
       d.cmd_is_ack[ci] = c.kind == CK_ACK || c.kind == CK_NACK || c.kind == CK_REJECT;
       if (c.kind == CK_CONTROL || c.kind == CK_TXBUF) {
         u32 cbase;
-        u32 g = reserve_upto(&d.ctr->ctrl_bytes, c.raw_len, (u32)d.ctrl_cap, &cbase);
+        u32 g = reserve_sat(&d.ctr->ctrl_bytes, c.raw_len, (u32)d.ctrl_cap, &cbase);
+        u32 ri = atomicAdd(&d.ctr->n_ctrl, 1u);
+        CtrlRec rec;
+        rec.conn = conn;
         if (g == c.raw_len) {
           for (u32 k = 0; k < c.raw_len; ++k) d.ctrl[cbase + k] = b[p + k];
-          u32 ri = atomicAdd(&d.ctr->n_ctrl, 1u);
-          CtrlRec rec;
-          rec.conn = conn; rec.off = cbase; rec.len = c.raw_len;
+          rec.off = cbase; rec.len = c.raw_len;
           rec.seg = c.kind == CK_TXBUF ? (CTRL_TXBUF | p) : s;
-          if (ri < d.seg_max * 2) d.ctrl_rec[ri] = rec;
+        } else {   // control buffer full: an event, the host closes the connection (506)
+          rec.off = INVALID; rec.len = 506; rec.seg = 0;
         }
+        if (ri < d.seg_max * 2) d.ctrl_rec[ri] = rec;
       }
     }
     run += tcnt;
@@ -1519,7 +1538,13 @@ DEV void store_one(const DS& d, u32 p, u32 lane) {
   Pub& pb = d.pubs[p];
   if (d.pub_nq[p] == 0) return;
   u64 base = *d.log_step_base;
-  if (base == INVALID) { if (lane == 0) pb.msg = INVALID; return; }
+  if (base == INVALID) {   // body log / message table full: dropped, confirmed with Basic.Nack
+    if (lane == 0) {
+      pb.msg = INVALID;
+      if (pb.chslot != INVALID) d.ch_pub_fail[pb.chslot] = 1u;
+    }
+    return;
+  }
   u32 rr = d.pub_routed_rank[p];
   u32 msg = d.msg_free[d.tot[8] - 1 - rr];
   u64 off = base + d.pub_slot_off[p];
@@ -1771,6 +1796,7 @@ DEV u32 enqueue_one(const DS& d, u32 src, u32 i, u32 n, PersistRec* pr, u32 hs_n
     }
   } else {
     drop = pb.msg;
+    if (pb.chslot != INVALID) d.ch_pub_fail[pb.chslot] = 1u;   // confirmed with Basic.Nack
   }
   if (last) {
     u64 cnt = rank + 1;
@@ -1943,7 +1969,7 @@ __global__ __launch_bounds__(256) void k_dequeue(DS d) {
   __shared__ u32 g_cons[RUNS_PER_Q];
   __shared__ u32 g_n[RUNS_PER_Q];
   __shared__ u64 s_head;
-  __shared__ u32 s_bytes;
+  __shared__ unsigned long long s_bytes;
   const u32 q = blockIdx.x, tid = threadIdx.x, lane = lane_id();
   if (q >= d.q_max) return;
   if (!d.q_active[q]) {
@@ -2031,49 +2057,41 @@ __global__ __launch_bounds__(256) void k_dequeue(DS d) {
       qp += cnt;
     }
     for (int o = 32; o > 0; o >>= 1) mine += __shfl_xor(mine, o, 64);
-    if (lane == 0 && mine) atomicAdd(&s_bytes, mine);
+    if (lane == 0 && mine) atomicAdd(&s_bytes, (unsigned long long)mine);
   }
   __syncthreads();
   if (tid == 0) {
-    const u32 ecap = (u32)(d.egress_cap > 0xffffffffull ? 0xffffffffu : d.egress_cap);
-    const u32 bytes = s_bytes;
-    u32 bb;
-    u32 gb = reserve_upto(d.egress_budget, bytes, ecap, &bb);
+    const u64 bytes = s_bytes;
+    const u64 gb = reserve_sat64(d.egress_budget, bytes, d.egress_cap);
     if (gb < bytes) {
-      // slow path (egress budget nearly spent): give it back and take, run by run, the
-      // longest prefix of each consumer's run that still fits
-      if (gb) atomicSub(d.egress_budget, gb);
+      // egress budget nearly spent: keep the longest prefix of the queue's granted
+      // entries (in run order) whose frames fit in what this queue was granted
+      u64 left = gb;
       u64 qp = head;
+      bool full = false;
       for (u32 j = 0; j < m; ++j) {
         u32 cnt = g_n[j];
         if (!cnt) continue;
         u32 c = g_cons[j];
         u32 conn = d.cons_ch[c] / d.chpc;
-        u32 rb = 0;
-        for (u32 k = 0; k < cnt; ++k) rb += deliver_size(d, c, d.msgs[ring[(qp + k) & mask].msg], conn);
-        u32 gj = reserve_upto(d.egress_budget, rb, ecap, &bb);
-        u32 keep = cnt;
-        if (gj < rb) {
-          u32 acc = 0;
-          keep = 0;
-          for (u32 k = 0; k < cnt; ++k) {
-            u32 sz = deliver_size(d, c, d.msgs[ring[(qp + k) & mask].msg], conn);
-            if (acc + sz > gj) break;
-            acc += sz;
-            ++keep;
-          }
-          if (gj > acc) atomicSub(d.egress_budget, gj - acc);
-          if (keep < cnt) unreserve(d, c, cnt - keep);
-          g_n[j] = keep;
+        u32 keep = 0;
+        while (!full && keep < cnt) {
+          u32 sz = deliver_size(d, c, d.msgs[ring[(qp + keep) & mask].msg], conn);
+          if (sz > left) { full = true; break; }
+          left -= sz;
+          ++keep;
         }
+        if (keep < cnt) unreserve(d, c, cnt - keep);
+        g_n[j] = keep;
         qp += keep;
       }
     }
-    // (3) delivery slots (capacity), trimmed from the last run backwards
+    // (3) delivery slots (capacity), trimmed from the last run backwards; k_runs
+    // rewrites n_deliv with the exact total of the kept runs
     u32 total = 0;
     for (u32 j = 0; j < m; ++j) total += g_n[j];
     u32 db;
-    u32 gt = reserve_upto(&d.ctr->n_deliv, total, d.deliv_max, &db);
+    u32 gt = reserve_sat(&d.ctr->n_deliv, total, d.deliv_max, &db);
     u32 excess = total - gt;
     for (int j = (int)m - 1; j >= 0 && excess; --j) {
       u32 take = g_n[j] < excess ? g_n[j] : excess;
@@ -2178,7 +2196,10 @@ __global__ __launch_bounds__(1024) void k_runs(DS d) {
     }
     run += all;
   }
-  if (tid == 0) d.tot[TS_NRUNS] = R;
+  if (tid == 0) {
+    d.tot[TS_NRUNS] = R;
+    d.ctr->n_deliv = run;   // the saturating slot counter may have ended above deliv_max
+  }
 }
 
 DEV void wave_consumed(const DS& d, u32 msg, u32 q, u64 qpos, u32 kind, bool valid);
@@ -2370,7 +2391,11 @@ __global__ __launch_bounds__(256) void k_render_deliv(DS d) {
   }
 }
 
-// confirms: one thread per connection writes its channels' coalesced Basic.Ack frames
+// confirms: one thread per connection writes its channels' coalesced confirm frames:
+// Basic.Ack(last, multiple) when every publish of the channel in this step was stored,
+// else Basic.Nack(last, multiple, requeue=0) over the step's whole range — a publisher
+// may resend a nacked message, it never loses an acked one (FrameStage.scala:571-596
+// confirms everything it asked the entities to store; drops are ours: ring full, no memory)
 DEV void render_confirms(const DS& d, u32 c) {
   u32 conf = d.conn_conf_bytes[c];
   u8* o = (u8*)d.in->egress + (u64)d.conn_base[c] + d.conn_ret_bytes[c];
@@ -2378,6 +2403,8 @@ DEV void render_confirms(const DS& d, u32 c) {
   for (u32 l = 0; l < d.chpc; ++l) {
     u32 ch = c * d.chpc + l;
     u32 cnt = d.ch_pub_cnt[ch];
+    const bool fail = d.ch_pub_fail[ch] != 0;
+    if (fail) d.ch_pub_fail[ch] = 0;
     if (!cnt) continue;
     d.ch_pub_cnt[ch] = 0;
     if (!d.ch_confirm[ch]) continue;
@@ -2386,7 +2413,7 @@ DEV void render_confirms(const DS& d, u32 c) {
     u32 chno = d.ch_num[ch];
     if (p + 21 > conf) break;
     put_frame_hdr(o + p, 1, chno, 13);
-    wr16(o + p + 7, 60); wr16(o + p + 9, 80);
+    wr16(o + p + 7, 60); wr16(o + p + 9, fail ? 120 : 80);
     wr64(o + p + 11, last);
     o[p + 19] = cnt > 1 ? 1 : 0;
     o[p + 20] = 0xCE;

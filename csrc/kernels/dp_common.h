@@ -5,13 +5,8 @@
 #include <hip/hip_runtime.h>
 #include <cstdint>
 
-typedef uint8_t u8;
-typedef uint16_t u16;
-typedef uint32_t u32;
-typedef uint64_t u64;
-typedef int32_t i32;
-typedef int8_t i8;
-typedef int64_t i64;
+#include "step_abi.h"
+
 
 #define DEV __device__ __forceinline__
 
@@ -53,11 +48,6 @@ enum : u32 {
 // ---- unacked slot states
 enum : u32 { US_FREE = 0, US_PENDING = 1, US_ACKED = 2, US_REQUEUE = 3, US_DONE = 4 };
 
-struct SegIn {          // host -> device, one per connection with bytes this step
-  u32 conn;
-  u32 len;              // new bytes
-  u64 src;              // offset of the new bytes in the ingress payload
-};
 
 struct StepIn {         // host -> device per step (64 B)
   u32 nseg;
@@ -71,15 +61,6 @@ struct StepIn {         // host -> device per step (64 B)
   u64 pad[2];
 };
 
-struct SegOut {         // device -> host per segment
-  u32 conn;
-  u32 status;
-  u32 consumed;         // bytes of the virtual segment consumed
-  u32 carry;            // carry length after this step
-  u32 ncmds;
-  u32 err_off;          // offset of the first malformed frame
-  u32 pad[2];
-};
 
 struct Cmd {            // one assembled command (device internal)
   u32 conn;
@@ -146,22 +127,6 @@ static_assert(sizeof(RDesc) == 64, "RDesc layout");
 // persistence (durable queue x persistent message): one record per enqueue, packed with
 // the message bytes into the host-mapped persist buffer at the end of the step
 struct PersistRec { u32 msg; u32 q; u64 qpos; i64 expire_ms; };
-struct PersistHdr {     // host-visible header of one packed persist record (48 B)
-  i64 msg_id;
-  i64 ts_ms;
-  u64 qpos;
-  i64 expire_ms;
-  u32 q;
-  u32 body_len;
-  u16 props_len;
-  u8 ex_len, rk_len;
-  u32 size;             // bytes of this record including the header (8-aligned)
-};
-static_assert(sizeof(PersistHdr) == 48, "PersistHdr layout");
-// a persistent message changed state in a durable queue (kind 0 consumed/acked, 1 expired,
-// 2 dropped, 3 delivered awaiting ack, 4 requeued)
-struct ConsumedRec { i64 msg_id; u64 qpos; u32 q; u32 kind; u32 pad[2]; };
-static_assert(sizeof(ConsumedRec) == 32, "ConsumedRec layout");
 
 struct Ack { u32 chslot; u32 kind; u64 tag; u32 multiple; u32 requeue; };
 
@@ -220,22 +185,6 @@ struct USlot {          // per-channel unacked window slot
 
 struct ReqItem { u32 q; u32 msg; u64 qpos; i64 expire_ms; };
 
-struct Counters {       // per-step counters (device -> host)
-  u32 n_cmds, n_frags, n_pubs, n_acks;
-  u32 n_ctrl, ctrl_bytes, n_pairs, n_deliv;
-  u32 egress_bytes, n_returns, n_confirm_frames, n_freed;
-  u32 n_requeue, n_unroutable, n_dropped_nomem, n_expired;
-  u32 n_routed_msgs, n_unknown_exchange, n_ring_full, n_acked;
-  u32 n_persist, n_consumed, persist_used, n_persist_overflow;
-  u32 lat_hist[32];     // deliveries by (deliver_step - publish_step), last bin = overflow
-  u64 log_head, log_tail;
-  u32 msg_free_top, n_live_msgs;
-  i64 live_bytes;       // body-log slot bytes of live messages (exact, unlike head - tail)
-  u32 pad[4];
-};
-
-struct CtrlRec { u32 conn; u32 off; u32 len; u32 seg; };
-
 // Basic.Get result (k_basic_get -> host-mapped); exp[] = persistent messages of durable
 // queues dropped by the TTL skip (their store rows go, like ConsumedRec kind 1)
 #define GET_EXP_MAX 64
@@ -253,7 +202,6 @@ struct GetRes {
   ConsumedRec exp[GET_EXP_MAX];
 };
 
-struct ConnOut { u32 off; u32 len; };
 
 // ---- FNV-1a 64 (host mirror: chanamq_amd/engine/layout.py fnv1a64)
 DEV u64 fnv1a64_dev(const u8* p, u32 n, u64 h = 0xcbf29ce484222325ULL) {

@@ -134,6 +134,7 @@ struct DS {
   // ---------------- channels
   u32* ch_confirm;
   u32* ch_pub_cnt;
+  u32* ch_pub_fail;         // a publish of this step was dropped (ring full / no memory): confirm with Nack
   u64* ch_confirm_next;
   u64* ch_next_tag;
   u64* ch_uhead;
@@ -191,7 +192,7 @@ struct DS {
   u32* hist;                // radix histograms
   u32* hist_scan;
   u32* tot;                 // scan totals [64]
-  u32* egress_budget;       // bytes reserved by dequeue this step
+  u64* egress_budget;       // bytes reserved by dequeue this step (saturating, reserve_sat64)
   u64* dbg;                 // per-segment phase timestamps (s_memrealtime, 100 MHz)
 
   // ---------------- sharding (cross-rank publish exchange; world == 1: unused)

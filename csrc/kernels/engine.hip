@@ -299,6 +299,7 @@ class Engine {
 
     d_.ch_confirm = (u32*)dev("ch_confirm", 4ull * nch);
     d_.ch_pub_cnt = (u32*)dev("ch_pub_cnt", 4ull * nch);
+    d_.ch_pub_fail = (u32*)dev("ch_pub_fail", 4ull * nch);
     d_.ch_confirm_next = (u64*)dev("ch_confirm_next", 8ull * nch);
     d_.ch_next_tag = (u64*)dev("ch_next_tag", 8ull * nch);
     d_.ch_uhead = (u64*)dev("ch_uhead", 8ull * nch);
@@ -368,7 +369,7 @@ class Engine {
       scan_ctl_ = (u32*)dev("scan_ctl", 64);
     }
     d_.tot = (u32*)dev("tot", 4ull * 128);
-    d_.egress_budget = (u32*)dev("egress_budget", 4);
+    d_.egress_budget = (u64*)dev("egress_budget", 8);
     // Basic.Get: rendered frames + result, host-mapped (a stored body never exceeds the
     // carry, which bounds an assembled command)
     get_cap_ = (u64)d_.carry_cap + d_.carry_cap / 64 + 4096;
@@ -384,7 +385,7 @@ class Engine {
       io.seg_out_h = io_[p].seg_out_h; io.conn_out_h = io_[p].conn_out_h; io.ctrl_h = io_[p].ctrl_h;
       io.ctrl_rec_h = io_[p].ctrl_rec_h;
       io.persist_h = io_[p].persist_h; io.crec_h = io_[p].crec_h;
-      io_[p] = io;
+      static_cast<DS&>(io_[p]) = io;
     }
     if (copy_mode_ == 3) init_sdma();
     HIPCHECK(hipStreamCreateWithFlags(&s_comp_, hipStreamNonBlocking));
@@ -541,11 +542,20 @@ class Engine {
   // egress_wait(p) -> egress_host(p) is valid.
   int submit(py::buffer segs, u64 payload_ptr, u64 payload_len, i64 now_ms, u64 step, u64 id_ms,
              u32 worker) {
-    HostTimer ht(&ht_[0]);
-    Range rg("chanamq.step.submit");
     py::buffer_info si = segs.request();
     size_t sb = (size_t)si.size * si.itemsize;
-    u32 nseg = (u32)(sb / sizeof(SegIn));
+    return submit_raw((const SegIn*)si.ptr, (u32)(sb / sizeof(SegIn)), payload_ptr, payload_len, now_ms, id_ms,
+                      worker);
+  }
+
+  // step numbers are the engine's own submit sequence (latency histogram, message
+  // publish step): identical whether Python or the native front end drives the steps
+  int submit_raw(const SegIn* segp, u32 nseg, u64 payload_ptr, u64 payload_len, i64 now_ms, u64 id_ms,
+                 u32 worker) {
+    HostTimer ht(&ht_[0]);
+    Range rg("chanamq.step.submit");
+    const size_t sb = (size_t)nseg * sizeof(SegIn);
+    const u64 step = seq_;
     if (nseg > d_.seg_max) throw std::runtime_error("too many segments");
     if (payload_len > d_.ingress_cap) throw std::runtime_error("ingress payload exceeds ingress_cap");
     int p = (int)(seq_ & 1);
@@ -561,7 +571,7 @@ class Engine {
     const int e = (int)(seq_ % EGRESS_SLOTS);
     in->egress = (u64)egress_dev_[e];
     slot_of_[p] = e;
-    memcpy(stage_segs_[p], si.ptr, sb);
+    if (sb) memcpy(stage_segs_[p], segp, sb);
     HIPCHECK(hipMemcpyAsync((void*)io_[p].in, in, sizeof(StepIn), hipMemcpyHostToDevice, s_h2d_));
     if (sb) HIPCHECK(hipMemcpyAsync((void*)io_[p].segs, stage_segs_[p], sb, hipMemcpyHostToDevice, s_h2d_));
     if (payload_len)
@@ -735,6 +745,70 @@ class Engine {
       if (graph_b_[p]) { HIPCHECK(hipGraphExecDestroy(graph_b_[p])); graph_b_[p] = nullptr; }
     }
     xfer_set_ = true;
+  }
+
+  // ------------------------------------------------------------- native front end
+  // C entry points (step_abi.h) for csrc/core/frontend.cpp: the front end's stepper
+  // thread drives submit / wait_results / egress copies directly, without the GIL.  The
+  // table lives as long as the Engine; the front end is stopped before the Engine dies.
+  u64 c_api() {
+    CmqEngineApi& a = api_;
+    a.abi = CMQ_STEP_ABI;
+    a.c_max = d_.c_max; a.seg_max = d_.seg_max; a.carry_cap = d_.carry_cap;
+    a.persist = d_.persist; a.persist_max = d_.persist_max;
+    a.ingress_cap = d_.ingress_cap; a.ctrl_cap = d_.ctrl_cap;
+    a.eng = this;
+    a.submit = [](void* e, const SegIn* sg, u32 n, const u8* pay, u64 len, i64 now, u32 worker) -> int {
+      return ((Engine*)e)->guard([&] { return ((Engine*)e)->submit_raw(sg, n, (u64)pay, len, now, (u64)now, worker); });
+    };
+    a.wait_results = [](void* e, int p) -> int {
+      return ((Engine*)e)->guard([&] { ((Engine*)e)->wait_results(p); return 0; });
+    };
+    a.egress_slot = [](void* e, int p) -> int { return ((Engine*)e)->egress_slot(p); };
+    a.egress_copy = [](void* e, int p) -> int {
+      return ((Engine*)e)->guard([&] { ((Engine*)e)->egress_copy(p); return 0; });
+    };
+    a.egress_wait_slot = [](void* e, int slot) -> int {
+      return ((Engine*)e)->guard([&] { ((Engine*)e)->egress_wait_slot(slot); return 0; });
+    };
+    a.error = [](void* e) -> const char* { return ((Engine*)e)->err_.c_str(); };
+    a.counters = [](void* e, int p) -> const Counters* { return ((Engine*)e)->io_[p].ctr_host_h; };
+    a.seg_out = [](void* e, int p) -> const SegOut* { return ((Engine*)e)->io_[p].seg_out_hh; };
+    a.conn_out = [](void* e, int p) -> const ConnOut* { return ((Engine*)e)->io_[p].conn_out_hh; };
+    a.ctrl_rec = [](void* e, int p) -> const CtrlRec* { return ((Engine*)e)->io_[p].ctrl_rec_hh; };
+    a.ctrl = [](void* e, int p) -> const u8* { return ((Engine*)e)->io_[p].ctrl_hh; };
+    a.egress_host = [](void* e, int slot) -> const u8* { return ((Engine*)e)->egress_host_[slot]; };
+    a.persist_host = [](void* e, int p) -> const u8* { return ((Engine*)e)->io_[p].persist_hh; };
+    a.consumed_host = [](void* e, int p) -> const ConsumedRec* { return ((Engine*)e)->io_[p].crec_hh; };
+    for (int p = 0; p < 2; ++p) {
+      std::string sfx = std::to_string(p);
+      HostIO& h = io_[p];
+      h.ctr_host_h = (const Counters*)buf("ctr_host" + sfx).ptr;
+      h.seg_out_hh = (const SegOut*)buf("seg_out" + sfx).ptr;
+      h.conn_out_hh = (const ConnOut*)buf("conn_out" + sfx).ptr;
+      h.ctrl_rec_hh = (const CtrlRec*)buf("ctrl_rec" + sfx).ptr;
+      h.ctrl_hh = (const u8*)buf("ctrl" + sfx).ptr;
+      h.persist_hh = d_.persist ? (const u8*)buf("persist" + sfx).ptr : nullptr;
+      h.crec_hh = d_.persist ? (const ConsumedRec*)buf("consumed" + sfx).ptr : nullptr;
+    }
+    return (u64)&api_;
+  }
+
+  template <class F>
+  int guard(F&& f) {
+    try {
+      HIPCHECK(hipSetDevice(device_));   // the caller may be any host thread
+      return f();
+    } catch (std::exception& ex) {
+      err_ = ex.what();
+      return -1;
+    }
+  }
+
+  void egress_wait_slot(int e) {
+    HostTimer ht(&ht_[5]);
+    if (copy_mode_ == 3) { if (sdma_pending_[e]) sdma_wait(e); return; }
+    if (d2h_issued_[e]) HIPCHECK(hipEventSynchronize(ev_d2h_[e]));
   }
 
   void wait_results(int p) {
@@ -1031,7 +1105,18 @@ class Engine {
   std::vector<u32> lag_recv_;
   u64 lag_stream_ = 0;
   bool xfer_set_ = false;
-  DS io_[2];
+  struct HostIO : DS {   // per-parity device view + host addresses of its mapped outputs
+    const Counters* ctr_host_h = nullptr;
+    const SegOut* seg_out_hh = nullptr;
+    const ConnOut* conn_out_hh = nullptr;
+    const CtrlRec* ctrl_rec_hh = nullptr;
+    const u8* ctrl_hh = nullptr;
+    const u8* persist_hh = nullptr;
+    const ConsumedRec* crec_hh = nullptr;
+  };
+  HostIO io_[2];
+  CmqEngineApi api_{};
+  std::string err_;
   u8* egress_dev_[EGRESS_SLOTS] = {};
   u8* egress_host_[EGRESS_SLOTS] = {};
   u8* egress_host_dev_[EGRESS_SLOTS] = {};
@@ -1105,6 +1190,7 @@ PYBIND11_MODULE(_dataplane, m) {
       .def("egress_wait", &Engine::egress_wait)
       .def("egress_slot", &Engine::egress_slot)
       .def("sync", &Engine::sync)
+      .def("c_api", &Engine::c_api)
       .def("counters", &Engine::counters)
       .def("host_times", &Engine::host_times, py::arg("reset") = false);
 }

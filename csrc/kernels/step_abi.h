@@ -1,0 +1,93 @@
+// Host-visible step ABI of the MI355X data plane: the structs the engine exchanges with
+// the host every step, and the C entry points through which the native front end
+// (csrc/core/frontend.cpp, built by g++ into _core) drives the engine (csrc/kernels/
+// engine.hip, built by hipcc into _dataplane) without Python on the per-step path.
+// Plain C++ (no HIP headers): included by both builds.
+#pragma once
+#include <cstdint>
+
+typedef uint8_t u8;
+typedef uint16_t u16;
+typedef uint32_t u32;
+typedef uint64_t u64;
+typedef int32_t i32;
+typedef int8_t i8;
+typedef int64_t i64;
+
+struct SegIn {          // host -> device, one per connection with bytes this step
+  u32 conn;
+  u32 len;              // new bytes
+  u64 src;              // offset of the new bytes in the ingress payload
+};
+
+struct SegOut {         // device -> host per segment
+  u32 conn;
+  u32 status;
+  u32 consumed;         // bytes of the virtual segment consumed
+  u32 carry;            // carry length after this step
+  u32 ncmds;
+  u32 err_off;          // offset of the first malformed frame
+  u32 pad[2];
+};
+
+// persistence: header of one packed persist record in the host-mapped persist buffer
+struct PersistHdr {     // host-visible header of one packed persist record (48 B)
+  i64 msg_id;
+  i64 ts_ms;
+  u64 qpos;
+  i64 expire_ms;
+  u32 q;
+  u32 body_len;
+  u16 props_len;
+  u8 ex_len, rk_len;
+  u32 size;             // bytes of this record including the header (8-aligned)
+};
+static_assert(sizeof(PersistHdr) == 48, "PersistHdr layout");
+
+// a persistent message changed state in a durable queue (kind 0 consumed/acked, 1 expired,
+// 2 dropped, 3 delivered awaiting ack, 4 requeued)
+struct ConsumedRec { i64 msg_id; u64 qpos; u32 q; u32 kind; u32 pad[2]; };
+static_assert(sizeof(ConsumedRec) == 32, "ConsumedRec layout");
+
+struct Counters {       // per-step counters (device -> host)
+  u32 n_cmds, n_frags, n_pubs, n_acks;
+  u32 n_ctrl, ctrl_bytes, n_pairs, n_deliv;
+  u32 egress_bytes, n_returns, n_confirm_frames, n_freed;
+  u32 n_requeue, n_unroutable, n_dropped_nomem, n_expired;
+  u32 n_routed_msgs, n_unknown_exchange, n_ring_full, n_acked;
+  u32 n_persist, n_consumed, persist_used, n_persist_overflow;
+  u32 lat_hist[32];     // deliveries by (deliver_step - publish_step), last bin = overflow
+  u64 log_head, log_tail;
+  u32 msg_free_top, n_live_msgs;
+  i64 live_bytes;       // body-log slot bytes of live messages (exact, unlike head - tail)
+  u32 pad[4];
+};
+
+struct CtrlRec { u32 conn; u32 off; u32 len; u32 seg; };
+
+struct ConnOut { u32 off; u32 len; };
+
+// C entry points of one Engine (engine.hip: Engine::c_api).  All return 0 / a parity on
+// success and -1 on error (message: error()).  Parity p = the double-buffered step IO set
+// of a submitted step; its host-mapped outputs stay valid until the next submit of p.
+#define CMQ_STEP_ABI 1
+struct CmqEngineApi {
+  u32 abi;
+  u32 c_max, seg_max, carry_cap, persist, persist_max;
+  u64 ingress_cap, ctrl_cap;
+  void* eng;
+  int (*submit)(void* eng, const SegIn* segs, u32 nseg, const u8* payload, u64 len, i64 now_ms, u32 worker);
+  int (*wait_results)(void* eng, int p);
+  int (*egress_slot)(void* eng, int p);                  // egress slot of the last step of parity p
+  int (*egress_copy)(void* eng, int p);                  // D2H of that step's rendered bytes
+  int (*egress_wait_slot)(void* eng, int slot);
+  const char* (*error)(void* eng);
+  const Counters* (*counters)(void* eng, int p);
+  const SegOut* (*seg_out)(void* eng, int p);
+  const ConnOut* (*conn_out)(void* eng, int p);
+  const CtrlRec* (*ctrl_rec)(void* eng, int p);
+  const u8* (*ctrl)(void* eng, int p);
+  const u8* (*egress_host)(void* eng, int slot);
+  const u8* (*persist_host)(void* eng, int p);           // packed PersistHdr records (persist=1)
+  const ConsumedRec* (*consumed_host)(void* eng, int p);
+};

@@ -192,7 +192,43 @@ def sc_window_wrap(dp):
     return [{1: publish_stream(200, "", lambda i: "wq", 16, seed=10 + k)} for k in range(4)] + [{}]
 
 
+def sc_confirm_ring_full(dp):
+    """A confirm-mode publisher fills a 16-slot queue with no consumer: the step that
+    overflows the ring confirms its range with Basic.Nack (never an Ack for a dropped
+    message); later steps that store everything are acked again."""
+    dp.declare_exchange(VH, "rx", "direct")
+    dp.declare_queue(VH, "small", capacity=16)
+    dp.declare_queue(VH, "big")
+    dp.bind(VH, "small", "rx", "s")
+    dp.bind(VH, "big", "rx", "b")
+    dp.open_connection(1, VH)
+    dp.open_channel(1, 1)
+    dp.confirm_select(1, 1)
+    dp.open_channel(1, 2)
+    dp.confirm_select(1, 2)
+    s1 = publish_stream(10, "rx", lambda i: "s", 32, seed=21)
+    s2 = publish_stream(10, "rx", lambda i: "s", 32, seed=22)
+    b2 = publish_stream(5, "rx", lambda i: "b", 32, channel=2, seed=23)
+    s3 = publish_stream(3, "rx", lambda i: "b", 32, seed=24)
+    return [{1: s1}, {1: s2 + b2}, {1: s3}, {}]
+
+
+def sc_big_segment(dp):
+    """One connection segment above 128 KB (the frame scan's re-validating path)."""
+    dp.declare_queue(VH, "bs")
+    dp.open_connection(1, VH)
+    dp.open_channel(1, 1)
+    dp.open_connection(2, VH)
+    dp.open_channel(2, 1)
+    dp.consume(2, 1, VH, "bs", "bsc", no_ack=True)
+    s = publish_stream(150, "", lambda i: "bs", 1000, seed=25)
+    assert len(s) > 128 << 10
+    return [{1: s}, {}]
+
+
 SCENARIOS = {
+    "confirm_ring_full": sc_confirm_ring_full,
+    "big_segment": sc_big_segment,
     "window_wrap": sc_window_wrap,
     "tx_hold": sc_tx_hold,
     "basic_get": sc_basic_get,

@@ -129,3 +129,20 @@ def test_tx_channel_commands_held_not_applied():
     assert len(d) == 4                         # only the non-transactional channel's
     assert [c.body for c in d] == [bytes([9 - i]) * 41 for i in range(4)]
     assert any(o["ctrl"] for o in outs)        # tx.commit reached the host and paused the connection
+
+
+def test_ring_full_confirms_with_nack_never_ack():
+    g, outs, pc = run_sc("confirm_ring_full")
+    per_step = [[(c.channel, c.method.name, c.method.delivery_tag, c.method.multiple)
+                 for c in decode(o["egress"].get(1, b""))] for o in outs]
+    assert per_step[0] == [(1, "basic.ack", 10, True)]
+    # step 2: 6 of channel 1's 10 publishes did not fit the 16-slot ring -> Nack over the range
+    assert (1, "basic.nack", 20, True) in per_step[1] and (2, "basic.ack", 5, True) in per_step[1]
+    assert per_step[2] == [(1, "basic.ack", 23, True)]
+    assert g.counters is not None
+
+
+def test_big_segment_delivers_all():
+    g, outs, pc = run_sc("big_segment")
+    d = [c for c in pc[2] if c.method.name == "basic.deliver"]
+    assert len(d) == 150 and all(len(c.body) == 1000 for c in d)
