@@ -1,10 +1,15 @@
 #!/usr/bin/env python3
-"""End-to-end over TCP: the native load generator (csrc/core/loadgen.cpp) against the
-GPU-data-path server (server/gpu_broker.py + GpuDataPlane) on one MI355X.  Unlike
-bench.py (which feeds pre-rendered wire bytes straight into the data plane), this includes
-the Python socket front end, so it measures the full broker as a client sees it.
+"""End-to-end over TCP: the native load generator (csrc/core/loadgen.cpp, epoll threads)
+against the GPU-data-path server (server/gpu_broker.py + GpuDataPlane) on one MI355X.
+Unlike bench.py (pre-rendered wire bytes handed straight to the data plane), this is the
+broker as a client sees it: loopback TCP, the front end, the control plane, the GPU.
 
-python bench/gpu_server_e2e.py [--seconds S] [--out FILE]
+Front ends: ``pipeline`` (native IO threads + stepper, csrc/core/frontend.cpp; swept over
+--io-threads) and ``native`` (round-1 Python step loop over the C++ gateway) for reference.
+Latency = publish->deliver measured by the consumers from the send timestamp carried in
+every message body; ``--paced`` re-runs a spec at a fraction of its measured throughput.
+
+python bench/gpu_server_e2e.py [--seconds S] [--only NAME] [--io-threads 1,2,4,8] [--out FILE]
 """
 
 import argparse
@@ -12,68 +17,110 @@ import json
 import os
 import sys
 import tempfile
+import time
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 from chanamq_amd.broker import load  # noqa: E402
 
 SPECS = {
-    "topic_16q_1KB_auto_ack": dict(producers=4, consumers=16, queues=16, msg_size=1024, auto_ack=True,
-                                   prefetch=5000, exchange_type="topic"),
+    # BASELINE config 2 over TCP: 1 topic exchange, 16 bound queues, 1 KB, auto-ack
+    "config2_topic_16q_1KB_auto_ack": dict(producers=16, consumers=16, queues=16, msg_size=1024, auto_ack=True,
+                                           prefetch=5000, exchange_type="topic"),
+    # BASELINE config 1 shape through the GPU server (the round-1 1P1C starvation case)
     "direct_1p1c_256B": dict(producers=1, consumers=1, msg_size=256, auto_ack=True, prefetch=5000),
-    "direct_4p4c_1KB_manual_ack": dict(producers=4, consumers=4, msg_size=1024, auto_ack=False, prefetch=1000),
-    # BASELINE config 4 shape: durable queue, delivery-mode 2, 4 KB, publisher confirms, manual ack
-    "config4_durable_4KB_confirms": dict(producers=1, consumers=1, msg_size=4096, auto_ack=False, prefetch=1000,
-                                         persistent=True, durable=True, confirm=True),
+    "direct_4p4c_1KB_manual_ack": dict(producers=4, consumers=4, queues=4, msg_size=1024, auto_ack=False,
+                                       prefetch=1000),
+    # BASELINE config 4: durable queues, delivery-mode 2, 4 KB, publisher confirms, manual ack
+    "config4_durable_4KB_confirms": dict(producers=16, consumers=4, queues=4, msg_size=4096, auto_ack=False,
+                                         prefetch=1000, persistent=True, durable=True, confirm=True),
 }
+
+
+def plane_for(spec):
+    from chanamq_amd.engine.dataplane import GpuDataPlane
+    persist = bool(spec.get("persistent"))
+    return GpuDataPlane(c_max=512, chpc=8, q_max=256, cons_max=1024, seg_max=512, cmd_max=1 << 17,
+                        deliv_max=1 << 17, msg_max=1 << 21, ucap=8192, deliver_cap=8192,
+                        ingress_cap=64 << 20, egress_cap=160 << 20, log_bytes=8 << 30, ring_pool=1 << 25,
+                        tb_max=256, default_queue_capacity=1 << 20, persist=int(persist),
+                        persist_max=1 << 16, persist_bytes=512 << 20, carry_cap=1 << 18)
+
+
+def run_one(core, name, spec, io, io_threads, seconds, rate=0.0, lg_threads=8, store_dir=None):
+    from chanamq_amd.server.gpu_broker import GpuBroker
+    persist = bool(spec.get("persistent"))
+    plane = plane_for(spec)
+    store = None
+    if persist:
+        store = core.Store()
+        store.open(store_dir or tempfile.mkdtemp(prefix="cmq-gpu-store-"), True)
+    b = GpuBroker(plane, idle_step_ms=0.5, store=store, io=io, io_threads=io_threads,
+                  per_conn_read=128 << 10).start()
+    t0 = time.time()
+    try:
+        r = core.run_load(dict(port=b.port, seconds=seconds, warmup=1.0, queue=f"e2e.{name}",
+                               exchange=f"e2e.x.{name}", threads=lg_threads, rate=rate, **spec))
+    finally:
+        b.stop()
+        if store is not None:
+            store.close()
+    lc = getattr(plane, "last_counters", {}) or {}
+    st = dict(b.stats)
+    fes = getattr(b, "_fe_stats", None) or {}
+    r.update(name=name, io=io, io_threads=io_threads if io == "pipeline" else 1, loadgen_threads=lg_threads,
+             rate_per_producer=rate, recv_msgs_per_s=r["received"] / r["elapsed"],
+             sent_msgs_per_s=r["sent"] / r["elapsed"], confirmed_per_s=r["confirmed"] / r["elapsed"],
+             wall_s=time.time() - t0, steps=st.get("steps"), spec=spec,
+             front_end={k: fes.get(k) for k in ("steps", "idle_steps", "gather_segs", "io_phase_s", "wait_s",
+                                                "submit_s", "rx_bytes", "tx_bytes", "held_steps")},
+             last_step={k: lc.get(k) for k in ("n_ring_full", "n_dropped_nomem")})
+    del plane
+    return r
 
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--seconds", type=float, default=5.0)
+    ap.add_argument("--seconds", type=float, default=4.0)
     ap.add_argument("--out", default="")
     ap.add_argument("--only", default="")
+    ap.add_argument("--io", default="pipeline", help="comma list of front ends: pipeline,native")
+    ap.add_argument("--io-threads", default="4", help="comma list (pipeline front end)")
+    ap.add_argument("--loadgen-threads", type=int, default=8)
+    ap.add_argument("--paced", type=float, default=0.5,
+                    help="re-run each spec with producers paced at this fraction of the measured rate (0 = off)")
     args = ap.parse_args()
-    import torch
-    from chanamq_amd.engine.dataplane import GpuDataPlane
-    from chanamq_amd.server.gpu_broker import GpuBroker
-    assert torch.cuda.is_available()
+    import torch  # noqa: F401  (HIP runtime up before the first plane)
     core = load()
-    results = {}
+    results = []
     for name, spec in SPECS.items():
         if args.only and args.only not in name:
             continue
-        persist = bool(spec.get("persistent"))
-        plane = GpuDataPlane(c_max=256, chpc=8, q_max=256, cons_max=1024, seg_max=256, cmd_max=1 << 16,
-                             deliv_max=1 << 16, msg_max=1 << 20, ucap=8192, deliver_cap=8192,
-                             ingress_cap=64 << 20, egress_cap=128 << 20, log_bytes=4 << 30, ring_pool=1 << 24,
-                             tb_max=256, default_queue_capacity=1 << 18, persist=int(persist),
-                             persist_max=1 << 15, persist_bytes=256 << 20)
-        store = None
-        if persist:
-            store = core.Store()
-            store.open(tempfile.mkdtemp(prefix="cmq-gpu-store-"), True)
-        b = GpuBroker(plane, idle_step_ms=0.5, store=store).start()
-        try:
-            r = core.run_load(dict(port=b.port, seconds=args.seconds, queue=f"e2e.{name}", exchange=f"e2e.x.{name}",
-                                   **spec))
-        finally:
-            b.stop()
-            if store is not None:
-                store.close()
-        lc = getattr(plane, "last_counters", {}) or {}
-        r.update(name=name, spec=spec, recv_msgs_per_s=r["received"] / r["elapsed"],
-                 sent_msgs_per_s=r["sent"] / r["elapsed"], steps=b.stats["steps"], server=dict(b.stats),
-                 last_step={k: lc.get(k) for k in ("n_pubs", "n_deliv", "n_ring_full", "n_live_msgs", "live_bytes",
-                                                   "n_dropped_nomem", "egress_bytes")})
-        results[name] = r
-        print(json.dumps({k: r[k] for k in ("name", "recv_msgs_per_s", "sent_msgs_per_s", "p50_us", "p99_us",
-                                            "steps", "error", "server", "last_step")}), flush=True)
-        del plane
+        for io in args.io.split(","):
+            for nt in ([int(x) for x in args.io_threads.split(",")] if io == "pipeline" else [1]):
+                r = run_one(core, name, spec, io, nt, args.seconds, lg_threads=args.loadgen_threads)
+                results.append(r)
+                print(json.dumps({k: r[k] for k in ("name", "io", "io_threads", "recv_msgs_per_s", "sent_msgs_per_s",
+                                                    "confirmed_per_s", "p50_us", "p99_us", "error", "front_end")}),
+                      flush=True)
+                if args.paced > 0 and r["recv_msgs_per_s"] > 0 and not r["error"]:
+                    rate = args.paced * r["recv_msgs_per_s"] / max(1, spec.get("producers", 1))
+                    if spec.get("exchange_type") == "fanout":   # deliveries = publishes x queues
+                        rate /= max(1, spec.get("queues", 1))
+                    rp = run_one(core, name, spec, io, nt, args.seconds, rate=rate, lg_threads=args.loadgen_threads)
+                    rp["paced_fraction"] = args.paced
+                    results.append(rp)
+                    print(json.dumps({k: rp[k] for k in ("name", "io", "io_threads", "rate_per_producer",
+                                                         "recv_msgs_per_s", "p50_us", "p95_us", "p99_us",
+                                                         "error")}), flush=True)
     if args.out:
+        import platform
         with open(args.out, "w") as f:
-            json.dump({"meta": {"transport": "loopback TCP", "front_end": "python selectors (1 thread)",
-                                "data_plane": "HIP gfx950"}, "results": results}, f, indent=1)
+            json.dump({"meta": {"transport": "loopback TCP", "data_plane": "HIP gfx950 (1 GPU)",
+                                "host_cpus_visible": os.cpu_count(), "machine": platform.machine(),
+                                "latency": "publish->deliver from the send timestamp in each body (steady clock)",
+                                "seconds": args.seconds, "warmup_s": 1.0},
+                       "results": results}, f, indent=1)
 
 
 if __name__ == "__main__":

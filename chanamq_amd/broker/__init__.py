@@ -12,8 +12,9 @@ _ROOT = os.path.dirname(os.path.dirname(_HERE))
 _SRC = os.path.join(_ROOT, "csrc", "core")
 _EXT = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
 EXT_PATH = os.path.join(_HERE, "_core" + _EXT)
-SOURCES = ["codec.cpp", "store.cpp", "broker.cpp", "loadgen.cpp", "gateway.cpp", "bindings.cpp"]
-HEADERS = ["codec.hpp", "store.hpp", "broker.hpp", "loadgen.hpp", "gateway.hpp"]
+SOURCES = ["codec.cpp", "store.cpp", "broker.cpp", "loadgen.cpp", "gateway.cpp", "frontend.cpp", "bindings.cpp"]
+HEADERS = ["codec.hpp", "store.hpp", "broker.hpp", "loadgen.hpp", "gateway.hpp", "frontend.hpp",
+           "../kernels/step_abi.h"]
 
 
 def _src_hash():

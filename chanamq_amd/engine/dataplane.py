@@ -22,6 +22,30 @@ from .layout import (CONN_OUT, CONSUMED_REC, CTRL_REC, CTRL_TXBUF, INVALID, MF_P
 ONES64 = np.uint64((1 << 64) - 1)
 
 
+def parse_persist(raw):
+    """Packed persist records (PersistHdr + [ex][rk][props][body]) -> [(msg_id, ts_ms, q,
+    qpos, expire_ms, ex, rk, props, body)]."""
+    raw = np.frombuffer(raw, np.uint8) if isinstance(raw, (bytes, bytearray)) else raw
+    out, off = [], 0
+    while off + PERSIST_HDR.itemsize <= len(raw):
+        h = raw[off:off + PERSIST_HDR.itemsize].view(PERSIST_HDR)[0]
+        b = off + PERSIST_HDR.itemsize
+        el, rl, pl, bl = int(h["ex_len"]), int(h["rk_len"]), int(h["props_len"]), int(h["body_len"])
+        data = bytes(raw[b:b + el + rl + pl + bl])
+        out.append((int(h["msg_id"]), int(h["ts_ms"]), int(h["q"]), int(h["qpos"]), int(h["expire_ms"]),
+                    data[:el], data[el:el + rl], data[el + rl:el + rl + pl], data[el + rl + pl:]))
+        if int(h["size"]) <= 0:
+            break
+        off += int(h["size"])
+    return out
+
+
+def parse_consumed(raw):
+    """ConsumedRec[] -> [(msg_id, q, qpos, kind)]."""
+    recs = np.frombuffer(bytes(raw), CONSUMED_REC) if isinstance(raw, (bytes, bytearray)) else raw.view(CONSUMED_REC)
+    return [(int(r["msg_id"]), int(r["q"]), int(r["qpos"]), int(r["kind"])) for r in recs]
+
+
 class StepResult:
     __slots__ = ("egress", "ctrl", "txbuf", "events", "segs", "counters", "elapsed")
 
@@ -318,16 +342,7 @@ class GpuDataPlane(ControlState):
         if c["n_persist_overflow"] or c["n_persist"] > self.info["persist_max"]:
             raise RuntimeError("persist buffer overflow: raise persist_max / persist_bytes")
         raw = self.eng.host_view(f"persist{self._last_parity}")[:c["persist_used"]]
-        out, off = [], 0
-        for _ in range(n):
-            h = raw[off:off + PERSIST_HDR.itemsize].view(PERSIST_HDR)[0]
-            b = off + PERSIST_HDR.itemsize
-            el, rl, pl, bl = int(h["ex_len"]), int(h["rk_len"]), int(h["props_len"]), int(h["body_len"])
-            data = bytes(raw[b:b + el + rl + pl + bl])
-            out.append((int(h["msg_id"]), int(h["ts_ms"]), int(h["q"]), int(h["qpos"]), int(h["expire_ms"]),
-                        data[:el], data[el:el + rl], data[el + rl:el + rl + pl], data[el + rl + pl:]))
-            off += int(h["size"])
-        return out
+        return parse_persist(raw)
 
     def take_consumed(self):
         """[(msg_id, q, qpos, kind)] of persistent messages that left durable queues."""
@@ -336,8 +351,13 @@ class GpuDataPlane(ControlState):
         n = min(c["n_consumed"], self.info["persist_max"])
         if not n:
             return out
-        recs = self.eng.host_view(f"consumed{self._last_parity}")[:n * CONSUMED_REC.itemsize].view(CONSUMED_REC)
-        return out + [(int(r["msg_id"]), int(r["q"]), int(r["qpos"]), int(r["kind"])) for r in recs]
+        return out + parse_consumed(self.eng.host_view(f"consumed{self._last_parity}")[:n * CONSUMED_REC.itemsize])
+
+    def take_get_consumed(self):
+        """Store records of Basic.Get calls since the last call (native front end mode,
+        where no Python-run step collects them)."""
+        out, self._get_consumed = self._get_consumed, []
+        return out
 
     def basic_get(self, conn, ch, q, no_ack, now_ms=None):
         """Basic.Get between steps (k_basic_get): the head of queue slot ``q`` after the
@@ -454,17 +474,18 @@ class GpuDataPlane(ControlState):
             pin = self._pin[parity] = self.mod.alloc_pinned(max(n, 1 << 20))
         return pin
 
-    def step(self, inputs=None, now_ms=None, collect=True):
+    def step(self, inputs=None, now_ms=None, collect=True, with_carry=True):
         """One synchronous data-plane step.  ``inputs``: {conn: bytes}.  Connections
-        holding carry (partial commands) are re-presented once unpaused."""
-        segs, ptr, n = self.stage(inputs)
+        holding carry (partial commands) are re-presented once unpaused (``with_carry``;
+        off when the native front end owns the other connections' bytes)."""
+        segs, ptr, n = self.stage(inputs, with_carry)
         return self.step_raw(segs, ptr, n, now_ms, collect)
 
-    def stage(self, inputs):
+    def stage(self, inputs, with_carry=True):
         """{conn: bytes} (+ connections holding carry) -> (SegIn[], pinned ptr, bytes)."""
         inputs = inputs or {}
         conns = set(inputs)
-        for c in np.nonzero(self.carry)[0]:
+        for c in np.nonzero(self.carry)[0] if with_carry else ():
             c = int(c)
             if c in self.conns and not self.conns[c].paused:
                 conns.add(c)

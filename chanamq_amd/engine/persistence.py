@@ -48,9 +48,11 @@ class GpuPersistence:
     def after_step(self):
         """Apply the step's records.  Device queue positions change on requeue, so rows
         are addressed by (queue, message id) -> the offset they were stored at."""
+        return self.apply(self.plane.take_persist(), self.plane.take_consumed())
+
+    def apply(self, persisted, consumed):
+        """Store rows for a step's persist / consumed records (see after_step)."""
         st = self.store
-        persisted = self.plane.take_persist()
-        consumed = self.plane.take_consumed()
         for mid, ts, q, qpos, exp, ex, rk, props, body in persisted:
             qid = self._qid(q)
             if qid is None:

@@ -58,6 +58,31 @@ class _Conn:
         self.cap_blocked = False
 
 
+FE_OPEN, FE_CLOSED, FE_HOST, FE_CTRL, FE_TXBUF, FE_EVENT, FE_STATUS, FE_PERSIST, FE_ERROR = range(1, 10)
+
+
+class _PlaneLock:
+    """Exclusive access to the data plane's device tables.  With the pipelined front end
+    the outermost acquisition pauses its stepper (steps in flight finished, their egress
+    written) and the release resumes it."""
+
+    def __init__(self, broker):
+        self.b, self.rl, self.depth = broker, threading.RLock(), 0
+
+    def __enter__(self):
+        self.rl.acquire()
+        self.depth += 1
+        if self.depth == 1 and self.b.fe is not None:
+            self.b.fe.pause()
+        return self
+
+    def __exit__(self, *exc):
+        self.depth -= 1
+        if self.depth == 0 and self.b.fe is not None:
+            self.b.fe.resume()
+        self.rl.release()
+
+
 class _Hard(Exception):
     """Connection-level error: Connection.Close(code, text, class, method)."""
 
@@ -84,12 +109,22 @@ class GpuBroker:
     def __init__(self, plane, host="127.0.0.1", port=0, heartbeat=0, frame_max=131072, channel_max=2047,
                  idle_step_ms=2.0, product="chanamq-amd", version="0.1.0", io="native",
                  ingress_bytes=64 << 20, per_conn_read=256 << 10, mem_high_watermark=0, mem_low_watermark=0,
-                 store=None, node=None, reuseport=False):
-        """``io``: "native" = C++ batched gateway (csrc/core/gateway.cpp), "python" =
-        selectors loop (portable fallback)."""
+                 store=None, node=None, reuseport=False, io_threads=4):
+        """``io``: "pipeline" = native pipelined front end (csrc/core/frontend.cpp: IO
+        threads + a stepper thread keeping two steps in flight, no Python per step),
+        "native" = C++ batched gateway polled by a Python step loop (csrc/core/
+        gateway.cpp), "python" = selectors loop (portable fallback); "auto" = pipeline
+        for a single-rank GPU plane, else native."""
         self.plane = plane
+        if io == "auto":
+            io = "pipeline" if (hasattr(plane, "eng") and node is None) else "native"
+        if io == "pipeline" and (not hasattr(plane, "eng") or node is not None):
+            raise ValueError("io='pipeline' needs a single-rank GPU data plane")
         self.io = io
+        self.io_threads = io_threads
         self.gw = None
+        self.fe = None
+        self._fe_stats = None
         self.ingress_bytes, self.per_conn_read = ingress_bytes, per_conn_read
         # back-pressure (SURVEY A.Q17 / config 5): above the high watermark of stored
         # message bytes publishers get Connection.Blocked (if they announced the
@@ -127,10 +162,22 @@ class GpuBroker:
         self._running = False
         self._wake_r, self._wake_w = os.pipe()
         self.stats = dict(steps=0, published=0, delivered=0, connections=0)
-        self.lock = threading.RLock()
+        self.lock = _PlaneLock(self)
 
     # ------------------------------------------------------------------ lifecycle
     def start(self):
+        if self.io == "pipeline":
+            from ..broker import load
+            self.fe = load().Frontend(self.plane.eng.c_api(), dict(
+                host=self.host, port=self.port, io_threads=self.io_threads, per_conn_read=self.per_conn_read,
+                idle_step_ms=self.idle_step_s * 1000.0, worker=self.plane.worker, max_slot=self.plane.c_max - 2,
+                reuseport=self.reuseport))
+            self.port = self.fe.port
+            self._running = True
+            self.fe.start()
+            self._thread = threading.Thread(target=self._loop_pipeline, name="gpu-broker-ctl", daemon=True)
+            self._thread.start()
+            return self
         if self.io == "native":
             from ..broker import load
             self.gw = load().Gateway(self.host, self.port, self.plane.c_max, self.reuseport)
@@ -165,6 +212,10 @@ class GpuBroker:
             self._thread.join(timeout=10)
         for c in list(self.conns.values()):
             self._drop(c)
+        if self.fe is not None:
+            self.fe.stop()
+            self._sync_fe_stats()
+            self.fe = None
         self._sel.close()
         if self._lsock is not None:
             self._lsock.close()
@@ -200,6 +251,121 @@ class GpuBroker:
                     "ready": self.plane.message_count(q.slot) if q.owner == self.plane.rank else None,
                     "consumers": len(q.consumers)} for q in self.plane.queues.values()]
         return json.dumps(out)
+
+    # ------------------------------------------------------------------ pipelined native loop
+    def _loop_pipeline(self):
+        """Control plane of the native front end: blocks on its events (handshakes,
+        control commands, closes, store records) and takes the device (``self.lock``
+        pauses the stepper) only while it handles them; steps never wait for Python."""
+        fe = self.fe
+        last_stats = 0.0
+        while self._running:
+            evs = fe.poll_events(20)
+            persist = [e for e in evs if e[0] == FE_PERSIST]
+            dev = [e for e in evs if e[0] != FE_PERSIST]
+            if dev or self._tx_pending:
+                with self.lock:
+                    while dev or self._tx_pending:
+                        self._handle_fe(dev)
+                        while self._tx_pending:   # committed transactions: host-run injection steps
+                            self._host_step({})
+                        more = fe.poll_events(0)
+                        persist += [e for e in more if e[0] == FE_PERSIST]
+                        dev = [e for e in more if e[0] != FE_PERSIST]
+                    if self.persistence is not None and self.plane._get_consumed:
+                        self.persistence.apply([], self.plane.take_get_consumed())
+                        self.persistence.commit()
+                    self._flush_all()
+            if persist:
+                self._persist_native(persist)
+            now = time.monotonic()
+            if now - last_stats > 0.05:
+                last_stats = now
+                self._sync_fe_stats()
+                self._watermarks()
+                self._flush_all()
+
+    def _handle_fe(self, evs):
+        ctrl, events, seg_status, txbuf = [], [], [], []
+        for kind, conn, a, b, data, data2 in evs:
+            if kind == FE_OPEN:
+                self.conns[conn] = _Conn(None, conn, None)
+                self.stats["connections"] += 1
+            elif kind == FE_CLOSED:
+                c = self.conns.get(conn)
+                if c is not None:
+                    c.state = "gone"
+                    self._drop(c)
+                else:
+                    self.fe.close(conn)
+            elif kind == FE_HOST:
+                c = self.conns.get(conn)
+                data = self.fe.take(conn)
+                if c is None or not data:
+                    continue
+                was_open = c.state == "open"
+                rest = self._host_bytes(c, data)
+                if c.state == "open" and not was_open:
+                    self._flush(c)
+                    self.fe.set_heartbeat(conn, c.heartbeat)
+                    self.fe.set_data_mode(conn, rest)
+            elif kind == FE_CTRL:
+                ctrl.append((conn, data))
+            elif kind == FE_TXBUF:
+                txbuf.append((conn, a, data))
+            elif kind == FE_EVENT:
+                events.append((conn, a, b))
+            elif kind == FE_STATUS:
+                seg_status.append((conn, a))
+            elif kind == FE_ERROR:
+                import logging
+                logging.getLogger("chanamq.gpu").error("data-plane engine failed: %s", data.decode(errors="replace"))
+                self._running = False
+        if ctrl or events or seg_status or txbuf:
+            txbuf.sort()
+            self._after_step(ctrl, events, seg_status, {}, False, False, txbuf)
+
+    def _persist_native(self, evs):
+        """Write-behind group commit: the store rows of every held step in this batch,
+        one fsync, then their egress (with the publisher confirms) is released."""
+        from ..engine.dataplane import parse_consumed, parse_persist
+        top = max(e[2] for e in evs)
+        if self.persistence is not None:
+            for kind, conn, step, overflow, data, data2 in evs:
+                if overflow:
+                    raise RuntimeError("persist buffer overflow: raise persist_max / persist_bytes")
+                self.persistence.apply(parse_persist(data) if data else [], parse_consumed(data2) if data2 else [])
+            self.persistence.commit()
+        self.fe.release(top)
+
+    def _sync_fe_stats(self):
+        if self.fe is None:
+            return
+        st = self.fe.stats()
+        self.stats.update(steps=st["steps"], published=st["published"], delivered=st["delivered"])
+        self._fe_stats = st
+
+    def _host_step(self, inputs):
+        """A synchronous step run by the control plane while the front end is paused
+        (transaction injection, queue purge): only the given connections take part; its
+        egress goes out through the front end."""
+        inj = self._tx_begin()
+        if inj:
+            inputs = dict(inputs)
+            inputs[self.txc] = inj
+        res = self.plane.step(inputs, now_ms=int(time.time() * 1000), with_carry=False)
+        self._persist_step()
+        egress = dict(res.egress)
+        if self.txc in egress:
+            data = egress.pop(self.txc)
+            if self._tx_active is not None:
+                egress[self._tx_active[0]] = egress.get(self._tx_active[0], b"") + data
+        for conn, data in egress.items():
+            c = self.conns.get(conn)
+            if c is not None and c.state == "open":
+                c.out += data
+        seg_status = [(sg[0], sg[1]) for sg in res.segs]
+        self._after_step(res.ctrl, res.events, seg_status, res.counters, bool(inputs), bool(egress), res.txbuf)
 
     # ------------------------------------------------------------------ native loop
     def _loop_native(self):
@@ -512,10 +678,11 @@ class GpuBroker:
         if self._tx_active is None:
             return
         conn, ch = self._tx_active
+        self._tx_active = None
         c = self.conns.get(conn)
         if c is not None and c.state == "open":
             self._send(c, ch, Method("tx.commit_ok"))
-            self.plane.unpause(conn)
+            self._unpause(conn)
 
     def _tx_commit(self, c, ch):
         """Apply the channel's held acks now (window marks between steps) and queue its
@@ -556,6 +723,9 @@ class GpuBroker:
             c = self.conns.get(conn)
             if c is None or c.state != "open":
                 continue
+            if code == C.RESOURCE_ERROR:   # the step's control buffer overflowed: command lost
+                self._conn_close(c, C.RESOURCE_ERROR, "control command buffer full")
+                continue
             ch = self._chan_of_slot(conn, chslot)
             if code == 404 and ch is not None:
                 self._chan_close(c, ch, C.NOT_FOUND, "no exchange", 60, 40)
@@ -581,7 +751,7 @@ class GpuBroker:
                 except _Hard as e:
                     self._conn_close(c, e.code, e.text, e.cls, e.mid)
             if c.state == "open" and not deferred:
-                self.plane.unpause(conn)
+                self._unpause(conn)
         return had_input or had_egress or bool(ctrl) or cnt.get("n_deliv", 0) > 0
 
     def _read_backpressure(self, segs):
@@ -614,6 +784,11 @@ class GpuBroker:
             if conn * self.plane.chpc + chan.local == chslot:
                 return ch
         return None
+
+    def _unpause(self, conn):
+        self.plane.unpause(conn)
+        if self.fe is not None:
+            self.fe.kick(conn)
 
     # ------------------------------------------------------------------ control methods
     def _control(self, c, raw):
@@ -739,8 +914,11 @@ class GpuBroker:
             if m.if_empty and cnt:
                 raise ControlError(C.PRECONDITION_FAILED, f"queue '{q.name}' not empty", 50, 40)
             p.purge(q.slot)
-            p.step({}, now_ms=int(time.time() * 1000))   # releases the purged messages
-            self._persist_step()
+            if self.fe is not None:     # releases the purged messages (front end paused)
+                self._host_step({})
+            else:
+                p.step({}, now_ms=int(time.time() * 1000))
+                self._persist_step()
             p.delete_queue(vh, q.name)
             if self.persistence is not None:
                 self.persistence.queue_deleted(vh, q.name)
@@ -882,7 +1060,7 @@ class GpuBroker:
             elif reply is not None:
                 self._send(c, ch, reply(res))
             if c.state == "open":
-                self.plane.unpause(conn)
+                self._unpause(conn)
 
     def _queue(self, vh, name, cls, mid):
         q = self.plane.queues.get((vh, name))
@@ -907,10 +1085,18 @@ class GpuBroker:
                                 method_id=mid))
         with self.lock:
             self.plane.close_connection(c.id)
+            if self.fe is not None:   # its bytes go to the host again (waiting for CloseOk)
+                self._flush(c)
+                self.fe.set_host_mode(c.id)
         c.state = "closing"
 
     def _flush(self, c):
         if not c.out or c.state == "closed":
+            return
+        if self.fe is not None:
+            self.fe.send(c.id, bytes(c.out))
+            c.out.clear()
+            c.last_tx = time.monotonic()
             return
         if self.gw is not None:
             self.gw.send(c.id, bytes(c.out))
@@ -935,7 +1121,7 @@ class GpuBroker:
     def _watermarks(self):
         if not self.mem_high:
             return
-        used = self.plane.memory_in_use()
+        used = self._fe_stats["live_bytes"] if self.fe is not None and self._fe_stats else self.plane.memory_in_use()
         if not self.blocked and used >= self.mem_high:
             self.blocked = True
             self._set_flow(False)
@@ -972,6 +1158,15 @@ class GpuBroker:
             return
         prev = c.state
         c.state = "closed"
+        if self.fe is not None:
+            if prev != "gone":
+                self._flush(c)
+            if prev == "open" or c.id in self.plane.conns:
+                with self.lock:
+                    self.plane.close_connection(c.id)
+            self.conns.pop(c.id, None)
+            self.fe.close(c.id)
+            return
         if self.gw is not None:
             if prev != "gone":
                 self._flush(c)

@@ -6,6 +6,7 @@
 
 #include "broker.hpp"
 #include "codec.hpp"
+#include "frontend.hpp"
 #include "gateway.hpp"
 #include "loadgen.hpp"
 #include "store.hpp"
@@ -177,6 +178,72 @@ PYBIND11_MODULE(_core, m) {
       .def("close", &Gateway::close)
       .def("pending_bytes", &Gateway::pending_bytes);
 
+  py::class_<Frontend>(m, "Frontend")
+      .def(py::init([](uint64_t api, py::dict d) {
+             FrontendCfg c;
+#define S(k, f) if (d.contains(k)) c.f = d[k].cast<decltype(c.f)>()
+             S("host", host); S("port", port); S("io_threads", io_threads); S("per_conn_read", per_conn_read);
+             S("idle_step_ms", idle_step_ms); S("worker", worker); S("max_slot", max_slot); S("reuseport", reuseport);
+             S("sndbuf", sndbuf); S("rcvbuf", rcvbuf);
+#undef S
+             return new Frontend(c, (const CmqEngineApi*)api);
+           }), py::arg("engine_api"), py::arg("cfg") = py::dict())
+      .def_property_readonly("port", &Frontend::port)
+      .def("start", &Frontend::start, py::call_guard<py::gil_scoped_release>())
+      .def("stop", &Frontend::stop, py::call_guard<py::gil_scoped_release>())
+      .def("poll_events", [](Frontend& f, int timeout_ms) {
+             std::vector<FeEvent> evs;
+             {
+               py::gil_scoped_release nogil;
+               evs = f.poll_events(timeout_ms);
+             }
+             py::list out;
+             for (auto& e : evs)
+               out.append(py::make_tuple(e.kind, e.conn, e.a, e.b, py::bytes(e.data), py::bytes(e.data2)));
+             return out;
+           }, py::arg("timeout_ms") = 100)
+      .def("take", [](Frontend& f, uint32_t conn) { return py::bytes(f.take(conn)); })
+      .def("send", [](Frontend& f, uint32_t conn, py::bytes b) {
+             std::string s = b;
+             py::gil_scoped_release nogil;
+             f.send(conn, s.data(), s.size());
+           })
+      .def("send_egress", [](Frontend& f, py::buffer egress, py::buffer conn_out, uint32_t n_slots) {
+             py::buffer_info e = egress.request(), c = conn_out.request();
+             if ((uint64_t)c.size * c.itemsize < 8ull * n_slots) throw std::runtime_error("conn_out too small");
+             py::gil_scoped_release nogil;
+             f.send_egress((const u8*)e.ptr, (const ConnOut*)c.ptr, n_slots);
+           })
+      .def("set_data_mode", [](Frontend& f, uint32_t conn, py::bytes leftover) {
+             std::string s = leftover;
+             f.set_data_mode(conn, s);
+           }, py::arg("conn"), py::arg("leftover") = py::bytes(""))
+      .def("set_host_mode", &Frontend::set_host_mode)
+      .def("set_heartbeat", &Frontend::set_heartbeat)
+      .def("close", &Frontend::close)
+      .def("kick", &Frontend::kick)
+      .def("pause", &Frontend::pause, py::call_guard<py::gil_scoped_release>())
+      .def("resume", &Frontend::resume, py::call_guard<py::gil_scoped_release>())
+      .def("release", &Frontend::release)
+      .def("pending_out", &Frontend::pending_out)
+      .def("stats", [](Frontend& f) {
+             FeStats s = f.stats();
+             py::dict o;
+             o["steps"] = s.steps; o["published"] = s.published; o["delivered"] = s.delivered;
+             o["rx_bytes"] = s.rx_bytes; o["tx_bytes"] = s.tx_bytes; o["egress_bytes"] = s.egress_bytes;
+             o["held_steps"] = s.held_steps; o["idle_steps"] = s.idle_steps; o["gather_segs"] = s.gather_segs;
+             o["live_bytes"] = s.live_bytes; o["io_phase_s"] = s.io_phase_s; o["wait_s"] = s.wait_s;
+             o["submit_s"] = s.submit_s;
+             o["lat_hist"] = std::vector<u64>(s.lat_hist, s.lat_hist + 32);
+             return o;
+           });
+  py::class_<EchoEngine>(m, "EchoEngine")
+      .def(py::init<u32, u32, u64, u32>(), py::arg("c_max") = 64, py::arg("seg_max") = 64,
+           py::arg("ingress_cap") = 1 << 20, py::arg("carry_cap") = 1 << 16)
+      .def("c_api", &EchoEngine::c_api)
+      .def("unpause", &EchoEngine::unpause)
+      .def_readonly("steps", &EchoEngine::steps);
+
   m.def("run_load", [](py::dict d) {
     LoadSpec s;
 #define S(k, f) if (d.contains(k)) s.f = d[k].cast<decltype(s.f)>()
@@ -184,7 +251,7 @@ PYBIND11_MODULE(_core, m) {
     S("msg_size", msg_size); S("seconds", seconds); S("exchange", exchange); S("exchange_type", exchange_type);
     S("routing_key", routing_key); S("queue", queue); S("queues", queues); S("auto_ack", auto_ack);
     S("prefetch", prefetch); S("persistent", persistent); S("durable", durable); S("confirm", confirm);
-    S("rate", rate);
+    S("rate", rate); S("threads", threads); S("warmup", warmup);
 #undef S
     LoadResult r;
     {
@@ -194,6 +261,7 @@ PYBIND11_MODULE(_core, m) {
     py::dict o;
     o["sent"] = r.sent; o["received"] = r.received; o["elapsed"] = r.elapsed; o["p50_us"] = r.p50_us;
     o["p95_us"] = r.p95_us; o["p99_us"] = r.p99_us; o["error"] = r.error;
+    o["confirmed"] = r.confirmed; o["nacked"] = r.nacked; o["threads"] = r.threads;
     return o;
   });
   m.def("decode_method", &decode);

@@ -1,0 +1,1003 @@
+#include "frontend.hpp"
+
+#include <arpa/inet.h>
+#include <fcntl.h>
+#include <netinet/in.h>
+#include <netinet/tcp.h>
+#include <pthread.h>
+#include <sys/epoll.h>
+#include <sys/eventfd.h>
+#include <sys/ioctl.h>
+#include <sys/socket.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstring>
+#include <stdexcept>
+
+namespace cmq {
+
+namespace {
+i64 now_ns() {
+  return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch())
+      .count();
+}
+i64 wall_ms() {
+  return std::chrono::duration_cast<std::chrono::milliseconds>(std::chrono::system_clock::now().time_since_epoch())
+      .count();
+}
+double secs_since(i64 t0) { return (now_ns() - t0) * 1e-9; }
+const char HEARTBEAT_FRAME[8] = {8, 0, 0, 0, 0, 0, 0, (char)0xCE};
+constexpr u64 LISTENER = ~0ull, WAKE = ~0ull - 1;
+}  // namespace
+
+enum : int { M_FREE = 0, M_HOST = 1, M_DATA = 2, M_DEAD = 3 };
+
+struct FeConn {
+  int fd = -1;
+  u32 id = 0;
+  int io = 0;
+  std::atomic<int> mode{M_FREE};
+  // IO-thread owned
+  bool in_ready = false;
+  bool rdhup = false;
+  // guarded by mu
+  std::mutex mu;
+  std::string out;
+  size_t out_pos = 0;
+  std::string inject;    // bytes for the data plane ahead of the socket's (handshake leftovers)
+  std::string hostbuf;   // host-mode bytes not yet taken by the control plane
+  bool host_notified = false;
+  // stepper-owned: read by IO threads only inside the gather phase, by the control plane
+  // only while paused
+  u32 carry = 0, inflight = 0;
+  bool paused = false, kicked = false;
+  // heartbeats
+  std::atomic<i64> last_rx{0}, last_tx{0};
+  std::atomic<u32> hb_s{0};
+};
+
+struct FeIo {
+  int epfd = -1, evfd = -1;
+  std::thread th;
+  std::mutex qmu;
+  std::vector<u32> adopt;     // new connections to register (accepted by thread 0)
+  std::vector<u32> pending;   // connections to put on the ready list (kick / data mode)
+  std::vector<u32> closing;   // close() requests
+  std::vector<u32> ready;     // data connections with unread socket bytes or pending input
+  std::vector<u32> owned;
+  std::vector<SegIn> segs;    // this phase's gathered segments
+  u64 phase_seen = 0;
+  i64 last_hb = 0;
+};
+
+static void poke(int evfd) {
+  u64 one = 1;
+  ssize_t r = ::write(evfd, &one, 8);
+  (void)r;
+}
+
+// ============================================================================ lifecycle
+Frontend::Frontend(const FrontendCfg& cfg, const CmqEngineApi* api) : cfg_(cfg), api_(api) {
+  if (!api_ || api_->abi != CMQ_STEP_ABI) throw std::runtime_error("frontend: engine C API missing or ABI mismatch");
+  c_max_ = api_->c_max;
+  if (cfg_.io_threads < 1) cfg_.io_threads = 1;
+  if (!cfg_.max_slot || cfg_.max_slot > c_max_ - 2) cfg_.max_slot = c_max_ - 2;
+  conns_.resize(c_max_);
+  for (u32 i = 0; i < c_max_; ++i) {
+    conns_[i].reset(new FeConn());
+    conns_[i]->id = i;
+    conns_[i]->io = (int)(i % (u32)cfg_.io_threads);
+  }
+  for (u32 i = cfg_.max_slot; i >= 1; --i) free_.push_back(i);
+  for (int k = 0; k < 3; ++k) {
+    arena_[k] = (u8*)aligned_alloc(4096, ((api_->ingress_cap + 64 + 4095) / 4096) * 4096);
+    if (!arena_[k]) throw std::runtime_error("frontend: arena allocation failed");
+  }
+  lfd_ = ::socket(AF_INET, SOCK_STREAM | SOCK_NONBLOCK | SOCK_CLOEXEC, 0);
+  if (lfd_ < 0) throw std::runtime_error("frontend: socket failed");
+  int one = 1;
+  setsockopt(lfd_, SOL_SOCKET, SO_REUSEADDR, &one, sizeof one);
+  if (cfg_.reuseport) setsockopt(lfd_, SOL_SOCKET, SO_REUSEPORT, &one, sizeof one);
+  sockaddr_in a{};
+  a.sin_family = AF_INET;
+  a.sin_port = htons((uint16_t)cfg_.port);
+  if (inet_pton(AF_INET, cfg_.host.c_str(), &a.sin_addr) != 1) a.sin_addr.s_addr = htonl(INADDR_ANY);
+  if (::bind(lfd_, (sockaddr*)&a, sizeof a) < 0) throw std::runtime_error(std::string("frontend: bind: ") + strerror(errno));
+  if (::listen(lfd_, 4096) < 0) throw std::runtime_error("frontend: listen failed");
+  socklen_t l = sizeof a;
+  getsockname(lfd_, (sockaddr*)&a, &l);
+  port_ = ntohs(a.sin_port);
+  for (int i = 0; i < cfg_.io_threads; ++i) {
+    std::unique_ptr<FeIo> io(new FeIo());
+    io->epfd = epoll_create1(EPOLL_CLOEXEC);
+    io->evfd = eventfd(0, EFD_NONBLOCK | EFD_CLOEXEC);
+    epoll_event ev{};
+    ev.events = EPOLLIN;
+    ev.data.u64 = WAKE;
+    epoll_ctl(io->epfd, EPOLL_CTL_ADD, io->evfd, &ev);
+    if (i == 0) {
+      ev.events = EPOLLIN;
+      ev.data.u64 = LISTENER;
+      epoll_ctl(io->epfd, EPOLL_CTL_ADD, lfd_, &ev);
+    }
+    io_.push_back(std::move(io));
+  }
+}
+
+Frontend::~Frontend() {
+  stop();
+  for (auto& c : conns_)
+    if (c->fd >= 0) ::close(c->fd);
+  for (auto& io : io_) {
+    if (io->epfd >= 0) ::close(io->epfd);
+    if (io->evfd >= 0) ::close(io->evfd);
+  }
+  if (lfd_ >= 0) ::close(lfd_);
+  for (auto* a : arena_) free(a);
+}
+
+void Frontend::start() {
+  if (running_.exchange(true)) return;
+  for (int i = 0; i < (int)io_.size(); ++i) io_[i]->th = std::thread([this, i] { io_loop(i); });
+  stepper_ = std::thread([this] { stepper(); });
+}
+
+void Frontend::stop() {
+  if (!running_.exchange(false)) return;
+  {
+    std::lock_guard<std::mutex> g(st_mu_);
+    wake_ = true;
+  }
+  st_cv_.notify_all();
+  pause_cv_.notify_all();
+  {   // an IO phase in progress completes: IO threads finish it before they look at running_
+    std::lock_guard<std::mutex> g(ph_mu_);
+  }
+  if (stepper_.joinable()) stepper_.join();
+  for (auto& io : io_) {
+    poke(io->evfd);
+    if (io->th.joinable()) io->th.join();
+  }
+  ev_cv_.notify_all();
+}
+
+bool Frontend::check(int rc) {
+  if (rc >= 0) return true;
+  FeEvent e;
+  e.kind = FE_ERROR;
+  e.data = api_->error(api_->eng);
+  failed_ = true;
+  post(std::move(e));
+  return false;
+}
+
+void Frontend::post(FeEvent&& e) {
+  {
+    std::lock_guard<std::mutex> g(ev_mu_);
+    events_.push_back(std::move(e));
+  }
+  ev_cv_.notify_one();
+}
+
+void Frontend::wake_stepper() {
+  {
+    std::lock_guard<std::mutex> g(st_mu_);
+    wake_ = true;
+  }
+  st_cv_.notify_one();
+}
+
+// ============================================================================ control-plane API
+std::vector<FeEvent> Frontend::poll_events(int timeout_ms) {
+  std::unique_lock<std::mutex> g(ev_mu_);
+  if (events_.empty() && timeout_ms != 0)
+    ev_cv_.wait_for(g, std::chrono::milliseconds(timeout_ms < 0 ? 1000 : timeout_ms),
+                    [&] { return !events_.empty() || !running_; });
+  std::vector<FeEvent> out(std::make_move_iterator(events_.begin()), std::make_move_iterator(events_.end()));
+  events_.clear();
+  return out;
+}
+
+std::string Frontend::take(u32 conn) {
+  if (conn >= c_max_) return {};
+  FeConn& c = *conns_[conn];
+  std::lock_guard<std::mutex> g(c.mu);
+  std::string s;
+  s.swap(c.hostbuf);
+  c.host_notified = false;
+  return s;
+}
+
+bool Frontend::write_some(FeConn& c) {
+  while (c.out_pos < c.out.size()) {
+    ssize_t k = ::send(c.fd, c.out.data() + c.out_pos, c.out.size() - c.out_pos, MSG_NOSIGNAL);
+    if (k > 0) {
+      c.out_pos += (size_t)k;
+      tx_bytes_ += (u64)k;
+      continue;
+    }
+    if (k < 0 && errno == EINTR) continue;
+    if (k < 0 && (errno == EAGAIN || errno == EWOULDBLOCK)) return false;   // EPOLLOUT edge resumes
+    c.out.clear();
+    c.out_pos = 0;
+    return false;   // broken: the IO thread sees EPOLLERR/HUP and drops it
+  }
+  c.out.clear();
+  c.out_pos = 0;
+  c.last_tx = now_ns();
+  return true;
+}
+
+void Frontend::scatter_conn(FeConn& c, const u8* data, u32 n) {
+  std::lock_guard<std::mutex> g(c.mu);
+  if (c.fd < 0) return;
+  if (c.out_pos >= c.out.size()) {   // nothing queued: write straight from the egress slot
+    c.out.clear();
+    c.out_pos = 0;
+    u32 o = 0;
+    while (o < n) {
+      ssize_t k = ::send(c.fd, data + o, n - o, MSG_NOSIGNAL);
+      if (k > 0) { o += (u32)k; continue; }
+      if (k < 0 && errno == EINTR) continue;
+      break;
+    }
+    tx_bytes_ += o;
+    c.last_tx = now_ns();
+    if (o < n) c.out.append((const char*)data + o, n - o);
+  } else {
+    c.out.append((const char*)data, n);
+  }
+}
+
+void Frontend::send(u32 conn, const char* data, size_t n) {
+  if (conn >= c_max_ || !n) return;
+  FeConn& c = *conns_[conn];
+  std::lock_guard<std::mutex> g(c.mu);
+  if (c.fd < 0) return;
+  c.out.append(data, n);
+  write_some(c);
+}
+
+void Frontend::send_egress(const u8* egress, const ConnOut* co, u32 n_slots) {
+  for (u32 i = 0; i < n_slots && i < c_max_; ++i)
+    if (co[i].len) send(i, (const char*)egress + co[i].off, co[i].len);
+}
+
+void Frontend::set_data_mode(u32 conn, const std::string& leftover) {
+  if (conn >= c_max_) return;
+  FeConn& c = *conns_[conn];
+  {
+    std::lock_guard<std::mutex> g(c.mu);
+    if (c.fd < 0) return;
+    c.inject = leftover + c.hostbuf;
+    c.hostbuf.clear();
+    c.host_notified = false;
+    c.carry = c.inflight = 0;
+    c.paused = false;
+    c.kicked = !c.inject.empty();
+    c.mode = M_DATA;
+  }
+  FeIo& io = *io_[c.io];
+  {
+    std::lock_guard<std::mutex> g(io.qmu);
+    io.pending.push_back(conn);
+  }
+  poke(io.evfd);
+  wake_stepper();
+}
+
+void Frontend::set_host_mode(u32 conn) {
+  if (conn >= c_max_) return;
+  FeConn& c = *conns_[conn];
+  std::lock_guard<std::mutex> g(c.mu);
+  if (c.mode == M_DATA) c.mode = M_HOST;
+  c.inject.clear();
+  FeIo& io = *io_[c.io];
+  std::lock_guard<std::mutex> g2(io.qmu);
+  io.pending.push_back(conn);   // its socket may hold bytes: read them as host bytes now
+  poke(io.evfd);
+}
+
+void Frontend::set_heartbeat(u32 conn, u32 seconds) {
+  if (conn < c_max_) conns_[conn]->hb_s = seconds;
+}
+
+void Frontend::close(u32 conn) {
+  if (conn == 0 || conn >= c_max_) return;
+  FeIo& io = *io_[conns_[conn]->io];
+  {
+    std::lock_guard<std::mutex> g(io.qmu);
+    io.closing.push_back(conn);
+  }
+  poke(io.evfd);
+}
+
+void Frontend::kick(u32 conn) {
+  if (conn >= c_max_) return;
+  FeConn& c = *conns_[conn];
+  c.paused = false;
+  c.kicked = true;
+  FeIo& io = *io_[c.io];
+  {
+    std::lock_guard<std::mutex> g(io.qmu);
+    io.pending.push_back(conn);
+  }
+  wake_stepper();
+}
+
+void Frontend::pause() {
+  std::unique_lock<std::mutex> g(st_mu_);
+  ++pause_req_;
+  wake_ = true;
+  st_cv_.notify_all();
+  pause_cv_.wait(g, [&] { return paused_ || !running_ || failed_; });
+}
+
+void Frontend::resume() {
+  {
+    std::lock_guard<std::mutex> g(st_mu_);
+    if (pause_req_ > 0) --pause_req_;
+    wake_ = true;
+  }
+  st_cv_.notify_all();
+}
+
+void Frontend::release(u64 step) {
+  u64 cur = released_.load();
+  while (step > cur && !released_.compare_exchange_weak(cur, step)) {
+  }
+  have_released_ = true;
+  wake_stepper();
+}
+
+FeStats Frontend::stats() {
+  std::lock_guard<std::mutex> g(stats_mu_);
+  FeStats s = stats_;
+  s.rx_bytes = rx_bytes_;
+  s.tx_bytes = tx_bytes_;
+  return s;
+}
+
+u64 Frontend::pending_out() const {
+  u64 t = 0;
+  for (auto& c : conns_) {
+    std::lock_guard<std::mutex> g(c->mu);
+    t += c->out.size() - c->out_pos;
+  }
+  return t;
+}
+
+// ============================================================================ IO threads
+void Frontend::accept_all(FeIo& io0) {
+  for (;;) {
+    sockaddr_in a{};
+    socklen_t l = sizeof a;
+    int fd = ::accept4(lfd_, (sockaddr*)&a, &l, SOCK_NONBLOCK | SOCK_CLOEXEC);
+    if (fd < 0) return;
+    u32 id = 0;
+    {
+      std::lock_guard<std::mutex> g(free_mu_);
+      if (!free_.empty()) { id = free_.back(); free_.pop_back(); }
+    }
+    if (!id) { ::close(fd); continue; }
+    int one = 1;
+    setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof one);
+    if (cfg_.sndbuf) setsockopt(fd, SOL_SOCKET, SO_SNDBUF, &cfg_.sndbuf, sizeof cfg_.sndbuf);
+    if (cfg_.rcvbuf) setsockopt(fd, SOL_SOCKET, SO_RCVBUF, &cfg_.rcvbuf, sizeof cfg_.rcvbuf);
+    FeConn& c = *conns_[id];
+    {
+      std::lock_guard<std::mutex> g(c.mu);
+      c.fd = fd;
+      c.out.clear();
+      c.out_pos = 0;
+      c.inject.clear();
+      c.hostbuf.clear();
+      c.host_notified = false;
+    }
+    c.in_ready = false;
+    c.rdhup = false;
+    c.carry = c.inflight = 0;
+    c.paused = c.kicked = false;
+    c.hb_s = 0;
+    c.last_rx = c.last_tx = now_ns();
+    c.mode = M_HOST;
+    FeEvent e;
+    e.kind = FE_OPEN;
+    e.conn = id;
+    post(std::move(e));
+    FeIo& io = *io_[c.io];
+    if (&io == &io0) {
+      io.owned.push_back(id);
+      epoll_event ev{};
+      ev.events = EPOLLIN | EPOLLOUT | EPOLLRDHUP | EPOLLET;
+      ev.data.u64 = id;
+      epoll_ctl(io.epfd, EPOLL_CTL_ADD, fd, &ev);
+    } else {
+      {
+        std::lock_guard<std::mutex> g(io.qmu);
+        io.adopt.push_back(id);
+      }
+      poke(io.evfd);
+    }
+  }
+}
+
+void Frontend::drop(FeConn& c, bool notify) {
+  std::lock_guard<std::mutex> g(c.mu);
+  if (c.fd < 0) return;
+  epoll_ctl(io_[c.io]->epfd, EPOLL_CTL_DEL, c.fd, nullptr);
+  ::close(c.fd);
+  c.fd = -1;
+  c.mode = M_DEAD;
+  c.out.clear();
+  c.out_pos = 0;
+  c.inject.clear();
+  if (notify) {
+    FeEvent e;
+    e.kind = FE_CLOSED;
+    e.conn = c.id;
+    post(std::move(e));
+  }
+}
+
+static void host_read(Frontend* fe, FeConn& c, std::atomic<u64>& rx, bool& eof, bool& notify) {
+  char buf[1 << 16];
+  for (;;) {
+    ssize_t k = ::recv(c.fd, buf, sizeof buf, 0);
+    if (k > 0) {
+      rx += (u64)k;
+      std::lock_guard<std::mutex> g(c.mu);
+      c.hostbuf.append(buf, (size_t)k);
+      if (!c.host_notified) { c.host_notified = true; notify = true; }
+      continue;
+    }
+    if (k == 0) eof = true;
+    else if (errno == EINTR) continue;
+    else if (errno != EAGAIN && errno != EWOULDBLOCK) eof = true;
+    break;
+  }
+  (void)fe;
+}
+
+void Frontend::io_loop(int i) {
+  FeIo& io = *io_[i];
+  char tname[16];
+  snprintf(tname, sizeof tname, "cmq-io%d", i);
+  pthread_setname_np(pthread_self(), tname);
+  epoll_event evs[512];
+  while (true) {
+    const bool run = running_.load();
+    int n = epoll_wait(io.epfd, evs, 512, run ? 50 : 2);
+    // ---- queued requests
+    std::vector<u32> adopt, pend, closing;
+    {
+      std::lock_guard<std::mutex> g(io.qmu);
+      adopt.swap(io.adopt);
+      pend.swap(io.pending);
+      closing.swap(io.closing);
+    }
+    for (u32 id : adopt) {
+      FeConn& c = *conns_[id];
+      io.owned.push_back(id);
+      epoll_event ev{};
+      ev.events = EPOLLIN | EPOLLOUT | EPOLLRDHUP | EPOLLET;
+      ev.data.u64 = id;
+      epoll_ctl(io.epfd, EPOLL_CTL_ADD, c.fd, &ev);
+    }
+    for (u32 id : pend) {
+      FeConn& c = *conns_[id];
+      if (c.mode == M_DATA) {
+        if (!c.in_ready) { c.in_ready = true; io.ready.push_back(id); }
+      } else if (c.mode == M_HOST && c.fd >= 0) {
+        bool eof = false, notify = false;
+        host_read(this, c, rx_bytes_, eof, notify);
+        if (notify) { FeEvent e; e.kind = FE_HOST; e.conn = id; post(std::move(e)); }
+        if (eof) drop(c, true);
+      }
+    }
+    for (u32 id : closing) {
+      FeConn& c = *conns_[id];
+      {
+        std::lock_guard<std::mutex> g(c.mu);
+        if (c.fd >= 0) {
+          write_some(c);
+          epoll_ctl(io.epfd, EPOLL_CTL_DEL, c.fd, nullptr);
+          ::close(c.fd);
+          c.fd = -1;
+        }
+        c.mode = M_FREE;
+        c.out.clear();
+        c.out_pos = 0;
+        c.inject.clear();
+        c.hostbuf.clear();
+      }
+      c.in_ready = false;
+      io.owned.erase(std::remove(io.owned.begin(), io.owned.end(), id), io.owned.end());
+      io.ready.erase(std::remove(io.ready.begin(), io.ready.end(), id), io.ready.end());
+      std::lock_guard<std::mutex> g(free_mu_);
+      free_.push_back(id);
+    }
+    // ---- socket events
+    bool data_ready = false;
+    for (int k = 0; k < n; ++k) {
+      u64 id = evs[k].data.u64;
+      if (id == WAKE) {
+        u64 v;
+        while (::read(io.evfd, &v, 8) > 0) {
+        }
+        continue;
+      }
+      if (id == LISTENER) { accept_all(io); continue; }
+      FeConn& c = *conns_[id];
+      if (c.fd < 0) continue;
+      const u32 e = evs[k].events;
+      if (e & EPOLLOUT) {
+        std::lock_guard<std::mutex> g(c.mu);
+        if (c.fd >= 0 && c.out_pos < c.out.size()) write_some(c);
+      }
+      if (e & (EPOLLRDHUP | EPOLLHUP | EPOLLERR)) c.rdhup = true;
+      if (!(e & (EPOLLIN | EPOLLRDHUP | EPOLLHUP | EPOLLERR))) continue;
+      c.last_rx = now_ns();
+      const int m = c.mode;
+      if (m == M_DATA) {
+        if (!c.in_ready) { c.in_ready = true; io.ready.push_back((u32)id); }
+        data_ready = true;
+      } else if (m == M_HOST) {
+        bool eof = false, notify = false;
+        host_read(this, c, rx_bytes_, eof, notify);
+        if (notify) { FeEvent ev; ev.kind = FE_HOST; ev.conn = (u32)id; post(std::move(ev)); }
+        if (eof) drop(c, true);
+      }
+    }
+    if (data_ready) wake_stepper();
+    // ---- IO phase requested by the stepper
+    const u64 ph = ph_id_.load(std::memory_order_acquire);
+    if (ph != io.phase_seen) {
+      io.phase_seen = ph;
+      io.segs.clear();
+      // scatter: the egress of finished steps, in step order, for this thread's connections
+      for (Scatter* sc : *ph_scat_) {
+        const u8* base = sc->own.empty() ? sc->egress : (const u8*)sc->own.data();
+        for (u32 id : io.owned) {
+          const ConnOut& o = sc->co[id];
+          if (o.len) {
+            FeConn& c = *conns_[id];
+            if (c.mode == M_DATA || c.mode == M_HOST) scatter_conn(c, base + o.off, o.len);
+          }
+        }
+      }
+      if (ph_gather_) {
+        std::vector<u32> keep;
+        for (u32 id : io.ready) {
+          FeConn& c = *conns_[id];
+          c.in_ready = false;
+          if (c.mode != M_DATA) continue;
+          gather_conn(io, c, ph_arena_, ph_cap_);
+          if (c.in_ready) keep.push_back(id);
+        }
+        io.ready.swap(keep);
+      }
+      if (ph_left_.fetch_sub(1) == 1) {
+        std::lock_guard<std::mutex> g(ph_mu_);
+        ph_cv_.notify_all();
+      }
+    }
+    if (!run && stepper_done_) break;
+    // ---- heartbeats (every 100 ms): send when idle for hb/2, drop after 2*hb of silence
+    const i64 t = now_ns();
+    if (t - io.last_hb > 100000000) {
+      io.last_hb = t;
+      for (u32 id : io.owned) {
+        FeConn& c = *conns_[id];
+        const u32 hb = c.hb_s;
+        if (!hb || c.fd < 0) continue;
+        const i64 hbn = (i64)hb * 1000000000;
+        if (t - c.last_rx > 2 * hbn) { drop(c, true); continue; }
+        if (t - c.last_tx >= hbn / 2) {
+          std::lock_guard<std::mutex> g(c.mu);
+          if (c.out_pos >= c.out.size()) {
+            c.out.append(HEARTBEAT_FRAME, 8);
+            write_some(c);
+          }
+        }
+      }
+    }
+  }
+}
+
+// one connection's bytes for this step: queued inject bytes, then what its socket holds,
+// within the per-connection budget; reserved densely in the shared arena
+void Frontend::gather_conn(FeIo& io, FeConn& c, u8* arena, u64 cap) {
+  u64 lim = cfg_.per_conn_read;
+  const u64 room = api_->carry_cap > (u64)c.carry + c.inflight ? api_->carry_cap - c.carry - c.inflight : 0;
+  if (lim > room) lim = room;
+  if (c.paused) {   // behind a control command: bytes wait in the socket (TCP back-pressure)
+    c.in_ready = true;
+    return;
+  }
+  std::string inj;
+  {
+    std::lock_guard<std::mutex> g(c.mu);
+    if (!c.inject.empty()) {
+      if (c.inject.size() <= lim) inj.swap(c.inject);
+      else { inj = c.inject.substr(0, lim); c.inject.erase(0, lim); c.in_ready = true; }
+    }
+  }
+  int avail = 0;
+  if (c.fd >= 0 && ioctl(c.fd, FIONREAD, &avail) < 0) avail = 0;
+  u64 want = (u64)avail;
+  if (inj.size() + want > lim) { want = lim > inj.size() ? lim - inj.size() : 0; if (avail) c.in_ready = true; }
+  const u64 total = inj.size() + want;
+  const bool eof = avail == 0 && c.rdhup;
+  if (total == 0 && !c.kicked) {
+    if (eof) drop(c, true);
+    return;
+  }
+  // reserve a segment slot and arena bytes
+  const u32 si = ph_nseg_.fetch_add(1);
+  if (si >= api_->seg_max) {
+    ph_nseg_.fetch_sub(1);
+    std::lock_guard<std::mutex> g(c.mu);
+    c.inject.insert(0, inj);
+    c.in_ready = true;
+    return;
+  }
+  const u64 need = (total + 15) & ~15ull;
+  u64 off = ph_used_.load();
+  while (true) {
+    if (off + need > cap) {
+      ph_nseg_.fetch_sub(1);
+      std::lock_guard<std::mutex> g(c.mu);
+      c.inject.insert(0, inj);
+      c.in_ready = true;
+      return;
+    }
+    if (ph_used_.compare_exchange_weak(off, off + need)) break;
+  }
+  u8* dst = arena + off;
+  if (!inj.empty()) memcpy(dst, inj.data(), inj.size());
+  u64 got = 0;
+  while (got < want) {
+    ssize_t k = ::recv(c.fd, dst + inj.size() + got, want - got, 0);
+    if (k > 0) { got += (u64)k; continue; }
+    if (k < 0 && errno == EINTR) continue;
+    break;
+  }
+  const u64 len = inj.size() + got;
+  rx_bytes_ += got;
+  if (got) c.last_rx = now_ns();
+  c.kicked = false;
+  io.segs.push_back(SegIn{c.id, (u32)len, off});
+  if (eof && !c.in_ready) drop(c, true);
+}
+
+void Frontend::io_phase(std::vector<Scatter*>& scat, bool gather) {
+  ph_scat_ = &scat;
+  ph_gather_ = gather;
+  ph_arena_ = arena_[arena_i_];
+  ph_cap_ = api_->ingress_cap;
+  ph_used_ = 0;
+  ph_nseg_ = 0;
+  ph_left_ = (int)io_.size();
+  ph_id_.fetch_add(1, std::memory_order_release);
+  for (auto& io : io_) poke(io->evfd);
+  std::unique_lock<std::mutex> g(ph_mu_);
+  ph_cv_.wait(g, [&] { return ph_left_.load() == 0; });
+}
+
+// ============================================================================ stepper
+void Frontend::finish_oldest(std::deque<Inflight>& inflight) {
+  if (pend_valid_ && !stash_pend(true)) return;   // its egress is written by the next IO phase
+  Inflight f = std::move(inflight.front());
+  inflight.pop_front();
+  const int p = f.p;
+  i64 t0 = now_ns();
+  if (!check(api_->wait_results(api_->eng, p))) return;
+  double w = secs_since(t0);
+  const Counters& c = *api_->counters(api_->eng, p);
+  const SegOut* so = api_->seg_out(api_->eng, p);
+  for (size_t k = 0; k < f.segs.size(); ++k) {
+    const SegOut& s = so[k];
+    if (s.conn >= c_max_) continue;
+    FeConn& cc = *conns_[s.conn];
+    cc.carry = s.carry;
+    const u32 len = f.segs[k].second;
+    cc.inflight = cc.inflight > len ? cc.inflight - len : 0;
+    if (s.status & SS_CTRL) cc.paused = true;
+    if (s.status & (SS_FRAME_ERROR | SS_UNEXPECTED | SS_TOO_LARGE)) {
+      FeEvent e;
+      e.kind = FE_STATUS;
+      e.conn = s.conn;
+      e.a = s.status;
+      post(std::move(e));
+    }
+    if (cc.carry && !cc.paused && !(s.status & (SS_FRAME_ERROR | SS_UNEXPECTED | SS_TOO_LARGE)) &&
+        (s.status & SS_OVERFLOW)) {   // per-step capacity hit: re-present the carry next step
+      cc.kicked = true;
+      FeIo& io = *io_[cc.io];
+      std::lock_guard<std::mutex> g(io.qmu);
+      io.pending.push_back(s.conn);
+    }
+  }
+  u32 nc = c.n_ctrl;
+  if (nc > api_->seg_max * 2) nc = api_->seg_max * 2;
+  if (nc) {
+    const CtrlRec* cr = api_->ctrl_rec(api_->eng, p);
+    const u8* cb = api_->ctrl(api_->eng, p);
+    for (u32 k = 0; k < nc; ++k) {
+      FeEvent e;
+      e.conn = cr[k].conn;
+      if (cr[k].off == 0xffffffffu) {
+        e.kind = FE_EVENT;
+        e.a = cr[k].len;
+        e.b = cr[k].seg;
+      } else if (cr[k].seg & CTRL_TXBUF) {
+        e.kind = FE_TXBUF;
+        e.a = cr[k].seg & ~CTRL_TXBUF;
+        e.data.assign((const char*)cb + cr[k].off, cr[k].len);
+      } else {
+        e.kind = FE_CTRL;
+        e.data.assign((const char*)cb + cr[k].off, cr[k].len);
+      }
+      post(std::move(e));
+    }
+  }
+  bool needs_commit = false;
+  if (api_->persist && (c.n_persist || c.n_consumed)) {
+    FeEvent e;
+    e.kind = FE_PERSIST;
+    e.a = f.step;
+    e.b = c.n_persist_overflow || c.n_persist > api_->persist_max;
+    const u32 np = std::min(c.n_persist, api_->persist_max), ncs = std::min(c.n_consumed, api_->persist_max);
+    if (np) e.data.assign((const char*)api_->persist_host(api_->eng, p), c.persist_used);
+    if (ncs) e.data2.assign((const char*)api_->consumed_host(api_->eng, p), (size_t)ncs * sizeof(ConsumedRec));
+    post(std::move(e));
+    needs_commit = true;
+  }
+  const int slot = api_->egress_slot(api_->eng, p);
+  const ConnOut* co = api_->conn_out(api_->eng, p);
+  Held h;
+  h.step = f.step;
+  h.needs_commit = needs_commit;
+  h.sc.co.assign(co, co + c_max_);
+  h.sc.egress = api_->egress_host(api_->eng, slot);
+  if (c.egress_bytes && !check(api_->egress_copy(api_->eng, p))) return;
+  {
+    std::lock_guard<std::mutex> g(stats_mu_);
+    stats_.steps++;
+    stats_.published += c.n_pubs;
+    stats_.delivered += c.n_deliv;
+    stats_.egress_bytes += c.egress_bytes;
+    stats_.live_bytes = c.live_bytes;
+    stats_.wait_s += w;
+    for (int k = 0; k < 32; ++k) stats_.lat_hist[k] += c.lat_hist[k];
+    if (needs_commit) stats_.held_steps++;
+  }
+  // busy: keep stepping while the device still has work (backlog, carry, deliveries)
+  bool busy = !f.segs.empty() || c.n_deliv || c.egress_bytes || c.n_ctrl;
+  pend_slot_ = slot;
+  pend_valid_ = true;
+  pend_bytes_ = c.egress_bytes;
+  pend_ = std::move(h);
+  last_busy_ = busy;
+}
+
+void Frontend::stepper() {
+  pthread_setname_np(pthread_self(), "cmq-stepper");
+  std::deque<Inflight> inflight;
+  i64 last_step = now_ns();
+  while (running_ && !failed_) {
+    // ---- exclusive access for the control plane: drain, write out, park
+    bool want_pause;
+    {
+      std::lock_guard<std::mutex> g(st_mu_);
+      want_pause = pause_req_ > 0;
+    }
+    if (want_pause) {
+      while (!inflight.empty() && !failed_) finish_oldest(inflight);
+      flush_pending(false);
+      std::unique_lock<std::mutex> g(st_mu_);
+      paused_ = true;
+      pause_cv_.notify_all();
+      st_cv_.wait(g, [&] { return pause_req_ == 0 || !running_; });
+      paused_ = false;
+      wake_ = true;
+      continue;
+    }
+    // ---- idle: nothing in flight, nothing to write, nothing readable
+    if (inflight.empty() && !pend_valid_ && out_.empty() && !last_busy_ && !releasable()) {
+      std::unique_lock<std::mutex> g(st_mu_);
+      const double idle = cfg_.idle_step_ms > 0 ? cfg_.idle_step_ms : 1000.0;
+      st_cv_.wait_for(g, std::chrono::microseconds((i64)(idle * 1000)),
+                      [&] { return wake_ || pause_req_ > 0 || !running_; });
+      bool woke = wake_;
+      wake_ = false;
+      if (pause_req_ > 0 || !running_) continue;
+      if (!woke) {
+        if (now_ns() - last_step < (i64)(idle * 1e6)) continue;
+        idle_tick_ = any_data_conn();
+        if (!idle_tick_) { last_step = now_ns(); continue; }
+      }
+    } else {
+      std::lock_guard<std::mutex> g(st_mu_);
+      wake_ = false;
+    }
+    // ---- IO phase: write the oldest finished step's egress, gather the next step
+    std::vector<Scatter*> scat;
+    if (!collect_scatter(scat)) break;
+    i64 t0 = now_ns();
+    io_phase(scat, true);
+    double tio = secs_since(t0);
+    scat_done();
+    std::vector<SegIn> segs;
+    std::vector<std::pair<u32, u32>> seglens;
+    for (auto& io : io_) {
+      for (auto& s : io->segs) {
+        segs.push_back(s);
+        seglens.emplace_back(s.conn, s.len);
+        conns_[s.conn]->inflight += s.len;
+      }
+    }
+    const u64 used = ph_used_.load();
+    const bool submit = !segs.empty() || last_busy_ || idle_tick_;
+    idle_tick_ = false;
+    bool submitted = false;
+    if (submit) {
+      if (inflight.size() >= 2) finish_oldest(inflight);
+      if (failed_) break;
+      i64 t1 = now_ns();
+      int p = api_->submit(api_->eng, segs.data(), (u32)segs.size(), arena_[arena_i_], used, wall_ms(), cfg_.worker);
+      if (!check(p)) break;
+      {
+        std::lock_guard<std::mutex> g(stats_mu_);
+        stats_.submit_s += secs_since(t1);
+        stats_.io_phase_s += tio;
+        stats_.gather_segs += segs.size();
+        if (segs.empty() && !last_busy_) stats_.idle_steps++;
+      }
+      Inflight f;
+      f.p = p;
+      f.step = ++step_no_;
+      f.segs = std::move(seglens);
+      inflight.push_back(std::move(f));
+      arena_i_ = (arena_i_ + 1) % 3;
+      last_step = now_ns();
+      submitted = true;
+      last_busy_ = false;
+    }
+    // ---- results: the older step once two are in flight (or when nothing new went out)
+    if (inflight.size() >= 2 || (!submitted && !inflight.empty())) finish_oldest(inflight);
+  }
+  // stopping: complete what is in flight so the engine is idle
+  while (!inflight.empty() && !failed_) finish_oldest(inflight);
+  flush_pending(true);
+  stepper_done_ = true;
+  std::lock_guard<std::mutex> g(st_mu_);
+  paused_ = true;
+  pause_cv_.notify_all();
+}
+
+// the finished step's egress (D2H complete) and any released held steps, oldest first
+bool Frontend::stash_pend(bool copy) {
+  if (!pend_valid_) return true;
+  pend_valid_ = false;
+  if (pend_bytes_ && !check(api_->egress_wait_slot(api_->eng, pend_slot_))) return false;
+  const bool hold = pend_.needs_commit || !held_.empty();
+  if (hold || copy) {   // write-behind (or the slot may be reused before it is written): copy
+    pend_.sc.own.assign((const char*)pend_.sc.egress, pend_bytes_);
+    pend_.sc.egress = nullptr;
+  }
+  if (hold) held_.push_back(std::move(pend_));
+  else out_.push_back(std::move(pend_.sc));
+  return true;
+}
+
+bool Frontend::collect_scatter(std::vector<Scatter*>& scat) {
+  if (!stash_pend(false)) return false;
+  const u64 rel = released_.load();
+  while (!held_.empty() && (!held_.front().needs_commit || held_.front().step <= rel)) {
+    out_.push_back(std::move(held_.front().sc));
+    held_.pop_front();
+  }
+  for (auto& sc : out_) scat.push_back(&sc);
+  return true;
+}
+
+bool Frontend::releasable() const {
+  return !held_.empty() && (!held_.front().needs_commit || held_.front().step <= released_.load());
+}
+
+bool Frontend::any_data_conn() const {
+  for (auto& c : conns_)
+    if (c->mode == M_DATA) return true;
+  return false;
+}
+
+void Frontend::flush_pending(bool final) {
+  if (final) {   // shutting down: the engine goes idle, nothing more is written
+    if (pend_valid_ && pend_bytes_) api_->egress_wait_slot(api_->eng, pend_slot_);
+    pend_valid_ = false;
+    out_.clear();
+    return;
+  }
+  std::vector<Scatter*> scat;
+  if (!collect_scatter(scat)) return;
+  if (!scat.empty()) io_phase(scat, false);
+  scat_done();
+}
+
+// ============================================================================ EchoEngine
+EchoEngine::EchoEngine(u32 c_max, u32 seg_max, u64 ingress_cap, u32 carry_cap) {
+  api_.abi = CMQ_STEP_ABI;
+  api_.c_max = c_max;
+  api_.seg_max = seg_max;
+  api_.carry_cap = carry_cap;
+  api_.ingress_cap = ingress_cap;
+  api_.ctrl_cap = 1 << 20;
+  api_.eng = this;
+  paused_.assign(c_max, 0);
+  for (auto& io : io_) { io.so.resize(seg_max); io.co.resize(c_max); }
+  api_.submit = [](void* e, const SegIn* sg, u32 n, const u8* pay, u64 len, i64, u32) -> int {
+    EchoEngine& E = *(EchoEngine*)e;
+    const int p = (int)(E.seq_ & 1);
+    const int slot = (int)(E.seq_ % 3);
+    E.slot_of_[p] = slot;
+    ++E.seq_;
+    ++E.steps;
+    Io& io = E.io_[p];
+    io.ctr = Counters{};
+    io.cr.clear();
+    io.ctrl.clear();
+    std::fill(io.co.begin(), io.co.end(), ConnOut{0, 0});
+    std::string& eg = E.slot_[slot];
+    eg.clear();
+    if (n > E.api_.seg_max) { E.err_ = "too many segments"; return -1; }
+    for (u32 k = 0; k < n; ++k) {
+      const SegIn& s = sg[k];
+      if (s.src + s.len > len) { E.err_ = "segment outside the payload"; return -1; }
+      SegOut o{};
+      o.conn = s.conn;
+      std::string b((const char*)pay + s.src, s.len);
+      if (E.paused_[s.conn]) o.status = SS_PAUSED;
+      size_t cpos = b.find("CTRL");
+      if (!E.paused_[s.conn] && cpos != std::string::npos) {   // control command: pause, hand to host
+        CtrlRec r{s.conn, (u32)io.ctrl.size(), 4, (u32)k};
+        io.ctrl += "CTRL";
+        io.cr.push_back(r);
+        o.status |= SS_CTRL;
+        E.paused_[s.conn] = 1;
+        b.resize(cpos);
+      }
+      if (!b.empty() && !(o.status & SS_PAUSED)) {
+        io.co[s.conn] = ConnOut{(u32)eg.size(), (u32)b.size()};
+        eg += b;
+        io.ctr.n_deliv++;
+      }
+      io.so[k] = o;
+    }
+    io.ctr.n_ctrl = (u32)io.cr.size();
+    io.ctr.egress_bytes = (u32)eg.size();
+    return p;
+  };
+  api_.wait_results = [](void*, int) -> int { return 0; };
+  api_.egress_slot = [](void* e, int p) -> int { return ((EchoEngine*)e)->slot_of_[p]; };
+  api_.egress_copy = [](void*, int) -> int { return 0; };
+  api_.egress_wait_slot = [](void*, int) -> int { return 0; };
+  api_.error = [](void* e) -> const char* { return ((EchoEngine*)e)->err_.c_str(); };
+  api_.counters = [](void* e, int p) -> const Counters* { return &((EchoEngine*)e)->io_[p].ctr; };
+  api_.seg_out = [](void* e, int p) -> const SegOut* { return ((EchoEngine*)e)->io_[p].so.data(); };
+  api_.conn_out = [](void* e, int p) -> const ConnOut* { return ((EchoEngine*)e)->io_[p].co.data(); };
+  api_.ctrl_rec = [](void* e, int p) -> const CtrlRec* { return ((EchoEngine*)e)->io_[p].cr.data(); };
+  api_.ctrl = [](void* e, int p) -> const u8* { return (const u8*)((EchoEngine*)e)->io_[p].ctrl.data(); };
+  api_.egress_host = [](void* e, int slot) -> const u8* { return (const u8*)((EchoEngine*)e)->slot_[slot].data(); };
+  api_.persist_host = [](void*, int) -> const u8* { return nullptr; };
+  api_.consumed_host = [](void*, int) -> const ConsumedRec* { return nullptr; };
+}
+
+void EchoEngine::unpause(u32 conn) {
+  if (conn < paused_.size()) paused_[conn] = 0;
+}
+
+}  // namespace cmq

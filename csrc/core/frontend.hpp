@@ -122,6 +122,12 @@ class Frontend {
   void io_loop(int i);
   void io_phase(std::vector<Scatter*>& scat, bool gather);
   void finish_oldest(std::deque<Inflight>& inflight);
+  bool collect_scatter(std::vector<Scatter*>& scat);
+  bool stash_pend(bool copy);
+  void scat_done() { out_.clear(); }
+  void flush_pending(bool final);
+  bool releasable() const;
+  bool any_data_conn() const;
   void post(FeEvent&& e);
   void wake_stepper();
   void accept_all(FeIo& io);
@@ -170,6 +176,15 @@ class Frontend {
   std::condition_variable ev_cv_;
   std::deque<FeEvent> events_;
 
+  // finished step whose egress D2H is in flight
+  Held pend_;
+  bool pend_valid_ = false;
+  int pend_slot_ = 0;
+  u64 pend_bytes_ = 0;
+  bool last_busy_ = false, idle_tick_ = false;
+  std::deque<Scatter> out_;   // egress being written in the current IO phase
+  std::atomic<bool> stepper_done_{false};
+
   // persistence write-behind
   std::deque<Held> held_;
   std::atomic<u64> released_{0};
@@ -189,6 +204,7 @@ class EchoEngine {
  public:
   EchoEngine(u32 c_max, u32 seg_max, u64 ingress_cap, u32 carry_cap);
   u64 c_api() { return (u64)&api_; }
+  void unpause(u32 conn);
   u64 steps = 0;
 
  private:

@@ -1,11 +1,20 @@
 // Native AMQP load generator: the RabbitMQ PerfTest(Multi) shapes of
 // chana-mq-test/perf/publish-consume-spec*.js (producer/consumer counts, minMsgSize,
-// auto-ack, channel-prefetch, persistent, time-limit), run against any AMQP 0-9-1 broker.
-// Producers stamp a steady-clock send time into the first 8 body bytes; consumers
-// histogram publish->deliver latency.
+// auto-ack, channel-prefetch, persistent, confirms, time-limit, producer rate), run against
+// any AMQP 0-9-1 broker.
+//
+// Connections are opened blocking (handshake, qos, consume), then driven non-blocking by
+// `threads` epoll loops.  Producers send pre-rendered batches of publishes whose bodies
+// carry a steady-clock send timestamp in their first 8 bytes (patched in place per batch);
+// consumers parse frames in place in one receive buffer and histogram publish->deliver
+// latency; manual-ack consumers ack with multiple=true every prefetch/2 deliveries and
+// whenever their receive buffer runs dry.  Channel.Flow(active=false) from the broker pauses
+// the connection's publishing (and is answered with FlowOk).
 #include <arpa/inet.h>
+#include <fcntl.h>
 #include <netinet/in.h>
 #include <netinet/tcp.h>
+#include <sys/epoll.h>
 #include <sys/socket.h>
 #include <unistd.h>
 
@@ -14,8 +23,9 @@
 #include <chrono>
 #include <cmath>
 #include <cstring>
-#include <string>
+#include <memory>
 #include <mutex>
+#include <string>
 #include <thread>
 #include <vector>
 
@@ -63,13 +73,11 @@ struct Client {
   }
   void flush() { if (!out.empty()) { send_all(out); out.clear(); } }
   void method(u16 ch, const Method& m) { append_method_frame(out, ch, m); }
-  // read one frame (blocking)
   bool frame(Frame& f, int timeout_ms = 10000) {
+    timeval tv{timeout_ms / 1000, (timeout_ms % 1000) * 1000};
+    setsockopt(fd, SOL_SOCKET, SO_RCVTIMEO, &tv, sizeof tv);
     while (!parser.next(in, pos, f)) {
-      if (pos > (1u << 20)) { in.erase(0, pos); pos = 0; }
       char buf[1 << 16];
-      timeval tv{timeout_ms / 1000, (timeout_ms % 1000) * 1000};
-      setsockopt(fd, SOL_SOCKET, SO_RCVTIMEO, &tv, sizeof tv);
       ssize_t k = ::recv(fd, buf, sizeof buf, 0);
       if (k <= 0) return false;
       in.append(buf, (size_t)k);
@@ -137,10 +145,36 @@ struct Hist {   // log2-spaced microsecond buckets with 8 sub-buckets each
     u64 want = (u64)std::ceil(p * n), acc = 0;
     for (size_t i = 0; i < b.size(); ++i) {
       acc += b[i];
-      if (acc >= want) return std::pow(2.0, (double)i / 8.0);
+      if (acc >= want) return std::pow(2.0, (double)(i + 1) / 8.0);   // bucket upper edge
     }
     return 0;
   }
+};
+
+u64 rd64(const u8* p) { u64 v = 0; for (int i = 0; i < 8; ++i) v = (v << 8) | p[i]; return v; }
+u32 rd32(const u8* p) { return (u32(p[0]) << 24) | (u32(p[1]) << 16) | (u32(p[2]) << 8) | p[3]; }
+
+// one non-blocking AMQP connection after setup
+struct Peer {
+  Client cl;
+  bool producer = false;
+  // producer: pre-rendered batch, body-timestamp offsets, pending output
+  std::string batch;
+  std::vector<size_t> ts_off;
+  std::string out;
+  size_t out_pos = 0;
+  std::atomic<u64> sent{0}, confirmed{0}, nacked{0};
+  bool flow = true;
+  // any: receive buffer parsed in place
+  std::string in;
+  size_t pos = 0;
+  // consumer
+  bool want_body = false;
+  u64 body_left = 0, last_tag = 0, unacked = 0;
+  std::atomic<u64> recv{0};
+  u8 ts[8];
+  u32 tsn = 0;
+  bool writable = true;
 };
 
 }  // namespace
@@ -184,151 +218,257 @@ LoadResult run_load(const LoadSpec& s) {
     }
     a.close();
   }
+  const int nq = std::max(1, s.queues);
+  std::vector<std::unique_ptr<Peer>> peers;
+  // consumers first: they are attached before any message is published
+  for (int ci = 0; ci < s.consumers; ++ci) {
+    std::unique_ptr<Peer> p(new Peer());
+    p->cl.open(s.host, s.port, s.vhost);
+    Method qos = make_method(60, 10);
+    qos.args[1].i = s.prefetch;
+    p->cl.method(1, qos);
+    p->cl.flush();
+    p->cl.expect(60, 11);
+    Method cm = make_method(60, 20);
+    cm.args[1].s = s.queues > 1 ? s.queue + "." + std::to_string(ci % nq) : s.queue;
+    cm.args[2].s = "lg-" + std::to_string(ci);
+    cm.args[4].i = s.auto_ack;
+    p->cl.method(1, cm);
+    p->cl.flush();
+    p->cl.expect(60, 21);
+    p->in = p->cl.in.substr(p->cl.pos);   // deliveries may already follow ConsumeOk
+    peers.push_back(std::move(p));
+  }
+  // producers: batch of K publishes, keys cycling over the queues
+  const double rate = s.rate;   // msgs/s per producer (0 = unthrottled)
+  int K = 64;
+  if (rate > 0) K = std::max(1, std::min(64, (int)(rate * 0.0005)));   // <= 0.5 ms of traffic per batch
+  for (int pi = 0; pi < s.producers; ++pi) {
+    std::unique_ptr<Peer> p(new Peer());
+    p->producer = true;
+    p->cl.open(s.host, s.port, s.vhost);
+    if (s.confirm) {
+      p->cl.method(1, make_method(85, 10));
+      p->cl.flush();
+      p->cl.expect(85, 11);
+    }
+    std::string props = encode_props_simple(s.persistent ? 2 : 1);
+    std::string body(std::max(s.msg_size, 0), 'x');
+    for (int k = 0; k < K; ++k) {
+      u64 seq = (u64)pi * 7 + k;
+      Method pm = make_method(60, 40);
+      pm.args[1].s = s.exchange;
+      if (s.exchange.empty()) pm.args[2].s = s.queues > 1 ? s.queue + "." + std::to_string(seq % nq) : s.queue;
+      else if (s.queues > 1) pm.args[2].s = s.routing_key + "." + std::to_string(seq % nq) + (s.exchange_type == "topic" ? ".x" : "");
+      else pm.args[2].s = s.routing_key;
+      append_method_frame(p->batch, 1, pm);
+      size_t before = p->batch.size();
+      append_content(p->batch, 1, 60, props, body, p->cl.frame_max);
+      if (body.size() >= 8) {   // first body frame payload: after the header frame
+        size_t hdr = 7 + 12 + props.size() + 1;
+        p->ts_off.push_back(before + hdr + 7);
+      }
+    }
+    p->in = p->cl.in.substr(p->cl.pos);
+    peers.push_back(std::move(p));
+  }
+  for (auto& p : peers) {
+    int fl = fcntl(p->cl.fd, F_GETFL);
+    fcntl(p->cl.fd, F_SETFL, fl | O_NONBLOCK);
+    timeval tv{0, 0};
+    setsockopt(p->cl.fd, SOL_SOCKET, SO_RCVTIMEO, &tv, sizeof tv);
+  }
+  int nthreads = s.threads > 0 ? s.threads : std::min<int>(8, (int)peers.size());
+  nthreads = std::max(1, std::min<int>(nthreads, (int)peers.size()));
   std::atomic<bool> stop{false};
-  std::atomic<int> ready{0};
-  std::vector<std::thread> th;
-  std::vector<u64> sent(s.producers, 0), recv(s.consumers, 0), confirmed(s.producers, 0);
-  std::vector<Hist> hists(s.consumers);
   std::string err;
   std::mutex err_mu;
-  auto fail = [&](const std::exception& e) { std::lock_guard<std::mutex> g(err_mu); if (err.empty()) err = e.what(); stop = true; };
+  std::vector<Hist> hists(nthreads);
+  const i64 t_start = mono_ns();
+  const u64 ack_every = (u64)std::max(1, s.prefetch / 2);
 
-  for (int ci = 0; ci < s.consumers; ++ci) {
-    th.emplace_back([&, ci] {
-      try {
-        Client c;
-        c.open(s.host, s.port, s.vhost);
-        Method qos = make_method(60, 10);
-        qos.args[1].i = s.prefetch;
-        c.method(1, qos);
-        c.flush();
-        c.expect(60, 11);
-        int nq = std::max(1, s.queues);
-        std::string qn = s.queues > 1 ? s.queue + "." + std::to_string(ci % nq) : s.queue;
-        Method cm = make_method(60, 20);
-        cm.args[1].s = qn;
-        cm.args[2].s = "lg-" + std::to_string(ci);
-        cm.args[4].i = s.auto_ack;
-        c.method(1, cm);
-        c.flush();
-        c.expect(60, 21);
-        ++ready;
-        Frame f;
-        u64 unacked = 0, last_tag = 0;
-        bool want_body = false;
-        u64 body_left = 0;
-        std::string body;
-        while (!stop) {
-          if (!c.frame(f, 200)) continue;
-          if (f.type == FRAME_METHOD) {
-            const u8* p = (const u8*)f.payload.data();
-            u16 cls = (u16(p[0]) << 8) | p[1], mid = (u16(p[2]) << 8) | p[3];
-            if (cls == 60 && mid == 60) {
-              Method m = decode_method(p, f.payload.size());
-              last_tag = (u64)m.i(1);
-              want_body = true;
+  auto worker = [&](int ti) {
+    try {
+      int ep = epoll_create1(0);
+      std::vector<Peer*> mine;
+      for (size_t i = ti; i < peers.size(); i += nthreads) {
+        Peer* p = peers[i].get();
+        mine.push_back(p);
+        epoll_event ev{};
+        ev.events = EPOLLIN | EPOLLET | (p->producer ? EPOLLOUT : 0);
+        ev.data.ptr = p;
+        epoll_ctl(ep, EPOLL_CTL_ADD, p->cl.fd, &ev);
+      }
+      Hist& h = hists[ti];
+      epoll_event evs[256];
+      std::vector<char> rbuf(1 << 20);
+      bool any_producer = false;
+      for (Peer* p : mine) any_producer |= p->producer;
+      auto pump = [&](Peer* p) {   // producer: send until the socket is full or paced out
+        while (!stop && p->flow) {
+          if (p->out_pos >= p->out.size()) {
+            if (rate > 0 && (double)(p->sent.load(std::memory_order_relaxed) + K) > rate * ((mono_ns() - t_start) * 1e-9)) return;
+            p->out = p->batch;
+            const i64 t = mono_ns();
+            for (size_t o : p->ts_off) memcpy(&p->out[o], &t, 8);
+            p->out_pos = 0;
+            p->sent.fetch_add((u64)K, std::memory_order_relaxed);
+          }
+          ssize_t k = ::send(p->cl.fd, p->out.data() + p->out_pos, p->out.size() - p->out_pos, MSG_NOSIGNAL);
+          if (k > 0) { p->out_pos += (size_t)k; continue; }
+          if (k < 0 && errno == EINTR) continue;
+          if (k < 0 && (errno == EAGAIN || errno == EWOULDBLOCK)) { p->writable = false; return; }
+          throw std::runtime_error("loadgen: producer send failed");
+        }
+      };
+      auto send_small = [&](Peer* p, const std::string& b) {   // acks / FlowOk: tiny, retry until written
+        size_t o = 0;
+        while (o < b.size() && !stop) {
+          ssize_t k = ::send(p->cl.fd, b.data() + o, b.size() - o, MSG_NOSIGNAL);
+          if (k > 0) o += (size_t)k;
+          else if (k < 0 && (errno == EAGAIN || errno == EINTR)) std::this_thread::yield();
+          else throw std::runtime_error("loadgen: send failed");
+        }
+      };
+      auto parse = [&](Peer* p) {
+        const u8* b = (const u8*)p->in.data();
+        size_t n = p->in.size(), pos = p->pos;
+        while (n - pos >= 8) {
+          u32 size = rd32(b + pos + 3);
+          if (n - pos < (size_t)size + 8) break;
+          const u8 type = b[pos];
+          const u8* pl = b + pos + 7;
+          if (b[pos + 7 + size] != 0xCE) throw std::runtime_error("loadgen: bad frame end");
+          if (type == FRAME_METHOD && size >= 4) {
+            u16 cls = (u16(pl[0]) << 8) | pl[1], mid = (u16(pl[2]) << 8) | pl[3];
+            if (cls == 60 && mid == 60) {             // Basic.Deliver
+              u32 tl = pl[4];
+              p->last_tag = rd64(pl + 5 + tl);
+              p->want_body = true;
+              p->tsn = 0;
+            } else if (cls == 60 && (mid == 80 || mid == 120)) {   // confirm Ack / Nack
+              u64 tag = rd64(pl + 4);
+              bool multiple = pl[12] & 1;
+              u64 before = p->confirmed.load(std::memory_order_relaxed) + p->nacked.load(std::memory_order_relaxed);
+              u64 cnt = multiple ? (tag > before ? tag - before : 0) : 1;
+              (mid == 80 ? p->confirmed : p->nacked).fetch_add(cnt, std::memory_order_relaxed);
+            } else if (cls == 20 && mid == 20) {      // Channel.Flow
+              p->flow = pl[4] & 1;
+              std::string fo;
+              Method m = make_method(20, 21);
+              m.args[0].i = p->flow;
+              append_method_frame(fo, 1, m);
+              send_small(p, fo);
+            } else if (cls == 10 && mid == 50) {
+              throw std::runtime_error("loadgen: connection closed by broker");
+            } else if (cls == 20 && mid == 40) {
+              throw std::runtime_error("loadgen: channel closed by broker");
             }
-          } else if (f.type == FRAME_HEADER && want_body) {
-            const u8* p = (const u8*)f.payload.data();
-            body_left = 0;
-            for (int i = 0; i < 8; ++i) body_left = (body_left << 8) | p[4 + i];
-            body.clear();
-            if (body_left == 0) { want_body = false; ++recv[ci]; ++unacked; }
-          } else if (f.type == FRAME_BODY && want_body) {
-            if (body.size() < 8) body.append(f.payload, 0, std::min<size_t>(8 - body.size(), f.payload.size()));
-            body_left -= f.payload.size();
-            if (body_left == 0) {
-              want_body = false;
-              ++recv[ci];
-              ++unacked;
-              if (body.size() >= 8) {
+          } else if (type == FRAME_HEADER && p->want_body && size >= 12) {
+            p->body_left = rd64(pl + 4);
+            if (p->body_left == 0) { p->want_body = false; p->recv.fetch_add(1, std::memory_order_relaxed); ++p->unacked; }
+          } else if (type == FRAME_BODY && p->want_body) {
+            if (p->tsn < 8) {
+              u32 take = std::min<u32>(8 - p->tsn, size);
+              memcpy(p->ts + p->tsn, pl, take);
+              p->tsn += take;
+            }
+            p->body_left -= std::min<u64>(p->body_left, size);
+            if (p->body_left == 0) {
+              p->want_body = false;
+              p->recv.fetch_add(1, std::memory_order_relaxed);
+              ++p->unacked;
+              if (p->tsn == 8) {
                 i64 t0;
-                memcpy(&t0, body.data(), 8);
-                hists[ci].add((mono_ns() - t0) / 1000.0);
+                memcpy(&t0, p->ts, 8);
+                h.add((mono_ns() - t0) / 1000.0);
               }
             }
           }
-          if (!s.auto_ack && unacked && (unacked >= (u64)std::max(1, s.prefetch / 2) || c.pos == c.in.size())) {
-            Method ak = make_method(60, 80);
-            ak.args[0].i = (i64)last_tag;
-            ak.args[1].i = 1;
-            c.method(1, ak);
-            c.flush();
-            unacked = 0;
-          }
+          pos += (size_t)size + 8;
         }
-        c.close();
-      } catch (std::exception& e) { fail(e); }
-    });
-  }
-  for (int i = 0; i < 500 && ready < s.consumers && !stop; ++i) std::this_thread::sleep_for(std::chrono::milliseconds(10));
-  i64 t_start = mono_ns();
-  for (int pi = 0; pi < s.producers; ++pi) {
-    th.emplace_back([&, pi] {
-      try {
-        Client c;
-        c.open(s.host, s.port, s.vhost);
-        if (s.confirm) {
-          c.method(1, make_method(85, 10));
-          c.flush();
-          c.expect(85, 11);
-        }
-        std::string props = encode_props_simple(s.persistent ? 2 : 1);
-        std::string body(std::max(s.msg_size, 0), 'x');
-        int nq = std::max(1, s.queues);
-        u64 seq = 0;
-        std::string x = s.exchange;
-        while (!stop) {
-          for (int k = 0; k < 64; ++k) {   // batch 64 publishes per send
-            if (body.size() >= 8) { i64 t = mono_ns(); memcpy(&body[0], &t, 8); }
-            Method pm = make_method(60, 40);
-            pm.args[1].s = x;
-            if (x.empty()) pm.args[2].s = s.queues > 1 ? s.queue + "." + std::to_string(seq % nq) : s.queue;
-            else if (s.queues > 1) pm.args[2].s = s.routing_key + "." + std::to_string(seq % nq) + (s.exchange_type == "topic" ? ".x" : "");
-            else pm.args[2].s = s.routing_key;
-            append_method_frame(c.out, 1, pm);
-            append_content(c.out, 1, 60, props, body, c.frame_max);
-            ++seq;
-          }
-          c.flush();
-          sent[pi] = seq;
-          if (s.confirm) {   // keep the confirm stream drained (non-blocking)
-            char buf[1 << 16];
-            ssize_t k;
-            while ((k = ::recv(c.fd, buf, sizeof buf, MSG_DONTWAIT)) > 0) c.in.append(buf, (size_t)k);
-            Frame f;
-            while (c.parser.next(c.in, c.pos, f)) {
-              if (f.type == FRAME_METHOD && f.payload.size() >= 12 && f.payload[1] == 60 && f.payload[3] == 80) {
-                const u8* p = (const u8*)f.payload.data() + 4;
-                u64 tag = 0;
-                for (int i = 0; i < 8; ++i) tag = (tag << 8) | p[i];
-                confirmed[pi] = tag;
-              }
+        p->pos = pos;
+        if (p->pos > (1u << 20) || p->pos == p->in.size()) { p->in.erase(0, p->pos); p->pos = 0; }
+      };
+      auto drain = [&](Peer* p) {
+        for (;;) {
+          ssize_t k = ::recv(p->cl.fd, rbuf.data(), rbuf.size(), 0);
+          if (k > 0) {
+            p->in.append(rbuf.data(), (size_t)k);
+            parse(p);
+            if (!p->producer && !s.auto_ack && p->unacked >= ack_every) {
+              std::string ak;
+              Method m = make_method(60, 80);
+              m.args[0].i = (i64)p->last_tag;
+              m.args[1].i = 1;
+              append_method_frame(ak, 1, m);
+              send_small(p, ak);
+              p->unacked = 0;
             }
-            if (c.pos > (1u << 20)) { c.in.erase(0, c.pos); c.pos = 0; }
+            continue;
           }
-          if (s.rate && seq >= (u64)((mono_ns() - t_start) / 1e9 * s.rate)) std::this_thread::sleep_for(std::chrono::microseconds(200));
+          if (k == 0) throw std::runtime_error("loadgen: broker closed the connection");
+          if (errno == EINTR) continue;
+          break;
         }
-        c.close();
-      } catch (std::exception& e) { fail(e); }
-    });
+        if (!p->producer && !s.auto_ack && p->unacked) {   // buffer ran dry: ack what we have
+          std::string ak;
+          Method m = make_method(60, 80);
+          m.args[0].i = (i64)p->last_tag;
+          m.args[1].i = 1;
+          append_method_frame(ak, 1, m);
+          send_small(p, ak);
+          p->unacked = 0;
+        }
+      };
+      for (Peer* p : mine) if (!p->in.empty()) parse(p);
+      while (!stop) {
+        for (Peer* p : mine)
+          if (p->producer && p->writable) pump(p);
+        int n = epoll_wait(ep, evs, 256, any_producer && rate > 0 ? 0 : 2);
+        for (int i = 0; i < n; ++i) {
+          Peer* p = (Peer*)evs[i].data.ptr;
+          if (evs[i].events & EPOLLOUT) p->writable = true;
+          if (evs[i].events & (EPOLLIN | EPOLLHUP | EPOLLERR)) drain(p);
+        }
+        if (any_producer && rate > 0 && n == 0) std::this_thread::sleep_for(std::chrono::microseconds(50));
+      }
+      ::close(ep);
+    } catch (std::exception& e) {
+      std::lock_guard<std::mutex> g(err_mu);
+      if (err.empty()) err = e.what();
+      stop = true;
+    }
+  };
+  std::vector<std::thread> th;
+  for (int t = 0; t < nthreads; ++t) th.emplace_back(worker, t);
+  // warm-up excluded from the counts: snapshot after `warmup` seconds
+  const double warm = std::max(0.0, s.warmup);
+  u64 sent0 = 0, recv0 = 0, conf0 = 0;
+  if (warm > 0) {
+    std::this_thread::sleep_for(std::chrono::milliseconds((i64)(warm * 1000)));
+    for (auto& p : peers) { sent0 += p->sent; recv0 += p->recv; conf0 += p->confirmed; }
   }
+  const i64 t_meas = mono_ns();
   std::this_thread::sleep_for(std::chrono::milliseconds((i64)(s.seconds * 1000)));
-  u64 s_sent = 0, s_recv = 0;
-  for (u64 x : sent) s_sent += x;
-  for (u64 x : recv) s_recv += x;
-  i64 t_end = mono_ns();
+  u64 s_sent = 0, s_recv = 0, s_conf = 0, s_nack = 0;
+  for (auto& p : peers) { s_sent += p->sent; s_recv += p->recv; s_conf += p->confirmed; s_nack += p->nacked; }
+  const i64 t_end = mono_ns();
   stop = true;
   for (auto& t : th) t.join();
   Hist all;
   for (auto& h : hists) all.merge(h);
-  r.elapsed = (t_end - t_start) / 1e9;
-  r.sent = s_sent;
-  r.received = s_recv;
+  for (auto& p : peers) p->cl.close();
+  r.elapsed = (t_end - t_meas) / 1e9;
+  r.sent = s_sent - sent0;
+  r.received = s_recv - recv0;
+  r.confirmed = s_conf - conf0;
+  r.nacked = s_nack;
   r.p50_us = all.q(0.50);
   r.p95_us = all.q(0.95);
   r.p99_us = all.q(0.99);
   r.error = err;
+  r.threads = nthreads;
   return r;
 }
 

@@ -17,10 +17,13 @@ struct LoadSpec {
   int prefetch = 5000;
   bool persistent = false, durable = false, confirm = false;
   double rate = 0;   // msgs/s per producer, 0 = unthrottled
+  int threads = 0;   // epoll worker threads (0 = min(8, connections))
+  double warmup = 0; // seconds excluded from the counts
 };
 
 struct LoadResult {
-  unsigned long long sent = 0, received = 0;
+  unsigned long long sent = 0, received = 0, confirmed = 0, nacked = 0;
+  int threads = 0;
   double elapsed = 0, p50_us = 0, p95_us = 0, p99_us = 0;
   std::string error;
 };

@@ -21,22 +21,10 @@ enum : u32 {
   CK_TXBUF = 6,     // publish / ack / nack / reject on a transactional channel: raw bytes
                     // to the host (buffered until Tx.Commit), connection not paused
 };
-#define CTRL_TXBUF 0x80000000u   // CtrlRec.seg flag: CK_TXBUF record, low bits = wire position
 
 // ---- exchange types (constants.py EX_*)
 enum : u32 { EX_DIRECT = 0, EX_FANOUT = 1, EX_TOPIC = 2, EX_HEADERS = 3 };
 
-// ---- per-segment status bits (SegOut.status)
-enum : u32 {
-  SS_OK = 0,
-  SS_PAUSED = 1,        // connection paused behind a control command
-  SS_CTRL = 2,          // a control command was emitted (connection now paused)
-  SS_FRAME_ERROR = 4,   // malformed frame (501); host closes connection
-  SS_UNEXPECTED = 8,    // frame sequence error (505)
-  SS_TOO_LARGE = 16,    // command exceeds carry capacity (host fallback)
-  SS_OVERFLOW = 32,     // per-step capacity hit; remainder carried
-  SS_CHANNEL = 64,      // data command on a channel the device does not know (sent as control)
-};
 
 // ---- message flags
 enum : u32 {

@@ -14,6 +14,20 @@ typedef int32_t i32;
 typedef int8_t i8;
 typedef int64_t i64;
 
+// ---- per-segment status bits (SegOut.status)
+enum : u32 {
+  SS_OK = 0,
+  SS_PAUSED = 1,        // connection paused behind a control command
+  SS_CTRL = 2,          // a control command was emitted (connection now paused)
+  SS_FRAME_ERROR = 4,   // malformed frame (501); host closes connection
+  SS_UNEXPECTED = 8,    // frame sequence error (505)
+  SS_TOO_LARGE = 16,    // command exceeds carry capacity (host fallback)
+  SS_OVERFLOW = 32,     // per-step capacity hit; remainder carried
+  SS_CHANNEL = 64,      // data command on a channel the device does not know (sent as control)
+};
+
+#define CTRL_TXBUF 0x80000000u   // CtrlRec.seg flag: CK_TXBUF record, low bits = wire position
+
 struct SegIn {          // host -> device, one per connection with bytes this step
   u32 conn;
   u32 len;              // new bytes

@@ -29,7 +29,8 @@ def make_plane(kind):
 
 
 @pytest.fixture(params=["golden-native", "golden-python", pytest.param("gpu-native", marks=pytest.mark.gpu),
-                        pytest.param("gpu-python", marks=pytest.mark.gpu)])
+                        pytest.param("gpu-python", marks=pytest.mark.gpu),
+                        pytest.param("gpu-pipeline", marks=pytest.mark.gpu)])
 def broker(request):
     from chanamq_amd.server.gpu_broker import GpuBroker
     kind, io = request.param.split("-")
@@ -231,10 +232,12 @@ def test_transactions_commit_and_rollback(broker):
     c.close()
 
 
-@pytest.fixture(params=["golden", pytest.param("gpu", marks=pytest.mark.gpu)])
+@pytest.fixture(params=["golden", pytest.param("gpu", marks=pytest.mark.gpu),
+                        pytest.param("gpu-pipeline", marks=pytest.mark.gpu)])
 def wm_broker(request):
     from chanamq_amd.server.gpu_broker import GpuBroker
-    b = GpuBroker(make_plane(request.param), idle_step_ms=1.0, ingress_bytes=8 << 20,
+    kind, _, io = request.param.partition("-")
+    b = GpuBroker(make_plane(kind), idle_step_ms=1.0, ingress_bytes=8 << 20, io=io or "native",
                   mem_high_watermark=40_000, mem_low_watermark=10_000).start()
     yield b
     b.stop()
@@ -273,7 +276,8 @@ def make_persist_plane(kind):
                         restore_max=1024, restore_bytes=8 << 20, **GPU_CFG)
 
 
-@pytest.mark.parametrize("kind", ["golden", pytest.param("gpu", marks=pytest.mark.gpu)])
+@pytest.mark.parametrize("kind", ["golden", pytest.param("gpu", marks=pytest.mark.gpu),
+                                  pytest.param("gpu-pipeline", marks=pytest.mark.gpu)])
 def test_durable_persistent_messages_survive_restart(kind, tmp_path):
     """Config 4 path: durable queue + delivery-mode 2 + confirms; restart recovers the
     unacked (redelivered first) and the unconsumed messages; non-persistent ones are gone."""
@@ -282,7 +286,9 @@ def test_durable_persistent_messages_survive_restart(kind, tmp_path):
     core = load()
     st = core.Store()
     st.open(str(tmp_path / "store"), True)
-    b = GpuBroker(make_persist_plane(kind), idle_step_ms=1.0, ingress_bytes=8 << 20, store=st).start()
+    kind, _, io = kind.partition("-")
+    io = io or "native"
+    b = GpuBroker(make_persist_plane(kind), idle_step_ms=1.0, ingress_bytes=8 << 20, store=st, io=io).start()
     p = conn(b)
     ch = p.channel()
     ch.exchange_declare("dur.x", "direct", durable=True)
@@ -309,7 +315,7 @@ def test_durable_persistent_messages_survive_restart(kind, tmp_path):
 
     st2 = core.Store()
     st2.open(str(tmp_path / "store"), True)
-    b2 = GpuBroker(make_persist_plane(kind), idle_step_ms=1.0, ingress_bytes=8 << 20, store=st2).start()
+    b2 = GpuBroker(make_persist_plane(kind), idle_step_ms=1.0, ingress_bytes=8 << 20, store=st2, io=io).start()
     assert b2.recovered == 8
     c2 = conn(b2)
     ch2 = c2.channel()
