@@ -33,7 +33,8 @@ SPECS = {
                                        prefetch=1000),
     # BASELINE config 4: durable queues, delivery-mode 2, 4 KB, publisher confirms, manual ack
     "config4_durable_4KB_confirms": dict(producers=16, consumers=4, queues=4, msg_size=4096, auto_ack=False,
-                                         prefetch=1000, persistent=True, durable=True, confirm=True),
+                                         prefetch=1000, persistent=True, durable=True, confirm=True,
+                                         confirm_window=512),
 }
 
 
@@ -74,7 +75,8 @@ def run_one(core, name, spec, io, io_threads, seconds, rate=0.0, lg_threads=8, s
              wall_s=time.time() - t0, steps=st.get("steps"), spec=spec,
              front_end={k: fes.get(k) for k in ("steps", "idle_steps", "gather_segs", "io_phase_s", "wait_s",
                                                 "submit_s", "rx_bytes", "tx_bytes", "held_steps")},
-             last_step={k: lc.get(k) for k in ("n_ring_full", "n_dropped_nomem")})
+             last_step={k: lc.get(k) for k in ("n_ring_full", "n_dropped_nomem")},
+             store=getattr(b, "_pw_stats", None))
     del plane
     return r
 
@@ -101,7 +103,8 @@ def main():
                 r = run_one(core, name, spec, io, nt, args.seconds, lg_threads=args.loadgen_threads)
                 results.append(r)
                 print(json.dumps({k: r[k] for k in ("name", "io", "io_threads", "recv_msgs_per_s", "sent_msgs_per_s",
-                                                    "confirmed_per_s", "p50_us", "p99_us", "error", "front_end")}),
+                                                    "confirmed_per_s", "p50_us", "p99_us", "error", "front_end",
+                                                    "store")}),
                       flush=True)
                 if args.paced > 0 and r["recv_msgs_per_s"] > 0 and not r["error"]:
                     rate = args.paced * r["recv_msgs_per_s"] / max(1, spec.get("producers", 1))

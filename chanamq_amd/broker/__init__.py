@@ -12,8 +12,9 @@ _ROOT = os.path.dirname(os.path.dirname(_HERE))
 _SRC = os.path.join(_ROOT, "csrc", "core")
 _EXT = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
 EXT_PATH = os.path.join(_HERE, "_core" + _EXT)
-SOURCES = ["codec.cpp", "store.cpp", "broker.cpp", "loadgen.cpp", "gateway.cpp", "frontend.cpp", "bindings.cpp"]
-HEADERS = ["codec.hpp", "store.hpp", "broker.hpp", "loadgen.hpp", "gateway.hpp", "frontend.hpp",
+SOURCES = ["codec.cpp", "store.cpp", "broker.cpp", "loadgen.cpp", "gateway.cpp", "frontend.cpp", "persist.cpp",
+           "bindings.cpp"]
+HEADERS = ["codec.hpp", "store.hpp", "broker.hpp", "loadgen.hpp", "gateway.hpp", "frontend.hpp", "persist.hpp",
            "../kernels/step_abi.h"]
 
 
@@ -47,7 +48,7 @@ def build(force=False, verbose=False, sanitize=None):
     if sanitize:
         flags += [f"-fsanitize={sanitize}", "-fno-omit-frame-pointer"]
     cmd = [cxx, *flags, f"-I{pybind11.get_include()}", f"-I{sysconfig.get_paths()['include']}",
-           *[os.path.join(_SRC, s) for s in SOURCES], "-o", out + ".tmp", "-lssl", "-lcrypto", "-lpthread"]
+           *[os.path.join(_SRC, s) for s in SOURCES], "-o", out + ".tmp", "-lssl", "-lcrypto", "-lz", "-lpthread"]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)

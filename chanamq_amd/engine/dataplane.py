@@ -353,6 +353,20 @@ class GpuDataPlane(ControlState):
             return out
         return out + parse_consumed(self.eng.host_view(f"consumed{self._last_parity}")[:n * CONSUMED_REC.itemsize])
 
+    def take_persist_raw(self):
+        """(packed persist records, ConsumedRec bytes) of the last finished step, as the
+        native PersistWorker consumes them."""
+        c = getattr(self, "last_counters", None)
+        if not c:
+            return b"", b""
+        if c["n_persist_overflow"] or c["n_persist"] > self.info["persist_max"]:
+            raise RuntimeError("persist buffer overflow: raise persist_max / persist_bytes")
+        p = self._last_parity
+        persist = bytes(self.eng.host_view(f"persist{p}")[:c["persist_used"]]) if c["n_persist"] else b""
+        n = min(c["n_consumed"], self.info["persist_max"])
+        consumed = bytes(self.eng.host_view(f"consumed{p}")[:n * CONSUMED_REC.itemsize]) if n else b""
+        return persist, consumed
+
     def take_get_consumed(self):
         """Store records of Basic.Get calls since the last call (native front end mode,
         where no Python-run step collects them)."""
@@ -401,6 +415,21 @@ class GpuDataPlane(ControlState):
             total += self.eng.restore(desc.view(np.uint8), np.frombuffer(bytes(pay) or b"\0", np.uint8)[:len(pay)],
                                       now)
         return total
+
+    ID_SLOT_BITS = 18   # dp_state.h: snowflake id slots per millisecond (64 worker ids x 4096)
+
+    def seed_ids(self, min_ms):
+        """Recovery: new snowflake ids start at millisecond >= ``min_ms`` (above every
+        recovered id), whatever the wall clock says."""
+        cur = self._u64("id_next", 0)
+        want = int(min_ms) << self.ID_SLOT_BITS
+        if want > cur:
+            self._up_at("id_next", want, 0, np.uint64)
+
+    @staticmethod
+    def id_group_workers(group):
+        """Worker ids (10-bit snowflake field) owned by GPU id group ``group``."""
+        return list(range(group * 64, group * 64 + 64))
 
     def memory_in_use(self):
         """Body-log slot bytes held by live messages (after the last finished step)."""

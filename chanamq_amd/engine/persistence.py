@@ -39,6 +39,26 @@ class GpuPersistence:
         self.rows = {}            # (queue id, msg id) -> [stored offset, size, is_unack]
         self.rows_written = 0
         self.dirty = False
+        self.native = None        # PersistWorker (csrc/core/persist.cpp) once attached
+
+    def attach_native(self, worker):
+        """Hand the row bookkeeping to the native write-behind worker (pipelined front
+        end): from now on every record goes through it, Python keeps only control rows."""
+        self.native = worker
+        for q in self.plane.queue_by_slot.values():
+            if q.durable:
+                worker.set_queue(q.slot, entity_id(q.vhost, q.name))
+        for (qid, mid), (off, size, unack) in self.rows.items():
+            worker.seed_row(qid, mid, off, size, bool(unack), self.refs.get(mid, 1))
+        self.rows, self.refs = {}, {}
+        worker.start()
+
+    def submit_raw(self, persist=b"", consumed=b""):
+        """Native mode: records of a host-run step / Basic.Get, applied and committed
+        before the caller sends that step's egress."""
+        if persist or consumed:
+            self.native.submit(0, persist, consumed)
+            self.native.drain()
 
     def _qid(self, slot):
         q = self.plane.queue_by_slot.get(slot)
@@ -48,6 +68,18 @@ class GpuPersistence:
     def after_step(self):
         """Apply the step's records.  Device queue positions change on requeue, so rows
         are addressed by (queue, message id) -> the offset they were stored at."""
+        if self.native is not None:
+            from .layout import CONSUMED_REC
+            import numpy as np
+            persist, consumed = self.plane.take_persist_raw()
+            gets = self.plane.take_get_consumed()
+            if gets:
+                a = np.zeros(len(gets), CONSUMED_REC)
+                for i, (mid, q, qpos, kind) in enumerate(gets):
+                    a[i] = (mid, qpos, q, kind, (0, 0))
+                consumed += a.tobytes()
+            self.submit_raw(persist, consumed)
+            return bool(persist)
         return self.apply(self.plane.take_persist(), self.plane.take_consumed())
 
     def apply(self, persisted, consumed):
@@ -104,6 +136,9 @@ class GpuPersistence:
         return bool(persisted)
 
     def commit(self):
+        if self.native is not None:
+            self.native.drain()
+            return
         if self.dirty:
             self.store.sync()
             self.dirty = False
@@ -123,9 +158,14 @@ class GpuPersistence:
     def queue(self, q):
         if q.durable:
             self.store.insert_queue_meta(entity_id(q.vhost, q.name), -1, set(), True, q.ttl_ms)
+            if self.native is not None:
+                self.native.set_queue(q.slot, entity_id(q.vhost, q.name))
 
-    def queue_deleted(self, vhost, name):
+    def queue_deleted(self, vhost, name, slot=None):
         qid = entity_id(vhost, name)
+        if self.native is not None and slot is not None:
+            self.native.drain()
+            self.native.set_queue(slot, "")
         self.store.force_delete_queue(qid)
         self.store.delete_binds_of_queue(qid)
 
@@ -187,6 +227,13 @@ class GpuPersistence:
             if (v, q) in p.queues:
                 p.bind(v, q, x, key)
         n = p.restore(items, now_ms) if items else 0
+        # new ids strictly above every stored one (snowflake ms field), even if the device
+        # clock ran ahead of the wall clock before the restart or the clock went back
+        top = max((it[1] for it in items), default=0)
+        for mid in st.message_ids() if hasattr(st, "message_ids") else ():
+            top = max(top, mid)
+        if top and hasattr(p, "seed_ids"):
+            p.seed_ids((top >> 22) + 1)
         # device offsets restart at 0: move the rows to them
         for qid, off, new_off, mid, size, red in rewrite:
             if red:

@@ -173,6 +173,10 @@ class GpuBroker:
                 idle_step_ms=self.idle_step_s * 1000.0, worker=self.plane.worker, max_slot=self.plane.c_max - 2,
                 reuseport=self.reuseport))
             self.port = self.fe.port
+            if self.persistence is not None:   # native write-behind: records never touch Python
+                self._pw = load().PersistWorker(self.persistence.store)
+                self.fe.attach_persist(self._pw)
+                self.persistence.attach_native(self._pw)
             self._running = True
             self.fe.start()
             self._thread = threading.Thread(target=self._loop_pipeline, name="gpu-broker-ctl", daemon=True)
@@ -215,6 +219,9 @@ class GpuBroker:
         if self.fe is not None:
             self.fe.stop()
             self._sync_fe_stats()
+            if getattr(self, "_pw", None) is not None:
+                self._pw.stop()
+                self._pw_stats = self._pw.stats()
             self.fe = None
         self._sel.close()
         if self._lsock is not None:
@@ -273,8 +280,7 @@ class GpuBroker:
                         persist += [e for e in more if e[0] == FE_PERSIST]
                         dev = [e for e in more if e[0] != FE_PERSIST]
                     if self.persistence is not None and self.plane._get_consumed:
-                        self.persistence.apply([], self.plane.take_get_consumed())
-                        self.persistence.commit()
+                        self._persist_gets()
                     self._flush_all()
             if persist:
                 self._persist_native(persist)
@@ -337,6 +343,19 @@ class GpuBroker:
                 self.persistence.apply(parse_persist(data) if data else [], parse_consumed(data2) if data2 else [])
             self.persistence.commit()
         self.fe.release(top)
+
+    def _persist_gets(self):
+        """Store records of Basic.Get calls (between steps, no step collected them)."""
+        if self.persistence.native is not None:
+            from ..engine.layout import CONSUMED_REC
+            gets = self.plane.take_get_consumed()
+            a = np.zeros(len(gets), CONSUMED_REC)
+            for i, (mid, q, qpos, kind) in enumerate(gets):
+                a[i] = (mid, qpos, q, kind, (0, 0))
+            self.persistence.submit_raw(b"", a.tobytes())
+        else:
+            self.persistence.apply([], self.plane.take_get_consumed())
+            self.persistence.commit()
 
     def _sync_fe_stats(self):
         if self.fe is None:
@@ -921,7 +940,7 @@ class GpuBroker:
                 self._persist_step()
             p.delete_queue(vh, q.name)
             if self.persistence is not None:
-                self.persistence.queue_deleted(vh, q.name)
+                self.persistence.queue_deleted(vh, q.name, slot=q.slot)
             if not m.nowait:
                 self._send(c, ch, Method("queue.delete_ok", message_count=cnt))
         elif n == "basic.qos":

@@ -7,6 +7,7 @@
 #include "broker.hpp"
 #include "codec.hpp"
 #include "frontend.hpp"
+#include "persist.hpp"
 #include "gateway.hpp"
 #include "loadgen.hpp"
 #include "store.hpp"
@@ -76,6 +77,7 @@ PYBIND11_MODULE(_core, m) {
       .def("compact", &Store::compact)
       .def("row_count", &Store::rowCount)
       .def("queue_ids", &Store::queueIds)
+      .def("message_ids", &Store::messageIds)
       .def("exchange_ids", &Store::exchangeIds)
       .def("vhost_ids", &Store::vhostIds)
       .def("insert_vhost", &Store::insertVhost)
@@ -184,7 +186,7 @@ PYBIND11_MODULE(_core, m) {
 #define S(k, f) if (d.contains(k)) c.f = d[k].cast<decltype(c.f)>()
              S("host", host); S("port", port); S("io_threads", io_threads); S("per_conn_read", per_conn_read);
              S("idle_step_ms", idle_step_ms); S("worker", worker); S("max_slot", max_slot); S("reuseport", reuseport);
-             S("sndbuf", sndbuf); S("rcvbuf", rcvbuf);
+             S("sndbuf", sndbuf); S("rcvbuf", rcvbuf); S("wblock_high", wblock_high); S("wblock_low", wblock_low);
 #undef S
              return new Frontend(c, (const CmqEngineApi*)api);
            }), py::arg("engine_api"), py::arg("cfg") = py::dict())
@@ -225,6 +227,7 @@ PYBIND11_MODULE(_core, m) {
       .def("pause", &Frontend::pause, py::call_guard<py::gil_scoped_release>())
       .def("resume", &Frontend::resume, py::call_guard<py::gil_scoped_release>())
       .def("release", &Frontend::release)
+      .def("attach_persist", &Frontend::attach_persist, py::keep_alive<1, 2>())
       .def("pending_out", &Frontend::pending_out)
       .def("stats", [](Frontend& f) {
              FeStats s = f.stats();
@@ -235,6 +238,21 @@ PYBIND11_MODULE(_core, m) {
              o["live_bytes"] = s.live_bytes; o["io_phase_s"] = s.io_phase_s; o["wait_s"] = s.wait_s;
              o["submit_s"] = s.submit_s;
              o["lat_hist"] = std::vector<u64>(s.lat_hist, s.lat_hist + 32);
+             return o;
+           });
+  py::class_<PersistWorker>(m, "PersistWorker")
+      .def(py::init<Store*>(), py::keep_alive<1, 2>())
+      .def("start", &PersistWorker::start)
+      .def("stop", &PersistWorker::stop, py::call_guard<py::gil_scoped_release>())
+      .def("set_queue", &PersistWorker::set_queue)
+      .def("seed_row", &PersistWorker::seed_row)
+      .def("submit", [](PersistWorker& w, u64 step, py::bytes persist, py::bytes consumed) {
+             w.submit(step, std::string(persist), std::string(consumed));
+           })
+      .def("drain", &PersistWorker::drain, py::call_guard<py::gil_scoped_release>())
+      .def("stats", [](PersistWorker& w) {
+             py::dict o;
+             o["rows"] = w.rows(); o["commits"] = w.commits(); o["body_bytes"] = w.bytes(); o["busy_s"] = w.busy_s();
              return o;
            });
   py::class_<EchoEngine>(m, "EchoEngine")
@@ -251,7 +269,7 @@ PYBIND11_MODULE(_core, m) {
     S("msg_size", msg_size); S("seconds", seconds); S("exchange", exchange); S("exchange_type", exchange_type);
     S("routing_key", routing_key); S("queue", queue); S("queues", queues); S("auto_ack", auto_ack);
     S("prefetch", prefetch); S("persistent", persistent); S("durable", durable); S("confirm", confirm);
-    S("rate", rate); S("threads", threads); S("warmup", warmup);
+    S("rate", rate); S("threads", threads); S("warmup", warmup); S("confirm_window", confirm_window);
 #undef S
     LoadResult r;
     {

@@ -1,5 +1,7 @@
 #include "frontend.hpp"
 
+#include "persist.hpp"
+
 #include <arpa/inet.h>
 #include <fcntl.h>
 #include <netinet/in.h>
@@ -53,6 +55,7 @@ struct FeConn {
   // only while paused
   u32 carry = 0, inflight = 0;
   bool paused = false, kicked = false;
+  bool wblocked = false;  // egress back-pressure flag raised on the device (mu held)
   // heartbeats
   std::atomic<i64> last_rx{0}, last_tx{0};
   std::atomic<u32> hb_s{0};
@@ -210,7 +213,22 @@ std::string Frontend::take(u32 conn) {
   return s;
 }
 
+// egress back-pressure: above wblock_high bytes queued for a socket the device stops
+// dequeuing to that connection (its messages wait in HBM); below wblock_low it resumes
+void Frontend::wblock_update(FeConn& c) {
+  const size_t pend = c.out.size() - c.out_pos;
+  if (!c.wblocked && pend > cfg_.wblock_high) {
+    c.wblocked = true;
+    if (api_->wblock) api_->wblock[c.id] = 1;
+  } else if (c.wblocked && pend < cfg_.wblock_low) {
+    c.wblocked = false;
+    if (api_->wblock) api_->wblock[c.id] = 0;
+    wake_stepper();
+  }
+}
+
 bool Frontend::write_some(FeConn& c) {
+  struct WB { Frontend* f; FeConn& c; ~WB() { f->wblock_update(c); } } wb{this, c};
   while (c.out_pos < c.out.size()) {
     ssize_t k = ::send(c.fd, c.out.data() + c.out_pos, c.out.size() - c.out_pos, MSG_NOSIGNAL);
     if (k > 0) {
@@ -249,6 +267,7 @@ void Frontend::scatter_conn(FeConn& c, const u8* data, u32 n) {
   } else {
     c.out.append((const char*)data, n);
   }
+  wblock_update(c);
 }
 
 void Frontend::send(u32 conn, const char* data, size_t n) {
@@ -352,6 +371,11 @@ void Frontend::release(u64 step) {
   wake_stepper();
 }
 
+void Frontend::attach_persist(PersistWorker* w) {
+  persist_ = w;
+  w->on_commit([this](u64 step) { release(step); });
+}
+
 FeStats Frontend::stats() {
   std::lock_guard<std::mutex> g(stats_mu_);
   FeStats s = stats_;
@@ -398,6 +422,8 @@ void Frontend::accept_all(FeIo& io0) {
     }
     c.in_ready = false;
     c.rdhup = false;
+    c.wblocked = false;
+    if (api_->wblock) api_->wblock[id] = 0;
     c.carry = c.inflight = 0;
     c.paused = c.kicked = false;
     c.hb_s = 0;
@@ -434,6 +460,8 @@ void Frontend::drop(FeConn& c, bool notify) {
   c.out.clear();
   c.out_pos = 0;
   c.inject.clear();
+  c.wblocked = false;
+  if (api_->wblock) api_->wblock[c.id] = 0;
   if (notify) {
     FeEvent e;
     e.kind = FE_CLOSED;
@@ -510,6 +538,8 @@ void Frontend::io_loop(int i) {
         c.mode = M_FREE;
         c.out.clear();
         c.out_pos = 0;
+        c.wblocked = false;
+        if (api_->wblock) api_->wblock[id] = 0;
         c.inject.clear();
         c.hostbuf.clear();
       }
@@ -753,7 +783,8 @@ void Frontend::finish_oldest(std::deque<Inflight>& inflight) {
     const u32 np = std::min(c.n_persist, api_->persist_max), ncs = std::min(c.n_consumed, api_->persist_max);
     if (np) e.data.assign((const char*)api_->persist_host(api_->eng, p), c.persist_used);
     if (ncs) e.data2.assign((const char*)api_->consumed_host(api_->eng, p), (size_t)ncs * sizeof(ConsumedRec));
-    post(std::move(e));
+    if (persist_ && !e.b) persist_->submit(f.step, std::move(e.data), std::move(e.data2));
+    else post(std::move(e));
     needs_commit = true;
   }
   const int slot = api_->egress_slot(api_->eng, p);
@@ -938,6 +969,8 @@ EchoEngine::EchoEngine(u32 c_max, u32 seg_max, u64 ingress_cap, u32 carry_cap) {
   api_.ctrl_cap = 1 << 20;
   api_.eng = this;
   paused_.assign(c_max, 0);
+  wblock_.assign(c_max, 0);
+  api_.wblock = wblock_.data();
   for (auto& io : io_) { io.so.resize(seg_max); io.co.resize(c_max); }
   api_.submit = [](void* e, const SegIn* sg, u32 n, const u8* pay, u64 len, i64, u32) -> int {
     EchoEngine& E = *(EchoEngine*)e;
@@ -970,6 +1003,7 @@ EchoEngine::EchoEngine(u32 c_max, u32 seg_max, u64 ingress_cap, u32 carry_cap) {
         E.paused_[s.conn] = 1;
         b.resize(cpos);
       }
+      if (E.wblock_[s.conn]) o.status |= SS_PAUSED;   // back-pressured: nothing delivered
       if (!b.empty() && !(o.status & SS_PAUSED)) {
         io.co[s.conn] = ConnOut{(u32)eg.size(), (u32)b.size()};
         eg += b;

@@ -71,6 +71,7 @@ struct FrontendCfg {
   u32 max_slot = 0;                // connection slots 1..max_slot (default c_max - 2)
   bool reuseport = false;
   int sndbuf = 4 << 20, rcvbuf = 4 << 20;
+  u64 wblock_high = 8 << 20, wblock_low = 2 << 20;   // egress back-pressure watermarks per connection
 };
 
 struct FeStats {
@@ -83,6 +84,7 @@ struct FeStats {
 
 struct FeConn;
 struct FeIo;
+class PersistWorker;
 
 class Frontend {
  public:
@@ -105,6 +107,9 @@ class Frontend {
   void pause();                                          // exclusive device access (nests)
   void resume();
   void release(u64 step);                                // store commit of steps <= step landed
+  // native write-behind: step records go to the worker (not to the control plane) and
+  // its group commits release the held egress
+  void attach_persist(PersistWorker* w);
   FeStats stats();
   u64 pending_out() const;
 
@@ -133,6 +138,7 @@ class Frontend {
   void accept_all(FeIo& io);
   void drop(FeConn& c, bool notify);
   bool write_some(FeConn& c);   // mu held
+  void wblock_update(FeConn& c);   // mu held
   void scatter_conn(FeConn& c, const u8* data, u32 n);
   void gather_conn(FeIo& io, FeConn& c, u8* arena, u64 cap);
   bool check(int rc);
@@ -187,6 +193,7 @@ class Frontend {
 
   // persistence write-behind
   std::deque<Held> held_;
+  PersistWorker* persist_ = nullptr;
   std::atomic<u64> released_{0};
   bool have_released_ = false;
 
@@ -221,6 +228,7 @@ class EchoEngine {
   std::string slot_[3];
   int slot_of_[2] = {0, 0};
   std::vector<u8> paused_;
+  std::vector<u32> wblock_;
   u64 seq_ = 0;
   std::string err_;
 };

@@ -280,6 +280,20 @@ LoadResult run_load(const LoadSpec& s) {
   }
   int nthreads = s.threads > 0 ? s.threads : std::min<int>(8, (int)peers.size());
   nthreads = std::max(1, std::min<int>(nthreads, (int)peers.size()));
+  // consumers and producers on separate threads (a thread that can always send would
+  // otherwise starve the consumers it also serves)
+  const int ncons = s.consumers, nprod = s.producers;
+  int tc = 0, tp = 0;
+  if (nthreads >= 2 && ncons && nprod) {
+    tc = std::max(1, std::min(ncons, nthreads / 2));
+    tp = std::max(1, std::min(nprod, nthreads - tc));
+    nthreads = tc + tp;
+  }
+  auto thread_of = [&](size_t i) -> int {   // peers: consumers first, then producers
+    if (!tc) return (int)(i % nthreads);
+    return i < (size_t)ncons ? (int)(i % tc) : tc + (int)((i - ncons) % tp);
+  };
+  const u64 window = s.confirm ? (u64)std::max(0, s.confirm_window) : 0;
   std::atomic<bool> stop{false};
   std::string err;
   std::mutex err_mu;
@@ -291,7 +305,8 @@ LoadResult run_load(const LoadSpec& s) {
     try {
       int ep = epoll_create1(0);
       std::vector<Peer*> mine;
-      for (size_t i = ti; i < peers.size(); i += nthreads) {
+      for (size_t i = 0; i < peers.size(); ++i) {
+        if (thread_of(i) != ti) continue;
         Peer* p = peers[i].get();
         mine.push_back(p);
         epoll_event ev{};
@@ -307,7 +322,10 @@ LoadResult run_load(const LoadSpec& s) {
       auto pump = [&](Peer* p) {   // producer: send until the socket is full or paced out
         while (!stop && p->flow) {
           if (p->out_pos >= p->out.size()) {
-            if (rate > 0 && (double)(p->sent.load(std::memory_order_relaxed) + K) > rate * ((mono_ns() - t_start) * 1e-9)) return;
+            const u64 sent = p->sent.load(std::memory_order_relaxed);
+            if (rate > 0 && (double)(sent + K) > rate * ((mono_ns() - t_start) * 1e-9)) return;
+            if (window && sent + K > window + p->confirmed.load(std::memory_order_relaxed) +
+                                         p->nacked.load(std::memory_order_relaxed)) return;   // confirm window full
             p->out = p->batch;
             const i64 t = mono_ns();
             for (size_t o : p->ts_off) memcpy(&p->out[o], &t, 8);

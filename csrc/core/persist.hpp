@@ -1,0 +1,73 @@
+// Native write-behind persistence for the GPU data plane (BASELINE config 4).
+//
+// The device emits, per step, one PersistHdr record per enqueue of a persistent message
+// into a durable queue (packed with the message bytes) and one ConsumedRec per persistent
+// message that changes state in a durable queue (step_abi.h).  PersistWorker turns them
+// into rows of the Cassandra-schema store (store.hpp — the tables of the reference's
+// create-cassantra.cql) on its own thread: it applies every pending batch, commits them
+// with one fsync (group commit) and then releases the held egress of those steps to the
+// front end, so a publisher confirm never leaves before its message is durable
+// (CassandraOpService.scala:395-417 insertMessage / insertQueueMsg; FrameStage.scala:571-596
+// confirms after the entities answered).  Steps keep running while the commit is in flight.
+//
+// Rows are addressed by (queue, message id) -> the queue offset they were stored at, since
+// device queue positions change on requeue; a message row is deleted when the last queue
+// row referencing it goes (MessageEntity.scala:134-166 refer counting).
+#pragma once
+#include <atomic>
+#include <condition_variable>
+#include <deque>
+#include <functional>
+#include <map>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <unordered_map>
+#include <vector>
+
+#include "../kernels/step_abi.h"
+#include "store.hpp"
+
+namespace cmq {
+
+class PersistWorker {
+ public:
+  explicit PersistWorker(Store* store);
+  ~PersistWorker();
+  void start();
+  void stop();
+  // committed steps are reported here (the front end releases their held egress)
+  void on_commit(std::function<void(u64)> cb) { commit_cb_ = std::move(cb); }
+  void set_queue(u32 slot, const std::string& qid);   // durable queue slot -> entity id ("" = none)
+  void seed_row(const std::string& qid, i64 msgid, i64 offset, i32 size, bool unack, int refs);
+  // records of step `step` (0 = a host-run step / Basic.Get: no egress held)
+  void submit(u64 step, std::string persist, std::string consumed);
+  void drain();                                       // every submitted batch committed
+  u64 rows() const { return rows_; }
+  u64 commits() const { return commits_; }
+  u64 bytes() const { return bytes_; }
+  double busy_s() const { return busy_s_; }
+
+ private:
+  struct Batch { u64 step; std::string persist, consumed; };
+  struct Row { i64 offset; i32 size; bool unack; };
+  void loop();
+  void apply(const Batch& b);
+
+  Store* st_;
+  std::function<void(u64)> commit_cb_;
+  std::mutex mu_;
+  std::condition_variable cv_, done_cv_;
+  std::deque<Batch> q_;
+  u64 submitted_ = 0, committed_ = 0;
+  bool running_ = false;
+  std::thread th_;
+  std::mutex qid_mu_;
+  std::vector<std::string> qid_;                      // by queue slot
+  std::unordered_map<i64, int> refs_;                 // msg id -> durable queue rows
+  std::map<std::pair<std::string, i64>, Row> rows_by_;   // (queue id, msg id) -> row
+  std::atomic<u64> rows_{0}, commits_{0}, bytes_{0};
+  double busy_s_ = 0;
+};
+
+}  // namespace cmq

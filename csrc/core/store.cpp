@@ -9,6 +9,8 @@
 #include <cstring>
 #include <stdexcept>
 
+#include <zlib.h>
+
 #include "codec.hpp"
 
 namespace cmq {
@@ -20,21 +22,10 @@ enum Op : uint8_t {
   OP_BIND_DEL_Q, OP_X_DEL, OP_VH_INS, OP_VH_DEL, OP_QMSG_DEL
 };
 
-uint32_t crc32(const std::string& s) {
-  static uint32_t T[256];
-  static bool init = false;
-  if (!init) {
-    for (uint32_t i = 0; i < 256; ++i) {
-      uint32_t c = i;
-      for (int k = 0; k < 8; ++k) c = c & 1 ? 0xEDB88320u ^ (c >> 1) : c >> 1;
-      T[i] = c;
-    }
-    init = true;
-  }
-  uint32_t c = 0xFFFFFFFFu;
-  for (unsigned char b : s) c = T[(c ^ b) & 255] ^ (c >> 8);
-  return c ^ 0xFFFFFFFFu;
-}
+// CRC-32 (reflected 0xEDB88320, init/xorout 0xFFFFFFFF): zlib's, so the WAL format is
+// unchanged from the round-1 table-driven version and the check runs at memory speed
+uint32_t crc32(const char* p, size_t n) { return (uint32_t)::crc32(0L, (const Bytef*)p, (uInt)n); }
+uint32_t crc32(const std::string& s) { return crc32(s.data(), s.size()); }
 
 void w_map(Writer& w, const std::map<std::string, std::string>& m) {
   w.lng((u32)m.size());
@@ -87,22 +78,32 @@ void Store::write_all(const std::string& rec) {
   wal_bytes_ += rec.size();
 }
 
+// WAL records are buffered in memory and written in large chunks: by sync() (the group
+// commit, before confirms leave) or when the buffer passes 16 MB
 void Store::append(uint8_t op, const std::string& payload) {
   apply(op, payload);
   if (fd_ < 0 || replaying_) return;
-  std::string rec;
-  u32 len = (u32)payload.size() + 1;
-  for (int s = 24; s >= 0; s -= 8) rec.push_back((char)(len >> s));
-  rec.push_back((char)op);
-  rec += payload;
-  u32 c = crc32(rec.substr(4));
-  for (int s = 24; s >= 0; s -= 8) rec.push_back((char)(c >> s));
-  write_all(rec);
+  const u32 len = (u32)payload.size() + 1;
+  const size_t at = wbuf_.size();
+  wbuf_.resize(at + 4 + len + 4);
+  char* r = &wbuf_[at];
+  for (int i = 0; i < 4; ++i) r[i] = (char)(len >> (24 - 8 * i));
+  r[4] = (char)op;
+  memcpy(r + 5, payload.data(), payload.size());
+  const u32 c = crc32(r + 4, len);
+  for (int i = 0; i < 4; ++i) r[4 + len + i] = (char)(c >> (24 - 8 * i));
   dirty_ = true;
+  if (wbuf_.size() > (16u << 20)) flush_wal();
+}
+
+void Store::flush_wal() {
+  if (fd_ >= 0 && !wbuf_.empty()) write_all(wbuf_);
+  wbuf_.clear();
 }
 
 void Store::sync() {
   std::lock_guard<std::recursive_mutex> g(mu_);
+  flush_wal();
   if (fd_ >= 0 && dirty_) {
     if (fsync_) ::fdatasync(fd_);
     dirty_ = false;
@@ -141,6 +142,7 @@ void Store::compact() {
   std::string tmp = path_ + ".tmp";
   int nfd = ::open(tmp.c_str(), O_RDWR | O_CREAT | O_TRUNC, 0644);
   if (nfd < 0) throw std::runtime_error("store: compact open failed");
+  flush_wal();
   int old = fd_;
   fd_ = nfd;
   wal_bytes_ = 0;
@@ -166,6 +168,7 @@ void Store::compact() {
     for (auto& r : kv.second) insertQueueUnack(kv.first, r.second.offset, r.second.msgid, r.second.size);
   for (auto& kv : ms)
     insertMessage(kv.second, kv.second.expire_at ? std::max<int64_t>(1, kv.second.expire_at - now) : 0);
+  flush_wal();
   if (fsync_) ::fdatasync(fd_);
   ::rename(tmp.c_str(), path_.c_str());
   ::close(old);
@@ -431,6 +434,9 @@ std::vector<std::string> Store::exchangeIds() {
 }
 std::vector<std::string> Store::queueIds() {
   LOCK; std::vector<std::string> v; for (auto& kv : queue_metas_) v.push_back(kv.first); return v;
+}
+std::vector<int64_t> Store::messageIds() {
+  LOCK; std::vector<int64_t> v; for (auto& kv : msgs_) v.push_back(kv.first); return v;
 }
 size_t Store::rowCount(const std::string& t) {
   LOCK;

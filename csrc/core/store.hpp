@@ -101,13 +101,16 @@ class Store {
   std::vector<std::string> exchangeIds();
   std::vector<std::string> queueIds();
   size_t rowCount(const std::string& table);
-  uint64_t walBytes() const { return wal_bytes_; }
+  uint64_t walBytes() const { return wal_bytes_ + wbuf_.size(); }
+  std::vector<int64_t> messageIds();
 
  private:
   void append(uint8_t op, const std::string& payload);
   void apply(uint8_t op, const std::string& payload);
   void replay();
   void write_all(const std::string& rec);
+  void flush_wal();
+  std::string wbuf_;       // WAL records not yet written
 
   std::recursive_mutex mu_;
   int fd_ = -1;

@@ -237,6 +237,18 @@ DEV void wave_release(const DS& d, u32 msg, bool valid) {
   wave_add_i64(d.log_live, blk, -sb, freed);
 }
 
+// ---- K13 snowflake ids: id = ms << 22 | worker << 12 | seq (IdGenerator.scala:14-34).
+// The reference's generator allows 4096 ids per ms per node and waits for the next ms
+// (IdGenerator.scala:55-83); one MI355X publishes ~10x that.  A GPU therefore owns
+// ID_WORKERS worker ids (group g = StepIn.worker owns g*64 .. g*64+63): 2^18 ids per ms
+// (262 M msgs/s), so the virtual position (ms << 18 | slot) never outruns the wall clock
+// and ids stay unique across restarts (the host seeds id_next above recovered ids).
+DEV u64 snowflake_id(u64 pos, u32 group) {
+  const u64 ms = pos >> ID_SLOT_BITS;
+  const u64 worker = (u64)(group & (1023 / ID_WORKERS)) * ID_WORKERS + ((pos >> 12) & (ID_WORKERS - 1));
+  return (ms << 22) | (worker << 12) | (pos & 4095);
+}
+
 // ============================================================================ topic words
 // Java String.split("\\.") semantics (QueueMatcher.scala:69-71): trailing empty
 // words dropped, "" -> [""], "..." -> [].
@@ -325,8 +337,8 @@ __global__ __launch_bounds__(1024) void k_prep(DS d) {
   if (tid == 0) {
     *d.egress_budget = 0;
     d.tot[15] = running;  // work bytes used
-    // snowflake virtual position base for this step
-    u64 floor_pos = d.in->id_ms << 12;
+    // snowflake virtual position base for this step (ID_SLOT_BITS slots per wall-clock ms)
+    u64 floor_pos = d.in->id_ms << ID_SLOT_BITS;
     u64 cur = *d.id_next;
     *d.id_next = cur > floor_pos ? cur : floor_pos;
   }
@@ -1564,7 +1576,7 @@ DEV void store_one(const DS& d, u32 p, u32 lane) {
     MsgEnt m;
     m.log_off = off;
     u64 pos = (*d.id_base) + rr;
-    m.msg_id = (pb.flags & MF_RESTORE) ? pb.xid : ((pos >> 12) << 22) | (u64(d.in->worker & 1023) << 12) | (pos & 4095);
+    m.msg_id = (pb.flags & MF_RESTORE) ? pb.xid : snowflake_id(pos, d.in->worker);
     m.ts_ms = pb.ts_ms;
     m.slot_bytes = pb.slot_bytes;
     m.body_len = pb.body_size;
@@ -2018,7 +2030,9 @@ __global__ __launch_bounds__(256) void k_dequeue(DS d) {
       g_n[j] = 0;
       if (remaining == 0) continue;
       u32 ch = d.cons_ch[c];
-      if (!d.cons_active[c] || !d.ch_flow[ch]) continue;
+      // wblock: the front end's socket backlog for this connection is above its high
+      // watermark (host-mapped, written by the IO threads): its messages stay queued in HBM
+      if (!d.cons_active[c] || !d.ch_flow[ch] || d.conn_wblock[ch / d.chpc]) continue;
       u64 share = (remaining + (m - j) - 1) / (m - j);
       u32 want = (u32)(share < d.deliver_cap ? share : d.deliver_cap);
       bool noack = d.cons_noack[c];

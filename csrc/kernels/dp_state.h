@@ -5,6 +5,8 @@
 #include "dp_common.h"
 
 #define CAND_MAX 8192         // frame candidates per segment held in LDS
+#define ID_WORKERS 64         // snowflake worker ids per GPU (K13)
+#define ID_SLOT_BITS 18       // log2(ID_WORKERS * 4096): id slots per millisecond
 #define SORT_TILE 1024        // radix-sort tile (256 threads x 4): more tiles, more blocks in flight
 #define TOPIC_K 256           // topic key vector: 8 words x 32 hash bits (int8 +-1)
 #define TOPIC_WORDS 8
@@ -63,6 +65,7 @@ struct DS {
   u32* conn_conf_bytes;
   u32* conn_dfirst;         // first sorted delivery of the connection (0xffffffff none)
   u32* conn_dlast;
+  const u32* conn_wblock;   // host-mapped: egress back-pressure per connection (front end)
   u32* conn_total;
   u32* conn_base;
 

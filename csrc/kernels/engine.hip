@@ -200,6 +200,7 @@ class Engine {
     d_.conn_conf_bytes = (u32*)dev("conn_conf_bytes", 4ull * d_.c_max);
     d_.conn_dfirst = (u32*)dev("conn_dfirst", 4ull * d_.c_max);
     d_.conn_dlast = (u32*)dev("conn_dlast", 4ull * d_.c_max);
+    d_.conn_wblock = (const u32*)hst("conn_wblock", 4ull * d_.c_max);
     d_.conn_total = (u32*)dev("conn_total", 4ull * d_.c_max);
     d_.conn_base = (u32*)dev("conn_base", 4ull * d_.c_max);
 
@@ -780,6 +781,7 @@ class Engine {
     a.egress_host = [](void* e, int slot) -> const u8* { return ((Engine*)e)->egress_host_[slot]; };
     a.persist_host = [](void* e, int p) -> const u8* { return ((Engine*)e)->io_[p].persist_hh; };
     a.consumed_host = [](void* e, int p) -> const ConsumedRec* { return ((Engine*)e)->io_[p].crec_hh; };
+    a.wblock = (u32*)buf("conn_wblock").ptr;
     for (int p = 0; p < 2; ++p) {
       std::string sfx = std::to_string(p);
       HostIO& h = io_[p];

@@ -104,4 +104,5 @@ struct CmqEngineApi {
   const u8* (*egress_host)(void* eng, int slot);
   const u8* (*persist_host)(void* eng, int p);           // packed PersistHdr records (persist=1)
   const ConsumedRec* (*consumed_host)(void* eng, int p);
+  u32* wblock;   // host-mapped u32[c_max]: nonzero = do not dequeue to this connection (egress back-pressure)
 };
