@@ -57,6 +57,7 @@ class Queue:
     consumers: list = field(default_factory=list)  # consumer ids, in registration order
     owner: int = 0                                  # owning rank (sharded data plane)
     requested: int = 0                              # requested ring capacity (for re-homing)
+    max_capacity: int = 0                           # ring growth limit (0 = the ring pool)
 
 
 @dataclass
@@ -255,7 +256,7 @@ class ControlState:
         return off
 
     def declare_queue(self, vhost, name, durable=False, exclusive_owner=-1, auto_delete=False,
-                      ttl_ms=0, capacity=None, passive=False):
+                      ttl_ms=0, capacity=None, passive=False, max_capacity=0):
         key = (vhost, name)
         q = self.queues.get(key)
         if q is not None:
@@ -271,7 +272,7 @@ class ControlState:
             cap <<= 1
         slot = self._free_q.pop()
         q = Queue(slot, vhost, name, durable, exclusive_owner, auto_delete, ttl_ms, cap,
-                  self._ring_alloc(cap), owner=owner, requested=capacity)
+                  self._ring_alloc(cap), owner=owner, requested=capacity, max_capacity=max_capacity)
         self.queues[key] = q
         self.queue_by_slot[slot] = q
         dx = self.exchanges.get((vhost, ""))
@@ -280,6 +281,31 @@ class ControlState:
         self.queue_declared(q)
         self.routing_changed()
         return slot
+
+    def grow_target(self, q, depth):
+        """Ring capacity for a queue holding ``depth`` entries once it passed half its ring:
+        doubled until the depth is at most half of it, within max_capacity and the pool
+        (None = no growth).  QueueEntity.scala:271-316 is an unbounded Vector; here the
+        bound is the HBM ring pool (16 B per entry), and the body-log watermark pushes back
+        on publishers long before it."""
+        cap = q.capacity
+        limit = q.max_capacity or self.ring_pool
+        new = cap
+        while depth * 2 > new and new * 2 <= limit:
+            new *= 2
+        return new if new > cap else None
+
+    def regrow_ring(self, q, new_cap):
+        """Allocate a ring of ``new_cap`` for queue ``q`` and release the old one; returns
+        (old offset, old capacity) or None when the pool has no room."""
+        try:
+            off = self._ring_alloc(new_cap)
+        except ControlError:
+            return None
+        old = (q.ring_off, q.capacity)
+        self._ring_free.setdefault(q.capacity, []).append(q.ring_off)
+        q.ring_off, q.capacity = off, new_cap
+        return old
 
     def delete_queue(self, vhost, name):
         q = self.queues.pop((vhost, name), None)

@@ -84,6 +84,7 @@ class GpuDataPlane(ControlState):
         self._egress = [self.eng.host_view(f"egress_host{e}") for e in range(i["egress_slots"])]
         self._pin = [None, None]
         self.exchanger = exchanger
+        self._grow = set()        # queue slots the device reported past half their ring
         self._get_consumed = []   # store records of Basic.Get, emitted with the next step's
         self._pending = None
         self.lag = False
@@ -534,7 +535,34 @@ class GpuDataPlane(ControlState):
 
     def step_raw(self, segs, payload_ptr, payload_len, now_ms=None, collect=True):
         t = self.submit_raw(segs, payload_ptr, payload_len, now_ms)
-        return self.finish(t, collect=collect)
+        res = self.finish(t, collect=collect)
+        self.grow_queues()
+        return res
+
+    def grow_queues(self, slots=None):
+        """Between steps: double the rings of queues the device reported past half full
+        (k_enqueue -> grow list), moving their live entries on the device.  Returns the
+        slots grown."""
+        if slots is not None:
+            self._grow.update(slots)
+        done = []
+        for slot in sorted(self._grow):
+            q = self.queue_by_slot.get(slot)
+            if q is None or q.owner != self.rank:
+                continue
+            head, tail = self._u64("q_head", slot), self._u64("q_tail", slot)
+            new = self.grow_target(q, tail - head)
+            if new is None:
+                continue
+            old = self.regrow_ring(q, new)
+            if old is None:
+                continue
+            self.eng.ring_move(old[0], old[1] - 1, q.ring_off, new - 1, head, tail)
+            self._up_at("q_ring_off", q.ring_off, slot, np.uint64)
+            self._up_at("q_ring_mask", new - 1, slot, np.uint64)
+            done.append(slot)
+        self._grow.clear()
+        return done
 
     def submit_raw(self, segs, payload_ptr, payload_len, now_ms=None):
         """Asynchronous half of a step: returns a ticket for ``finish``.  At most two
@@ -598,6 +626,9 @@ class GpuDataPlane(ControlState):
         res = StepResult()
         res.counters = c = self.eng.counters(p)
         self.last_counters = c
+        if c["n_grow"]:
+            g = np.frombuffer(self.eng.host_view(f"grow{p}")[:4 * min(c["n_grow"], 4096)].tobytes(), np.uint32)
+            self._grow.update(int(x) for x in g)
         io = self._io[p]
         so = io["seg_out"][:nseg]
         self.carry[so["conn"]] = so["carry"]

@@ -27,16 +27,17 @@ def main(argv=None):
     ap.add_argument("--stats-interval", type=float, default=10.0)
     ap.add_argument("--log-level", default="INFO")
     ap.add_argument("--data-plane", choices=["host", "gpu"], default="host")
-    ap.add_argument("--device", type=int, default=0)
-    ap.add_argument("--admin-port", type=int, default=-1, help="GPU mode: admin REST port (0 = any, -1 = off)")
+    ap.add_argument("--device", type=int, default=None, help="GPU mode: device (default chana.mq.gpu.device)")
+    ap.add_argument("--admin-port", type=int, default=None,
+                    help="GPU mode: admin REST port (0 = any, -1 = off; default chana.mq.amqp.admin.port)")
     args = ap.parse_args(argv)
     logging.basicConfig(level=args.log_level, format="%(asctime)s:%(levelname)s %(threadName)s - %(message)s")
     log = logging.getLogger("chanamq")
     overrides = dict(kv.split("=", 1) for kv in args.set)
     cfg = Config.load(args.config, overrides)
     bc = cfg.broker_config()
-    if args.data_plane == "gpu":
-        return _main_gpu(args, bc, log)
+    if args.data_plane == "gpu" or bool(cfg.get("chana.mq.gpu.enable", False)):
+        return _main_gpu(args, bc, cfg, log)
     core = load()
     broker = core.Broker(bc)
     broker.start()
@@ -58,15 +59,35 @@ def main(argv=None):
     return 0
 
 
-def _main_gpu(args, bc, log):
+def _main_gpu(args, bc, cfg, log):
+    """GPU data plane behind the pipelined native front end, configured from
+    ``chana.mq.gpu.*`` / ``chana.mq.store.*`` / ``chana.mq.flow.*`` / ``chana.mq.amqps.*``
+    (AMQPServer.scala:52-106: store, AMQP + AMQPS listeners, admin REST)."""
     from ..engine.dataplane import GpuDataPlane
     from .gpu_broker import GpuBroker
-    plane = GpuDataPlane(device=args.device, hash_wildcard=bc["hash_wildcard"], frame_max=bc["frame_max"])
-    broker = GpuBroker(plane, host=bc["host"], port=bc["port"], heartbeat=bc["heartbeat"],
-                       frame_max=bc["frame_max"], channel_max=bc["channel_max"] or 2047).start()
-    log.info("AMQP (GPU data plane, device %d) listening on %s:%s", args.device, bc["host"], broker.port)
-    from ..utils.config import Config  # noqa: F401  (admin port from the same config)
-    admin = AdminServer(broker, int(args.admin_port)).start() if args.admin_port >= 0 else None
+    plane_kw, broker_kw = cfg.gpu_config()
+    if args.device is not None:
+        plane_kw["device"] = args.device
+    core = load()
+    store = None
+    if bc["data_dir"]:
+        store = core.Store()
+        store.open(bc["data_dir"], bc["fsync"])
+    plane = GpuDataPlane(**plane_kw)
+    broker = GpuBroker(plane, host=bc["host"], port=bc["port"], heartbeat=bc["heartbeat"], frame_max=bc["frame_max"],
+                       channel_max=bc["channel_max"] or 2047, store=store, **broker_kw).start()
+    log.info("AMQP (GPU data plane, device %d, %s front end) listening on %s:%s; recovered %d messages",
+             plane_kw["device"], broker.io, bc["host"], broker.port, broker.recovered)
+    tls = None
+    if bc["tls_enable"]:
+        tls = core.TlsProxy(dict(host=bc["host"], port=bc["tls_port"], upstream_port=broker.port,
+                                 cert=bc["tls_cert"], key=bc["tls_key"], p12=bc["tls_p12"],
+                                 p12_password=bc["tls_p12_password"]))
+        tls.start()
+        log.info("AMQPS (TLS) on %s:%d -> the GPU front end", bc["host"], tls.port)
+    broker.tls = tls
+    admin_port = args.admin_port if args.admin_port is not None else int(cfg.get("chana.mq.amqp.admin.port"))
+    admin = AdminServer(broker, admin_port).start() if admin_port >= 0 else None
     if admin is not None:
         log.info("admin REST on 127.0.0.1:%d", admin.port)
     stop = threading.Event()
@@ -80,7 +101,11 @@ def _main_gpu(args, bc, log):
         last = s
     if admin is not None:
         admin.stop()
+    if tls is not None:
+        tls.stop()
     broker.stop()
+    if store is not None:
+        store.close()
     return 0
 
 

@@ -58,7 +58,7 @@ class _Conn:
         self.cap_blocked = False
 
 
-FE_OPEN, FE_CLOSED, FE_HOST, FE_CTRL, FE_TXBUF, FE_EVENT, FE_STATUS, FE_PERSIST, FE_ERROR = range(1, 10)
+FE_OPEN, FE_CLOSED, FE_HOST, FE_CTRL, FE_TXBUF, FE_EVENT, FE_STATUS, FE_PERSIST, FE_ERROR, FE_GROW = range(1, 11)
 
 
 class _PlaneLock:
@@ -108,7 +108,7 @@ def _frames(buf):
 class GpuBroker:
     def __init__(self, plane, host="127.0.0.1", port=0, heartbeat=0, frame_max=131072, channel_max=2047,
                  idle_step_ms=2.0, product="chanamq-amd", version="0.1.0", io="native",
-                 ingress_bytes=64 << 20, per_conn_read=256 << 10, mem_high_watermark=0, mem_low_watermark=0,
+                 ingress_bytes=64 << 20, per_conn_read=256 << 10, mem_high_watermark=None, mem_low_watermark=None,
                  store=None, node=None, reuseport=False, io_threads=4):
         """``io``: "pipeline" = native pipelined front end (csrc/core/frontend.cpp: IO
         threads + a stepper thread keeping two steps in flight, no Python per step),
@@ -129,7 +129,11 @@ class GpuBroker:
         # back-pressure (SURVEY A.Q17 / config 5): above the high watermark of stored
         # message bytes publishers get Connection.Blocked (if they announced the
         # capability) or Channel.Flow(active=false); released below the low watermark
-        self.mem_high, self.mem_low = mem_high_watermark, mem_low_watermark or mem_high_watermark // 2
+        # (on by default for a GPU plane: 40% of its HBM body log; 0 = off)
+        if mem_high_watermark is None:
+            mem_high_watermark = int(0.4 * plane.info["log_bytes"]) if hasattr(plane, "info") else 0
+        self.mem_high = mem_high_watermark
+        self.mem_low = mem_low_watermark if mem_low_watermark is not None else mem_high_watermark // 2
         self.blocked = False
         # durable queues x persistent messages -> store (write-behind, confirm gating)
         self.persistence = None
@@ -323,6 +327,8 @@ class GpuBroker:
                 events.append((conn, a, b))
             elif kind == FE_STATUS:
                 seg_status.append((conn, a))
+            elif kind == FE_GROW:   # rings past half full: double them (stepper paused)
+                self.plane.grow_queues(np.frombuffer(data, np.uint32).tolist())
             elif kind == FE_ERROR:
                 import logging
                 logging.getLogger("chanamq.gpu").error("data-plane engine failed: %s", data.decode(errors="replace"))
@@ -729,6 +735,8 @@ class GpuBroker:
         return "deferred"
 
     def _after_step(self, ctrl, events, seg_status, cnt, had_input, had_egress, txbuf=()):
+        if getattr(self.plane, "_grow", None):   # the plane is idle here: grow full rings
+            self.plane.grow_queues()
         self._tx_end()
         for conn, _, raw in txbuf:   # data commands of transactional channels, in wire order
             ch = struct.unpack_from(">H", raw, 1)[0]

@@ -15,6 +15,11 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 REFERENCE_CONF = os.path.join(os.path.dirname(os.path.dirname(_HERE)), "conf", "reference.conf")
 
 
+def _auto_wm(v, auto):
+    """-1 = automatic (host broker: 1 GiB high watermark; the low one then defaults to half)."""
+    return auto if v < 0 else v
+
+
 class ConfigError(Exception):
     pass
 
@@ -220,11 +225,44 @@ class Config:
             "default_vhost": g("chana.mq.amqp.vhost.default-id"),
             "data_dir": g("chana.mq.store.dir", ""),
             "fsync": bool(g("chana.mq.store.fsync", True)),
-            "mem_high_watermark": int(g("chana.mq.flow.memory-high-watermark", 0)),
-            "mem_low_watermark": int(g("chana.mq.flow.memory-low-watermark", 0)),
+            "mem_high_watermark": _auto_wm(int(g("chana.mq.flow.memory-high-watermark", -1)), 1 << 30),
+            "mem_low_watermark": _auto_wm(int(g("chana.mq.flow.memory-low-watermark", -1)),
+                                          _auto_wm(int(g("chana.mq.flow.memory-high-watermark", -1)), 1 << 30) // 2),
             "flow_channel": bool(g("chana.mq.flow.channel-flow", False)),
             "hash_wildcard": bool(g("chana.mq.routing.topic-hash-wildcard", True)),
         }
+
+    def gpu_config(self):
+        """``chana.mq.gpu.*`` -> (GpuDataPlane keyword arguments, GpuBroker keyword arguments)."""
+        g = self.get
+        k = "chana.mq.gpu."
+        store_dir = g("chana.mq.store.dir", "")
+        plane = dict(
+            device=int(g(k + "device", 0)), c_max=int(g(k + "max-connections", 1024)),
+            chpc=int(g(k + "channels-per-connection", 16)), q_max=int(g(k + "max-queues", 4096)),
+            x_max=int(g(k + "max-exchanges", 1024)), cons_max=int(g(k + "max-consumers", 16384)),
+            seg_max=int(g(k + "max-segments-per-step", 1024)), cmd_max=int(g(k + "max-commands-per-step", 131072)),
+            deliv_max=int(g(k + "max-deliveries-per-step", 65536)), deliver_cap=int(g(k + "deliver-cap", 8192)),
+            msg_max=int(g(k + "message-table", 1 << 22)), log_bytes=int(g(k + "body-log-bytes", 16 << 30)),
+            ring_pool=int(g(k + "queue-ring-pool", 1 << 26)),
+            default_queue_capacity=int(g(k + "queue-capacity", 1 << 16)), ucap=int(g(k + "unacked-window", 8192)),
+            ingress_cap=int(g(k + "ingress-bytes", 64 << 20)), egress_cap=int(g(k + "egress-bytes", 128 << 20)),
+            carry_cap=int(g(k + "carry-bytes", 256 << 10)), tb_max=int(g(k + "topic-bindings", 4096)),
+            frame_max=int(g("chana.mq.amqp.connection.frame-max")),
+            hash_wildcard=bool(g("chana.mq.routing.topic-hash-wildcard", True)))
+        if store_dir:
+            plane.update(persist=1, persist_max=int(g(k + "persist-records", 1 << 16)),
+                         persist_bytes=int(g(k + "persist-bytes", 256 << 20)))
+        hi = int(g("chana.mq.flow.memory-high-watermark", -1))
+        lo = int(g("chana.mq.flow.memory-low-watermark", -1))
+        if hi < 0:
+            hi = int(0.4 * plane["log_bytes"])
+        if lo < 0:
+            lo = hi // 2
+        broker = dict(io=str(g(k + "front-end", "pipeline")), io_threads=int(g(k + "io-threads", 4)),
+                      idle_step_ms=float(g(k + "idle-step-ms", 1.0)), per_conn_read=int(g(k + "per-conn-read", 256 << 10)),
+                      mem_high_watermark=hi, mem_low_watermark=lo)
+        return plane, broker
 
     def __repr__(self):
         return json.dumps(self.tree, indent=1, default=str)

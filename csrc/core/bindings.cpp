@@ -8,6 +8,7 @@
 #include "codec.hpp"
 #include "frontend.hpp"
 #include "persist.hpp"
+#include "tls_proxy.hpp"
 #include "gateway.hpp"
 #include "loadgen.hpp"
 #include "store.hpp"
@@ -255,6 +256,19 @@ PYBIND11_MODULE(_core, m) {
              o["rows"] = w.rows(); o["commits"] = w.commits(); o["body_bytes"] = w.bytes(); o["busy_s"] = w.busy_s();
              return o;
            });
+  py::class_<TlsProxy>(m, "TlsProxy")
+      .def(py::init([](py::dict d) {
+             TlsProxyCfg c;
+#define S(k, f) if (d.contains(k)) c.f = d[k].cast<decltype(c.f)>()
+             S("host", host); S("port", port); S("upstream_host", upstream_host); S("upstream_port", upstream_port);
+             S("cert", cert); S("key", key); S("p12", p12); S("p12_password", p12_password); S("buffer", buffer);
+#undef S
+             return new TlsProxy(c);
+           }))
+      .def_property_readonly("port", &TlsProxy::port)
+      .def("start", &TlsProxy::start)
+      .def("stop", &TlsProxy::stop, py::call_guard<py::gil_scoped_release>())
+      .def("connections", &TlsProxy::connections);
   py::class_<EchoEngine>(m, "EchoEngine")
       .def(py::init<u32, u32, u64, u32>(), py::arg("c_max") = 64, py::arg("seg_max") = 64,
            py::arg("ingress_cap") = 1 << 20, py::arg("carry_cap") = 1 << 16)

@@ -774,6 +774,12 @@ void Frontend::finish_oldest(std::deque<Inflight>& inflight) {
       post(std::move(e));
     }
   }
+  if (c.n_grow && api_->grow_host) {
+    FeEvent e;
+    e.kind = FE_GROW;
+    e.data.assign((const char*)api_->grow_host(api_->eng, p), 4ull * std::min<u32>(c.n_grow, GROW_MAX));
+    post(std::move(e));
+  }
   bool needs_commit = false;
   if (api_->persist && (c.n_persist || c.n_consumed)) {
     FeEvent e;
@@ -1027,6 +1033,7 @@ EchoEngine::EchoEngine(u32 c_max, u32 seg_max, u64 ingress_cap, u32 carry_cap) {
   api_.ctrl = [](void* e, int p) -> const u8* { return (const u8*)((EchoEngine*)e)->io_[p].ctrl.data(); };
   api_.egress_host = [](void* e, int slot) -> const u8* { return (const u8*)((EchoEngine*)e)->slot_[slot].data(); };
   api_.persist_host = [](void*, int) -> const u8* { return nullptr; };
+  api_.grow_host = [](void*, int) -> const u32* { return nullptr; };
   api_.consumed_host = [](void*, int) -> const ConsumedRec* { return nullptr; };
 }
 

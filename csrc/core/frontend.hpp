@@ -52,6 +52,7 @@ enum FeEventKind : int {
   FE_PERSIST = 8,   // store records of step a (data = packed PersistHdr records, data2 = ConsumedRec[]);
                     // that step's egress is held until release(a)
   FE_ERROR = 9,     // engine failure (data = message); the stepper stopped
+  FE_GROW = 10,     // queues past half their ring (data = u32 slots): the control plane grows them
 };
 
 struct FeEvent {

@@ -112,7 +112,7 @@ void PersistWorker::apply(const Batch& b) {
       m.body.assign(d + h.ex_len + h.rk_len + h.props_len, h.body_len);
       m.durable = true;
       m.refer = 1;
-      st_->insertMessage(m, 0);
+      st_->insertMessage(std::move(m), 0);
       bytes_ += h.body_len;
     } else {
       st_->updateMessageReferCount(h.msg_id, refs + 1);

@@ -82,6 +82,10 @@ void Store::write_all(const std::string& rec) {
 // commit, before confirms leave) or when the buffer passes 16 MB
 void Store::append(uint8_t op, const std::string& payload) {
   apply(op, payload);
+  append_wal(op, payload);
+}
+
+void Store::append_wal(uint8_t op, const std::string& payload) {
   if (fd_ < 0 || replaying_) return;
   const u32 len = (u32)payload.size() + 1;
   const size_t at = wbuf_.size();
@@ -310,6 +314,21 @@ void Store::insertMessage(const MsgRow& m, int64_t ttl_ms) {
   w.llng((u64)ttl_ms); w.llng((u64)now_ms());
   append(OP_MSG_INS, w.done());
 }
+// hot path of the GPU write-behind (persist.cpp): the row moves into the table instead of
+// being re-decoded from its WAL record
+void Store::insertMessage(MsgRow&& m, int64_t ttl_ms) {
+  LOCK;
+  Writer w;
+  const int64_t now = now_ms();
+  w.llng((u64)m.id); w.llng((u64)m.tstamp); w.longstr(m.header); w.longstr(m.body); w.longstr(m.exchange);
+  w.longstr(m.routing); w.octet(m.durable); w.lng((u32)m.refer);
+  w.llng((u64)ttl_ms); w.llng((u64)now);
+  append_wal(OP_MSG_INS, w.done());
+  m.expire_at = ttl_ms > 0 ? now + ttl_ms : 0;
+  const int64_t id = m.id;
+  msgs_[id] = std::move(m);
+}
+
 void Store::updateMessageReferCount(int64_t id, int32_t refer) {
   LOCK; Writer w; w.llng((u64)id); w.lng((u32)refer); append(OP_MSG_REFER, w.done());
 }

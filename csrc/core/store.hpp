@@ -66,6 +66,7 @@ class Store {
 
   // ---- messages
   void insertMessage(const MsgRow& m, int64_t ttl_ms);
+  void insertMessage(MsgRow&& m, int64_t ttl_ms);
   void updateMessageReferCount(int64_t id, int32_t refer);
   bool selectMessage(int64_t id, MsgRow* out);
   void deleteMessage(int64_t id);
@@ -106,6 +107,7 @@ class Store {
 
  private:
   void append(uint8_t op, const std::string& payload);
+  void append_wal(uint8_t op, const std::string& payload);
   void apply(uint8_t op, const std::string& payload);
   void replay();
   void write_all(const std::string& rec);

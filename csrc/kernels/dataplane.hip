@@ -317,6 +317,7 @@ __global__ __launch_bounds__(1024) void k_prep(DS d) {
   if (tid < sizeof(Counters) / 4) {
     u32* c = (u32*)d.ctr;
     if (tid * 4 < offsetof(Counters, log_head)) c[tid] = 0;
+    if (tid == 0) d.ctr->n_grow = 0;
   }
   u32 running = 0;
   for (u32 base = 0; base < d.seg_max; base += 1024) {
@@ -1812,9 +1813,22 @@ DEV u32 enqueue_one(const DS& d, u32 src, u32 i, u32 n, PersistRec* pr, u32 hs_n
   }
   if (last) {
     u64 cnt = rank + 1;
-    d.q_tail[q] = tail + (cnt < freec ? cnt : freec);
+    u64 nt = tail + (cnt < freec ? cnt : freec);
+    d.q_tail[q] = nt;
+    // past half the ring: ask the host to double it before the next step (unbounded queues,
+    // QueueEntity.scala:271-316 keeps a growing Vector)
+    if ((nt - head) * 2 > cap) {
+      u32 gi = atomicAdd(&d.ctr->n_grow, 1u);
+      if (gi < GROW_MAX) d.grow_h[gi] = q;
+    }
   }
   return drop;
+}
+
+// queue growth (host-driven, between steps): copy a ring's live range to its new ring
+__global__ void k_ring_move(Desc* ring, u64 old_off, u64 old_mask, u64 new_off, u64 new_mask, u64 head, u64 tail) {
+  for (u64 pos = head + (u64)blockIdx.x * blockDim.x + threadIdx.x; pos < tail; pos += (u64)gridDim.x * blockDim.x)
+    ring[new_off + (pos & new_mask)] = ring[old_off + (pos & old_mask)];
 }
 
 __global__ void k_enqueue(DS d, u32 src, u32 hs_ntiles) {

@@ -52,6 +52,7 @@ struct DS {
   ConnOut* conn_out_h;
   u8* ctrl_h;
   CtrlRec* ctrl_rec_h;
+  u32* grow_h;              // host-mapped: queue slots past half their ring this step
 
   // ---------------- per connection
   u8* carry;                // [c_max][carry_cap]

@@ -167,6 +167,7 @@ class Engine {
       io.ctrl_h = (u8*)hst(("ctrl" + sfx).c_str(), d_.ctrl_cap);
       io.ctrl_rec = (CtrlRec*)dev(("ctrl_rec_d" + sfx).c_str(), sizeof(CtrlRec) * d_.seg_max * 2);
       io.ctrl_rec_h = (CtrlRec*)hst(("ctrl_rec" + sfx).c_str(), sizeof(CtrlRec) * d_.seg_max * 2);
+      io.grow_h = (u32*)hst(("grow" + sfx).c_str(), 4ull * GROW_MAX);
       io.xchg = (u32*)hst(("xchg" + sfx).c_str(), 4ull * (4 * WORLD_MAX + 4));
       if (d_.persist) {
         io.persist_h = (u8*)hst(("persist" + sfx).c_str(), d_.persist_bytes + 64);
@@ -384,7 +385,7 @@ class Engine {
       io.ctr_host = io_[p].ctr_host; io.conn_out = io_[p].conn_out;
       io.ctrl = io_[p].ctrl; io.ctrl_rec = io_[p].ctrl_rec; io.xchg = io_[p].xchg;
       io.seg_out_h = io_[p].seg_out_h; io.conn_out_h = io_[p].conn_out_h; io.ctrl_h = io_[p].ctrl_h;
-      io.ctrl_rec_h = io_[p].ctrl_rec_h;
+      io.ctrl_rec_h = io_[p].ctrl_rec_h; io.grow_h = io_[p].grow_h;
       io.persist_h = io_[p].persist_h; io.crec_h = io_[p].crec_h;
       static_cast<DS&>(io_[p]) = io;
     }
@@ -699,6 +700,24 @@ class Engine {
     return c->n_routed_msgs;
   }
 
+  // queue growth between steps: move the live entries [head, tail) of one ring to a new,
+  // larger ring (positions stay absolute: entry pos lives at off + (pos & mask))
+  void ring_move(u64 old_off, u64 old_mask, u64 new_off, u64 new_mask, u64 head, u64 tail) {
+    if (inflight_[0] || inflight_[1]) throw std::runtime_error("ring_move() between steps only");
+    if (tail < head || tail - head > old_mask + 1 || tail - head > new_mask + 1 ||
+        new_off + new_mask + 1 > d_.ring_pool || old_off + old_mask + 1 > d_.ring_pool)
+      throw std::runtime_error("ring_move: bad ring geometry");
+    sync();
+    if (tail > head) {
+      u64 n = tail - head;
+      u32 nb = (u32)std::min<u64>(4096, (n + 255) / 256);
+      hipLaunchKernelGGL(k_ring_move, dim3(nb), dim3(256), 0, s_comp_, d_.ring, old_off, old_mask, new_off, new_mask,
+                         head, tail);
+      HIPCHECK(hipGetLastError());
+    }
+    HIPCHECK(hipStreamSynchronize(s_comp_));
+  }
+
   // Basic.Get between steps: (status, message_count, frames, tag, msg_id, qpos, persist,
   // expired [(msg_id, q, qpos)] of durable x persistent messages dropped by the TTL skip)
   py::tuple basic_get(u32 q, u32 chslot, u32 noack, i64 now_ms) {
@@ -782,6 +801,7 @@ class Engine {
     a.persist_host = [](void* e, int p) -> const u8* { return ((Engine*)e)->io_[p].persist_hh; };
     a.consumed_host = [](void* e, int p) -> const ConsumedRec* { return ((Engine*)e)->io_[p].crec_hh; };
     a.wblock = (u32*)buf("conn_wblock").ptr;
+    a.grow_host = [](void* e, int p) -> const u32* { return ((Engine*)e)->io_[p].grow_hh; };
     for (int p = 0; p < 2; ++p) {
       std::string sfx = std::to_string(p);
       HostIO& h = io_[p];
@@ -792,6 +812,7 @@ class Engine {
       h.ctrl_hh = (const u8*)buf("ctrl" + sfx).ptr;
       h.persist_hh = d_.persist ? (const u8*)buf("persist" + sfx).ptr : nullptr;
       h.crec_hh = d_.persist ? (const ConsumedRec*)buf("consumed" + sfx).ptr : nullptr;
+      h.grow_hh = (const u32*)buf("grow" + sfx).ptr;
     }
     return (u64)&api_;
   }
@@ -925,7 +946,7 @@ class Engine {
     F(n_dropped_nomem); F(n_expired); F(n_routed_msgs); F(n_unknown_exchange); F(n_ring_full);
     F(n_acked); F(log_head); F(log_tail); F(msg_free_top); F(n_live_msgs);
     F(n_persist); F(n_consumed); F(persist_used); F(n_persist_overflow);
-    F(live_bytes);
+    F(live_bytes); F(n_grow);
 #undef F
     std::vector<u32> lat(c.lat_hist, c.lat_hist + LAT_BINS);
     o["lat_hist"] = lat;
@@ -1115,6 +1136,7 @@ class Engine {
     const u8* ctrl_hh = nullptr;
     const u8* persist_hh = nullptr;
     const ConsumedRec* crec_hh = nullptr;
+    const u32* grow_hh = nullptr;
   };
   HostIO io_[2];
   CmqEngineApi api_{};
@@ -1186,6 +1208,7 @@ PYBIND11_MODULE(_dataplane, m) {
       .def("set_xfer_parity", &Engine::set_xfer_parity)
       .def("set_import", &Engine::set_import, py::arg("recv"), py::arg("stream") = 0)
       .def("restore", &Engine::restore, py::arg("desc"), py::arg("payload"), py::arg("now_ms"))
+      .def("ring_move", &Engine::ring_move)
       .def("basic_get", &Engine::basic_get, py::arg("q"), py::arg("chslot"), py::arg("noack"), py::arg("now_ms"))
       .def("wait_results", &Engine::wait_results)
       .def("egress_copy", &Engine::egress_copy)

@@ -74,7 +74,8 @@ struct Counters {       // per-step counters (device -> host)
   u64 log_head, log_tail;
   u32 msg_free_top, n_live_msgs;
   i64 live_bytes;       // body-log slot bytes of live messages (exact, unlike head - tail)
-  u32 pad[4];
+  u32 n_grow;           // queues past half their ring this step (grow_host list)
+  u32 pad[3];
 };
 
 struct CtrlRec { u32 conn; u32 off; u32 len; u32 seg; };
@@ -105,4 +106,6 @@ struct CmqEngineApi {
   const u8* (*persist_host)(void* eng, int p);           // packed PersistHdr records (persist=1)
   const ConsumedRec* (*consumed_host)(void* eng, int p);
   u32* wblock;   // host-mapped u32[c_max]: nonzero = do not dequeue to this connection (egress back-pressure)
+  const u32* (*grow_host)(void* eng, int p);             // queue slots to grow (Counters.n_grow of them)
 };
+#define GROW_MAX 4096   // grow requests reported per step

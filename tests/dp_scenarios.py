@@ -197,7 +197,7 @@ def sc_confirm_ring_full(dp):
     overflows the ring confirms its range with Basic.Nack (never an Ack for a dropped
     message); later steps that store everything are acked again."""
     dp.declare_exchange(VH, "rx", "direct")
-    dp.declare_queue(VH, "small", capacity=16)
+    dp.declare_queue(VH, "small", capacity=16, max_capacity=16)
     dp.declare_queue(VH, "big")
     dp.bind(VH, "small", "rx", "s")
     dp.bind(VH, "big", "rx", "b")
@@ -226,7 +226,19 @@ def sc_big_segment(dp):
     return [{1: s}, {}]
 
 
+def sc_ring_growth(dp):
+    """Queues grow: an 8-slot ring past half full doubles between steps, so a confirm-mode
+    publisher's messages are all stored (acked) and later all delivered in order."""
+    dp.declare_queue(VH, "grow", capacity=8)
+    dp.open_connection(1, VH)
+    dp.open_channel(1, 1)
+    dp.confirm_select(1, 1)
+    s = [publish_stream(n, "", lambda i: "grow", 24, seed=30 + k) for k, n in enumerate((6, 10, 15))]
+    return [{1: s[0]}, {1: s[1]}, {1: s[2]}, {"__consume__": [(2, 1, "grow", "gc")]}, {}, {}]
+
+
 SCENARIOS = {
+    "ring_growth": sc_ring_growth,
     "confirm_ring_full": sc_confirm_ring_full,
     "big_segment": sc_big_segment,
     "window_wrap": sc_window_wrap,
@@ -254,6 +266,10 @@ def run(dp, steps, now_step_ms=None):
         inp = dict(inp)
         for c in inp.pop("__unpause__", []):
             dp.unpause(c)
+        for conn, ch, qn, tag in inp.pop("__consume__", []):   # a consumer attaches between steps
+            dp.open_connection(conn, VH)
+            dp.open_channel(conn, ch)
+            dp.consume(conn, ch, VH, qn, tag, no_ack=True)
         now = NOW + (now_step_ms or 0) * k
         gets = []
         for conn, ch, qn, no_ack in inp.pop("__get__", []):   # Basic.Get between steps

@@ -146,3 +146,13 @@ def test_big_segment_delivers_all():
     g, outs, pc = run_sc("big_segment")
     d = [c for c in pc[2] if c.method.name == "basic.deliver"]
     assert len(d) == 150 and all(len(c.body) == 1000 for c in d)
+
+
+def test_ring_growth_stores_and_delivers_everything():
+    g, outs, pc = run_sc("ring_growth")
+    acks = [c.method for c in pc[1]]
+    assert [(m.name, m.delivery_tag) for m in acks] == [("basic.ack", 6), ("basic.ack", 16), ("basic.ack", 31)]
+    d = [c for c in pc[2] if c.method.name == "basic.deliver"]
+    assert len(d) == 31 and [c.method.delivery_tag for c in d] == list(range(1, 32))
+    assert g.queues[("AMQ.DEFAULT", "grow")].capacity == 64
+    assert g.counters["n_ring_full"] == 0

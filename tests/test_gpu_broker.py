@@ -356,3 +356,27 @@ def test_admin_rest_on_gpu_server(broker):
         p.close()
     finally:
         adm.stop()
+
+
+def test_confirmed_publishes_into_a_small_queue_are_never_lost(broker):
+    """A confirm-mode publisher fills a consumer-less queue declared with a 4,096-slot ring
+    (GPU_CFG default) with 20,000 messages: rings grow between steps, so every publish is
+    acked (none nacked) and every message is later delivered, in order."""
+    n = 20000 if hasattr(broker.plane, "eng") else 5000   # the golden (CPU) plane is slow
+    p = conn(broker)
+    ch = p.channel()
+    ch.queue_declare("deep")
+    ch.confirm_select()
+    for i in range(n):
+        ch.basic_publish("", "deep", i.to_bytes(4, "big"))
+        if i % 2000 == 1999:
+            p.process(0.01)
+    assert ch.wait_for_confirms(timeout=60)
+    assert ch.queue_declare("deep", passive=True).message_count == n
+    c = conn(broker)
+    cc = c.channel()
+    cc.basic_consume("deep", "deepc", no_ack=True)
+    got = cc.consume_n(n, timeout=120)
+    assert [int.from_bytes(d.body, "big") for d in got] == list(range(n))
+    p.close()
+    c.close()

@@ -41,3 +41,37 @@ def test_tls_publish_consume(tmp_path, kind):
         c.close()
     finally:
         b.stop()
+
+
+@pytest.mark.parametrize("kind", ["pem", "p12"])
+def test_tls_proxy_terminates_for_a_plain_broker(tmp_path, kind):
+    """The AMQPS front of the GPU-path server (csrc/core/tls_proxy.cpp): TLS clients on one
+    port, plain AMQP to the broker's listener.  Upstream here is the host broker."""
+    key, crt, p12 = make_cert(tmp_path)
+    core = load()
+    b = core.Broker({"port": 0, "host": "127.0.0.1", "heartbeat": 0})
+    b.start()
+    cfg = {"port": 0, "upstream_port": b.port}
+    if kind == "pem":
+        cfg.update(cert=str(crt), key=str(key))
+    else:
+        cfg.update(p12=str(p12), p12_password="abcdef")
+    px = core.TlsProxy(cfg)
+    px.start()
+    try:
+        conns = [Connection(port=px.port, tls=True) for _ in range(3)]
+        ch = conns[0].channel()
+        ch.queue_declare("via.proxy")
+        body = bytes(range(256)) * 3000
+        for i in range(5):
+            ch.basic_publish("", "via.proxy", body + bytes([i]))
+        cc = conns[1].channel()
+        cc.basic_consume("via.proxy", "pc", no_ack=True)
+        got = cc.consume_n(5)
+        assert [g.body for g in got] == [body + bytes([i]) for i in range(5)]
+        assert px.connections() == 3
+        for c in conns:
+            c.close()
+    finally:
+        px.stop()
+        b.stop()
