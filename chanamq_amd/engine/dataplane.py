@@ -15,7 +15,7 @@ import numpy as np
 from .. import ops
 from ..protocol import constants as C
 from .control import ControlError, ControlState
-from .layout import (CONN_OUT, CONSUMED_REC, CTRL_REC, CTRL_TXBUF, INVALID, MF_PERSIST, MF_REDELIVERED, MF_RESTORE,
+from .layout import (CONN_OUT, CONSUMED_REC, RING_MOVE, CTRL_REC, CTRL_TXBUF, INVALID, MF_PERSIST, MF_REDELIVERED, MF_RESTORE,
                      PERSIST_HDR, RDESC, SEG_IN, SEG_OUT, SS_CTRL, US_ACKED, US_PENDING, US_REQUEUE, USLOT,
                      chan_hash, direct_key, exch_hash, fnv1a64, topic_pattern_row, topic_word_offsets)
 
@@ -84,7 +84,6 @@ class GpuDataPlane(ControlState):
         self._egress = [self.eng.host_view(f"egress_host{e}") for e in range(i["egress_slots"])]
         self._pin = [None, None]
         self.exchanger = exchanger
-        self._grow = set()        # queue slots the device reported past half their ring
         self._get_consumed = []   # store records of Basic.Get, emitted with the next step's
         self._pending = None
         self.lag = False
@@ -286,6 +285,7 @@ class GpuDataPlane(ControlState):
         self._up_at("q_durable", int(q.durable), q.slot, np.uint32)
         self._up_at("q_ring_off", q.ring_off, q.slot, np.uint64)
         self._up_at("q_ring_mask", q.capacity - 1, q.slot, np.uint64)
+        self._up_at("q_max_cap", q.max_capacity, q.slot, np.uint64)
         self._up_at("q_head", 0, q.slot, np.uint64)
         self._up_at("q_tail", 0, q.slot, np.uint64)
         self._up_at("q_ttl", q.ttl_ms, q.slot, np.int64)
@@ -296,6 +296,12 @@ class GpuDataPlane(ControlState):
 
     def queue_deleted(self, q):
         self._up_at("q_active", 0, q.slot, np.uint32)
+        # if the device grew the ring since the host last looked, ControlState just freed the
+        # abandoned range (free anyway); the live one goes back to the pool too
+        off = self._u64("q_ring_off", q.slot)
+        cap = self._u64("q_ring_mask", q.slot) + 1
+        if (off, cap) != (q.ring_off, q.capacity):
+            self._ring_free.setdefault(cap, []).append(off)
         self._sync_consumers()
 
     def consumers_changed(self, q, cid, removed=False):
@@ -449,6 +455,7 @@ class GpuDataPlane(ControlState):
         if n <= 0:
             return 0
         qq = self.queue_by_slot[q]
+        self._refresh_ring(qq)
         mask = qq.capacity - 1
         base = qq.ring_off * 16
         for lo in range(head, tail, mask + 1):
@@ -535,34 +542,37 @@ class GpuDataPlane(ControlState):
 
     def step_raw(self, segs, payload_ptr, payload_len, now_ms=None, collect=True):
         t = self.submit_raw(segs, payload_ptr, payload_len, now_ms)
-        res = self.finish(t, collect=collect)
-        self.grow_queues()
-        return res
+        return self.finish(t, collect=collect)
 
-    def grow_queues(self, slots=None):
-        """Between steps: double the rings of queues the device reported past half full
-        (k_enqueue -> grow list), moving their live entries on the device.  Returns the
-        slots grown."""
-        if slots is not None:
-            self._grow.update(slots)
-        done = []
-        for slot in sorted(self._grow):
-            q = self.queue_by_slot.get(slot)
-            if q is None or q.owner != self.rank:
-                continue
-            head, tail = self._u64("q_head", slot), self._u64("q_tail", slot)
-            new = self.grow_target(q, tail - head)
-            if new is None:
-                continue
-            old = self.regrow_ring(q, new)
-            if old is None:
-                continue
-            self.eng.ring_move(old[0], old[1] - 1, q.ring_off, new - 1, head, tail)
-            self._up_at("q_ring_off", q.ring_off, slot, np.uint64)
-            self._up_at("q_ring_mask", new - 1, slot, np.uint64)
-            done.append(slot)
-        self._grow.clear()
-        return done
+    # ---- unbounded queues: the device grows rings (k_ring_plan); the host mirrors it
+    def _ring_alloc(self, cap):
+        """Rings come from one pool whose bump pointer lives on the device (k_ring_plan
+        allocates from it mid-step); ranges returned by deletes / growth are reused first."""
+        lst = self._ring_free.get(cap)
+        if lst:
+            return lst.pop()
+        top = self._u64("ring_top", 0)
+        if top + cap > self.ring_pool:
+            raise ControlError(C.RESOURCE_ERROR, "ring pool exhausted")
+        self._up_at("ring_top", top + cap, 0, np.uint64)
+        return top
+
+    def _refresh_ring(self, q):
+        """The device may have moved the queue's ring: adopt its current one and return the
+        range the host knew to the pool."""
+        off = self._u64("q_ring_off", q.slot)
+        cap = self._u64("q_ring_mask", q.slot) + 1
+        if (off, cap) != (q.ring_off, q.capacity):
+            self._ring_free.setdefault(q.capacity, []).append(q.ring_off)
+            q.ring_off, q.capacity = off, cap
+
+    def rings_moved(self, raw):
+        """RingMove records of a finished step (or the front end's FE_GROW event)."""
+        for mv in np.frombuffer(raw, RING_MOVE):
+            q = self.queue_by_slot.get(int(mv["q"]))
+            if q is not None and q.owner == self.rank and q.ring_off == int(mv["old_off"]):
+                self._ring_free.setdefault(q.capacity, []).append(q.ring_off)
+                q.ring_off, q.capacity = int(mv["new_off"]), int(mv["new_mask"]) + 1
 
     def submit_raw(self, segs, payload_ptr, payload_len, now_ms=None):
         """Asynchronous half of a step: returns a ticket for ``finish``.  At most two
@@ -627,8 +637,7 @@ class GpuDataPlane(ControlState):
         res.counters = c = self.eng.counters(p)
         self.last_counters = c
         if c["n_grow"]:
-            g = np.frombuffer(self.eng.host_view(f"grow{p}")[:4 * min(c["n_grow"], 4096)].tobytes(), np.uint32)
-            self._grow.update(int(x) for x in g)
+            self.rings_moved(self.eng.host_view(f"grow{p}")[:RING_MOVE.itemsize * min(c["n_grow"], 4096)].tobytes())
         io = self._io[p]
         so = io["seg_out"][:nseg]
         self.carry[so["conn"]] = so["carry"]

@@ -588,21 +588,9 @@ class GoldenDataPlane(ControlState):
                 self._consumed(d["msg"], d["q"], d["qpos"], 0)
                 self._release(d["msg"])
         cnt["n_deliv"] = len(delivs)
-        self._grow_rings()
         self.step_no += 1
         out["counters"] = dict(cnt)
         return out
-
-    def _grow_rings(self):
-        """Mirror of GpuDataPlane.grow_queues: after the step, rings past half full double."""
-        for q, qq in self.queue_by_slot.items():
-            if qq.owner != self.rank:
-                continue
-            depth = len(self.ring.get(q, []))
-            if depth * 2 > qq.capacity:
-                new = self.grow_target(qq, depth)
-                if new is not None:
-                    self.regrow_ring(qq, new)
 
     def _release(self, msg):
         msg.refcnt -= 1
@@ -680,6 +668,10 @@ class GoldenDataPlane(ControlState):
         for q in qs:
             qq = self.queue_by_slot[q]
             ring = self.ring[q]
+            if len(ring) >= qq.capacity:   # the device grows the ring before enqueueing (k_ring_plan)
+                new = self.grow_target(qq, len(ring) + 1)
+                if new is not None:
+                    self.regrow_ring(qq, new)
             if len(ring) >= qq.capacity:
                 cnt["n_ring_full"] += 1
                 self._release(msg)

@@ -22,6 +22,9 @@ PERSIST_HDR = np.dtype([("msg_id", "<i8"), ("ts_ms", "<i8"), ("qpos", "<u8"), ("
                         ("body_len", "<u4"), ("props_len", "<u2"), ("ex_len", "u1"), ("rk_len", "u1"),
                         ("size", "<u4")])
 CONSUMED_REC = np.dtype([("msg_id", "<i8"), ("qpos", "<u8"), ("q", "<u4"), ("kind", "<u4"), ("pad", "<u4", 2)])
+# a queue ring grown by the device (step_abi.h RingMove)
+RING_MOVE = np.dtype([("q", "<u4"), ("pad", "<u4"), ("old_off", "<u8"), ("old_mask", "<u8"), ("new_off", "<u8"),
+                      ("new_mask", "<u8"), ("head", "<u8"), ("tail", "<u8")])
 assert PERSIST_HDR.itemsize == 48 and CONSUMED_REC.itemsize == 32
 
 # per-channel unacked window slot (dp_common.h USlot)

@@ -327,8 +327,8 @@ class GpuBroker:
                 events.append((conn, a, b))
             elif kind == FE_STATUS:
                 seg_status.append((conn, a))
-            elif kind == FE_GROW:   # rings past half full: double them (stepper paused)
-                self.plane.grow_queues(np.frombuffer(data, np.uint32).tolist())
+            elif kind == FE_GROW:   # the device grew rings: return the old ranges to the pool
+                self.plane.rings_moved(data)
             elif kind == FE_ERROR:
                 import logging
                 logging.getLogger("chanamq.gpu").error("data-plane engine failed: %s", data.decode(errors="replace"))
@@ -735,8 +735,6 @@ class GpuBroker:
         return "deferred"
 
     def _after_step(self, ctrl, events, seg_status, cnt, had_input, had_egress, txbuf=()):
-        if getattr(self.plane, "_grow", None):   # the plane is idle here: grow full rings
-            self.plane.grow_queues()
         self._tx_end()
         for conn, _, raw in txbuf:   # data commands of transactional channels, in wire order
             ch = struct.unpack_from(">H", raw, 1)[0]

@@ -777,7 +777,7 @@ void Frontend::finish_oldest(std::deque<Inflight>& inflight) {
   if (c.n_grow && api_->grow_host) {
     FeEvent e;
     e.kind = FE_GROW;
-    e.data.assign((const char*)api_->grow_host(api_->eng, p), 4ull * std::min<u32>(c.n_grow, GROW_MAX));
+    e.data.assign((const char*)api_->grow_host(api_->eng, p), sizeof(RingMove) * std::min<u32>(c.n_grow, GROW_MAX));
     post(std::move(e));
   }
   bool needs_commit = false;
@@ -1033,7 +1033,7 @@ EchoEngine::EchoEngine(u32 c_max, u32 seg_max, u64 ingress_cap, u32 carry_cap) {
   api_.ctrl = [](void* e, int p) -> const u8* { return (const u8*)((EchoEngine*)e)->io_[p].ctrl.data(); };
   api_.egress_host = [](void* e, int slot) -> const u8* { return (const u8*)((EchoEngine*)e)->slot_[slot].data(); };
   api_.persist_host = [](void*, int) -> const u8* { return nullptr; };
-  api_.grow_host = [](void*, int) -> const u32* { return nullptr; };
+  api_.grow_host = [](void*, int) -> const RingMove* { return nullptr; };
   api_.consumed_host = [](void*, int) -> const ConsumedRec* { return nullptr; };
 }
 

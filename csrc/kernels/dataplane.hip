@@ -317,7 +317,7 @@ __global__ __launch_bounds__(1024) void k_prep(DS d) {
   if (tid < sizeof(Counters) / 4) {
     u32* c = (u32*)d.ctr;
     if (tid * 4 < offsetof(Counters, log_head)) c[tid] = 0;
-    if (tid == 0) d.ctr->n_grow = 0;
+    if (tid == 0) { d.ctr->n_grow = 0; d.tot[TS_NMOVE] = 0; }
   }
   u32 running = 0;
   for (u32 base = 0; base < d.seg_max; base += 1024) {
@@ -1815,20 +1815,64 @@ DEV u32 enqueue_one(const DS& d, u32 src, u32 i, u32 n, PersistRec* pr, u32 hs_n
     u64 cnt = rank + 1;
     u64 nt = tail + (cnt < freec ? cnt : freec);
     d.q_tail[q] = nt;
-    // past half the ring: ask the host to double it before the next step (unbounded queues,
-    // QueueEntity.scala:271-316 keeps a growing Vector)
-    if ((nt - head) * 2 > cap) {
-      u32 gi = atomicAdd(&d.ctr->n_grow, 1u);
-      if (gi < GROW_MAX) d.grow_h[gi] = q;
-    }
   }
   return drop;
 }
 
-// queue growth (host-driven, between steps): copy a ring's live range to its new ring
-__global__ void k_ring_move(Desc* ring, u64 old_off, u64 old_mask, u64 new_off, u64 new_mask, u64 head, u64 tail) {
-  for (u64 pos = head + (u64)blockIdx.x * blockDim.x + threadIdx.x; pos < tail; pos += (u64)gridDim.x * blockDim.x)
-    ring[new_off + (pos & new_mask)] = ring[old_off + (pos & old_mask)];
+// ---- unbounded queues (QueueEntity.scala:271-316 keeps a growing Vector): before the
+// step's enqueue, the last pair of every queue checks that the queue's ring holds this
+// step's entries; if not, the ring moves to one of >= 2x the needed size taken from the
+// ring pool (one bump pointer shared with the host's allocator), within the queue's
+// max_capacity.  Positions stay absolute (entry pos lives at off + (pos & mask)), so
+// unacked windows, requeues and store rows keep their queue offsets.
+__global__ void k_ring_plan(DS d, u32 src, u32 hs_ntiles) {
+  const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+  const u32 n = d.tot[TS_PAIR_N];
+  if (i >= n) return;
+  const u32* kk = d.pair_k[src];
+  const u32 rb = d.rank_bits;
+  const u32 q = kk[i] >> rb;
+  if (i + 1 < n && (kk[i + 1] >> rb) == q) return;   // not the queue's last pair
+  const u32 first = hs_ntiles ? d.hist_scan[(q << rb) * hs_ntiles] : d.q_first[q];
+  const u64 cnt = (u64)(i - first) + 1;
+  const u64 head = d.q_head[q], tail = d.q_tail[q];
+  const u64 mask = d.q_ring_mask[q], cap = mask + 1;
+  const u64 need = tail - head + cnt;
+  if (need <= cap) return;
+  const u64 limit = d.q_max_cap[q] ? d.q_max_cap[q] : d.ring_pool;
+  u64 want = cap;
+  while (want < 2 * need && want * 2 <= limit) want *= 2;
+  if (want <= cap) return;                            // at max_capacity: the overflow drops (nack)
+  unsigned long long* top = (unsigned long long*)d.ring_top;
+  u64 off = __hip_atomic_load(top, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  while (true) {
+    if (off + want > d.ring_pool) return;            // pool exhausted: drops (nack)
+    u64 prev = atomicCAS(top, off, off + want);
+    if (prev == off) break;
+    off = prev;
+  }
+  RingMove mv;
+  mv.q = q; mv.pad = 0;
+  mv.old_off = d.q_ring_off[q]; mv.old_mask = mask;
+  mv.new_off = off; mv.new_mask = want - 1;
+  mv.head = head; mv.tail = tail;
+  const u32 mi = atomicAdd(&d.tot[TS_NMOVE], 1u);
+  d.moves[mi] = mv;                                  // mi < q_max: one move per queue
+  d.q_ring_off[q] = off;
+  d.q_ring_mask[q] = want - 1;
+  const u32 gi = atomicAdd(&d.ctr->n_grow, 1u);      // the host reclaims the old ring
+  if (gi < GROW_MAX) d.grow_h[gi] = mv;
+}
+
+// copy every moved ring's live entries (all blocks stride over each move in turn)
+__global__ __launch_bounds__(256) void k_ring_moves(DS d) {
+  const u32 nm = d.tot[TS_NMOVE];
+  const u64 g = (u64)blockIdx.x * blockDim.x + threadIdx.x, gs = (u64)gridDim.x * blockDim.x;
+  for (u32 m = 0; m < nm; ++m) {
+    const RingMove mv = d.moves[m];
+    for (u64 pos = mv.head + g; pos < mv.tail; pos += gs)
+      d.ring[mv.new_off + (pos & mv.new_mask)] = d.ring[mv.old_off + (pos & mv.old_mask)];
+  }
 }
 
 __global__ void k_enqueue(DS d, u32 src, u32 hs_ntiles) {

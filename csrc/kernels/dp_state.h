@@ -25,6 +25,7 @@ enum : u32 {
   TS_NRUNS = 27,                        // delivery runs of the step (k_runs)
   TS_REQ_TICKET = 28,                   // k_requeue finished-block ticket (last block compacts)
   TS_RS_TICKET = 29,                    // k_rs_hist finished-block ticket (last block: offsets)
+  TS_NMOVE = 30,                        // rings moved (grown) this step (k_ring_plan)
   TS_XSCAN = 32                         // + 2*r: per-destination record / byte totals
 };
 
@@ -52,7 +53,10 @@ struct DS {
   ConnOut* conn_out_h;
   u8* ctrl_h;
   CtrlRec* ctrl_rec_h;
-  u32* grow_h;              // host-mapped: queue slots past half their ring this step
+  RingMove* grow_h;         // host-mapped: rings grown this step (the host reclaims the old ones)
+  RingMove* moves;          // this step's ring moves (k_ring_plan -> k_ring_moves)
+  u64* ring_top;            // ring pool bump pointer (shared with the host allocator)
+  u64* q_max_cap;           // per queue ring growth limit (0 = the pool)
 
   // ---------------- per connection
   u8* carry;                // [c_max][carry_cap]

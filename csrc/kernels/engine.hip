@@ -167,7 +167,7 @@ class Engine {
       io.ctrl_h = (u8*)hst(("ctrl" + sfx).c_str(), d_.ctrl_cap);
       io.ctrl_rec = (CtrlRec*)dev(("ctrl_rec_d" + sfx).c_str(), sizeof(CtrlRec) * d_.seg_max * 2);
       io.ctrl_rec_h = (CtrlRec*)hst(("ctrl_rec" + sfx).c_str(), sizeof(CtrlRec) * d_.seg_max * 2);
-      io.grow_h = (u32*)hst(("grow" + sfx).c_str(), 4ull * GROW_MAX);
+      io.grow_h = (RingMove*)hst(("grow" + sfx).c_str(), sizeof(RingMove) * GROW_MAX);
       io.xchg = (u32*)hst(("xchg" + sfx).c_str(), 4ull * (4 * WORLD_MAX + 4));
       if (d_.persist) {
         io.persist_h = (u8*)hst(("persist" + sfx).c_str(), d_.persist_bytes + 64);
@@ -298,6 +298,9 @@ class Engine {
     d_.q_active = (u32*)dev("q_active", 4ull * d_.q_max);
     d_.q_cons = (u32*)dev("q_cons", 4ull * d_.cons_max);
     d_.ring = (Desc*)dev("ring", sizeof(Desc) * d_.ring_pool);
+    d_.ring_top = (u64*)dev("ring_top", 8);
+    d_.q_max_cap = (u64*)dev("q_max_cap", 8ull * d_.q_max);
+    d_.moves = (RingMove*)dev("moves", sizeof(RingMove) * (u64)d_.q_max);
 
     d_.ch_confirm = (u32*)dev("ch_confirm", 4ull * nch);
     d_.ch_pub_cnt = (u32*)dev("ch_pub_cnt", 4ull * nch);
@@ -700,24 +703,6 @@ class Engine {
     return c->n_routed_msgs;
   }
 
-  // queue growth between steps: move the live entries [head, tail) of one ring to a new,
-  // larger ring (positions stay absolute: entry pos lives at off + (pos & mask))
-  void ring_move(u64 old_off, u64 old_mask, u64 new_off, u64 new_mask, u64 head, u64 tail) {
-    if (inflight_[0] || inflight_[1]) throw std::runtime_error("ring_move() between steps only");
-    if (tail < head || tail - head > old_mask + 1 || tail - head > new_mask + 1 ||
-        new_off + new_mask + 1 > d_.ring_pool || old_off + old_mask + 1 > d_.ring_pool)
-      throw std::runtime_error("ring_move: bad ring geometry");
-    sync();
-    if (tail > head) {
-      u64 n = tail - head;
-      u32 nb = (u32)std::min<u64>(4096, (n + 255) / 256);
-      hipLaunchKernelGGL(k_ring_move, dim3(nb), dim3(256), 0, s_comp_, d_.ring, old_off, old_mask, new_off, new_mask,
-                         head, tail);
-      HIPCHECK(hipGetLastError());
-    }
-    HIPCHECK(hipStreamSynchronize(s_comp_));
-  }
-
   // Basic.Get between steps: (status, message_count, frames, tag, msg_id, qpos, persist,
   // expired [(msg_id, q, qpos)] of durable x persistent messages dropped by the TTL skip)
   py::tuple basic_get(u32 q, u32 chslot, u32 noack, i64 now_ms) {
@@ -801,7 +786,7 @@ class Engine {
     a.persist_host = [](void* e, int p) -> const u8* { return ((Engine*)e)->io_[p].persist_hh; };
     a.consumed_host = [](void* e, int p) -> const ConsumedRec* { return ((Engine*)e)->io_[p].crec_hh; };
     a.wblock = (u32*)buf("conn_wblock").ptr;
-    a.grow_host = [](void* e, int p) -> const u32* { return ((Engine*)e)->io_[p].grow_hh; };
+    a.grow_host = [](void* e, int p) -> const RingMove* { return ((Engine*)e)->io_[p].grow_hh; };
     for (int p = 0; p < 2; ++p) {
       std::string sfx = std::to_string(p);
       HostIO& h = io_[p];
@@ -812,7 +797,7 @@ class Engine {
       h.ctrl_hh = (const u8*)buf("ctrl" + sfx).ptr;
       h.persist_hh = d_.persist ? (const u8*)buf("persist" + sfx).ptr : nullptr;
       h.crec_hh = d_.persist ? (const ConsumedRec*)buf("consumed" + sfx).ptr : nullptr;
-      h.grow_hh = (const u32*)buf("grow" + sfx).ptr;
+      h.grow_hh = (const RingMove*)buf("grow" + sfx).ptr;
     }
     return (u64)&api_;
   }
@@ -1041,6 +1026,8 @@ class Engine {
     const u32 pbits = d.q_bits + d.rank_bits;
     const u32 hs_ntiles = pbits <= 8 ? ceil_div(d.pair_max, SORT_TILE) : 0;   // single pass: starts from hist_scan
     if (!hs_ntiles) hipLaunchKernelGGL(k_qfirst, blocks(d.pair_max, 256), dim3(256), 0, s, d, psrc);
+    hipLaunchKernelGGL(k_ring_plan, blocks(d.pair_max, 256), dim3(256), 0, s, d, psrc, hs_ntiles);
+    hipLaunchKernelGGL(k_ring_moves, dim3(256), dim3(256), 0, s, d);
     hipLaunchKernelGGL(k_enqueue, blocks(d.pair_max, 256), dim3(256), 0, s, d, psrc, hs_ntiles);
     hipLaunchKernelGGL(k_chan_advance, dim3(nch < 2048 ? nch : 2048), dim3(256), 0, s, d);
     // requeued deliveries go back in front of their queues' heads before this step's
@@ -1136,7 +1123,7 @@ class Engine {
     const u8* ctrl_hh = nullptr;
     const u8* persist_hh = nullptr;
     const ConsumedRec* crec_hh = nullptr;
-    const u32* grow_hh = nullptr;
+    const RingMove* grow_hh = nullptr;
   };
   HostIO io_[2];
   CmqEngineApi api_{};
@@ -1208,7 +1195,6 @@ PYBIND11_MODULE(_dataplane, m) {
       .def("set_xfer_parity", &Engine::set_xfer_parity)
       .def("set_import", &Engine::set_import, py::arg("recv"), py::arg("stream") = 0)
       .def("restore", &Engine::restore, py::arg("desc"), py::arg("payload"), py::arg("now_ms"))
-      .def("ring_move", &Engine::ring_move)
       .def("basic_get", &Engine::basic_get, py::arg("q"), py::arg("chslot"), py::arg("noack"), py::arg("now_ms"))
       .def("wait_results", &Engine::wait_results)
       .def("egress_copy", &Engine::egress_copy)

