@@ -579,6 +579,10 @@ class GpuDataPlane(ControlState):
         steps may be outstanding (double-buffered step IO)."""
         now = int(time.time() * 1000) if now_ms is None else int(now_ms)
         t0 = time.perf_counter()
+        if len(segs):   # the device stages every segment's carry in front of its new bytes
+            staged = int(self.carry[segs["conn"]].sum()) + 48 * len(segs)
+            if staged > self.info["carry_budget"]:
+                raise RuntimeError(f"step carries {staged} B > carry_budget {self.info['carry_budget']} B")
         p = self.eng.submit(segs, int(payload_ptr), int(payload_len), now, self.step_no, now, self.worker)
         self.step_no += 1
         if self.world > 1:

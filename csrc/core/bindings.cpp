@@ -186,7 +186,7 @@ PYBIND11_MODULE(_core, m) {
              FrontendCfg c;
 #define S(k, f) if (d.contains(k)) c.f = d[k].cast<decltype(c.f)>()
              S("host", host); S("port", port); S("io_threads", io_threads); S("per_conn_read", per_conn_read);
-             S("idle_step_ms", idle_step_ms); S("worker", worker); S("max_slot", max_slot); S("reuseport", reuseport);
+             S("idle_step_ms", idle_step_ms); S("sweep_ms", sweep_ms); S("worker", worker); S("max_slot", max_slot); S("reuseport", reuseport);
              S("sndbuf", sndbuf); S("rcvbuf", rcvbuf); S("wblock_high", wblock_high); S("wblock_low", wblock_low);
 #undef S
              return new Frontend(c, (const CmqEngineApi*)api);

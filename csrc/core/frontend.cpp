@@ -665,10 +665,21 @@ void Frontend::gather_conn(FeIo& io, FeConn& c, u8* arena, u64 cap) {
     if (eof) drop(c, true);
     return;
   }
+  // work-buffer budget: the device stages this connection's carry (<= carry + bytes still
+  // in flight) in front of the new bytes
+  const u64 wneed = (u64)c.carry + c.inflight + 48;
+  if (ph_carry_.fetch_add(wneed) + wneed > api_->carry_budget) {
+    ph_carry_.fetch_sub(wneed);
+    std::lock_guard<std::mutex> g(c.mu);
+    c.inject.insert(0, inj);
+    c.in_ready = true;
+    return;
+  }
   // reserve a segment slot and arena bytes
   const u32 si = ph_nseg_.fetch_add(1);
   if (si >= api_->seg_max) {
     ph_nseg_.fetch_sub(1);
+    ph_carry_.fetch_sub(wneed);
     std::lock_guard<std::mutex> g(c.mu);
     c.inject.insert(0, inj);
     c.in_ready = true;
@@ -679,6 +690,7 @@ void Frontend::gather_conn(FeIo& io, FeConn& c, u8* arena, u64 cap) {
   while (true) {
     if (off + need > cap) {
       ph_nseg_.fetch_sub(1);
+      ph_carry_.fetch_sub(wneed);
       std::lock_guard<std::mutex> g(c.mu);
       c.inject.insert(0, inj);
       c.in_ready = true;
@@ -710,6 +722,7 @@ void Frontend::io_phase(std::vector<Scatter*>& scat, bool gather) {
   ph_cap_ = api_->ingress_cap;
   ph_used_ = 0;
   ph_nseg_ = 0;
+  ph_carry_ = 0;
   ph_left_ = (int)io_.size();
   ph_id_.fetch_add(1, std::memory_order_release);
   for (auto& io : io_) poke(io->evfd);
@@ -854,8 +867,15 @@ void Frontend::stepper() {
       if (pause_req_ > 0 || !running_) continue;
       if (!woke) {
         if (now_ns() - last_step < (i64)(idle * 1e6)) continue;
-        idle_tick_ = any_data_conn();
-        if (!idle_tick_) { last_step = now_ns(); continue; }
+        // open connections: the idle step period; none: a TTL sweep (K12 at the queue heads
+        // in k_dequeue) every sweep_ms while the device still holds messages
+        i64 live;
+        {
+          std::lock_guard<std::mutex> sg(stats_mu_);
+          live = stats_.live_bytes;
+        }
+        idle_tick_ = any_data_conn() || (live > 0 && now_ns() - last_step >= (i64)(cfg_.sweep_ms * 1e6));
+        if (!idle_tick_) continue;
       }
     } else {
       std::lock_guard<std::mutex> g(st_mu_);
@@ -973,6 +993,7 @@ EchoEngine::EchoEngine(u32 c_max, u32 seg_max, u64 ingress_cap, u32 carry_cap) {
   api_.carry_cap = carry_cap;
   api_.ingress_cap = ingress_cap;
   api_.ctrl_cap = 1 << 20;
+  api_.carry_budget = 64ull << 20;
   api_.eng = this;
   paused_.assign(c_max, 0);
   wblock_.assign(c_max, 0);

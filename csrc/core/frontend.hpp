@@ -68,6 +68,7 @@ struct FrontendCfg {
   int io_threads = 4;
   u64 per_conn_read = 256 << 10;   // max bytes gathered per connection per step
   double idle_step_ms = 2.0;       // step period with open data connections and no traffic
+  double sweep_ms = 200.0;         // no connections: TTL sweep period while messages are held
   u32 worker = 0;                  // snowflake worker id
   u32 max_slot = 0;                // connection slots 1..max_slot (default c_max - 2)
   bool reuseport = false;
@@ -170,6 +171,7 @@ class Frontend {
   u64 ph_cap_ = 0;
   std::atomic<u64> ph_used_{0};
   std::atomic<u32> ph_nseg_{0};
+  std::atomic<u64> ph_carry_{0};
 
   // stepper wake-up / pause
   std::mutex st_mu_;

@@ -118,7 +118,12 @@ class Engine {
     d_.ingress_cap = get("ingress_cap", 64ull << 20);
     d_.xfer_bytes = d_.world > 1 ? get("xfer_bytes", (d_.world - 1) * (d_.ingress_cap + 64))
                                  : (restore_max_ ? get("restore_bytes", 64ull << 20) : 0);
-    d_.work_cap = d_.ingress_cap + (u64)d_.seg_max * (d_.carry_cap + 64);
+    // work buffer = this step's new bytes + the carries of the connections in the step.
+    // carry_cap bounds one connection's (= the largest command assembled on the device,
+    // e.g. a multi-MB message); carry_budget bounds their sum per step (the front end
+    // gathers within it), so large carries do not multiply by seg_max
+    carry_budget_ = std::min<u64>((u64)d_.seg_max * (d_.carry_cap + 64), get("carry_budget", 512ull << 20));
+    d_.work_cap = d_.ingress_cap + carry_budget_;
     d_.work_cap = d_.work_cap > (3ull << 30) ? (3ull << 30) : d_.work_cap;  // u32 offsets
     if (d_.work_cap + d_.xfer_bytes + 8192 > (4ull << 30))
       throw std::runtime_error("work buffer + imported bytes must stay below 4 GiB (u32 offsets): lower ingress_cap");
@@ -521,6 +526,7 @@ class Engine {
     o["tb_max"] = d_.tb_max; o["tb_pad"] = d_.tb_pad; o["log_bytes"] = d_.log_bytes;
     o["ingress_cap"] = d_.ingress_cap; o["egress_cap"] = d_.egress_cap; o["ring_pool"] = d_.ring_pool;
     o["work_cap"] = d_.work_cap; o["total_bytes"] = total_bytes_; o["req_max"] = d_.req_max;
+    o["carry_budget"] = carry_budget_;
     o["exchange_lag"] = lag_ ? 1 : 0;
     o["world"] = d_.world; o["rank"] = d_.my_rank; o["import_max"] = d_.import_max; o["pub_cap"] = d_.pub_cap;
     o["copy_engine"] = copy_mode_ == 3 ? "hsa-sdma" : copy_mode_ == 2 ? "kernel" : (sdma_ ? "nocu" : "blit");
@@ -761,7 +767,7 @@ class Engine {
     a.abi = CMQ_STEP_ABI;
     a.c_max = d_.c_max; a.seg_max = d_.seg_max; a.carry_cap = d_.carry_cap;
     a.persist = d_.persist; a.persist_max = d_.persist_max;
-    a.ingress_cap = d_.ingress_cap; a.ctrl_cap = d_.ctrl_cap;
+    a.ingress_cap = d_.ingress_cap; a.ctrl_cap = d_.ctrl_cap; a.carry_budget = carry_budget_;
     a.eng = this;
     a.submit = [](void* e, const SegIn* sg, u32 n, const u8* pay, u64 len, i64 now, u32 worker) -> int {
       return ((Engine*)e)->guard([&] { return ((Engine*)e)->submit_raw(sg, n, (u64)pay, len, now, (u64)now, worker); });
@@ -1098,6 +1104,7 @@ class Engine {
   u64 egress_alloc_ = 0;
   u32 ntiles_max_ = 0;
   u32 restore_max_ = 0;
+  u64 carry_budget_ = 0;
   u64 get_cap_ = 0;
   u8* get_out_dev_ = nullptr;
   GetRes* get_res_dev_ = nullptr;

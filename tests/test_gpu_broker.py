@@ -380,3 +380,66 @@ def test_confirmed_publishes_into_a_small_queue_are_never_lost(broker):
     assert [int.from_bytes(d.body, "big") for d in got] == list(range(n))
     p.close()
     c.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("io", ["native", "pipeline"])
+def test_large_message_4mb_roundtrip(gpu, io):
+    """A 4 MB message (32 body frames at frame-max 128 KB) is assembled on the device in
+    a large per-connection carry, stored, routed and delivered intact (SURVEY §5.7;
+    FrameParser.scala:67 has no size limit)."""
+    from chanamq_amd.engine.dataplane import GpuDataPlane
+    from chanamq_amd.server.gpu_broker import GpuBroker
+    cfg = dict(GPU_CFG, carry_cap=8 << 20, egress_cap=64 << 20, log_bytes=256 << 20, log_block=16 << 20)
+    b = GpuBroker(GpuDataPlane(default_queue_capacity=1 << 12, **cfg), idle_step_ms=1.0, io=io,
+                  ingress_bytes=8 << 20).start()
+    try:
+        p = conn(b)
+        ch = p.channel()
+        ch.queue_declare("big")
+        ch.confirm_select()
+        body = bytes((i * 7 + 3) & 0xFF for i in range(4 << 20))
+        ch.basic_publish("", "big", body)
+        ch.basic_publish("", "big", b"small-after")
+        assert ch.wait_for_confirms(timeout=30)
+        c = conn(b)
+        cc = c.channel()
+        cc.basic_consume("big", "bigc", no_ack=True)
+        got = cc.consume_n(2, timeout=30)
+        assert len(got[0].body) == len(body) and got[0].body == body
+        assert got[1].body == b"small-after"
+        p.close()
+        c.close()
+    finally:
+        b.stop()
+
+
+@pytest.mark.gpu
+def test_ttl_expired_bodies_freed_without_consumers_or_connections(gpu):
+    """K12: messages with a per-message TTL in a queue nobody consumes are dropped at the
+    queue head and their HBM freed, even after every connection is gone (the front end
+    keeps sweeping while the device holds messages; MessageEntity.scala:168-198)."""
+    import time
+    from chanamq_amd.engine.dataplane import GpuDataPlane
+    from chanamq_amd.server.gpu_broker import GpuBroker
+    b = GpuBroker(GpuDataPlane(default_queue_capacity=1 << 12, **GPU_CFG), idle_step_ms=1.0, io="pipeline",
+                  ingress_bytes=8 << 20).start()
+    try:
+        p = conn(b)
+        ch = p.channel()
+        ch.queue_declare("ttl.nobody")
+        for i in range(200):
+            ch.basic_publish("", "ttl.nobody", bytes(2000), {"expiration": "300"})
+        p.process(0.3)
+        b._sync_fe_stats()
+        assert b._fe_stats["live_bytes"] > 200 * 2000
+        p.close()
+        end = time.time() + 10
+        while time.time() < end:
+            time.sleep(0.2)
+            b._sync_fe_stats()
+            if b._fe_stats["live_bytes"] == 0:
+                break
+        assert b._fe_stats["live_bytes"] == 0
+    finally:
+        b.stop()
