@@ -203,29 +203,48 @@ def main():
     base = pool.ctypes.data
     step_i = 0
 
-    def run(n):
+    sub_t = {}      # step index -> host time its ingress was handed to the GPU (submit)
+    lat_w = []      # (publish->deliver seconds, deliveries) of the timed steps
+
+    def run(n, measure=False):
         # software pipeline, 3 steps in flight: H2D(t+1) || kernels(t) || D2H(t-1);
         # the host consumes step t-1's results/egress while the GPU runs step t
         nonlocal step_i
         dl = pb = 0
         hist = np.zeros(32, np.int64)
         eg = 0
-        pending = []
+        pending = []    # (ticket, step index)
         done = []
+        lat_of = {}     # step index -> its lat_hist (deliveries by publish-step lag)
 
-        def account(r):
+        def account(r, s):
             nonlocal dl, pb, eg
             c = r.counters
             dl += c["n_deliv"]
             pb += c["n_pubs"]
             eg += c["egress_bytes"]
-            hist[:] += np.array(c["lat_hist"], np.int64)
+            lh = np.array(c["lat_hist"], np.int64)
+            hist[:] += lh
+            lat_of[s] = lh
             if storm:
                 flow["requeued"] += c["n_requeue"]
                 flow["paused"] = c["live_bytes"] > flow_high
 
+        def ready(s):
+            # measured latency: a delivery rendered in step s whose message was published
+            # k steps earlier waited from that step's submit until s's egress was in host
+            # memory (bin 31 = 31 or more steps: counted as 31)
+            t = time.perf_counter()
+            lh = lat_of.pop(s, None)
+            if measure and lh is not None:
+                for k in np.nonzero(lh)[0]:
+                    t0 = sub_t.get(s - int(k))
+                    if t0 is not None:
+                        lat_w.append((t - t0, int(lh[k])))
+
         for _ in range(n):
             b = step_i % args.blocks
+            sub_t[step_i] = time.perf_counter()
             if storm:   # ack-all each step, nack-all-requeue every 4th: a redelivery storm
                 cs = extra["nack" if step_i % 4 == 3 else "ack"][b]
                 if flow["paused"]:
@@ -233,20 +252,24 @@ def main():
                     sg = cs
                 else:
                     sg = np.concatenate([segs[b], cs])
-                pending.append(dp.submit_raw(sg, base + offs[b], blens[b]))
+                pending.append((dp.submit_raw(sg, base + offs[b], blens[b]), step_i))
             else:
-                pending.append(dp.submit_raw(segs[b], base + offs[b], blens[b]))
+                pending.append((dp.submit_raw(segs[b], base + offs[b], blens[b]), step_i))
             step_i += 1
             if len(pending) > 1:
-                t = pending.pop(0)
-                account(dp.finish(t, collect=False, wait_egress=False))
+                t, s = pending.pop(0)
+                account(dp.finish(t, collect=False, wait_egress=False), s)
                 if done:
-                    dp.egress_wait(done.pop(0))
-                done.append(t)
-        for t in pending:
-            account(dp.finish(t, collect=False, wait_egress=True))
-        for t in done:
+                    t2, s2 = done.pop(0)
+                    dp.egress_wait(t2)
+                    ready(s2)
+                done.append((t, s))
+        for t, s in done:
             dp.egress_wait(t)
+            ready(s)
+        for t, s in pending:
+            account(dp.finish(t, collect=False, wait_egress=True), s)
+            ready(s)
         return dl, pb, hist, eg
 
     run(args.warmup)
@@ -258,7 +281,7 @@ def main():
         dp.exchanger.bytes_sent = 0
     dp.eng.host_times(True)
     t0 = time.perf_counter()
-    dl, pb, hist, eg = run(args.steps)
+    dl, pb, hist, eg = run(args.steps, measure=True)
     dp.eng.sync()
     torch.cuda.synchronize()
     if dist:
@@ -281,12 +304,20 @@ def main():
         dl, pb, eg = (float(x) for x in ss.tolist())
         hist = hh.cpu().numpy()
     ms_step = 1000.0 * t / args.steps
-    # p50: deliveries by (deliver step - publish step).  With the 3-deep pipeline a message
-    # submitted in step s is in host memory ~3 step periods later (H2D, kernels, D2H), plus
-    # k more periods if it waited k steps in its queue
-    cum = np.cumsum(hist)
-    p50_bin = int(np.searchsorted(cum, cum[-1] / 2.0)) if cum[-1] else 0
-    p50_ms = (p50_bin + 3) * ms_step
+    # p50 publish->deliver, measured on the host clock per delivery: from the submit of the
+    # step that carried the publish to the moment the delivering step's egress bytes were in
+    # host memory (the step pipeline, queueing and the D2H included; no TCP)
+    lat = np.array(lat_w, np.float64).reshape(-1, 2)
+    p50_ms = p99_ms = None
+    if len(lat):
+        order = np.argsort(lat[:, 0])
+        cw = np.cumsum(lat[order, 1])
+        p50_ms = 1000.0 * float(lat[order[np.searchsorted(cw, 0.5 * cw[-1])], 0])
+        p99_ms = 1000.0 * float(lat[order[min(len(order) - 1, np.searchsorted(cw, 0.99 * cw[-1]))], 0])
+    if dist:   # the slowest rank's median
+        lt = torch.tensor([p50_ms or 0.0, p99_ms or 0.0], dtype=torch.float64, device=rdev)
+        dist.all_reduce(lt, op=dist.ReduceOp.MAX)
+        p50_ms, p99_ms = (float(x) for x in lt.tolist())
     if rank == 0:
         out = {
             "metric": METRIC,
@@ -320,9 +351,12 @@ def main():
                 "bytes_per_msg_on_wire": msg_bytes,
             },
             "p50_latency_ms": p50_ms,
+            "p99_latency_ms": p99_ms,
             "published_msgs_per_s": pb / t,
             "egress_GBps": eg / t / 1e9,
-            "latency_note": "in-broker publish->deliver (ingress submit to egress bytes ready), no TCP",
+            "latency_note": "measured per delivery on the host clock: submit of the publishing step -> egress "
+                            "bytes of the delivering step in host memory (no TCP; bench/gpu_server_e2e.py "
+                            "measures client-to-client over TCP)",
             "diag": errs,
             "host_us_per_step": {k: round(v * 1e6 / args.steps, 1) for k, v in dp.eng.host_times(False).items()},
             "storm": ({"requeued_msgs": flow["requeued"], "flow_paused_steps": flow["paused_steps"]}

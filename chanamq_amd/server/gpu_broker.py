@@ -783,14 +783,17 @@ class GpuBroker:
         """Stop reading a connection while the device still holds a large backlog of its
         bytes (carry); resume once it drains."""
         carry = self.plane.carry
+        # a connection's carry may legitimately grow to carry_cap (a large command being
+        # assembled); stop reading only when the next read could overflow it
+        lim = max(self.plane.info["carry_cap"] - self.per_conn_read, self.per_conn_read)
         for cid in segs["conn"]:
             cid = int(cid)
-            big = carry[cid] > self.per_conn_read
+            big = carry[cid] > lim
             if big != (cid in self._rpaused):
                 self.gw.set_read_paused(cid, big)
                 (self._rpaused.add if big else self._rpaused.discard)(cid)
         for cid in list(self._rpaused):
-            if carry[cid] <= self.per_conn_read:
+            if carry[cid] <= lim:
                 self.gw.set_read_paused(cid, False)
                 self._rpaused.discard(cid)
 
