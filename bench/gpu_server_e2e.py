@@ -48,7 +48,7 @@ def plane_for(spec):
                         persist_max=1 << 16, persist_bytes=512 << 20, carry_cap=1 << 18)
 
 
-def run_one(core, name, spec, io, io_threads, seconds, rate=0.0, lg_threads=8, store_dir=None):
+def run_one(core, name, spec, io, io_threads, seconds, rate=0.0, lg_threads=12, store_dir=None, cons_threads=8):
     from chanamq_amd.server.gpu_broker import GpuBroker
     persist = bool(spec.get("persistent"))
     plane = plane_for(spec)
@@ -61,7 +61,8 @@ def run_one(core, name, spec, io, io_threads, seconds, rate=0.0, lg_threads=8, s
     t0 = time.time()
     try:
         r = core.run_load(dict(port=b.port, seconds=seconds, warmup=1.0, queue=f"e2e.{name}",
-                               exchange=f"e2e.x.{name}", threads=lg_threads, rate=rate, **spec))
+                               exchange=f"e2e.x.{name}", threads=lg_threads, consumer_threads=cons_threads,
+                               rate=rate, **spec))
     finally:
         b.stop()
         if store is not None:
@@ -88,7 +89,8 @@ def main():
     ap.add_argument("--only", default="")
     ap.add_argument("--io", default="pipeline", help="comma list of front ends: pipeline,native")
     ap.add_argument("--io-threads", default="4", help="comma list (pipeline front end)")
-    ap.add_argument("--loadgen-threads", type=int, default=8)
+    ap.add_argument("--loadgen-threads", type=int, default=12)
+    ap.add_argument("--consumer-threads", type=int, default=8, help="of the load generator's threads")
     ap.add_argument("--paced", type=float, default=0.5,
                     help="re-run each spec with producers paced at this fraction of the measured rate (0 = off)")
     args = ap.parse_args()
@@ -100,7 +102,8 @@ def main():
             continue
         for io in args.io.split(","):
             for nt in ([int(x) for x in args.io_threads.split(",")] if io == "pipeline" else [1]):
-                r = run_one(core, name, spec, io, nt, args.seconds, lg_threads=args.loadgen_threads)
+                r = run_one(core, name, spec, io, nt, args.seconds, lg_threads=args.loadgen_threads,
+                               cons_threads=args.consumer_threads)
                 results.append(r)
                 print(json.dumps({k: r[k] for k in ("name", "io", "io_threads", "recv_msgs_per_s", "sent_msgs_per_s",
                                                     "confirmed_per_s", "p50_us", "p99_us", "error", "front_end",
@@ -110,7 +113,8 @@ def main():
                     rate = args.paced * r["recv_msgs_per_s"] / max(1, spec.get("producers", 1))
                     if spec.get("exchange_type") == "fanout":   # deliveries = publishes x queues
                         rate /= max(1, spec.get("queues", 1))
-                    rp = run_one(core, name, spec, io, nt, args.seconds, rate=rate, lg_threads=args.loadgen_threads)
+                    rp = run_one(core, name, spec, io, nt, args.seconds, rate=rate, lg_threads=args.loadgen_threads,
+                               cons_threads=args.consumer_threads)
                     rp["paced_fraction"] = args.paced
                     results.append(rp)
                     print(json.dumps({k: rp[k] for k in ("name", "io", "io_threads", "rate_per_producer",

@@ -134,6 +134,11 @@ class GpuBroker:
             mem_high_watermark = int(0.4 * plane.info["log_bytes"]) if hasattr(plane, "info") else 0
         self.mem_high = mem_high_watermark
         self.mem_low = mem_low_watermark if mem_low_watermark is not None else mem_high_watermark // 2
+        # the HBM message table is the other finite store: above 75% of it publishers are
+        # paused too (down to 40%), else it fills before the byte watermark and drops
+        msg_max = plane.info["msg_max"] if hasattr(plane, "info") else 0
+        self.msg_high = int(0.75 * msg_max) if self.mem_high else 0
+        self.msg_low = int(0.4 * msg_max) if self.mem_high else 0
         self.blocked = False
         # durable queues x persistent messages -> store (write-behind, confirm gating)
         self.persistence = None
@@ -1149,11 +1154,17 @@ class GpuBroker:
     def _watermarks(self):
         if not self.mem_high:
             return
-        used = self._fe_stats["live_bytes"] if self.fe is not None and self._fe_stats else self.plane.memory_in_use()
-        if not self.blocked and used >= self.mem_high:
+        if self.fe is not None and self._fe_stats:
+            used, msgs = self._fe_stats["live_bytes"], self._fe_stats["live_msgs"]
+        else:
+            lc = getattr(self.plane, "last_counters", None) or {}
+            used, msgs = self.plane.memory_in_use(), lc.get("n_live_msgs", 0)
+        high = used >= self.mem_high or (self.msg_high and msgs >= self.msg_high)
+        low = used <= self.mem_low and (not self.msg_high or msgs <= self.msg_low)
+        if not self.blocked and high:
             self.blocked = True
             self._set_flow(False)
-        elif self.blocked and used <= self.mem_low:
+        elif self.blocked and low:
             self.blocked = False
             self._set_flow(True)
 

@@ -236,7 +236,8 @@ PYBIND11_MODULE(_core, m) {
              o["steps"] = s.steps; o["published"] = s.published; o["delivered"] = s.delivered;
              o["rx_bytes"] = s.rx_bytes; o["tx_bytes"] = s.tx_bytes; o["egress_bytes"] = s.egress_bytes;
              o["held_steps"] = s.held_steps; o["idle_steps"] = s.idle_steps; o["gather_segs"] = s.gather_segs;
-             o["live_bytes"] = s.live_bytes; o["io_phase_s"] = s.io_phase_s; o["wait_s"] = s.wait_s;
+             o["live_bytes"] = s.live_bytes; o["live_msgs"] = s.live_msgs; o["io_phase_s"] = s.io_phase_s;
+             o["wait_s"] = s.wait_s;
              o["submit_s"] = s.submit_s;
              o["lat_hist"] = std::vector<u64>(s.lat_hist, s.lat_hist + 32);
              return o;
@@ -284,6 +285,7 @@ PYBIND11_MODULE(_core, m) {
     S("routing_key", routing_key); S("queue", queue); S("queues", queues); S("auto_ack", auto_ack);
     S("prefetch", prefetch); S("persistent", persistent); S("durable", durable); S("confirm", confirm);
     S("rate", rate); S("threads", threads); S("warmup", warmup); S("confirm_window", confirm_window);
+    S("consumer_threads", consumer_threads);
 #undef S
     LoadResult r;
     {

@@ -821,6 +821,7 @@ void Frontend::finish_oldest(std::deque<Inflight>& inflight) {
     stats_.delivered += c.n_deliv;
     stats_.egress_bytes += c.egress_bytes;
     stats_.live_bytes = c.live_bytes;
+    stats_.live_msgs = c.n_live_msgs;
     stats_.wait_s += w;
     for (int k = 0; k < 32; ++k) stats_.lat_hist[k] += c.lat_hist[k];
     if (needs_commit) stats_.held_steps++;

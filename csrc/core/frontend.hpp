@@ -80,6 +80,7 @@ struct FeStats {
   u64 steps = 0, published = 0, delivered = 0, rx_bytes = 0, tx_bytes = 0, egress_bytes = 0;
   u64 held_steps = 0, idle_steps = 0, gather_segs = 0;
   i64 live_bytes = 0;
+  u64 live_msgs = 0;
   u64 lat_hist[32] = {};
   double io_phase_s = 0, wait_s = 0, submit_s = 0;
 };

@@ -165,9 +165,9 @@ struct Peer {
   size_t out_pos = 0;
   std::atomic<u64> sent{0}, confirmed{0}, nacked{0};
   bool flow = true;
-  // any: receive buffer parsed in place
-  std::string in;
-  size_t pos = 0;
+  // any: receive buffer (recv lands in place, frames parsed in place)
+  std::vector<char> in = std::vector<char>(4 << 20);
+  size_t ilen = 0, pos = 0;
   // consumer
   bool want_body = false;
   u64 body_left = 0, last_tag = 0, unacked = 0;
@@ -236,7 +236,8 @@ LoadResult run_load(const LoadSpec& s) {
     p->cl.method(1, cm);
     p->cl.flush();
     p->cl.expect(60, 21);
-    p->in = p->cl.in.substr(p->cl.pos);   // deliveries may already follow ConsumeOk
+    p->ilen = p->cl.in.size() - p->cl.pos;   // deliveries may already follow ConsumeOk
+    memcpy(p->in.data(), p->cl.in.data() + p->cl.pos, p->ilen);
     peers.push_back(std::move(p));
   }
   // producers: batch of K publishes, keys cycling over the queues
@@ -269,7 +270,8 @@ LoadResult run_load(const LoadSpec& s) {
         p->ts_off.push_back(before + hdr + 7);
       }
     }
-    p->in = p->cl.in.substr(p->cl.pos);
+    p->ilen = p->cl.in.size() - p->cl.pos;
+    memcpy(p->in.data(), p->cl.in.data() + p->cl.pos, p->ilen);
     peers.push_back(std::move(p));
   }
   for (auto& p : peers) {
@@ -285,7 +287,7 @@ LoadResult run_load(const LoadSpec& s) {
   const int ncons = s.consumers, nprod = s.producers;
   int tc = 0, tp = 0;
   if (nthreads >= 2 && ncons && nprod) {
-    tc = std::max(1, std::min(ncons, nthreads / 2));
+    tc = std::max(1, std::min(ncons, s.consumer_threads > 0 ? s.consumer_threads : nthreads / 2));
     tp = std::max(1, std::min(nprod, nthreads - tc));
     nthreads = tc + tp;
   }
@@ -316,7 +318,6 @@ LoadResult run_load(const LoadSpec& s) {
       }
       Hist& h = hists[ti];
       epoll_event evs[256];
-      std::vector<char> rbuf(1 << 20);
       bool any_producer = false;
       for (Peer* p : mine) any_producer |= p->producer;
       auto pump = [&](Peer* p) {   // producer: send until the socket is full or paced out
@@ -350,7 +351,7 @@ LoadResult run_load(const LoadSpec& s) {
       };
       auto parse = [&](Peer* p) {
         const u8* b = (const u8*)p->in.data();
-        size_t n = p->in.size(), pos = p->pos;
+        size_t n = p->ilen, pos = p->pos;
         while (n - pos >= 8) {
           u32 size = rd32(b + pos + 3);
           if (n - pos < (size_t)size + 8) break;
@@ -406,13 +407,20 @@ LoadResult run_load(const LoadSpec& s) {
           pos += (size_t)size + 8;
         }
         p->pos = pos;
-        if (p->pos > (1u << 20) || p->pos == p->in.size()) { p->in.erase(0, p->pos); p->pos = 0; }
+        if (p->pos == p->ilen) {
+          p->pos = p->ilen = 0;
+        } else if (p->pos > p->in.size() / 2 || p->in.size() - p->ilen < (64u << 10)) {   // compact the tail
+          memmove(p->in.data(), p->in.data() + p->pos, p->ilen - p->pos);
+          p->ilen -= p->pos;
+          p->pos = 0;
+          if (p->in.size() - p->ilen < (64u << 10)) p->in.resize(p->in.size() * 2);   // a frame larger than the buffer
+        }
       };
       auto drain = [&](Peer* p) {
         for (;;) {
-          ssize_t k = ::recv(p->cl.fd, rbuf.data(), rbuf.size(), 0);
+          ssize_t k = ::recv(p->cl.fd, p->in.data() + p->ilen, p->in.size() - p->ilen, 0);
           if (k > 0) {
-            p->in.append(rbuf.data(), (size_t)k);
+            p->ilen += (size_t)k;
             parse(p);
             if (!p->producer && !s.auto_ack && p->unacked >= ack_every) {
               std::string ak;
@@ -439,7 +447,7 @@ LoadResult run_load(const LoadSpec& s) {
           p->unacked = 0;
         }
       };
-      for (Peer* p : mine) if (!p->in.empty()) parse(p);
+      for (Peer* p : mine) if (p->ilen) parse(p);
       while (!stop) {
         for (Peer* p : mine)
           if (p->producer && p->writable) pump(p);

@@ -19,7 +19,8 @@ struct LoadSpec {
   double rate = 0;   // msgs/s per producer, 0 = unthrottled
   int threads = 0;   // epoll worker threads (0 = min(8, connections))
   double warmup = 0; // seconds excluded from the counts
-  int confirm_window = 0;   // confirm mode: max unconfirmed publishes per producer (PerfTest -c), 0 = unlimited
+  int confirm_window = 0;
+  int consumer_threads = 0; // of `threads`, serving consumers (0 = half)   // confirm mode: max unconfirmed publishes per producer (PerfTest -c), 0 = unlimited
 };
 
 struct LoadResult {

@@ -24,7 +24,7 @@ pytestmark = pytest.mark.gpu
 
 VH = "AMQ.DEFAULT"
 BENCH = dict(c_max=1024, chpc=4, q_max=2048, x_max=64, cons_max=2048, seg_max=1024, cmd_max=1 << 17,
-             deliv_max=1 << 17, msg_max=1 << 20, ucap=4096, deliver_cap=8192, ingress_cap=40 << 20,
+             deliv_max=1 << 18, msg_max=1 << 20, ucap=4096, deliver_cap=8192, ingress_cap=40 << 20,
              egress_cap=192 << 20, log_bytes=2 << 30, log_block=4 << 20, ring_pool=1 << 22, tb_max=64,
              fan_max=1 << 20, carry_cap=256 << 10, dhash=4096, req_max=1 << 16)
 
