@@ -48,6 +48,24 @@ def plane_for(spec):
                         persist_max=1 << 16, persist_bytes=512 << 20, carry_cap=1 << 18)
 
 
+def thread_cpu():
+    """CPU seconds (user + system) of this process's threads, grouped by name prefix
+    (cmq-io / cmq-stepper = front end, lg-c / lg-p = load generator consumers / producers)."""
+    out = {}
+    tck = os.sysconf("SC_CLK_TCK")
+    for tid in os.listdir("/proc/self/task"):
+        try:
+            with open(f"/proc/self/task/{tid}/stat") as f:
+                st = f.read()
+        except OSError:
+            continue
+        name = st[st.index("(") + 1:st.rindex(")")]
+        f = st[st.rindex(")") + 2:].split()
+        key = name.rstrip("0123456789")
+        out[key] = out.get(key, 0.0) + (int(f[11]) + int(f[12])) / tck
+    return out
+
+
 def run_one(core, name, spec, io, io_threads, seconds, rate=0.0, lg_threads=12, store_dir=None, cons_threads=8):
     from chanamq_amd.server.gpu_broker import GpuBroker
     persist = bool(spec.get("persistent"))
@@ -59,15 +77,18 @@ def run_one(core, name, spec, io, io_threads, seconds, rate=0.0, lg_threads=12, 
     b = GpuBroker(plane, idle_step_ms=0.5, store=store, io=io, io_threads=io_threads,
                   per_conn_read=128 << 10).start()
     t0 = time.time()
+    cpu0 = thread_cpu()
     try:
         r = core.run_load(dict(port=b.port, seconds=seconds, warmup=1.0, queue=f"e2e.{name}",
                                exchange=f"e2e.x.{name}", threads=lg_threads, consumer_threads=cons_threads,
                                rate=rate, **spec))
     finally:
+        cpu1 = thread_cpu()
         b.stop()
         if store is not None:
             store.close()
     lc = getattr(plane, "last_counters", {}) or {}
+    r["thread_cpu_s"] = {k: round(cpu1[k] - cpu0.get(k, 0.0), 2) for k in cpu1 if cpu1[k] - cpu0.get(k, 0.0) > 0.05}
     st = dict(b.stats)
     fes = getattr(b, "_fe_stats", None) or {}
     r.update(name=name, io=io, io_threads=io_threads if io == "pipeline" else 1, loadgen_threads=lg_threads,
@@ -91,6 +112,7 @@ def main():
     ap.add_argument("--io-threads", default="4", help="comma list (pipeline front end)")
     ap.add_argument("--loadgen-threads", type=int, default=12)
     ap.add_argument("--consumer-threads", type=int, default=8, help="of the load generator's threads")
+    ap.add_argument("--rates", default="", help="comma list of aggregate publish rates (msgs/s) to run paced")
     ap.add_argument("--paced", type=float, default=0.5,
                     help="re-run each spec with producers paced at this fraction of the measured rate (0 = off)")
     args = ap.parse_args()
@@ -107,8 +129,16 @@ def main():
                 results.append(r)
                 print(json.dumps({k: r[k] for k in ("name", "io", "io_threads", "recv_msgs_per_s", "sent_msgs_per_s",
                                                     "confirmed_per_s", "p50_us", "p99_us", "error", "front_end",
-                                                    "store")}),
+                                                    "store", "thread_cpu_s")}),
                       flush=True)
+                for agg in [float(x) for x in args.rates.split(",") if x]:
+                    rr = run_one(core, name, spec, io, nt, args.seconds, rate=agg / max(1, spec.get("producers", 1)),
+                                 lg_threads=args.loadgen_threads, cons_threads=args.consumer_threads)
+                    rr["aggregate_rate"] = agg
+                    results.append(rr)
+                    print(json.dumps({k: rr[k] for k in ("name", "io_threads", "aggregate_rate", "sent_msgs_per_s",
+                                                         "recv_msgs_per_s", "p50_us", "p99_us", "thread_cpu_s",
+                                                         "error")}), flush=True)
                 if args.paced > 0 and r["recv_msgs_per_s"] > 0 and not r["error"]:
                     rate = args.paced * r["recv_msgs_per_s"] / max(1, spec.get("producers", 1))
                     if spec.get("exchange_type") == "fanout":   # deliveries = publishes x queues

@@ -11,6 +11,7 @@
 // whenever their receive buffer runs dry.  Channel.Flow(active=false) from the broker pauses
 // the connection's publishing (and is answered with FlowOk).
 #include <arpa/inet.h>
+#include <pthread.h>
 #include <fcntl.h>
 #include <netinet/in.h>
 #include <netinet/tcp.h>
@@ -304,6 +305,11 @@ LoadResult run_load(const LoadSpec& s) {
   const u64 ack_every = (u64)std::max(1, s.prefetch / 2);
 
   auto worker = [&](int ti) {
+    {
+      char nm[16];
+      snprintf(nm, sizeof nm, "lg-%s%d", (tc && ti >= tc) ? "p" : (tc ? "c" : "x"), ti);
+      pthread_setname_np(pthread_self(), nm);
+    }
     try {
       int ep = epoll_create1(0);
       std::vector<Peer*> mine;
