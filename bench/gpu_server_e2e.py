@@ -66,6 +66,9 @@ def thread_cpu():
     return out
 
 
+FE_CFG = {}
+
+
 def run_one(core, name, spec, io, io_threads, seconds, rate=0.0, lg_threads=12, store_dir=None, cons_threads=8):
     from chanamq_amd.server.gpu_broker import GpuBroker
     persist = bool(spec.get("persistent"))
@@ -75,7 +78,7 @@ def run_one(core, name, spec, io, io_threads, seconds, rate=0.0, lg_threads=12, 
         store = core.Store()
         store.open(store_dir or tempfile.mkdtemp(prefix="cmq-gpu-store-"), True)
     b = GpuBroker(plane, idle_step_ms=0.5, store=store, io=io, io_threads=io_threads,
-                  per_conn_read=128 << 10).start()
+                  per_conn_read=128 << 10, fe_cfg=FE_CFG).start()
     t0 = time.time()
     cpu0 = thread_cpu()
     try:
@@ -112,10 +115,13 @@ def main():
     ap.add_argument("--io-threads", default="4", help="comma list (pipeline front end)")
     ap.add_argument("--loadgen-threads", type=int, default=12)
     ap.add_argument("--consumer-threads", type=int, default=8, help="of the load generator's threads")
+    ap.add_argument("--wblock-high", type=int, default=0, help="front end egress back-pressure high watermark (B)")
     ap.add_argument("--rates", default="", help="comma list of aggregate publish rates (msgs/s) to run paced")
     ap.add_argument("--paced", type=float, default=0.5,
                     help="re-run each spec with producers paced at this fraction of the measured rate (0 = off)")
     args = ap.parse_args()
+    if args.wblock_high:
+        FE_CFG.update(wblock_high=args.wblock_high, wblock_low=args.wblock_high // 4)
     import torch  # noqa: F401  (HIP runtime up before the first plane)
     core = load()
     results = []
@@ -129,7 +135,8 @@ def main():
                 results.append(r)
                 print(json.dumps({k: r[k] for k in ("name", "io", "io_threads", "recv_msgs_per_s", "sent_msgs_per_s",
                                                     "confirmed_per_s", "p50_us", "p99_us", "error", "front_end",
-                                                    "store", "thread_cpu_s")}),
+                                                    "store", "thread_cpu_s", "cpu_consumers_s",
+                                                    "cpu_producers_s")}),
                       flush=True)
                 for agg in [float(x) for x in args.rates.split(",") if x]:
                     rr = run_one(core, name, spec, io, nt, args.seconds, rate=agg / max(1, spec.get("producers", 1)),
@@ -138,7 +145,7 @@ def main():
                     results.append(rr)
                     print(json.dumps({k: rr[k] for k in ("name", "io_threads", "aggregate_rate", "sent_msgs_per_s",
                                                          "recv_msgs_per_s", "p50_us", "p99_us", "thread_cpu_s",
-                                                         "error")}), flush=True)
+                                                         "cpu_consumers_s", "cpu_producers_s", "error")}), flush=True)
                 if args.paced > 0 and r["recv_msgs_per_s"] > 0 and not r["error"]:
                     rate = args.paced * r["recv_msgs_per_s"] / max(1, spec.get("producers", 1))
                     if spec.get("exchange_type") == "fanout":   # deliveries = publishes x queues

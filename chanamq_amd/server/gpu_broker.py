@@ -109,7 +109,7 @@ class GpuBroker:
     def __init__(self, plane, host="127.0.0.1", port=0, heartbeat=0, frame_max=131072, channel_max=2047,
                  idle_step_ms=2.0, product="chanamq-amd", version="0.1.0", io="native",
                  ingress_bytes=64 << 20, per_conn_read=256 << 10, mem_high_watermark=None, mem_low_watermark=None,
-                 store=None, node=None, reuseport=False, io_threads=4):
+                 store=None, node=None, reuseport=False, io_threads=4, fe_cfg=None):
         """``io``: "pipeline" = native pipelined front end (csrc/core/frontend.cpp: IO
         threads + a stepper thread keeping two steps in flight, no Python per step),
         "native" = C++ batched gateway polled by a Python step loop (csrc/core/
@@ -122,6 +122,7 @@ class GpuBroker:
             raise ValueError("io='pipeline' needs a single-rank GPU data plane")
         self.io = io
         self.io_threads = io_threads
+        self.fe_cfg = dict(fe_cfg or {})    # extra native front-end settings (frontend.hpp FrontendCfg)
         self.gw = None
         self.fe = None
         self._fe_stats = None
@@ -180,7 +181,7 @@ class GpuBroker:
             self.fe = load().Frontend(self.plane.eng.c_api(), dict(
                 host=self.host, port=self.port, io_threads=self.io_threads, per_conn_read=self.per_conn_read,
                 idle_step_ms=self.idle_step_s * 1000.0, worker=self.plane.worker, max_slot=self.plane.c_max - 2,
-                reuseport=self.reuseport))
+                reuseport=self.reuseport, **self.fe_cfg))
             self.port = self.fe.port
             if self.persistence is not None:   # native write-behind: records never touch Python
                 self._pw = load().PersistWorker(self.persistence.store)

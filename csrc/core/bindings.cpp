@@ -296,6 +296,7 @@ PYBIND11_MODULE(_core, m) {
     o["sent"] = r.sent; o["received"] = r.received; o["elapsed"] = r.elapsed; o["p50_us"] = r.p50_us;
     o["p95_us"] = r.p95_us; o["p99_us"] = r.p99_us; o["error"] = r.error;
     o["confirmed"] = r.confirmed; o["nacked"] = r.nacked; o["threads"] = r.threads;
+    o["cpu_consumers_s"] = r.cpu_consumers_s; o["cpu_producers_s"] = r.cpu_producers_s;
     return o;
   });
   m.def("decode_method", &decode);

@@ -17,6 +17,7 @@
 #include <netinet/tcp.h>
 #include <sys/epoll.h>
 #include <sys/socket.h>
+#include <time.h>
 #include <unistd.h>
 
 #include <algorithm>
@@ -466,6 +467,10 @@ LoadResult run_load(const LoadSpec& s) {
         if (any_producer && rate > 0 && n == 0) std::this_thread::sleep_for(std::chrono::microseconds(50));
       }
       ::close(ep);
+      timespec ts;
+      clock_gettime(CLOCK_THREAD_CPUTIME_ID, &ts);
+      std::lock_guard<std::mutex> g(err_mu);
+      (tc && ti >= tc ? r.cpu_producers_s : r.cpu_consumers_s) += ts.tv_sec + ts.tv_nsec * 1e-9;
     } catch (std::exception& e) {
       std::lock_guard<std::mutex> g(err_mu);
       if (err.empty()) err = e.what();

@@ -19,13 +19,14 @@ struct LoadSpec {
   double rate = 0;   // msgs/s per producer, 0 = unthrottled
   int threads = 0;   // epoll worker threads (0 = min(8, connections))
   double warmup = 0; // seconds excluded from the counts
-  int confirm_window = 0;
-  int consumer_threads = 0; // of `threads`, serving consumers (0 = half)   // confirm mode: max unconfirmed publishes per producer (PerfTest -c), 0 = unlimited
+  int confirm_window = 0;    // confirm mode: max unconfirmed publishes per producer (PerfTest -c), 0 = unlimited
+  int consumer_threads = 0;  // of `threads`, serving consumers (0 = half)
 };
 
 struct LoadResult {
   unsigned long long sent = 0, received = 0, confirmed = 0, nacked = 0;
   int threads = 0;
+  double cpu_consumers_s = 0, cpu_producers_s = 0;   // thread CPU time of the load generator
   double elapsed = 0, p50_us = 0, p95_us = 0, p99_us = 0;
   std::string error;
 };
