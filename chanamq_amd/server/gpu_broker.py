@@ -1164,6 +1164,7 @@ class GpuBroker:
         low = used <= self.mem_low and (not self.msg_high or msgs <= self.msg_low)
         if not self.blocked and high:
             self.blocked = True
+            self.stats["flow_off"] = self.stats.get("flow_off", 0) + 1
             self._set_flow(False)
         elif self.blocked and low:
             self.blocked = False

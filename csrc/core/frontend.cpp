@@ -821,6 +821,12 @@ void Frontend::finish_oldest(std::deque<Inflight>& inflight) {
     stats_.delivered += c.n_deliv;
     stats_.egress_bytes += c.egress_bytes;
     stats_.live_bytes = c.live_bytes;
+    stats_.dropped_nomem += c.n_dropped_nomem;
+    stats_.ring_full += c.n_ring_full;
+    stats_.unroutable += c.n_unroutable;
+    stats_.routed += c.n_routed_msgs;
+    stats_.expired += c.n_expired;
+    stats_.ctrl += c.n_ctrl;
     stats_.live_msgs = c.n_live_msgs;
     stats_.wait_s += w;
     for (int k = 0; k < 32; ++k) stats_.lat_hist[k] += c.lat_hist[k];
