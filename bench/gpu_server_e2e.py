@@ -101,7 +101,7 @@ def run_one(core, name, spec, io, io_threads, seconds, rate=0.0, lg_threads=12, 
              front_end={k: fes.get(k) for k in ("steps", "idle_steps", "gather_segs", "io_phase_s", "wait_s",
                                                 "submit_s", "rx_bytes", "tx_bytes", "held_steps", "published",
                                                 "delivered", "routed", "dropped_nomem", "ring_full", "unroutable",
-                                                "expired", "ctrl", "live_msgs", "live_bytes")},
+                                                "expired", "ctrl", "live_msgs", "live_bytes", "log_used")},
              flow_off=st.get("flow_off", 0),
              last_step={k: lc.get(k) for k in ("n_ring_full", "n_dropped_nomem")},
              store=getattr(b, "_pw_stats", None))

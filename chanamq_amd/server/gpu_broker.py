@@ -140,6 +140,11 @@ class GpuBroker:
         msg_max = plane.info["msg_max"] if hasattr(plane, "info") else 0
         self.msg_high = int(0.75 * msg_max) if self.mem_high else 0
         self.msg_low = int(0.4 * msg_max) if self.mem_high else 0
+        # and the body log's occupancy (head - tail: one old live message pins the tail):
+        # publishers pause above 50% of it, resume below 25%
+        log_bytes = plane.info["log_bytes"] if hasattr(plane, "info") else 0
+        self.log_high = log_bytes // 2 if self.mem_high else 0
+        self.log_low = log_bytes // 4 if self.mem_high else 0
         self.blocked = False
         # durable queues x persistent messages -> store (write-behind, confirm gating)
         self.persistence = None
@@ -1156,12 +1161,15 @@ class GpuBroker:
         if not self.mem_high:
             return
         if self.fe is not None and self._fe_stats:
-            used, msgs = self._fe_stats["live_bytes"], self._fe_stats["live_msgs"]
+            used, msgs, logu = self._fe_stats["live_bytes"], self._fe_stats["live_msgs"], self._fe_stats["log_used"]
         else:
             lc = getattr(self.plane, "last_counters", None) or {}
             used, msgs = self.plane.memory_in_use(), lc.get("n_live_msgs", 0)
-        high = used >= self.mem_high or (self.msg_high and msgs >= self.msg_high)
-        low = used <= self.mem_low and (not self.msg_high or msgs <= self.msg_low)
+            logu = lc.get("log_head", 0) - lc.get("log_tail", 0)
+        high = used >= self.mem_high or (self.msg_high and msgs >= self.msg_high) or \
+            (self.log_high and logu >= self.log_high)
+        low = used <= self.mem_low and (not self.msg_high or msgs <= self.msg_low) and \
+            (not self.log_high or logu <= self.log_low)
         if not self.blocked and high:
             self.blocked = True
             self.stats["flow_off"] = self.stats.get("flow_off", 0) + 1

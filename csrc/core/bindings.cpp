@@ -238,7 +238,7 @@ PYBIND11_MODULE(_core, m) {
              o["held_steps"] = s.held_steps; o["idle_steps"] = s.idle_steps; o["gather_segs"] = s.gather_segs;
              o["live_bytes"] = s.live_bytes; o["live_msgs"] = s.live_msgs; o["io_phase_s"] = s.io_phase_s;
              o["dropped_nomem"] = s.dropped_nomem; o["ring_full"] = s.ring_full; o["unroutable"] = s.unroutable;
-             o["routed"] = s.routed; o["expired"] = s.expired; o["ctrl"] = s.ctrl;
+             o["routed"] = s.routed; o["expired"] = s.expired; o["ctrl"] = s.ctrl; o["log_used"] = s.log_used;
              o["wait_s"] = s.wait_s;
              o["submit_s"] = s.submit_s;
              o["lat_hist"] = std::vector<u64>(s.lat_hist, s.lat_hist + 32);

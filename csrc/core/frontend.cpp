@@ -720,6 +720,20 @@ void Frontend::io_phase(std::vector<Scatter*>& scat, bool gather) {
   ph_gather_ = gather;
   ph_arena_ = arena_[arena_i_];
   ph_cap_ = api_->ingress_cap;
+  if (api_->log_bytes) {
+    // ingress throttle: the device drops a step's publishes when the body log cannot take
+    // them (the oldest live message pins the log tail), so near a full log only a trickle
+    // is read (acks still get through and free it); TCP pushes back on publishers
+    u64 used;
+    {
+      std::lock_guard<std::mutex> g(stats_mu_);
+      used = stats_.log_used;
+    }
+    // two steps may already be in flight with up to ingress_cap each
+    const u64 reserve = 2 * api_->ingress_cap + (api_->log_bytes >> 6);
+    const u64 freeb = api_->log_bytes > used + reserve ? api_->log_bytes - used - reserve : 0;
+    if (freeb < ph_cap_) ph_cap_ = std::max<u64>(freeb, 256u << 10);
+  }
   ph_used_ = 0;
   ph_nseg_ = 0;
   ph_carry_ = 0;
@@ -828,6 +842,7 @@ void Frontend::finish_oldest(std::deque<Inflight>& inflight) {
     stats_.expired += c.n_expired;
     stats_.ctrl += c.n_ctrl;
     stats_.live_msgs = c.n_live_msgs;
+    stats_.log_used = c.log_head - c.log_tail;
     stats_.wait_s += w;
     for (int k = 0; k < 32; ++k) stats_.lat_hist[k] += c.lat_hist[k];
     if (needs_commit) stats_.held_steps++;
@@ -1001,6 +1016,7 @@ EchoEngine::EchoEngine(u32 c_max, u32 seg_max, u64 ingress_cap, u32 carry_cap) {
   api_.ingress_cap = ingress_cap;
   api_.ctrl_cap = 1 << 20;
   api_.carry_budget = 64ull << 20;
+  api_.log_bytes = 0;
   api_.eng = this;
   paused_.assign(c_max, 0);
   wblock_.assign(c_max, 0);

@@ -82,6 +82,7 @@ struct FeStats {
   u64 dropped_nomem = 0, ring_full = 0, unroutable = 0, routed = 0, expired = 0, ctrl = 0;
   i64 live_bytes = 0;
   u64 live_msgs = 0;
+  u64 log_used = 0;          // body-log occupancy (head - tail): the oldest live message pins it
   u64 lat_hist[32] = {};
   double io_phase_s = 0, wait_s = 0, submit_s = 0;
 };

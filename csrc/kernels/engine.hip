@@ -768,6 +768,7 @@ class Engine {
     a.c_max = d_.c_max; a.seg_max = d_.seg_max; a.carry_cap = d_.carry_cap;
     a.persist = d_.persist; a.persist_max = d_.persist_max;
     a.ingress_cap = d_.ingress_cap; a.ctrl_cap = d_.ctrl_cap; a.carry_budget = carry_budget_;
+    a.log_bytes = d_.log_bytes;
     a.eng = this;
     a.submit = [](void* e, const SegIn* sg, u32 n, const u8* pay, u64 len, i64 now, u32 worker) -> int {
       return ((Engine*)e)->guard([&] { return ((Engine*)e)->submit_raw(sg, n, (u64)pay, len, now, (u64)now, worker); });

@@ -95,6 +95,7 @@ struct CmqEngineApi {
   u32 c_max, seg_max, carry_cap, persist, persist_max;
   u64 ingress_cap, ctrl_cap;
   u64 carry_budget;   // per step: sum over the step's connections of (device carry + 48) <= this
+  u64 log_bytes;      // HBM body log capacity (Counters.log_head - log_tail = occupancy)
   void* eng;
   int (*submit)(void* eng, const SegIn* segs, u32 nseg, const u8* payload, u64 len, i64 now_ms, u32 worker);
   int (*wait_results)(void* eng, int p);
