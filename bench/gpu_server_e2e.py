@@ -19,6 +19,8 @@ import sys
 import tempfile
 import time
 
+import numpy as np
+
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 from chanamq_amd.broker import load  # noqa: E402
@@ -87,10 +89,23 @@ def run_one(core, name, spec, io, io_threads, seconds, rate=0.0, lg_threads=12, 
                                rate=rate, **spec))
     finally:
         cpu1 = thread_cpu()
+        after = {}
+        try:   # the broker after the load: what stays live / pinned once every client is gone
+            time.sleep(0.6)
+            if b.fe is not None:
+                b._sync_fe_stats()
+                after = {k: b._fe_stats[k] for k in ("live_msgs", "live_bytes", "log_used")}
+                with b.lock:
+                    after["queue_depths"] = {q.name: plane.message_count(q.slot) for q in plane.queue_by_slot.values()
+                                             if plane.message_count(q.slot)}
+                    after["log_live_blocks"] = int((np.frombuffer(plane.eng.download("log_live"), np.int64) != 0).sum())
+        except Exception as e:   # diagnostics only
+            after = {"error": repr(e)}
         b.stop()
         if store is not None:
             store.close()
     lc = getattr(plane, "last_counters", {}) or {}
+    r["after"] = after
     r["thread_cpu_s"] = {k: round(cpu1[k] - cpu0.get(k, 0.0), 2) for k in cpu1 if cpu1[k] - cpu0.get(k, 0.0) > 0.05}
     st = dict(b.stats)
     fes = getattr(b, "_fe_stats", None) or {}

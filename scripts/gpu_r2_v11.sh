@@ -1,0 +1,8 @@
+set -o pipefail
+O=gpurun_out/r2_v11; mkdir -p $O
+timeout -k 10 300 python -u bench/gpu_server_e2e.py --seconds 3 --io-threads 2 --only config2 --paced 0 --out $O/e2e.json > $O/e2e.log 2>&1 || exit $?
+python -c "
+import json
+for r in json.load(open('$O/e2e.json'))['results']:
+    fe=r.get('front_end') or {}
+    print(r['io_threads'], 'recv', round(r['recv_msgs_per_s']), 'sent', round(r['sent_msgs_per_s']), 'flow_off', r.get('flow_off'), r['after'], {k: fe.get(k) for k in ('dropped_nomem','routed','delivered','log_used','live_msgs')})"
