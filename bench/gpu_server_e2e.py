@@ -99,6 +99,20 @@ def run_one(core, name, spec, io, io_threads, seconds, rate=0.0, lg_threads=12, 
                     after["queue_depths"] = {q.name: plane.message_count(q.slot) for q in plane.queue_by_slot.values()
                                              if plane.message_count(q.slot)}
                     after["log_live_blocks"] = int((np.frombuffer(plane.eng.download("log_live"), np.int64) != 0).sum())
+                    if after["live_msgs"]:
+                        ent = np.dtype([("log_off", "<u8"), ("msg_id", "<u8"), ("ts", "<i8"), ("slot_bytes", "<u4"),
+                                        ("body_len", "<u4"), ("body_off", "<u4"), ("props_len", "<u2"), ("ex_len", "u1"),
+                                        ("rk_len", "u1"), ("refcnt", "<i4"), ("flags", "<u4"), ("pub_step", "<u4"),
+                                        ("pad", "<u4")])
+                        m = np.frombuffer(plane.eng.download("msgs"), ent)
+                        free_top = plane.info["msg_max"] - after["live_msgs"]
+                        fl = set(np.frombuffer(plane.eng.download("msg_free", 0, 4 * free_top), np.uint32).tolist())
+                        live = [i for i in range(len(m)) if i not in fl]
+                        lm = m[live]
+                        after["leaked"] = dict(n=len(live), refcnt=sorted(set(lm["refcnt"].tolist()))[:8],
+                                               pub_step=[int(lm["pub_step"].min()), int(lm["pub_step"].max())],
+                                               steps_total=b._fe_stats["steps"], flags=sorted(set(lm["flags"].tolist())),
+                                               body_len=sorted(set(lm["body_len"].tolist()))[:5])
         except Exception as e:   # diagnostics only
             after = {"error": repr(e)}
         b.stop()
