@@ -157,6 +157,42 @@ def test_bench_config2_shape_every_delivery_checked(gpu):
             assert (pid, seq) not in seen
             seen.add((pid, seq))
     assert len(seen) == producers * n
+    # nothing leaked: every message released, the body log fully reclaimed
+    assert c["n_live_msgs"] == 0 and c["live_bytes"] == 0
+    assert c["log_head"] - c["log_tail"] <= BENCH["log_block"]
+
+
+def test_closing_consumers_and_producers_leak_nothing(gpu):
+    """Connections close mid-stream (consumers with deliveries in the step, producers with
+    partial commands in their carry): every stored message is either delivered once or
+    still queued, and live messages == queued messages."""
+    from chanamq_amd.engine.dataplane import GpuDataPlane
+    producers, queues, size = 32, 8, 1024
+    d = GpuDataPlane(**BENCH)
+    x, cons = setup(d, producers, queues, "topic")
+    key = lambda pid, i: f"scale.{(pid + i) % queues}.k"   # noqa: E731
+    streams = {p + 1: producer_stream(p, 400, x, key, size) for p in range(producers)}
+    steps = steps_for(streams, 8, 21)
+    delivered = set()
+    for k, inp in enumerate(steps):
+        r = d.step(inp, now_ms=1_800_000_000_000 + k)
+        for q in range(queues):
+            for cm in decode_all(r.egress.get(cons + q, b"")):
+                key2 = struct.unpack(">II", cm.body[:8])
+                assert key2 not in delivered
+                delivered.add(key2)
+        if k == 4:   # half the consumers and a quarter of the producers go away mid-stream
+            for q in range(0, queues, 2):
+                d.close_connection(cons + q)
+            for p in range(0, producers, 4):
+                d.close_connection(p + 1)
+            steps = [{c: b for c, b in s.items() if c not in {p + 1 for p in range(0, producers, 4)}}
+                     for s in steps]
+    for k in range(3):
+        d.step({}, now_ms=1_800_000_000_100 + k)
+    c = d.last_counters
+    queued = sum(d.message_count(d.queues[(VH, f"sq{q}")].slot) for q in range(queues))
+    assert c["n_live_msgs"] == queued, (c["n_live_msgs"], queued)
 
 
 def test_storm_redeliveries_flagged_and_complete(gpu):
