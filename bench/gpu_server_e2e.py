@@ -107,8 +107,16 @@ def run_one(core, name, spec, io, io_threads, seconds, rate=0.0, lg_threads=12, 
                         m = np.frombuffer(plane.eng.download("msgs"), ent)
                         free_top = plane.info["msg_max"] - after["live_msgs"]
                         fl = set(np.frombuffer(plane.eng.download("msg_free", 0, 4 * free_top), np.uint32).tolist())
-                        live = [i for i in range(len(m)) if i not in fl]
-                        lm = m[live]
+                        queued = set()
+                        for q in plane.queue_by_slot.values():
+                            plane._refresh_ring(q)
+                            h, t = plane._u64("q_head", q.slot), plane._u64("q_tail", q.slot)
+                            raw = np.frombuffer(plane.eng.download("ring", q.ring_off * 16, q.capacity * 16), np.uint32)
+                            for pos in range(h, t):
+                                queued.add(int(raw[(pos & (q.capacity - 1)) * 4]))
+                        live = [i for i in range(len(m)) if i not in fl and i not in queued]
+                        after["queued_msgs"] = len(queued)
+                        lm = m[live] if live else m[:1]
                         after["leaked"] = dict(n=len(live), refcnt=sorted(set(lm["refcnt"].tolist()))[:8],
                                                pub_step=[int(lm["pub_step"].min()), int(lm["pub_step"].max())],
                                                steps_total=b._fe_stats["steps"], flags=sorted(set(lm["flags"].tolist())),
