@@ -117,6 +117,18 @@ def run_one(core, name, spec, io, io_threads, seconds, rate=0.0, lg_threads=12, 
                         live = [i for i in range(len(m)) if i not in fl and i not in queued]
                         after["queued_msgs"] = len(queued)
                         lm = m[live] if live else m[:1]
+                        # where do the leaked indices still appear?  whole ring pool scan
+                        top = plane._u64("ring_top", 0)
+                        pool = np.frombuffer(plane.eng.download("ring", 0, top * 16), np.uint32).reshape(-1, 4)
+                        lset = set(live)
+                        hits = [i for i in range(len(pool)) if int(pool[i, 0]) in lset]
+                        owner = {}
+                        for q in plane.queue_by_slot.values():
+                            owner.update({i: (q.name, q.ring_off, q.capacity) for i in range(q.ring_off, q.ring_off + q.capacity)})
+                        after["leak_where"] = dict(n_hits=len(hits), in_live_ring=sum(1 for i in hits if i in owner),
+                                                   sample=[(i, owner.get(i)) for i in hits[:8]])
+                        after["leak_steps"] = sorted(set(lm["pub_step"].tolist()))[:40]
+                        after["grow_log"] = getattr(b, "_grow_log", [])[:40]
                         after["leaked"] = dict(n=len(live), refcnt=sorted(set(lm["refcnt"].tolist()))[:8],
                                                pub_step=[int(lm["pub_step"].min()), int(lm["pub_step"].max())],
                                                steps_total=b._fe_stats["steps"], flags=sorted(set(lm["flags"].tolist())),

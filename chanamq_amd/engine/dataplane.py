@@ -447,6 +447,10 @@ class GpuDataPlane(ControlState):
         """Ready messages of queue slot ``q`` (AMQP Queue.DeclareOk message-count)."""
         return self._u64("q_tail", q) - self._u64("q_head", q)
 
+    def queue_tail(self, q):
+        """Queue position the next enqueue into slot ``q`` gets."""
+        return self._u64("q_tail", q)
+
     def purge(self, q):
         """Queue.Purge: mark every ready entry expired; the next step's dequeue (K12 TTL
         skip) releases them and their body-log bytes.  Returns the purged count."""

@@ -92,6 +92,16 @@ class GoldenDataPlane(ControlState):
         if self.persist and qq is not None and qq.durable and (msg.flags & MF_PERSIST):
             self._consumed_out.append((msg.id, q, qpos, kind))
 
+    def _mid(self):
+        """Message ids unique across ranks (the device uses per-GPU snowflake workers):
+        a rank's store may be adopted by a survivor whose own ids must not collide."""
+        _Msg._next += 1
+        return _Msg._next * 1024 + self.rank if self.world > 1 else _Msg._next
+
+    def queue_tail(self, q):
+        """Queue position the next enqueue into slot ``q`` gets."""
+        return self.qpos_head[q] + len(self.ring[q])
+
     def take_persist(self):
         out, self._persist_out = self._persist_out, []
         return out
@@ -421,7 +431,7 @@ class GoldenDataPlane(ControlState):
                 qs = [q for q in self._route(x, rk) if self.queue_by_slot[q].owner == self.rank]
                 if not qs:
                     continue
-                msg = _Msg(ex, rk, props, body, len(qs), self.step_no, flags & MF_PERSIST)
+                msg = _Msg(ex, rk, props, body, len(qs), self.step_no, flags & MF_PERSIST, mid=self._mid())
                 self._enqueue(msg, qs, expire, now_ms)
 
     def step_a(self, inputs=None, now_ms=0):
@@ -657,7 +667,8 @@ class GoldenDataPlane(ControlState):
             return
         flags = 1 if self._persistent(props) else 0
         tsp = self._prop_fields(props).get("timestamp")
-        msg = _Msg(ex, rk, props, body, len(qs), self.step_no, flags, ts=int(tsp) * 1000 if tsp else 0)
+        msg = _Msg(ex, rk, props, body, len(qs), self.step_no, flags, ts=int(tsp) * 1000 if tsp else 0,
+                   mid=self._mid())
         if self.world > 1:   # enqueued in step_b, ordered by source rank (see _import)
             self._deferred.append((msg, qs, expire, s))
         else:

@@ -179,6 +179,68 @@ class GpuPersistence:
     def unbind(self, vhost, queue, exchange, key):
         self.store.delete_bind(entity_id(vhost, exchange), entity_id(vhost, queue), key)
 
+    # ------------------------------------------------------------------ failover
+    def adopt(self, src, queues, now_ms=0):
+        """HA failover: this rank now owns ``queues`` (Queue objects re-homed
+        from a dead rank whose store is ``src``).  Their stored messages go into this
+        plane — unacked ones first, flagged redelivered, then the ready ones in offset
+        order — exactly like ``recover`` for a restart (reference: a re-homed QueueEntity
+        reloads its rows from Cassandra, QueueEntity.scala:80-140).  The rows move into
+        this rank's store (committed) before they are deleted from the dead rank's, so a
+        crash in between duplicates rather than loses.  Returns messages restored."""
+        p, st = self.plane, self.store
+        if self.native is not None:
+            self.native.drain()
+        items, moved, seeds = [], [], []
+        for q in queues:
+            if not q.durable:
+                continue
+            qid = entity_id(q.vhost, q.name)
+            r = src.select_queue(qid)
+            if r is None:
+                continue
+            (lconsumed, _, _, _), msgs, unacks = r
+            order = [(off, mid, True) for off, mid, _ in sorted(unacks)] + \
+                    [(off, mid, False) for off, mid, _ in sorted(msgs) if off > lconsumed]
+            base = p.queue_tail(q.slot)
+            st.insert_queue_meta(qid, -1, set(), True, q.ttl_ms)
+            for i, (off, mid, red) in enumerate(order):
+                m = src.select_message(mid)
+                if m is None:
+                    continue
+                _, ts, header, body, ex, rk, _, _ = m
+                items.append((q.slot, mid, ts, 0, ex.encode(), rk.encode(), header[10:], body, True, red))
+                moved.append((qid, off, mid, red))
+                n = self.refs.get(mid, 0) if self.native is None else 0
+                if self.native is None:
+                    self.refs[mid] = n + 1
+                if n == 0 and st.select_message(mid) is None:
+                    st.insert_message(mid, ts, header, body, ex, rk, True, 1, 0)
+                elif n:
+                    st.update_message_refer_count(mid, n + 1)
+                st.insert_queue_msg(qid, base + i, mid, len(body), 0)
+                if self.native is None:
+                    self.rows[(qid, mid)] = [base + i, len(body), False]
+                else:
+                    seeds.append((qid, mid, base + i, len(body)))
+        n = p.restore(items, now_ms) if items else 0
+        st.sync()
+        for qid, mid, off, size in seeds:
+            self.native.seed_row(qid, mid, off, size, False, 1)
+        # handed over: the dead rank's store no longer holds them (its restart must not
+        # deliver them a second time)
+        for qid, off, mid, red in moved:
+            if red:
+                src.delete_queue_unack(qid, mid)
+            else:
+                src.delete_queue_msg(qid, off)
+            src.delete_message(mid)
+        for q in queues:
+            if q.durable:
+                src.force_delete_queue(entity_id(q.vhost, q.name))
+        src.sync()
+        return n
+
     # ------------------------------------------------------------------ recovery
     def recover(self, now_ms=0):
         """Durable topology + messages from the store into the plane.  Returns the number

@@ -24,8 +24,13 @@ log = logging.getLogger("chanamq.node")
 
 
 class ShardedNode:
-    def __init__(self, plane, comm: Comm = None, membership: Membership = None, hb_timeout_s=2.0):
+    def __init__(self, plane, comm: Comm = None, membership: Membership = None, hb_timeout_s=2.0,
+                 persistence=None, peer_store=None):
+        """persistence: this rank's GpuPersistence; peer_store(rank) -> an opened Store of
+        that rank's (shared-filesystem) store directory, used to adopt the durable queues
+        of a dead rank (``handle_failure``)."""
         self.plane = plane
+        self.persistence, self.peer_store = persistence, peer_store
         self.comm = comm or Comm()
         self.exchanger = Exchanger(self.comm)
         plane.exchanger = None   # the node drives the exchange (and retries it on failover)
@@ -98,10 +103,32 @@ class ShardedNode:
         self.comm.rebuild(self.members.live)
         for r in dead:
             self.plane.shard_map.fail(r)
+        prev = {q.slot: q.owner for q in self.plane.queue_by_slot.values()}
         moved = self.plane.rehome(dead)
-        self.failovers.append((sorted(dead), moved))
-        log.warning("rank %d: ranks %s left; re-homed %d queues", self.rank, sorted(dead), len(moved))
+        adopted = self._adopt(dead, prev)
+        self.failovers.append((sorted(dead), moved, adopted))
+        log.warning("rank %d: ranks %s left; re-homed %d queues, reloaded %d durable messages",
+                    self.rank, sorted(dead), len(moved), adopted)
         return dead, moved
+
+    def _adopt(self, dead, prev):
+        """Durable queues that moved here from a dead rank: reload their stored messages
+        from that rank's store (the reference's re-homed QueueEntity reloads from
+        Cassandra)."""
+        if self.persistence is None or self.peer_store is None:
+            return 0
+        n = 0
+        for r in sorted(dead):
+            mine = [q for q in self.plane.queue_by_slot.values()
+                    if prev.get(q.slot) == r and q.owner == self.rank and q.durable]
+            if not mine:
+                continue
+            src = self.peer_store(r)
+            try:
+                n += self.persistence.adopt(src, mine)
+            finally:
+                src.close()
+        return n
 
     def close(self):
         self.members.stop()

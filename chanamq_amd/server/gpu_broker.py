@@ -126,6 +126,7 @@ class GpuBroker:
         self.gw = None
         self.fe = None
         self._fe_stats = None
+        self._grow_log = []       # (front-end step count, rings moved): diagnostics
         self.ingress_bytes, self.per_conn_read = ingress_bytes, per_conn_read
         # back-pressure (SURVEY A.Q17 / config 5): above the high watermark of stored
         # message bytes publishers get Connection.Blocked (if they announced the
@@ -340,6 +341,8 @@ class GpuBroker:
                 seg_status.append((conn, a))
             elif kind == FE_GROW:   # the device grew rings: return the old ranges to the pool
                 self.plane.rings_moved(data)
+                if len(self._grow_log) < 256:
+                    self._grow_log.append(((self._fe_stats or {}).get("steps", 0), len(data) // 56))
             elif kind == FE_ERROR:
                 import logging
                 logging.getLogger("chanamq.gpu").error("data-plane engine failed: %s", data.decode(errors="replace"))

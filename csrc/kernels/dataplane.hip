@@ -204,6 +204,7 @@ DEV void release_msg(const DS& d, u32 msg) {
     MsgEnt& m = d.msgs[msg];
     u64 blk = (m.log_off / d.log_block) % d.n_log_blocks;
     atomicAdd((unsigned long long*)&d.log_live[blk], (unsigned long long)(-(i64)m.slot_bytes));
+    atomicAdd((unsigned long long*)d.live_bytes, (unsigned long long)(-(i64)m.slot_bytes));
     u32 slot = atomicAdd(d.msg_free_top, 1u);
     d.msg_free[slot] = msg;
     atomicAdd(&d.ctr->n_freed, 1u);
@@ -317,7 +318,7 @@ __global__ __launch_bounds__(1024) void k_prep(DS d) {
   if (tid < sizeof(Counters) / 4) {
     u32* c = (u32*)d.ctr;
     if (tid * 4 < offsetof(Counters, log_head)) c[tid] = 0;
-    if (tid == 0) { d.ctr->n_grow = 0; d.tot[TS_NMOVE] = 0; }
+    if (tid == 0) { d.ctr->n_grow = 0; d.tot[TS_NMOVE] = 0; d.tot[TS_NDEFER] = 0; }
   }
   u32 running = 0;
   for (u32 base = 0; base < d.seg_max; base += 1024) {
@@ -1345,6 +1346,7 @@ DEV void route_emit(const DS& d, RouteAcc<PASS>& a, u32 p, u32 wbase, u32 srank,
   u32 pos = a.nq + (u32)__popcll(lm & lanemask_lt());
   if (local) {
     if (PASS) {
+      if (wbase + pos >= d.pair_max) return;   // pair table full: store_one trims refcnt
       d.pair_k[0][wbase + pos] = (q << d.rank_bits) | srank;
       d.pair_v[0][wbase + pos] = p;
     } else if (pos < 8) {
@@ -1366,9 +1368,10 @@ DEV void route_one(const DS& d, u32 p, u32 lane) {
     if (lane == 0 && d.pub_ret_sz[p]) atomicMin(&d.conn_ret_min[pb.conn], d.pub_ret_off[p]);
     u32 nq0 = d.pub_nq[p];
     if (nq0 == 0) return;
-    if (wbase + nq0 > d.pair_max) return;  // capacity: k_log_reserve clamps the pair count
+    if (wbase >= d.pair_max) return;  // capacity: log_reserve clamps the pair count
+    const u32 fit = d.pair_max - wbase < nq0 ? d.pair_max - wbase : nq0;
     if (nq0 <= 8) {  // routing result cached by pass 0
-      if (lane < nq0) {
+      if (lane < fit) {
         d.pair_k[0][wbase + lane] = (d.pub_qc[(u64)p * 8 + lane] << d.rank_bits) | srank;
         d.pair_v[0][wbase + lane] = p;
       }
@@ -1585,12 +1588,25 @@ DEV void store_one(const DS& d, u32 p, u32 lane) {
     m.props_len = (u16)pb.props_len;
     m.ex_len = (u8)pb.ex_len;
     m.rk_len = (u8)pb.rk_len;
-    m.refcnt = (i32)pb.nq;
+    // pairs past the pair table were not written (route_one): those queues never get
+    // the message, so it holds only the references that were enqueued, and the
+    // publisher gets Basic.Nack
+    const u32 wbase = d.tot[TS_PAIR_BASE] + d.pub_pair_off[p];
+    const u32 fit = wbase >= d.pair_max ? 0u : (d.pair_max - wbase < pb.nq ? d.pair_max - wbase : pb.nq);
+    m.refcnt = (i32)(fit ? fit : 1u);
     m.flags = pb.flags;
     m.pub_step = (u32)d.in->step;
     m.pad = 0;
     d.msgs[msg] = m;
     pb.msg = msg;
+    if (fit < pb.nq) {
+      atomicAdd(&d.ctr->n_ring_full, pb.nq - fit);
+      if (pb.chslot != INVALID) d.ch_pub_fail[pb.chslot] = 1u;
+    }
+    if (!fit) {   // freed by k_post: this kernel's waves are still popping the free list
+      pb.msg = INVALID;
+      d.defer_free[atomicAdd(&d.tot[TS_NDEFER], 1u)] = msg;
+    }
   }
 }
 
@@ -1789,7 +1805,9 @@ DEV u32 enqueue_one(const DS& d, u32 src, u32 i, u32 n, PersistRec* pr, u32 hs_n
   u32 rank = i - first;
   bool last = (i + 1 == n) || (kk[i + 1] >> rb) != q;
   const Pub& pb = d.pubs[p];
-  u64 head = d.q_head[q], tail = d.q_tail[q];
+  // the queue's last pair moves q_tail in this kernel: every pair reads the tail that
+  // k_ring_plan recorded before the enqueue, never q_tail itself
+  u64 head = d.q_head[q], tail = d.q_enq_tail[q];
   u64 cap = d.q_ring_mask[q] + 1;
   u64 freec = cap - (tail - head);
   u32 drop = INVALID;
@@ -1836,6 +1854,7 @@ __global__ void k_ring_plan(DS d, u32 src, u32 hs_ntiles) {
   const u32 first = hs_ntiles ? d.hist_scan[(q << rb) * hs_ntiles] : d.q_first[q];
   const u64 cnt = (u64)(i - first) + 1;
   const u64 head = d.q_head[q], tail = d.q_tail[q];
+  d.q_enq_tail[q] = tail;
   const u64 mask = d.q_ring_mask[q], cap = mask + 1;
   const u64 need = tail - head + cnt;
   if (need <= cap) return;
@@ -2584,6 +2603,9 @@ __global__ void k_post(DS d) {
   }
   wave_consumed(d, msg, q, qpos, 0u, aa);
   wave_release(d, msg, aa);
+  const u32 nd = d.tot[TS_NDEFER], gs = gridDim.x * blockDim.x;
+  for (u32 b = 0; b < nd; b += gs)   // grid-uniform trip count (wave_release ballots)
+    wave_release(d, b + i < nd ? d.defer_free[b + i] : INVALID, b + i < nd);
   // reset per-connection scratch (fused k_post2)
   if (i < d.c_max) {
     d.conn_dfirst[i] = INVALID;

@@ -26,6 +26,7 @@ enum : u32 {
   TS_REQ_TICKET = 28,                   // k_requeue finished-block ticket (last block compacts)
   TS_RS_TICKET = 29,                    // k_rs_hist finished-block ticket (last block: offsets)
   TS_NMOVE = 30,                        // rings moved (grown) this step (k_ring_plan)
+  TS_NDEFER = 31,                       // stored messages released at the end of the step
   TS_XSCAN = 32                         // + 2*r: per-destination record / byte totals
 };
 
@@ -55,8 +56,10 @@ struct DS {
   CtrlRec* ctrl_rec_h;
   RingMove* grow_h;         // host-mapped: rings grown this step (the host reclaims the old ones)
   RingMove* moves;          // this step's ring moves (k_ring_plan -> k_ring_moves)
+  u32* defer_free;          // [pub_cap] messages stored without a queue (pair table full): k_post frees
   u64* ring_top;            // ring pool bump pointer (shared with the host allocator)
   u64* q_max_cap;           // per queue ring growth limit (0 = the pool)
+  u64* q_enq_tail;          // per queue tail before this step's enqueue (k_ring_plan -> k_enqueue)
 
   // ---------------- per connection
   u8* carry;                // [c_max][carry_cap]

@@ -305,7 +305,9 @@ class Engine {
     d_.ring = (Desc*)dev("ring", sizeof(Desc) * d_.ring_pool);
     d_.ring_top = (u64*)dev("ring_top", 8);
     d_.q_max_cap = (u64*)dev("q_max_cap", 8ull * d_.q_max);
+    d_.q_enq_tail = (u64*)dev("q_enq_tail", 8ull * d_.q_max);
     d_.moves = (RingMove*)dev("moves", sizeof(RingMove) * (u64)d_.q_max);
+    d_.defer_free = (u32*)dev("defer_free", 4ull * d_.pub_cap);
 
     d_.ch_confirm = (u32*)dev("ch_confirm", 4ull * nch);
     d_.ch_pub_cnt = (u32*)dev("ch_pub_cnt", 4ull * nch);

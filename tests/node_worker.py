@@ -26,11 +26,72 @@ def count_delivers(b):
     return n
 
 
+def durable(out, die_rank, die_after):
+    """Persistent messages on durable queues survive their rank: nobody consumes until
+    after the failover, then every message published by any rank (including the ones
+    only rank ``die_rank``'s store held) is delivered once by the queues' new owners."""
+    from chanamq_amd.broker import load
+    from chanamq_amd.engine.persistence import GpuPersistence
+    core = load()
+    rank, world = dist.get_rank(), dist.get_world_size()
+
+    def open_store(r):
+        st = core.Store()
+        os.makedirs(os.path.join(out, "store"), exist_ok=True)
+        st.open(os.path.join(out, "store", f"rank{r}"), False)
+        return st
+
+    plane = GoldenDataPlane(default_queue_capacity=1 << 12, ring_pool=1 << 22, world=world, rank=rank, persist=True)
+    store = open_store(rank)
+    pers = GpuPersistence(plane, store)
+    node = ShardedNode(plane, Comm(timeout_s=20), hb_timeout_s=1.0, persistence=pers, peer_store=open_store)
+    nq, steps, per_step = 6, 8, 5
+    if rank == 0:
+        node.submit("declare_exchange", VH, "dfx", "fanout", durable=True)
+        for i in range(nq):
+            node.submit("declare_queue", VH, f"d{i}", durable=True)
+            node.submit("bind", VH, f"d{i}", "dfx", "")
+    node.step({}, now_ms=1)
+    for q in plane.queues.values():   # every rank records the durable topology (server: declare)
+        pers.queue(q)
+    store.sync()
+    plane.open_connection(1, VH)
+    plane.open_channel(1, 1)
+    got, cons = {}, {}
+    for k in range(steps + 6):
+        if rank == die_rank and k == die_after:
+            os._exit(0)
+        if k >= steps:   # drain: consumers on whatever this rank owns now
+            for q in plane.queues.values():
+                if q.owner == rank and q.name not in cons:
+                    c = 200 + int(q.name[1:])
+                    plane.open_connection(c, VH)
+                    plane.open_channel(c, 1)
+                    plane.consume(c, 1, VH, q.name, "c-" + q.name, no_ack=True)
+                    cons[q.name] = c
+        data = publish_stream(per_step, "dfx", lambda i: "", 40, persistent=True,
+                              seed=rank * 100 + k) if k < steps else b""
+        res, _ = node.step({1: data} if data else {}, now_ms=1000 + k)
+        pers.after_step()
+        pers.commit()
+        for c, b in res["egress"].items():
+            if c in cons.values():
+                got[str(c)] = got.get(str(c), 0) + count_delivers(b)
+    owned = sorted(q.name for q in plane.queues.values() if q.owner == rank)
+    with open(os.path.join(out, f"rank{rank}.json"), "w") as f:
+        json.dump({"owned": owned, "failovers": node.failovers, "live": sorted(node.members.live),
+                   "deliveries": got, "rows": store.row_count("queues")}, f)
+    node.close()
+    store.close()
+
+
 def main():
     scen, out = sys.argv[1], sys.argv[2]
     die_rank = int(sys.argv[3]) if len(sys.argv) > 3 else -1
     die_after = int(sys.argv[4]) if len(sys.argv) > 4 else -1
     dist.init_process_group("gloo")
+    if scen == "durable":
+        return durable(out, die_rank, die_after)
     rank, world = dist.get_rank(), dist.get_world_size()
     plane = GoldenDataPlane(default_queue_capacity=1 << 12, ring_pool=1 << 22, world=world, rank=rank)
     node = ShardedNode(plane, Comm(timeout_s=20), hb_timeout_s=1.0)

@@ -16,11 +16,11 @@ from test_sharded_golden import _free_port
 HERE = os.path.dirname(os.path.abspath(__file__))
 
 
-def _run(world, die_rank=-1, die_after=-1):
+def _run(world, die_rank=-1, die_after=-1, scen="fanout"):
     d = tempfile.mkdtemp()
     env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()), WORLD_SIZE=str(world),
                PYTHONPATH=os.pathsep.join([os.path.dirname(HERE), HERE]))
-    procs = [subprocess.Popen([sys.executable, os.path.join(HERE, "node_worker.py"), "fanout", d, str(die_rank),
+    procs = [subprocess.Popen([sys.executable, os.path.join(HERE, "node_worker.py"), scen, d, str(die_rank),
                                str(die_after)], env=dict(env, RANK=str(r))) for r in range(world)]
     for p in procs:
         assert p.wait(timeout=240) == 0
@@ -57,3 +57,25 @@ def test_failover_rehomes_queues():
             else:   # re-homed from rank 2 in step 4: everything published from then on
                 assert o["deliveries"][c] == 4 * 2 * 5, (r, q, o["deliveries"][c])
     assert sorted(q for o in out.values() for q in o["owned"]) == [f"q{i}" for i in range(6)]
+
+
+@pytest.mark.timeout(300)
+def test_failover_reloads_durable_queues():
+    """HA: rank 2 dies holding persistent messages on its durable
+    queues; the survivors that inherit those queues reload them from rank 2's store and
+    every message any rank published is delivered exactly once."""
+    out = _run(3, die_rank=2, die_after=4, scen="durable")
+    assert set(out) == {0, 1}
+    orig = ShardMap(3)
+    total = 0
+    for r, o in out.items():
+        assert o["live"] == [0, 1]
+        for q in o["owned"]:
+            c = str(200 + int(q[1:]))
+            # steps 0-3: 3 ranks x 5 persistent messages, steps 4-7: 2 ranks x 5
+            assert o["deliveries"].get(c) == 4 * 3 * 5 + 4 * 2 * 5, (r, q, o["deliveries"])
+            total += o["deliveries"][c]
+        moved_here = [q for q in o["owned"] if orig.owner("AMQ.DEFAULT", q) == 2]
+        assert o["failovers"][0][2] == 4 * 3 * 5 * len(moved_here)
+        assert o["rows"] == 0            # consumed (auto-ack): the store rows are gone too
+    assert total == 6 * 100
