@@ -439,7 +439,7 @@ class GoldenDataPlane(ControlState):
         self.counters = defaultdict(int)
         cnt = self.counters
         out = {"egress": {}, "ctrl": [], "txbuf": [], "events": [], "segs": []}
-        conns = set(inputs)
+        conns = {c for c in inputs if c in self.conns}   # bytes of a connection closed meanwhile: dropped
         for c, cl in self.carry.items():
             if cl and c in self.conns and not self.conns[c].paused:
                 conns.add(c)

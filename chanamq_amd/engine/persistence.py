@@ -180,7 +180,7 @@ class GpuPersistence:
         self.store.delete_bind(entity_id(vhost, exchange), entity_id(vhost, queue), key)
 
     # ------------------------------------------------------------------ failover
-    def adopt(self, src, queues, now_ms=0):
+    def adopt(self, src, queues, now_ms=None):
         """HA failover: this rank now owns ``queues`` (Queue objects re-homed
         from a dead rank whose store is ``src``).  Their stored messages go into this
         plane — unacked ones first, flagged redelivered, then the ready ones in offset
@@ -197,8 +197,9 @@ class GpuPersistence:
                 continue
             qid = entity_id(q.vhost, q.name)
             r = src.select_queue(qid)
-            if r is None:
-                continue
+            if r is None:   # declared through another rank: the dead rank stored only rows
+                src.insert_queue_meta(qid, -1, set(), True, q.ttl_ms)
+                r = src.select_queue(qid)
             (lconsumed, _, _, _), msgs, unacks = r
             order = [(off, mid, True) for off, mid, _ in sorted(unacks)] + \
                     [(off, mid, False) for off, mid, _ in sorted(msgs) if off > lconsumed]

@@ -16,7 +16,8 @@ import torch.distributed as dist
 
 
 class Comm:
-    def __init__(self, pg=None, rank=None, world=None, store=None, backend=None, device=None, timeout_s=60):
+    def __init__(self, pg=None, rank=None, world=None, store=None, backend=None, device=None, timeout_s=60,
+                 wait_s=None):
         if pg is None:
             pg = dist.distributed_c10d._get_default_group()
             rank = dist.get_rank() if rank is None else rank
@@ -30,7 +31,17 @@ class Comm:
         self.backend = backend or "gloo"
         self.device = device
         self.timeout_s = timeout_s
+        # RCCL: Work.wait(timeout) blocks the host and raises when a peer stops answering
+        # (without it the wait only orders streams and a dead peer hangs the GPU stream)
+        self.wait_s = timeout_s if wait_s is None else wait_s
         self.epoch = 0
+
+    def _wait(self, work):
+        if self.backend == "nccl":
+            if not work.wait(datetime.timedelta(seconds=self.wait_s)):
+                raise RuntimeError("collective timed out (peer lost)")
+        else:
+            work.wait()
 
     # ---------------------------------------------------------------- membership
     @property
@@ -44,6 +55,11 @@ class Comm:
         if self.rank not in live:
             raise RuntimeError("this rank is not in the live set")
         self.epoch += 1
+        if self.backend == "nccl":   # free the old communicator's stuck kernels / streams
+            try:
+                self.pg.abort()
+            except Exception:   # already torn down, or not supported by this build
+                pass
         prefix = dist.PrefixStore(f"comm-epoch{self.epoch}-{','.join(map(str, live))}/", self.store)
         tmo = datetime.timedelta(seconds=self.timeout_s)
         if self.backend == "nccl":
@@ -65,7 +81,7 @@ class Comm:
         isp = [int(in_splits[r]) for r in self.members]
         if sum(osp) != sum(out_splits) or sum(isp) != sum(in_splits):
             raise RuntimeError("traffic addressed to a rank that is not a member")
-        self.pg.alltoall_base(out, inp, osp, isp, dist.AllToAllOptions()).wait()
+        self._wait(self.pg.alltoall_base(out, inp, osp, isp, dist.AllToAllOptions()))
 
     def alltoall_counts(self, counts):
         """counts[r] = list of k ints for logical rank r -> received[r] (k ints each)."""
@@ -73,7 +89,7 @@ class Comm:
         m = len(self.members)
         t = torch.tensor([v for r in self.members for v in counts[r]], dtype=torch.int64, device=self._dev())
         o = torch.empty_like(t)
-        self.pg.alltoall_base(o, t, [k] * m, [k] * m, dist.AllToAllOptions()).wait()
+        self._wait(self.pg.alltoall_base(o, t, [k] * m, [k] * m, dist.AllToAllOptions()))
         vals = o.view(m, k).cpu().tolist()
         out = [[0] * k for _ in range(self.world)]
         for i, r in enumerate(self.members):
@@ -86,14 +102,14 @@ class Comm:
         m = len(self.members)
         n = torch.tensor([len(data)], dtype=torch.int64, device=dev)
         ns = [torch.empty(1, dtype=torch.int64, device=dev) for _ in range(m)]
-        self.pg.allgather([ns], [n]).wait()
+        self._wait(self.pg.allgather([ns], [n]))
         sizes = [int(x.item()) for x in ns]
         cap = max(sizes) if sizes else 0
         buf = torch.zeros(max(cap, 1), dtype=torch.uint8, device=dev)
         if data:
             buf[:len(data)] = torch.frombuffer(bytearray(data), dtype=torch.uint8).to(dev)
         outs = [torch.empty(max(cap, 1), dtype=torch.uint8, device=dev) for _ in range(m)]
-        self.pg.allgather([outs], [buf]).wait()
+        self._wait(self.pg.allgather([outs], [buf]))
         return {r: outs[i][:sizes[i]].cpu().numpy().tobytes() for i, r in enumerate(self.members)}
 
     def allgather_json(self, obj):

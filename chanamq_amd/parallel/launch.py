@@ -27,6 +27,10 @@ def join(backend="gloo", timeout_s=60):
                           timeout=datetime.timedelta(seconds=timeout_s), wait_for_workers=False)
     kw = {}
     if backend == "nccl":
+        # a peer that dies mid-collective must surface as an exception in this rank's
+        # step (Comm._wait -> ShardedNode.handle_failure), not as the RCCL watchdog
+        # tearing the process down: no async error handling, bounded blocking waits
+        os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "0")
         import torch
         local = int(os.environ.get("LOCAL_RANK", rank)) % max(1, torch.cuda.device_count())
         torch.cuda.set_device(local)

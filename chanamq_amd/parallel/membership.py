@@ -33,6 +33,8 @@ class Membership:
 
     def stop(self):
         self._stop.set()
+        if self._t.is_alive() and self._t is not threading.current_thread():
+            self._t.join(timeout=5 * self.interval_s + 1.0)
 
     def suspects(self):
         now = time.monotonic()

@@ -79,6 +79,9 @@ class ShardedNode:
     def _data_step(self, inputs, now_ms, retries):
         p = self.plane
         gpu = hasattr(p, "eng")
+        # a connection the control-log sync just closed (or that closed while its bytes
+        # were gathered) takes no part in the step
+        inputs = {c: v for c, v in inputs.items() if c in p.conns}
         if gpu:
             segs, ptr, n = p.stage(inputs)
             ticket = p.submit_raw(segs, ptr, n, now_ms)     # phase A (no exchanger on the plane)

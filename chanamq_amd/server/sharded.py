@@ -27,6 +27,9 @@ def main(argv=None):
     ap.add_argument("--info-dir", default="")
     ap.add_argument("--idle-step-ms", type=float, default=1.0)
     ap.add_argument("--c-max", type=int, default=256)
+    ap.add_argument("--store-dir", default="", help="durable store root: rank r keeps <dir>/rank<r>; "
+                                                    "survivors adopt a dead rank's durable queues from it")
+    ap.add_argument("--no-fsync", action="store_true")
     ap.add_argument("--backend", default="", help="default: nccl (RCCL) for --plane gpu, gloo for golden; "
                                                   "gloo + gpu rehearses several ranks on one GPU")
     args = ap.parse_args(argv)
@@ -46,16 +49,29 @@ def main(argv=None):
                              c_max=args.c_max, chpc=8, q_max=1024, cons_max=4096, seg_max=args.c_max,
                              cmd_max=1 << 16, deliv_max=1 << 16, msg_max=1 << 20, ingress_cap=32 << 20,
                              egress_cap=64 << 20, log_bytes=2 << 30, ring_pool=1 << 24, tb_max=1024,
-                             default_queue_capacity=1 << 14)
+                             default_queue_capacity=1 << 14, persist=int(bool(args.store_dir)))
     else:
         from ..engine.golden import GoldenDataPlane
         plane = GoldenDataPlane(world=world, rank=rank, c_max=args.c_max, chpc=8, q_max=1024,
-                                default_queue_capacity=1 << 14, ring_pool=1 << 24)
-    node = ShardedNode(plane, Comm(store=store, backend=backend, timeout_s=60))
+                                default_queue_capacity=1 << 14, ring_pool=1 << 24, persist=bool(args.store_dir))
+    node = ShardedNode(plane, Comm(store=store, backend=backend, timeout_s=60, wait_s=20))
+    st = None
+    if args.store_dir:
+        from ..broker import load
+        core = load()
+
+        def open_store(r):
+            s = core.Store()
+            os.makedirs(args.store_dir, exist_ok=True)
+            s.open(os.path.join(args.store_dir, f"rank{r}"), not args.no_fsync)
+            return s
+        st = open_store(rank)
+        node.peer_store = open_store
     from .gpu_broker import GpuBroker
     port = args.port if args.reuseport else args.port + rank
     broker = GpuBroker(plane, host=args.host, port=port, idle_step_ms=args.idle_step_ms, node=node,
-                       reuseport=args.reuseport, ingress_bytes=32 << 20).start()
+                       reuseport=args.reuseport, ingress_bytes=32 << 20, store=st).start()
+    node.persistence = broker.persistence if st is not None else None
     if args.info_dir:
         with open(os.path.join(args.info_dir, f"rank{rank}.json"), "w") as f:
             json.dump({"rank": rank, "world": world, "port": broker.port}, f)
@@ -65,6 +81,8 @@ def main(argv=None):
     stop.wait()
     broker.stop()
     node.close()
+    if st is not None:
+        st.close()
     return 0
 
 

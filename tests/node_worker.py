@@ -81,6 +81,7 @@ def durable(out, die_rank, die_after):
     with open(os.path.join(out, f"rank{rank}.json"), "w") as f:
         json.dump({"owned": owned, "failovers": node.failovers, "live": sorted(node.members.live),
                    "deliveries": got, "rows": store.row_count("queues")}, f)
+    node.comm.barrier()   # the c10d store lives in rank 0: nobody leaves while others still use it
     node.close()
     store.close()
 
@@ -131,8 +132,14 @@ def main():
     with open(os.path.join(out, f"rank{rank}.json"), "w") as f:
         json.dump({"owned": owned, "failovers": node.failovers, "live": sorted(node.members.live),
                    "deliveries": got}, f)
+    node.comm.barrier()
     node.close()
 
 
 if __name__ == "__main__":
     main()
+    # leave without running C++ destructors: a process group torn down at interpreter exit
+    # (while gloo / store threads still run) can abort with std::terminate
+    sys.stdout.flush()
+    sys.stderr.flush()
+    os._exit(0)

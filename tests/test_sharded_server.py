@@ -61,3 +61,53 @@ def test_cross_rank_routing_and_replicated_topology(cluster):
     assert e.value.code == 530
     c0.close()
     c1.close()
+
+
+@pytest.mark.timeout(300)
+def test_rank_death_durable_queue_reloaded(tmp_path):
+    """HA at the protocol level: a client on rank 2 declares a durable queue there (queues
+    live where they are declared) and publishes persistent messages with confirms; rank 2
+    is killed; the survivor that inherits the queue reloads it from rank 2's store and a
+    consumer on that rank receives every message."""
+    from chanamq_amd.parallel.launch import Launcher
+    port = _free_port()
+    env = dict(os.environ, PYTHONPATH=os.path.dirname(HERE))
+    ln = Launcher(3, ["-m", "chanamq_amd.server.sharded", "--plane", "golden", "--port", str(port),
+                      "--info-dir", str(tmp_path), "--store-dir", str(tmp_path / "store"), "--no-fsync"],
+                  env=env).start()
+    try:
+        deadline = time.time() + 120
+        while time.time() < deadline and not all((tmp_path / f"rank{r}.json").exists() for r in range(3)):
+            assert not ln.poll(), f"rank exited early: {ln.poll()}"
+            time.sleep(0.2)
+        ports = [json.load(open(tmp_path / f"rank{r}.json"))["port"] for r in range(3)]
+        c2 = Connection(port=ports[2], vhost="/")
+        ch = c2.channel()
+        ch.exchange_declare("hx", "direct", durable=True)
+        ch.queue_declare("hq", durable=True)
+        ch.queue_bind("hq", "hx", "k")
+        ch.confirm_select()
+        for i in range(20):
+            ch.basic_publish("hx", "k", b"m%d" % i, {"delivery_mode": 2})
+        assert ch.wait_for_confirms()
+        ln.procs[2].kill()
+        ln.procs[2].wait(30)
+        got = None
+        deadline = time.time() + 90
+        while got is None and time.time() < deadline:
+            for p in ports[:2]:
+                c = Connection(port=p, vhost="/")
+                try:
+                    cc = c.channel()
+                    cc.basic_consume("hq", "hc", no_ack=True)
+                    got = [d.body for d in cc.consume_n(20, timeout=20)]
+                    break
+                except ChannelClosed:   # not (yet) the owner
+                    pass
+                finally:
+                    c.close()
+            if got is None:
+                time.sleep(0.5)
+        assert got == [b"m%d" % i for i in range(20)]
+    finally:
+        ln.stop()
