@@ -360,6 +360,16 @@ class GpuDataPlane(ControlState):
             return out
         return out + parse_consumed(self.eng.host_view(f"consumed{self._last_parity}")[:n * CONSUMED_REC.itemsize])
 
+    def take_link_consumed(self, slots):
+        """The last finished step's consumed records of the shadow queues ``slots``
+        (parallel/links.py); the per-step buffer is left intact for ``take_consumed``."""
+        c = getattr(self, "last_counters", None)
+        n = min(c["n_consumed"], self.info["persist_max"]) if c and self.info.get("persist") else 0
+        if not n:
+            return []
+        recs = parse_consumed(self.eng.host_view(f"consumed{self._last_parity}")[:n * CONSUMED_REC.itemsize])
+        return [r for r in recs if r[1] in slots]
+
     def take_persist_raw(self):
         """(packed persist records, ConsumedRec bytes) of the last finished step, as the
         native PersistWorker consumes them."""
@@ -404,10 +414,22 @@ class GpuDataPlane(ControlState):
         """Recovery: enqueue stored messages into their queues in the given order.
         items: [(q_slot, msg_id, ts_ms, expire_ms, ex, rk, props, body, persistent, redelivered)]."""
         now = int(time.time() * 1000) if now_ms is None else int(now_ms)
-        cap = self.info["restore_max"]
+        if self.lag:
+            raise RuntimeError("restore() would overwrite the lagged exchange's pending imports")
+        cap = max(1, min(self.info["restore_max"] or self.info["import_max"], self.info["import_max"]))
+        room = self.info["xfer_bytes"]
+        chunks, cur, cur_b = [], [], 0
+        for it in items:   # batches within the import buffers: records and payload bytes
+            b = len(it[4]) + len(it[5]) + len(it[6]) + len(it[7]) + 16
+            if cur and (len(cur) == cap or cur_b + b > room):
+                chunks.append(cur)
+                cur, cur_b = [], 0
+            cur.append(it)
+            cur_b += b
+        if cur:
+            chunks.append(cur)
         total = 0
-        for k0 in range(0, len(items), max(1, cap)):
-            chunk = items[k0:k0 + cap]
+        for chunk in chunks:
             desc = np.zeros(len(chunk), RDESC)
             pay = bytearray()
             for i, (q, mid, ts, exp, ex, rk, props, body, persistent, red) in enumerate(chunk):

@@ -47,6 +47,7 @@ class GoldenDataPlane(ControlState):
         self.lag = bool(exchange_lag) and self.world > 1
         self._lag_prev = []                 # exchange_lag: records received last step
         self._persist_out, self._consumed_out = [], []
+        self.link_slots = set()   # shadow queues of remote consumers: consumed records always
         self.exchanger = exchanger
         self._outbox = defaultdict(list)  # dest rank -> [(RDesc fields, payload)]
         self._deferred = []                # this rank's routed publishes awaiting step_b
@@ -89,8 +90,16 @@ class GoldenDataPlane(ControlState):
     # ---- persistence (same records as the GPU plane's take_persist / take_consumed)
     def _consumed(self, msg, q, qpos, kind):
         qq = self.queue_by_slot.get(q)
-        if self.persist and qq is not None and qq.durable and (msg.flags & MF_PERSIST):
+        if (self.persist or q in self.link_slots) and qq is not None and qq.durable and (msg.flags & MF_PERSIST):
             self._consumed_out.append((msg.id, q, qpos, kind))
+
+    def take_link_consumed(self, slots):
+        """Consumed records of the remote-consumer shadow queues ``slots`` (parallel/
+        links.py), taken out; the rest stay for the persistence layer."""
+        mine = [r for r in self._consumed_out if r[1] in slots]
+        if mine:
+            self._consumed_out = [r for r in self._consumed_out if r[1] not in slots]
+        return mine
 
     def _mid(self):
         """Message ids unique across ranks (the device uses per-GPU snowflake workers):

@@ -5,6 +5,7 @@ reference for the one-process-per-GPU deployment (each rank then owns one plane 
 order so queue/exchange slots agree across ranks."""
 
 from .exchange import local_exchange
+from .links import RemoteLinks
 from .shard import ShardMap
 
 
@@ -13,6 +14,7 @@ class LocalCluster:
         self.world = world
         self.shard_map = shard_map or ShardMap(world)
         self.planes = [make_plane(rank=r, world=world, shard_map=self.shard_map) for r in range(world)]
+        self.links = [RemoteLinks(p) for p in self.planes]
 
     def __getitem__(self, r):
         return self.planes[r]
@@ -21,9 +23,22 @@ class LocalCluster:
         """Apply a control-plane op (declare/bind/delete ...) on every rank."""
         return [getattr(p, fn)(*args, **kw) for p in self.planes]
 
+    def link_open(self, lid, vhost, queue, dest, prefetch=0):
+        """Remote consumer link (parallel/links.py), replicated like a control op;
+        returns the shadow queue's name (consume it on rank ``dest``)."""
+        for lk in self.links:
+            lk.open(lid, vhost, queue, dest, prefetch)
+        return self.links[0].shadow_of(lid)
+
+    def link_close(self, lid):
+        for lk in self.links:
+            lk.close(lid)
+
     def step(self, inputs_by_rank, now_ms=0):
         """``inputs_by_rank``: [ {conn: bytes} per rank ] -> [StepResult/dict per rank]."""
         gpu = hasattr(self.planes[0], "eng")
+        for lk in self.links:
+            lk.before_step()
         tickets = []
         for r, p in enumerate(self.planes):
             inp = inputs_by_rank[r] if r < len(inputs_by_rank) else {}
@@ -42,6 +57,12 @@ class LocalCluster:
                 out.append(p.finish(tickets[r]))
             else:
                 out.append(p.step_b(recv[r]))
+        if self.links[0].active:   # X2/X3 link traffic, local copies
+            sent = [lk.outgoing(o["egress"] if isinstance(o, dict) else o.egress) for lk, o in zip(self.links, out)]
+            for r, lk in enumerate(self.links):
+                lk.incoming({s: sent[s].get(r, b"") for s in range(self.world)})
+            for lk in self.links:
+                lk.after_step()
         return out
 
 

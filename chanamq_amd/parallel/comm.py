@@ -112,6 +112,26 @@ class Comm:
         self._wait(self.pg.allgather([outs], [buf]))
         return {r: outs[i][:sizes[i]].cpu().numpy().tobytes() for i, r in enumerate(self.members)}
 
+    def alltoall_bytes(self, out):
+        """Variable-size all-to-all: ``out`` = {logical rank: bytes} -> {logical rank: bytes}
+        received from each live member (the host side of X2/X3, parallel/links.py)."""
+        m = len(self.members)
+        sizes = [[len(out.get(r, b""))] for r in range(self.world)]
+        got = self.alltoall_counts(sizes)
+        osz = [len(out.get(r, b"")) for r in self.members]
+        isz = [got[r][0] for r in self.members]
+        dev = self._dev()
+        flat = b"".join(out.get(r, b"") for r in self.members)
+        inp = torch.frombuffer(bytearray(flat or b"\0"), dtype=torch.uint8)[:len(flat)].to(dev)
+        o = torch.empty(sum(isz), dtype=torch.uint8, device=dev)
+        self._wait(self.pg.alltoall_base(o, inp, isz, osz, dist.AllToAllOptions()))   # every member calls it
+        data = o.cpu().numpy().tobytes()
+        res, pos = {}, 0
+        for i, r in enumerate(self.members):
+            res[r] = data[pos:pos + isz[i]]
+            pos += isz[i]
+        return res
+
     def allgather_json(self, obj):
         got = self.allgather_bytes(json.dumps(obj).encode())
         return {r: json.loads(b.decode()) for r, b in got.items()}

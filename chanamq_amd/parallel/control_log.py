@@ -13,7 +13,7 @@ from ..protocol import constants as C
 from .comm import Comm
 
 REPLICATED = {"declare_exchange", "delete_exchange", "declare_queue", "delete_queue", "bind", "unbind",
-              "place_queue", "ensure_vhost"}
+              "place_queue", "ensure_vhost", "link_open", "link_close"}
 
 
 class ControlLog:
@@ -22,6 +22,7 @@ class ControlLog:
         self.outbox = []
         self.applied = 0
         self.results = {}     # local seq -> result or ControlError tuple
+        self.handlers = {}    # op -> callable for ops served above the plane (parallel/links.py)
 
     def submit(self, op, *args, **kw):
         if op not in REPLICATED:
@@ -49,6 +50,8 @@ class ControlLog:
 
     def _apply(self, op, args, kw):
         p = self.plane
+        if op in self.handlers:
+            return self.handlers[op](*args, **kw)
         if op == "place_queue":
             vhost, name, rank = args
             q = p.queues.get((vhost, name))

@@ -1,0 +1,275 @@
+"""Remote consumption across ranks: a consumer on any rank for a queue
+owned by another.
+
+The reference lets a consumer on any node pull from any queue: the QueueEntity (owner)
+pushes deliveries to the consumer's FrameStage on another node and acks / requeues go
+back to the entity (FrameStage.scala:395-429, QueueEntity.scala:318-446).  Here a
+*link* joins the two ranks:
+
+* owner side (rank A, owns queue Q): a pseudo connection holding one manual-ack consumer
+  on Q with the remote consumer's prefetch.  A's own ``k_dequeue`` serves it (credit,
+  round-robin with A's local consumers, TTL skip) and assigns *A's* delivery tags; the
+  unacked window of that pseudo channel is the owner's record of what the remote
+  consumer holds (X2a credits = that window).
+* connection side (rank B): a shadow queue ``amq.link.<id>`` placed on B, into which the
+  owner's deliveries are restored (bodies, properties, exchange / routing key and the
+  redelivered bit preserved; the message id carries A's tag).  The client's consumer is a
+  plain local consumer of the shadow queue, so B assigns the client's delivery tags,
+  renders Basic.Deliver at the client's frame-max and enforces its prefetch (X2b).
+* acks (X3): consumption of a shadow message on B (ack, auto-ack) is reported by B's
+  data plane like a durable-queue consumed record (the shadow is marked durable and its
+  messages persistent) and sent back to A, which acks the matching tag on the pseudo
+  channel.  Nack / reject with requeue on B put the message back at the head of the
+  shadow (redelivered to the same consumer); cancel / channel close / connection close
+  close the link: A closes the pseudo channel, so everything the remote consumer still
+  held goes back to Q flagged redelivered, and B drops the shadow.
+
+The per-step traffic (owner -> consumer deliveries, consumer -> owner acks) is one
+variable-size all-to-all between the live ranks after the data step (``Comm.alltoall_bytes``,
+or local copies in ``LocalCluster``); it runs only while links exist, and every rank
+knows that from the replicated control log.
+"""
+
+import struct
+
+from ..engine.control import ControlError, C
+
+LINK_PREFIX = "amq.link."
+_EPOCH_SHIFT = 40
+K_DELIVER, K_ACK = 1, 2
+
+
+class Link:
+    __slots__ = ("id", "vhost", "queue", "dest", "prefetch", "shadow", "epoch", "pc", "closing")
+
+    def __init__(self, lid, vhost, queue, dest, prefetch):
+        self.id, self.vhost, self.queue, self.dest, self.prefetch = lid, vhost, queue, dest, prefetch
+        self.shadow = LINK_PREFIX + str(lid)
+        self.epoch, self.pc, self.closing = 0, None, False
+
+
+def parse_delivers(buf):
+    """Basic.Deliver + content frames -> [(tag, redelivered, exchange, routing_key,
+    raw properties, body)]."""
+    out, pos, n = [], 0, len(buf)
+    cur = None
+    while pos + 7 <= n:
+        t, _, size = struct.unpack_from(">BHI", buf, pos)
+        p = pos + 7
+        if t == 1:
+            cls, mid = struct.unpack_from(">HH", buf, p)
+            if cls == 60 and mid == 60:
+                q = p + 4
+                q += 1 + buf[q]                                  # consumer tag
+                tag = struct.unpack_from(">Q", buf, q)[0]
+                red = bool(buf[q + 8] & 1)
+                q += 9
+                ex = bytes(buf[q + 1:q + 1 + buf[q]])
+                q += 1 + buf[q]
+                rk = bytes(buf[q + 1:q + 1 + buf[q]])
+                cur = [tag, red, ex, rk, b"", bytearray(), 0]
+        elif t == 2 and cur is not None:
+            cur[6] = struct.unpack_from(">Q", buf, p + 4)[0]
+            cur[4] = bytes(buf[p + 12:p + size])
+            if cur[6] == 0:
+                out.append(tuple(cur[:5]) + (b"",))
+                cur = None
+        elif t == 3 and cur is not None:
+            cur[5] += buf[p:p + size]
+            if len(cur[5]) >= cur[6]:
+                out.append(tuple(cur[:5]) + (bytes(cur[5]),))
+                cur = None
+        pos = p + size + 1
+    return out
+
+
+class RemoteLinks:
+    """Links of one rank (one per plane).  ``alloc_conn`` / ``free_conn`` hand out the
+    pseudo-connection slots (the server passes its connection-slot allocator)."""
+
+    def __init__(self, plane, alloc_conn=None, free_conn=None):
+        self.plane = plane
+        self.links = {}          # id -> Link (replicated: every rank knows every link)
+        self.by_shadow = {}      # shadow queue slot -> Link (connection side)
+        self._restore = []       # received deliveries, restored before the next step
+        self._next_pc = plane.c_max - 2
+        self._alloc = alloc_conn or self._default_alloc
+        self._free = free_conn or (lambda c: None)
+
+    def _default_alloc(self):
+        while self._next_pc > 0 and self._next_pc in self.plane.conns:
+            self._next_pc -= 1
+        if self._next_pc <= 0:
+            raise ControlError(C.RESOURCE_ERROR, "no connection slot for a link", 60, 20)
+        c, self._next_pc = self._next_pc, self._next_pc - 1
+        return c
+
+    @property
+    def active(self):
+        return bool(self.links)
+
+    # ------------------------------------------------------------------ control ops
+    def open(self, lid, vhost, queue, dest, prefetch=0):
+        """Replicated (control log ``link_open``): applied in the same order on every rank."""
+        p = self.plane
+        q = p.queues.get((vhost, queue))
+        if q is None:
+            raise ControlError(C.NOT_FOUND, f"no queue '{queue}' in vhost '{vhost}'", 60, 20)
+        if dest == p.rank and hasattr(p, "eng") and not p.info.get("persist"):
+            raise ControlError(C.NOT_IMPLEMENTED, "remote consumers need the engine built with persist=1", 60, 20)
+        lk = Link(lid, vhost, queue, dest, int(prefetch) or 1024)
+        p.shard_map.place(vhost, lk.shadow, dest)
+        slot = p.declare_queue(vhost, lk.shadow, durable=True)
+        self.links[lid] = lk
+        if dest == p.rank:
+            self.by_shadow[slot] = lk
+            if hasattr(p, "link_slots"):
+                p.link_slots.add(slot)
+        if q.owner == p.rank:
+            self._attach(lk)
+        return slot
+
+    def _attach(self, lk):
+        """Owner side: the pseudo consumer on the source queue (a fresh epoch: tags
+        restart with the new pseudo channel)."""
+        p = self.plane
+        pc = self._alloc()
+        p.open_connection(pc, lk.vhost)
+        p.open_channel(pc, 1)
+        p.qos(pc, 1, prefetch_count=lk.prefetch)
+        p.consume(pc, 1, lk.vhost, lk.queue, "amq.link-" + str(lk.id), no_ack=False)
+        lk.pc, lk.epoch = pc, lk.epoch + 1
+
+    def _detach(self, lk):
+        if lk.pc is not None:
+            self.plane.close_connection(lk.pc)   # unacked -> back to the queue, redelivered
+            self._free(lk.pc)
+            lk.pc = None
+
+    def close(self, lid):
+        """Replicated (``link_close``).  The owner keeps the pseudo channel until the
+        step's acks came back (``after_step``); the connection side purges the shadow now
+        and deletes it after the next step released the purged entries."""
+        lk = self.links.get(lid)
+        if lk is None or lk.closing:
+            return None
+        lk.closing = True
+        sq = self.plane.queues.get((lk.vhost, lk.shadow))
+        if sq is not None and sq.owner == self.plane.rank:
+            self.plane.purge(sq.slot)
+        return None
+
+    def shadow_of(self, lid):
+        lk = self.links.get(lid)
+        return lk.shadow if lk else None
+
+    # ------------------------------------------------------------------ per step
+    def before_step(self, now_ms=None):
+        """Deliveries the last exchange brought go into the shadow queues (connection
+        side).  Deferred to just before the next step: a GPU restore is a small step of its
+        own and would overwrite the host-visible records the server still reads."""
+        p = self.plane
+        items, self._restore = self._restore, []
+        if items:
+            p.restore(items, now_ms) if now_ms is not None else p.restore(items)
+
+    def outgoing(self, eg):
+        """After the data step: {dest rank: bytes}.  Takes the pseudo connections' bytes
+        out of the step's egress {conn: bytes} (no socket behind them)."""
+        p = self.plane
+        out = {}
+        for lk in self.links.values():
+            if lk.pc is None:
+                continue
+            buf = eg.pop(lk.pc, None)
+            if not buf:
+                continue
+            b = out.setdefault(lk.dest, bytearray())
+            for tag, red, ex, rk, props, body in parse_delivers(buf):
+                b += struct.pack(">BIIQBBBII", K_DELIVER, lk.id, lk.epoch, tag, int(red), len(ex), len(rk),
+                                 len(props), len(body)) + ex + rk + props + body
+        if self.by_shadow:
+            for mid, q, _qpos, kind in p.take_link_consumed(self.by_shadow):
+                lk = self.by_shadow[q]
+                if kind != 0:   # only consumption is reported; requeues stay in the shadow
+                    continue
+                owner = p.queues[(lk.vhost, lk.queue)].owner
+                out.setdefault(owner, bytearray()).extend(
+                    struct.pack(">BIIQ", K_ACK, lk.id, mid >> _EPOCH_SHIFT, mid & ((1 << _EPOCH_SHIFT) - 1)))
+        return {r: bytes(b) for r, b in out.items()}
+
+    def incoming(self, got):
+        """Records from every rank -> pending acks / restores (applied by ``before_step``)."""
+        p = self.plane
+        for src in sorted(got):
+            buf, pos = got[src], 0
+            while pos < len(buf):
+                k = buf[pos]
+                if k == K_ACK:   # owner side: ack the tag on the pseudo channel now (before
+                    _, lid, epoch, tag = struct.unpack_from(">BIIQ", buf, pos)   # a closing link
+                    pos += 17                                                     # is detached)
+                    lk = self.links.get(lid)
+                    if lk is not None and lk.pc is not None and lk.epoch == epoch:
+                        p.apply_ack(lk.pc, 1, tag)
+                    continue
+                _, lid, epoch, tag, red, lex, lrk, lp, lb = struct.unpack_from(">BIIQBBBII", buf, pos)
+                pos += 28
+                ex = buf[pos:pos + lex]
+                pos += lex
+                rk = buf[pos:pos + lrk]
+                pos += lrk
+                props = buf[pos:pos + lp]
+                pos += lp
+                body = buf[pos:pos + lb]
+                pos += lb
+                lk = self.links.get(lid)
+                if lk is None or lk.closing:
+                    continue   # the owner requeued it when the link closed
+                sq = p.queues.get((lk.vhost, lk.shadow))
+                if sq is None:
+                    continue
+                self._restore.append((sq.slot, (epoch << _EPOCH_SHIFT) | tag, 0, 0, bytes(ex), bytes(rk),
+                                      bytes(props), bytes(body), True, bool(red)))
+
+    def after_step(self):
+        """Finish closing links: the owner closes the pseudo channel (after this step's
+        acks were applied), the connection side deletes the drained shadow."""
+        p = self.plane
+        for lid in [l for l, lk in self.links.items() if lk.closing]:
+            lk = self.links.pop(lid)
+            self._detach(lk)
+            sq = p.queues.get((lk.vhost, lk.shadow))
+            if sq is not None:
+                self.by_shadow.pop(sq.slot, None)
+                getattr(p, "link_slots", set()).discard(sq.slot)
+                p.delete_queue(lk.vhost, lk.shadow)
+            p.shard_map.placement.pop(_eid(lk.vhost, lk.shadow), None)
+
+    # ------------------------------------------------------------------ failover
+    def on_failure(self, dead):
+        """Before the queues are re-homed: links whose consumer side died close (their
+        shadows go; the owner requeues what they held); links whose owner died lose the
+        pseudo channel (its window was on the dead GPU) and re-attach at the queue's new
+        owner after ``rehome`` (``after_rehome``)."""
+        p = self.plane
+        for lid in [l for l, lk in self.links.items() if lk.dest in dead]:
+            lk = self.links.pop(lid)
+            self._detach(lk)
+            sq = p.queues.get((lk.vhost, lk.shadow))
+            if sq is not None:
+                self.by_shadow.pop(sq.slot, None)
+                getattr(p, "link_slots", set()).discard(sq.slot)
+                p.delete_queue(lk.vhost, lk.shadow)
+            p.shard_map.placement.pop(_eid(lk.vhost, lk.shadow), None)
+
+    def after_rehome(self):
+        p = self.plane
+        for lk in self.links.values():
+            q = p.queues.get((lk.vhost, lk.queue))
+            if q is not None and q.owner == p.rank and lk.pc is None and not lk.closing:
+                self._attach(lk)
+
+
+def _eid(vhost, name):
+    from ..engine.control import entity_id
+    return entity_id(vhost, name)

@@ -18,6 +18,7 @@ import logging
 from .comm import Comm
 from .control_log import ControlLog
 from .exchange import Exchanger
+from .links import RemoteLinks
 from .membership import Membership
 
 log = logging.getLogger("chanamq.node")
@@ -38,6 +39,11 @@ class ShardedNode:
         self.members = membership or Membership(self.comm.store, self.comm.rank, self.comm.world,
                                                 timeout_s=hb_timeout_s)
         self.failovers = []
+        # remote consumers (X2/X3): link ops ride the control log, link traffic one
+        # all-to-all after each data step while links exist
+        self.links = RemoteLinks(plane)
+        self.log.handlers["link_open"] = self.links.open
+        self.log.handlers["link_close"] = self.links.close
 
     @property
     def rank(self):
@@ -48,12 +54,27 @@ class ShardedNode:
 
     def step(self, inputs=None, now_ms=0, retries=3):
         """One lockstep step -> (plane step result, {seq: result} of this rank's ops)."""
+        self.links.before_step()
         results = self._retry(self.log.sync, retries)
-        return self._data_step(inputs or {}, now_ms, retries), results
+        res = self._data_step(inputs or {}, now_ms, retries)
+        self.relay(res["egress"] if isinstance(res, dict) else res.egress, retries)
+        return res, results
+
+    def relay(self, egress, retries=3):
+        """After a data step: owner-side deliveries of the remote consumers' pseudo
+        connections (taken out of ``egress``) and connection-side acks, one all-to-all."""
+        if not self.links.active:
+            return
+        out = self.links.outgoing(egress)
+        got = self._retry(lambda: self.comm.alltoall_bytes(out), retries)
+        self.links.incoming(got)
+        self.links.after_step()
 
     def step_raw(self, segs, ptr, nbytes, now_ms, retries=3):
         """GPU plane, pre-staged ingress (server gateway): runs phase A, the exchange and
-        phase B; returns (ticket for plane.finish, {seq: result})."""
+        phase B; returns (ticket for plane.finish, {seq: result}).  The caller runs
+        ``relay`` with the pseudo connections' egress once the step finished."""
+        self.links.before_step()
         results = self._retry(self.log.sync, retries)
         p = self.plane
         ticket = p.submit_raw(segs, ptr, nbytes, now_ms)
@@ -106,8 +127,10 @@ class ShardedNode:
         self.comm.rebuild(self.members.live)
         for r in dead:
             self.plane.shard_map.fail(r)
+        self.links.on_failure(dead)
         prev = {q.slot: q.owner for q in self.plane.queue_by_slot.values()}
         moved = self.plane.rehome(dead)
+        self.links.after_rehome()
         adopted = self._adopt(dead, prev)
         self.failovers.append((sorted(dead), moved, adopted))
         log.warning("rank %d: ranks %s left; re-homed %d queues, reloaded %d durable messages",

@@ -168,7 +168,16 @@ class GpuBroker:
         self.conns = {}
         # slot c_max-1: pseudo-connection through which committed transactions publish
         self.txc = plane.c_max - 1
-        self._free = list(range(plane.c_max - 2, 0, -1))   # slot 0 unused
+        # sharded: the slots below txc serve remote-consumer links (parallel/links.py)
+        n_link = min(64, max(2, plane.c_max // 16)) if node is not None else 0
+        self._top_slot = plane.c_max - 2 - n_link          # highest client connection slot
+        self._free = list(range(self._top_slot, 0, -1))   # slot 0 unused
+        self._link_free = list(range(self._top_slot + 1, plane.c_max - 1))
+        self._links = {}        # (conn, channel, consumer tag) -> link id (remote consumers)
+        self._link_seq = 0
+        if node is not None:
+            node.links._alloc = self._alloc_link_slot
+            node.links._free = self._link_free.append
         self._txbuf = {}        # (conn, channel) -> raw data commands held since Tx.Select / last commit
         self._tx_pending = []   # commits waiting for their injection step: (conn, channel, bytes)
         self._tx_active = None  # (conn, channel) injected in the current step
@@ -186,7 +195,7 @@ class GpuBroker:
             from ..broker import load
             self.fe = load().Frontend(self.plane.eng.c_api(), dict(
                 host=self.host, port=self.port, io_threads=self.io_threads, per_conn_read=self.per_conn_read,
-                idle_step_ms=self.idle_step_s * 1000.0, worker=self.plane.worker, max_slot=self.plane.c_max - 2,
+                idle_step_ms=self.idle_step_s * 1000.0, worker=self.plane.worker, max_slot=self._top_slot,
                 reuseport=self.reuseport, **self.fe_cfg))
             self.port = self.fe.port
             if self.persistence is not None:   # native write-behind: records never touch Python
@@ -200,7 +209,7 @@ class GpuBroker:
             return self
         if self.io == "native":
             from ..broker import load
-            self.gw = load().Gateway(self.host, self.port, self.plane.c_max, self.reuseport)
+            self.gw = load().Gateway(self.host, self.port, self._top_slot + 1, self.reuseport)
             self.port = self.gw.port
             if hasattr(self.plane, "mod"):
                 self._pin = self.plane.mod.alloc_pinned(self.ingress_bytes)
@@ -492,6 +501,14 @@ class GpuBroker:
         res = p.finish(t, collect=True, collect_egress=False)
         self._persist_step()
         eg, co = p.host_egress(t)
+        if self.node is not None and self.node.links.active:   # remote consumers: link traffic
+            pe = {}
+            for lk in self.node.links.links.values():
+                if lk.pc is not None and co["len"][lk.pc]:
+                    o, n = int(co["off"][lk.pc]), int(co["len"][lk.pc])
+                    pe[lk.pc] = bytes(eg[o:o + n])
+                    co["len"][lk.pc] = 0
+            self.node.relay(pe)
         if co["len"][self.txc]:    # Basic.Return of committed publishes -> their connection
             o, n = int(co["off"][self.txc]), int(co["len"][self.txc])
             if self._tx_active is not None and self._tx_active[0] in self.conns:
@@ -886,6 +903,8 @@ class GpuBroker:
         if n == "channel.close":
             self._txbuf.pop((c.id, ch), None)
             p.close_channel(c.id, ch)
+            if self._links:
+                self._close_links(c.id, ch)
             self._send(c, ch, Method("channel.close_ok"))
         elif n == "channel.close_ok":
             pass
@@ -971,13 +990,19 @@ class GpuBroker:
             self._send(c, ch, Method("basic.qos_ok"))
         elif n == "basic.consume":
             qn = m.queue or c.last_queue.get(ch, "")
-            self._queue(vh, qn, 60, 20)
+            q = self._queue(vh, qn, 60, 20)
             tag = m.consumer_tag or ("amq.ctag-" + uuid.uuid4().hex)
+            if self.node is not None and q.owner != p.rank:
+                if (c.id, ch, tag) in self._links or tag in p.channel(c.id, ch).consumers:
+                    raise ControlError(C.NOT_ALLOWED, f"consumer tag '{tag}' in use", 60, 20)
+                return self._remote_consume(c, ch, vh, q, tag, m)
             p.consume(c.id, ch, vh, qn, tag, no_ack=m.no_ack)
             if not m.nowait:
                 self._send(c, ch, Method("basic.consume_ok", consumer_tag=tag))
         elif n == "basic.cancel":
             p.cancel(c.id, ch, m.consumer_tag)
+            if self._links:
+                self._close_links(c.id, ch, m.consumer_tag)
             if not m.nowait:
                 self._send(c, ch, Method("basic.cancel_ok", consumer_tag=m.consumer_tag))
         elif n in ("basic.recover", "basic.recover_async"):
@@ -1090,6 +1115,8 @@ class GpuBroker:
         for seq, (conn, ch, reply, m) in pending.items():
             c = self.conns.get(conn)
             if c is None or c.state != "open":
+                if hasattr(reply, "abandon"):   # e.g. a link opened for a connection now gone
+                    reply.abandon()
                 continue
             res = results.get(seq)
             err = error_of(res)
@@ -1100,9 +1127,46 @@ class GpuBroker:
                     continue
                 self._chan_close(c, ch, code, text, m.class_id, m.method_id)
             elif reply is not None:
-                self._send(c, ch, reply(res))
+                out = reply(res)
+                if out is not None:
+                    self._send(c, ch, out)
             if c.state == "open":
                 self._unpause(conn)
+
+    def _alloc_link_slot(self):
+        if not self._link_free:
+            raise ControlError(C.RESOURCE_ERROR, "no connection slot left for a remote consumer", 60, 20)
+        return self._link_free.pop()
+
+    def _remote_consume(self, c, ch, vh, q, tag, m):
+        """Basic.Consume of a queue another rank owns (X2/X3): a link through the control
+        log; once applied on every rank the client's consumer attaches here to the link's
+        shadow queue (parallel/links.py)."""
+        p = self.plane
+        self._link_seq += 1
+        lid = (p.rank << 24) | self._link_seq
+        pf = p.channel(c.id, ch).prefetch_count
+        seq = self.node.submit("link_open", lid, vh, q.name, p.rank, 0 if m.no_ack else pf)
+
+        def reply(res, lid=lid):
+            shadow = self.node.links.shadow_of(lid)
+            try:
+                p.consume(c.id, ch, vh, shadow, tag, no_ack=m.no_ack)
+            except ControlError as e:
+                self.node.submit("link_close", lid)
+                self._chan_close(c, ch, e.code, e.text, 60, 20)
+                return None
+            self._links[(c.id, ch, tag)] = lid
+            return None if m.nowait else Method("basic.consume_ok", consumer_tag=tag)
+        reply.abandon = lambda lid=lid: self.node.submit("link_close", lid)
+        self._deferred[seq] = (c.id, ch, reply, m)
+        return "deferred"
+
+    def _close_links(self, conn, ch=None, tag=None):
+        """Cancel / channel close / connection close of remote consumers."""
+        for key in [k for k in self._links if k[0] == conn and (ch is None or k[1] == ch)
+                    and (tag is None or k[2] == tag)]:
+            self.node.submit("link_close", self._links.pop(key))
 
     def _queue(self, vh, name, cls, mid):
         q = self.plane.queues.get((vh, name))
@@ -1116,6 +1180,8 @@ class GpuBroker:
 
     def _chan_close(self, c, ch, code, text, cls, mid):
         self.plane.close_channel(c.id, ch)
+        if self._links:
+            self._close_links(c.id, ch)
         c.closing_channels.add(ch)
         self._send(c, ch, Method("channel.close", reply_code=code, reply_text=text[:255], class_id=cls,
                                  method_id=mid))
@@ -1125,6 +1191,8 @@ class GpuBroker:
             return
         self._send(c, 0, Method("connection.close", reply_code=code, reply_text=text[:255], class_id=cls,
                                 method_id=mid))
+        if self._links:
+            self._close_links(c.id)
         with self.lock:
             self.plane.close_connection(c.id)
             if self.fe is not None:   # its bytes go to the host again (waiting for CloseOk)
@@ -1210,6 +1278,8 @@ class GpuBroker:
             return
         prev = c.state
         c.state = "closed"
+        if self._links:
+            self._close_links(c.id)
         if self.fe is not None:
             if prev != "gone":
                 self._flush(c)

@@ -49,7 +49,7 @@ def main(argv=None):
                              c_max=args.c_max, chpc=8, q_max=1024, cons_max=4096, seg_max=args.c_max,
                              cmd_max=1 << 16, deliv_max=1 << 16, msg_max=1 << 20, ingress_cap=32 << 20,
                              egress_cap=64 << 20, log_bytes=2 << 30, ring_pool=1 << 24, tb_max=1024,
-                             default_queue_capacity=1 << 14, persist=int(bool(args.store_dir)))
+                             default_queue_capacity=1 << 14, persist=1)   # persist: store rows and remote-consumer acks
     else:
         from ..engine.golden import GoldenDataPlane
         plane = GoldenDataPlane(world=world, rank=rank, c_max=args.c_max, chpc=8, q_max=1024,

@@ -705,7 +705,7 @@ class Engine {
     x[3 * WORLD_MAX + d_.my_rank] = (u32)pb;
     launch_ingest(s_comp_, io);
     launch_route(s_comp_, io, d_.pub_max);
-    launch_phase_b(s_comp_, io);
+    launch_phase_b(s_comp_, io, /*dispatch=*/false);
     HIPCHECK(hipStreamSynchronize(s_comp_));
     const Counters* c = (const Counters*)buf("ctr_host0").ptr;
     return c->n_routed_msgs;
@@ -1026,7 +1026,9 @@ class Engine {
   }
 
   // enqueue, acks, dispatch, render (K7-K11)
-  void launch_tail(hipStream_t s, const DS& d) {
+  // dispatch = false (restore): enqueue only; nothing is delivered or rendered between
+  // steps (the restored messages go out with the next step's dispatch)
+  void launch_tail(hipStream_t s, const DS& d, bool dispatch = true) {
     Range rg("chanamq.K7-K11.tail");
     u32 nch = d.c_max * d.chpc;
     u32* pk[2] = {d.pair_k[0], d.pair_k[1]};
@@ -1038,6 +1040,12 @@ class Engine {
     hipLaunchKernelGGL(k_ring_plan, blocks(d.pair_max, 256), dim3(256), 0, s, d, psrc, hs_ntiles);
     hipLaunchKernelGGL(k_ring_moves, dim3(256), dim3(256), 0, s, d);
     hipLaunchKernelGGL(k_enqueue, blocks(d.pair_max, 256), dim3(256), 0, s, d, psrc, hs_ntiles);
+    if (!dispatch) {
+      const u64 pn = d.deliv_max > d.c_max ? d.deliv_max : d.c_max;
+      hipLaunchKernelGGL(k_post, blocks(pn, 256), dim3(256), 0, s, d);   // n_deliv = 0: frees only
+      hipLaunchKernelGGL(k_host_out, dim3(64), dim3(256), 0, s, d);
+      return;
+    }
     hipLaunchKernelGGL(k_chan_advance, dim3(nch < 2048 ? nch : 2048), dim3(256), 0, s, d);
     // requeued deliveries go back in front of their queues' heads before this step's
     // dispatch, in queue-offset order (QueueEntity.scala:415-446)
@@ -1074,12 +1082,12 @@ class Engine {
   }
 
   // world > 1, after the all-to-all: import, route against local queues, rest of the step
-  void launch_phase_b(hipStream_t s, const DS& d) {
+  void launch_phase_b(hipStream_t s, const DS& d, bool dispatch = true) {
     Range rg("chanamq.X1.import");
     hipLaunchKernelGGL(k_import_prep, dim3(1), dim3(64), 0, s, d);
     hipLaunchKernelGGL(k_import, wave_blocks(d.import_max), dim3(256), 0, s, d);
     launch_route(s, d, d.import_max);
-    launch_tail(s, d);
+    launch_tail(s, d, dispatch);
   }
 
   void capture_main(int p) {

@@ -78,17 +78,6 @@ def test_cluster_matches_single_plane(name, world):
     assert any(single), "scenario produced no egress"
 
 
-def test_remote_consume_rejected():
-    from chanamq_amd.engine.control import ControlError
-    dp = golden(world=2, rank=0)
-    dp.shard_map.place("/", "elsewhere", 1)
-    dp.declare_queue("/", "elsewhere")
-    dp.open_connection(1, "/")
-    dp.open_channel(1, 1)
-    with pytest.raises(ControlError):
-        dp.consume(1, 1, "/", "elsewhere", "t")
-
-
 def _free_port():
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))

@@ -54,11 +54,33 @@ def test_cross_rank_routing_and_replicated_topology(cluster):
     p1 = c1.channel()
     p1.basic_publish("sx", "a.q", b"from-1")
     assert a.consume_n(1)[0].body == b"from-1"
-    # consumers attach on the owning rank
-    with pytest.raises(ChannelClosed) as e:
-        c1.channel().basic_consume("qa", "remote")
-        c1.process(1.0)
-    assert e.value.code == 530
+    # a consumer on rank 1 of rank 0's queue (X2/X3 link): manual ack, nack-requeue
+    p.basic_publish("sx", "a.r", b"r1")
+    p.basic_publish("sx", "a.r", b"r2")
+    assert [d.body for d in a.consume_n(2)] == [b"r1", b"r2"]
+    a.basic_cancel("ca")
+    r = c1.channel()
+    r.basic_qos(prefetch_count=5)
+    r.basic_consume("qa", "remote")
+    c1.process(0.5)
+    for i in range(8):
+        p.basic_publish("sx", "a.z", b"z%d" % i)
+    got = r.consume_n(5)
+    assert [d.body for d in got] == [b"z%d" % i for i in range(5)]     # prefetch 5 across ranks
+    r.basic_nack(got[1].delivery_tag, requeue=True)
+    again = r.consume_n(1)[0]
+    assert again.body == b"z1" and again.method.redelivered
+    r.basic_ack(got[4].delivery_tag, multiple=True)
+    rest = r.consume_n(3)
+    assert [d.body for d in rest] == [b"z5", b"z6", b"z7"]
+    r.basic_ack(rest[-1].delivery_tag, multiple=True)
+    r.basic_ack(again.delivery_tag)
+    r.basic_cancel("remote")
+    c1.process(0.5)
+    # everything was acked through the link: nothing comes back to a new consumer
+    a.basic_consume("qa", "ca2", no_ack=True)
+    p.basic_publish("sx", "a.end", b"end")
+    assert a.consume_n(1)[0].body == b"end"
     c0.close()
     c1.close()
 
