@@ -235,7 +235,14 @@ class GpuPersistence:
                 src.delete_queue_unack(qid, mid)
             else:
                 src.delete_queue_msg(qid, off)
-            src.delete_message(mid)
+            # a message row may still back another of the dead rank's queues that a
+            # different survivor adopts (concurrently): drop only this queue's reference
+            m = src.select_message(mid)
+            if m is not None:
+                if m[7] <= 1:
+                    src.delete_message(mid)
+                else:
+                    src.update_message_refer_count(mid, m[7] - 1)
         for q in queues:
             if q.durable:
                 src.force_delete_queue(entity_id(q.vhost, q.name))

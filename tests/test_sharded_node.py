@@ -73,7 +73,7 @@ def test_failover_reloads_durable_queues():
         for q in o["owned"]:
             c = str(200 + int(q[1:]))
             # steps 0-3: 3 ranks x 5 persistent messages, steps 4-7: 2 ranks x 5
-            assert o["deliveries"].get(c) == 4 * 3 * 5 + 4 * 2 * 5, (r, q, o["deliveries"])
+            assert o["deliveries"].get(c) == 4 * 3 * 5 + 4 * 2 * 5, (r, q, o["deliveries"], o["failovers"])
             total += o["deliveries"][c]
         moved_here = [q for q in o["owned"] if orig.owner("AMQ.DEFAULT", q) == 2]
         assert o["failovers"][0][2] == 4 * 3 * 5 * len(moved_here)
