@@ -48,7 +48,7 @@ def build(force=False, verbose=False, sanitize=None):
     if sanitize:
         flags += [f"-fsanitize={sanitize}", "-fno-omit-frame-pointer"]
     cmd = [cxx, *flags, f"-I{pybind11.get_include()}", f"-I{sysconfig.get_paths()['include']}",
-           *[os.path.join(_SRC, s) for s in SOURCES], "-o", out + ".tmp", "-lssl", "-lcrypto", "-lz", "-lpthread"]
+           *[os.path.join(_SRC, s) for s in SOURCES], "-o", out + ".tmp", "-lssl", "-lcrypto", "-lpthread"]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)

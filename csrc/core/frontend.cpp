@@ -85,6 +85,7 @@ static void poke(int evfd) {
 Frontend::Frontend(const FrontendCfg& cfg, const CmqEngineApi* api) : cfg_(cfg), api_(api) {
   if (!api_ || api_->abi != CMQ_STEP_ABI) throw std::runtime_error("frontend: engine C API missing or ABI mismatch");
   c_max_ = api_->c_max;
+  held_cnt_.assign(c_max_, 0);
   if (cfg_.io_threads < 1) cfg_.io_threads = 1;
   if (!cfg_.max_slot || cfg_.max_slot > c_max_ - 2) cfg_.max_slot = c_max_ - 2;
   conns_.resize(c_max_);
@@ -827,6 +828,10 @@ void Frontend::finish_oldest(std::deque<Inflight>& inflight) {
   h.needs_commit = needs_commit;
   h.sc.co.assign(co, co + c_max_);
   h.sc.egress = api_->egress_host(api_->eng, slot);
+  if (needs_commit && api_->conn_conf) {
+    const u32* cf = api_->conn_conf(api_->eng, p);
+    h.conf.assign(cf, cf + c_max_);
+  }
   if (c.egress_bytes && !check(api_->egress_copy(api_->eng, p))) return;
   {
     std::lock_guard<std::mutex> g(stats_mu_);
@@ -963,13 +968,46 @@ bool Frontend::stash_pend(bool copy) {
   if (!pend_valid_) return true;
   pend_valid_ = false;
   if (pend_bytes_ && !check(api_->egress_wait_slot(api_->eng, pend_slot_))) return false;
-  const bool hold = pend_.needs_commit || !held_.empty();
-  if (hold || copy) {   // write-behind (or the slot may be reused before it is written): copy
+  if (!pend_.needs_commit && held_total_ == 0) {
+    if (copy) {   // the slot may be reused before it is written: copy
+      pend_.sc.own.assign((const char*)pend_.sc.egress, pend_bytes_);
+      pend_.sc.egress = nullptr;
+    }
+    out_.push_back(std::move(pend_.sc));
+    return true;
+  }
+  // write-behind: only the connections with publisher confirms in this step wait for the
+  // commit (deliveries need no durability), plus any connection that still has older
+  // held bytes (its stream stays in order)
+  Scatter now;
+  now.co.assign(c_max_, ConnOut{0, 0});
+  bool now_any = false, held_any = false;
+  for (u32 c = 0; c < c_max_; ++c) {
+    if (!pend_.sc.co[c].len) continue;
+    const bool gated = pend_.needs_commit && (pend_.conf.empty() || pend_.conf[c] != 0);
+    if (gated || held_cnt_[c]) {
+      ++held_cnt_[c];
+      ++held_total_;
+      held_any = true;
+    } else {
+      now.co[c] = pend_.sc.co[c];
+      pend_.sc.co[c].len = 0;
+      now_any = true;
+    }
+  }
+  if (now_any) {
+    now.egress = pend_.sc.egress;
+    if (copy) {
+      now.own.assign((const char*)pend_.sc.egress, pend_bytes_);
+      now.egress = nullptr;
+    }
+    out_.push_back(std::move(now));
+  }
+  if (held_any) {
     pend_.sc.own.assign((const char*)pend_.sc.egress, pend_bytes_);
     pend_.sc.egress = nullptr;
+    held_.push_back(std::move(pend_));
   }
-  if (hold) held_.push_back(std::move(pend_));
-  else out_.push_back(std::move(pend_.sc));
   return true;
 }
 
@@ -977,7 +1015,10 @@ bool Frontend::collect_scatter(std::vector<Scatter*>& scat) {
   if (!stash_pend(false)) return false;
   const u64 rel = released_.load();
   while (!held_.empty() && (!held_.front().needs_commit || held_.front().step <= rel)) {
-    out_.push_back(std::move(held_.front().sc));
+    Scatter& sc = held_.front().sc;
+    for (u32 c = 0; c < c_max_; ++c)
+      if (sc.co[c].len) { --held_cnt_[c]; --held_total_; }
+    out_.push_back(std::move(sc));
     held_.pop_front();
   }
   for (auto& sc : out_) scat.push_back(&sc);
@@ -1078,6 +1119,7 @@ EchoEngine::EchoEngine(u32 c_max, u32 seg_max, u64 ingress_cap, u32 carry_cap) {
   api_.egress_host = [](void* e, int slot) -> const u8* { return (const u8*)((EchoEngine*)e)->slot_[slot].data(); };
   api_.persist_host = [](void*, int) -> const u8* { return nullptr; };
   api_.grow_host = [](void*, int) -> const RingMove* { return nullptr; };
+  api_.conn_conf = nullptr;   // every connection's egress is commit-gated
   api_.consumed_host = [](void*, int) -> const ConsumedRec* { return nullptr; };
 }
 

@@ -126,7 +126,9 @@ class Frontend {
     std::vector<ConnOut> co;
     std::string own;         // held copy (persistence) or host-run step
   };
-  struct Held { u64 step; bool needs_commit; Scatter sc; };
+  // needs_commit: the step's store records must commit before the confirm-gated part of
+  // its egress leaves; conf = that step's confirm bytes per connection (empty = all gated)
+  struct Held { u64 step; bool needs_commit; Scatter sc; std::vector<u32> conf; };
 
   void stepper();
   void io_loop(int i);
@@ -199,6 +201,8 @@ class Frontend {
 
   // persistence write-behind
   std::deque<Held> held_;
+  std::vector<u32> held_cnt_;   // per connection: held entries carrying its bytes (keeps its order)
+  u64 held_total_ = 0;
   PersistWorker* persist_ = nullptr;
   std::atomic<u64> released_{0};
   bool have_released_ = false;

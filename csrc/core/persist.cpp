@@ -37,12 +37,19 @@ void PersistWorker::stop() {
 void PersistWorker::set_queue(u32 slot, const std::string& qid) {
   std::lock_guard<std::mutex> g(qid_mu_);
   if (slot >= qid_.size()) qid_.resize(slot + 1);
+  if (!qid_[slot].empty()) slot_of_.erase(qid_[slot]);
+  if (qid.empty() || qid != qid_[slot])   // slot freed / reused: its old rows are gone
+    for (auto it = rows_by_.begin(); it != rows_by_.end();)
+      it = it->first.q == slot ? rows_by_.erase(it) : std::next(it);
   qid_[slot] = qid;
+  if (!qid.empty()) slot_of_[qid] = slot;
 }
 
 void PersistWorker::seed_row(const std::string& qid, i64 msgid, i64 offset, i32 size, bool unack, int refs) {
   std::lock_guard<std::mutex> g(qid_mu_);
-  rows_by_[{qid, msgid}] = Row{offset, size, unack};
+  auto it = slot_of_.find(qid);
+  if (it == slot_of_.end()) return;
+  rows_by_[RowKey{it->second, msgid}] = Row{offset, size, unack};
   refs_[msgid] = refs;
 }
 
@@ -77,6 +84,7 @@ void PersistWorker::loop() {
         apply(b);
         if (b.step > top) top = b.step;
       }
+      flush_born();   // rows that outlived the group (their batches are still alive here)
     }
     st_->sync();   // group commit: one fsync for every batch that was waiting
     ++commits_;
@@ -89,7 +97,7 @@ void PersistWorker::loop() {
 }
 
 void PersistWorker::apply(const Batch& b) {
-  // ---- enqueues of persistent messages into durable queues
+  // ---- enqueues of persistent messages into durable queues: held as this group's rows
   const u8* p = (const u8*)b.persist.data();
   size_t off = 0, n = b.persist.size();
   while (off + sizeof(PersistHdr) <= n) {
@@ -98,28 +106,19 @@ void PersistWorker::apply(const Batch& b) {
     if (h.size < sizeof(PersistHdr) || off + h.size > n) break;
     const char* d = (const char*)p + off + sizeof(PersistHdr);
     off += h.size;
-    const std::string& qid = h.q < qid_.size() ? qid_[h.q] : std::string();
-    if (qid.empty()) continue;
-    int& refs = refs_[h.msg_id];
-    if (refs == 0) {
-      MsgRow m;
-      m.id = h.msg_id;
-      m.tstamp = h.ts_ms;
-      m.exchange.assign(d, h.ex_len);
-      m.routing.assign(d + h.ex_len, h.rk_len);
-      m.header = std::string(2, '\0') + be64(h.body_len);   // weight u16 | body size u64 | props
-      m.header.append(d + h.ex_len + h.rk_len, h.props_len);
-      m.body.assign(d + h.ex_len + h.rk_len + h.props_len, h.body_len);
-      m.durable = true;
-      m.refer = 1;
-      st_->insertMessage(std::move(m), 0);
-      bytes_ += h.body_len;
-    } else {
-      st_->updateMessageReferCount(h.msg_id, refs + 1);
+    if (h.q >= qid_.size() || qid_[h.q].empty()) continue;
+    auto rf = refs_.find(h.msg_id);
+    if (rf != refs_.end()) {   // a message already in the store gains a queue row
+      st_->updateMessageReferCount(h.msg_id, ++rf->second);
+      st_->insertQueueMsg(qid_[h.q], (i64)h.qpos, h.msg_id, (i32)h.body_len, 0);
+      rows_by_[RowKey{h.q, h.msg_id}] = Row{(i64)h.qpos, (i32)h.body_len, false};
+      ++rows_;
+      continue;
     }
-    ++refs;
-    st_->insertQueueMsg(qid, (i64)h.qpos, h.msg_id, (i32)h.body_len, 0);
-    rows_by_[{qid, h.msg_id}] = Row{(i64)h.qpos, (i32)h.body_len, false};
+    auto& bm = born_msg_[h.msg_id];
+    if (bm.refs == 0) { bm.d = d; bm.h = h; }
+    ++bm.refs;
+    born_[RowKey{h.q, h.msg_id}] = Born{d, h, false};
     ++rows_;
   }
   // ---- state changes: 0 consumed/acked, 1 expired, 2 dropped, 3 delivered awaiting ack, 4 requeued
@@ -127,9 +126,21 @@ void PersistWorker::apply(const Batch& b) {
   for (size_t k = 0; k < nc; ++k) {
     ConsumedRec r;
     memcpy(&r, b.consumed.data() + k * sizeof(ConsumedRec), sizeof r);
-    const std::string& qid = r.q < qid_.size() ? qid_[r.q] : std::string();
-    if (qid.empty()) continue;
-    auto it = rows_by_.find({qid, r.msg_id});
+    if (r.q >= qid_.size() || qid_[r.q].empty()) continue;
+    const RowKey key{r.q, r.msg_id};
+    auto bi = born_.find(key);
+    if (bi != born_.end()) {   // the row never reached the store: update it in memory
+      if (r.kind == 3) bi->second.unack = true;
+      else if (r.kind == 4) bi->second.unack = false;
+      else {
+        born_.erase(bi);
+        auto bm = born_msg_.find(r.msg_id);
+        if (bm != born_msg_.end() && --bm->second.refs <= 0) born_msg_.erase(bm);
+      }
+      continue;
+    }
+    const std::string& qid = qid_[r.q];
+    auto it = rows_by_.find(key);
     if (it == rows_by_.end()) continue;
     Row& row = it->second;
     if (r.kind == 3) {
@@ -161,6 +172,36 @@ void PersistWorker::apply(const Batch& b) {
       st_->updateMessageReferCount(r.msg_id, left);
     }
   }
+}
+
+// the group's surviving messages and rows go to the store (before its one fsync)
+void PersistWorker::flush_born() {
+  for (auto& kv : born_msg_) {
+    const PersistHdr& h = kv.second.h;
+    const char* d = kv.second.d;
+    MsgRow m;
+    m.id = h.msg_id;
+    m.tstamp = h.ts_ms;
+    m.exchange.assign(d, h.ex_len);
+    m.routing.assign(d + h.ex_len, h.rk_len);
+    m.header = std::string(2, '\0') + be64(h.body_len);   // weight u16 | body size u64 | props
+    m.header.append(d + h.ex_len + h.rk_len, h.props_len);
+    m.body.assign(d + h.ex_len + h.rk_len + h.props_len, h.body_len);
+    m.durable = true;
+    m.refer = kv.second.refs;
+    st_->insertMessage(std::move(m), 0);
+    refs_[h.msg_id] = kv.second.refs;
+    bytes_ += h.body_len;
+  }
+  for (auto& kv : born_) {
+    const PersistHdr& h = kv.second.h;
+    const std::string& qid = qid_[h.q];
+    if (kv.second.unack) st_->insertQueueUnack(qid, (i64)h.qpos, h.msg_id, (i32)h.body_len);
+    else st_->insertQueueMsg(qid, (i64)h.qpos, h.msg_id, (i32)h.body_len, 0);
+    rows_by_[kv.first] = Row{(i64)h.qpos, (i32)h.body_len, kv.second.unack};
+  }
+  born_.clear();
+  born_msg_.clear();
 }
 
 }  // namespace cmq

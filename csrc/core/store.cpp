@@ -9,7 +9,7 @@
 #include <cstring>
 #include <stdexcept>
 
-#include <zlib.h>
+#include <nmmintrin.h>
 
 #include "codec.hpp"
 
@@ -22,9 +22,22 @@ enum Op : uint8_t {
   OP_BIND_DEL_Q, OP_X_DEL, OP_VH_INS, OP_VH_DEL, OP_QMSG_DEL
 };
 
-// CRC-32 (reflected 0xEDB88320, init/xorout 0xFFFFFFFF): zlib's, so the WAL format is
-// unchanged from the round-1 table-driven version and the check runs at memory speed
-uint32_t crc32(const char* p, size_t n) { return (uint32_t)::crc32(0L, (const Bytef*)p, (uInt)n); }
+// CRC-32C (Castagnoli, init/xorout 0xFFFFFFFF) on the SSE4.2 crc32 instruction: the
+// record check is on the persistence hot path (every 4 KB message body of BASELINE
+// config 4), where zlib's table-driven CRC-32 ran at < 1 GB/s
+__attribute__((target("sse4.2"))) uint32_t crc32(const char* p, size_t n) {
+  uint64_t c = 0xFFFFFFFFu;
+  while (n >= 8) {
+    uint64_t v;
+    memcpy(&v, p, 8);
+    c = _mm_crc32_u64(c, v);
+    p += 8;
+    n -= 8;
+  }
+  uint32_t c32 = (uint32_t)c;
+  while (n--) c32 = _mm_crc32_u8(c32, (uint8_t)*p++);
+  return c32 ^ 0xFFFFFFFFu;
+}
 uint32_t crc32(const std::string& s) { return crc32(s.data(), s.size()); }
 
 void w_map(Writer& w, const std::map<std::string, std::string>& m) {
@@ -319,6 +332,7 @@ void Store::insertMessage(const MsgRow& m, int64_t ttl_ms) {
 void Store::insertMessage(MsgRow&& m, int64_t ttl_ms) {
   LOCK;
   Writer w;
+  w.b.reserve(64 + m.header.size() + m.body.size() + m.exchange.size() + m.routing.size());
   const int64_t now = now_ms();
   w.llng((u64)m.id); w.llng((u64)m.tstamp); w.longstr(m.header); w.longstr(m.body); w.longstr(m.exchange);
   w.longstr(m.routing); w.octet(m.durable); w.lng((u32)m.refer);

@@ -310,55 +310,50 @@ DEV bool topic_match(const u8* pat, u32 plen, const u8* key, u32 klen, bool hash
 }
 
 // ============================================================================ K0 prep + stage
-// one block of 1024: zero step counters, lay out work segments (16-aligned)
-__global__ __launch_bounds__(1024) void k_prep(DS d) {
-  __shared__ u32 lds[1024 / 64 + 1];
-  u32 tid = threadIdx.x;
-  u32 nseg = d.in->nseg;
-  if (tid < sizeof(Counters) / 4) {
-    u32* c = (u32*)d.ctr;
-    if (tid * 4 < offsetof(Counters, log_head)) c[tid] = 0;
-    if (tid == 0) { d.ctr->n_grow = 0; d.tot[TS_NMOVE] = 0; d.tot[TS_NDEFER] = 0; }
-  }
-  u32 running = 0;
-  for (u32 base = 0; base < d.seg_max; base += 1024) {
-    u32 s = base + tid;
-    u32 tot = 0;
-    if (s < nseg) {
-      u32 conn = d.segs[s].conn;
-      tot = d.carry_len[conn] + d.segs[s].len;
-      d.seg_total[s] = tot;
-    }
-    u32 sz = s < nseg ? align16(tot + 32) : 0;
-    u32 all;
-    u32 off = block_scan<1024>(sz, lds, all);
-    if (s < nseg) d.seg_start[s] = running + off;
-    running += all;
-    if (base + 1024 >= nseg) break;
-  }
-  if (tid == 0) {
-    *d.egress_budget = 0;
-    d.tot[15] = running;  // work bytes used
-    // snowflake virtual position base for this step (ID_SLOT_BITS slots per wall-clock ms)
-    u64 floor_pos = d.in->id_ms << ID_SLOT_BITS;
-    u64 cur = *d.id_next;
-    *d.id_next = cur > floor_pos ? cur : floor_pos;
-  }
-}
-
-// grid (seg_max, 8): copy carry then new bytes into the work segment
+// grid (seg_max, 4): copy carry then new bytes into the work segment.  Fused k_prep: every
+// block derives its segment's work offset (prefix of the 16-aligned slot sizes of the
+// segments before it) itself, and block (0, 0) resets the step counters
 __global__ __launch_bounds__(256) void k_stage(DS d) {
-  u32 s = blockIdx.x;
-  if (s >= d.in->nseg) return;
-  if (d.tot[15] > d.work_cap) return;  // host sizes steps so this never triggers
-  u32 conn = d.segs[s].conn;
-  u32 cl = d.carry_len[conn];
-  u32 len = d.segs[s].len;
-  u8* dst = d.work + d.seg_start[s];
+  __shared__ u32 lds[256 / 64 + 1];
+  const u32 s = blockIdx.x, tid = threadIdx.x;
+  const u32 nseg = d.in->nseg;
+  const bool head = s == 0 && blockIdx.y == 0;
+  if (head) {
+    u32* c = (u32*)d.ctr;
+    for (u32 k = tid; k < sizeof(Counters) / 4; k += 256)
+      if (k * 4 < offsetof(Counters, log_head)) c[k] = 0;
+    if (tid == 0) {
+      d.ctr->n_grow = 0; d.tot[TS_NMOVE] = 0; d.tot[TS_NDEFER] = 0;
+      *d.egress_budget = 0;
+      // snowflake virtual position base for this step (ID_SLOT_BITS slots per wall-clock ms)
+      u64 floor_pos = d.in->id_ms << ID_SLOT_BITS;
+      u64 cur = *d.id_next;
+      *d.id_next = cur > floor_pos ? cur : floor_pos;
+    }
+  }
+  if (s >= nseg && !head) return;
+  u32 before = 0, total = 0;
+  for (u32 k = tid; k < nseg; k += 256) {
+    const u32 sz = align16(d.carry_len[d.segs[k].conn] + d.segs[k].len + 32);
+    total += sz;
+    before += k < s ? sz : 0u;
+  }
+  u32 all_b, all_t;
+  block_scan<256>(before, lds, all_b);
+  __syncthreads();
+  block_scan<256>(total, lds, all_t);
+  if (head && tid == 0) d.tot[15] = all_t;  // work bytes used
+  if (s >= nseg) return;
+  const u32 conn = d.segs[s].conn;
+  const u32 cl = d.carry_len[conn];
+  const u32 len = d.segs[s].len;
+  if (blockIdx.y == 0 && tid == 0) { d.seg_total[s] = cl + len; d.seg_start[s] = all_b; }
+  if (all_t > d.work_cap) return;  // host sizes steps so this never triggers
+  u8* dst = d.work + all_b;
   u32 part = blockIdx.y, nparts = gridDim.y;
-  u32 tid = threadIdx.x + part * 256, nt = 256 * nparts;
-  if (cl) block_copy(dst, d.carry + (u64)conn * d.carry_cap, cl, tid, nt);
-  if (len) block_copy(dst + cl, d.ingress + d.segs[s].src, len, tid, nt);
+  u32 t = tid + part * 256, nt = 256 * nparts;
+  if (cl) block_copy(dst, d.carry + (u64)conn * d.carry_cap, cl, t, nt);
+  if (len) block_copy(dst + cl, d.ingress + d.segs[s].src, len, t, nt);
 }
 
 // ============================================================================ K1 frame scan
@@ -392,28 +387,27 @@ DEV i32 chan_lookup(const DS& d, u32 conn, u32 ch) {
   return -1;
 }
 
-// chip-wide candidate screen: one u16 mask per 16 work bytes; bit j set when byte j
-// looks like a frame header (type 1/2/3/8, size within the broker frame-max)
-__global__ __launch_bounds__(256) void k_cand(DS d) {
-  const u64 used = d.tot[15];
-  const u64 nch = (used + 15) >> 4;
-  const u32 fm = d.frame_max_global;
-  for (u64 c = (u64)blockIdx.x * 256 + threadIdx.x; c < nch; c += (u64)gridDim.x * 256) {
-    const uint4* q = (const uint4*)(d.work + c * 16);
-    uint4 A = q[0], B = q[1];
-    u32 w[8] = {A.x, A.y, A.z, A.w, B.x, B.y, B.z, B.w};
-    u32 m = 0;
+// candidate screen: one u16 mask per 16 work bytes; bit j set when byte j looks like a
+// frame header (type 1/2/3/8, size within the broker frame-max).  Reads 32 bytes (the
+// header of a frame starting at byte 15 ends in the next word); segments are padded
+// by >= 32 bytes in the work buffer
+DEV u32 cand_bits(uint4 A, uint4 B, u32 fm) {
+  u32 w[8] = {A.x, A.y, A.z, A.w, B.x, B.y, B.z, B.w};
+  u32 m = 0;
 #pragma unroll
-    for (int j = 0; j < 16; ++j) {
+  for (int j = 0; j < 16; ++j) {
 #define BYTE(k) ((w[(k) >> 2] >> (8 * ((k) & 3))) & 255u)
-      u32 t = BYTE(j);
-      u32 sz = (BYTE(j + 3) << 24) | (BYTE(j + 4) << 16) | (BYTE(j + 5) << 8) | BYTE(j + 6);
+    u32 t = BYTE(j);
+    u32 sz = (BYTE(j + 3) << 24) | (BYTE(j + 4) << 16) | (BYTE(j + 5) << 8) | BYTE(j + 6);
 #undef BYTE
-      bool ok = (t == 1 || t == 2 || t == 3 || t == 8) && (fm == 0 || sz <= fm - 8);
-      m |= (ok ? 1u : 0u) << j;
-    }
-    d.cmask[c] = (u16)m;
+    bool ok = (t == 1 || t == 2 || t == 3 || t == 8) && (fm == 0 || sz <= fm - 8);
+    m |= (ok ? 1u : 0u) << j;
   }
+  return m;
+}
+DEV u32 cand_word(const u8* w16, u32 fm) {
+  const uint4* q = (const uint4*)w16;
+  return cand_bits(q[0], q[1], fm);
 }
 
 #define FS_MARK(k) \
@@ -428,6 +422,9 @@ __global__ __launch_bounds__(256) void k_frame_scan(DS d) {
   u16* const chain = chain_am;
   u16* const amask = chain_am;
   __shared__ u8 claim[CAND_MAX];
+  // per 16-byte word with exactly one accepted candidate: its frame end | complete << 31
+  // (phase b reuses it instead of re-reading the header from memory); ~0u = recompute
+  __shared__ u32 wend[FS_AM_MAX];
   __shared__ u32 sc[8];
   __shared__ u32 sh_m, sh_over, sh_ok, sh_nf, sh_stop, sh_brk;
   __shared__ u32 sh_cmd_base, sh_frag_base, sh_ncmd;
@@ -467,7 +464,6 @@ __global__ __launch_bounds__(256) void k_frame_scan(DS d) {
   // validate against the connection's frame-max / end marker, append the trailing
   // positions that can only hold a partial header
   {
-    const u32 m0 = d.seg_start[s] >> 4;
     const u32 nm = (L + 15) >> 4;
     const u32 per = (nm + 255) >> 8;
     const u32 c0 = tid * per;
@@ -477,24 +473,51 @@ __global__ __launch_bounds__(256) void k_frame_scan(DS d) {
     // pass 2 only emits positions instead of re-reading every frame header from HBM;
     // segments longer than FS_AM_MAX mask words fall back to re-validating
     const bool use_am = nm <= FS_AM_MAX;
+    const u32 fmg = d.frame_max_global;
+    if (use_am) {   // candidate screen of the segment into LDS (fused k_cand), coalesced reads
+      const uint4* W = (const uint4*)b;   // 16-aligned; >= 32 bytes of padding after the segment
+      for (u32 c0 = tid; c0 < nm; c0 += 256 * 8) {
+        uint4 x[8], y[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {   // every load of the batch in flight before any use
+          const u32 c = c0 + k * 256;
+          if (c < nm) { x[k] = W[c]; y[k] = W[c + 1]; }
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const u32 c = c0 + k * 256;
+          if (c < nm) amask[c] = (u16)cand_bits(x[k], y[k], fmg);
+        }
+      }
+      __syncthreads();
+    }
     u32 cnt = 0;
     for (u32 c = c0; c < c1; ++c) {
-      u32 mk = d.cmask[m0 + c];
-      u32 acc = 0;
+      u32 mk = use_am ? (u32)amask[c] : cand_word(b + c * 16, fmg);
+      u32 acc = 0, we = ~0u, na = 0;
       while (mk) {
         u32 j = __ffs(mk) - 1;
         mk &= mk - 1;
         u32 p = c * 16 + j;
         if (p >= lim) break;
         FInfo f = frame_at(b, p, L, fmax);
-        if (f.valid_hdr && (f.complete || (u64)p + 8 + f.size > L)) { ++cnt; acc |= 1u << j; }
+        if (f.valid_hdr && (f.complete || (u64)p + 8 + f.size > L)) {
+          ++cnt;
+          acc |= 1u << j;
+          const u64 e64 = (u64)p + 8 + f.size;
+          we = e64 < 0x7fffffffull ? ((f.complete ? 0x80000000u : 0u) | (u32)e64) : ~0u;
+          ++na;
+        }
       }
-      if (use_am) amask[c] = (u16)acc;
+      if (use_am) {
+        amask[c] = (u16)acc;
+        wend[c] = na == 1 ? we : ~0u;
+      }
     }
     u32 tot;
     u32 off = block_scan<256>(cnt, sc, tot);
     for (u32 c = c0; c < c1; ++c) {
-      u32 mk = use_am ? (u32)amask[c] : (u32)d.cmask[m0 + c];
+      u32 mk = use_am ? (u32)amask[c] : cand_word(b + c * 16, fmg);
       while (mk) {
         u32 j = __ffs(mk) - 1;
         mk &= mk - 1;
@@ -528,13 +551,23 @@ __global__ __launch_bounds__(256) void k_frame_scan(DS d) {
   const bool over = sh_over != 0;
 
   // ---- (b) successor of every candidate (-1 exact end, -2 partial/unknown, -3 broken)
+  const bool use_we = ((L + 15) >> 4) <= FS_AM_MAX;
   for (u32 i = tid; i < m; i += 256) {
     u32 p = cpos[i];
-    FInfo f = frame_at(b, p, L, fmax);
+    bool complete;
+    u32 e;
+    const u32 we = use_we && p < (L >= 7 ? L - 6 : 0) ? wend[p >> 4] : ~0u;
+    if (we != ~0u) {
+      complete = (we >> 31) != 0;
+      e = we & 0x7fffffffu;
+    } else {
+      FInfo f = frame_at(b, p, L, fmax);
+      complete = f.complete;
+      e = p + 8 + f.size;
+    }
     i32 sx;
-    if (!f.complete) sx = -2;
+    if (!complete) sx = -2;
     else {
-      u32 e = p + 8 + f.size;
       if (e == L) sx = -1;
       else {
         u32 lo = i + 1, hi = m;  // successor lies strictly after i
@@ -812,16 +845,6 @@ __global__ __launch_bounds__(256) void k_frame_scan(DS d) {
 }
 
 // ============================================================================ K3 classify / decode
-__global__ void k_classify(DS d) {
-  u32 i = blockIdx.x * blockDim.x + threadIdx.x;
-  u32 n = d.ctr->n_cmds;
-  if (n > d.cmd_max) n = d.cmd_max;
-  if (i >= d.cmd_max) return;
-  u32 k = i < n ? d.cmds[i].kind : CK_NONE;
-  d.cmd_is_pub[i] = (k == CK_PUBLISH);
-  d.cmd_is_ack[i] = (k == CK_ACK || k == CK_NACK || k == CK_REJECT);
-}
-
 DEV void set_counts(const DS& d) {
   u32 np = d.tot[4], na = d.tot[5];
   d.ctr->n_pubs = np < d.pub_max ? np : d.pub_max;
@@ -832,11 +855,6 @@ DEV void set_counts(const DS& d) {
   d.tot[TS_PAIR_BASE] = 0;
   d.tot[TS_PAIR_N] = 0;
   d.tot[TS_NIMPORT] = 0;
-}
-__global__ void k_set_counts(DS d) { if (threadIdx.x == 0) set_counts(d); }
-
-__global__ void k_reset_dirty(DS d) {
-  if (threadIdx.x == 0) *d.n_dirty = 0;
 }
 
 DEV bool skip_shortstr(const u8* p, u32& o, u32 end) {
@@ -1081,28 +1099,45 @@ __global__ __launch_bounds__(1024) void k_scan(ScanArgs a, u32* tot, u64* status
       agg[k] = all;
       __syncthreads();
     }
-    if (tid < a.narr) {
-      const u32 k = tid;
-      u32 A = tid == 0 ? agg[0] : tid == 1 ? agg[1] : tid == 2 ? agg[2] : agg[3];
+    // look-back, one wave per array: the wave's 64 lanes read the 64 preceding tiles'
+    // status words at once, so a tile waits one round trip for all its (concurrently
+    // running) predecessors instead of a chain of them
+    const u32 wv = tid >> 6, lane = tid & 63;
+    if (wv < a.narr) {
+      const u32 k = wv;
+      u32 A = k == 0 ? agg[0] : k == 1 ? agg[1] : k == 2 ? agg[2] : agg[3];
       // agent-scope acquire/release: the tiles run on different XCDs (separate L2s)
       u64* st = status + (u64)k * smax;
       const u64 tag = (u64)epoch << 34;
       u32 excl = 0;
       if (tile > 0) {
-        __hip_atomic_store(&st[tile], tag | (1ull << 32) | A, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-        for (u32 j = tile; j > 0;) {
-          --j;
-          u64 w;
-          do {
-            w = __hip_atomic_load(&st[j], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
-          } while ((w >> 34) != epoch || ((w >> 32) & 3) == 0);
-          excl += (u32)w;
-          if (((w >> 32) & 3) == 2) break;
+        if (lane == 0)
+          __hip_atomic_store(&st[tile], tag | (1ull << 32) | A, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        u32 top = tile;   // predecessors [0, top) not yet summed
+        while (top > 0) {
+          const bool has = lane < top;
+          const u32 j = has ? top - 1 - lane : 0;   // lane 0 = nearest predecessor
+          u64 w = 0;
+          if (has) {
+            do {
+              w = __hip_atomic_load(&st[j], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+            } while ((w >> 34) != epoch || ((w >> 32) & 3) == 0);
+          }
+          const u64 incl = __ballot(has && ((w >> 32) & 3) == 2);
+          // sum lanes up to (and including) the nearest inclusive prefix, or the window
+          const u32 last = incl ? (u32)(__ffsll((unsigned long long)incl) - 1) : 63u;
+          u32 v = (has && lane <= last) ? (u32)w : 0u;
+          for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+          excl += v;
+          if (incl) break;
+          top = top > 64 ? top - 64 : 0;
         }
       }
-      __hip_atomic_store(&st[tile], tag | (2ull << 32) | (excl + A), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-      s_excl[k] = excl;
-      if (base + SCAN_TILE >= n) tot[a.tot_slot + k] = excl + A;   // the last data tile
+      if (lane == 0) {
+        __hip_atomic_store(&st[tile], tag | (2ull << 32) | (excl + A), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        s_excl[k] = excl;
+        if (base + SCAN_TILE >= n) tot[a.tot_slot + k] = excl + A;   // the last data tile
+      }
     }
     __syncthreads();
 #pragma unroll
@@ -1128,31 +1163,10 @@ __global__ __launch_bounds__(1024) void k_scan(ScanArgs a, u32* tot, u64* status
 
 // ============================================================================ radix sort
 // stable LSD radix sort of (key, val) u32 pairs, 8 bits per pass; n from device.
-__global__ __launch_bounds__(256) void k_rs_hist(const u32* keys, const u32* np, u32 shift, u32* hist,
-                                                 u32 ntiles) {
-  __shared__ u32 cnt[256];
-  u32 tid = threadIdx.x, t = blockIdx.x;
-  cnt[tid] = 0;
-  __syncthreads();
-  u32 n = *np;
-  u32 base = t * SORT_TILE;
-  if (base < n) {
-    for (u32 j = 0; j < SORT_TILE / 256; ++j) {
-      u32 i = base + j * 256 + tid;
-      if (i < n) atomicAdd(&cnt[(keys[i] >> shift) & 255], 1u);
-    }
-  }
-  __syncthreads();
-  hist[tid * ntiles + t] = cnt[tid];
-}
-
-// digit-major offsets for the occupied tiles only: one thread per digit
-__global__ __launch_bounds__(256) void k_rs_offsets(const u32* hist, u32* hscan, const u32* np, u32 ntiles) {
-  __shared__ u32 lds[256 / 64 + 1];
-  u32 n = *np;
-  u32 T = (n + SORT_TILE - 1) / SORT_TILE;
-  if (T > ntiles) T = ntiles;
-  u32 dg = threadIdx.x;
+// per-tile digit histograms; the last occupied tile to finish turns them into the
+// digit-major offsets of the occupied tiles (fused k_rs_offsets: one launch less per pass)
+DEV void rs_offsets(const u32* hist, u32* hscan, u32 T, u32 ntiles, u32* lds) {
+  const u32 dg = threadIdx.x;
   u32 sum = 0;
   for (u32 t = 0; t < T; ++t) sum += hist[dg * ntiles + t];
   u32 all;
@@ -1162,6 +1176,35 @@ __global__ __launch_bounds__(256) void k_rs_offsets(const u32* hist, u32* hscan,
     hscan[dg * ntiles + t] = run;
     run += h;
   }
+}
+
+__global__ __launch_bounds__(256) void k_rs_hist(const u32* keys, const u32* np, u32 shift, u32* hist,
+                                                 u32* hscan, u32* ticket, u32 ntiles) {
+  __shared__ u32 cnt[256];
+  __shared__ u32 lds[256 / 64 + 1];
+  __shared__ u32 s_last;
+  u32 tid = threadIdx.x, t = blockIdx.x;
+  u32 n = *np;
+  u32 T = (n + SORT_TILE - 1) / SORT_TILE;
+  if (T > ntiles) T = ntiles;
+  if (t >= T) return;   // only occupied tiles take part (and take a ticket)
+  cnt[tid] = 0;
+  __syncthreads();
+  u32 base = t * SORT_TILE;
+  for (u32 j = 0; j < SORT_TILE / 256; ++j) {
+    u32 i = base + j * 256 + tid;
+    if (i < n) atomicAdd(&cnt[(keys[i] >> shift) & 255], 1u);
+  }
+  __syncthreads();
+  hist[tid * ntiles + t] = cnt[tid];
+  __threadfence();
+  __syncthreads();
+  if (tid == 0) s_last = atomicAdd(ticket, 1u) == T - 1;
+  __syncthreads();
+  if (!s_last) return;
+  __threadfence();
+  if (tid == 0) *ticket = 0;
+  rs_offsets(hist, hscan, T, ntiles, lds);
 }
 
 __global__ __launch_bounds__(256) void k_rs_scatter(const u32* kin, const u32* vin, u32* kout, u32* vout,
@@ -1535,7 +1578,6 @@ DEV void live_add_blocks(const DS& d, u32 lane) {
     }
   }
 }
-__global__ void k_log_reserve(DS d) { if (threadIdx.x == 0) log_reserve(d); }
 
 // one wave per publish: allocate, fill MsgEnt, copy exchange/rk/props/body into the log
 DEV void store_one(const DS& d, u32 p, u32 lane);
@@ -1608,25 +1650,6 @@ DEV void store_one(const DS& d, u32 p, u32 lane) {
       d.defer_free[atomicAdd(&d.tot[TS_NDEFER], 1u)] = msg;
     }
   }
-}
-
-// thread per publish: account stored bytes per log block (one atomic per block per wave)
-__global__ void k_live_add(DS d) {
-  u32 p = d.tot[TS_RANGE_LO] + blockIdx.x * blockDim.x + threadIdx.x;
-  u32 n = d.tot[TS_RANGE_HI];
-  if (n > d.pub_cap) n = d.pub_cap;
-  u64 base = *d.log_step_base;
-  bool valid = p < n && base != INVALID && d.pub_nq[p] > 0;
-  u64 blk = 0;
-  i64 sb = 0;
-  if (valid) {
-    u64 off = base + d.pub_slot_off[p];
-    blk = (off / d.log_block) % d.n_log_blocks;
-    sb = d.pub_slot[p];
-  }
-  wave_add_i64(d.log_live, blk, sb, valid);
-  i64 tot = wave_sum64(valid ? sb : 0);
-  if (lane_id() == 0 && tot) atomicAdd((unsigned long long*)d.live_bytes, (unsigned long long)tot);
 }
 
 // ============================================================================ sharded queues
@@ -1843,10 +1866,7 @@ DEV u32 enqueue_one(const DS& d, u32 src, u32 i, u32 n, PersistRec* pr, u32 hs_n
 // ring pool (one bump pointer shared with the host's allocator), within the queue's
 // max_capacity.  Positions stay absolute (entry pos lives at off + (pos & mask)), so
 // unacked windows, requeues and store rows keep their queue offsets.
-__global__ void k_ring_plan(DS d, u32 src, u32 hs_ntiles) {
-  const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
-  const u32 n = d.tot[TS_PAIR_N];
-  if (i >= n) return;
+DEV void ring_plan_one(const DS& d, u32 src, u32 hs_ntiles, u32 i, u32 n) {
   const u32* kk = d.pair_k[src];
   const u32 rb = d.rank_bits;
   const u32 q = kk[i] >> rb;
@@ -1883,13 +1903,26 @@ __global__ void k_ring_plan(DS d, u32 src, u32 hs_ntiles) {
   if (gi < GROW_MAX) d.grow_h[gi] = mv;
 }
 
-// copy every moved ring's live entries (all blocks stride over each move in turn)
-__global__ __launch_bounds__(256) void k_ring_moves(DS d) {
+// the last (occupied) block to finish copies every moved ring's live entries (fused
+// k_ring_moves: growth is rare, so one block does it and the common step saves a launch)
+__global__ __launch_bounds__(256) void k_ring_plan(DS d, u32 src, u32 hs_ntiles) {
+  __shared__ u32 s_last;
+  const u32 n = d.tot[TS_PAIR_N];
+  const u32 nb = (n + 255) / 256;
+  if (blockIdx.x >= nb) return;
+  const u32 i = blockIdx.x * 256 + threadIdx.x;
+  if (i < n) ring_plan_one(d, src, hs_ntiles, i, n);
+  __threadfence();
+  __syncthreads();
+  if (threadIdx.x == 0) s_last = atomicAdd(&d.tot[TS_RP_TICKET], 1u) == nb - 1;
+  __syncthreads();
+  if (!s_last) return;
+  __threadfence();
+  if (threadIdx.x == 0) d.tot[TS_RP_TICKET] = 0;
   const u32 nm = d.tot[TS_NMOVE];
-  const u64 g = (u64)blockIdx.x * blockDim.x + threadIdx.x, gs = (u64)gridDim.x * blockDim.x;
   for (u32 m = 0; m < nm; ++m) {
     const RingMove mv = d.moves[m];
-    for (u64 pos = mv.head + g; pos < mv.tail; pos += gs)
+    for (u64 pos = mv.head + threadIdx.x; pos < mv.tail; pos += 256)
       d.ring[mv.new_off + (pos & mv.new_mask)] = d.ring[mv.old_off + (pos & mv.old_mask)];
   }
 }
@@ -2374,6 +2407,27 @@ __global__ void k_conn_sizes(DS d) {
 #define CONN_LAYOUT_MAX 8192
 __global__ __launch_bounds__(1024) void k_conn_layout(DS d) {
   __shared__ u32 lds[1024 / 64 + 1];
+  // exclusive scan of the deliveries' rendered sizes (fused k_scan: one block walks the
+  // step's deliveries 4096 at a time, cheaper than a separate launch at these sizes)
+  {
+    u32 n = d.ctr->n_deliv;
+    if (n > d.deliv_max) n = d.deliv_max;
+    u32 acc = 0;
+    for (u32 b0 = 0; b0 < n; b0 += 4096) {
+      const u32 i = b0 + threadIdx.x * 4;
+      u32 v0 = i < n ? d.dv_size[i] : 0, v1 = i + 1 < n ? d.dv_size[i + 1] : 0;
+      u32 v2 = i + 2 < n ? d.dv_size[i + 2] : 0, v3 = i + 3 < n ? d.dv_size[i + 3] : 0;
+      u32 all;
+      const u32 o = acc + block_scan<1024>(v0 + v1 + v2 + v3, lds, all);
+      if (i < n) d.dv_off[i] = o;
+      if (i + 1 < n) d.dv_off[i + 1] = o + v0;
+      if (i + 2 < n) d.dv_off[i + 2] = o + v0 + v1;
+      if (i + 3 < n) d.dv_off[i + 3] = o + v0 + v1 + v2;
+      acc += all;
+    }
+    if (threadIdx.x == 0) d.tot[6] = acc;
+    __syncthreads();
+  }
   u32 run = 0;
   for (u32 b0 = 0; b0 < d.c_max; b0 += 1024) {
     const u32 c = b0 + threadIdx.x;
@@ -2427,8 +2481,9 @@ DEV u32 put_frame_hdr(u8* o, u32 type, u32 ch, u32 size) {
 }
 
 // one wave per delivery
-__global__ __launch_bounds__(256) void k_render_deliv(DS d) {
-  u32 i = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+DEV void render_deliv(const DS& d, u32 blk);
+DEV void render_deliv(const DS& d, u32 blk) {
+  u32 i = (blk * blockDim.x + threadIdx.x) >> 6;
   u32 lane = lane_id();
   u32 n = d.ctr->n_deliv;
   if (i >= n) return;
@@ -2573,20 +2628,29 @@ DEV void render_return(const DS& d, u32 i, u32 lane) {
 // blocks [0, RC_RET_BLOCKS): returns, grid-stride, one wave each; the rest: confirms,
 // one thread per connection
 #define RC_RET_BLOCKS 512
-__global__ __launch_bounds__(256) void k_render_rc(DS d) {
-  if (blockIdx.x >= RC_RET_BLOCKS) {
-    u32 c = (blockIdx.x - RC_RET_BLOCKS) * blockDim.x + threadIdx.x;
+DEV void render_rc(const DS& d, u32 blk);
+// one launch for all egress rendering: returns / confirms blocks first, then one wave per
+// delivery (the two write disjoint byte ranges of each connection's egress)
+__global__ __launch_bounds__(256) void k_render(DS d, u32 n_rc) {
+  if (blockIdx.x < n_rc) render_rc(d, blockIdx.x);
+  else render_deliv(d, blockIdx.x - n_rc);
+}
+DEV void render_rc(const DS& d, u32 blk) {
+  if (blk >= RC_RET_BLOCKS) {
+    u32 c = (blk - RC_RET_BLOCKS) * blockDim.x + threadIdx.x;
     if (c < d.c_max) render_confirms(d, c);
     return;
   }
   u32 n = d.ctr->n_returns;
   if (n > d.pub_max) n = d.pub_max;
   const u32 lane = lane_id();
-  for (u32 i = (blockIdx.x * blockDim.x + threadIdx.x) >> 6; i < n; i += RC_RET_BLOCKS * 4) render_return(d, i, lane);
+  for (u32 i = (blk * blockDim.x + threadIdx.x) >> 6; i < n; i += RC_RET_BLOCKS * 4) render_return(d, i, lane);
 }
 
 // ============================================================================ post / final
-__global__ void k_post(DS d) {
+// (a last-block ticket here to fold k_host_out in costs more than the launch it saves:
+// hundreds of blocks serialise on the ticket word)
+__global__ __launch_bounds__(256) void k_post(DS d) {
   u32 i = blockIdx.x * blockDim.x + threadIdx.x;
   u32 n = d.ctr->n_deliv;
   u32 msg = INVALID, q = 0;
@@ -2615,10 +2679,6 @@ __global__ void k_post(DS d) {
   }
 }
 
-__global__ void k_post2(DS d) {
-  u32 i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < d.c_max) { d.conn_ret_bytes[i] = 0; d.conn_ret_min[i] = INVALID; }
-}
 
 DEV void final_step(const DS& d) {
   // advance the log tail over fully released blocks (K11)
@@ -2639,7 +2699,6 @@ DEV void final_step(const DS& d) {
   c->live_bytes = *d.live_bytes;
   *d.ctr_host = *c;
 }
-__global__ void k_final(DS d) { if (threadIdx.x == 0) final_step(d); }
 
 // persistence: size + pack the step's persist records (header + message bytes) into the
 // host-mapped persist buffer; the host writes them to the store before it releases the
@@ -2704,13 +2763,17 @@ DEV void copy16(u8* dst, const u8* src, u64 n, u64 gtid, u64 gsz) {
   for (u64 i = (nv << 4) + gtid; i < n; i += gsz) dst[i] = src[i];
 }
 
-DEV void final_step(const DS& d);
+DEV void host_out_copies(const DS& d, u64 gtid, u64 gsz);
 __global__ __launch_bounds__(256) void k_host_out(DS d) {
   if (blockIdx.x == 0 && threadIdx.x == 0) final_step(d);   // log tail, counters -> host
-  const u64 gtid = blockIdx.x * blockDim.x + threadIdx.x, gsz = (u64)gridDim.x * blockDim.x;
+  host_out_copies(d, blockIdx.x * blockDim.x + threadIdx.x, (u64)gridDim.x * blockDim.x);
+}
+
+DEV void host_out_copies(const DS& d, u64 gtid, u64 gsz) {
   u32 nseg = d.in->nseg;
   copy16((u8*)d.seg_out_h, (const u8*)d.seg_out, (u64)nseg * sizeof(SegOut), gtid, gsz);
   copy16((u8*)d.conn_out_h, (const u8*)d.conn_out, (u64)d.c_max * sizeof(ConnOut), gtid, gsz);
+  copy16((u8*)d.conn_conf_h, (const u8*)d.conn_conf_bytes, (u64)d.c_max * 4, gtid, gsz);
   u32 nc = d.ctr->n_ctrl;
   if (nc > d.seg_max * 2) nc = d.seg_max * 2;
   copy16((u8*)d.ctrl_rec_h, (const u8*)d.ctrl_rec, (u64)nc * sizeof(CtrlRec), gtid, gsz);

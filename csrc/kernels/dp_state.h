@@ -27,6 +27,7 @@ enum : u32 {
   TS_RS_TICKET = 29,                    // k_rs_hist finished-block ticket (last block: offsets)
   TS_NMOVE = 30,                        // rings moved (grown) this step (k_ring_plan)
   TS_NDEFER = 31,                       // stored messages released at the end of the step
+  TS_RP_TICKET = 14,                    // k_ring_plan finished-block ticket (last block: ring moves)
   TS_XSCAN = 32                         // + 2*r: per-destination record / byte totals
 };
 
@@ -55,6 +56,7 @@ struct DS {
   u8* ctrl_h;
   CtrlRec* ctrl_rec_h;
   RingMove* grow_h;         // host-mapped: rings grown this step (the host reclaims the old ones)
+  u32* conn_conf_h;         // host-mapped: conn_conf_bytes of the step (confirm-gated connections)
   RingMove* moves;          // this step's ring moves (k_ring_plan -> k_ring_moves)
   u32* defer_free;          // [pub_cap] messages stored without a queue (pair table full): k_post frees
   u64* ring_top;            // ring pool bump pointer (shared with the host allocator)
@@ -81,7 +83,6 @@ struct DS {
   u32* seg_start;
   u32* seg_total;
   u8* work;
-  u16* cmask;               // candidate bitmask, one u16 per 16 work bytes
 
   // ---------------- commands
   Cmd* cmds;

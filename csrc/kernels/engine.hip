@@ -173,6 +173,7 @@ class Engine {
       io.ctrl_rec = (CtrlRec*)dev(("ctrl_rec_d" + sfx).c_str(), sizeof(CtrlRec) * d_.seg_max * 2);
       io.ctrl_rec_h = (CtrlRec*)hst(("ctrl_rec" + sfx).c_str(), sizeof(CtrlRec) * d_.seg_max * 2);
       io.grow_h = (RingMove*)hst(("grow" + sfx).c_str(), sizeof(RingMove) * GROW_MAX);
+      io.conn_conf_h = (u32*)hst(("conn_conf" + sfx).c_str(), 4ull * d_.c_max);
       io.xchg = (u32*)hst(("xchg" + sfx).c_str(), 4ull * (4 * WORLD_MAX + 4));
       if (d_.persist) {
         io.persist_h = (u8*)hst(("persist" + sfx).c_str(), d_.persist_bytes + 64);
@@ -213,7 +214,6 @@ class Engine {
     d_.seg_start = (u32*)dev("seg_start", 4ull * d_.seg_max);
     d_.seg_total = (u32*)dev("seg_total", 4ull * d_.seg_max);
     d_.work = (u8*)dev("work", d_.work_cap + 4096 + (d_.xfer_bytes ? d_.xfer_bytes + 128 : 0));
-    d_.cmask = (u16*)dev("cmask", 2ull * ((d_.work_cap + 4096) / 16 + 1));
 
     d_.cmds = (Cmd*)dev("cmds", sizeof(Cmd) * (u64)d_.cmd_max);
     d_.frags = (Frag*)dev("frags", sizeof(Frag) * ((u64)d_.frag_max + d_.import_max));
@@ -395,7 +395,7 @@ class Engine {
       io.ctr_host = io_[p].ctr_host; io.conn_out = io_[p].conn_out;
       io.ctrl = io_[p].ctrl; io.ctrl_rec = io_[p].ctrl_rec; io.xchg = io_[p].xchg;
       io.seg_out_h = io_[p].seg_out_h; io.conn_out_h = io_[p].conn_out_h; io.ctrl_h = io_[p].ctrl_h;
-      io.ctrl_rec_h = io_[p].ctrl_rec_h; io.grow_h = io_[p].grow_h;
+      io.ctrl_rec_h = io_[p].ctrl_rec_h; io.grow_h = io_[p].grow_h; io.conn_conf_h = io_[p].conn_conf_h;
       io.persist_h = io_[p].persist_h; io.crec_h = io_[p].crec_h;
       static_cast<DS&>(io_[p]) = io;
     }
@@ -796,6 +796,7 @@ class Engine {
     a.consumed_host = [](void* e, int p) -> const ConsumedRec* { return ((Engine*)e)->io_[p].crec_hh; };
     a.wblock = (u32*)buf("conn_wblock").ptr;
     a.grow_host = [](void* e, int p) -> const RingMove* { return ((Engine*)e)->io_[p].grow_hh; };
+    a.conn_conf = [](void* e, int p) -> const u32* { return ((Engine*)e)->io_[p].conn_conf_hh; };
     for (int p = 0; p < 2; ++p) {
       std::string sfx = std::to_string(p);
       HostIO& h = io_[p];
@@ -807,6 +808,7 @@ class Engine {
       h.persist_hh = d_.persist ? (const u8*)buf("persist" + sfx).ptr : nullptr;
       h.crec_hh = d_.persist ? (const ConsumedRec*)buf("consumed" + sfx).ptr : nullptr;
       h.grow_hh = (const RingMove*)buf("grow" + sfx).ptr;
+      h.conn_conf_hh = (const u32*)buf("conn_conf" + sfx).ptr;
     }
     return (u64)&api_;
   }
@@ -967,8 +969,8 @@ class Engine {
     u32 ntiles = ceil_div(nmax, SORT_TILE);
     u32 src = 0;
     for (u32 shift = 0; shift < bits; shift += 8) {
-      hipLaunchKernelGGL(k_rs_hist, dim3(ntiles), dim3(256), 0, s, keys[src], n, shift, d_.hist, ntiles);
-      hipLaunchKernelGGL(k_rs_offsets, dim3(1), dim3(256), 0, s, d_.hist, d_.hist_scan, n, ntiles);
+      hipLaunchKernelGGL(k_rs_hist, dim3(ntiles), dim3(256), 0, s, keys[src], n, shift, d_.hist, d_.hist_scan,
+                         &d_.tot[TS_RS_TICKET], ntiles);
       hipLaunchKernelGGL(k_rs_scatter, dim3(ntiles), dim3(256), 0, s, keys[src], vals[src], keys[src ^ 1],
                          vals[src ^ 1], n, shift, d_.hist_scan, ntiles);
       src ^= 1;
@@ -983,9 +985,7 @@ class Engine {
   // frame scan, command assembly, decode (K1-K5)
   void launch_ingest(hipStream_t s, const DS& d) {
     Range rg("chanamq.K1-K4.ingest");
-    hipLaunchKernelGGL(k_prep, dim3(1), dim3(1024), 0, s, d);
     hipLaunchKernelGGL(k_stage, dim3(d.seg_max, 4), dim3(256), 0, s, d);
-    hipLaunchKernelGGL(k_cand, dim3(2048), dim3(256), 0, s, d);
     hipLaunchKernelGGL(k_frame_scan, dim3(d.seg_max), dim3(256), 0, s, d);
     launch_scan(s, {{d.cmd_is_pub, d.cmd_pub_rank}, {d.cmd_is_ack, d.cmd_ack_rank}}, &d.ctr->n_cmds,
                 d.cmd_max, 4);
@@ -1038,7 +1038,6 @@ class Engine {
     const u32 hs_ntiles = pbits <= 8 ? ceil_div(d.pair_max, SORT_TILE) : 0;   // single pass: starts from hist_scan
     if (!hs_ntiles) hipLaunchKernelGGL(k_qfirst, blocks(d.pair_max, 256), dim3(256), 0, s, d, psrc);
     hipLaunchKernelGGL(k_ring_plan, blocks(d.pair_max, 256), dim3(256), 0, s, d, psrc, hs_ntiles);
-    hipLaunchKernelGGL(k_ring_moves, dim3(256), dim3(256), 0, s, d);
     hipLaunchKernelGGL(k_enqueue, blocks(d.pair_max, 256), dim3(256), 0, s, d, psrc, hs_ntiles);
     if (!dispatch) {
       const u64 pn = d.deliv_max > d.c_max ? d.deliv_max : d.c_max;
@@ -1053,16 +1052,18 @@ class Engine {
     hipLaunchKernelGGL(k_dequeue, dim3(d.q_max), dim3(256), 0, s, d);
     hipLaunchKernelGGL(k_runs, dim3(1), dim3(1024), 0, s, d);
     hipLaunchKernelGGL(k_dv_write, blocks(d.deliv_max, 256), dim3(256), 0, s, d);
-    launch_scan(s, {{d.dv_size, d.dv_off}}, &d.ctr->n_deliv, d.deliv_max, 6);
     if (d.c_max <= CONN_LAYOUT_MAX) {
-      hipLaunchKernelGGL(k_conn_layout, dim3(1), dim3(1024), 0, s, d);
+      hipLaunchKernelGGL(k_conn_layout, dim3(1), dim3(1024), 0, s, d);   // + the delivery-size scan
     } else {
+      launch_scan(s, {{d.dv_size, d.dv_off}}, &d.ctr->n_deliv, d.deliv_max, 6);
       hipLaunchKernelGGL(k_conn_sizes, blocks(d.c_max, 256), dim3(256), 0, s, d);
       launch_scan(s, {{d.conn_total, d.conn_base}}, nullptr, d.c_max, 7);
       hipLaunchKernelGGL(k_conn_out, blocks(d.c_max, 256), dim3(256), 0, s, d);
     }
-    hipLaunchKernelGGL(k_render_rc, dim3(RC_RET_BLOCKS + ceil_div(d.c_max, 256)), dim3(256), 0, s, d);
-    hipLaunchKernelGGL(k_render_deliv, blocks((u64)d.deliv_max * 64, 256), dim3(256), 0, s, d);
+    {
+      const u32 n_rc = RC_RET_BLOCKS + ceil_div(d.c_max, 256);
+      hipLaunchKernelGGL(k_render, dim3(n_rc + blocks((u64)d.deliv_max * 64, 256).x), dim3(256), 0, s, d, n_rc);
+    }
     u64 pn = d.deliv_max > d.c_max ? d.deliv_max : d.c_max;
     hipLaunchKernelGGL(k_post, blocks(pn, 256), dim3(256), 0, s, d);
     if (d.persist) {
@@ -1142,6 +1143,7 @@ class Engine {
     const u8* persist_hh = nullptr;
     const ConsumedRec* crec_hh = nullptr;
     const RingMove* grow_hh = nullptr;
+    const u32* conn_conf_hh = nullptr;
   };
   HostIO io_[2];
   CmqEngineApi api_{};

@@ -89,7 +89,7 @@ struct ConnOut { u32 off; u32 len; };
 // C entry points of one Engine (engine.hip: Engine::c_api).  All return 0 / a parity on
 // success and -1 on error (message: error()).  Parity p = the double-buffered step IO set
 // of a submitted step; its host-mapped outputs stay valid until the next submit of p.
-#define CMQ_STEP_ABI 1
+#define CMQ_STEP_ABI 2
 struct CmqEngineApi {
   u32 abi;
   u32 c_max, seg_max, carry_cap, persist, persist_max;
@@ -113,5 +113,8 @@ struct CmqEngineApi {
   const ConsumedRec* (*consumed_host)(void* eng, int p);
   u32* wblock;   // host-mapped u32[c_max]: nonzero = do not dequeue to this connection (egress back-pressure)
   const RingMove* (*grow_host)(void* eng, int p);        // rings grown in that step (Counters.n_grow)
+  // u32[c_max]: publisher-confirm bytes in each connection's egress of that step — only
+  // those connections wait for the step's persistence commit (null = every connection)
+  const u32* (*conn_conf)(void* eng, int p);
 };
 #define GROW_MAX 4096   // grow requests reported per step
