@@ -373,7 +373,8 @@ void Broker::accept_all(int lfd, bool tls) {
 void Broker::on_readable(Conn* c) {
   if (c->blocked) return;
   char buf[65536];
-  int budget = 16;   // fairness: at most 1 MB per connection per loop iteration
+  int budget = 2;    // fairness: at most 128 KB per connection per loop iteration (a publisher
+                     // flood must not starve the acks that reopen consumer windows)
   while (budget-- > 0) {
     ssize_t k;
     if (c->ssl) {
