@@ -147,7 +147,8 @@ void Store::replay() {
     pos += 8 + len;
     good = pos;
   }
-  if (good < data.size()) (void)::ftruncate(fd_, (off_t)good);
+  if (good < data.size() && ::ftruncate(fd_, (off_t)good) != 0)
+    throw std::runtime_error("store: cannot truncate the torn WAL tail");
   wal_bytes_ = good;
   ::lseek(fd_, 0, SEEK_END);
   replaying_ = false;
