@@ -71,8 +71,8 @@ def _main_gpu(args, bc, cfg, log):
     core = load()
     store = None
     if bc["data_dir"]:
-        store = core.Store()
-        store.open(bc["data_dir"], bc["fsync"])
+        from ..store import open_store
+        store = open_store(bc["data_dir"], bc["fsync"])
     plane = GpuDataPlane(**plane_kw)
     broker = GpuBroker(plane, host=bc["host"], port=bc["port"], heartbeat=bc["heartbeat"], frame_max=bc["frame_max"],
                        channel_max=bc["channel_max"] or 2047, store=store, **broker_kw).start()

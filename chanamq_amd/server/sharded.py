@@ -57,14 +57,10 @@ def main(argv=None):
     node = ShardedNode(plane, Comm(store=store, backend=backend, timeout_s=60, wait_s=20))
     st = None
     if args.store_dir:
-        from ..broker import load
-        core = load()
+        from ..store import open_store as _open, rank_dir
 
         def open_store(r):
-            s = core.Store()
-            os.makedirs(args.store_dir, exist_ok=True)
-            s.open(os.path.join(args.store_dir, f"rank{r}"), not args.no_fsync)
-            return s
+            return _open(rank_dir(args.store_dir, r), not args.no_fsync)
         st = open_store(rank)
         node.peer_store = open_store
     from .gpu_broker import GpuBroker

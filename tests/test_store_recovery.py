@@ -98,3 +98,20 @@ def test_durable_messages_survive_restart(tmp_path):
     assert ch.consume_n(1)[0].body == b"again"
     c2.close()
     b2.stop()
+
+
+def test_store_api_open_summary_and_rank_dirs(tmp_path):
+    """chanamq_amd.store: open (nested directories created), table summary, per-rank dirs."""
+    from chanamq_amd.store import open_store, rank_dir, summary
+    d = rank_dir(str(tmp_path / "cluster"), 2)
+    assert d.endswith("rank2")
+    st = open_store(d, fsync=False)
+    st.insert_queue_meta("AMQ.DEFAULT-_.q", -1, set(), True, 0)
+    st.insert_message(7, 0, b"\0" * 10, b"body", "x", "k", True, 1, 0)
+    st.insert_queue_msg("AMQ.DEFAULT-_.q", 0, 7, 4, 0)
+    st.sync()
+    st.close()
+    st = open_store(d, fsync=False)
+    s = summary(st)
+    assert s["msgs"] == 1 and s["queues"] == 1 and s["queue_metas"] == 1
+    st.close()
