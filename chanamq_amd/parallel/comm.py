@@ -36,8 +36,12 @@ class Comm:
         self.wait_s = timeout_s if wait_s is None else wait_s
         self.epoch = 0
 
-    def _wait(self, work):
-        if self.backend == "nccl":
+    def _wait(self, work, block=True):
+        """RCCL: ``block`` = wait on the host with a timeout (a lost peer raises here and
+        the node fails over); otherwise only order the current stream behind the
+        collective (the bulk payload all-to-all, which must not stall the host: the
+        per-step count exchange before it already detects a lost peer)."""
+        if self.backend == "nccl" and block:
             if not work.wait(datetime.timedelta(seconds=self.wait_s)):
                 raise RuntimeError("collective timed out (peer lost)")
         else:
@@ -81,7 +85,7 @@ class Comm:
         isp = [int(in_splits[r]) for r in self.members]
         if sum(osp) != sum(out_splits) or sum(isp) != sum(in_splits):
             raise RuntimeError("traffic addressed to a rank that is not a member")
-        self._wait(self.pg.alltoall_base(out, inp, osp, isp, dist.AllToAllOptions()))
+        self._wait(self.pg.alltoall_base(out, inp, osp, isp, dist.AllToAllOptions()), block=False)
 
     def alltoall_counts(self, counts):
         """counts[r] = list of k ints for logical rank r -> received[r] (k ints each)."""
