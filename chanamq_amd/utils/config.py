@@ -243,11 +243,11 @@ class Config:
             x_max=int(g(k + "max-exchanges", 1024)), cons_max=int(g(k + "max-consumers", 16384)),
             seg_max=int(g(k + "max-segments-per-step", 1024)), cmd_max=int(g(k + "max-commands-per-step", 131072)),
             deliv_max=int(g(k + "max-deliveries-per-step", 65536)), deliver_cap=int(g(k + "deliver-cap", 8192)),
-            msg_max=int(g(k + "message-table", 1 << 22)), log_bytes=int(g(k + "body-log-bytes", 16 << 30)),
-            ring_pool=int(g(k + "queue-ring-pool", 1 << 26)),
+            msg_max=int(g(k + "message-table", 1 << 24)), log_bytes=int(g(k + "body-log-bytes", 64 << 30)),
+            ring_pool=int(g(k + "queue-ring-pool", 1 << 28)),
             default_queue_capacity=int(g(k + "queue-capacity", 1 << 16)), ucap=int(g(k + "unacked-window", 8192)),
             ingress_cap=int(g(k + "ingress-bytes", 64 << 20)), egress_cap=int(g(k + "egress-bytes", 128 << 20)),
-            carry_cap=int(g(k + "carry-bytes", 256 << 10)), tb_max=int(g(k + "topic-bindings", 4096)),
+            carry_cap=int(g(k + "carry-bytes", 16 << 20)), tb_max=int(g(k + "topic-bindings", 4096)),
             frame_max=int(g("chana.mq.amqp.connection.frame-max")),
             hash_wildcard=bool(g("chana.mq.routing.topic-hash-wildcard", True)))
         if store_dir:

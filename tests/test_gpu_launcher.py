@@ -102,3 +102,35 @@ chana.mq.gpu {{
         p2.send_signal(signal.SIGTERM)
         p2.wait(timeout=60)
     assert "recovered 20 messages" in open(tmp_path / "s2.log").read()
+
+
+@pytest.mark.timeout(300)
+def test_gpu_server_default_sizing_carries_a_12mb_message(gpu, tmp_path):
+    """The shipped chana.mq.gpu defaults (64 GiB body log, 16 M message table, 16 MiB
+    largest message) come up on one MI355X, and a 12 MB message goes through the device
+    path intact."""
+    port = _free_port()
+    conf = tmp_path / "default.conf"
+    conf.write_text(f"""
+chana.mq.amqp.server {{ interface = "127.0.0.1", port = {port} }}
+chana.mq.amqp.admin.port = {_free_port()}
+chana.mq.amqp.connection.heartbeat = 0
+chana.mq.gpu.enable = true
+""")
+    with open(tmp_path / "srv.log", "w") as log:
+        p = _start(conf, log)
+        try:
+            _wait_port(port, p)
+            c = Connection(port=port, vhost="/")
+            ch = c.channel()
+            ch.queue_declare("big")
+            body = os.urandom(12 << 20)
+            ch.basic_publish("", "big", body)
+            cc = c.channel()
+            cc.basic_consume("big", "bc", no_ack=True)
+            got = cc.consume_n(1, timeout=60)[0]
+            assert got.body == body
+            c.close()
+        finally:
+            p.send_signal(signal.SIGTERM)
+            p.wait(60)
