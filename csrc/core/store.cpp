@@ -40,6 +40,27 @@ __attribute__((target("sse4.2"))) uint32_t crc32(const char* p, size_t n) {
 }
 uint32_t crc32(const std::string& s) { return crc32(s.data(), s.size()); }
 
+// round-1 WALs (no header): records checked with CRC-32 (reflected 0xEDB88320); replayed
+// once and rewritten in the current format
+uint32_t crc32_legacy(const std::string& s) {
+  static uint32_t tab[256];
+  static bool init = false;
+  if (!init) {
+    for (uint32_t i = 0; i < 256; ++i) {
+      uint32_t c = i;
+      for (int k = 0; k < 8; ++k) c = (c & 1) ? 0xEDB88320u ^ (c >> 1) : c >> 1;
+      tab[i] = c;
+    }
+    init = true;
+  }
+  uint32_t c = 0xFFFFFFFFu;
+  for (unsigned char ch : s) c = tab[(c ^ ch) & 0xff] ^ (c >> 8);
+  return c ^ 0xFFFFFFFFu;
+}
+
+// a WAL starts with this header (format 2: CRC-32C records)
+const char WAL_MAGIC[8] = {'C', 'M', 'Q', 'W', 'A', 'L', '2', '\n'};
+
 void w_map(Writer& w, const std::map<std::string, std::string>& m) {
   w.lng((u32)m.size());
   for (auto& kv : m) { w.longstr(kv.first); w.longstr(kv.second); }
@@ -134,7 +155,13 @@ void Store::replay() {
   char buf[1 << 16];
   ssize_t k;
   while ((k = ::read(fd_, buf, sizeof buf)) > 0) data.append(buf, (size_t)k);
-  size_t pos = 0, good = 0;
+  const bool v2 = data.size() >= sizeof WAL_MAGIC && memcmp(data.data(), WAL_MAGIC, sizeof WAL_MAGIC) == 0;
+  const bool legacy = !v2 && !data.empty();
+  if (data.empty()) {   // a new WAL: the format header first
+    std::string h(WAL_MAGIC, sizeof WAL_MAGIC);
+    write_all(h);
+  }
+  size_t pos = v2 ? sizeof WAL_MAGIC : 0, good = data.empty() ? sizeof WAL_MAGIC : pos;
   while (pos + 9 <= data.size()) {
     const u8* p = (const u8*)data.data() + pos;
     u32 len = (u32(p[0]) << 24) | (u32(p[1]) << 16) | (u32(p[2]) << 8) | p[3];
@@ -142,16 +169,17 @@ void Store::replay() {
     std::string body = data.substr(pos + 4, len);
     const u8* q = p + 4 + len;
     u32 crc = (u32(q[0]) << 24) | (u32(q[1]) << 16) | (u32(q[2]) << 8) | q[3];
-    if (crc != crc32(body)) break;  // torn tail: stop at the last good record
+    if (crc != (legacy ? crc32_legacy(body) : crc32(body))) break;  // torn tail: stop at the last good record
     apply((uint8_t)body[0], body.substr(1));
     pos += 8 + len;
     good = pos;
   }
-  if (good < data.size() && ::ftruncate(fd_, (off_t)good) != 0)
+  if (!data.empty() && good < data.size() && ::ftruncate(fd_, (off_t)good) != 0)
     throw std::runtime_error("store: cannot truncate the torn WAL tail");
   wal_bytes_ = good;
   ::lseek(fd_, 0, SEEK_END);
   replaying_ = false;
+  if (legacy) compact();   // rewrite a round-1 WAL in the current format
 }
 
 void Store::compact() {
@@ -164,6 +192,7 @@ void Store::compact() {
   int old = fd_;
   fd_ = nfd;
   wal_bytes_ = 0;
+  write_all(std::string(WAL_MAGIC, sizeof WAL_MAGIC));
   // re-emit live rows (replaying_ stays false so records are written, apply is idempotent)
   auto vh = vhosts_;
   auto xs = exchanges_;

@@ -115,3 +115,26 @@ def test_store_api_open_summary_and_rank_dirs(tmp_path):
     s = summary(st)
     assert s["msgs"] == 1 and s["queues"] == 1 and s["queue_metas"] == 1
     st.close()
+
+
+def test_round1_wal_replays_and_is_rewritten(tmp_path):
+    """A WAL written before the CRC-32C format (no header, zlib CRC-32 records) is read
+    and rewritten in the current format on open."""
+    import struct
+    import zlib
+
+    from chanamq_amd.store import open_store
+    d = tmp_path / "old"
+    d.mkdir()
+    recs = b""
+    for name in ("AMQ.DEFAULT", "v2"):
+        body = bytes([18]) + struct.pack(">I", len(name)) + name.encode() + b"\x01"   # OP_VH_INS
+        recs += struct.pack(">I", len(body)) + body + struct.pack(">I", zlib.crc32(body))
+    (d / "chanamq.wal").write_bytes(recs)
+    st = open_store(str(d), fsync=False)
+    assert sorted(st.vhost_ids()) == ["AMQ.DEFAULT", "v2"]
+    st.close()
+    assert (d / "chanamq.wal").read_bytes().startswith(b"CMQWAL2\n")
+    st = open_store(str(d), fsync=False)
+    assert sorted(st.vhost_ids()) == ["AMQ.DEFAULT", "v2"]
+    st.close()
