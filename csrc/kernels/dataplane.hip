@@ -1082,11 +1082,13 @@ __global__ __launch_bounds__(1024) void k_scan(ScanArgs a, u32* tot, u64* status
   const u32 base = tile * SCAN_TILE;
   if (base < n || (tile == 0)) {
     const u32 i = base + tid * 4;
-    u32 v[4][4], off[4], agg[4];
+    u32 v[4][4], off[4], agg[4], sm[4];
+    // every array's loads in flight at once, then one block scan of the 4 sums together
+    // (2 barriers instead of 3 per array)
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      if ((u32)k >= a.narr) break;
       v[k][0] = v[k][1] = v[k][2] = v[k][3] = 0;
+      if ((u32)k >= a.narr) continue;
       if (i + 3 < n && !(((uintptr_t)(a.in[k] + i)) & 15)) {
         uint4 x = *(const uint4*)(a.in[k] + i);
         v[k][0] = x.x; v[k][1] = x.y; v[k][2] = x.z; v[k][3] = x.w;
@@ -1094,10 +1096,35 @@ __global__ __launch_bounds__(1024) void k_scan(ScanArgs a, u32* tot, u64* status
         for (u32 e = 0; e < 4; ++e)
           if (i + e < n) v[k][e] = a.in[k][i + e];
       }
-      u32 sum = v[k][0] + v[k][1] + v[k][2] + v[k][3], all;
-      off[k] = block_scan<1024>(sum, lds, all);
-      agg[k] = all;
-      __syncthreads();
+    }
+    const u32 ln = tid & 63, w = tid >> 6;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) sm[k] = v[k][0] + v[k][1] + v[k][2] + v[k][3];
+    u32 x[4] = {sm[0], sm[1], sm[2], sm[3]};
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        u32 y = __shfl_up(x[k], o, 64);
+        if (ln >= (u32)o) x[k] += y;
+      }
+    }
+    __shared__ u32 wsum[4][1024 / 64 + 1];
+    if (ln == 63) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) wsum[k][w] = x[k];
+    }
+    __syncthreads();
+    if (tid < 4) {
+      u32 run = 0;
+      for (u32 j = 0; j < 1024 / 64; ++j) { u32 t = wsum[tid][j]; wsum[tid][j] = run; run += t; }
+      wsum[tid][1024 / 64] = run;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      off[k] = wsum[k][w] + x[k] - sm[k];
+      agg[k] = wsum[k][1024 / 64];
     }
     // look-back, one wave per array: the wave's 64 lanes read the 64 preceding tiles'
     // status words at once, so a tile waits one round trip for all its (concurrently
