@@ -422,9 +422,9 @@ __global__ __launch_bounds__(256) void k_frame_scan(DS d) {
   u16* const chain = chain_am;
   u16* const amask = chain_am;
   __shared__ u8 claim[CAND_MAX];
-  // per 16-byte word with exactly one accepted candidate: its frame end | complete << 31
-  // (phase b reuses it instead of re-reading the header from memory); ~0u = recompute
-  __shared__ u32 wend[FS_AM_MAX];
+  // per accepted candidate: its frame end | complete << 31 (phase b reuses it instead of
+  // re-reading the header from memory); ~0u = recompute
+  __shared__ u32 wend[CAND_MAX];
   __shared__ u32 sc[8];
   __shared__ u32 sh_m, sh_over, sh_ok, sh_nf, sh_stop, sh_brk;
   __shared__ u32 sh_cmd_base, sh_frag_base, sh_ncmd;
@@ -449,88 +449,123 @@ __global__ __launch_bounds__(256) void k_frame_scan(DS d) {
       so.status |= SS_PAUSED;
       d.carry_len[conn] = so.carry;
       d.seg_out[s] = so;
+      d.seg_cmd_base[s] = INVALID;
+      d.seg_npub[s] = 0;
     }
     return;
   }
   if (L == 0) {
-    if (tid == 0) { d.carry_len[conn] = 0; d.seg_out[s] = so; }
+    if (tid == 0) { d.carry_len[conn] = 0; d.seg_out[s] = so; d.seg_cmd_base[s] = INVALID; d.seg_npub[s] = 0; }
     return;
   }
   if (tid == 0) { sh_m = 0; sh_over = 0; }
   __syncthreads();
 
   FS_MARK(0);
-  // ---- (a) candidates: compact the chip-wide candidate mask (k_cand) of this segment,
-  // validate against the connection's frame-max / end marker, append the trailing
-  // positions that can only hold a partial header
+  // ---- (a) candidates: screen the segment (one mask bit per byte that looks like a frame
+  // header), validate them against the connection's frame-max / end marker, append the
+  // trailing positions that can only hold a partial header.  cpos = accepted positions in
+  // order; wend[i] = candidate i's frame end | complete << 31 (~0u: phase b re-reads it)
   {
     const u32 nm = (L + 15) >> 4;
     const u32 per = (nm + 255) >> 8;
     const u32 c0 = tid * per;
     const u32 c1 = c0 + per < nm ? c0 + per : nm;
     const u32 lim = L >= 7 ? L - 6 : 0;   // full-header positions are p < lim
-    // pass 1 validates each candidate once and keeps the accepted bits in LDS (amask), so
-    // pass 2 only emits positions instead of re-reading every frame header from HBM;
-    // segments longer than FS_AM_MAX mask words fall back to re-validating
     const bool use_am = nm <= FS_AM_MAX;
     const u32 fmg = d.frame_max_global;
     if (use_am) {   // candidate screen of the segment into LDS (fused k_cand), coalesced reads
       const uint4* W = (const uint4*)b;   // 16-aligned; >= 32 bytes of padding after the segment
-      for (u32 c0 = tid; c0 < nm; c0 += 256 * 8) {
+      for (u32 cc = tid; cc < nm; cc += 256 * 8) {
         uint4 x[8], y[8];
 #pragma unroll
         for (int k = 0; k < 8; ++k) {   // every load of the batch in flight before any use
-          const u32 c = c0 + k * 256;
+          const u32 c = cc + k * 256;
           if (c < nm) { x[k] = W[c]; y[k] = W[c + 1]; }
         }
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
-          const u32 c = c0 + k * 256;
+          const u32 c = cc + k * 256;
           if (c < nm) amask[c] = (u16)cand_bits(x[k], y[k], fmg);
         }
       }
       __syncthreads();
     }
-    u32 cnt = 0;
-    for (u32 c = c0; c < c1; ++c) {
-      u32 mk = use_am ? (u32)amask[c] : cand_word(b + c * 16, fmg);
-      u32 acc = 0, we = ~0u, na = 0;
-      while (mk) {
-        u32 j = __ffs(mk) - 1;
-        mk &= mk - 1;
-        u32 p = c * 16 + j;
-        if (p >= lim) break;
-        FInfo f = frame_at(b, p, L, fmax);
-        if (f.valid_hdr && (f.complete || (u64)p + 8 + f.size > L)) {
-          ++cnt;
-          acc |= 1u << j;
+    // raw candidates per thread (its words are contiguous: the scan keeps position order)
+    u32 rc = 0;
+    if (use_am)
+      for (u32 c = c0; c < c1; ++c) {
+        u32 mk = amask[c];
+        if (c * 16 + 16 > lim) mk &= lim > c * 16 ? (1u << (lim - c * 16)) - 1u : 0u;
+        rc += __popc(mk);
+      }
+    u32 rtot;
+    u32 roff = block_scan<256>(rc, sc, rtot);
+    u32 tot = 0;
+    if (use_am && rtot <= CAND_MAX) {
+      // every raw candidate validated in parallel (one thread each), then compacted in
+      // place chunk by chunk: accepted entries only move left, after the chunk was read
+      for (u32 c = c0; c < c1; ++c) {
+        u32 mk = amask[c];
+        while (mk) {
+          const u32 j = __ffs(mk) - 1;
+          mk &= mk - 1;
+          const u32 p = c * 16 + j;
+          if (p >= lim) break;
+          cpos[roff++] = p;
+        }
+      }
+      __syncthreads();
+      for (u32 k0 = 0; k0 < rtot; k0 += 256) {
+        const u32 i = k0 + tid;
+        bool ok = false;
+        u32 p = 0, we = ~0u;
+        if (i < rtot) {
+          p = cpos[i];
+          const FInfo f = frame_at(b, p, L, fmax);
+          ok = f.valid_hdr && (f.complete || (u64)p + 8 + f.size > L);
           const u64 e64 = (u64)p + 8 + f.size;
           we = e64 < 0x7fffffffull ? ((f.complete ? 0x80000000u : 0u) | (u32)e64) : ~0u;
-          ++na;
         }
+        u32 all;
+        const u32 o = block_scan<256>(ok ? 1u : 0u, sc, all);
+        if (ok) { cpos[tot + o] = p; wend[tot + o] = we; }
+        tot += all;
       }
-      if (use_am) {
-        amask[c] = (u16)acc;
-        wend[c] = na == 1 ? we : ~0u;
-      }
-    }
-    u32 tot;
-    u32 off = block_scan<256>(cnt, sc, tot);
-    for (u32 c = c0; c < c1; ++c) {
-      u32 mk = use_am ? (u32)amask[c] : cand_word(b + c * 16, fmg);
-      while (mk) {
-        u32 j = __ffs(mk) - 1;
-        mk &= mk - 1;
-        u32 p = c * 16 + j;
-        if (p >= lim) break;
-        bool acc = use_am;
-        if (!use_am) {
+    } else {
+      // very long segment (no LDS mask) or more raw candidates than CAND_MAX: each
+      // thread validates its own words, twice (count, then emit)
+      u32 cnt = 0;
+      for (u32 c = c0; c < c1; ++c) {
+        u32 mk = use_am ? (u32)amask[c] : cand_word(b + c * 16, fmg);
+        u32 acc = 0;
+        while (mk) {
+          u32 j = __ffs(mk) - 1;
+          mk &= mk - 1;
+          u32 p = c * 16 + j;
+          if (p >= lim) break;
           FInfo f = frame_at(b, p, L, fmax);
-          acc = f.valid_hdr && (f.complete || (u64)p + 8 + f.size > L);
+          if (f.valid_hdr && (f.complete || (u64)p + 8 + f.size > L)) { ++cnt; acc |= 1u << j; }
         }
-        if (acc) {
-          if (off < CAND_MAX) cpos[off] = p;
-          ++off;
+        if (use_am) amask[c] = (u16)acc;
+      }
+      u32 off = block_scan<256>(cnt, sc, tot);
+      for (u32 c = c0; c < c1; ++c) {
+        u32 mk = use_am ? (u32)amask[c] : cand_word(b + c * 16, fmg);
+        while (mk) {
+          u32 j = __ffs(mk) - 1;
+          mk &= mk - 1;
+          u32 p = c * 16 + j;
+          if (p >= lim) break;
+          bool acc = use_am;
+          if (!use_am) {
+            FInfo f = frame_at(b, p, L, fmax);
+            acc = f.valid_hdr && (f.complete || (u64)p + 8 + f.size > L);
+          }
+          if (acc) {
+            if (off < CAND_MAX) { cpos[off] = p; wend[off] = ~0u; }
+            ++off;
+          }
         }
       }
     }
@@ -538,7 +573,7 @@ __global__ __launch_bounds__(256) void k_frame_scan(DS d) {
     if (tid == 0) {
       u32 nmc = tot;
       for (u32 p = lim; p < L; ++p) {
-        if (nmc < CAND_MAX) cpos[nmc] = p;
+        if (nmc < CAND_MAX) { cpos[nmc] = p; wend[nmc] = ~0u; }
         ++nmc;
       }
       if (nmc > CAND_MAX) { sh_over = 1; nmc = CAND_MAX; }
@@ -551,12 +586,11 @@ __global__ __launch_bounds__(256) void k_frame_scan(DS d) {
   const bool over = sh_over != 0;
 
   // ---- (b) successor of every candidate (-1 exact end, -2 partial/unknown, -3 broken)
-  const bool use_we = ((L + 15) >> 4) <= FS_AM_MAX;
   for (u32 i = tid; i < m; i += 256) {
     u32 p = cpos[i];
     bool complete;
     u32 e;
-    const u32 we = use_we && p < (L >= 7 ? L - 6 : 0) ? wend[p >> 4] : ~0u;
+    const u32 we = wend[i];
     if (we != ~0u) {
       complete = (we >> 31) != 0;
       e = we & 0x7fffffffu;
@@ -742,6 +776,7 @@ __global__ __launch_bounds__(256) void k_frame_scan(DS d) {
   }
   FS_MARK(6);
   const i64 now = d.in->now_ms;
+  u32 my_pubs = 0;
   for (u32 f0 = 0; f0 < kf; f0 += 256) {
     u32 f = f0 + tid;
     u32 is_cmd = 0, nfr = 0;
@@ -804,6 +839,7 @@ __global__ __launch_bounds__(256) void k_frame_scan(DS d) {
       d.cmds[ci] = c;
       // classification for the publish / ack rank scans (fused k_classify)
       d.cmd_is_pub[ci] = c.kind == CK_PUBLISH;
+      my_pubs += c.kind == CK_PUBLISH;
       d.cmd_is_ack[ci] = c.kind == CK_ACK || c.kind == CK_NACK || c.kind == CK_REJECT;
       if (c.kind == CK_CONTROL || c.kind == CK_TXBUF) {
         u32 cbase;
@@ -826,6 +862,14 @@ __global__ __launch_bounds__(256) void k_frame_scan(DS d) {
   }
   if (tid == 0 && kf > 0) d.conn_last_rx[conn] = now;
   if (reason == 0) so.status |= SS_CTRL;
+  {   // the segment's publish count: k_decode numbers publishes in segment order
+    u32 np;
+    block_scan<256>(my_pubs, sc, np);
+    if (tid == 0) {
+      d.seg_cmd_base[s] = (run && sh_cmd_base != INVALID) ? sh_cmd_base : INVALID;
+      d.seg_npub[s] = d.seg_cmd_base[s] == INVALID ? 0u : np;
+    }
+  }
 
   FS_MARK(7);
   // ---- (f) carry out: bytes [consumed, L)
@@ -921,8 +965,32 @@ DEV void apply_ack(const DS& d, const Ack& a) {
   atomicAdd(&d.ctr->n_acked, 1u);
 }
 
-__global__ void k_decode(DS d) {
+// publishes are numbered in segment order (segment s's publishes follow those of the
+// segments before it), not in the order the frame-scan blocks reserved their commands:
+// queue order across connections is then deterministic (the golden model's order)
+#define DEC_SEG_LDS 4096
+__global__ __launch_bounds__(256) void k_decode(DS d) {
+  __shared__ u32 spref[DEC_SEG_LDS];
+  __shared__ u32 lds[256 / 64 + 1];
   if (blockIdx.x == 0 && threadIdx.x == 0) set_counts(d);  // fused: counts + phase-0 range
+  {
+    u32 n0 = d.ctr->n_cmds;
+    if (blockIdx.x * 256 >= (n0 < d.cmd_max ? n0 : d.cmd_max)) return;   // whole block idle
+  }
+  const u32 nseg = d.in->nseg;
+  const bool seg_order = nseg <= DEC_SEG_LDS;
+  if (seg_order) {
+    u32 run = 0;
+    for (u32 b0 = 0; b0 < nseg; b0 += 256) {
+      const u32 k = b0 + threadIdx.x;
+      const u32 v = k < nseg ? d.seg_npub[k] : 0;
+      u32 all;
+      const u32 o = block_scan<256>(v, lds, all);
+      if (k < nseg) spref[k] = run + o;
+      run += all;
+    }
+    __syncthreads();
+  }
   u32 i = blockIdx.x * blockDim.x + threadIdx.x;
   u32 n = d.ctr->n_cmds;
   if (n > d.cmd_max) n = d.cmd_max;
@@ -931,6 +999,8 @@ __global__ void k_decode(DS d) {
   const u8* w = d.work;
   if (c.kind == CK_PUBLISH) {
     u32 pi = d.cmd_pub_rank[i];
+    if (seg_order && c.seg < nseg && d.seg_cmd_base[c.seg] != INVALID)
+      pi = spref[c.seg] + (pi - d.cmd_pub_rank[d.seg_cmd_base[c.seg]]);
     if (pi >= d.pub_max) return;
     Pub pb;
     pb.conn = c.conn;

@@ -82,6 +82,8 @@ struct DS {
   // ---------------- per segment / work
   u32* seg_start;
   u32* seg_total;
+  u32* seg_cmd_base;        // first command of each segment (INVALID: none / overflowed)
+  u32* seg_npub;            // publishes of each segment: publishes get segment-ordered indices
   u8* work;
 
   // ---------------- commands

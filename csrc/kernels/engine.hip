@@ -213,6 +213,8 @@ class Engine {
 
     d_.seg_start = (u32*)dev("seg_start", 4ull * d_.seg_max);
     d_.seg_total = (u32*)dev("seg_total", 4ull * d_.seg_max);
+    d_.seg_cmd_base = (u32*)dev("seg_cmd_base", 4ull * d_.seg_max);
+    d_.seg_npub = (u32*)dev("seg_npub", 4ull * d_.seg_max);
     d_.work = (u8*)dev("work", d_.work_cap + 4096 + (d_.xfer_bytes ? d_.xfer_bytes + 128 : 0));
 
     d_.cmds = (Cmd*)dev("cmds", sizeof(Cmd) * (u64)d_.cmd_max);
