@@ -32,8 +32,10 @@ class Comm:
         self.device = device
         self.timeout_s = timeout_s
         # RCCL: Work.wait(timeout) blocks the host and raises when a peer stops answering
-        # (without it the wait only orders streams and a dead peer hangs the GPU stream)
-        self.wait_s = timeout_s if wait_s is None else wait_s
+        # (without it the wait only orders streams and a dead peer hangs the GPU stream).
+        # Opt-in (the failover-capable sharded server sets it; the benchmark keeps the
+        # plain stream-ordered waits)
+        self.wait_s = wait_s
         self.epoch = 0
 
     def _wait(self, work, block=True):
@@ -41,7 +43,7 @@ class Comm:
         the node fails over); otherwise only order the current stream behind the
         collective (the bulk payload all-to-all, which must not stall the host: the
         per-step count exchange before it already detects a lost peer)."""
-        if self.backend == "nccl" and block:
+        if self.backend == "nccl" and block and self.wait_s:
             if not work.wait(datetime.timedelta(seconds=self.wait_s)):
                 raise RuntimeError("collective timed out (peer lost)")
         else:
