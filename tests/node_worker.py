@@ -86,6 +86,52 @@ def durable(out, die_rank, die_after):
     store.close()
 
 
+def links(out, die_rank, die_after):
+    """Remote consumer across a failure.  Queue lq lives on rank 2, its consumer on rank 1
+    (a link), the publisher on rank 0 (which also hosts the c10d store, so it must live).
+    die_rank 1 (the consumer's rank): the owner closes the link, everything the consumer
+      held (it never acks) returns to lq and a new consumer on rank 2 gets every message.
+    die_rank 2 (the owner): lq re-homes and the link re-attaches at the new owner; the
+      consumer keeps receiving what is published after the failover."""
+    rank, world = dist.get_rank(), dist.get_world_size()
+    plane = GoldenDataPlane(default_queue_capacity=1 << 12, ring_pool=1 << 22, world=world, rank=rank)
+    node = ShardedNode(plane, Comm(timeout_s=20), hb_timeout_s=1.0)
+    if rank == 0:
+        node.submit("declare_exchange", VH, "lx", "direct")
+        node.submit("place_queue", VH, "lq", 2)
+        node.submit("declare_queue", VH, "lq")
+        node.submit("bind", VH, "lq", "lx", "k")
+    node.step({}, now_ms=1)
+    if rank == 1:
+        node.submit("link_open", 7, VH, "lq", 1, 1000)
+    node.step({}, now_ms=2)
+    if rank == 1:
+        plane.open_connection(20, VH)
+        plane.open_channel(20, 1)
+        plane.consume(20, 1, VH, node.links.shadow_of(7), "remote", no_ack=(die_rank == 2))
+    plane.open_connection(1, VH)
+    plane.open_channel(1, 1)
+    got, steps, per = {}, 10, 5
+    local = False
+    for k in range(steps + 4):
+        if rank == die_rank and k == die_after:
+            os._exit(0)
+        if k == steps and die_rank == 1 and rank == 2:   # after the failover: drain lq here
+            plane.open_connection(30, VH)
+            plane.open_channel(30, 1)
+            plane.consume(30, 1, VH, "lq", "local", no_ack=True)
+            local = True
+        data = publish_stream(per, "lx", lambda i: "k", 40, seed=k) if (rank == 0 and k < steps) else b""
+        res, _ = node.step({1: data} if data else {}, now_ms=1000 + k)
+        for c, b in res["egress"].items():
+            got[str(c)] = got.get(str(c), 0) + count_delivers(b)
+    with open(os.path.join(out, f"rank{rank}.json"), "w") as f:
+        json.dump({"deliveries": got, "failovers": node.failovers, "links": sorted(node.links.links),
+                   "local": local, "live": sorted(node.members.live)}, f)
+    node.comm.barrier()
+    node.close()
+
+
 def main():
     scen, out = sys.argv[1], sys.argv[2]
     die_rank = int(sys.argv[3]) if len(sys.argv) > 3 else -1
@@ -93,6 +139,8 @@ def main():
     dist.init_process_group("gloo")
     if scen == "durable":
         return durable(out, die_rank, die_after)
+    if scen == "links":
+        return links(out, die_rank, die_after)
     rank, world = dist.get_rank(), dist.get_world_size()
     plane = GoldenDataPlane(default_queue_capacity=1 << 12, ring_pool=1 << 22, world=world, rank=rank)
     node = ShardedNode(plane, Comm(timeout_s=20), hb_timeout_s=1.0)

@@ -79,3 +79,25 @@ def test_failover_reloads_durable_queues():
         assert o["failovers"][0][2] == 4 * 3 * 5 * len(moved_here)
         assert o["rows"] == 0            # consumed (auto-ack): the store rows are gone too
     assert total == 6 * 100
+
+
+@pytest.mark.timeout(300)
+def test_remote_consumer_rank_dies_messages_return_to_the_queue():
+    """The consumer's rank dies holding unacked deliveries of a remote queue: the owner
+    closes the link, the messages go back to the queue, and a consumer on the owner gets
+    every message that was published."""
+    out = _run(3, die_rank=1, die_after=6, scen="links")
+    assert set(out) == {0, 2}
+    assert out[2]["links"] == [] and out[2]["local"]
+    assert out[2]["deliveries"].get("30") == 10 * 5, out[2]
+
+
+@pytest.mark.timeout(300)
+def test_remote_consumer_survives_its_queue_owner_dying():
+    """The queue's owner dies: the queue re-homes to a survivor, the link re-attaches
+    there and the remote consumer keeps receiving new publishes."""
+    out = _run(3, die_rank=2, die_after=5, scen="links")
+    assert set(out) == {0, 1}
+    assert out[1]["links"] == [7]
+    # steps 5..9 are published after the failover (5 messages each)
+    assert out[1]["deliveries"].get("20", 0) >= 5 * 5, out[1]
