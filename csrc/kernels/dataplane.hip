@@ -413,7 +413,10 @@ DEV u32 cand_word(const u8* w16, u32 fm) {
 #define FS_MARK(k) \
   do { if (tid == 0 && d.dbg) d.dbg[(u64)s * 16 + (k)] = __builtin_amdgcn_s_memrealtime(); } while (0)
 constexpr u32 FS_AM_MAX = 8192;  // 128 KB segment; 16 KB of LDS
-__global__ __launch_bounds__(256) void k_frame_scan(DS d) {
+// one block of FS_NT threads per segment: 16 waves (4 per SIMD) hide the screen's
+// dependent integer chains, which one wave per SIMD could not
+#define FS_NT 1024
+__global__ __launch_bounds__(FS_NT) void k_frame_scan(DS d) {
   __shared__ u32 cpos[CAND_MAX];
   __shared__ int16_t csucc[CAND_MAX];
   // chain (first written in phase c) aliases amask (used only in phase a, which ends on
@@ -425,7 +428,7 @@ __global__ __launch_bounds__(256) void k_frame_scan(DS d) {
   // per accepted candidate: its frame end | complete << 31 (phase b reuses it instead of
   // re-reading the header from memory); ~0u = recompute
   __shared__ u32 wend[CAND_MAX];
-  __shared__ u32 sc[8];
+  __shared__ u32 sc[FS_NT / 64 + 1];
   __shared__ u32 sh_m, sh_over, sh_ok, sh_nf, sh_stop, sh_brk;
   __shared__ u32 sh_cmd_base, sh_frag_base, sh_ncmd;
 
@@ -444,7 +447,7 @@ __global__ __launch_bounds__(256) void k_frame_scan(DS d) {
   if (d.conn_paused[conn]) {
     // hold everything; write carry back (k_stage already appended new bytes)
     if (L > d.carry_cap) { so.status = SS_TOO_LARGE; so.carry = 0; }
-    else block_copy(d.carry + (u64)conn * d.carry_cap, b, L, tid, 256);
+    else block_copy(d.carry + (u64)conn * d.carry_cap, b, L, tid, FS_NT);
     if (tid == 0) {
       so.status |= SS_PAUSED;
       d.carry_len[conn] = so.carry;
@@ -468,7 +471,7 @@ __global__ __launch_bounds__(256) void k_frame_scan(DS d) {
   // order; wend[i] = candidate i's frame end | complete << 31 (~0u: phase b re-reads it)
   {
     const u32 nm = (L + 15) >> 4;
-    const u32 per = (nm + 255) >> 8;
+    const u32 per = (nm + FS_NT - 1) / FS_NT;
     const u32 c0 = tid * per;
     const u32 c1 = c0 + per < nm ? c0 + per : nm;
     const u32 lim = L >= 7 ? L - 6 : 0;   // full-header positions are p < lim
@@ -476,16 +479,16 @@ __global__ __launch_bounds__(256) void k_frame_scan(DS d) {
     const u32 fmg = d.frame_max_global;
     if (use_am) {   // candidate screen of the segment into LDS (fused k_cand), coalesced reads
       const uint4* W = (const uint4*)b;   // 16-aligned; >= 32 bytes of padding after the segment
-      for (u32 cc = tid; cc < nm; cc += 256 * 8) {
-        uint4 x[8], y[8];
+      for (u32 cc = tid; cc < nm; cc += FS_NT * 4) {
+        uint4 x[4], y[4];
 #pragma unroll
-        for (int k = 0; k < 8; ++k) {   // every load of the batch in flight before any use
-          const u32 c = cc + k * 256;
+        for (int k = 0; k < 4; ++k) {   // every load of the batch in flight before any use
+          const u32 c = cc + k * FS_NT;
           if (c < nm) { x[k] = W[c]; y[k] = W[c + 1]; }
         }
 #pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          const u32 c = cc + k * 256;
+        for (int k = 0; k < 4; ++k) {
+          const u32 c = cc + k * FS_NT;
           if (c < nm) amask[c] = (u16)cand_bits(x[k], y[k], fmg);
         }
       }
@@ -500,7 +503,7 @@ __global__ __launch_bounds__(256) void k_frame_scan(DS d) {
         rc += __popc(mk);
       }
     u32 rtot;
-    u32 roff = block_scan<256>(rc, sc, rtot);
+    u32 roff = block_scan<FS_NT>(rc, sc, rtot);
     u32 tot = 0;
     if (use_am && rtot <= CAND_MAX) {
       // every raw candidate validated in parallel (one thread each), then compacted in
@@ -516,7 +519,7 @@ __global__ __launch_bounds__(256) void k_frame_scan(DS d) {
         }
       }
       __syncthreads();
-      for (u32 k0 = 0; k0 < rtot; k0 += 256) {
+      for (u32 k0 = 0; k0 < rtot; k0 += FS_NT) {
         const u32 i = k0 + tid;
         bool ok = false;
         u32 p = 0, we = ~0u;
@@ -528,7 +531,7 @@ __global__ __launch_bounds__(256) void k_frame_scan(DS d) {
           we = e64 < 0x7fffffffull ? ((f.complete ? 0x80000000u : 0u) | (u32)e64) : ~0u;
         }
         u32 all;
-        const u32 o = block_scan<256>(ok ? 1u : 0u, sc, all);
+        const u32 o = block_scan<FS_NT>(ok ? 1u : 0u, sc, all);
         if (ok) { cpos[tot + o] = p; wend[tot + o] = we; }
         tot += all;
       }
@@ -549,7 +552,7 @@ __global__ __launch_bounds__(256) void k_frame_scan(DS d) {
         }
         if (use_am) amask[c] = (u16)acc;
       }
-      u32 off = block_scan<256>(cnt, sc, tot);
+      u32 off = block_scan<FS_NT>(cnt, sc, tot);
       for (u32 c = c0; c < c1; ++c) {
         u32 mk = use_am ? (u32)amask[c] : cand_word(b + c * 16, fmg);
         while (mk) {
@@ -586,7 +589,7 @@ __global__ __launch_bounds__(256) void k_frame_scan(DS d) {
   const bool over = sh_over != 0;
 
   // ---- (b) successor of every candidate (-1 exact end, -2 partial/unknown, -3 broken)
-  for (u32 i = tid; i < m; i += 256) {
+  for (u32 i = tid; i < m; i += FS_NT) {
     u32 p = cpos[i];
     bool complete;
     u32 e;
@@ -616,7 +619,7 @@ __global__ __launch_bounds__(256) void k_frame_scan(DS d) {
   if (tid == 0) sh_ok = 1;
   __syncthreads();
   // ---- (c) chain: optimistic (every candidate a real frame) else serial walk
-  for (u32 i = tid; i < m; i += 256) {
+  for (u32 i = tid; i < m; i += FS_NT) {
     i32 sx = csucc[i];
     bool good = (i + 1 < m) ? (sx == (i32)(i + 1)) : (sx == -1 || sx == -2);
     if (!good) atomicAnd(&sh_ok, 0u);
@@ -648,11 +651,11 @@ __global__ __launch_bounds__(256) void k_frame_scan(DS d) {
 #define CPOS(f) (cpos[implicit_chain ? (f) : chain[f]])
 
   // ---- (d) commands: each method frame walks its content frames
-  for (u32 f = tid; f < nf; f += 256) claim[f] = 0;
+  for (u32 f = tid; f < nf; f += FS_NT) claim[f] = 0;
   if (tid == 0) sh_stop = (nf << 3) | 7;  // (frame << 3) | reason; 7 = none
   __syncthreads();
   // stop reasons: 0 = after control, 1 = incomplete, 2 = unexpected frame, 3 = frame error
-  for (u32 f = tid; f < nf; f += 256) {
+  for (u32 f = tid; f < nf; f += FS_NT) {
     u32 p = CPOS(f);
     FInfo fi = frame_at(b, p, L, fmax);
     if (!fi.complete) {
@@ -699,7 +702,7 @@ __global__ __launch_bounds__(256) void k_frame_scan(DS d) {
     if (!data) atomicMin(&sh_stop, ((e + 1) << 3) | 0);
   }
   __syncthreads();
-  for (u32 f = tid; f < nf; f += 256) {
+  for (u32 f = tid; f < nf; f += FS_NT) {
     if (claim[f]) continue;
     FInfo fi = frame_at(b, CPOS(f), L, fmax);
     if (fi.complete) atomicMin(&sh_stop, (f << 3) | 2);
@@ -733,7 +736,7 @@ __global__ __launch_bounds__(256) void k_frame_scan(DS d) {
   __syncthreads();
   // count first
   u32 my_cmds = 0, my_frags = 0;
-  for (u32 f = tid; f < kf; f += 256) {
+  for (u32 f = tid; f < kf; f += FS_NT) {
     u32 p = CPOS(f);
     if (b[p] != 1) continue;
     ++my_cmds;
@@ -744,8 +747,8 @@ __global__ __launch_bounds__(256) void k_frame_scan(DS d) {
     }
   }
   u32 tc, tfr;
-  block_scan<256>(my_cmds, sc, tc);
-  block_scan<256>(my_frags, sc, tfr);
+  block_scan<FS_NT>(my_cmds, sc, tc);
+  block_scan<FS_NT>(my_frags, sc, tfr);
   // one uncontended atomicAdd per block (a CAS loop here serialises all blocks);
   // on overflow the reserved in-range slots are filled with CK_NONE and the whole
   // segment is carried to the next step
@@ -759,7 +762,7 @@ __global__ __launch_bounds__(256) void k_frame_scan(DS d) {
   __syncthreads();
   if (sh_ncmd && tc > 0) {
     u32 cb = sh_cmd_base;
-    for (u32 i = cb + tid; i < cb + tc && i < d.cmd_max; i += 256) {
+    for (u32 i = cb + tid; i < cb + tc && i < d.cmd_max; i += FS_NT) {
       d.cmds[i].kind = CK_NONE;
       d.cmd_is_pub[i] = 0;
       d.cmd_is_ack[i] = 0;
@@ -777,7 +780,7 @@ __global__ __launch_bounds__(256) void k_frame_scan(DS d) {
   FS_MARK(6);
   const i64 now = d.in->now_ms;
   u32 my_pubs = 0;
-  for (u32 f0 = 0; f0 < kf; f0 += 256) {
+  for (u32 f0 = 0; f0 < kf; f0 += FS_NT) {
     u32 f = f0 + tid;
     u32 is_cmd = 0, nfr = 0;
     u32 p = 0;
@@ -792,8 +795,8 @@ __global__ __launch_bounds__(256) void k_frame_scan(DS d) {
       }
     }
     u32 tcnt, tf;
-    u32 r = block_scan<256>(is_cmd, sc, tcnt);
-    u32 fr = block_scan<256>(nfr, sc, tf);
+    u32 r = block_scan<FS_NT>(is_cmd, sc, tcnt);
+    u32 fr = block_scan<FS_NT>(nfr, sc, tf);
     if (is_cmd) {
       Cmd c;
       FInfo fi = frame_at(b, p, L, fmax);
@@ -864,7 +867,7 @@ __global__ __launch_bounds__(256) void k_frame_scan(DS d) {
   if (reason == 0) so.status |= SS_CTRL;
   {   // the segment's publish count: k_decode numbers publishes in segment order
     u32 np;
-    block_scan<256>(my_pubs, sc, np);
+    block_scan<FS_NT>(my_pubs, sc, np);
     if (tid == 0) {
       d.seg_cmd_base[s] = (run && sh_cmd_base != INVALID) ? sh_cmd_base : INVALID;
       d.seg_npub[s] = d.seg_cmd_base[s] == INVALID ? 0u : np;
@@ -875,7 +878,7 @@ __global__ __launch_bounds__(256) void k_frame_scan(DS d) {
   // ---- (f) carry out: bytes [consumed, L)
   u32 rest = L - consumed;
   if (rest > d.carry_cap) { so.status |= SS_TOO_LARGE; rest = 0; }
-  else block_copy(d.carry + (u64)conn * d.carry_cap, b + consumed, rest, tid, 256);
+  else block_copy(d.carry + (u64)conn * d.carry_cap, b + consumed, rest, tid, FS_NT);
   FS_MARK(8);
   if (tid == 0) {
     so.consumed = consumed;

@@ -988,7 +988,7 @@ class Engine {
   void launch_ingest(hipStream_t s, const DS& d) {
     Range rg("chanamq.K1-K4.ingest");
     hipLaunchKernelGGL(k_stage, dim3(d.seg_max, 4), dim3(256), 0, s, d);
-    hipLaunchKernelGGL(k_frame_scan, dim3(d.seg_max), dim3(256), 0, s, d);
+    hipLaunchKernelGGL(k_frame_scan, dim3(d.seg_max), dim3(FS_NT), 0, s, d);
     launch_scan(s, {{d.cmd_is_pub, d.cmd_pub_rank}, {d.cmd_is_ack, d.cmd_ack_rank}}, &d.ctr->n_cmds,
                 d.cmd_max, 4);
     hipLaunchKernelGGL(k_decode, blocks(d.cmd_max, 256), dim3(256), 0, s, d);
