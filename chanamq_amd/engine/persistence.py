@@ -24,6 +24,8 @@ import struct
 
 from .control import entity_id
 
+LINK_SHADOW = "amq.link."   # shadow queues of cross-rank links (parallel/links.py): never stored
+
 
 def _split_eid(eid):
     if "-_." in eid:
@@ -46,7 +48,7 @@ class GpuPersistence:
         end): from now on every record goes through it, Python keeps only control rows."""
         self.native = worker
         for q in self.plane.queue_by_slot.values():
-            if q.durable:
+            if q.durable and not q.name.startswith(LINK_SHADOW):
                 worker.set_queue(q.slot, entity_id(q.vhost, q.name))
         for (qid, mid), (off, size, unack) in self.rows.items():
             worker.seed_row(qid, mid, off, size, bool(unack), self.refs.get(mid, 1))
@@ -156,7 +158,7 @@ class GpuPersistence:
         self.store.delete_exchange(entity_id(vhost, name))
 
     def queue(self, q):
-        if q.durable:
+        if q.durable and not q.name.startswith(LINK_SHADOW):   # link shadows hold no rows
             self.store.insert_queue_meta(entity_id(q.vhost, q.name), -1, set(), True, q.ttl_ms)
             if self.native is not None:
                 self.native.set_queue(q.slot, entity_id(q.vhost, q.name))

@@ -23,12 +23,17 @@ class LocalCluster:
         """Apply a control-plane op (declare/bind/delete ...) on every rank."""
         return [getattr(p, fn)(*args, **kw) for p in self.planes]
 
-    def link_open(self, lid, vhost, queue, dest, prefetch=0):
+    def link_open(self, lid, vhost, queue, dest, prefetch=0, get=False):
         """Remote consumer link (parallel/links.py), replicated like a control op;
-        returns the shadow queue's name (consume it on rank ``dest``)."""
+        returns the shadow queue's name (consume it on rank ``dest``; a get link's shadow
+        receives the messages its pulls fetched)."""
         for lk in self.links:
-            lk.open(lid, vhost, queue, dest, prefetch)
+            lk.open(lid, vhost, queue, dest, prefetch, get)
         return self.links[0].shadow_of(lid)
+
+    def link_pull(self, lid, pn, now_ms=None):
+        """One remote Basic.Get on get link ``lid`` (answered after the next step)."""
+        return [lk.pull(lid, pn, now_ms) for lk in self.links][0]
 
     def link_close(self, lid):
         for lk in self.links:

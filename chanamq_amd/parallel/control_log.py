@@ -13,7 +13,7 @@ from ..protocol import constants as C
 from .comm import Comm
 
 REPLICATED = {"declare_exchange", "delete_exchange", "declare_queue", "delete_queue", "bind", "unbind",
-              "place_queue", "ensure_vhost", "link_open", "link_close"}
+              "place_queue", "ensure_vhost", "link_open", "link_close", "link_pull"}
 
 
 class ControlLog:

@@ -24,6 +24,15 @@ back to the entity (FrameStage.scala:395-429, QueueEntity.scala:318-446).  Here 
   close the link: A closes the pseudo channel, so everything the remote consumer still
   held goes back to Q flagged redelivered, and B drops the shadow.
 
+Basic.Get of a queue another rank owns rides a *get link* (``get=True``): the owner side
+is a pseudo channel without a consumer, and each Get on rank B is a replicated
+``link_pull`` op; when it is applied the owner runs Basic.Get on its queue for the pseudo
+channel (manual ack, so the message stays the owner's until B's client acks it) and sends
+the message — or "empty" — with the owner's remaining count back to B, which restores it
+into the get link's shadow and answers the client with a local Basic.Get on the shadow
+(reference: Basic.Get pulls one message from the QueueEntity on whatever node owns it,
+FrameStage.scala:1199-1229, QueueEntity.scala:318-393).
+
 The per-step traffic (owner -> consumer deliveries, consumer -> owner acks) is one
 variable-size all-to-all between the live ranks after the data step (``Comm.alltoall_bytes``,
 or local copies in ``LocalCluster``); it runs only while links exist, and every rank
@@ -36,16 +45,19 @@ from ..engine.control import ControlError, C
 
 LINK_PREFIX = "amq.link."
 _EPOCH_SHIFT = 40
-K_DELIVER, K_ACK = 1, 2
+K_DELIVER, K_ACK, K_GOT, K_EMPTY = 1, 2, 3, 4
+_HDR = ">BIIQBBBII"          # kind, link, epoch, tag, redelivered, |ex|, |rk|, |props|, |body|
 
 
 class Link:
-    __slots__ = ("id", "vhost", "queue", "dest", "prefetch", "shadow", "epoch", "pc", "closing")
+    __slots__ = ("id", "vhost", "queue", "dest", "prefetch", "shadow", "epoch", "pc", "closing", "get",
+                 "pending")
 
-    def __init__(self, lid, vhost, queue, dest, prefetch):
+    def __init__(self, lid, vhost, queue, dest, prefetch, get=False):
         self.id, self.vhost, self.queue, self.dest, self.prefetch = lid, vhost, queue, dest, prefetch
         self.shadow = LINK_PREFIX + str(lid)
-        self.epoch, self.pc, self.closing = 0, None, False
+        self.epoch, self.pc, self.closing, self.get = 0, None, False, bool(get)
+        self.pending = set()     # connection side of a get link: pulls not answered yet
 
 
 def parse_delivers(buf):
@@ -83,6 +95,41 @@ def parse_delivers(buf):
     return out
 
 
+def parse_get_ok(buf):
+    """Basic.GetOk + content frames -> (tag, redelivered, exchange, routing_key, raw
+    properties, body, message_count)."""
+    p = 7 + 4
+    tag = struct.unpack_from(">Q", buf, p)[0]
+    red = bool(buf[p + 8] & 1)
+    q = p + 9
+    ex = bytes(buf[q + 1:q + 1 + buf[q]])
+    q += 1 + buf[q]
+    rk = bytes(buf[q + 1:q + 1 + buf[q]])
+    q += 1 + buf[q]
+    cnt = struct.unpack_from(">I", buf, q)[0]
+    pos = 7 + struct.unpack_from(">I", buf, 3)[0] + 1
+    size = struct.unpack_from(">I", buf, pos + 3)[0]
+    blen = struct.unpack_from(">Q", buf, pos + 7 + 4)[0]
+    props = bytes(buf[pos + 7 + 12:pos + 7 + size])
+    pos += 7 + size + 1
+    body = bytearray()
+    while len(body) < blen and pos + 7 <= len(buf):
+        size = struct.unpack_from(">I", buf, pos + 3)[0]
+        body += buf[pos + 7:pos + 7 + size]
+        pos += 7 + size + 1
+    return tag, red, ex, rk, props, bytes(body), cnt
+
+
+def set_get_ok_count(frames, count):
+    """The message-count field of a rendered Basic.GetOk (the first frame of ``frames``)."""
+    b = bytearray(frames)
+    q = 7 + 4 + 9
+    q += 1 + b[q]
+    q += 1 + b[q]
+    struct.pack_into(">I", b, q, int(count))
+    return bytes(b)
+
+
 class RemoteLinks:
     """Links of one rank (one per plane).  ``alloc_conn`` / ``free_conn`` hand out the
     pseudo-connection slots (the server passes its connection-slot allocator)."""
@@ -93,6 +140,8 @@ class RemoteLinks:
         self.by_shadow = {}      # shadow queue slot -> Link (connection side)
         self._restore = []       # received deliveries, restored before the next step
         self._next_pc = plane.c_max - 2
+        self._pulled = {}        # owner side of get links: dest rank -> records of this step
+        self.got = []            # connection side: answered pulls [(pull id, link id, count | None)]
         self._alloc = alloc_conn or self._default_alloc
         self._free = free_conn or (lambda c: None)
 
@@ -109,7 +158,7 @@ class RemoteLinks:
         return bool(self.links)
 
     # ------------------------------------------------------------------ control ops
-    def open(self, lid, vhost, queue, dest, prefetch=0):
+    def open(self, lid, vhost, queue, dest, prefetch=0, get=False):
         """Replicated (control log ``link_open``): applied in the same order on every rank."""
         p = self.plane
         q = p.queues.get((vhost, queue))
@@ -117,7 +166,7 @@ class RemoteLinks:
             raise ControlError(C.NOT_FOUND, f"no queue '{queue}' in vhost '{vhost}'", 60, 20)
         if dest == p.rank and hasattr(p, "eng") and not p.info.get("persist"):
             raise ControlError(C.NOT_IMPLEMENTED, "remote consumers need the engine built with persist=1", 60, 20)
-        lk = Link(lid, vhost, queue, dest, int(prefetch) or 1024)
+        lk = Link(lid, vhost, queue, dest, int(prefetch) or 1024, get)
         p.shard_map.place(vhost, lk.shadow, dest)
         slot = p.declare_queue(vhost, lk.shadow, durable=True)
         self.links[lid] = lk
@@ -136,8 +185,9 @@ class RemoteLinks:
         pc = self._alloc()
         p.open_connection(pc, lk.vhost)
         p.open_channel(pc, 1)
-        p.qos(pc, 1, prefetch_count=lk.prefetch)
-        p.consume(pc, 1, lk.vhost, lk.queue, "amq.link-" + str(lk.id), no_ack=False)
+        if not lk.get:
+            p.qos(pc, 1, prefetch_count=lk.prefetch)
+            p.consume(pc, 1, lk.vhost, lk.queue, "amq.link-" + str(lk.id), no_ack=False)
         lk.pc, lk.epoch = pc, lk.epoch + 1
 
     def _detach(self, lk):
@@ -159,6 +209,43 @@ class RemoteLinks:
             self.plane.purge(sq.slot)
         return None
 
+    def pull(self, lid, pn, now_ms=None):
+        """Replicated (``link_pull``): one Basic.Get for get link ``lid``, pull id ``pn``.
+        The owner takes the head of the queue for its pseudo channel now (between steps)
+        and answers after the step (``outgoing``).  Returns False when the link is gone
+        (the connection side then answers Get-Empty itself)."""
+        lk = self.links.get(lid)
+        if lk is None or lk.closing or not lk.get:
+            return False
+        if lk.dest == self.plane.rank:
+            lk.pending.add(pn)
+        if lk.pc is None:   # owner side not attached here
+            return True
+        p = self.plane
+        q = p.queues.get((lk.vhost, lk.queue))
+        rec = self._pulled.setdefault(lk.dest, bytearray())
+        frames, cnt = None, 0
+        if q is not None and q.owner == p.rank:
+            try:
+                frames, cnt = (p.basic_get(lk.pc, 1, q.slot, False, now_ms) if now_ms is not None
+                               else p.basic_get(lk.pc, 1, q.slot, False))
+            except ControlError:   # the pseudo channel's delivery window is full
+                frames = None
+        if frames is None:
+            rec += struct.pack(">BIQI", K_EMPTY, lid, pn, cnt)
+        else:
+            tag, red, ex, rk, props, body, cnt = parse_get_ok(frames)
+            rec += struct.pack(_HDR + "QI", K_GOT, lid, lk.epoch, tag, int(red), len(ex), len(rk), len(props),
+                               len(body), pn, cnt) + ex + rk + props + body
+        return True
+
+    def take_gets(self):
+        """Connection side: answered pulls since the last call, [(pull id, link id, owner's
+        remaining count, or None for empty)]; the messages are in the shadows once
+        ``before_step`` ran."""
+        out, self.got = self.got, []
+        return out
+
     def shadow_of(self, lid):
         lk = self.links.get(lid)
         return lk.shadow if lk else None
@@ -177,16 +264,16 @@ class RemoteLinks:
         """After the data step: {dest rank: bytes}.  Takes the pseudo connections' bytes
         out of the step's egress {conn: bytes} (no socket behind them)."""
         p = self.plane
-        out = {}
+        out, self._pulled = self._pulled, {}
         for lk in self.links.values():
-            if lk.pc is None:
+            if lk.pc is None or lk.get:
                 continue
             buf = eg.pop(lk.pc, None)
             if not buf:
                 continue
             b = out.setdefault(lk.dest, bytearray())
             for tag, red, ex, rk, props, body in parse_delivers(buf):
-                b += struct.pack(">BIIQBBBII", K_DELIVER, lk.id, lk.epoch, tag, int(red), len(ex), len(rk),
+                b += struct.pack(_HDR, K_DELIVER, lk.id, lk.epoch, tag, int(red), len(ex), len(rk),
                                  len(props), len(body)) + ex + rk + props + body
         if self.by_shadow:
             for mid, q, _qpos, kind in p.take_link_consumed(self.by_shadow):
@@ -212,8 +299,16 @@ class RemoteLinks:
                     if lk is not None and lk.pc is not None and lk.epoch == epoch:
                         p.apply_ack(lk.pc, 1, tag)
                     continue
-                _, lid, epoch, tag, red, lex, lrk, lp, lb = struct.unpack_from(">BIIQBBBII", buf, pos)
+                if k == K_EMPTY:   # connection side: the owner's queue was empty
+                    _, lid, pn, cnt = struct.unpack_from(">BIQI", buf, pos)
+                    pos += 17
+                    self._answered(lid, pn, None)
+                    continue
+                _, lid, epoch, tag, red, lex, lrk, lp, lb = struct.unpack_from(_HDR, buf, pos)
                 pos += 28
+                if k == K_GOT:
+                    pn, cnt = struct.unpack_from(">QI", buf, pos)
+                    pos += 12
                 ex = buf[pos:pos + lex]
                 pos += lex
                 rk = buf[pos:pos + lrk]
@@ -223,13 +318,19 @@ class RemoteLinks:
                 body = buf[pos:pos + lb]
                 pos += lb
                 lk = self.links.get(lid)
-                if lk is None or lk.closing:
-                    continue   # the owner requeued it when the link closed
-                sq = p.queues.get((lk.vhost, lk.shadow))
+                sq = p.queues.get((lk.vhost, lk.shadow)) if lk is not None and not lk.closing else None
+                if k == K_GOT:
+                    self._answered(lid, pn, cnt if sq is not None else None)
                 if sq is None:
-                    continue
+                    continue   # the owner requeued it when the link closed
                 self._restore.append((sq.slot, (epoch << _EPOCH_SHIFT) | tag, 0, 0, bytes(ex), bytes(rk),
                                       bytes(props), bytes(body), True, bool(red)))
+
+    def _answered(self, lid, pn, cnt):
+        lk = self.links.get(lid)
+        if lk is not None:
+            lk.pending.discard(pn)
+        self.got.append((pn, lid, cnt))
 
     def after_step(self):
         """Finish closing links: the owner closes the pseudo channel (after this step's
@@ -252,6 +353,7 @@ class RemoteLinks:
         pseudo channel (its window was on the dead GPU) and re-attach at the queue's new
         owner after ``rehome`` (``after_rehome``)."""
         p = self.plane
+        self.lost_owner(dead)
         for lid in [l for l, lk in self.links.items() if lk.dest in dead]:
             lk = self.links.pop(lid)
             self._detach(lk)
@@ -261,6 +363,17 @@ class RemoteLinks:
                 getattr(p, "link_slots", set()).discard(sq.slot)
                 p.delete_queue(lk.vhost, lk.shadow)
             p.shard_map.placement.pop(_eid(lk.vhost, lk.shadow), None)
+
+    def lost_owner(self, dead):
+        """Connection side of get links whose queue owner died: their outstanding pulls
+        will not be answered by it (``on_failure`` runs before the re-home)."""
+        p = self.plane
+        for lk in self.links.values():
+            q = p.queues.get((lk.vhost, lk.queue))
+            if lk.get and lk.pending and q is not None and q.owner in dead:
+                for pn in sorted(lk.pending):
+                    self.got.append((pn, lk.id, None))
+                lk.pending.clear()
 
     def after_rehome(self):
         p = self.plane

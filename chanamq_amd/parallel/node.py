@@ -44,6 +44,7 @@ class ShardedNode:
         self.links = RemoteLinks(plane)
         self.log.handlers["link_open"] = self.links.open
         self.log.handlers["link_close"] = self.links.close
+        self.log.handlers["link_pull"] = self.links.pull
 
     @property
     def rank(self):

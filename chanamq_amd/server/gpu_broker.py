@@ -18,6 +18,7 @@ channel the device hands publishes / acks to the host instead of applying them
 (CK_TXBUF); Tx.Commit applies the acks between steps and injects the publishes through a
 pseudo-connection in the next step, Tx.Rollback drops them.  Not on the GPU path yet
 (540 NOT_IMPLEMENTED; the host-path broker in csrc/core serves it): Exchange.Bind/Unbind.
+Sharded: consumers and Basic.Get may name a queue another rank owns (parallel/links.py).
 """
 
 import os
@@ -174,6 +175,11 @@ class GpuBroker:
         self._free = list(range(self._top_slot, 0, -1))   # slot 0 unused
         self._link_free = list(range(self._top_slot + 1, plane.c_max - 1))
         self._links = {}        # (conn, channel, consumer tag) -> link id (remote consumers)
+        self._get_links = {}    # (vhost, queue) -> get link id (Basic.Get of remote queues)
+        self._get_wait = {}     # pull id -> (conn, channel, no_ack, link id)
+        self._get_holders = {}  # get link id -> {(conn, channel)} holding unacked Get messages
+        self._get_used = {}     # get link id -> monotonic time of its last Get
+        self._pull_seq = 0
         self._link_seq = 0
         if node is not None:
             node.links._alloc = self._alloc_link_slot
@@ -494,6 +500,8 @@ class GpuBroker:
             segs = np.concatenate([segs, np.array([(self.txc, len(inj), off)], segs.dtype)])
             used = off + len(inj)
         if self.node is not None:
+            if self._get_wait or self._get_links:
+                self._serve_gets()
             t, results = self.node.step_raw(segs, self._pin.ctypes.data, used, now)
             self._answer(results)
         else:
@@ -681,6 +689,8 @@ class GpuBroker:
             inputs = dict(inputs)
             inputs[self.txc] = inj
         if self.node is not None:
+            if self._get_wait or self._get_links:
+                self._serve_gets()
             res, results = self.node.step(inputs, now_ms=int(time.time() * 1000))
             self._answer(results)
         else:
@@ -1020,7 +1030,7 @@ class GpuBroker:
             if q.exclusive_owner not in (-1, c.id):
                 raise ControlError(C.RESOURCE_LOCKED, f"queue '{q.name}' is exclusive to another connection", 60, 70)
             if q.owner != p.rank:
-                raise ControlError(C.NOT_IMPLEMENTED, "basic.get on a queue owned by another GPU", 60, 70)
+                return self._remote_get(c, ch, vh, q, m)
             frames, _ = p.basic_get(c.id, ch, q.slot, m.no_ack, int(time.time() * 1000))
             if frames is None:
                 self._send(c, ch, Method("basic.get_empty"))
@@ -1130,8 +1140,110 @@ class GpuBroker:
                 out = reply(res)
                 if out is not None:
                     self._send(c, ch, out)
-            if c.state == "open":
+            if c.state == "open" and not (hasattr(reply, "keep_paused") and reply.keep_paused(res)):
                 self._unpause(conn)
+
+    def _remote_get(self, c, ch, vh, q, m):
+        """Basic.Get of a queue another rank owns: a pull on this rank's get link for the
+        queue (opened on first use, closed when idle); the owner's answer comes back after
+        the step and ``_serve_gets`` replies (parallel/links.py)."""
+        p, links = self.plane, self.node.links
+        key = (vh, q.name)
+        lid = self._get_links.get(key)
+        lk = links.links.get(lid) if lid is not None else None
+        if lk is not None and lk.closing:
+            lid = lk = None
+        if lk is not None and not lk.pending and not any(w[3] == lid for w in self._get_wait.values()):
+            sq = p.queues.get((vh, lk.shadow))
+            if sq is not None and p.message_count(sq.slot):   # a requeued one is still here
+                self._get_used[lid] = time.monotonic()
+                self._serve_get(c, ch, m.no_ack, lid, None)
+                return None
+        if lid is None:
+            self._link_seq += 1
+            lid = (p.rank << 24) | self._link_seq
+            self.node.submit("link_open", lid, vh, q.name, p.rank, 0, get=True)
+            self._get_links[key] = lid
+        self._pull_seq += 1
+        pn = (p.rank << 40) | self._pull_seq
+        seq = self.node.submit("link_pull", lid, pn)
+        self._get_wait[pn] = (c.id, ch, bool(m.no_ack), lid)
+        self._get_used[lid] = time.monotonic()
+
+        def reply(res, pn=pn, lid=lid, key=key):
+            if res is False:   # the link is gone (or never opened): nothing to get
+                self._get_wait.pop(pn, None)
+                if self._get_links.get(key) == lid and lid not in self.node.links.links:
+                    self._get_links.pop(key, None)
+                return Method("basic.get_empty")
+            return None
+        reply.keep_paused = lambda res: res is not False   # until the owner's answer
+        reply.abandon = lambda pn=pn: self._get_wait.pop(pn, None)
+        self._deferred[seq] = (c.id, ch, reply, m)
+        return "deferred"
+
+    def _serve_get(self, c, ch, no_ack, lid, cnt):
+        """Answer a Get from the get link's shadow queue (the message the owner sent is
+        there once ``links.before_step`` ran): GetOk with this channel's delivery tag and
+        the owner's remaining count."""
+        from ..parallel.links import set_get_ok_count
+        p = self.plane
+        lk = self.node.links.links.get(lid)
+        sq = p.queues.get((lk.vhost, lk.shadow)) if lk is not None else None
+        frames = None
+        if sq is not None:
+            try:
+                frames, left = p.basic_get(c.id, ch, sq.slot, False)
+            except (ControlError, KeyError):
+                frames = None
+        if frames is None:
+            self._send(c, ch, Method("basic.get_empty"))
+            return
+        frames = set_get_ok_count(frames, left if cnt is None else cnt)
+        if no_ack:   # consumed now: the shadow's consumed record acks it at the owner
+            p.apply_ack(c.id, ch, struct.unpack_from(">Q", frames, 11)[0])
+        else:
+            self._get_holders.setdefault(lid, set()).add((c.id, ch))
+        c.out += frames
+
+    def _serve_gets(self):
+        """Before a step: answers that came back for remote Gets; close get links idle
+        for a second with nobody holding their messages (what a closed link held goes
+        back to the owner's queue)."""
+        links = self.node.links
+        links.before_step()
+        for pn, lid, cnt in links.take_gets():
+            w = self._get_wait.pop(pn, None)
+            if w is None:
+                continue
+            conn, ch, no_ack, _ = w
+            c = self.conns.get(conn)
+            if c is None or c.state != "open" or ch in c.closing_channels:
+                continue
+            if cnt is None:
+                self._send(c, ch, Method("basic.get_empty"))
+            else:
+                self._serve_get(c, ch, no_ack, lid, cnt)
+            self._unpause(conn)
+        if not self._get_links:
+            return
+        now = time.monotonic()
+        waiting = {w[3] for w in self._get_wait.values()}
+        for key, lid in list(self._get_links.items()):
+            if lid in waiting or now - self._get_used.get(lid, 0.0) < 1.0:
+                continue
+            pc = self.plane.conns
+            hold = {(cn, ch) for cn, ch in self._get_holders.get(lid, ())
+                    if cn in self.conns and self.conns[cn].state == "open"
+                    and ch not in self.conns[cn].closing_channels and cn in pc and ch in pc[cn].channels}
+            if hold:
+                self._get_holders[lid] = hold
+                continue
+            self._get_links.pop(key)
+            self._get_holders.pop(lid, None)
+            self._get_used.pop(lid, None)
+            if lid in links.links:
+                self.node.submit("link_close", lid)
 
     def _alloc_link_slot(self):
         if not self._link_free:

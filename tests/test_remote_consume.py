@@ -204,3 +204,93 @@ def test_gpu_remote_consumer_stream_matches_single_plane(gpu, name, world):
                    [d[5] for d in b if d[5].split(b"-")[0] == seed]
     for p in cl.planes:
         assert p.memory_in_use() == 0
+
+
+# ------------------------------------------------------------------ remote Basic.Get
+def _get_setup(world, make=golden, n=5):
+    """Queue ``rq`` on rank 0 holding ``n`` messages; connection 2 on the last rank."""
+    sc = Scenario({"rq": 0}, {1: 0}, [], [{1: pubs(n, "rq", 0)}, {}])
+    cl, _ = run_cluster(sc, world, make)
+    b = world - 1
+    cl[b].open_connection(2, VH)
+    cl[b].open_channel(2, 1)
+    shadow = cl.link_open(300, VH, "rq", b, get=True)
+    return cl, b, shadow
+
+
+def _remote_get(cl, b, shadow, pn, no_ack=False, now_ms=5000):
+    """One pull, answered after a step; the answer is served from the shadow on rank b
+    like the server does (parallel/links.py, server/gpu_broker.py _serve_gets)."""
+    from chanamq_amd.parallel.links import set_get_ok_count
+    assert cl.link_pull(300, pn) is True
+    cl.step([{} for _ in cl.planes], now_ms=now_ms)
+    got = cl.links[b].take_gets()
+    assert [g[0] for g in got] == [pn]
+    cl.links[b].before_step()   # restore the fetched message into the shadow
+    _, _, cnt = got[0]
+    if cnt is None:
+        return None
+    p = cl[b]
+    frames, _ = p.basic_get(2, 1, p.queues[(VH, shadow)].slot, False)
+    return set_get_ok_count(frames, cnt)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_remote_basic_get_matches_single_plane(world):
+    """Basic.Get on rank b of a queue owned by rank 0: GetOk frames (tag, redelivered,
+    exchange, routing key, remaining count, properties, body) equal a single plane's,
+    the client's acks reach the owner, Get-Empty once drained."""
+    single = golden()
+    _topology(single)
+    single.declare_queue(VH, "rq")
+    single.bind(VH, "rq", "rx", "rq")
+    for c in (1, 2):
+        single.open_connection(c, VH)
+        single.open_channel(c, 1)
+    single.step({1: pubs(5, "rq", 0)}, now_ms=1000)
+    want = [single.basic_get(2, 1, single.queues[(VH, "rq")].slot, False)[0] for _ in range(5)]
+
+    cl, b, shadow = _get_setup(world)
+    got = [_remote_get(cl, b, shadow, pn) for pn in range(1, 6)]
+    assert got == want
+    assert _remote_get(cl, b, shadow, 6) is None          # empty
+    a = cl[0]
+    assert a.message_count(a.queues[(VH, "rq")].slot) == 0
+    # acks on rank b go back to the owner: every message released everywhere
+    cl.step([{} if r != b else {2: ack_frame(1, 5, multiple=True)} for r in range(world)], now_ms=6000)
+    for k in range(3):
+        cl.step([{} for _ in range(world)], now_ms=6001 + k)
+    assert all(p.memory_in_use() == 0 for p in cl.planes)
+
+
+def test_remote_basic_get_unacked_returns_on_link_close():
+    """A manual-ack Get never acked: closing the get link (idle close in the server)
+    returns the message to the owner's queue, flagged redelivered."""
+    cl, b, shadow = _get_setup(2, n=3)
+    assert _remote_get(cl, b, shadow, 1) is not None
+    cl[b].close_channel(2, 1)
+    cl.link_close(300)
+    for k in range(3):
+        cl.step([{}, {}], now_ms=7000 + k)
+    a = cl[0]
+    assert a.message_count(a.queues[(VH, "rq")].slot) == 3
+    frames, cnt = a.basic_get(1, 1, a.queues[(VH, "rq")].slot, True)
+    assert frames[7 + 4 + 8] & 1 and cnt == 2           # redelivered, two left
+
+
+@pytest.mark.gpu
+def test_gpu_remote_basic_get_matches_golden(gpu):
+    """GPU planes (LocalCluster on one device): the remote GetOk frames equal the golden
+    cluster's, and acks release everything."""
+    want = []
+    cl, b, shadow = _get_setup(2)
+    for pn in range(1, 4):
+        want.append(_remote_get(cl, b, shadow, pn))
+    gcl, gb, gshadow = _get_setup(2, make=gpu_plane)
+    got = [_remote_get(gcl, gb, gshadow, pn) for pn in range(1, 4)]
+    assert got == want and all(g is not None for g in got)
+    gcl.step([{}, {2: ack_frame(1, 3, multiple=True)}], now_ms=6000)
+    for k in range(3):
+        gcl.step([{}, {}], now_ms=6001 + k)
+    a = gcl[0]
+    assert a.message_count(a.queues[(VH, "rq")].slot) == 2

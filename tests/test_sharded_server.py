@@ -81,6 +81,27 @@ def test_cross_rank_routing_and_replicated_topology(cluster):
     a.basic_consume("qa", "ca2", no_ack=True)
     p.basic_publish("sx", "a.end", b"end")
     assert a.consume_n(1)[0].body == b"end"
+    # Basic.Get on rank 1 of rank 0's queue (pulled through a get link)
+    a.basic_cancel("ca2")
+    c0.process(0.3)
+    for i in range(3):
+        p.basic_publish("sx", "a.g", b"g%d" % i)
+    c0.process(0.5)
+    g = c1.channel()
+    g0 = g.basic_get("qa")
+    assert g0.body == b"g0" and g0.method.message_count == 2 and not g0.method.redelivered
+    g1 = g.basic_get("qa", no_ack=True)
+    assert g1.body == b"g1" and g1.method.delivery_tag == g0.method.delivery_tag + 1
+    g.basic_nack(g0.method.delivery_tag, requeue=True)     # back at the head (of the get link)
+    again = g.basic_get("qa")
+    assert again.body == b"g0" and again.method.redelivered
+    g.basic_ack(again.method.delivery_tag)
+    assert g.basic_get("qa", no_ack=True).body == b"g2"
+    assert g.basic_get("qa") is None
+    c1.process(1.5)   # the idle get link closes; acks reached the owner: nothing comes back
+    a.basic_consume("qa", "ca3", no_ack=True)
+    p.basic_publish("sx", "a.end", b"end2")
+    assert a.consume_n(1)[0].body == b"end2"
     c0.close()
     c1.close()
 
