@@ -13,6 +13,7 @@
 #include <chrono>
 #include <cstdio>
 #include <cstring>
+#include <memory>
 #include <random>
 #include <stdexcept>
 #include <string>
@@ -143,7 +144,8 @@ static void broker_and_loadgen(const std::string& dir) {
   cfg.heartbeat = 0;
   cfg.data_dir = dir;
   cfg.fsync = false;
-  Broker b(cfg);
+  auto bp = std::make_unique<Broker>(cfg);
+  Broker& b = *bp;
   b.start();
   for (bool ack : {true, false}) {
     LoadSpec s;
@@ -167,7 +169,11 @@ static void frontend_echo() {
   cfg.port = 0;
   cfg.io_threads = 2;
   cfg.idle_step_ms = 1.0;
-  Frontend f(cfg, (const CmqEngineApi*)eng.c_api());
+  // heap objects: std::mutex members are statically initialised (no pthread_mutex_init),
+  // so a mutex on stack memory an earlier object's destroyed mutex used looks like that
+  // destroyed mutex to ThreadSanitizer
+  auto fp = std::make_unique<Frontend>(cfg, (const CmqEngineApi*)eng.c_api());
+  Frontend& f = *fp;
   f.start();
   int fd = ::socket(AF_INET, SOCK_STREAM, 0);
   sockaddr_in a{};
