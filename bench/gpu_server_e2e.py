@@ -37,6 +37,12 @@ SPECS = {
     "config4_durable_4KB_confirms": dict(producers=16, consumers=4, queues=4, msg_size=4096, auto_ack=False,
                                          prefetch=1000, persistent=True, durable=True, confirm=True,
                                          confirm_window=512),
+    # BASELINE config 5 on one GPU: 64P x 64C manual ack, every 2nd ack of each consumer is
+    # Basic.Nack(multiple, requeue) (redelivery storm); a 256 MB memory watermark turns
+    # producers off with Channel.Flow and back on below 128 MB
+    "config5_storm_64p64c_nack_flow": dict(producers=64, consumers=64, queues=16, msg_size=1024, auto_ack=False,
+                                           prefetch=512, nack_every=2,
+                                           _broker=dict(mem_high_watermark=256 << 20)),
 }
 
 
@@ -79,15 +85,30 @@ def run_one(core, name, spec, io, io_threads, seconds, rate=0.0, lg_threads=12, 
     if persist:
         store = core.Store()
         store.open(store_dir or tempfile.mkdtemp(prefix="cmq-gpu-store-"), True)
+    bkw = dict(spec.get("_broker", {}))
+    spec = {k: v for k, v in spec.items() if not k.startswith("_")}
     b = GpuBroker(plane, idle_step_ms=0.5, store=store, io=io, io_threads=io_threads,
-                  per_conn_read=128 << 10, fe_cfg=FE_CFG).start()
+                  per_conn_read=128 << 10, fe_cfg=FE_CFG, **bkw).start()
     t0 = time.time()
     cpu0 = thread_cpu()
+    timeline, done = [], [False]
+
+    def sample():   # (s, live MB, blocked, published, delivered) every 100 ms
+        while not done[0]:
+            fs = getattr(b, "_fe_stats", None) or {}
+            timeline.append((round(time.time() - t0, 2), round(fs.get("live_bytes", 0) / 2**20, 1), int(b.blocked),
+                             fs.get("published", 0), fs.get("delivered", 0)))
+            time.sleep(0.1)
+    import threading
+    smp = threading.Thread(target=sample, daemon=True)
+    smp.start()
     try:
         r = core.run_load(dict(port=b.port, seconds=seconds, warmup=1.0, queue=f"e2e.{name}",
                                exchange=f"e2e.x.{name}", threads=lg_threads, consumer_threads=cons_threads,
                                rate=rate, **spec))
     finally:
+        done[0] = True
+        smp.join()
         cpu1 = thread_cpu()
         after = {}
         try:   # the broker after the load: what stays live / pinned once every client is gone
@@ -140,6 +161,7 @@ def run_one(core, name, spec, io, io_threads, seconds, rate=0.0, lg_threads=12, 
             store.close()
     lc = getattr(plane, "last_counters", {}) or {}
     r["after"] = after
+    r["timeline"] = timeline
     r["thread_cpu_s"] = {k: round(cpu1[k] - cpu0.get(k, 0.0), 2) for k in cpu1 if cpu1[k] - cpu0.get(k, 0.0) > 0.05}
     st = dict(b.stats)
     fes = getattr(b, "_fe_stats", None) or {}
@@ -151,7 +173,7 @@ def run_one(core, name, spec, io, io_threads, seconds, rate=0.0, lg_threads=12, 
                                                 "submit_s", "rx_bytes", "tx_bytes", "held_steps", "published",
                                                 "delivered", "routed", "dropped_nomem", "ring_full", "unroutable",
                                                 "expired", "ctrl", "live_msgs", "live_bytes", "log_used")},
-             flow_off=st.get("flow_off", 0),
+             flow_off_server=st.get("flow_off", 0),
              last_step={k: lc.get(k) for k in ("n_ring_full", "n_dropped_nomem")},
              store=getattr(b, "_pw_stats", None))
     del plane
@@ -186,7 +208,8 @@ def main():
                                cons_threads=args.consumer_threads)
                 results.append(r)
                 print(json.dumps({k: r[k] for k in ("name", "io", "io_threads", "recv_msgs_per_s", "sent_msgs_per_s",
-                                                    "confirmed_per_s", "p50_us", "p99_us", "error", "front_end",
+                                                    "confirmed_per_s", "p50_us", "p99_us", "error", "redelivered",
+                                                    "requeued", "flow_off", "flow_off_server", "front_end",
                                                     "store", "thread_cpu_s", "cpu_consumers_s",
                                                     "cpu_producers_s")}),
                       flush=True)

@@ -243,6 +243,7 @@ class GpuDataPlane(ControlState):
         s = chan.conn * self.chpc + chan.local
         for name, v, dt in (("ch_next_tag", 1, np.uint64), ("ch_uhead", 1, np.uint64),
                             ("ch_ack_upto", 0, np.uint64), ("ch_req_upto", 0, np.uint64),
+                            ("ch_mlo", 0xFFFFFFFF, np.uint32), ("ch_mhi", 0, np.uint32),
                             ("ch_confirm_next", 1, np.uint64), ("ch_confirm", 0, np.uint32),
                             ("ch_pub_cnt", 0, np.uint32), ("ch_pub_fail", 0, np.uint32), ("ch_prefetch", 0, np.uint32),
                             ("ch_global", 0, np.uint32), ("ch_flow", 1, np.uint32),

@@ -164,9 +164,8 @@ class GoldenDataPlane(ControlState):
         st = self.ch[s]
         if tag == 0 and multiple:
             tag = st["next_tag"] - 1
-        if multiple:
-            key = "req_upto" if requeue else "ack_upto"
-            st[key] = max(st[key], tag)
+        if multiple:   # resolved in wire order at the window advance: first cover wins
+            st.setdefault("msettles", []).append((tag, bool(requeue)))
         elif st["uhead"] <= tag < st["next_tag"]:
             sl = st["slots"].get(tag)
             if sl and sl["state"] == "pending":
@@ -513,13 +512,26 @@ class GoldenDataPlane(ControlState):
             contiguous = True
             t = st["uhead"]
             released = 0
+            # multiple settles of the step: record-breaking uptos in wire order (a tag's
+            # fate is the first settle that covers it; spec of chan_advance_one)
+            marks, top = [], 0
+            for up, rq in st.pop("msettles", ()):
+                if up > top:
+                    marks.append((up, rq))
+                    top = up
             while t < st["next_tag"]:
                 sl = st["slots"].get(t)
                 state = sl["state"]
-                if state == "pending" and t <= st["ack_upto"]:
-                    state = "acked"
-                if state == "pending" and t <= st["req_upto"]:
-                    state = "requeue"
+                if state == "pending":
+                    if t <= st["ack_upto"]:
+                        state = "acked"
+                    elif t <= st["req_upto"]:
+                        state = "requeue"
+                    else:
+                        for up, rq in marks:
+                            if t <= up:
+                                state = "requeue" if rq else "acked"
+                                break
                 if state == "acked":
                     self._consumed(sl["msg"], sl["q"], sl["qpos"], 0)
                     self._release(sl["msg"])

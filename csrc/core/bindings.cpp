@@ -287,7 +287,7 @@ PYBIND11_MODULE(_core, m) {
     S("routing_key", routing_key); S("queue", queue); S("queues", queues); S("auto_ack", auto_ack);
     S("prefetch", prefetch); S("persistent", persistent); S("durable", durable); S("confirm", confirm);
     S("rate", rate); S("threads", threads); S("warmup", warmup); S("confirm_window", confirm_window);
-    S("consumer_threads", consumer_threads);
+    S("consumer_threads", consumer_threads); S("nack_every", nack_every);
 #undef S
     LoadResult r;
     {
@@ -299,6 +299,7 @@ PYBIND11_MODULE(_core, m) {
     o["p95_us"] = r.p95_us; o["p99_us"] = r.p99_us; o["error"] = r.error;
     o["confirmed"] = r.confirmed; o["nacked"] = r.nacked; o["threads"] = r.threads;
     o["cpu_consumers_s"] = r.cpu_consumers_s; o["cpu_producers_s"] = r.cpu_producers_s;
+    o["redelivered"] = r.redelivered; o["requeued"] = r.requeued; o["flow_off"] = r.flow_off;
     return o;
   });
   m.def("decode_method", &decode);

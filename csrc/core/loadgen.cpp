@@ -173,7 +173,9 @@ struct Peer {
   // consumer
   bool want_body = false;
   u64 body_left = 0, last_tag = 0, unacked = 0;
-  std::atomic<u64> recv{0};
+  std::atomic<u64> recv{0}, redelivered{0}, requeued{0}, flow_off{0};
+  u64 acks = 0, first_unacked = 0;
+  bool cur_red = false;
   u8 ts[8];
   u32 tsn = 0;
   bool writable = true;
@@ -328,8 +330,9 @@ LoadResult run_load(const LoadSpec& s) {
       bool any_producer = false;
       for (Peer* p : mine) any_producer |= p->producer;
       auto pump = [&](Peer* p) {   // producer: send until the socket is full or paced out
-        while (!stop && p->flow) {
+        while (!stop) {
           if (p->out_pos >= p->out.size()) {
+            if (!p->flow) return;   // paused: a started batch is still finished (whole frames)
             const u64 sent = p->sent.load(std::memory_order_relaxed);
             if (rate > 0 && (double)(sent + K) > rate * ((mono_ns() - t_start) * 1e-9)) return;
             if (window && sent + K > window + p->confirmed.load(std::memory_order_relaxed) +
@@ -370,6 +373,8 @@ LoadResult run_load(const LoadSpec& s) {
             if (cls == 60 && mid == 60) {             // Basic.Deliver
               u32 tl = pl[4];
               p->last_tag = rd64(pl + 5 + tl);
+              p->cur_red = pl[5 + tl + 8] & 1;
+              if (p->cur_red) p->redelivered.fetch_add(1, std::memory_order_relaxed);
               p->want_body = true;
               p->tsn = 0;
             } else if (cls == 60 && (mid == 80 || mid == 120)) {   // confirm Ack / Nack
@@ -380,11 +385,17 @@ LoadResult run_load(const LoadSpec& s) {
               (mid == 80 ? p->confirmed : p->nacked).fetch_add(cnt, std::memory_order_relaxed);
             } else if (cls == 20 && mid == 20) {      // Channel.Flow
               p->flow = pl[4] & 1;
+              if (!p->flow && p->producer) p->flow_off.fetch_add(1, std::memory_order_relaxed);
               std::string fo;
               Method m = make_method(20, 21);
               m.args[0].i = p->flow;
               append_method_frame(fo, 1, m);
-              send_small(p, fo);
+              if (p->producer && p->out_pos < p->out.size()) {
+                p->out += fo;   // after the partly sent batch: frames must not interleave
+                p->writable = true;
+              } else {
+                send_small(p, fo);
+              }
             } else if (cls == 10 && mid == 50) {
               throw std::runtime_error("loadgen: connection closed by broker");
             } else if (cls == 20 && mid == 40) {
@@ -404,7 +415,7 @@ LoadResult run_load(const LoadSpec& s) {
               p->want_body = false;
               p->recv.fetch_add(1, std::memory_order_relaxed);
               ++p->unacked;
-              if (p->tsn == 8) {
+              if (p->tsn == 8 && !p->cur_red) {   // latency of first deliveries only
                 i64 t0;
                 memcpy(&t0, p->ts, 8);
                 h.add((mono_ns() - t0) / 1000.0);
@@ -423,36 +434,34 @@ LoadResult run_load(const LoadSpec& s) {
           if (p->in.size() - p->ilen < (64u << 10)) p->in.resize(p->in.size() * 2);   // a frame larger than the buffer
         }
       };
+      auto ack = [&](Peer* p) {   // everything up to last_tag: Ack, or every nack_every-th time Nack+requeue
+        std::string ak;
+        const bool nack = s.nack_every > 0 && ++p->acks % (u64)s.nack_every == 0;
+        Method m = make_method(60, nack ? 120 : 80);
+        m.args[0].i = (i64)p->last_tag;
+        m.args[1].i = 1;
+        if (nack) {
+          m.args[2].i = 1;
+          p->requeued.fetch_add(p->unacked, std::memory_order_relaxed);
+        }
+        append_method_frame(ak, 1, m);
+        send_small(p, ak);
+        p->unacked = 0;
+      };
       auto drain = [&](Peer* p) {
         for (;;) {
           ssize_t k = ::recv(p->cl.fd, p->in.data() + p->ilen, p->in.size() - p->ilen, 0);
           if (k > 0) {
             p->ilen += (size_t)k;
             parse(p);
-            if (!p->producer && !s.auto_ack && p->unacked >= ack_every) {
-              std::string ak;
-              Method m = make_method(60, 80);
-              m.args[0].i = (i64)p->last_tag;
-              m.args[1].i = 1;
-              append_method_frame(ak, 1, m);
-              send_small(p, ak);
-              p->unacked = 0;
-            }
+            if (!p->producer && !s.auto_ack && p->unacked >= ack_every) ack(p);
             continue;
           }
           if (k == 0) throw std::runtime_error("loadgen: broker closed the connection");
           if (errno == EINTR) continue;
           break;
         }
-        if (!p->producer && !s.auto_ack && p->unacked) {   // buffer ran dry: ack what we have
-          std::string ak;
-          Method m = make_method(60, 80);
-          m.args[0].i = (i64)p->last_tag;
-          m.args[1].i = 1;
-          append_method_frame(ak, 1, m);
-          send_small(p, ak);
-          p->unacked = 0;
-        }
+        if (!p->producer && !s.auto_ack && p->unacked) ack(p);   // buffer ran dry: settle what we have
       };
       for (Peer* p : mine) if (p->ilen) parse(p);
       while (!stop) {
@@ -481,15 +490,21 @@ LoadResult run_load(const LoadSpec& s) {
   for (int t = 0; t < nthreads; ++t) th.emplace_back(worker, t);
   // warm-up excluded from the counts: snapshot after `warmup` seconds
   const double warm = std::max(0.0, s.warmup);
-  u64 sent0 = 0, recv0 = 0, conf0 = 0;
+  u64 sent0 = 0, recv0 = 0, conf0 = 0, red0 = 0, rq0 = 0, fl0 = 0;
   if (warm > 0) {
     std::this_thread::sleep_for(std::chrono::milliseconds((i64)(warm * 1000)));
-    for (auto& p : peers) { sent0 += p->sent; recv0 += p->recv; conf0 += p->confirmed; }
+    for (auto& p : peers) {
+      sent0 += p->sent; recv0 += p->recv; conf0 += p->confirmed;
+      red0 += p->redelivered; rq0 += p->requeued; fl0 += p->flow_off;
+    }
   }
   const i64 t_meas = mono_ns();
   std::this_thread::sleep_for(std::chrono::milliseconds((i64)(s.seconds * 1000)));
-  u64 s_sent = 0, s_recv = 0, s_conf = 0, s_nack = 0;
-  for (auto& p : peers) { s_sent += p->sent; s_recv += p->recv; s_conf += p->confirmed; s_nack += p->nacked; }
+  u64 s_sent = 0, s_recv = 0, s_conf = 0, s_nack = 0, s_red = 0, s_rq = 0, s_fl = 0;
+  for (auto& p : peers) {
+    s_sent += p->sent; s_recv += p->recv; s_conf += p->confirmed; s_nack += p->nacked;
+    s_red += p->redelivered; s_rq += p->requeued; s_fl += p->flow_off;
+  }
   const i64 t_end = mono_ns();
   stop = true;
   for (auto& t : th) t.join();
@@ -501,6 +516,9 @@ LoadResult run_load(const LoadSpec& s) {
   r.received = s_recv - recv0;
   r.confirmed = s_conf - conf0;
   r.nacked = s_nack;
+  r.redelivered = s_red - red0;
+  r.requeued = s_rq - rq0;
+  r.flow_off = s_fl - fl0;
   r.p50_us = all.q(0.50);
   r.p95_us = all.q(0.95);
   r.p99_us = all.q(0.99);

@@ -21,10 +21,15 @@ struct LoadSpec {
   double warmup = 0; // seconds excluded from the counts
   int confirm_window = 0;    // confirm mode: max unconfirmed publishes per producer (PerfTest -c), 0 = unlimited
   int consumer_threads = 0;  // of `threads`, serving consumers (0 = half)
+  int nack_every = 0;        // manual ack: every n-th ack of a consumer is Basic.Nack(multiple,
+                             // requeue) instead (redelivery storm, BASELINE config 5)
 };
 
 struct LoadResult {
   unsigned long long sent = 0, received = 0, confirmed = 0, nacked = 0;
+  unsigned long long redelivered = 0;   // deliveries flagged redelivered (within received)
+  unsigned long long requeued = 0;      // messages the consumers nacked back (nack_every)
+  unsigned long long flow_off = 0;      // Channel.Flow(active=false) received by producers
   int threads = 0;
   double cpu_consumers_s = 0, cpu_producers_s = 0;   // thread CPU time of the load generator
   double elapsed = 0, p50_us = 0, p95_us = 0, p99_us = 0;

@@ -947,16 +947,22 @@ DEV u32 build_keyvec(const DS& d, const u8* key, u32 len, u32 pi) {
 }
 
 // K9 ack mark (AMQChannel.scala:128-174): single tag -> its window slot; multiple -> the
-// channel's ack/requeue watermark.  Marks only depend on earlier steps' deliveries.
-DEV void apply_ack(const DS& d, const Ack& a) {
+// record (tag resolved) stays in d.acks and the channel's [first, last] ack index range
+// grows, so k_chan_advance resolves the step's multiple settles in wire order (ack index
+// = command order): a tag's fate is the first settle covering it, e.g. Nack(4, requeue)
+// then Ack(8) requeues 1-4.  Marks only depend on earlier steps' deliveries.
+DEV void apply_ack(const DS& d, Ack a, u32 ai) {
   const u32 ch = a.chslot;
-  if (ch == INVALID) return;
+  if (ch == INVALID) { d.acks[ai] = a; return; }
   const u64 nt = d.ch_next_tag[ch];
   u64 tag = a.tag;
   if (tag == 0 && a.multiple) tag = nt - 1;  // ack everything outstanding
+  a.tag = tag;
+  d.acks[ai] = a;
   const bool requeue = (a.kind != CK_ACK) && a.requeue;
   if (a.multiple) {
-    atomicMax((unsigned long long*)(requeue ? &d.ch_req_upto[ch] : &d.ch_ack_upto[ch]), (unsigned long long)tag);
+    atomicMin(&d.ch_mlo[ch], ai);
+    atomicMax(&d.ch_mhi[ch], ai);
   } else if (tag >= d.ch_uhead[ch] && tag < nt) {
     USlot& u = d.uwin[(u64)ch * (d.ucap_mask + 1) + ((tag - 1) & d.ucap_mask)];
     atomicCAS(&u.state, (u32)US_PENDING, requeue ? (u32)US_REQUEUE : (u32)US_ACKED);
@@ -1117,8 +1123,7 @@ __global__ __launch_bounds__(256) void k_decode(DS d) {
     if (c.kind == CK_ACK) { a.multiple = bits & 1; a.requeue = 0; }
     else if (c.kind == CK_REJECT) { a.multiple = 0; a.requeue = bits & 1; }
     else { a.multiple = bits & 1; a.requeue = (bits >> 1) & 1; }
-    d.acks[ai] = a;
-    apply_ack(d, a);   // fused K9 mark: k_chan_advance resolves the window next
+    apply_ack(d, a, ai);   // fused K9 mark: k_chan_advance resolves the window next
   }
 }
 
@@ -2060,46 +2065,77 @@ DEV void wave_consumed(const DS& d, u32 msg, u32 q, u64 qpos, u32 kind, bool val
 }
 
 
-// ============================================================================ K9 acks
-__global__ void k_acks(DS d) {
-  u32 i = blockIdx.x * blockDim.x + threadIdx.x;
-  u32 n = d.ctr->n_acks;
-  if (n > d.ack_max) n = d.ack_max;
-  if (i >= n) return;
-  Ack a = d.acks[i];
-  u32 ch = a.chslot;
-  if (ch == INVALID) return;
-  u64 nt = d.ch_next_tag[ch];
-  u64 tag = a.tag;
-  if (tag == 0 && a.multiple) tag = nt - 1;  // ack everything outstanding
-  bool requeue = (a.kind != CK_ACK) && a.requeue;
-  if (a.multiple) {
-    atomicMax((unsigned long long*)(requeue ? &d.ch_req_upto[ch] : &d.ch_ack_upto[ch]),
-              (unsigned long long)tag);
-  } else if (tag >= d.ch_uhead[ch] && tag < nt) {
-    USlot& u = d.uwin[(u64)ch * (d.ucap_mask + 1) + ((tag - 1) & d.ucap_mask)];
-    atomicCAS(&u.state, (u32)US_PENDING, requeue ? (u32)US_REQUEUE : (u32)US_ACKED);
-  }
-  if (atomicExch(&d.ch_dirty[ch], 1u) == 0) {
-    u32 k = atomicAdd(d.n_dirty, 1u);
-    d.dirty_list[k] = ch;
-  }
-  atomicAdd(&d.ctr->n_acked, 1u);
-}
-
+// ============================================================================ K9 window advance
 // one block (4 waves) per dirty channel: resolve marks, release/requeue, advance the
 // window head over the contiguous run of finished slots, 256 slots per iteration
-DEV void chan_advance_one(const DS& d, u32 ch, u32 tid, u32 lane, u32 w, u32* s_first, u32* s_done);
+#define MS_MAX 256   // multiple settles per channel per step resolved exactly (more: folded)
+struct MsLds {
+  u64 up[MS_MAX];
+  u32 rq[MS_MAX];
+  u32 wc[4];
+  u32 n, nb;
+  unsigned long long ovf_a, ovf_r;
+};
+DEV void chan_advance_one(const DS& d, u32 ch, u32 tid, u32 lane, u32 w, u32* s_first, u32* s_done, MsLds& ms);
 __global__ __launch_bounds__(256) void k_chan_advance(DS d) {
   __shared__ u32 s_first[4];
   __shared__ u32 s_done[4];
+  __shared__ MsLds ms;
   const u32 tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
   const u32 nd = *d.n_dirty;
   for (u32 wv = blockIdx.x; wv < nd; wv += gridDim.x) chan_advance_one(d, d.dirty_list[wv], tid, lane, w, s_first,
-                                                                        s_done);
+                                                                        s_done, ms);
 }
 
-DEV void chan_advance_one(const DS& d, u32 ch, u32 tid, u32 lane, u32 w, u32* s_first, u32* s_done) {
+// the channel's multiple settles of this step (ack indices [lo, hi]) in wire order, reduced
+// to record-breaking uptos: ms.up[0..nb) increasing, the first one >= t decides tag t
+DEV void collect_settles(const DS& d, u32 ch, u32 tid, u32 lane, u32 w, MsLds& ms) {
+  const u32 lo = d.ch_mlo[ch], hi = d.ch_mhi[ch];
+  if (tid == 0) { ms.n = 0; ms.nb = 0; ms.ovf_a = 0; ms.ovf_r = 0; }
+  __syncthreads();
+  if (lo == INVALID) return;   // block-uniform
+  for (u32 base = lo; base <= hi; base += 256) {
+    const u32 i = base + tid;
+    bool take = false;
+    Ack a;
+    a.tag = 0; a.kind = 0; a.requeue = 0;
+    if (i <= hi) {
+      a = d.acks[i];
+      take = a.chslot == ch && a.multiple;
+    }
+    const bool rq = (a.kind != CK_ACK) && a.requeue;
+    const u64 m = __ballot(take);
+    if (lane == 0) ms.wc[w] = (u32)__popcll(m);
+    __syncthreads();
+    u32 pos = ms.n + (u32)__popcll(m & lanemask_lt());
+    for (u32 k = 0; k < w; ++k) pos += ms.wc[k];
+    if (take) {
+      if (pos < MS_MAX) { ms.up[pos] = a.tag; ms.rq[pos] = rq; }
+      else atomicMax(rq ? &ms.ovf_r : &ms.ovf_a, (unsigned long long)a.tag);
+    }
+    __syncthreads();
+    if (tid == 0) ms.n += ms.wc[0] + ms.wc[1] + ms.wc[2] + ms.wc[3];
+    __syncthreads();
+  }
+  if (tid == 0) {
+    const u32 n = ms.n < MS_MAX ? ms.n : MS_MAX;
+    u64 top = 0;
+    u32 nb = 0;
+    for (u32 k = 0; k < n; ++k)
+      if (ms.up[k] > top) { ms.up[nb] = ms.up[k]; ms.rq[nb] = ms.rq[k]; ++nb; top = ms.up[k]; }
+    const u64 oa = ms.ovf_a, orq = ms.ovf_r;   // past MS_MAX: the larger cover, appended
+    const u64 om = oa > orq ? oa : orq;
+    if (om > top && nb < MS_MAX) { ms.up[nb] = om; ms.rq[nb] = orq > oa; ++nb; }
+    ms.nb = nb;
+    d.ch_mlo[ch] = INVALID;
+    d.ch_mhi[ch] = 0;
+  }
+  __syncthreads();
+}
+
+DEV void chan_advance_one(const DS& d, u32 ch, u32 tid, u32 lane, u32 w, u32* s_first, u32* s_done, MsLds& ms) {
+  collect_settles(d, ch, tid, lane, w, ms);
+  const u32 nb = ms.nb;
   const u64 head = d.ch_uhead[ch], nt = d.ch_next_tag[ch];
   const u64 aup = d.ch_ack_upto[ch], rup = d.ch_req_upto[ch];
   USlot* win = d.uwin + (u64)ch * (d.ucap_mask + 1);
@@ -2115,8 +2151,13 @@ DEV void chan_advance_one(const DS& d, u32 ch, u32 tid, u32 lane, u32 w, u32* s_
     if (valid) {
       u = win[(t - 1) & d.ucap_mask];
       st = u.state;
-      if (st == US_PENDING && t <= aup) st = US_ACKED;
-      if (st == US_PENDING && t <= rup) st = US_REQUEUE;
+      if (st == US_PENDING) {   // host marks (between steps) first, then this step's settles
+        if (t <= aup) st = US_ACKED;
+        else if (t <= rup) st = US_REQUEUE;
+        else
+          for (u32 k = 0; k < nb; ++k)
+            if (t <= ms.up[k]) { st = ms.rq[k] ? US_REQUEUE : US_ACKED; break; }
+      }
     }
     const bool acked = valid && st == US_ACKED;
     const bool req = valid && st == US_REQUEUE;

@@ -154,6 +154,8 @@ struct DS {
   u64* ch_uhead;
   u64* ch_ack_upto;
   u64* ch_req_upto;
+  u32* ch_mlo;        // this step's multiple settles of the channel: first / last ack index
+  u32* ch_mhi;        // (INVALID / 0 when none; reset by k_chan_advance)
   u32* ch_prefetch;
   u32* ch_global;
   u32* ch_flow;

@@ -319,6 +319,8 @@ class Engine {
     d_.ch_uhead = (u64*)dev("ch_uhead", 8ull * nch);
     d_.ch_ack_upto = (u64*)dev("ch_ack_upto", 8ull * nch);
     d_.ch_req_upto = (u64*)dev("ch_req_upto", 8ull * nch);
+    d_.ch_mlo = (u32*)dev("ch_mlo", 4ull * nch);
+    d_.ch_mhi = (u32*)dev("ch_mhi", 4ull * nch);
     d_.ch_prefetch = (u32*)dev("ch_prefetch", 4ull * nch);
     d_.ch_global = (u32*)dev("ch_global", 4ull * nch);
     d_.ch_flow = (u32*)dev("ch_flow", 4ull * nch);
@@ -417,6 +419,7 @@ class Engine {
     fill("conn_ret_min", 0xff);
     fill("conn_dlast", 0xff);
     fill("x_hval", 0xff);
+    fill("ch_mlo", 0xff);
     fill("d_exch", 0xff);
     std::vector<u32> fl(d_.msg_max);
     for (u32 i = 0; i < d_.msg_max; ++i) fl[i] = d_.msg_max - 1 - i;

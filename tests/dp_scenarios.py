@@ -237,7 +237,29 @@ def sc_ring_growth(dp):
     return [{1: s[0]}, {1: s[1]}, {1: s[2]}, {"__consume__": [(2, 1, "grow", "gc")]}, {}, {}]
 
 
+def sc_mixed_multiple_settles(dp):
+    """Several multiple-settles of both kinds on one channel in one step: each tag's fate
+    is the first settle (wire order) that covers it (AMQChannel.scala:128-174), not
+    "acks win" — a nack-requeue storm acks and nacks alternately within one step."""
+    dp.declare_queue(VH, "mq")
+    dp.open_connection(1, VH)
+    dp.open_channel(1, 1)
+    dp.open_connection(2, VH)
+    dp.open_channel(2, 1)
+    dp.qos(2, 1, prefetch_count=20)
+    dp.consume(2, 1, VH, "mq", "m", no_ack=False)
+    s = publish_stream(16, "", lambda i: "mq", 20, seed=40)
+
+    def nack(tag, multiple=True, requeue=True):
+        return render_command(1, Method("basic.nack", delivery_tag=tag, multiple=multiple, requeue=requeue))
+    mixed = (nack(4) + ack_frame(1, 8, multiple=True) + nack(10, requeue=False) + ack_frame(1, 12, multiple=False)
+             + nack(14))
+    rev = ack_frame(1, 18, multiple=True) + nack(22) + ack_frame(1, 20, multiple=True)
+    return [{1: s}, {2: mixed}, {}, {2: rev}, {}, {2: ack_frame(1, 0)}, {}]
+
+
 SCENARIOS = {
+    "mixed_multiple_settles": sc_mixed_multiple_settles,
     "ring_growth": sc_ring_growth,
     "confirm_ring_full": sc_confirm_ring_full,
     "big_segment": sc_big_segment,

@@ -156,3 +156,17 @@ def test_ring_growth_stores_and_delivers_everything():
     assert len(d) == 31 and [c.method.delivery_tag for c in d] == list(range(1, 32))
     assert g.queues[("AMQ.DEFAULT", "grow")].capacity >= 31
     assert g.counters["n_ring_full"] == 0
+
+
+def test_mixed_multiple_settles_first_cover_wins():
+    """nack(4,multiple,requeue) ack(8,multiple) nack(10,multiple,drop) ack(12) nack(14,
+    multiple,requeue) in one step: 1-4, 11, 13, 14 come back redelivered, 5-8 and 12 are
+    acked, 9-10 dropped; the reversed order later (ack 18 multiple, nack 22, ack 20) acks
+    up to 18 and requeues 19-22."""
+    g, outs, pc = run_sc("mixed_multiple_settles")
+    d = [c for c in pc[2] if c.method.name == "basic.deliver"]
+    first = {c.method.delivery_tag: c.body for c in d[:16]}
+    red = [c for c in d[16:] if c.method.redelivered]
+    assert [c.body for c in red[:7]] == [first[t] for t in (1, 2, 3, 4, 11, 13, 14)]
+    assert not any(c.body in (first[9], first[10]) for c in d[16:])
+    assert g.memory_in_use() == 0
