@@ -40,8 +40,9 @@ def broker(request):
 
 
 class Soak:
-    def __init__(self, port):
+    def __init__(self, port, ports=None):
         self.port = port
+        self.ports = ports or {}   # client role -> port (sharded: a rank per role)
         self.lock = threading.Lock()
         self.done = []            # bodies settled as consumed (ack / auto-ack)
         self.routable, self.unroutable, self.returned = set(), set(), []
@@ -49,8 +50,8 @@ class Soak:
         self.pubs_left = N_PUB
         self.errors = []
 
-    def conn(self):
-        return Connection(port=self.port, vhost="/")
+    def conn(self, role=""):
+        return Connection(port=self.ports.get(role, self.port), vhost="/")
 
     def finished(self):
         with self.lock:
@@ -63,7 +64,7 @@ class Soak:
     # ------------------------------------------------------------------ clients
     def publisher(self, pid):
         rng = random.Random(pid)
-        c = self.conn()
+        c = self.conn("pub%d" % pid)
         ch = c.channel()
         ch.confirm_select()
         mine_r, mine_u = set(), set()
@@ -91,7 +92,7 @@ class Soak:
     def mixer(self, deadline):
         """q0 + q1 on one channel (prefetch 30), every settle pattern."""
         rng = random.Random(7)
-        c = self.conn()
+        c = self.conn("mixer")
         ch = c.channel()
         ch.basic_qos(prefetch_count=30)
         ch.basic_consume("q0", "m0")
@@ -133,7 +134,7 @@ class Soak:
 
     def auto(self, deadline):
         """q2, auto-ack, cancels and re-consumes every ~40 deliveries."""
-        c = self.conn()
+        c = self.conn("auto")
         ch = c.channel()
         k, n = 0, 0
         ch.basic_consume("q2", "a0", no_ack=True)
@@ -157,7 +158,7 @@ class Soak:
     def getter(self, deadline):
         """q3 by Basic.Get: ack, reject(requeue), or hold and Basic.Recover."""
         rng = random.Random(3)
-        c = self.conn()
+        c = self.conn("getter")
         ch = c.channel()
         held = 0
         while time.time() < deadline and not self.finished():
@@ -182,16 +183,7 @@ class Soak:
         c.close()
 
 
-@pytest.mark.timeout(180)
-def test_mixed_clients_every_message_consumed_exactly_once(broker):
-    c = Connection(port=broker.port, vhost="/")
-    ch = c.channel()
-    ch.exchange_declare("sx", "direct")
-    for q in range(QUEUES):
-        ch.queue_declare("q%d" % q)
-        ch.queue_bind("q%d" % q, "sx", "k%d" % q)
-    c.close()
-    s = Soak(broker.port)
+def run_soak(s):
     deadline = time.time() + 90
     ths = [threading.Thread(target=fn, args=a) for fn, a in
            [(s.publisher, (p,)) for p in range(N_PUB)] + [(s.mixer, (deadline,)), (s.auto, (deadline,)),
@@ -217,6 +209,55 @@ def test_mixed_clients_every_message_consumed_exactly_once(broker):
     assert sorted(s.returned) == sorted(s.unroutable)
     assert len(s.done) == len(set(s.done)), "a message was consumed twice"
     assert set(s.done) == s.routable
+
+
+def _topology(port, queues):
+    c = Connection(port=port, vhost="/")
+    ch = c.channel()
+    ch.exchange_declare("sx", "direct")
+    for q in queues:
+        ch.queue_declare("q%d" % q)
+        ch.queue_bind("q%d" % q, "sx", "k%d" % q)
+    c.close()
+
+
+@pytest.mark.timeout(180)
+def test_mixed_clients_every_message_consumed_exactly_once(broker):
+    _topology(broker.port, range(QUEUES))
+    run_soak(Soak(broker.port))
     time.sleep(0.3)
     with broker.lock:
         assert broker.plane.memory_in_use() == 0
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("plane", ["golden", pytest.param("gpu", marks=pytest.mark.gpu)])
+def test_mixed_clients_across_ranks(tmp_path, plane):
+    """Two ranks of the sharded server (gloo): q0/q1 live on rank 0 and are
+    consumed by the mixer on rank 1 (links), q2/q3 live on rank 1 and are consumed on rank
+    0 by the auto-ack consumer (link) and the Basic.Get client (get link); a publisher on
+    each rank."""
+    import json
+    import os
+
+    from chanamq_amd.parallel.launch import Launcher
+    from test_sharded_golden import _free_port
+    here = os.path.dirname(os.path.abspath(__file__))
+    port = _free_port()
+    env = dict(os.environ, PYTHONPATH=os.path.dirname(here))
+    extra = ["--backend", "gloo"] if plane == "gpu" else []   # 2 ranks share the one test GPU
+    ln = Launcher(2, ["-m", "chanamq_amd.server.sharded", "--plane", plane, "--port", str(port),
+                      "--info-dir", str(tmp_path)] + extra, env=env).start()
+    try:
+        deadline = time.time() + 120
+        while time.time() < deadline and not all((tmp_path / f"rank{r}.json").exists() for r in range(2)):
+            assert not ln.poll(), f"rank exited early: {ln.poll()}"
+            time.sleep(0.2)
+        ports = [json.load(open(tmp_path / f"rank{r}.json"))["port"] for r in range(2)]
+        _topology(ports[0], (0, 1))
+        _topology(ports[1], (2, 3))
+        s = Soak(ports[0], ports=dict(pub0=ports[0], pub1=ports[1], mixer=ports[1], auto=ports[0],
+                                      getter=ports[0]))
+        run_soak(s)
+    finally:
+        ln.stop()
