@@ -19,29 +19,40 @@ from test_gpu_broker import GPU_CFG, SMALL, _gpu_present
 N_PUB, PER_PUB, QUEUES = 2, 500, 4
 
 
-def make_plane(kind):
+def make_plane(kind, persist=False):
     if kind == "golden":
         from chanamq_amd.engine.golden import GoldenDataPlane
-        return GoldenDataPlane(default_queue_capacity=1 << 12, ring_pool=1 << 20, **SMALL)
+        return GoldenDataPlane(default_queue_capacity=1 << 12, ring_pool=1 << 20, persist=persist, **SMALL)
     if not _gpu_present():
         pytest.fail("GPU test scheduled on a machine without a GPU")
     from chanamq_amd.engine.dataplane import GpuDataPlane
-    return GpuDataPlane(default_queue_capacity=1 << 12, **GPU_CFG)
+    return GpuDataPlane(default_queue_capacity=1 << 12, persist=int(persist), **GPU_CFG)
 
 
 @pytest.fixture(params=["golden-native", pytest.param("gpu-pipeline", marks=pytest.mark.gpu),
-                        pytest.param("gpu-native", marks=pytest.mark.gpu)])
-def broker(request):
+                        pytest.param("gpu-native", marks=pytest.mark.gpu), "golden-native-store",
+                        pytest.param("gpu-pipeline-store", marks=pytest.mark.gpu)])
+def broker(request, tmp_path):
+    from chanamq_amd.broker import load
     from chanamq_amd.server.gpu_broker import GpuBroker
-    kind, io = request.param.split("-")
-    b = GpuBroker(make_plane(kind), idle_step_ms=1.0, io=io, ingress_bytes=8 << 20).start()
+    kind, io, *store = request.param.split("-")
+    st = None
+    if store:   # durable queues, persistent messages, the WAL store behind them
+        st = load().Store()
+        st.open(str(tmp_path / "store"), False)
+    b = GpuBroker(make_plane(kind, persist=bool(store)), idle_step_ms=1.0, io=io, ingress_bytes=8 << 20,
+                  store=st).start()
+    b.durable = bool(store)
+    b.store_handle = st
     yield b
     b.stop()
+    if st is not None:
+        st.close()
 
 
 class Soak:
-    def __init__(self, port, ports=None):
-        self.port = port
+    def __init__(self, port, ports=None, durable=False):
+        self.port, self.durable = port, durable
         self.ports = ports or {}   # client role -> port (sharded: a rank per role)
         self.lock = threading.Lock()
         self.done = []            # bodies settled as consumed (ack / auto-ack)
@@ -70,11 +81,12 @@ class Soak:
         mine_r, mine_u = set(), set()
         for i in range(PER_PUB):
             body = b"p%d-%d" % (pid, i)
+            props = {"delivery_mode": 2} if self.durable else None
             if rng.random() < 0.05:
-                ch.basic_publish("sx", "nokey", body, mandatory=True)
+                ch.basic_publish("sx", "nokey", body, props, mandatory=True)
                 mine_u.add(body)
             else:
-                ch.basic_publish("sx", "k%d" % rng.randrange(QUEUES), body)
+                ch.basic_publish("sx", "k%d" % rng.randrange(QUEUES), body, props)
                 mine_r.add(body)
             if i % 25 == 24:
                 c.process(0.002)
@@ -211,23 +223,32 @@ def run_soak(s):
     assert set(s.done) == s.routable
 
 
-def _topology(port, queues):
+def _topology(port, queues, durable=False):
     c = Connection(port=port, vhost="/")
     ch = c.channel()
-    ch.exchange_declare("sx", "direct")
+    ch.exchange_declare("sx", "direct", durable=durable)
     for q in queues:
-        ch.queue_declare("q%d" % q)
+        ch.queue_declare("q%d" % q, durable=durable)
         ch.queue_bind("q%d" % q, "sx", "k%d" % q)
     c.close()
 
 
 @pytest.mark.timeout(180)
 def test_mixed_clients_every_message_consumed_exactly_once(broker):
-    _topology(broker.port, range(QUEUES))
-    run_soak(Soak(broker.port))
+    _topology(broker.port, range(QUEUES), broker.durable)
+    run_soak(Soak(broker.port, durable=broker.durable))
     time.sleep(0.3)
     with broker.lock:
         assert broker.plane.memory_in_use() == 0
+    if broker.durable:   # the store agrees: every persistent message's rows are gone
+        time.sleep(0.3)
+        with broker.lock:
+            if broker.persistence.native is not None:
+                broker.persistence.native.drain()
+            st = broker.store_handle
+            left = {q: (len(r[1]), len(r[2])) for q in st.queue_ids() if (r := st.select_queue(q)) and (r[1] or r[2])}
+            assert not left, left
+            assert not st.message_ids()
 
 
 @pytest.mark.timeout(300)
