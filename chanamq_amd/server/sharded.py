@@ -64,13 +64,17 @@ def main(argv=None):
         st = open_store(rank)
         node.peer_store = open_store
     from .gpu_broker import GpuBroker
-    port = args.port if args.reuseport else args.port + rank
+    # --port 0: every rank takes an ephemeral port (reported through --info-dir)
+    port = args.port if (args.reuseport or args.port == 0) else args.port + rank
     broker = GpuBroker(plane, host=args.host, port=port, idle_step_ms=args.idle_step_ms, node=node,
                        reuseport=args.reuseport, ingress_bytes=32 << 20, store=st).start()
     node.persistence = broker.persistence if st is not None else None
     if args.info_dir:
-        with open(os.path.join(args.info_dir, f"rank{rank}.json"), "w") as f:
+        # written then renamed: a watcher polling for the file never reads it half-written
+        path = os.path.join(args.info_dir, f"rank{rank}.json")
+        with open(path + ".tmp", "w") as f:
             json.dump({"rank": rank, "world": world, "port": broker.port}, f)
+        os.replace(path + ".tmp", path)
     stop = threading.Event()
     for sig in (signal.SIGINT, signal.SIGTERM):
         signal.signal(sig, lambda *a: stop.set())

@@ -262,12 +262,10 @@ def test_mixed_clients_across_ranks(tmp_path, plane):
     import os
 
     from chanamq_amd.parallel.launch import Launcher
-    from test_sharded_golden import _free_port
     here = os.path.dirname(os.path.abspath(__file__))
-    port = _free_port()
     env = dict(os.environ, PYTHONPATH=os.path.dirname(here))
     extra = ["--backend", "gloo"] if plane == "gpu" else []   # 2 ranks share the one test GPU
-    ln = Launcher(2, ["-m", "chanamq_amd.server.sharded", "--plane", plane, "--port", str(port),
+    ln = Launcher(2, ["-m", "chanamq_amd.server.sharded", "--plane", plane, "--port", "0",
                       "--info-dir", str(tmp_path)] + extra, env=env).start()
     try:
         deadline = time.time() + 120

@@ -17,10 +17,9 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 @pytest.fixture(params=["golden", pytest.param("gpu", marks=pytest.mark.gpu)])
 def cluster(request, tmp_path):
     from chanamq_amd.parallel.launch import Launcher
-    port = _free_port()
     env = dict(os.environ, PYTHONPATH=os.path.dirname(HERE))
     extra = ["--backend", "gloo"] if request.param == "gpu" else []   # 2 ranks share the one test GPU
-    ln = Launcher(2, ["-m", "chanamq_amd.server.sharded", "--plane", request.param, "--port", str(port),
+    ln = Launcher(2, ["-m", "chanamq_amd.server.sharded", "--plane", request.param, "--port", "0",
                       "--info-dir", str(tmp_path)] + extra, env=env).start()
     deadline = time.time() + 120
     while time.time() < deadline and not all((tmp_path / f"rank{r}.json").exists() for r in range(2)):
@@ -113,9 +112,8 @@ def test_rank_death_durable_queue_reloaded(tmp_path):
     is killed; the survivor that inherits the queue reloads it from rank 2's store and a
     consumer on that rank receives every message."""
     from chanamq_amd.parallel.launch import Launcher
-    port = _free_port()
     env = dict(os.environ, PYTHONPATH=os.path.dirname(HERE))
-    ln = Launcher(3, ["-m", "chanamq_amd.server.sharded", "--plane", "golden", "--port", str(port),
+    ln = Launcher(3, ["-m", "chanamq_amd.server.sharded", "--plane", "golden", "--port", "0",
                       "--info-dir", str(tmp_path), "--store-dir", str(tmp_path / "store"), "--no-fsync"],
                   env=env).start()
     try:
