@@ -86,6 +86,7 @@ class GpuDataPlane(ControlState):
         self.exchanger = exchanger
         self._get_consumed = []   # store records of Basic.Get, emitted with the next step's
         self._pending = None
+        self._xprev = None        # parity of the launched step whose exchange is still due
         self.lag = False
         if world > 1:
             # exchange operands live in torch's allocator so RCCL can use them directly
@@ -610,6 +611,18 @@ class GpuDataPlane(ControlState):
             staged = int(self.carry[segs["conn"]].sum()) + 48 * len(segs)
             if staged > self.info["carry_budget"]:
                 raise RuntimeError(f"step carries {staged} B > carry_budget {self.info['carry_budget']} B")
+        if self.world > 1 and self.lag and self.exchanger is not None:
+            # one process per rank, pipelined exchange: queue H2D(t), then run step t-1's
+            # all-to-all while those bytes cross PCIe, then launch step t (whose phase B
+            # imports t-1's exchange) -- the host never waits on H2D(t) + phase A(t)
+            p = self.eng.submit(segs, int(payload_ptr), int(payload_len), now, self.step_no, now, self.worker,
+                                True)
+            self.step_no += 1
+            if self._xprev is not None:
+                self._exchange_parity(self._xprev)
+            self.eng.launch(p)
+            self._pending = self._xprev = p
+            return (p, len(segs), t0)
         p = self.eng.submit(segs, int(payload_ptr), int(payload_len), now, self.step_no, now, self.worker)
         self.step_no += 1
         if self.world > 1:
@@ -626,6 +639,17 @@ class GpuDataPlane(ControlState):
                 else:
                     self.submit_b(recv)
         return (p, len(segs), t0)
+
+    def _exchange_parity(self, q):
+        """All-to-all of the launched step of parity ``q`` (its phase A packed S[q]; the
+        received records land in R[q], imported by the next launched step)."""
+        cnt = self.eng.send_counts(q)
+        if cnt[-1]:
+            raise RuntimeError("cross-rank send buffers overflowed (xfer_desc_max / xfer_bytes)")
+        self._send_counts = cnt[:-1]
+        recv = self.exchanger.exchange(self._send_counts, self._xs[q][0], self._xs[q][1],
+                                       self._xr[q][0], self._xr[q][1])
+        self.set_import(recv)
 
     # ---- sharded step, phase B (LocalCluster drives it after its in-process exchange)
     def pending_send_counts(self):

@@ -558,18 +558,21 @@ class Engine {
   // the compute stream behind it.  wait_results(p) -> host-mapped SegOut/Counters/ConnOut
   // are valid; egress_copy(p) DMAs exactly the rendered bytes on the D2H stream;
   // egress_wait(p) -> egress_host(p) is valid.
+  // defer: queue only the ingress H2D and return; launch(p) starts the step's kernels.  A
+  // sharded driver uses the gap to run the previous step's exchange while this step's
+  // bytes cross PCIe (the host waits on phase A of t-1, not on H2D(t) + phase A(t))
   int submit(py::buffer segs, u64 payload_ptr, u64 payload_len, i64 now_ms, u64 step, u64 id_ms,
-             u32 worker) {
+             u32 worker, bool defer) {
     py::buffer_info si = segs.request();
     size_t sb = (size_t)si.size * si.itemsize;
     return submit_raw((const SegIn*)si.ptr, (u32)(sb / sizeof(SegIn)), payload_ptr, payload_len, now_ms, id_ms,
-                      worker);
+                      worker, defer);
   }
 
   // step numbers are the engine's own submit sequence (latency histogram, message
   // publish step): identical whether Python or the native front end drives the steps
   int submit_raw(const SegIn* segp, u32 nseg, u64 payload_ptr, u64 payload_len, i64 now_ms, u64 id_ms,
-                 u32 worker) {
+                 u32 worker, bool defer = false) {
     HostTimer ht(&ht_[0]);
     Range rg("chanamq.step.submit");
     const size_t sb = (size_t)nseg * sizeof(SegIn);
@@ -596,6 +599,18 @@ class Engine {
       HIPCHECK(hipMemcpyAsync((void*)io_[p].ingress, (const void*)payload_ptr, payload_len,
                               sdma_ ? hipMemcpyDeviceToDeviceNoCU : hipMemcpyHostToDevice, s_h2d_));
     HIPCHECK(hipEventRecord(ev_h2d_[p], s_h2d_));
+    inflight_[p] = true;
+    staged_[p] = true;
+    ++seq_;
+    if (!defer) launch(p);
+    return p;
+  }
+
+  // second half of submit(): the kernels of the staged step of parity p
+  void launch(int p) {
+    if (!staged_[p]) throw std::runtime_error("launch: no staged step of this parity");
+    staged_[p] = false;
+    const int e = slot_of_[p];
     // egress slot e (last used by step t-EGRESS_SLOTS) drained before this step's kernels
     // overwrite it; waited for only after this step's ingress H2D is queued, so the H2D
     // and the in-flight D2H overlap on their two SDMA engines
@@ -639,9 +654,6 @@ class Engine {
     } else {
       HIPCHECK(hipEventRecord(ev_done_[p], s_comp_));
     }
-    inflight_[p] = true;
-    ++seq_;
-    return p;
   }
 
   // sharded step, after submit(): wait for phase A and return the per-destination send
@@ -839,6 +851,7 @@ class Engine {
     HostTimer ht(&ht_[3]);
     Range rg("chanamq.step.wait_results");
     if (phase_a_[p]) throw std::runtime_error("wait_results: phase B of this sharded step not submitted");
+    if (staged_[p]) throw std::runtime_error("wait_results: step staged but never launched");
     HIPCHECK(hipEventSynchronize(ev_done_[p]));
     inflight_[p] = false;
   }
@@ -1170,6 +1183,7 @@ class Engine {
   hipStream_t s_comp_ = nullptr, s_h2d_ = nullptr, s_d2h_ = nullptr;
   hipEvent_t ev_h2d_[2], ev_done_[2], ev_d2h_[EGRESS_SLOTS];
   bool inflight_[2] = {false, false};
+  bool staged_[2] = {false, false};   // submitted with defer, kernels not launched yet
   bool d2h_issued_[EGRESS_SLOTS] = {};
   u64 seq_ = 0;
 };
@@ -1213,7 +1227,9 @@ PYBIND11_MODULE(_dataplane, m) {
       .def("upload", &Engine::upload, py::arg("name"), py::arg("data"), py::arg("offset") = 0)
       .def("download", &Engine::download, py::arg("name"), py::arg("offset") = 0, py::arg("n") = 0)
       .def("host_view", &Engine::host_view)
-      .def("submit", &Engine::submit)
+      .def("submit", &Engine::submit, py::arg("segs"), py::arg("payload_ptr"), py::arg("payload_len"),
+           py::arg("now_ms"), py::arg("step"), py::arg("id_ms"), py::arg("worker"), py::arg("defer") = false)
+      .def("launch", &Engine::launch)
       .def("send_counts", &Engine::send_counts)
       .def("submit_b", &Engine::submit_b, py::arg("parity"), py::arg("recv"), py::arg("stream") = 0)
       .def("set_xfer_buffers", &Engine::set_xfer_buffers)

@@ -54,25 +54,38 @@ def test_gpu_cluster_eager_matches_graph(gpu):
     assert a == b
 
 
-@pytest.mark.timeout(400)
-def test_gpu_two_process_exchange(gpu):
-    """One process per rank (both on device 0), gloo all_to_all with host staging."""
-    spec = SHARDED["fanout_confirm"]()
-    single = run_single(spec, 2)
+def _two_process_gpu(spec_name, steps, lag=False):
     with tempfile.TemporaryDirectory() as d:
         env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()), WORLD_SIZE="2",
                    PYTHONPATH=os.pathsep.join([os.path.dirname(HERE), HERE]))
-        procs = [subprocess.Popen([sys.executable, os.path.join(HERE, "sharded_worker.py"), "fanout_confirm", d,
-                                   "gpu"], env=dict(env, RANK=str(r))) for r in range(2)]
+        procs = [subprocess.Popen([sys.executable, os.path.join(HERE, "sharded_worker.py"), spec_name, d, "gpu"]
+                                  + (["lag"] if lag else []), env=dict(env, RANK=str(r))) for r in range(2)]
         for p in procs:
             assert p.wait(timeout=360) == 0
-        got = [dict() for _ in spec.steps]
+        got = [dict() for _ in range(steps)]
         for r in range(2):
             with open(os.path.join(d, f"rank{r}.json")) as f:
                 for k, eg in enumerate(json.load(f)):
                     for c, hx in eg.items():
                         got[k][int(c)] = bytes.fromhex(hx)
-    assert single == got
+    return got
+
+
+@pytest.mark.timeout(400)
+def test_gpu_two_process_exchange(gpu):
+    """One process per rank (both on device 0), gloo all_to_all with host staging."""
+    spec = SHARDED["fanout_confirm"]()
+    assert run_single(spec, 2) == _two_process_gpu("fanout_confirm", len(spec.steps))
+
+
+@pytest.mark.timeout(400)
+@pytest.mark.parametrize("name", ["fanout_confirm", "topic"])
+def test_gpu_two_process_pipelined_exchange(gpu, name):
+    """The benchmark's exchange schedule, one process per rank: step t's ingress is queued
+    (deferred launch), step t-1's all-to-all runs, then step t's kernels import it --
+    byte-identical to the golden cluster with exchange_lag=1."""
+    want = run_cluster_lag(SHARDED[name](), 2, extra_steps=2)
+    assert _two_process_gpu(name, len(want), lag=True) == want
 
 
 @pytest.mark.parametrize("world", [2, 3])
