@@ -391,17 +391,29 @@ DEV i32 chan_lookup(const DS& d, u32 conn, u32 ch) {
 // frame header (type 1/2/3/8, size within the broker frame-max).  Reads 32 bytes (the
 // header of a frame starting at byte 15 ends in the next word); segments are padded
 // by >= 32 bytes in the work buffer
+// SWAR: 0x80 in every byte of v that is zero (exact per byte: no borrow between bytes)
+DEV u32 zero_bytes(u32 v) { return ~(((v & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | v | 0x7F7F7F7Fu); }
+// bits 0..3 = bytes 0..3 of v hold a frame type (1, 2, 3 or 8); the multiply gathers the
+// four 0x80 flags (bits 0, 8, 16, 24 after the shift) into bits 21..24 without carries
+DEV u32 type_nibble(u32 v) {
+  const u32 h = (zero_bytes(v & 0xFCFCFCFCu) & ~zero_bytes(v)) | zero_bytes(v ^ 0x08080808u);
+  return (((h >> 7) * 0x00204081u) >> 21) & 0xFu;
+}
 DEV u32 cand_bits(uint4 A, uint4 B, u32 fm) {
-  u32 w[8] = {A.x, A.y, A.z, A.w, B.x, B.y, B.z, B.w};
+  const u32 w[6] = {A.x, A.y, A.z, A.w, B.x, B.y};
   u32 m = 0;
 #pragma unroll
-  for (int j = 0; j < 16; ++j) {
-#define BYTE(k) ((w[(k) >> 2] >> (8 * ((k) & 3))) & 255u)
-    u32 t = BYTE(j);
-    u32 sz = (BYTE(j + 3) << 24) | (BYTE(j + 4) << 16) | (BYTE(j + 5) << 8) | BYTE(j + 6);
-#undef BYTE
-    bool ok = (t == 1 || t == 2 || t == 3 || t == 8) && (fm == 0 || sz <= fm - 8);
-    m |= (ok ? 1u : 0u) << j;
+  for (int i = 0; i < 4; ++i) {
+    u32 h = type_nibble(w[i]);
+    // the rare type hits: big-endian size from bytes k+3..k+6 of the 4i-byte window
+    while (h) {
+      const u32 k = __ffs(h) - 1;
+      h &= h - 1;
+      const u32 v = k == 0 ? __builtin_amdgcn_alignbyte(w[i + 1], w[i], 3)
+                           : __builtin_amdgcn_alignbyte(w[i + 2], w[i + 1], k - 1);
+      const u32 sz = __builtin_bswap32(v);
+      if (fm == 0 || sz <= fm - 8) m |= 1u << (4 * i + k);
+    }
   }
   return m;
 }
@@ -616,38 +628,76 @@ __global__ __launch_bounds__(FS_NT) void k_frame_scan(DS d) {
     csucc[i] = (int16_t)sx;
   }
   FS_MARK(2);
-  if (tid == 0) sh_ok = 1;
-  __syncthreads();
-  // ---- (c) chain: optimistic (every candidate a real frame) else serial walk
-  for (u32 i = tid; i < m; i += FS_NT) {
-    i32 sx = csucc[i];
-    bool good = (i + 1 < m) ? (sx == (i32)(i + 1)) : (sx == -1 || sx == -2);
-    if (!good) atomicAnd(&sh_ok, 0u);
-  }
-  __syncthreads();
-  if (tid == 0) {
-    u32 nf = 0, brk = 0;
-    if (m == 0 || cpos[0] != 0) {
-      brk = 1;  // first bytes are not a frame header
-    } else if (sh_ok) {
-      nf = m;
-    } else {
-      i32 i = 0;
-      while (true) {
-        chain[nf++] = (u16)i;
-        i32 sx = csucc[i];
-        if (sx >= 0) { i = sx; continue; }
-        if (sx == -3) brk = 1;
-        break;
+  // ---- (c) chain.  A failure is a candidate whose successor is not the next candidate;
+  // between failures the chain runs through consecutive candidates.  The failures are
+  // compacted in order (into wend, dead after (b)), then one thread walks failure to
+  // failure -- one step per jump over false candidates (e.g. timestamp bytes inside a
+  // header that look like a frame running past the segment end), not one per frame --
+  // recording runs, which all threads expand into chain[].  A single run starting at 0
+  // is the implicit chain (frame f = candidate f)
+  constexpr u32 FS_RUNS = 1024;            // run records at the top of wend
+  constexpr u32 FS_FAIL_MAX = CAND_MAX - 2 * FS_RUNS;
+  __syncthreads();   // csucc / wend of (b) complete
+  FS_MARK(9);
+  {
+    const u32 per = (m + FS_NT - 1) / FS_NT;
+    const u32 i0 = tid * per < m ? tid * per : m;
+    const u32 i1 = i0 + per < m ? i0 + per : m;
+    u32 nfl = 0;
+    for (u32 i = i0; i < i1; ++i) nfl += csucc[i] != (i32)(i + 1);
+    u32 tfl;
+    u32 o = block_scan<FS_NT>(nfl, sc, tfl);
+    for (u32 i = i0; i < i1; ++i)
+      if (csucc[i] != (i32)(i + 1) && o < FS_FAIL_MAX) wend[o++] = i;
+    __syncthreads();
+    FS_MARK(10);
+    if (tid == 0) {
+      u32 nf = 0, brk = 0, nrun = 0;
+      if (m == 0 || cpos[0] != 0) {
+        brk = 1;  // first bytes are not a frame header
+      } else if (tfl <= FS_FAIL_MAX) {
+        u32 i = 0, fp = 0;
+        while (true) {   // the last candidate always fails (no successor after it)
+          while (wend[fp] < i) ++fp;
+          const u32 k = wend[fp];
+          if (nrun < FS_RUNS) { wend[FS_FAIL_MAX + 2 * nrun] = i; wend[FS_FAIL_MAX + 2 * nrun + 1] = nf; }
+          ++nrun;
+          nf += k - i + 1;
+          const i32 sx = csucc[k];
+          if (sx < 0) { brk = sx == -3; break; }
+          i = (u32)sx;
+        }
+      }
+      if (m != 0 && cpos[0] == 0 && (tfl > FS_FAIL_MAX || nrun > FS_RUNS)) {
+        nf = 0; brk = 0; nrun = FS_RUNS + 1;   // pathological: serial walk
+        i32 i = 0;
+        while (true) {
+          chain[nf++] = (u16)i;
+          i32 sx = csucc[i];
+          if (sx >= 0) { i = sx; continue; }
+          if (sx == -3) brk = 1;
+          break;
+        }
+      }
+      sh_nf = nf;
+      sh_brk = brk;
+      sh_ok = nrun;
+    }
+    __syncthreads();
+    FS_MARK(11);
+    const u32 nrun = sh_ok;
+    if (nrun > 1 && nrun <= FS_RUNS) {
+      for (u32 r = tid; r < nrun; r += FS_NT) {
+        const u32 ci = wend[FS_FAIL_MAX + 2 * r], f0 = wend[FS_FAIL_MAX + 2 * r + 1];
+        const u32 f1 = r + 1 < nrun ? wend[FS_FAIL_MAX + 2 * r + 3] : sh_nf;
+        for (u32 f = f0; f < f1; ++f) chain[f] = (u16)(ci + (f - f0));
       }
     }
-    sh_nf = nf;
-    sh_brk = brk;
+    __syncthreads();
   }
-  __syncthreads();
   FS_MARK(3);
   const u32 nf = sh_nf;
-  const bool implicit_chain = sh_ok && !(m == 0 || cpos[0] != 0);
+  const bool implicit_chain = sh_ok == 1;
 #define CPOS(f) (cpos[implicit_chain ? (f) : chain[f]])
 
   // ---- (d) commands: each method frame walks its content frames
@@ -1155,7 +1205,10 @@ __global__ __launch_bounds__(1024) void k_scan(ScanArgs a, u32* tot, u64* status
   if (a.lo) {
     u32 lo = *a.lo;
     n = n > lo ? n - lo : 0;
-    for (u32 k = 0; k < a.narr; ++k) { a.in[k] += lo; a.out[k] += lo; }
+    // constant trip count: a runtime-bounded loop indexes a.in/a.out dynamically and puts
+    // the argument struct in scratch memory
+#pragma unroll
+    for (int k = 0; k < 4; ++k) { a.in[k] += lo; a.out[k] += lo; }
   }
   const u32 base = tile * SCAN_TILE;
   if (base < n || (tile == 0)) {
@@ -3078,6 +3131,9 @@ __global__ __launch_bounds__(256) void k_requeue(DS d) {
   __shared__ u32 cnt;
   __shared__ u32 s_last;
   if (blockIdx.x == 0 && threadIdx.x == 0) *d.n_dirty = 0;   // fused k_reset_dirty (after k_chan_advance)
+  // nothing requeued (the common step): no block takes the ticket, nothing to compact.
+  // req_n only changes in the compaction, which runs after every block has read it
+  if (*d.req_n == 0) return;
   // grid-stride over queues: a bounded grid keeps the completion ticket below (one
   // same-address atomic per block) from serialising thousands of blocks
   for (u32 q = blockIdx.x; q < d.q_max; q += gridDim.x)
