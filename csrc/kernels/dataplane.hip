@@ -650,22 +650,37 @@ __global__ __launch_bounds__(FS_NT) void k_frame_scan(DS d) {
     for (u32 i = i0; i < i1; ++i)
       if (csucc[i] != (i32)(i + 1) && o < FS_FAIL_MAX) wend[o++] = i;
     __syncthreads();
+    // per failure x (candidate F[x] = wend[x]) with a successor: the first failure at or
+    // after that successor, in parallel (binary search over F); kept in chain[] (free
+    // until the expansion below), 0xFFFF = the chain ends at this failure
+    if (tfl <= FS_FAIL_MAX)
+      for (u32 x = tid; x < tfl; x += FS_NT) {
+        const i32 sx = csucc[wend[x]];
+        u32 nx = 0xFFFFu;
+        if (sx >= 0) {
+          u32 lo = x + 1, hi = tfl;   // successors lie after the failure
+          while (lo < hi) { u32 mid = (lo + hi) >> 1; if (wend[mid] < (u32)sx) lo = mid + 1; else hi = mid; }
+          nx = lo;   // < tfl: the last candidate is a failure
+        }
+        chain[x] = (u16)nx;
+      }
+    __syncthreads();
     FS_MARK(10);
     if (tid == 0) {
       u32 nf = 0, brk = 0, nrun = 0;
       if (m == 0 || cpos[0] != 0) {
         brk = 1;  // first bytes are not a frame header
       } else if (tfl <= FS_FAIL_MAX) {
-        u32 i = 0, fp = 0;
-        while (true) {   // the last candidate always fails (no successor after it)
-          while (wend[fp] < i) ++fp;
-          const u32 k = wend[fp];
+        // failure to failure: the run [i, F[x]], then the run from F[x]'s successor
+        u32 i = 0, x = 0;
+        while (true) {
+          const u32 k = wend[x], nx = chain[x];
           if (nrun < FS_RUNS) { wend[FS_FAIL_MAX + 2 * nrun] = i; wend[FS_FAIL_MAX + 2 * nrun + 1] = nf; }
           ++nrun;
           nf += k - i + 1;
-          const i32 sx = csucc[k];
-          if (sx < 0) { brk = sx == -3; break; }
-          i = (u32)sx;
+          if (nx == 0xFFFFu) { brk = csucc[k] == -3; break; }
+          i = (u32)csucc[k];
+          x = nx;
         }
       }
       if (m != 0 && cpos[0] == 0 && (tfl > FS_FAIL_MAX || nrun > FS_RUNS)) {
@@ -1180,18 +1195,24 @@ __global__ __launch_bounds__(256) void k_decode(DS d) {
 // ============================================================================ scans
 // single-block multi-array exclusive scan; n read from device; totals -> tot[slot+k]
 // lo != null: scan elements [*lo, *n) (absolute indices), else [0, *n)
-struct ScanArgs { const u32* in[4]; u32* out[4]; const u32* n; const u32* lo; u32 narr; u32 nmax; u32 tot_slot; };
-// Single-pass exclusive scan over up to 4 arrays, one 4096-element tile per block, tiles
-// chained by decoupled look-back: each tile publishes its aggregate, then its inclusive
-// prefix, in a per-(array, tile) status word tagged with the launch epoch, so the status
-// array never needs clearing.  Tickets (not blockIdx) order the tiles, so a tile only
-// ever waits on tiles whose blocks are already running.
+// NA <= 4: arrays in[k] / out[k].  NA = 8 (per-rank pairs): array k is in[k & 1] +
+// (k >> 1) * stride
+struct ScanArgs { const u32* in[4]; u32* out[4]; const u32* n; const u32* lo; u32 narr; u32 nmax; u32 tot_slot; u64 stride; };
+// Single-pass exclusive scan over up to NA arrays, 4 elements per thread, 4096-element
+// tiles (NA = 8: the per-rank counts of the cross-GPU pack, 4 ranks per launch; 16 arrays
+// spill registers; 1024-element tiles lengthen the look-back chain), tiles chained by
+// decoupled look-back: each tile publishes its aggregate, then its inclusive prefix, in a
+// per-(array, tile) status word tagged with the launch epoch, so the status array never
+// needs clearing.  Tickets (not blockIdx) order the tiles, so a tile only ever waits on
+// tiles whose blocks are already running.
 //   status word = epoch << 34 | flag << 32 | value   (flag 1 = aggregate, 2 = inclusive)
 #define SCAN_TILE 4096
+template <int NA, int EPT>
 __global__ __launch_bounds__(1024) void k_scan(ScanArgs a, u32* tot, u64* status, u32* ctl, u32 smax) {
-  __shared__ u32 lds[1024 / 64 + 1];
+  constexpr u32 TILE = 1024 * EPT;
   __shared__ u32 s_tile, s_epoch;
-  __shared__ u32 s_excl[4];
+  __shared__ u32 s_excl[NA];
+  __shared__ u32 wsum[NA][1024 / 64 + 1];
   const u32 tid = threadIdx.x;
   if (tid == 0) {
     s_epoch = atomicAdd(&ctl[1], 0u);
@@ -1202,68 +1223,68 @@ __global__ __launch_bounds__(1024) void k_scan(ScanArgs a, u32* tot, u64* status
   const bool last_block = tile == gridDim.x - 1;
   u32 n = a.n ? *a.n : a.nmax;
   if (n > a.nmax) n = a.nmax;
-  if (a.lo) {
-    u32 lo = *a.lo;
-    n = n > lo ? n - lo : 0;
-    // constant trip count: a runtime-bounded loop indexes a.in/a.out dynamically and puts
-    // the argument struct in scratch memory
-#pragma unroll
-    for (int k = 0; k < 4; ++k) { a.in[k] += lo; a.out[k] += lo; }
-  }
-  const u32 base = tile * SCAN_TILE;
+  // lo: elements [lo, lo + n) -- applied at each access (rewriting the argument struct's
+  // pointers would copy it to scratch memory)
+  const u32 lo = a.lo ? *a.lo : 0u;
+  n = n > lo ? n - lo : 0;
+  const u32 base = tile * TILE;
   if (base < n || (tile == 0)) {
-    const u32 i = base + tid * 4;
-    u32 v[4][4], off[4], agg[4], sm[4];
-    // every array's loads in flight at once, then one block scan of the 4 sums together
-    // (2 barriers instead of 3 per array)
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      v[k][0] = v[k][1] = v[k][2] = v[k][3] = 0;
+    const u32 i = base + tid * EPT;
+    u32 v[NA][EPT], off[NA], sm[NA];
+    // every array's loads in flight at once, then one block scan of the sums together
+#pragma clang loop unroll(full)
+    for (int k = 0; k < NA; ++k) {
+#pragma clang loop unroll(full)
+      for (int e = 0; e < EPT; ++e) v[k][e] = 0;
       if ((u32)k >= a.narr) continue;
-      if (i + 3 < n && !(((uintptr_t)(a.in[k] + i)) & 15)) {
-        uint4 x = *(const uint4*)(a.in[k] + i);
-        v[k][0] = x.x; v[k][1] = x.y; v[k][2] = x.z; v[k][3] = x.w;
+      const u32* in = (NA <= 4 ? a.in[k & 3] : a.in[k & 1] + (u64)(k >> 1) * a.stride) + lo;
+      if (EPT == 4 && i + 3 < n && !(((uintptr_t)(in + i)) & 15)) {
+        uint4 x = *(const uint4*)(in + i);
+        v[k][0] = x.x; v[k][EPT > 1 ? 1 : 0] = x.y; v[k][EPT > 2 ? 2 : 0] = x.z; v[k][EPT > 3 ? 3 : 0] = x.w;
       } else {
-        for (u32 e = 0; e < 4; ++e)
-          if (i + e < n) v[k][e] = a.in[k][i + e];
+#pragma clang loop unroll(full)
+        for (int e = 0; e < EPT; ++e)
+          if (i + e < n) v[k][e] = in[i + e];
       }
     }
     const u32 ln = tid & 63, w = tid >> 6;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) sm[k] = v[k][0] + v[k][1] + v[k][2] + v[k][3];
-    u32 x[4] = {sm[0], sm[1], sm[2], sm[3]};
-#pragma unroll
+    u32 x[NA];
+#pragma clang loop unroll(full)
+    for (int k = 0; k < NA; ++k) {
+      u32 t = 0;
+#pragma clang loop unroll(full)
+      for (int e = 0; e < EPT; ++e) t += v[k][e];
+      sm[k] = t;
+      x[k] = t;
+    }
+#pragma clang loop unroll(full)
     for (int o = 1; o < 64; o <<= 1) {
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
+#pragma clang loop unroll(full)
+      for (int k = 0; k < NA; ++k) {
         u32 y = __shfl_up(x[k], o, 64);
         if (ln >= (u32)o) x[k] += y;
       }
     }
-    __shared__ u32 wsum[4][1024 / 64 + 1];
     if (ln == 63) {
-#pragma unroll
-      for (int k = 0; k < 4; ++k) wsum[k][w] = x[k];
+#pragma clang loop unroll(full)
+      for (int k = 0; k < NA; ++k) wsum[k][w] = x[k];
     }
     __syncthreads();
-    if (tid < 4) {
+    if (tid < NA) {
       u32 run = 0;
       for (u32 j = 0; j < 1024 / 64; ++j) { u32 t = wsum[tid][j]; wsum[tid][j] = run; run += t; }
       wsum[tid][1024 / 64] = run;
     }
     __syncthreads();
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      off[k] = wsum[k][w] + x[k] - sm[k];
-      agg[k] = wsum[k][1024 / 64];
-    }
+#pragma clang loop unroll(full)
+    for (int k = 0; k < NA; ++k) off[k] = wsum[k][w] + x[k] - sm[k];
     // look-back, one wave per array: the wave's 64 lanes read the 64 preceding tiles'
     // status words at once, so a tile waits one round trip for all its (concurrently
     // running) predecessors instead of a chain of them
     const u32 wv = tid >> 6, lane = tid & 63;
-    if (wv < a.narr) {
+    if (wv < a.narr && wv < (u32)NA) {
       const u32 k = wv;
-      u32 A = k == 0 ? agg[0] : k == 1 ? agg[1] : k == 2 ? agg[2] : agg[3];
+      const u32 A = wsum[k][1024 / 64];   // the tile's aggregate of array k
       // agent-scope acquire/release: the tiles run on different XCDs (separate L2s)
       u64* st = status + (u64)k * smax;
       const u64 tag = (u64)epoch << 34;
@@ -1294,22 +1315,31 @@ __global__ __launch_bounds__(1024) void k_scan(ScanArgs a, u32* tot, u64* status
       if (lane == 0) {
         __hip_atomic_store(&st[tile], tag | (2ull << 32) | (excl + A), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
         s_excl[k] = excl;
-        if (base + SCAN_TILE >= n) tot[a.tot_slot + k] = excl + A;   // the last data tile
+        if (base + TILE >= n) tot[a.tot_slot + k] = excl + A;   // the last data tile
       }
     }
     __syncthreads();
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      if ((u32)k >= a.narr) break;
+#pragma clang loop unroll(full)
+    for (int k = 0; k < NA; ++k) {
+      if ((u32)k >= a.narr) continue;   // (continue, not break: a single-exit loop unrolls)
       u32 o0 = s_excl[k] + off[k];
-      uint4 o;
-      o.x = o0; o.y = o0 + v[k][0]; o.z = o.y + v[k][1]; o.w = o.z + v[k][2];
-      if (i + 3 < n && !(((uintptr_t)(a.out[k] + i)) & 15)) *(uint4*)(a.out[k] + i) = o;
-      else {
-        if (i < n) a.out[k][i] = o.x;
-        if (i + 1 < n) a.out[k][i + 1] = o.y;
-        if (i + 2 < n) a.out[k][i + 2] = o.z;
-        if (i + 3 < n) a.out[k][i + 3] = o.w;
+      u32* out = (NA <= 4 ? a.out[k & 3] : a.out[k & 1] + (u64)(k >> 1) * a.stride) + lo;
+      if (EPT == 4) {
+        uint4 o;
+        o.x = o0; o.y = o0 + v[k][0]; o.z = o.y + v[k][EPT > 1 ? 1 : 0]; o.w = o.z + v[k][EPT > 2 ? 2 : 0];
+        if (i + 3 < n && !(((uintptr_t)(out + i)) & 15)) *(uint4*)(out + i) = o;
+        else {
+          if (i < n) out[i] = o.x;
+          if (i + 1 < n) out[i + 1] = o.y;
+          if (i + 2 < n) out[i + 2] = o.z;
+          if (i + 3 < n) out[i + 3] = o.w;
+        }
+      } else {
+#pragma clang loop unroll(full)
+        for (int e = 0; e < EPT; ++e) {
+          if (i + e < n) out[i + e] = o0;
+          o0 += v[k][e];
+        }
       }
     }
   }
@@ -1464,13 +1494,17 @@ __global__ __launch_bounds__(256) void k_topic_mfma(DS d) {
 // pattern word byte-equal to the key word at its position.  Word offsets are precomputed
 // (host: t_woff, decode: pub_kwoff), so the compares of all words issue together instead
 // of walking both strings byte by byte.
+// bytes of a publish: the step's work buffer, or for a record imported from another
+// rank the all-to-all receive buffer itself (k_import copies nothing)
+DEV const u8* pub_src(const DS& d, const Pub& pb) { return (pb.flags & MF_IMPORTED) ? d.recv_pay : d.work; }
+
 DEV bool topic_verify_words(const DS& d, const Pub& pb, u32 pidx, u32 t, u32 fl) {
   const u32 nw = pb.nwords < TOPIC_WORDS ? pb.nwords : TOPIC_WORDS;
   const u32 star = (fl >> 16) & 0xffu;
   const u16* pw = d.t_woff + (u64)t * TOPIC_WORDS;
   const u16* kw = d.pub_kwoff + (u64)pidx * TOPIC_WORDS;
   const u8* pat = d.kpool + d.t_kb_off[t];
-  const u8* key = d.work + pb.rk_off;
+  const u8* key = pub_src(d, pb) + pb.rk_off;
   u32 diff = 0;
   for (u32 i = 0; i < nw; ++i) {
     if ((star >> i) & 1) continue;
@@ -1497,7 +1531,7 @@ DEV bool topic_bind_hit(const DS& d, const Pub& pb, u32 pidx, u32 t) {
     if (!((mw >> (t & 15)) & 1)) return false;
     return topic_verify_words(d, pb, pidx, t, fl);
   }
-  return topic_match(d.kpool + d.t_kb_off[t], d.t_kb_len[t], d.work + pb.rk_off, pb.rk_len,
+  return topic_match(d.kpool + d.t_kb_off[t], d.t_kb_len[t], pub_src(d, pb) + pb.rk_off, pb.rk_len,
                      d.hash_wildcard != 0);
 }
 
@@ -1509,7 +1543,7 @@ DEV i32 direct_find(const DS& d, const Pub& pb) {
     i32 ex = d.d_exch[s];
     if (ex < 0) return -1;
     if (ex == pb.exch && d.d_key[s] == k &&
-        word_eq(d.kpool + d.d_kb_off[s], d.d_kb_len[s], d.work + pb.rk_off, pb.rk_len))
+        word_eq(d.kpool + d.d_kb_off[s], d.d_kb_len[s], pub_src(d, pb) + pb.rk_off, pb.rk_len))
       return (i32)s;
   }
   return -1;
@@ -1765,7 +1799,7 @@ DEV void store_one(const DS& d, u32 p, u32 lane) {
   u32 msg = d.msg_free[d.tot[8] - 1 - rr];
   u64 off = base + d.pub_slot_off[p];
   u8* slot = d.log + (off % d.log_bytes);
-  const u8* w = d.work;
+  const u8* w = pub_src(d, pb);
   u32 meta = align16(pb.ex_len + pb.rk_len + pb.props_len);
   wave_copy(slot, w + pb.ex_off, pb.ex_len);
   wave_copy(slot + pb.ex_len, w + pb.rk_off, pb.rk_len);
@@ -1908,8 +1942,8 @@ __global__ void k_import_prep(DS d) {
     dsum += d.xchg[2 * WORLD_MAX + r];
     psum += d.xchg[3 * WORLD_MAX + r];
   }
-  u32 base = align16(d.tot[15]) + 64;
-  bool fits = dsum <= d.import_max && (u64)base + psum <= d.work_cap + d.xfer_bytes;
+  u32 base = 0;   // imported bytes stay in the receive buffer (pub_src)
+  bool fits = dsum <= d.import_max && psum <= d.xfer_bytes;
   u32 ni = fits ? dsum : 0;
   if (!fits) d.ctr->n_dropped_nomem += dsum;
   d.tot[TS_NIMPORT] = ni;
@@ -1919,25 +1953,21 @@ __global__ void k_import_prep(DS d) {
   d.tot[TS_PAIR_BASE] = d.tot[TS_PAIR_N];
 }
 
-// one wave per received record: payload -> work buffer, record -> imported Publish
-DEV void import_one(const DS& d, u32 i, u32 lane);
+// one thread per received record -> imported Publish whose bytes stay in recv_pay (no
+// copy: a thread builds the record's key hash / key vector, as k_decode does per publish)
+DEV void import_one(const DS& d, u32 i);
 __global__ __launch_bounds__(256) void k_import(DS d) {
-  u32 lane = lane_id();
-  const u32 nw = (gridDim.x * blockDim.x) >> 6;
   const u32 n = d.tot[TS_NIMPORT];
-  for (u32 i = (blockIdx.x * blockDim.x + threadIdx.x) >> 6; i < n; i += nw) import_one(d, i, lane);
+  for (u32 i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) import_one(d, i);
 }
 
-DEV void import_one(const DS& d, u32 i, u32 lane) {
+DEV void import_one(const DS& d, u32 i) {
   u32 src = 0;
   for (u32 r = 1; r < d.world; ++r)
     if (d.xr_base[r] <= i) src = r;
   const RDesc rd = d.recv_desc[i];
-  u32 roff = d.xr_base[WORLD_MAX + src] + rd.pay_off;
-  u32 len = rd.ex_len + rd.rk_len + rd.props_len + rd.body_len;
-  u32 wo = d.tot[TS_IMPORT_BASE] + roff;
-  wave_copy(d.work + wo, d.recv_pay + roff, len);
-  if (lane) return;
+  const u32 roff = d.xr_base[WORLD_MAX + src] + rd.pay_off;
+  const u32 wo = roff;   // offsets relative to recv_pay (MF_IMPORTED, pub_src)
   u32 pi = d.ctr->n_pubs + i;
   Pub pb;
   pb.conn = INVALID;
@@ -1957,7 +1987,7 @@ DEV void import_one(const DS& d, u32 i, u32 lane) {
   pb.flags = rd.flags | MF_IMPORTED;
   pb.expire_ms = rd.expire_ms;
   pb.ts_ms = rd.ts_ms;
-  const u8* key = d.recv_pay + roff + rd.ex_len;  // read from the source: same wave wrote work
+  const u8* key = d.recv_pay + roff + rd.ex_len;
   pb.keyhash = (rd.flags & MF_RESTORE) ? (u64)rd.tq : fnv1a64_dev(key, rd.rk_len);
   pb.nwords = build_keyvec(d, key, rd.rk_len, pi);
   pb.nq = 0; pb.slot_bytes = 0; pb.msg = INVALID; pb.xid = rd.xid;

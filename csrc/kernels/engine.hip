@@ -215,7 +215,7 @@ class Engine {
     d_.seg_total = (u32*)dev("seg_total", 4ull * d_.seg_max);
     d_.seg_cmd_base = (u32*)dev("seg_cmd_base", 4ull * d_.seg_max);
     d_.seg_npub = (u32*)dev("seg_npub", 4ull * d_.seg_max);
-    d_.work = (u8*)dev("work", d_.work_cap + 4096 + (d_.xfer_bytes ? d_.xfer_bytes + 128 : 0));
+    d_.work = (u8*)dev("work", d_.work_cap + 4096);   // imports are read in place (k_import)
 
     d_.cmds = (Cmd*)dev("cmds", sizeof(Cmd) * (u64)d_.cmd_max);
     d_.frags = (Frag*)dev("frags", sizeof(Frag) * ((u64)d_.frag_max + d_.import_max));
@@ -381,7 +381,8 @@ class Engine {
       big = big > d_.deliv_max ? big : d_.deliv_max;
       big = big > d_.c_max ? big : d_.c_max;
       scan_smax_ = ceil_div(big, SCAN_TILE) + 1;
-      scan_status_ = (u64*)dev("scan_status", 8ull * 4 * scan_smax_);
+      // 4 arrays x smax 4096-tiles, or 16 arrays x 4*smax 1024-tiles
+      scan_status_ = (u64*)dev("scan_status", 8ull * 16 * (SCAN_TILE / 1024) * scan_smax_);
       scan_ctl_ = (u32*)dev("scan_ctl", 64);
     }
     d_.tot = (u32*)dev("tot", 4ull * 128);
@@ -970,6 +971,7 @@ class Engine {
  private:
   void launch_scan(hipStream_t s, std::initializer_list<std::pair<const u32*, u32*>> arrs, const u32* n,
                    u32 nmax, u32 slot, const u32* lo = nullptr) {
+    if (arrs.size() > 4) throw std::runtime_error("launch_scan: at most 4 arrays");
     ScanArgs a{};
     a.lo = lo;
     u32 k = 0;
@@ -979,7 +981,22 @@ class Engine {
     a.nmax = nmax;
     a.tot_slot = slot;
     u32 nb = ceil_div(nmax ? nmax : 1, SCAN_TILE);
-    hipLaunchKernelGGL(k_scan, dim3(nb), dim3(1024), 0, s, a, d_.tot, scan_status_, scan_ctl_, scan_smax_);
+    hipLaunchKernelGGL((k_scan<4, 4>), dim3(nb), dim3(1024), 0, s, a, d_.tot, scan_status_, scan_ctl_, scan_smax_);
+  }
+  // nr (<= 4) rank pairs of arrays (in0 + r*stride -> out0 + r*stride, in1 + ... -> out1 +
+  // ...) in one launch; totals -> tot[slot + 2r], tot[slot + 2r + 1]
+  void launch_scan_ranks(hipStream_t s, const u32* in0, u32* out0, const u32* in1, u32* out1, u64 stride, u32 nr,
+                         const u32* n, u32 nmax, u32 slot) {
+    if (nr == 0 || nr > 4) throw std::runtime_error("launch_scan_ranks: 1..4 ranks per launch");
+    ScanArgs a{};
+    a.in[0] = in0; a.out[0] = out0; a.in[1] = in1; a.out[1] = out1;
+    a.stride = stride;
+    a.narr = 2 * nr;
+    a.n = n;
+    a.nmax = nmax;
+    a.tot_slot = slot;
+    u32 nb = ceil_div(nmax ? nmax : 1, SCAN_TILE);
+    hipLaunchKernelGGL((k_scan<8, 4>), dim3(nb), dim3(1024), 0, s, a, d_.tot, scan_status_, scan_ctl_, scan_smax_);
   }
 
   // returns index (0/1) of the buffer holding the sorted output
@@ -1029,15 +1046,12 @@ class Engine {
   void launch_pack(hipStream_t s, const DS& d) {
     Range rg("chanamq.X1.pack");
     hipLaunchKernelGGL(k_pack_count, blocks(d.pub_max, 256), dim3(256), 0, s, d);
-    for (u32 r = 0; r < d.world; r += 2) {
-      u64 a = (u64)r * d.pub_cap, b = (u64)(r + 1) * d.pub_cap;
-      if (r + 1 < d.world)
-        launch_scan(s, {{d.xp_cnt + a, d.xp_cnt_off + a}, {d.xp_byt + a, d.xp_byt_off + a},
-                        {d.xp_cnt + b, d.xp_cnt_off + b}, {d.xp_byt + b, d.xp_byt_off + b}},
-                    &d.ctr->n_pubs, d.pub_max, TS_XSCAN + 2 * r);
-      else
-        launch_scan(s, {{d.xp_cnt + a, d.xp_cnt_off + a}, {d.xp_byt + a, d.xp_byt_off + a}}, &d.ctr->n_pubs,
-                    d.pub_max, TS_XSCAN + 2 * r);
+    // per destination rank: record and byte offsets; 4 ranks (8 arrays) per launch
+    for (u32 r0 = 0; r0 < d.world; r0 += 4) {
+      const u64 a = (u64)r0 * d.pub_cap;
+      const u32 nr = d.world - r0 < 4 ? d.world - r0 : 4;
+      launch_scan_ranks(s, d.xp_cnt + a, d.xp_cnt_off + a, d.xp_byt + a, d.xp_byt_off + a, d.pub_cap, nr,
+                        &d.ctr->n_pubs, d.pub_max, TS_XSCAN + 2 * r0);
     }
     hipLaunchKernelGGL(k_pack_bases, dim3(1), dim3(64), 0, s, d);
     hipLaunchKernelGGL(k_pack, blocks((u64)d.pub_max * 64, 256), dim3(256), 0, s, d);
@@ -1104,7 +1118,7 @@ class Engine {
   void launch_phase_b(hipStream_t s, const DS& d, bool dispatch = true) {
     Range rg("chanamq.X1.import");
     hipLaunchKernelGGL(k_import_prep, dim3(1), dim3(64), 0, s, d);
-    hipLaunchKernelGGL(k_import, wave_blocks(d.import_max), dim3(256), 0, s, d);
+    hipLaunchKernelGGL(k_import, blocks(d.import_max, 256), dim3(256), 0, s, d);
     launch_route(s, d, d.import_max);
     launch_tail(s, d, dispatch);
   }
