@@ -1564,6 +1564,7 @@ DEV u32 wave_or(u32 v) {
 template <int PASS>
 struct RouteAcc {
   u32 nq = 0, nq_all = 0, rmask = 0;
+  u32 nrem = 0, rq = INVALID;   // remote queues matched, the first of them
   bool has_cons = false;
 };
 
@@ -1575,6 +1576,11 @@ DEV void route_emit(const DS& d, RouteAcc<PASS>& a, u32 p, u32 wbase, u32 srank,
   bool remote = valid && owner != me;
   bool local = valid && !remote;
   a.rmask |= wave_or(remote ? (1u << owner) : 0u);
+  const u64 rm = __ballot(remote);
+  if (rm) {
+    if (a.rq == INVALID) a.rq = (u32)__shfl((int)q, (int)(__ffsll((unsigned long long)rm) - 1));
+    a.nrem += (u32)__popcll(rm);
+  }
   u64 lm = __ballot(local);
   bool cons = local && d.q_cons_n[q] != 0;
   if (__ballot(cons || remote)) a.has_cons = true;
@@ -1615,7 +1621,7 @@ DEV void route_one(const DS& d, u32 p, u32 lane) {
   }
   RouteAcc<PASS> a;
   const i32 ex = pb.exch;
-  if (pb.flags & MF_RESTORE) {   // recovered message: exactly its queue
+  if (pb.flags & (MF_RESTORE | MF_ONEQ)) {   // recovered / origin-routed: exactly its queue
     route_emit<PASS>(d, a, p, wbase, srank, (u32)pb.keyhash, lane == 0, lane);
   } else if (ex >= 0) {
     u32 xt = d.x_type[ex];
@@ -1658,6 +1664,8 @@ DEV void route_one(const DS& d, u32 p, u32 lane) {
   if (PASS == 0 && lane == 0) {
     u32 nq = a.nq, rmask = a.rmask;
     u32 ret = 0;
+    if (!(pb.flags & MF_IMPORTED))   // a single remote queue travels with the record (MF_ONEQ)
+      pb.xid = a.nrem == 1 ? (u64)a.rq : ~0ull;
     if (pb.flags & MF_IMPORTED) {
       rmask = 0;  // imported records are never forwarded again
     } else if (ex < 0 && !(pb.flags & MF_RESTORE)) {
@@ -1923,6 +1931,10 @@ __global__ __launch_bounds__(256) void k_pack(DS d) {
       rd.props_len = pb.props_len;
       rd.exch = pb.exch;
       rd.flags = pb.flags & (MF_PERSIST | MF_HAS_TS);
+      if (pb.xid != ~0ull) {   // the owner skips re-routing: its one queue is known
+        rd.flags |= MF_ONEQ;
+        rd.tq = (u32)pb.xid;
+      }
       rd.ex_len = (u8)pb.ex_len;
       rd.rk_len = (u8)pb.rk_len;
       rd.expire_ms = pb.expire_ms;
@@ -1988,8 +2000,9 @@ DEV void import_one(const DS& d, u32 i) {
   pb.expire_ms = rd.expire_ms;
   pb.ts_ms = rd.ts_ms;
   const u8* key = d.recv_pay + roff + rd.ex_len;
-  pb.keyhash = (rd.flags & MF_RESTORE) ? (u64)rd.tq : fnv1a64_dev(key, rd.rk_len);
-  pb.nwords = build_keyvec(d, key, rd.rk_len, pi);
+  const bool routed = rd.flags & (MF_RESTORE | MF_ONEQ);   // target queue in tq, no matching
+  pb.keyhash = routed ? (u64)rd.tq : fnv1a64_dev(key, rd.rk_len);
+  pb.nwords = routed ? 0u : build_keyvec(d, key, rd.rk_len, pi);
   pb.nq = 0; pb.slot_bytes = 0; pb.msg = INVALID; pb.xid = rd.xid;
   pb.pad = src;  // source rank (pair ordering)
   d.pubs[pi] = pb;

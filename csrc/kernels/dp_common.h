@@ -30,7 +30,8 @@ enum : u32 { EX_DIRECT = 0, EX_FANOUT = 1, EX_TOPIC = 2, EX_HEADERS = 3 };
 enum : u32 {
   MF_PERSIST = 1, MF_MANDATORY = 2, MF_IMMEDIATE = 4, MF_HAS_TS = 8, MF_IMPORTED = 16,
   MF_RESTORE = 32,      // recovered from the store: enqueue into exactly RDesc.tq, keep RDesc.xid
-  MF_REDELIVERED = 64   // enqueue with the redelivered flag (recovered unacks)
+  MF_REDELIVERED = 64,  // enqueue with the redelivered flag (recovered unacks)
+  MF_ONEQ = 128         // cross-rank record routed at its origin to exactly one queue: RDesc.tq
 };
 
 // ---- unacked slot states
@@ -90,7 +91,8 @@ struct Pub {            // decoded Basic.Publish
   u32 slot_bytes;       // bytes reserved in the body log
   u32 msg;              // message-table index, -1 if not stored
   u32 pad;
-  u64 xid;              // MF_RESTORE: message id to keep
+  u64 xid;              // MF_RESTORE: message id to keep; local publish (route pass 0):
+                        // its only remote queue, ~0 if it routed to none or several
 };
 
 // cross-rank publish record (sharded queues): the ingress rank ships each publish once
@@ -107,7 +109,7 @@ struct RDesc {
   i64 expire_ms;
   i64 ts_ms;
   u64 xid;              // MF_RESTORE: the message id to keep
-  u32 tq;               // MF_RESTORE: target queue slot
+  u32 tq;               // MF_RESTORE / MF_ONEQ: target queue slot
   u32 pad[3];
 };
 static_assert(sizeof(RDesc) == 64, "RDesc layout");
