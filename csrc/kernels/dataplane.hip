@@ -1486,6 +1486,11 @@ __global__ __launch_bounds__(256) void k_topic_mfma(DS d) {
   const u32 nw = (gridDim.x * blockDim.x) >> 6;
   for (u32 wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6; wave < ntiles; wave += nw) {
     u32 it = wave / ntb, jt = wave % ntb;
+    // a tile of records that all arrived routed (MF_ONEQ / MF_RESTORE: phase B imports)
+    // has nothing to match
+    const u32 pi = lo + it * 16 + lane;
+    const bool need = lane < 16 && pi < npub && !(d.pubs[pi].flags & (MF_ONEQ | MF_RESTORE));
+    if (!__ballot(need)) continue;
     topic_tile(d, lo + it * 16, jt * 16, jt, ntb, npub, lane);
   }
 }
