@@ -1350,25 +1350,32 @@ __global__ __launch_bounds__(1024) void k_scan(ScanArgs a, u32* tot, u64* status
 }
 
 // ============================================================================ radix sort
-// stable LSD radix sort of (key, val) u32 pairs, 8 bits per pass; n from device.
-// per-tile digit histograms; the last occupied tile to finish turns them into the
-// digit-major offsets of the occupied tiles (fused k_rs_offsets: one launch less per pass)
+// stable LSD radix sort of (key, val) u32 pairs, DB bits per pass (8, or 11 for keys of
+// 9..11 bits -- queue << rank_bits | rank at 4..8 GPUs -- in one pass instead of two);
+// n from device.  Per-tile digit histograms; the last occupied tile to finish turns them
+// into the digit-major offsets of the occupied tiles (fused k_rs_offsets)
+template <int DB>
 DEV void rs_offsets(const u32* hist, u32* hscan, u32 T, u32 ntiles, u32* lds) {
-  const u32 dg = threadIdx.x;
+  constexpr u32 PER = (1u << DB) / 256;   // consecutive digits per thread
+  const u32 d0 = threadIdx.x * PER;
   u32 sum = 0;
-  for (u32 t = 0; t < T; ++t) sum += hist[dg * ntiles + t];
+  for (u32 j = 0; j < PER; ++j)
+    for (u32 t = 0; t < T; ++t) sum += hist[(d0 + j) * ntiles + t];
   u32 all;
   u32 run = block_scan<256>(sum, lds, all);
-  for (u32 t = 0; t < T; ++t) {
-    u32 h = hist[dg * ntiles + t];
-    hscan[dg * ntiles + t] = run;
-    run += h;
-  }
+  for (u32 j = 0; j < PER; ++j)
+    for (u32 t = 0; t < T; ++t) {
+      u32 h = hist[(d0 + j) * ntiles + t];
+      hscan[(d0 + j) * ntiles + t] = run;
+      run += h;
+    }
 }
 
+template <int DB>
 __global__ __launch_bounds__(256) void k_rs_hist(const u32* keys, const u32* np, u32 shift, u32* hist,
                                                  u32* hscan, u32* ticket, u32 ntiles) {
-  __shared__ u32 cnt[256];
+  constexpr u32 D = 1u << DB;
+  __shared__ u32 cnt[D];
   __shared__ u32 lds[256 / 64 + 1];
   __shared__ u32 s_last;
   u32 tid = threadIdx.x, t = blockIdx.x;
@@ -1376,15 +1383,15 @@ __global__ __launch_bounds__(256) void k_rs_hist(const u32* keys, const u32* np,
   u32 T = (n + SORT_TILE - 1) / SORT_TILE;
   if (T > ntiles) T = ntiles;
   if (t >= T) return;   // only occupied tiles take part (and take a ticket)
-  cnt[tid] = 0;
+  for (u32 k = tid; k < D; k += 256) cnt[k] = 0;
   __syncthreads();
   u32 base = t * SORT_TILE;
   for (u32 j = 0; j < SORT_TILE / 256; ++j) {
     u32 i = base + j * 256 + tid;
-    if (i < n) atomicAdd(&cnt[(keys[i] >> shift) & 255], 1u);
+    if (i < n) atomicAdd(&cnt[(keys[i] >> shift) & (D - 1)], 1u);
   }
   __syncthreads();
-  hist[tid * ntiles + t] = cnt[tid];
+  for (u32 k = tid; k < D; k += 256) hist[k * ntiles + t] = cnt[k];
   __threadfence();
   __syncthreads();
   if (tid == 0) s_last = atomicAdd(ticket, 1u) == T - 1;
@@ -1392,27 +1399,30 @@ __global__ __launch_bounds__(256) void k_rs_hist(const u32* keys, const u32* np,
   if (!s_last) return;
   __threadfence();
   if (tid == 0) *ticket = 0;
-  rs_offsets(hist, hscan, T, ntiles, lds);
+  rs_offsets<DB>(hist, hscan, T, ntiles, lds);
 }
 
+template <int DB>
 __global__ __launch_bounds__(256) void k_rs_scatter(const u32* kin, const u32* vin, u32* kout, u32* vout,
                                                     const u32* np, u32 shift, const u32* hscan,
                                                     u32 ntiles) {
-  __shared__ u32 wc[4][256];
+  constexpr u32 D = 1u << DB;
+  __shared__ u32 wc[4][D];
   u32 tid = threadIdx.x, t = blockIdx.x, w = tid >> 6, lane = tid & 63;
   u32 n = *np;
   u32 base = t * SORT_TILE;
   if (base >= n) return;
-  for (u32 i = tid; i < 1024; i += 256) ((u32*)wc)[i] = 0;
+  for (u32 i = tid; i < 4 * D; i += 256) ((u32*)wc)[i] = 0;
   __syncthreads();
   u32 wbase = base + w * (SORT_TILE / 4);
   // pass 1: per-wave digit counts
   for (u32 c = 0; c < SORT_TILE / 256; ++c) {
     u32 i = wbase + c * 64 + lane;
     bool valid = i < n;
-    u32 dg = valid ? (kin[i] >> shift) & 255 : 0;
+    u32 dg = valid ? (kin[i] >> shift) & (D - 1) : 0;
     u64 peers = __ballot(valid);
-    for (u32 bb = 0; bb < 8; ++bb) {
+#pragma unroll
+    for (u32 bb = 0; bb < DB; ++bb) {
       u64 m = __ballot((dg >> bb) & 1);
       peers &= ((dg >> bb) & 1) ? m : ~m;
     }
@@ -1421,8 +1431,7 @@ __global__ __launch_bounds__(256) void k_rs_scatter(const u32* kin, const u32* v
     __builtin_amdgcn_wave_barrier();
   }
   __syncthreads();
-  {
-    u32 dg = tid;
+  for (u32 dg = tid; dg < D; dg += 256) {
     u32 run = hscan[dg * ntiles + t];
     for (u32 ww = 0; ww < 4; ++ww) { u32 x = wc[ww][dg]; wc[ww][dg] = run; run += x; }
   }
@@ -1431,9 +1440,10 @@ __global__ __launch_bounds__(256) void k_rs_scatter(const u32* kin, const u32* v
     u32 i = wbase + c * 64 + lane;
     bool valid = i < n;
     u32 key = valid ? kin[i] : 0;
-    u32 dg = (key >> shift) & 255;
+    u32 dg = (key >> shift) & (D - 1);
     u64 peers = __ballot(valid);
-    for (u32 bb = 0; bb < 8; ++bb) {
+#pragma unroll
+    for (u32 bb = 0; bb < DB; ++bb) {
       u64 m = __ballot((dg >> bb) & 1);
       peers &= ((dg >> bb) & 1) ? m : ~m;
     }

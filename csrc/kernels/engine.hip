@@ -373,8 +373,8 @@ class Engine {
     d_.req_q_n = (u32*)dev("req_q_n", 4ull * d_.q_max);
 
     ntiles_max_ = ceil_div(d_.pair_max, SORT_TILE);
-    d_.hist = (u32*)dev("hist", 4ull * 256 * ntiles_max_);
-    d_.hist_scan = (u32*)dev("hist_scan", 4ull * 256 * ntiles_max_);
+    d_.hist = (u32*)dev("hist", 4ull * 2048 * ntiles_max_);        // up to 11-bit digits
+    d_.hist_scan = (u32*)dev("hist_scan", 4ull * 2048 * ntiles_max_);
     d_.scan_tmp = (u32*)dev("scan_tmp", 4ull * 1024);
     {   // look-back scan state: status words for the largest scan, ticket/epoch
       u64 big = d_.pub_cap > d_.cmd_max ? d_.pub_cap : d_.cmd_max;
@@ -1002,11 +1002,18 @@ class Engine {
   // returns index (0/1) of the buffer holding the sorted output
   u32 radix_sort(hipStream_t s, u32** keys, u32** vals, const u32* n, u32 nmax, u32 bits) {
     u32 ntiles = ceil_div(nmax, SORT_TILE);
+    if (bits > 8 && bits <= 11) {   // one 11-bit pass instead of two 8-bit ones
+      hipLaunchKernelGGL(k_rs_hist<11>, dim3(ntiles), dim3(256), 0, s, keys[0], n, 0u, d_.hist, d_.hist_scan,
+                         &d_.tot[TS_RS_TICKET], ntiles);
+      hipLaunchKernelGGL(k_rs_scatter<11>, dim3(ntiles), dim3(256), 0, s, keys[0], vals[0], keys[1], vals[1], n, 0u,
+                         d_.hist_scan, ntiles);
+      return 1;
+    }
     u32 src = 0;
     for (u32 shift = 0; shift < bits; shift += 8) {
-      hipLaunchKernelGGL(k_rs_hist, dim3(ntiles), dim3(256), 0, s, keys[src], n, shift, d_.hist, d_.hist_scan,
+      hipLaunchKernelGGL(k_rs_hist<8>, dim3(ntiles), dim3(256), 0, s, keys[src], n, shift, d_.hist, d_.hist_scan,
                          &d_.tot[TS_RS_TICKET], ntiles);
-      hipLaunchKernelGGL(k_rs_scatter, dim3(ntiles), dim3(256), 0, s, keys[src], vals[src], keys[src ^ 1],
+      hipLaunchKernelGGL(k_rs_scatter<8>, dim3(ntiles), dim3(256), 0, s, keys[src], vals[src], keys[src ^ 1],
                          vals[src ^ 1], n, shift, d_.hist_scan, ntiles);
       src ^= 1;
     }
@@ -1067,7 +1074,8 @@ class Engine {
     u32* pv[2] = {d.pair_v[0], d.pair_v[1]};
     u32 psrc = radix_sort(s, pk, pv, &d.tot[TS_PAIR_N], d.pair_max, d.q_bits + d.rank_bits);
     const u32 pbits = d.q_bits + d.rank_bits;
-    const u32 hs_ntiles = pbits <= 8 ? ceil_div(d.pair_max, SORT_TILE) : 0;   // single pass: starts from hist_scan
+    // single pass (<= 11 key bits): queue starts straight from the digit offsets
+    const u32 hs_ntiles = pbits <= 11 ? ceil_div(d.pair_max, SORT_TILE) : 0;
     if (!hs_ntiles) hipLaunchKernelGGL(k_qfirst, blocks(d.pair_max, 256), dim3(256), 0, s, d, psrc);
     hipLaunchKernelGGL(k_ring_plan, blocks(d.pair_max, 256), dim3(256), 0, s, d, psrc, hs_ntiles);
     hipLaunchKernelGGL(k_enqueue, blocks(d.pair_max, 256), dim3(256), 0, s, d, psrc, hs_ntiles);

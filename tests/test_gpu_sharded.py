@@ -18,13 +18,14 @@ pytestmark = pytest.mark.gpu
 HERE = os.path.dirname(os.path.abspath(__file__))
 
 
-def run_gpu_cluster(spec, world, graph=True, lag=0, extra_steps=0):
+def run_gpu_cluster(spec, world, graph=True, lag=0, extra_steps=0, cfg=None):
     import torch
 
     from chanamq_amd.engine.dataplane import GpuDataPlane
     from chanamq_amd.parallel.cluster import LocalCluster
     torch.cuda.set_device(0)
-    cl = LocalCluster(lambda **kw: GpuDataPlane(graph=graph, exchange_lag=lag, **CFG, **kw), world)
+    c = dict(CFG, **(cfg or {}))
+    cl = LocalCluster(lambda **kw: GpuDataPlane(graph=graph, exchange_lag=lag, **c, **kw), world)
     for r in range(world):
         apply(cl[r], spec, rank=r, world=world)
     outs = []
@@ -42,6 +43,19 @@ def run_gpu_cluster(spec, world, graph=True, lag=0, extra_steps=0):
 def test_gpu_cluster_matches_oracle(gpu, name, world):
     single = run_single(SHARDED[name](), world)
     got = run_gpu_cluster(SHARDED[name](), world)
+    for k, (a, b) in enumerate(zip(single, got)):
+        assert set(a) == set(b), (k, sorted(a), sorted(b))
+        for c in a:
+            assert a[c] == b[c], (k, c)
+
+
+@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("name", sorted(SHARDED))
+def test_gpu_cluster_wide_pair_keys(gpu, name, world):
+    """q_max 512: pair keys of 10-11 bits (queue << rank_bits | rank), sorted in the single
+    11-bit radix pass, queue starts read from its digit offsets (no k_qfirst)."""
+    single = run_single(SHARDED[name](), world)
+    got = run_gpu_cluster(SHARDED[name](), world, cfg=dict(q_max=512))
     for k, (a, b) in enumerate(zip(single, got)):
         assert set(a) == set(b), (k, sorted(a), sorted(b))
         for c in a:
