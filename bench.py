@@ -181,7 +181,7 @@ def main():
     Q = max(1, args.queues // shards) if fan else args.queues    # queues per rank
     qtot = Q * shards
     qcap = (1 << 20) if not fan else (1 << 14)
-    cfg = dict(c_max=max(1024, P + Q + 1), chpc=4, q_max=max(64, qtot * 2), cons_max=max(1024, Q + 16),
+    cfg = dict(c_max=max(1024, P + Q + 1), chpc=4, q_max=max(64, qtot + 64), cons_max=max(1024, Q + 16),
                seg_max=max(1024, P + Q), cmd_max=1 << 17, deliv_max=(1 << 16) if not fan else (1 << 18),
                msg_max=1 << 22, ucap=4096, deliver_cap=8192,
                ingress_cap=max(32 << 20, P * args.chunk + (4 << 20)),

@@ -46,7 +46,7 @@ def main():
     W, P, Q = args.world, args.producers, args.queues
     qtot = Q * W
     sm = ShardMap(W)
-    cfg = dict(c_max=max(1024, P + Q + 1), chpc=4, q_max=max(64, qtot * 2), cons_max=max(1024, Q + 16),
+    cfg = dict(c_max=max(1024, P + Q + 1), chpc=4, q_max=max(64, qtot + 64), cons_max=max(1024, Q + 16),
                seg_max=max(1024, P + Q), cmd_max=1 << 17, deliv_max=1 << 16, msg_max=1 << 22, ucap=4096,
                deliver_cap=8192, ingress_cap=max(32 << 20, P * args.chunk + (4 << 20)), egress_cap=128 << 20,
                log_bytes=args.log_gib << 30, ring_pool=Q * (1 << 20) + qtot + 1024, tb_max=max(64, qtot),

@@ -1354,21 +1354,63 @@ __global__ __launch_bounds__(1024) void k_scan(ScanArgs a, u32* tot, u64* status
 // 9..11 bits -- queue << rank_bits | rank at 4..8 GPUs -- in one pass instead of two);
 // n from device.  Per-tile digit histograms; the last occupied tile to finish turns them
 // into the digit-major offsets of the occupied tiles (fused k_rs_offsets)
+// hist is tile-major (hist[t * D + digit]: each tile writes, and the offsets pass reads,
+// contiguous words); hscan is digit-major (hscan[digit * ntiles + t]) for the scatter and
+// for the queue starts (k_ring_plan / k_enqueue read tile 0 of a digit)
 template <int DB>
 DEV void rs_offsets(const u32* hist, u32* hscan, u32 T, u32 ntiles, u32* lds) {
-  constexpr u32 PER = (1u << DB) / 256;   // consecutive digits per thread
+  constexpr u32 D = 1u << DB, PER = D / 256;   // consecutive digits per thread
   const u32 d0 = threadIdx.x * PER;
+  u32 tot[PER];
+#pragma unroll
+  for (u32 j = 0; j < PER; ++j) tot[j] = 0;
+  // tiles 4 at a time: 4 * PER independent loads in flight per round trip
+  u32 t = 0;
+  for (; t + 4 <= T; t += 4) {
+    u32 h[4][PER];
+#pragma unroll
+    for (u32 a = 0; a < 4; ++a)
+#pragma unroll
+      for (u32 j = 0; j < PER; ++j) h[a][j] = hist[(t + a) * D + d0 + j];
+#pragma unroll
+    for (u32 a = 0; a < 4; ++a)
+#pragma unroll
+      for (u32 j = 0; j < PER; ++j) tot[j] += h[a][j];
+  }
+  for (; t < T; ++t) {
+#pragma unroll
+    for (u32 j = 0; j < PER; ++j) tot[j] += hist[t * D + d0 + j];
+  }
   u32 sum = 0;
-  for (u32 j = 0; j < PER; ++j)
-    for (u32 t = 0; t < T; ++t) sum += hist[(d0 + j) * ntiles + t];
+#pragma unroll
+  for (u32 j = 0; j < PER; ++j) sum += tot[j];
   u32 all;
   u32 run = block_scan<256>(sum, lds, all);
-  for (u32 j = 0; j < PER; ++j)
-    for (u32 t = 0; t < T; ++t) {
-      u32 h = hist[(d0 + j) * ntiles + t];
-      hscan[(d0 + j) * ntiles + t] = run;
-      run += h;
+#pragma unroll
+  for (u32 j = 0; j < PER; ++j) { const u32 x = tot[j]; tot[j] = run; run += x; }   // digit starts
+  t = 0;
+  for (; t + 4 <= T; t += 4) {
+    u32 h[4][PER];
+#pragma unroll
+    for (u32 a = 0; a < 4; ++a)
+#pragma unroll
+      for (u32 j = 0; j < PER; ++j) h[a][j] = hist[(t + a) * D + d0 + j];
+#pragma unroll
+    for (u32 a = 0; a < 4; ++a)
+#pragma unroll
+      for (u32 j = 0; j < PER; ++j) {
+        hscan[(d0 + j) * ntiles + t + a] = tot[j];
+        tot[j] += h[a][j];
+      }
+  }
+  for (; t < T; ++t) {
+#pragma unroll
+    for (u32 j = 0; j < PER; ++j) {
+      const u32 h = hist[t * D + d0 + j];
+      hscan[(d0 + j) * ntiles + t] = tot[j];
+      tot[j] += h;
     }
+  }
 }
 
 template <int DB>
@@ -1391,7 +1433,7 @@ __global__ __launch_bounds__(256) void k_rs_hist(const u32* keys, const u32* np,
     if (i < n) atomicAdd(&cnt[(keys[i] >> shift) & (D - 1)], 1u);
   }
   __syncthreads();
-  for (u32 k = tid; k < D; k += 256) hist[k * ntiles + t] = cnt[k];
+  for (u32 k = tid; k < D; k += 256) hist[t * D + k] = cnt[k];
   __threadfence();
   __syncthreads();
   if (tid == 0) s_last = atomicAdd(ticket, 1u) == T - 1;

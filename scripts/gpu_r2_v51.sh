@@ -1,0 +1,7 @@
+set -o pipefail
+O=gpurun_out/r2_v51; mkdir -p $O
+timeout -k 10 400 python -u -m pytest tests/test_gpu_sharded.py tests/test_gpu_dataplane.py tests/test_gpu_scale.py -m gpu -x -v --timeout 120 --timeout-method thread > $O/gpu_tests.log 2>&1 && tail -2 $O/gpu_tests.log &&
+timeout -k 10 240 python -u bench.py --workload fanout > $O/bench_fanout.json 2> $O/f.err && cat $O/bench_fanout.json &&
+cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT &&
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/prof_w8 -o run -- python3 bench/world_rehearsal.py --world 8 --steps 16 --warmup 4 > $O/prof_w8.log 2>&1 && grep '"world"' $O/prof_w8.log &&
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/prof_w4 -o run -- python3 bench/world_rehearsal.py --world 4 --steps 16 --warmup 4 > $O/prof_w4.log 2>&1 && grep '"world"' $O/prof_w4.log
