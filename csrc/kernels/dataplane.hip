@@ -1364,16 +1364,17 @@ DEV void rs_offsets(const u32* hist, u32* hscan, u32 T, u32 ntiles, u32* lds) {
   u32 tot[PER];
 #pragma unroll
   for (u32 j = 0; j < PER; ++j) tot[j] = 0;
-  // tiles 4 at a time: 4 * PER independent loads in flight per round trip
+  // tiles RB at a time: RB * PER independent loads in flight per round trip
+  constexpr u32 RB = 8;
   u32 t = 0;
-  for (; t + 4 <= T; t += 4) {
-    u32 h[4][PER];
+  for (; t + RB <= T; t += RB) {
+    u32 h[RB][PER];
 #pragma unroll
-    for (u32 a = 0; a < 4; ++a)
+    for (u32 a = 0; a < RB; ++a)
 #pragma unroll
       for (u32 j = 0; j < PER; ++j) h[a][j] = hist[(t + a) * D + d0 + j];
 #pragma unroll
-    for (u32 a = 0; a < 4; ++a)
+    for (u32 a = 0; a < RB; ++a)
 #pragma unroll
       for (u32 j = 0; j < PER; ++j) tot[j] += h[a][j];
   }
@@ -1389,14 +1390,14 @@ DEV void rs_offsets(const u32* hist, u32* hscan, u32 T, u32 ntiles, u32* lds) {
 #pragma unroll
   for (u32 j = 0; j < PER; ++j) { const u32 x = tot[j]; tot[j] = run; run += x; }   // digit starts
   t = 0;
-  for (; t + 4 <= T; t += 4) {
-    u32 h[4][PER];
+  for (; t + RB <= T; t += RB) {
+    u32 h[RB][PER];
 #pragma unroll
-    for (u32 a = 0; a < 4; ++a)
+    for (u32 a = 0; a < RB; ++a)
 #pragma unroll
       for (u32 j = 0; j < PER; ++j) h[a][j] = hist[(t + a) * D + d0 + j];
 #pragma unroll
-    for (u32 a = 0; a < 4; ++a)
+    for (u32 a = 0; a < RB; ++a)
 #pragma unroll
       for (u32 j = 0; j < PER; ++j) {
         hscan[(d0 + j) * ntiles + t + a] = tot[j];
