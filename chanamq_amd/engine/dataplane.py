@@ -345,18 +345,25 @@ class GpuDataPlane(ControlState):
         """Persist records of the last finished step: [(msg_id, ts_ms, q, qpos, expire_ms,
         ex, rk, props, body)] — durable queue x persistent message, one per enqueue."""
         c = self.last_counters
+        self._check_records(c)
         n = min(c["n_persist"], self.info["persist_max"])
         if not n:
             return []
-        if c["n_persist_overflow"] or c["n_persist"] > self.info["persist_max"]:
-            raise RuntimeError("persist buffer overflow: raise persist_max / persist_bytes")
         raw = self.eng.host_view(f"persist{self._last_parity}")[:c["persist_used"]]
         return parse_persist(raw)
+
+    def _check_records(self, c):
+        """The device drops store records past persist_max: never commit a partial step."""
+        if c["n_persist_overflow"] or c["n_persist"] > self.info["persist_max"] or \
+                c["n_consumed"] > self.info["persist_max"]:
+            raise RuntimeError(f"persist record buffer overflow ({c['n_persist']} persist / {c['n_consumed']} "
+                               f"consumed records > persist_max {self.info['persist_max']})")
 
     def take_consumed(self):
         """[(msg_id, q, qpos, kind)] of persistent messages that left durable queues."""
         out, self._get_consumed = self._get_consumed, []
         c = self.last_counters
+        self._check_records(c)
         n = min(c["n_consumed"], self.info["persist_max"])
         if not n:
             return out
@@ -378,8 +385,7 @@ class GpuDataPlane(ControlState):
         c = getattr(self, "last_counters", None)
         if not c:
             return b"", b""
-        if c["n_persist_overflow"] or c["n_persist"] > self.info["persist_max"]:
-            raise RuntimeError("persist buffer overflow: raise persist_max / persist_bytes")
+        self._check_records(c)
         p = self._last_parity
         persist = bytes(self.eng.host_view(f"persist{p}")[:c["persist_used"]]) if c["n_persist"] else b""
         n = min(c["n_consumed"], self.info["persist_max"])

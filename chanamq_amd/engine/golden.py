@@ -41,9 +41,11 @@ class _Msg:
 class GoldenDataPlane(ControlState):
     def __init__(self, hash_wildcard=True, ucap=8192, deliver_cap=4096, carry_cap=1 << 20,
                  egress_cap=96 << 20, deliv_max=65536, exchanger=None, xfer_desc_max=1 << 15,
-                 xfer_bytes=1 << 24, persist=False, exchange_lag=0, **kw):
+                 xfer_bytes=1 << 24, persist=False, exchange_lag=0, persist_max=1 << 16, **kw):
         super().__init__(hash_wildcard=hash_wildcard, **kw)
         self.persist = persist
+        self.persist_max = persist_max    # k_dequeue: durable TTL skips <= persist_max / 4 a step
+        self._ttl_budget = 0
         self.lag = bool(exchange_lag) and self.world > 1
         self._lag_prev = []                 # exchange_lag: records received last step
         self._persist_out, self._consumed_out = [], []
@@ -574,6 +576,7 @@ class GoldenDataPlane(ControlState):
         # ---- dequeue (k_dequeue)
         delivs = []
         budget = [0]
+        self._ttl_budget = 0
         for q in sorted(self.queue_by_slot):
             delivs.extend(self._dequeue(q, now_ms, budget))
         # ---- tags: stable sort by chslot
@@ -759,7 +762,15 @@ class GoldenDataPlane(ControlState):
         qq = self.queue_by_slot[q]
         ring = self.ring[q]
         cnt = self.counters
+        budget_q = self.persist and qq.durable
+        left = 0
         while ring and ring[0][2] and ring[0][2] <= now_ms:
+            if budget_q and not left:   # reserved 64 at a time (dataplane.hip k_dequeue)
+                if self._ttl_budget + 64 > self.persist_max >> 2:
+                    break
+                self._ttl_budget += 64
+                left = 64
+            left -= 1
             self._consumed(ring[0][0], q, self.qpos_head[q], 1)
             self._release(ring.pop(0)[0])
             self.qpos_head[q] += 1

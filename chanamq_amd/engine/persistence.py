@@ -146,6 +146,12 @@ class GpuPersistence:
             self.dirty = False
 
     # ------------------------------------------------------------------ control rows
+    def control_commit(self):
+        """Topology rows (vhosts, exchanges, queues, bindings) written by the control
+        plane reach the disk before the reply: the store buffers WAL records until a sync
+        (the write-behind worker syncs only when it has step records)."""
+        self.store.sync()
+
     def vhost(self, name):
         self.store.insert_vhost(name, True)
 
@@ -194,6 +200,7 @@ class GpuPersistence:
         if self.native is not None:
             self.native.drain()
         items, moved, seeds = [], [], []
+        adopt_refs = {}
         for q in queues:
             if not q.durable:
                 continue
@@ -214,9 +221,11 @@ class GpuPersistence:
                 _, ts, header, body, ex, rk, _, _ = m
                 items.append((q.slot, mid, ts, 0, ex.encode(), rk.encode(), header[10:], body, True, red))
                 moved.append((qid, off, mid, red))
-                n = self.refs.get(mid, 0) if self.native is None else 0
-                if self.native is None:
-                    self.refs[mid] = n + 1
+                # references of this message among the adopted rows (one message routed to
+                # several of the dead rank's durable queues keeps one row with refer = n)
+                refs = self.refs if self.native is None else adopt_refs
+                n = refs.get(mid, 0)
+                refs[mid] = n + 1
                 if n == 0 and st.select_message(mid) is None:
                     st.insert_message(mid, ts, header, body, ex, rk, True, 1, 0)
                 elif n:
@@ -229,7 +238,7 @@ class GpuPersistence:
         n = p.restore(items, now_ms) if items else 0
         st.sync()
         for qid, mid, off, size in seeds:
-            self.native.seed_row(qid, mid, off, size, False, 1)
+            self.native.seed_row(qid, mid, off, size, False, adopt_refs[mid])
         # handed over: the dead rank's store no longer holds them (its restart must not
         # deliver them a second time)
         for qid, off, mid, red in moved:

@@ -39,6 +39,7 @@ from ..protocol.codec import Method, decode_method, encode_method_frame, encode_
 HEARTBEAT = C.HEARTBEAT_FRAME
 _REPLICATED_METHODS = {"exchange.declare", "exchange.delete", "queue.declare", "queue.bind", "queue.unbind",
                        "queue.delete"}
+_STORED_METHODS = _REPLICATED_METHODS
 
 
 class _Conn:
@@ -267,6 +268,7 @@ class GpuBroker:
             self.plane.ensure_vhost(name)
             if self.persistence is not None:
                 self.persistence.vhost(name)
+                self.persistence.control_commit()
         return True
 
     def delete_vhost(self, name):
@@ -890,7 +892,12 @@ class GpuBroker:
         try:
             if self.node is not None and m.name in _REPLICATED_METHODS:
                 return self._replicated(c, ch, m)
-            return self._channel_method(c, ch, m)
+            r = self._channel_method(c, ch, m)
+            if self.persistence is not None and m.name in _STORED_METHODS:
+                # topology rows are durable before the *_ok reply leaves (c.out is
+                # flushed after this command)
+                self.persistence.control_commit()
+            return r
         except ControlError as e:
             if e.code >= 500 or e.code in (C.CONNECTION_FORCED, C.INVALID_PATH):
                 raise _Hard(e.code, e.text, e.class_id or m.class_id, e.method_id or m.method_id)
@@ -985,11 +992,19 @@ class GpuBroker:
             if m.if_empty and cnt:
                 raise ControlError(C.PRECONDITION_FAILED, f"queue '{q.name}' not empty", 50, 40)
             p.purge(q.slot)
-            if self.fe is not None:     # releases the purged messages (front end paused)
-                self._host_step({})
-            else:
-                p.step({}, now_ms=int(time.time() * 1000))
-                self._persist_step()
+            # steps release the purged messages (front end paused); a deep durable queue
+            # takes several: each step's TTL skip is bounded by its store-record buffer
+            left = cnt
+            while True:
+                if self.fe is not None:
+                    self._host_step({})
+                else:
+                    p.step({}, now_ms=int(time.time() * 1000))
+                    self._persist_step()
+                now_left = p.message_count(q.slot)
+                if not now_left or now_left >= left:   # drained, or no progress (requeues)
+                    break
+                left = now_left
             p.delete_queue(vh, q.name)
             if self.persistence is not None:
                 self.persistence.queue_deleted(vh, q.name, slot=q.slot)

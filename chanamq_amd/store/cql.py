@@ -31,8 +31,17 @@ SCHEMA = {
     "binds": ([("id", "text"), ("queue", "text"), ("key", "text"), ("args", "map<text, text>")], ["id"],
               ["queue", "key"]),
     "vhosts": ([("id", "text"), ("active", "boolean")], ["id"], []),
+    # rows of queues removed by pendingDeleteQueue (create-cassantra.cql:48-74,
+    # CassandraOpService.scala:561-604; nconsumer is an int, SURVEY A.Q22)
+    "queues_deleted": ([("id", "text"), ("offset", "bigint"), ("msgid", "bigint"), ("size", "int")], ["id"],
+                       ["offset"]),
+    "queue_metas_deleted": ([("id", "text"), ("lconsumed", "bigint"), ("nconsumer", "int"), ("durable", "boolean")],
+                            ["id"], []),
+    "queue_unacks_deleted": ([("id", "text"), ("offset", "bigint"), ("msgid", "bigint"), ("size", "int")], ["id"],
+                             ["msgid"]),
 }
-ORDER = ["vhosts", "exchanges", "binds", "queue_metas", "msgs", "queues", "queue_unacks"]
+ORDER = ["vhosts", "exchanges", "binds", "queue_metas", "msgs", "queues", "queue_unacks", "queues_deleted",
+         "queue_metas_deleted", "queue_unacks_deleted"]
 
 
 def ddl(keyspace="chanamq", replication=1):
@@ -74,6 +83,13 @@ def rows(store):
                                        ttl=ttl))
         out["queues"] += [dict(id=qid, offset=o, msgid=m, size=s) for o, m, s in msgs]
         out["queue_unacks"] += [dict(id=qid, offset=o, msgid=m, size=s) for o, m, s in unacks]
+    for qid in (store.deleted_queue_ids() if hasattr(store, "deleted_queue_ids") else ()):
+        meta, msgs, unacks = store.select_deleted_queue(qid)
+        if meta is not None:
+            lconsumed, ncons, durable = meta
+            out["queue_metas_deleted"].append(dict(id=qid, lconsumed=lconsumed, nconsumer=ncons, durable=durable))
+        out["queues_deleted"] += [dict(id=qid, offset=o, msgid=m, size=s) for o, m, s in msgs]
+        out["queue_unacks_deleted"] += [dict(id=qid, offset=o, msgid=m, size=s) for o, m, s in unacks]
     for mid in store.message_ids():
         m = store.select_message(mid)
         if m is None:
@@ -233,6 +249,12 @@ def _insert(st, t, r):
         st.insert_queue_msg(r["id"], r["offset"], r["msgid"], r["size"], 0)
     elif t == "queue_unacks":
         st.insert_queue_unack(r["id"], r["offset"], r["msgid"], r["size"])
+    elif t == "queues_deleted":
+        st.insert_deleted_queue_msg(r["id"], r["offset"], r["msgid"], r["size"])
+    elif t == "queue_metas_deleted":
+        st.insert_deleted_queue_meta(r["id"], r["lconsumed"], r["nconsumer"], r["durable"])
+    elif t == "queue_unacks_deleted":
+        st.insert_deleted_queue_unack(r["id"], r["offset"], r["msgid"], r["size"])
 
 
 __all__ = ["SCHEMA", "ORDER", "ddl", "rows", "export_cql", "export_csv", "import_csv"]

@@ -73,9 +73,34 @@ PYBIND11_MODULE(_core, m) {
   py::class_<Store>(m, "Store")
       .def(py::init<>())
       .def("open", &Store::open, py::arg("dir"), py::arg("fsync") = true)
-      .def("close", &Store::close)
-      .def("sync", &Store::sync)
-      .def("compact", &Store::compact)
+      .def("close", &Store::close, py::call_guard<py::gil_scoped_release>())
+      .def("sync", &Store::sync, py::call_guard<py::gil_scoped_release>())
+      .def("compact", &Store::compact, py::call_guard<py::gil_scoped_release>())
+      .def("set_auto_compact", &Store::set_auto_compact, py::arg("ratio"), py::arg("min_bytes"))
+      .def("wait_compaction", &Store::wait_compaction, py::call_guard<py::gil_scoped_release>())
+      .def("wal_bytes", &Store::walBytes)
+      .def("live_estimate", &Store::liveEstimate)
+      .def("compact_stats", [](Store& s) {
+             CompactStats c = s.compactStats();
+             py::dict d;
+             d["runs"] = c.runs; d["last_before"] = c.last_before; d["last_after"] = c.last_after;
+             d["tail_bytes"] = c.tail_bytes; d["last_s"] = c.last_s; d["max_lock_s"] = c.max_lock_s;
+             return d;
+           })
+      .def("deleted_queue_ids", &Store::deletedQueueIds)
+      .def("select_deleted_queue", [](Store& s, std::string q) -> py::object {
+             QueueMetaDeletedRow meta;
+             std::vector<QueueMsgRow> msgs, unacks;
+             bool has = s.selectDeletedQueue(q, &meta, &msgs, &unacks);
+             py::list ml, ul;
+             for (auto& r : msgs) ml.append(py::make_tuple(r.offset, r.msgid, r.size));
+             for (auto& r : unacks) ul.append(py::make_tuple(r.offset, r.msgid, r.size));
+             py::object m = has ? (py::object)py::make_tuple(meta.lconsumed, meta.nconsumer, meta.durable) : py::none();
+             return py::make_tuple(m, ml, ul);
+           })
+      .def("insert_deleted_queue_meta", &Store::insertDeletedQueueMeta)
+      .def("insert_deleted_queue_msg", &Store::insertDeletedQueueMsg)
+      .def("insert_deleted_queue_unack", &Store::insertDeletedQueueUnack)
       .def("row_count", &Store::rowCount)
       .def("queue_ids", &Store::queueIds)
       .def("message_ids", &Store::messageIds)

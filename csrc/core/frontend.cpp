@@ -41,6 +41,7 @@ struct FeConn {
   u32 id = 0;
   int io = 0;
   std::atomic<int> mode{M_FREE};
+  std::atomic<u32> gen{0};   // bumped when the slot is freed: egress of older steps is stale
   // IO-thread owned
   bool in_ready = false;
   bool rdhup = false;
@@ -458,6 +459,7 @@ void Frontend::drop(FeConn& c, bool notify) {
   ::close(c.fd);
   c.fd = -1;
   c.mode = M_DEAD;
+  c.gen.fetch_add(1);
   c.out.clear();
   c.out_pos = 0;
   c.inject.clear();
@@ -537,6 +539,7 @@ void Frontend::io_loop(int i) {
           c.fd = -1;
         }
         c.mode = M_FREE;
+        c.gen.fetch_add(1);
         c.out.clear();
         c.out_pos = 0;
         c.wblocked = false;
@@ -595,6 +598,7 @@ void Frontend::io_loop(int i) {
           const ConnOut& o = sc->co[id];
           if (o.len) {
             FeConn& c = *conns_[id];
+            if (!sc->gen.empty() && sc->gen[id] != c.gen.load()) continue;   // closed since: stale
             if (c.mode == M_DATA || c.mode == M_HOST) scatter_conn(c, base + o.off, o.len);
           }
         }
@@ -810,14 +814,27 @@ void Frontend::finish_oldest(std::deque<Inflight>& inflight) {
   }
   bool needs_commit = false;
   if (api_->persist && (c.n_persist || c.n_consumed)) {
+    if (c.n_persist_overflow || c.n_persist > api_->persist_max || c.n_consumed > api_->persist_max) {
+      // the device dropped store records of this step: committing the rest and releasing
+      // its confirms would acknowledge messages that are not durable (or keep rows of
+      // consumed ones).  Fail closed: the stepper stops, nothing of this step is released
+      FeEvent e;
+      e.kind = FE_ERROR;
+      e.data = "persist record buffer overflow (step " + std::to_string(f.step) + ": " +
+               std::to_string(c.n_persist) + " persist / " + std::to_string(c.n_consumed) +
+               " consumed records > persist_max " + std::to_string(api_->persist_max) + ")";
+      failed_ = true;
+      post(std::move(e));
+      return;
+    }
     FeEvent e;
     e.kind = FE_PERSIST;
     e.a = f.step;
-    e.b = c.n_persist_overflow || c.n_persist > api_->persist_max;
-    const u32 np = std::min(c.n_persist, api_->persist_max), ncs = std::min(c.n_consumed, api_->persist_max);
-    if (np) e.data.assign((const char*)api_->persist_host(api_->eng, p), c.persist_used);
-    if (ncs) e.data2.assign((const char*)api_->consumed_host(api_->eng, p), (size_t)ncs * sizeof(ConsumedRec));
-    if (persist_ && !e.b) persist_->submit(f.step, std::move(e.data), std::move(e.data2));
+    e.b = 0;
+    if (c.n_persist) e.data.assign((const char*)api_->persist_host(api_->eng, p), c.persist_used);
+    if (c.n_consumed)
+      e.data2.assign((const char*)api_->consumed_host(api_->eng, p), (size_t)c.n_consumed * sizeof(ConsumedRec));
+    if (persist_) persist_->submit(f.step, std::move(e.data), std::move(e.data2));
     else post(std::move(e));
     needs_commit = true;
   }
@@ -827,6 +844,7 @@ void Frontend::finish_oldest(std::deque<Inflight>& inflight) {
   h.step = f.step;
   h.needs_commit = needs_commit;
   h.sc.co.assign(co, co + c_max_);
+  h.sc.gen = std::move(f.gen);
   h.sc.egress = api_->egress_host(api_->eng, slot);
   if (needs_commit && api_->conn_conf) {
     const u32* cf = api_->conn_conf(api_->eng, p);
@@ -945,6 +963,8 @@ void Frontend::stepper() {
       f.p = p;
       f.step = ++step_no_;
       f.segs = std::move(seglens);
+      f.gen.resize(c_max_);
+      for (u32 k = 0; k < c_max_; ++k) f.gen[k] = conns_[k]->gen.load();
       inflight.push_back(std::move(f));
       arena_i_ = (arena_i_ + 1) % 3;
       last_step = now_ns();
@@ -981,6 +1001,7 @@ bool Frontend::stash_pend(bool copy) {
   // held bytes (its stream stays in order)
   Scatter now;
   now.co.assign(c_max_, ConnOut{0, 0});
+  now.gen = pend_.sc.gen;
   bool now_any = false, held_any = false;
   for (u32 c = 0; c < c_max_; ++c) {
     if (!pend_.sc.co[c].len) continue;

@@ -120,11 +120,14 @@ class Frontend {
 
  private:
   friend struct FeIo;
-  struct Inflight { int p; u64 step; std::vector<std::pair<u32, u32>> segs; };
+  struct Inflight { int p; u64 step; std::vector<std::pair<u32, u32>> segs; std::vector<u32> gen; };
   struct Scatter {   // one step's rendered egress, ready to write
     const u8* egress = nullptr;
     std::vector<ConnOut> co;
     std::string own;         // held copy (persistence) or host-run step
+    // connection generations when the step was submitted: bytes of a connection that
+    // closed since (its slot possibly reused by a new client) are dropped, never written
+    std::vector<u32> gen;
   };
   // needs_commit: the step's store records must commit before the confirm-gated part of
   // its egress leaves; conf = that step's confirm bytes per connection (empty = all gated)

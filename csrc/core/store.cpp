@@ -5,6 +5,9 @@
 #include <sys/stat.h>
 #include <unistd.h>
 
+#include <climits>
+#include <libgen.h>
+
 #include <chrono>
 #include <cstring>
 #include <stdexcept>
@@ -19,7 +22,7 @@ namespace {
 enum Op : uint8_t {
   OP_MSG_INS = 1, OP_MSG_REFER, OP_MSG_DEL, OP_QMETA_INS, OP_QMSG_INS, OP_QLAST, OP_QCONSUMED, OP_QFORCE_DEL,
   OP_QPENDING_DEL, OP_QDEL_CONSUMED, OP_QUNACK_INS, OP_QUNACK_DEL, OP_X_INS, OP_BIND_INS, OP_BIND_DEL,
-  OP_BIND_DEL_Q, OP_X_DEL, OP_VH_INS, OP_VH_DEL, OP_QMSG_DEL
+  OP_BIND_DEL_Q, OP_X_DEL, OP_VH_INS, OP_VH_DEL, OP_QMSG_DEL, OP_QDMETA_INS, OP_QDMSG_INS, OP_QDUNACK_INS
 };
 
 // CRC-32C (Castagnoli, init/xorout 0xFFFFFFFF) on the SSE4.2 crc32 instruction: the
@@ -71,9 +74,102 @@ std::map<std::string, std::string> r_map(Reader& r) {
   for (u32 i = 0; i < n; ++i) { std::string k = r.longstr(); m[k] = r.longstr(); }
   return m;
 }
+
+// one framed WAL record: u32 len | op | payload | CRC-32C(op | payload)
+void add_rec(std::string& buf, uint8_t op, const std::string& payload) {
+  const u32 len = (u32)payload.size() + 1;
+  const size_t at = buf.size();
+  buf.resize(at + 4 + len + 4);
+  char* r = &buf[at];
+  for (int i = 0; i < 4; ++i) r[i] = (char)(len >> (24 - 8 * i));
+  r[4] = (char)op;
+  memcpy(r + 5, payload.data(), payload.size());
+  const u32 c = crc32(r + 4, len);
+  for (int i = 0; i < 4; ++i) r[4 + len + i] = (char)(c >> (24 - 8 * i));
+}
+
+// record payloads (the encoders of the operations; compaction re-emits rows with them)
+std::string enc_msg(const MsgRow& m, int64_t ttl_ms, int64_t now) {
+  Writer w;
+  w.b.reserve(64 + m.header.size() + m.body.size() + m.exchange.size() + m.routing.size());
+  w.llng((u64)m.id); w.llng((u64)m.tstamp); w.longstr(m.header); w.longstr(m.body); w.longstr(m.exchange);
+  w.longstr(m.routing); w.octet(m.durable); w.lng((u32)m.refer);
+  // Cassandra TTL is whole seconds (CassandraOpService.scala:157-159); keep ms precision internally
+  w.llng((u64)ttl_ms); w.llng((u64)now);
+  return std::move(w.done());
+}
+std::string enc_qmeta(const std::string& q, int64_t lconsumed, const std::set<std::string>& consumers, bool durable,
+                      int64_t ttl) {
+  Writer w;
+  w.longstr(q); w.llng((u64)lconsumed); w.lng((u32)consumers.size());
+  for (auto& c : consumers) w.longstr(c);
+  w.octet(durable); w.llng((u64)ttl);
+  return std::move(w.done());
+}
+std::string enc_qmsg(const std::string& q, int64_t offset, int64_t msgid, int32_t size, int64_t ttl_ms, int64_t now) {
+  Writer w;
+  w.longstr(q); w.llng((u64)offset); w.llng((u64)msgid); w.lng((u32)size); w.llng((u64)ttl_ms); w.llng((u64)now);
+  return std::move(w.done());
+}
+std::string enc_qrow(const std::string& q, int64_t offset, int64_t msgid, int32_t size) {
+  Writer w;
+  w.longstr(q); w.llng((u64)offset); w.llng((u64)msgid); w.lng((u32)size);
+  return std::move(w.done());
+}
+std::string enc_x(const std::string& id, const ExchangeRow& x) {
+  Writer w;
+  w.longstr(id); w.longstr(x.tpe); w.octet(x.durable); w.octet(x.autodel); w.octet(x.internal); w_map(w, x.args);
+  return std::move(w.done());
+}
+std::string enc_bind(const std::string& id, const std::string& queue, const std::string& key,
+                     const std::map<std::string, std::string>& args) {
+  Writer w;
+  w.longstr(id); w.longstr(queue); w.longstr(key); w_map(w, args);
+  return std::move(w.done());
+}
+std::string enc_vh(const std::string& id, bool active) {
+  Writer w;
+  w.longstr(id); w.octet(active);
+  return std::move(w.done());
+}
+std::string enc_qdmeta(const std::string& q, const QueueMetaDeletedRow& d) {
+  Writer w;
+  w.longstr(q); w.llng((u64)d.lconsumed); w.lng((u32)d.nconsumer); w.octet(d.durable);
+  return std::move(w.done());
+}
+uint64_t msg_size(const MsgRow& m) { return 64 + m.header.size() + m.body.size() + m.exchange.size() + m.routing.size(); }
+int64_t ttl_left(int64_t expire_at, int64_t now) { return expire_at ? std::max<int64_t>(1, expire_at - now) : 0; }
+
+void write_fd(int fd, const char* p, size_t n) {
+  while (n) {
+    ssize_t k = ::write(fd, p, n);
+    if (k < 0) { if (errno == EINTR) continue; throw std::runtime_error("store: WAL write failed"); }
+    p += k;
+    n -= (size_t)k;
+  }
+}
+// bytes [from, to) of the WAL file `src` appended to `dst`
+void copy_range(int src, int dst, uint64_t from, uint64_t to) {
+  std::string buf(1 << 20, '\0');
+  while (from < to) {
+    size_t want = (size_t)std::min<uint64_t>(buf.size(), to - from);
+    ssize_t k = ::pread(src, &buf[0], want, (off_t)from);
+    if (k < 0 && errno == EINTR) continue;
+    if (k <= 0) throw std::runtime_error("store: WAL read failed during compaction");
+    write_fd(dst, buf.data(), (size_t)k);
+    from += (uint64_t)k;
+  }
+}
+double mono_s() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
 }  // namespace
 
 Store::~Store() { close(); }
+
+void Store::wait_compaction() {
+  if (compact_th_.joinable() && compact_th_.get_id() != std::this_thread::get_id()) compact_th_.join();
+}
 
 int64_t Store::now_ms() const {
   return std::chrono::duration_cast<std::chrono::milliseconds>(
@@ -92,6 +188,9 @@ void Store::open(const std::string& dir, bool fsync_enabled) {
 }
 
 void Store::close() {
+  compact_stop_ = true;
+  wait_compaction();
+  compact_stop_ = false;
   std::lock_guard<std::recursive_mutex> g(mu_);
   if (fd_ >= 0) {
     sync();
@@ -101,14 +200,7 @@ void Store::close() {
 }
 
 void Store::write_all(const std::string& rec) {
-  const char* p = rec.data();
-  size_t n = rec.size();
-  while (n) {
-    ssize_t k = ::write(fd_, p, n);
-    if (k < 0) throw std::runtime_error("store: WAL write failed");
-    p += k;
-    n -= (size_t)k;
-  }
+  write_fd(fd_, rec.data(), rec.size());
   wal_bytes_ += rec.size();
 }
 
@@ -121,15 +213,7 @@ void Store::append(uint8_t op, const std::string& payload) {
 
 void Store::append_wal(uint8_t op, const std::string& payload) {
   if (fd_ < 0 || replaying_) return;
-  const u32 len = (u32)payload.size() + 1;
-  const size_t at = wbuf_.size();
-  wbuf_.resize(at + 4 + len + 4);
-  char* r = &wbuf_[at];
-  for (int i = 0; i < 4; ++i) r[i] = (char)(len >> (24 - 8 * i));
-  r[4] = (char)op;
-  memcpy(r + 5, payload.data(), payload.size());
-  const u32 c = crc32(r + 4, len);
-  for (int i = 0; i < 4; ++i) r[4 + len + i] = (char)(c >> (24 - 8 * i));
+  add_rec(wbuf_, op, payload);
   dirty_ = true;
   if (wbuf_.size() > (16u << 20)) flush_wal();
 }
@@ -146,6 +230,29 @@ void Store::sync() {
     if (fsync_) ::fdatasync(fd_);
     dirty_ = false;
   }
+  maybe_compact();
+}
+
+uint64_t Store::liveEstimate() {
+  std::lock_guard<std::recursive_mutex> g(mu_);
+  uint64_t rows = 0;
+  for (auto& kv : queues_) rows += kv.second.size();
+  for (auto& kv : queue_unacks_) rows += kv.second.size();
+  for (auto& kv : binds_) rows += kv.second.size();
+  return msg_bytes_ + 96 * rows + 256 * (queue_metas_.size() + exchanges_.size() + vhosts_.size());
+}
+
+CompactStats Store::compactStats() {
+  std::lock_guard<std::recursive_mutex> g(mu_);
+  return cstats_;
+}
+
+void Store::maybe_compact() {
+  if (auto_ratio_ <= 0 || fd_ < 0 || compacting_ || compact_stop_ || wal_bytes_ < auto_min_) return;
+  if ((double)wal_bytes_ < auto_ratio_ * (double)liveEstimate()) return;
+  if (compact_th_.joinable()) compact_th_.join();   // the previous run has finished
+  compacting_ = true;
+  compact_th_ = std::thread([this] { compact_run(); });
 }
 
 void Store::replay() {
@@ -183,43 +290,155 @@ void Store::replay() {
 }
 
 void Store::compact() {
-  std::lock_guard<std::recursive_mutex> g(mu_);
-  if (fd_ < 0) return;
-  std::string tmp = path_ + ".tmp";
-  int nfd = ::open(tmp.c_str(), O_RDWR | O_CREAT | O_TRUNC, 0644);
-  if (nfd < 0) throw std::runtime_error("store: compact open failed");
-  flush_wal();
-  int old = fd_;
-  fd_ = nfd;
-  wal_bytes_ = 0;
-  write_all(std::string(WAL_MAGIC, sizeof WAL_MAGIC));
-  // re-emit live rows (replaying_ stays false so records are written, apply is idempotent)
-  auto vh = vhosts_;
-  auto xs = exchanges_;
-  auto bs = binds_;
-  auto qm = queue_metas_;
-  auto qs = queues_;
-  auto qu = queue_unacks_;
-  auto ms = msgs_;
-  for (auto& kv : vh) insertVhost(kv.first, kv.second);
-  for (auto& kv : xs) insertExchange(kv.first, kv.second);
-  for (auto& kv : bs)
-    for (auto& b : kv.second) insertBind(kv.first, b.second.queue, b.second.key, b.second.args);
-  for (auto& kv : qm) insertQueueMeta(kv.first, kv.second.lconsumed, kv.second.consumers, kv.second.durable, kv.second.ttl);
-  int64_t now = now_ms();
-  for (auto& kv : qs)
-    for (auto& r : kv.second)
-      insertQueueMsg(kv.first, r.second.offset, r.second.msgid, r.second.size,
-                     r.second.expire_at ? std::max<int64_t>(1, r.second.expire_at - now) : 0);
-  for (auto& kv : qu)
-    for (auto& r : kv.second) insertQueueUnack(kv.first, r.second.offset, r.second.msgid, r.second.size);
-  for (auto& kv : ms)
-    insertMessage(kv.second, kv.second.expire_at ? std::max<int64_t>(1, kv.second.expire_at - now) : 0);
-  flush_wal();
-  if (fsync_) ::fdatasync(fd_);
-  ::rename(tmp.c_str(), path_.c_str());
-  ::close(old);
-  dirty_ = false;
+  wait_compaction();
+  {
+    std::lock_guard<std::recursive_mutex> g(mu_);
+    if (fd_ < 0) return;
+    compacting_ = true;
+  }
+  compact_run();
+}
+
+// live rows of table `t` after the continuation point (key, sub) as WAL records; false
+// when the table is done.  Chunks bound the time mu_ is held.
+bool Store::snapshot_chunk(int t, std::string& key, int64_t& sub, std::string& out) {
+  const int64_t now = now_ms();
+  const size_t budget = 8u << 20;
+  const size_t start = out.size();
+  switch (t) {
+    case 0: for (auto& kv : vhosts_) add_rec(out, OP_VH_INS, enc_vh(kv.first, kv.second)); return false;
+    case 1: for (auto& kv : exchanges_) add_rec(out, OP_X_INS, enc_x(kv.first, kv.second)); return false;
+    case 2:
+      for (auto& kv : binds_)
+        for (auto& b : kv.second) add_rec(out, OP_BIND_INS, enc_bind(kv.first, b.second.queue, b.second.key, b.second.args));
+      return false;
+    case 3:
+      for (auto& kv : queue_metas_)
+        add_rec(out, OP_QMETA_INS, enc_qmeta(kv.first, kv.second.lconsumed, kv.second.consumers, kv.second.durable,
+                                             kv.second.ttl));
+      return false;
+    case 4:
+    case 5: {   // queue rows (by offset) / unacks (by msg id), continued at (queue, last key)
+      auto& tab = t == 4 ? queues_ : queue_unacks_;
+      for (auto qi = tab.lower_bound(key); qi != tab.end(); ++qi) {
+        if (qi->first != key) sub = LLONG_MIN;
+        key = qi->first;
+        for (auto it = qi->second.upper_bound(sub); it != qi->second.end(); ++it) {
+          const QueueMsgRow& r = it->second;
+          if (t == 4) {
+            if (!r.expire_at || r.expire_at > now)
+              add_rec(out, OP_QMSG_INS, enc_qmsg(key, r.offset, r.msgid, r.size, ttl_left(r.expire_at, now), now));
+          } else {
+            add_rec(out, OP_QUNACK_INS, enc_qrow(key, r.offset, r.msgid, r.size));
+          }
+          sub = it->first;
+          if (out.size() - start > budget) return true;
+        }
+      }
+      return false;
+    }
+    case 6: {   // messages, continued at the last id
+      for (auto it = msgs_.upper_bound(sub); it != msgs_.end(); ++it) {
+        if (!it->second.expire_at || it->second.expire_at > now)
+          add_rec(out, OP_MSG_INS, enc_msg(it->second, ttl_left(it->second.expire_at, now), now));
+        sub = it->first;
+        if (out.size() - start > budget) return true;
+      }
+      return false;
+    }
+    case 7:
+      for (auto& kv : queue_metas_deleted_) add_rec(out, OP_QDMETA_INS, enc_qdmeta(kv.first, kv.second));
+      for (auto& kv : queues_deleted_)
+        for (auto& r : kv.second) add_rec(out, OP_QDMSG_INS, enc_qrow(kv.first, r.second.offset, r.second.msgid, r.second.size));
+      for (auto& kv : queue_unacks_deleted_)
+        for (auto& r : kv.second)
+          add_rec(out, OP_QDUNACK_INS, enc_qrow(kv.first, r.second.offset, r.second.msgid, r.second.size));
+      return false;
+    default: return false;
+  }
+}
+
+void Store::compact_run() {
+  const double t0 = mono_s();
+  double max_lock = 0;
+  std::string tmp;
+  int nfd = -1;
+  uint64_t switch_off = 0, before = 0;
+  try {
+    {
+      std::lock_guard<std::recursive_mutex> g(mu_);
+      if (fd_ < 0) { compacting_ = false; return; }
+      flush_wal();
+      switch_off = before = wal_bytes_;
+      tmp = path_ + ".compact";
+      nfd = ::open(tmp.c_str(), O_RDWR | O_CREAT | O_TRUNC | O_APPEND, 0644);
+      if (nfd < 0) throw std::runtime_error("store: compact open failed");
+    }
+    // ---- snapshot of the live rows (short locked chunks; appends continue meanwhile)
+    std::string out(WAL_MAGIC, sizeof WAL_MAGIC);
+    uint64_t written = 0;
+    for (int t = 0; t <= 7; ++t) {
+      std::string key;
+      int64_t sub = LLONG_MIN;
+      bool more = true;
+      while (more) {
+        {
+          std::lock_guard<std::recursive_mutex> g(mu_);
+          const double l0 = mono_s();
+          more = snapshot_chunk(t, key, sub, out);
+          max_lock = std::max(max_lock, mono_s() - l0);
+        }
+        if (out.size() > (4u << 20)) { write_fd(nfd, out.data(), out.size()); written += out.size(); out.clear(); }
+        if (compact_stop_) throw std::runtime_error("store closing");
+      }
+    }
+    write_fd(nfd, out.data(), out.size());
+    written += out.size();
+    out.clear();
+    // ---- the old WAL's records since the switch point, then swap files under the lock
+    uint64_t copied = switch_off;
+    while (true) {
+      uint64_t cur;
+      int oldfd;
+      {
+        std::lock_guard<std::recursive_mutex> g(mu_);
+        const double l0 = mono_s();
+        flush_wal();
+        cur = wal_bytes_;
+        oldfd = fd_;
+        if (cur - copied <= (4u << 20) || compact_stop_) {
+          copy_range(fd_, nfd, copied, cur);
+          if (fsync_) ::fdatasync(nfd);
+          if (::rename(tmp.c_str(), path_.c_str()) != 0) throw std::runtime_error("store: compact rename failed");
+          if (fsync_) {   // the rename itself is durable
+            std::string dir = path_;
+            int dfd = ::open(dirname(&dir[0]), O_RDONLY | O_DIRECTORY);
+            if (dfd >= 0) { ::fsync(dfd); ::close(dfd); }
+          }
+          ::close(fd_);
+          fd_ = nfd;
+          nfd = -1;
+          wal_bytes_ = written + (cur - switch_off);
+          dirty_ = false;
+          cstats_.runs++;
+          cstats_.last_before = before + (cur - switch_off);
+          cstats_.last_after = wal_bytes_;
+          cstats_.tail_bytes = cur - switch_off;
+          max_lock = std::max(max_lock, mono_s() - l0);
+          cstats_.max_lock_s = std::max(cstats_.max_lock_s, max_lock);
+          cstats_.last_s = mono_s() - t0;
+          compacting_ = false;
+          return;
+        }
+      }
+      copy_range(oldfd, nfd, copied, cur);   // bytes already in the file: no lock needed
+      copied = cur;
+    }
+  } catch (std::exception&) {
+    if (nfd >= 0) { ::close(nfd); ::unlink(tmp.c_str()); }
+    compacting_ = false;
+    if (!compact_stop_) throw;
+  }
 }
 
 // ------------------------------------------------------------------ apply (row semantics)
@@ -234,12 +453,19 @@ void Store::apply(uint8_t op, const std::string& pl) {
       int64_t ttl = (int64_t)r.llng();
       int64_t at = (int64_t)r.llng();
       m.expire_at = ttl > 0 ? at + ttl : 0;
-      msgs_[m.id] = m;
+      auto it = msgs_.find(m.id);
+      if (it != msgs_.end()) msg_bytes_ -= msg_size(it->second);
+      msg_bytes_ += msg_size(m);
+      msgs_[m.id] = std::move(m);
       break;
     }
     case OP_MSG_REFER: { int64_t id = (int64_t)r.llng(); int32_t ref = (int32_t)r.lng();
       auto it = msgs_.find(id); if (it != msgs_.end()) it->second.refer = ref; break; }
-    case OP_MSG_DEL: msgs_.erase((int64_t)r.llng()); break;
+    case OP_MSG_DEL: {
+      auto it = msgs_.find((int64_t)r.llng());
+      if (it != msgs_.end()) { msg_bytes_ -= msg_size(it->second); msgs_.erase(it); }
+      break;
+    }
     case OP_QMETA_INS: {
       std::string q = r.longstr();
       QueueMetaRow m;
@@ -338,6 +564,22 @@ void Store::apply(uint8_t op, const std::string& pl) {
       break;
     }
     case OP_X_DEL: { std::string id = r.longstr(); exchanges_.erase(id); binds_.erase(id); break; }
+    case OP_QDMETA_INS: {
+      std::string q = r.longstr();
+      QueueMetaDeletedRow d;
+      d.lconsumed = (int64_t)r.llng(); d.nconsumer = (int32_t)r.lng(); d.durable = r.octet();
+      queue_metas_deleted_[q] = d;
+      break;
+    }
+    case OP_QDMSG_INS:
+    case OP_QDUNACK_INS: {
+      std::string q = r.longstr();
+      QueueMsgRow u;
+      u.offset = (int64_t)r.llng(); u.msgid = (int64_t)r.llng(); u.size = (int32_t)r.lng();
+      if (op == OP_QDMSG_INS) queues_deleted_[q][u.offset] = u;
+      else queue_unacks_deleted_[q][u.msgid] = u;
+      break;
+    }
     case OP_VH_INS: { std::string id = r.longstr(); vhosts_[id] = r.octet(); break; }
     case OP_VH_DEL: vhosts_.erase(r.longstr()); break;
     default: break;
@@ -350,26 +592,19 @@ void Store::apply(uint8_t op, const std::string& pl) {
 
 void Store::insertMessage(const MsgRow& m, int64_t ttl_ms) {
   LOCK;
-  Writer w;
-  w.llng((u64)m.id); w.llng((u64)m.tstamp); w.longstr(m.header); w.longstr(m.body); w.longstr(m.exchange);
-  w.longstr(m.routing); w.octet(m.durable); w.lng((u32)m.refer);
-  // Cassandra TTL is whole seconds (CassandraOpService.scala:157-159); keep ms precision internally
-  w.llng((u64)ttl_ms); w.llng((u64)now_ms());
-  append(OP_MSG_INS, w.done());
+  append(OP_MSG_INS, enc_msg(m, ttl_ms, now_ms()));
 }
 // hot path of the GPU write-behind (persist.cpp): the row moves into the table instead of
 // being re-decoded from its WAL record
 void Store::insertMessage(MsgRow&& m, int64_t ttl_ms) {
   LOCK;
-  Writer w;
-  w.b.reserve(64 + m.header.size() + m.body.size() + m.exchange.size() + m.routing.size());
   const int64_t now = now_ms();
-  w.llng((u64)m.id); w.llng((u64)m.tstamp); w.longstr(m.header); w.longstr(m.body); w.longstr(m.exchange);
-  w.longstr(m.routing); w.octet(m.durable); w.lng((u32)m.refer);
-  w.llng((u64)ttl_ms); w.llng((u64)now);
-  append_wal(OP_MSG_INS, w.done());
+  append_wal(OP_MSG_INS, enc_msg(m, ttl_ms, now));
   m.expire_at = ttl_ms > 0 ? now + ttl_ms : 0;
   const int64_t id = m.id;
+  auto it = msgs_.find(id);
+  if (it != msgs_.end()) msg_bytes_ -= msg_size(it->second);
+  msg_bytes_ += msg_size(m);
   msgs_[id] = std::move(m);
 }
 
@@ -477,9 +712,7 @@ void Store::deleteBindsOfQueue(const std::string& queue) {
   LOCK; Writer w; w.longstr(queue); append(OP_BIND_DEL_Q, w.done());
 }
 void Store::deleteExchange(const std::string& id) { LOCK; Writer w; w.longstr(id); append(OP_X_DEL, w.done()); }
-void Store::insertVhost(const std::string& id, bool active) {
-  LOCK; Writer w; w.longstr(id); w.octet(active); append(OP_VH_INS, w.done());
-}
+void Store::insertVhost(const std::string& id, bool active) { LOCK; append(OP_VH_INS, enc_vh(id, active)); }
 bool Store::selectVhost(const std::string& id, bool* active) {
   LOCK;
   auto it = vhosts_.find(id);
@@ -488,6 +721,44 @@ bool Store::selectVhost(const std::string& id, bool* active) {
   return true;
 }
 void Store::deleteVhost(const std::string& id) { LOCK; Writer w; w.longstr(id); append(OP_VH_DEL, w.done()); }
+
+std::vector<std::string> Store::deletedQueueIds() {
+  LOCK;
+  std::set<std::string> ids;
+  for (auto& kv : queue_metas_deleted_) ids.insert(kv.first);
+  for (auto& kv : queues_deleted_) if (!kv.second.empty()) ids.insert(kv.first);
+  for (auto& kv : queue_unacks_deleted_) if (!kv.second.empty()) ids.insert(kv.first);
+  return std::vector<std::string>(ids.begin(), ids.end());
+}
+bool Store::selectDeletedQueue(const std::string& q, QueueMetaDeletedRow* meta, std::vector<QueueMsgRow>* msgs,
+                               std::vector<QueueMsgRow>* unacks) {
+  LOCK;
+  auto mi = queue_metas_deleted_.find(q);
+  if (meta) *meta = mi != queue_metas_deleted_.end() ? mi->second : QueueMetaDeletedRow{};
+  if (msgs) {
+    msgs->clear();
+    auto it = queues_deleted_.find(q);
+    if (it != queues_deleted_.end()) for (auto& kv : it->second) msgs->push_back(kv.second);
+  }
+  if (unacks) {
+    unacks->clear();
+    auto it = queue_unacks_deleted_.find(q);
+    if (it != queue_unacks_deleted_.end()) for (auto& kv : it->second) unacks->push_back(kv.second);
+  }
+  return mi != queue_metas_deleted_.end();
+}
+void Store::insertDeletedQueueMeta(const std::string& q, int64_t lconsumed, int32_t nconsumer, bool durable) {
+  LOCK;
+  QueueMetaDeletedRow d;
+  d.lconsumed = lconsumed; d.nconsumer = nconsumer; d.durable = durable;
+  append(OP_QDMETA_INS, enc_qdmeta(q, d));
+}
+void Store::insertDeletedQueueMsg(const std::string& q, int64_t offset, int64_t msgid, int32_t size) {
+  LOCK; append(OP_QDMSG_INS, enc_qrow(q, offset, msgid, size));
+}
+void Store::insertDeletedQueueUnack(const std::string& q, int64_t offset, int64_t msgid, int32_t size) {
+  LOCK; append(OP_QDUNACK_INS, enc_qrow(q, offset, msgid, size));
+}
 
 std::vector<std::string> Store::vhostIds() {
   LOCK; std::vector<std::string> v; for (auto& kv : vhosts_) v.push_back(kv.first); return v;

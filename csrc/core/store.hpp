@@ -6,14 +6,25 @@
 // clustering order ASC on queues.offset, and per-row TTL (USING TTL seconds).
 // Durability: every mutation is appended to a CRC-checked write-ahead log; sync() is a
 // group-commit fsync the broker calls before it sends publisher confirms for persistent
-// messages (SURVEY §3.3 "confirm only after the durable write").  open() replays the log;
-// compact() rewrites it from the live tables.
+// messages (SURVEY §3.3 "confirm only after the durable write").  open() replays the log.
+//
+// Reclamation (the reference's Cassandra drops deleted rows itself,
+// CassandraOpService.scala:395-417): the WAL is compacted in the background once it is
+// auto_ratio x the live rows (and >= auto_min bytes).  A compaction snapshots the live
+// rows into a new file in short locked chunks while appends continue into the old WAL,
+// then copies the old WAL's tail written since the switch point (mostly unlocked) and
+// atomically renames the new file over it.  Every record is an upsert / delete / field
+// set by key, so replaying the tail over a snapshot that already saw some of those
+// changes yields the same rows; group commits are never blocked for a whole rewrite.
 #pragma once
+#include <atomic>
+#include <condition_variable>
 #include <cstdint>
 #include <map>
 #include <mutex>
 #include <set>
 #include <string>
+#include <thread>
 #include <tuple>
 #include <vector>
 
@@ -52,6 +63,11 @@ struct ExchangeRow {       // exchanges
 };
 struct BindRow { std::string queue, key; std::map<std::string, std::string> args; };
 
+struct CompactStats {
+  uint64_t runs = 0, last_before = 0, last_after = 0, tail_bytes = 0;
+  double last_s = 0, max_lock_s = 0;
+};
+
 class Store {
  public:
   Store() = default;
@@ -59,8 +75,13 @@ class Store {
   // dir == "" -> memory only (the in-memory fake of SURVEY §4.2 item 5)
   void open(const std::string& dir, bool fsync_enabled = true);
   void close();
-  void sync();             // group commit
-  void compact();          // rewrite the WAL from live rows
+  void sync();             // group commit (may start a background compaction)
+  void compact();          // rewrite the WAL from live rows now (waits for it)
+  // background compaction policy: WAL > ratio x live estimate and > min_bytes (ratio 0 = off)
+  void set_auto_compact(double ratio, uint64_t min_bytes) { auto_ratio_ = ratio; auto_min_ = min_bytes; }
+  void wait_compaction();
+  CompactStats compactStats();
+  uint64_t liveEstimate();
   bool persistent() const { return fd_ >= 0; }
   int64_t now_ms() const;
 
@@ -96,6 +117,13 @@ class Store {
   void insertVhost(const std::string& id, bool active);
   bool selectVhost(const std::string& id, bool* active);
   void deleteVhost(const std::string& id);
+  // ---- *_deleted tables (pendingDeleteQueue copies; Cassandra interop import/export)
+  std::vector<std::string> deletedQueueIds();
+  bool selectDeletedQueue(const std::string& q, QueueMetaDeletedRow* meta, std::vector<QueueMsgRow>* msgs,
+                          std::vector<QueueMsgRow>* unacks);
+  void insertDeletedQueueMeta(const std::string& q, int64_t lconsumed, int32_t nconsumer, bool durable);
+  void insertDeletedQueueMsg(const std::string& q, int64_t offset, int64_t msgid, int32_t size);
+  void insertDeletedQueueUnack(const std::string& q, int64_t offset, int64_t msgid, int32_t size);
 
   // ---- recovery / inspection
   std::vector<std::string> vhostIds();
@@ -112,7 +140,16 @@ class Store {
   void replay();
   void write_all(const std::string& rec);
   void flush_wal();
+  void maybe_compact();               // mu_ held
+  void compact_run();                 // the compaction (background thread or compact())
+  bool snapshot_chunk(int table, std::string& key, int64_t& sub, std::string& out);
   std::string wbuf_;       // WAL records not yet written
+  uint64_t msg_bytes_ = 0;            // live message row bytes (liveEstimate)
+  double auto_ratio_ = 4.0;
+  uint64_t auto_min_ = 256ull << 20;
+  std::thread compact_th_;
+  std::atomic<bool> compacting_{false}, compact_stop_{false};
+  CompactStats cstats_;
 
   std::recursive_mutex mu_;
   int fd_ = -1;

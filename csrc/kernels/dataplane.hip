@@ -323,7 +323,7 @@ __global__ __launch_bounds__(256) void k_stage(DS d) {
     for (u32 k = tid; k < sizeof(Counters) / 4; k += 256)
       if (k * 4 < offsetof(Counters, log_head)) c[k] = 0;
     if (tid == 0) {
-      d.ctr->n_grow = 0; d.tot[TS_NMOVE] = 0; d.tot[TS_NDEFER] = 0;
+      d.ctr->n_grow = 0; d.tot[TS_NMOVE] = 0; d.tot[TS_NDEFER] = 0; d.tot[TS_TTL_BUDGET] = 0;
       *d.egress_budget = 0;
       // snowflake virtual position base for this step (ID_SLOT_BITS slots per wall-clock ms)
       u64 floor_pos = d.in->id_ms << ID_SLOT_BITS;
@@ -2399,7 +2399,17 @@ __global__ __launch_bounds__(256) void k_dequeue(DS d) {
   const Desc* ring = d.ring + d.q_ring_off[q];
   const i64 now = d.in->now_ms;
   if (tid < 64) {   // TTL skip at the head (K12)
+    // durable queues: every skipped persistent entry is a store record (ConsumedRec); a
+    // purge of a deep queue marks its whole backlog expired, so the skip takes at most a
+    // quarter of the step's record buffer (reserved 64 at a time) and the next steps
+    // continue it -- the record buffer never overflows (the store would miss deletions)
+    const bool budget = d.persist && d.q_durable[q];
     while (head < tail) {
+      if (budget) {
+        u32 ok = 1;
+        if (lane == 0) ok = atomicAdd(&d.tot[TS_TTL_BUDGET], 64u) + 64u <= (d.persist_max >> 2);
+        if (!__shfl(ok, 0, 64)) break;
+      }
       u64 idx = head + lane;
       bool valid = idx < tail;
       Desc ds;

@@ -28,7 +28,8 @@ enum : u32 {
   TS_NMOVE = 30,                        // rings moved (grown) this step (k_ring_plan)
   TS_NDEFER = 31,                       // stored messages released at the end of the step
   TS_RP_TICKET = 14,                    // k_ring_plan finished-block ticket (last block: ring moves)
-  TS_XSCAN = 32                         // + 2*r: per-destination record / byte totals
+  TS_XSCAN = 32,                        // + 2*r: per-destination record / byte totals
+  TS_TTL_BUDGET = 64                    // durable TTL-skip records reserved this step (k_dequeue)
 };
 
 struct DS {

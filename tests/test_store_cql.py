@@ -48,3 +48,37 @@ def test_cql_export_and_csv_round_trip(tmp_path):
         assert sorted(map(key, before[t])) == sorted(map(key, after[t])), t
     assert summary(st2)["msgs"] == 5
     st2.close()
+
+
+def test_deleted_tables_ddl_export_and_round_trip(tmp_path):
+    """queues_deleted / queue_metas_deleted / queue_unacks_deleted (create-cassantra.cql:48-74):
+    pendingDeleteQueue copies a queue's rows there; DDL, CQL export and the CSV round trip
+    carry them, and a compaction keeps them."""
+    text = ddl()
+    for t in ("queues_deleted", "queue_metas_deleted", "queue_unacks_deleted"):
+        assert f"CREATE TABLE IF NOT EXISTS {t} (" in text
+    assert "nconsumer int" in text
+    st = open_store(str(tmp_path / "a"), fsync=False)
+    _fill(st)
+    st.pending_delete_queue("AMQ.DEFAULT-_.q")
+    st.sync()
+    assert summary(st)["queue_metas_deleted"] == 1
+    assert summary(st)["queues_deleted"] == 5 and summary(st)["queue_unacks_deleted"] == 1
+    n = export_cql(st, str(tmp_path / "dump.cql"))
+    assert n["queues_deleted"] == 5 and n["queue_metas_deleted"] == 1 and n["queue_unacks_deleted"] == 1
+    assert "INSERT INTO queue_metas_deleted (id, lconsumed, nconsumer, durable) VALUES ('AMQ.DEFAULT-_.q', -1, 2, true);" \
+        in (tmp_path / "dump.cql").read_text()
+    export_csv(st, str(tmp_path / "csv"))
+    before = rows(st)
+    st.compact()
+    assert rows(st) == before
+    st.close()
+    st2 = open_store(str(tmp_path / "b"), fsync=False)
+    import_csv(st2, str(tmp_path / "csv"))
+    after = rows(st2)
+    for t in ("queues_deleted", "queue_metas_deleted", "queue_unacks_deleted"):
+        assert sorted(map(repr, before[t])) == sorted(map(repr, after[t])), t
+    st2.close()
+    st3 = open_store(str(tmp_path / "b"), fsync=False)   # replayed from its WAL
+    assert summary(st3)["queues_deleted"] == 5 and summary(st3)["queue_metas_deleted"] == 1
+    st3.close()
