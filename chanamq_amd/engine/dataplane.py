@@ -88,7 +88,12 @@ class GpuDataPlane(ControlState):
         self._pending = None
         self._xprev = None        # parity of the launched step whose exchange is still due
         self.lag = False
-        if world > 1:
+        self.native_xchg = bool(i.get("native_xchg"))
+        if world > 1 and self.native_xchg:
+            # the engine owns the exchange buffers and moves them itself (RCCL / shared
+            # memory) under the native front end's sharded stepper (frontend.cpp)
+            self.lag = True
+        elif world > 1:
             # exchange operands live in torch's allocator so RCCL can use them directly
             import torch
             dev = torch.device("cuda", device)
@@ -578,6 +583,15 @@ class GpuDataPlane(ControlState):
         t = self.submit_raw(segs, payload_ptr, payload_len, now_ms)
         return self.finish(t, collect=collect)
 
+    def xchg_setup(self, kind, arg, members, timeout_ms=10000, failover=False):
+        """Native exchange backend over the live ranks ``members``: "rccl" (arg = the
+        128-byte unique id from ``xchg_unique_id()``) or "shm" (arg = a shared-memory name
+        common to the group, for ranks sharing one host)."""
+        self.eng.xchg_setup(kind, arg, sorted(int(m) for m in members), int(timeout_ms), bool(failover))
+
+    def xchg_unique_id(self):
+        return self.mod.Engine.xchg_unique_id()
+
     # ---- unbounded queues: the device grows rings (k_ring_plan); the host mirrors it
     def _ring_alloc(self, cap):
         """Rings come from one pool whose bump pointer lives on the device (k_ring_plan
@@ -617,6 +631,17 @@ class GpuDataPlane(ControlState):
             staged = int(self.carry[segs["conn"]].sum()) + 48 * len(segs)
             if staged > self.info["carry_budget"]:
                 raise RuntimeError(f"step carries {staged} B > carry_budget {self.info['carry_budget']} B")
+        if self.world > 1 and self.native_xchg:
+            # a step run by the control plane at a synchronisation point (no exchange
+            # pending on any rank): phase A, no exchange (it carries no client bytes that
+            # could route to another rank), phase B
+            if len(segs):
+                raise RuntimeError("host-run steps of a sharded node carry no client bytes")
+            p = self.eng.submit(segs, int(payload_ptr), int(payload_len), now, self.step_no, now, self.worker)
+            self.step_no += 1
+            self.eng.drop_exchange(p)
+            self.eng.launch_b(p)
+            return (p, len(segs), t0)
         if self.world > 1 and self.lag and self.exchanger is not None:
             # one process per rank, pipelined exchange: queue H2D(t), then run step t-1's
             # all-to-all while those bytes cross PCIe, then launch step t (whose phase B

@@ -17,7 +17,7 @@ _ROOT = os.path.dirname(os.path.dirname(_HERE))
 _SRC = os.path.join(_ROOT, "csrc", "kernels")
 _EXT = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
 EXT_PATH = os.path.join(_HERE, "_dataplane" + _EXT)
-SOURCES = ["engine.hip", "dataplane.hip", "dp_state.h", "dp_common.h", "step_abi.h"]
+SOURCES = ["engine.hip", "dataplane.hip", "dp_state.h", "dp_common.h", "step_abi.h", "xchg_host.h", "xchg_rccl.h"]
 
 
 def _src_hash():
@@ -46,7 +46,7 @@ def build(force=False, verbose=False):
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
     inc = [f"-I{pybind11.get_include()}", f"-I{sysconfig.get_paths()['include']}", f"-I{_SRC}"]
     cmd = [hipcc, "--offload-arch=gfx950", "-O3", "-std=c++17", "-shared", "-fPIC", *inc,
-           os.path.join(_SRC, "engine.hip"), "-o", EXT_PATH + ".tmp", "-L/opt/rocm/lib", "-lhsa-runtime64", "-lrocprofiler-sdk-roctx"]
+           os.path.join(_SRC, "engine.hip"), "-o", EXT_PATH + ".tmp", "-L/opt/rocm/lib", "-lhsa-runtime64", "-lrocprofiler-sdk-roctx", "-ldl", "-lrt"]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)

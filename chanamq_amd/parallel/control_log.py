@@ -23,6 +23,7 @@ class ControlLog:
         self.applied = 0
         self.results = {}     # local seq -> result or ControlError tuple
         self.handlers = {}    # op -> callable for ops served above the plane (parallel/links.py)
+        self.on_applied = None   # (op, args, kw, result) after each applied op (store rows)
 
     def submit(self, op, *args, **kw):
         if op not in REPLICATED:
@@ -42,6 +43,8 @@ class ControlLog:
                     res = self._apply(op, args, kw)
                 except ControlError as e:
                     res = ("error", e.code, e.text, e.class_id, e.method_id)
+                if self.on_applied is not None:
+                    self.on_applied(op, args, kw, res)
                 self.applied += 1
                 if r == self.comm.rank:
                     mine[seq] = res

@@ -2,10 +2,13 @@
 failure detector, SURVEY C41, and of the cluster singleton's leader choice, C44).
 
 Every rank bumps a heartbeat counter ``hb/<rank>`` in the c10d store from a background
-thread; ``suspects()`` reports ranks whose counter has not moved for ``timeout_s``.  A
-rank is declared dead only when every survivor agrees (``agree_dead``: each survivor
-publishes its suspicion set and the intersection is taken), so all survivors re-home the
-same queues.  The leader (singleton duties: admin REST, store compaction) is the lowest
+thread -- only while ``health()`` holds: a pipelined sharded rank gates it on its stepper
+(``Frontend.healthy``: no failed engine, no GPU wait stuck past a deadline), so a wedged
+GPU or a dead engine stops the beat even though the process lives.  ``suspects()``
+reports ranks whose counter has not moved for ``timeout_s``.  ``agree_dead`` makes the
+survivors converge: each publishes its suspicion set and the dead set is the union of
+what the survivors report (a rank one survivor cannot reach would break every
+collective), so all survivors re-home the same queues.  The leader (singleton duties: admin REST, store compaction) is the lowest
 live rank.  The store must outlive any rank (launcher-hosted, parallel/launch.py).
 """
 
@@ -14,9 +17,10 @@ import time
 
 
 class Membership:
-    def __init__(self, store, rank, world, interval_s=0.2, timeout_s=2.0):
+    def __init__(self, store, rank, world, interval_s=0.2, timeout_s=2.0, health=None):
         self.store, self.rank, self.world = store, rank, world
         self.interval_s, self.timeout_s = interval_s, timeout_s
+        self.health = health     # () -> bool: beat only while this rank makes progress
         self.live = set(range(world))
         self._seen = {r: (-1, time.monotonic()) for r in range(world)}
         self._stop = threading.Event()
@@ -26,7 +30,8 @@ class Membership:
     def _beat(self):
         while not self._stop.is_set():
             try:
-                self.store.add(f"hb/{self.rank}", 1)
+                if self.health is None or self.health():
+                    self.store.add(f"hb/{self.rank}", 1)
             except Exception:   # store gone: the node is shutting down
                 return
             self._stop.wait(self.interval_s)

@@ -39,6 +39,8 @@ class ShardedNode:
         self.members = membership or Membership(self.comm.store, self.comm.rank, self.comm.world,
                                                 timeout_s=hb_timeout_s)
         self.failovers = []
+        self.fe = None              # native front end (pipelined sharded server)
+        self.rebuild_xchg = None    # (live ranks, epoch) -> rebuild the engine's exchange
         # remote consumers (X2/X3): link ops ride the control log, link traffic one
         # all-to-all after each data step while links exist
         self.links = RemoteLinks(plane)
@@ -51,7 +53,30 @@ class ShardedNode:
         return self.comm.rank
 
     def submit(self, op, *args, **kw):
-        return self.log.submit(op, *args, **kw)
+        seq = self.log.submit(op, *args, **kw)
+        if self.fe is not None:   # every rank syncs at the next step (frontend.cpp XF_SYNC)
+            self.fe.request_sync()
+        return seq
+
+    # ------------------------------------------------------------------ pipelined server
+    def attach_frontend(self, fe, stuck_s=5.0):
+        """The native front end steps this rank (frontend.cpp stepper_sharded): control
+        ops sync at its FE_SYNC points, failovers run at FE_XFAIL, and this rank's
+        heartbeat only beats while the stepper makes progress (a wedged GPU or a failed
+        engine stops it, so the peers fail this rank over instead of hanging on it)."""
+        self.fe = fe
+        self.members.health = lambda: fe.healthy(stuck_s)
+
+    def sync_point(self):
+        """All ranks parked at the same step: the control log all-gather (on the host
+        control group) applied everywhere -> {seq: result} of this rank's ops."""
+        return self._retry(self.log.sync, 3)
+
+    def failover_point(self):
+        """An exchange peer stopped answering: agree on the dead ranks, rebuild the
+        communicators (control group and the engine's exchange) over the survivors,
+        re-home the dead ranks' queues and reload their durable messages."""
+        return self.handle_failure()
 
     def step(self, inputs=None, now_ms=0, retries=3):
         """One lockstep step -> (plane step result, {seq: result} of this rank's ops)."""
@@ -126,6 +151,8 @@ class ShardedNode:
             raise RuntimeError("collective failed but no peer is suspected")
         dead = self.members.agree_dead(suspects, epoch=self.comm.epoch + 1)
         self.comm.rebuild(self.members.live)
+        if self.rebuild_xchg is not None:
+            self.rebuild_xchg(sorted(self.members.live), self.comm.epoch)
         for r in dead:
             self.plane.shard_map.fail(r)
         self.links.on_failure(dead)

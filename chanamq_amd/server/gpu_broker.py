@@ -60,7 +60,8 @@ class _Conn:
         self.cap_blocked = False
 
 
-FE_OPEN, FE_CLOSED, FE_HOST, FE_CTRL, FE_TXBUF, FE_EVENT, FE_STATUS, FE_PERSIST, FE_ERROR, FE_GROW = range(1, 11)
+FE_OPEN, FE_CLOSED, FE_HOST, FE_CTRL, FE_TXBUF, FE_EVENT, FE_STATUS, FE_PERSIST, FE_ERROR, FE_GROW, FE_SYNC, \
+    FE_XFAIL = range(1, 13)
 
 
 class _PlaneLock:
@@ -118,10 +119,11 @@ class GpuBroker:
         gateway.cpp), "python" = selectors loop (portable fallback); "auto" = pipeline
         for a single-rank GPU plane, else native."""
         self.plane = plane
+        native_x = bool(getattr(plane, "native_xchg", False))
         if io == "auto":
-            io = "pipeline" if (hasattr(plane, "eng") and node is None) else "native"
-        if io == "pipeline" and (not hasattr(plane, "eng") or node is not None):
-            raise ValueError("io='pipeline' needs a single-rank GPU data plane")
+            io = "pipeline" if (hasattr(plane, "eng") and (node is None or native_x)) else "native"
+        if io == "pipeline" and (not hasattr(plane, "eng") or (node is not None and not native_x)):
+            raise ValueError("io='pipeline' needs a GPU data plane (sharded: built with native_xchg=1)")
         self.io = io
         self.io_threads = io_threads
         self.fe_cfg = dict(fe_cfg or {})    # extra native front-end settings (frontend.hpp FrontendCfg)
@@ -209,6 +211,13 @@ class GpuBroker:
                 self._pw = load().PersistWorker(self.persistence.store)
                 self.fe.attach_persist(self._pw)
                 self.persistence.attach_native(self._pw)
+            if self.node is not None:
+                # sharded: lockstep steps with the native exchange; control-log syncs and
+                # failovers happen at FE_SYNC / FE_XFAIL; the failure detector's heartbeat
+                # is gated on this rank's step progress
+                self.node.attach_frontend(self.fe)
+                if self.persistence is not None:
+                    self.node.log.on_applied = self._persist_replicated
             self._running = True
             self.fe.start()
             self._thread = threading.Thread(target=self._loop_pipeline, name="gpu-broker-ctl", daemon=True)
@@ -326,7 +335,11 @@ class GpuBroker:
 
     def _handle_fe(self, evs):
         ctrl, events, seg_status, txbuf = [], [], [], []
+        sync = None
         for kind, conn, a, b, data, data2 in evs:
+            if kind in (FE_SYNC, FE_XFAIL):
+                sync = kind if sync is None else max(sync, kind)
+                continue
             if kind == FE_OPEN:
                 self.conns[conn] = _Conn(None, conn, None)
                 self.stats["connections"] += 1
@@ -367,6 +380,47 @@ class GpuBroker:
         if ctrl or events or seg_status or txbuf:
             txbuf.sort()
             self._after_step(ctrl, events, seg_status, {}, False, False, txbuf)
+        if sync is not None:
+            self._sync_point(sync == FE_XFAIL)
+
+    def _sync_point(self, failed):
+        """Every rank's stepper parked at the same step (no exchange in flight): fail over
+        if a peer stopped answering, then apply the replicated control log everywhere and
+        answer this rank's deferred control commands; the steps resume afterwards."""
+        node = self.node
+        try:
+            if failed:
+                node.failover_point()
+            self._answer(node.sync_point())
+            if self.persistence is not None:
+                self.persistence.control_commit()
+        finally:
+            self.fe.sync_done()
+
+    def _persist_replicated(self, op, args, kw, res):
+        """Durable topology applied from the control log goes into this rank's store too
+        (every rank holds the replicated exchanges / queues / bindings; a survivor adopting
+        a dead rank's queues finds their rows)."""
+        from ..parallel.control_log import error_of
+        if error_of(res) or self.persistence is None:
+            return
+        p, ps = self.plane, self.persistence
+        if op == "declare_exchange":
+            x = p.exchanges.get((args[0], args[1]))
+            if x is not None:
+                ps.exchange(x)
+        elif op == "delete_exchange":
+            ps.exchange_deleted(args[0], args[1])
+        elif op == "declare_queue":
+            q = p.queues.get((args[0], args[1]))
+            if q is not None:
+                ps.queue(q)
+        elif op == "delete_queue":
+            ps.queue_deleted(args[0], args[1])
+        elif op == "bind":
+            ps.bind(*args[:4])
+        elif op == "unbind":
+            ps.unbind(*args[:4])
 
     def _persist_native(self, evs):
         """Write-behind group commit: the store rows of every held step in this batch,

@@ -3,11 +3,18 @@
 
     python -m chanamq_amd.parallel.launch 8 -- -m chanamq_amd.server.sharded --port 5672
 
-Each rank owns one MI355X (``--plane gpu``, RCCL between ranks) or a golden CPU plane
-(``--plane golden``, gloo; tests).  With ``--reuseport`` all ranks listen on the same port
-and the kernel spreads connections over them; otherwise rank r listens on port + r.
-Queues are placed on the rank where they are declared; publishes reach them from any
-rank through the per-step all-to-all.
+Each rank owns one MI355X (``--plane gpu``) or a golden CPU plane (``--plane golden``,
+gloo; tests).  With ``--reuseport`` all ranks listen on the same port and the kernel
+spreads connections over them; otherwise rank r listens on port + r.  Queues are placed
+on the rank where they are declared; publishes reach them from any rank through the
+per-step exchange, consumers on any rank reach any queue through device links.
+
+``--io pipeline`` (GPU default): the native front end (csrc/core/frontend.cpp) steps the
+rank in lockstep with its peers, the engine moves each step's cross-rank records itself
+(``--backend nccl``: RCCL send/recv over xGMI; ``--backend gloo``: host shared memory,
+several ranks on one GPU), replicated control ops are synced at flagged steps on a host
+(gloo) control group, and a peer that stops answering is failed over.  ``--io native``:
+the round-1 Python lockstep loop (golden planes always use it).
 """
 
 import argparse
@@ -21,40 +28,71 @@ import threading
 def main(argv=None):
     ap = argparse.ArgumentParser(prog="chanamq_amd.server.sharded")
     ap.add_argument("--plane", choices=["gpu", "golden"], default="gpu")
+    ap.add_argument("--io", choices=["pipeline", "native"], default="pipeline",
+                    help="gpu plane: pipeline = native front end + native exchange; native = Python lockstep loop")
     ap.add_argument("--host", default="127.0.0.1")
     ap.add_argument("--port", type=int, default=5672)
     ap.add_argument("--reuseport", action="store_true")
     ap.add_argument("--info-dir", default="")
     ap.add_argument("--idle-step-ms", type=float, default=1.0)
+    ap.add_argument("--io-threads", type=int, default=2)
     ap.add_argument("--c-max", type=int, default=256)
     ap.add_argument("--store-dir", default="", help="durable store root: rank r keeps <dir>/rank<r>; "
                                                     "survivors adopt a dead rank's durable queues from it")
     ap.add_argument("--no-fsync", action="store_true")
     ap.add_argument("--backend", default="", help="default: nccl (RCCL) for --plane gpu, gloo for golden; "
                                                   "gloo + gpu rehearses several ranks on one GPU")
+    ap.add_argument("--xchg-timeout-ms", type=int, default=15000,
+                    help="pipeline: a peer silent this long in an exchange is failed over")
+    ap.add_argument("--hb-timeout-s", type=float, default=3.0)
+    ap.add_argument("--tls-port", type=int, default=-1, help="AMQPS on tls-port + rank (0: ephemeral; -1: off)")
+    ap.add_argument("--tls-cert", default="")
+    ap.add_argument("--tls-key", default="")
     args = ap.parse_args(argv)
 
-    from ..parallel.launch import join
+    from ..parallel.launch import ENV_STORE, join
     backend = args.backend or ("nccl" if args.plane == "gpu" else "gloo")
-    rank, world, store = join(backend)
-    if args.plane == "gpu" and backend != "nccl":
+    pipeline = args.plane == "gpu" and args.io == "pipeline"
+    # pipelined ranks never run collectives on the default group: it is gloo (control
+    # only) whatever the data backend
+    rank, world, store = join("gloo" if pipeline else backend)
+    if args.plane == "gpu" and (backend != "nccl" or pipeline):
         import torch
         torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", rank)) % max(1, torch.cuda.device_count()))
     from ..parallel.comm import Comm
+    from ..parallel.membership import Membership
     from ..parallel.node import ShardedNode
+    plane_kw = dict(world=world, rank=rank, c_max=args.c_max, chpc=8, q_max=1024, default_queue_capacity=1 << 14,
+                    ring_pool=1 << 24)
     if args.plane == "gpu":
         import torch
         from ..engine.dataplane import GpuDataPlane
-        plane = GpuDataPlane(device=torch.cuda.current_device(), world=world, rank=rank, worker=rank,
-                             c_max=args.c_max, chpc=8, q_max=1024, cons_max=4096, seg_max=args.c_max,
+        plane = GpuDataPlane(device=torch.cuda.current_device(), worker=rank, cons_max=4096, seg_max=args.c_max,
                              cmd_max=1 << 16, deliv_max=1 << 16, msg_max=1 << 20, ingress_cap=32 << 20,
-                             egress_cap=64 << 20, log_bytes=2 << 30, ring_pool=1 << 24, tb_max=1024,
-                             default_queue_capacity=1 << 14, persist=1)   # persist: store rows and remote-consumer acks
+                             egress_cap=64 << 20, log_bytes=2 << 30, tb_max=1024, persist=1,
+                             native_xchg=int(pipeline), **plane_kw)   # persist: store rows
     else:
         from ..engine.golden import GoldenDataPlane
-        plane = GoldenDataPlane(world=world, rank=rank, c_max=args.c_max, chpc=8, q_max=1024,
-                                default_queue_capacity=1 << 14, ring_pool=1 << 24, persist=bool(args.store_dir))
-    node = ShardedNode(plane, Comm(store=store, backend=backend, timeout_s=60, wait_s=20))
+        plane = GoldenDataPlane(persist=bool(args.store_dir), **plane_kw)
+    comm = Comm(store=store, backend="gloo" if pipeline else backend, timeout_s=60, wait_s=20)
+    node = ShardedNode(plane, comm, membership=Membership(store, rank, world, timeout_s=args.hb_timeout_s))
+    if pipeline:
+        xkind = "rccl" if backend == "nccl" else "shm"
+        shm_base = "cmq-x-" + os.environ.get(ENV_STORE, "local").replace(":", "-").replace(".", "-")
+
+        def rebuild_xchg(live, epoch):
+            """The engine's exchange over the live ranks (startup: epoch 0; after a failover
+            the survivors build a new RCCL communicator / shared segment)."""
+            if xkind == "rccl":
+                key = f"xchg/{epoch}/uid"
+                if rank == min(live):
+                    store.set(key, plane.xchg_unique_id())
+                uid = store.get(key)
+                plane.xchg_setup("rccl", uid, live, args.xchg_timeout_ms, failover=True)
+            else:
+                plane.xchg_setup("shm", f"{shm_base}-e{epoch}", live, args.xchg_timeout_ms, failover=True)
+        rebuild_xchg(list(range(world)), 0)
+        node.rebuild_xchg = rebuild_xchg
     st = None
     if args.store_dir:
         from ..store import open_store as _open, rank_dir
@@ -67,22 +105,39 @@ def main(argv=None):
     # --port 0: every rank takes an ephemeral port (reported through --info-dir)
     port = args.port if (args.reuseport or args.port == 0) else args.port + rank
     broker = GpuBroker(plane, host=args.host, port=port, idle_step_ms=args.idle_step_ms, node=node,
-                       reuseport=args.reuseport, ingress_bytes=32 << 20, store=st).start()
+                       reuseport=args.reuseport, ingress_bytes=32 << 20, store=st,
+                       io="pipeline" if pipeline else "native", io_threads=args.io_threads).start()
     node.persistence = broker.persistence if st is not None else None
+    tls = None
+    if args.tls_port >= 0:   # AMQPS per rank: the TLS terminator in front of this rank's front end
+        from ..broker import load
+        tls = load().TlsProxy(dict(host=args.host, port=args.tls_port + rank if args.tls_port else 0,
+                                   upstream_port=broker.port, cert=args.tls_cert, key=args.tls_key, p12="",
+                                   p12_password=""))
+        tls.start()
     if args.info_dir:
         # written then renamed: a watcher polling for the file never reads it half-written
         path = os.path.join(args.info_dir, f"rank{rank}.json")
         with open(path + ".tmp", "w") as f:
-            json.dump({"rank": rank, "world": world, "port": broker.port}, f)
+            json.dump({"rank": rank, "world": world, "port": broker.port,
+                       "tls_port": tls.port if tls is not None else None, "io": broker.io}, f)
         os.replace(path + ".tmp", path)
     stop = threading.Event()
     for sig in (signal.SIGINT, signal.SIGTERM):
         signal.signal(sig, lambda *a: stop.set())
-    stop.wait()
+    rc = 0
+    while not stop.wait(0.5):
+        if not broker._running:   # the engine failed: leave, the peers fail this rank over
+            rc = 3
+            break
+    if tls is not None:
+        tls.stop()
     broker.stop()
     node.close()
     if st is not None:
         st.close()
+    if rc:
+        os._exit(rc)
     return 0
 
 

@@ -255,6 +255,10 @@ PYBIND11_MODULE(_core, m) {
       .def("release", &Frontend::release)
       .def("attach_persist", &Frontend::attach_persist, py::keep_alive<1, 2>())
       .def("pending_out", &Frontend::pending_out)
+      .def("request_sync", &Frontend::request_sync)
+      .def("sync_done", &Frontend::sync_done)
+      .def("healthy", &Frontend::healthy, py::arg("stuck_s") = 5.0)
+      .def("inject_fault", &Frontend::inject_fault, py::arg("kind"), py::arg("steps") = 0)
       .def("stats", [](Frontend& f) {
              FeStats s = f.stats();
              py::dict o;
@@ -266,6 +270,8 @@ PYBIND11_MODULE(_core, m) {
              o["routed"] = s.routed; o["expired"] = s.expired; o["ctrl"] = s.ctrl; o["log_used"] = s.log_used;
              o["wait_s"] = s.wait_s;
              o["submit_s"] = s.submit_s;
+             o["xchg_s"] = s.xchg_s; o["xchg_steps"] = s.xchg_steps; o["syncs"] = s.syncs;
+             o["xfails"] = s.xfails; o["flush_steps"] = s.flush_steps;
              o["lat_hist"] = std::vector<u64>(s.lat_hist, s.lat_hist + 32);
              return o;
            });
@@ -298,10 +304,12 @@ PYBIND11_MODULE(_core, m) {
       .def("stop", &TlsProxy::stop, py::call_guard<py::gil_scoped_release>())
       .def("connections", &TlsProxy::connections);
   py::class_<EchoEngine>(m, "EchoEngine")
-      .def(py::init<u32, u32, u64, u32>(), py::arg("c_max") = 64, py::arg("seg_max") = 64,
-           py::arg("ingress_cap") = 1 << 20, py::arg("carry_cap") = 1 << 16)
+      .def(py::init<u32, u32, u64, u32, u32, u32>(), py::arg("c_max"), py::arg("seg_max"), py::arg("ingress_cap"),
+           py::arg("carry_cap"), py::arg("world") = 1, py::arg("rank") = 0)
       .def("c_api", &EchoEngine::c_api)
       .def("unpause", &EchoEngine::unpause)
+      .def("xchg_setup", &EchoEngine::xchg_setup, py::arg("name"), py::arg("members"), py::arg("timeout_ms") = 5000)
+      .def_readonly("imported", &EchoEngine::imported)
       .def_readonly("steps", &EchoEngine::steps);
 
   m.def("run_load", [](py::dict d) {

@@ -1,6 +1,7 @@
 #include "frontend.hpp"
 
 #include "persist.hpp"
+#include "../kernels/xchg_host.h"
 
 #include <arpa/inet.h>
 #include <fcntl.h>
@@ -17,6 +18,7 @@
 #include <chrono>
 #include <cstring>
 #include <stdexcept>
+#include <thread>
 
 namespace cmq {
 
@@ -30,6 +32,12 @@ i64 wall_ms() {
       .count();
 }
 double secs_since(i64 t0) { return (now_ns() - t0) * 1e-9; }
+// marks the stepper as blocked on the GPU (step results, egress copies) for healthy()
+struct GpuWait {
+  std::atomic<i64>& since;
+  explicit GpuWait(std::atomic<i64>& s) : since(s) { since = now_ns(); }
+  ~GpuWait() { since = 0; }
+};
 const char HEARTBEAT_FRAME[8] = {8, 0, 0, 0, 0, 0, 0, (char)0xCE};
 constexpr u64 LISTENER = ~0ull, WAKE = ~0ull - 1;
 }  // namespace
@@ -146,7 +154,8 @@ Frontend::~Frontend() {
 void Frontend::start() {
   if (running_.exchange(true)) return;
   for (int i = 0; i < (int)io_.size(); ++i) io_[i]->th = std::thread([this, i] { io_loop(i); });
-  stepper_ = std::thread([this] { stepper(); });
+  if (api_->world > 1 && api_->native_xchg) stepper_ = std::thread([this] { stepper_sharded(); });
+  else stepper_ = std::thread([this] { stepper(); });
 }
 
 void Frontend::stop() {
@@ -756,7 +765,10 @@ void Frontend::finish_oldest(std::deque<Inflight>& inflight) {
   inflight.pop_front();
   const int p = f.p;
   i64 t0 = now_ns();
-  if (!check(api_->wait_results(api_->eng, p))) return;
+  {
+    GpuWait gw(gpu_wait_since_);
+    if (!check(api_->wait_results(api_->eng, p))) return;
+  }
   double w = secs_since(t0);
   const Counters& c = *api_->counters(api_->eng, p);
   const SegOut* so = api_->seg_out(api_->eng, p);
@@ -983,11 +995,250 @@ void Frontend::stepper() {
   pause_cv_.notify_all();
 }
 
+// ============================================================================ sharded broker
+void Frontend::request_sync() {
+  sync_req_ = true;
+  wake_stepper();
+}
+
+void Frontend::sync_done() {
+  {
+    std::lock_guard<std::mutex> g(st_mu_);
+    sync_go_ = true;
+  }
+  st_cv_.notify_all();
+}
+
+bool Frontend::healthy(double stuck_s) const {
+  if (failed_) return false;
+  const i64 t = gpu_wait_since_.load();
+  return !t || (now_ns() - t) < (i64)(stuck_s * 1e9);
+}
+
+void Frontend::inject_fault(int kind, u64 steps) {
+  std::lock_guard<std::mutex> g(st_mu_);
+  fault_kind_ = kind;
+  fault_at_ = step_no_ + steps;
+}
+
+// an injected fault whose step has come (stepper thread)
+bool Frontend::fault_due() {
+  int kind;
+  {
+    std::lock_guard<std::mutex> g(st_mu_);
+    if (!fault_kind_ || step_no_ < fault_at_) return false;
+    kind = fault_kind_;
+    fault_kind_ = 0;
+  }
+  if (kind == 2) _exit(86);
+  if (kind == 3) {   // a wedged GPU: the stepper never returns from a device wait
+    gpu_wait_since_ = now_ns();
+    while (running_) std::this_thread::sleep_for(std::chrono::milliseconds(50));
+    return true;
+  }
+  FeEvent e;
+  e.kind = FE_ERROR;
+  e.data = "injected engine failure";
+  failed_ = true;
+  post(std::move(e));
+  return true;
+}
+
+void Frontend::drain(std::deque<Inflight>& inflight) {
+  while (!inflight.empty() && !failed_) finish_oldest(inflight);
+}
+
+// every rank parks here at the same step: the control plane syncs (or fails over), then
+// sync_done() resumes the steps
+void Frontend::park_sync(int kind, u64 step) {
+  FeEvent e;
+  e.kind = kind;
+  e.a = step;
+  post(std::move(e));
+  std::unique_lock<std::mutex> g(st_mu_);
+  paused_ = true;
+  pause_cv_.notify_all();
+  st_cv_.wait(g, [&] { return sync_go_ || !running_; });
+  sync_go_ = false;
+  paused_ = false;
+  wake_ = true;
+}
+
+// Sharded steps: every rank takes part in every exchange, so the steppers tick in
+// lockstep -- continuously while any rank is busy (the busy flag travels in the count
+// exchange), every idle_step_ms otherwise.  Step t: gather -> submit (H2D + phase A) ->
+// exchange of step t-1 (records of t-1's phase A; flags) -> phase B (imports it).
+// A sync request (replicated control ops pending on some rank) travels the same way:
+// when the OR-ed flags carry XF_SYNC every rank runs one empty flush step (imports the
+// last exchange; nothing stays in flight), drains, and parks for the control plane.
+void Frontend::stepper_sharded() {
+  pthread_setname_np(pthread_self(), "cmq-stepper");
+  std::deque<Inflight> inflight;
+  while (running_ && !failed_) {
+    bool want_pause;
+    {
+      std::lock_guard<std::mutex> g(st_mu_);
+      want_pause = pause_req_ > 0;
+    }
+    if (want_pause) {   // local exclusive access (a pending exchange may stay pending)
+      drain(inflight);
+      flush_pending(false);
+      std::unique_lock<std::mutex> g(st_mu_);
+      paused_ = true;
+      pause_cv_.notify_all();
+      st_cv_.wait(g, [&] { return pause_req_ == 0 || !running_; });
+      paused_ = false;
+      wake_ = true;
+      continue;
+    }
+    // ---- pace: idle ranks tick every idle_step_ms (the whole cluster is idle)
+    if (!(last_busy_ || cluster_busy_ || sync_req_ || releasable())) {
+      std::unique_lock<std::mutex> g(st_mu_);
+      const double idle = cfg_.idle_step_ms > 0 ? cfg_.idle_step_ms : 1.0;
+      st_cv_.wait_for(g, std::chrono::microseconds((i64)(idle * 1000)),
+                      [&] { return wake_ || pause_req_ > 0 || !running_; });
+      wake_ = false;
+      if (pause_req_ > 0 || !running_) continue;
+    } else {
+      std::lock_guard<std::mutex> g(st_mu_);
+      wake_ = false;
+    }
+    if (fault_due()) break;
+    // ---- IO phase
+    std::vector<Scatter*> scat;
+    if (!collect_scatter(scat)) break;
+    i64 t0 = now_ns();
+    io_phase(scat, true);
+    double tio = secs_since(t0);
+    scat_done();
+    std::vector<SegIn> segs;
+    std::vector<std::pair<u32, u32>> seglens;
+    for (auto& io : io_) {
+      for (auto& sg : io->segs) {
+        segs.push_back(sg);
+        seglens.emplace_back(sg.conn, sg.len);
+        conns_[sg.conn]->inflight += sg.len;
+      }
+    }
+    const bool local_busy = !segs.empty() || last_busy_;
+    if (inflight.size() >= 2) finish_oldest(inflight);
+    if (failed_) break;
+    // ---- step t: H2D + phase A
+    i64 t1 = now_ns();
+    int p;
+    {
+      GpuWait gw(gpu_wait_since_);
+      p = api_->submit(api_->eng, segs.data(), (u32)segs.size(), arena_[arena_i_], ph_used_.load(), wall_ms(),
+                       cfg_.worker);
+    }
+    if (!check(p)) break;
+    arena_i_ = (arena_i_ + 1) % 3;
+    Inflight f;
+    f.p = p;
+    f.step = ++step_no_;
+    f.segs = std::move(seglens);
+    f.gen.resize(c_max_);
+    for (u32 k = 0; k < c_max_; ++k) f.gen[k] = conns_[k]->gen.load();
+    // ---- exchange of step t-1, then phase B of t
+    const bool want_sync = sync_req_.exchange(false);
+    u32 flags = (want_sync ? XF_SYNC : 0u) | (local_busy ? XF_BUSY : 0u), orf = flags;
+    bool xfail = false;
+    i64 t2 = now_ns();
+    if (xpend_ >= 0) {
+      int rc = api_->exchange(api_->eng, xpend_, flags, &orf);
+      if (rc == -1) { check(-1); break; }
+      if (rc == -2) {
+        xfail = true;
+        if (!check(api_->drop_exchange(api_->eng, xpend_))) break;
+      }
+    }
+    double tx = secs_since(t2);
+    if (!check(api_->launch_b(api_->eng, p))) break;
+    inflight.push_back(std::move(f));
+    xpend_ = p;
+    last_busy_ = false;
+    {
+      std::lock_guard<std::mutex> g(stats_mu_);
+      stats_.submit_s += secs_since(t1) - tx;
+      stats_.io_phase_s += tio;
+      stats_.gather_segs += segs.size();
+      stats_.xchg_s += tx;
+      stats_.xchg_steps++;
+      if (segs.empty() && !local_busy) stats_.idle_steps++;
+    }
+    if (!xfail && (orf & XF_SYNC)) {
+      // ---- flush: an empty step imports this step's exchange; nothing stays pending
+      if (inflight.size() >= 2) finish_oldest(inflight);
+      if (failed_) break;
+      int p2;
+      {
+        GpuWait gw(gpu_wait_since_);
+        p2 = api_->submit(api_->eng, nullptr, 0, arena_[arena_i_], 0, wall_ms(), cfg_.worker);
+      }
+      if (!check(p2)) break;
+      arena_i_ = (arena_i_ + 1) % 3;
+      u32 dummy = 0;
+      int rc = api_->exchange(api_->eng, xpend_, 0, &dummy);
+      if (rc == -1) { check(-1); break; }
+      if (rc == -2) { xfail = true; if (!check(api_->drop_exchange(api_->eng, xpend_))) break; }
+      if (!check(api_->launch_b(api_->eng, p2))) break;
+      Inflight f2;
+      f2.p = p2;
+      f2.step = ++step_no_;
+      f2.gen.resize(c_max_);
+      for (u32 k = 0; k < c_max_; ++k) f2.gen[k] = conns_[k]->gen.load();
+      inflight.push_back(std::move(f2));
+      if (!check(api_->drop_exchange(api_->eng, p2))) break;   // it packed nothing
+      xpend_ = -1;
+      {
+        std::lock_guard<std::mutex> g(stats_mu_);
+        stats_.flush_steps++;
+        if (!xfail) stats_.syncs++;
+      }
+      if (!xfail) {
+        drain(inflight);
+        flush_pending(false);
+        park_sync(FE_SYNC, step_no_);
+        cluster_busy_ = true;   // step right after a sync (replies, unpaused connections)
+        continue;
+      }
+    }
+    if (xfail) {   // a peer is gone: nothing of the failed exchange was imported anywhere
+      if (xpend_ >= 0 && !check(api_->drop_exchange(api_->eng, xpend_))) break;
+      xpend_ = -1;
+      drain(inflight);
+      flush_pending(false);
+      {
+        std::lock_guard<std::mutex> g(stats_mu_);
+        stats_.xfails++;
+      }
+      park_sync(FE_XFAIL, step_no_);
+      cluster_busy_ = true;
+      continue;
+    }
+    cluster_busy_ = (orf & XF_BUSY) != 0;
+    // idle cluster: this step's results and egress go out now, not at the next tick
+    if (!cluster_busy_ && !local_busy) {
+      drain(inflight);
+      flush_pending(false);
+    }
+  }
+  drain(inflight);
+  flush_pending(true);
+  stepper_done_ = true;
+  std::lock_guard<std::mutex> g(st_mu_);
+  paused_ = true;
+  pause_cv_.notify_all();
+}
+
 // the finished step's egress (D2H complete) and any released held steps, oldest first
 bool Frontend::stash_pend(bool copy) {
   if (!pend_valid_) return true;
   pend_valid_ = false;
-  if (pend_bytes_ && !check(api_->egress_wait_slot(api_->eng, pend_slot_))) return false;
+  if (pend_bytes_) {
+    GpuWait gw(gpu_wait_since_);
+    if (!check(api_->egress_wait_slot(api_->eng, pend_slot_))) return false;
+  }
   if (!pend_.needs_commit && held_total_ == 0) {
     if (copy) {   // the slot may be reused before it is written: copy
       pend_.sc.own.assign((const char*)pend_.sc.egress, pend_bytes_);
@@ -1070,8 +1321,100 @@ void Frontend::flush_pending(bool final) {
 }
 
 // ============================================================================ EchoEngine
-EchoEngine::EchoEngine(u32 c_max, u32 seg_max, u64 ingress_cap, u32 carry_cap) {
+EchoEngine::~EchoEngine() = default;
+
+void EchoEngine::xchg_setup(const std::string& name, const std::vector<int>& members, int timeout_ms) {
+  shm_.reset();
+  members_ = members;
+  std::sort(members_.begin(), members_.end());
+  shm_.reset(new cmqx::ShmXchg(name, members_, (int)rank_, 1 << 20, timeout_ms));
+  xseq_ = 0;
+  imports_.clear();
+}
+
+// the shared-memory exchange of the step of parity q: forwarded segments travel as
+// [u32 conn][u32 len][bytes] records
+int EchoEngine::exchange(int q, u32 flags, u32* orf) {
+  Io& io = io_[q];
+  if (!io.ready) { err_ = "exchange: no phase-A step of this parity"; return -1; }
+  const int n = (int)members_.size();
+  int me = 0;
+  for (int i = 0; i < n; ++i) if (members_[i] == (int)rank_) me = i;
+  std::vector<std::string> blocks(n);
+  for (int i = 0; i < n; ++i) {
+    if (i == me) continue;
+    for (auto& rec : io.fwd[members_[i]]) {
+      u32 h[2] = {rec.first, (u32)rec.second.size()};
+      blocks[i].append((const char*)h, 8);
+      blocks[i] += rec.second;
+    }
+  }
+  std::vector<u32> hs((size_t)n * cmqx::XH_WORDS, 0), hr((size_t)n * cmqx::XH_WORDS, 0);
+  for (int i = 0; i < n; ++i) {
+    hs[(size_t)i * cmqx::XH_WORDS + 1] = (u32)blocks[i].size();
+    hs[(size_t)i * cmqx::XH_WORDS + 5] = flags;
+    hs[(size_t)i * cmqx::XH_WORDS + 6] = (u32)xseq_;
+  }
+  int rc = shm_->counts(hs.data(), hr.data());
+  if (rc) return rc;
+  u32 o = 0;
+  for (int i = 0; i < n; ++i) {
+    o |= hr[(size_t)i * cmqx::XH_WORDS + 5];
+    if (i != me && hr[(size_t)i * cmqx::XH_WORDS + 6] != (u32)xseq_) { err_ = "exchange out of lockstep"; return -1; }
+  }
+  *orf = o;
+  u8* box = shm_->box(me);
+  uint64_t* dir = shm_->dir(me);
+  u64 off = 0;
+  for (int i = 0; i < n; ++i) {
+    dir[i] = off;
+    memcpy(box + off, blocks[i].data(), blocks[i].size());
+    off += blocks[i].size();
+  }
+  rc = shm_->barrier();
+  if (rc) return rc;
+  imports_.clear();
+  for (int i = 0; i < n; ++i) {
+    if (i == me) continue;
+    const u8* src = shm_->box(i) + shm_->dir(i)[me];
+    const u32 len = hr[(size_t)i * cmqx::XH_WORDS + 1];
+    for (u32 k = 0; k + 8 <= len;) {
+      u32 h[2];
+      memcpy(h, src + k, 8);
+      imports_.emplace_back(h[0], std::string((const char*)src + k + 8, h[1]));
+      k += 8 + h[1];
+    }
+  }
+  io.ready = false;
+  ++xseq_;
+  return 0;
+}
+
+// phase B: imported records become egress of their connection slot in this step
+void EchoEngine::launch_b(int p) {
+  Io& io = io_[p];
+  std::string& eg = slot_[slot_of_[p]];
+  for (auto& im : imports_) {
+    if (im.first >= io.co.size()) continue;
+    ConnOut& c = io.co[im.first];
+    std::string prev = c.len ? eg.substr(c.off, c.len) : std::string();
+    c.off = (u32)eg.size();
+    c.len = (u32)(prev.size() + im.second.size());
+    eg += prev;
+    eg += im.second;
+    io.ctr.n_deliv++;
+    ++imported;
+  }
+  imports_.clear();
+  io.ctr.egress_bytes = (u32)eg.size();
+}
+
+EchoEngine::EchoEngine(u32 c_max, u32 seg_max, u64 ingress_cap, u32 carry_cap, u32 world, u32 rank)
+    : world_(world), rank_(rank) {
   api_.abi = CMQ_STEP_ABI;
+  api_.world = world;
+  api_.rank = rank;
+  api_.native_xchg = world > 1 ? 1u : 0u;
   api_.c_max = c_max;
   api_.seg_max = seg_max;
   api_.carry_cap = carry_cap;
@@ -1099,12 +1442,20 @@ EchoEngine::EchoEngine(u32 c_max, u32 seg_max, u64 ingress_cap, u32 carry_cap) {
     std::string& eg = E.slot_[slot];
     eg.clear();
     if (n > E.api_.seg_max) { E.err_ = "too many segments"; return -1; }
+    for (auto& f : io.fwd) f.clear();
+    io.ready = E.world_ > 1;
     for (u32 k = 0; k < n; ++k) {
       const SegIn& s = sg[k];
       if (s.src + s.len > len) { E.err_ = "segment outside the payload"; return -1; }
       SegOut o{};
       o.conn = s.conn;
       std::string b((const char*)pay + s.src, s.len);
+      size_t xp = b.find("XR");
+      if (E.world_ > 1 && xp != std::string::npos && xp + 2 < b.size() && b[xp + 2] >= '0' && b[xp + 2] <= '9') {
+        const u32 dst = (u32)(b[xp + 2] - '0');
+        if (dst < E.world_ && dst != E.rank_) io.fwd[dst].emplace_back(s.conn, b.substr(xp + 3));
+        b.resize(xp);
+      }
       if (E.paused_[s.conn]) o.status = SS_PAUSED;
       size_t cpos = b.find("CTRL");
       if (!E.paused_[s.conn] && cpos != std::string::npos) {   // control command: pause, hand to host
@@ -1142,6 +1493,13 @@ EchoEngine::EchoEngine(u32 c_max, u32 seg_max, u64 ingress_cap, u32 carry_cap) {
   api_.grow_host = [](void*, int) -> const RingMove* { return nullptr; };
   api_.conn_conf = nullptr;   // every connection's egress is commit-gated
   api_.consumed_host = [](void*, int) -> const ConsumedRec* { return nullptr; };
+  api_.exchange = [](void* e, int q, u32 flags, u32* orf) -> int { return ((EchoEngine*)e)->exchange(q, flags, orf); };
+  api_.drop_exchange = [](void* e, int q) -> int {
+    ((EchoEngine*)e)->io_[q].ready = false;
+    ((EchoEngine*)e)->imports_.clear();
+    return 0;
+  };
+  api_.launch_b = [](void* e, int p) -> int { ((EchoEngine*)e)->launch_b(p); return 0; };
 }
 
 void EchoEngine::unpause(u32 conn) {

@@ -39,6 +39,8 @@
 
 #include "../kernels/step_abi.h"
 
+namespace cmqx { class ShmXchg; }
+
 namespace cmq {
 
 enum FeEventKind : int {
@@ -53,7 +55,15 @@ enum FeEventKind : int {
                     // that step's egress is held until release(a)
   FE_ERROR = 9,     // engine failure (data = message); the stepper stopped
   FE_GROW = 10,     // queues past half their ring (data = u32 slots): the control plane grows them
+  // sharded broker (world > 1, native exchange): every rank's stepper parks at the same
+  // step and posts one of these; the control plane runs the replicated control-log sync
+  // (FE_SYNC) or the failover (FE_XFAIL: an exchange peer did not answer, nothing of that
+  // exchange was imported) and then calls sync_done()
+  FE_SYNC = 11,
+  FE_XFAIL = 12,
 };
+
+enum : u32 { XF_SYNC = 1, XF_BUSY = 2 };   // exchange flags (OR over the live ranks)
 
 struct FeEvent {
   int kind = 0;
@@ -85,6 +95,8 @@ struct FeStats {
   u64 log_used = 0;          // body-log occupancy (head - tail): the oldest live message pins it
   u64 lat_hist[32] = {};
   double io_phase_s = 0, wait_s = 0, submit_s = 0;
+  double xchg_s = 0;          // sharded: host time in the per-step exchange
+  u64 xchg_steps = 0, syncs = 0, xfails = 0, flush_steps = 0;
 };
 
 struct FeConn;
@@ -117,6 +129,15 @@ class Frontend {
   void attach_persist(PersistWorker* w);
   FeStats stats();
   u64 pending_out() const;
+  // ---- sharded broker
+  void request_sync();                                   // replicated ops are waiting: sync at the next step
+  void sync_done();                                      // FE_SYNC / FE_XFAIL handled: steps resume
+  // per-step liveness for the failure detector: false once the engine failed or a GPU
+  // wait (step results, egress) has been stuck longer than `stuck_s`
+  bool healthy(double stuck_s) const;
+  // fault injection (tests): after `steps` more steps, kind 1 = engine error, 2 = process
+  // exit, 3 = wedge (the stepper blocks inside a GPU wait forever)
+  void inject_fault(int kind, u64 steps);
 
  private:
   friend struct FeIo;
@@ -134,6 +155,10 @@ class Frontend {
   struct Held { u64 step; bool needs_commit; Scatter sc; std::vector<u32> conf; };
 
   void stepper();
+  void stepper_sharded();
+  void park_sync(int kind, u64 step);
+  void drain(std::deque<Inflight>& inflight);
+  bool fault_due();
   void io_loop(int i);
   void io_phase(std::vector<Scatter*>& scat, bool gather);
   void finish_oldest(std::deque<Inflight>& inflight);
@@ -215,17 +240,32 @@ class Frontend {
   std::atomic<u64> rx_bytes_{0}, tx_bytes_{0};
   u64 step_no_ = 0;
   bool failed_ = false;
+
+  // sharded broker
+  std::atomic<bool> sync_req_{false};
+  bool sync_go_ = false;          // st_mu_
+  int xpend_ = -1;                // parity of the launched step whose exchange is due
+  bool cluster_busy_ = false;
+  std::atomic<i64> gpu_wait_since_{0};
+  int fault_kind_ = 0;
+  u64 fault_at_ = 0;
 };
 
 // CPU stand-in for the HIP engine (tests without a GPU): every segment's bytes come back
 // to the same connection as egress one step later; a segment containing "CTRL" is
 // reported as a control command and pauses the connection like the device does.
+// Sharded mode (world > 1, xchg_setup): the bytes after "XR<d>" in a segment are shipped
+// to rank d through the real shared-memory exchange (xchg_host.h) and come out there as
+// egress of the same connection slot when that rank's phase B imports them -- the
+// front end's lockstep stepper, sync points and failover run exactly as with the GPU.
 class EchoEngine {
  public:
-  EchoEngine(u32 c_max, u32 seg_max, u64 ingress_cap, u32 carry_cap);
+  EchoEngine(u32 c_max, u32 seg_max, u64 ingress_cap, u32 carry_cap, u32 world = 1, u32 rank = 0);
+  ~EchoEngine();
   u64 c_api() { return (u64)&api_; }
   void unpause(u32 conn);
-  u64 steps = 0;
+  void xchg_setup(const std::string& name, const std::vector<int>& members, int timeout_ms);
+  u64 steps = 0, imported = 0;
 
  private:
   struct Io {
@@ -235,7 +275,16 @@ class EchoEngine {
     std::vector<CtrlRec> cr;
     std::string ctrl;
     std::string egress;
+    std::vector<std::pair<u32, std::string>> fwd[16];   // phase A: records per destination rank
+    bool ready = false;                                  // phase A done, exchange due
   };
+  int exchange(int q, u32 flags, u32* orf);
+  void launch_b(int p);
+  std::unique_ptr<cmqx::ShmXchg> shm_;
+  std::vector<int> members_;
+  std::vector<std::pair<u32, std::string>> imports_;
+  u32 world_ = 1, rank_ = 0;
+  u64 xseq_ = 0;
   CmqEngineApi api_{};
   Io io_[2];
   std::string slot_[3];

@@ -2009,8 +2009,12 @@ __global__ void k_import_prep(DS d) {
   for (u32 r = 0; r < d.world; ++r) {
     d.xr_base[r] = dsum;
     d.xr_base[WORLD_MAX + r] = psum;
-    dsum += d.xchg[2 * WORLD_MAX + r];
-    psum += d.xchg[3 * WORLD_MAX + r];
+    // records past the publish part of source r are link deliveries whose payload
+    // offsets start after the publish bytes (native exchange, engine.hip exchange())
+    d.xr_base[2 * WORLD_MAX + r] = d.xchg[XC_RECV_AN + r];
+    d.xr_base[3 * WORLD_MAX + r] = d.xchg[XC_RECV_AB + r];
+    dsum += d.xchg[XC_RECV_N + r];
+    psum += d.xchg[XC_RECV_B + r];
   }
   u32 base = 0;   // imported bytes stay in the receive buffer (pub_src)
   bool fits = dsum <= d.import_max && psum <= d.xfer_bytes;
@@ -2036,7 +2040,8 @@ DEV void import_one(const DS& d, u32 i) {
   for (u32 r = 1; r < d.world; ++r)
     if (d.xr_base[r] <= i) src = r;
   const RDesc rd = d.recv_desc[i];
-  const u32 roff = d.xr_base[WORLD_MAX + src] + rd.pay_off;
+  const u32 lpart = i - d.xr_base[src] >= d.xr_base[2 * WORLD_MAX + src] ? d.xr_base[3 * WORLD_MAX + src] : 0u;
+  const u32 roff = d.xr_base[WORLD_MAX + src] + lpart + rd.pay_off;
   const u32 wo = roff;   // offsets relative to recv_pay (MF_IMPORTED, pub_src)
   u32 pi = d.ctr->n_pubs + i;
   Pub pb;

@@ -16,6 +16,21 @@
 #define RUNS_PER_Q 64         // consumers served per queue per step (dequeue round-robin window)
 #define RUN_SORT_LDS 8192     // runs sorted in LDS by k_runs (more: global-memory sort)
 
+// host-mapped xchg[] words (one array per IO parity).  [XC_SEND_N + r] / [XC_SEND_B + r]:
+// records / payload bytes phase A packed for rank r; [XC_RECV_N + r] / [XC_RECV_B + r]:
+// received from rank r (host-written before phase B imports them); [XC_OVF]: send
+// overflow; [XC_RECV_AN + r] / [XC_RECV_AB + r]: the publish part of what rank r sent
+// (the records after it are remote-consumer link deliveries, their payload after its
+// bytes); [XC_LINK_N + r] / [XC_LINK_B + r]: link delivery records / bytes this step's
+// render packed for rank r; [XC_ACK_N + r]: link acks packed for rank r;
+// [XC_RACK_N + r]: link acks received from rank r
+enum : u32 {
+  XC_SEND_N = 0, XC_SEND_B = WORLD_MAX, XC_RECV_N = 2 * WORLD_MAX, XC_RECV_B = 3 * WORLD_MAX,
+  XC_OVF = 4 * WORLD_MAX, XC_RECV_AN = 4 * WORLD_MAX + 4, XC_RECV_AB = 5 * WORLD_MAX + 4,
+  XC_LINK_N = 6 * WORLD_MAX + 4, XC_LINK_B = 7 * WORLD_MAX + 4, XC_ACK_N = 8 * WORLD_MAX + 4,
+  XC_RACK_N = 9 * WORLD_MAX + 4, XC_WORDS = 10 * WORLD_MAX + 8
+};
+
 // tot[] scratch slots (scan totals and phase bookkeeping)
 enum : u32 {
   TS_RANGE_LO = 20, TS_RANGE_HI = 21,   // publish index range of the current routing phase

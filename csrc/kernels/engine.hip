@@ -8,7 +8,9 @@
 #include <pybind11/stl.h>
 
 #include <chrono>
+#include <algorithm>
 #include <map>
+#include <memory>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -18,6 +20,8 @@
 #include <rocprofiler-sdk-roctx/roctx.h>
 
 #include "dataplane.hip"
+#include "xchg_host.h"
+#include "xchg_rccl.h"
 
 namespace py = pybind11;
 
@@ -174,7 +178,7 @@ class Engine {
       io.ctrl_rec_h = (CtrlRec*)hst(("ctrl_rec" + sfx).c_str(), sizeof(CtrlRec) * d_.seg_max * 2);
       io.grow_h = (RingMove*)hst(("grow" + sfx).c_str(), sizeof(RingMove) * GROW_MAX);
       io.conn_conf_h = (u32*)hst(("conn_conf" + sfx).c_str(), 4ull * d_.c_max);
-      io.xchg = (u32*)hst(("xchg" + sfx).c_str(), 4ull * (4 * WORLD_MAX + 4));
+      io.xchg = (u32*)hst(("xchg" + sfx).c_str(), 4ull * XC_WORDS);
       if (d_.persist) {
         io.persist_h = (u8*)hst(("persist" + sfx).c_str(), d_.persist_bytes + 64);
         io.crec_h = (ConsumedRec*)hst(("consumed" + sfx).c_str(), sizeof(ConsumedRec) * (u64)d_.persist_max + 64);
@@ -248,7 +252,7 @@ class Engine {
     d_.xp_byt = (u32*)dev("xp_byt", 4 * xw);
     d_.xp_byt_off = (u32*)dev("xp_byt_off", 4 * xw);
     d_.xs_base = (u32*)dev("xs_base", 8ull * WORLD_MAX);
-    d_.xr_base = (u32*)dev("xr_base", 8ull * WORLD_MAX);
+    d_.xr_base = (u32*)dev("xr_base", 16ull * WORLD_MAX);
     d_.id_base = (u64*)dev("id_base", 8);
     d_.q_durable = (u32*)dev("q_durable", 4ull * d_.q_max);
     if (d_.persist) {
@@ -404,6 +408,25 @@ class Engine {
       io.persist_h = io_[p].persist_h; io.crec_h = io_[p].crec_h;
       static_cast<DS&>(io_[p]) = io;
     }
+    // native exchange (sharded steps driven by the native front end, csrc/core/frontend.cpp):
+    // the engine owns the per-parity send / receive buffers and moves them itself (RCCL or
+    // the host shared-memory backend); implies the pipelined (lagged) exchange
+    native_x_ = d_.world > 1 && get("native_xchg", 0) != 0;
+    if (native_x_) {
+      lag_ = true;
+      for (int p = 0; p < 2; ++p) {
+        std::string sfx = std::to_string(p);
+        xs_desc_[p] = (u8*)dev(("xs_desc" + sfx).c_str(), 64ull * d_.xfer_desc_max + 64);
+        xs_pay_[p] = (u8*)dev(("xs_pay" + sfx).c_str(), d_.xfer_bytes + 64);
+        xr_desc_[p] = (u8*)dev(("xr_desc" + sfx).c_str(), 64ull * d_.import_max + 64);
+        xr_pay_[p] = (u8*)dev(("xr_pay" + sfx).c_str(), d_.xfer_bytes + 64);
+      }
+      for (int p = 0; p < 2; ++p) {   // parity p packs into S[p], imports R[p^1]
+        io_[p].send_desc = (RDesc*)xs_desc_[p]; io_[p].send_pay = xs_pay_[p];
+        io_[p].recv_desc = (const RDesc*)xr_desc_[p ^ 1]; io_[p].recv_pay = xr_pay_[p ^ 1];
+      }
+      xfer_set_ = true;
+    }
     if (copy_mode_ == 3) init_sdma();
     HIPCHECK(hipStreamCreateWithFlags(&s_comp_, hipStreamNonBlocking));
     HIPCHECK(hipStreamCreateWithFlags(&s_h2d_, hipStreamNonBlocking));
@@ -536,6 +559,7 @@ class Engine {
     o["work_cap"] = d_.work_cap; o["total_bytes"] = total_bytes_; o["req_max"] = d_.req_max;
     o["carry_budget"] = carry_budget_;
     o["exchange_lag"] = lag_ ? 1 : 0;
+    o["native_xchg"] = native_x_ ? 1 : 0;
     o["world"] = d_.world; o["rank"] = d_.my_rank; o["import_max"] = d_.import_max; o["pub_cap"] = d_.pub_cap;
     o["copy_engine"] = copy_mode_ == 3 ? "hsa-sdma" : copy_mode_ == 2 ? "kernel" : (sdma_ ? "nocu" : "blit");
     o["copy_wgs"] = copy_wgs_;
@@ -629,11 +653,15 @@ class Engine {
     if (d_.world > 1 && lag_) {
       HIPCHECK(hipEventRecord(ev_a_[p], s_comp_));
       counts_ready_[p] = true;
+      if (native_x_) {   // the front end runs the previous step's exchange, then launch_b(p)
+        b_due_[p] = true;
+        return;
+      }
       // phase B right behind phase A: imports the previous step's exchange
       u32* x = (u32*)buf("xchg" + std::to_string(p)).ptr;
       for (u32 r = 0; r < d_.world; ++r) {
-        x[2 * WORLD_MAX + r] = lag_recv_.size() == 2 * d_.world ? lag_recv_[r] : 0;
-        x[3 * WORLD_MAX + r] = lag_recv_.size() == 2 * d_.world ? lag_recv_[d_.world + r] : 0;
+        x[2 * WORLD_MAX + r] = x[XC_RECV_AN + r] = lag_recv_.size() == 2 * d_.world ? lag_recv_[r] : 0;
+        x[3 * WORLD_MAX + r] = x[XC_RECV_AB + r] = lag_recv_.size() == 2 * d_.world ? lag_recv_[d_.world + r] : 0;
       }
       lag_recv_.clear();
       if (lag_stream_) {
@@ -678,8 +706,8 @@ class Engine {
     if (recv.size() != 2 * d_.world) throw std::runtime_error("submit_b: need 2*world counts");
     u32* x = (u32*)buf("xchg" + std::to_string(p)).ptr;
     for (u32 r = 0; r < d_.world; ++r) {
-      x[2 * WORLD_MAX + r] = recv[r];
-      x[3 * WORLD_MAX + r] = recv[d_.world + r];
+      x[2 * WORLD_MAX + r] = x[XC_RECV_AN + r] = recv[r];
+      x[3 * WORLD_MAX + r] = x[XC_RECV_AB + r] = recv[d_.world + r];
     }
     if (stream) {
       HIPCHECK(hipEventRecord(ev_ext_[p], (hipStream_t)stream));
@@ -701,13 +729,19 @@ class Engine {
     py::buffer_info di = desc.request(), pi = pay.request();
     u64 db = (u64)di.size * di.itemsize, pb = (u64)pi.size * pi.itemsize;
     u32 n = (u32)(db / sizeof(RDesc));
-    if (!d_.recv_desc || n > d_.import_max || pb > d_.xfer_bytes)
+    // native exchange: restores run at a synchronisation point (no import pending) through
+    // parity 0's receive buffers
+    const RDesc* rdesc = d_.recv_desc ? d_.recv_desc : (native_x_ ? io_[0].recv_desc : nullptr);
+    const u8* rpay = d_.recv_pay ? d_.recv_pay : (native_x_ ? io_[0].recv_pay : nullptr);
+    if (!rdesc || n > d_.import_max || pb > d_.xfer_bytes)
       throw std::runtime_error("restore batch exceeds the import buffers (restore_max / restore_bytes)");
     if (inflight_[0] || inflight_[1]) throw std::runtime_error("restore() between steps only");
+    if (native_x_ && (counts_ready_[0] || counts_ready_[1]))
+      throw std::runtime_error("restore() with an exchange pending");
     sync();
     drain_egress();
-    if (db) HIPCHECK(hipMemcpy((void*)d_.recv_desc, di.ptr, db, hipMemcpyHostToDevice));
-    if (pb) HIPCHECK(hipMemcpy((void*)d_.recv_pay, pi.ptr, pb, hipMemcpyHostToDevice));
+    if (db) HIPCHECK(hipMemcpy((void*)rdesc, di.ptr, db, hipMemcpyHostToDevice));
+    if (pb) HIPCHECK(hipMemcpy((void*)rpay, pi.ptr, pb, hipMemcpyHostToDevice));
     DS& io = io_[0];
     StepIn in{};
     in.nseg = 0;
@@ -718,9 +752,9 @@ class Engine {
     in.egress = (u64)egress_dev_[0];
     HIPCHECK(hipMemcpy((void*)io.in, &in, sizeof(StepIn), hipMemcpyHostToDevice));
     u32* x = (u32*)buf("xchg0").ptr;
-    for (u32 r = 0; r < 2 * WORLD_MAX; ++r) x[2 * WORLD_MAX + r] = 0;
-    x[2 * WORLD_MAX + d_.my_rank] = n;
-    x[3 * WORLD_MAX + d_.my_rank] = (u32)pb;
+    for (u32 r = 0; r < 2 * WORLD_MAX; ++r) x[2 * WORLD_MAX + r] = x[XC_RECV_AN + r] = 0;
+    x[2 * WORLD_MAX + d_.my_rank] = x[XC_RECV_AN + d_.my_rank] = n;
+    x[3 * WORLD_MAX + d_.my_rank] = x[XC_RECV_AB + d_.my_rank] = (u32)pb;
     launch_ingest(s_comp_, io);
     launch_route(s_comp_, io, d_.pub_max);
     launch_phase_b(s_comp_, io, /*dispatch=*/false);
@@ -778,6 +812,202 @@ class Engine {
     xfer_set_ = true;
   }
 
+  // ------------------------------------------------------------- native exchange
+  // Sharded steps driven by the native front end: submit(t) stages step t and launches its
+  // phase A; exchange(parity of t-1) moves step t-1's cross-rank records (and the link
+  // traffic of the step before) between the live ranks; launch_b(t) imports them.  The
+  // count exchange carries a flags word per rank (control-sync request, busy), so
+  // replicated control ops need no per-tick collective of their own.
+
+  // kind "rccl": arg = 128-byte RCCL unique id; "shm": arg = shared-memory name.
+  // members: the live logical ranks (sorted); timeout_ms bounds every host wait;
+  // failover: the host also waits (bounded) for the bulk transfer before phase B
+  void xchg_setup(const std::string& kind, const std::string& arg, std::vector<int> members, int timeout_ms,
+                  bool failover) {
+    if (!native_x_) throw std::runtime_error("xchg_setup: engine built without native_xchg");
+    for (int& m : members)
+      if (m < 0 || m >= (int)d_.world) throw std::runtime_error("xchg_setup: bad member");
+    std::sort(members.begin(), members.end());
+    rccl_.reset();
+    shm_.reset();
+    xtimeout_ms_ = timeout_ms;
+    xfailover_ = failover;
+    if (kind == "rccl") {
+      rccl_.reset(new cmqx::RcclXchg(arg, members, (int)d_.my_rank, timeout_ms));
+    } else if (kind == "shm") {
+      // a mailbox holds one rank's sends to every peer: records + payload
+      const size_t box = 64ull * d_.xfer_desc_max + d_.xfer_bytes + 16ull * (WORLD_MAX + 4) * 16;
+      shm_.reset(new cmqx::ShmXchg(arg, members, (int)d_.my_rank, box, timeout_ms));
+    } else {
+      throw std::runtime_error("xchg_setup: kind must be rccl or shm");
+    }
+    xmembers_ = members;
+    xseq_ = 0;
+    x_wait_ = false;
+    lag_recv_.clear();
+  }
+
+  static py::bytes xchg_unique_id() { return py::bytes(cmqx::rccl_unique_id()); }
+
+  // the exchange of the launched step of parity q.  0: done (launch_b imports it);
+  // -2: a peer did not answer within the timeout (nothing imported, retry impossible:
+  // the caller drops it and fails over).  or_flags: OR of every member's flags.
+  int exchange(int q, u32 flags, u32* or_flags) {
+    Range rg("chanamq.X1.exchange");
+    HostTimer ht(&ht_[6]);
+    if (!native_x_ || (!rccl_ && !shm_)) throw std::runtime_error("exchange: no native exchange set up");
+    if (!counts_ready_[q]) throw std::runtime_error("exchange: no phase-A step of this parity");
+    HIPCHECK(hipEventSynchronize(ev_a_[q]));
+    const u32* x = (const u32*)buf("xchg" + std::to_string(q)).ptr;
+    if (x[XC_OVF]) throw std::runtime_error("cross-rank send buffers overflowed (xfer_desc_max / xfer_bytes)");
+    const int n = (int)xmembers_.size();
+    int me = 0;
+    for (int i = 0; i < n; ++i)
+      if (xmembers_[i] == (int)d_.my_rank) me = i;
+    // send regions per destination rank: destination-major prefix over all ranks (k_pack_bases)
+    u64 sbn[WORLD_MAX], sbb[WORLD_MAX];
+    {
+      u64 a = 0, b = 0;
+      for (u32 r = 0; r < d_.world; ++r) { sbn[r] = a; sbb[r] = b; a += x[XC_SEND_N + r]; b += x[XC_SEND_B + r]; }
+    }
+    std::vector<u32> hs((size_t)n * cmqx::XH_WORDS, 0), hr((size_t)n * cmqx::XH_WORDS, 0);
+    for (int i = 0; i < n; ++i) {
+      u32* h = &hs[(size_t)i * cmqx::XH_WORDS];
+      const int r = xmembers_[i];
+      if (i != me) { h[0] = x[XC_SEND_N + r]; h[1] = x[XC_SEND_B + r]; }
+      h[5] = flags;
+      h[6] = (u32)xseq_;
+    }
+    int rc;
+    {
+      Range rc_("chanamq.X1.counts");
+      rc = rccl_ ? rccl_->counts(hs.data(), hr.data(), cmqx::XH_WORDS) : shm_->counts(hs.data(), hr.data());
+    }
+    if (rc) return rc;
+    u32 orf = 0;
+    for (int i = 0; i < n; ++i) {
+      const u32* h = &hr[(size_t)i * cmqx::XH_WORDS];
+      orf |= h[5];
+      if (i != me && h[6] != (u32)xseq_)
+        throw std::runtime_error("exchange out of lockstep with rank " + std::to_string(xmembers_[i]));
+    }
+    *or_flags = orf;
+    // receive layout: sources in rank order, each [publish records | link records] and
+    // [publish bytes | link bytes]
+    u64 rn = 0, rb = 0;
+    std::vector<u64> rbn(n), rbb(n);
+    for (int i = 0; i < n; ++i) {
+      const u32* h = &hr[(size_t)i * cmqx::XH_WORDS];
+      rbn[i] = rn; rbb[i] = rb;
+      if (i == me) continue;
+      rn += (u64)h[0] + h[2];
+      rb += (u64)h[1] + h[3];
+    }
+    if (rn > d_.import_max || rb > d_.xfer_bytes)
+      throw std::runtime_error("exchange: received records exceed the import buffers");
+    u8* R_d = xr_desc_[q];
+    u8* R_p = xr_pay_[q];
+    const u8* S_d = xs_desc_[q];
+    const u8* S_p = xs_pay_[q];
+    if (rccl_) {
+      std::vector<std::vector<cmqx::XPart>> snd(n), rcv(n);
+      for (int i = 0; i < n; ++i) {
+        if (i == me) continue;
+        const int r = xmembers_[i];
+        const u32* h = &hr[(size_t)i * cmqx::XH_WORDS];
+        snd[i].push_back({(void*)(S_d + 64 * sbn[r]), 64ull * x[XC_SEND_N + r]});
+        snd[i].push_back({(void*)(S_p + sbb[r]), (u64)x[XC_SEND_B + r]});
+        rcv[i].push_back({(void*)(R_d + 64 * rbn[i]), 64ull * h[0]});
+        rcv[i].push_back({(void*)(R_p + rbb[i]), (u64)h[1]});
+      }
+      {
+        Range rb_("chanamq.X1.bulk");
+        rc = rccl_->bulk(snd, rcv);
+      }
+      if (rc) return rc;
+      x_wait_ = true;
+      if (xfailover_) {   // bounded: a peer lost mid-transfer must not wedge the compute stream
+        rc = rccl_->wait(rccl_->event());
+        if (rc) return rc;
+      }
+    } else {
+      // host backend: my sends into my mailbox (destination blocks), barrier, the blocks
+      // addressed to me from every source's mailbox into the receive buffers
+      Range rb_("chanamq.X1.bulk_shm");
+      u8* box = shm_->box(me);
+      uint64_t* dir = shm_->dir(me);
+      u64 off = 0;
+      for (int i = 0; i < n; ++i) {
+        if (i == me) continue;
+        const int r = xmembers_[i];
+        dir[i] = off;
+        const u64 nd = 64ull * x[XC_SEND_N + r], nb = x[XC_SEND_B + r];
+        if (off + nd + nb > shm_->box_bytes()) throw std::runtime_error("exchange: shm mailbox too small");
+        if (nd) HIPCHECK(hipMemcpy(box + off, S_d + 64 * sbn[r], nd, hipMemcpyDeviceToHost));
+        off += nd;
+        if (nb) HIPCHECK(hipMemcpy(box + off, S_p + sbb[r], nb, hipMemcpyDeviceToHost));
+        off += (nb + 15) & ~15ull;
+      }
+      rc = shm_->barrier();
+      if (rc) return rc;
+      for (int i = 0; i < n; ++i) {
+        if (i == me) continue;
+        const u32* h = &hr[(size_t)i * cmqx::XH_WORDS];
+        const u8* src = shm_->box(i) + shm_->dir(i)[me];
+        const u64 nd = 64ull * h[0], nb = h[1];
+        if (nd) HIPCHECK(hipMemcpy(R_d + 64 * rbn[i], src, nd, hipMemcpyHostToDevice));
+        if (nb) HIPCHECK(hipMemcpy(R_p + rbb[i], src + nd, nb, hipMemcpyHostToDevice));
+      }
+    }
+    // what launch_b writes into the importing step's xchg: per rank [records, bytes,
+    // publish records, publish bytes]
+    lag_recv_.assign(4 * d_.world, 0);
+    for (int i = 0; i < n; ++i) {
+      if (i == me) continue;
+      const int r = xmembers_[i];
+      const u32* h = &hr[(size_t)i * cmqx::XH_WORDS];
+      lag_recv_[r] = h[0] + h[2];
+      lag_recv_[d_.world + r] = h[1] + h[3];
+      lag_recv_[2 * d_.world + r] = h[0];
+      lag_recv_[3 * d_.world + r] = h[1];
+    }
+    counts_ready_[q] = false;
+    ++xseq_;
+    return 0;
+  }
+
+  // the launched step of parity q will not be exchanged (it packed nothing, or a peer
+  // failed): the next phase B imports nothing
+  void drop_exchange(int q) {
+    counts_ready_[q] = false;
+    lag_recv_.clear();
+    x_wait_ = false;
+  }
+
+  // phase B of the launched step of parity p, importing the last exchange (if any)
+  void launch_b(int p) {
+    if (!b_due_[p]) throw std::runtime_error("launch_b: no phase-A step of this parity");
+    b_due_[p] = false;
+    u32* x = (u32*)buf("xchg" + std::to_string(p)).ptr;
+    const bool have = lag_recv_.size() == 4 * d_.world;
+    for (u32 r = 0; r < d_.world; ++r) {
+      x[XC_RECV_N + r] = have ? lag_recv_[r] : 0;
+      x[XC_RECV_B + r] = have ? lag_recv_[d_.world + r] : 0;
+      x[XC_RECV_AN + r] = have ? lag_recv_[2 * d_.world + r] : 0;
+      x[XC_RECV_AB + r] = have ? lag_recv_[3 * d_.world + r] : 0;
+    }
+    lag_recv_.clear();
+    if (x_wait_ && rccl_) HIPCHECK(hipStreamWaitEvent(s_comp_, rccl_->event(), 0));
+    x_wait_ = false;
+    if (graph_enabled_) {
+      if (!graph_b_[p]) capture_b(p);
+      HIPCHECK(hipGraphLaunch(graph_b_[p], s_comp_));
+    } else {
+      launch_phase_b(s_comp_, io_[p]);
+    }
+    HIPCHECK(hipEventRecord(ev_done_[p], s_comp_));
+  }
+
   // ------------------------------------------------------------- native front end
   // C entry points (step_abi.h) for csrc/core/frontend.cpp: the front end's stepper
   // thread drives submit / wait_results / egress copies directly, without the GIL.  The
@@ -815,6 +1045,21 @@ class Engine {
     a.wblock = (u32*)buf("conn_wblock").ptr;
     a.grow_host = [](void* e, int p) -> const RingMove* { return ((Engine*)e)->io_[p].grow_hh; };
     a.conn_conf = [](void* e, int p) -> const u32* { return ((Engine*)e)->io_[p].conn_conf_hh; };
+    a.world = d_.world;
+    a.rank = d_.my_rank;
+    a.native_xchg = native_x_ ? 1u : 0u;
+    a.exchange = [](void* e, int q, u32 flags, u32* orf) -> int {
+      Engine* E = (Engine*)e;
+      int rc = 0;
+      int g = E->guard([&] { rc = E->exchange(q, flags, orf); return 0; });
+      return g < 0 ? -1 : rc;
+    };
+    a.drop_exchange = [](void* e, int q) -> int {
+      return ((Engine*)e)->guard([&] { ((Engine*)e)->drop_exchange(q); return 0; });
+    };
+    a.launch_b = [](void* e, int p) -> int {
+      return ((Engine*)e)->guard([&] { ((Engine*)e)->launch_b(p); return 0; });
+    };
     for (int p = 0; p < 2; ++p) {
       std::string sfx = std::to_string(p);
       HostIO& h = io_[p];
@@ -851,7 +1096,7 @@ class Engine {
   void wait_results(int p) {
     HostTimer ht(&ht_[3]);
     Range rg("chanamq.step.wait_results");
-    if (phase_a_[p]) throw std::runtime_error("wait_results: phase B of this sharded step not submitted");
+    if (phase_a_[p] || b_due_[p]) throw std::runtime_error("wait_results: phase B of this sharded step not submitted");
     if (staged_[p]) throw std::runtime_error("wait_results: step staged but never launched");
     HIPCHECK(hipEventSynchronize(ev_done_[p]));
     inflight_[p] = false;
@@ -945,10 +1190,10 @@ class Engine {
 
   // seconds spent in each host phase since the last reset
   py::dict host_times(bool reset) {
-    static const char* names[6] = {"submit", "submit_sdma_wait", "submit_graph_launch", "wait_results",
-                                   "egress_copy", "egress_wait"};
+    static const char* names[7] = {"submit", "submit_sdma_wait", "submit_graph_launch", "wait_results",
+                                   "egress_copy", "egress_wait", "exchange"};
     py::dict o;
-    for (int i = 0; i < 6; ++i) { o[names[i]] = ht_[i]; if (reset) ht_[i] = 0; }
+    for (int i = 0; i < 7; ++i) { o[names[i]] = ht_[i]; if (reset) ht_[i] = 0; }
     return o;
   }
 
@@ -1174,6 +1419,20 @@ class Engine {
   std::vector<u32> lag_recv_;
   u64 lag_stream_ = 0;
   bool xfer_set_ = false;
+  // native exchange
+  bool native_x_ = false;
+  bool b_due_[2] = {false, false};   // phase A launched, phase B not yet (native exchange)
+  std::unique_ptr<cmqx::RcclXchg> rccl_;
+  std::unique_ptr<cmqx::ShmXchg> shm_;
+  std::vector<int> xmembers_;
+  int xtimeout_ms_ = 10000;
+  bool xfailover_ = false;
+  bool x_wait_ = false;              // phase B waits on the RCCL bulk transfer
+  u64 xseq_ = 0;
+  u8* xs_desc_[2] = {nullptr, nullptr};
+  u8* xs_pay_[2] = {nullptr, nullptr};
+  u8* xr_desc_[2] = {nullptr, nullptr};
+  u8* xr_pay_[2] = {nullptr, nullptr};
   struct HostIO : DS {   // per-parity device view + host addresses of its mapped outputs
     const Counters* ctr_host_h = nullptr;
     const SegOut* seg_out_hh = nullptr;
@@ -1199,7 +1458,7 @@ class Engine {
   bool sdma_pending_[EGRESS_SLOTS] = {};
   u32 copy_wgs_ = 16;
   int sdma_pref_ = -1;
-  double ht_[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  double ht_[8] = {0, 0, 0, 0, 0, 0, 0, 0};   // host_times() phases
   StepIn* stage_in_[2] = {nullptr, nullptr};
   SegIn* stage_segs_[2] = {nullptr, nullptr};
   hipStream_t s_comp_ = nullptr, s_h2d_ = nullptr, s_d2h_ = nullptr;
@@ -1265,6 +1524,20 @@ PYBIND11_MODULE(_dataplane, m) {
       .def("egress_slot", &Engine::egress_slot)
       .def("sync", &Engine::sync)
       .def("c_api", &Engine::c_api)
+      .def("xchg_setup", &Engine::xchg_setup, py::arg("kind"), py::arg("arg"), py::arg("members"),
+           py::arg("timeout_ms") = 10000, py::arg("failover") = false, py::call_guard<py::gil_scoped_release>())
+      .def_static("xchg_unique_id", &Engine::xchg_unique_id)
+      .def("exchange", [](Engine& e, int q, u32 flags) {
+             u32 orf = 0;
+             int rc;
+             {
+               py::gil_scoped_release nogil;
+               rc = e.exchange(q, flags, &orf);
+             }
+             return py::make_tuple(rc, orf);
+           }, py::arg("parity"), py::arg("flags") = 0)
+      .def("drop_exchange", &Engine::drop_exchange)
+      .def("launch_b", &Engine::launch_b)
       .def("counters", &Engine::counters)
       .def("host_times", &Engine::host_times, py::arg("reset") = false);
 }

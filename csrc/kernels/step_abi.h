@@ -89,7 +89,7 @@ struct ConnOut { u32 off; u32 len; };
 // C entry points of one Engine (engine.hip: Engine::c_api).  All return 0 / a parity on
 // success and -1 on error (message: error()).  Parity p = the double-buffered step IO set
 // of a submitted step; its host-mapped outputs stay valid until the next submit of p.
-#define CMQ_STEP_ABI 2
+#define CMQ_STEP_ABI 3
 struct CmqEngineApi {
   u32 abi;
   u32 c_max, seg_max, carry_cap, persist, persist_max;
@@ -116,5 +116,13 @@ struct CmqEngineApi {
   // u32[c_max]: publisher-confirm bytes in each connection's egress of that step — only
   // those connections wait for the step's persistence commit (null = every connection)
   const u32* (*conn_conf)(void* eng, int p);
+  // ---- sharded broker (world > 1, engine built with native_xchg): submit() launches only
+  // phase A of the step; the front end then calls exchange() for the previous step (count
+  // exchange + bulk move, flags OR-reduced over the live ranks; -2 = a peer failed) and
+  // launch_b() for this one
+  u32 world, rank, native_xchg;
+  int (*exchange)(void* eng, int q, u32 flags, u32* or_flags);
+  int (*drop_exchange)(void* eng, int q);
+  int (*launch_b)(void* eng, int p);
 };
 #define GROW_MAX 4096   // grow requests reported per step
