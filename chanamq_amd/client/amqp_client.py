@@ -125,7 +125,8 @@ class Channel:
         m = Method("basic.publish", exchange=exchange, routing_key=routing_key, mandatory=mandatory,
                    immediate=immediate)
         self.conn._send_raw(render_command(self.number, m, properties or {}, body, self.conn.frame_max))
-        self.published += 1
+        if self.confirm_mode:   # publish sequence numbers start at 1 with Confirm.Select
+            self.published += 1
 
     def basic_get(self, queue, no_ack=False):
         self._send("basic.get", queue=queue, no_ack=no_ack)

@@ -592,6 +592,31 @@ class GpuDataPlane(ControlState):
     def xchg_unique_id(self):
         return self.mod.Engine.xchg_unique_id()
 
+    # ---- remote-consumer links on the device (parallel/links.py DeviceLinks)
+    def set_link_queue(self, slot, owner):
+        """Connection side: consumption of shadow queue ``slot`` acks at rank ``owner``
+        (None: no acks)."""
+        self._up_at("q_link_owner", 0 if owner is None else int(owner) + 1, slot, np.uint32)
+
+    def set_link_conn(self, pc, dest, tq, epoch):
+        """Owner side: pseudo connection ``pc`` ships its deliveries to rank ``dest`` as
+        restore records for shadow slot ``tq``; acks for ``tq`` settle its channel 1."""
+        self._up_at("conn_link", int(dest) + 1, pc, np.uint32)
+        self._up_at("conn_link_tq", tq, pc, np.uint32)
+        self._up_at("conn_link_epoch", epoch, pc, np.uint32)
+        self._up_at("q_link_ch", self.chslot(pc, 1), tq, np.uint32)
+        self._up_at("q_link_epoch", epoch, tq, np.uint32)
+
+    def clear_link_conn(self, pc, tq):
+        self._up_at("conn_link", 0, pc, np.uint32)
+        self._up_at("q_link_ch", 0xFFFFFFFF, tq, np.uint32)
+
+    def set_link_conns(self, conns):
+        a = np.zeros(64, np.uint32)
+        a[:len(conns)] = conns
+        self._up("link_conns", a)
+        self._up_at("n_link_conns", len(conns), 0, np.uint32)
+
     # ---- unbounded queues: the device grows rings (k_ring_plan); the host mirrors it
     def _ring_alloc(self, cap):
         """Rings come from one pool whose bump pointer lives on the device (k_ring_plan
@@ -637,7 +662,9 @@ class GpuDataPlane(ControlState):
             # could route to another rank), phase B
             if len(segs):
                 raise RuntimeError("host-run steps of a sharded node carry no client bytes")
-            p = self.eng.submit(segs, int(payload_ptr), int(payload_len), now, self.step_no, now, self.worker)
+            # SF_NODISPATCH: nothing is delivered or shipped to links (it could not travel)
+            p = self.eng.submit(segs, int(payload_ptr), int(payload_len), now, self.step_no, now, self.worker,
+                                False, 1)
             self.step_no += 1
             self.eng.drop_exchange(p)
             self.eng.launch_b(p)

@@ -13,7 +13,7 @@ from ..protocol import constants as C
 from .comm import Comm
 
 REPLICATED = {"declare_exchange", "delete_exchange", "declare_queue", "delete_queue", "bind", "unbind",
-              "place_queue", "ensure_vhost", "link_open", "link_close", "link_pull"}
+              "place_queue", "ensure_vhost", "link_open", "link_close", "link_pull", "link_got"}
 
 
 class ControlLog:
@@ -35,7 +35,14 @@ class ControlLog:
     def sync(self):
         """All-gather and apply.  Returns {local seq: result} for this rank's ops."""
         from ..engine.control import ControlError
-        got = self.comm.allgather_json(self.outbox)
+        # ops submitted while this batch is applied (e.g. an owner's link_got answer) go
+        # into the next batch
+        batch, self.outbox = self.outbox, []
+        try:
+            got = self.comm.allgather_json(batch)
+        except RuntimeError:
+            self.outbox = batch + self.outbox   # retried after the failover
+            raise
         mine = {}
         for r in sorted(got):
             for seq, (op, args, kw) in enumerate(got[r]):
@@ -48,7 +55,6 @@ class ControlLog:
                 self.applied += 1
                 if r == self.comm.rank:
                     mine[seq] = res
-        self.outbox = []
         return mine
 
     def _apply(self, op, args, kw):

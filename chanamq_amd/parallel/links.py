@@ -51,13 +51,14 @@ _HDR = ">BIIQBBBII"          # kind, link, epoch, tag, redelivered, |ex|, |rk|, 
 
 class Link:
     __slots__ = ("id", "vhost", "queue", "dest", "prefetch", "shadow", "epoch", "pc", "closing", "get",
-                 "pending")
+                 "pending", "slot")
 
     def __init__(self, lid, vhost, queue, dest, prefetch, get=False):
         self.id, self.vhost, self.queue, self.dest, self.prefetch = lid, vhost, queue, dest, prefetch
         self.shadow = LINK_PREFIX + str(lid)
         self.epoch, self.pc, self.closing, self.get = 0, None, False, bool(get)
         self.pending = set()     # connection side of a get link: pulls not answered yet
+        self.slot = None         # shadow queue slot (device links)
 
 
 def parse_delivers(buf):
@@ -386,3 +387,191 @@ class RemoteLinks:
 def _eid(vhost, name):
     from ..engine.control import entity_id
     return entity_id(vhost, name)
+
+
+class DeviceLinks:
+    """Remote consumers on the device (the pipelined sharded server, X2/X3).
+
+    Same link model as ``RemoteLinks`` -- owner-side pseudo connection + consumer on the
+    source queue, connection-side shadow queue holding the owner's deliveries, acks back
+    to the owner -- but the per-message traffic never reaches the host: the owner's
+    ``k_render`` turns the pseudo connection's deliveries into restore records (RDesc,
+    MF_RESTORE into the shadow, redelivered bit, id = epoch << 40 | owner tag) that ride
+    the next per-step exchange with the publishes; the connection side's data plane turns
+    every consumption of a shadow message into an ack record for the owner, whose phase B
+    marks the tag acked in the pseudo channel (``k_link_acks``).  Link open / close run at
+    the control syncs (every rank applies them at the same step, nothing in flight).
+
+    Basic.Get of a remote queue (get link): the owner runs Basic.Get on its pseudo
+    channel at the sync that applies the ``link_pull`` and answers with a replicated
+    ``link_got`` op; the connection side restores the message into the get link's shadow
+    at the next sync.  Reference: FrameStage.scala:395-429 / 1199-1229,
+    QueueEntity.scala:318-446.
+    """
+
+    def __init__(self, plane, alloc_conn, free_conn, submit):
+        self.plane = plane
+        self.links = {}
+        self._alloc, self._free, self._submit = alloc_conn, free_conn, submit
+        self.got = []             # connection side: answered pulls [(pull id, link id, count | None)]
+        self._link_conns = []     # owner side: pseudo connections (device list, <= 64)
+
+    @property
+    def active(self):
+        return bool(self.links)
+
+    def shadow_of(self, lid):
+        lk = self.links.get(lid)
+        return lk.shadow if lk else None
+
+    def before_step(self, now_ms=None):
+        """Device links restore nothing between steps (records arrive with the exchange)."""
+
+    def take_gets(self):
+        out, self.got = self.got, []
+        return out
+
+    def _sync_conns(self):
+        self.plane.set_link_conns(self._link_conns)
+
+    # ------------------------------------------------------------------ replicated ops
+    def open(self, lid, vhost, queue, dest, prefetch=0, get=False):
+        p = self.plane
+        q = p.queues.get((vhost, queue))
+        if q is None:
+            raise ControlError(C.NOT_FOUND, f"no queue '{queue}' in vhost '{vhost}'", 60, 20)
+        if len(self._link_conns) >= 64 and q.owner == p.rank:
+            raise ControlError(C.RESOURCE_ERROR, "too many remote-consumer links on this rank", 60, 20)
+        lk = Link(lid, vhost, queue, dest, int(prefetch) or 1024, get)
+        p.shard_map.place(vhost, lk.shadow, dest)
+        slot = p.declare_queue(vhost, lk.shadow)
+        lk.slot = slot
+        self.links[lid] = lk
+        if dest == p.rank:
+            p.set_link_queue(slot, q.owner)   # consumption here -> acks to the owner
+        if q.owner == p.rank:
+            self._attach(lk)
+        return slot
+
+    def _attach(self, lk):
+        p = self.plane
+        pc = self._alloc()
+        p.open_connection(pc, lk.vhost)
+        p.open_channel(pc, 1)
+        if not lk.get:
+            p.qos(pc, 1, prefetch_count=lk.prefetch)
+            p.consume(pc, 1, lk.vhost, lk.queue, "amq.link-" + str(lk.id), no_ack=False)
+        lk.pc, lk.epoch = pc, lk.epoch + 1
+        p.set_link_conn(pc, lk.dest, lk.slot, lk.epoch)
+        self._link_conns.append(pc)
+        self._sync_conns()
+
+    def _detach(self, lk):
+        """Owner side: the pseudo channel closes -- what the remote consumer still held goes
+        back to the queue, redelivered (its requeue settles in the next step)."""
+        p = self.plane
+        if lk.pc is not None:
+            p.clear_link_conn(lk.pc, lk.slot)
+            if lk.pc in self._link_conns:
+                self._link_conns.remove(lk.pc)
+            self._sync_conns()
+            p.close_connection(lk.pc)
+            p.step({})            # settle the requeue before the slot can be reused
+            self._free(lk.pc)
+            lk.pc = None
+
+    def _drop_shadow(self, lk):
+        p = self.plane
+        sq = p.queues.get((lk.vhost, lk.shadow))
+        if sq is not None:
+            if sq.owner == p.rank:
+                p.set_link_queue(sq.slot, None)
+                left = p.purge(sq.slot)
+                while left:   # release the purged entries (no acks any more)
+                    p.step({})
+                    now = p.message_count(sq.slot)
+                    if now >= left:
+                        break
+                    left = now
+            p.delete_queue(lk.vhost, lk.shadow)
+        p.shard_map.placement.pop(_eid(lk.vhost, lk.shadow), None)
+
+    def close(self, lid):
+        lk = self.links.pop(lid, None)
+        if lk is None:
+            return None
+        lk.closing = True
+        self._detach(lk)
+        self._drop_shadow(lk)
+        for pn in sorted(lk.pending):   # unanswered Gets of a closed get link: empty
+            self.got.append((pn, lk.id, None))
+        return None
+
+    def pull(self, lid, pn, now_ms=None):
+        lk = self.links.get(lid)
+        if lk is None or lk.closing or not lk.get:
+            return False
+        p = self.plane
+        if lk.dest == p.rank:
+            lk.pending.add(pn)
+        if lk.pc is None:
+            return True
+        q = p.queues.get((lk.vhost, lk.queue))
+        frames, cnt = None, 0
+        if q is not None and q.owner == p.rank:
+            try:
+                frames, cnt = p.basic_get(lk.pc, 1, q.slot, False)
+            except ControlError:   # the pseudo channel's window is full
+                frames = None
+        if frames is None:
+            self._submit("link_got", lid, pn, None)
+        else:
+            tag, red, ex, rk, props, body, cnt = parse_get_ok(frames)
+            self._submit("link_got", lid, pn, [cnt, lk.epoch, tag, int(red), ex.hex(), rk.hex(), props.hex(),
+                                               body.hex()])
+        return True
+
+    def got_answer(self, lid, pn, ans):
+        """Replicated ``link_got``: the connection side restores the message into the get
+        link's shadow queue (at this sync point) and records the answer."""
+        lk = self.links.get(lid)
+        p = self.plane
+        if lk is None or lk.dest != p.rank:
+            return None
+        lk.pending.discard(pn)
+        sq = p.queues.get((lk.vhost, lk.shadow))
+        if ans is None or sq is None:
+            self.got.append((pn, lid, None))
+            return None
+        cnt, epoch, tag, red, ex, rk, props, body = ans
+        p.restore([(sq.slot, (int(epoch) << _EPOCH_SHIFT) | int(tag), 0, 0, bytes.fromhex(ex), bytes.fromhex(rk),
+                    bytes.fromhex(props), bytes.fromhex(body), False, bool(red))])
+        self.got.append((pn, lid, int(cnt)))
+        return None
+
+    # ------------------------------------------------------------------ failover
+    def on_failure(self, dead):
+        p = self.plane
+        for lk in list(self.links.values()):
+            q = p.queues.get((lk.vhost, lk.queue))
+            if lk.get and lk.pending and q is not None and q.owner in dead:
+                for pn in sorted(lk.pending):
+                    self.got.append((pn, lk.id, None))
+                lk.pending.clear()
+            if lk.dest in dead:   # the consumer side is gone: the owner requeues what it held
+                self.links.pop(lk.id)
+                self._detach(lk)
+                self._drop_shadow(lk)
+
+    def after_rehome(self):
+        """Links whose queue moved here re-attach (a new epoch: acks of deliveries made by
+        the dead owner are ignored); connection sides point their acks at the new owner."""
+        p = self.plane
+        for lk in self.links.values():
+            q = p.queues.get((lk.vhost, lk.queue))
+            if q is None:
+                continue
+            if lk.dest == p.rank:
+                p.set_link_queue(lk.slot, q.owner)
+            if q.owner == p.rank and lk.pc is None and not lk.closing:
+                self._attach(lk)

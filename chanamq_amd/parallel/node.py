@@ -59,6 +59,16 @@ class ShardedNode:
         return seq
 
     # ------------------------------------------------------------------ pipelined server
+    def use_device_links(self, alloc_conn, free_conn):
+        """Remote consumers through the data plane (X2/X3 records in the exchange) instead
+        of the host relay: the pipelined server has no per-step host collective."""
+        from .links import DeviceLinks
+        self.links = DeviceLinks(self.plane, alloc_conn, free_conn, self.submit)
+        self.log.handlers["link_open"] = self.links.open
+        self.log.handlers["link_close"] = self.links.close
+        self.log.handlers["link_pull"] = self.links.pull
+        self.log.handlers["link_got"] = self.links.got_answer
+
     def attach_frontend(self, fe, stuck_s=5.0):
         """The native front end steps this rank (frontend.cpp stepper_sharded): control
         ops sync at its FE_SYNC points, failovers run at FE_XFAIL, and this rank's

@@ -214,8 +214,11 @@ class GpuBroker:
             if self.node is not None:
                 # sharded: lockstep steps with the native exchange; control-log syncs and
                 # failovers happen at FE_SYNC / FE_XFAIL; the failure detector's heartbeat
-                # is gated on this rank's step progress
+                # is gated on this rank's step progress; remote consumers ride the device
+                # exchange (DeviceLinks) when the engine has links
                 self.node.attach_frontend(self.fe)
+                if self.plane.info.get("links"):
+                    self.node.use_device_links(self._alloc_link_slot, self._link_free.append)
                 if self.persistence is not None:
                     self.node.log.on_applied = self._persist_replicated
             self._running = True
@@ -392,6 +395,8 @@ class GpuBroker:
             if failed:
                 node.failover_point()
             self._answer(node.sync_point())
+            if self._get_wait or self._get_links:   # remote Basic.Get answers restored at this sync
+                self._serve_gets()
             if self.persistence is not None:
                 self.persistence.control_commit()
         finally:

@@ -70,7 +70,7 @@ def main(argv=None):
         plane = GpuDataPlane(device=torch.cuda.current_device(), worker=rank, cons_max=4096, seg_max=args.c_max,
                              cmd_max=1 << 16, deliv_max=1 << 16, msg_max=1 << 20, ingress_cap=32 << 20,
                              egress_cap=64 << 20, log_bytes=2 << 30, tb_max=1024, persist=1,
-                             native_xchg=int(pipeline), **plane_kw)   # persist: store rows
+                             native_xchg=int(pipeline), links=int(pipeline), **plane_kw)   # persist: store rows
     else:
         from ..engine.golden import GoldenDataPlane
         plane = GoldenDataPlane(persist=bool(args.store_dir), **plane_kw)
@@ -115,18 +115,25 @@ def main(argv=None):
                                    upstream_port=broker.port, cert=args.tls_cert, key=args.tls_key, p12="",
                                    p12_password=""))
         tls.start()
-    if args.info_dir:
+    def write_info():
+        if not args.info_dir:
+            return
         # written then renamed: a watcher polling for the file never reads it half-written
         path = os.path.join(args.info_dir, f"rank{rank}.json")
+        fes = getattr(broker, "_fe_stats", None) or {}
         with open(path + ".tmp", "w") as f:
             json.dump({"rank": rank, "world": world, "port": broker.port,
-                       "tls_port": tls.port if tls is not None else None, "io": broker.io}, f)
+                       "tls_port": tls.port if tls is not None else None, "io": broker.io,
+                       "stats": dict(broker.stats), "failovers": len(node.failovers),
+                       "front_end": {k: v for k, v in fes.items() if k != "lat_hist"}}, f)
         os.replace(path + ".tmp", path)
+    write_info()
     stop = threading.Event()
     for sig in (signal.SIGINT, signal.SIGTERM):
         signal.signal(sig, lambda *a: stop.set())
     rc = 0
     while not stop.wait(0.5):
+        write_info()
         if not broker._running:   # the engine failed: leave, the peers fail this rank over
             rc = 3
             break

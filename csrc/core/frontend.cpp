@@ -1167,28 +1167,36 @@ void Frontend::stepper_sharded() {
       if (segs.empty() && !local_busy) stats_.idle_steps++;
     }
     if (!xfail && (orf & XF_SYNC)) {
-      // ---- flush: an empty step imports this step's exchange; nothing stays pending
-      if (inflight.size() >= 2) finish_oldest(inflight);
-      if (failed_) break;
-      int p2;
-      {
-        GpuWait gw(gpu_wait_since_);
-        p2 = api_->submit(api_->eng, nullptr, 0, arena_[arena_i_], 0, wall_ms(), cfg_.worker);
+      // ---- flush: empty no-dispatch steps import the pending exchange (and, with device
+      // links, the link records / acks that travel one exchange later); nothing stays
+      // pending, so the control plane may change replicated tables
+      const int nflush = api_->links ? 2 : 1;
+      bool bad = false;
+      for (int k = 0; k < nflush && !xfail; ++k) {
+        if (inflight.size() >= 2) finish_oldest(inflight);
+        if (failed_) { bad = true; break; }
+        int p2;
+        {
+          GpuWait gw(gpu_wait_since_);
+          p2 = api_->flush_submit ? api_->flush_submit(api_->eng, wall_ms(), cfg_.worker)
+                                  : api_->submit(api_->eng, nullptr, 0, arena_[arena_i_], 0, wall_ms(), cfg_.worker);
+        }
+        if (!check(p2)) { bad = true; break; }
+        u32 dummy = 0;
+        int rc = api_->exchange(api_->eng, xpend_, 0, &dummy);
+        if (rc == -1) { check(-1); bad = true; break; }
+        if (rc == -2) { xfail = true; if (!check(api_->drop_exchange(api_->eng, xpend_))) { bad = true; break; } }
+        if (!check(api_->launch_b(api_->eng, p2))) { bad = true; break; }
+        Inflight f2;
+        f2.p = p2;
+        f2.step = ++step_no_;
+        f2.gen.resize(c_max_);
+        for (u32 j = 0; j < c_max_; ++j) f2.gen[j] = conns_[j]->gen.load();
+        inflight.push_back(std::move(f2));
+        xpend_ = p2;
       }
-      if (!check(p2)) break;
-      arena_i_ = (arena_i_ + 1) % 3;
-      u32 dummy = 0;
-      int rc = api_->exchange(api_->eng, xpend_, 0, &dummy);
-      if (rc == -1) { check(-1); break; }
-      if (rc == -2) { xfail = true; if (!check(api_->drop_exchange(api_->eng, xpend_))) break; }
-      if (!check(api_->launch_b(api_->eng, p2))) break;
-      Inflight f2;
-      f2.p = p2;
-      f2.step = ++step_no_;
-      f2.gen.resize(c_max_);
-      for (u32 k = 0; k < c_max_; ++k) f2.gen[k] = conns_[k]->gen.load();
-      inflight.push_back(std::move(f2));
-      if (!check(api_->drop_exchange(api_->eng, p2))) break;   // it packed nothing
+      if (bad) break;
+      if (xpend_ >= 0 && !check(api_->drop_exchange(api_->eng, xpend_))) break;   // packed nothing
       xpend_ = -1;
       {
         std::lock_guard<std::mutex> g(stats_mu_);
@@ -1500,6 +1508,8 @@ EchoEngine::EchoEngine(u32 c_max, u32 seg_max, u64 ingress_cap, u32 carry_cap, u
     return 0;
   };
   api_.launch_b = [](void* e, int p) -> int { ((EchoEngine*)e)->launch_b(p); return 0; };
+  api_.links = 0;
+  api_.flush_submit = nullptr;
 }
 
 void EchoEngine::unpause(u32 conn) {

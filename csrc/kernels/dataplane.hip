@@ -324,6 +324,8 @@ __global__ __launch_bounds__(256) void k_stage(DS d) {
       if (k * 4 < offsetof(Counters, log_head)) c[k] = 0;
     if (tid == 0) {
       d.ctr->n_grow = 0; d.tot[TS_NMOVE] = 0; d.tot[TS_NDEFER] = 0; d.tot[TS_TTL_BUDGET] = 0;
+      if (d.links)
+        for (u32 r = 0; r < WORLD_MAX; ++r) d.lk_cnt[r] = 0;
       *d.egress_budget = 0;
       // snowflake virtual position base for this step (ID_SLOT_BITS slots per wall-clock ms)
       u64 floor_pos = d.in->id_ms << ID_SLOT_BITS;
@@ -2017,7 +2019,13 @@ __global__ void k_import_prep(DS d) {
     psum += d.xchg[XC_RECV_B + r];
   }
   u32 base = 0;   // imported bytes stay in the receive buffer (pub_src)
-  bool fits = dsum <= d.import_max && psum <= d.xfer_bytes;
+  bool fits = dsum <= d.import_max && psum <= d.import_bytes;
+  if (d.links) {
+    u32 nk = 0;
+    for (u32 r = 0; r < d.world; ++r) nk += d.xchg[XC_RACK_N + r];
+    const u32 kcap = (d.world - 1) * d.lk_cap;
+    d.tot[TS_NRACK] = nk < kcap ? nk : kcap;
+  }
   u32 ni = fits ? dsum : 0;
   if (!fits) d.ctr->n_dropped_nomem += dsum;
   d.tot[TS_NIMPORT] = ni;
@@ -2209,6 +2217,20 @@ __global__ void k_enqueue(DS d, u32 src, u32 hs_ntiles) {
 // a persistent message changed state in a durable queue: record it for the store
 // (kind 0 consumed/acked, 1 expired, 2 dropped, 3 delivered awaiting ack, 4 requeued)
 DEV void wave_consumed(const DS& d, u32 msg, u32 q, u64 qpos, u32 kind, bool valid) {
+  // X3: a shadow message left its queue (consumed, expired, dropped): ack it at the owner
+  if (d.links && valid && msg != INVALID && kind <= 2u) {
+    const u32 ow = d.q_link_owner[q];
+    if (ow) {
+      const u32 k = atomicAdd(&d.lk_cnt[ow - 1], 1u);
+      if (k < d.lk_cap) {
+        AckRec a;
+        a.tq = q;
+        a.pad = 0;
+        a.xid = d.msgs[msg].msg_id;
+        d.lk_send[(u64)(ow - 1) * d.lk_cap + k] = a;
+      }
+    }
+  }
   if (!d.persist) return;
   bool want = valid && msg != INVALID && d.q_durable[q] && (d.msgs[msg].flags & MF_PERSIST);
   u32 k = wave_reserve(&d.ctr->n_consumed, want);
@@ -2367,6 +2389,8 @@ DEV void chan_advance_one(const DS& d, u32 ch, u32 tid, u32 lane, u32 w, u32* s_
 
 // ============================================================================ K8 dequeue
 DEV u32 deliver_size(const DS& d, u32 cons, const MsgEnt& m, u32 conn) {
+  // a link pseudo-connection ships [ex][rk][props][body] as a restore record (render_deliv)
+  if (d.links && d.conn_link[conn]) return align16(m.ex_len + m.rk_len + m.props_len + m.body_len);
   u32 mp = 4 + 1 + d.cons_tag_len[cons] + 8 + 1 + 1 + m.ex_len + 1 + m.rk_len;
   u32 sz = 8 + mp + 8 + 12 + m.props_len;
   u32 fm = d.conn_frame_max[conn];
@@ -2395,6 +2419,11 @@ __global__ __launch_bounds__(256) void k_dequeue(DS d) {
   const u32 q = blockIdx.x, tid = threadIdx.x, lane = lane_id();
   if (q >= d.q_max) return;
   if (!d.q_active[q]) {
+    if (tid == 0) d.q_nruns[q] = 0;
+    return;
+  }
+  const bool nodisp = (d.in->flags & SF_NODISPATCH) != 0;
+  if (nodisp && d.links && d.q_link_owner[q]) {   // a live link shadow: its acks could not travel
     if (tid == 0) d.q_nruns[q] = 0;
     return;
   }
@@ -2435,7 +2464,7 @@ __global__ __launch_bounds__(256) void k_dequeue(DS d) {
   head = s_head;
   const u32 mall = d.q_cons_n[q];
   const u64 avail = tail - head;
-  if (mall == 0 || avail == 0) {
+  if (mall == 0 || avail == 0 || nodisp) {
     if (tid == 0) { d.q_head[q] = head; d.q_nruns[q] = 0; }
     return;
   }
@@ -2763,10 +2792,10 @@ __global__ __launch_bounds__(1024) void k_conn_layout(DS d) {
     if (c < d.c_max) {
       ConnOut o;
       o.off = run + off;
-      o.len = total;
+      o.len = d.links && d.conn_link[c] ? 0u : total;   // links: their bytes go to lsend_*
       d.conn_base[c] = o.off;
       d.conn_out[c] = o;
-      if (c == d.c_max - 1) d.ctr->egress_bytes = o.off + o.len;
+      if (c == d.c_max - 1) d.ctr->egress_bytes = o.off + total;
     }
     run += all;
   }
@@ -2777,9 +2806,68 @@ __global__ void k_conn_out(DS d) {
   if (c >= d.c_max) return;
   ConnOut o;
   o.off = d.conn_base[c];
-  o.len = d.conn_total[c];
+  o.len = d.links && d.conn_link[c] ? 0u : d.conn_total[c];
   d.conn_out[c] = o;
-  if (c == d.c_max - 1) d.ctr->egress_bytes = o.off + o.len;
+  if (c == d.c_max - 1) d.ctr->egress_bytes = o.off + d.conn_total[c];
+}
+
+// ============================================================================ links (X2/X3)
+// one wave: record / payload bases of every link pseudo-connection's deliveries in this
+// parity's link send buffers, destination-major (the host reads the per-destination
+// totals from xchg and sends each destination's region to it in the next exchange)
+__global__ __launch_bounds__(64) void k_link_bases(DS d) {
+  const u32 lane = threadIdx.x;
+  const u32 nl = *d.n_link_conns;
+  u32 c = INVALID, dest = INVALID, n = 0, b = 0;
+  if (lane < nl && lane < 64) {
+    c = d.link_conns[lane];
+    const u32 lk = d.conn_link[c];
+    const u32 f = d.conn_dfirst[c];
+    if (lk) {
+      dest = lk - 1;
+      if (f != INVALID) { n = d.conn_dlast[c] - f + 1; b = d.conn_total[c]; }
+    }
+  }
+  u32 npre = 0, bpre = 0, tn = 0, tb = 0;
+  for (u32 j = 0; j < 64; ++j) {
+    const u32 dj = __shfl(dest, j, 64), nj = __shfl(n, j, 64), bj = __shfl(b, j, 64);
+    if (j < lane && dj == dest) { npre += nj; bpre += bj; }
+    if (dj == lane) { tn += nj; tb += bj; }
+  }
+  u32 basen = 0, baseb = 0;
+  for (u32 r = 0; r < 64; ++r) {
+    const u32 x = __shfl(tn, r, 64), y = __shfl(tb, r, 64);
+    if (r < lane) { basen += x; baseb += y; }
+  }
+  if (lane < d.world) {
+    d.link_dbase[lane] = baseb;
+    d.xchg[XC_LINK_N + lane] = tn;
+    d.xchg[XC_LINK_B + lane] = tb;
+  }
+  const u32 sl = dest < 64 ? dest : 0;
+  const u32 dbn = __shfl(basen, sl, 64);
+  if (c != INVALID) {
+    d.link_nbase[c] = dbn + npre;
+    d.link_bbase[c] = bpre;
+  }
+}
+
+// owner side, phase B: acks the connection sides sent for the link pseudo channels
+// (the device form of Basic.Ack on the owner's pseudo channel; k_chan_advance settles)
+__global__ __launch_bounds__(256) void k_link_acks(DS d) {
+  const u32 n = d.tot[TS_NRACK];
+  for (u32 i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const AckRec a = d.rack[i];
+    if (a.tq >= d.q_max) continue;
+    const u32 ch = d.q_link_ch[a.tq];
+    if (ch == INVALID || (u32)(a.xid >> 40) != d.q_link_epoch[a.tq]) continue;
+    const u64 tag = a.xid & ((1ull << 40) - 1);
+    if (tag < d.ch_uhead[ch] || tag >= d.ch_next_tag[ch]) continue;
+    USlot* u = &d.uwin[(u64)ch * (d.ucap_mask + 1) + ((tag - 1) & d.ucap_mask)];
+    if (atomicCAS(&u->state, (u32)US_PENDING, (u32)US_ACKED) == US_PENDING &&
+        atomicExch(&d.ch_dirty[ch], 1u) == 0)
+      d.dirty_list[atomicAdd(d.n_dirty, 1u)] = ch;
+  }
 }
 
 // ============================================================================ K5 render
@@ -2802,11 +2890,35 @@ DEV void render_deliv(const DS& d, u32 blk) {
   const MsgEnt m = d.msgs[dv.msg];
   u32 conn = ch / d.chpc;
   u32 f = d.conn_dfirst[conn];
+  const u8* slot = d.log + (m.log_off % d.log_bytes);
+  if (d.links && d.conn_link[conn]) {   // X2: a restore record for the shadow queue
+    const u32 dest = d.conn_link[conn] - 1;
+    const u32 po = d.link_bbase[conn] + (d.dv_off[i] - d.dv_off[f]);
+    u8* lo = d.lsend_pay + (u64)d.link_dbase[dest] + po;
+    const u32 meta = m.ex_len + m.rk_len + m.props_len;
+    wave_copy(lo, slot, meta);
+    wave_copy(lo + meta, slot + m.body_off, m.body_len);
+    if (lane == 0) {
+      RDesc rd{};
+      rd.pay_off = po;
+      rd.body_len = m.body_len;
+      rd.props_len = m.props_len;
+      rd.exch = -1;
+      rd.flags = MF_RESTORE | ((dv.flags & 1) ? MF_REDELIVERED : 0u);
+      rd.ex_len = m.ex_len;
+      rd.rk_len = m.rk_len;
+      rd.expire_ms = dv.expire_ms;
+      rd.ts_ms = m.ts_ms;
+      rd.xid = ((u64)d.conn_link_epoch[conn] << 40) | (dv.tag & ((1ull << 40) - 1));
+      rd.tq = d.conn_link_tq[conn];
+      d.lsend_desc[d.link_nbase[conn] + (i - f)] = rd;
+    }
+    return;
+  }
   u64 off = (u64)d.conn_base[conn] + d.conn_ret_bytes[conn] + d.conn_conf_bytes[conn] + d.dv_off[i] -
             d.dv_off[f];
   if (off + dv.size > d.egress_cap) return;  // never: dequeue reserves an egress byte budget
   u8* o = (u8*)d.in->egress + off;
-  const u8* slot = d.log + (m.log_off % d.log_bytes);
   u32 chno = d.ch_num[ch];
   u32 taglen = d.cons_tag_len[dv.cons];
   u32 mp = 4 + 1 + taglen + 8 + 1 + 1 + m.ex_len + 1 + m.rk_len;
@@ -3007,6 +3119,8 @@ DEV void final_step(const DS& d) {
   c->msg_free_top = *d.msg_free_top;
   c->n_live_msgs = d.msg_max - *d.msg_free_top;
   c->live_bytes = *d.live_bytes;
+  if (d.links)
+    for (u32 r = 0; r < d.world; ++r) d.xchg[XC_ACK_N + r] = d.lk_cnt[r] < d.lk_cap ? d.lk_cnt[r] : d.lk_cap;
   *d.ctr_host = *c;
 }
 

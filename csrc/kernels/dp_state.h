@@ -44,7 +44,18 @@ enum : u32 {
   TS_NDEFER = 31,                       // stored messages released at the end of the step
   TS_RP_TICKET = 14,                    // k_ring_plan finished-block ticket (last block: ring moves)
   TS_XSCAN = 32,                        // + 2*r: per-destination record / byte totals
-  TS_TTL_BUDGET = 64                    // durable TTL-skip records reserved this step (k_dequeue)
+  TS_TTL_BUDGET = 64,                   // durable TTL-skip records reserved this step (k_dequeue)
+  TS_NRACK = 65                         // link acks received this step (k_import_prep -> k_link_acks)
+};
+
+// remote-consumer link ack (X3): the connection side consumed message `xid` (owner's
+// epoch << 40 | owner's delivery tag) of shadow queue `tq`
+struct AckRec { u32 tq; u32 pad; u64 xid; };
+
+// StepIn.flags
+enum : u32 {
+  SF_NODISPATCH = 1   // flush / host step of a sharded node: no grants (nothing rendered or
+                      // shipped to links), no TTL skip on live link shadows
 };
 
 struct DS {
@@ -256,4 +267,29 @@ struct DS {
   u32* ps_off;
   u8* persist_h;            // host-mapped [persist_bytes]
   ConsumedRec* crec_h;      // host-mapped [persist_max]
+
+  // ---------------- remote-consumer links (X2/X3; links == 0: unused).  Owner side: a
+  // link pseudo-connection's deliveries are not rendered as frames but shipped as restore
+  // records (RDesc, MF_RESTORE into the shadow queue, xid = epoch << 40 | tag) in the
+  // next exchange; connection side: consumption of a shadow message sends an AckRec back
+  // to the owner, whose phase B marks the tag acked in the pseudo channel's window
+  u32 links;
+  u64 import_bytes;         // receive payload capacity (publishes + link deliveries)
+  u32* conn_link;           // [c_max] dest rank + 1 of a link pseudo-connection (0: a client)
+  u32* conn_link_tq;        // [c_max] its shadow queue slot (replicated: same slot on every rank)
+  u32* conn_link_epoch;     // [c_max]
+  u32* link_conns;          // [64] link pseudo-connections of this rank
+  u32* n_link_conns;        // [1]
+  u32* link_nbase;          // [c_max] first record of the connection's deliveries in lsend_desc
+  u32* link_bbase;          // [c_max] payload offset of its deliveries in its destination region
+  u32* link_dbase;          // [WORLD_MAX] payload region base of each destination in lsend_pay
+  u32* q_link_owner;        // [q_max] connection side: owner rank + 1 of a shadow queue
+  u32* q_link_ch;           // [q_max] owner side: pseudo channel slot of the link of shadow q
+  u32* q_link_epoch;        // [q_max] owner side: its epoch
+  RDesc* lsend_desc;        // [deliv_max] this parity's link records (destination-major)
+  u8* lsend_pay;            // [egress_cap]
+  AckRec* lk_send;          // [WORLD_MAX][lk_cap] acks per owner rank
+  u32 lk_cap;
+  u32* lk_cnt;              // [WORLD_MAX] acks packed this step
+  const AckRec* rack;       // acks received for this step (contiguous, all sources)
 };

@@ -101,6 +101,13 @@ class Engine {
     }
     d_.pair_max = (u32)get("pair_max", d_.cmd_max * 4);
     d_.deliv_max = (u32)get("deliv_max", 65536);
+    // remote-consumer links (X2/X3) on the native exchange: a peer's link deliveries (at
+    // most its deliv_max per step) arrive with its publishes and are imported with them
+    links_ = d_.world > 1 && get("native_xchg", 0) != 0 && get("links", 0) != 0;
+    if (links_) {
+      d_.import_max += (d_.world - 1) * d_.deliv_max;
+      d_.pub_cap = ((d_.pub_max + d_.import_max + 63) / 64) * 64;
+    }
     d_.msg_max = (u32)get("msg_max", 1u << 22);
     u32 ucap = next_pow2((u32)get("ucap", 8192));
     d_.ucap_mask = ucap - 1;
@@ -132,6 +139,11 @@ class Engine {
     if (d_.work_cap + d_.xfer_bytes + 8192 > (4ull << 30))
       throw std::runtime_error("work buffer + imported bytes must stay below 4 GiB (u32 offsets): lower ingress_cap");
     d_.egress_cap = get("egress_cap", 96ull << 20);
+    // receive payload: the peers' publishes + (links) their link deliveries, each bounded
+    // by the sender's egress budget
+    d_.import_bytes = d_.xfer_bytes + (links_ ? (u64)(d_.world - 1) * d_.egress_cap : 0);
+    if (d_.import_bytes + 8192 > (4ull << 30))
+      throw std::runtime_error("import buffer must stay below 4 GiB (u32 offsets): lower ingress_cap / egress_cap");
     d_.ctrl_cap = get("ctrl_cap", 4ull << 20);
     d_.ring_pool = get("ring_pool", 1ull << 26);
     u32 fan_max = (u32)get("fan_max", 1u << 20);
@@ -419,7 +431,7 @@ class Engine {
         xs_desc_[p] = (u8*)dev(("xs_desc" + sfx).c_str(), 64ull * d_.xfer_desc_max + 64);
         xs_pay_[p] = (u8*)dev(("xs_pay" + sfx).c_str(), d_.xfer_bytes + 64);
         xr_desc_[p] = (u8*)dev(("xr_desc" + sfx).c_str(), 64ull * d_.import_max + 64);
-        xr_pay_[p] = (u8*)dev(("xr_pay" + sfx).c_str(), d_.xfer_bytes + 64);
+        xr_pay_[p] = (u8*)dev(("xr_pay" + sfx).c_str(), d_.import_bytes + 64);
       }
       for (int p = 0; p < 2; ++p) {   // parity p packs into S[p], imports R[p^1]
         io_[p].send_desc = (RDesc*)xs_desc_[p]; io_[p].send_pay = xs_pay_[p];
@@ -427,6 +439,42 @@ class Engine {
       }
       xfer_set_ = true;
     }
+    if (links_) {
+      DS& L = d_;
+      L.links = 1;
+      L.lk_cap = (u32)get("link_acks", 2ull * d_.deliv_max);
+      L.conn_link = (u32*)dev("conn_link", 4ull * d_.c_max);
+      L.conn_link_tq = (u32*)dev("conn_link_tq", 4ull * d_.c_max);
+      L.conn_link_epoch = (u32*)dev("conn_link_epoch", 4ull * d_.c_max);
+      L.link_conns = (u32*)dev("link_conns", 4ull * 64);
+      L.n_link_conns = (u32*)dev("n_link_conns", 4);
+      L.link_nbase = (u32*)dev("link_nbase", 4ull * d_.c_max);
+      L.link_bbase = (u32*)dev("link_bbase", 4ull * d_.c_max);
+      L.link_dbase = (u32*)dev("link_dbase", 4ull * WORLD_MAX);
+      L.q_link_owner = (u32*)dev("q_link_owner", 4ull * d_.q_max);
+      L.q_link_ch = (u32*)dev("q_link_ch", 4ull * d_.q_max);
+      L.q_link_epoch = (u32*)dev("q_link_epoch", 4ull * d_.q_max);
+      L.lk_cnt = (u32*)dev("lk_cnt", 4ull * WORLD_MAX);
+      fill("q_link_ch", 0xff);
+      for (int p = 0; p < 2; ++p) {
+        std::string sfx = std::to_string(p);
+        ls_desc_[p] = (u8*)dev(("ls_desc" + sfx).c_str(), 64ull * d_.deliv_max + 64);
+        ls_pay_[p] = (u8*)dev(("ls_pay" + sfx).c_str(), d_.egress_cap + 64);
+        lk_send_[p] = (u8*)dev(("lk_send" + sfx).c_str(), 16ull * d_.world * L.lk_cap + 64);
+        rack_[p] = (u8*)dev(("rack" + sfx).c_str(), 16ull * d_.world * L.lk_cap + 64);
+      }
+      for (int p = 0; p < 2; ++p) {
+        DS& io = io_[p];
+        io.links = 1; io.lk_cap = L.lk_cap;
+        io.conn_link = L.conn_link; io.conn_link_tq = L.conn_link_tq; io.conn_link_epoch = L.conn_link_epoch;
+        io.link_conns = L.link_conns; io.n_link_conns = L.n_link_conns; io.link_nbase = L.link_nbase;
+        io.link_bbase = L.link_bbase; io.link_dbase = L.link_dbase; io.q_link_owner = L.q_link_owner;
+        io.q_link_ch = L.q_link_ch; io.q_link_epoch = L.q_link_epoch; io.lk_cnt = L.lk_cnt;
+        io.lsend_desc = (RDesc*)ls_desc_[p]; io.lsend_pay = ls_pay_[p]; io.lk_send = (AckRec*)lk_send_[p];
+        io.rack = (const AckRec*)rack_[p ^ 1];   // the acks of the exchange this parity imports
+      }
+    }
+    for (int p = 0; p < 2; ++p) io_[p].import_bytes = d_.import_bytes;
     if (copy_mode_ == 3) init_sdma();
     HIPCHECK(hipStreamCreateWithFlags(&s_comp_, hipStreamNonBlocking));
     HIPCHECK(hipStreamCreateWithFlags(&s_h2d_, hipStreamNonBlocking));
@@ -560,6 +608,8 @@ class Engine {
     o["carry_budget"] = carry_budget_;
     o["exchange_lag"] = lag_ ? 1 : 0;
     o["native_xchg"] = native_x_ ? 1 : 0;
+    o["links"] = links_ ? 1 : 0;
+    o["import_bytes"] = d_.import_bytes;
     o["world"] = d_.world; o["rank"] = d_.my_rank; o["import_max"] = d_.import_max; o["pub_cap"] = d_.pub_cap;
     o["copy_engine"] = copy_mode_ == 3 ? "hsa-sdma" : copy_mode_ == 2 ? "kernel" : (sdma_ ? "nocu" : "blit");
     o["copy_wgs"] = copy_wgs_;
@@ -587,17 +637,17 @@ class Engine {
   // sharded driver uses the gap to run the previous step's exchange while this step's
   // bytes cross PCIe (the host waits on phase A of t-1, not on H2D(t) + phase A(t))
   int submit(py::buffer segs, u64 payload_ptr, u64 payload_len, i64 now_ms, u64 step, u64 id_ms,
-             u32 worker, bool defer) {
+             u32 worker, bool defer, u32 flags) {
     py::buffer_info si = segs.request();
     size_t sb = (size_t)si.size * si.itemsize;
     return submit_raw((const SegIn*)si.ptr, (u32)(sb / sizeof(SegIn)), payload_ptr, payload_len, now_ms, id_ms,
-                      worker, defer);
+                      worker, defer, flags);
   }
 
   // step numbers are the engine's own submit sequence (latency histogram, message
   // publish step): identical whether Python or the native front end drives the steps
   int submit_raw(const SegIn* segp, u32 nseg, u64 payload_ptr, u64 payload_len, i64 now_ms, u64 id_ms,
-                 u32 worker, bool defer = false) {
+                 u32 worker, bool defer = false, u32 sflags = 0) {
     HostTimer ht(&ht_[0]);
     Range rg("chanamq.step.submit");
     const size_t sb = (size_t)nseg * sizeof(SegIn);
@@ -610,6 +660,7 @@ class Engine {
     StepIn* in = stage_in_[p];
     *in = StepIn{};
     in->nseg = nseg;
+    in->flags = sflags;
     in->now_ms = now_ms;
     in->step = step;
     in->id_ms = id_ms;
@@ -753,6 +804,7 @@ class Engine {
     HIPCHECK(hipMemcpy((void*)io.in, &in, sizeof(StepIn), hipMemcpyHostToDevice));
     u32* x = (u32*)buf("xchg0").ptr;
     for (u32 r = 0; r < 2 * WORLD_MAX; ++r) x[2 * WORLD_MAX + r] = x[XC_RECV_AN + r] = 0;
+    for (u32 r = 0; r < WORLD_MAX; ++r) x[XC_RACK_N + r] = 0;
     x[2 * WORLD_MAX + d_.my_rank] = x[XC_RECV_AN + d_.my_rank] = n;
     x[3 * WORLD_MAX + d_.my_rank] = x[XC_RECV_AB + d_.my_rank] = (u32)pb;
     launch_ingest(s_comp_, io);
@@ -870,11 +922,29 @@ class Engine {
       u64 a = 0, b = 0;
       for (u32 r = 0; r < d_.world; ++r) { sbn[r] = a; sbb[r] = b; a += x[XC_SEND_N + r]; b += x[XC_SEND_B + r]; }
     }
+    // link deliveries / acks of the step before (its phase B preceded this phase A): the
+    // other parity's link buffers, destination-major (k_link_bases)
+    const u32* xl = (const u32*)buf("xchg" + std::to_string(q ^ 1)).ptr;
+    u64 lbn[WORLD_MAX], lbb[WORLD_MAX];
+    u32 lnn[WORLD_MAX], lnb[WORLD_MAX], lnk[WORLD_MAX];
+    {
+      u64 a = 0, b = 0;
+      for (u32 r = 0; r < d_.world; ++r) {
+        lnn[r] = links_ ? xl[XC_LINK_N + r] : 0;
+        lnb[r] = links_ ? xl[XC_LINK_B + r] : 0;
+        lnk[r] = links_ ? std::min<u32>(xl[XC_ACK_N + r], d_.lk_cap) : 0;
+        lbn[r] = a; lbb[r] = b;
+        a += lnn[r]; b += lnb[r];
+      }
+    }
     std::vector<u32> hs((size_t)n * cmqx::XH_WORDS, 0), hr((size_t)n * cmqx::XH_WORDS, 0);
     for (int i = 0; i < n; ++i) {
       u32* h = &hs[(size_t)i * cmqx::XH_WORDS];
       const int r = xmembers_[i];
-      if (i != me) { h[0] = x[XC_SEND_N + r]; h[1] = x[XC_SEND_B + r]; }
+      if (i != me) {
+        h[0] = x[XC_SEND_N + r]; h[1] = x[XC_SEND_B + r];
+        h[2] = lnn[r]; h[3] = lnb[r]; h[4] = lnk[r];
+      }
       h[5] = flags;
       h[6] = (u32)xseq_;
     }
@@ -894,31 +964,49 @@ class Engine {
     *or_flags = orf;
     // receive layout: sources in rank order, each [publish records | link records] and
     // [publish bytes | link bytes]
-    u64 rn = 0, rb = 0;
-    std::vector<u64> rbn(n), rbb(n);
+    u64 rn = 0, rb = 0, rk = 0;
+    std::vector<u64> rbn(n), rbb(n), rbk(n);
     for (int i = 0; i < n; ++i) {
       const u32* h = &hr[(size_t)i * cmqx::XH_WORDS];
-      rbn[i] = rn; rbb[i] = rb;
+      rbn[i] = rn; rbb[i] = rb; rbk[i] = rk;
       if (i == me) continue;
       rn += (u64)h[0] + h[2];
       rb += (u64)h[1] + h[3];
+      rk += h[4];
     }
-    if (rn > d_.import_max || rb > d_.xfer_bytes)
+    if (rn > d_.import_max || rb > d_.import_bytes || (rk && (!links_ || rk > (u64)d_.world * d_.lk_cap)))
       throw std::runtime_error("exchange: received records exceed the import buffers");
     u8* R_d = xr_desc_[q];
     u8* R_p = xr_pay_[q];
     const u8* S_d = xs_desc_[q];
     const u8* S_p = xs_pay_[q];
+    // link buffers: sent from the other parity (step t-1), received with this exchange
+    const u8* L_d = links_ ? ls_desc_[q ^ 1] : nullptr;
+    const u8* L_p = links_ ? ls_pay_[q ^ 1] : nullptr;
+    const u8* K_s = links_ ? lk_send_[q ^ 1] : nullptr;
+    u8* RK = links_ ? rack_[q] : nullptr;
     if (rccl_) {
       std::vector<std::vector<cmqx::XPart>> snd(n), rcv(n);
       for (int i = 0; i < n; ++i) {
         if (i == me) continue;
         const int r = xmembers_[i];
         const u32* h = &hr[(size_t)i * cmqx::XH_WORDS];
+        // per peer, both sides in this order: publish records, link records, publish
+        // payload, link payload, link acks
         snd[i].push_back({(void*)(S_d + 64 * sbn[r]), 64ull * x[XC_SEND_N + r]});
+        if (links_) snd[i].push_back({(void*)(L_d + 64 * lbn[r]), 64ull * lnn[r]});
         snd[i].push_back({(void*)(S_p + sbb[r]), (u64)x[XC_SEND_B + r]});
+        if (links_) {
+          snd[i].push_back({(void*)(L_p + lbb[r]), (u64)lnb[r]});
+          snd[i].push_back({(void*)(K_s + 16ull * d_.lk_cap * r), 16ull * lnk[r]});
+        }
         rcv[i].push_back({(void*)(R_d + 64 * rbn[i]), 64ull * h[0]});
+        if (links_) rcv[i].push_back({(void*)(R_d + 64 * (rbn[i] + h[0])), 64ull * h[2]});
         rcv[i].push_back({(void*)(R_p + rbb[i]), (u64)h[1]});
+        if (links_) {
+          rcv[i].push_back({(void*)(R_p + rbb[i] + h[1]), (u64)h[3]});
+          rcv[i].push_back({(void*)(RK + 16 * rbk[i]), 16ull * h[4]});
+        }
       }
       {
         Range rb_("chanamq.X1.bulk");
@@ -942,11 +1030,19 @@ class Engine {
         const int r = xmembers_[i];
         dir[i] = off;
         const u64 nd = 64ull * x[XC_SEND_N + r], nb = x[XC_SEND_B + r];
-        if (off + nd + nb > shm_->box_bytes()) throw std::runtime_error("exchange: shm mailbox too small");
+        const u64 ld = 64ull * lnn[r], lb = lnb[r], kb = 16ull * lnk[r];
+        if (off + nd + ld + nb + 16 + lb + kb > shm_->box_bytes())
+          throw std::runtime_error("exchange: shm mailbox too small");
         if (nd) HIPCHECK(hipMemcpy(box + off, S_d + 64 * sbn[r], nd, hipMemcpyDeviceToHost));
         off += nd;
+        if (ld) HIPCHECK(hipMemcpy(box + off, L_d + 64 * lbn[r], ld, hipMemcpyDeviceToHost));
+        off += ld;
         if (nb) HIPCHECK(hipMemcpy(box + off, S_p + sbb[r], nb, hipMemcpyDeviceToHost));
         off += (nb + 15) & ~15ull;
+        if (lb) HIPCHECK(hipMemcpy(box + off, L_p + lbb[r], lb, hipMemcpyDeviceToHost));
+        off += (lb + 15) & ~15ull;
+        if (kb) HIPCHECK(hipMemcpy(box + off, K_s + 16ull * d_.lk_cap * r, kb, hipMemcpyDeviceToHost));
+        off += kb;
       }
       rc = shm_->barrier();
       if (rc) return rc;
@@ -954,14 +1050,19 @@ class Engine {
         if (i == me) continue;
         const u32* h = &hr[(size_t)i * cmqx::XH_WORDS];
         const u8* src = shm_->box(i) + shm_->dir(i)[me];
-        const u64 nd = 64ull * h[0], nb = h[1];
-        if (nd) HIPCHECK(hipMemcpy(R_d + 64 * rbn[i], src, nd, hipMemcpyHostToDevice));
-        if (nb) HIPCHECK(hipMemcpy(R_p + rbb[i], src + nd, nb, hipMemcpyHostToDevice));
+        const u64 nd = 64ull * h[0], nb = h[1], ld = 64ull * h[2], lb = h[3], kb = 16ull * h[4];
+        if (nd + ld) HIPCHECK(hipMemcpy(R_d + 64 * rbn[i], src, nd + ld, hipMemcpyHostToDevice));
+        src += nd + ld;
+        if (nb) HIPCHECK(hipMemcpy(R_p + rbb[i], src, nb, hipMemcpyHostToDevice));
+        src += (nb + 15) & ~15ull;
+        if (lb) HIPCHECK(hipMemcpy(R_p + rbb[i] + nb, src, lb, hipMemcpyHostToDevice));
+        src += (lb + 15) & ~15ull;
+        if (kb) HIPCHECK(hipMemcpy(RK + 16 * rbk[i], src, kb, hipMemcpyHostToDevice));
       }
     }
     // what launch_b writes into the importing step's xchg: per rank [records, bytes,
     // publish records, publish bytes]
-    lag_recv_.assign(4 * d_.world, 0);
+    lag_recv_.assign(5 * d_.world, 0);
     for (int i = 0; i < n; ++i) {
       if (i == me) continue;
       const int r = xmembers_[i];
@@ -970,6 +1071,7 @@ class Engine {
       lag_recv_[d_.world + r] = h[1] + h[3];
       lag_recv_[2 * d_.world + r] = h[0];
       lag_recv_[3 * d_.world + r] = h[1];
+      lag_recv_[4 * d_.world + r] = h[4];
     }
     counts_ready_[q] = false;
     ++xseq_;
@@ -989,12 +1091,13 @@ class Engine {
     if (!b_due_[p]) throw std::runtime_error("launch_b: no phase-A step of this parity");
     b_due_[p] = false;
     u32* x = (u32*)buf("xchg" + std::to_string(p)).ptr;
-    const bool have = lag_recv_.size() == 4 * d_.world;
+    const bool have = lag_recv_.size() == 5 * d_.world;
     for (u32 r = 0; r < d_.world; ++r) {
       x[XC_RECV_N + r] = have ? lag_recv_[r] : 0;
       x[XC_RECV_B + r] = have ? lag_recv_[d_.world + r] : 0;
       x[XC_RECV_AN + r] = have ? lag_recv_[2 * d_.world + r] : 0;
       x[XC_RECV_AB + r] = have ? lag_recv_[3 * d_.world + r] : 0;
+      x[XC_RACK_N + r] = have ? lag_recv_[4 * d_.world + r] : 0;
     }
     lag_recv_.clear();
     if (x_wait_ && rccl_) HIPCHECK(hipStreamWaitEvent(s_comp_, rccl_->event(), 0));
@@ -1059,6 +1162,12 @@ class Engine {
     };
     a.launch_b = [](void* e, int p) -> int {
       return ((Engine*)e)->guard([&] { ((Engine*)e)->launch_b(p); return 0; });
+    };
+    a.links = links_ ? 1u : 0u;
+    a.flush_submit = [](void* e, i64 now, u32 worker) -> int {
+      return ((Engine*)e)->guard([&] {
+        return ((Engine*)e)->submit_raw(nullptr, 0, 0, 0, now, (u64)now, worker, false, SF_NODISPATCH);
+      });
     };
     for (int p = 0; p < 2; ++p) {
       std::string sfx = std::to_string(p);
@@ -1345,6 +1454,7 @@ class Engine {
       launch_scan(s, {{d.conn_total, d.conn_base}}, nullptr, d.c_max, 7);
       hipLaunchKernelGGL(k_conn_out, blocks(d.c_max, 256), dim3(256), 0, s, d);
     }
+    if (d.links) hipLaunchKernelGGL(k_link_bases, dim3(1), dim3(64), 0, s, d);
     {
       const u32 n_rc = RC_RET_BLOCKS + ceil_div(d.c_max, 256);
       hipLaunchKernelGGL(k_render, dim3(n_rc + blocks((u64)d.deliv_max * 64, 256).x), dim3(256), 0, s, d, n_rc);
@@ -1371,6 +1481,7 @@ class Engine {
   void launch_phase_b(hipStream_t s, const DS& d, bool dispatch = true) {
     Range rg("chanamq.X1.import");
     hipLaunchKernelGGL(k_import_prep, dim3(1), dim3(64), 0, s, d);
+    if (d.links) hipLaunchKernelGGL(k_link_acks, dim3(64), dim3(256), 0, s, d);
     hipLaunchKernelGGL(k_import, blocks(d.import_max, 256), dim3(256), 0, s, d);
     launch_route(s, d, d.import_max);
     launch_tail(s, d, dispatch);
@@ -1433,6 +1544,11 @@ class Engine {
   u8* xs_pay_[2] = {nullptr, nullptr};
   u8* xr_desc_[2] = {nullptr, nullptr};
   u8* xr_pay_[2] = {nullptr, nullptr};
+  bool links_ = false;
+  u8* ls_desc_[2] = {nullptr, nullptr};
+  u8* ls_pay_[2] = {nullptr, nullptr};
+  u8* lk_send_[2] = {nullptr, nullptr};
+  u8* rack_[2] = {nullptr, nullptr};
   struct HostIO : DS {   // per-parity device view + host addresses of its mapped outputs
     const Counters* ctr_host_h = nullptr;
     const SegOut* seg_out_hh = nullptr;
@@ -1509,7 +1625,8 @@ PYBIND11_MODULE(_dataplane, m) {
       .def("download", &Engine::download, py::arg("name"), py::arg("offset") = 0, py::arg("n") = 0)
       .def("host_view", &Engine::host_view)
       .def("submit", &Engine::submit, py::arg("segs"), py::arg("payload_ptr"), py::arg("payload_len"),
-           py::arg("now_ms"), py::arg("step"), py::arg("id_ms"), py::arg("worker"), py::arg("defer") = false)
+           py::arg("now_ms"), py::arg("step"), py::arg("id_ms"), py::arg("worker"), py::arg("defer") = false,
+           py::arg("flags") = 0)
       .def("launch", &Engine::launch)
       .def("send_counts", &Engine::send_counts)
       .def("submit_b", &Engine::submit_b, py::arg("parity"), py::arg("recv"), py::arg("stream") = 0)

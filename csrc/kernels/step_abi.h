@@ -124,5 +124,9 @@ struct CmqEngineApi {
   int (*exchange)(void* eng, int q, u32 flags, u32* or_flags);
   int (*drop_exchange)(void* eng, int q);
   int (*launch_b)(void* eng, int p);
+  // remote-consumer links on the device (X2/X3): a control sync flushes with two empty
+  // no-dispatch steps (their link records and acks travel one exchange later)
+  u32 links;
+  int (*flush_submit)(void* eng, i64 now_ms, u32 worker);   // an empty no-dispatch step: parity
 };
 #define GROW_MAX 4096   // grow requests reported per step

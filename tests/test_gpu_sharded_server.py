@@ -1,0 +1,139 @@
+"""The pipelined sharded GPU server (server/sharded.py --io pipeline): two ranks on the one
+test MI355X, each behind the native front end, stepping in lockstep with the engine's own
+exchange (host shared-memory backend: RCCL refuses two ranks on one device).  Clients on
+different ranks declare, bind, publish and consume; replicated ops are answered at the
+flagged sync steps; cross-rank publishes travel through the per-step exchange."""
+
+import json
+import os
+import time
+
+import pytest
+
+from chanamq_amd.client import Connection
+
+pytestmark = pytest.mark.gpu
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+@pytest.fixture
+def cluster(tmp_path):
+    from chanamq_amd.parallel.launch import Launcher
+    env = dict(os.environ, PYTHONPATH=os.path.dirname(HERE))
+    ln = Launcher(2, ["-m", "chanamq_amd.server.sharded", "--plane", "gpu", "--port", "0", "--backend", "gloo",
+                      "--info-dir", str(tmp_path), "--xchg-timeout-ms", "20000"], env=env).start()
+    deadline = time.time() + 180
+    while time.time() < deadline and not all((tmp_path / f"rank{r}.json").exists() for r in range(2)):
+        assert not ln.poll(), f"rank exited early: {ln.poll()}"
+        time.sleep(0.2)
+    info = [json.load(open(tmp_path / f"rank{r}.json")) for r in range(2)]
+    assert all(i["io"] == "pipeline" for i in info)
+    yield [i["port"] for i in info], ln
+    for r in range(2):   # the ranks' counters (front end: steps, syncs, exchanges) for the log
+        print(f"rank {r}:", (tmp_path / f"rank{r}.json").read_text())
+    ln.stop()
+
+
+@pytest.mark.timeout(300)
+def test_pipelined_cross_rank_routing_and_topology(cluster):
+    ports, ln = cluster
+    c0 = Connection(port=ports[0], vhost="/")
+    c1 = Connection(port=ports[1], vhost="/")
+    a = c0.channel()
+    a.exchange_declare("px", "topic")
+    a.queue_declare("pqa")
+    a.queue_bind("pqa", "px", "a.*")
+    b = c1.channel()
+    b.exchange_declare("px", "topic", passive=True)   # replicated to rank 1 at the sync step
+    b.queue_declare("pqb")
+    b.queue_bind("pqb", "px", "*.b")
+    a.basic_consume("pqa", "ca", no_ack=True)
+    b.basic_consume("pqb", "cb", no_ack=True)
+    p = c0.channel()
+    for k in ("a.b", "a.x", "z.b"):
+        p.basic_publish("px", k, k.encode())
+    assert [d.body for d in a.consume_n(2)] == [b"a.b", b"a.x"]
+    assert [d.body for d in b.consume_n(2)] == [b"a.b", b"z.b"]
+    p1 = c1.channel()
+    for i in range(200):   # rank 1 -> rank 0's queue, order kept
+        p1.basic_publish("px", "a.q", b"from-1-%d" % i)
+    assert [d.body for d in a.consume_n(200)] == [b"from-1-%d" % i for i in range(200)]
+    # confirms for cross-rank publishes
+    p1.confirm_select()
+    for i in range(50):
+        p1.basic_publish("px", "a.c", b"c%d" % i)
+    assert p1.wait_for_confirms()
+    assert [d.body for d in a.consume_n(50)] == [b"c%d" % i for i in range(50)]
+    # a queue deleted on one rank is gone everywhere
+    b.queue_delete("pqb")
+    p.basic_publish("px", "z.b", b"nowhere", mandatory=True)
+    c0.process(0.5)
+    c0.close()
+    c1.close()
+    assert not ln.poll()
+
+
+@pytest.mark.timeout(300)
+def test_pipelined_remote_consumers_and_gets(cluster):
+    """X2/X3 on the device: a consumer on rank 1 of rank 0's queue (deliveries shipped as
+    restore records in the exchange, acks back as ack records), manual ack with prefetch,
+    nack-requeue inside the link, cancel, then Basic.Get through a get link."""
+    ports, ln = cluster
+    c0 = Connection(port=ports[0], vhost="/")
+    c1 = Connection(port=ports[1], vhost="/")
+    a = c0.channel()
+    a.exchange_declare("lx", "topic")
+    a.queue_declare("lqa")
+    a.queue_bind("lqa", "lx", "a.*")
+    p = c0.channel()
+    r = c1.channel()
+    r.basic_qos(prefetch_count=5)
+    r.basic_consume("lqa", "remote")
+    c1.process(0.3)
+    for i in range(8):
+        p.basic_publish("lx", "a.z", b"z%d" % i)
+    got = r.consume_n(5)
+    assert [d.body for d in got] == [b"z%d" % i for i in range(5)]     # prefetch 5 across ranks
+    r.basic_nack(got[1].delivery_tag, requeue=True)
+    again = r.consume_n(1)[0]
+    assert again.body == b"z1" and again.method.redelivered
+    r.basic_ack(got[4].delivery_tag, multiple=True)
+    rest = r.consume_n(3)
+    assert [d.body for d in rest] == [b"z5", b"z6", b"z7"]
+    r.basic_ack(rest[-1].delivery_tag, multiple=True)
+    r.basic_ack(again.delivery_tag)
+    # a burst through the link with auto-ack on a second remote consumer
+    r2 = c1.channel()
+    r2.basic_consume("lqa", "remote2", no_ack=True)
+    r.basic_cancel("remote")
+    c1.process(0.3)
+    for i in range(300):
+        p.basic_publish("lx", "a.b", b"b%03d" % i)
+    assert [d.body for d in r2.consume_n(300)] == [b"b%03d" % i for i in range(300)]
+    r2.basic_cancel("remote2")
+    c1.process(0.5)
+    # everything was acked through the links: nothing comes back to a local consumer
+    a.basic_consume("lqa", "ca2", no_ack=True)
+    p.basic_publish("lx", "a.end", b"end")
+    assert a.consume_n(1)[0].body == b"end"
+    a.basic_cancel("ca2")
+    c0.process(0.3)
+    # Basic.Get on rank 1 of rank 0's queue (get link, answered through the control log)
+    for i in range(3):
+        p.basic_publish("lx", "a.g", b"g%d" % i)
+    c0.process(0.5)
+    g = c1.channel()
+    g0 = g.basic_get("lqa")
+    assert g0.body == b"g0" and g0.method.message_count == 2 and not g0.method.redelivered
+    g1 = g.basic_get("lqa", no_ack=True)
+    assert g1.body == b"g1"
+    g.basic_ack(g0.method.delivery_tag)
+    assert g.basic_get("lqa", no_ack=True).body == b"g2"
+    assert g.basic_get("lqa") is None
+    c1.process(1.5)   # the idle get link closes; acks reached the owner: nothing comes back
+    a.basic_consume("lqa", "ca3", no_ack=True)
+    p.basic_publish("lx", "a.end", b"end2")
+    assert a.consume_n(1)[0].body == b"end2"
+    c0.close()
+    c1.close()
+    assert not ln.poll()

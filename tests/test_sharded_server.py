@@ -18,7 +18,9 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 def cluster(request, tmp_path):
     from chanamq_amd.parallel.launch import Launcher
     env = dict(os.environ, PYTHONPATH=os.path.dirname(HERE))
-    extra = ["--backend", "gloo"] if request.param == "gpu" else []   # 2 ranks share the one test GPU
+    # 2 ranks share the one test GPU; the Python lockstep loop (remote consumers over the
+    # Python link relay).  The pipelined front end: tests/test_gpu_sharded_server.py
+    extra = ["--backend", "gloo", "--io", "native"] if request.param == "gpu" else []
     ln = Launcher(2, ["-m", "chanamq_amd.server.sharded", "--plane", request.param, "--port", "0",
                       "--info-dir", str(tmp_path)] + extra, env=env).start()
     deadline = time.time() + 120
