@@ -180,6 +180,48 @@ def run_one(core, name, spec, io, io_threads, seconds, rate=0.0, lg_threads=12, 
     return r
 
 
+def run_sharded(core, name, spec, world, mode, seconds, rate=0.0, io_threads=2, lg_threads=12, cons_threads=8):
+    """The pipelined sharded server (server/sharded.py, ``world`` rank processes on this
+    one GPU, shared-memory exchange): the topology is declared on rank 0 (its queues live
+    there), producers attach to rank 1 (every publish crosses the per-step exchange) and
+    consumers to rank 0 (``mode`` "local") or rank 1 (``mode`` "remote": every delivery
+    travels back through a device link and every ack through the exchange)."""
+    from chanamq_amd.parallel.launch import Launcher
+    tmp = tempfile.mkdtemp(prefix="cmq-sharded-")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, PYTHONPATH=root)
+    ln = Launcher(world, ["-m", "chanamq_amd.server.sharded", "--plane", "gpu", "--port", "0", "--backend", "gloo",
+                          "--info-dir", tmp, "--io-threads", str(io_threads), "--idle-step-ms", "0.5"],
+                  env=env).start()
+    try:
+        deadline = time.time() + 180
+        while not all(os.path.exists(os.path.join(tmp, f"rank{r}.json")) for r in range(world)):
+            if ln.poll() or time.time() > deadline:
+                raise RuntimeError(f"sharded server did not come up: {ln.poll()}")
+            time.sleep(0.2)
+        ports = [json.load(open(os.path.join(tmp, f"rank{r}.json")))["port"] for r in range(world)]
+        spec = {k: v for k, v in spec.items() if not k.startswith("_")}
+        t0 = time.time()
+        r = core.run_load(dict(port=ports[0], consumer_port=ports[0] if mode == "local" else ports[1 % world],
+                               producer_port=ports[1 % world], seconds=seconds, warmup=1.0,
+                               queue=f"e2e.{name}", exchange=f"e2e.x.{name}", threads=lg_threads,
+                               consumer_threads=cons_threads, rate=rate, **spec))
+        time.sleep(0.7)
+        ranks = [json.load(open(os.path.join(tmp, f"rank{k}.json"))) for k in range(world)]
+    finally:
+        ln.stop()
+    r.update(name=name, io="pipeline-sharded", world=world, consumers_on=mode, io_threads=io_threads,
+             rate_per_producer=rate, recv_msgs_per_s=r["received"] / r["elapsed"],
+             sent_msgs_per_s=r["sent"] / r["elapsed"], confirmed_per_s=r["confirmed"] / r["elapsed"],
+             wall_s=time.time() - t0, spec=spec,
+             ranks=[{"rank": k["rank"], "front_end": {x: k["front_end"].get(x) for x in
+                                                      ("steps", "idle_steps", "xchg_steps", "syncs", "xfails",
+                                                       "flush_steps", "xchg_s", "submit_s", "io_phase_s", "wait_s",
+                                                       "published", "delivered", "held_steps")}}
+                    for k in ranks])
+    return r
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--seconds", type=float, default=4.0)
@@ -193,12 +235,40 @@ def main():
     ap.add_argument("--rates", default="", help="comma list of aggregate publish rates (msgs/s) to run paced")
     ap.add_argument("--paced", type=float, default=0.5,
                     help="re-run each spec with producers paced at this fraction of the measured rate (0 = off)")
+    ap.add_argument("--sharded", type=int, default=0,
+                    help="N > 1: the pipelined sharded server with N ranks on this GPU (producers on rank 1, "
+                         "consumers on rank 0 and then on rank 1 through device links)")
     args = ap.parse_args()
     if args.wblock_high:
         FE_CFG.update(wblock_high=args.wblock_high, wblock_low=args.wblock_high // 4)
-    import torch  # noqa: F401  (HIP runtime up before the first plane)
     core = load()
     results = []
+    if args.sharded > 1:
+        keys = ("name", "world", "consumers_on", "recv_msgs_per_s", "sent_msgs_per_s", "confirmed_per_s", "p50_us",
+                "p99_us", "error", "ranks")
+        for name, spec in SPECS.items():
+            if args.only and args.only not in name:
+                continue
+            for mode in ("local", "remote"):
+                r = run_sharded(core, name, spec, args.sharded, mode, args.seconds, io_threads=int(args.io_threads.split(",")[0]),
+                                lg_threads=args.loadgen_threads, cons_threads=args.consumer_threads)
+                results.append(r)
+                print(json.dumps({k: r.get(k) for k in keys}), flush=True)
+                if args.paced > 0 and r["recv_msgs_per_s"] > 0 and not r["error"]:
+                    rate = args.paced * r["recv_msgs_per_s"] / max(1, spec.get("producers", 1))
+                    rp = run_sharded(core, name, spec, args.sharded, mode, args.seconds, rate=rate,
+                                     io_threads=int(args.io_threads.split(",")[0]), lg_threads=args.loadgen_threads,
+                                     cons_threads=args.consumer_threads)
+                    rp["paced_fraction"] = args.paced
+                    results.append(rp)
+                    print(json.dumps({k: rp.get(k) for k in keys + ("rate_per_producer", "p95_us")}), flush=True)
+        if args.out:
+            with open(args.out, "w") as f:
+                json.dump({"meta": {"transport": "loopback TCP", "data_plane": f"HIP gfx950, {args.sharded} ranks on 1 GPU",
+                                    "exchange": "host shared memory (RCCL needs one GPU per rank)",
+                                    "seconds": args.seconds}, "results": results}, f, indent=1)
+        return
+    import torch  # noqa: F401  (HIP runtime up before the first plane)
     for name, spec in SPECS.items():
         if args.only and args.only not in name:
             continue

@@ -61,7 +61,7 @@ class _Conn:
 
 
 FE_OPEN, FE_CLOSED, FE_HOST, FE_CTRL, FE_TXBUF, FE_EVENT, FE_STATUS, FE_PERSIST, FE_ERROR, FE_GROW, FE_SYNC, \
-    FE_XFAIL = range(1, 13)
+    FE_XFAIL, FE_INJECTED = range(1, 14)
 
 
 class _PlaneLock:
@@ -317,10 +317,12 @@ class GpuBroker:
             dev = [e for e in evs if e[0] != FE_PERSIST]
             if dev or self._tx_pending:
                 with self.lock:
-                    while dev or self._tx_pending:
+                    while dev or (self._tx_pending and self.node is None):
                         self._handle_fe(dev)
-                        while self._tx_pending:   # committed transactions: host-run injection steps
-                            self._host_step({})
+                        if self.node is not None:   # sharded: injected into the lockstep steps
+                            self._tx_inject()
+                        while self._tx_pending and self.node is None:   # committed transactions:
+                            self._host_step({})                         # host-run injection steps
                         more = fe.poll_events(0)
                         persist += [e for e in more if e[0] == FE_PERSIST]
                         dev = [e for e in more if e[0] != FE_PERSIST]
@@ -342,6 +344,10 @@ class GpuBroker:
         for kind, conn, a, b, data, data2 in evs:
             if kind in (FE_SYNC, FE_XFAIL):
                 sync = kind if sync is None else max(sync, kind)
+                continue
+            if kind == FE_INJECTED:   # a committed transaction's publishes were stepped
+                if conn == self.txc:
+                    self._tx_end()
                 continue
             if kind == FE_OPEN:
                 self.conns[conn] = _Conn(None, conn, None)
@@ -800,6 +806,16 @@ class GpuBroker:
             return data
         return b""
 
+    def _tx_inject(self):
+        """Sharded pipelined node: the next committed transaction's publishes go through
+        the pseudo-connection ``txc`` in the next lockstep step (a host-run step would
+        bypass the exchange); Tx.CommitOk and the unpause follow at FE_INJECTED."""
+        if self._tx_active is not None or not self._tx_pending:
+            return
+        data = self._tx_begin()
+        if data:
+            self.fe.inject(self.txc, data)
+
     def _tx_end(self):
         """After the injection step: Tx.CommitOk, and the connection resumes."""
         if self._tx_active is None:
@@ -810,6 +826,8 @@ class GpuBroker:
         if c is not None and c.state == "open":
             self._send(c, ch, Method("tx.commit_ok"))
             self._unpause(conn)
+        if self.node is not None and self.fe is not None:
+            self._tx_inject()
 
     def _tx_commit(self, c, ch):
         """Apply the channel's held acks now (window marks between steps) and queue its
@@ -837,7 +855,8 @@ class GpuBroker:
         return "deferred"
 
     def _after_step(self, ctrl, events, seg_status, cnt, had_input, had_egress, txbuf=()):
-        self._tx_end()
+        if self.node is None or self.fe is None:   # sharded pipelined: at FE_INJECTED
+            self._tx_end()
         for conn, _, raw in txbuf:   # data commands of transactional channels, in wire order
             ch = struct.unpack_from(">H", raw, 1)[0]
             if (conn, ch) in self._txbuf:

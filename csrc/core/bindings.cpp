@@ -256,6 +256,7 @@ PYBIND11_MODULE(_core, m) {
       .def("attach_persist", &Frontend::attach_persist, py::keep_alive<1, 2>())
       .def("pending_out", &Frontend::pending_out)
       .def("request_sync", &Frontend::request_sync)
+      .def("inject", [](Frontend& f, uint32_t conn, py::bytes b) { f.inject(conn, std::string(b)); })
       .def("sync_done", &Frontend::sync_done)
       .def("healthy", &Frontend::healthy, py::arg("stuck_s") = 5.0)
       .def("inject_fault", &Frontend::inject_fault, py::arg("kind"), py::arg("steps") = 0)
@@ -317,6 +318,7 @@ PYBIND11_MODULE(_core, m) {
 #define S(k, f) if (d.contains(k)) s.f = d[k].cast<decltype(s.f)>()
     S("host", host); S("port", port); S("vhost", vhost); S("producers", producers); S("consumers", consumers);
     S("msg_size", msg_size); S("seconds", seconds); S("exchange", exchange); S("exchange_type", exchange_type);
+    S("consumer_port", consumer_port); S("producer_port", producer_port);
     S("routing_key", routing_key); S("queue", queue); S("queues", queues); S("auto_ack", auto_ack);
     S("prefetch", prefetch); S("persistent", persistent); S("durable", durable); S("confirm", confirm);
     S("rate", rate); S("threads", threads); S("warmup", warmup); S("confirm_window", confirm_window);

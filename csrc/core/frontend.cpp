@@ -95,6 +95,7 @@ Frontend::Frontend(const FrontendCfg& cfg, const CmqEngineApi* api) : cfg_(cfg),
   if (!api_ || api_->abi != CMQ_STEP_ABI) throw std::runtime_error("frontend: engine C API missing or ABI mismatch");
   c_max_ = api_->c_max;
   held_cnt_.assign(c_max_, 0);
+  notify_.assign(c_max_, 0);
   if (cfg_.io_threads < 1) cfg_.io_threads = 1;
   if (!cfg_.max_slot || cfg_.max_slot > c_max_ - 2) cfg_.max_slot = c_max_ - 2;
   conns_.resize(c_max_);
@@ -342,6 +343,27 @@ void Frontend::close(u32 conn) {
     io.closing.push_back(conn);
   }
   poke(io.evfd);
+}
+
+void Frontend::inject(u32 conn, const std::string& bytes) {
+  if (conn == 0 || conn >= c_max_) return;
+  FeConn& c = *conns_[conn];
+  {
+    std::lock_guard<std::mutex> g(c.mu);
+    c.inject += bytes;
+    c.carry = c.inflight = 0;
+    c.paused = false;
+    c.kicked = true;
+    c.mode = M_DATA;
+  }
+  notify_[conn] = 1;
+  FeIo& io = *io_[c.io];
+  {
+    std::lock_guard<std::mutex> g(io.qmu);
+    io.pending.push_back(conn);
+  }
+  poke(io.evfd);
+  wake_stepper();
 }
 
 void Frontend::kick(u32 conn) {
@@ -780,6 +802,17 @@ void Frontend::finish_oldest(std::deque<Inflight>& inflight) {
     const u32 len = f.segs[k].second;
     cc.inflight = cc.inflight > len ? cc.inflight - len : 0;
     if (s.status & SS_CTRL) cc.paused = true;
+    if (notify_[s.conn] && cc.fd < 0) {   // an injected pseudo-connection's bytes were stepped
+      std::lock_guard<std::mutex> g(cc.mu);
+      if (cc.inject.empty()) {
+        notify_[s.conn] = 0;
+        FeEvent e;
+        e.kind = FE_INJECTED;
+        e.conn = s.conn;
+        e.a = s.carry;
+        post(std::move(e));
+      }
+    }
     if (s.status & (SS_FRAME_ERROR | SS_UNEXPECTED | SS_TOO_LARGE)) {
       FeEvent e;
       e.kind = FE_STATUS;

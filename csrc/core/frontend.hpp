@@ -61,6 +61,7 @@ enum FeEventKind : int {
   // exchange was imported) and then calls sync_done()
   FE_SYNC = 11,
   FE_XFAIL = 12,
+  FE_INJECTED = 13,   // the bytes inject()ed into a pseudo-connection were stepped (a = its carry)
 };
 
 enum : u32 { XF_SYNC = 1, XF_BUSY = 2 };   // exchange flags (OR over the live ranks)
@@ -121,6 +122,9 @@ class Frontend {
   void set_heartbeat(u32 conn, u32 seconds);
   void close(u32 conn);                                  // flush, close the socket, free the slot
   void kick(u32 conn);                                   // unpaused: re-present its device carry
+  // bytes for a socketless pseudo-connection (committed transactions): stepped with the
+  // next step like a client's, FE_INJECTED once that step finished; egress is dropped
+  void inject(u32 conn, const std::string& bytes);
   void pause();                                          // exclusive device access (nests)
   void resume();
   void release(u64 step);                                // store commit of steps <= step landed
@@ -135,6 +139,7 @@ class Frontend {
   // per-step liveness for the failure detector: false once the engine failed or a GPU
   // wait (step results, egress) has been stuck longer than `stuck_s`
   bool healthy(double stuck_s) const;
+  std::vector<u8> notify_;   // per connection: post FE_INJECTED when its segment was stepped
   // fault injection (tests): after `steps` more steps, kind 1 = engine error, 2 = process
   // exit, 3 = wedge (the stepper blocks inside a GPU wait forever)
   void inject_fault(int kind, u64 steps);

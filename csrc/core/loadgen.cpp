@@ -227,7 +227,7 @@ LoadResult run_load(const LoadSpec& s) {
   // consumers first: they are attached before any message is published
   for (int ci = 0; ci < s.consumers; ++ci) {
     std::unique_ptr<Peer> p(new Peer());
-    p->cl.open(s.host, s.port, s.vhost);
+    p->cl.open(s.host, s.consumer_port ? s.consumer_port : s.port, s.vhost);
     Method qos = make_method(60, 10);
     qos.args[1].i = s.prefetch;
     p->cl.method(1, qos);
@@ -251,7 +251,7 @@ LoadResult run_load(const LoadSpec& s) {
   for (int pi = 0; pi < s.producers; ++pi) {
     std::unique_ptr<Peer> p(new Peer());
     p->producer = true;
-    p->cl.open(s.host, s.port, s.vhost);
+    p->cl.open(s.host, s.producer_port ? s.producer_port : s.port, s.vhost);
     if (s.confirm) {
       p->cl.method(1, make_method(85, 10));
       p->cl.flush();

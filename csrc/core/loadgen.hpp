@@ -23,6 +23,9 @@ struct LoadSpec {
   int consumer_threads = 0;  // of `threads`, serving consumers (0 = half)
   int nack_every = 0;        // manual ack: every n-th ack of a consumer is Basic.Nack(multiple,
                              // requeue) instead (redelivery storm, BASELINE config 5)
+  // sharded broker: the topology is declared through `port` (queues live on that rank);
+  // consumers / producers may attach to other ranks (0 = `port`)
+  int consumer_port = 0, producer_port = 0;
 };
 
 struct LoadResult {

@@ -137,3 +137,98 @@ def test_pipelined_remote_consumers_and_gets(cluster):
     c0.close()
     c1.close()
     assert not ln.poll()
+
+
+@pytest.mark.timeout(300)
+def test_pipelined_transactions_and_durable_topology(cluster):
+    """Tx.Commit on a sharded node: the held publishes are injected into the next lockstep
+    step (they may route to another rank), CommitOk after that step; rollback drops."""
+    ports, ln = cluster
+    c0 = Connection(port=ports[0], vhost="/")
+    c1 = Connection(port=ports[1], vhost="/")
+    a = c0.channel()
+    a.exchange_declare("tx.x", "direct")
+    a.queue_declare("tx.q")
+    a.queue_bind("tx.q", "tx.x", "k")
+    a.basic_consume("tx.q", "tc", no_ack=True)
+    t = c1.channel()
+    t.tx_select()
+    for i in range(5):
+        t.basic_publish("tx.x", "k", b"t%d" % i)
+    c1.process(0.3)
+    t.tx_rollback()
+    for i in range(5, 10):
+        t.basic_publish("tx.x", "k", b"t%d" % i)
+    t.tx_commit()
+    assert [d.body for d in a.consume_n(5)] == [b"t%d" % i for i in range(5, 10)]
+    t.basic_publish("tx.x", "k", b"after")
+    t.tx_commit()
+    assert a.consume_n(1)[0].body == b"after"
+    c0.close()
+    c1.close()
+    assert not ln.poll()
+
+
+@pytest.mark.timeout(400)
+def test_pipelined_rank_death_durable_redelivery(tmp_path):
+    """HA on GPU planes: 3 pipelined ranks on the one GPU.  A client on rank 2 declares a
+    durable queue there, publishes persistent messages with confirms and holds 5 of them
+    unacked; rank 2 is killed.  The survivors' next exchange times out (bounded wait),
+    they agree on the dead rank, rebuild the exchange over themselves, re-home the queue and
+    reload it from rank 2's store through the device restore path: every message comes
+    back, the 5 it held flagged redelivered (README.md:50, QueueEntity.scala:107-135)."""
+    from chanamq_amd.client import ChannelClosed
+    from chanamq_amd.parallel.launch import Launcher
+    env = dict(os.environ, PYTHONPATH=os.path.dirname(HERE))
+    ln = Launcher(3, ["-m", "chanamq_amd.server.sharded", "--plane", "gpu", "--port", "0", "--backend", "gloo",
+                      "--info-dir", str(tmp_path), "--store-dir", str(tmp_path / "store"), "--no-fsync",
+                      "--xchg-timeout-ms", "4000", "--hb-timeout-s", "2"], env=env).start()
+    try:
+        deadline = time.time() + 180
+        while time.time() < deadline and not all((tmp_path / f"rank{r}.json").exists() for r in range(3)):
+            assert not ln.poll(), f"rank exited early: {ln.poll()}"
+            time.sleep(0.2)
+        ports = [json.load(open(tmp_path / f"rank{r}.json"))["port"] for r in range(3)]
+        c2 = Connection(port=ports[2], vhost="/")
+        ch = c2.channel()
+        ch.exchange_declare("hx", "direct", durable=True)
+        ch.queue_declare("hq", durable=True)
+        ch.queue_bind("hq", "hx", "k")
+        ch.confirm_select()
+        for i in range(20):
+            ch.basic_publish("hx", "k", b"m%d" % i, {"delivery_mode": 2})
+        assert ch.wait_for_confirms()
+        cc = c2.channel()
+        cc.basic_qos(prefetch_count=5)
+        cc.basic_consume("hq", "held")
+        held = cc.consume_n(5)
+        assert [d.body for d in held] == [b"m%d" % i for i in range(5)]
+        c2.process(0.5)   # the unack rows reach rank 2's store (write-behind)
+        ln.procs[2].kill()
+        ln.procs[2].wait(30)
+        got, red = None, None
+        deadline = time.time() + 120
+        while got is None and time.time() < deadline:
+            for p in ports[:2]:
+                c = Connection(port=p, vhost="/")
+                try:
+                    q = c.channel()
+                    q.basic_consume("hq", "hc", no_ack=True)
+                    ds = q.consume_n(20, timeout=20)
+                    got = [d.body for d in ds]
+                    red = [d.method.redelivered for d in ds]
+                    break
+                except (ChannelClosed, TimeoutError):   # not (yet) the owner
+                    pass
+                finally:
+                    c.close()
+            if got is None:
+                time.sleep(0.5)
+        assert got is not None, [json.load(open(tmp_path / f"rank{r}.json")) for r in range(2)]
+        assert sorted(got) == sorted(b"m%d" % i for i in range(20))
+        assert got[:5] == [b"m%d" % i for i in range(5)] and all(red[:5]) and not any(red[5:])
+        infos = [json.load(open(tmp_path / f"rank{r}.json")) for r in range(2)]
+        assert all(i["failovers"] == 1 for i in infos), infos
+        assert all(i["front_end"]["xfails"] >= 1 for i in infos), infos
+    finally:
+        ln.stop()
