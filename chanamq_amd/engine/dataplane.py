@@ -427,7 +427,7 @@ class GpuDataPlane(ControlState):
         """Recovery: enqueue stored messages into their queues in the given order.
         items: [(q_slot, msg_id, ts_ms, expire_ms, ex, rk, props, body, persistent, redelivered)]."""
         now = int(time.time() * 1000) if now_ms is None else int(now_ms)
-        if self.lag:
+        if self.lag and not self.native_xchg:   # native: the engine refuses it while an exchange is pending
             raise RuntimeError("restore() would overwrite the lagged exchange's pending imports")
         cap = max(1, min(self.info["restore_max"] or self.info["import_max"], self.info["import_max"]))
         room = self.info["xfer_bytes"]

@@ -50,6 +50,10 @@ class ControlLog:
                     res = self._apply(op, args, kw)
                 except ControlError as e:
                     res = ("error", e.code, e.text, e.class_id, e.method_id)
+                except Exception as e:   # a failing op must not read as a lost peer (_retry)
+                    import logging
+                    logging.getLogger("chanamq.control").exception("control op %s failed", op)
+                    res = ("error", C.INTERNAL_ERROR, f"{op}: {e}"[:255], 0, 0)
                 if self.on_applied is not None:
                     self.on_applied(op, args, kw, res)
                 self.applied += 1
