@@ -180,6 +180,59 @@ def run_one(core, name, spec, io, io_threads, seconds, rate=0.0, lg_threads=12, 
     return r
 
 
+def wal_soak(core, seconds, io_threads=4, lg_threads=12, cons_threads=8, rate=0.0):
+    """BASELINE config 4 over TCP for ``seconds`` with the store on disk: the WAL size is
+    sampled every second (background compaction keeps it bounded by the live rows), then
+    the store is reopened (WAL replay) and a fresh plane recovers from it -- the restart
+    cost after a long run."""
+    from chanamq_amd.engine.persistence import GpuPersistence
+    from chanamq_amd.server.gpu_broker import GpuBroker
+    spec = {k: v for k, v in SPECS["config4_durable_4KB_confirms"].items() if not k.startswith("_")}
+    d = tempfile.mkdtemp(prefix="cmq-wal-soak-")
+    store = core.Store()
+    store.open(d, True)
+    plane = plane_for(spec)
+    b = GpuBroker(plane, idle_step_ms=0.5, store=store, io="pipeline", io_threads=io_threads,
+                  per_conn_read=128 << 10).start()
+    samples, done = [], [False]
+    t0 = time.time()
+
+    def sample():
+        while not done[0]:
+            samples.append((round(time.time() - t0, 1), store.wal_bytes(), store.live_estimate(),
+                            store.compact_stats()["runs"]))
+            time.sleep(1.0)
+    import threading
+    th = threading.Thread(target=sample, daemon=True)
+    th.start()
+    try:
+        r = core.run_load(dict(port=b.port, seconds=seconds, warmup=1.0, queue="soak.q", exchange="soak.x",
+                               threads=lg_threads, consumer_threads=cons_threads, rate=rate, **spec))
+    finally:
+        done[0] = True
+        th.join()
+        b.stop()
+    cs = store.compact_stats()
+    wal_end = store.wal_bytes()
+    rows = {t: store.row_count(t) for t in ("msgs", "queues", "queue_unacks")}
+    store.close()
+    del plane
+    t1 = time.perf_counter()
+    st2 = core.Store()
+    st2.open(d, True)
+    replay_s = time.perf_counter() - t1
+    plane2 = plane_for(spec)
+    t2 = time.perf_counter()
+    recovered = GpuPersistence(plane2, st2).recover(int(time.time() * 1000))
+    recover_s = time.perf_counter() - t2
+    st2.close()
+    return dict(name="config4_wal_soak", seconds=seconds, recv_msgs_per_s=r["received"] / r["elapsed"],
+                confirmed_per_s=r["confirmed"] / r["elapsed"], error=r["error"], wal_samples=samples,
+                wal_end_bytes=wal_end, rows_at_end=rows, compactions=cs, reopen_replay_s=replay_s,
+                recover_s=recover_s, recovered_msgs=recovered,
+                body_bytes_written=getattr(b, "_pw_stats", {}).get("body_bytes"))
+
+
 def run_sharded(core, name, spec, world, mode, seconds, rate=0.0, io_threads=2, lg_threads=12, cons_threads=8):
     """The pipelined sharded server (server/sharded.py, ``world`` rank processes on this
     one GPU, shared-memory exchange): the topology is declared on rank 0 (its queues live
@@ -235,6 +288,9 @@ def main():
     ap.add_argument("--rates", default="", help="comma list of aggregate publish rates (msgs/s) to run paced")
     ap.add_argument("--paced", type=float, default=0.5,
                     help="re-run each spec with producers paced at this fraction of the measured rate (0 = off)")
+    ap.add_argument("--wal-soak", type=float, default=0,
+                    help="run config 4 for this many seconds with the store on disk, sample the WAL, "
+                         "then time the reopen + recovery")
     ap.add_argument("--sharded", type=int, default=0,
                     help="N > 1: the pipelined sharded server with N ranks on this GPU (producers on rank 1, "
                          "consumers on rank 0 and then on rank 1 through device links)")
@@ -243,6 +299,14 @@ def main():
         FE_CFG.update(wblock_high=args.wblock_high, wblock_low=args.wblock_high // 4)
     core = load()
     results = []
+    if args.wal_soak > 0:
+        import torch  # noqa: F401
+        r = wal_soak(core, args.wal_soak, io_threads=int(args.io_threads.split(",")[0]))
+        print(json.dumps({k: v for k, v in r.items() if k != "wal_samples"}), flush=True)
+        if args.out:
+            with open(args.out, "w") as f:
+                json.dump(r, f, indent=1)
+        return
     if args.sharded > 1:
         keys = ("name", "world", "consumers_on", "recv_msgs_per_s", "sent_msgs_per_s", "confirmed_per_s", "p50_us",
                 "p99_us", "error", "ranks")

@@ -1172,9 +1172,11 @@ void Frontend::stepper_sharded() {
     f.segs = std::move(seglens);
     f.gen.resize(c_max_);
     for (u32 k = 0; k < c_max_; ++k) f.gen[k] = conns_[k]->gen.load();
-    // ---- exchange of step t-1, then phase B of t
-    const bool want_sync = sync_req_.exchange(false);
-    u32 flags = (want_sync ? XF_SYNC : 0u) | (local_busy ? XF_BUSY : 0u), orf = flags;
+    // ---- exchange of step t-1, then phase B of t.  A sync request only counts once it
+    // travelled in an exchange: the first step after a sync has none, and a rank must
+    // never park for a sync its peers did not see
+    const bool want_sync = sync_req_.load();
+    u32 flags = (want_sync ? XF_SYNC : 0u) | (local_busy ? XF_BUSY : 0u), orf = flags & ~XF_SYNC;
     bool xfail = false;
     i64 t2 = now_ns();
     if (xpend_ >= 0) {
@@ -1183,6 +1185,8 @@ void Frontend::stepper_sharded() {
       if (rc == -2) {
         xfail = true;
         if (!check(api_->drop_exchange(api_->eng, xpend_))) break;
+      } else if (orf & XF_SYNC) {
+        sync_req_ = false;   // served by this sync (later requests join its control batch)
       }
     }
     double tx = secs_since(t2);

@@ -25,7 +25,7 @@ def main():
     with open(out + ".tmp", "w") as f:
         f.write(str(fe.port))
     os.replace(out + ".tmp", out)
-    conns, waiting = set(), []
+    conns, waiting, chain = set(), [], 0
     deadline = time.time() + 120
     while time.time() < deadline and not os.path.exists(out + ".stop"):
         for kind, conn, a, b, data, data2 in fe.poll_events(20):
@@ -37,6 +37,7 @@ def main():
                 fe.close(conn)
             elif kind == FE_CTRL:
                 waiting.append(conn)
+                chain = 1       # a second sync requested while the first is handled
                 fe.request_sync()
             elif kind in (FE_SYNC, FE_XFAIL):
                 if kind == FE_XFAIL:   # the peer is gone: this rank goes on alone
@@ -44,6 +45,9 @@ def main():
                 tag = b"SYNC" if kind == FE_SYNC else b"FAILOVER"
                 for c in sorted(conns):
                     fe.send(c, tag + str(a).encode() + b";")
+                if kind == FE_SYNC and chain:
+                    chain -= 1
+                    fe.request_sync()
                 for c in waiting:
                     eng.unpause(c)
                     fe.kick(c)

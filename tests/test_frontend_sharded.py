@@ -84,13 +84,16 @@ def test_lockstep_exchange_sync_and_failover(ranks):
         c0.sendall(b"XR1m%03d." % i)
     got = _read_until(c1, b"m049.")
     assert [int(x) for x in re.findall(rb"m(\d{3})\.", got)] == list(range(50))
-    # a control command on rank 1: both ranks park at the same step
+    # a control command on rank 1: both ranks park at the same step, twice in a row (the
+    # second sync is requested while the first is handled, as an owner's link_got answer)
     c1.sendall(b"CTRL")
-    s1 = _read_until(c1, b";")
-    s0 = _read_until(c0, b";")
-    n1 = int(s1[s1.index(b"SYNC") + 4:s1.index(b";", s1.index(b"SYNC"))])
-    n0 = int(s0[s0.index(b"SYNC") + 4:s0.index(b";", s0.index(b"SYNC"))])
-    assert n0 == n1 and n0 > 0
+    s1 = _read_until(c1, b";", timeout=10)
+    s1 += _read_until(c1, b";") if s1.count(b";") < 2 else b""
+    s0 = _read_until(c0, b";", timeout=10)
+    s0 += _read_until(c0, b";") if s0.count(b";") < 2 else b""
+    n1 = [int(x) for x in re.findall(rb"SYNC(\d+);", s1)]
+    n0 = [int(x) for x in re.findall(rb"SYNC(\d+);", s0)]
+    assert n0 == n1 and len(n0) == 2 and n0[0] > 0 and n0[1] > n0[0], (s0, s1)
     c1.sendall(b"after-sync")
     _read_until(c1, b"after-sync")
     # rank 1 dies: rank 0's next exchange times out, it fails over and serves alone

@@ -227,7 +227,12 @@ def test_pipelined_rank_death_durable_redelivery(tmp_path):
         assert got is not None, [json.load(open(tmp_path / f"rank{r}.json")) for r in range(2)]
         assert sorted(got) == sorted(b"m%d" % i for i in range(20))
         assert got[:5] == [b"m%d" % i for i in range(5)] and all(red[:5]) and not any(red[5:])
-        infos = [json.load(open(tmp_path / f"rank{r}.json")) for r in range(2)]
+        end = time.time() + 10   # the rank files refresh every 0.5 s
+        while True:
+            infos = [json.load(open(tmp_path / f"rank{r}.json")) for r in range(2)]
+            if all(i["failovers"] == 1 for i in infos) or time.time() > end:
+                break
+            time.sleep(0.3)
         assert all(i["failovers"] == 1 for i in infos), infos
         assert all(i["front_end"]["xfails"] >= 1 for i in infos), infos
     finally:
