@@ -67,9 +67,10 @@ def main():
         for r, dp in enumerate(planes):
             pool, segs, offs, blens = work[r][:4]
             tickets.append(dp.submit_raw(segs[b], pool.ctypes.data + offs[b], blens[b]))
-        recv = local_exchange(planes)
+        recv = local_exchange(planes) if W > 1 else None   # world 1: no phase B
         for r, dp in enumerate(planes):
-            dp.set_import(recv[r])
+            if recv is not None:
+                dp.set_import(recv[r])
             res = dp.finish(tickets[r], collect=False, wait_egress=True)
             delivered += res.counters["n_deliv"]
         step_i += 1
