@@ -623,17 +623,24 @@ void Frontend::io_loop(int i) {
       io.phase_seen = ph;
       io.segs.clear();
       // scatter: the egress of finished steps, in step order, for this thread's connections
-      for (Scatter* sc : *ph_scat_) {
-        const u8* base = sc->own.empty() ? sc->egress : (const u8*)sc->own.data();
-        for (u32 id : io.owned) {
-          const ConnOut& o = sc->co[id];
-          if (o.len) {
-            FeConn& c = *conns_[id];
-            if (!sc->gen.empty() && sc->gen[id] != c.gen.load()) continue;   // closed since: stale
-            if (c.mode == M_DATA || c.mode == M_HOST) scatter_conn(c, base + o.off, o.len);
+      // (async phase: after the gather has released the stepper; the Scatter objects live
+      // in out_prev_ until every IO thread has passed the next phase)
+      const std::vector<Scatter*> scat = *ph_scat_;
+      const bool async = ph_async_;
+      auto scatter = [&] {
+        for (Scatter* sc : scat) {
+          const u8* base = sc->own.empty() ? sc->egress : (const u8*)sc->own.data();
+          for (u32 id : io.owned) {
+            const ConnOut& o = sc->co[id];
+            if (o.len) {
+              FeConn& c = *conns_[id];
+              if (!sc->gen.empty() && sc->gen[id] != c.gen.load()) continue;   // closed since: stale
+              if (c.mode == M_DATA || c.mode == M_HOST) scatter_conn(c, base + o.off, o.len);
+            }
           }
         }
-      }
+      };
+      if (!async) scatter();
       if (ph_gather_) {
         std::vector<u32> keep;
         for (u32 id : io.ready) {
@@ -649,6 +656,7 @@ void Frontend::io_loop(int i) {
         std::lock_guard<std::mutex> g(ph_mu_);
         ph_cv_.notify_all();
       }
+      if (async) scatter();
     }
     if (!run && stepper_done_) break;
     // ---- heartbeats (every 100 ms): send when idle for hb/2, drop after 2*hb of silence
@@ -751,9 +759,10 @@ void Frontend::gather_conn(FeIo& io, FeConn& c, u8* arena, u64 cap) {
   if (eof && !c.in_ready) drop(c, true);
 }
 
-void Frontend::io_phase(std::vector<Scatter*>& scat, bool gather) {
+void Frontend::io_phase(std::vector<Scatter*>& scat, bool gather, bool async) {
   ph_scat_ = &scat;
   ph_gather_ = gather;
+  ph_async_ = async && gather && !scat.empty();
   ph_arena_ = arena_[arena_i_];
   ph_cap_ = api_->ingress_cap;
   if (api_->log_bytes) {
@@ -776,8 +785,15 @@ void Frontend::io_phase(std::vector<Scatter*>& scat, bool gather) {
   ph_left_ = (int)io_.size();
   ph_id_.fetch_add(1, std::memory_order_release);
   for (auto& io : io_) poke(io->evfd);
-  std::unique_lock<std::mutex> g(ph_mu_);
-  ph_cv_.wait(g, [&] { return ph_left_.load() == 0; });
+  {
+    std::unique_lock<std::mutex> g(ph_mu_);
+    ph_cv_.wait(g, [&] { return ph_left_.load() == 0; });
+  }
+  // every IO thread passed this phase, so the previous async scatter is written; this
+  // phase's egress stays alive while the IO threads write it (async) or is done
+  out_prev_.clear();
+  if (ph_async_) out_prev_.swap(out_);
+  out_.clear();
 }
 
 // ============================================================================ stepper
@@ -975,9 +991,8 @@ void Frontend::stepper() {
     std::vector<Scatter*> scat;
     if (!collect_scatter(scat)) break;
     i64 t0 = now_ns();
-    io_phase(scat, true);
+    io_phase(scat, true, cfg_.async_scatter);
     double tio = secs_since(t0);
-    scat_done();
     std::vector<SegIn> segs;
     std::vector<std::pair<u32, u32>> seglens;
     for (auto& io : io_) {
@@ -1141,9 +1156,8 @@ void Frontend::stepper_sharded() {
     std::vector<Scatter*> scat;
     if (!collect_scatter(scat)) break;
     i64 t0 = now_ns();
-    io_phase(scat, true);
+    io_phase(scat, true);   // sync: flush steps may reuse egress slots before the next phase
     double tio = secs_since(t0);
-    scat_done();
     std::vector<SegIn> segs;
     std::vector<std::pair<u32, u32>> seglens;
     for (auto& io : io_) {
@@ -1361,8 +1375,9 @@ void Frontend::flush_pending(bool final) {
   }
   std::vector<Scatter*> scat;
   if (!collect_scatter(scat)) return;
-  if (!scat.empty()) io_phase(scat, false);
-  scat_done();
+  // an empty phase still waits out the last async scatter: control replies written after
+  // this are ordered behind every earlier delivery
+  if (!scat.empty() || !out_prev_.empty()) io_phase(scat, false);
 }
 
 // ============================================================================ EchoEngine

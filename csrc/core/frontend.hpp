@@ -85,6 +85,10 @@ struct FrontendCfg {
   bool reuseport = false;
   int sndbuf = 4 << 20, rcvbuf = 4 << 20;
   u64 wblock_high = 8 << 20, wblock_low = 2 << 20;   // egress back-pressure watermarks per connection
+  // gather phases of the (unsharded) stepper: each IO thread releases the stepper once its
+  // connections are gathered and writes the finished step's egress after that, while the
+  // step is submitted (the sockets' send path no longer sits on the step's critical path)
+  bool async_scatter = true;
 };
 
 struct FeStats {
@@ -165,11 +169,10 @@ class Frontend {
   void drain(std::deque<Inflight>& inflight);
   bool fault_due();
   void io_loop(int i);
-  void io_phase(std::vector<Scatter*>& scat, bool gather);
+  void io_phase(std::vector<Scatter*>& scat, bool gather, bool async = false);
   void finish_oldest(std::deque<Inflight>& inflight);
   bool collect_scatter(std::vector<Scatter*>& scat);
   bool stash_pend(bool copy);
-  void scat_done() { out_.clear(); }
   void flush_pending(bool final);
   bool releasable() const;
   bool any_data_conn() const;
@@ -204,7 +207,7 @@ class Frontend {
   std::atomic<u64> ph_id_{0};
   std::atomic<int> ph_left_{0};
   std::vector<Scatter*>* ph_scat_ = nullptr;
-  bool ph_gather_ = false;
+  bool ph_gather_ = false, ph_async_ = false;
   u8* ph_arena_ = nullptr;
   u64 ph_cap_ = 0;
   std::atomic<u64> ph_used_{0};
@@ -230,6 +233,9 @@ class Frontend {
   u64 pend_bytes_ = 0;
   bool last_busy_ = false, idle_tick_ = false;
   std::deque<Scatter> out_;   // egress being written in the current IO phase
+  // egress of the last async-scatter phase: IO threads may still be writing it until every
+  // one of them has passed the next phase (io_phase frees it then)
+  std::deque<Scatter> out_prev_;
   std::atomic<bool> stepper_done_{false};
 
   // persistence write-behind

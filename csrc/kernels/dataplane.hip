@@ -315,9 +315,9 @@ DEV bool topic_match(const u8* pat, u32 plen, const u8* key, u32 klen, bool hash
 // segments before it) itself, and block (0, 0) resets the step counters
 __global__ __launch_bounds__(256) void k_stage(DS d) {
   __shared__ u32 lds[256 / 64 + 1];
-  const u32 s = blockIdx.x, tid = threadIdx.x;
+  const u32 tid = threadIdx.x;
   const u32 nseg = d.in->nseg;
-  const bool head = s == 0 && blockIdx.y == 0;
+  const bool head = blockIdx.x == 0 && blockIdx.y == 0;
   if (head) {
     u32* c = (u32*)d.ctr;
     for (u32 k = tid; k < sizeof(Counters) / 4; k += 256)
@@ -333,29 +333,30 @@ __global__ __launch_bounds__(256) void k_stage(DS d) {
       *d.id_next = cur > floor_pos ? cur : floor_pos;
     }
   }
-  if (s >= nseg && !head) return;
-  u32 before = 0, total = 0;
-  for (u32 k = tid; k < nseg; k += 256) {
-    const u32 sz = align16(d.carry_len[d.segs[k].conn] + d.segs[k].len + 32);
-    total += sz;
-    before += k < s ? sz : 0u;
-  }
-  u32 all_b, all_t;
-  block_scan<256>(before, lds, all_b);
-  __syncthreads();
+  if (blockIdx.x >= nseg && !head) return;
+  u32 total = 0;
+  for (u32 k = tid; k < nseg; k += 256) total += align16(d.carry_len[d.segs[k].conn] + d.segs[k].len + 32);
+  u32 all_t;
   block_scan<256>(total, lds, all_t);
   if (head && tid == 0) d.tot[15] = all_t;  // work bytes used
-  if (s >= nseg) return;
-  const u32 conn = d.segs[s].conn;
-  const u32 cl = d.carry_len[conn];
-  const u32 len = d.segs[s].len;
-  if (blockIdx.y == 0 && tid == 0) { d.seg_total[s] = cl + len; d.seg_start[s] = all_b; }
   if (all_t > d.work_cap) return;  // host sizes steps so this never triggers
-  u8* dst = d.work + all_b;
-  u32 part = blockIdx.y, nparts = gridDim.y;
-  u32 t = tid + part * 256, nt = 256 * nparts;
-  if (cl) block_copy(dst, d.carry + (u64)conn * d.carry_cap, cl, t, nt);
-  if (len) block_copy(dst + cl, d.ingress + d.segs[s].src, len, t, nt);
+  // block-stride over the segments (the grid is capped: seg_max blocks would mostly idle)
+  for (u32 s = blockIdx.x; s < nseg; s += gridDim.x) {
+    u32 before = 0;
+    for (u32 k = tid; k < s; k += 256) before += align16(d.carry_len[d.segs[k].conn] + d.segs[k].len + 32);
+    u32 all_b;
+    __syncthreads();   // lds of the previous scan
+    block_scan<256>(before, lds, all_b);
+    const u32 conn = d.segs[s].conn;
+    const u32 cl = d.carry_len[conn];
+    const u32 len = d.segs[s].len;
+    if (blockIdx.y == 0 && tid == 0) { d.seg_total[s] = cl + len; d.seg_start[s] = all_b; }
+    u8* dst = d.work + all_b;
+    u32 part = blockIdx.y, nparts = gridDim.y;
+    u32 t = tid + part * 256, nt = 256 * nparts;
+    if (cl) block_copy(dst, d.carry + (u64)conn * d.carry_cap, cl, t, nt);
+    if (len) block_copy(dst + cl, d.ingress + d.segs[s].src, len, t, nt);
+  }
 }
 
 // ============================================================================ K1 frame scan
@@ -430,7 +431,7 @@ constexpr u32 FS_AM_MAX = 8192;  // 128 KB segment; 16 KB of LDS
 // one block of FS_NT threads per segment: 16 waves (4 per SIMD) hide the screen's
 // dependent integer chains, which one wave per SIMD could not
 #define FS_NT 1024
-__global__ __launch_bounds__(FS_NT) void k_frame_scan(DS d) {
+DEV void frame_scan_seg(const DS& d, const u32 s) {
   __shared__ u32 cpos[CAND_MAX];
   __shared__ int16_t csucc[CAND_MAX];
   // chain (first written in phase c) aliases amask (used only in phase a, which ends on
@@ -446,8 +447,6 @@ __global__ __launch_bounds__(FS_NT) void k_frame_scan(DS d) {
   __shared__ u32 sh_m, sh_over, sh_ok, sh_nf, sh_stop, sh_brk;
   __shared__ u32 sh_cmd_base, sh_frag_base, sh_ncmd;
 
-  const u32 s = blockIdx.x;
-  if (s >= d.in->nseg) return;
   const u32 tid = threadIdx.x;
   const u32 conn = d.segs[s].conn;
   const u32 L = d.seg_total[s];
@@ -958,6 +957,16 @@ __global__ __launch_bounds__(FS_NT) void k_frame_scan(DS d) {
 #undef CPOS
 }
 
+// block-stride over the segments: the grid is capped below seg_max (a 1024-thread block
+// per segment slot of the capacity would mostly launch idle waves)
+__global__ __launch_bounds__(FS_NT) void k_frame_scan(DS d) {
+  const u32 nseg = d.in->nseg;
+  for (u32 s = blockIdx.x; s < nseg; s += gridDim.x) {
+    frame_scan_seg(d, s);
+    __syncthreads();   // the next segment reuses the LDS
+  }
+}
+
 // ============================================================================ K3 classify / decode
 DEV void set_counts(const DS& d) {
   u32 np = d.tot[4], na = d.tot[5];
@@ -1209,8 +1218,10 @@ struct ScanArgs { const u32* in[4]; u32* out[4]; const u32* n; const u32* lo; u3
 // tiles whose blocks are already running.
 //   status word = epoch << 34 | flag << 32 | value   (flag 1 = aggregate, 2 = inclusive)
 #define SCAN_TILE 4096
+// one tile of the scan (1024 threads); true (block-uniform) in the block that holds the
+// last data tile, after its totals are written
 template <int NA, int EPT>
-__global__ __launch_bounds__(1024) void k_scan(ScanArgs a, u32* tot, u64* status, u32* ctl, u32 smax) {
+DEV bool scan_tile(const ScanArgs& a, u32* tot, u64* status, u32* ctl, u32 smax) {
   constexpr u32 TILE = 1024 * EPT;
   __shared__ u32 s_tile, s_epoch;
   __shared__ u32 s_excl[NA];
@@ -1230,7 +1241,8 @@ __global__ __launch_bounds__(1024) void k_scan(ScanArgs a, u32* tot, u64* status
   const u32 lo = a.lo ? *a.lo : 0u;
   n = n > lo ? n - lo : 0;
   const u32 base = tile * TILE;
-  if (base < n || (tile == 0)) {
+  const bool data = base < n || tile == 0;
+  if (data) {
     const u32 i = base + tid * EPT;
     u32 v[NA][EPT], off[NA], sm[NA];
     // every array's loads in flight at once, then one block scan of the sums together
@@ -1287,13 +1299,15 @@ __global__ __launch_bounds__(1024) void k_scan(ScanArgs a, u32* tot, u64* status
     if (wv < a.narr && wv < (u32)NA) {
       const u32 k = wv;
       const u32 A = wsum[k][1024 / 64];   // the tile's aggregate of array k
-      // agent-scope acquire/release: the tiles run on different XCDs (separate L2s)
+      // agent-scope (coherent across the XCDs' L2s) relaxed status words: a word carries
+      // its own value, nothing else has to become visible with it, so no release fence
+      // (an agent-scope release writes back the whole L2: ~1 us per tile, measured)
       u64* st = status + (u64)k * smax;
       const u64 tag = (u64)epoch << 34;
       u32 excl = 0;
       if (tile > 0) {
         if (lane == 0)
-          __hip_atomic_store(&st[tile], tag | (1ull << 32) | A, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(&st[tile], tag | (1ull << 32) | A, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         u32 top = tile;   // predecessors [0, top) not yet summed
         while (top > 0) {
           const bool has = lane < top;
@@ -1301,7 +1315,7 @@ __global__ __launch_bounds__(1024) void k_scan(ScanArgs a, u32* tot, u64* status
           u64 w = 0;
           if (has) {
             do {
-              w = __hip_atomic_load(&st[j], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+              w = __hip_atomic_load(&st[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             } while ((w >> 34) != epoch || ((w >> 32) & 3) == 0);
           }
           const u64 incl = __ballot(has && ((w >> 32) & 3) == 2);
@@ -1315,7 +1329,7 @@ __global__ __launch_bounds__(1024) void k_scan(ScanArgs a, u32* tot, u64* status
         }
       }
       if (lane == 0) {
-        __hip_atomic_store(&st[tile], tag | (2ull << 32) | (excl + A), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&st[tile], tag | (2ull << 32) | (excl + A), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         s_excl[k] = excl;
         if (base + TILE >= n) tot[a.tot_slot + k] = excl + A;   // the last data tile
       }
@@ -1349,24 +1363,70 @@ __global__ __launch_bounds__(1024) void k_scan(ScanArgs a, u32* tot, u64* status
     atomicExch(&ctl[0], 0u);
     atomicExch(&ctl[1], epoch + 1);
   }
+  return data && base + TILE >= n;
+}
+
+template <int NA, int EPT>
+__global__ __launch_bounds__(1024) void k_scan(ScanArgs a, u32* tot, u64* status, u32* ctl, u32 smax) {
+  (void)scan_tile<NA, EPT>(a, tot, status, ctl, smax);
+}
+
+// the route phase's scan (pub_nq, pub_slot, pub_routed, pub_ret_sz) with the phase's
+// body-log / message-table reservation done by the block of the last data tile once its
+// totals are out (fused: k_route<1> used to reserve, so k_route<1> + k_store can be one)
+DEV void log_reserve(const DS& d);
+__global__ __launch_bounds__(1024) void k_scan_route(ScanArgs a, u32* tot, u64* status, u32* ctl, u32 smax, DS d) {
+  const bool last = scan_tile<4, 4>(a, tot, status, ctl, smax);
+  if (last) {
+    __syncthreads();   // the totals (tot[0..3]) were written by lane 0 of waves 0..3
+    if (threadIdx.x == 0) log_reserve(d);
+  }
 }
 
 // ============================================================================ radix sort
 // stable LSD radix sort of (key, val) u32 pairs, DB bits per pass (8, or 11 for keys of
 // 9..11 bits -- queue << rank_bits | rank at 4..8 GPUs -- in one pass instead of two);
 // n from device.  Per-tile digit histograms; the last occupied tile to finish turns them
-// into the digit-major offsets of the occupied tiles (fused k_rs_offsets)
-// hist is tile-major (hist[t * D + digit]: each tile writes, and the offsets pass reads,
-// contiguous words); hscan is digit-major (hscan[digit * ntiles + t]) for the scatter and
-// for the queue starts (k_ring_plan / k_enqueue read tile 0 of a digit)
+// into the offsets of the occupied tiles (fused k_rs_offsets).  hist and hscan are both
+// tile-major (hist[t * D + digit], hscan[t * D + digit]): the tiles write and the offsets
+// pass reads / writes contiguous words, and the queue starts (k_ring_plan / k_enqueue) are
+// row 0.  The offsets block keeps up to RS_RT tiles' counts in registers: one round of
+// loads, one block scan, one round of stores.
+constexpr u32 RS_RT = 16;
+template <int DB> struct RsNt { static constexpr u32 v = DB > 8 ? 1024u : 256u; };
 template <int DB>
-DEV void rs_offsets(const u32* hist, u32* hscan, u32 T, u32 ntiles, u32* lds) {
-  constexpr u32 D = 1u << DB, PER = D / 256;   // consecutive digits per thread
+DEV void rs_offsets(const u32* hist, u32* hscan, u32 T, u32* lds) {
+  constexpr u32 NT = RsNt<DB>::v, D = 1u << DB, PER = D / NT;   // consecutive digits per thread
   const u32 d0 = threadIdx.x * PER;
   u32 tot[PER];
 #pragma unroll
   for (u32 j = 0; j < PER; ++j) tot[j] = 0;
-  // tiles RB at a time: RB * PER independent loads in flight per round trip
+  if (T <= RS_RT) {
+    u32 h[RS_RT][PER];
+#pragma unroll
+    for (u32 a = 0; a < RS_RT; ++a)
+#pragma unroll
+      for (u32 j = 0; j < PER; ++j) h[a][j] = a < T ? hist[a * D + d0 + j] : 0u;
+#pragma unroll
+    for (u32 a = 0; a < RS_RT; ++a)
+#pragma unroll
+      for (u32 j = 0; j < PER; ++j) tot[j] += h[a][j];
+    u32 sum = 0;
+#pragma unroll
+    for (u32 j = 0; j < PER; ++j) sum += tot[j];
+    u32 all;
+    u32 run = block_scan<NT>(sum, lds, all);
+#pragma unroll
+    for (u32 j = 0; j < PER; ++j) { const u32 x = tot[j]; tot[j] = run; run += x; }   // digit starts
+#pragma unroll
+    for (u32 a = 0; a < RS_RT; ++a) {
+      if (a >= T) break;
+#pragma unroll
+      for (u32 j = 0; j < PER; ++j) { hscan[a * D + d0 + j] = tot[j]; tot[j] += h[a][j]; }
+    }
+    return;
+  }
+  // many tiles: two passes over the histograms, RB tiles at a time
   constexpr u32 RB = 8;
   u32 t = 0;
   for (; t + RB <= T; t += RB) {
@@ -1388,63 +1448,54 @@ DEV void rs_offsets(const u32* hist, u32* hscan, u32 T, u32 ntiles, u32* lds) {
 #pragma unroll
   for (u32 j = 0; j < PER; ++j) sum += tot[j];
   u32 all;
-  u32 run = block_scan<256>(sum, lds, all);
+  u32 run = block_scan<NT>(sum, lds, all);
 #pragma unroll
   for (u32 j = 0; j < PER; ++j) { const u32 x = tot[j]; tot[j] = run; run += x; }   // digit starts
-  t = 0;
-  for (; t + RB <= T; t += RB) {
-    u32 h[RB][PER];
+  for (t = 0; t < T; ++t) {
+    u32 h[PER];
 #pragma unroll
-    for (u32 a = 0; a < RB; ++a)
+    for (u32 j = 0; j < PER; ++j) h[j] = hist[t * D + d0 + j];
 #pragma unroll
-      for (u32 j = 0; j < PER; ++j) h[a][j] = hist[(t + a) * D + d0 + j];
-#pragma unroll
-    for (u32 a = 0; a < RB; ++a)
-#pragma unroll
-      for (u32 j = 0; j < PER; ++j) {
-        hscan[(d0 + j) * ntiles + t + a] = tot[j];
-        tot[j] += h[a][j];
-      }
-  }
-  for (; t < T; ++t) {
-#pragma unroll
-    for (u32 j = 0; j < PER; ++j) {
-      const u32 h = hist[t * D + d0 + j];
-      hscan[(d0 + j) * ntiles + t] = tot[j];
-      tot[j] += h;
-    }
+    for (u32 j = 0; j < PER; ++j) { hscan[t * D + d0 + j] = tot[j]; tot[j] += h[j]; }
   }
 }
 
 template <int DB>
-__global__ __launch_bounds__(256) void k_rs_hist(const u32* keys, const u32* np, u32 shift, u32* hist,
-                                                 u32* hscan, u32* ticket, u32 ntiles) {
-  constexpr u32 D = 1u << DB;
+__global__ __launch_bounds__(RsNt<DB>::v) void k_rs_hist(const u32* keys, const u32* np, u32 shift, u32* hist,
+                                                        u32* hscan, u32* ticket, u32 ntiles) {
+  constexpr u32 NT = RsNt<DB>::v, D = 1u << DB;
   __shared__ u32 cnt[D];
-  __shared__ u32 lds[256 / 64 + 1];
+  __shared__ u32 lds[NT / 64 + 1];
   __shared__ u32 s_last;
   u32 tid = threadIdx.x, t = blockIdx.x;
   u32 n = *np;
   u32 T = (n + SORT_TILE - 1) / SORT_TILE;
   if (T > ntiles) T = ntiles;
   if (t >= T) return;   // only occupied tiles take part (and take a ticket)
-  for (u32 k = tid; k < D; k += 256) cnt[k] = 0;
-  __syncthreads();
-  u32 base = t * SORT_TILE;
-  for (u32 j = 0; j < SORT_TILE / 256; ++j) {
-    u32 i = base + j * 256 + tid;
-    if (i < n) atomicAdd(&cnt[(keys[i] >> shift) & (D - 1)], 1u);
+  bool last = false;
+  for (; t < T; t += gridDim.x) {   // tile-stride: the grid is capped below ntiles
+    for (u32 k = tid; k < D; k += NT) cnt[k] = 0;
+    __syncthreads();
+    u32 base = t * SORT_TILE;
+    for (u32 j = 0; j < SORT_TILE / NT; ++j) {
+      u32 i = base + j * NT + tid;
+      if (i < n) atomicAdd(&cnt[(keys[i] >> shift) & (D - 1)], 1u);
+    }
+    __syncthreads();
+    // agent-coherent stores + a workgroup-scope release (wait for them) before the
+    // ticket: no L2 writeback per tile (__threadfence: +11 us at 15 tiles, measured)
+    for (u32 k = tid; k < D; k += NT)
+      __hip_atomic_store(&hist[t * D + k], cnt[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __syncthreads();
+    if (tid == 0) s_last = atomicAdd(ticket, 1u) == T - 1;
+    __syncthreads();
+    last = last || s_last;
   }
-  __syncthreads();
-  for (u32 k = tid; k < D; k += 256) hist[t * D + k] = cnt[k];
-  __threadfence();
-  __syncthreads();
-  if (tid == 0) s_last = atomicAdd(ticket, 1u) == T - 1;
-  __syncthreads();
-  if (!s_last) return;
-  __threadfence();
+  if (!last) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   if (tid == 0) *ticket = 0;
-  rs_offsets<DB>(hist, hscan, T, ntiles, lds);
+  rs_offsets<DB>(hist, hscan, T, lds);
 }
 
 template <int DB>
@@ -1453,55 +1504,57 @@ __global__ __launch_bounds__(256) void k_rs_scatter(const u32* kin, const u32* v
                                                     u32 ntiles) {
   constexpr u32 D = 1u << DB;
   __shared__ u32 wc[4][D];
-  u32 tid = threadIdx.x, t = blockIdx.x, w = tid >> 6, lane = tid & 63;
-  u32 n = *np;
-  u32 base = t * SORT_TILE;
-  if (base >= n) return;
-  for (u32 i = tid; i < 4 * D; i += 256) ((u32*)wc)[i] = 0;
-  __syncthreads();
-  u32 wbase = base + w * (SORT_TILE / 4);
-  // pass 1: per-wave digit counts
-  for (u32 c = 0; c < SORT_TILE / 256; ++c) {
-    u32 i = wbase + c * 64 + lane;
-    bool valid = i < n;
-    u32 dg = valid ? (kin[i] >> shift) & (D - 1) : 0;
-    u64 peers = __ballot(valid);
+  const u32 tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+  const u32 n = *np;
+  for (u32 t = blockIdx.x; t * SORT_TILE < n; t += gridDim.x) {   // tile-stride (capped grid)
+    const u32 base = t * SORT_TILE;
+    __syncthreads();   // wc of the previous tile
+    for (u32 i = tid; i < 4 * D; i += 256) ((u32*)wc)[i] = 0;
+    __syncthreads();
+    u32 wbase = base + w * (SORT_TILE / 4);
+    // pass 1: per-wave digit counts
+    for (u32 c = 0; c < SORT_TILE / 256; ++c) {
+      u32 i = wbase + c * 64 + lane;
+      bool valid = i < n;
+      u32 dg = valid ? (kin[i] >> shift) & (D - 1) : 0;
+      u64 peers = __ballot(valid);
 #pragma unroll
-    for (u32 bb = 0; bb < DB; ++bb) {
-      u64 m = __ballot((dg >> bb) & 1);
-      peers &= ((dg >> bb) & 1) ? m : ~m;
+      for (u32 bb = 0; bb < DB; ++bb) {
+        u64 m = __ballot((dg >> bb) & 1);
+        peers &= ((dg >> bb) & 1) ? m : ~m;
+      }
+      bool leader = valid && ((peers & lanemask_lt()) == 0);
+      if (leader) wc[w][dg] += __popcll(peers);
+      __builtin_amdgcn_wave_barrier();
     }
-    bool leader = valid && ((peers & lanemask_lt()) == 0);
-    if (leader) wc[w][dg] += __popcll(peers);
-    __builtin_amdgcn_wave_barrier();
-  }
-  __syncthreads();
-  for (u32 dg = tid; dg < D; dg += 256) {
-    u32 run = hscan[dg * ntiles + t];
-    for (u32 ww = 0; ww < 4; ++ww) { u32 x = wc[ww][dg]; wc[ww][dg] = run; run += x; }
-  }
-  __syncthreads();
-  for (u32 c = 0; c < SORT_TILE / 256; ++c) {
-    u32 i = wbase + c * 64 + lane;
-    bool valid = i < n;
-    u32 key = valid ? kin[i] : 0;
-    u32 dg = (key >> shift) & (D - 1);
-    u64 peers = __ballot(valid);
+    __syncthreads();
+    for (u32 dg = tid; dg < D; dg += 256) {
+      u32 run = hscan[t * D + dg];
+      for (u32 ww = 0; ww < 4; ++ww) { u32 x = wc[ww][dg]; wc[ww][dg] = run; run += x; }
+    }
+    __syncthreads();
+    for (u32 c = 0; c < SORT_TILE / 256; ++c) {
+      u32 i = wbase + c * 64 + lane;
+      bool valid = i < n;
+      u32 key = valid ? kin[i] : 0;
+      u32 dg = (key >> shift) & (D - 1);
+      u64 peers = __ballot(valid);
 #pragma unroll
-    for (u32 bb = 0; bb < DB; ++bb) {
-      u64 m = __ballot((dg >> bb) & 1);
-      peers &= ((dg >> bb) & 1) ? m : ~m;
+      for (u32 bb = 0; bb < DB; ++bb) {
+        u64 m = __ballot((dg >> bb) & 1);
+        peers &= ((dg >> bb) & 1) ? m : ~m;
+      }
+      u32 basepos = ((volatile u32*)wc[w])[dg];
+      u32 rank = __popcll(peers & lanemask_lt());
+      if (valid) {
+        kout[basepos + rank] = key;
+        vout[basepos + rank] = vin[i];
+      }
+      __builtin_amdgcn_wave_barrier();
+      bool leader = valid && ((peers & lanemask_lt()) == 0);
+      if (leader) ((volatile u32*)wc[w])[dg] = basepos + __popcll(peers);
+      __builtin_amdgcn_wave_barrier();
     }
-    u32 basepos = ((volatile u32*)wc[w])[dg];
-    u32 rank = __popcll(peers & lanemask_lt());
-    if (valid) {
-      kout[basepos + rank] = key;
-      vout[basepos + rank] = vin[i];
-    }
-    __builtin_amdgcn_wave_barrier();
-    bool leader = valid && ((peers & lanemask_lt()) == 0);
-    if (leader) ((volatile u32*)wc[w])[dg] = basepos + __popcll(peers);
-    __builtin_amdgcn_wave_barrier();
   }
 }
 
@@ -1770,17 +1823,15 @@ DEV void route_one(const DS& d, u32 p, u32 lane) {
   }
 }
 
-DEV void log_reserve(const DS& d);
-template <int PASS>
+// routing pass 0 (count queues, destination ranks); pass 1 runs fused with the store
+// (k_route_store) after k_scan_route reserved the phase's log region
 __global__ __launch_bounds__(256) void k_route(DS d) {
-  // pass 1 also reserves the phase's body-log region (consumed by k_store, next kernel)
-  if (PASS == 1 && blockIdx.x == 0 && threadIdx.x == 0) log_reserve(d);
   const u32 lane = lane_id();
   const u32 nw = (gridDim.x * blockDim.x) >> 6;
   u32 n = d.tot[TS_RANGE_HI];
   if (n > d.pub_cap) n = d.pub_cap;
   for (u32 p = d.tot[TS_RANGE_LO] + ((blockIdx.x * blockDim.x + threadIdx.x) >> 6); p < n; p += nw)
-    route_one<PASS>(d, p, lane);
+    route_one<0>(d, p, lane);
 }
 
 // reserve the step's contiguous body-log region and message-table indices
@@ -1839,17 +1890,21 @@ DEV void live_add_blocks(const DS& d, u32 lane) {
   }
 }
 
-// one wave per publish: allocate, fill MsgEnt, copy exchange/rk/props/body into the log
+// one wave per publish: write its queue pairs (route pass 1), then allocate the message,
+// fill its MsgEnt and copy exchange / rk / props / body into the log (fused k_route<1> +
+// k_store: one pass over the phase's publishes)
 DEV void store_one(const DS& d, u32 p, u32 lane);
 DEV void live_add_blocks(const DS& d, u32 lane);
-__global__ __launch_bounds__(256) void k_store(DS d) {
+__global__ __launch_bounds__(256) void k_route_store(DS d) {
   u32 lane = lane_id();
   if (blockIdx.x == 0 && threadIdx.x < 64) live_add_blocks(d, lane);
   u32 n = d.tot[TS_RANGE_HI];
   if (n > d.pub_cap) n = d.pub_cap;
   const u32 nw = (gridDim.x * blockDim.x) >> 6;
-  for (u32 p = d.tot[TS_RANGE_LO] + ((blockIdx.x * blockDim.x + threadIdx.x) >> 6); p < n; p += nw)
+  for (u32 p = d.tot[TS_RANGE_LO] + ((blockIdx.x * blockDim.x + threadIdx.x) >> 6); p < n; p += nw) {
+    route_one<1>(d, p, lane);
     store_one(d, p, lane);
+  }
 }
 
 DEV void store_one(const DS& d, u32 p, u32 lane) {
@@ -1920,56 +1975,136 @@ DEV void store_one(const DS& d, u32 p, u32 lane) {
 // destination-major so one RCCL all_to_all_single moves them.  Phase B imports the
 // received records as publishes and routes them against local queues only.
 
-// thread per local publish: record / payload bytes per destination rank
-__global__ void k_pack_count(DS d) {
-  u32 p = blockIdx.x * blockDim.x + threadIdx.x;
+// Per-destination record / byte offsets of the step's own publishes (phase A), without
+// any inter-block waiting: a block per 1024-publish tile ranks its records per wave and
+// destination (ballot: records, shuffle scan: payload bytes), scans the 16 waves' totals
+// in LDS and writes tile-relative offsets for the destinations each publish goes to, plus
+// the tile's 2W aggregates.  The last tile to finish (ticket) turns the aggregates into
+// per-tile prefixes (one wave per value, 64 tiles per round) and the totals
+// (tot[TS_XSCAN + 2r], tot[TS_XSCAN + 2r + 1]); k_pack adds the prefix of its tile.
+// The tile aggregates are agent-coherent relaxed stores ordered before the ticket by a
+// workgroup-scope release: no L2 writeback per tile.
+constexpr u32 PK_TILE = 1024;
+__global__ __launch_bounds__(1024) void k_pack_scan(DS d, u32* agg, u32* ticket) {
+  __shared__ u32 wtot[16][2 * WORLD_MAX];
+  __shared__ u32 s_last;
+  const u32 tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   u32 n = d.ctr->n_pubs;
-  if (p >= d.pub_max) return;
+  if (n > d.pub_max) n = d.pub_max;
+  const u32 W = d.world, V = 2 * W;
+  const u32 T = n ? (n + PK_TILE - 1) / PK_TILE : 1;   // tile 0 always runs (publishes totals)
+  const u32 tile = blockIdx.x;
+  if (tile >= T) return;
+  const u32 p = tile * PK_TILE + tid;
   u32 m = 0, sz = 0;
   if (p < n) {
     m = d.pub_rmask[p];
-    const Pub& pb = d.pubs[p];
-    sz = align16(pb.ex_len + pb.rk_len + pb.props_len + pb.body_size);
+    if (m) {
+      const Pub& pb = d.pubs[p];
+      sz = align16(pb.ex_len + pb.rk_len + pb.props_len + pb.body_size);
+    }
   }
-  for (u32 r = 0; r < d.world; ++r) {
-    u32 b = (m >> r) & 1;
-    d.xp_cnt[(u64)r * d.pub_cap + p] = b;
-    d.xp_byt[(u64)r * d.pub_cap + p] = b ? sz : 0;
+  u32 myc[WORLD_MAX], myb[WORLD_MAX];
+#pragma unroll
+  for (u32 r = 0; r < WORLD_MAX; ++r) {
+    myc[r] = myb[r] = 0;
+    if (r >= W) continue;
+    const u32 bit = (m >> r) & 1u;
+    const u64 bal = __ballot(bit);
+    myc[r] = (u32)__popcll(bal & lanemask_lt());
+    const u32 v = bit ? sz : 0u;
+    u32 x = v;
+#pragma unroll
+    for (u32 o = 1; o < 64; o <<= 1) {
+      const u32 y = __shfl_up(x, o, 64);
+      if (lane >= o) x += y;
+    }
+    myb[r] = x - v;
+    const u32 bt = (u32)__shfl((int)x, 63);
+    if (lane == 0) { wtot[w][2 * r] = (u32)__popcll(bal); wtot[w][2 * r + 1] = bt; }
+  }
+  __syncthreads();
+  if (tid < V) {   // value tid: exclusive offsets of the 16 waves, the tile aggregate
+    u32 run = 0;
+    for (u32 ww = 0; ww < 16; ++ww) { const u32 t = wtot[ww][tid]; wtot[ww][tid] = run; run += t; }
+    __hip_atomic_store(&agg[(u64)tile * 2 * WORLD_MAX + tid], run, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+#pragma unroll
+  for (u32 r = 0; r < WORLD_MAX; ++r) {
+    if (r >= W || !((m >> r) & 1u)) continue;
+    d.xp_cnt_off[(u64)r * d.pub_cap + p] = wtot[w][2 * r] + myc[r];
+    d.xp_byt_off[(u64)r * d.pub_cap + p] = wtot[w][2 * r + 1] + myb[r];
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");   // the agent-coherent agg stores are done
+  __syncthreads();
+  if (tid == 0) s_last = atomicAdd(ticket, 1u) == T - 1;
+  __syncthreads();
+  if (!s_last) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  if (tid == 0) *ticket = 0;
+  // aggregates -> per-tile exclusive prefixes, in place; totals
+  for (u32 v = w; v < V; v += 16) {
+    u32 carry = 0;
+    for (u32 t0 = 0; t0 < T; t0 += 64) {
+      const u32 t = t0 + lane;
+      const u32 a = t < T ? __hip_atomic_load(&agg[(u64)t * 2 * WORLD_MAX + v], __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_AGENT) : 0u;
+      u32 x = a;
+#pragma unroll
+      for (u32 o = 1; o < 64; o <<= 1) {
+        const u32 y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+      }
+      if (t < T) agg[(u64)t * 2 * WORLD_MAX + v] = carry + x - a;
+      carry += (u32)__shfl((int)x, 63);
+    }
+    if (lane == 0) d.tot[TS_XSCAN + v] = carry;
   }
 }
 
-// destination bases (exclusive scans over ranks) + host-visible send counts
-__global__ void k_pack_bases(DS d) {
-  if (threadIdx.x) return;
-  u32 dsum = 0, psum = 0;
-  for (u32 r = 0; r < d.world; ++r) {
-    u32 c = d.tot[TS_XSCAN + 2 * r], b = d.tot[TS_XSCAN + 2 * r + 1];
-    d.xs_base[r] = dsum;
-    d.xs_base[WORLD_MAX + r] = psum;
-    d.xchg[r] = c;
-    d.xchg[WORLD_MAX + r] = b;
-    dsum += c;
-    psum += b;
-  }
-  d.xchg[4 * WORLD_MAX] = (dsum > d.xfer_desc_max || psum > d.xfer_bytes) ? 1u : 0u;
-}
-
-// one wave per local publish with remote owners: write one record per destination
+// one wave per local publish with remote owners: write one record per destination.
+// Fused k_pack_bases: every block turns the per-rank totals of k_pack_scan into destination bases
+// itself (one wave, lane r = rank r, one load round trip and a shuffle scan); block 0
+// also publishes the send counts to the host-visible words
+DEV void pack_one(const DS& d, u32 p, u32 lane, const u32* s_base);
 __global__ __launch_bounds__(256) void k_pack(DS d) {
-  u32 p = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  u32 n = d.ctr->n_pubs;
-  if (p >= n) return;
+  __shared__ u32 s_base[2 * WORLD_MAX];
+  const u32 tid = threadIdx.x, lane = lane_id();
+  if (tid < 64) {
+    const bool v = lane < d.world;
+    const u32 c = v ? d.tot[TS_XSCAN + 2 * lane] : 0u, b = v ? d.tot[TS_XSCAN + 2 * lane + 1] : 0u;
+    u32 sc = c, sb = b;
+#pragma unroll
+    for (u32 o = 1; o < WORLD_MAX; o <<= 1) {
+      const u32 yc = __shfl_up(sc, o, 64), yb = __shfl_up(sb, o, 64);
+      if (lane >= o) { sc += yc; sb += yb; }
+    }
+    if (v) { s_base[lane] = sc - c; s_base[WORLD_MAX + lane] = sb - b; }
+    if (blockIdx.x == 0) {
+      if (v) { d.xs_base[lane] = sc - c; d.xs_base[WORLD_MAX + lane] = sb - b; d.xchg[lane] = c; d.xchg[WORLD_MAX + lane] = b; }
+      const u32 dsum = (u32)__shfl((int)sc, (int)d.world - 1), psum = (u32)__shfl((int)sb, (int)d.world - 1);
+      if (lane == 0) d.xchg[4 * WORLD_MAX] = (dsum > d.xfer_desc_max || psum > d.xfer_bytes) ? 1u : 0u;
+    }
+  }
+  __syncthreads();
+  const u32 n = d.ctr->n_pubs, nw = (gridDim.x * blockDim.x) >> 6;
+  for (u32 p = (blockIdx.x * blockDim.x + tid) >> 6; p < n; p += nw) pack_one(d, p, lane, s_base);
+}
+
+DEV void pack_one(const DS& d, u32 p, u32 lane, const u32* s_base) {
   u32 m = d.pub_rmask[p];
   if (!m) return;
-  u32 lane = lane_id();
   const Pub pb = d.pubs[p];
   const u8* w = d.work;
   while (m) {
     u32 r = __builtin_ctz(m);
     m &= m - 1;
-    u32 di = d.xs_base[r] + d.xp_cnt_off[(u64)r * d.pub_cap + p];
-    u32 rel = d.xp_byt_off[(u64)r * d.pub_cap + p];
-    u64 po = (u64)d.xs_base[WORLD_MAX + r] + rel;
+    // tile prefix (k_pack_scan) + offset within the tile
+    const u32* tp = d.pk_agg + (u64)(p / PK_TILE) * 2 * WORLD_MAX;
+    u32 di = s_base[r] + tp[2 * r] + d.xp_cnt_off[(u64)r * d.pub_cap + p];
+    u32 rel = tp[2 * r + 1] + d.xp_byt_off[(u64)r * d.pub_cap + p];
+    u64 po = (u64)s_base[WORLD_MAX + r] + rel;
     u32 sz = align16(pb.ex_len + pb.rk_len + pb.props_len + pb.body_size);
     if (di >= d.xfer_desc_max || po + sz > d.xfer_bytes) continue;  // overflow flagged by k_pack_bases
     u8* o = d.send_pay + po;
@@ -2004,52 +2139,70 @@ __global__ __launch_bounds__(256) void k_pack(DS d) {
   }
 }
 
-// phase B set-up: source bases from the received counts (host-mapped xchg), import range
-__global__ void k_import_prep(DS d) {
-  if (threadIdx.x) return;
-  u32 dsum = 0, psum = 0;
-  for (u32 r = 0; r < d.world; ++r) {
-    d.xr_base[r] = dsum;
-    d.xr_base[WORLD_MAX + r] = psum;
-    // records past the publish part of source r are link deliveries whose payload
-    // offsets start after the publish bytes (native exchange, engine.hip exchange())
-    d.xr_base[2 * WORLD_MAX + r] = d.xchg[XC_RECV_AN + r];
-    d.xr_base[3 * WORLD_MAX + r] = d.xchg[XC_RECV_AB + r];
-    dsum += d.xchg[XC_RECV_N + r];
-    psum += d.xchg[XC_RECV_B + r];
-  }
-  u32 base = 0;   // imported bytes stay in the receive buffer (pub_src)
-  bool fits = dsum <= d.import_max && psum <= d.import_bytes;
-  if (d.links) {
-    u32 nk = 0;
-    for (u32 r = 0; r < d.world; ++r) nk += d.xchg[XC_RACK_N + r];
+// Phase B head: one kernel imports the received records and applies the received link
+// acks (fused k_import_prep + k_link_acks).  Every block derives the per-source bases from
+// the received counts (host-mapped xchg) itself -- one wave, lane r = source r, one load
+// round trip and a shuffle scan -- and block 0 also publishes the import range for the
+// kernels after it.  xr: [0,W) record bases, [W,2W) byte bases, [2W,3W) publish records
+// of each source (the link deliveries after them have payload offsets past the publish
+// bytes, [3W,4W): native exchange, engine.hip exchange())
+DEV void import_one(const DS& d, u32 i, const u32* xr);
+DEV void link_ack_one(const DS& d, u32 i);
+__global__ __launch_bounds__(256) void k_import(DS d) {
+  __shared__ u32 xr[4 * WORLD_MAX];
+  __shared__ u32 s_n, s_k;
+  const u32 tid = threadIdx.x;
+  if (tid < 64) {
+    const u32 lane = tid;
+    const bool v = lane < d.world;
+    const u32 cn = v ? d.xchg[XC_RECV_N + lane] : 0u, cb = v ? d.xchg[XC_RECV_B + lane] : 0u;
+    const u32 an = v ? d.xchg[XC_RECV_AN + lane] : 0u, ab = v ? d.xchg[XC_RECV_AB + lane] : 0u;
+    const u32 rk = (v && d.links) ? d.xchg[XC_RACK_N + lane] : 0u;
+    u32 sn = cn, sb = cb, sk = rk;
+#pragma unroll
+    for (u32 o = 1; o < WORLD_MAX; o <<= 1) {
+      const u32 yn = __shfl_up(sn, o, 64), yb = __shfl_up(sb, o, 64), yk = __shfl_up(sk, o, 64);
+      if (lane >= o) { sn += yn; sb += yb; sk += yk; }
+    }
+    if (v) { xr[lane] = sn - cn; xr[WORLD_MAX + lane] = sb - cb; xr[2 * WORLD_MAX + lane] = an; xr[3 * WORLD_MAX + lane] = ab; }
+    const u32 last = d.world - 1;
+    const u32 dsum = (u32)__shfl((int)sn, (int)last), psum = (u32)__shfl((int)sb, (int)last);
+    const u32 nk = (u32)__shfl((int)sk, (int)last);
+    const bool fits = dsum <= d.import_max && psum <= d.import_bytes;
+    const u32 ni = fits ? dsum : 0u;
     const u32 kcap = (d.world - 1) * d.lk_cap;
-    d.tot[TS_NRACK] = nk < kcap ? nk : kcap;
+    const u32 nr = d.links ? (nk < kcap ? nk : kcap) : 0u;
+    if (lane == 0) { s_n = ni; s_k = nr; }
+    if (blockIdx.x == 0) {
+      if (v)
+        for (u32 k = 0; k < 4; ++k) d.xr_base[k * WORLD_MAX + lane] = xr[k * WORLD_MAX + lane];
+      if (lane == 0) {
+        if (!fits) d.ctr->n_dropped_nomem += dsum;
+        d.tot[TS_NRACK] = nr;
+        d.tot[TS_NIMPORT] = ni;
+        d.tot[TS_IMPORT_BASE] = 0;   // imported bytes stay in the receive buffer (pub_src)
+        d.tot[TS_RANGE_LO] = d.ctr->n_pubs;
+        d.tot[TS_RANGE_HI] = d.ctr->n_pubs + ni;
+        d.tot[TS_PAIR_BASE] = d.tot[TS_PAIR_N];
+      }
+    }
   }
-  u32 ni = fits ? dsum : 0;
-  if (!fits) d.ctr->n_dropped_nomem += dsum;
-  d.tot[TS_NIMPORT] = ni;
-  d.tot[TS_IMPORT_BASE] = base;
-  d.tot[TS_RANGE_LO] = d.ctr->n_pubs;
-  d.tot[TS_RANGE_HI] = d.ctr->n_pubs + ni;
-  d.tot[TS_PAIR_BASE] = d.tot[TS_PAIR_N];
+  __syncthreads();
+  const u32 n = s_n, nk = s_k;
+  const u32 g = blockIdx.x * blockDim.x + tid, gs = gridDim.x * blockDim.x;
+  for (u32 i = g; i < n; i += gs) import_one(d, i, xr);
+  for (u32 i = g; i < nk; i += gs) link_ack_one(d, i);
 }
 
 // one thread per received record -> imported Publish whose bytes stay in recv_pay (no
 // copy: a thread builds the record's key hash / key vector, as k_decode does per publish)
-DEV void import_one(const DS& d, u32 i);
-__global__ __launch_bounds__(256) void k_import(DS d) {
-  const u32 n = d.tot[TS_NIMPORT];
-  for (u32 i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) import_one(d, i);
-}
-
-DEV void import_one(const DS& d, u32 i) {
+DEV void import_one(const DS& d, u32 i, const u32* xr) {
   u32 src = 0;
   for (u32 r = 1; r < d.world; ++r)
-    if (d.xr_base[r] <= i) src = r;
+    if (xr[r] <= i) src = r;
   const RDesc rd = d.recv_desc[i];
-  const u32 lpart = i - d.xr_base[src] >= d.xr_base[2 * WORLD_MAX + src] ? d.xr_base[3 * WORLD_MAX + src] : 0u;
-  const u32 roff = d.xr_base[WORLD_MAX + src] + lpart + rd.pay_off;
+  const u32 lpart = i - xr[src] >= xr[2 * WORLD_MAX + src] ? xr[3 * WORLD_MAX + src] : 0u;
+  const u32 roff = xr[WORLD_MAX + src] + lpart + rd.pay_off;
   const u32 wo = roff;   // offsets relative to recv_pay (MF_IMPORTED, pub_src)
   u32 pi = d.ctr->n_pubs + i;
   Pub pb;
@@ -2096,7 +2249,7 @@ DEV u32 enqueue_one(const DS& d, u32 src, u32 i, u32 n, PersistRec* pr, u32 hs_n
   u32 p = d.pair_v[src][i];
   // single-pass sort (queue|rank key <= 8 bits): the queue's first pair is where digit
   // (q << rank_bits) starts; otherwise k_qfirst recorded it
-  u32 first = hs_ntiles ? d.hist_scan[(q << rb) * hs_ntiles] : d.q_first[q];
+  u32 first = hs_ntiles ? d.hist_scan[q << rb] : d.q_first[q];
   u32 rank = i - first;
   bool last = (i + 1 == n) || (kk[i + 1] >> rb) != q;
   const Pub& pb = d.pubs[p];
@@ -2143,7 +2296,7 @@ DEV void ring_plan_one(const DS& d, u32 src, u32 hs_ntiles, u32 i, u32 n) {
   const u32 rb = d.rank_bits;
   const u32 q = kk[i] >> rb;
   if (i + 1 < n && (kk[i + 1] >> rb) == q) return;   // not the queue's last pair
-  const u32 first = hs_ntiles ? d.hist_scan[(q << rb) * hs_ntiles] : d.q_first[q];
+  const u32 first = hs_ntiles ? d.hist_scan[q << rb] : d.q_first[q];
   const u64 cnt = (u64)(i - first) + 1;
   const u64 head = d.q_head[q], tail = d.q_tail[q];
   d.q_enq_tail[q] = tail;
@@ -2173,23 +2326,28 @@ DEV void ring_plan_one(const DS& d, u32 src, u32 hs_ntiles, u32 i, u32 n) {
   d.q_ring_mask[q] = want - 1;
   const u32 gi = atomicAdd(&d.ctr->n_grow, 1u);      // the host reclaims the old ring
   if (gi < GROW_MAX) d.grow_h[gi] = mv;
+  __threadfence();   // the move is visible to the last block of k_ring_plan (which copies)
 }
 
 // the last (occupied) block to finish copies every moved ring's live entries (fused
 // k_ring_moves: growth is rare, so one block does it and the common step saves a launch)
+// Grid-stride over the pairs with a capped grid (the graph's grid is sized for pair_max;
+// a block per 256 pairs of the capacity would mostly launch waves with nothing to do)
 __global__ __launch_bounds__(256) void k_ring_plan(DS d, u32 src, u32 hs_ntiles) {
   __shared__ u32 s_last;
   const u32 n = d.tot[TS_PAIR_N];
-  const u32 nb = (n + 255) / 256;
+  u32 nb = (n + 255) / 256;
+  if (nb > gridDim.x) nb = gridDim.x;   // blocks taking part
   if (blockIdx.x >= nb) return;
-  const u32 i = blockIdx.x * 256 + threadIdx.x;
-  if (i < n) ring_plan_one(d, src, hs_ntiles, i, n);
-  __threadfence();
+  for (u32 i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) ring_plan_one(d, src, hs_ntiles, i, n);
+  // a thread that planned a ring move fenced it itself (rare); the common step only waits
+  // for its own stores before the ticket (no L2 writeback per block)
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
   __syncthreads();
   if (threadIdx.x == 0) s_last = atomicAdd(&d.tot[TS_RP_TICKET], 1u) == nb - 1;
   __syncthreads();
   if (!s_last) return;
-  __threadfence();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   if (threadIdx.x == 0) d.tot[TS_RP_TICKET] = 0;
   const u32 nm = d.tot[TS_NMOVE];
   for (u32 m = 0; m < nm; ++m) {
@@ -2200,17 +2358,21 @@ __global__ __launch_bounds__(256) void k_ring_plan(DS d, u32 src, u32 hs_ntiles)
 }
 
 __global__ void k_enqueue(DS d, u32 src, u32 hs_ntiles) {
-  u32 i = blockIdx.x * blockDim.x + threadIdx.x;
-  u32 n = d.tot[TS_PAIR_N];
-  PersistRec pr;
-  pr.msg = INVALID;
-  u32 drop = i < n ? enqueue_one(d, src, i, n, &pr, hs_ntiles) : INVALID;
-  wave_release(d, drop, drop != INVALID);
-  if (drop != INVALID) atomicAdd(&d.ctr->n_ring_full, 1u);
-  if (d.persist) {
-    bool want = pr.msg != INVALID;
-    u32 k = wave_reserve(&d.ctr->n_persist, want);
-    if (want && k < d.persist_max) d.prec[k] = pr;
+  const u32 n = d.tot[TS_PAIR_N];
+  const u32 stride = gridDim.x * blockDim.x;
+  // whole waves iterate together (the wave collectives below need every lane)
+  for (u32 b = blockIdx.x * blockDim.x; b < n; b += stride) {
+    const u32 i = b + threadIdx.x;
+    PersistRec pr;
+    pr.msg = INVALID;
+    u32 drop = i < n ? enqueue_one(d, src, i, n, &pr, hs_ntiles) : INVALID;
+    wave_release(d, drop, drop != INVALID);
+    if (drop != INVALID) atomicAdd(&d.ctr->n_ring_full, 1u);
+    if (d.persist) {
+      bool want = pr.msg != INVALID;
+      u32 k = wave_reserve(&d.ctr->n_persist, want);
+      if (want && k < d.persist_max) d.prec[k] = pr;
+    }
   }
 }
 
@@ -2852,22 +3014,19 @@ __global__ __launch_bounds__(64) void k_link_bases(DS d) {
   }
 }
 
-// owner side, phase B: acks the connection sides sent for the link pseudo channels
+// owner side, phase B (k_import): an ack a connection side sent for a link pseudo channel
 // (the device form of Basic.Ack on the owner's pseudo channel; k_chan_advance settles)
-__global__ __launch_bounds__(256) void k_link_acks(DS d) {
-  const u32 n = d.tot[TS_NRACK];
-  for (u32 i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-    const AckRec a = d.rack[i];
-    if (a.tq >= d.q_max) continue;
-    const u32 ch = d.q_link_ch[a.tq];
-    if (ch == INVALID || (u32)(a.xid >> 40) != d.q_link_epoch[a.tq]) continue;
-    const u64 tag = a.xid & ((1ull << 40) - 1);
-    if (tag < d.ch_uhead[ch] || tag >= d.ch_next_tag[ch]) continue;
-    USlot* u = &d.uwin[(u64)ch * (d.ucap_mask + 1) + ((tag - 1) & d.ucap_mask)];
-    if (atomicCAS(&u->state, (u32)US_PENDING, (u32)US_ACKED) == US_PENDING &&
-        atomicExch(&d.ch_dirty[ch], 1u) == 0)
-      d.dirty_list[atomicAdd(d.n_dirty, 1u)] = ch;
-  }
+DEV void link_ack_one(const DS& d, u32 i) {
+  const AckRec a = d.rack[i];
+  if (a.tq >= d.q_max) return;
+  const u32 ch = d.q_link_ch[a.tq];
+  if (ch == INVALID || (u32)(a.xid >> 40) != d.q_link_epoch[a.tq]) return;
+  const u64 tag = a.xid & ((1ull << 40) - 1);
+  if (tag < d.ch_uhead[ch] || tag >= d.ch_next_tag[ch]) return;
+  USlot* u = &d.uwin[(u64)ch * (d.ucap_mask + 1) + ((tag - 1) & d.ucap_mask)];
+  if (atomicCAS(&u->state, (u32)US_PENDING, (u32)US_ACKED) == US_PENDING &&
+      atomicExch(&d.ch_dirty[ch], 1u) == 0)
+    d.dirty_list[atomicAdd(d.n_dirty, 1u)] = ch;
 }
 
 // ============================================================================ K5 render
@@ -2879,12 +3038,10 @@ DEV u32 put_frame_hdr(u8* o, u32 type, u32 ch, u32 size) {
 }
 
 // one wave per delivery
-DEV void render_deliv(const DS& d, u32 blk);
-DEV void render_deliv(const DS& d, u32 blk) {
-  u32 i = (blk * blockDim.x + threadIdx.x) >> 6;
+DEV void render_deliv(const DS& d, u32 i);
+// one wave per delivery i (< n_deliv)
+DEV void render_deliv(const DS& d, u32 i) {
   u32 lane = lane_id();
-  u32 n = d.ctr->n_deliv;
-  if (i >= n) return;
   const Deliv dv = d.deliv[i];
   const u32 ch = dv.chslot;
   const MsgEnt m = d.msgs[dv.msg];
@@ -3054,8 +3211,10 @@ DEV void render_rc(const DS& d, u32 blk);
 // one launch for all egress rendering: returns / confirms blocks first, then one wave per
 // delivery (the two write disjoint byte ranges of each connection's egress)
 __global__ __launch_bounds__(256) void k_render(DS d, u32 n_rc) {
-  if (blockIdx.x < n_rc) render_rc(d, blockIdx.x);
-  else render_deliv(d, blockIdx.x - n_rc);
+  if (blockIdx.x < n_rc) { render_rc(d, blockIdx.x); return; }
+  const u32 n = d.ctr->n_deliv;
+  const u32 nw = ((gridDim.x - n_rc) * blockDim.x) >> 6;
+  for (u32 i = ((blockIdx.x - n_rc) * blockDim.x + threadIdx.x) >> 6; i < n; i += nw) render_deliv(d, i);
 }
 DEV void render_rc(const DS& d, u32 blk) {
   if (blk >= RC_RET_BLOCKS) {

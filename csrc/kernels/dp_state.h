@@ -45,7 +45,8 @@ enum : u32 {
   TS_RP_TICKET = 14,                    // k_ring_plan finished-block ticket (last block: ring moves)
   TS_XSCAN = 32,                        // + 2*r: per-destination record / byte totals
   TS_TTL_BUDGET = 64,                   // durable TTL-skip records reserved this step (k_dequeue)
-  TS_NRACK = 65                         // link acks received this step (k_import_prep -> k_link_acks)
+  TS_NRACK = 65,                        // link acks received this step (k_import -> link_ack_one)
+  TS_PK_TICKET = 66                     // k_pack_scan finished-tile ticket (last tile: prefixes)
 };
 
 // remote-consumer link ack (X3): the connection side consumed message `xid` (owner's
@@ -249,6 +250,7 @@ struct DS {
   u32* xp_byt;              // [world][pub_cap] payload bytes for rank r
   u32* xp_byt_off;
   u32* xs_base;             // [2*WORLD_MAX] send record / byte bases per destination
+  u32* pk_agg;              // [pub tiles][2*WORLD_MAX] k_pack_scan tile aggregates -> prefixes
   u32* xr_base;             // [2*WORLD_MAX] recv record / byte bases per source
   u32* xchg;                // host-mapped [4*WORLD_MAX+4]: send counts/bytes (out), recv counts/bytes (in), overflow
   RDesc* send_desc;         // caller-provided (torch tensors: RCCL all-to-all operands)

@@ -259,10 +259,12 @@ class Engine {
     u64 xw = d_.world > 1 ? (u64)d_.world * d_.pub_cap : 64;
     d_.q_owner = (u32*)dev("q_owner", 4ull * d_.q_max);
     d_.pub_rmask = (u32*)dev("pub_rmask", 4ull * d_.pub_cap);
-    d_.xp_cnt = (u32*)dev("xp_cnt", 4 * xw);
+    d_.xp_cnt = nullptr;   // (per-rank count arrays: k_pack_scan counts in registers)
     d_.xp_cnt_off = (u32*)dev("xp_cnt_off", 4 * xw);
-    d_.xp_byt = (u32*)dev("xp_byt", 4 * xw);
+    d_.xp_byt = nullptr;
     d_.xp_byt_off = (u32*)dev("xp_byt_off", 4 * xw);
+    // k_pack_scan: per-tile aggregates / prefixes (2 * WORLD_MAX values per 1024 publishes)
+    d_.pk_agg = (u32*)dev("pk_agg", 4ull * 2 * WORLD_MAX * (ceil_div(d_.pub_max ? d_.pub_max : 1, 1024) + 1));
     d_.xs_base = (u32*)dev("xs_base", 8ull * WORLD_MAX);
     d_.xr_base = (u32*)dev("xr_base", 16ull * WORLD_MAX);
     d_.id_base = (u64*)dev("id_base", 8);
@@ -1323,8 +1325,8 @@ class Engine {
   }
 
  private:
-  void launch_scan(hipStream_t s, std::initializer_list<std::pair<const u32*, u32*>> arrs, const u32* n,
-                   u32 nmax, u32 slot, const u32* lo = nullptr) {
+  static ScanArgs scan_args(std::initializer_list<std::pair<const u32*, u32*>> arrs, const u32* n, u32 nmax,
+                            u32 slot, const u32* lo) {
     if (arrs.size() > 4) throw std::runtime_error("launch_scan: at most 4 arrays");
     ScanArgs a{};
     a.lo = lo;
@@ -1334,40 +1336,29 @@ class Engine {
     a.n = n;
     a.nmax = nmax;
     a.tot_slot = slot;
+    return a;
+  }
+  void launch_scan(hipStream_t s, std::initializer_list<std::pair<const u32*, u32*>> arrs, const u32* n,
+                   u32 nmax, u32 slot, const u32* lo = nullptr) {
+    const ScanArgs a = scan_args(arrs, n, nmax, slot, lo);
     u32 nb = ceil_div(nmax ? nmax : 1, SCAN_TILE);
     hipLaunchKernelGGL((k_scan<4, 4>), dim3(nb), dim3(1024), 0, s, a, d_.tot, scan_status_, scan_ctl_, scan_smax_);
   }
-  // nr (<= 4) rank pairs of arrays (in0 + r*stride -> out0 + r*stride, in1 + ... -> out1 +
-  // ...) in one launch; totals -> tot[slot + 2r], tot[slot + 2r + 1]
-  void launch_scan_ranks(hipStream_t s, const u32* in0, u32* out0, const u32* in1, u32* out1, u64 stride, u32 nr,
-                         const u32* n, u32 nmax, u32 slot) {
-    if (nr == 0 || nr > 4) throw std::runtime_error("launch_scan_ranks: 1..4 ranks per launch");
-    ScanArgs a{};
-    a.in[0] = in0; a.out[0] = out0; a.in[1] = in1; a.out[1] = out1;
-    a.stride = stride;
-    a.narr = 2 * nr;
-    a.n = n;
-    a.nmax = nmax;
-    a.tot_slot = slot;
-    u32 nb = ceil_div(nmax ? nmax : 1, SCAN_TILE);
-    hipLaunchKernelGGL((k_scan<8, 4>), dim3(nb), dim3(1024), 0, s, a, d_.tot, scan_status_, scan_ctl_, scan_smax_);
-  }
-
   // returns index (0/1) of the buffer holding the sorted output
   u32 radix_sort(hipStream_t s, u32** keys, u32** vals, const u32* n, u32 nmax, u32 bits) {
     u32 ntiles = ceil_div(nmax, SORT_TILE);
     if (bits > 8 && bits <= 11) {   // one 11-bit pass instead of two 8-bit ones
-      hipLaunchKernelGGL(k_rs_hist<11>, dim3(ntiles), dim3(256), 0, s, keys[0], n, 0u, d_.hist, d_.hist_scan,
+      hipLaunchKernelGGL(k_rs_hist<11>, capped(ntiles, 256), dim3(RsNt<11>::v), 0, s, keys[0], n, 0u, d_.hist, d_.hist_scan,
                          &d_.tot[TS_RS_TICKET], ntiles);
-      hipLaunchKernelGGL(k_rs_scatter<11>, dim3(ntiles), dim3(256), 0, s, keys[0], vals[0], keys[1], vals[1], n, 0u,
+      hipLaunchKernelGGL(k_rs_scatter<11>, capped(ntiles, 256), dim3(256), 0, s, keys[0], vals[0], keys[1], vals[1], n, 0u,
                          d_.hist_scan, ntiles);
       return 1;
     }
     u32 src = 0;
     for (u32 shift = 0; shift < bits; shift += 8) {
-      hipLaunchKernelGGL(k_rs_hist<8>, dim3(ntiles), dim3(256), 0, s, keys[src], n, shift, d_.hist, d_.hist_scan,
+      hipLaunchKernelGGL(k_rs_hist<8>, capped(ntiles, 256), dim3(RsNt<8>::v), 0, s, keys[src], n, shift, d_.hist, d_.hist_scan,
                          &d_.tot[TS_RS_TICKET], ntiles);
-      hipLaunchKernelGGL(k_rs_scatter<8>, dim3(ntiles), dim3(256), 0, s, keys[src], vals[src], keys[src ^ 1],
+      hipLaunchKernelGGL(k_rs_scatter<8>, capped(ntiles, 256), dim3(256), 0, s, keys[src], vals[src], keys[src ^ 1],
                          vals[src ^ 1], n, shift, d_.hist_scan, ntiles);
       src ^= 1;
     }
@@ -1376,13 +1367,19 @@ class Engine {
 
   static dim3 blocks(u64 n, u32 per) { return dim3(n ? ceil_div(n, per) : 1); }
   // wave-per-item grid-stride kernels: 4 waves per block, at most 8192 blocks
+  // wave-per-item grid-stride kernels: 4 waves per block, at most 8192 blocks.  Grids are
+  // fixed at graph capture, sized for capacity; the cap keeps a step with a fraction of
+  // the capacity from launching (and retiring) 100K+ idle waves, while still giving the
+  // latency-bound per-item chains (route, store, render) one wave per item at the usual
+  // step sizes (measured: a 2048-block cap made k_route / k_route_store / k_render slower)
   static dim3 wave_blocks(u64 n) { u64 b = n ? ceil_div(n, 4) : 1; return dim3(b > 8192 ? 8192 : (u32)b); }
+  static dim3 capped(u64 b, u32 cap) { return dim3(b == 0 ? 1u : (b > cap ? cap : (u32)b)); }
 
   // frame scan, command assembly, decode (K1-K5)
   void launch_ingest(hipStream_t s, const DS& d) {
     Range rg("chanamq.K1-K4.ingest");
-    hipLaunchKernelGGL(k_stage, dim3(d.seg_max, 4), dim3(256), 0, s, d);
-    hipLaunchKernelGGL(k_frame_scan, dim3(d.seg_max), dim3(FS_NT), 0, s, d);
+    hipLaunchKernelGGL(k_stage, dim3(capped(d.seg_max, 256).x, 4), dim3(256), 0, s, d);
+    hipLaunchKernelGGL(k_frame_scan, capped(d.seg_max, 512), dim3(FS_NT), 0, s, d);
     launch_scan(s, {{d.cmd_is_pub, d.cmd_pub_rank}, {d.cmd_is_ack, d.cmd_ack_rank}}, &d.ctr->n_cmds,
                 d.cmd_max, 4);
     hipLaunchKernelGGL(k_decode, blocks(d.cmd_max, 256), dim3(256), 0, s, d);
@@ -1395,27 +1392,23 @@ class Engine {
       u64 waves = (u64)((nmax + 15) / 16) * (d.tb_pad / 16);
       hipLaunchKernelGGL(k_topic_mfma, wave_blocks(waves), dim3(256), 0, s, d);
     }
-    hipLaunchKernelGGL(k_route<0>, wave_blocks(nmax), dim3(256), 0, s, d);
-    launch_scan(s, {{d.pub_nq, d.pub_pair_off}, {d.pub_slot, d.pub_slot_off}, {d.pub_routed, d.pub_routed_rank},
-                    {d.pub_ret_sz, d.pub_ret_off}},
-                &d.tot[TS_RANGE_HI], d.pub_cap, 0, &d.tot[TS_RANGE_LO]);
-    hipLaunchKernelGGL(k_route<1>, wave_blocks(nmax), dim3(256), 0, s, d);
-    hipLaunchKernelGGL(k_store, wave_blocks(nmax), dim3(256), 0, s, d);
+    hipLaunchKernelGGL(k_route, wave_blocks(nmax), dim3(256), 0, s, d);
+    // scan of the routing counts + the phase's log reservation, then pairs + store
+    const ScanArgs a = scan_args({{d.pub_nq, d.pub_pair_off}, {d.pub_slot, d.pub_slot_off},
+                                  {d.pub_routed, d.pub_routed_rank}, {d.pub_ret_sz, d.pub_ret_off}},
+                                 &d.tot[TS_RANGE_HI], d.pub_cap, 0, &d.tot[TS_RANGE_LO]);
+    hipLaunchKernelGGL(k_scan_route, dim3(ceil_div(d.pub_cap ? d.pub_cap : 1, SCAN_TILE)), dim3(1024), 0, s, a, d_.tot,
+                       scan_status_, scan_ctl_, scan_smax_, d);
+    hipLaunchKernelGGL(k_route_store, wave_blocks(nmax), dim3(256), 0, s, d);
   }
 
   // serialise publishes with remote owners into the per-destination send buffers
   void launch_pack(hipStream_t s, const DS& d) {
     Range rg("chanamq.X1.pack");
-    hipLaunchKernelGGL(k_pack_count, blocks(d.pub_max, 256), dim3(256), 0, s, d);
-    // per destination rank: record and byte offsets; 4 ranks (8 arrays) per launch
-    for (u32 r0 = 0; r0 < d.world; r0 += 4) {
-      const u64 a = (u64)r0 * d.pub_cap;
-      const u32 nr = d.world - r0 < 4 ? d.world - r0 : 4;
-      launch_scan_ranks(s, d.xp_cnt + a, d.xp_cnt_off + a, d.xp_byt + a, d.xp_byt_off + a, d.pub_cap, nr,
-                        &d.ctr->n_pubs, d.pub_max, TS_XSCAN + 2 * r0);
-    }
-    hipLaunchKernelGGL(k_pack_bases, dim3(1), dim3(64), 0, s, d);
-    hipLaunchKernelGGL(k_pack, blocks((u64)d.pub_max * 64, 256), dim3(256), 0, s, d);
+    // per destination rank: record and byte offsets of every publish (one pass, all
+    // ranks); k_pack derives the destination bases itself and serialises
+    hipLaunchKernelGGL(k_pack_scan, blocks(d.pub_max, PK_TILE), dim3(1024), 0, s, d, d.pk_agg, &d.tot[TS_PK_TICKET]);
+    hipLaunchKernelGGL(k_pack, wave_blocks(d.pub_max), dim3(256), 0, s, d);
   }
 
   // enqueue, acks, dispatch, render (K7-K11)
@@ -1431,15 +1424,15 @@ class Engine {
     // single pass (<= 11 key bits): queue starts straight from the digit offsets
     const u32 hs_ntiles = pbits <= 11 ? ceil_div(d.pair_max, SORT_TILE) : 0;
     if (!hs_ntiles) hipLaunchKernelGGL(k_qfirst, blocks(d.pair_max, 256), dim3(256), 0, s, d, psrc);
-    hipLaunchKernelGGL(k_ring_plan, blocks(d.pair_max, 256), dim3(256), 0, s, d, psrc, hs_ntiles);
-    hipLaunchKernelGGL(k_enqueue, blocks(d.pair_max, 256), dim3(256), 0, s, d, psrc, hs_ntiles);
+    hipLaunchKernelGGL(k_ring_plan, capped(ceil_div(d.pair_max, 256), 1024), dim3(256), 0, s, d, psrc, hs_ntiles);
+    hipLaunchKernelGGL(k_enqueue, capped(ceil_div(d.pair_max, 256), 1024), dim3(256), 0, s, d, psrc, hs_ntiles);
     if (!dispatch) {
       const u64 pn = d.deliv_max > d.c_max ? d.deliv_max : d.c_max;
       hipLaunchKernelGGL(k_post, blocks(pn, 256), dim3(256), 0, s, d);   // n_deliv = 0: frees only
       hipLaunchKernelGGL(k_host_out, dim3(64), dim3(256), 0, s, d);
       return;
     }
-    hipLaunchKernelGGL(k_chan_advance, dim3(nch < 2048 ? nch : 2048), dim3(256), 0, s, d);
+    hipLaunchKernelGGL(k_chan_advance, capped(nch, 1024), dim3(256), 0, s, d);
     // requeued deliveries go back in front of their queues' heads before this step's
     // dispatch, in queue-offset order (QueueEntity.scala:415-446)
     hipLaunchKernelGGL(k_requeue, dim3(d.q_max < 256 ? d.q_max : 256), dim3(256), 0, s, d);
@@ -1457,7 +1450,7 @@ class Engine {
     if (d.links) hipLaunchKernelGGL(k_link_bases, dim3(1), dim3(64), 0, s, d);
     {
       const u32 n_rc = RC_RET_BLOCKS + ceil_div(d.c_max, 256);
-      hipLaunchKernelGGL(k_render, dim3(n_rc + blocks((u64)d.deliv_max * 64, 256).x), dim3(256), 0, s, d, n_rc);
+      hipLaunchKernelGGL(k_render, dim3(n_rc + wave_blocks(d.deliv_max).x), dim3(256), 0, s, d, n_rc);
     }
     u64 pn = d.deliv_max > d.c_max ? d.deliv_max : d.c_max;
     hipLaunchKernelGGL(k_post, blocks(pn, 256), dim3(256), 0, s, d);
@@ -1480,9 +1473,7 @@ class Engine {
   // world > 1, after the all-to-all: import, route against local queues, rest of the step
   void launch_phase_b(hipStream_t s, const DS& d, bool dispatch = true) {
     Range rg("chanamq.X1.import");
-    hipLaunchKernelGGL(k_import_prep, dim3(1), dim3(64), 0, s, d);
-    if (d.links) hipLaunchKernelGGL(k_link_acks, dim3(64), dim3(256), 0, s, d);
-    hipLaunchKernelGGL(k_import, blocks(d.import_max, 256), dim3(256), 0, s, d);
+    hipLaunchKernelGGL(k_import, capped(ceil_div(d.import_max, 256), 1024), dim3(256), 0, s, d);   // + prep, link acks
     launch_route(s, d, d.import_max);
     launch_tail(s, d, dispatch);
   }

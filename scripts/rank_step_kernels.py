@@ -1,9 +1,13 @@
 #!/usr/bin/env python3
 """Kernel time per rank-step from a rocprofv3 rocpd db of bench/world_rehearsal.py (or
 bench.py with --world 1): data-plane kernels only (k_*), runtime copies/fills excluded.
+Second table: the launch sequence of each graph (split at k_stage = phase A / whole step,
+k_import = phase B), mean time per position, so repeated kernels (k_route in phase A and
+in phase B) are told apart.
 usage: rank_step_kernels.py DB RANK_STEPS [out.csv]"""
 import sqlite3
 import sys
+from collections import defaultdict
 
 
 def main(db, rank_steps, out=None):
@@ -22,6 +26,31 @@ def main(db, rank_steps, out=None):
         tot_l += l
         lines.append(f"{n},{l:.2f},{us:.2f}")
     lines.append(f"TOTAL,{tot_l:.2f},{tot_us:.2f}")
+    # per graph position
+    seqs, cur_seq = [], None
+    for n, s, e in cur.execute(f"select {name}, start, end from kernels order by start"):
+        n = n.split("(")[0].replace("void ", "")
+        if "k_" not in n:
+            continue
+        if n in ("k_stage", "k_import"):
+            cur_seq = []
+            seqs.append(cur_seq)
+        if cur_seq is not None:
+            cur_seq.append((n, (e - s) / 1e3))
+    groups = defaultdict(list)
+    for sq in seqs:
+        groups[tuple(n for n, _ in sq)].append([t for _, t in sq])
+    for sig, runs in sorted(groups.items(), key=lambda kv: -len(kv[1])):
+        if len(runs) < 2:
+            continue
+        lines.append("")
+        lines.append(f"graph starting {sig[0]} ({len(runs)} runs): position,kernel,mean_us")
+        tot = 0.0
+        for i, n in enumerate(sig):
+            m = sum(r[i] for r in runs) / len(runs)
+            tot += m
+            lines.append(f"{i},{n},{m:.2f}")
+        lines.append(f"TOTAL,{len(sig)},{tot:.2f}")
     text = "\n".join(lines) + "\n"
     if out:
         open(out, "w").write(text)

@@ -444,3 +444,32 @@ def test_ttl_expired_bodies_freed_without_consumers_or_connections(gpu):
         assert b._fe_stats["live_bytes"] == 0
     finally:
         b.stop()
+
+
+@pytest.mark.gpu
+def test_config5_storm_setup_64p64c_against_pipelined_server(gpu):
+    """Regression (round-2 config-5 setup timeout): 64 producer and 64 consumer connections
+    open, declare and attach against the pipelined server, then run a short Basic.Nack
+    (requeue) storm under a memory watermark; setup must finish and traffic must flow both
+    ways with no load-generator error."""
+    import time
+    from chanamq_amd.broker import load
+    from chanamq_amd.engine.dataplane import GpuDataPlane
+    from chanamq_amd.server.gpu_broker import GpuBroker
+    plane = GpuDataPlane(c_max=512, chpc=8, q_max=256, cons_max=1024, seg_max=512, cmd_max=1 << 16,
+                         deliv_max=1 << 16, msg_max=1 << 20, ucap=8192, deliver_cap=8192, ingress_cap=32 << 20,
+                         egress_cap=96 << 20, log_bytes=1 << 30, ring_pool=1 << 23, tb_max=256,
+                         default_queue_capacity=1 << 18, carry_cap=1 << 18)
+    b = GpuBroker(plane, idle_step_ms=0.5, io="pipeline", io_threads=4, per_conn_read=128 << 10,
+                  mem_high_watermark=256 << 20).start()
+    try:
+        t0 = time.time()
+        r = load().run_load(dict(port=b.port, seconds=2.0, warmup=0.5, queue="c5.q", exchange="c5.x", threads=8,
+                                 consumer_threads=4, producers=64, consumers=64, queues=16, msg_size=1024,
+                                 auto_ack=False, prefetch=512, nack_every=2))
+        wall = time.time() - t0
+    finally:
+        b.stop()
+    assert r["error"] == "", r["error"]
+    assert r["sent"] > 0 and r["received"] > 0
+    assert wall < 60, f"64P x 64C setup + 2.5 s of load took {wall:.1f} s"
