@@ -1384,8 +1384,8 @@ __global__ __launch_bounds__(1024) void k_scan_route(ScanArgs a, u32* tot, u64* 
 }
 
 // ============================================================================ radix sort
-// stable LSD radix sort of (key, val) u32 pairs, DB bits per pass (8, or 11 for keys of
-// 9..11 bits -- queue << rank_bits | rank at 4..8 GPUs -- in one pass instead of two);
+// stable LSD radix sort of (key, val) u32 pairs, DB bits per pass (8, or 9..11 for keys
+// of 9..11 bits in one pass instead of two);
 // n from device.  Per-tile digit histograms; the last occupied tile to finish turns them
 // into the offsets of the occupied tiles (fused k_rs_offsets).  hist and hscan are both
 // tile-major (hist[t * D + digit], hscan[t * D + digit]): the tiles write and the offsets
@@ -1393,7 +1393,7 @@ __global__ __launch_bounds__(1024) void k_scan_route(ScanArgs a, u32* tot, u64* 
 // row 0.  The offsets block keeps up to RS_RT tiles' counts in registers: one round of
 // loads, one block scan, one round of stores.
 constexpr u32 RS_RT = 16;
-template <int DB> struct RsNt { static constexpr u32 v = DB > 8 ? 1024u : 256u; };
+template <int DB> struct RsNt { static constexpr u32 v = DB > 10 ? 1024u : (DB > 9 ? 512u : 256u); };
 template <int DB>
 DEV void rs_offsets(const u32* hist, u32* hscan, u32 T, u32* lds) {
   constexpr u32 NT = RsNt<DB>::v, D = 1u << DB, PER = D / NT;   // consecutive digits per thread
@@ -1583,32 +1583,27 @@ DEV void topic_tile(const DS& d, u32 i0, u32 j0, u32 jt, u32 ntb, u32 npub, u32 
   }
 }
 
-// grid-stride over 16x16 (publish x binding) tiles of the current phase range
-__global__ __launch_bounds__(256) void k_topic_mfma(DS d) {
-  if (d.tb_max == 0) return;
-  u32 lane = lane_id();
-  u32 ntb = d.tb_pad >> 4;
-  u32 lo = d.tot[TS_RANGE_LO], npub = d.tot[TS_RANGE_HI];
-  if (npub > d.pub_cap) npub = d.pub_cap;
-  u32 ntiles = (npub > lo ? (npub - lo + 15) / 16 : 0) * ntb;
-  const u32 nw = (gridDim.x * blockDim.x) >> 6;
-  for (u32 wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6; wave < ntiles; wave += nw) {
-    u32 it = wave / ntb, jt = wave % ntb;
-    // a tile of records that all arrived routed (MF_ONEQ / MF_RESTORE: phase B imports)
-    // has nothing to match
-    const u32 pi = lo + it * 16 + lane;
-    const bool need = lane < 16 && pi < npub && !(d.pubs[pi].flags & (MF_ONEQ | MF_RESTORE));
-    if (!__ballot(need)) continue;
-    topic_tile(d, lo + it * 16, jt * 16, jt, ntb, npub, lane);
-  }
+// the topic prefilter tiles of one group of 16 publishes [g0, g0 + 16) (all binding tiles,
+// spread over the block's 16 waves); tiles whose publishes all arrived routed (MF_ONEQ /
+// MF_RESTORE) or are not topic-routed have nothing to match.  The rows are written to
+// pub_match (global: k_route_store re-reads them for publishes with > 8 queues) and made
+// visible to the block's waves before they route.
+DEV void topic_group(const DS& d, u32 g0, u32 n, u32 w, u32 lane) {
+  const u32 ntb = d.tb_max ? d.tb_pad >> 4 : 0u;
+  if (ntb == 0) return;
+  const u32 pi = g0 + lane;
+  const bool need = lane < 16 && pi < n && !(d.pubs[pi].flags & (MF_ONEQ | MF_RESTORE));
+  if (!__ballot(need)) return;
+  for (u32 jt = w; jt < ntb; jt += 16) topic_tile(d, g0, jt * 16, jt, ntb, n, lane);
 }
+
 
 // exact check behind an MFMA prefilter hit: same word count (checked) and every non-'*'
 // pattern word byte-equal to the key word at its position.  Word offsets are precomputed
 // (host: t_woff, decode: pub_kwoff), so the compares of all words issue together instead
 // of walking both strings byte by byte.
 // bytes of a publish: the step's work buffer, or for a record imported from another
-// rank the all-to-all receive buffer itself (k_import copies nothing)
+// rank the all-to-all receive buffer itself (k_import_route copies nothing)
 DEV const u8* pub_src(const DS& d, const Pub& pb) { return (pb.flags & MF_IMPORTED) ? d.recv_pay : d.work; }
 
 DEV bool topic_verify_words(const DS& d, const Pub& pb, u32 pidx, u32 t, u32 fl) {
@@ -1714,10 +1709,14 @@ DEV void route_emit(const DS& d, RouteAcc<PASS>& a, u32 p, u32 wbase, u32 srank,
 template <int PASS>
 DEV void route_one(const DS& d, u32 p, u32 lane) {
   Pub& pb = d.pubs[p];
+  // pass 0 of an imported record that arrived with its queue ran in import_one
+  if (PASS == 0 && (pb.flags & MF_IMPORTED) && (pb.flags & (MF_ONEQ | MF_RESTORE))) return;
   const u32 wbase = PASS ? d.tot[TS_PAIR_BASE] + d.pub_pair_off[p] : 0;
-  // pair key = queue << rank_bits | source rank: a queue's messages are ordered by
-  // (source rank, connection, publish order) whichever rank owns it
-  const u32 srank = (pb.flags & MF_IMPORTED) ? pb.pad : d.my_rank;
+  // pair key = queue << rank_bits | (source rank >= this rank) (engine.hip): with the
+  // stable sort and the generation order (own publishes, then imports by source rank) a
+  // queue's messages are ordered by (source rank, connection, publish order) whichever
+  // rank owns it
+  const u32 srank = d.rank_bits ? (((pb.flags & MF_IMPORTED) ? pb.pad : d.my_rank) >= d.my_rank ? 1u : 0u) : 0u;
   if (PASS == 1) {
     if (lane == 0 && d.pub_ret_sz[p]) atomicMin(&d.conn_ret_min[pb.conn], d.pub_ret_off[p]);
     u32 nq0 = d.pub_nq[p];
@@ -1823,15 +1822,22 @@ DEV void route_one(const DS& d, u32 p, u32 lane) {
   }
 }
 
-// routing pass 0 (count queues, destination ranks); pass 1 runs fused with the store
-// (k_route_store) after k_scan_route reserved the phase's log region
-__global__ __launch_bounds__(256) void k_route(DS d) {
-  const u32 lane = lane_id();
-  const u32 nw = (gridDim.x * blockDim.x) >> 6;
+// routing pass 0 (count queues, destination ranks) of the step's own publishes, 16 per
+// 1024-thread block: the group's topic prefilter tiles on MFMA (fused k_topic_mfma), then
+// one wave per publish.  Pass 1 runs fused with the store (k_route_store) after
+// k_scan_route reserved the phase's log region.  The imports' pass 0 is k_import_route.
+__global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void k_route(DS d) {
+  const u32 lane = lane_id(), w = threadIdx.x >> 6;
+  const u32 lo = d.tot[TS_RANGE_LO];
   u32 n = d.tot[TS_RANGE_HI];
   if (n > d.pub_cap) n = d.pub_cap;
-  for (u32 p = d.tot[TS_RANGE_LO] + ((blockIdx.x * blockDim.x + threadIdx.x) >> 6); p < n; p += nw)
-    route_one<0>(d, p, lane);
+  for (u32 g0 = lo + blockIdx.x * 16; g0 < n; g0 += gridDim.x * 16) {
+    topic_group(d, g0, n, w, lane);
+    __threadfence_block();
+    __syncthreads();
+    if (g0 + w < n) route_one<0>(d, g0 + w, lane);
+    __syncthreads();   // the next group's tiles overwrite nothing this group reads, but keep waves together
+  }
 }
 
 // reserve the step's contiguous body-log region and message-table indices
@@ -1924,14 +1930,21 @@ DEV void store_one(const DS& d, u32 p, u32 lane) {
   u8* slot = d.log + (off % d.log_bytes);
   const u8* w = pub_src(d, pb);
   u32 meta = align16(pb.ex_len + pb.rk_len + pb.props_len);
-  wave_copy(slot, w + pb.ex_off, pb.ex_len);
-  wave_copy(slot + pb.ex_len, w + pb.rk_off, pb.rk_len);
-  wave_copy(slot + pb.ex_len + pb.rk_len, w + pb.props_off, pb.props_len);
-  u32 bo = meta;
-  for (u32 k = 0; k < pb.nfrag; ++k) {
-    Frag fg = d.frags[pb.frag0 + k];
-    wave_copy(slot + bo, w + fg.off, fg.len);
-    bo += fg.len;
+  if ((pb.flags & (MF_IMPORTED | MF_SLOTFMT)) == (MF_IMPORTED | MF_SLOTFMT)) {
+    // a record already in slot layout, 16-aligned on both sides: one vector copy
+    const uint4* src = (const uint4*)(w + pb.ex_off);
+    uint4* dst = (uint4*)slot;
+    for (u32 i = lane; i < (pb.slot_bytes >> 4); i += 64) dst[i] = src[i];
+  } else {
+    wave_copy(slot, w + pb.ex_off, pb.ex_len);
+    wave_copy(slot + pb.ex_len, w + pb.rk_off, pb.rk_len);
+    wave_copy(slot + pb.ex_len + pb.rk_len, w + pb.props_off, pb.props_len);
+    u32 bo = meta;
+    for (u32 k = 0; k < pb.nfrag; ++k) {
+      Frag fg = d.frags[pb.frag0 + k];
+      wave_copy(slot + bo, w + fg.off, fg.len);
+      bo += fg.len;
+    }
   }
   if (lane == 0) {
     MsgEnt m;
@@ -2001,7 +2014,7 @@ __global__ __launch_bounds__(1024) void k_pack_scan(DS d, u32* agg, u32* ticket)
     m = d.pub_rmask[p];
     if (m) {
       const Pub& pb = d.pubs[p];
-      sz = align16(pb.ex_len + pb.rk_len + pb.props_len + pb.body_size);
+      sz = align16(align16(pb.ex_len + pb.rk_len + pb.props_len) + pb.body_size);   // slot layout
     }
   }
   u32 myc[WORLD_MAX], myb[WORLD_MAX];
@@ -2105,15 +2118,15 @@ DEV void pack_one(const DS& d, u32 p, u32 lane, const u32* s_base) {
     u32 di = s_base[r] + tp[2 * r] + d.xp_cnt_off[(u64)r * d.pub_cap + p];
     u32 rel = tp[2 * r + 1] + d.xp_byt_off[(u64)r * d.pub_cap + p];
     u64 po = (u64)s_base[WORLD_MAX + r] + rel;
-    u32 sz = align16(pb.ex_len + pb.rk_len + pb.props_len + pb.body_size);
+    // the record is laid out as the owner's body-log slot (MF_SLOTFMT)
+    const u32 meta = align16(pb.ex_len + pb.rk_len + pb.props_len);
+    u32 sz = align16(meta + pb.body_size);
     if (di >= d.xfer_desc_max || po + sz > d.xfer_bytes) continue;  // overflow flagged by k_pack_bases
     u8* o = d.send_pay + po;
     wave_copy(o, w + pb.ex_off, pb.ex_len);
-    o += pb.ex_len;
-    wave_copy(o, w + pb.rk_off, pb.rk_len);
-    o += pb.rk_len;
-    wave_copy(o, w + pb.props_off, pb.props_len);
-    o += pb.props_len;
+    wave_copy(o + pb.ex_len, w + pb.rk_off, pb.rk_len);
+    wave_copy(o + pb.ex_len + pb.rk_len, w + pb.props_off, pb.props_len);
+    o += meta;
     for (u32 k = 0; k < pb.nfrag; ++k) {
       Frag fg = d.frags[pb.frag0 + k];
       wave_copy(o, w + fg.off, fg.len);
@@ -2125,7 +2138,7 @@ DEV void pack_one(const DS& d, u32 p, u32 lane, const u32* s_base) {
       rd.body_len = pb.body_size;
       rd.props_len = pb.props_len;
       rd.exch = pb.exch;
-      rd.flags = pb.flags & (MF_PERSIST | MF_HAS_TS);
+      rd.flags = (pb.flags & (MF_PERSIST | MF_HAS_TS)) | MF_SLOTFMT;
       if (pb.xid != ~0ull) {   // the owner skips re-routing: its one queue is known
         rd.flags |= MF_ONEQ;
         rd.tq = (u32)pb.xid;
@@ -2145,10 +2158,14 @@ DEV void pack_one(const DS& d, u32 p, u32 lane, const u32* s_base) {
 // round trip and a shuffle scan -- and block 0 also publishes the import range for the
 // kernels after it.  xr: [0,W) record bases, [W,2W) byte bases, [2W,3W) publish records
 // of each source (the link deliveries after them have payload offsets past the publish
-// bytes, [3W,4W): native exchange, engine.hip exchange())
+// bytes, [3W,4W): native exchange, engine.hip exchange()).  The same kernel runs routing
+// pass 0 of the imports (fused k_topic_mfma + k_route): 16 records per 1024-thread block
+// -- 16 threads import them, the block computes their topic tiles, one wave per record
+// routes it (records that arrived with their queue were routed by import_one and return
+// at once)
 DEV void import_one(const DS& d, u32 i, const u32* xr);
 DEV void link_ack_one(const DS& d, u32 i);
-__global__ __launch_bounds__(256) void k_import(DS d) {
+__global__ __launch_bounds__(1024) void k_import_route(DS d) {
   __shared__ u32 xr[4 * WORLD_MAX];
   __shared__ u32 s_n, s_k;
   const u32 tid = threadIdx.x;
@@ -2190,8 +2207,18 @@ __global__ __launch_bounds__(256) void k_import(DS d) {
   __syncthreads();
   const u32 n = s_n, nk = s_k;
   const u32 g = blockIdx.x * blockDim.x + tid, gs = gridDim.x * blockDim.x;
-  for (u32 i = g; i < n; i += gs) import_one(d, i, xr);
   for (u32 i = g; i < nk; i += gs) link_ack_one(d, i);
+  const u32 base = d.ctr->n_pubs, lane = tid & 63, w = tid >> 6;
+  for (u32 g0 = blockIdx.x * 16; g0 < n; g0 += gridDim.x * 16) {
+    if (tid < 16 && g0 + tid < n) import_one(d, g0 + tid, xr);
+    __threadfence_block();
+    __syncthreads();
+    topic_group(d, base + g0, base + n, w, lane);
+    __threadfence_block();
+    __syncthreads();
+    if (g0 + w < n) route_one<0>(d, base + g0 + w, lane);
+    __syncthreads();
+  }
 }
 
 // one thread per received record -> imported Publish whose bytes stay in recv_pay (no
@@ -2216,7 +2243,8 @@ DEV void import_one(const DS& d, u32 i, const u32* xr) {
   pb.props_off = pb.rk_off + rd.rk_len;
   pb.props_len = rd.props_len;
   u32 fi = d.frag_max + i;  // imported bodies live past the step's own fragments
-  d.frags[fi] = Frag{pb.props_off + rd.props_len, rd.body_len};
+  d.frags[fi] = Frag{(rd.flags & MF_SLOTFMT) ? wo + align16(rd.ex_len + rd.rk_len + rd.props_len)
+                                            : pb.props_off + rd.props_len, rd.body_len};
   pb.frag0 = fi;
   pb.nfrag = rd.body_len ? 1 : 0;
   pb.body_size = rd.body_len;
@@ -2229,6 +2257,22 @@ DEV void import_one(const DS& d, u32 i, const u32* xr) {
   pb.nwords = routed ? 0u : build_keyvec(d, key, rd.rk_len, pi);
   pb.nq = 0; pb.slot_bytes = 0; pb.msg = INVALID; pb.xid = rd.xid;
   pb.pad = src;  // source rank (pair ordering)
+  if (routed) {
+    // routing pass 0 for a record that arrived with its queue (what route_one<0> computes
+    // for it: one local queue, no return, never forwarded); route_one<0> skips it
+    const u32 q = rd.tq;
+    const u32 nq = (d.world == 1 || d.q_owner[q] == d.my_rank) ? 1u : 0u;
+    const u32 slot = nq ? align16(align16(pb.ex_len + pb.rk_len + pb.props_len) + pb.body_size) : 0u;
+    pb.nq = nq;
+    pb.slot_bytes = slot;
+    d.pub_qc[(u64)pi * 8] = q;
+    d.pub_nq[pi] = nq;
+    d.pub_slot[pi] = slot;
+    d.pub_routed[pi] = nq;
+    d.pub_ret[pi] = 0;
+    d.pub_ret_sz[pi] = 0;
+    if (d.world > 1) d.pub_rmask[pi] = 0;
+  }
   d.pubs[pi] = pb;
 }
 
@@ -3014,7 +3058,7 @@ __global__ __launch_bounds__(64) void k_link_bases(DS d) {
   }
 }
 
-// owner side, phase B (k_import): an ack a connection side sent for a link pseudo channel
+// owner side, phase B (k_import_route): an ack a connection side sent for a link pseudo channel
 // (the device form of Basic.Ack on the owner's pseudo channel; k_chan_advance settles)
 DEV void link_ack_one(const DS& d, u32 i) {
   const AckRec a = d.rack[i];

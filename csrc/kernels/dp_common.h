@@ -31,7 +31,9 @@ enum : u32 {
   MF_PERSIST = 1, MF_MANDATORY = 2, MF_IMMEDIATE = 4, MF_HAS_TS = 8, MF_IMPORTED = 16,
   MF_RESTORE = 32,      // recovered from the store: enqueue into exactly RDesc.tq, keep RDesc.xid
   MF_REDELIVERED = 64,  // enqueue with the redelivered flag (recovered unacks)
-  MF_ONEQ = 128         // cross-rank record routed at its origin to exactly one queue: RDesc.tq
+  MF_ONEQ = 128,        // cross-rank record routed at its origin to exactly one queue: RDesc.tq
+  MF_SLOTFMT = 256      // cross-rank record laid out as a body-log slot ([ex][rk][props] padded
+                        // to 16, then the body): the owner stores it with one aligned copy
 };
 
 // ---- unacked slot states

@@ -45,7 +45,7 @@ enum : u32 {
   TS_RP_TICKET = 14,                    // k_ring_plan finished-block ticket (last block: ring moves)
   TS_XSCAN = 32,                        // + 2*r: per-destination record / byte totals
   TS_TTL_BUDGET = 64,                   // durable TTL-skip records reserved this step (k_dequeue)
-  TS_NRACK = 65,                        // link acks received this step (k_import -> link_ack_one)
+  TS_NRACK = 65,                        // link acks received this step (k_import_route -> link_ack_one)
   TS_PK_TICKET = 66                     // k_pack_scan finished-tile ticket (last tile: prefixes)
 };
 

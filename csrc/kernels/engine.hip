@@ -150,7 +150,12 @@ class Engine {
     u32 dq_max = (u32)get("dq_max", 1u << 20);
     u64 kpool = get("kpool", 16ull << 20);
     u32 nch = d_.c_max * d_.chpc;
-    d_.rank_bits = d_.world > 1 ? bits_for(d_.world - 1) : 0;
+    // pair key = queue << 1 | (source rank >= this rank) at world > 1: the pairs are
+    // generated as (this rank's publishes, then imports in source-rank order) and the sort
+    // is stable, so one key bit restores (source rank, connection, publish) order per queue
+    // (imports from lower ranks, own publishes, higher ranks) -- 9 key bits at q_max 256
+    // instead of q_bits + log2(world)
+    d_.rank_bits = d_.world > 1 ? 1 : 0;
     d_.q_bits = bits_for(d_.q_max);
     if (d_.q_bits + d_.rank_bits > 32) throw std::runtime_error("q_max too large for sharded pair keys");
     d_.ch_bits = bits_for(nch);
@@ -231,7 +236,7 @@ class Engine {
     d_.seg_total = (u32*)dev("seg_total", 4ull * d_.seg_max);
     d_.seg_cmd_base = (u32*)dev("seg_cmd_base", 4ull * d_.seg_max);
     d_.seg_npub = (u32*)dev("seg_npub", 4ull * d_.seg_max);
-    d_.work = (u8*)dev("work", d_.work_cap + 4096);   // imports are read in place (k_import)
+    d_.work = (u8*)dev("work", d_.work_cap + 4096);   // imports are read in place (k_import_route)
 
     d_.cmds = (Cmd*)dev("cmds", sizeof(Cmd) * (u64)d_.cmd_max);
     d_.frags = (Frag*)dev("frags", sizeof(Frag) * ((u64)d_.frag_max + d_.import_max));
@@ -1347,11 +1352,23 @@ class Engine {
   // returns index (0/1) of the buffer holding the sorted output
   u32 radix_sort(hipStream_t s, u32** keys, u32** vals, const u32* n, u32 nmax, u32 bits) {
     u32 ntiles = ceil_div(nmax, SORT_TILE);
-    if (bits > 8 && bits <= 11) {   // one 11-bit pass instead of two 8-bit ones
-      hipLaunchKernelGGL(k_rs_hist<11>, capped(ntiles, 256), dim3(RsNt<11>::v), 0, s, keys[0], n, 0u, d_.hist, d_.hist_scan,
-                         &d_.tot[TS_RS_TICKET], ntiles);
-      hipLaunchKernelGGL(k_rs_scatter<11>, capped(ntiles, 256), dim3(256), 0, s, keys[0], vals[0], keys[1], vals[1], n, 0u,
-                         d_.hist_scan, ntiles);
+    if (bits > 8 && bits <= 11) {   // one 9..11-bit pass instead of two 8-bit ones
+      if (bits == 9) {
+        hipLaunchKernelGGL(k_rs_hist<9>, capped(ntiles, 256), dim3(RsNt<9>::v), 0, s, keys[0], n, 0u, d_.hist,
+                           d_.hist_scan, &d_.tot[TS_RS_TICKET], ntiles);
+        hipLaunchKernelGGL(k_rs_scatter<9>, capped(ntiles, 256), dim3(256), 0, s, keys[0], vals[0], keys[1], vals[1], n,
+                           0u, d_.hist_scan, ntiles);
+      } else if (bits == 10) {
+        hipLaunchKernelGGL(k_rs_hist<10>, capped(ntiles, 256), dim3(RsNt<10>::v), 0, s, keys[0], n, 0u, d_.hist,
+                           d_.hist_scan, &d_.tot[TS_RS_TICKET], ntiles);
+        hipLaunchKernelGGL(k_rs_scatter<10>, capped(ntiles, 256), dim3(256), 0, s, keys[0], vals[0], keys[1], vals[1],
+                           n, 0u, d_.hist_scan, ntiles);
+      } else {
+        hipLaunchKernelGGL(k_rs_hist<11>, capped(ntiles, 256), dim3(RsNt<11>::v), 0, s, keys[0], n, 0u, d_.hist,
+                           d_.hist_scan, &d_.tot[TS_RS_TICKET], ntiles);
+        hipLaunchKernelGGL(k_rs_scatter<11>, capped(ntiles, 256), dim3(256), 0, s, keys[0], vals[0], keys[1], vals[1],
+                           n, 0u, d_.hist_scan, ntiles);
+      }
       return 1;
     }
     u32 src = 0;
@@ -1385,14 +1402,13 @@ class Engine {
     hipLaunchKernelGGL(k_decode, blocks(d.cmd_max, 256), dim3(256), 0, s, d);
   }
 
-  // route + store the publishes of the current phase range (K6); nmax = range capacity
-  void launch_route(hipStream_t s, const DS& d, u32 nmax) {
+  // route + store the publishes of the current phase range (K6); nmax = range capacity.
+  // imports: phase B's import + routing pass 0 kernel (k_import_route) instead of k_route
+  void launch_route(hipStream_t s, const DS& d, u32 nmax, bool imports = false) {
     Range rg("chanamq.K6-K13.route_store");
-    if (d.tb_max) {
-      u64 waves = (u64)((nmax + 15) / 16) * (d.tb_pad / 16);
-      hipLaunchKernelGGL(k_topic_mfma, wave_blocks(waves), dim3(256), 0, s, d);
-    }
-    hipLaunchKernelGGL(k_route, wave_blocks(nmax), dim3(256), 0, s, d);
+    const dim3 groups = capped(ceil_div(nmax ? nmax : 1, 16), 2048);   // 16 publishes per block
+    if (imports) hipLaunchKernelGGL(k_import_route, groups, dim3(1024), 0, s, d);   // + prep, link acks
+    else hipLaunchKernelGGL(k_route, groups, dim3(1024), 0, s, d);
     // scan of the routing counts + the phase's log reservation, then pairs + store
     const ScanArgs a = scan_args({{d.pub_nq, d.pub_pair_off}, {d.pub_slot, d.pub_slot_off},
                                   {d.pub_routed, d.pub_routed_rank}, {d.pub_ret_sz, d.pub_ret_off}},
@@ -1473,8 +1489,7 @@ class Engine {
   // world > 1, after the all-to-all: import, route against local queues, rest of the step
   void launch_phase_b(hipStream_t s, const DS& d, bool dispatch = true) {
     Range rg("chanamq.X1.import");
-    hipLaunchKernelGGL(k_import, capped(ceil_div(d.import_max, 256), 1024), dim3(256), 0, s, d);   // + prep, link acks
-    launch_route(s, d, d.import_max);
+    launch_route(s, d, d.import_max, /*imports=*/true);
     launch_tail(s, d, dispatch);
   }
 

@@ -32,7 +32,7 @@ def main(db, rank_steps, out=None):
         n = n.split("(")[0].replace("void ", "")
         if "k_" not in n:
             continue
-        if n in ("k_stage", "k_import"):
+        if n in ("k_stage", "k_import", "k_import_route"):
             cur_seq = []
             seqs.append(cur_seq)
         if cur_seq is not None:
