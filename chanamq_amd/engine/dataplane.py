@@ -15,7 +15,8 @@ import numpy as np
 from .. import ops
 from ..protocol import constants as C
 from .control import ControlError, ControlState
-from .layout import (CONN_OUT, CONSUMED_REC, RING_MOVE, CTRL_REC, CTRL_TXBUF, INVALID, MF_PERSIST, MF_REDELIVERED, MF_RESTORE,
+from .layout import (CONN_OUT, CONSUMED_REC, RING_MOVE, CTRL_REC, CTRL_TXBUF, INVALID, MF_HAS_TS, MF_HOSTPUB, MF_PERSIST,
+                     MF_REDELIVERED, MF_RESTORE,
                      PERSIST_HDR, RDESC, SEG_IN, SEG_OUT, SS_CTRL, US_ACKED, US_PENDING, US_REQUEUE, USLOT,
                      chan_hash, direct_key, exch_hash, fnv1a64, topic_pattern_row, topic_word_offsets)
 
@@ -457,6 +458,43 @@ class GpuDataPlane(ControlState):
             total += self.eng.restore(desc.view(np.uint8), np.frombuffer(bytes(pay) or b"\0", np.uint8)[:len(pay)],
                                       now)
         return total
+
+    # ---- messages larger than a connection's carry (host-assembled publishes)
+    def take_carry(self, conn):
+        """The bytes the device holds for a paused connection (its carry: the frames after
+        a command the host took over), removed from the device."""
+        n = int(np.frombuffer(self.eng.download("carry_len", 4 * conn, 4), np.uint32)[0])
+        data = bytes(self.eng.download("carry", conn * self.info["carry_cap"], n)) if n else b""
+        self._up_at("carry_len", 0, conn, np.uint32)
+        self.carry[conn] = 0
+        return data
+
+    def max_host_message(self):
+        """Largest message the host-publish path takes: it must fit the restore buffers and
+        one step's egress (its Basic.Deliver frames) with room to spare."""
+        i = self.info
+        return max(0, min(i["xfer_bytes"] - 4096, i["egress_cap"] // 2, i["log_bytes"] // 4))
+
+    def publish_host(self, conn, ch, exch_slot, ex, rk, props, body, flags, expire_ms=0, ts_ms=0, now_ms=None):
+        """Enqueue a publish the host assembled (larger than the connection's carry):
+        routed on the device by its exchange like any publish, counted for the publisher
+        channel's confirms (the next step's Basic.Ack / Nack covers it).  Between steps.
+        Returns the number of messages stored (0: unroutable or dropped)."""
+        now = int(time.time() * 1000) if now_ms is None else int(now_ms)
+        if self.world > 1:
+            raise ControlError(C.NOT_IMPLEMENTED, "messages larger than the connection carry are not "
+                                                  "supported on sharded planes", 60, 40)
+        desc = np.zeros(1, RDESC)
+        d = desc[0]
+        d["pay_off"], d["body_len"], d["props_len"], d["exch"] = 0, len(body), len(props), exch_slot
+        d["flags"] = MF_HOSTPUB | (flags & (MF_PERSIST | MF_HAS_TS))
+        d["ex_len"], d["rk_len"] = len(ex), len(rk)
+        d["expire_ms"], d["ts_ms"], d["xid"], d["tq"] = expire_ms, ts_ms, 0, 0
+        d["pad"][0] = self.chslot(conn, ch)
+        d["pad"][1] = conn
+        rec = bytes(ex) + bytes(rk) + bytes(props) + bytes(body)
+        pay = np.frombuffer(rec + b"\0" * ((-len(rec)) % 16), np.uint8)
+        return self.eng.restore(desc.view(np.uint8), pay, now)
 
     ID_SLOT_BITS = 18   # dp_state.h: snowflake id slots per millisecond (64 worker ids x 4096)
 

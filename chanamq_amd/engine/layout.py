@@ -16,7 +16,7 @@ RDESC = np.dtype([("pay_off", "<u4"), ("body_len", "<u4"), ("props_len", "<u4"),
                   ("flags", "<u4"), ("ex_len", "u1"), ("rk_len", "u1"), ("pad0", "<u2"),
                   ("expire_ms", "<i8"), ("ts_ms", "<i8"), ("xid", "<u8"), ("tq", "<u4"), ("pad", "<u4", 3)])
 MF_PERSIST, MF_MANDATORY, MF_IMMEDIATE, MF_HAS_TS, MF_IMPORTED = 1, 2, 4, 8, 16
-MF_RESTORE, MF_REDELIVERED, MF_ONEQ, MF_SLOTFMT = 32, 64, 128, 256
+MF_RESTORE, MF_REDELIVERED, MF_ONEQ, MF_SLOTFMT, MF_HOSTPUB = 32, 64, 128, 256, 512
 # persistence records (dp_common.h PersistHdr / ConsumedRec)
 PERSIST_HDR = np.dtype([("msg_id", "<i8"), ("ts_ms", "<i8"), ("qpos", "<u8"), ("expire_ms", "<i8"), ("q", "<u4"),
                         ("body_len", "<u4"), ("props_len", "<u2"), ("ex_len", "u1"), ("rk_len", "u1"),

@@ -32,9 +32,10 @@ import uuid
 import numpy as np
 
 from ..engine.control import ControlError, normalize_vhost
-from ..engine.layout import SS_FRAME_ERROR, SS_OVERFLOW, SS_TOO_LARGE, SS_UNEXPECTED
+from ..engine.layout import MF_HAS_TS, MF_PERSIST, SS_FRAME_ERROR, SS_OVERFLOW, SS_TOO_LARGE, SS_UNEXPECTED
 from ..protocol import constants as C
-from ..protocol.codec import Method, decode_method, encode_method_frame, encode_table
+from ..protocol.codec import (Method, decode_content_header, decode_method, encode_method_frame, encode_table,
+                              render_command)
 
 HEARTBEAT = C.HEARTBEAT_FRAME
 _REPLICATED_METHODS = {"exchange.declare", "exchange.delete", "queue.declare", "queue.bind", "queue.unbind",
@@ -44,11 +45,12 @@ _STORED_METHODS = _REPLICATED_METHODS
 
 class _Conn:
     __slots__ = ("sock", "id", "state", "inbuf", "out", "frame_max", "heartbeat", "last_rx", "last_tx",
-                 "closing_channels", "last_queue", "peer", "user", "cap_blocked")
+                 "closing_channels", "last_queue", "peer", "user", "cap_blocked", "big")
 
     def __init__(self, sock, cid, peer):
         self.sock, self.id, self.peer = sock, cid, peer
-        self.state = "header"   # header -> start -> tune -> open -> closing -> closed
+        self.state = "header"   # header -> start -> tune -> open (<-> bigpub) -> closing -> closed
+        self.big = None         # a publish larger than the device carry being assembled on the host
         self.inbuf = bytearray()
         self.out = bytearray()
         self.frame_max = 131072
@@ -654,7 +656,10 @@ class GpuBroker:
 
     def _host_bytes(self, c, data):
         """Bytes of a connection that is not (yet / any more) on the data plane:
-        handshake, or waiting for Connection.CloseOk.  Returns data-plane leftovers."""
+        handshake, a large publish being assembled, or waiting for Connection.CloseOk.
+        Returns data-plane leftovers."""
+        if c.state == "bigpub":
+            return self._big_feed(c, data)
         if c.state in ("header", "start", "tune"):
             c.inbuf += data
             try:
@@ -967,6 +972,8 @@ class GpuBroker:
             return self._send(c, ch, Method("channel.open_ok"))
         if ch not in chans:
             raise _Hard(C.CHANNEL_ERROR, f"channel {ch} is not open", m.class_id, m.method_id)
+        if m.name == "basic.publish":   # the device hands over only publishes larger than its carry
+            return self._big_begin(c, ch, m, raw, size)
         try:
             if self.node is not None and m.name in _REPLICATED_METHODS:
                 return self._replicated(c, ch, m)
@@ -980,6 +987,116 @@ class GpuBroker:
             if e.code >= 500 or e.code in (C.CONNECTION_FORCED, C.INVALID_PATH):
                 raise _Hard(e.code, e.text, e.class_id or m.class_id, e.method_id or m.method_id)
             self._chan_close(c, ch, e.code, e.text, m.class_id, m.method_id)
+
+    # ------------------------------------------------------------------ large messages
+    # A publish whose frames cannot fit the connection's device carry (64 MB bodies, say)
+    # reaches the host as a control command (its method + header frames).  The host reads
+    # the body frames -- the device's carry first, then the socket in host mode --, then
+    # enqueues the message through the device's import path (GpuDataPlane.publish_host:
+    # routed by its exchange, counted for the channel's confirms) and hands the connection
+    # back to the data plane with whatever followed the body.
+    def _big_begin(self, c, ch, m, raw, msize):
+        p = self.plane
+        hoff = 8 + msize
+        _, _, hsize = struct.unpack_from(">BHI", raw, hoff)
+        hp = bytes(raw[hoff + 7:hoff + 7 + hsize])
+        _, body_size, props = decode_content_header(hp)
+        vh = p.conns[c.id].vhost
+        x = p.exchanges.get((vh, m.exchange))
+        err = None
+        if x is None:
+            err = (C.NOT_FOUND, f"no exchange '{m.exchange}' in vhost '{vh}'")
+        elif getattr(p.channel(c.id, ch), "tx", False):
+            err = (C.NOT_IMPLEMENTED, "a message larger than the connection buffer inside a transaction")
+        elif body_size > p.max_host_message():
+            err = (C.CONTENT_TOO_LARGE, f"message body of {body_size} bytes exceeds the broker's "
+                                        f"{p.max_host_message()}-byte limit")
+        c.big = dict(ch=ch, m=m, x=x, props=props, props_raw=hp[12:], size=body_size, body=bytearray(), got=0,
+                     other=bytearray(), buf=bytearray(), err=err)
+        c.state = "bigpub"
+        carry = p.take_carry(c.id)
+        if self.fe is not None:
+            self.fe.set_host_mode(c.id)
+        elif self.gw is not None:
+            self.gw.set_data_mode(c.id, False)
+        rest = self._big_feed(c, carry)
+        if c.state == "open" and rest:   # (the body was already complete: cannot happen for a
+            self._big_replay(c, rest)     # message larger than the carry, kept for safety)
+        return "deferred"
+
+    def _big_replay(self, c, rest):
+        if self.fe is not None:
+            self.fe.set_data_mode(c.id, rest)
+        elif self.gw is not None:
+            self.gw.set_data_mode(c.id, True)
+
+    def _big_feed(self, c, data):
+        """Host-mode bytes of a connection assembling a large publish; returns the bytes
+        after it (frames of other channels read meanwhile first) once it is complete."""
+        b = c.big
+        b["buf"] += data
+        buf, pos, done = b["buf"], 0, False
+        while len(buf) - pos >= 8:
+            t, fch, size = struct.unpack_from(">BHI", buf, pos)
+            end = pos + 8 + size
+            if len(buf) < end:
+                break
+            if buf[end - 1] != 0xCE:
+                self._conn_close(c, C.FRAME_ERROR, "malformed frame")
+                return b""
+            if t == C.FRAME_BODY and fch == b["ch"]:
+                if b["err"] is None:   # a rejected message is read and dropped
+                    b["body"] += buf[pos + 7:end - 1]
+                b["got"] += size
+                if b["got"] > b["size"]:
+                    self._conn_close(c, C.FRAME_ERROR, "body frames exceed the announced size")
+                    return b""
+            elif t == C.FRAME_HEARTBEAT:
+                pass
+            elif fch == b["ch"]:
+                self._conn_close(c, C.UNEXPECTED_FRAME, "frame inside a message's content", 60, 40)
+                return b""
+            else:   # another channel's frame: replayed to the data plane after the message
+                b["other"] += buf[pos:end]
+            pos = end
+            if b["got"] == b["size"]:
+                done = True
+                break
+        if not done:
+            del buf[:pos]
+            return b""
+        rest = bytes(b["other"]) + bytes(buf[pos:])
+        self._big_finish(c)
+        return rest
+
+    def _big_finish(self, c):
+        b, c.big = c.big, None
+        c.state = "open"
+        m, ch, props = b["m"], b["ch"], b["props"]
+        with self.lock:
+            if b["err"] is not None:
+                code, text = b["err"]
+                self._chan_close(c, ch, code, text, 60, 40)
+            else:
+                now = int(time.time() * 1000)
+                flags = MF_PERSIST if props.get("delivery_mode") == 2 else 0
+                ts = props.get("timestamp")
+                ts_ms = int(ts) * 1000 if ts is not None else 0
+                if ts is not None:
+                    flags |= MF_HAS_TS
+                exp = props.get("expiration")
+                exp = exp.decode() if isinstance(exp, (bytes, bytearray)) else exp
+                expire_ms = now + int(exp) if isinstance(exp, str) and exp.isdigit() else 0
+                n = self.plane.publish_host(c.id, ch, b["x"].slot, m.exchange.encode(), m.routing_key.encode(),
+                                           b["props_raw"], bytes(b["body"]), flags, expire_ms, ts_ms, now)
+                self.stats["big_publishes"] = self.stats.get("big_publishes", 0) + 1
+                if n == 0 and m.mandatory:
+                    c.out += render_command(ch, Method("basic.return", reply_code=C.NO_ROUTE,
+                                                       reply_text=C.REPLY_TEXT.get(C.NO_ROUTE, "NO_ROUTE"),
+                                                       exchange=m.exchange, routing_key=m.routing_key),
+                                            props, bytes(b["body"]), c.frame_max)
+            self._unpause(c.id)
+        self._flush(c)
 
     def _connection_method(self, c, m):
         if m.name == "connection.close":

@@ -56,7 +56,9 @@ DEV u32 fnv1a32(const u8* p, u32 n) {
 
 struct __attribute__((packed, aligned(1))) U4 { u32 x, y, z, w; };
 
-// unaligned-source, unaligned-dest byte copy by the 64 lanes of one wave
+// unaligned-source, unaligned-dest byte copy by the 64 lanes of one wave (kept minimal:
+// it is inlined into the store / render / pack kernels, and a batched variant with 8
+// loads in flight raised their VGPR count and cost them ~20% at 1 KB messages, measured)
 DEV void wave_copy(u8* dst, const u8* src, u32 n) {
   u32 lane = lane_id();
   u32 nv = n >> 4;
@@ -431,6 +433,15 @@ constexpr u32 FS_AM_MAX = 8192;  // 128 KB segment; 16 KB of LDS
 // one block of FS_NT threads per segment: 16 waves (4 per SIMD) hide the screen's
 // dependent integer chains, which one wave per SIMD could not
 #define FS_NT 1024
+// a content publish whose whole command (method + header + body frames) cannot fit the
+// connection's carry: the host assembles it (FE_CTRL of its method + header frames; the
+// body is read on the host and enqueued as an MF_HOSTPUB record)
+DEV bool big_publish(const DS& d, u32 msize, u32 hsize, u64 bsz, u32 fmax) {
+  const u64 fb = fmax > 8 ? fmax - 8 : 0;
+  const u64 nb = bsz == 0 ? 0 : (fb ? (bsz + fb - 1) / fb : 1);
+  return (u64)msize + 8 + hsize + 8 + bsz + 8 * nb > d.carry_cap;
+}
+
 DEV void frame_scan_seg(const DS& d, const u32 s) {
   __shared__ u32 cpos[CAND_MAX];
   __shared__ int16_t csucc[CAND_MAX];
@@ -749,6 +760,10 @@ DEV void frame_scan_seg(const DS& d, const u32 s) {
     if (hi.type != 2 || hi.ch != fi.ch || hi.size < 14) { atomicMin(&sh_stop, (f << 3) | 2); continue; }
     claim[g] = 1;
     u64 bsz = be64(b + hp + 7 + 4);
+    if (data && big_publish(d, fi.size, hi.size, bsz, fmax)) {   // host-assembled: stop after its header
+      atomicMin(&sh_stop, ((g + 1) << 3) | 0);
+      continue;
+    }
     u64 got = 0;
     u32 e = g;
     bool bad = false, incomplete = false;
@@ -890,6 +905,9 @@ DEV void frame_scan_seg(const DS& d, const u32 s) {
         c.h_off = wbase + hp + 7;
         c.h_len = hi.size;
         c.body_size = (u32)be64(b + hp + 7 + 4);
+        // a publish too large for the carry is a control command: the host assembles it
+        if ((c.kind == CK_PUBLISH || c.kind == CK_TXBUF) && big_publish(d, fi.size, hi.size, be64(b + hp + 7 + 4), fmax))
+          c.kind = CK_CONTROL;
         c.frag0 = sh_frag_base + frun + fr;
         c.nfrag = nfr;
         endp = hp + 8 + hi.size;
@@ -2257,6 +2275,11 @@ DEV void import_one(const DS& d, u32 i, const u32* xr) {
   pb.nwords = routed ? 0u : build_keyvec(d, key, rd.rk_len, pi);
   pb.nq = 0; pb.slot_bytes = 0; pb.msg = INVALID; pb.xid = rd.xid;
   pb.pad = src;  // source rank (pair ordering)
+  if (rd.flags & MF_HOSTPUB) {   // the publisher's channel: confirm counting, Nack on a drop
+    pb.chslot = rd.pad[0];
+    pb.conn = rd.pad[1];
+    if (pb.chslot < d.c_max * d.chpc && d.ch_confirm[pb.chslot]) atomicAdd(&d.ch_pub_cnt[pb.chslot], 1u);
+  }
   if (routed) {
     // routing pass 0 for a record that arrived with its queue (what route_one<0> computes
     // for it: one local queue, no return, never forwarded); route_one<0> skips it
@@ -2617,12 +2640,36 @@ DEV void unreserve(const DS& d, u32 c, u32 take) {
 // sizes), then one delivery run per granted consumer.  k_runs orders the runs by channel
 // and k_dv_write expands them into Deliv records at their final positions, so no sort
 // over individual deliveries is needed (QueueEntity.scala:318-393, FrameStage.scala:380-406).
+#define REQ_BLK 1024
+DEV void requeue_compact(const DS& d);
+DEV void requeue_queue(const DS& d, u32 q, u64* kpos, u32* kidx, u32* cnt_p);
 __global__ __launch_bounds__(256) void k_dequeue(DS d) {
   __shared__ u32 g_cons[RUNS_PER_Q];
   __shared__ u32 g_n[RUNS_PER_Q];
   __shared__ u64 s_head;
   __shared__ unsigned long long s_bytes;
+  __shared__ u64 kpos[REQ_BLK];
+  __shared__ u32 kidx[REQ_BLK];
+  __shared__ u32 rq_cnt, rq_last;
   const u32 q = blockIdx.x, tid = threadIdx.x, lane = lane_id();
+  if (q == 0 && tid == 0) *d.n_dirty = 0;   // fused k_reset_dirty (k_chan_advance consumed the list)
+  // fused k_requeue: requeued deliveries go back in front of their queues' heads before this
+  // step's dispatch, in queue-offset order.  Every block takes the ticket (req_n only
+  // changes in the compaction, which runs after every block has read it); the last one
+  // compacts the unconsumed items
+  if (*d.req_n != 0) {
+    if (q < d.q_max && d.req_q_n[q] != 0) requeue_queue(d, q, kpos, kidx, &rq_cnt);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __syncthreads();
+    if (tid == 0) rq_last = atomicAdd(&d.tot[TS_REQ_TICKET], 1u) == gridDim.x - 1;
+    __syncthreads();
+    if (rq_last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      if (tid == 0) d.tot[TS_REQ_TICKET] = 0;
+      requeue_compact(d);
+      __syncthreads();
+    }
+  }
   if (q >= d.q_max) return;
   if (!d.q_active[q]) {
     if (tid == 0) d.q_nruns[q] = 0;
@@ -2633,7 +2680,9 @@ __global__ __launch_bounds__(256) void k_dequeue(DS d) {
     if (tid == 0) d.q_nruns[q] = 0;
     return;
   }
-  u64 head = d.q_head[q];
+  // agent-scope load: the requeue above (this block's thread 0) may have moved the head
+  // after this wave read the line
+  u64 head = __hip_atomic_load(&d.q_head[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const u64 tail = d.q_tail[q];
   const u64 mask = d.q_ring_mask[q];
   const Desc* ring = d.ring + d.q_ring_off[q];
@@ -2953,22 +3002,52 @@ __global__ void k_conn_sizes(DS d) {
 __global__ __launch_bounds__(1024) void k_conn_layout(DS d) {
   __shared__ u32 lds[1024 / 64 + 1];
   // exclusive scan of the deliveries' rendered sizes (fused k_scan: one block walks the
-  // step's deliveries 4096 at a time, cheaper than a separate launch at these sizes)
+  // step's deliveries 16K at a time -- 16 per thread, all loads of a pass in flight at
+  // once, one block scan per pass: a step's deliveries usually take one pass)
   {
     u32 n = d.ctr->n_deliv;
     if (n > d.deliv_max) n = d.deliv_max;
     u32 acc = 0;
-    for (u32 b0 = 0; b0 < n; b0 += 4096) {
-      const u32 i = b0 + threadIdx.x * 4;
-      u32 v0 = i < n ? d.dv_size[i] : 0, v1 = i + 1 < n ? d.dv_size[i + 1] : 0;
-      u32 v2 = i + 2 < n ? d.dv_size[i + 2] : 0, v3 = i + 3 < n ? d.dv_size[i + 3] : 0;
+    constexpr u32 EPT = 16;
+    for (u32 b0 = 0; b0 < n; b0 += 1024 * EPT) {
+      const u32 i0 = b0 + threadIdx.x * EPT;
+      u32 v[EPT];
+      if (i0 + EPT <= n) {   // dv_size is 16-byte aligned and i0 a multiple of 16
+        const uint4* src = (const uint4*)(d.dv_size + i0);
+#pragma unroll
+        for (u32 k = 0; k < EPT / 4; ++k) {
+          const uint4 x = src[k];
+          v[4 * k] = x.x; v[4 * k + 1] = x.y; v[4 * k + 2] = x.z; v[4 * k + 3] = x.w;
+        }
+      } else {
+#pragma unroll
+        for (u32 k = 0; k < EPT; ++k) v[k] = i0 + k < n ? d.dv_size[i0 + k] : 0u;
+      }
+      u32 sum = 0;
+#pragma unroll
+      for (u32 k = 0; k < EPT; ++k) sum += v[k];
       u32 all;
-      const u32 o = acc + block_scan<1024>(v0 + v1 + v2 + v3, lds, all);
-      if (i < n) d.dv_off[i] = o;
-      if (i + 1 < n) d.dv_off[i + 1] = o + v0;
-      if (i + 2 < n) d.dv_off[i + 2] = o + v0 + v1;
-      if (i + 3 < n) d.dv_off[i + 3] = o + v0 + v1 + v2;
+      u32 o = acc + block_scan<1024>(sum, lds, all);
+      if (i0 + EPT <= n) {
+        uint4* dst = (uint4*)(d.dv_off + i0);
+#pragma unroll
+        for (u32 k = 0; k < EPT / 4; ++k) {
+          uint4 x;
+          x.x = o; o += v[4 * k];
+          x.y = o; o += v[4 * k + 1];
+          x.z = o; o += v[4 * k + 2];
+          x.w = o; o += v[4 * k + 3];
+          dst[k] = x;
+        }
+      } else {
+#pragma unroll
+        for (u32 k = 0; k < EPT; ++k) {
+          if (i0 + k < n) d.dv_off[i0 + k] = o;
+          o += v[k];
+        }
+      }
       acc += all;
+      __syncthreads();   // lds of the next pass's scan
     }
     if (threadIdx.x == 0) d.tot[6] = acc;
     __syncthreads();
@@ -3553,35 +3632,9 @@ __global__ __launch_bounds__(64) void k_basic_get(DS d, u32 q, u32 ch, u32 noack
 }
 
 // ============================================================================ requeue (pre-step)
-// one block per queue with requeued items: gather, bitonic-sort by queue position,
-// push back in front of the head with the redelivered flag (QueueEntity.scala:415-446)
-#define REQ_BLK 1024
-DEV void requeue_compact(const DS& d);
-DEV void requeue_queue(const DS& d, u32 q, u64* kpos, u32* kidx, u32* cnt_p);
-__global__ __launch_bounds__(256) void k_requeue(DS d) {
-  __shared__ u64 kpos[REQ_BLK];
-  __shared__ u32 kidx[REQ_BLK];
-  __shared__ u32 cnt;
-  __shared__ u32 s_last;
-  if (blockIdx.x == 0 && threadIdx.x == 0) *d.n_dirty = 0;   // fused k_reset_dirty (after k_chan_advance)
-  // nothing requeued (the common step): no block takes the ticket, nothing to compact.
-  // req_n only changes in the compaction, which runs after every block has read it
-  if (*d.req_n == 0) return;
-  // grid-stride over queues: a bounded grid keeps the completion ticket below (one
-  // same-address atomic per block) from serialising thousands of blocks
-  for (u32 q = blockIdx.x; q < d.q_max; q += gridDim.x)
-    if (d.req_q_n[q] != 0) requeue_queue(d, q, kpos, kidx, &cnt);
-  // the last block to finish compacts the unconsumed items (fused k_requeue_compact)
-  __threadfence();
-  __syncthreads();
-  if (threadIdx.x == 0) s_last = atomicAdd(&d.tot[TS_REQ_TICKET], 1u) == gridDim.x - 1;
-  __syncthreads();
-  if (!s_last) return;
-  __threadfence();
-  if (threadIdx.x == 0) d.tot[TS_REQ_TICKET] = 0;
-  requeue_compact(d);
-}
-
+// run by k_dequeue (fused k_requeue): the block of a queue with requeued items gathers
+// them, bitonic-sorts by queue position and pushes them back in front of the head with
+// the redelivered flag (QueueEntity.scala:415-446); the last block compacts the rest
 DEV void requeue_queue(const DS& d, u32 q, u64* kpos, u32* kidx, u32* cnt_p) {
   u32& cnt = *cnt_p;
   u32 tid = threadIdx.x;
@@ -3627,7 +3680,8 @@ DEV void requeue_queue(const DS& d, u32 q, u64* kpos, u32* kidx, u32* cnt_p) {
     ds.flags = 1;
     ds.expire_ms = r.expire_ms;
     d.ring[d.q_ring_off[q] + ((head - k + i) & mask)] = ds;
-    d.req[kidx[i]].q = INVALID;  // consumed
+    // consumed (agent-coherent: the compacting block of another XCD reads it after the ticket)
+    __hip_atomic_store(&d.req[kidx[i]].q, INVALID, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   __syncthreads();
   if (tid == 0) {

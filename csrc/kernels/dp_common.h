@@ -32,8 +32,10 @@ enum : u32 {
   MF_RESTORE = 32,      // recovered from the store: enqueue into exactly RDesc.tq, keep RDesc.xid
   MF_REDELIVERED = 64,  // enqueue with the redelivered flag (recovered unacks)
   MF_ONEQ = 128,        // cross-rank record routed at its origin to exactly one queue: RDesc.tq
-  MF_SLOTFMT = 256      // cross-rank record laid out as a body-log slot ([ex][rk][props] padded
+  MF_SLOTFMT = 256,     // cross-rank record laid out as a body-log slot ([ex][rk][props] padded
                         // to 16, then the body): the owner stores it with one aligned copy
+  MF_HOSTPUB = 512      // a publish assembled by the host (larger than the connection carry):
+                        // routed by its exchange, publisher channel in RDesc.pad[0], conn pad[1]
 };
 
 // ---- unacked slot states

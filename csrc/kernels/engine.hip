@@ -94,7 +94,9 @@ class Engine {
     d_.persist = (u32)get("persist", 0);
     d_.persist_max = d_.persist ? (u32)get("persist_max", d_.cmd_max) : 0;
     d_.persist_bytes = d_.persist ? get("persist_bytes", 64ull << 20) : 0;
-    restore_max_ = (u32)get("restore_max", d_.persist ? (1u << 14) : 0);
+    // restore / host-publish records at world 1: recovery batches (persist) and messages
+    // larger than a connection's carry, assembled by the host (MF_HOSTPUB)
+    restore_max_ = (u32)get("restore_max", d_.persist ? (1u << 14) : 64);
     if (d_.world == 1 && restore_max_) {
       d_.import_max = restore_max_;
       d_.pub_cap = ((d_.pub_max + d_.import_max + 63) / 64) * 64;
@@ -128,7 +130,7 @@ class Engine {
     d_.n_log_blocks = d_.log_bytes / d_.log_block;
     d_.ingress_cap = get("ingress_cap", 64ull << 20);
     d_.xfer_bytes = d_.world > 1 ? get("xfer_bytes", (d_.world - 1) * (d_.ingress_cap + 64))
-                                 : (restore_max_ ? get("restore_bytes", 64ull << 20) : 0);
+                                 : (restore_max_ ? get("restore_bytes", 80ull << 20) : 0);
     // work buffer = this step's new bytes + the carries of the connections in the step.
     // carry_cap bounds one connection's (= the largest command assembled on the device,
     // e.g. a multi-MB message); carry_budget bounds their sum per step (the front end
@@ -1449,9 +1451,8 @@ class Engine {
       return;
     }
     hipLaunchKernelGGL(k_chan_advance, capped(nch, 1024), dim3(256), 0, s, d);
-    // requeued deliveries go back in front of their queues' heads before this step's
-    // dispatch, in queue-offset order (QueueEntity.scala:415-446)
-    hipLaunchKernelGGL(k_requeue, dim3(d.q_max < 256 ? d.q_max : 256), dim3(256), 0, s, d);
+    // k_dequeue first puts requeued deliveries back in front of their queues' heads, in
+    // queue-offset order (QueueEntity.scala:415-446), then dispatches
     hipLaunchKernelGGL(k_dequeue, dim3(d.q_max), dim3(256), 0, s, d);
     hipLaunchKernelGGL(k_runs, dim3(1), dim3(1024), 0, s, d);
     hipLaunchKernelGGL(k_dv_write, blocks(d.deliv_max, 256), dim3(256), 0, s, d);

@@ -473,3 +473,54 @@ def test_config5_storm_setup_64p64c_against_pipelined_server(gpu):
     assert r["error"] == "", r["error"]
     assert r["sent"] > 0 and r["received"] > 0
     assert wall < 60, f"64P x 64C setup + 2.5 s of load took {wall:.1f} s"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("io", ["native", "pipeline"])
+def test_64mb_message_assembled_on_the_host(gpu, io):
+    """A 64 MB publish (512 body frames, 256x the 256 KB connection carry) is handed to the
+    host by the frame scan, assembled from the device carry + the socket, enqueued through
+    the device's import path and delivered intact; its confirm comes from the device, the
+    connection carries on with the publishes after it, a mandatory unroutable one comes
+    back as Basic.Return, and one above the broker's limit closes the channel with 311
+    (FrameParser.scala:67 has no size limit)."""
+    from chanamq_amd.engine.dataplane import GpuDataPlane
+    from chanamq_amd.server.gpu_broker import GpuBroker
+    cfg = dict(GPU_CFG, egress_cap=192 << 20, log_bytes=512 << 20, log_block=32 << 20)
+    plane = GpuDataPlane(default_queue_capacity=1 << 12, **cfg)
+    b = GpuBroker(plane, idle_step_ms=1.0, io=io, ingress_bytes=8 << 20).start()
+    try:
+        assert plane.max_host_message() >= (64 << 20)
+        p = conn(b)
+        ch = p.channel()
+        ch.queue_declare("huge")
+        ch.confirm_select()
+        body = bytes((i * 131 + 7) & 0xFF for i in range(256)) * ((64 << 20) // 256)
+        ch.basic_publish("", "huge", b"before")
+        ch.basic_publish("", "huge", body, {"delivery_mode": 1, "content_type": "application/octet-stream"})
+        ch.basic_publish("", "huge", b"after")
+        assert ch.wait_for_confirms(timeout=120)
+        c = conn(b)
+        cc = c.channel()
+        cc.basic_consume("huge", "hc", no_ack=True)
+        got = cc.consume_n(3, timeout=120)
+        assert got[0].body == b"before" and got[2].body == b"after"
+        assert len(got[1].body) == len(body) and got[1].body == body
+        assert got[1].props.get("content_type") in ("application/octet-stream", b"application/octet-stream")
+        # mandatory + unroutable: the host returns it
+        ch.basic_publish("", "no.such.queue", body[:(1 << 20) * 3], mandatory=True)
+        p._wait(lambda: ch.returns or None, ch, timeout=60)
+        r = ch.returns[0]
+        assert r.method.reply_code == 312 and r.body == body[:(1 << 20) * 3]
+        # above the limit: the channel is closed with CONTENT_TOO_LARGE
+        ch2 = p.channel()
+        too_big = plane.max_host_message() + (1 << 20)
+        with pytest.raises(Exception) as e:
+            ch2.basic_publish("", "huge", bytes(too_big))
+            ch2.queue_declare("huge", passive=True)
+        assert "311" in str(e.value) or "CONTENT_TOO_LARGE" in str(e.value).upper()
+        assert b.stats.get("big_publishes", 0) >= 2
+        p.close()
+        c.close()
+    finally:
+        b.stop()
