@@ -52,6 +52,7 @@ class Channel:
         self.flow_active = True
         self.cancelled = []
         self.published = 0
+        self.confirmed_upto = 0   # highest confirmed publish sequence seen (across waits)
         self.confirm_mode = False
 
     # ---------------------------------------------------------------- plumbing
@@ -175,15 +176,15 @@ class Channel:
 
     def wait_for_confirms(self, timeout=10.0):
         """Block until every publish so far is acked; returns False if any was nacked."""
-        state = {"upto": 0, "nacked": False}
+        state = {"nacked": False}
 
         def pred():
             while self.confirms:
                 tag, multiple, ok = self.confirms.popleft()
                 if not ok:
                     state["nacked"] = True
-                state["upto"] = max(state["upto"], tag)
-            return True if state["upto"] >= self.published else None
+                self.confirmed_upto = max(self.confirmed_upto, tag)
+            return True if self.confirmed_upto >= self.published else None
         self.conn._wait(pred, self, timeout)
         return not state["nacked"]
 

@@ -496,6 +496,23 @@ class GpuDataPlane(ControlState):
         pay = np.frombuffer(rec + b"\0" * ((-len(rec)) % 16), np.uint8)
         return self.eng.restore(desc.view(np.uint8), pay, now)
 
+    # ---- cold bodies to host memory (built with spill_bytes > 0)
+    def spill(self, frac=0.5, hot=1024):
+        """Move cold message bodies to the host spill ring (between steps): queued
+        messages whose slot lies in the oldest ``frac`` of the HBM log (but the first
+        ``hot`` of a queue with consumers).  Returns the bytes moved; the log tail advances
+        over the emptied blocks at the next step."""
+        if not self.info.get("spill_bytes"):
+            return 0
+        tail = self._u64("log_tail", 0)
+        return int(self.eng.spill(int(tail + frac * self.info["log_bytes"]), int(hot)))
+
+    def spill_used(self):
+        """Bytes between the spill ring's tail and head (live + not yet reclaimed)."""
+        if not self.info.get("spill_bytes"):
+            return 0
+        return self._u64("spill_head", 0) - self._u64("spill_tail", 0)
+
     ID_SLOT_BITS = 18   # dp_state.h: snowflake id slots per millisecond (64 worker ids x 4096)
 
     def seed_ids(self, min_ms):

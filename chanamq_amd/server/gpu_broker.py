@@ -114,7 +114,7 @@ class GpuBroker:
     def __init__(self, plane, host="127.0.0.1", port=0, heartbeat=0, frame_max=131072, channel_max=2047,
                  idle_step_ms=2.0, product="chanamq-amd", version="0.1.0", io="native",
                  ingress_bytes=64 << 20, per_conn_read=256 << 10, mem_high_watermark=None, mem_low_watermark=None,
-                 store=None, node=None, reuseport=False, io_threads=4, fe_cfg=None):
+                 store=None, node=None, reuseport=False, io_threads=4, fe_cfg=None, spill_at=None, spill_hot=1024):
         """``io``: "pipeline" = native pipelined front end (csrc/core/frontend.cpp: IO
         threads + a stepper thread keeping two steps in flight, no Python per step),
         "native" = C++ batched gateway polled by a Python step loop (csrc/core/
@@ -153,6 +153,14 @@ class GpuBroker:
         self.log_high = log_bytes // 2 if self.mem_high else 0
         self.log_low = log_bytes // 4 if self.mem_high else 0
         self.blocked = False
+        # cold bodies to host memory (a plane built with spill_bytes): once the HBM log is
+        # this full, queued messages whose bodies sit in the oldest half of the log move
+        # to the host spill ring (but the first ``spill_hot`` of a queue with consumers),
+        # so the log tail advances and publishers keep going until the spill ring fills
+        sb = plane.info.get("spill_bytes", 0) if hasattr(plane, "info") else 0
+        self.spill_at = (int(0.3 * log_bytes) if spill_at is None else int(spill_at)) if sb else 0
+        self.spill_hot = spill_hot
+        self._last_spill = 0.0
         # durable queues x persistent messages -> store (write-behind, confirm gating)
         self.persistence = None
         self.recovered = 0
@@ -1551,6 +1559,8 @@ class GpuBroker:
                 self._flush(c)
 
     def _watermarks(self):
+        if self.spill_at:
+            self._maybe_spill()
         if not self.mem_high:
             return
         if self.fe is not None and self._fe_stats:
@@ -1570,6 +1580,22 @@ class GpuBroker:
         elif self.blocked and low:
             self.blocked = False
             self._set_flow(True)
+
+    def _maybe_spill(self):
+        if self.fe is not None and self._fe_stats:
+            logu = self._fe_stats["log_used"]
+        else:
+            lc = getattr(self.plane, "last_counters", None) or {}
+            logu = lc.get("log_head", 0) - lc.get("log_tail", 0)
+        now = time.monotonic()
+        if logu < self.spill_at or now - self._last_spill < 0.05:
+            return
+        self._last_spill = now
+        with self.lock:
+            moved = self.plane.spill(0.5, self.spill_hot)
+        if moved:
+            self.stats["spilled_bytes"] = self.stats.get("spilled_bytes", 0) + moved
+            self.stats["spills"] = self.stats.get("spills", 0) + 1
 
     def _set_flow(self, active):
         for c in list(self.conns.values()):

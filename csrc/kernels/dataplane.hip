@@ -198,15 +198,30 @@ DEV u32 wave_reserve(u32* ctr, bool want, u32* total_out = nullptr) {
   return base + __popcll(m & lanemask_lt());
 }
 
+// a message's slot: the HBM body log, or the host spill ring for a spilled cold body
+DEV const u8* msg_slot(const DS& d, u64 log_off) {
+  return (log_off & SPILL_BIT) ? d.spill + ((log_off & ~SPILL_BIT) % d.spill_bytes) : d.log + (log_off % d.log_bytes);
+}
+
+// live-bytes accounting of a freed slot in the spill ring
+DEV void spill_free(const DS& d, u64 log_off, u32 slot_bytes) {
+  const u64 blk = ((log_off & ~SPILL_BIT) / d.log_block) % d.n_spill_blocks;
+  atomicAdd((unsigned long long*)&d.spill_live[blk], (unsigned long long)(-(i64)slot_bytes));
+}
+
 // ---- message release (K11): refcount -1, free slot + table index at zero
 DEV void release_msg(const DS& d, u32 msg) {
   if (msg == INVALID) return;
   i32 old = atomicSub(&d.msgs[msg].refcnt, 1);
   if (old == 1) {
     MsgEnt& m = d.msgs[msg];
-    u64 blk = (m.log_off / d.log_block) % d.n_log_blocks;
-    atomicAdd((unsigned long long*)&d.log_live[blk], (unsigned long long)(-(i64)m.slot_bytes));
-    atomicAdd((unsigned long long*)d.live_bytes, (unsigned long long)(-(i64)m.slot_bytes));
+    if (m.log_off & SPILL_BIT) {
+      spill_free(d, m.log_off, m.slot_bytes);
+    } else {
+      u64 blk = (m.log_off / d.log_block) % d.n_log_blocks;
+      atomicAdd((unsigned long long*)&d.log_live[blk], (unsigned long long)(-(i64)m.slot_bytes));
+      atomicAdd((unsigned long long*)d.live_bytes, (unsigned long long)(-(i64)m.slot_bytes));
+    }
     u32 slot = atomicAdd(d.msg_free_top, 1u);
     d.msg_free[slot] = msg;
     atomicAdd(&d.ctr->n_freed, 1u);
@@ -216,15 +231,18 @@ DEV void release_msg(const DS& d, u32 msg) {
 // wave-uniform release: refcount atomics per lane, one free-list reservation and one
 // live-bytes atomic per distinct log block per wave (avoids serialising on hot words)
 DEV void wave_release(const DS& d, u32 msg, bool valid) {
-  bool freed = false;
+  bool freed = false, spilled = false;
   u64 blk = 0;
   i64 sb = 0;
   if (valid && msg != INVALID) {
     i32 old = atomicSub(&d.msgs[msg].refcnt, 1);
     if (old == 1) {
       freed = true;
-      blk = (d.msgs[msg].log_off / d.log_block) % d.n_log_blocks;
+      const u64 lo = d.msgs[msg].log_off;
       sb = d.msgs[msg].slot_bytes;
+      spilled = (lo & SPILL_BIT) != 0;
+      if (spilled) spill_free(d, lo, (u32)sb);   // (rare: cold bodies)
+      else blk = (lo / d.log_block) % d.n_log_blocks;
     }
   }
   u64 fm = __ballot(freed);
@@ -232,12 +250,12 @@ DEV void wave_release(const DS& d, u32 msg, bool valid) {
   u32 nf;
   u32 pos = wave_reserve(d.msg_free_top, freed, &nf);
   if (freed) d.msg_free[pos] = msg;
-  i64 tot = wave_sum64(freed ? sb : 0);
+  i64 tot = wave_sum64(freed && !spilled ? sb : 0);
   if (lane_id() == __ffsll((unsigned long long)fm) - 1) {
     atomicAdd(&d.ctr->n_freed, nf);
-    atomicAdd((unsigned long long*)d.live_bytes, (unsigned long long)(-tot));
+    if (tot) atomicAdd((unsigned long long*)d.live_bytes, (unsigned long long)(-tot));
   }
-  wave_add_i64(d.log_live, blk, -sb, freed);
+  wave_add_i64(d.log_live, blk, -sb, freed && !spilled);
 }
 
 // ---- K13 snowflake ids: id = ms << 22 | worker << 12 | seq (IdGenerator.scala:14-34).
@@ -3170,7 +3188,7 @@ DEV void render_deliv(const DS& d, u32 i) {
   const MsgEnt m = d.msgs[dv.msg];
   u32 conn = ch / d.chpc;
   u32 f = d.conn_dfirst[conn];
-  const u8* slot = d.log + (m.log_off % d.log_bytes);
+  const u8* slot = msg_slot(d, m.log_off);
   if (d.links && d.conn_link[conn]) {   // X2: a restore record for the shadow queue
     const u32 dest = d.conn_link[conn] - 1;
     const u32 po = d.link_bbase[conn] + (d.dv_off[i] - d.dv_off[f]);
@@ -3395,6 +3413,17 @@ DEV void final_step(const DS& d) {
   }
   if (tail > head) tail = head;
   *d.log_tail = tail;
+  if (d.spill_bytes) {   // the spill ring's tail, the same way
+    const u64 sh = *d.spill_head;
+    u64 st = *d.spill_tail;
+    while (st < sh) {
+      const u64 bi = st / d.log_block;
+      if (bi == sh / d.log_block) break;
+      if (d.spill_live[bi % d.n_spill_blocks] > 0) break;
+      st = (bi + 1) * d.log_block;
+    }
+    *d.spill_tail = st > sh ? sh : st;
+  }
   Counters* c = d.ctr;
   c->log_head = head;
   c->log_tail = tail;
@@ -3437,7 +3466,7 @@ __global__ __launch_bounds__(256) void k_persist_pack(DS d) {
       continue;
     }
     u8* o = d.persist_h + off;
-    const u8* slot = d.log + (m.log_off % d.log_bytes);
+    const u8* slot = msg_slot(d, m.log_off);
     if (lane == 0) {
       PersistHdr h;
       h.msg_id = (i64)m.msg_id; h.ts_ms = m.ts_ms; h.qpos = r.qpos; h.expire_ms = r.expire_ms;
@@ -3597,7 +3626,7 @@ __global__ __launch_bounds__(64) void k_basic_get(DS d, u32 q, u32 ch, u32 noack
     res->persist = d.q_durable[q] && (m.flags & MF_PERSIST) ? 1u : 0u;
   }
   // render: GetOk(tag, redelivered, exchange, routing-key, message-count) + header + body
-  const u8* slot = d.log + (m.log_off % d.log_bytes);
+  const u8* slot = msg_slot(d, m.log_off);
   const u32 chno = d.ch_num[ch];
   if (lane == 0) {
     u32 p = 0;
@@ -3629,6 +3658,62 @@ __global__ __launch_bounds__(64) void k_basic_get(DS d, u32 q, u32 ch, u32 noack
     bp += bl + 8;
   }
   wave_release(d, ds.msg, noack && lane == 0);
+}
+
+// ============================================================================ spill (between steps)
+// reserve `sz` bytes in the spill ring (never across its wrap), false when it is full
+DEV bool spill_reserve(const DS& d, u32 sz, u64* pos) {
+  unsigned long long cur = __hip_atomic_load(d.spill_head, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const u64 tail = *d.spill_tail;
+  while (true) {
+    u64 h = cur;
+    const u64 phys = h % d.spill_bytes;
+    if (phys + sz > d.spill_bytes) h += d.spill_bytes - phys;
+    if (h + sz - tail > d.spill_bytes) return false;
+    const unsigned long long prev = atomicCAS((unsigned long long*)d.spill_head, cur, (unsigned long long)(h + sz));
+    if (prev == cur) { *pos = h; return true; }
+    cur = prev;
+  }
+}
+
+// Cold bodies to host memory (host-driven, between steps, when the HBM log fills): one
+// block per queue, one wave per ring entry whose body sits in the log below position
+// `lim` -- the oldest part, which pins the log tail: the log is a ring, only its tail
+// frees space -- skipping the first `hot` entries of a queue that has consumers (about to
+// be delivered; a backlog without consumers moves from its head).
+// The slot is copied into the spill ring (pinned host memory), then MsgEnt.log_off is
+// switched with a CAS (a message in several queues moves once; a lost race leaves a
+// never-live gap the spill tail passes).  Its log block loses the bytes, so the next
+// step's final_step can advance the log tail.  Unacked deliveries stay in the log.
+__global__ __launch_bounds__(256) void k_spill(DS d, u64 lim, u32 hot, unsigned long long* moved) {
+  const u32 q = blockIdx.x, lane = lane_id(), w = threadIdx.x >> 6;
+  if (q >= d.q_max || !d.q_active[q] || d.spill_bytes == 0) return;
+  const u64 head = d.q_head[q], tail = d.q_tail[q], mask = d.q_ring_mask[q];
+  const Desc* ring = d.ring + d.q_ring_off[q];
+  const u64 skip = d.q_cons_n[q] ? hot : 0;
+  for (u64 i = head + skip + w; i < tail; i += 4) {
+    const u32 msg = ring[i & mask].msg;
+    if (msg == INVALID || msg >= d.msg_max) continue;
+    MsgEnt& m = d.msgs[msg];
+    const u64 lo = __hip_atomic_load(&m.log_off, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if ((lo & SPILL_BIT) || lo >= lim) continue;
+    const u32 sz = m.slot_bytes;
+    u64 pos = 0;
+    u32 ok = 0;
+    if (lane == 0) ok = spill_reserve(d, sz, &pos) ? 1u : 0u;
+    ok = (u32)__shfl((int)ok, 0);
+    if (!ok) break;   // the spill ring is full
+    pos = shfl64(pos, 0);
+    wave_copy(d.spill + (pos % d.spill_bytes), d.log + (lo % d.log_bytes), sz);
+    __threadfence_system();   // the copy reached host memory before the slot is switched
+    if (lane == 0 &&
+        atomicCAS((unsigned long long*)&m.log_off, (unsigned long long)lo, (unsigned long long)(SPILL_BIT | pos)) == lo) {
+      atomicAdd((unsigned long long*)&d.log_live[(lo / d.log_block) % d.n_log_blocks], (unsigned long long)(-(i64)sz));
+      atomicAdd((unsigned long long*)&d.spill_live[(pos / d.log_block) % d.n_spill_blocks], (unsigned long long)sz);
+      atomicAdd((unsigned long long*)d.live_bytes, (unsigned long long)(-(i64)sz));
+      atomicAdd(moved, (unsigned long long)sz);
+    }
+  }
 }
 
 // ============================================================================ requeue (pre-step)

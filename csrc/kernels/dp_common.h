@@ -124,8 +124,9 @@ struct PersistRec { u32 msg; u32 q; u64 qpos; i64 expire_ms; };
 
 struct Ack { u32 chslot; u32 kind; u64 tag; u32 multiple; u32 requeue; };
 
+#define SPILL_BIT (1ull << 63)   // MsgEnt.log_off: the slot lives in the host spill ring
 struct MsgEnt {         // message table (one per stored message; body stored once per rank)
-  u64 log_off;          // start of slot in body log
+  u64 log_off;          // start of slot in body log (| SPILL_BIT: in the host spill ring)
   u64 msg_id;           // snowflake id
   i64 ts_ms;
   u32 slot_bytes;

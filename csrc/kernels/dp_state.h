@@ -210,7 +210,15 @@ struct DS {
   u64* log_tail;
   u64* log_step_base;
   i64* log_live;            // live bytes per log block
-  i64* live_bytes;          // live slot bytes, all blocks
+  i64* live_bytes;          // live slot bytes in the (HBM) log
+  // cold bodies spilled to host memory (spill_bytes > 0): a ring of pinned host memory in
+  // log_block blocks, read over PCIe when its messages are delivered (MsgEnt.log_off has
+  // SPILL_BIT set and is a position in this ring)
+  u8* spill;
+  u64 spill_bytes, n_spill_blocks;
+  u64* spill_head;
+  u64* spill_tail;
+  i64* spill_live;          // live bytes per spill block
   u64* id_next;             // snowflake virtual sequence position
 
   // ---------------- deliveries

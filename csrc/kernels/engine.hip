@@ -377,6 +377,14 @@ class Engine {
     d_.log_live = (i64*)dev("log_live", 8ull * d_.n_log_blocks);
     d_.live_bytes = (i64*)dev("live_bytes", 8);
     d_.id_next = (u64*)dev("id_next", 8);
+    // cold-body spill ring in pinned host memory (mapped: kernels read / write it over PCIe)
+    d_.spill_bytes = (get("spill_bytes", 0) / d_.log_block) * d_.log_block;
+    d_.n_spill_blocks = d_.spill_bytes / d_.log_block;
+    d_.spill_head = (u64*)dev("spill_head", 8);
+    d_.spill_tail = (u64*)dev("spill_tail", 8);
+    d_.spill_live = (i64*)dev("spill_live", 8ull * (d_.n_spill_blocks ? d_.n_spill_blocks : 1));
+    d_.spill = d_.spill_bytes ? (u8*)hst("spill", d_.spill_bytes + 4096) : nullptr;
+    spill_moved_ = (unsigned long long*)dev("spill_moved", 8);
 
     d_.deliv = (Deliv*)dev("deliv", sizeof(Deliv) * (u64)d_.deliv_max);
     {
@@ -612,6 +620,7 @@ class Engine {
     o["msg_max"] = d_.msg_max; o["ucap"] = d_.ucap_mask + 1; o["deliver_cap"] = d_.deliver_cap;
     o["chmap_size"] = d_.chmap_size; o["xhash"] = d_.xhash_mask + 1; o["dhash"] = d_.dhash_mask + 1;
     o["tb_max"] = d_.tb_max; o["tb_pad"] = d_.tb_pad; o["log_bytes"] = d_.log_bytes;
+    o["spill_bytes"] = d_.spill_bytes;
     o["ingress_cap"] = d_.ingress_cap; o["egress_cap"] = d_.egress_cap; o["ring_pool"] = d_.ring_pool;
     o["work_cap"] = d_.work_cap; o["total_bytes"] = total_bytes_; o["req_max"] = d_.req_max;
     o["carry_budget"] = carry_budget_;
@@ -785,6 +794,24 @@ class Engine {
 
   // recovery: enqueue store records (RDesc with MF_RESTORE, payload [ex][rk][props][body])
   // through the import path, between steps; returns the number of messages enqueued
+  // cold bodies to the host spill ring, between steps: every queued message past the first
+  // `hot` entries of its queue whose slot lies below log position `lim` (k_spill); returns
+  // the bytes moved (the log tail advances over the emptied blocks at the next step)
+  u64 spill(u64 lim, u32 hot) {
+    if (!d_.spill_bytes) return 0;
+    if (inflight_[0] || inflight_[1]) throw std::runtime_error("spill() between steps only");
+    if (native_x_ && (counts_ready_[0] || counts_ready_[1])) throw std::runtime_error("spill() with an exchange pending");
+    Range rg("chanamq.spill");
+    sync();
+    HIPCHECK(hipMemsetAsync(spill_moved_, 0, 8, s_comp_));
+    hipLaunchKernelGGL(k_spill, dim3(d_.q_max), dim3(256), 0, s_comp_, io_[0], lim, hot, spill_moved_);
+    HIPCHECK(hipGetLastError());
+    unsigned long long moved = 0;
+    HIPCHECK(hipMemcpyAsync(&moved, spill_moved_, 8, hipMemcpyDeviceToHost, s_comp_));
+    HIPCHECK(hipStreamSynchronize(s_comp_));
+    return moved;
+  }
+
   u32 restore(py::buffer desc, py::buffer pay, i64 now_ms) {
     py::buffer_info di = desc.request(), pi = pay.request();
     u64 db = (u64)di.size * di.itemsize, pb = (u64)pi.size * pi.itemsize;
@@ -1524,6 +1551,7 @@ class Engine {
   u8* get_out_dev_ = nullptr;
   GetRes* get_res_dev_ = nullptr;
   u64* scan_status_ = nullptr;
+  unsigned long long* spill_moved_ = nullptr;
   u32* scan_ctl_ = nullptr;
   u32 scan_smax_ = 0;
   bool graph_enabled_ = true;
@@ -1641,6 +1669,7 @@ PYBIND11_MODULE(_dataplane, m) {
       .def("set_xfer_parity", &Engine::set_xfer_parity)
       .def("set_import", &Engine::set_import, py::arg("recv"), py::arg("stream") = 0)
       .def("restore", &Engine::restore, py::arg("desc"), py::arg("payload"), py::arg("now_ms"))
+      .def("spill", &Engine::spill, py::arg("lim"), py::arg("hot"), py::call_guard<py::gil_scoped_release>())
       .def("basic_get", &Engine::basic_get, py::arg("q"), py::arg("chslot"), py::arg("noack"), py::arg("now_ms"))
       .def("wait_results", &Engine::wait_results)
       .def("egress_copy", &Engine::egress_copy)
