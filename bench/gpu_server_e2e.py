@@ -53,7 +53,7 @@ def plane_for(spec):
                         deliv_max=1 << 17, msg_max=1 << 21, ucap=8192, deliver_cap=8192,
                         ingress_cap=64 << 20, egress_cap=160 << 20, log_bytes=8 << 30, ring_pool=1 << 25,
                         tb_max=256, default_queue_capacity=1 << 20, persist=int(persist),
-                        persist_max=1 << 16, persist_bytes=512 << 20, carry_cap=1 << 18)
+                        persist_max=1 << 16, persist_bytes=512 << 20, carry_cap=SIZING["carry_cap"])
 
 
 def thread_cpu():
@@ -75,6 +75,10 @@ def thread_cpu():
 
 
 FE_CFG = {}
+# per-connection bytes per step (the front end reads at most this, and at most the room
+# left in the connection's device carry, so two steps in flight need carry >= 2x): the
+# batch a step can take from one producer, so the ceiling of throughput per step period
+SIZING = {"per_conn_read": 128 << 10, "carry_cap": 1 << 18}
 
 
 def run_one(core, name, spec, io, io_threads, seconds, rate=0.0, lg_threads=12, store_dir=None, cons_threads=8):
@@ -88,7 +92,7 @@ def run_one(core, name, spec, io, io_threads, seconds, rate=0.0, lg_threads=12, 
     bkw = dict(spec.get("_broker", {}))
     spec = {k: v for k, v in spec.items() if not k.startswith("_")}
     b = GpuBroker(plane, idle_step_ms=0.5, store=store, io=io, io_threads=io_threads,
-                  per_conn_read=128 << 10, fe_cfg=FE_CFG, **bkw).start()
+                  per_conn_read=SIZING["per_conn_read"], fe_cfg=FE_CFG, **bkw).start()
     t0 = time.time()
     cpu0 = thread_cpu()
     timeline, done = [], [False]
@@ -160,6 +164,7 @@ def run_one(core, name, spec, io, io_threads, seconds, rate=0.0, lg_threads=12, 
         if store is not None:
             store.close()
     lc = getattr(plane, "last_counters", {}) or {}
+    r["engine_host_s"] = {k: round(v, 4) for k, v in plane.eng.host_times(False).items()}
     r["after"] = after
     r["timeline"] = timeline
     r["thread_cpu_s"] = {k: round(cpu1[k] - cpu0.get(k, 0.0), 2) for k in cpu1 if cpu1[k] - cpu0.get(k, 0.0) > 0.05}
@@ -193,7 +198,7 @@ def wal_soak(core, seconds, io_threads=4, lg_threads=12, cons_threads=8, rate=0.
     store.open(d, True)
     plane = plane_for(spec)
     b = GpuBroker(plane, idle_step_ms=0.5, store=store, io="pipeline", io_threads=io_threads,
-                  per_conn_read=128 << 10).start()
+                  per_conn_read=SIZING["per_conn_read"]).start()
     samples, done = [], [False]
     t0 = time.time()
 
@@ -285,6 +290,8 @@ def main():
     ap.add_argument("--loadgen-threads", type=int, default=12)
     ap.add_argument("--consumer-threads", type=int, default=8, help="of the load generator's threads")
     ap.add_argument("--wblock-high", type=int, default=0, help="front end egress back-pressure high watermark (B)")
+    ap.add_argument("--per-conn-read", type=int, default=128 << 10, help="bytes per connection per step")
+    ap.add_argument("--carry-cap", type=int, default=1 << 18, help="device carry per connection (>= 2x per-conn-read)")
     ap.add_argument("--rates", default="", help="comma list of aggregate publish rates (msgs/s) to run paced")
     ap.add_argument("--paced", type=float, default=0.5,
                     help="re-run each spec with producers paced at this fraction of the measured rate (0 = off)")
@@ -295,6 +302,7 @@ def main():
                     help="N > 1: the pipelined sharded server with N ranks on this GPU (producers on rank 1, "
                          "consumers on rank 0 and then on rank 1 through device links)")
     args = ap.parse_args()
+    SIZING.update(per_conn_read=args.per_conn_read, carry_cap=max(args.carry_cap, 2 * args.per_conn_read))
     if args.wblock_high:
         FE_CFG.update(wblock_high=args.wblock_high, wblock_low=args.wblock_high // 4)
     core = load()
@@ -345,7 +353,7 @@ def main():
                                                     "confirmed_per_s", "p50_us", "p99_us", "error", "redelivered",
                                                     "requeued", "flow_off", "flow_off_server", "front_end",
                                                     "store", "thread_cpu_s", "cpu_consumers_s",
-                                                    "cpu_producers_s")}),
+                                                    "cpu_producers_s", "engine_host_s")}),
                       flush=True)
                 for agg in [float(x) for x in args.rates.split(",") if x]:
                     rr = run_one(core, name, spec, io, nt, args.seconds, rate=agg / max(1, spec.get("producers", 1)),

@@ -105,9 +105,16 @@ Frontend::Frontend(const FrontendCfg& cfg, const CmqEngineApi* api) : cfg_(cfg),
     conns_[i]->io = (int)(i % (u32)cfg_.io_threads);
   }
   for (u32 i = cfg_.max_slot; i >= 1; --i) free_.push_back(i);
+  const u64 arena_bytes = ((api_->ingress_cap + 64 + 4095) / 4096) * 4096;
   for (int k = 0; k < 3; ++k) {
-    arena_[k] = (u8*)aligned_alloc(4096, ((api_->ingress_cap + 64 + 4095) / 4096) * 4096);
+    arena_[k] = (u8*)aligned_alloc(4096, arena_bytes);
     if (!arena_[k]) throw std::runtime_error("frontend: arena allocation failed");
+    // page-locked: the step's H2D is a DMA straight from the arena (a pageable source is
+    // staged through a bounce buffer by a CPU copy inside submit: ~80 us of a 1.7 MB step,
+    // measured).  The engine's submit waits for the H2D of the step two back before
+    // reusing its buffers, so by the time an arena is gathered into again (three steps
+    // later) its copy is done
+    if (api_->host_register && api_->host_register(api_->eng, arena_[k], arena_bytes) == 0) arena_pinned_[k] = true;
   }
   lfd_ = ::socket(AF_INET, SOCK_STREAM | SOCK_NONBLOCK | SOCK_CLOEXEC, 0);
   if (lfd_ < 0) throw std::runtime_error("frontend: socket failed");
@@ -176,6 +183,9 @@ void Frontend::stop() {
     if (io->th.joinable()) io->th.join();
   }
   ev_cv_.notify_all();
+  // the engine is alive until the front end is stopped (and no step is in flight now)
+  for (int k = 0; k < 3; ++k)
+    if (arena_pinned_[k]) { api_->host_unregister(api_->eng, arena_[k]); arena_pinned_[k] = false; }
 }
 
 bool Frontend::check(int rc) {
@@ -629,6 +639,8 @@ void Frontend::io_loop(int i) {
       const bool async = ph_async_;
       auto scatter = [&] {
         for (Scatter* sc : scat) {
+          // the step's D2H was issued by the stepper, which did not wait for it (stash_pend)
+          if (sc->wait_slot >= 0) api_->egress_ready(api_->eng, sc->wait_slot);
           const u8* base = sc->own.empty() ? sc->egress : (const u8*)sc->own.data();
           for (u32 id : io.owned) {
             const ConnOut& o = sc->co[id];
@@ -1294,7 +1306,10 @@ void Frontend::stepper_sharded() {
 bool Frontend::stash_pend(bool copy) {
   if (!pend_valid_) return true;
   pend_valid_ = false;
-  if (pend_bytes_) {
+  // the common case (no copy, nothing held): the IO threads wait for the D2H themselves
+  // before writing the slot out, so the stepper goes on to gather and submit meanwhile
+  const bool defer = !copy && !pend_.needs_commit && held_total_ == 0 && api_->egress_ready != nullptr;
+  if (pend_bytes_ && !defer) {
     GpuWait gw(gpu_wait_since_);
     if (!check(api_->egress_wait_slot(api_->eng, pend_slot_))) return false;
   }
@@ -1302,6 +1317,8 @@ bool Frontend::stash_pend(bool copy) {
     if (copy) {   // the slot may be reused before it is written: copy
       pend_.sc.own.assign((const char*)pend_.sc.egress, pend_bytes_);
       pend_.sc.egress = nullptr;
+    } else if (pend_bytes_ && defer) {
+      pend_.sc.wait_slot = pend_slot_;
     }
     out_.push_back(std::move(pend_.sc));
     return true;
@@ -1562,6 +1579,9 @@ EchoEngine::EchoEngine(u32 c_max, u32 seg_max, u64 ingress_cap, u32 carry_cap, u
   api_.launch_b = [](void* e, int p) -> int { ((EchoEngine*)e)->launch_b(p); return 0; };
   api_.links = 0;
   api_.flush_submit = nullptr;
+  api_.host_register = nullptr;
+  api_.host_unregister = nullptr;
+  api_.egress_ready = nullptr;
 }
 
 void EchoEngine::unpause(u32 conn) {

@@ -158,6 +158,7 @@ class Frontend {
     // connection generations when the step was submitted: bytes of a connection that
     // closed since (its slot possibly reused by a new client) are dropped, never written
     std::vector<u32> gen;
+    int wait_slot = -1;      // egress slot whose D2H the writer waits for first (-1: ready)
   };
   // needs_commit: the step's store records must commit before the confirm-gated part of
   // its egress leaves; conf = that step's confirm bytes per connection (empty = all gated)
@@ -199,6 +200,7 @@ class Frontend {
 
   // pinned ingress arenas (3: the H2D of step t is done before step t+3 gathers)
   u8* arena_[3] = {nullptr, nullptr, nullptr};
+  bool arena_pinned_[3] = {false, false, false};
   int arena_i_ = 0;
 
   // IO phase

@@ -1205,6 +1205,15 @@ class Engine {
         return ((Engine*)e)->submit_raw(nullptr, 0, 0, 0, now, (u64)now, worker, false, SF_NODISPATCH);
       });
     };
+    a.host_register = [](void* e, void* ptr, u64 bytes) -> int {
+      return ((Engine*)e)->guard([&] { HIPCHECK(hipHostRegister(ptr, bytes, hipHostRegisterDefault)); return 0; });
+    };
+    a.host_unregister = [](void* e, void* ptr) -> int {
+      return ((Engine*)e)->guard([&] { HIPCHECK(hipHostUnregister(ptr)); return 0; });
+    };
+    a.egress_ready = [](void* e, int slot) -> int {
+      return ((Engine*)e)->guard([&] { ((Engine*)e)->egress_ready(slot); return 0; });
+    };
     for (int p = 0; p < 2; ++p) {
       std::string sfx = std::to_string(p);
       HostIO& h = io_[p];
@@ -1230,6 +1239,17 @@ class Engine {
       err_ = ex.what();
       return -1;
     }
+  }
+
+  // egress_wait_slot without touching engine state (any thread; the slot's D2H was
+  // issued before the caller learnt of the slot)
+  void egress_ready(int e) {
+    if (copy_mode_ == 3) {
+      if (sdma_pending_[e])
+        hsa_signal_wait_scacquire(sdma_sig_[e], HSA_SIGNAL_CONDITION_EQ, 0, UINT64_MAX, HSA_WAIT_STATE_ACTIVE);
+      return;
+    }
+    if (d2h_issued_[e]) HIPCHECK(hipEventSynchronize(ev_d2h_[e]));
   }
 
   void egress_wait_slot(int e) {

@@ -89,7 +89,7 @@ struct ConnOut { u32 off; u32 len; };
 // C entry points of one Engine (engine.hip: Engine::c_api).  All return 0 / a parity on
 // success and -1 on error (message: error()).  Parity p = the double-buffered step IO set
 // of a submitted step; its host-mapped outputs stay valid until the next submit of p.
-#define CMQ_STEP_ABI 3
+#define CMQ_STEP_ABI 4
 struct CmqEngineApi {
   u32 abi;
   u32 c_max, seg_max, carry_cap, persist, persist_max;
@@ -128,5 +128,12 @@ struct CmqEngineApi {
   // no-dispatch steps (their link records and acks travel one exchange later)
   u32 links;
   int (*flush_submit)(void* eng, i64 now_ms, u32 worker);   // an empty no-dispatch step: parity
+  // page-lock a front-end buffer (its ingress arenas: their H2D copy is then an async DMA
+  // instead of a staged CPU copy inside submit); 0 or -1
+  int (*host_register)(void* eng, void* p, u64 bytes);
+  int (*host_unregister)(void* eng, void* p);
+  // thread-safe wait for an egress slot's D2H (IO threads, before writing it out): unlike
+  // egress_wait_slot it changes no engine state
+  int (*egress_ready)(void* eng, int slot);
 };
 #define GROW_MAX 4096   // grow requests reported per step
