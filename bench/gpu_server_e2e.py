@@ -78,7 +78,7 @@ FE_CFG = {}
 # per-connection bytes per step (the front end reads at most this, and at most the room
 # left in the connection's device carry, so two steps in flight need carry >= 2x): the
 # batch a step can take from one producer, so the ceiling of throughput per step period
-SIZING = {"per_conn_read": 128 << 10, "carry_cap": 1 << 18}
+SIZING = {"per_conn_read": 512 << 10, "carry_cap": 1 << 20}
 
 
 def run_one(core, name, spec, io, io_threads, seconds, rate=0.0, lg_threads=12, store_dir=None, cons_threads=8):
@@ -290,8 +290,8 @@ def main():
     ap.add_argument("--loadgen-threads", type=int, default=12)
     ap.add_argument("--consumer-threads", type=int, default=8, help="of the load generator's threads")
     ap.add_argument("--wblock-high", type=int, default=0, help="front end egress back-pressure high watermark (B)")
-    ap.add_argument("--per-conn-read", type=int, default=128 << 10, help="bytes per connection per step")
-    ap.add_argument("--carry-cap", type=int, default=1 << 18, help="device carry per connection (>= 2x per-conn-read)")
+    ap.add_argument("--per-conn-read", type=int, default=512 << 10, help="bytes per connection per step")
+    ap.add_argument("--carry-cap", type=int, default=1 << 20, help="device carry per connection (>= 2x per-conn-read)")
     ap.add_argument("--rates", default="", help="comma list of aggregate publish rates (msgs/s) to run paced")
     ap.add_argument("--paced", type=float, default=0.5,
                     help="re-run each spec with producers paced at this fraction of the measured rate (0 = off)")

@@ -249,7 +249,9 @@ class Config:
             ingress_cap=int(g(k + "ingress-bytes", 64 << 20)), egress_cap=int(g(k + "egress-bytes", 128 << 20)),
             carry_cap=int(g(k + "carry-bytes", 16 << 20)), tb_max=int(g(k + "topic-bindings", 4096)),
             frame_max=int(g("chana.mq.amqp.connection.frame-max")),
-            hash_wildcard=bool(g("chana.mq.routing.topic-hash-wildcard", True)))
+            hash_wildcard=bool(g("chana.mq.routing.topic-hash-wildcard", True)),
+            # cold message bodies spill to this much pinned host memory once the HBM log fills
+            spill_bytes=int(g(k + "spill-bytes", 0)))
         if store_dir:
             plane.update(persist=1, persist_max=int(g(k + "persist-records", 1 << 16)),
                          persist_bytes=int(g(k + "persist-bytes", 256 << 20)))
@@ -260,7 +262,7 @@ class Config:
         if lo < 0:
             lo = hi // 2
         broker = dict(io=str(g(k + "front-end", "pipeline")), io_threads=int(g(k + "io-threads", 4)),
-                      idle_step_ms=float(g(k + "idle-step-ms", 1.0)), per_conn_read=int(g(k + "per-conn-read", 256 << 10)),
+                      idle_step_ms=float(g(k + "idle-step-ms", 1.0)), per_conn_read=int(g(k + "per-conn-read", 512 << 10)),
                       mem_high_watermark=hi, mem_low_watermark=lo)
         return plane, broker
 
