@@ -3372,7 +3372,12 @@ DEV void render_rc(const DS& d, u32 blk) {
 // ============================================================================ post / final
 // (a last-block ticket here to fold k_host_out in costs more than the launch it saves:
 // hundreds of blocks serialise on the ticket word)
-__global__ __launch_bounds__(256) void k_post(DS d) {
+DEV void final_step(const DS& d);
+DEV void host_out_copies(const DS& d, u64 gtid, u64 gsz);
+// fin (no persistence: nothing runs after it): the host-visible copies and, by the last
+// block to finish (ticket), the log tail + counters (fused k_host_out)
+__global__ __launch_bounds__(256) void k_post(DS d, u32 fin) {
+  __shared__ u32 s_last;
   u32 i = blockIdx.x * blockDim.x + threadIdx.x;
   u32 n = d.ctr->n_deliv;
   u32 msg = INVALID, q = 0;
@@ -3398,6 +3403,19 @@ __global__ __launch_bounds__(256) void k_post(DS d) {
     d.conn_dlast[i] = INVALID;
     d.conn_ret_bytes[i] = 0;
     d.conn_ret_min[i] = INVALID;
+  }
+  if (!fin) return;
+  host_out_copies(d, i, (u64)gridDim.x * blockDim.x);
+  // every block's releases are done (their atomics returned) before its ticket
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __syncthreads();
+  if (threadIdx.x == 0) s_last = atomicAdd(&d.tot[TS_POST_TICKET], 1u) == gridDim.x - 1;
+  __syncthreads();
+  if (!s_last) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  if (threadIdx.x == 0) {
+    d.tot[TS_POST_TICKET] = 0;
+    final_step(d);
   }
 }
 

@@ -46,7 +46,8 @@ enum : u32 {
   TS_XSCAN = 32,                        // + 2*r: per-destination record / byte totals
   TS_TTL_BUDGET = 64,                   // durable TTL-skip records reserved this step (k_dequeue)
   TS_NRACK = 65,                        // link acks received this step (k_import_route -> link_ack_one)
-  TS_PK_TICKET = 66                     // k_pack_scan finished-tile ticket (last tile: prefixes)
+  TS_PK_TICKET = 66,                    // k_pack_scan finished-tile ticket (last tile: prefixes)
+  TS_POST_TICKET = 67                   // k_post finished-block ticket (last block: final_step)
 };
 
 // remote-consumer link ack (X3): the connection side consumed message `xid` (owner's

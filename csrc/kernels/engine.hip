@@ -1491,10 +1491,13 @@ class Engine {
     if (!hs_ntiles) hipLaunchKernelGGL(k_qfirst, blocks(d.pair_max, 256), dim3(256), 0, s, d, psrc);
     hipLaunchKernelGGL(k_ring_plan, capped(ceil_div(d.pair_max, 256), 1024), dim3(256), 0, s, d, psrc, hs_ntiles);
     hipLaunchKernelGGL(k_enqueue, capped(ceil_div(d.pair_max, 256), 1024), dim3(256), 0, s, d, psrc, hs_ntiles);
+    // without persistence nothing runs after k_post: it also writes the host-visible
+    // outputs and its last block the counters (fused k_host_out)
+    const u32 fin = d.persist ? 0u : 1u;
     if (!dispatch) {
       const u64 pn = d.deliv_max > d.c_max ? d.deliv_max : d.c_max;
-      hipLaunchKernelGGL(k_post, blocks(pn, 256), dim3(256), 0, s, d);   // n_deliv = 0: frees only
-      hipLaunchKernelGGL(k_host_out, dim3(64), dim3(256), 0, s, d);
+      hipLaunchKernelGGL(k_post, blocks(pn, 256), dim3(256), 0, s, d, fin);   // n_deliv = 0: frees only
+      if (!fin) hipLaunchKernelGGL(k_host_out, dim3(64), dim3(256), 0, s, d);
       return;
     }
     hipLaunchKernelGGL(k_chan_advance, capped(nch, 1024), dim3(256), 0, s, d);
@@ -1517,13 +1520,13 @@ class Engine {
       hipLaunchKernelGGL(k_render, dim3(n_rc + wave_blocks(d.deliv_max).x), dim3(256), 0, s, d, n_rc);
     }
     u64 pn = d.deliv_max > d.c_max ? d.deliv_max : d.c_max;
-    hipLaunchKernelGGL(k_post, blocks(pn, 256), dim3(256), 0, s, d);
+    hipLaunchKernelGGL(k_post, blocks(pn, 256), dim3(256), 0, s, d, fin);
     if (d.persist) {
       hipLaunchKernelGGL(k_persist_size, blocks(d.persist_max, 256), dim3(256), 0, s, d);
       launch_scan(s, {{d.ps_size, d.ps_off}}, &d.ctr->n_persist, d.persist_max, TS_PERSIST);
       hipLaunchKernelGGL(k_persist_pack, wave_blocks(d.persist_max), dim3(256), 0, s, d);
+      hipLaunchKernelGGL(k_host_out, dim3(64), dim3(256), 0, s, d);
     }
-    hipLaunchKernelGGL(k_host_out, dim3(64), dim3(256), 0, s, d);
   }
 
   // world == 1: the whole step; world > 1: phase A (ingest, local route, pack)

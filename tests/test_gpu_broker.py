@@ -564,3 +564,48 @@ def test_cold_bodies_spill_to_host_memory_and_come_back(gpu, io):
         c.close()
     finally:
         b.stop()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("io", ["native", "pipeline"])
+def test_purge_of_more_durable_messages_than_persist_records_per_step(gpu, io, tmp_path):
+    """A purge of a durable queue holding 3x persist_max persistent messages: the device's
+    TTL skip takes at most a quarter of a step's store-record buffer and continues in the
+    following steps, so every deletion reaches the store (no record buffer overflow, no
+    rows left behind) and a restart recovers nothing (consumed > persist_max)."""
+    import time
+    from chanamq_amd.broker import load
+    from chanamq_amd.server.gpu_broker import GpuBroker
+    core = load()
+    st = core.Store()
+    st.open(str(tmp_path / "store"), True)
+    b = GpuBroker(make_persist_plane("gpu"), idle_step_ms=1.0, ingress_bytes=8 << 20, store=st, io=io).start()
+    try:
+        p = conn(b)
+        ch = p.channel()
+        ch.queue_declare("deep.dur", durable=True)
+        ch.confirm_select()
+        n = 3 * 4096
+        for i in range(n):
+            ch.basic_publish("", "deep.dur", b"m%d" % i, {"delivery_mode": 2})
+            if i % 1024 == 1023:
+                assert ch.wait_for_confirms(timeout=60)
+        assert ch.wait_for_confirms(timeout=60)
+        assert st.row_count("msgs") == n
+        assert ch.queue_purge("deep.dur") == n
+        deadline = time.time() + 30
+        while st.row_count("msgs") and time.time() < deadline:
+            p.process(0.1)
+        assert st.row_count("msgs") == 0
+        p.close()
+    finally:
+        b.stop()
+        st.close()
+    st2 = core.Store()
+    st2.open(str(tmp_path / "store"), True)
+    b2 = GpuBroker(make_persist_plane("gpu"), idle_step_ms=1.0, ingress_bytes=8 << 20, store=st2, io=io).start()
+    try:
+        assert b2.recovered == 0
+    finally:
+        b2.stop()
+        st2.close()
