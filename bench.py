@@ -129,6 +129,9 @@ def main():
     ap.add_argument("--body", type=int, default=1024)
     ap.add_argument("--chunk", type=int, default=65536, help="bytes per producer per step (TCP read)")
     ap.add_argument("--blocks", type=int, default=8)
+    ap.add_argument("--soak-s", type=float, default=2.0,
+                    help="after the timed steps (and the result line), keep stepping untimed for this long so "
+                         "an external GPU-utilisation sampler sees the workload (0 = off)")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--copy-engine", choices=["kernel", "nocu", "blit", "sdma"], default="sdma",
                     help="egress D2H: an SDMA engine other than the ingress H2D's (default: H2D and D2H "
@@ -362,8 +365,15 @@ def main():
             "storm": ({"requeued_msgs": flow["requeued"], "flow_paused_steps": flow["paused_steps"]}
                       if storm else None),
             "cross_gpu_bytes_per_s": (dp.exchanger.bytes_sent * world / t) if shards > 1 else 0.0,
+            "post_soak_s": args.soak_s,
         }
-        print(json.dumps(out))
+        print(json.dumps(out), flush=True)
+    if args.soak_s > 0:
+        # untimed: the same step count on every rank (ms_step is the max over ranks), so the
+        # lockstep exchange stays matched
+        run(max(1, min(20000, int(args.soak_s * 1000.0 / max(ms_step, 1e-3)))))
+        dp.eng.sync()
+        torch.cuda.synchronize()
     if dist:
         dist.destroy_process_group()
 
