@@ -425,7 +425,9 @@ class Engine {
     get_cap_ = (u64)d_.carry_cap + d_.carry_cap / 64 + 4096;
     get_out_dev_ = (u8*)hst("get_out", get_cap_);
     get_res_dev_ = (GetRes*)hst("get_res", sizeof(GetRes));
-    d_.dbg = (u64*)dev("dbg", 8ull * 16 * d_.seg_max);
+    // k_frame_scan phase timestamps (scripts/frame_scan_phases.py): off unless asked for --
+    // each mark is a clock read plus a store on the block's critical path
+    d_.dbg = get("fs_marks", 0) ? (u64*)dev("dbg", 8ull * 16 * d_.seg_max) : nullptr;
 
     for (int p = 0; p < 2; ++p) {
       DS io = d_;

@@ -6,7 +6,7 @@ from chanamq_amd.engine.dataplane import GpuDataPlane
 P, Q = 256, 16
 cfg = dict(c_max=1024, chpc=4, q_max=64, cons_max=1024, seg_max=1024, cmd_max=1 << 17, deliv_max=1 << 16,
            msg_max=1 << 22, ucap=4096, deliver_cap=8192, ingress_cap=64 << 20, egress_cap=128 << 20,
-           log_bytes=16 << 30, ring_pool=Q * 2 * (1 << 20), tb_max=64, carry_cap=256 << 10)
+           log_bytes=16 << 30, ring_pool=Q * 2 * (1 << 20), tb_max=64, carry_cap=256 << 10, fs_marks=1)
 dp = GpuDataPlane(**cfg)
 pool, segs, offs, blens, mps, mb, _ = bench.build_workload(dp, 0, P, Q, 1024, 65536, 8, cons_base=P)
 for s in range(6):
