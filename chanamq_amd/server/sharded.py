@@ -23,6 +23,7 @@ import os
 import signal
 import sys
 import threading
+import uuid
 
 
 def main(argv=None):
@@ -90,7 +91,13 @@ def main(argv=None):
                 uid = store.get(key)
                 plane.xchg_setup("rccl", uid, live, args.xchg_timeout_ms, failover=True)
             else:
-                plane.xchg_setup("shm", f"{shm_base}-e{epoch}", live, args.xchg_timeout_ms, failover=True)
+                # a fresh segment name per launch and epoch, chosen by the lowest live rank: a
+                # segment left by a killed earlier run (same store address) is never reused
+                key = f"xchg/{epoch}/shm"
+                if rank == min(live):
+                    store.set(key, f"{shm_base}-{os.getpid()}-{uuid.uuid4().hex[:12]}-e{epoch}")
+                name = store.get(key).decode()
+                plane.xchg_setup("shm", name, live, args.xchg_timeout_ms, failover=True)
         rebuild_xchg(list(range(world)), 0)
         node.rebuild_xchg = rebuild_xchg
     st = None

@@ -70,9 +70,9 @@ class ShmXchg {
   ~ShmXchg() {
     if (base_ && base_ != MAP_FAILED) ::munmap(base_, total_);
     if (fd_ >= 0) ::close(fd_);
-    // the last rank out removes the name; a survivor group uses a new name anyway
+    // (normally unlinked after the first exchange; a group that never exchanged)
     std::string nm = "/" + name_;
-    if (idx_ == 0) ::shm_unlink(nm.c_str());
+    if (idx_ == 0 && !unlinked_) ::shm_unlink(nm.c_str());
   }
   ShmXchg(const ShmXchg&) = delete;
   ShmXchg& operator=(const ShmXchg&) = delete;
@@ -123,6 +123,10 @@ class ShmXchg {
     std::atomic_thread_fence(std::memory_order_release);
     int rc = barrier();
     if (rc) return rc;
+    if (!unlinked_) {   // every member has it mapped now: drop the name (nothing left in
+      unlinked_ = true; // /dev/shm if a process is killed later)
+      if (idx_ == 0) ::shm_unlink(("/" + name_).c_str());
+    }
     for (int s = 0; s < n; ++s) memcpy(recv + (size_t)s * XH_WORDS, hdr(s, k) + (size_t)idx_ * XH_WORDS, XH_WORDS * 4);
     return 0;
   }
@@ -137,6 +141,7 @@ class ShmXchg {
   ShmCtl* ctl_ = nullptr;
   uint32_t gen_seen_ = 0;
   uint64_t seq_ = 0;
+  bool unlinked_ = false;
 };
 
 }  // namespace cmqx
