@@ -448,6 +448,20 @@ DEV u32 cand_word(const u8* w16, u32 fm) {
 #define FS_MARK(k) \
   do { if (tid == 0 && d.dbg) d.dbg[(u64)s * 16 + (k)] = __builtin_amdgcn_s_memrealtime(); } while (0)
 constexpr u32 FS_AM_MAX = 8192;  // 128 KB segment; 16 KB of LDS
+// Segments up to FS_STAGE bytes (the screen's 32-byte read-ahead included) are copied
+// into LDS by the screen pass itself, and every later phase reads the segment's bytes
+// from LDS instead of HBM (frame headers, method ids, body sizes, control bytes: ~15
+// dependent global round trips per segment before).  The block's LDS is one pool carved
+// per segment: staged segments hold up to FS_CAND_STAGED candidates next to the 72 KB
+// stage, other segments CAND_MAX candidates (a 128 KB segment of 1-byte messages)
+constexpr u32 FS_STAGE = 72u << 10;
+constexpr u32 FS_CAND_STAGED = 6144;
+// candidate arrays: wend + cpos (u32), chain / screen mask (u16), csucc (i16), claim (u8)
+constexpr u32 fs_cand_bytes(u32 cmax, u32 amw) { return cmax * 4 * 2 + (cmax > amw ? cmax : amw) * 2 + cmax * 2 + cmax; }
+constexpr u32 FS_POOL_STAGED = FS_STAGE + fs_cand_bytes(FS_CAND_STAGED, FS_STAGE / 16);
+constexpr u32 FS_POOL_FULL = fs_cand_bytes(CAND_MAX, FS_AM_MAX);
+constexpr u32 FS_POOL = ((FS_POOL_STAGED > FS_POOL_FULL ? FS_POOL_STAGED : FS_POOL_FULL) + 15) & ~15u;
+static_assert(FS_POOL <= 156u << 10, "k_frame_scan LDS pool");
 // one block of FS_NT threads per segment: 16 waves (4 per SIMD) hide the screen's
 // dependent integer chains, which one wave per SIMD could not
 #define FS_NT 1024
@@ -461,17 +475,7 @@ DEV bool big_publish(const DS& d, u32 msize, u32 hsize, u64 bsz, u32 fmax) {
 }
 
 DEV void frame_scan_seg(const DS& d, const u32 s) {
-  __shared__ u32 cpos[CAND_MAX];
-  __shared__ int16_t csucc[CAND_MAX];
-  // chain (first written in phase c) aliases amask (used only in phase a, which ends on
-  // a __syncthreads): 16 KB less LDS per block, two blocks fit on a CU
-  __shared__ u16 chain_am[CAND_MAX > FS_AM_MAX ? CAND_MAX : FS_AM_MAX];
-  u16* const chain = chain_am;
-  u16* const amask = chain_am;
-  __shared__ u8 claim[CAND_MAX];
-  // per accepted candidate: its frame end | complete << 31 (phase b reuses it instead of
-  // re-reading the header from memory); ~0u = recompute
-  __shared__ u32 wend[CAND_MAX];
+  __shared__ uint4 fs_pool[FS_POOL / 16];
   __shared__ u32 sc[FS_NT / 64 + 1];
   __shared__ u32 sh_m, sh_over, sh_ok, sh_nf, sh_stop, sh_brk;
   __shared__ u32 sh_cmd_base, sh_frag_base, sh_ncmd;
@@ -479,7 +483,25 @@ DEV void frame_scan_seg(const DS& d, const u32 s) {
   const u32 tid = threadIdx.x;
   const u32 conn = d.segs[s].conn;
   const u32 L = d.seg_total[s];
-  const u8* b = d.work + d.seg_start[s];
+  const u8* const bg = d.work + d.seg_start[s];   // the segment in the work buffer (HBM)
+  const u8* b = bg;                              // switched to the LDS stage after the screen
+  // the pool for this segment: [stage] wend cpos chain/amask csucc claim
+  const u32 nm16 = (L + 15) >> 4;
+  const bool staged = nm16 * 16 + 32 <= FS_STAGE;
+  const u32 cmax = staged ? FS_CAND_STAGED : CAND_MAX;
+  u8* const pool = (u8*)fs_pool;
+  uint4* const fs_stage = fs_pool;
+  // per accepted candidate: its frame end | complete << 31 (phase b reuses it instead of
+  // re-reading the header); ~0u = recompute
+  u32* const wend = (u32*)(pool + (staged ? FS_STAGE : 0u));
+  u32* const cpos = wend + cmax;
+  // chain (first written in phase c) aliases amask (used only in phase a, which ends on a
+  // __syncthreads)
+  u16* const chain_am = (u16*)(cpos + cmax);
+  u16* const chain = chain_am;
+  u16* const amask = chain_am;
+  int16_t* const csucc = (int16_t*)(chain_am + (staged ? FS_CAND_STAGED : (CAND_MAX > FS_AM_MAX ? CAND_MAX : FS_AM_MAX)));
+  u8* const claim = (u8*)(csucc + cmax);
   const u32 fmax = d.conn_frame_max[conn];
   const u32 wbase = d.seg_start[s];
   SegOut so;
@@ -520,7 +542,7 @@ DEV void frame_scan_seg(const DS& d, const u32 s) {
     const bool use_am = nm <= FS_AM_MAX;
     const u32 fmg = d.frame_max_global;
     if (use_am) {   // candidate screen of the segment into LDS (fused k_cand), coalesced reads
-      const uint4* W = (const uint4*)b;   // 16-aligned; >= 32 bytes of padding after the segment
+      const uint4* W = (const uint4*)bg;   // 16-aligned; >= 32 bytes of padding after the segment
       for (u32 cc = tid; cc < nm; cc += FS_NT * 4) {
         uint4 x[4], y[4];
 #pragma unroll
@@ -531,10 +553,15 @@ DEV void frame_scan_seg(const DS& d, const u32 s) {
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
           const u32 c = cc + k * FS_NT;
-          if (c < nm) amask[c] = (u16)cand_bits(x[k], y[k], fmg);
+          if (c < nm) {
+            amask[c] = (u16)cand_bits(x[k], y[k], fmg);
+            if (staged) fs_stage[c] = x[k];
+          }
         }
       }
+      if (staged && tid < 2) fs_stage[nm + tid] = make_uint4(0, 0, 0, 0);   // the screen's read-ahead
       __syncthreads();
+      if (staged) b = (const u8*)fs_stage;
     }
     // raw candidates per thread (its words are contiguous: the scan keeps position order)
     u32 rc = 0;
@@ -547,7 +574,7 @@ DEV void frame_scan_seg(const DS& d, const u32 s) {
     u32 rtot;
     u32 roff = block_scan<FS_NT>(rc, sc, rtot);
     u32 tot = 0;
-    if (use_am && rtot <= CAND_MAX) {
+    if (use_am && rtot <= cmax) {
       // every raw candidate validated in parallel (one thread each), then compacted in
       // place chunk by chunk: accepted entries only move left, after the chunk was read
       for (u32 c = c0; c < c1; ++c) {
@@ -578,7 +605,7 @@ DEV void frame_scan_seg(const DS& d, const u32 s) {
         tot += all;
       }
     } else {
-      // very long segment (no LDS mask) or more raw candidates than CAND_MAX: each
+      // very long segment (no LDS mask) or more raw candidates than cmax: each
       // thread validates its own words, twice (count, then emit)
       u32 cnt = 0;
       for (u32 c = c0; c < c1; ++c) {
@@ -608,7 +635,7 @@ DEV void frame_scan_seg(const DS& d, const u32 s) {
             acc = f.valid_hdr && (f.complete || (u64)p + 8 + f.size > L);
           }
           if (acc) {
-            if (off < CAND_MAX) { cpos[off] = p; wend[off] = ~0u; }
+            if (off < cmax) { cpos[off] = p; wend[off] = ~0u; }
             ++off;
           }
         }
@@ -618,10 +645,10 @@ DEV void frame_scan_seg(const DS& d, const u32 s) {
     if (tid == 0) {
       u32 nmc = tot;
       for (u32 p = lim; p < L; ++p) {
-        if (nmc < CAND_MAX) { cpos[nmc] = p; wend[nmc] = ~0u; }
+        if (nmc < cmax) { cpos[nmc] = p; wend[nmc] = ~0u; }
         ++nmc;
       }
-      if (nmc > CAND_MAX) { sh_over = 1; nmc = CAND_MAX; }
+      if (nmc > cmax) { sh_over = 1; nmc = cmax; }
       sh_m = nmc;
     }
     __syncthreads();
@@ -666,7 +693,7 @@ DEV void frame_scan_seg(const DS& d, const u32 s) {
   // recording runs, which all threads expand into chain[].  A single run starting at 0
   // is the implicit chain (frame f = candidate f)
   constexpr u32 FS_RUNS = 1024;            // run records at the top of wend
-  constexpr u32 FS_FAIL_MAX = CAND_MAX - 2 * FS_RUNS;
+  const u32 FS_FAIL_MAX = cmax - 2 * FS_RUNS;
   __syncthreads();   // csucc / wend of (b) complete
   FS_MARK(9);
   {
@@ -980,7 +1007,7 @@ DEV void frame_scan_seg(const DS& d, const u32 s) {
   // ---- (f) carry out: bytes [consumed, L)
   u32 rest = L - consumed;
   if (rest > d.carry_cap) { so.status |= SS_TOO_LARGE; rest = 0; }
-  else block_copy(d.carry + (u64)conn * d.carry_cap, b + consumed, rest, tid, FS_NT);
+  else block_copy(d.carry + (u64)conn * d.carry_cap, bg + consumed, rest, tid, FS_NT);   // 16-B moves from HBM
   FS_MARK(8);
   if (tid == 0) {
     so.consumed = consumed;
@@ -1056,6 +1083,102 @@ DEV u32 build_keyvec(const DS& d, const u8* key, u32 len, u32 pi) {
     }
   }
   return kw.count;
+}
+
+// ---- 32-byte register windows of a publish's method arguments and routing key.  The
+// byte loops above cost one memory round trip per byte wherever a loop's exit depends on
+// the byte (word_len, the trailing-'.' strip), ~20 dependent trips per publish at one
+// thread per command; here two 16-byte loads bring the bytes in and every loop below is
+// unrolled over compile-time positions (register selects, no scratch).  Callers guarantee
+// 32 readable bytes at the window start (the work buffer has 4 KB of slack past work_cap).
+// named words, not an array: no dynamic index can pin the window to scratch memory
+struct Win32 { u32 w0, w1, w2, w3, w4, w5, w6, w7; };
+DEV Win32 load_win(const u8* p) {
+  const U4 a = *(const U4*)p, b = *(const U4*)(p + 16);
+  return Win32{a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+}
+// word k < 8: folds to one register for a compile-time k, a select chain otherwise
+DEV u32 win_word(const Win32& s, u32 k) {
+  // selects over values (a ?: over the members themselves selects their addresses)
+  const u32 a0 = s.w0, a1 = s.w1, a2 = s.w2, a3 = s.w3, a4 = s.w4, a5 = s.w5, a6 = s.w6, a7 = s.w7;
+  const u32 lo = k < 2 ? (k == 0 ? a0 : a1) : (k == 2 ? a2 : a3);
+  const u32 hi = k < 6 ? (k == 4 ? a4 : a5) : (k == 6 ? a6 : a7);
+  return k < 4 ? lo : hi;
+}
+// byte i < 32 of the window
+DEV u32 win_byte(const Win32& s, u32 i) { return (win_word(s, i >> 2) >> (8 * (i & 3))) & 255u; }
+DEV u32 win_get(const Win32& s, u32 i) { return win_byte(s, i); }
+// FNV-1a 64 of bytes [S, S + n) of the window (S + n <= 32)
+template <u32 S>
+DEV u64 win_fnv64(const Win32& s, u32 n, u64 h) {
+#pragma unroll
+  for (u32 i = 0; i + S < 32; ++i) {
+    if (i < n) {   // predicated, not a break: the loop stays fully unrolled (constant indices)
+      h ^= win_byte(s, i + S);
+      h *= FNV64_PRIME;
+    }
+  }
+  return h;
+}
+
+// build_keyvec for a routing key of n <= 32 bytes held in a window: same rows, same count
+DEV u32 build_keyvec_win(const DS& d, const Win32& s, u32 n, u32 pi) {
+  const u32 lenmask = n >= 32 ? ~0u : ((1u << n) - 1u);
+  u32 dots = 0;
+#pragma unroll
+  for (u32 i = 0; i < 32; ++i) dots |= (win_byte(s, i) == '.' ? 1u : 0u) << i;
+  dots &= lenmask;
+  const u32 nd = ~dots & lenmask;                 // trailing '.' stripped (words_of)
+  const u32 eff = nd ? 32u - __clz(nd) : 0u;
+  const u32 effmask = eff >= 32 ? ~0u : ((1u << eff) - 1u);
+  const u32 de = dots & effmask;
+  const u32 count = n == 0 ? 1u : (eff == 0 ? 0u : 1u + __popc(de));
+  if (!d.tb_max) return count;
+  // per-word FNV-1a 32 in one pass: a '.' commits the running hash to its word slot
+  u32 hw[TOPIC_WORDS];
+#pragma unroll
+  for (u32 k = 0; k < TOPIC_WORDS; ++k) hw[k] = 0x811c9dc5u;
+  u32 h = 0x811c9dc5u, wi = 0;
+#pragma unroll
+  for (u32 i = 0; i < 32; ++i) {
+    const u32 c = win_byte(s, i);
+    const bool in = i < eff, dot = in && c == '.';
+#pragma unroll
+    for (u32 k = 0; k < TOPIC_WORDS; ++k) hw[k] = (dot && wi == k) ? h : hw[k];
+    wi += dot ? 1u : 0u;
+    h = dot ? 0x811c9dc5u : (in ? (h ^ c) * 0x01000193u : h);
+  }
+#pragma unroll
+  for (u32 k = 0; k < TOPIC_WORDS; ++k) hw[k] = wi == k ? h : hw[k];
+  const u32 nw = count < TOPIC_WORDS ? count : TOPIC_WORDS;
+  uint4* kv = (uint4*)(d.pub_keyvec + (u64)pi * TOPIC_K);
+  u16* kwo = d.pub_kwoff + (u64)pi * TOPIC_WORDS;
+  u32 off = 0;
+#pragma unroll
+  for (u32 k = 0; k < TOPIC_WORDS; ++k) {
+    if (k < nw) {
+      const u32 rest = off >= 32 ? 0u : (de & ~((1u << off) - 1u));   // separators at or after off
+      u32 e = rest ? (u32)(__ffs(rest) - 1) : eff;
+      if (e > eff) e = eff;
+      const u32 wl = e - off;
+      kwo[k] = (u16)((off << 8) | (wl & 255));
+      u32 pk[8];
+#pragma unroll
+      for (int g = 0; g < 8; ++g) {
+        u32 v = 0;
+#pragma unroll
+        for (int bb = 0; bb < 4; ++bb) v |= (((hw[k] >> (g * 4 + bb)) & 1) ? 0x01u : 0xffu) << (8 * bb);
+        pk[g] = v;
+      }
+      kv[k * 2] = make_uint4(pk[0], pk[1], pk[2], pk[3]);
+      kv[k * 2 + 1] = make_uint4(pk[4], pk[5], pk[6], pk[7]);
+      off = e + 1;
+    } else {
+      kv[k * 2] = make_uint4(0, 0, 0, 0);
+      kv[k * 2 + 1] = make_uint4(0, 0, 0, 0);
+    }
+  }
+  return count;
 }
 
 // K9 ack mark (AMQChannel.scala:128-174): single tag -> its window slot; multiple -> the
@@ -1134,21 +1257,30 @@ __global__ __launch_bounds__(256) void k_decode(DS d) {
     pb.ts_ms = 0;
     pb.nq = 0; pb.slot_bytes = 0; pb.msg = INVALID; pb.pad = 0; pb.xid = 0;
     // method args: class u16, method u16, ticket u16, exchange ss, rk ss, bits
+    // (skip_shortstr inlined over register windows: [ex_len][exchange][rk_len] in one,
+    // exchange names up to 30 bytes; the routing key and the bits octet in a second)
     u32 o = c.m_off + 6, end = c.m_off + c.m_len;
+    const u32 o0 = o;
+    const Win32 ma = load_win(w + o0);
     bool ok = o <= end;
     pb.ex_off = o + 1;
-    pb.ex_len = ok && o < end ? w[o] : 0;
-    ok = ok && skip_shortstr(w, o, end);
+    const u32 b0 = ok && o < end ? win_byte(ma, 0) : 0u;
+    pb.ex_len = b0;
+    if (ok) { if (o + 1 > end) ok = false; else { o += 1 + b0; ok = o <= end; } }
     pb.rk_off = o + 1;
-    pb.rk_len = ok && o < end ? w[o] : 0;
-    ok = ok && skip_shortstr(w, o, end);
-    u32 bits = (ok && o < end) ? w[o] : 0;
+    const u32 b1 = ok && o < end ? (o - o0 < 32 ? win_get(ma, o - o0) : (u32)w[o]) : 0u;
+    pb.rk_len = b1;
+    if (ok) { if (o + 1 > end) ok = false; else { o += 1 + b1; ok = o <= end; } }
+    const Win32 rkw = load_win(w + pb.rk_off);
+    u32 bits = (ok && o < end) ? (o - pb.rk_off < 32 ? win_get(rkw, o - pb.rk_off) : (u32)w[o]) : 0u;
     if (bits & 1) pb.flags |= MF_MANDATORY;
     if (bits & 2) pb.flags |= MF_IMMEDIATE;
     // exchange
     i32 xs = -1;
     if (ok) {
-      u64 hk = exch_hash(d.conn_vhost[c.conn], w + pb.ex_off, pb.ex_len);
+      const u32 vh = d.conn_vhost[c.conn];
+      u64 hk = pb.ex_len <= 31 ? win_fnv64<1>(ma, pb.ex_len, FNV64_BASIS ^ (u64(vh) * 0x9E3779B97F4A7C15ULL))
+                               : exch_hash(vh, w + pb.ex_off, pb.ex_len);
       u32 mask = d.xhash_mask;
       for (u32 j = 0; j <= mask; ++j) {
         u32 slot = (u32)(hk + j) & mask;
@@ -1158,22 +1290,21 @@ __global__ __launch_bounds__(256) void k_decode(DS d) {
       }
     }
     pb.exch = ok ? xs : -2;
-    pb.keyhash = fnv1a64_dev(w + pb.rk_off, pb.rk_len);
+    pb.keyhash = pb.rk_len <= 32 ? win_fnv64<0>(rkw, pb.rk_len, FNV64_BASIS) : fnv1a64_dev(w + pb.rk_off, pb.rk_len);
     // properties (flags chain then values)
     u32 ho = c.h_off + 12, hend = c.h_off + c.h_len;
     pb.props_off = ho;
     pb.props_len = hend > ho ? hend - ho : 0;
-    u32 flagw[2] = {0, 0};
+    u32 fl = 0;   // the first property-flags word (continuation words are skipped)
     u32 nfl = 0;
     u32 q = ho;
     while (q + 2 <= hend) {
       u32 fw = be16(w + q);
       q += 2;
-      if (nfl < 2) flagw[nfl] = fw;
+      if (nfl == 0) fl = fw;
       ++nfl;
       if (!(fw & 1)) break;
     }
-    u32 fl = flagw[0];
     bool pok = true;
     // field order: 15 ctype ss, 14 cenc ss, 13 headers tbl, 12 dmode oct, 11 prio oct,
     // 10 corr ss, 9 replyto ss, 8 expiration ss, 7 msgid ss, 6 timestamp u64, 5 type,
@@ -1219,7 +1350,7 @@ __global__ __launch_bounds__(256) void k_decode(DS d) {
           pok = skip_shortstr(w, q, hend);
       }
     }
-    pb.nwords = build_keyvec(d, w + pb.rk_off, pb.rk_len, pi);
+    pb.nwords = pb.rk_len <= 32 ? build_keyvec_win(d, rkw, pb.rk_len, pi) : build_keyvec(d, w + pb.rk_off, pb.rk_len, pi);
     d.pubs[pi] = pb;
     if (pb.chslot != INVALID && d.ch_confirm[pb.chslot]) atomicAdd(&d.ch_pub_cnt[pb.chslot], 1u);
   } else if (c.kind == CK_ACK || c.kind == CK_NACK || c.kind == CK_REJECT) {
@@ -1642,19 +1773,45 @@ DEV void topic_group(const DS& d, u32 g0, u32 n, u32 w, u32 lane) {
 // rank the all-to-all receive buffer itself (k_import_route copies nothing)
 DEV const u8* pub_src(const DS& d, const Pub& pb) { return (pb.flags & MF_IMPORTED) ? d.recv_pay : d.work; }
 
-DEV bool topic_verify_words(const DS& d, const Pub& pb, u32 pidx, u32 t, u32 fl) {
+// word i (offset << 8 | length) of a row of TOPIC_WORDS u16 held in one 16-byte load
+DEV u32 woff_at(const uint4& v, u32 i) {
+  const u32 w = i < 2 ? v.x : i < 4 ? v.y : i < 6 ? v.z : v.w;
+  return (w >> (16 * (i & 1))) & 0xffffu;
+}
+
+// a binding is a candidate for a publish when its pattern needs the full matcher (flags
+// bit 0: '#', long keys) or the word counts agree and the MFMA prefilter bit is set: two
+// small loads per binding lane (flags, prefilter row), nothing else for the non-candidates
+DEV bool topic_cand(const DS& d, const Pub& pb, u32 pidx, u32 t, u32& fl) {
+  fl = d.t_flags[t];
+  const u16 mw = d.pub_match[(u64)pidx * (d.tb_pad >> 4) + (t >> 4)];
+  return (fl & 1) || ((((fl >> 8) & 0xffu) == pb.nwords) && ((mw >> (t & 15)) & 1));
+}
+
+// exact check of a candidate: both word-offset rows (one 16-byte load each) and the
+// pattern offset in one round, the word lengths checked without memory, then every byte
+// compare issued together (was: word offsets one by one, each a round trip)
+DEV bool topic_verify(const DS& d, const Pub& pb, u32 pidx, u32 t, u32 fl) {
+  const uint4 pw = *(const uint4*)(d.t_woff + (u64)t * TOPIC_WORDS);
+  const uint4 kw = *(const uint4*)(d.pub_kwoff + (u64)pidx * TOPIC_WORDS);
+  const u32 kb = d.t_kb_off[t];
+  if (fl & 1)   // pattern the prefilter cannot express: full matcher
+    return topic_match(d.kpool + kb, d.t_kb_len[t], pub_src(d, pb) + pb.rk_off, pb.rk_len, d.hash_wildcard != 0);
   const u32 nw = pb.nwords < TOPIC_WORDS ? pb.nwords : TOPIC_WORDS;
   const u32 star = (fl >> 16) & 0xffu;
-  const u16* pw = d.t_woff + (u64)t * TOPIC_WORDS;
-  const u16* kw = d.pub_kwoff + (u64)pidx * TOPIC_WORDS;
-  const u8* pat = d.kpool + d.t_kb_off[t];
+  bool lens_ok = true;
+#pragma unroll
+  for (u32 i = 0; i < TOPIC_WORDS; ++i)
+    if (i < nw && !((star >> i) & 1)) lens_ok &= (woff_at(pw, i) & 255) == (woff_at(kw, i) & 255);
+  if (!lens_ok) return false;
+  const u8* pat = d.kpool + kb;
   const u8* key = pub_src(d, pb) + pb.rk_off;
   u32 diff = 0;
-  for (u32 i = 0; i < nw; ++i) {
-    if ((star >> i) & 1) continue;
-    const u32 pe = pw[i], ke = kw[i];
+#pragma unroll
+  for (u32 i = 0; i < TOPIC_WORDS; ++i) {
+    if (i >= nw || ((star >> i) & 1)) continue;
+    const u32 pe = woff_at(pw, i), ke = woff_at(kw, i);
     const u32 len = pe & 255;
-    if (len != (ke & 255)) return false;
     const u8* a = pat + (pe >> 8);
     const u8* b = key + (ke >> 8);
     for (u32 k0 = 0; k0 < len; k0 += 8) {
@@ -1664,19 +1821,6 @@ DEV bool topic_verify_words(const DS& d, const Pub& pb, u32 pidx, u32 t, u32 fl)
     }
   }
   return diff == 0;
-}
-
-DEV bool topic_bind_hit(const DS& d, const Pub& pb, u32 pidx, u32 t) {
-  u32 fl = d.t_flags[t];
-  bool dp_only = fl & 1;
-  if (!dp_only) {
-    if (((fl >> 8) & 0xffu) != pb.nwords) return false;
-    u16 mw = d.pub_match[(u64)pidx * (d.tb_pad >> 4) + (t >> 4)];
-    if (!((mw >> (t & 15)) & 1)) return false;
-    return topic_verify_words(d, pb, pidx, t, fl);
-  }
-  return topic_match(d.kpool + d.t_kb_off[t], d.t_kb_len[t], pub_src(d, pb) + pb.rk_off, pb.rk_len,
-                     d.hash_wildcard != 0);
 }
 
 DEV i32 direct_find(const DS& d, const Pub& pb) {
@@ -1712,11 +1856,13 @@ struct RouteAcc {
   bool has_cons = false;
 };
 
-// emit one candidate queue per lane (valid lanes), preserving lane order
+// emit one candidate queue per lane (valid lanes), preserving lane order.  qo / qc: the
+// queue's owner and consumer count when the caller loaded them already (INVALID: load)
 template <int PASS>
-DEV void route_emit(const DS& d, RouteAcc<PASS>& a, u32 p, u32 wbase, u32 srank, u32 q, bool valid, u32 lane) {
+DEV void route_emit(const DS& d, RouteAcc<PASS>& a, u32 p, u32 wbase, u32 srank, u32 q, bool valid, u32 lane,
+                    u32 qo = INVALID, u32 qc = INVALID) {
   const u32 me = d.my_rank;
-  u32 owner = (valid && d.world > 1) ? d.q_owner[q] : me;
+  u32 owner = (valid && d.world > 1) ? (qo != INVALID ? qo : d.q_owner[q]) : me;
   bool remote = valid && owner != me;
   bool local = valid && !remote;
   a.rmask |= wave_or(remote ? (1u << owner) : 0u);
@@ -1726,7 +1872,7 @@ DEV void route_emit(const DS& d, RouteAcc<PASS>& a, u32 p, u32 wbase, u32 srank,
     a.nrem += (u32)__popcll(rm);
   }
   u64 lm = __ballot(local);
-  bool cons = local && d.q_cons_n[q] != 0;
+  bool cons = local && (qc != INVALID ? qc : d.q_cons_n[q]) != 0;
   if (__ballot(cons || remote)) a.has_cons = true;
   u32 pos = a.nq + (u32)__popcll(lm & lanemask_lt());
   if (local) {
@@ -1794,17 +1940,26 @@ DEV void route_one(const DS& d, u32 p, u32 lane) {
       u32 o = d.x_t_off[ex], c = d.x_t_n[ex];
       u32 lastq = INVALID;
       for (u32 k0 = 0; k0 < c; k0 += 64) {
-        u32 t = o + k0 + lane;
         bool v = k0 + lane < c;
-        u32 q = v ? d.t_queue[t] : INVALID;
-        bool hit = v && topic_bind_hit(d, pb, p, t);
+        u32 t = o + k0 + lane;
+        u32 q = INVALID, fl = 0, qo = INVALID, qc = INVALID;
+        bool hit = false;
+        if (v) {
+          q = d.t_queue[t];
+          if (topic_cand(d, pb, p, t, fl)) {
+            // the queue's owner / consumer count load alongside the exact check's loads
+            qo = d.world > 1 ? d.q_owner[q] : d.my_rank;
+            qc = d.q_cons_n[q];
+            hit = topic_verify(d, pb, p, t, fl);
+          }
+        }
         // bindings are sorted by queue: a queue is emitted once, by its first hit
         u64 hm = __ballot(hit);
         u64 below = hm & lanemask_lt();
         u32 qb = (u32)__shfl((int)q, below ? 63 - __clzll(below) : 0);  // nearest lower hit
         u32 qtop = (u32)__shfl((int)q, hm ? 63 - __clzll(hm) : 0);     // highest hit
         bool emit = hit && (below ? qb : lastq) != q;
-        route_emit<PASS>(d, a, p, wbase, srank, q, emit, lane);
+        route_emit<PASS>(d, a, p, wbase, srank, q, emit, lane, qo, qc);
         if (hm) lastq = qtop;
       }
     }
