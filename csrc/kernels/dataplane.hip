@@ -329,18 +329,19 @@ DEV bool topic_match(const u8* pat, u32 plen, const u8* key, u32 klen, bool hash
   return true;
 }
 
-// ============================================================================ K0 prep + stage
-// grid (seg_max, 4): copy carry then new bytes into the work segment.  Fused k_prep: every
-// block derives its segment's work offset (prefix of the 16-aligned slot sizes of the
-// segments before it) itself, and block (0, 0) resets the step counters
-__global__ __launch_bounds__(256) void k_stage(DS d) {
-  __shared__ u32 lds[256 / 64 + 1];
+// ============================================================================ K0 step init
+// one block: resets the step counters and lays the step's segments out in the work buffer
+// (segment k at the prefix of the 16-aligned sizes carry + new bytes + 32 of the segments
+// before it).  The copy itself is done by k_frame_scan's block for the segment, which
+// stages the bytes through its LDS anyway (was: a grid-wide copy kernel, 12 us per 16.7 MB
+// step, whose output the frame scan then read back)
+__global__ __launch_bounds__(1024) void k_stage(DS d) {
+  __shared__ u32 lds[1024 / 64 + 1];
   const u32 tid = threadIdx.x;
   const u32 nseg = d.in->nseg;
-  const bool head = blockIdx.x == 0 && blockIdx.y == 0;
-  if (head) {
+  {
     u32* c = (u32*)d.ctr;
-    for (u32 k = tid; k < sizeof(Counters) / 4; k += 256)
+    for (u32 k = tid; k < sizeof(Counters) / 4; k += 1024)
       if (k * 4 < offsetof(Counters, log_head)) c[k] = 0;
     if (tid == 0) {
       d.ctr->n_grow = 0; d.tot[TS_NMOVE] = 0; d.tot[TS_NDEFER] = 0; d.tot[TS_TTL_BUDGET] = 0;
@@ -353,29 +354,26 @@ __global__ __launch_bounds__(256) void k_stage(DS d) {
       *d.id_next = cur > floor_pos ? cur : floor_pos;
     }
   }
-  if (blockIdx.x >= nseg && !head) return;
   u32 total = 0;
-  for (u32 k = tid; k < nseg; k += 256) total += align16(d.carry_len[d.segs[k].conn] + d.segs[k].len + 32);
+  for (u32 k = tid; k < nseg; k += 1024) total += align16(d.carry_len[d.segs[k].conn] + d.segs[k].len + 32);
   u32 all_t;
-  block_scan<256>(total, lds, all_t);
-  if (head && tid == 0) d.tot[15] = all_t;  // work bytes used
-  if (all_t > d.work_cap) return;  // host sizes steps so this never triggers
-  // block-stride over the segments (the grid is capped: seg_max blocks would mostly idle)
-  for (u32 s = blockIdx.x; s < nseg; s += gridDim.x) {
-    u32 before = 0;
-    for (u32 k = tid; k < s; k += 256) before += align16(d.carry_len[d.segs[k].conn] + d.segs[k].len + 32);
-    u32 all_b;
+  block_scan<1024>(total, lds, all_t);
+  if (tid == 0) d.tot[15] = all_t;  // work bytes used
+  if (all_t > d.work_cap) return;   // host sizes steps so this never triggers
+  u32 run = 0;
+  for (u32 b0 = 0; b0 < nseg; b0 += 1024) {
+    const u32 k = b0 + tid;
+    u32 cl = 0, len = 0, v = 0;
+    if (k < nseg) {
+      cl = d.carry_len[d.segs[k].conn];
+      len = d.segs[k].len;
+      v = align16(cl + len + 32);
+    }
+    u32 all;
     __syncthreads();   // lds of the previous scan
-    block_scan<256>(before, lds, all_b);
-    const u32 conn = d.segs[s].conn;
-    const u32 cl = d.carry_len[conn];
-    const u32 len = d.segs[s].len;
-    if (blockIdx.y == 0 && tid == 0) { d.seg_total[s] = cl + len; d.seg_start[s] = all_b; }
-    u8* dst = d.work + all_b;
-    u32 part = blockIdx.y, nparts = gridDim.y;
-    u32 t = tid + part * 256, nt = 256 * nparts;
-    if (cl) block_copy(dst, d.carry + (u64)conn * d.carry_cap, cl, t, nt);
-    if (len) block_copy(dst + cl, d.ingress + d.segs[s].src, len, t, nt);
+    const u32 o = block_scan<1024>(v, lds, all);
+    if (k < nseg) { d.seg_total[k] = cl + len; d.seg_start[k] = run + o; }
+    run += all;
   }
 }
 
@@ -504,6 +502,17 @@ DEV void frame_scan_seg(const DS& d, const u32 s) {
   u8* const claim = (u8*)(csucc + cmax);
   const u32 fmax = d.conn_frame_max[conn];
   const u32 wbase = d.seg_start[s];
+  if (d.tot[15] <= d.work_cap) {
+    // the segment into the work buffer (fused k_stage copy): the connection's carry, then
+    // its new ingress bytes.  k_decode / k_route_store read publishes from there; the
+    // screen below reads it back while it is hot in L2 and stages it in LDS
+    const u32 len = d.segs[s].len, cl = L - len;
+    u8* const dst = d.work + wbase;
+    if (cl) block_copy(dst, d.carry + (u64)conn * d.carry_cap, cl, tid, FS_NT);
+    if (len) block_copy(dst + cl, d.ingress + d.segs[s].src, len, tid, FS_NT);
+  }
+  __threadfence_block();
+  __syncthreads();
   SegOut so;
   so.conn = conn; so.status = 0; so.consumed = 0; so.carry = L; so.ncmds = 0; so.err_off = 0;
   so.pad[0] = so.pad[1] = 0;
@@ -2090,7 +2099,7 @@ DEV void live_add_blocks(const DS& d, u32 lane) {
 // one wave per publish: write its queue pairs (route pass 1), then allocate the message,
 // fill its MsgEnt and copy exchange / rk / props / body into the log (fused k_route<1> +
 // k_store: one pass over the phase's publishes)
-DEV void store_one(const DS& d, u32 p, u32 lane);
+DEV void store_one_pre(const DS& d, u32 p, u32 lane, const Pub& pb, u32 nq, u32 rr, u32 soff, u32 wbase);
 DEV void live_add_blocks(const DS& d, u32 lane);
 __global__ __launch_bounds__(256) void k_route_store(DS d) {
   u32 lane = lane_id();
@@ -2099,25 +2108,30 @@ __global__ __launch_bounds__(256) void k_route_store(DS d) {
   if (n > d.pub_cap) n = d.pub_cap;
   const u32 nw = (gridDim.x * blockDim.x) >> 6;
   for (u32 p = d.tot[TS_RANGE_LO] + ((blockIdx.x * blockDim.x + threadIdx.x) >> 6); p < n; p += nw) {
+    // the store's loads go out before pass 1's pair stores (which the compiler cannot
+    // move them past: every table is a global pointer of DS), one round instead of two
+    const Pub pb = d.pubs[p];
+    const u32 nq = d.pub_nq[p];
+    const u32 rr = d.pub_routed_rank[p];
+    const u32 soff = d.pub_slot_off[p];
+    const u32 wbase = d.tot[TS_PAIR_BASE] + d.pub_pair_off[p];
     route_one<1>(d, p, lane);
-    store_one(d, p, lane);
+    store_one_pre(d, p, lane, pb, nq, rr, soff, wbase);
   }
 }
 
-DEV void store_one(const DS& d, u32 p, u32 lane) {
-  Pub& pb = d.pubs[p];
-  if (d.pub_nq[p] == 0) return;
+DEV void store_one_pre(const DS& d, u32 p, u32 lane, const Pub& pb, u32 nq, u32 rr, u32 soff, u32 wbase) {
+  if (nq == 0) return;
   u64 base = *d.log_step_base;
   if (base == INVALID) {   // body log / message table full: dropped, confirmed with Basic.Nack
     if (lane == 0) {
-      pb.msg = INVALID;
+      d.pubs[p].msg = INVALID;
       if (pb.chslot != INVALID) d.ch_pub_fail[pb.chslot] = 1u;
     }
     return;
   }
-  u32 rr = d.pub_routed_rank[p];
   u32 msg = d.msg_free[d.tot[8] - 1 - rr];
-  u64 off = base + d.pub_slot_off[p];
+  u64 off = base + soff;
   u8* slot = d.log + (off % d.log_bytes);
   const u8* w = pub_src(d, pb);
   u32 meta = align16(pb.ex_len + pb.rk_len + pb.props_len);
@@ -2152,22 +2166,22 @@ DEV void store_one(const DS& d, u32 p, u32 lane) {
     // pairs past the pair table were not written (route_one): those queues never get
     // the message, so it holds only the references that were enqueued, and the
     // publisher gets Basic.Nack
-    const u32 wbase = d.tot[TS_PAIR_BASE] + d.pub_pair_off[p];
     const u32 fit = wbase >= d.pair_max ? 0u : (d.pair_max - wbase < pb.nq ? d.pair_max - wbase : pb.nq);
     m.refcnt = (i32)(fit ? fit : 1u);
     m.flags = pb.flags;
     m.pub_step = (u32)d.in->step;
     m.pad = 0;
     d.msgs[msg] = m;
-    pb.msg = msg;
+    u32 pmsg = msg;
     if (fit < pb.nq) {
       atomicAdd(&d.ctr->n_ring_full, pb.nq - fit);
       if (pb.chslot != INVALID) d.ch_pub_fail[pb.chslot] = 1u;
     }
     if (!fit) {   // freed by k_post: this kernel's waves are still popping the free list
-      pb.msg = INVALID;
+      pmsg = INVALID;
       d.defer_free[atomicAdd(&d.tot[TS_NDEFER], 1u)] = msg;
     }
+    d.pubs[p].msg = pmsg;
   }
 }
 

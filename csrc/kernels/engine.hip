@@ -1446,7 +1446,7 @@ class Engine {
   // frame scan, command assembly, decode (K1-K5)
   void launch_ingest(hipStream_t s, const DS& d) {
     Range rg("chanamq.K1-K4.ingest");
-    hipLaunchKernelGGL(k_stage, dim3(capped(d.seg_max, 256).x, 4), dim3(256), 0, s, d);
+    hipLaunchKernelGGL(k_stage, dim3(1), dim3(1024), 0, s, d);
     hipLaunchKernelGGL(k_frame_scan, capped(d.seg_max, 512), dim3(FS_NT), 0, s, d);
     launch_scan(s, {{d.cmd_is_pub, d.cmd_pub_rank}, {d.cmd_is_ack, d.cmd_ack_rank}}, &d.ctr->n_cmds,
                 d.cmd_max, 4);

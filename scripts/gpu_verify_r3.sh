@@ -14,4 +14,9 @@ timeout -k 10 150 python bench.py --gpus 1 --steps 50 --warmup 10 > $O/bench_k50
 rc=$?; [ $rc -ne 0 ] && exit $rc
 CHANAMQ_BENCH_BACKEND=gloo timeout -k 10 240 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
   --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 20 --warmup 5 --soak-s 0 > $O/bench_2rank_gloo.json 2> $O/bench_2rank_gloo.err
-echo "2rank exit $?" >> $O/bench_2rank_gloo.err
+rc=$?; echo "2rank exit $rc" >> $O/bench_2rank_gloo.err; [ $rc -ne 0 ] && exit $rc
+# kernel statistics of the headline bench itself (rocprofv3 --kernel-trace --stats)
+export TMPDIR=/tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o bench -- python3 bench.py --steps 20 --warmup 5 --soak-s 0 > $O/prof.log 2>&1
+echo "prof exit $?" >> $O/prof.log
+find $O/prof -name "*kernel_stats.csv" -exec cp {} $O/bench_kernel_stats.csv \;
