@@ -502,6 +502,7 @@ DEV void frame_scan_seg(const DS& d, const u32 s) {
   u8* const claim = (u8*)(csucc + cmax);
   const u32 fmax = d.conn_frame_max[conn];
   const u32 wbase = d.seg_start[s];
+  FS_MARK(15);
   if (d.tot[15] <= d.work_cap) {
     // the segment into the work buffer (fused k_stage copy): the connection's carry, then
     // its new ingress bytes.  k_decode / k_route_store read publishes from there; the
@@ -572,6 +573,7 @@ DEV void frame_scan_seg(const DS& d, const u32 s) {
       __syncthreads();
       if (staged) b = (const u8*)fs_stage;
     }
+    FS_MARK(12);
     // raw candidates per thread (its words are contiguous: the scan keeps position order)
     u32 rc = 0;
     if (use_am)
@@ -582,6 +584,7 @@ DEV void frame_scan_seg(const DS& d, const u32 s) {
       }
     u32 rtot;
     u32 roff = block_scan<FS_NT>(rc, sc, rtot);
+    FS_MARK(13);
     u32 tot = 0;
     if (use_am && rtot <= cmax) {
       // every raw candidate validated in parallel (one thread each), then compacted in
@@ -597,6 +600,7 @@ DEV void frame_scan_seg(const DS& d, const u32 s) {
         }
       }
       __syncthreads();
+      FS_MARK(14);
       for (u32 k0 = 0; k0 < rtot; k0 += FS_NT) {
         const u32 i = k0 + tid;
         bool ok = false;

@@ -17,7 +17,8 @@ print("phase us (median / max over segments):")
 for k in range(8):
     print(k, f"{np.median(ph[:, k]):8.1f} {ph[:, k].max():8.1f}")
 print("total", np.median(dbg[:, 8] - dbg[:, 0]) / 100, (dbg[:, 8] - dbg[:, 0]).max() / 100)
-sub = [(2, 9, "c: (b) tails + sync"), (9, 10, "c: fail compaction"), (10, 11, "c: walk"), (11, 3, "c: expand")]
+sub = [(15, 0, "segment copy (carry + ingress -> work)"), (0, 12, "a: screen + LDS stage"), (12, 13, "a: raw count + scan"), (13, 14, "a: compaction"),
+       (14, 1, "a: validation + tail"), (2, 9, "c: (b) tails + sync"), (9, 10, "c: fail compaction"), (10, 11, "c: walk"), (11, 3, "c: expand")]
 for a, b, name in sub:
     print(name, f"{np.median(dbg[:, b] - dbg[:, a]) / 100:8.2f}")
 print("block start spread us", (dbg[:, 0].max() - dbg[:, 0].min()) / 100)
