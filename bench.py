@@ -345,7 +345,8 @@ def main():
                           "auto-ack, non-persistent"),
                 "global_batch": int(round(mps * world)),
                 "seq_len": args.body,
-                "parallelism": (f"queue-sharded x{world}: one broker, cross-GPU routing by RCCL all-to-all"
+                "parallelism": (f"queue-sharded x{world}: one broker, cross-GPU routing by "
+                                + ("RCCL all-to-all" if backend == "nccl" else f"{backend} all-to-all staged through the host")
                                 + (" (pipelined, +1 step for cross-GPU messages)" if args.exchange_lag else "")
                                 if shards > 1 else
                                 (f"x{world} independent broker shards" if world > 1 else "single GPU")),
