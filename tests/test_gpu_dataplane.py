@@ -83,3 +83,62 @@ def test_topic_mfma_prefilter_exact(gpu):
                 got.append(c.method.routing_key)
         want = [k for k in keys if topic_match(p, k)]
         assert got == want, p
+
+
+def test_decode_windows_name_and_key_lengths(gpu):
+    """k_decode reads exchange names (up to 31 bytes) and routing keys (up to 32) from
+    32-byte register windows and takes the byte loops beyond: names and keys on both sides
+    of those edges (trailing dots, empty words, more than 8 words) route exactly as the
+    golden topic matcher and the direct bindings say."""
+    from chanamq_amd.engine.dataplane import GpuDataPlane
+    from chanamq_amd.engine.traffic import publish_stream
+    from chanamq_amd.models.matcher import topic_match
+    from chanamq_amd.protocol.codec import CommandAssembler, FrameParser
+
+    keys = ["", "zz", "a..zz", "." * 32, "a" + "." * 31, ".".join("abcdefghijklmnop")]
+    keys += ["a." + "b" * (n - 2) for n in (30, 31, 32, 33, 40)]
+    keys += ["c" * (n - 3) + ".zz" for n in (32, 33)]
+    k31, k32, k33 = keys[7], keys[8], keys[9]
+    assert (len(k31), len(k32), len(k33)) == (31, 32, 33)
+    pats = ["*", "*.*", "#", "a.#", "#.zz", k31, k32, k33]
+    d = GpuDataPlane(**CFG)
+    vh = "AMQ.DEFAULT"
+    conn, want, stream = 10, {}, b""
+    for n in (1, 30, 31, 32, 40):            # exchange name lengths
+        x = "t" + "x" * (n - 1)
+        d.declare_exchange(vh, x, "topic")
+        for j, p in enumerate(pats):
+            q = f"q{n}.{j}"
+            d.declare_queue(vh, q)
+            d.bind(vh, q, x, p)
+            d.open_connection(conn, vh)
+            d.open_channel(conn, 1)
+            d.consume(conn, 1, vh, q, f"c{conn}", no_ack=True)
+            want[conn] = [k for k in keys if topic_match(p, k)]
+            conn += 1
+        stream += publish_stream(len(keys), x, lambda i: keys[i], 8, seed=n)
+    for n in (1, 40):                        # direct: the key hash from the window
+        x = "d" + "y" * (n - 1)
+        d.declare_exchange(vh, x, "direct")
+        for k in (k31, k32, k33):
+            q = f"dq{n}.{len(k)}"
+            d.declare_queue(vh, q)
+            d.bind(vh, q, x, k)
+            d.open_connection(conn, vh)
+            d.open_channel(conn, 1)
+            d.consume(conn, 1, vh, q, f"c{conn}", no_ack=True)
+            want[conn] = [k]
+            conn += 1
+        stream += publish_stream(len(keys), x, lambda i: keys[i], 8, seed=100 + n)
+    d.open_connection(1, vh)
+    d.open_channel(1, 1)
+    r = d.step({1: stream})
+    egress = r["egress"] if isinstance(r, dict) else r.egress
+    for c, w in want.items():
+        got = []
+        fp, ca = FrameParser(), CommandAssembler()
+        for fr in fp.feed(egress.get(c, b"")):
+            cm = ca.feed(fr)
+            if cm is not None and cm.method is not None:
+                got.append(cm.method.routing_key)
+        assert got == w, (c, w)
