@@ -112,3 +112,15 @@ def test_gpu_lagged_exchange_matches_golden(gpu, name, world):
         assert set(a) == set(b), (k, sorted(a), sorted(b))
         for c in a:
             assert a[c] == b[c], (k, c)
+
+
+@pytest.mark.timeout(180)
+def test_rccl_single_rank_paths(gpu):
+    """RCCL on the device: the bench's all-to-all exchange (device tensors, exact splits,
+    empty steps) and all_reduce through a one-rank communicator, and the engine's dlopen'ed
+    librccl binding (every symbol resolved, a unique id drawn)."""
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()), WORLD_SIZE="1", RANK="0",
+               LOCAL_RANK="0", PYTHONPATH=os.path.dirname(HERE))
+    p = subprocess.run([sys.executable, os.path.join(HERE, "rccl_single_worker.py")], env=env,
+                       capture_output=True, text=True, timeout=170)
+    assert p.returncode == 0 and "RCCL ok" in p.stdout, (p.returncode, p.stdout[-2000:], p.stderr[-3000:])
