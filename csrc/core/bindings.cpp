@@ -249,6 +249,7 @@ PYBIND11_MODULE(_core, m) {
            }, py::arg("conn"), py::arg("leftover") = py::bytes(""))
       .def("set_host_mode", &Frontend::set_host_mode)
       .def("set_heartbeat", &Frontend::set_heartbeat)
+      .def("set_read_cap", &Frontend::set_read_cap)
       .def("close", &Frontend::close)
       .def("kick", &Frontend::kick)
       .def("pause", &Frontend::pause, py::call_guard<py::gil_scoped_release>())

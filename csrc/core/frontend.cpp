@@ -68,6 +68,9 @@ struct FeConn {
   // heartbeats
   std::atomic<i64> last_rx{0}, last_tx{0};
   std::atomic<u32> hb_s{0};
+  // per-connection read budget per step (0: the front end's per_conn_read); the control
+  // plane lowers it for publisher-confirm channels (set_read_cap)
+  std::atomic<u64> read_cap{0};
 };
 
 struct FeIo {
@@ -345,6 +348,10 @@ void Frontend::set_heartbeat(u32 conn, u32 seconds) {
   if (conn < c_max_) conns_[conn]->hb_s = seconds;
 }
 
+void Frontend::set_read_cap(u32 conn, u64 bytes) {
+  if (conn < c_max_) conns_[conn]->read_cap = bytes;
+}
+
 void Frontend::close(u32 conn) {
   if (conn == 0 || conn >= c_max_) return;
   FeIo& io = *io_[conns_[conn]->io];
@@ -501,6 +508,7 @@ void Frontend::drop(FeConn& c, bool notify) {
   c.fd = -1;
   c.mode = M_DEAD;
   c.gen.fetch_add(1);
+  c.read_cap = 0;
   c.out.clear();
   c.out_pos = 0;
   c.inject.clear();
@@ -581,6 +589,7 @@ void Frontend::io_loop(int i) {
         }
         c.mode = M_FREE;
         c.gen.fetch_add(1);
+        c.read_cap = 0;
         c.out.clear();
         c.out_pos = 0;
         c.wblocked = false;
@@ -697,6 +706,8 @@ void Frontend::io_loop(int i) {
 // within the per-connection budget; reserved densely in the shared arena
 void Frontend::gather_conn(FeIo& io, FeConn& c, u8* arena, u64 cap) {
   u64 lim = cfg_.per_conn_read;
+  const u64 rc = c.read_cap.load(std::memory_order_relaxed);
+  if (rc && rc < lim) lim = rc;
   const u64 room = api_->carry_cap > (u64)c.carry + c.inflight ? api_->carry_cap - c.carry - c.inflight : 0;
   if (lim > room) lim = room;
   if (c.paused) {   // behind a control command: bytes wait in the socket (TCP back-pressure)

@@ -124,6 +124,7 @@ class Frontend {
   void set_data_mode(u32 conn, const std::string& leftover);   // bytes now go to the GPU
   void set_host_mode(u32 conn);                          // bytes go to the control plane again
   void set_heartbeat(u32 conn, u32 seconds);
+  void set_read_cap(u32 conn, u64 bytes);                // per-step read budget (0: per_conn_read)
   void close(u32 conn);                                  // flush, close the socket, free the slot
   void kick(u32 conn);                                   // unpaused: re-present its device carry
   // bytes for a socketless pseudo-connection (committed transactions): stepped with the

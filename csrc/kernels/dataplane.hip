@@ -2035,6 +2035,10 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
   const u32 lo = d.tot[TS_RANGE_LO];
   u32 n = d.tot[TS_RANGE_HI];
   if (n > d.pub_cap) n = d.pub_cap;
+  // a block past the step's publishes leaves before any per-wave set-up: the grid is sized
+  // for capacity (2048 blocks), and the register allocator spills loop-invariant state to
+  // scratch in the prologue -- 1 KB of HBM writes per idle wave otherwise (PMC WRITE_SIZE)
+  if (lo + blockIdx.x * 16 >= n) return;
   for (u32 g0 = lo + blockIdx.x * 16; g0 < n; g0 += gridDim.x * 16) {
     topic_group(d, g0, n, w, lane);
     __threadfence_block();
