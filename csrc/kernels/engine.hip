@@ -64,6 +64,11 @@ class Engine {
     };
     device_ = (int)get("device", 0);
     HIPCHECK(hipSetDevice(device_));
+    {
+      int ncu = 0;
+      if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device_) == hipSuccess && ncu > 0)
+        n_cu_ = (u32)ncu;
+    }
     d_ = DS{};
     d_.c_max = (u32)get("c_max", 1024);
     d_.chpc = next_pow2((u32)get("chpc", 16));
@@ -1447,7 +1452,10 @@ class Engine {
   void launch_ingest(hipStream_t s, const DS& d) {
     Range rg("chanamq.K1-K4.ingest");
     hipLaunchKernelGGL(k_stage, dim3(1), dim3(1024), 0, s, d);
-    hipLaunchKernelGGL(k_frame_scan, capped(d.seg_max, 512), dim3(FS_NT), 0, s, d);
+    // one block per CU fits (154 KB of LDS): more blocks than CUs only queue behind the
+    // busy ones, and blocks past the step's segments would still be dispatched one by one
+    // after them (the grid is sized for capacity at capture)
+    hipLaunchKernelGGL(k_frame_scan, capped(d.seg_max, n_cu_), dim3(FS_NT), 0, s, d);
     launch_scan(s, {{d.cmd_is_pub, d.cmd_pub_rank}, {d.cmd_is_ack, d.cmd_ack_rank}}, &d.ctr->n_cmds,
                 d.cmd_max, 4);
     hipLaunchKernelGGL(k_decode, blocks(d.cmd_max, 256), dim3(256), 0, s, d);
@@ -1457,9 +1465,12 @@ class Engine {
   // imports: phase B's import + routing pass 0 kernel (k_import_route) instead of k_route
   void launch_route(hipStream_t s, const DS& d, u32 nmax, bool imports = false) {
     Range rg("chanamq.K6-K13.route_store");
-    const dim3 groups = capped(ceil_div(nmax ? nmax : 1, 16), 2048);   // 16 publishes per block
-    if (imports) hipLaunchKernelGGL(k_import_route, groups, dim3(1024), 0, s, d);   // + prep, link acks
-    else hipLaunchKernelGGL(k_route, groups, dim3(1024), 0, s, d);
+    // 16 publishes per block, grid-stride; the grid is the blocks that can be resident
+    // (k_route: 2 per CU at 64 VGPRs; k_import_route: 1), not the capacity's groups --
+    // the idle blocks of a capacity-sized grid were still dispatched after the busy ones
+    const u64 ngroups = ceil_div(nmax ? nmax : 1, 16);
+    if (imports) hipLaunchKernelGGL(k_import_route, capped(ngroups, n_cu_), dim3(1024), 0, s, d);   // + prep, link acks
+    else hipLaunchKernelGGL(k_route, capped(ngroups, 2 * n_cu_), dim3(1024), 0, s, d);
     // scan of the routing counts + the phase's log reservation, then pairs + store
     const ScanArgs a = scan_args({{d.pub_nq, d.pub_pair_off}, {d.pub_slot, d.pub_slot_off},
                                   {d.pub_routed, d.pub_routed_rank}, {d.pub_ret_sz, d.pub_ret_off}},
@@ -1565,6 +1576,7 @@ class Engine {
   }
 
   int device_ = 0;
+  u32 n_cu_ = 256;   // compute units of the device (grid caps of the block-per-segment / group kernels)
   DS d_;
   std::map<std::string, Buf> bufs_;
   u64 total_bytes_ = 0;
