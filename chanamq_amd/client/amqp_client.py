@@ -6,6 +6,7 @@ load generator.  ``pika`` is not installed in this image, so this is our own cli
 """
 
 import collections
+import select
 import socket
 import ssl as _ssl
 import struct
@@ -254,10 +255,25 @@ class Connection:
         self._send_raw(encode_method_frame(ch, m))
 
     def _pump(self, timeout):
-        self.sock.settimeout(timeout)
+        """Read what is available within ``timeout`` seconds and dispatch it.
+
+        The socket itself always stays in blocking mode with ``self.timeout``
+        (so ``sendall`` never sees ``EAGAIN``); the read window is enforced
+        with ``select``.  A window of <= 0 is a poll.  TLS sockets can hold
+        decrypted bytes that ``select`` does not see, so ``pending()`` is
+        checked first.
+        """
+        pending = isinstance(self.sock, _ssl.SSLSocket) and self.sock.pending() > 0
+        if not pending:
+            try:
+                ready, _, _ = select.select([self.sock], [], [], max(0.0, timeout))
+            except (OSError, ValueError):
+                ready = [self.sock]   # closed fd: let recv report it
+            if not ready:
+                return
         try:
             data = self.sock.recv(1 << 20)
-        except (socket.timeout, _ssl.SSLWantReadError):
+        except (socket.timeout, BlockingIOError, InterruptedError, _ssl.SSLWantReadError):
             return
         if not data:
             if self.closed is None:

@@ -85,6 +85,7 @@ PYBIND11_MODULE(_core, m) {
              py::dict d;
              d["runs"] = c.runs; d["last_before"] = c.last_before; d["last_after"] = c.last_after;
              d["tail_bytes"] = c.tail_bytes; d["last_s"] = c.last_s; d["max_lock_s"] = c.max_lock_s;
+             d["failures"] = c.failures; d["last_error"] = c.last_error;
              return d;
            })
       .def("deleted_queue_ids", &Store::deletedQueueIds)

@@ -9,6 +9,7 @@
 #include <libgen.h>
 
 #include <chrono>
+#include <cstdio>
 #include <cstring>
 #include <stdexcept>
 
@@ -249,10 +250,26 @@ CompactStats Store::compactStats() {
 
 void Store::maybe_compact() {
   if (auto_ratio_ <= 0 || fd_ < 0 || compacting_ || compact_stop_ || wal_bytes_ < auto_min_) return;
+  if (wal_bytes_ < auto_backoff_) return;
   if ((double)wal_bytes_ < auto_ratio_ * (double)liveEstimate()) return;
   if (compact_th_.joinable()) compact_th_.join();   // the previous run has finished
   compacting_ = true;
-  compact_th_ = std::thread([this] { compact_run(); });
+  // A background run must never let an exception escape the thread (std::terminate
+  // would take the broker down with unsynced state).  A failed run (typically ENOSPC
+  // while writing the second copy) is recorded and auto-compaction backs off until the
+  // WAL has grown by half again; the live WAL is untouched by a failed run.
+  compact_th_ = std::thread([this] {
+    try {
+      compact_run();
+    } catch (std::exception& e) {
+      std::lock_guard<std::recursive_mutex> g(mu_);
+      cstats_.failures++;
+      cstats_.last_error = e.what();
+      auto_backoff_ = wal_bytes_ + wal_bytes_ / 2;
+      std::fprintf(stderr, "chanamq store: background compaction failed (%s); retry after %llu WAL bytes\n",
+                   e.what(), (unsigned long long)auto_backoff_);
+    }
+  });
 }
 
 void Store::replay() {
@@ -427,6 +444,7 @@ void Store::compact_run() {
           max_lock = std::max(max_lock, mono_s() - l0);
           cstats_.max_lock_s = std::max(cstats_.max_lock_s, max_lock);
           cstats_.last_s = mono_s() - t0;
+          auto_backoff_ = 0;
           compacting_ = false;
           return;
         }

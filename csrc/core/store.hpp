@@ -66,6 +66,8 @@ struct BindRow { std::string queue, key; std::map<std::string, std::string> args
 struct CompactStats {
   uint64_t runs = 0, last_before = 0, last_after = 0, tail_bytes = 0;
   double last_s = 0, max_lock_s = 0;
+  uint64_t failures = 0;        // background runs that failed (ENOSPC, EIO, rename, ...)
+  std::string last_error;
 };
 
 class Store {
@@ -147,6 +149,7 @@ class Store {
   uint64_t msg_bytes_ = 0;            // live message row bytes (liveEstimate)
   double auto_ratio_ = 4.0;
   uint64_t auto_min_ = 256ull << 20;
+  uint64_t auto_backoff_ = 0;         // after a failed background run: retry once the WAL passes this
   std::thread compact_th_;
   std::atomic<bool> compacting_{false}, compact_stop_{false};
   CompactStats cstats_;

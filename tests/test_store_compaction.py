@@ -95,3 +95,41 @@ def test_compaction_under_concurrent_commits(tmp_path):
     st2 = open_store(d, fsync=False)
     assert rows(st2) == before
     st2.close()
+
+
+def test_background_compaction_failure_is_contained(tmp_path):
+    """an error inside the background compaction thread (here the
+    .compact file cannot be created, standing in for ENOSPC/EIO) must not escape the
+    thread.  The store keeps appending, records the failure, backs off, and a later run
+    succeeds once the cause is gone; the synchronous compact() still raises."""
+    import pytest
+    d = str(tmp_path / "f")
+    st = open_store(d, fsync=False)
+    os.mkdir(os.path.join(d, "chanamq.wal.compact"))   # open(O_CREAT|O_TRUNC) -> EISDIR
+    st.set_auto_compact(1.5, 1 << 16)
+    st.insert_vhost("v", True)
+    st.insert_queue_meta("v-_.q", -1, set(), True, 0)
+    body = b"z" * 2048
+    for i in range(1, 400):
+        st.insert_message(i, 1, b"h" * 10, body, "x", "k", True, 1, 0)
+        st.delete_message(i)
+        if i % 16 == 0:
+            st.sync()
+            st.wait_compaction()
+    cs = st.compact_stats()
+    assert cs["runs"] == 0 and cs["failures"] >= 1, cs
+    assert "compact" in cs["last_error"]
+    # failures back off: far fewer attempts than group commits
+    assert cs["failures"] < 400 // 16, cs
+    with pytest.raises(RuntimeError):
+        st.compact()
+    os.rmdir(os.path.join(d, "chanamq.wal.compact"))
+    st.compact()
+    assert st.compact_stats()["runs"] == 1
+    st.insert_message(10_000, 1, b"h" * 10, body, "x", "k", True, 1, 0)
+    st.sync()
+    before = rows(st)
+    st.close()
+    st2 = open_store(d, fsync=False)
+    assert rows(st2) == before
+    st2.close()
