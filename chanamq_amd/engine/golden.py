@@ -44,7 +44,9 @@ class GoldenDataPlane(ControlState):
                  xfer_bytes=1 << 24, persist=False, exchange_lag=0, persist_max=1 << 16, **kw):
         super().__init__(hash_wildcard=hash_wildcard, **kw)
         self.persist = persist
-        self.persist_max = persist_max    # k_dequeue: durable TTL skips <= persist_max / 4 a step
+        # k_dequeue: durable TTL skips <= persist_max / 4 a step; the engine raises
+        # persist_max to 2 * deliv_max + 4096 (a step's consumed records always fit)
+        self.persist_max = max(persist_max, 2 * deliv_max + 4096) if persist else persist_max
         self._ttl_budget = 0
         self.lag = bool(exchange_lag) and self.world > 1
         self._lag_prev = []                 # exchange_lag: records received last step

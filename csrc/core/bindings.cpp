@@ -12,6 +12,7 @@
 #include "gateway.hpp"
 #include "loadgen.hpp"
 #include "store.hpp"
+#include "../kernels/xchg_host.h"
 
 namespace py = pybind11;
 using namespace cmq;
@@ -315,6 +316,12 @@ PYBIND11_MODULE(_core, m) {
       .def("xchg_setup", &EchoEngine::xchg_setup, py::arg("name"), py::arg("members"), py::arg("timeout_ms") = 5000)
       .def_readonly("imported", &EchoEngine::imported)
       .def_readonly("steps", &EchoEngine::steps);
+
+  // the shared-memory exchange's barrier alone (tests of its failure semantics)
+  py::class_<cmqx::ShmXchg>(m, "ShmXchg")
+      .def(py::init<const std::string&, const std::vector<int>&, int, size_t, int>(), py::arg("name"),
+           py::arg("members"), py::arg("me"), py::arg("box_bytes") = 4096, py::arg("timeout_ms") = 1000)
+      .def("barrier", &cmqx::ShmXchg::barrier, py::call_guard<py::gil_scoped_release>());
 
   m.def("run_load", [](py::dict d) {
     LoadSpec s;

@@ -64,6 +64,7 @@ struct FeConn {
   // only while paused
   u32 carry = 0, inflight = 0;
   bool paused = false, kicked = false;
+  u64 inj_step = 0;       // the step whose gather took the last inject() bytes (FE_INJECTED)
   bool wblocked = false;  // egress back-pressure flag raised on the device (mu held)
   // heartbeats
   std::atomic<i64> last_rx{0}, last_tx{0};
@@ -98,7 +99,7 @@ Frontend::Frontend(const FrontendCfg& cfg, const CmqEngineApi* api) : cfg_(cfg),
   if (!api_ || api_->abi != CMQ_STEP_ABI) throw std::runtime_error("frontend: engine C API missing or ABI mismatch");
   c_max_ = api_->c_max;
   held_cnt_.assign(c_max_, 0);
-  notify_.assign(c_max_, 0);
+  notify_.reset(new std::atomic<u8>[c_max_]());
   if (cfg_.io_threads < 1) cfg_.io_threads = 1;
   if (!cfg_.max_slot || cfg_.max_slot > c_max_ - 2) cfg_.max_slot = c_max_ - 2;
   conns_.resize(c_max_);
@@ -720,6 +721,7 @@ void Frontend::gather_conn(FeIo& io, FeConn& c, u8* arena, u64 cap) {
     if (!c.inject.empty()) {
       if (c.inject.size() <= lim) inj.swap(c.inject);
       else { inj = c.inject.substr(0, lim); c.inject.erase(0, lim); c.in_ready = true; }
+      c.inj_step = ph_step_;
     }
   }
   int avail = 0;
@@ -802,6 +804,7 @@ void Frontend::io_phase(std::vector<Scatter*>& scat, bool gather, bool async) {
     const u64 freeb = api_->log_bytes > used + reserve ? api_->log_bytes - used - reserve : 0;
     if (freeb < ph_cap_) ph_cap_ = std::max<u64>(freeb, 256u << 10);
   }
+  ph_step_ = step_no_ + 1;   // the step these segments go into (f.step = ++step_no_)
   ph_used_ = 0;
   ph_nseg_ = 0;
   ph_carry_ = 0;
@@ -843,7 +846,9 @@ void Frontend::finish_oldest(std::deque<Inflight>& inflight) {
     if (s.status & SS_CTRL) cc.paused = true;
     if (notify_[s.conn] && cc.fd < 0) {   // an injected pseudo-connection's bytes were stepped
       std::lock_guard<std::mutex> g(cc.mu);
-      if (cc.inject.empty()) {
+      // only once the step that took the LAST injected bytes has finished (an inject
+      // larger than one step's read budget spans several steps)
+      if (cc.inject.empty() && f.step >= cc.inj_step) {
         notify_[s.conn] = 0;
         FeEvent e;
         e.kind = FE_INJECTED;

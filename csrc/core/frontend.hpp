@@ -144,7 +144,9 @@ class Frontend {
   // per-step liveness for the failure detector: false once the engine failed or a GPU
   // wait (step results, egress) has been stuck longer than `stuck_s`
   bool healthy(double stuck_s) const;
-  std::vector<u8> notify_;   // per connection: post FE_INJECTED when its segment was stepped
+  // per connection: post FE_INJECTED when its segment was stepped (inject() on the control
+  // thread sets it, the stepper clears it)
+  std::unique_ptr<std::atomic<u8>[]> notify_;
   // fault injection (tests): after `steps` more steps, kind 1 = engine error, 2 = process
   // exit, 3 = wedge (the stepper blocks inside a GPU wait forever)
   void inject_fault(int kind, u64 steps);
@@ -214,6 +216,7 @@ class Frontend {
   u8* ph_arena_ = nullptr;
   u64 ph_cap_ = 0;
   std::atomic<u64> ph_used_{0};
+  u64 ph_step_ = 0;   // step number of the gather phase in progress
   std::atomic<u32> ph_nseg_{0};
   std::atomic<u64> ph_carry_{0};
 
@@ -253,7 +256,7 @@ class Frontend {
   FeStats stats_;
   std::atomic<u64> rx_bytes_{0}, tx_bytes_{0};
   u64 step_no_ = 0;
-  bool failed_ = false;
+  std::atomic<bool> failed_{false};   // read by healthy() (heartbeat thread)
 
   // sharded broker
   std::atomic<bool> sync_req_{false};

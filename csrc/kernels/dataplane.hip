@@ -2640,8 +2640,20 @@ __global__ void k_enqueue(DS d, u32 src, u32 hs_ntiles) {
 
 // a persistent message changed state in a durable queue: record it for the store
 // (kind 0 consumed/acked, 1 expired, 2 dropped, 3 delivered awaiting ack, 4 requeued)
-DEV void wave_consumed(const DS& d, u32 msg, u32 q, u64 qpos, u32 kind, bool valid) {
-  // X3: a shadow message left its queue (consumed, expired, dropped): ack it at the owner
+DEV bool wants_record(const DS& d, u32 msg, u32 q, bool valid) {
+  return d.persist && valid && msg != INVALID && d.q_durable[q] && (d.msgs[msg].flags & MF_PERSIST);
+}
+DEV void consumed_rec_at(const DS& d, u32 msg, u32 q, u64 qpos, u32 kind, u32 k) {
+  ConsumedRec r;
+  r.msg_id = (i64)d.msgs[msg].msg_id;
+  r.qpos = qpos;
+  r.q = q;
+  r.kind = kind;
+  r.pad[0] = r.pad[1] = 0;
+  d.crec[k] = r;
+}
+// X3: a shadow message left its queue (consumed, expired, dropped): ack it at the owner
+DEV void link_consumed(const DS& d, u32 msg, u32 q, u32 kind, bool valid) {
   if (d.links && valid && msg != INVALID && kind <= 2u) {
     const u32 ow = d.q_link_owner[q];
     if (ow) {
@@ -2655,18 +2667,13 @@ DEV void wave_consumed(const DS& d, u32 msg, u32 q, u64 qpos, u32 kind, bool val
       }
     }
   }
+}
+DEV void wave_consumed(const DS& d, u32 msg, u32 q, u64 qpos, u32 kind, bool valid) {
+  link_consumed(d, msg, q, kind, valid);
   if (!d.persist) return;
-  bool want = valid && msg != INVALID && d.q_durable[q] && (d.msgs[msg].flags & MF_PERSIST);
+  bool want = wants_record(d, msg, q, valid);
   u32 k = wave_reserve(&d.ctr->n_consumed, want);
-  if (want && k < d.persist_max) {
-    ConsumedRec r;
-    r.msg_id = (i64)d.msgs[msg].msg_id;
-    r.qpos = qpos;
-    r.q = q;
-    r.kind = kind;
-    r.pad[0] = r.pad[1] = 0;
-    d.crec[k] = r;
-  }
+  if (want && k < d.persist_max) consumed_rec_at(d, msg, q, qpos, kind, k);
 }
 
 
@@ -2678,6 +2685,8 @@ struct MsLds {
   u64 up[MS_MAX];
   u32 rq[MS_MAX];
   u32 wc[4];
+  u32 rc[4];     // store records per wave of the current chunk
+  u32 rbase;     // their block reservation (INVALID: budget exhausted)
   u32 n, nb;
   unsigned long long ovf_a, ovf_r;
 };
@@ -2738,6 +2747,21 @@ DEV void collect_settles(const DS& d, u32 ch, u32 tid, u32 lane, u32 w, MsLds& m
   __syncthreads();
 }
 
+// k_chan_advance's share of a step's consumed-store records: persist_max minus what the
+// later producers can take (deliveries <= deliv_max in k_dv_write / k_post, the durable
+// TTL skip <= persist_max / 4 in k_dequeue); the engine sizes persist_max so this is
+// >= deliv_max / 2.  Reserved per 256-slot chunk, never past the budget (CAS).
+DEV u32 ca_reserve(const DS& d, u32 n) {
+  const u32 lim = d.persist_max - d.deliv_max - (d.persist_max >> 2) - 64u;
+  u32 cur = *(volatile u32*)&d.ctr->n_consumed;
+  while (true) {
+    if (cur + n > lim) return INVALID;
+    const u32 prev = atomicCAS(&d.ctr->n_consumed, cur, cur + n);
+    if (prev == cur) return cur;
+    cur = prev;
+  }
+}
+
 DEV void chan_advance_one(const DS& d, u32 ch, u32 tid, u32 lane, u32 w, u32* s_first, u32* s_done, MsLds& ms) {
   collect_settles(d, ch, tid, lane, w, ms);
   const u32 nb = ms.nb;
@@ -2745,6 +2769,7 @@ DEV void chan_advance_one(const DS& d, u32 ch, u32 tid, u32 lane, u32 w, u32* s_
   const u64 aup = d.ch_ack_upto[ch], rup = d.ch_req_upto[ch];
   USlot* win = d.uwin + (u64)ch * (d.ucap_mask + 1);
   bool contiguous = true;
+  bool deferred = false;   // block-uniform: the record budget ran out at some chunk
   u64 newhead = head;
   u32 manual_done = 0;
   for (u64 t0 = head; t0 < nt; t0 += 256) {
@@ -2766,6 +2791,32 @@ DEV void chan_advance_one(const DS& d, u32 ch, u32 tid, u32 lane, u32 w, u32* s_
     }
     const bool acked = valid && st == US_ACKED;
     const bool req = valid && st == US_REQUEUE;
+    // store records of this chunk, reserved for the whole block within the step's budget.
+    // Past the budget the channel keeps its decided marks (ACKED / REQUEUE slot states,
+    // which the next step resolves first) and stays dirty (a burst of settles
+    // of durable persistent messages must not overflow persist_max and stop the broker)
+    u32 rec_k = INVALID;
+    const bool want_rec = wants_record(d, u.msg, u.q, acked || req);
+    if (d.persist) {   // kernel-uniform
+      const u64 rm = __ballot(want_rec);
+      if (lane == 0) ms.rc[w] = (u32)__popcll(rm);
+      __syncthreads();
+      if (tid == 0) {
+        const u32 tot = ms.rc[0] + ms.rc[1] + ms.rc[2] + ms.rc[3];
+        ms.rbase = deferred ? INVALID : (tot ? ca_reserve(d, tot) : 0u);
+      }
+      __syncthreads();
+      if (ms.rbase == INVALID) deferred = true;
+      if (!deferred) {
+        rec_k = ms.rbase + (u32)__popcll(rm & lanemask_lt());
+        for (u32 k = 0; k < w; ++k) rec_k += ms.rc[k];
+      }
+    }
+    if (deferred) {   // block-uniform
+      if (valid && (st == US_ACKED || st == US_REQUEUE) && st != u.state) win[(t - 1) & d.ucap_mask].state = st;
+      contiguous = false;
+      continue;
+    }
     // requeue list (one reservation per wave)
     u32 rtot;
     u32 ri = wave_reserve(d.req_n, req, &rtot);
@@ -2776,7 +2827,8 @@ DEV void chan_advance_one(const DS& d, u32 ch, u32 tid, u32 lane, u32 w, u32* s_
       d.req[ri] = r;
     }
     wave_add_u32(d.req_q_n, u.q, 1u, req_ok);
-    wave_consumed(d, u.msg, u.q, u.qpos, acked ? 0u : (req_ok ? 4u : 2u), acked || req);
+    link_consumed(d, u.msg, u.q, acked ? 0u : (req_ok ? 4u : 2u), acked || req);
+    if (want_rec) consumed_rec_at(d, u.msg, u.q, u.qpos, acked ? 0u : (req_ok ? 4u : 2u), rec_k);
     wave_release(d, u.msg, acked || (req && !req_ok));
     wave_sub_u32(d.cons_unacked, u.cons, 1u, acked || req);
     manual_done += __popcll(__ballot(acked || req));
@@ -2807,7 +2859,8 @@ DEV void chan_advance_one(const DS& d, u32 ch, u32 tid, u32 lane, u32 w, u32* s_
   if (tid == 0) {
     atomicSub(&d.ch_win[ch], (u32)(newhead - head));
     d.ch_uhead[ch] = newhead;
-    d.ch_dirty[ch] = 0;
+    if (deferred) d.def_list[atomicAdd(&d.tot[TS_NCADEF], 1u)] = ch;   // stays dirty: k_dequeue re-lists it
+    else d.ch_dirty[ch] = 0;
   }
 }
 
@@ -2847,7 +2900,13 @@ __global__ __launch_bounds__(256) void k_dequeue(DS d) {
   __shared__ u32 kidx[REQ_BLK];
   __shared__ u32 rq_cnt, rq_last;
   const u32 q = blockIdx.x, tid = threadIdx.x, lane = lane_id();
-  if (q == 0 && tid == 0) *d.n_dirty = 0;   // fused k_reset_dirty (k_chan_advance consumed the list)
+  if (q == 0 && tid == 0) {   // fused k_reset_dirty (k_chan_advance consumed the list)
+    // channels it deferred (store-record budget) start the next step's list
+    const u32 nd = d.tot[TS_NCADEF];
+    for (u32 k = 0; k < nd; ++k) d.dirty_list[k] = d.def_list[k];
+    *d.n_dirty = nd;
+    d.tot[TS_NCADEF] = 0;
+  }
   // fused k_requeue: requeued deliveries go back in front of their queues' heads before this
   // step's dispatch, in queue-offset order.  Every block takes the ticket (req_n only
   // changes in the compaction, which runs after every block has read it); the last one

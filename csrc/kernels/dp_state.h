@@ -47,7 +47,8 @@ enum : u32 {
   TS_TTL_BUDGET = 64,                   // durable TTL-skip records reserved this step (k_dequeue)
   TS_NRACK = 65,                        // link acks received this step (k_import_route -> link_ack_one)
   TS_PK_TICKET = 66,                    // k_pack_scan finished-tile ticket (last tile: prefixes)
-  TS_POST_TICKET = 67                   // k_post finished-block ticket (last block: final_step)
+  TS_POST_TICKET = 67,                  // k_post finished-block ticket (last block: final_step)
+  TS_NCADEF = 68                        // channels k_chan_advance deferred (store-record budget)
 };
 
 // remote-consumer link ack (X3): the connection side consumed message `xid` (owner's
@@ -195,6 +196,7 @@ struct DS {
   u32* ch_dirty;
   u32* dirty_list;
   u32* n_dirty;
+  u32* def_list;            // [nch] channels left dirty by k_chan_advance (record budget hit)
   USlot* uwin;              // [chslots][ucap]
 
   // ---------------- consumers

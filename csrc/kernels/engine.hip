@@ -108,6 +108,13 @@ class Engine {
     }
     d_.pair_max = (u32)get("pair_max", d_.cmd_max * 4);
     d_.deliv_max = (u32)get("deliv_max", 65536);
+    if (d_.persist) {
+      // a step's consumed-store records: deliveries (<= deliv_max), the durable TTL skip
+      // (<= persist_max / 4) and k_chan_advance's settles, budgeted to what is left and
+      // carried to the next step past it -- so the record buffer can never overflow
+      const u64 need = 2ull * d_.deliv_max + 4096;
+      if (d_.persist_max < need) d_.persist_max = (u32)std::min<u64>(need, 1u << 30);
+    }
     // remote-consumer links (X2/X3) on the native exchange: a peer's link deliveries (at
     // most its deliv_max per step) arrive with its publishes and are imported with them
     links_ = d_.world > 1 && get("native_xchg", 0) != 0 && get("links", 0) != 0;
@@ -361,6 +368,7 @@ class Engine {
     d_.ch_dirty = (u32*)dev("ch_dirty", 4ull * nch);
     d_.dirty_list = (u32*)dev("dirty_list", 4ull * nch);
     d_.n_dirty = (u32*)dev("n_dirty", 4);
+    d_.def_list = (u32*)dev("def_list", 4ull * nch);
     d_.uwin = (USlot*)dev("uwin", sizeof(USlot) * (u64)nch * ucap);
 
     d_.cons_q = (u32*)dev("cons_q", 4ull * d_.cons_max);
@@ -931,7 +939,10 @@ class Engine {
       rccl_.reset(new cmqx::RcclXchg(arg, members, (int)d_.my_rank, timeout_ms));
     } else if (kind == "shm") {
       // a mailbox holds one rank's sends to every peer: records + payload
-      const size_t box = 64ull * d_.xfer_desc_max + d_.xfer_bytes + 16ull * (WORLD_MAX + 4) * 16;
+      // (+ with remote-consumer links: link delivery records, their payload and link acks,
+      // as the receive side's import sizing already allows)
+      size_t box = 64ull * d_.xfer_desc_max + d_.xfer_bytes + 16ull * (WORLD_MAX + 4) * 16;
+      if (links_) box += 64ull * d_.deliv_max + d_.egress_cap + 16ull * d_.world * d_.lk_cap;
       shm_.reset(new cmqx::ShmXchg(arg, members, (int)d_.my_rank, box, timeout_ms));
     } else {
       throw std::runtime_error("xchg_setup: kind must be rccl or shm");

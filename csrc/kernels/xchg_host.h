@@ -111,7 +111,25 @@ class ShmXchg {
       if ((spin & 63) == 0 &&
           std::chrono::duration_cast<std::chrono::milliseconds>(std::chrono::steady_clock::now() - t0).count() >
               timeout_ms_)
-        return -2;
+        return withdraw(g);
+    }
+  }
+
+  // Timed out: take this rank's arrival back, so the generation cannot complete without
+  // it and every member reports the same outcome (all pass, or all time out and drop the
+  // step's exchange together).  If the last member arrived meanwhile, the generation did
+  // complete and this rank passes too.
+  int withdraw(uint32_t g) {
+    uint32_t a = ctl_->arrive.load(std::memory_order_acquire);
+    while (true) {
+      if (ctl_->gen.load(std::memory_order_acquire) != g) return 0;
+      if (a == 0) {   // the completing member reset the count: its gen store follows
+        sched_yield();
+        a = ctl_->arrive.load(std::memory_order_acquire);
+        continue;
+      }
+      if (ctl_->arrive.compare_exchange_weak(a, a - 1, std::memory_order_acq_rel, std::memory_order_acquire))
+        return ctl_->gen.load(std::memory_order_acquire) != g ? 0 : -2;
     }
   }
 

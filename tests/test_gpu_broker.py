@@ -609,3 +609,56 @@ def test_purge_of_more_durable_messages_than_persist_records_per_step(gpu, io, t
     finally:
         b2.stop()
         st2.close()
+
+
+@pytest.mark.gpu
+def test_manual_ack_durable_drain_past_record_budget(gpu, tmp_path):
+    """one multiple Basic.Ack settling more durable persistent deliveries than a
+    step's store-record budget (k_chan_advance's share of persist_max).  The device keeps
+    the settles past the budget as slot marks and resolves them in the following steps,
+    so the broker keeps running and every acked message leaves the store."""
+    import time
+    from chanamq_amd.broker import load
+    from chanamq_amd.engine.dataplane import GpuDataPlane
+    from chanamq_amd.server.gpu_broker import GpuBroker
+    core = load()
+    st = core.Store()
+    st.open(str(tmp_path / "store"), True)
+    cfg = dict(GPU_CFG, ucap=4096, deliv_max=256, persist_max=1024)
+    plane = GpuDataPlane(default_queue_capacity=1 << 14, persist=1, persist_bytes=16 << 20, restore_max=1024,
+                         restore_bytes=8 << 20, **cfg)
+    pm = plane.info["persist_max"]
+    budget = pm - 256 - (pm >> 2) - 64
+    assert pm >= 2 * 256 + 4096 and budget < 4096     # one 4096-slot settle exceeds it
+    b = GpuBroker(plane, idle_step_ms=1.0, ingress_bytes=8 << 20, store=st).start()
+    try:
+        p = conn(b)
+        ch = p.channel()
+        ch.queue_declare("drain.dur", durable=True)
+        ch.confirm_select()
+        n = 6000
+        for i in range(n):
+            ch.basic_publish("", "drain.dur", b"d%d" % i, {"delivery_mode": 2})
+            if i % 1000 == 999:
+                assert ch.wait_for_confirms(timeout=60)
+        assert ch.wait_for_confirms(timeout=60)
+        assert st.row_count("msgs") == n
+        c = conn(b)
+        cc = c.channel()
+        cc.basic_consume("drain.dur", "drainer", no_ack=False)
+        first = cc.consume_n(4096, timeout=60)
+        assert len(first) == 4096
+        cc.basic_ack(first[-1].delivery_tag, multiple=True)
+        rest = cc.consume_n(n - 4096, timeout=60)
+        assert [d.body for d in first + rest] == [b"d%d" % i for i in range(n)]
+        cc.basic_ack(rest[-1].delivery_tag, multiple=True)
+        deadline = time.time() + 30
+        while st.row_count("msgs") and time.time() < deadline:
+            c.process(0.1)
+        assert st.row_count("msgs") == 0
+        assert b._running
+        p.close()
+        c.close()
+    finally:
+        b.stop()
+        st.close()
