@@ -119,6 +119,40 @@ def build_workload(dp, rank, producers, queues, body, chunk, blocks, cons_base, 
     return pool, segs, offs, block_len, msgs_per_step, len(probe), extra
 
 
+def setup_native_exchange(args, cfg, GpuDataPlane, dist, backend, local, rank, world):
+    """The sharded plane on the engine's native exchange, as the sharded server builds it
+    (server/sharded.py): rank 0 draws the RCCL unique id and names the shared-memory
+    segments, every rank receives them over the launcher's process group.  Returns None on
+    every rank when any rank could not set it up (all ranks then use the torch exchange)."""
+    import uuid
+
+    import torch
+    dp, err = None, None
+    kind = "rccl" if backend == "nccl" else "shm"
+    try:
+        dp = GpuDataPlane(device=local, worker=rank, world=world, rank=rank, native_xchg=1, **cfg)
+        names = [None]
+        if rank == 0:
+            tag = f"cmq-bench-{os.getpid()}-{uuid.uuid4().hex[:10]}"
+            names = [{"uid": dp.xchg_unique_id() if kind == "rccl" else None, "shm": tag}]
+        dist.broadcast_object_list(names, src=0)
+        nm = names[0]
+        if kind == "rccl":
+            dp.xchg_setup("rccl", nm["uid"], list(range(world)), args.xchg_timeout_ms, counts_shm=nm["shm"] + "-c")
+        else:
+            dp.xchg_setup("shm", nm["shm"], list(range(world)), args.xchg_timeout_ms)
+    except Exception as e:   # noqa: BLE001 - reported, then agreed on below
+        err = e
+    bad = torch.tensor([1.0 if err is not None else 0.0], device="cuda" if backend == "nccl" else "cpu")
+    dist.all_reduce(bad, op=dist.ReduceOp.MAX)
+    if bad.item() > 0:
+        if err is not None:
+            print(f"rank {rank}: native exchange setup failed: {err!r}", file=sys.stderr, flush=True)
+        del dp
+        return None
+    return dp
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -148,6 +182,12 @@ def main():
                          "the collective overlaps the next step); 0 = synchronous")
     ap.add_argument("--mode", choices=["sharded", "independent"], default="sharded",
                     help="N>1: one sharded broker (cross-GPU routing over RCCL) or N unconnected shards")
+    ap.add_argument("--xchg", choices=["native", "torch"], default="native",
+                    help="N>1 sharded: the engine's own exchange -- grouped RCCL send/recv on its exchange "
+                         "stream, counts through host shared memory (the code the sharded server runs; "
+                         "CHANAMQ_BENCH_BACKEND=gloo: the shared-memory backend) -- or torch.distributed "
+                         "all_to_all_single (parallel/exchange.py)")
+    ap.add_argument("--xchg-timeout-ms", type=int, default=30000)
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -192,11 +232,17 @@ def main():
                log_bytes=16 << 30, ring_pool=Q * qcap + qtot + 1024, tb_max=max(64, qtot) if not fan else 64,
                fan_max=max(1 << 20, qtot * 2), carry_cap=256 << 10, graph=0 if args.no_graph else 1,
                copy_engine={"blit": 0, "nocu": 1, "kernel": 2, "sdma": 3}[args.copy_engine], copy_wgs=args.copy_wgs, sdma_engine=args.sdma_engine)
-    if shards > 1:
+    native = shards > 1 and args.xchg == "native"
+    if native:
+        dp = setup_native_exchange(args, cfg, GpuDataPlane, dist, backend, local, rank, world)
+        if dp is None:   # refused on some rank (e.g. librccl): every rank falls back together
+            native = False
+            args.xchg = "torch (native exchange setup failed)"
+    if shards > 1 and not native:
         from chanamq_amd.parallel.exchange import Exchanger
         dp = GpuDataPlane(device=local, worker=rank, world=world, rank=rank, exchanger=Exchanger(),
                           exchange_lag=args.exchange_lag, **cfg)
-    else:
+    elif shards == 1:
         dp = GpuDataPlane(device=local, worker=rank, **cfg)
     pool, segs, offs, blens, mps, msg_bytes, extra = build_workload(dp, rank, P, Q, args.body, args.chunk,
                                                                     args.blocks, cons_base=P, shards=shards,
@@ -205,6 +251,7 @@ def main():
     flow = {"paused": False, "paused_steps": 0, "requeued": 0}
     base = pool.ctypes.data
     step_i = 0
+    submit = dp.submit_lockstep if native else dp.submit_raw
 
     sub_t = {}      # step index -> host time its ingress was handed to the GPU (submit)
     lat_w = []      # (publish->deliver seconds, deliveries) of the timed steps
@@ -255,9 +302,9 @@ def main():
                     sg = cs
                 else:
                     sg = np.concatenate([segs[b], cs])
-                pending.append((dp.submit_raw(sg, base + offs[b], blens[b]), step_i))
+                pending.append((submit(sg, base + offs[b], blens[b]), step_i))
             else:
-                pending.append((dp.submit_raw(segs[b], base + offs[b], blens[b]), step_i))
+                pending.append((submit(segs[b], base + offs[b], blens[b]), step_i))
             step_i += 1
             if len(pending) > 1:
                 t, s = pending.pop(0)
@@ -280,7 +327,7 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     dp.eng.sync()
-    if shards > 1:
+    if shards > 1 and not native:
         dp.exchanger.bytes_sent = 0
     dp.eng.host_times(True)
     t0 = time.perf_counter()
@@ -346,7 +393,10 @@ def main():
                 "global_batch": int(round(mps * world)),
                 "seq_len": args.body,
                 "parallelism": (f"queue-sharded x{world}: one broker, cross-GPU routing by "
-                                + ("RCCL all-to-all" if backend == "nccl" else f"{backend} all-to-all staged through the host")
+                                + (("engine-native grouped RCCL send/recv over xGMI, counts via host shared memory"
+                                    if backend == "nccl" else "engine-native shared-memory exchange (host-staged)")
+                                   if native else
+                                   "RCCL all-to-all" if backend == "nccl" else f"{backend} all-to-all staged through the host")
                                 + (" (pipelined, +1 step for cross-GPU messages)" if args.exchange_lag else "")
                                 if shards > 1 else
                                 (f"x{world} independent broker shards" if world > 1 else "single GPU")),
@@ -365,7 +415,8 @@ def main():
             "host_us_per_step": {k: round(v * 1e6 / args.steps, 1) for k, v in dp.eng.host_times(False).items()},
             "storm": ({"requeued_msgs": flow["requeued"], "flow_paused_steps": flow["paused_steps"]}
                       if storm else None),
-            "cross_gpu_bytes_per_s": (dp.exchanger.bytes_sent * world / t) if shards > 1 else 0.0,
+            "cross_gpu_bytes_per_s": (dp.exchanger.bytes_sent * world / t) if shards > 1 and not native else None,
+            "exchange": args.xchg if shards > 1 else None,
             "post_soak_s": args.soak_s,
         }
         print(json.dumps(out), flush=True)

@@ -638,11 +638,13 @@ class GpuDataPlane(ControlState):
         t = self.submit_raw(segs, payload_ptr, payload_len, now_ms)
         return self.finish(t, collect=collect)
 
-    def xchg_setup(self, kind, arg, members, timeout_ms=10000, failover=False):
+    def xchg_setup(self, kind, arg, members, timeout_ms=10000, failover=False, counts_shm=""):
         """Native exchange backend over the live ranks ``members``: "rccl" (arg = the
         128-byte unique id from ``xchg_unique_id()``) or "shm" (arg = a shared-memory name
-        common to the group, for ranks sharing one host)."""
-        self.eng.xchg_setup(kind, arg, sorted(int(m) for m in members), int(timeout_ms), bool(failover))
+        common to the group, for ranks sharing one host).  ``counts_shm`` (rccl): move the
+        per-step counts through host shared memory (ranks of one node), the bulk on RCCL."""
+        self.eng.xchg_setup(kind, arg, sorted(int(m) for m in members), int(timeout_ms), bool(failover),
+                            counts_shm)
 
     def xchg_unique_id(self):
         return self.mod.Engine.xchg_unique_id()
@@ -751,6 +753,29 @@ class GpuDataPlane(ControlState):
                     self.set_import(recv)
                 else:
                     self.submit_b(recv)
+        return (p, len(segs), t0)
+
+    def submit_lockstep(self, segs, payload_ptr, payload_len, now_ms=None):
+        """One lockstep step of a sharded plane on the engine's native exchange (RCCL over
+        xGMI, or host shared memory), in the order the native front end's sharded stepper
+        runs it (frontend.cpp ``stepper_sharded``): H2D(t) and phase A(t) are queued, then
+        the previous step's exchange runs on the exchange stream while A(t) executes, then
+        phase B(t) -- which imports that exchange -- is queued behind it.  The host only
+        blocks in the count exchange (``counts_shm``: a shared-memory barrier)."""
+        if not (self.world > 1 and self.native_xchg):
+            raise RuntimeError("submit_lockstep: needs a sharded plane built with native_xchg=1")
+        now = int(time.time() * 1000) if now_ms is None else int(now_ms)
+        t0 = time.perf_counter()
+        p = self.eng.submit(segs, int(payload_ptr), int(payload_len), now, self.step_no, now, self.worker)
+        self.step_no += 1
+        q = self._xprev
+        if q is not None:
+            rc, _ = self.eng.exchange(q, 0)
+            if rc != 0:
+                self.eng.drop_exchange(q)
+                raise RuntimeError(f"rank {self.rank}: native exchange failed (rc {rc}: a peer did not answer)")
+        self.eng.launch_b(p)
+        self._xprev = p
         return (p, len(segs), t0)
 
     def _exchange_parity(self, q):

@@ -3220,9 +3220,18 @@ __global__ void k_dv_write(DS d) {
     lat = (u32)d.in->step - m.pub_step;
     // the channel's last delivery this step: the window needs a k_chan_advance pass
     bool last = i + 1 == n || (k + 1 == rn.cnt && (lo + 1 >= R || d.runs[d.run_order[lo + 1]].ch != ch));
-    if (last && atomicExch(&d.ch_dirty[ch], 1u) == 0) {
-      u32 kk = atomicAdd(d.n_dirty, 1u);
-      d.dirty_list[kk] = ch;
+    if (last) {
+      // auto-ack channel with nothing pending (no manual delivery awaiting a settle, no
+      // deferred marks): every slot up to this tag is done, so the window head moves here
+      // and k_chan_advance has nothing to walk for it
+      if (rn.noack && d.ch_unacked[ch] == 0 && d.ch_dirty[ch] == 0) {
+        const u64 head = d.ch_uhead[ch];
+        atomicSub(&d.ch_win[ch], (u32)(tag + 1 - head));
+        d.ch_uhead[ch] = tag + 1;
+      } else if (atomicExch(&d.ch_dirty[ch], 1u) == 0) {
+        u32 kk = atomicAdd(d.n_dirty, 1u);
+        d.dirty_list[kk] = ch;
+      }
     }
   } else if (i < d.deliv_max) {
     d.dv_size[i] = 0;

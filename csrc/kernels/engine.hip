@@ -925,18 +925,24 @@ class Engine {
   // kind "rccl": arg = 128-byte RCCL unique id; "shm": arg = shared-memory name.
   // members: the live logical ranks (sorted); timeout_ms bounds every host wait;
   // failover: the host also waits (bounded) for the bulk transfer before phase B
+  // counts_shm (rccl only): a shared-memory name common to the group -- the per-step count
+  // exchange then runs through host shared memory (a spin barrier, ~µs) instead of an
+  // RCCL round trip with two PCIe copies; the bulk records stay on RCCL over xGMI.  All
+  // ranks of one node (the bench, the sharded server on one host) can use it.
   void xchg_setup(const std::string& kind, const std::string& arg, std::vector<int> members, int timeout_ms,
-                  bool failover) {
+                  bool failover, const std::string& counts_shm) {
     if (!native_x_) throw std::runtime_error("xchg_setup: engine built without native_xchg");
     for (int& m : members)
       if (m < 0 || m >= (int)d_.world) throw std::runtime_error("xchg_setup: bad member");
     std::sort(members.begin(), members.end());
     rccl_.reset();
     shm_.reset();
+    cshm_.reset();
     xtimeout_ms_ = timeout_ms;
     xfailover_ = failover;
     if (kind == "rccl") {
       rccl_.reset(new cmqx::RcclXchg(arg, members, (int)d_.my_rank, timeout_ms));
+      if (!counts_shm.empty()) cshm_.reset(new cmqx::ShmXchg(counts_shm, members, (int)d_.my_rank, 4096, timeout_ms));
     } else if (kind == "shm") {
       // a mailbox holds one rank's sends to every peer: records + payload
       // (+ with remote-consumer links: link delivery records, their payload and link acks,
@@ -1005,7 +1011,9 @@ class Engine {
     int rc;
     {
       Range rc_("chanamq.X1.counts");
-      rc = rccl_ ? rccl_->counts(hs.data(), hr.data(), cmqx::XH_WORDS) : shm_->counts(hs.data(), hr.data());
+      HostTimer hc(&ht_[7]);   // the host's blocking part: waiting for every peer's counts
+      rc = cshm_ ? cshm_->counts(hs.data(), hr.data())
+                 : rccl_ ? rccl_->counts(hs.data(), hr.data(), cmqx::XH_WORDS) : shm_->counts(hs.data(), hr.data());
     }
     if (rc) return rc;
     u32 orf = 0;
@@ -1373,10 +1381,10 @@ class Engine {
 
   // seconds spent in each host phase since the last reset
   py::dict host_times(bool reset) {
-    static const char* names[7] = {"submit", "submit_sdma_wait", "submit_graph_launch", "wait_results",
-                                   "egress_copy", "egress_wait", "exchange"};
+    static const char* names[8] = {"submit", "submit_sdma_wait", "submit_graph_launch", "wait_results",
+                                   "egress_copy", "egress_wait", "exchange", "exchange_counts"};
     py::dict o;
-    for (int i = 0; i < 7; ++i) { o[names[i]] = ht_[i]; if (reset) ht_[i] = 0; }
+    for (int i = 0; i < 8; ++i) { o[names[i]] = ht_[i]; if (reset) ht_[i] = 0; }
     return o;
   }
 
@@ -1618,6 +1626,7 @@ class Engine {
   bool b_due_[2] = {false, false};   // phase A launched, phase B not yet (native exchange)
   std::unique_ptr<cmqx::RcclXchg> rccl_;
   std::unique_ptr<cmqx::ShmXchg> shm_;
+  std::unique_ptr<cmqx::ShmXchg> cshm_;   // rccl + host shared-memory count exchange
   std::vector<int> xmembers_;
   int xtimeout_ms_ = 10000;
   bool xfailover_ = false;
@@ -1726,7 +1735,8 @@ PYBIND11_MODULE(_dataplane, m) {
       .def("sync", &Engine::sync)
       .def("c_api", &Engine::c_api)
       .def("xchg_setup", &Engine::xchg_setup, py::arg("kind"), py::arg("arg"), py::arg("members"),
-           py::arg("timeout_ms") = 10000, py::arg("failover") = false, py::call_guard<py::gil_scoped_release>())
+           py::arg("timeout_ms") = 10000, py::arg("failover") = false, py::arg("counts_shm") = "",
+           py::call_guard<py::gil_scoped_release>())
       .def_static("xchg_unique_id", &Engine::xchg_unique_id)
       .def("exchange", [](Engine& e, int q, u32 flags) {
              u32 orf = 0;
