@@ -25,6 +25,8 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 from chanamq_amd.broker import load  # noqa: E402
 
+SMALL_CONF = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests", "sharded_small.conf")
+
 SPECS = {
     # BASELINE config 2 over TCP: 1 topic exchange, 16 bound queues, 1 KB, auto-ack
     "config2_topic_16q_1KB_auto_ack": dict(producers=16, consumers=16, queues=16, msg_size=1024, auto_ack=True,
@@ -248,7 +250,7 @@ def run_sharded(core, name, spec, world, mode, seconds, rate=0.0, io_threads=2, 
     tmp = tempfile.mkdtemp(prefix="cmq-sharded-")
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     env = dict(os.environ, PYTHONPATH=root)
-    ln = Launcher(world, ["-m", "chanamq_amd.server.sharded", "--plane", "gpu", "--port", "0", "--backend", "gloo",
+    ln = Launcher(world, ["-m", "chanamq_amd.server.sharded", "--config", SMALL_CONF, "--plane", "gpu", "--port", "0", "--backend", "gloo",
                           "--info-dir", tmp, "--io-threads", str(io_threads), "--idle-step-ms", "0.5"],
                   env=env).start()
     try:

@@ -369,6 +369,18 @@ class ControlState:
             x.bindings.append((q.slot, kb))
             self.routing_changed()
 
+    def route_host(self, x, key):
+        """Queue slots a publish with routing key ``key`` (bytes) reaches through exchange
+        ``x``, from the replicated binding table (what the device routes; headers routes as
+        topic).  Host-side routing for host-assembled large publishes."""
+        from ..models.matcher import topic_match
+        if x.type == "fanout":
+            return sorted({s for s, _ in x.bindings})
+        if x.type == "direct":
+            return sorted({s for s, k in x.bindings if k == key})
+        ks = key.decode(errors="replace")
+        return sorted({s for s, k in x.bindings if topic_match(k.decode(errors="replace"), ks, self.hash_wildcard)})
+
     def unbind(self, vhost, queue, exchange, key):
         x = self.exchanges.get((vhost, exchange))
         q = self.queues.get((vhost, queue))

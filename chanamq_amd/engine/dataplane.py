@@ -16,7 +16,7 @@ from .. import ops
 from ..protocol import constants as C
 from .control import ControlError, ControlState
 from .layout import (CONN_OUT, CONSUMED_REC, RING_MOVE, CTRL_REC, CTRL_TXBUF, INVALID, MF_HAS_TS, MF_HOSTPUB, MF_PERSIST,
-                     MF_REDELIVERED, MF_RESTORE,
+                     MF_ONEQ, MF_REDELIVERED, MF_RESTORE,
                      PERSIST_HDR, RDESC, SEG_IN, SEG_OUT, SS_CTRL, US_ACKED, US_PENDING, US_REQUEUE, USLOT,
                      chan_hash, direct_key, exch_hash, fnv1a64, topic_pattern_row, topic_word_offsets)
 
@@ -481,9 +481,9 @@ class GpuDataPlane(ControlState):
         channel's confirms (the next step's Basic.Ack / Nack covers it).  Between steps.
         Returns the number of messages stored (0: unroutable or dropped)."""
         now = int(time.time() * 1000) if now_ms is None else int(now_ms)
-        if self.world > 1:
-            raise ControlError(C.NOT_IMPLEMENTED, "messages larger than the connection carry are not "
-                                                  "supported on sharded planes", 60, 40)
+        # sharded plane (at a sync point, server/gpu_broker.py _apply_big): stored in this
+        # rank's queues only -- imported records are never forwarded; the owners of the
+        # other queues enqueue their copies themselves (publish_to_queues)
         desc = np.zeros(1, RDESC)
         d = desc[0]
         d["pay_off"], d["body_len"], d["props_len"], d["exch"] = 0, len(body), len(props), exch_slot
@@ -495,6 +495,26 @@ class GpuDataPlane(ControlState):
         rec = bytes(ex) + bytes(rk) + bytes(props) + bytes(body)
         pay = np.frombuffer(rec + b"\0" * ((-len(rec)) % 16), np.uint8)
         return self.eng.restore(desc.view(np.uint8), pay, now)
+
+    def publish_to_queues(self, slots, ex, rk, props, body, flags, expire_ms=0, ts_ms=0, now_ms=None):
+        """A host-assembled publish into exactly the given local queues (a sharded owner's
+        part of a large publish routed on another rank): one MF_ONEQ record per queue,
+        each stored with a new message id.  Between steps / at a sync point."""
+        now = int(time.time() * 1000) if now_ms is None else int(now_ms)
+        if not slots:
+            return 0
+        desc = np.zeros(len(slots), RDESC)
+        rec = bytes(ex) + bytes(rk) + bytes(props) + bytes(body)
+        pad = rec + b"\0" * ((-len(rec)) % 16)
+        pay = bytearray()
+        for i, q in enumerate(slots):
+            d = desc[i]
+            d["pay_off"], d["body_len"], d["props_len"], d["exch"] = len(pay), len(body), len(props), -1
+            d["flags"] = MF_ONEQ | (flags & (MF_PERSIST | MF_HAS_TS))
+            d["ex_len"], d["rk_len"] = len(ex), len(rk)
+            d["expire_ms"], d["ts_ms"], d["xid"], d["tq"] = expire_ms, ts_ms, 0, int(q)
+            pay += pad
+        return self.eng.restore(desc.view(np.uint8), np.frombuffer(bytes(pay), np.uint8), now)
 
     # ---- cold bodies to host memory (built with spill_bytes > 0)
     def spill(self, frac=0.5, hot=1024):

@@ -45,12 +45,13 @@ _STORED_METHODS = _REPLICATED_METHODS
 
 class _Conn:
     __slots__ = ("sock", "id", "state", "inbuf", "out", "frame_max", "heartbeat", "last_rx", "last_tx",
-                 "closing_channels", "last_queue", "peer", "user", "cap_blocked", "big")
+                 "closing_channels", "last_queue", "peer", "user", "cap_blocked", "big", "big_rest")
 
     def __init__(self, sock, cid, peer):
         self.sock, self.id, self.peer = sock, cid, peer
-        self.state = "header"   # header -> start -> tune -> open (<-> bigpub) -> closing -> closed
+        self.state = "header"   # header -> start -> tune -> open (<-> bigpub [-> bigwait]) -> closing -> closed
         self.big = None         # a publish larger than the device carry being assembled on the host
+        self.big_rest = None    # sharded: bytes after such a publish, held until it is enqueued
         self.inbuf = bytearray()
         self.out = bytearray()
         self.frame_max = 131072
@@ -236,6 +237,7 @@ class GpuBroker:
                 self.node.attach_frontend(self.fe)
                 if self.plane.info.get("links"):
                     self.node.use_device_links(self._alloc_link_slot, self._link_free.append)
+                self.node.log.handlers["big_publish"] = self._apply_big
                 if self.persistence is not None:
                     self.node.log.on_applied = self._persist_replicated
             self._running = True
@@ -675,6 +677,9 @@ class GpuBroker:
         Returns data-plane leftovers."""
         if c.state == "bigpub":
             return self._big_feed(c, data)
+        if c.state == "bigwait":   # held until the sharded large publish is enqueued
+            c.big_rest += data
+            return b""
         if c.state in ("header", "start", "tune"):
             c.inbuf += data
             try:
@@ -1023,6 +1028,9 @@ class GpuBroker:
             err = (C.NOT_FOUND, f"no exchange '{m.exchange}' in vhost '{vh}'")
         elif getattr(p.channel(c.id, ch), "tx", False):
             err = (C.NOT_IMPLEMENTED, "a message larger than the connection buffer inside a transaction")
+        elif self.node is not None and self.fe is None:
+            err = (C.NOT_IMPLEMENTED, "messages larger than the connection carry need the pipelined front end "
+                                      "on a sharded node")
         elif body_size > p.max_host_message():
             err = (C.CONTENT_TOO_LARGE, f"message body of {body_size} bytes exceeds the broker's "
                                         f"{p.max_host_message()}-byte limit")
@@ -1081,13 +1089,16 @@ class GpuBroker:
             del buf[:pos]
             return b""
         rest = bytes(b["other"]) + bytes(buf[pos:])
-        self._big_finish(c)
-        return rest
+        return self._big_finish(c, rest)
 
-    def _big_finish(self, c):
+    def _big_finish(self, c, rest=b""):
+        """The body is complete: enqueue it.  Returns the bytes to hand back to the data
+        plane now (a sharded node holds them until the message is in its queues)."""
         b, c.big = c.big, None
         c.state = "open"
         m, ch, props = b["m"], b["ch"], b["props"]
+        if self.node is not None and b["err"] is None:
+            return self._big_sharded(c, b, rest)
         with self.lock:
             if b["err"] is not None:
                 code, text = b["err"]
@@ -1112,6 +1123,89 @@ class GpuBroker:
                                             props, bytes(b["body"]), c.frame_max)
             self._unpause(c.id)
         self._flush(c)
+        return rest
+
+    @staticmethod
+    def _big_meta(props):
+        now = int(time.time() * 1000)
+        flags = MF_PERSIST if props.get("delivery_mode") == 2 else 0
+        ts = props.get("timestamp")
+        ts_ms = int(ts) * 1000 if ts is not None else 0
+        if ts is not None:
+            flags |= MF_HAS_TS
+        exp = props.get("expiration")
+        exp = exp.decode() if isinstance(exp, (bytes, bytearray)) else exp
+        expire_ms = now + int(exp) if isinstance(exp, str) and exp.isdigit() else 0
+        return now, flags, expire_ms, ts_ms
+
+    def _big_sharded(self, c, b, rest):
+        """Sharded node: the queues the publish routes to may live on any rank.  Routed on
+        the host over the replicated bindings, the message goes out as a control-log op
+        whose body travels only to the owning ranks (ControlLog blob); at the sync every
+        owner enqueues it into its queues and this rank counts it for the channel's
+        confirms.  The connection stays off the data plane until then, so nothing it
+        publishes later is confirmed or delivered ahead of it (FrameParser.scala:67: no
+        size limit on any node)."""
+        p, m, ch = self.plane, b["m"], b["ch"]
+        x = b["x"]
+        targets = {}
+        for slot in p.route_host(x, m.routing_key.encode()):
+            q = p.queue_by_slot.get(slot)
+            if q is not None:
+                targets.setdefault(int(q.owner), []).append(int(slot))
+        now, flags, expire_ms, ts_ms = self._big_meta(b["props"])
+        payload = m.exchange.encode() + m.routing_key.encode() + bytes(b["props_raw"]) + bytes(b["body"])
+        meta = dict(origin=p.rank, conn=c.id, ch=ch, exch=x.slot, ex_len=len(m.exchange.encode()),
+                    rk_len=len(m.routing_key.encode()), props_len=len(b["props_raw"]), body_len=len(b["body"]),
+                    flags=flags, expire_ms=expire_ms, ts_ms=ts_ms, now=now,
+                    targets={str(r): v for r, v in targets.items()})
+        owners = sorted(set(targets) | {p.rank})
+        with self.lock:
+            seq = self.node.submit("big_publish", meta, blob=payload, blob_to=owners)
+        self.stats["big_publishes"] = self.stats.get("big_publishes", 0) + 1
+        c.state = "bigwait"
+        c.big_rest = bytearray(rest)
+        props, body = b["props"], bytes(b["body"])
+
+        def reply(res, c=c):
+            # the message is in its queues on every owner (this sync applied the op)
+            if not targets and m.mandatory:
+                c.out += render_command(ch, Method("basic.return", reply_code=C.NO_ROUTE,
+                                                   reply_text=C.REPLY_TEXT.get(C.NO_ROUTE, "NO_ROUTE"),
+                                                   exchange=m.exchange, routing_key=m.routing_key),
+                                        props, body, c.frame_max)
+            return None
+        self._deferred[seq] = (c.id, ch, reply, m)
+        return b""
+
+    def _big_resume(self, c):
+        """A sharded large publish was applied (or failed): the connection goes back to the
+        data plane with the bytes that followed the message (_answer unpauses it)."""
+        more = bytes(c.big_rest or b"")
+        c.big_rest = None
+        c.state = "open"
+        self.fe.set_data_mode(c.id, more)
+
+    def _apply_big(self, meta, blob=None):
+        """Replicated ``big_publish`` (every rank, at the sync): the owners enqueue the
+        message into their target queues; the origin's record also counts it for the
+        publisher channel's confirms (and Nacks it if its store fails)."""
+        p = self.plane
+        mine = [int(s) for s in meta["targets"].get(str(p.rank), [])]
+        origin = int(meta["origin"]) == p.rank
+        if not (mine or origin) or blob is None:
+            return 0
+        el, rl, pl = meta["ex_len"], meta["rk_len"], meta["props_len"]
+        ex, rk, props, body = blob[:el], blob[el:el + rl], blob[el + rl:el + rl + pl], blob[el + rl + pl:]
+        n = 0
+        if origin:   # routed by its exchange on this device: local queues + confirm counting
+            n += p.publish_host(int(meta["conn"]), int(meta["ch"]), int(meta["exch"]), ex, rk, props,
+                                body if mine else b"", int(meta["flags"]), int(meta["expire_ms"]),
+                                int(meta["ts_ms"]), int(meta["now"]))
+        else:
+            n += p.publish_to_queues(mine, ex, rk, props, body, int(meta["flags"]), int(meta["expire_ms"]),
+                                     int(meta["ts_ms"]), int(meta["now"]))
+        return n
 
     def _connection_method(self, c, m):
         if m.name == "connection.close":
@@ -1357,6 +1451,8 @@ class GpuBroker:
                 continue
             res = results.get(seq)
             err = error_of(res)
+            if c.state == "bigwait":
+                self._big_resume(c)
             if err:
                 code, text, cls, mid = err
                 if code >= 500:

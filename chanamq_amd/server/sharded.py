@@ -26,20 +26,43 @@ import threading
 import uuid
 
 
+def sharded_plane_config(cfg, args, world, rank, pipeline):
+    """(GpuDataPlane kwargs, GpuBroker kwargs) of one rank from ``chana.mq.gpu.*`` -- the
+    same keys and defaults as the single-GPU launcher (AMQPServer.scala:52-70: every node
+    boots from the same HOCON) -- plus the rank's place in the group.  Command-line flags
+    override their keys.  Every rank keeps store rows (persist) for failover adoption."""
+    plane, broker = cfg.gpu_config()
+    plane.pop("device", None)   # each rank drives its own LOCAL_RANK GPU
+    if args.c_max:
+        plane["c_max"] = args.c_max
+    plane["seg_max"] = min(plane["seg_max"], plane["c_max"])
+    plane.update(world=world, rank=rank, worker=rank, persist=1, native_xchg=int(pipeline), links=int(pipeline))
+    broker.pop("io", None)      # --io decides the front end of a sharded rank
+    if args.idle_step_ms is not None:
+        broker["idle_step_ms"] = args.idle_step_ms
+    if args.io_threads is not None:
+        broker["io_threads"] = args.io_threads
+    return plane, broker
+
+
 def main(argv=None):
     ap = argparse.ArgumentParser(prog="chanamq_amd.server.sharded")
+    ap.add_argument("--config", action="append", default=[],
+                    help="HOCON file over conf/reference.conf (every rank reads the same files)")
+    ap.add_argument("--set", action="append", default=[], metavar="KEY=VALUE")
     ap.add_argument("--plane", choices=["gpu", "golden"], default="gpu")
     ap.add_argument("--io", choices=["pipeline", "native"], default="pipeline",
                     help="gpu plane: pipeline = native front end + native exchange; native = Python lockstep loop")
-    ap.add_argument("--host", default="127.0.0.1")
-    ap.add_argument("--port", type=int, default=5672)
+    ap.add_argument("--host", default=None, help="default chana.mq.amqp.server.interface")
+    ap.add_argument("--port", type=int, default=None, help="default chana.mq.amqp.server.port")
     ap.add_argument("--reuseport", action="store_true")
     ap.add_argument("--info-dir", default="")
-    ap.add_argument("--idle-step-ms", type=float, default=1.0)
-    ap.add_argument("--io-threads", type=int, default=2)
-    ap.add_argument("--c-max", type=int, default=256)
-    ap.add_argument("--store-dir", default="", help="durable store root: rank r keeps <dir>/rank<r>; "
-                                                    "survivors adopt a dead rank's durable queues from it")
+    ap.add_argument("--idle-step-ms", type=float, default=None, help="default chana.mq.gpu.idle-step-ms")
+    ap.add_argument("--io-threads", type=int, default=None, help="default chana.mq.gpu.io-threads")
+    ap.add_argument("--c-max", type=int, default=None, help="default chana.mq.gpu.max-connections")
+    ap.add_argument("--store-dir", default=None, help="durable store root (default chana.mq.store.dir): rank r "
+                                                      "keeps <dir>/rank<r>; survivors adopt a dead rank's durable "
+                                                      "queues from it")
     ap.add_argument("--no-fsync", action="store_true")
     ap.add_argument("--backend", default="", help="default: nccl (RCCL) for --plane gpu, gloo for golden; "
                                                   "gloo + gpu rehearses several ranks on one GPU")
@@ -50,6 +73,17 @@ def main(argv=None):
     ap.add_argument("--tls-cert", default="")
     ap.add_argument("--tls-key", default="")
     args = ap.parse_args(argv)
+    from ..utils.config import Config
+    cfg = Config.load(args.config, dict(kv.split("=", 1) for kv in args.set))
+    bc = cfg.broker_config()
+    if args.host is None:
+        args.host = bc["host"]
+    if args.port is None:
+        args.port = bc["port"]
+    if args.store_dir is None:
+        args.store_dir = bc["data_dir"]
+    if args.no_fsync is False and not bc["fsync"]:
+        args.no_fsync = True
 
     from ..parallel.launch import ENV_STORE, join
     backend = args.backend or ("nccl" if args.plane == "gpu" else "gloo")
@@ -63,18 +97,16 @@ def main(argv=None):
     from ..parallel.comm import Comm
     from ..parallel.membership import Membership
     from ..parallel.node import ShardedNode
-    plane_kw = dict(world=world, rank=rank, c_max=args.c_max, chpc=8, q_max=1024, default_queue_capacity=1 << 14,
-                    ring_pool=1 << 24)
+    gpu_kw, broker_kw = sharded_plane_config(cfg, args, world, rank, pipeline)
     if args.plane == "gpu":
         import torch
         from ..engine.dataplane import GpuDataPlane
-        plane = GpuDataPlane(device=torch.cuda.current_device(), worker=rank, cons_max=4096, seg_max=args.c_max,
-                             cmd_max=1 << 16, deliv_max=1 << 16, msg_max=1 << 20, ingress_cap=32 << 20,
-                             egress_cap=64 << 20, log_bytes=2 << 30, tb_max=1024, persist=1,
-                             native_xchg=int(pipeline), links=int(pipeline), **plane_kw)   # persist: store rows
-    else:
+        plane = GpuDataPlane(device=torch.cuda.current_device(), **gpu_kw)
+    else:   # the CPU model (tests): small tables whatever the GPU sizing says
         from ..engine.golden import GoldenDataPlane
-        plane = GoldenDataPlane(persist=bool(args.store_dir), **plane_kw)
+        plane = GoldenDataPlane(persist=bool(args.store_dir), world=world, rank=rank,
+                                c_max=args.c_max or 256, chpc=8, q_max=1024, default_queue_capacity=1 << 14,
+                                ring_pool=1 << 24)
     comm = Comm(store=store, backend="gloo" if pipeline else backend, timeout_s=60, wait_s=20)
     node = ShardedNode(plane, comm, membership=Membership(store, rank, world, timeout_s=args.hb_timeout_s))
     if pipeline:
@@ -111,9 +143,10 @@ def main(argv=None):
     from .gpu_broker import GpuBroker
     # --port 0: every rank takes an ephemeral port (reported through --info-dir)
     port = args.port if (args.reuseport or args.port == 0) else args.port + rank
-    broker = GpuBroker(plane, host=args.host, port=port, idle_step_ms=args.idle_step_ms, node=node,
-                       reuseport=args.reuseport, ingress_bytes=32 << 20, store=st,
-                       io="pipeline" if pipeline else "native", io_threads=args.io_threads).start()
+    broker = GpuBroker(plane, host=args.host, port=port, node=node, reuseport=args.reuseport,
+                       ingress_bytes=min(32 << 20, plane.info["ingress_cap"]) if args.plane == "gpu" else 32 << 20,
+                       store=st, io="pipeline" if pipeline else "native", heartbeat=bc["heartbeat"],
+                       frame_max=bc["frame_max"], channel_max=bc["channel_max"] or 2047, **broker_kw).start()
     node.persistence = broker.persistence if st is not None else None
     tls = None
     if args.tls_port >= 0:   # AMQPS per rank: the TLS terminator in front of this rank's front end
@@ -132,6 +165,9 @@ def main(argv=None):
             json.dump({"rank": rank, "world": world, "port": broker.port,
                        "tls_port": tls.port if tls is not None else None, "io": broker.io,
                        "stats": dict(broker.stats), "failovers": len(node.failovers),
+                       "plane": {k: plane.info[k] for k in ("log_bytes", "msg_max", "c_max", "q_max", "ingress_cap",
+                                                            "egress_cap", "spill_bytes")
+                                 if hasattr(plane, "info") and k in plane.info},
                        "front_end": {k: v for k, v in fes.items() if k != "lat_hist"}}, f)
         os.replace(path + ".tmp", path)
     write_info()

@@ -20,6 +20,17 @@ def _auto_wm(v, auto):
     return auto if v < 0 else v
 
 
+def _auto_spill(v):
+    """spill-bytes: -1 = automatic (1/8 of physical memory, <= 64 GiB, whole 4 MiB log blocks)."""
+    if v >= 0:
+        return v
+    try:
+        total = os.sysconf("SC_PAGE_SIZE") * os.sysconf("SC_PHYS_PAGES")
+    except (ValueError, OSError):
+        return 0
+    return (min(64 << 30, total // 8) >> 22) << 22
+
+
 class ConfigError(Exception):
     pass
 
@@ -251,14 +262,15 @@ class Config:
             frame_max=int(g("chana.mq.amqp.connection.frame-max")),
             hash_wildcard=bool(g("chana.mq.routing.topic-hash-wildcard", True)),
             # cold message bodies spill to this much pinned host memory once the HBM log fills
-            spill_bytes=int(g(k + "spill-bytes", 0)))
+            # (-1 = auto: an eighth of the host's RAM, at most 64 GiB)
+            spill_bytes=_auto_spill(int(g(k + "spill-bytes", -1))))
         if store_dir:
             plane.update(persist=1, persist_max=int(g(k + "persist-records", 1 << 16)),
                          persist_bytes=int(g(k + "persist-bytes", 256 << 20)))
         hi = int(g("chana.mq.flow.memory-high-watermark", -1))
         lo = int(g("chana.mq.flow.memory-low-watermark", -1))
-        if hi < 0:
-            hi = int(0.4 * plane["log_bytes"])
+        if hi < 0:   # 40% of what the broker can hold: the HBM body log + the host spill ring
+            hi = int(0.4 * (plane["log_bytes"] + plane["spill_bytes"]))
         if lo < 0:
             lo = hi // 2
         broker = dict(io=str(g(k + "front-end", "pipeline")), io_threads=int(g(k + "io-threads", 4)),

@@ -7,6 +7,7 @@ every unroutable one comes back as a Basic.Return, all confirms are acks and the
 holds nothing afterwards.  (The settle-order bug this round — an Ack(multiple) applied
 before an earlier Nack(multiple, requeue) of the same step — breaks "exactly once".)"""
 
+import os
 import random
 import threading
 import time
@@ -15,6 +16,8 @@ import pytest
 
 from chanamq_amd.client import Connection
 from test_gpu_broker import GPU_CFG, SMALL, _gpu_present
+
+SMALL_CONF = os.path.join(os.path.dirname(os.path.abspath(__file__)), "sharded_small.conf")
 
 N_PUB, PER_PUB, QUEUES = 2, 500, 4
 
@@ -265,7 +268,7 @@ def test_mixed_clients_across_ranks(tmp_path, plane):
     here = os.path.dirname(os.path.abspath(__file__))
     env = dict(os.environ, PYTHONPATH=os.path.dirname(here))
     extra = ["--backend", "gloo"] if plane == "gpu" else []   # 2 ranks share the one test GPU
-    ln = Launcher(2, ["-m", "chanamq_amd.server.sharded", "--plane", plane, "--port", "0",
+    ln = Launcher(2, ["-m", "chanamq_amd.server.sharded", "--config", SMALL_CONF, "--plane", plane, "--port", "0",
                       "--info-dir", str(tmp_path)] + extra, env=env).start()
     try:
         deadline = time.time() + 120

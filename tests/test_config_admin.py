@@ -93,3 +93,26 @@ def test_server_launcher_subprocess(tmp_path):
         p.terminate()
         out = p.communicate(timeout=20)[0].decode()
     assert "published msgs" in out and "delivered msgs" in out
+
+
+def test_sharded_rank_reads_gpu_config(tmp_path):
+    """server/sharded.py sizes every rank from chana.mq.gpu.* (it used to
+    hard-code a 2 GB body log), command-line flags win, spill is on by default."""
+    import argparse
+
+    from chanamq_amd.server.sharded import sharded_plane_config
+    from chanamq_amd.utils.config import Config
+    f = tmp_path / "rank.conf"
+    f.write_text("chana.mq.gpu { body-log-bytes = 68719476736, message-table = 134217728, max-connections = 512 }\n")
+    cfg = Config.load([str(f)], {"chana.mq.gpu.io-threads": "6"})
+    args = argparse.Namespace(c_max=None, idle_step_ms=None, io_threads=None)
+    plane, broker = sharded_plane_config(cfg, args, world=8, rank=3, pipeline=True)
+    assert plane["log_bytes"] == 64 << 30 and plane["msg_max"] == 1 << 27 and plane["c_max"] == 512
+    assert plane["world"] == 8 and plane["rank"] == 3 and plane["native_xchg"] == 1 and plane["links"] == 1
+    assert "device" not in plane and plane["seg_max"] <= plane["c_max"]
+    assert plane["spill_bytes"] > 0 and plane["spill_bytes"] % (4 << 20) == 0
+    assert broker["io_threads"] == 6 and "io" not in broker
+    assert broker["mem_high_watermark"] == int(0.4 * (plane["log_bytes"] + plane["spill_bytes"]))
+    args = argparse.Namespace(c_max=64, idle_step_ms=0.5, io_threads=2)
+    plane, broker = sharded_plane_config(cfg, args, world=2, rank=0, pipeline=False)
+    assert plane["c_max"] == 64 and plane["native_xchg"] == 0 and broker["idle_step_ms"] == 0.5

@@ -12,6 +12,8 @@ import pytest
 
 from chanamq_amd.client import Connection
 
+SMALL_CONF = os.path.join(os.path.dirname(os.path.abspath(__file__)), "sharded_small.conf")
+
 pytestmark = pytest.mark.gpu
 HERE = os.path.dirname(os.path.abspath(__file__))
 
@@ -20,7 +22,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 def cluster(tmp_path):
     from chanamq_amd.parallel.launch import Launcher
     env = dict(os.environ, PYTHONPATH=os.path.dirname(HERE))
-    ln = Launcher(2, ["-m", "chanamq_amd.server.sharded", "--plane", "gpu", "--port", "0", "--backend", "gloo",
+    ln = Launcher(2, ["-m", "chanamq_amd.server.sharded", "--config", SMALL_CONF, "--plane", "gpu", "--port", "0", "--backend", "gloo",
                       "--info-dir", str(tmp_path), "--xchg-timeout-ms", "20000"], env=env).start()
     deadline = time.time() + 180
     while time.time() < deadline and not all((tmp_path / f"rank{r}.json").exists() for r in range(2)):
@@ -180,7 +182,7 @@ def test_pipelined_rank_death_durable_redelivery(tmp_path):
     from chanamq_amd.client import ChannelClosed
     from chanamq_amd.parallel.launch import Launcher
     env = dict(os.environ, PYTHONPATH=os.path.dirname(HERE))
-    ln = Launcher(3, ["-m", "chanamq_amd.server.sharded", "--plane", "gpu", "--port", "0", "--backend", "gloo",
+    ln = Launcher(3, ["-m", "chanamq_amd.server.sharded", "--config", SMALL_CONF, "--plane", "gpu", "--port", "0", "--backend", "gloo",
                       "--info-dir", str(tmp_path), "--store-dir", str(tmp_path / "store"), "--no-fsync",
                       "--xchg-timeout-ms", "4000", "--hb-timeout-s", "2"], env=env).start()
     try:
@@ -235,5 +237,64 @@ def test_pipelined_rank_death_durable_redelivery(tmp_path):
             time.sleep(0.3)
         assert all(i["failovers"] == 1 for i in infos), infos
         assert all(i["front_end"]["xfails"] >= 1 for i in infos), infos
+    finally:
+        ln.stop()
+
+
+@pytest.mark.timeout(400)
+def test_sharded_rank_config_and_large_message_to_owner(tmp_path):
+    """A sharded node sized by its config file (chana.mq.gpu.*: a 64 GiB body log per
+    rank) takes a 64 MiB publish on rank 1 for a queue owned by rank 0: routed on the host,
+    its body travels to the owner in the control log's all-to-all, the owner enqueues it,
+    the publisher gets its confirm, and the small publishes around it on the same channel
+    arrive in order (FrameParser.scala:67: any size on any node; AMQPServer.scala:52-70)."""
+    from chanamq_amd.parallel.launch import Launcher
+    conf = tmp_path / "big.conf"
+    conf.write_text(open(SMALL_CONF).read() + """
+chana.mq.gpu {
+  body-log-bytes = 68719476736
+  ingress-bytes = 100663296
+  egress-bytes = 167772160
+  message-table = 4194304
+}
+""")
+    env = dict(os.environ, PYTHONPATH=os.path.dirname(HERE))
+    ln = Launcher(2, ["-m", "chanamq_amd.server.sharded", "--config", str(conf), "--plane", "gpu", "--port", "0",
+                      "--backend", "gloo", "--info-dir", str(tmp_path), "--xchg-timeout-ms", "30000"], env=env).start()
+    try:
+        deadline = time.time() + 240
+        while time.time() < deadline and not all((tmp_path / f"rank{r}.json").exists() for r in range(2)):
+            assert not ln.poll(), f"rank exited early: {ln.poll()}"
+            time.sleep(0.2)
+        info = [json.load(open(tmp_path / f"rank{r}.json")) for r in range(2)]
+        assert all(i["plane"]["log_bytes"] >= 64 << 30 for i in info), info
+        assert all(i["plane"]["ingress_cap"] == 96 << 20 for i in info), info
+        c0 = Connection(port=info[0]["port"], vhost="/")
+        c1 = Connection(port=info[1]["port"], vhost="/", timeout=60)
+        a = c0.channel()
+        a.queue_declare("big.q")                       # placed on rank 0
+        a.basic_consume("big.q", "bigc", no_ack=True)
+        p = c1.channel()
+        p.queue_declare("big.q", passive=True)         # replicated to rank 1
+        p.confirm_select()
+        body = bytes(range(256)) * (1 << 18)           # 64 MiB
+        p.basic_publish("", "big.q", b"before")
+        p.basic_publish("", "big.q", body, {"delivery_mode": 1, "content_type": "application/octet-stream"})
+        for i in range(3):
+            p.basic_publish("", "big.q", b"after%d" % i)
+        assert p.wait_for_confirms(timeout=120)
+        got = a.consume_n(5, timeout=120)
+        assert [len(d.body) for d in got] == [6, len(body), 6, 6, 6]
+        assert got[1].body == body and got[1].props.get("content_type") in ("application/octet-stream",
+                                                                            b"application/octet-stream")
+        assert [d.body for d in got[2:]] == [b"after0", b"after1", b"after2"] and got[0].body == b"before"
+        # unroutable + mandatory: returned to the publisher
+        p.basic_publish("", "no.such.queue", body[:(20 << 20)], mandatory=True)
+        assert p.wait_for_confirms(timeout=120)
+        c1.process(1.0)
+        assert p.returns and len(p.returns[0].body) == 20 << 20
+        c0.close()
+        c1.close()
+        assert not ln.poll()
     finally:
         ln.stop()

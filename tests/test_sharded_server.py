@@ -11,6 +11,8 @@ import pytest
 from chanamq_amd.client import ChannelClosed, Connection
 from test_sharded_golden import _free_port
 
+SMALL_CONF = os.path.join(os.path.dirname(os.path.abspath(__file__)), "sharded_small.conf")
+
 HERE = os.path.dirname(os.path.abspath(__file__))
 
 
@@ -21,7 +23,7 @@ def cluster(request, tmp_path):
     # 2 ranks share the one test GPU; the Python lockstep loop (remote consumers over the
     # Python link relay).  The pipelined front end: tests/test_gpu_sharded_server.py
     extra = ["--backend", "gloo", "--io", "native"] if request.param == "gpu" else []
-    ln = Launcher(2, ["-m", "chanamq_amd.server.sharded", "--plane", request.param, "--port", "0",
+    ln = Launcher(2, ["-m", "chanamq_amd.server.sharded", "--config", SMALL_CONF, "--plane", request.param, "--port", "0",
                       "--info-dir", str(tmp_path)] + extra, env=env).start()
     deadline = time.time() + 120
     while time.time() < deadline and not all((tmp_path / f"rank{r}.json").exists() for r in range(2)):
@@ -115,7 +117,7 @@ def test_rank_death_durable_queue_reloaded(tmp_path):
     consumer on that rank receives every message."""
     from chanamq_amd.parallel.launch import Launcher
     env = dict(os.environ, PYTHONPATH=os.path.dirname(HERE))
-    ln = Launcher(3, ["-m", "chanamq_amd.server.sharded", "--plane", "golden", "--port", "0",
+    ln = Launcher(3, ["-m", "chanamq_amd.server.sharded", "--config", SMALL_CONF, "--plane", "golden", "--port", "0",
                       "--info-dir", str(tmp_path), "--store-dir", str(tmp_path / "store"), "--no-fsync"],
                   env=env).start()
     try:
