@@ -83,7 +83,43 @@ FE_CFG = {}
 SIZING = {"per_conn_read": 512 << 10, "carry_cap": 1 << 20}
 
 
-def run_one(core, name, spec, io, io_threads, seconds, rate=0.0, lg_threads=12, store_dir=None, cons_threads=8):
+def get_pollers(port, n, stop, out, prefill=200000):
+    """``n`` clients polling Basic.Get (no-ack) on their own pre-filled queue while the
+    load runs: every answer is served inside a step (k_dequeue) without draining the
+    pipeline.  Appends (gets ok, gets empty, seconds) per poller to ``out``."""
+    import threading
+
+    from chanamq_amd.client import Connection
+    c = Connection(port=port, vhost="/", timeout=60)
+    ch = c.channel()
+    for i in range(n):
+        ch.queue_declare(f"e2e.getq{i}")
+        for k in range(prefill // n):
+            ch.basic_publish("", f"e2e.getq{i}", b"g" * 256)
+    c.process(0.5)
+
+    def poll(i):
+        pc = Connection(port=port, vhost="/", timeout=60)
+        pch = pc.channel()
+        ok = empty = 0
+        t0 = time.time()
+        while not stop.is_set():
+            d = pch.basic_get(f"e2e.getq{i}", no_ack=True)
+            if d is None:
+                empty += 1
+            else:
+                ok += 1
+        out.append((ok, empty, time.time() - t0))
+        pc.close()
+    ths = [threading.Thread(target=poll, args=(i,), daemon=True) for i in range(n)]
+    for t in ths:
+        t.start()
+    c.close()
+    return ths
+
+
+def run_one(core, name, spec, io, io_threads, seconds, rate=0.0, lg_threads=12, store_dir=None, cons_threads=8,
+            n_getters=0):
     from chanamq_amd.server.gpu_broker import GpuBroker
     persist = bool(spec.get("persistent"))
     plane = plane_for(spec)
@@ -108,12 +144,18 @@ def run_one(core, name, spec, io, io_threads, seconds, rate=0.0, lg_threads=12, 
     import threading
     smp = threading.Thread(target=sample, daemon=True)
     smp.start()
+    gstop, gout, gths = threading.Event(), [], []
+    if n_getters:
+        gths = get_pollers(b.port, n_getters, gstop, gout)
     try:
         r = core.run_load(dict(port=b.port, seconds=seconds, warmup=1.0, queue=f"e2e.{name}",
                                exchange=f"e2e.x.{name}", threads=lg_threads, consumer_threads=cons_threads,
                                rate=rate, **spec))
     finally:
         done[0] = True
+        gstop.set()
+        for t in gths:
+            t.join(30)
         smp.join()
         cpu1 = thread_cpu()
         after = {}
@@ -181,6 +223,9 @@ def run_one(core, name, spec, io, io_threads, seconds, rate=0.0, lg_threads=12, 
                                                 "delivered", "routed", "dropped_nomem", "ring_full", "unroutable",
                                                 "expired", "ctrl", "live_msgs", "live_bytes", "log_used")},
              flow_off_server=st.get("flow_off", 0),
+             getters=(dict(n=n_getters, gets_ok=sum(g[0] for g in gout), gets_empty=sum(g[1] for g in gout),
+                           gets_per_s=sum(g[0] + g[1] for g in gout) / max(1e-9, max((g[2] for g in gout), default=1)),
+                           device_gets=st.get("device_gets", 0)) if n_getters else None),
              last_step={k: lc.get(k) for k in ("n_ring_full", "n_dropped_nomem")},
              store=getattr(b, "_pw_stats", None))
     del plane
@@ -303,6 +348,9 @@ def main():
     ap.add_argument("--sharded", type=int, default=0,
                     help="N > 1: the pipelined sharded server with N ranks on this GPU (producers on rank 1, "
                          "consumers on rank 0 and then on rank 1 through device links)")
+    ap.add_argument("--getters", type=int, default=0,
+                    help="also run each spec with this many Basic.Get pollers on pre-filled queues (the load's "
+                         "throughput with and without them, and the gets/s)")
     args = ap.parse_args()
     SIZING.update(per_conn_read=args.per_conn_read, carry_cap=max(args.carry_cap, 2 * args.per_conn_read))
     if args.wblock_high:
@@ -357,6 +405,13 @@ def main():
                                                     "store", "thread_cpu_s", "cpu_consumers_s",
                                                     "cpu_producers_s", "engine_host_s")}),
                       flush=True)
+                if args.getters:
+                    rg = run_one(core, name, spec, io, nt, args.seconds, lg_threads=args.loadgen_threads,
+                                 cons_threads=args.consumer_threads, n_getters=args.getters)
+                    rg["with_getters"] = args.getters
+                    results.append(rg)
+                    print(json.dumps({k: rg[k] for k in ("name", "io_threads", "recv_msgs_per_s", "sent_msgs_per_s",
+                                                         "p50_us", "p99_us", "getters", "error")}), flush=True)
                 for agg in [float(x) for x in args.rates.split(",") if x]:
                     rr = run_one(core, name, spec, io, nt, args.seconds, rate=agg / max(1, spec.get("producers", 1)),
                                  lg_threads=args.loadgen_threads, cons_threads=args.consumer_threads)

@@ -64,7 +64,8 @@ class _Conn:
 
 
 FE_OPEN, FE_CLOSED, FE_HOST, FE_CTRL, FE_TXBUF, FE_EVENT, FE_STATUS, FE_PERSIST, FE_ERROR, FE_GROW, FE_SYNC, \
-    FE_XFAIL, FE_INJECTED = range(1, 14)
+    FE_XFAIL, FE_INJECTED, FE_GET = range(1, 15)
+GS_EMPTY, GS_OK, GS_RETRY, GS_NO_SPACE, GS_WINDOW_FULL = range(5)   # step_abi.h GetOut.status
 
 
 class _PlaneLock:
@@ -198,6 +199,7 @@ class GpuBroker:
         self._links = {}        # (conn, channel, consumer tag) -> link id (remote consumers)
         self._get_links = {}    # (vhost, queue) -> get link id (Basic.Get of remote queues)
         self._get_wait = {}     # pull id -> (conn, channel, no_ack, link id)
+        self._dev_gets = {}     # Basic.Gets queued on the device: id -> (conn, channel, queue slot, no_ack)
         self._get_holders = {}  # get link id -> {(conn, channel)} holding unacked Get messages
         self._get_used = {}     # get link id -> monotonic time of its last Get
         self._pull_seq = 0
@@ -367,6 +369,9 @@ class GpuBroker:
             if kind == FE_INJECTED:   # a committed transaction's publishes were stepped
                 if conn == self.txc:
                     self._tx_end()
+                continue
+            if kind == FE_GET:        # a Basic.Get answered by its step
+                self._get_answer(conn, a, b)
                 continue
             if kind == FE_OPEN:
                 self.conns[conn] = _Conn(None, conn, None)
@@ -1352,6 +1357,14 @@ class GpuBroker:
                 raise ControlError(C.RESOURCE_LOCKED, f"queue '{q.name}' is exclusive to another connection", 60, 70)
             if q.owner != p.rank:
                 return self._remote_get(c, ch, vh, q, m)
+            if self.fe is not None and hasattr(p, "eng"):
+                # served inside the next step (k_dequeue, ahead of the queue's consumers): no
+                # pipeline drain; the connection stays paused until FE_GET answers it
+                gid = self._next_get = getattr(self, "_next_get", 0) + 1
+                self._dev_gets[gid] = (c.id, ch, q.slot, bool(m.no_ack))
+                self.fe.queue_get(c.id, p.chslot(c.id, ch), q.slot, int(bool(m.no_ack)), gid)
+                self.stats["device_gets"] = self.stats.get("device_gets", 0) + 1
+                return "deferred"
             frames, _ = p.basic_get(c.id, ch, q.slot, m.no_ack, int(time.time() * 1000))
             if frames is None:
                 self._send(c, ch, Method("basic.get_empty"))
@@ -1465,6 +1478,29 @@ class GpuBroker:
                     self._send(c, ch, out)
             if c.state == "open" and not (hasattr(reply, "keep_paused") and reply.keep_paused(res)):
                 self._unpause(conn)
+
+    def _get_answer(self, conn, a, gid):
+        """FE_GET: the step that carried Basic.Get ``gid`` finished.  OK: its GetOk + header
+        + body were rendered into the connection's egress of that step; EMPTY: GetEmpty
+        from here; RETRY (the step was full): with the next step."""
+        req = self._dev_gets.pop(gid, None)
+        c = self.conns.get(conn)
+        if req is None or c is None or c.state != "open":
+            return
+        st, cnt = a & 0xFFFFFFFF, a >> 32
+        _, ch, slot, no_ack = req
+        if st == GS_RETRY:
+            self._dev_gets[gid] = req
+            self.fe.queue_get(conn, self.plane.chslot(conn, ch), slot, int(no_ack), gid)
+            return
+        if st == GS_EMPTY:
+            self._send(c, ch, Method("basic.get_empty"))
+        elif st != GS_OK:
+            self._chan_close(c, ch, C.RESOURCE_ERROR, "basic.get: " + (
+                "message exceeds the egress buffer" if st == GS_NO_SPACE else "channel delivery window full"), 60, 70)
+        self._flush(c)
+        if c.state == "open":
+            self._unpause(conn)
 
     def _remote_get(self, c, ch, vh, q, m):
         """Basic.Get of a queue another rank owns: a pull on this rank's get link for the
@@ -1734,6 +1770,9 @@ class GpuBroker:
         if self._links:
             self._close_links(c.id)
         if self.fe is not None:
+            self.fe.cancel_gets(c.id)
+            for gid in [g for g, r in self._dev_gets.items() if r[0] == c.id]:
+                del self._dev_gets[gid]
             if prev != "gone":
                 self._flush(c)
             if prev == "open" or c.id in self.plane.conns:

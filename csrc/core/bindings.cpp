@@ -261,6 +261,9 @@ PYBIND11_MODULE(_core, m) {
       .def("pending_out", &Frontend::pending_out)
       .def("request_sync", &Frontend::request_sync)
       .def("inject", [](Frontend& f, uint32_t conn, py::bytes b) { f.inject(conn, std::string(b)); })
+      .def("queue_get", &Frontend::queue_get, py::arg("conn"), py::arg("chslot"), py::arg("q"), py::arg("noack"),
+           py::arg("id"))
+      .def("cancel_gets", &Frontend::cancel_gets)
       .def("sync_done", &Frontend::sync_done)
       .def("healthy", &Frontend::healthy, py::arg("stuck_s") = 5.0)
       .def("inject_fault", &Frontend::inject_fault, py::arg("kind"), py::arg("steps") = 0)

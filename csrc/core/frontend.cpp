@@ -384,6 +384,45 @@ void Frontend::inject(u32 conn, const std::string& bytes) {
   wake_stepper();
 }
 
+void Frontend::queue_get(u32 conn, u32 chslot, u32 q, u32 noack, u64 id) {
+  {
+    std::lock_guard<std::mutex> g(get_mu_);
+    gets_.push_back(PendGet{GetReq{conn, chslot, q, noack}, id});
+  }
+  wake_stepper();
+}
+
+void Frontend::cancel_gets(u32 conn) {
+  std::lock_guard<std::mutex> g(get_mu_);
+  gets_.erase(std::remove_if(gets_.begin(), gets_.end(), [&](const PendGet& x) { return x.r.conn == conn; }),
+              gets_.end());
+}
+
+bool Frontend::gets_pending() {
+  std::lock_guard<std::mutex> g(get_mu_);
+  return !gets_.empty();
+}
+
+// stepper thread, right before api_->submit: the step takes the oldest requests
+void Frontend::stage_gets(Inflight& f) {
+  if (!api_->stage_gets) return;
+  std::vector<GetReq> rs;
+  {
+    std::lock_guard<std::mutex> g(get_mu_);
+    if (gets_.empty()) return;
+    const size_t n = std::min<size_t>(gets_.size(), GET_STEP_MAX);
+    for (size_t i = 0; i < n; ++i) {
+      rs.push_back(gets_[i].r);
+      f.gets.emplace_back(gets_[i].r.conn, gets_[i].id);
+    }
+    gets_.erase(gets_.begin(), gets_.begin() + n);
+  }
+  if (api_->stage_gets(api_->eng, rs.data(), (u32)rs.size()) != 0) {
+    check(-1);
+    f.gets.clear();
+  }
+}
+
 void Frontend::kick(u32 conn) {
   if (conn >= c_max_) return;
   FeConn& c = *conns_[conn];
@@ -835,6 +874,17 @@ void Frontend::finish_oldest(std::deque<Inflight>& inflight) {
   }
   double w = secs_since(t0);
   const Counters& c = *api_->counters(api_->eng, p);
+  if (!f.gets.empty()) {   // Basic.Get answers of this step
+    const GetOut* go = api_->get_out(api_->eng, p);
+    for (size_t k = 0; k < f.gets.size(); ++k) {
+      FeEvent e;
+      e.kind = FE_GET;
+      e.conn = f.gets[k].first;
+      e.a = (u64)go[k].status | ((u64)go[k].msg_count << 32);
+      e.b = f.gets[k].second;
+      post(std::move(e));
+    }
+  }
   const SegOut* so = api_->seg_out(api_->eng, p);
   for (size_t k = 0; k < f.segs.size(); ++k) {
     const SegOut& s = so[k];
@@ -991,7 +1041,7 @@ void Frontend::stepper() {
       continue;
     }
     // ---- idle: nothing in flight, nothing to write, nothing readable
-    if (inflight.empty() && !pend_valid_ && out_.empty() && !last_busy_ && !releasable()) {
+    if (inflight.empty() && !pend_valid_ && out_.empty() && !last_busy_ && !releasable() && !gets_pending()) {
       std::unique_lock<std::mutex> g(st_mu_);
       const double idle = cfg_.idle_step_ms > 0 ? cfg_.idle_step_ms : 1000.0;
       st_cv_.wait_for(g, std::chrono::microseconds((i64)(idle * 1000)),
@@ -1031,13 +1081,15 @@ void Frontend::stepper() {
       }
     }
     const u64 used = ph_used_.load();
-    const bool submit = !segs.empty() || last_busy_ || idle_tick_;
+    const bool submit = !segs.empty() || last_busy_ || idle_tick_ || gets_pending();
     idle_tick_ = false;
     bool submitted = false;
     if (submit) {
       if (inflight.size() >= 2) finish_oldest(inflight);
       if (failed_) break;
       i64 t1 = now_ns();
+      Inflight f;
+      stage_gets(f);
       int p = api_->submit(api_->eng, segs.data(), (u32)segs.size(), arena_[arena_i_], used, wall_ms(), cfg_.worker);
       if (!check(p)) break;
       {
@@ -1047,7 +1099,6 @@ void Frontend::stepper() {
         stats_.gather_segs += segs.size();
         if (segs.empty() && !last_busy_) stats_.idle_steps++;
       }
-      Inflight f;
       f.p = p;
       f.step = ++step_no_;
       f.segs = std::move(seglens);
@@ -1168,7 +1219,7 @@ void Frontend::stepper_sharded() {
       continue;
     }
     // ---- pace: idle ranks tick every idle_step_ms (the whole cluster is idle)
-    if (!(last_busy_ || cluster_busy_ || sync_req_ || releasable())) {
+    if (!(last_busy_ || cluster_busy_ || sync_req_ || releasable() || gets_pending())) {
       std::unique_lock<std::mutex> g(st_mu_);
       const double idle = cfg_.idle_step_ms > 0 ? cfg_.idle_step_ms : 1.0;
       st_cv_.wait_for(g, std::chrono::microseconds((i64)(idle * 1000)),
@@ -1195,12 +1246,14 @@ void Frontend::stepper_sharded() {
         conns_[sg.conn]->inflight += sg.len;
       }
     }
-    const bool local_busy = !segs.empty() || last_busy_;
+    const bool local_busy = !segs.empty() || last_busy_ || gets_pending();
     if (inflight.size() >= 2) finish_oldest(inflight);
     if (failed_) break;
     // ---- step t: H2D + phase A
     i64 t1 = now_ns();
     int p;
+    Inflight f;
+    stage_gets(f);
     {
       GpuWait gw(gpu_wait_since_);
       p = api_->submit(api_->eng, segs.data(), (u32)segs.size(), arena_[arena_i_], ph_used_.load(), wall_ms(),
@@ -1208,7 +1261,6 @@ void Frontend::stepper_sharded() {
     }
     if (!check(p)) break;
     arena_i_ = (arena_i_ + 1) % 3;
-    Inflight f;
     f.p = p;
     f.step = ++step_no_;
     f.segs = std::move(seglens);

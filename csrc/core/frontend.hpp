@@ -62,6 +62,7 @@ enum FeEventKind : int {
   FE_SYNC = 11,
   FE_XFAIL = 12,
   FE_INJECTED = 13,   // the bytes inject()ed into a pseudo-connection were stepped (a = its carry)
+  FE_GET = 14,        // a queue_get() was answered by its step: a = status | message_count << 32, b = id
 };
 
 enum : u32 { XF_SYNC = 1, XF_BUSY = 2 };   // exchange flags (OR over the live ranks)
@@ -130,6 +131,10 @@ class Frontend {
   // bytes for a socketless pseudo-connection (committed transactions): stepped with the
   // next step like a client's, FE_INJECTED once that step finished; egress is dropped
   void inject(u32 conn, const std::string& bytes);
+  // Basic.Get served inside the next step (k_dequeue): FE_GET answers it once the step
+  // finished (GetOk rendered into the connection's egress of that step)
+  void queue_get(u32 conn, u32 chslot, u32 q, u32 noack, u64 id);
+  void cancel_gets(u32 conn);                            // the connection is gone: drop its requests
   void pause();                                          // exclusive device access (nests)
   void resume();
   void release(u64 step);                                // store commit of steps <= step landed
@@ -153,7 +158,18 @@ class Frontend {
 
  private:
   friend struct FeIo;
-  struct Inflight { int p; u64 step; std::vector<std::pair<u32, u32>> segs; std::vector<u32> gen; };
+  struct Inflight {
+    int p;
+    u64 step;
+    std::vector<std::pair<u32, u32>> segs;
+    std::vector<u32> gen;
+    std::vector<std::pair<u32, u64>> gets;   // (conn, id) of the Basic.Gets it serves
+  };
+  struct PendGet { GetReq r; u64 id; };
+  std::mutex get_mu_;
+  std::vector<PendGet> gets_;   // queue_get() requests not yet submitted
+  void stage_gets(Inflight& f);   // up to GET_STEP_MAX of them into the step about to be submitted
+  bool gets_pending();
   struct Scatter {   // one step's rendered egress, ready to write
     const u8* egress = nullptr;
     std::vector<ConnOut> co;

@@ -2868,7 +2868,8 @@ DEV void chan_advance_one(const DS& d, u32 ch, u32 tid, u32 lane, u32 w, u32* s_
 DEV u32 deliver_size(const DS& d, u32 cons, const MsgEnt& m, u32 conn) {
   // a link pseudo-connection ships [ex][rk][props][body] as a restore record (render_deliv)
   if (d.links && d.conn_link[conn]) return align16(m.ex_len + m.rk_len + m.props_len + m.body_len);
-  u32 mp = 4 + 1 + d.cons_tag_len[cons] + 8 + 1 + 1 + m.ex_len + 1 + m.rk_len;
+  // cons_max = a Basic.GetOk: no consumer tag, a 4-byte message-count instead
+  u32 mp = (cons == d.cons_max ? 4 + 4 : 4 + 1 + d.cons_tag_len[cons]) + 8 + 1 + 1 + m.ex_len + 1 + m.rk_len;
   u32 sz = 8 + mp + 8 + 12 + m.props_len;
   u32 fm = d.conn_frame_max[conn];
   u32 fmb = fm ? fm - 8 : 0xffffffffu;
@@ -2895,6 +2896,7 @@ __global__ __launch_bounds__(256) void k_dequeue(DS d) {
   __shared__ u32 g_cons[RUNS_PER_Q];
   __shared__ u32 g_n[RUNS_PER_Q];
   __shared__ u64 s_head;
+  __shared__ u32 s_ngr;
   __shared__ unsigned long long s_bytes;
   __shared__ u64 kpos[REQ_BLK];
   __shared__ u32 kidx[REQ_BLK];
@@ -2971,13 +2973,69 @@ __global__ __launch_bounds__(256) void k_dequeue(DS d) {
   }
   __syncthreads();
   head = s_head;
+  // Basic.Get requests of this queue, in request order, ahead of its consumers (the
+  // reference's Pull(1) with the channel's next delivery tag, FrameStage.scala:1199-1229):
+  // each answer is one run of cnt 1 on the requester's channel (consumer slot cons_max),
+  // rendered as GetOk + header + body by k_render; EMPTY / RETRY / WINDOW_FULL go back
+  // to the host through the step's host-mapped GetOut (the host initialised them RETRY)
+  u32 ngr = 0;
+  if (d.in->nget) {   // kernel-uniform
+    if (tid == 0) {
+      const u32 ng = d.in->nget < GET_STEP_MAX ? d.in->nget : GET_STEP_MAX;
+      u64 h = head;
+      for (u32 i = 0; i < ng; ++i) {
+        const GetReq rq = d.get_req[i];
+        if (rq.q != q) continue;
+        GetOut o;
+        o.status = GS_RETRY;
+        o.msg_count = 0;
+        if (!nodisp && h == tail) {
+          o.status = GS_EMPTY;
+        } else if (!nodisp && ngr < RUNS_PER_Q / 2 && rq.chslot < d.c_max * d.chpc) {
+          const u32 ch = rq.chslot;
+          const u32 sz = deliver_size(d, d.cons_max, d.msgs[ring[h & mask].msg], ch / d.chpc);
+          u32 wb, db;
+          if (sz > d.egress_cap / 2) {
+            o.status = GS_NO_SPACE;
+          } else if (!reserve_upto(&d.ch_win[ch], 1u, d.ucap_mask + 1, &wb)) {
+            o.status = GS_WINDOW_FULL;
+          } else if (reserve_sat64(d.egress_budget, sz, d.egress_cap) < sz ||
+                     !reserve_sat(&d.ctr->n_deliv, 1u, d.deliv_max, &db)) {
+            atomicSub(&d.ch_win[ch], 1u);   // step full: the host retries with a later step
+          } else {
+            if (!rq.noack) { atomicAdd(&d.ch_unacked[ch], 1u); atomicAdd(&d.cons_unacked[d.cons_max], 1u); }
+            const u64 left = tail - h - 1;
+            Run rn;
+            rn.ch = ch;
+            rn.cons = left < 0xffffffffull ? (u32)left : 0xffffffffu;
+            rn.cnt = 1;
+            rn.q = q;
+            rn.qpos = h;
+            rn.noack = rq.noack ? 1u : 0u;
+            rn.flags = RUN_GET;
+            d.runs[(u64)q * RUNS_PER_Q + ngr] = rn;
+            ++ngr;
+            ++h;
+            o.status = GS_OK;
+            o.msg_count = rn.cons;
+          }
+        }
+        d.get_out_h[i] = o;
+      }
+      s_head = h;
+      s_ngr = ngr;
+    }
+    __syncthreads();
+    head = s_head;
+    ngr = s_ngr;
+  }
   const u32 mall = d.q_cons_n[q];
   const u64 avail = tail - head;
   if (mall == 0 || avail == 0 || nodisp) {
-    if (tid == 0) { d.q_head[q] = head; d.q_nruns[q] = 0; }
+    if (tid == 0) { d.q_head[q] = head; d.q_nruns[q] = ngr; }
     return;
   }
-  const u32 m = mall > RUNS_PER_Q ? RUNS_PER_Q : mall;
+  const u32 m = mall > RUNS_PER_Q - ngr ? RUNS_PER_Q - ngr : mall;
   const u32 r = d.q_rr[q] % mall;
   // (1) counts by credit
   if (tid == 0) {
@@ -3072,8 +3130,8 @@ __global__ __launch_bounds__(256) void k_dequeue(DS d) {
       g_n[j] -= take;
       excess -= take;
     }
-    // (4) runs, in round-robin order
-    u32 nr = 0;
+    // (4) runs, in round-robin order (after this step's Basic.Get answers)
+    u32 nr = ngr;
     u64 qp = head;
     for (u32 j = 0; j < m; ++j) {
       u32 cnt = g_n[j];
@@ -3086,7 +3144,7 @@ __global__ __launch_bounds__(256) void k_dequeue(DS d) {
       rn.q = q;
       rn.qpos = qp;
       rn.noack = d.cons_noack[c];
-      rn.pad = 0;
+      rn.flags = 0;
       d.runs[(u64)q * RUNS_PER_Q + nr] = rn;
       ++nr;
       qp += cnt;
@@ -3196,24 +3254,26 @@ __global__ void k_dv_write(DS d) {
     const Desc ds = d.ring[d.q_ring_off[rn.q] + ((rn.qpos + k) & d.q_ring_mask[rn.q])];
     const u32 ch = rn.ch;
     const u64 tag = d.ch_next_tag[ch] + (i - d.ch_first[ch]);
+    const bool get = rn.flags & RUN_GET;
+    const u32 cons = get ? d.cons_max : rn.cons;   // Basic.Get: the reserved slot cons_max
     dv.chslot = ch;
-    dv.cons = rn.cons;
+    dv.cons = rn.cons;   // Basic.Get: the message-count of the GetOk
     dv.msg = ds.msg;
     dv.q = rn.q;
     dv.qpos = rn.qpos + k;
     dv.expire_ms = ds.expire_ms;
     dv.tag = tag;
-    dv.flags = (ds.flags & 1) | (rn.noack ? 2u : 0u);
+    dv.flags = (ds.flags & 1) | (rn.noack ? 2u : 0u) | (get ? DV_GET : 0u);
     USlot u;
     u.state = rn.noack ? US_DONE : US_PENDING;
     u.msg = ds.msg;
     u.q = rn.q;
-    u.cons = rn.cons;
+    u.cons = cons;
     u.qpos = dv.qpos;
     u.expire_ms = ds.expire_ms;
     d.uwin[(u64)ch * (d.ucap_mask + 1) + ((tag - 1) & d.ucap_mask)] = u;
     const MsgEnt& m = d.msgs[ds.msg];
-    const u32 sz = deliver_size(d, rn.cons, m, ch / d.chpc);
+    const u32 sz = deliver_size(d, cons, m, ch / d.chpc);
     dv.size = sz;
     d.dv_size[i] = sz;
     d.deliv[i] = dv;
@@ -3463,27 +3523,31 @@ DEV void render_deliv(const DS& d, u32 i) {
   if (off + dv.size > d.egress_cap) return;  // never: dequeue reserves an egress byte budget
   u8* o = (u8*)d.in->egress + off;
   u32 chno = d.ch_num[ch];
-  u32 taglen = d.cons_tag_len[dv.cons];
-  u32 mp = 4 + 1 + taglen + 8 + 1 + 1 + m.ex_len + 1 + m.rk_len;
+  const bool get = dv.flags & DV_GET;   // Basic.GetOk (60/71): no consumer tag, message-count last
+  u32 taglen = get ? 0u : d.cons_tag_len[dv.cons];
+  u32 mp = (get ? 4 + 4 : 4 + 1 + taglen) + 8 + 1 + 1 + m.ex_len + 1 + m.rk_len;
   u64 dtag = dv.tag;
   // method frame: scalar fields by lane 0, the variable-length strings (consumer tag,
   // exchange, routing key) by all lanes in parallel (no serial byte-load chains)
-  const u32 p_tag = 7 + 4 + 1, p_ex = p_tag + taglen + 8 + 1 + 1, p_rk = p_ex + m.ex_len + 1;
+  const u32 p_tag = 7 + 4 + (get ? 0 : 1), p_ex = p_tag + taglen + 8 + 1 + 1, p_rk = p_ex + m.ex_len + 1;
   if (lane == 0) {
     put_frame_hdr(o, 1, chno, mp);
-    wr16(o + 7, 60); wr16(o + 9, 60);
-    o[11] = (u8)taglen;
+    wr16(o + 7, 60); wr16(o + 9, get ? 71 : 60);
+    if (!get) o[11] = (u8)taglen;
     wr64(o + p_tag + taglen, dtag);
     o[p_tag + taglen + 8] = (dv.flags & 1) ? 1 : 0;
     o[p_ex - 1] = m.ex_len;
     o[p_rk - 1] = m.rk_len;
     u32 p = p_rk + m.rk_len;
+    if (get) { wr32(o + p, dv.cons); p += 4; }
     o[p++] = 0xCE;
     p += put_frame_hdr(o + p, 2, chno, 12 + m.props_len);
     wr16(o + p, 60); wr16(o + p + 2, 0); wr64(o + p + 4, m.body_len);
   }
-  const u8* tg = d.tpool + d.cons_tag_off[dv.cons];
-  for (u32 k = lane; k < taglen; k += 64) o[p_tag + k] = tg[k];
+  if (!get) {
+    const u8* tg = d.tpool + d.cons_tag_off[dv.cons];
+    for (u32 k = lane; k < taglen; k += 64) o[p_tag + k] = tg[k];
+  }
   for (u32 k = lane; k < m.ex_len; k += 64) o[p_ex + k] = slot[k];
   for (u32 k = lane; k < m.rk_len; k += 64) o[p_rk + k] = slot[m.ex_len + k];
   u32 hp = 8 + mp + 7 + 12;

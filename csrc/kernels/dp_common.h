@@ -49,7 +49,7 @@ struct StepIn {         // host -> device per step (64 B)
   u64 step;
   u64 id_ms;            // epoch ms for snowflake ids
   u32 worker;           // snowflake worker id (rank)
-  u32 pad0;
+  u32 nget;             // Basic.Get requests of this step (DS.get_req, <= GET_STEP_MAX)
   u64 egress;           // device pointer: this step's egress slot (engine rotates slots)
   u64 pad[2];
 };
@@ -161,13 +161,15 @@ struct Deliv {          // one delivery produced by the dequeue kernel
 
 struct Run {            // consecutive queue entries granted to one consumer this step
   u32 ch;               // channel slot
-  u32 cons;
+  u32 cons;             // RUN_GET: the queue's ready count left (Basic.GetOk message-count)
   u32 cnt;
   u32 q;
   u64 qpos;             // queue position of the first entry
   u32 noack;
-  u32 pad;
+  u32 flags;            // RUN_GET: one Basic.Get answer (consumer slot cons_max)
 };
+#define RUN_GET 1u
+#define DV_GET 4u       // Deliv.flags: a Basic.GetOk (Deliv.cons = message-count)
 
 struct USlot {          // per-channel unacked window slot
   u32 state;

@@ -216,6 +216,10 @@ class Engine {
       }
       stage_in_[p] = (StepIn*)pinned(("stage_in" + sfx).c_str(), sizeof(StepIn));
       stage_segs_[p] = (SegIn*)pinned(("stage_segs" + sfx).c_str(), sizeof(SegIn) * d_.seg_max);
+      // Basic.Get on the step: the requests (H2D with the step) and their answers
+      io.get_req = (const GetReq*)dev(("get_req" + sfx).c_str(), sizeof(GetReq) * GET_STEP_MAX);
+      io.get_out_h = (GetOut*)hst(("get_out" + sfx).c_str(), sizeof(GetOut) * GET_STEP_MAX);
+      stage_gets_[p] = (GetReq*)pinned(("stage_gets" + sfx).c_str(), sizeof(GetReq) * GET_STEP_MAX);
     }
 
     // egress slots rotate per step independently of the IO parity: step t renders into
@@ -702,6 +706,18 @@ class Engine {
     in->egress = (u64)egress_dev_[e];
     slot_of_[p] = e;
     if (sb) memcpy(stage_segs_[p], segp, sb);
+    // staged Basic.Get requests ride this step; their answers start out RETRY (a queue the
+    // device cannot serve now leaves it so)
+    in->nget = (u32)pend_gets_.size();
+    if (in->nget) {
+      memcpy(stage_gets_[p], pend_gets_.data(), sizeof(GetReq) * in->nget);
+      GetOut* go = (GetOut*)buf("get_out" + std::to_string(p)).ptr;
+      for (u32 i = 0; i < in->nget; ++i) go[i] = GetOut{GS_RETRY, 0};
+      HIPCHECK(hipMemcpyAsync((void*)io_[p].get_req, stage_gets_[p], sizeof(GetReq) * in->nget,
+                              hipMemcpyHostToDevice, s_h2d_));
+      pend_gets_.clear();
+    }
+    nget_[p] = in->nget;
     HIPCHECK(hipMemcpyAsync((void*)io_[p].in, in, sizeof(StepIn), hipMemcpyHostToDevice, s_h2d_));
     if (sb) HIPCHECK(hipMemcpyAsync((void*)io_[p].segs, stage_segs_[p], sb, hipMemcpyHostToDevice, s_h2d_));
     if (payload_len)
@@ -713,6 +729,22 @@ class Engine {
     ++seq_;
     if (!defer) launch(p);
     return p;
+  }
+
+  // Basic.Get requests for the next submitted step (validated by the caller: a local queue
+  // of this rank, a channel slot of an open channel)
+  void stage_gets(const GetReq* r, u32 n) {
+    if (pend_gets_.size() + n > GET_STEP_MAX) throw std::runtime_error("stage_gets: more than GET_STEP_MAX per step");
+    for (u32 i = 0; i < n; ++i) {
+      if (r[i].q >= d_.q_max || r[i].chslot >= d_.c_max * d_.chpc) throw std::runtime_error("stage_gets: bad queue / channel");
+      pend_gets_.push_back(r[i]);
+    }
+  }
+  py::list get_out_py(int p) {
+    const GetOut* go = (const GetOut*)buf("get_out" + std::to_string(p)).ptr;
+    py::list l;
+    for (u32 i = 0; i < nget_[p]; ++i) l.append(py::make_tuple(go[i].status, go[i].msg_count));
+    return l;
   }
 
   // second half of submit(): the kernels of the staged step of parity p
@@ -1240,6 +1272,10 @@ class Engine {
     a.egress_ready = [](void* e, int slot) -> int {
       return ((Engine*)e)->guard([&] { ((Engine*)e)->egress_ready(slot); return 0; });
     };
+    a.stage_gets = [](void* e, const GetReq* r, u32 n) -> int {
+      return ((Engine*)e)->guard([&] { ((Engine*)e)->stage_gets(r, n); return 0; });
+    };
+    a.get_out = [](void* e, int p) -> const GetOut* { return ((Engine*)e)->io_[p].get_out_hh; };
     for (int p = 0; p < 2; ++p) {
       std::string sfx = std::to_string(p);
       HostIO& h = io_[p];
@@ -1252,6 +1288,7 @@ class Engine {
       h.crec_hh = d_.persist ? (const ConsumedRec*)buf("consumed" + sfx).ptr : nullptr;
       h.grow_hh = (const RingMove*)buf("grow" + sfx).ptr;
       h.conn_conf_hh = (const u32*)buf("conn_conf" + sfx).ptr;
+      h.get_out_hh = (const GetOut*)buf("get_out" + sfx).ptr;
     }
     return (u64)&api_;
   }
@@ -1651,7 +1688,11 @@ class Engine {
     const ConsumedRec* crec_hh = nullptr;
     const RingMove* grow_hh = nullptr;
     const u32* conn_conf_hh = nullptr;
+    const GetOut* get_out_hh = nullptr;
   };
+  std::vector<GetReq> pend_gets_;   // Basic.Get requests for the next submit
+  GetReq* stage_gets_[2] = {nullptr, nullptr};
+  u32 nget_[2] = {0, 0};
   HostIO io_[2];
   CmqEngineApi api_{};
   std::string err_;
@@ -1720,6 +1761,13 @@ PYBIND11_MODULE(_dataplane, m) {
            py::arg("now_ms"), py::arg("step"), py::arg("id_ms"), py::arg("worker"), py::arg("defer") = false,
            py::arg("flags") = 0)
       .def("launch", &Engine::launch)
+      .def("stage_gets", [](Engine& e, py::buffer b) {
+             py::buffer_info bi = b.request();
+             const size_t nb = (size_t)bi.size * bi.itemsize;
+             if (nb % sizeof(GetReq)) throw std::runtime_error("stage_gets: GetReq[] (u32 conn, chslot, q, noack)");
+             e.stage_gets((const GetReq*)bi.ptr, (u32)(nb / sizeof(GetReq)));
+           })
+      .def("get_out", &Engine::get_out_py)
       .def("send_counts", &Engine::send_counts)
       .def("submit_b", &Engine::submit_b, py::arg("parity"), py::arg("recv"), py::arg("stream") = 0)
       .def("set_xfer_buffers", &Engine::set_xfer_buffers)

@@ -86,10 +86,20 @@ struct RingMove { u32 q, pad; u64 old_off, old_mask, new_off, new_mask, head, ta
 
 struct ConnOut { u32 off; u32 len; };
 
+// Basic.Get served inside a step (k_dequeue, before the queue's consumers): the front end
+// stages up to GET_STEP_MAX requests with a submit; the device answers each in the step's
+// host-mapped GetOut (OK: GetOk + header + body rendered into the connection's egress like
+// a delivery; EMPTY: the host sends Basic.GetEmpty; RETRY: resubmit with a later step).
+// Reference: FrameStage.scala:1199-1229, QueueEntity.scala:318-393
+#define GET_STEP_MAX 256
+struct GetReq { u32 conn; u32 chslot; u32 q; u32 noack; };
+enum : u32 { GS_EMPTY = 0, GS_OK = 1, GS_RETRY = 2, GS_NO_SPACE = 3, GS_WINDOW_FULL = 4 };
+struct GetOut { u32 status; u32 msg_count; };
+
 // C entry points of one Engine (engine.hip: Engine::c_api).  All return 0 / a parity on
 // success and -1 on error (message: error()).  Parity p = the double-buffered step IO set
 // of a submitted step; its host-mapped outputs stay valid until the next submit of p.
-#define CMQ_STEP_ABI 4
+#define CMQ_STEP_ABI 5
 struct CmqEngineApi {
   u32 abi;
   u32 c_max, seg_max, carry_cap, persist, persist_max;
@@ -135,5 +145,9 @@ struct CmqEngineApi {
   // thread-safe wait for an egress slot's D2H (IO threads, before writing it out): unlike
   // egress_wait_slot it changes no engine state
   int (*egress_ready)(void* eng, int slot);
+  // Basic.Get on the step: requests for the next submit (n <= GET_STEP_MAX), and the
+  // answers of the last step of parity p (in request order)
+  int (*stage_gets)(void* eng, const GetReq* reqs, u32 n);
+  const GetOut* (*get_out)(void* eng, int p);
 };
 #define GROW_MAX 4096   // grow requests reported per step

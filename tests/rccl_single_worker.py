@@ -57,7 +57,7 @@ def native_lockstep(uid):
 
     cfg = dict(c_max=96, chpc=4, q_max=64, cons_max=256, seg_max=96, cmd_max=1 << 14, deliv_max=1 << 14,
                msg_max=1 << 16, ucap=1024, deliver_cap=4096, ingress_cap=8 << 20, egress_cap=16 << 20,
-               log_bytes=256 << 20, ring_pool=1 << 18, tb_max=64, carry_cap=64 << 10)
+               log_bytes=256 << 20, ring_pool=1 << 23, tb_max=64, carry_cap=64 << 10)
     dp = GpuDataPlane(device=0, worker=0, world=2, rank=0, native_xchg=1, **cfg)
     dp.xchg_setup("rccl", uid, [0], 10000, counts_shm=f"cmq-rccl-test-{os.getpid()}")
     pool, segs, offs, blens, mps, _, _ = bench.build_workload(dp, 0, 64, 4, 1024, 8192, 4, cons_base=64,
