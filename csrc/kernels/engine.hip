@@ -454,6 +454,7 @@ class Engine {
       io.seg_out_h = io_[p].seg_out_h; io.conn_out_h = io_[p].conn_out_h; io.ctrl_h = io_[p].ctrl_h;
       io.ctrl_rec_h = io_[p].ctrl_rec_h; io.grow_h = io_[p].grow_h; io.conn_conf_h = io_[p].conn_conf_h;
       io.persist_h = io_[p].persist_h; io.crec_h = io_[p].crec_h;
+      io.get_req = io_[p].get_req; io.get_out_h = io_[p].get_out_h;
       static_cast<DS&>(io_[p]) = io;
     }
     // native exchange (sharded steps driven by the native front end, csrc/core/frontend.cpp):
