@@ -343,15 +343,10 @@ __global__ __launch_bounds__(1024) void k_stage(DS d) {
     u32* c = (u32*)d.ctr;
     for (u32 k = tid; k < sizeof(Counters) / 4; k += 1024)
       if (k * 4 < offsetof(Counters, log_head)) c[k] = 0;
-    if (tid == 0) {
+    if (tid == 0) {   // (per-parity scratch only: the link-ack counts and the id floor are
+                      // reset by k_marks, in the step's routing half)
       d.ctr->n_grow = 0; d.tot[TS_NMOVE] = 0; d.tot[TS_NDEFER] = 0; d.tot[TS_TTL_BUDGET] = 0;
-      if (d.links)
-        for (u32 r = 0; r < WORLD_MAX; ++r) d.lk_cnt[r] = 0;
       *d.egress_budget = 0;
-      // snowflake virtual position base for this step (ID_SLOT_BITS slots per wall-clock ms)
-      u64 floor_pos = d.in->id_ms << ID_SLOT_BITS;
-      u64 cur = *d.id_next;
-      *d.id_next = cur > floor_pos ? cur : floor_pos;
     }
   }
   u32 total = 0;
@@ -1364,8 +1359,7 @@ __global__ __launch_bounds__(256) void k_decode(DS d) {
       }
     }
     pb.nwords = pb.rk_len <= 32 ? build_keyvec_win(d, rkw, pb.rk_len, pi) : build_keyvec(d, w + pb.rk_off, pb.rk_len, pi);
-    d.pubs[pi] = pb;
-    if (pb.chslot != INVALID && d.ch_confirm[pb.chslot]) atomicAdd(&d.ch_pub_cnt[pb.chslot], 1u);
+    d.pubs[pi] = pb;   // (its channel's confirm count: k_marks)
   } else if (c.kind == CK_ACK || c.kind == CK_NACK || c.kind == CK_REJECT) {
     u32 ai = d.cmd_ack_rank[i];
     if (ai >= d.ack_max) return;
@@ -1379,7 +1373,29 @@ __global__ __launch_bounds__(256) void k_decode(DS d) {
     if (c.kind == CK_ACK) { a.multiple = bits & 1; a.requeue = 0; }
     else if (c.kind == CK_REJECT) { a.multiple = 0; a.requeue = bits & 1; }
     else { a.multiple = bits & 1; a.requeue = (bits >> 1) & 1; }
-    apply_ack(d, a, ai);   // fused K9 mark: k_chan_advance resolves the window next
+    d.acks[ai] = a;   // marked in the channel's window by k_marks (k_chan_advance resolves it)
+  }
+}
+
+// K9 marks + K10 confirm counts of the step's commands: the first kernel of the step's
+// routing half.  k_decode only records acks and publishes, so the ingest half never
+// touches delivery-side state and can run next to the previous step's k_chan_advance /
+// k_render (engine overlap).  Also the routing half's per-step resets.
+__global__ __launch_bounds__(256) void k_marks(DS d) {
+  const u32 i = blockIdx.x * 256 + threadIdx.x;
+  if (i == 0) {
+    if (d.links)
+      for (u32 r = 0; r < WORLD_MAX; ++r) d.lk_cnt[r] = 0;
+    // snowflake virtual position base for this step (ID_SLOT_BITS slots per wall-clock ms)
+    const u64 floor_pos = d.in->id_ms << ID_SLOT_BITS;
+    const u64 cur = *d.id_next;
+    *d.id_next = cur > floor_pos ? cur : floor_pos;
+  }
+  const u32 na = d.ctr->n_acks, np = d.ctr->n_pubs;
+  if (i < na) apply_ack(d, d.acks[i], i);
+  if (i < np) {
+    const u32 ch = d.pubs[i].chslot;
+    if (ch != INVALID && d.ch_confirm[ch]) atomicAdd(&d.ch_pub_cnt[ch], 1u);
   }
 }
 

@@ -9,6 +9,7 @@
 
 #include <chrono>
 #include <algorithm>
+#include <functional>
 #include <map>
 #include <memory>
 #include <stdexcept>
@@ -434,6 +435,10 @@ class Engine {
       // 4 arrays x smax 4096-tiles, or 16 arrays x 4*smax 1024-tiles
       scan_status_ = (u64*)dev("scan_status", 8ull * 16 * (SCAN_TILE / 1024) * scan_smax_);
       scan_ctl_ = (u32*)dev("scan_ctl", 64);
+      // the ingest half's command scan has its own look-back state (it may run next to a
+      // scan of the previous step's routing half)
+      scan_status_ing_ = (u64*)dev("scan_status_ing", 8ull * 16 * (SCAN_TILE / 1024) * scan_smax_);
+      scan_ctl_ing_ = (u32*)dev("scan_ctl_ing", 64);
     }
     d_.tot = (u32*)dev("tot", 4ull * 128);
     d_.egress_budget = (u64*)dev("egress_budget", 8);
@@ -446,8 +451,31 @@ class Engine {
     // each mark is a clock read plus a store on the block's critical path
     d_.dbg = get("fs_marks", 0) ? (u64*)dev("dbg", 8ull * 16 * d_.seg_max) : nullptr;
 
+    // the step's ingest buffers exist once per parity: with overlap (world 1), parity
+    // t+1's ingest half (k_stage .. k_decode) runs while parity t's routing / delivery half
+    // still reads its own commands, publishes, bodies, counters and scratch totals
+    dup(&DS::ctr, "ctr", sizeof(Counters));
+    dup(&DS::tot, "tot", 4ull * 128);
+    dup(&DS::egress_budget, "egress_budget", 8);
+    dup(&DS::seg_start, "seg_start", 4ull * d_.seg_max);
+    dup(&DS::seg_total, "seg_total", 4ull * d_.seg_max);
+    dup(&DS::seg_cmd_base, "seg_cmd_base", 4ull * d_.seg_max);
+    dup(&DS::seg_npub, "seg_npub", 4ull * d_.seg_max);
+    dup(&DS::work, "work", d_.work_cap + 4096);
+    dup(&DS::cmds, "cmds", sizeof(Cmd) * (u64)d_.cmd_max);
+    dup(&DS::frags, "frags", sizeof(Frag) * ((u64)d_.frag_max + d_.import_max));
+    dup(&DS::cmd_is_pub, "cmd_is_pub", 4ull * d_.cmd_max);
+    dup(&DS::cmd_is_ack, "cmd_is_ack", 4ull * d_.cmd_max);
+    dup(&DS::cmd_pub_rank, "cmd_pub_rank", 4ull * d_.cmd_max);
+    dup(&DS::cmd_ack_rank, "cmd_ack_rank", 4ull * d_.cmd_max);
+    dup(&DS::pubs, "pubs", sizeof(Pub) * (u64)d_.pub_cap);
+    dup(&DS::pub_keyvec, "pub_keyvec", (u64)d_.pub_cap * TOPIC_K + 64);
+    dup(&DS::pub_kwoff, "pub_kwoff", 2ull * TOPIC_WORDS * d_.pub_cap + 64);
+    dup(&DS::acks, "acks", sizeof(Ack) * (u64)d_.ack_max);
     for (int p = 0; p < 2; ++p) {
       DS io = d_;
+      if (p == 1)
+        for (auto& f : par1_) f(io);
       io.in = io_[p].in; io.segs = io_[p].segs; io.ingress = io_[p].ingress; io.seg_out = io_[p].seg_out;
       io.ctr_host = io_[p].ctr_host; io.conn_out = io_[p].conn_out;
       io.ctrl = io_[p].ctrl; io.ctrl_rec = io_[p].ctrl_rec; io.xchg = io_[p].xchg;
@@ -516,6 +544,14 @@ class Engine {
     HIPCHECK(hipStreamCreateWithFlags(&s_comp_, hipStreamNonBlocking));
     HIPCHECK(hipStreamCreateWithFlags(&s_h2d_, hipStreamNonBlocking));
     HIPCHECK(hipStreamCreateWithFlags(&s_d2h_, hipStreamNonBlocking));
+    HIPCHECK(hipStreamCreateWithFlags(&s_ing_, hipStreamNonBlocking));
+    for (int p = 0; p < 2; ++p) {
+      HIPCHECK(hipEventCreateWithFlags(&ev_ing_[p], hipEventDisableTiming));
+      HIPCHECK(hipEventCreateWithFlags(&ev_rest_[p], hipEventDisableTiming));
+    }
+    // overlap (world 1): the step's ingest half runs on its own stream, next to the
+    // previous step's routing / delivery half
+    overlap_ = d_.world == 1 && get("overlap", 1) != 0;
     for (int p = 0; p < 2; ++p) {
       HIPCHECK(hipEventCreateWithFlags(&ev_h2d_[p], hipEventDisableTiming));
       HIPCHECK(hipEventCreateWithFlags(&ev_done_[p], hipEventDisableTiming));
@@ -757,6 +793,30 @@ class Engine {
     // overwrite it; waited for only after this step's ingress H2D is queued, so the H2D
     // and the in-flight D2H overlap on their two SDMA engines
     if (copy_mode_ == 3 && sdma_pending_[e]) { HostTimer t(&ht_[1]); sdma_wait(e); }
+    if (overlap_) {
+      // ingest half on s_ing_: after this step's H2D and once parity p's buffers are free
+      // (the routing half of step t-2); the routing half on s_comp_ behind it and behind
+      // the previous step's routing half (stream order), as a single step would run
+      HIPCHECK(hipStreamWaitEvent(s_ing_, ev_h2d_[p], 0));
+      if (rest_issued_[p]) HIPCHECK(hipStreamWaitEvent(s_ing_, ev_rest_[p], 0));
+      {
+        HostTimer t(&ht_[2]);
+        if (!graph_ing_[p]) capture_on(s_ing_, &graph_ing_[p], [&] { launch_ingest(s_ing_, io_[p]); });
+        HIPCHECK(hipGraphLaunch(graph_ing_[p], s_ing_));
+      }
+      HIPCHECK(hipEventRecord(ev_ing_[p], s_ing_));
+      HIPCHECK(hipStreamWaitEvent(s_comp_, ev_ing_[p], 0));
+      if (d2h_issued_[e]) HIPCHECK(hipStreamWaitEvent(s_comp_, ev_d2h_[e], 0));
+      {
+        HostTimer t(&ht_[2]);
+        if (!graph_rest_[p]) capture_on(s_comp_, &graph_rest_[p], [&] { launch_rest(s_comp_, io_[p]); });
+        HIPCHECK(hipGraphLaunch(graph_rest_[p], s_comp_));
+      }
+      HIPCHECK(hipEventRecord(ev_rest_[p], s_comp_));
+      rest_issued_[p] = true;
+      HIPCHECK(hipEventRecord(ev_done_[p], s_comp_));
+      return;
+    }
     HIPCHECK(hipStreamWaitEvent(s_comp_, ev_h2d_[p], 0));
     if (d2h_issued_[e]) HIPCHECK(hipStreamWaitEvent(s_comp_, ev_d2h_[e], 0));
     if (d_.world > 1 && !xfer_set_) throw std::runtime_error("set_xfer_buffers() before the first sharded step");
@@ -892,6 +952,7 @@ class Engine {
     x[2 * WORLD_MAX + d_.my_rank] = x[XC_RECV_AN + d_.my_rank] = n;
     x[3 * WORLD_MAX + d_.my_rank] = x[XC_RECV_AB + d_.my_rank] = (u32)pb;
     launch_ingest(s_comp_, io);
+    launch_marks(s_comp_, io);   // (no commands: the routing half's id floor / link-ack resets)
     launch_route(s_comp_, io, d_.pub_max);
     launch_phase_b(s_comp_, io, /*dispatch=*/false);
     HIPCHECK(hipStreamSynchronize(s_comp_));
@@ -1413,6 +1474,7 @@ class Engine {
 
   void sync() {
     HIPCHECK(hipStreamSynchronize(s_h2d_));
+    HIPCHECK(hipStreamSynchronize(s_ing_));
     HIPCHECK(hipStreamSynchronize(s_comp_));
     HIPCHECK(hipStreamSynchronize(s_d2h_));
   }
@@ -1456,29 +1518,30 @@ class Engine {
     a.tot_slot = slot;
     return a;
   }
-  void launch_scan(hipStream_t s, std::initializer_list<std::pair<const u32*, u32*>> arrs, const u32* n,
-                   u32 nmax, u32 slot, const u32* lo = nullptr) {
+  void launch_scan(hipStream_t s, const DS& d, std::initializer_list<std::pair<const u32*, u32*>> arrs, const u32* n,
+                   u32 nmax, u32 slot, const u32* lo = nullptr, bool ingest = false) {
     const ScanArgs a = scan_args(arrs, n, nmax, slot, lo);
     u32 nb = ceil_div(nmax ? nmax : 1, SCAN_TILE);
-    hipLaunchKernelGGL((k_scan<4, 4>), dim3(nb), dim3(1024), 0, s, a, d_.tot, scan_status_, scan_ctl_, scan_smax_);
+    hipLaunchKernelGGL((k_scan<4, 4>), dim3(nb), dim3(1024), 0, s, a, d.tot, ingest ? scan_status_ing_ : scan_status_,
+                       ingest ? scan_ctl_ing_ : scan_ctl_, scan_smax_);
   }
   // returns index (0/1) of the buffer holding the sorted output
-  u32 radix_sort(hipStream_t s, u32** keys, u32** vals, const u32* n, u32 nmax, u32 bits) {
+  u32 radix_sort(hipStream_t s, const DS& d, u32** keys, u32** vals, const u32* n, u32 nmax, u32 bits) {
     u32 ntiles = ceil_div(nmax, SORT_TILE);
     if (bits > 8 && bits <= 11) {   // one 9..11-bit pass instead of two 8-bit ones
       if (bits == 9) {
         hipLaunchKernelGGL(k_rs_hist<9>, capped(ntiles, 256), dim3(RsNt<9>::v), 0, s, keys[0], n, 0u, d_.hist,
-                           d_.hist_scan, &d_.tot[TS_RS_TICKET], ntiles);
+                           d_.hist_scan, &d.tot[TS_RS_TICKET], ntiles);
         hipLaunchKernelGGL(k_rs_scatter<9>, capped(ntiles, 256), dim3(256), 0, s, keys[0], vals[0], keys[1], vals[1], n,
                            0u, d_.hist_scan, ntiles);
       } else if (bits == 10) {
         hipLaunchKernelGGL(k_rs_hist<10>, capped(ntiles, 256), dim3(RsNt<10>::v), 0, s, keys[0], n, 0u, d_.hist,
-                           d_.hist_scan, &d_.tot[TS_RS_TICKET], ntiles);
+                           d_.hist_scan, &d.tot[TS_RS_TICKET], ntiles);
         hipLaunchKernelGGL(k_rs_scatter<10>, capped(ntiles, 256), dim3(256), 0, s, keys[0], vals[0], keys[1], vals[1],
                            n, 0u, d_.hist_scan, ntiles);
       } else {
         hipLaunchKernelGGL(k_rs_hist<11>, capped(ntiles, 256), dim3(RsNt<11>::v), 0, s, keys[0], n, 0u, d_.hist,
-                           d_.hist_scan, &d_.tot[TS_RS_TICKET], ntiles);
+                           d_.hist_scan, &d.tot[TS_RS_TICKET], ntiles);
         hipLaunchKernelGGL(k_rs_scatter<11>, capped(ntiles, 256), dim3(256), 0, s, keys[0], vals[0], keys[1], vals[1],
                            n, 0u, d_.hist_scan, ntiles);
       }
@@ -1487,7 +1550,7 @@ class Engine {
     u32 src = 0;
     for (u32 shift = 0; shift < bits; shift += 8) {
       hipLaunchKernelGGL(k_rs_hist<8>, capped(ntiles, 256), dim3(RsNt<8>::v), 0, s, keys[src], n, shift, d_.hist, d_.hist_scan,
-                         &d_.tot[TS_RS_TICKET], ntiles);
+                         &d.tot[TS_RS_TICKET], ntiles);
       hipLaunchKernelGGL(k_rs_scatter<8>, capped(ntiles, 256), dim3(256), 0, s, keys[src], vals[src], keys[src ^ 1],
                          vals[src ^ 1], n, shift, d_.hist_scan, ntiles);
       src ^= 1;
@@ -1513,8 +1576,8 @@ class Engine {
     // busy ones, and blocks past the step's segments would still be dispatched one by one
     // after them (the grid is sized for capacity at capture)
     hipLaunchKernelGGL(k_frame_scan, capped(d.seg_max, n_cu_), dim3(FS_NT), 0, s, d);
-    launch_scan(s, {{d.cmd_is_pub, d.cmd_pub_rank}, {d.cmd_is_ack, d.cmd_ack_rank}}, &d.ctr->n_cmds,
-                d.cmd_max, 4);
+    launch_scan(s, d, {{d.cmd_is_pub, d.cmd_pub_rank}, {d.cmd_is_ack, d.cmd_ack_rank}}, &d.ctr->n_cmds,
+                d.cmd_max, 4, nullptr, /*ingest=*/true);
     hipLaunchKernelGGL(k_decode, blocks(d.cmd_max, 256), dim3(256), 0, s, d);
   }
 
@@ -1532,7 +1595,7 @@ class Engine {
     const ScanArgs a = scan_args({{d.pub_nq, d.pub_pair_off}, {d.pub_slot, d.pub_slot_off},
                                   {d.pub_routed, d.pub_routed_rank}, {d.pub_ret_sz, d.pub_ret_off}},
                                  &d.tot[TS_RANGE_HI], d.pub_cap, 0, &d.tot[TS_RANGE_LO]);
-    hipLaunchKernelGGL(k_scan_route, dim3(ceil_div(d.pub_cap ? d.pub_cap : 1, SCAN_TILE)), dim3(1024), 0, s, a, d_.tot,
+    hipLaunchKernelGGL(k_scan_route, dim3(ceil_div(d.pub_cap ? d.pub_cap : 1, SCAN_TILE)), dim3(1024), 0, s, a, d.tot,
                        scan_status_, scan_ctl_, scan_smax_, d);
     hipLaunchKernelGGL(k_route_store, wave_blocks(nmax), dim3(256), 0, s, d);
   }
@@ -1554,7 +1617,7 @@ class Engine {
     u32 nch = d.c_max * d.chpc;
     u32* pk[2] = {d.pair_k[0], d.pair_k[1]};
     u32* pv[2] = {d.pair_v[0], d.pair_v[1]};
-    u32 psrc = radix_sort(s, pk, pv, &d.tot[TS_PAIR_N], d.pair_max, d.q_bits + d.rank_bits);
+    u32 psrc = radix_sort(s, d, pk, pv, &d.tot[TS_PAIR_N], d.pair_max, d.q_bits + d.rank_bits);
     const u32 pbits = d.q_bits + d.rank_bits;
     // single pass (<= 11 key bits): queue starts straight from the digit offsets
     const u32 hs_ntiles = pbits <= 11 ? ceil_div(d.pair_max, SORT_TILE) : 0;
@@ -1579,9 +1642,9 @@ class Engine {
     if (d.c_max <= CONN_LAYOUT_MAX) {
       hipLaunchKernelGGL(k_conn_layout, dim3(1), dim3(1024), 0, s, d);   // + the delivery-size scan
     } else {
-      launch_scan(s, {{d.dv_size, d.dv_off}}, &d.ctr->n_deliv, d.deliv_max, 6);
+      launch_scan(s, d, {{d.dv_size, d.dv_off}}, &d.ctr->n_deliv, d.deliv_max, 6);
       hipLaunchKernelGGL(k_conn_sizes, blocks(d.c_max, 256), dim3(256), 0, s, d);
-      launch_scan(s, {{d.conn_total, d.conn_base}}, nullptr, d.c_max, 7);
+      launch_scan(s, d, {{d.conn_total, d.conn_base}}, nullptr, d.c_max, 7);
       hipLaunchKernelGGL(k_conn_out, blocks(d.c_max, 256), dim3(256), 0, s, d);
     }
     if (d.links) hipLaunchKernelGGL(k_link_bases, dim3(1), dim3(64), 0, s, d);
@@ -1593,7 +1656,7 @@ class Engine {
     hipLaunchKernelGGL(k_post, blocks(pn, 256), dim3(256), 0, s, d, fin);
     if (d.persist) {
       hipLaunchKernelGGL(k_persist_size, blocks(d.persist_max, 256), dim3(256), 0, s, d);
-      launch_scan(s, {{d.ps_size, d.ps_off}}, &d.ctr->n_persist, d.persist_max, TS_PERSIST);
+      launch_scan(s, d, {{d.ps_size, d.ps_off}}, &d.ctr->n_persist, d.persist_max, TS_PERSIST);
       hipLaunchKernelGGL(k_persist_pack, wave_blocks(d.persist_max), dim3(256), 0, s, d);
       hipLaunchKernelGGL(k_host_out, dim3(64), dim3(256), 0, s, d);
     }
@@ -1602,9 +1665,32 @@ class Engine {
   // world == 1: the whole step; world > 1: phase A (ingest, local route, pack)
   void launch_main(hipStream_t s, const DS& d) {
     launch_ingest(s, d);
+    launch_marks(s, d);
     launch_route(s, d, d.pub_max);
     if (d.world > 1) launch_pack(s, d);
     else launch_tail(s, d);
+  }
+
+  // the step's acks / nacks / rejects marked in the channel windows and its publishes
+  // counted for their channels' confirms: the first kernel of the routing half (k_decode
+  // only records them), so an overlapped ingest never touches delivery-side state
+  void launch_marks(hipStream_t s, const DS& d) {
+    const u64 n = d.ack_max > d.pub_max ? d.ack_max : d.pub_max;
+    hipLaunchKernelGGL(k_marks, blocks(n, 256), dim3(256), 0, s, d);
+  }
+  // world == 1 with overlap: the routing / delivery half of the step
+  void launch_rest(hipStream_t s, const DS& d) {
+    launch_marks(s, d);
+    launch_route(s, d, d.pub_max);
+    launch_tail(s, d);
+  }
+  void capture_on(hipStream_t st, hipGraphExec_t* ge, const std::function<void()>& f) {
+    hipGraph_t g;
+    HIPCHECK(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
+    f();
+    HIPCHECK(hipStreamEndCapture(st, &g));
+    HIPCHECK(hipGraphInstantiate(ge, g, nullptr, nullptr, 0));
+    HIPCHECK(hipGraphDestroy(g));
   }
 
   // world > 1, after the all-to-all: import, route against local queues, rest of the step
@@ -1692,6 +1778,22 @@ class Engine {
     const GetOut* get_out_hh = nullptr;
   };
   std::vector<GetReq> pend_gets_;   // Basic.Get requests for the next submit
+  // overlapped steps (world 1)
+  bool overlap_ = false;
+  hipStream_t s_ing_ = nullptr;
+  hipEvent_t ev_ing_[2], ev_rest_[2];
+  bool rest_issued_[2] = {false, false};
+  hipGraphExec_t graph_ing_[2] = {nullptr, nullptr};
+  hipGraphExec_t graph_rest_[2] = {nullptr, nullptr};
+  u64* scan_status_ing_ = nullptr;
+  u32* scan_ctl_ing_ = nullptr;
+  // parity 1's copies of the per-step buffers (parity 0 keeps d_'s)
+  std::vector<std::function<void(DS&)>> par1_;
+  template <class T>
+  void dup(T* DS::*m, const char* name, size_t bytes) {
+    T* p1 = (T*)alloc((std::string(name) + "_p1").c_str(), bytes, false);
+    par1_.push_back([m, p1](DS& io) { io.*m = p1; });
+  }
   GetReq* stage_gets_[2] = {nullptr, nullptr};
   u32 nget_[2] = {0, 0};
   HostIO io_[2];
