@@ -413,6 +413,11 @@ class GpuDataPlane(ControlState):
         while True:
             st, cnt, frames, tag, mid, qpos, persist, exp = self.eng.basic_get(q, s, int(bool(no_ack)), now)
             self._get_consumed.extend((int(m), int(qq), int(qp), 1) for m, qq, qp in exp)
+            if st == 5:   # GET_COLD: the head's body is in the cold store -- read it back
+                store = getattr(self, "cold_store", None)
+                if store is None or not self.cold_in(store):
+                    return None, int(cnt)
+                continue
             if st != 2:   # GET_RETRY: 64 expired entries skipped, more at the head
                 break
         if st == 1:
@@ -526,6 +531,48 @@ class GpuDataPlane(ControlState):
             return 0
         tail = self._u64("log_tail", 0)
         return int(self.eng.spill(int(tail + frac * self.info["log_bytes"]), int(hot)))
+
+    # ---- cold store: the third body tier (store/cold.py; built with spill_bytes > 0)
+    def cold_out(self, store, hot=1 << 16, max_bytes=256 << 20):
+        """Spilled bodies of single-queue non-persistent messages at least ``hot``
+        entries behind their queue's head go to ``store`` (between steps); returns the
+        bytes moved.  Their queues then hold deliveries at the first cold position until
+        ``cold_in`` reads them back."""
+        from ..store.cold import COLD_REC
+        if not self.info.get("spill_bytes"):
+            return 0
+        recs = np.frombuffer(self.eng.cold_pick(int(hot), 1 << 16, int(max_bytes)), COLD_REC).copy()
+        recs = recs[recs["bytes"] > 0]
+        if not len(recs):
+            return 0
+        ring, sb = self._spill_view(), self.info["spill_bytes"]
+        views = [memoryview(ring[int(p) % sb:int(p) % sb + int(n)]) for p, n in zip(recs["pos"], recs["bytes"])]
+        recs["cold"] = store.put_many(views)
+        self.eng.cold_commit(recs)
+        return int(recs["bytes"].sum())
+
+    def cold_in(self, store, window=1 << 15):
+        """Bodies of cold entries within ``window`` positions of their queue's head read
+        back into the spill ring (between steps); returns the bytes moved."""
+        from ..store.cold import COLD_REC
+        if not self.info.get("spill_bytes"):
+            return 0
+        recs = np.frombuffer(self.eng.cold_scan(int(window), 1 << 16), COLD_REC).copy()
+        ring, sb = self._spill_view(), self.info["spill_bytes"]
+        for p, n, c in zip(recs["pos"], recs["bytes"], recs["cold"]):
+            if n:
+                store.get_into(int(c), memoryview(ring[int(p) % sb:int(p) % sb + int(n)]))
+        self.eng.cold_in(recs)
+        return int(recs["bytes"].sum())
+
+    def cold_live(self):
+        return np.frombuffer(self.eng.download("cold_live"), np.int64)
+
+    def _spill_view(self):
+        v = getattr(self, "_spill_hv", None)
+        if v is None:
+            v = self._spill_hv = self.eng.host_view("spill")
+        return v
 
     def spill_used(self):
         """Bytes between the spill ring's tail and head (live + not yet reclaimed)."""

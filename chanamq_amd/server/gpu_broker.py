@@ -117,7 +117,7 @@ class GpuBroker:
                  idle_step_ms=2.0, product="chanamq-amd", version="0.1.0", io="native",
                  ingress_bytes=64 << 20, per_conn_read=256 << 10, mem_high_watermark=None, mem_low_watermark=None,
                  store=None, node=None, reuseport=False, io_threads=4, fe_cfg=None, spill_at=None, spill_hot=1024,
-                 confirm_read=128 << 10):
+                 confirm_read=128 << 10, cold_dir=None, cold=True, cold_hot=1 << 16, cold_window=1 << 15):
         """``io``: "pipeline" = native pipelined front end (csrc/core/frontend.cpp: IO
         threads + a stepper thread keeping two steps in flight, no Python per step),
         "native" = C++ batched gateway polled by a Python step loop (csrc/core/
@@ -170,6 +170,17 @@ class GpuBroker:
         self.spill_at = (int(0.3 * log_bytes) if spill_at is None else int(spill_at)) if sb else 0
         self.spill_hot = spill_hot
         self._last_spill = 0.0
+        # third tier (store/cold.py): once the spill ring is 60% full, spilled bodies of
+        # single-queue non-persistent messages cold_hot+ entries behind their queue's head
+        # go to the cold store on disk; the bodies within cold_window of a head come back
+        self.cold = None
+        if sb and cold:
+            from ..store.cold import ColdStore
+            self.cold = ColdStore(cold_dir)
+            plane.cold_store = self.cold
+        self.cold_hot, self.cold_window = cold_hot, cold_window
+        self._last_cold = self._last_cold_gc = 0.0
+        self._cold_pending = False
         # durable queues x persistent messages -> store (write-behind, confirm gating)
         self.persistence = None
         self.recovered = 0
@@ -292,6 +303,8 @@ class GpuBroker:
         if self._lsock is not None:
             self._lsock.close()
         self.gw = None
+        if self.cold is not None:
+            self.cold.close()
         os.close(self._wake_r)
         os.close(self._wake_w)
 
@@ -1702,6 +1715,8 @@ class GpuBroker:
     def _watermarks(self):
         if self.spill_at:
             self._maybe_spill()
+        if self.cold is not None:
+            self._maybe_cold()
         if not self.mem_high:
             return
         if self.fe is not None and self._fe_stats:
@@ -1737,6 +1752,33 @@ class GpuBroker:
         if moved:
             self.stats["spilled_bytes"] = self.stats.get("spilled_bytes", 0) + moved
             self.stats["spills"] = self.stats.get("spills", 0) + 1
+
+    def _maybe_cold(self):
+        """Cold tier upkeep (at most every 20 ms): page the bodies near the held queues'
+        heads back in, move cold spilled bodies out once the ring is 60% full, and unlink
+        released store segments (every second)."""
+        now = time.monotonic()
+        if now - self._last_cold < 0.02:
+            return
+        self._last_cold = now
+        p = self.plane
+        sb = p.info["spill_bytes"]
+        if self._cold_pending:
+            with self.lock:
+                got = p.cold_in(self.cold, self.cold_window)
+            self.stats["cold_in_bytes"] = self.stats.get("cold_in_bytes", 0) + got
+        if p.spill_used() > 0.6 * sb:
+            with self.lock:
+                moved = p.cold_out(self.cold, self.cold_hot, sb // 4)
+            if moved:
+                self._cold_pending = True
+                self.stats["cold_out_bytes"] = self.stats.get("cold_out_bytes", 0) + moved
+                self.stats["cold_outs"] = self.stats.get("cold_outs", 0) + 1
+        if self._cold_pending and now - self._last_cold_gc > 1.0:
+            self._last_cold_gc = now
+            live = p.cold_live()
+            self.cold.gc(live)
+            self._cold_pending = bool((live > 0).any())
 
     def _set_flow(self, active):
         for c in list(self.conns.values()):

@@ -215,7 +215,10 @@ DEV void release_msg(const DS& d, u32 msg) {
   i32 old = atomicSub(&d.msgs[msg].refcnt, 1);
   if (old == 1) {
     MsgEnt& m = d.msgs[msg];
-    if (m.log_off & SPILL_BIT) {
+    if (m.log_off & COLD_BIT) {
+      atomicAdd((unsigned long long*)&d.cold_live[((m.log_off & ~COLD_BIT) >> COLD_SEG_SHIFT) % COLD_SEGS],
+                (unsigned long long)(-(i64)m.slot_bytes));
+    } else if (m.log_off & SPILL_BIT) {
       spill_free(d, m.log_off, m.slot_bytes);
     } else {
       u64 blk = (m.log_off / d.log_block) % d.n_log_blocks;
@@ -240,8 +243,11 @@ DEV void wave_release(const DS& d, u32 msg, bool valid) {
       freed = true;
       const u64 lo = d.msgs[msg].log_off;
       sb = d.msgs[msg].slot_bytes;
-      spilled = (lo & SPILL_BIT) != 0;
-      if (spilled) spill_free(d, lo, (u32)sb);   // (rare: cold bodies)
+      spilled = (lo & (SPILL_BIT | COLD_BIT)) != 0;
+      if (lo & COLD_BIT)   // (rare: bodies in the cold store)
+        atomicAdd((unsigned long long*)&d.cold_live[((lo & ~COLD_BIT) >> COLD_SEG_SHIFT) % COLD_SEGS],
+                  (unsigned long long)(-sb));
+      else if (spilled) spill_free(d, lo, (u32)sb);   // (rare: cold bodies)
       else blk = (lo / d.log_block) % d.n_log_blocks;
     }
   }
@@ -2998,6 +3004,7 @@ __global__ __launch_bounds__(256) void k_dequeue(DS d) {
   if (d.in->nget) {   // kernel-uniform
     if (tid == 0) {
       const u32 ng = d.in->nget < GET_STEP_MAX ? d.in->nget : GET_STEP_MAX;
+      const u64 clim = d.q_cold_lim[q];   // a cold head waits for the host's page-in (RETRY)
       u64 h = head;
       for (u32 i = 0; i < ng; ++i) {
         const GetReq rq = d.get_req[i];
@@ -3007,7 +3014,7 @@ __global__ __launch_bounds__(256) void k_dequeue(DS d) {
         o.msg_count = 0;
         if (!nodisp && h == tail) {
           o.status = GS_EMPTY;
-        } else if (!nodisp && ngr < RUNS_PER_Q / 2 && rq.chslot < d.c_max * d.chpc) {
+        } else if (!nodisp && h < clim && ngr < RUNS_PER_Q / 2 && rq.chslot < d.c_max * d.chpc) {
           const u32 ch = rq.chslot;
           const u32 sz = deliver_size(d, d.cons_max, d.msgs[ring[h & mask].msg], ch / d.chpc);
           u32 wb, db;
@@ -3046,7 +3053,9 @@ __global__ __launch_bounds__(256) void k_dequeue(DS d) {
     ngr = s_ngr;
   }
   const u32 mall = d.q_cons_n[q];
-  const u64 avail = tail - head;
+  // bodies from q_cold_lim on may be in the cold store: delivered once paged back in
+  const u64 dlim = d.q_cold_lim[q] < tail ? d.q_cold_lim[q] : tail;
+  const u64 avail = dlim > head ? dlim - head : 0;
   if (mall == 0 || avail == 0 || nodisp) {
     if (tid == 0) { d.q_head[q] = head; d.q_nruns[q] = ngr; }
     return;
@@ -3919,6 +3928,15 @@ __global__ __launch_bounds__(64) void k_basic_get(DS d, u32 q, u32 ch, u32 noack
     }
     return;
   }
+  if (head >= d.q_cold_lim[q] && (d.msgs[ring[head & mask].msg].log_off & COLD_BIT)) {
+    if (lane == 0) {   // the host pages the queue's head back in, then asks again
+      d.q_head[q] = head;
+      res->status = GET_COLD;
+      res->msg_count = (u32)(tail - head);
+      res->out_len = 0;
+    }
+    return;
+  }
   const Desc ds = ring[head & mask];
   const MsgEnt m = d.msgs[ds.msg];
   const u32 conn = ch / d.chpc;
@@ -4057,6 +4075,135 @@ __global__ __launch_bounds__(256) void k_spill(DS d, u64 lim, u32 hot, unsigned 
       atomicAdd(moved, (unsigned long long)sz);
     }
   }
+}
+
+// ============================================================================ cold store (between steps)
+// Third body tier (MessageEntity.scala:174-186: idle bodies go to the store and are
+// read back on demand).  Out: k_cold_pick lists spilled bodies of single-queue,
+// non-persistent messages at least `hot` entries behind their queue's head; the host
+// writes them from the pinned ring to the cold store; k_cold_commit switches each
+// MsgEnt to COLD_BIT | store offset, frees its ring bytes and lowers q_cold_lim.
+__global__ __launch_bounds__(256) void k_cold_pick(DS d, u32 hot, ColdRec* out, u32 max_n, u32* n_out,
+                                                   unsigned long long* bytes, u64 max_bytes) {
+  const u32 q = blockIdx.x, lane = lane_id(), w = threadIdx.x >> 6;
+  if (q >= d.q_max || !d.q_active[q] || d.spill_bytes == 0) return;
+  const u64 head = d.q_head[q], tail = d.q_tail[q], mask = d.q_ring_mask[q];
+  const Desc* ring = d.ring + d.q_ring_off[q];
+  for (u64 b = head + hot + (u64)w * 64; b < tail; b += 256) {
+    const u64 i = b + lane;
+    bool want = false;
+    u32 msg = INVALID, sz = 0;
+    u64 lo = 0;
+    if (i < tail) {
+      msg = ring[i & mask].msg;
+      if (msg != INVALID && msg < d.msg_max) {
+        const MsgEnt& m = d.msgs[msg];
+        lo = m.log_off;
+        sz = m.slot_bytes;
+        want = (lo & SPILL_BIT) && !(lo & COLD_BIT) && m.refcnt == 1 && !(m.flags & MF_PERSIST);
+      }
+    }
+    const u32 k = wave_reserve(n_out, want);
+    bool ok = want && k < max_n;
+    if (ok) ok = atomicAdd(bytes, (unsigned long long)sz) + sz <= max_bytes;
+    if (want && k < max_n) {   // (a record of bytes 0 is skipped by the host)
+      ColdRec r;
+      r.msg = ok ? msg : INVALID; r.q = q; r.qpos = i; r.pos = lo & ~SPILL_BIT; r.cold = 0;
+      r.bytes = ok ? sz : 0; r.pad = 0;
+      out[k] = r;
+    }
+    if (__ballot(want && !ok)) break;   // the batch is full
+  }
+}
+
+__global__ void k_cold_commit(DS d, const ColdRec* recs, u32 n) {
+  const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const ColdRec r = recs[i];
+  if (!r.bytes || r.msg >= d.msg_max) return;
+  MsgEnt& m = d.msgs[r.msg];
+  const u64 expect = SPILL_BIT | r.pos;
+  if (atomicCAS((unsigned long long*)&m.log_off, (unsigned long long)expect, (unsigned long long)(COLD_BIT | r.cold)) !=
+      expect)
+    return;
+  spill_free(d, expect, r.bytes);
+  atomicAdd((unsigned long long*)&d.cold_live[(r.cold >> COLD_SEG_SHIFT) % COLD_SEGS], (unsigned long long)r.bytes);
+  atomicMin((unsigned long long*)&d.q_cold_lim[r.q], (unsigned long long)r.qpos);
+}
+
+// In: for every queue held at q_cold_lim, the cold entries among its next `window`
+// positions get a slot in the spill ring (in queue order; the scan stops where the ring
+// is full) and are listed for the host, which reads their bodies into those slots;
+// k_cold_in then switches them back to SPILL_BIT and moves q_cold_lim past the scan
+// (to ~0 when it reached the tail: entries behind the tail are never cold)
+__global__ __launch_bounds__(64) void k_cold_scan(DS d, u32 window, ColdRec* out, u32 max_n, u32* n_out,
+                                                  u64* scan_end) {
+  const u32 q = blockIdx.x, lane = lane_id();
+  if (q >= d.q_max) return;
+  const u64 lim = d.q_cold_lim[q];
+  if (lim == ~0ull) return;
+  const u64 head = d.q_head[q], tail = d.q_tail[q], mask = d.q_ring_mask[q];
+  const Desc* ring = d.ring + d.q_ring_off[q];
+  const u64 start = lim > head ? lim : head;
+  const u64 stop = tail < head + window ? tail : head + window;
+  u64 end = start;
+  for (u64 b = start; b < stop; b += 64) {
+    const u64 i = b + lane;
+    u32 msg = INVALID, sz = 0;
+    u64 lo = 0;
+    bool cold = false;
+    if (i < stop) {
+      msg = ring[i & mask].msg;
+      if (msg != INVALID && msg < d.msg_max) {
+        lo = d.msgs[msg].log_off;
+        sz = d.msgs[msg].slot_bytes;
+        cold = (lo & COLD_BIT) != 0;
+      }
+    }
+    // one ring reservation for the wave's cold bodies, in lane order
+    u32 off = cold ? sz : 0;
+    for (int o = 1; o < 64; o <<= 1) {
+      const u32 y = __shfl_up(off, o, 64);
+      if (lane >= (u32)o) off += y;
+    }
+    const u32 total = __shfl(off, 63, 64);
+    off -= cold ? sz : 0;
+    u64 pos = 0;
+    u32 ok = 1, k0 = 0;
+    const u64 cm = __ballot(cold);
+    const u32 nc = (u32)__popcll(cm);
+    if (lane == 0 && nc) {
+      k0 = atomicAdd(n_out, nc);
+      ok = k0 + nc <= max_n && spill_reserve(d, total, &pos) ? 1u : 0u;
+    }
+    ok = (u32)__shfl((int)ok, 0);
+    pos = shfl64(pos, 0);
+    k0 = (u32)__shfl((int)k0, 0);
+    const u32 k = k0 + (u32)__popcll(cm & lanemask_lt());
+    if (cold && k < max_n) {   // (not ok: a record of bytes 0, skipped by the host)
+      ColdRec r;
+      r.msg = ok ? msg : INVALID; r.q = q; r.qpos = i; r.pos = pos + off; r.cold = lo & ~COLD_BIT;
+      r.bytes = ok ? sz : 0; r.pad = 0;
+      out[k] = r;
+    }
+    if (!ok) break;   // ring (or the batch) full: the rest waits for the next call
+    end = b + 64 < stop ? b + 64 : stop;
+  }
+  if (lane == 0) scan_end[q] = end == tail ? ~0ull : end;
+}
+
+__global__ void k_cold_in(DS d, const ColdRec* recs, u32 n, const u64* scan_end) {
+  const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) {
+    const ColdRec r = recs[i];
+    if (r.bytes && r.msg < d.msg_max) {
+      d.msgs[r.msg].log_off = SPILL_BIT | r.pos;
+      atomicAdd((unsigned long long*)&d.spill_live[(r.pos / d.log_block) % d.n_spill_blocks], (unsigned long long)r.bytes);
+      atomicAdd((unsigned long long*)&d.cold_live[(r.cold >> COLD_SEG_SHIFT) % COLD_SEGS],
+                (unsigned long long)(-(i64)r.bytes));
+    }
+  }
+  if (i < d.q_max && scan_end[i] != 0) d.q_cold_lim[i] = scan_end[i];   // (0: not scanned)
 }
 
 // ============================================================================ requeue (pre-step)

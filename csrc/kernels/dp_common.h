@@ -125,6 +125,13 @@ struct PersistRec { u32 msg; u32 q; u64 qpos; i64 expire_ms; };
 struct Ack { u32 chslot; u32 kind; u64 tag; u32 multiple; u32 requeue; };
 
 #define SPILL_BIT (1ull << 63)   // MsgEnt.log_off: the slot lives in the host spill ring
+// MsgEnt.log_off: the slot lives in the cold store on disk (third body tier, below the
+// spill ring): never rendered -- k_dequeue holds a queue's deliveries at q_cold_lim, the
+// first position that may be cold, until the host pages the bodies back into the ring
+#define COLD_BIT (1ull << 62)
+#define COLD_SEG_SHIFT 30        // cold store segments (files) of 1 GiB
+#define COLD_SEGS 16384          // -> 16 TiB of cold bodies per GPU
+struct ColdRec { u32 msg; u32 q; u64 qpos; u64 pos; u64 cold; u32 bytes; u32 pad; };
 struct MsgEnt {         // message table (one per stored message; body stored once per rank)
   u64 log_off;          // start of slot in body log (| SPILL_BIT: in the host spill ring)
   u64 msg_id;           // snowflake id
@@ -185,7 +192,7 @@ struct ReqItem { u32 q; u32 msg; u64 qpos; i64 expire_ms; };
 // Basic.Get result (k_basic_get -> host-mapped); exp[] = persistent messages of durable
 // queues dropped by the TTL skip (their store rows go, like ConsumedRec kind 1)
 #define GET_EXP_MAX 64
-enum : u32 { GET_EMPTY = 0, GET_OK = 1, GET_RETRY = 2, GET_NO_SPACE = 3, GET_WINDOW_FULL = 4 };
+enum : u32 { GET_EMPTY = 0, GET_OK = 1, GET_RETRY = 2, GET_NO_SPACE = 3, GET_WINDOW_FULL = 4, GET_COLD = 5 };
 struct GetRes {
   u32 status;
   u32 msg_count;        // ready messages left in the queue

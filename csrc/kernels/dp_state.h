@@ -224,6 +224,8 @@ struct DS {
   u64* spill_head;
   u64* spill_tail;
   i64* spill_live;          // live bytes per spill block
+  i64* cold_live;           // [COLD_SEGS] live bytes per cold-store segment (host unlinks freed ones)
+  u64* q_cold_lim;          // [q_max] deliveries stop here (~0: nothing of the queue is cold)
   u64* id_next;             // snowflake virtual sequence position
 
   // ---------------- deliveries

@@ -403,6 +403,13 @@ class Engine {
     d_.spill_live = (i64*)dev("spill_live", 8ull * (d_.n_spill_blocks ? d_.n_spill_blocks : 1));
     d_.spill = d_.spill_bytes ? (u8*)hst("spill", d_.spill_bytes + 4096) : nullptr;
     spill_moved_ = (unsigned long long*)dev("spill_moved", 8);
+    d_.cold_live = (i64*)dev("cold_live", 8ull * COLD_SEGS);
+    cold_recs_ = (ColdRec*)dev("cold_recs", sizeof(ColdRec) * COLD_BATCH);
+    cold_cnt_ = (u32*)dev("cold_cnt", 16);
+    cold_bytes_ = (unsigned long long*)dev("cold_bytes", 8);
+    cold_end_ = (u64*)dev("cold_end", 8ull * d_.q_max);
+    d_.q_cold_lim = (u64*)dev("q_cold_lim", 8ull * d_.q_max);
+    HIPCHECK(hipMemset(d_.q_cold_lim, 0xff, 8ull * d_.q_max));
 
     d_.deliv = (Deliv*)dev("deliv", sizeof(Deliv) * (u64)d_.deliv_max);
     {
@@ -918,6 +925,66 @@ class Engine {
     HIPCHECK(hipMemcpyAsync(&moved, spill_moved_, 8, hipMemcpyDeviceToHost, s_comp_));
     HIPCHECK(hipStreamSynchronize(s_comp_));
     return moved;
+  }
+
+  // ---- cold store (third body tier), between steps; the host moves the bytes
+  // out: candidate records (ColdRec[], bytes 0 = skip) for the host to write to the store
+  py::bytes cold_pick(u32 hot, u32 max_n, u64 max_bytes) {
+    if (!d_.spill_bytes) return py::bytes("");
+    cold_guard("cold_pick");
+    if (max_n > COLD_BATCH) max_n = COLD_BATCH;
+    HIPCHECK(hipMemsetAsync(cold_cnt_, 0, 16, s_comp_));
+    HIPCHECK(hipMemsetAsync(cold_bytes_, 0, 8, s_comp_));
+    hipLaunchKernelGGL(k_cold_pick, dim3(d_.q_max), dim3(256), 0, s_comp_, io_[0], hot, cold_recs_, max_n, cold_cnt_,
+                       cold_bytes_, max_bytes);
+    return cold_fetch(max_n);
+  }
+  // ... the host stored them (ColdRec.cold = store offsets): switch the messages over
+  void cold_commit(py::buffer recs) {
+    const u32 n = cold_upload(recs);
+    if (n) hipLaunchKernelGGL(k_cold_commit, blocks(n, 256), dim3(256), 0, s_comp_, io_[0], cold_recs_, n);
+    HIPCHECK(hipStreamSynchronize(s_comp_));
+  }
+  // in: the cold entries near the heads of the held queues, each with a spill-ring slot
+  py::bytes cold_scan(u32 window, u32 max_n) {
+    if (!d_.spill_bytes) return py::bytes("");
+    cold_guard("cold_scan");
+    if (max_n > COLD_BATCH) max_n = COLD_BATCH;
+    HIPCHECK(hipMemsetAsync(cold_cnt_, 0, 16, s_comp_));
+    HIPCHECK(hipMemsetAsync(cold_end_, 0, 8ull * d_.q_max, s_comp_));
+    hipLaunchKernelGGL(k_cold_scan, dim3(d_.q_max), dim3(64), 0, s_comp_, io_[0], window, cold_recs_, max_n, cold_cnt_,
+                       cold_end_);
+    return cold_fetch(max_n);
+  }
+  // ... the host read their bodies into those slots: back to SPILL_BIT, q_cold_lim moved on
+  void cold_in(py::buffer recs) {
+    const u32 n = cold_upload(recs);
+    const u64 g = n > d_.q_max ? n : d_.q_max;
+    hipLaunchKernelGGL(k_cold_in, blocks(g, 256), dim3(256), 0, s_comp_, io_[0], cold_recs_, n, cold_end_);
+    HIPCHECK(hipStreamSynchronize(s_comp_));
+  }
+  void cold_guard(const char* what) {
+    if (inflight_[0] || inflight_[1]) throw std::runtime_error(std::string(what) + "() between steps only");
+    if (native_x_ && (counts_ready_[0] || counts_ready_[1]))
+      throw std::runtime_error(std::string(what) + "() with an exchange pending");
+    sync();
+  }
+  py::bytes cold_fetch(u32 max_n) {
+    u32 n = 0;
+    HIPCHECK(hipMemcpyAsync(&n, cold_cnt_, 4, hipMemcpyDeviceToHost, s_comp_));
+    HIPCHECK(hipStreamSynchronize(s_comp_));
+    if (n > max_n) n = max_n;
+    std::string out(sizeof(ColdRec) * (size_t)n, '\0');
+    if (n) HIPCHECK(hipMemcpy(&out[0], cold_recs_, out.size(), hipMemcpyDeviceToHost));
+    return py::bytes(out);
+  }
+  u32 cold_upload(py::buffer recs) {
+    py::buffer_info bi = recs.request();
+    const size_t nb = (size_t)bi.size * bi.itemsize;
+    if (nb % sizeof(ColdRec) || nb / sizeof(ColdRec) > COLD_BATCH) throw std::runtime_error("cold: bad ColdRec batch");
+    const u32 n = (u32)(nb / sizeof(ColdRec));
+    if (n) HIPCHECK(hipMemcpy(cold_recs_, bi.ptr, nb, hipMemcpyHostToDevice));
+    return n;
   }
 
   u32 restore(py::buffer desc, py::buffer pay, i64 now_ms) {
@@ -1778,6 +1845,11 @@ class Engine {
     const GetOut* get_out_hh = nullptr;
   };
   std::vector<GetReq> pend_gets_;   // Basic.Get requests for the next submit
+  static constexpr u32 COLD_BATCH = 1u << 16;   // cold records per pick / scan call
+  ColdRec* cold_recs_ = nullptr;
+  u32* cold_cnt_ = nullptr;
+  unsigned long long* cold_bytes_ = nullptr;
+  u64* cold_end_ = nullptr;
   // overlapped steps (world 1)
   bool overlap_ = false;
   hipStream_t s_ing_ = nullptr;
@@ -1878,6 +1950,10 @@ PYBIND11_MODULE(_dataplane, m) {
       .def("set_import", &Engine::set_import, py::arg("recv"), py::arg("stream") = 0)
       .def("restore", &Engine::restore, py::arg("desc"), py::arg("payload"), py::arg("now_ms"))
       .def("spill", &Engine::spill, py::arg("lim"), py::arg("hot"), py::call_guard<py::gil_scoped_release>())
+      .def("cold_pick", &Engine::cold_pick, py::arg("hot"), py::arg("max_n"), py::arg("max_bytes"))
+      .def("cold_commit", &Engine::cold_commit)
+      .def("cold_scan", &Engine::cold_scan, py::arg("window"), py::arg("max_n"))
+      .def("cold_in", &Engine::cold_in)
       .def("basic_get", &Engine::basic_get, py::arg("q"), py::arg("chslot"), py::arg("noack"), py::arg("now_ms"))
       .def("wait_results", &Engine::wait_results)
       .def("egress_copy", &Engine::egress_copy)

@@ -662,3 +662,47 @@ def test_manual_ack_durable_drain_past_record_budget(gpu, tmp_path):
     finally:
         b.stop()
         st.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("io", ["native", "pipeline"])
+def test_backlog_past_hbm_and_host_tiers_goes_to_the_cold_store(gpu, io, tmp_path):
+    """A backlog 6x the HBM body log plus the host spill ring: the log spills to pinned
+    host memory, the full ring moves cold bodies to the cold store on disk (third tier,
+    MessageEntity.scala:174-186), publishers are never paused or nacked; the consumer then
+    gets every message in order and intact -- each cold body read back into the ring
+    just before its queue position is delivered."""
+    import time
+    from chanamq_amd.engine.dataplane import GpuDataPlane
+    from chanamq_amd.server.gpu_broker import GpuBroker
+    cfg = dict(GPU_CFG, log_bytes=32 << 20, log_block=1 << 20, spill_bytes=64 << 20, msg_max=1 << 16)
+    plane = GpuDataPlane(default_queue_capacity=1 << 14, **cfg)
+    b = GpuBroker(plane, idle_step_ms=1.0, io=io, ingress_bytes=8 << 20, mem_high_watermark=0,
+                  cold_dir=str(tmp_path / "cold"), cold_hot=2048, cold_window=1024).start()
+    try:
+        p = conn(b)
+        ch = p.channel()
+        ch.queue_declare("deep")
+        ch.confirm_select()
+        n, size = 36864, 16 << 10   # 576 MB of bodies: 6x (log + ring)
+        for k in range(n):
+            ch.basic_publish("", "deep", k.to_bytes(4, "big") * (size // 4))
+            if k % 64 == 63:
+                assert ch.wait_for_confirms(timeout=60), f"publish {k} nacked"
+                time.sleep(0.001)
+        assert ch.wait_for_confirms(timeout=60)
+        assert not b.blocked and b.stats.get("flow_off", 0) == 0
+        assert b.stats.get("cold_out_bytes", 0) > (256 << 20), b.stats
+        assert b.cold.bytes_on_disk() > (256 << 20)
+        c = conn(b)
+        cc = c.channel()
+        cc.basic_qos(prefetch_count=512)
+        cc.basic_consume("deep", "dc", no_ack=True)
+        got = cc.consume_n(n, timeout=300)
+        assert [int.from_bytes(d.body[:4], "big") for d in got] == list(range(n))
+        assert all(d.body == d.body[:4] * (size // 4) for d in got[::101])
+        assert b.stats.get("cold_in_bytes", 0) > (256 << 20)
+        p.close()
+        c.close()
+    finally:
+        b.stop()
