@@ -33,7 +33,8 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 METRIC = "msgs/sec (whole node) + p50 publish→deliver latency, 1 KB payload, 1/2/4/8 GPUs"
 
 
-def build_workload(dp, rank, producers, queues, body, chunk, blocks, cons_base, shards=1, kind="topic"):
+def build_workload(dp, rank, producers, queues, body, chunk, blocks, cons_base, shards=1, kind="topic", consume=True,
+                   qcap=None):
     """``shards`` > 1: the replicated topology of a sharded broker (every rank declares
     every queue; queue bench.q.{r}.{i} is placed on rank r and consumed there).
     kind "topic" = config 2 (``queues`` per rank, one key pattern each); "fanout" =
@@ -52,7 +53,7 @@ def build_workload(dp, rank, producers, queues, body, chunk, blocks, cons_base, 
             qn = f"bench.q.{r}.{i}"
             if shards > 1:
                 dp.shard_map.place(vh, qn, r)
-            dp.declare_queue(vh, qn, capacity=1 << 14 if kind == "fanout" else 1 << 20)
+            dp.declare_queue(vh, qn, capacity=qcap or (1 << 14 if kind == "fanout" else 1 << 20))
             key = {"topic": f"bench.{r}.{i}.*", "fanout": "", "storm": f"bench.{r}.{i}"}[kind]
             dp.bind(vh, qn, xname, key)
     for p in range(producers):
@@ -64,7 +65,8 @@ def build_workload(dp, rank, producers, queues, body, chunk, blocks, cons_base, 
         dp.open_channel(c, 1)
         if kind == "storm":
             dp.qos(c, 1, prefetch_count=512)
-        dp.consume(c, 1, vh, f"bench.q.{rank}.{i}", f"ctag-{i}", no_ack=kind != "storm")
+        if consume:
+            dp.consume(c, 1, vh, f"bench.q.{rank}.{i}", f"ctag-{i}", no_ack=kind != "storm")
     # one message on the wire is ~1.08 KB; each producer gets `blocks` chunks of ~chunk bytes
     probe = publish_stream(1, xname, lambda i: f"bench.{rank}.0.x0", body)
     per_prod = max(1, (chunk * blocks) // len(probe))
