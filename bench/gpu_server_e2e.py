@@ -221,7 +221,9 @@ def run_one(core, name, spec, io, io_threads, seconds, rate=0.0, lg_threads=12, 
              front_end={k: fes.get(k) for k in ("steps", "idle_steps", "gather_segs", "io_phase_s", "wait_s",
                                                 "submit_s", "rx_bytes", "tx_bytes", "held_steps", "published",
                                                 "delivered", "routed", "dropped_nomem", "ring_full", "unroutable",
-                                                "expired", "ctrl", "live_msgs", "live_bytes", "log_used")},
+                                                "expired", "ctrl", "live_msgs", "live_bytes", "log_used",
+                                                "h_period_us_log2", "h_io_us_log2", "h_submit_us_log2",
+                                                "h_wait_us_log2", "max_period_s", "max_io_s", "max_wait_s")},
              flow_off_server=st.get("flow_off", 0),
              getters=(dict(n=n_getters, gets_ok=sum(g[0] for g in gout), gets_empty=sum(g[1] for g in gout),
                            gets_per_s=sum(g[0] + g[1] for g in gout) / max(1e-9, max((g[2] for g in gout), default=1)),

@@ -281,6 +281,11 @@ PYBIND11_MODULE(_core, m) {
              o["xchg_s"] = s.xchg_s; o["xchg_steps"] = s.xchg_steps; o["syncs"] = s.syncs;
              o["xfails"] = s.xfails; o["flush_steps"] = s.flush_steps;
              o["lat_hist"] = std::vector<u64>(s.lat_hist, s.lat_hist + 32);
+             o["h_period_us_log2"] = std::vector<u64>(s.h_period, s.h_period + 32);
+             o["h_io_us_log2"] = std::vector<u64>(s.h_io, s.h_io + 32);
+             o["h_submit_us_log2"] = std::vector<u64>(s.h_submit, s.h_submit + 32);
+             o["h_wait_us_log2"] = std::vector<u64>(s.h_wait, s.h_wait + 32);
+             o["max_period_s"] = s.max_period_s; o["max_io_s"] = s.max_io_s; o["max_wait_s"] = s.max_wait_s;
              return o;
            });
   py::class_<PersistWorker>(m, "PersistWorker")

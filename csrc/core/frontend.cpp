@@ -861,6 +861,14 @@ void Frontend::io_phase(std::vector<Scatter*>& scat, bool gather, bool async) {
   out_.clear();
 }
 
+// log2 µs bin of a duration in seconds (FeStats.h_*)
+static void hbin(u64* h, double s) {
+  u64 us = (u64)(s * 1e6);
+  int k = 0;
+  while (us > 1 && k < 31) { us >>= 1; ++k; }
+  h[k]++;
+}
+
 // ============================================================================ stepper
 void Frontend::finish_oldest(std::deque<Inflight>& inflight) {
   if (pend_valid_ && !stash_pend(true)) return;   // its egress is written by the next IO phase
@@ -1006,6 +1014,8 @@ void Frontend::finish_oldest(std::deque<Inflight>& inflight) {
     stats_.live_msgs = c.n_live_msgs;
     stats_.log_used = c.log_head - c.log_tail;
     stats_.wait_s += w;
+    hbin(stats_.h_wait, w);
+    stats_.max_wait_s = std::max(stats_.max_wait_s, w);
     for (int k = 0; k < 32; ++k) stats_.lat_hist[k] += c.lat_hist[k];
     if (needs_commit) stats_.held_steps++;
   }
@@ -1094,10 +1104,20 @@ void Frontend::stepper() {
       if (!check(p)) break;
       {
         std::lock_guard<std::mutex> g(stats_mu_);
-        stats_.submit_s += secs_since(t1);
+        const double ts = secs_since(t1);
+        stats_.submit_s += ts;
         stats_.io_phase_s += tio;
         stats_.gather_segs += segs.size();
         if (segs.empty() && !last_busy_) stats_.idle_steps++;
+        hbin(stats_.h_submit, ts);
+        hbin(stats_.h_io, tio);
+        stats_.max_io_s = std::max(stats_.max_io_s, tio);
+        if (last_submit_) {
+          const double per = (t1 - last_submit_) * 1e-9;
+          hbin(stats_.h_period, per);
+          stats_.max_period_s = std::max(stats_.max_period_s, per);
+        }
+        last_submit_ = t1;
       }
       f.p = p;
       f.step = ++step_no_;

@@ -103,6 +103,11 @@ struct FeStats {
   double io_phase_s = 0, wait_s = 0, submit_s = 0;
   double xchg_s = 0;          // sharded: host time in the per-step exchange
   u64 xchg_steps = 0, syncs = 0, xfails = 0, flush_steps = 0;
+  // per-stage latency histograms (bin k: [2^k, 2^(k+1)) µs) -- where a TCP message's time
+  // goes: the stepper's period between submits, its IO phase (write the older step's
+  // egress, gather the next one), the submit call, and its wait for a step's results
+  u64 h_period[32] = {}, h_io[32] = {}, h_submit[32] = {}, h_wait[32] = {};
+  double max_period_s = 0, max_io_s = 0, max_wait_s = 0;
 };
 
 struct FeConn;
@@ -272,6 +277,7 @@ class Frontend {
   FeStats stats_;
   std::atomic<u64> rx_bytes_{0}, tx_bytes_{0};
   u64 step_no_ = 0;
+  i64 last_submit_ = 0;   // (stats: the stepper's period between submits)
   std::atomic<bool> failed_{false};   // read by healthy() (heartbeat thread)
 
   // sharded broker
