@@ -27,17 +27,22 @@ def parse_persist(raw):
     """Packed persist records (PersistHdr + [ex][rk][props][body]) -> [(msg_id, ts_ms, q,
     qpos, expire_ms, ex, rk, props, body)]."""
     raw = np.frombuffer(raw, np.uint8) if isinstance(raw, (bytes, bytearray)) else raw
-    out, off = [], 0
+    hdrs, data_of, off = [], {}, 0
     while off + PERSIST_HDR.itemsize <= len(raw):
         h = raw[off:off + PERSIST_HDR.itemsize].view(PERSIST_HDR)[0]
         b = off + PERSIST_HDR.itemsize
         el, rl, pl, bl = int(h["ex_len"]), int(h["rk_len"]), int(h["props_len"]), int(h["body_len"])
-        data = bytes(raw[b:b + el + rl + pl + bl])
-        out.append((int(h["msg_id"]), int(h["ts_ms"]), int(h["q"]), int(h["qpos"]), int(h["expire_ms"]),
-                    data[:el], data[el:el + rl], data[el + rl:el + rl + pl], data[el + rl + pl:]))
+        if int(h["size"]) > PERSIST_HDR.itemsize:   # a message's bytes ride its first record only
+            data_of[int(h["msg_id"])] = bytes(raw[b:b + el + rl + pl + bl])
+        hdrs.append((h, el, rl, pl))
         if int(h["size"]) <= 0:
             break
         off += int(h["size"])
+    out = []
+    for h, el, rl, pl in hdrs:
+        data = data_of.get(int(h["msg_id"]), b"")
+        out.append((int(h["msg_id"]), int(h["ts_ms"]), int(h["q"]), int(h["qpos"]), int(h["expire_ms"]),
+                    data[:el], data[el:el + rl], data[el + rl:el + rl + pl], data[el + rl + pl:]))
     return out
 
 

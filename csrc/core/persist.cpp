@@ -97,14 +97,26 @@ void PersistWorker::loop() {
 }
 
 void PersistWorker::apply(const Batch& b) {
-  // ---- enqueues of persistent messages into durable queues: held as this group's rows
+  // ---- enqueues of persistent messages into durable queues: held as this group's rows.
+  // A message's bytes ride only its first record of the step (the others are headers,
+  // size == sizeof(PersistHdr)): find them first
   const u8* p = (const u8*)b.persist.data();
   size_t off = 0, n = b.persist.size();
+  std::unordered_map<i64, const char*> bytes_of;
   while (off + sizeof(PersistHdr) <= n) {
     PersistHdr h;
     memcpy(&h, p + off, sizeof h);
     if (h.size < sizeof(PersistHdr) || off + h.size > n) break;
-    const char* d = (const char*)p + off + sizeof(PersistHdr);
+    if (h.size > sizeof(PersistHdr)) bytes_of.emplace(h.msg_id, (const char*)p + off + sizeof(PersistHdr));
+    off += h.size;
+  }
+  off = 0;
+  while (off + sizeof(PersistHdr) <= n) {
+    PersistHdr h;
+    memcpy(&h, p + off, sizeof h);
+    if (h.size < sizeof(PersistHdr) || off + h.size > n) break;
+    auto bo = bytes_of.find(h.msg_id);
+    const char* d = bo != bytes_of.end() ? bo->second : (const char*)p + off + sizeof(PersistHdr);
     off += h.size;
     if (h.q >= qid_.size() || qid_[h.q].empty()) continue;
     auto rf = refs_.find(h.msg_id);

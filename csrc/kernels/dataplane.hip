@@ -3795,8 +3795,13 @@ __global__ void k_persist_size(DS d) {
   u32 n = d.ctr->n_persist;
   if (n > d.persist_max) n = d.persist_max;
   if (i >= n) return;
-  const MsgEnt& m = d.msgs[d.prec[i].msg];
-  d.ps_size[i] = (u32)sizeof(PersistHdr) + ((m.ex_len + m.rk_len + m.props_len + m.body_len + 7u) & ~7u);
+  // a message's bytes travel once per step: with its first record (claimed through the
+  // otherwise unused MsgEnt.pad, zeroed when the message is stored); its other queues'
+  // records are headers only (PersistHdr.size == sizeof(PersistHdr))
+  MsgEnt& m = d.msgs[d.prec[i].msg];
+  const u32 bytes = (m.ex_len + m.rk_len + m.props_len + m.body_len + 7u) & ~7u;
+  const bool first = atomicCAS(&m.pad, 0u, 1u) == 0u;
+  d.ps_size[i] = (u32)sizeof(PersistHdr) + (first ? bytes : 0u);
 }
 
 __global__ __launch_bounds__(256) void k_persist_pack(DS d) {
@@ -3826,6 +3831,7 @@ __global__ __launch_bounds__(256) void k_persist_pack(DS d) {
       h.size = sz;
       *(PersistHdr*)o = h;
     }
+    if (sz == sizeof(PersistHdr)) continue;   // header only: the bytes ride the message's first record
     u32 meta = m.ex_len + m.rk_len + m.props_len;
     wave_copy(o + sizeof(PersistHdr), slot, meta);
     wave_copy(o + sizeof(PersistHdr) + meta, slot + m.body_off, m.body_len);

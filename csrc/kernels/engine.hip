@@ -157,6 +157,14 @@ class Engine {
     // receive payload: the peers' publishes + (links) their link deliveries, each bounded
     // by the sender's egress budget
     d_.import_bytes = d_.xfer_bytes + (links_ ? (u64)(d_.world - 1) * d_.egress_cap : 0);
+    if (d_.persist) {
+      // a step's persist records: one 48-B header per enqueue (<= pair_max) and each
+      // message's bytes once (<= the step's work buffer + what it imported), so the
+      // packed buffer can never overflow (no fail-closed stop on a burst)
+      const u64 need = d_.work_cap + d_.xfer_bytes + 56ull * d_.pair_max + 4096;
+      if (d_.persist_bytes < need) d_.persist_bytes = need;
+      if (d_.persist_max < d_.pair_max) d_.persist_max = d_.pair_max;
+    }
     if (d_.import_bytes + 8192 > (4ull << 30))
       throw std::runtime_error("import buffer must stay below 4 GiB (u32 offsets): lower ingress_cap / egress_cap");
     d_.ctrl_cap = get("ctrl_cap", 4ull << 20);
