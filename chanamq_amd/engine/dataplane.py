@@ -538,15 +538,17 @@ class GpuDataPlane(ControlState):
         return int(self.eng.spill(int(tail + frac * self.info["log_bytes"]), int(hot)))
 
     # ---- cold store: the third body tier (store/cold.py; built with spill_bytes > 0)
-    def cold_out(self, store, hot=1 << 16, max_bytes=256 << 20):
-        """Spilled bodies of single-queue non-persistent messages at least ``hot``
-        entries behind their queue's head go to ``store`` (between steps); returns the
-        bytes moved.  Their queues then hold deliveries at the first cold position until
+    def cold_out(self, store, hot=1 << 16, max_bytes=256 << 20, frac=0.5):
+        """Spilled bodies of single-queue non-persistent messages in the oldest ``frac``
+        of the spill ring (the ring frees from its tail) go to ``store`` (between steps),
+        but not the first ``hot`` entries of a queue with consumers; returns the bytes
+        moved.  Their queues then hold deliveries at the first cold position until
         ``cold_in`` reads them back."""
         from ..store.cold import COLD_REC
         if not self.info.get("spill_bytes"):
             return 0
-        recs = np.frombuffer(self.eng.cold_pick(int(hot), 1 << 16, int(max_bytes)), COLD_REC).copy()
+        lim = self._u64("spill_tail", 0) + int(frac * self.info["spill_bytes"])
+        recs = np.frombuffer(self.eng.cold_pick(int(hot), int(lim), 1 << 16, int(max_bytes)), COLD_REC).copy()
         recs = recs[recs["bytes"] > 0]
         if not len(recs):
             return 0

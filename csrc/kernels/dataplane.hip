@@ -4089,13 +4089,17 @@ __global__ __launch_bounds__(256) void k_spill(DS d, u64 lim, u32 hot, unsigned 
 // non-persistent messages at least `hot` entries behind their queue's head; the host
 // writes them from the pinned ring to the cold store; k_cold_commit switches each
 // MsgEnt to COLD_BIT | store offset, frees its ring bytes and lowers q_cold_lim.
-__global__ __launch_bounds__(256) void k_cold_pick(DS d, u32 hot, ColdRec* out, u32 max_n, u32* n_out,
+// Candidates are taken from the oldest part of the ring (slot position below `lim`, like
+// k_spill's log limit): the ring is a FIFO, so only freeing its tail end makes room; a
+// queue with consumers keeps its first `hot` entries resident.
+__global__ __launch_bounds__(256) void k_cold_pick(DS d, u32 hot, u64 lim, ColdRec* out, u32 max_n, u32* n_out,
                                                    unsigned long long* bytes, u64 max_bytes) {
   const u32 q = blockIdx.x, lane = lane_id(), w = threadIdx.x >> 6;
   if (q >= d.q_max || !d.q_active[q] || d.spill_bytes == 0) return;
   const u64 head = d.q_head[q], tail = d.q_tail[q], mask = d.q_ring_mask[q];
   const Desc* ring = d.ring + d.q_ring_off[q];
-  for (u64 b = head + hot + (u64)w * 64; b < tail; b += 256) {
+  const u64 skip = d.q_cons_n[q] ? hot : 0;
+  for (u64 b = head + skip + (u64)w * 64; b < tail; b += 256) {
     const u64 i = b + lane;
     bool want = false;
     u32 msg = INVALID, sz = 0;
@@ -4106,7 +4110,8 @@ __global__ __launch_bounds__(256) void k_cold_pick(DS d, u32 hot, ColdRec* out, 
         const MsgEnt& m = d.msgs[msg];
         lo = m.log_off;
         sz = m.slot_bytes;
-        want = (lo & SPILL_BIT) && !(lo & COLD_BIT) && m.refcnt == 1 && !(m.flags & MF_PERSIST);
+        want = (lo & SPILL_BIT) && !(lo & COLD_BIT) && (lo & ~SPILL_BIT) < lim && m.refcnt == 1 &&
+               !(m.flags & MF_PERSIST);
       }
     }
     const u32 k = wave_reserve(n_out, want);

@@ -937,14 +937,14 @@ class Engine {
 
   // ---- cold store (third body tier), between steps; the host moves the bytes
   // out: candidate records (ColdRec[], bytes 0 = skip) for the host to write to the store
-  py::bytes cold_pick(u32 hot, u32 max_n, u64 max_bytes) {
+  py::bytes cold_pick(u32 hot, u64 lim, u32 max_n, u64 max_bytes) {
     if (!d_.spill_bytes) return py::bytes("");
     cold_guard("cold_pick");
     if (max_n > COLD_BATCH) max_n = COLD_BATCH;
     HIPCHECK(hipMemsetAsync(cold_cnt_, 0, 16, s_comp_));
     HIPCHECK(hipMemsetAsync(cold_bytes_, 0, 8, s_comp_));
-    hipLaunchKernelGGL(k_cold_pick, dim3(d_.q_max), dim3(256), 0, s_comp_, io_[0], hot, cold_recs_, max_n, cold_cnt_,
-                       cold_bytes_, max_bytes);
+    hipLaunchKernelGGL(k_cold_pick, dim3(d_.q_max), dim3(256), 0, s_comp_, io_[0], hot, lim, cold_recs_, max_n,
+                       cold_cnt_, cold_bytes_, max_bytes);
     return cold_fetch(max_n);
   }
   // ... the host stored them (ColdRec.cold = store offsets): switch the messages over
@@ -1958,7 +1958,7 @@ PYBIND11_MODULE(_dataplane, m) {
       .def("set_import", &Engine::set_import, py::arg("recv"), py::arg("stream") = 0)
       .def("restore", &Engine::restore, py::arg("desc"), py::arg("payload"), py::arg("now_ms"))
       .def("spill", &Engine::spill, py::arg("lim"), py::arg("hot"), py::call_guard<py::gil_scoped_release>())
-      .def("cold_pick", &Engine::cold_pick, py::arg("hot"), py::arg("max_n"), py::arg("max_bytes"))
+      .def("cold_pick", &Engine::cold_pick, py::arg("hot"), py::arg("lim"), py::arg("max_n"), py::arg("max_bytes"))
       .def("cold_commit", &Engine::cold_commit)
       .def("cold_scan", &Engine::cold_scan, py::arg("window"), py::arg("max_n"))
       .def("cold_in", &Engine::cold_in)

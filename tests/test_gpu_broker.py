@@ -624,7 +624,7 @@ def test_manual_ack_durable_drain_past_record_budget(gpu, tmp_path):
     core = load()
     st = core.Store()
     st.open(str(tmp_path / "store"), True)
-    cfg = dict(GPU_CFG, ucap=4096, deliv_max=256, persist_max=1024)
+    cfg = dict(GPU_CFG, ucap=4096, deliv_max=256, persist_max=1024, cmd_max=1024)   # pair_max 4096
     plane = GpuDataPlane(default_queue_capacity=1 << 14, persist=1, persist_bytes=16 << 20, restore_max=1024,
                          restore_bytes=8 << 20, **cfg)
     pm = plane.info["persist_max"]
