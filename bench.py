@@ -184,6 +184,9 @@ def main():
                          "the collective overlaps the next step); 0 = synchronous")
     ap.add_argument("--mode", choices=["sharded", "independent"], default="sharded",
                     help="N>1: one sharded broker (cross-GPU routing over RCCL) or N unconnected shards")
+    ap.add_argument("--prefetch", type=int, default=1,
+                    help="1: queue step t+1's ingress H2D right after submitting step t (the copy engine never "
+                         "idles between steps; the step's latency clock starts there); 0: H2D at submit")
     ap.add_argument("--xchg", choices=["native", "torch"], default="native",
                     help="N>1 sharded: the engine's own exchange -- grouped RCCL send/recv on its exchange "
                          "stream, counts through host shared memory (the code the sharded server runs; "
@@ -255,7 +258,8 @@ def main():
     step_i = 0
     submit = dp.submit_lockstep if native else dp.submit_raw
 
-    sub_t = {}      # step index -> host time its ingress was handed to the GPU (submit)
+    sub_t = {}      # step index -> host time its ingress was handed to the GPU (submit / prefetch)
+    pre = set()     # steps whose payload H2D is already queued (prefetch)
     lat_w = []      # (publish->deliver seconds, deliveries) of the timed steps
 
     def run(n, measure=False):
@@ -294,9 +298,11 @@ def main():
                     if t0 is not None:
                         lat_w.append((t - t0, int(lh[k])))
 
-        for _ in range(n):
+        for i in range(n):
             b = step_i % args.blocks
-            sub_t[step_i] = time.perf_counter()
+            if step_i not in pre:   # (a prefetched step's clock started when its bytes were queued)
+                sub_t[step_i] = time.perf_counter()
+            pre.discard(step_i)
             if storm:   # ack-all each step, nack-all-requeue every 4th: a redelivery storm
                 cs = extra["nack" if step_i % 4 == 3 else "ack"][b]
                 if flow["paused"]:
@@ -308,6 +314,11 @@ def main():
             else:
                 pending.append((submit(segs[b], base + offs[b], blens[b]), step_i))
             step_i += 1
+            if args.prefetch and i < n - 1:
+                nb = step_i % args.blocks
+                sub_t[step_i] = time.perf_counter()
+                if dp.prefetch(base + offs[nb], blens[nb]):
+                    pre.add(step_i)
             if len(pending) > 1:
                 t, s = pending.pop(0)
                 account(dp.finish(t, collect=False, wait_egress=False), s)
@@ -419,6 +430,7 @@ def main():
                       if storm else None),
             "cross_gpu_bytes_per_s": (dp.exchanger.bytes_sent * world / t) if shards > 1 and not native else None,
             "exchange": args.xchg if shards > 1 else None,
+            "prefetch": bool(args.prefetch), "chunk_bytes_per_producer": args.chunk,
             "post_soak_s": args.soak_s,
         }
         print(json.dumps(out), flush=True)

@@ -13,8 +13,8 @@ _SRC = os.path.join(_ROOT, "csrc", "core")
 _EXT = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
 EXT_PATH = os.path.join(_HERE, "_core" + _EXT)
 SOURCES = ["codec.cpp", "store.cpp", "broker.cpp", "loadgen.cpp", "gateway.cpp", "frontend.cpp", "persist.cpp",
-           "tls_proxy.cpp",            "bindings.cpp"]
-HEADERS = ["codec.hpp", "store.hpp", "broker.hpp", "loadgen.hpp", "gateway.hpp", "frontend.hpp", "persist.hpp", "tls_proxy.hpp",
+           "bodylog.cpp", "tls_proxy.cpp",            "bindings.cpp"]
+HEADERS = ["codec.hpp", "store.hpp", "broker.hpp", "loadgen.hpp", "gateway.hpp", "frontend.hpp", "persist.hpp", "bodylog.hpp", "flatmap.hpp", "tls_proxy.hpp",
            "../kernels/step_abi.h"]
 
 

@@ -829,6 +829,12 @@ class GpuDataPlane(ControlState):
                     self.submit_b(recv)
         return (p, len(segs), t0)
 
+    def prefetch(self, payload_ptr, payload_len):
+        """Queue the NEXT step's ingress payload H2D now (overlapped single-GPU engine): it
+        crosses PCIe while the current steps run; that step must then be submitted with the
+        same payload.  Returns False when not applicable (nothing queued)."""
+        return bool(self.eng.prefetch(int(payload_ptr), int(payload_len)))
+
     def submit_lockstep(self, segs, payload_ptr, payload_len, now_ms=None):
         """One lockstep step of a sharded plane on the engine's native exchange (RCCL over
         xGMI, or host shared memory), in the order the native front end's sharded stepper

@@ -345,8 +345,12 @@ class GpuBroker:
         pauses the stepper) only while it handles them; steps never wait for Python."""
         fe = self.fe
         last_stats = 0.0
+        # with body tiers the movers must keep pace with the publishers (a full HBM log and
+        # spill ring would nack): 5 ms upkeep instead of 50
+        tiers = bool(self.spill_at) or self.cold is not None
+        period = 0.005 if tiers else 0.05
         while self._running:
-            evs = fe.poll_events(20)
+            evs = fe.poll_events(5 if tiers else 20)
             persist = [e for e in evs if e[0] == FE_PERSIST]
             dev = [e for e in evs if e[0] != FE_PERSIST]
             if dev or self._tx_pending:
@@ -366,7 +370,7 @@ class GpuBroker:
             if persist:
                 self._persist_native(persist)
             now = time.monotonic()
-            if now - last_stats > 0.05:
+            if now - last_stats > period:
                 last_stats = now
                 self._sync_fe_stats()
                 self._watermarks()
@@ -1471,7 +1475,7 @@ class GpuBroker:
         pending, self._deferred = self._deferred, {}
         for seq, (conn, ch, reply, m) in pending.items():
             c = self.conns.get(conn)
-            if c is None or c.state != "open":
+            if c is None or c.state not in ("open", "bigwait"):
                 if hasattr(reply, "abandon"):   # e.g. a link opened for a connection now gone
                     reply.abandon()
                 continue
@@ -1744,7 +1748,7 @@ class GpuBroker:
             lc = getattr(self.plane, "last_counters", None) or {}
             logu = lc.get("log_head", 0) - lc.get("log_tail", 0)
         now = time.monotonic()
-        if logu < self.spill_at or now - self._last_spill < 0.05:
+        if logu < self.spill_at or now - self._last_spill < 0.01:
             return
         self._last_spill = now
         with self.lock:
@@ -1754,11 +1758,11 @@ class GpuBroker:
             self.stats["spills"] = self.stats.get("spills", 0) + 1
 
     def _maybe_cold(self):
-        """Cold tier upkeep (at most every 20 ms): page the bodies near the held queues'
+        """Cold tier upkeep (at most every 10 ms): page the bodies near the held queues'
         heads back in, move cold spilled bodies out once the ring is 60% full, and unlink
         released store segments (every second)."""
         now = time.monotonic()
-        if now - self._last_cold < 0.02:
+        if now - self._last_cold < 0.01:
             return
         self._last_cold = now
         p = self.plane

@@ -89,6 +89,16 @@ PYBIND11_MODULE(_core, m) {
              d["failures"] = c.failures; d["last_error"] = c.last_error;
              return d;
            })
+      .def("configure_body_log", &Store::configureBodyLog, py::arg("stripes"), py::arg("seg_bytes"))
+      .def("has_body_log", &Store::hasBodyLog)
+      .def("body_stats", [](Store& s) {
+             BodyLog::Stats b = s.bodyStats();
+             py::dict d;
+             d["written"] = b.written; d["records"] = b.records; d["live_bytes"] = b.live_bytes;
+             d["live_records"] = b.live_records; d["disk_bytes"] = b.disk_bytes; d["segments"] = b.segments;
+             d["reclaimed"] = b.reclaimed; d["bad_reads"] = b.bad_reads; d["write_s"] = b.write_s; d["sync_s"] = b.sync_s;
+             return d;
+           })
       .def("deleted_queue_ids", &Store::deletedQueueIds)
       .def("select_deleted_queue", [](Store& s, std::string q) -> py::object {
              QueueMetaDeletedRow meta;
@@ -301,6 +311,7 @@ PYBIND11_MODULE(_core, m) {
       .def("stats", [](PersistWorker& w) {
              py::dict o;
              o["rows"] = w.rows(); o["commits"] = w.commits(); o["body_bytes"] = w.bytes(); o["busy_s"] = w.busy_s();
+             o["apply_s"] = w.apply_s(); o["flush_s"] = w.flush_s(); o["sync_s"] = w.sync_s();
              return o;
            });
   py::class_<TlsProxy>(m, "TlsProxy")

@@ -1095,6 +1095,11 @@ void Frontend::stepper() {
     idle_tick_ = false;
     bool submitted = false;
     if (submit) {
+      // the gathered bytes start crossing PCIe now, while the oldest step finishes (the
+      // engine orders the copy behind the last reader of that ingress buffer on the GPU)
+      if (inflight.size() >= 2 && used && api_->prefetch &&
+          !check(api_->prefetch(api_->eng, arena_[arena_i_], used)))
+        break;
       if (inflight.size() >= 2) finish_oldest(inflight);
       if (failed_) break;
       i64 t1 = now_ns();

@@ -31,6 +31,7 @@
 #include <vector>
 
 #include "../kernels/step_abi.h"
+#include "flatmap.hpp"
 #include "store.hpp"
 
 namespace cmq {
@@ -52,6 +53,10 @@ class PersistWorker {
   u64 commits() const { return commits_; }
   u64 bytes() const { return bytes_; }
   double busy_s() const { return busy_s_; }
+  // busy time split: applying the batches / writing the group's rows / WAL write + fsync
+  double apply_s() const { return apply_s_; }
+  double flush_s() const { return flush_s_; }
+  double sync_s() const { return sync_s_; }
 
  private:
   struct Batch { u64 step; std::string persist, consumed; };
@@ -61,13 +66,15 @@ class PersistWorker {
     bool operator==(const RowKey& o) const { return q == o.q && id == o.id; }
   };
   struct RowHash {
-    size_t operator()(const RowKey& k) const { return std::hash<u64>()((u64)k.id * 0x9E3779B97F4A7C15ull ^ k.q); }
+    size_t operator()(const RowKey& k) const { return HashI64()(k.id ^ ((i64)k.q << 48)); }
   };
-  struct Born { const char* d; PersistHdr h; bool unack; };   // row of this group, not yet written
-  struct BornMsg { const char* d; PersistHdr h; int refs; };
+  struct Born { PersistHdr h; bool unack; };                  // row of this group, not yet written
+  struct BornMsg { const char* rec; PersistHdr h; int refs; };  // rec: the record holding the bytes
   void loop();
   void apply(const Batch& b);
   void flush_born();
+  u32 gq(u32 slot);
+  void op(u8 kind, u32 q, i64 offset, i64 msgid, i32 size);
 
   Store* st_;
   std::function<void(u64)> commit_cb_;
@@ -80,12 +87,21 @@ class PersistWorker {
   std::mutex qid_mu_;
   std::vector<std::string> qid_;                      // by queue slot
   std::unordered_map<std::string, u32> slot_of_;      // queue id -> slot
-  std::unordered_map<i64, int> refs_;                 // msg id -> durable queue rows (in the store)
-  std::unordered_map<RowKey, Row, RowHash> rows_by_;  // (queue slot, msg id) -> stored row
-  std::unordered_map<RowKey, Born, RowHash> born_;    // this group's rows
-  std::unordered_map<i64, BornMsg> born_msg_;         // this group's messages
+  FlatMap<i64, int, HashI64> refs_;                   // msg id -> durable queue rows (in the store)
+  FlatMap<RowKey, Row, RowHash> rows_by_;             // (queue slot, msg id) -> stored row
+  FlatMap<RowKey, Born, RowHash> born_;               // this group's rows
+  FlatMap<i64, BornMsg, HashI64> born_msg_;           // this group's messages
+  // the group's row changes, applied to the store as one WAL record
+  std::vector<RowOp> ops_;
+  std::vector<int> qlocal_;                           // queue slot -> index in gq_ (-1)
+  std::vector<const std::string*> gq_;
+  std::vector<u32> gslots_;
+  std::vector<const char*> recs_;
+  std::vector<uint32_t> lens_;
+  std::vector<i64> mids_;
+  std::vector<BodyLog::Loc> locs_;
   std::atomic<u64> rows_{0}, commits_{0}, bytes_{0};
-  double busy_s_ = 0;
+  double busy_s_ = 0, apply_s_ = 0, flush_s_ = 0, sync_s_ = 0;
 };
 
 }  // namespace cmq

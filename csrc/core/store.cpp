@@ -16,6 +16,7 @@
 #include <nmmintrin.h>
 
 #include "codec.hpp"
+#include "../kernels/step_abi.h"
 
 namespace cmq {
 
@@ -23,7 +24,9 @@ namespace {
 enum Op : uint8_t {
   OP_MSG_INS = 1, OP_MSG_REFER, OP_MSG_DEL, OP_QMETA_INS, OP_QMSG_INS, OP_QLAST, OP_QCONSUMED, OP_QFORCE_DEL,
   OP_QPENDING_DEL, OP_QDEL_CONSUMED, OP_QUNACK_INS, OP_QUNACK_DEL, OP_X_INS, OP_BIND_INS, OP_BIND_DEL,
-  OP_BIND_DEL_Q, OP_X_DEL, OP_VH_INS, OP_VH_DEL, OP_QMSG_DEL, OP_QDMETA_INS, OP_QDMSG_INS, OP_QDUNACK_INS
+  OP_BIND_DEL_Q, OP_X_DEL, OP_VH_INS, OP_VH_DEL, OP_QMSG_DEL, OP_QDMETA_INS, OP_QDMSG_INS, OP_QDUNACK_INS,
+  OP_MSG_REF,  // a msgs row whose bytes are in the body log (bodylog.hpp)
+  OP_ROWS      // a group of RowOps (little-endian: u32 nq | nq x (u32 len | id) | u32 n | n x RowOp)
 };
 
 // CRC-32C (Castagnoli, init/xorout 0xFFFFFFFF) on the SSE4.2 crc32 instruction: the
@@ -98,6 +101,29 @@ std::string enc_msg(const MsgRow& m, int64_t ttl_ms, int64_t now) {
   // Cassandra TTL is whole seconds (CassandraOpService.scala:157-159); keep ms precision internally
   w.llng((u64)ttl_ms); w.llng((u64)now);
   return std::move(w.done());
+}
+std::string enc_ref(const MsgRow& m, int64_t ttl_ms, int64_t now) {
+  Writer w;
+  w.llng((u64)m.id); w.llng((u64)m.tstamp); w.octet(m.durable); w.lng((u32)m.refer);
+  w.llng((u64)ttl_ms); w.llng((u64)now);
+  w.lng((u32)m.bseg); w.llng(m.boff); w.lng(m.blen);
+  return std::move(w.done());
+}
+// the row's columns from its body-log record (a device persist record)
+bool dec_body(const std::string& rec, MsgRow* m) {
+  if (rec.size() < sizeof(PersistHdr)) return false;
+  PersistHdr h;
+  memcpy(&h, rec.data(), sizeof h);
+  const size_t need = sizeof h + h.ex_len + h.rk_len + h.props_len + (size_t)h.body_len;
+  if (need > rec.size()) return false;
+  const char* d = rec.data() + sizeof h;
+  m->exchange.assign(d, h.ex_len);
+  m->routing.assign(d + h.ex_len, h.rk_len);
+  m->header.assign(2, '\0');   // weight u16 | body size u64 | props (persist.cpp)
+  for (int i = 7; i >= 0; --i) m->header.push_back((char)((u64)h.body_len >> (8 * i)));
+  m->header.append(d + h.ex_len + h.rk_len, h.props_len);
+  m->body.assign(d + h.ex_len + h.rk_len + h.props_len, h.body_len);
+  return true;
 }
 std::string enc_qmeta(const std::string& q, int64_t lconsumed, const std::set<std::string>& consumers, bool durable,
                       int64_t ttl) {
@@ -185,7 +211,9 @@ void Store::open(const std::string& dir, bool fsync_enabled) {
   path_ = dir + "/chanamq.wal";
   fd_ = ::open(path_.c_str(), O_RDWR | O_CREAT | O_APPEND, 0644);
   if (fd_ < 0) throw std::runtime_error("store: cannot open " + path_);
+  body_.reset(new BodyLog(dir + "/bodies", fsync_enabled));
   replay();
+  body_->open_existing();
 }
 
 void Store::close() {
@@ -198,6 +226,7 @@ void Store::close() {
     ::close(fd_);
     fd_ = -1;
   }
+  if (body_) body_->close();
 }
 
 void Store::write_all(const std::string& rec) {
@@ -230,6 +259,11 @@ void Store::sync() {
   if (fd_ >= 0 && dirty_) {
     if (fsync_) ::fdatasync(fd_);
     dirty_ = false;
+  }
+  if (body_) {   // the group's bodies (written by the stripes meanwhile) are durable too
+    std::string err;
+    if (!body_->wait(&err)) throw std::runtime_error("store: " + err);
+    body_->reap();   // segments whose last row went in a record now on disk
   }
   maybe_compact();
 }
@@ -357,7 +391,9 @@ bool Store::snapshot_chunk(int t, std::string& key, int64_t& sub, std::string& o
     case 6: {   // messages, continued at the last id
       for (auto it = msgs_.upper_bound(sub); it != msgs_.end(); ++it) {
         if (!it->second.expire_at || it->second.expire_at > now)
-          add_rec(out, OP_MSG_INS, enc_msg(it->second, ttl_left(it->second.expire_at, now), now));
+          add_rec(out, it->second.bseg >= 0 ? OP_MSG_REF : OP_MSG_INS,
+                  it->second.bseg >= 0 ? enc_ref(it->second, ttl_left(it->second.expire_at, now), now)
+                                       : enc_msg(it->second, ttl_left(it->second.expire_at, now), now));
         sub = it->first;
         if (out.size() - start > budget) return true;
       }
@@ -471,17 +507,25 @@ void Store::apply(uint8_t op, const std::string& pl) {
       int64_t ttl = (int64_t)r.llng();
       int64_t at = (int64_t)r.llng();
       m.expire_at = ttl > 0 ? at + ttl : 0;
-      auto it = msgs_.find(m.id);
-      if (it != msgs_.end()) msg_bytes_ -= msg_size(it->second);
-      msg_bytes_ += msg_size(m);
-      msgs_[m.id] = std::move(m);
+      put_msg(std::move(m));
+      break;
+    }
+    case OP_MSG_REF: {
+      MsgRow m;
+      m.id = (int64_t)r.llng(); m.tstamp = (int64_t)r.llng(); m.durable = r.octet(); m.refer = (int32_t)r.lng();
+      int64_t ttl = (int64_t)r.llng();
+      int64_t at = (int64_t)r.llng();
+      m.expire_at = ttl > 0 ? at + ttl : 0;
+      m.bseg = (int64_t)r.lng(); m.boff = r.llng(); m.blen = r.lng();
+      if (!body_) break;   // a memory-only store never wrote one
+      put_msg(std::move(m));
       break;
     }
     case OP_MSG_REFER: { int64_t id = (int64_t)r.llng(); int32_t ref = (int32_t)r.lng();
       auto it = msgs_.find(id); if (it != msgs_.end()) it->second.refer = ref; break; }
     case OP_MSG_DEL: {
       auto it = msgs_.find((int64_t)r.llng());
-      if (it != msgs_.end()) { msg_bytes_ -= msg_size(it->second); msgs_.erase(it); }
+      if (it != msgs_.end()) drop_msg(it);
       break;
     }
     case OP_QMETA_INS: {
@@ -598,6 +642,28 @@ void Store::apply(uint8_t op, const std::string& pl) {
       else queue_unacks_deleted_[q][u.msgid] = u;
       break;
     }
+    case OP_ROWS: {
+      const char* d = pl.data();
+      const size_t n = pl.size();
+      size_t at = 0;
+      auto u32at = [&](uint32_t* v) { if (at + 4 > n) return false; memcpy(v, d + at, 4); at += 4; return true; };
+      uint32_t nq = 0, nops = 0;
+      if (!u32at(&nq)) break;
+      std::vector<std::string> names(nq);
+      std::vector<const std::string*> qids(nq);
+      for (uint32_t i = 0; i < nq; ++i) {
+        uint32_t len = 0;
+        if (!u32at(&len) || at + len > n) return;
+        names[i].assign(d + at, len);
+        qids[i] = &names[i];
+        at += len;
+      }
+      if (!u32at(&nops) || at + (size_t)nops * sizeof(RowOp) > n) break;
+      std::vector<RowOp> ops(nops);
+      memcpy(ops.data(), d + at, (size_t)nops * sizeof(RowOp));
+      apply_rows(qids, ops.data(), nops);
+      break;
+    }
     case OP_VH_INS: { std::string id = r.longstr(); vhosts_[id] = r.octet(); break; }
     case OP_VH_DEL: vhosts_.erase(r.longstr()); break;
     default: break;
@@ -619,11 +685,131 @@ void Store::insertMessage(MsgRow&& m, int64_t ttl_ms) {
   const int64_t now = now_ms();
   append_wal(OP_MSG_INS, enc_msg(m, ttl_ms, now));
   m.expire_at = ttl_ms > 0 ? now + ttl_ms : 0;
-  const int64_t id = m.id;
-  auto it = msgs_.find(id);
-  if (it != msgs_.end()) msg_bytes_ -= msg_size(it->second);
+  m.bseg = -1;
+  put_msg(std::move(m));
+}
+
+void Store::put_msg(MsgRow&& m) {
+  auto it = msgs_.find(m.id);
+  if (it != msgs_.end()) drop_msg(it);
   msg_bytes_ += msg_size(m);
-  msgs_[id] = std::move(m);
+  if (m.bseg >= 0 && body_) body_->ref(BodyLog::Loc{(uint32_t)m.bseg, m.blen, m.boff});
+  const int64_t id = m.id;
+  msgs_.emplace(id, std::move(m));
+}
+
+void Store::drop_msg(std::map<int64_t, MsgRow>::iterator it) {
+  msg_bytes_ -= msg_size(it->second);
+  if (it->second.bseg >= 0 && body_) body_->unref(BodyLog::Loc{(uint32_t)it->second.bseg, it->second.blen, it->second.boff});
+  msgs_.erase(it);
+}
+
+void Store::apply_rows(const std::vector<const std::string*>& qids, const RowOp* ops, size_t n) {
+  std::vector<std::map<int64_t, QueueMsgRow>*> qm(qids.size(), nullptr), qu(qids.size(), nullptr);
+  auto rows = [&](uint32_t q) -> std::map<int64_t, QueueMsgRow>& {
+    if (!qm[q]) qm[q] = &queues_[*qids[q]];
+    return *qm[q];
+  };
+  auto unacks = [&](uint32_t q) -> std::map<int64_t, QueueMsgRow>& {
+    if (!qu[q]) qu[q] = &queue_unacks_[*qids[q]];
+    return *qu[q];
+  };
+  for (size_t i = 0; i < n; ++i) {
+    const RowOp& o = ops[i];
+    const bool qok = o.q < qids.size();
+    switch (o.op) {
+      case ROW_QMSG_INS:
+        if (qok) {
+          auto& t = rows(o.q);
+          t.insert_or_assign(t.end(), o.offset, QueueMsgRow{o.offset, o.msgid, o.size, 0});
+        }
+        break;
+      case ROW_QMSG_DEL: if (qok) rows(o.q).erase(o.offset); break;
+      case ROW_QUNACK_INS:
+        if (qok) unacks(o.q)[o.msgid] = QueueMsgRow{o.offset, o.msgid, o.size, 0};
+        break;
+      case ROW_QUNACK_DEL: if (qok) unacks(o.q).erase(o.msgid); break;
+      case ROW_MSG_DEL: {
+        auto it = msgs_.find(o.msgid);
+        if (it != msgs_.end()) drop_msg(it);
+        break;
+      }
+      case ROW_MSG_REFER: {
+        auto it = msgs_.find(o.msgid);
+        if (it != msgs_.end()) it->second.refer = o.size;
+        break;
+      }
+      case ROW_MSG_REF: {
+        if (!body_) break;
+        MsgRow m;
+        m.id = o.msgid;
+        m.tstamp = o.tstamp;
+        m.durable = true;
+        m.refer = (int32_t)o.q;
+        m.bseg = o.seg;
+        m.boff = (uint64_t)o.offset;
+        m.blen = (uint32_t)o.size;
+        put_msg(std::move(m));
+        break;
+      }
+      default: break;
+    }
+  }
+}
+
+void Store::applyRows(const std::vector<const std::string*>& qids, const RowOp* ops, size_t n) {
+  if (!n) return;
+  LOCK;
+  apply_rows(qids, ops, n);
+  if (fd_ < 0) return;
+  size_t bytes = 8 + n * sizeof(RowOp);
+  for (auto* q : qids) bytes += 4 + q->size();
+  std::string pl(bytes, '\0');
+  char* d = &pl[0];
+  uint32_t v = (uint32_t)qids.size();
+  memcpy(d, &v, 4);
+  d += 4;
+  for (auto* q : qids) {
+    v = (uint32_t)q->size();
+    memcpy(d, &v, 4);
+    memcpy(d + 4, q->data(), q->size());
+    d += 4 + q->size();
+  }
+  v = (uint32_t)n;
+  memcpy(d, &v, 4);
+  memcpy(d + 4, ops, n * sizeof(RowOp));
+  append_wal(OP_ROWS, pl);
+}
+
+void Store::placeBodies(const char* const* recs, const uint32_t* lens, size_t n, BodyLog::Loc* out) {
+  LOCK;
+  if (!body_) throw std::runtime_error("store: the body log needs a store on disk");
+  body_->put(recs, lens, n, out);
+  dirty_ = true;
+}
+
+void Store::insertMessageRefs(const BodyRef* refs, size_t n) {
+  LOCK;
+  if (!body_) throw std::runtime_error("store: the body log needs a store on disk");
+  std::vector<const char*> recs(n);
+  std::vector<uint32_t> lens(n);
+  std::vector<BodyLog::Loc> locs(n);
+  for (size_t i = 0; i < n; ++i) { recs[i] = refs[i].rec; lens[i] = refs[i].len; }
+  body_->put(recs.data(), lens.data(), n, locs.data());
+  dirty_ = true;
+  const int64_t now = now_ms();
+  for (size_t i = 0; i < n; ++i) {
+    MsgRow m;
+    m.id = refs[i].id;
+    m.tstamp = refs[i].tstamp;
+    m.durable = true;
+    m.refer = refs[i].refer;
+    m.bseg = locs[i].seg;
+    m.boff = locs[i].off;
+    m.blen = locs[i].len;
+    append_wal(OP_MSG_REF, enc_ref(m, 0, now));
+    put_msg(std::move(m));
+  }
 }
 
 void Store::updateMessageReferCount(int64_t id, int32_t refer) {
@@ -635,6 +821,12 @@ bool Store::selectMessage(int64_t id, MsgRow* out) {
   if (it == msgs_.end()) return false;
   if (it->second.expire_at && it->second.expire_at <= now_ms()) return false;
   *out = it->second;
+  if (it->second.bseg >= 0) {   // the bytes are in the body log
+    std::string rec;
+    if (!body_ || !body_->read(BodyLog::Loc{(uint32_t)it->second.bseg, it->second.blen, it->second.boff}, &rec) ||
+        !dec_body(rec, out))
+      return false;   // a torn body: its message was never confirmed
+  }
   return true;
 }
 void Store::deleteMessage(int64_t id) { LOCK; Writer w; w.llng((u64)id); append(OP_MSG_DEL, w.done()); }

@@ -21,12 +21,15 @@
 #include <condition_variable>
 #include <cstdint>
 #include <map>
+#include <memory>
 #include <mutex>
 #include <set>
 #include <string>
 #include <thread>
 #include <tuple>
 #include <vector>
+
+#include "bodylog.hpp"
 
 namespace cmq {
 
@@ -39,7 +42,30 @@ struct MsgRow {            // msgs
   bool durable = false;
   int32_t refer = 0;
   int64_t expire_at = 0;   // from USING TTL; 0 = none
+  // body in the body log (bodylog.hpp) instead of in this row: header/body/exchange/routing
+  // are read back from (bseg, boff, blen) by selectMessage; bseg < 0 = inline row
+  int64_t bseg = -1;
+  uint64_t boff = 0;
+  uint32_t blen = 0;
 };
+// a persistent message of the GPU write-behind whose bytes are a device persist record
+// (step_abi.h PersistHdr + exchange | routing key | properties | body)
+struct BodyRef { int64_t id, tstamp; const char* rec; uint32_t len; int32_t refer; };
+// one row change of the write-behind's batched path (Store::applyRows); q indexes the
+// batch's queue ids
+enum RowOpKind : uint8_t {
+  ROW_QMSG_INS, ROW_QMSG_DEL, ROW_QUNACK_INS, ROW_QUNACK_DEL, ROW_MSG_DEL, ROW_MSG_REFER /* refer in size */,
+  ROW_MSG_REF /* msgs row in the body log: refer in q, (seg, offset, size) the body, tstamp */
+};
+struct RowOp {
+  uint8_t op, pad[3];
+  uint32_t q;
+  int64_t offset, msgid;
+  int32_t size;
+  uint32_t seg;
+  int64_t tstamp;
+};
+static_assert(sizeof(RowOp) == 40, "RowOp layout (WAL format)");
 struct QueueMsgRow {       // queues / queues_deleted / queue_unacks / queue_unacks_deleted
   int64_t offset = 0, msgid = 0;
   int32_t size = 0;
@@ -90,6 +116,16 @@ class Store {
   // ---- messages
   void insertMessage(const MsgRow& m, int64_t ttl_ms);
   void insertMessage(MsgRow&& m, int64_t ttl_ms);
+  // bodies to the body log (written by its stripes from the given records, which must stay
+  // valid until the next sync()), rows to the WAL.  Needs a store on disk
+  void insertMessageRefs(const BodyRef* refs, size_t n);
+  // start writing bodies to the body log (locations now, durable by the next sync())
+  void placeBodies(const char* const* recs, const uint32_t* lens, size_t n, BodyLog::Loc* out);
+  // a group of row changes as one WAL record, applied in order
+  void applyRows(const std::vector<const std::string*>& qids, const RowOp* ops, size_t n);
+  bool hasBodyLog() const { return body_ != nullptr; }
+  void configureBodyLog(int stripes, uint64_t seg_bytes) { if (body_) body_->configure(stripes, seg_bytes); }
+  BodyLog::Stats bodyStats() { return body_ ? body_->stats() : BodyLog::Stats{}; }
   void updateMessageReferCount(int64_t id, int32_t refer);
   bool selectMessage(int64_t id, MsgRow* out);
   void deleteMessage(int64_t id);
@@ -141,6 +177,9 @@ class Store {
   void apply(uint8_t op, const std::string& payload);
   void replay();
   void write_all(const std::string& rec);
+  void put_msg(MsgRow&& m);
+  void apply_rows(const std::vector<const std::string*>& qids, const RowOp* ops, size_t n);           // upsert into msgs_ (body log accounting)
+  void drop_msg(std::map<int64_t, MsgRow>::iterator it);
   void flush_wal();
   void maybe_compact();               // mu_ held
   void compact_run();                 // the compaction (background thread or compact())
@@ -162,6 +201,7 @@ class Store {
   bool replaying_ = false;
   uint64_t wal_bytes_ = 0;
 
+  std::unique_ptr<BodyLog> body_;     // with a store on disk
   std::map<int64_t, MsgRow> msgs_;
   std::map<std::string, std::map<int64_t, QueueMsgRow>> queues_, queues_deleted_;
   std::map<std::string, QueueMetaRow> queue_metas_;

@@ -559,7 +559,12 @@ class Engine {
     HIPCHECK(hipStreamCreateWithFlags(&s_comp_, hipStreamNonBlocking));
     HIPCHECK(hipStreamCreateWithFlags(&s_h2d_, hipStreamNonBlocking));
     HIPCHECK(hipStreamCreateWithFlags(&s_d2h_, hipStreamNonBlocking));
-    HIPCHECK(hipStreamCreateWithFlags(&s_ing_, hipStreamNonBlocking));
+    {   // the ingest half gets its own (high-priority) hardware queue: next to the routing
+        // half of the previous step, not queued behind it
+      int lo = 0, hi = 0;
+      HIPCHECK(hipDeviceGetStreamPriorityRange(&lo, &hi));
+      HIPCHECK(hipStreamCreateWithPriority(&s_ing_, hipStreamNonBlocking, hi));
+    }
     for (int p = 0; p < 2; ++p) {
       HIPCHECK(hipEventCreateWithFlags(&ev_ing_[p], hipEventDisableTiming));
       HIPCHECK(hipEventCreateWithFlags(&ev_rest_[p], hipEventDisableTiming));
@@ -770,9 +775,15 @@ class Engine {
       pend_gets_.clear();
     }
     nget_[p] = in->nget;
+    // the payload may already be on its way (prefetch): then only the step's descriptors
+    // follow it on the H2D stream
+    const bool pre = pre_[p];
+    if (pre && (pre_ptr_[p] != payload_ptr || pre_len_[p] != payload_len))
+      throw std::runtime_error("submit: payload differs from the one prefetched for this step");
+    pre_[p] = false;
     HIPCHECK(hipMemcpyAsync((void*)io_[p].in, in, sizeof(StepIn), hipMemcpyHostToDevice, s_h2d_));
     if (sb) HIPCHECK(hipMemcpyAsync((void*)io_[p].segs, stage_segs_[p], sb, hipMemcpyHostToDevice, s_h2d_));
-    if (payload_len)
+    if (payload_len && !pre)
       HIPCHECK(hipMemcpyAsync((void*)io_[p].ingress, (const void*)payload_ptr, payload_len,
                               sdma_ ? hipMemcpyDeviceToDeviceNoCU : hipMemcpyHostToDevice, s_h2d_));
     HIPCHECK(hipEventRecord(ev_h2d_[p], s_h2d_));
@@ -781,6 +792,25 @@ class Engine {
     ++seq_;
     if (!defer) launch(p);
     return p;
+  }
+
+  // Early ingress of the NEXT step (overlapped single-GPU steps): its payload crosses PCIe
+  // while the current steps run -- the H2D stream only waits (on the GPU) for the ingest
+  // half of the step two back, the last reader of this parity's ingress buffer -- so the
+  // copy engine never idles between steps.  The step is then submit()ed with the same
+  // payload.  false: not applicable (no overlap), nothing queued.
+  bool prefetch(u64 payload_ptr, u64 payload_len) {
+    if (!overlap_ || !payload_len) return false;
+    const int p = (int)(seq_ & 1);
+    if (pre_[p] || staged_[p]) throw std::runtime_error("prefetch: this step's payload is already queued");
+    if (payload_len > d_.ingress_cap) throw std::runtime_error("ingress payload exceeds ingress_cap");
+    if (ing_issued_[p]) HIPCHECK(hipStreamWaitEvent(s_h2d_, ev_ing_[p], 0));
+    HIPCHECK(hipMemcpyAsync((void*)io_[p].ingress, (const void*)payload_ptr, payload_len,
+                            sdma_ ? hipMemcpyDeviceToDeviceNoCU : hipMemcpyHostToDevice, s_h2d_));
+    pre_[p] = true;
+    pre_ptr_[p] = payload_ptr;
+    pre_len_[p] = payload_len;
+    return true;
   }
 
   // Basic.Get requests for the next submitted step (validated by the caller: a local queue
@@ -820,6 +850,7 @@ class Engine {
         HIPCHECK(hipGraphLaunch(graph_ing_[p], s_ing_));
       }
       HIPCHECK(hipEventRecord(ev_ing_[p], s_ing_));
+      ing_issued_[p] = true;
       HIPCHECK(hipStreamWaitEvent(s_comp_, ev_ing_[p], 0));
       if (d2h_issued_[e]) HIPCHECK(hipStreamWaitEvent(s_comp_, ev_d2h_[e], 0));
       {
@@ -1357,6 +1388,9 @@ class Engine {
     a.submit = [](void* e, const SegIn* sg, u32 n, const u8* pay, u64 len, i64 now, u32 worker) -> int {
       return ((Engine*)e)->guard([&] { return ((Engine*)e)->submit_raw(sg, n, (u64)pay, len, now, (u64)now, worker); });
     };
+    a.prefetch = [](void* e, const u8* pay, u64 len) -> int {
+      return ((Engine*)e)->guard([&] { return ((Engine*)e)->prefetch((u64)pay, len) ? 1 : 0; });
+    };
     a.wait_results = [](void* e, int p) -> int {
       return ((Engine*)e)->guard([&] { ((Engine*)e)->wait_results(p); return 0; });
     };
@@ -1862,7 +1896,9 @@ class Engine {
   bool overlap_ = false;
   hipStream_t s_ing_ = nullptr;
   hipEvent_t ev_ing_[2], ev_rest_[2];
-  bool rest_issued_[2] = {false, false};
+  bool rest_issued_[2] = {false, false}, ing_issued_[2] = {false, false};
+  bool pre_[2] = {false, false};        // the next step's payload H2D already queued (prefetch)
+  u64 pre_ptr_[2] = {0, 0}, pre_len_[2] = {0, 0};
   hipGraphExec_t graph_ing_[2] = {nullptr, nullptr};
   hipGraphExec_t graph_rest_[2] = {nullptr, nullptr};
   u64* scan_status_ing_ = nullptr;
@@ -1944,6 +1980,7 @@ PYBIND11_MODULE(_dataplane, m) {
            py::arg("now_ms"), py::arg("step"), py::arg("id_ms"), py::arg("worker"), py::arg("defer") = false,
            py::arg("flags") = 0)
       .def("launch", &Engine::launch)
+      .def("prefetch", &Engine::prefetch, py::arg("payload_ptr"), py::arg("payload_len"))
       .def("stage_gets", [](Engine& e, py::buffer b) {
              py::buffer_info bi = b.request();
              const size_t nb = (size_t)bi.size * bi.itemsize;

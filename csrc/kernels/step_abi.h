@@ -99,7 +99,7 @@ struct GetOut { u32 status; u32 msg_count; };
 // C entry points of one Engine (engine.hip: Engine::c_api).  All return 0 / a parity on
 // success and -1 on error (message: error()).  Parity p = the double-buffered step IO set
 // of a submitted step; its host-mapped outputs stay valid until the next submit of p.
-#define CMQ_STEP_ABI 5
+#define CMQ_STEP_ABI 6
 struct CmqEngineApi {
   u32 abi;
   u32 c_max, seg_max, carry_cap, persist, persist_max;
@@ -149,5 +149,8 @@ struct CmqEngineApi {
   // answers of the last step of parity p (in request order)
   int (*stage_gets)(void* eng, const GetReq* reqs, u32 n);
   const GetOut* (*get_out)(void* eng, int p);
+  // the NEXT submit's payload H2D queued now (overlapped single-GPU engine): 1 queued, 0 not
+  // applicable, -1 error; that submit must pass the same payload
+  int (*prefetch)(void* eng, const u8* payload, u64 len);
 };
 #define GROW_MAX 4096   // grow requests reported per step

@@ -8,7 +8,7 @@ set -euo pipefail
 cd "$(dirname "$0")/.."
 OUT=${1:-build/sanitize}
 mkdir -p "$OUT"
-SRC="csrc/core/store.cpp csrc/core/persist.cpp csrc/core/codec.cpp csrc/core/broker.cpp csrc/core/loadgen.cpp csrc/core/frontend.cpp"
+SRC="csrc/core/store.cpp csrc/core/bodylog.cpp csrc/core/persist.cpp csrc/core/codec.cpp csrc/core/broker.cpp csrc/core/loadgen.cpp csrc/core/frontend.cpp"
 g++ -std=c++17 -O1 -g -fno-omit-frame-pointer -fsanitize=address,undefined -fno-sanitize-recover=all \
     -Icsrc/kernels csrc/tests/host_sanitize.cpp $SRC -o "$OUT/host_sanitize" -lssl -lcrypto -lpthread
 rm -rf /tmp/cmq-sanitize
