@@ -174,6 +174,8 @@ def main():
                          "overlap at ~47 GB/s each, bench/pcie_probe.hip), the runtime blit kernel (holds CUs "
                          "for the whole transfer), the runtime's NoCU request, or our copy kernel")
     ap.add_argument("--copy-wgs", type=int, default=16)
+    ap.add_argument("--sdma-split", type=int, default=2,
+                    help="--copy-engine sdma: egress D2H of >= 2 MB split over this many SDMA engines (1 or 2)")
     ap.add_argument("--sdma-engine", type=int, default=-1,
                     help="--copy-engine sdma: SDMA engine for the egress D2H (-1 = highest available)")
     ap.add_argument("--workload", choices=["topic", "fanout", "storm"], default="topic",
@@ -236,7 +238,8 @@ def main():
                egress_cap=(128 << 20) if not fan else (320 << 20),
                log_bytes=16 << 30, ring_pool=Q * qcap + qtot + 1024, tb_max=max(64, qtot) if not fan else 64,
                fan_max=max(1 << 20, qtot * 2), carry_cap=256 << 10, graph=0 if args.no_graph else 1,
-               copy_engine={"blit": 0, "nocu": 1, "kernel": 2, "sdma": 3}[args.copy_engine], copy_wgs=args.copy_wgs, sdma_engine=args.sdma_engine)
+               copy_engine={"blit": 0, "nocu": 1, "kernel": 2, "sdma": 3}[args.copy_engine], copy_wgs=args.copy_wgs, sdma_engine=args.sdma_engine,
+               sdma_split=args.sdma_split)
     native = shards > 1 and args.xchg == "native"
     if native:
         dp = setup_native_exchange(args, cfg, GpuDataPlane, dist, backend, local, rank, world)

@@ -83,39 +83,31 @@ FE_CFG = {}
 SIZING = {"per_conn_read": 512 << 10, "carry_cap": 1 << 20}
 
 
-def get_pollers(port, n, stop, out, prefill=200000):
+def get_pollers(port, n, prefill=200000):
     """``n`` clients polling Basic.Get (no-ack) on their own pre-filled queue while the
-    load runs: every answer is served inside a step (k_dequeue) without draining the
-    pipeline.  Appends (gets ok, gets empty, seconds) per poller to ``out``."""
-    import threading
+    load runs (bench/get_poller.py, a separate process): every answer is served inside a
+    step (k_dequeue) without draining the pipeline.  Returns the process once its queues
+    are filled; ``stop_pollers`` ends it and returns [(gets ok, gets empty, seconds)]."""
+    import subprocess
+    p = subprocess.Popen([sys.executable, os.path.join(os.path.dirname(os.path.abspath(__file__)), "get_poller.py"),
+                          "--port", str(port), "--n", str(n), "--prefill", str(prefill)],
+                         stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True)
+    line = p.stdout.readline()
+    if line.strip() != "ready":
+        p.kill()
+        raise RuntimeError(f"get pollers failed to start: {line!r}")
+    return p
 
-    from chanamq_amd.client import Connection
-    c = Connection(port=port, vhost="/", timeout=60)
-    ch = c.channel()
-    for i in range(n):
-        ch.queue_declare(f"e2e.getq{i}")
-        for k in range(prefill // n):
-            ch.basic_publish("", f"e2e.getq{i}", b"g" * 256)
-    c.process(0.5)
 
-    def poll(i):
-        pc = Connection(port=port, vhost="/", timeout=60)
-        pch = pc.channel()
-        ok = empty = 0
-        t0 = time.time()
-        while not stop.is_set():
-            d = pch.basic_get(f"e2e.getq{i}", no_ack=True)
-            if d is None:
-                empty += 1
-            else:
-                ok += 1
-        out.append((ok, empty, time.time() - t0))
-        pc.close()
-    ths = [threading.Thread(target=poll, args=(i,), daemon=True) for i in range(n)]
-    for t in ths:
-        t.start()
-    c.close()
-    return ths
+def stop_pollers(p):
+    import subprocess
+    try:
+        out, _ = p.communicate("", timeout=60)
+    except subprocess.TimeoutExpired:
+        p.kill()
+        return []
+    lines = [x for x in out.splitlines() if x.startswith("[")]
+    return [tuple(x) for x in json.loads(lines[-1])] if lines else []
 
 
 def run_one(core, name, spec, io, io_threads, seconds, rate=0.0, lg_threads=12, store_dir=None, cons_threads=8,
@@ -144,18 +136,17 @@ def run_one(core, name, spec, io, io_threads, seconds, rate=0.0, lg_threads=12, 
     import threading
     smp = threading.Thread(target=sample, daemon=True)
     smp.start()
-    gstop, gout, gths = threading.Event(), [], []
+    gout, gproc = [], None
     if n_getters:
-        gths = get_pollers(b.port, n_getters, gstop, gout)
+        gproc = get_pollers(b.port, n_getters)
     try:
         r = core.run_load(dict(port=b.port, seconds=seconds, warmup=1.0, queue=f"e2e.{name}",
                                exchange=f"e2e.x.{name}", threads=lg_threads, consumer_threads=cons_threads,
                                rate=rate, **spec))
     finally:
         done[0] = True
-        gstop.set()
-        for t in gths:
-            t.join(30)
+        if gproc is not None:
+            gout = stop_pollers(gproc)
         smp.join()
         cpu1 = thread_cpu()
         after = {}

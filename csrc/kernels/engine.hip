@@ -193,6 +193,7 @@ class Engine {
     sdma_ = copy_mode_ == 1;
     copy_wgs_ = (u32)get("copy_wgs", 16);
     sdma_pref_ = cfg.contains("sdma_engine") ? cfg["sdma_engine"].cast<int>() : -1;
+    sdma_split_ = cfg.contains("sdma_split") ? std::max(1, std::min(2, cfg["sdma_split"].cast<int>())) : 2;
 
     // ---- allocations
     auto dev = [&](const char* name, size_t bytes) { return alloc(name, bytes, false); };
@@ -709,6 +710,7 @@ class Engine {
     o["copy_wgs"] = copy_wgs_;
     o["egress_slots"] = EGRESS_SLOTS;
     { u32 e = 0; while (copy_mode_ == 3 && e < 32 && !(((u32)sdma_engine_ >> e) & 1u)) ++e; o["sdma_engine"] = copy_mode_ == 3 ? (int)e : -1; }
+    { u32 e = 0; while (sdma_engine2_ && e < 32 && !(((u32)sdma_engine2_ >> e) & 1u)) ++e; o["sdma_engine2"] = sdma_engine2_ ? (int)e : -1; }
     o["persist"] = d_.persist; o["persist_max"] = d_.persist_max; o["persist_bytes"] = d_.persist_bytes;
     o["restore_max"] = restore_max_;
     o["xfer_desc_max"] = d_.xfer_desc_max; o["xfer_bytes"] = d_.xfer_bytes; o["world_max"] = WORLD_MAX;
@@ -1510,10 +1512,18 @@ class Engine {
     HIPCHECK(hipStreamWaitEvent(s_d2h_, ev_done_[p], 0));
     if (n && copy_mode_ == 3) {
       HIPCHECK(hipEventSynchronize(ev_done_[p]));
-      hsa_signal_store_screlease(sdma_sig_[e], 1);
-      hsa_status_t st = hsa_amd_memory_async_copy_on_engine(egress_host_[e], cpu_agent_, egress_dev_[e], gpu_agent_, n,
-                                                            0, nullptr, sdma_sig_[e], sdma_engine_, true);
-      if (st != HSA_STATUS_SUCCESS) throw std::runtime_error("hsa_amd_memory_async_copy_on_engine failed");
+      // large egress split over two SDMA engines (one engine tops out below the link's
+      // device -> host rate); each part decrements the slot's signal once
+      const int k = (n >= (2u << 20) && sdma_engine2_) ? 2 : 1;
+      hsa_signal_store_screlease(sdma_sig_[e], k);
+      const u64 half = k == 2 ? ((n / 2) & ~(u64)4095) : n;
+      for (int i = 0; i < k; ++i) {
+        const u64 off = i ? half : 0, len = i ? n - half : half;
+        hsa_status_t st = hsa_amd_memory_async_copy_on_engine(
+            (u8*)egress_host_[e] + off, cpu_agent_, (u8*)egress_dev_[e] + off, gpu_agent_, len, 0, nullptr,
+            sdma_sig_[e], i ? sdma_engine2_ : sdma_engine_, true);
+        if (st != HSA_STATUS_SUCCESS) throw std::runtime_error("hsa_amd_memory_async_copy_on_engine failed");
+      }
       sdma_pending_[e] = true;
       return n;
     }
@@ -1569,6 +1579,12 @@ class Engine {
     else if ((mask >> 1) & 1u) pick = 1;
     else while (!((mask >> pick) & 1u)) ++pick;
     sdma_engine_ = (hsa_amd_sdma_engine_id_t)(1u << pick);
+    // a second engine for split egress copies: another full-rate one (0-3), not engine 0
+    // (the runtime's H2D engine) when there is a choice
+    sdma_engine2_ = (hsa_amd_sdma_engine_id_t)0;
+    if (sdma_split_ > 1)
+      for (u32 c : {2u, 3u, 0u})
+        if (c != pick && ((mask >> c) & 1u)) { sdma_engine2_ = (hsa_amd_sdma_engine_id_t)(1u << c); break; }
     for (int e = 0; e < EGRESS_SLOTS; ++e)
       if (hsa_signal_create(0, 0, nullptr, &sdma_sig_[e]) != HSA_STATUS_SUCCESS)
         throw std::runtime_error("hsa_signal_create failed");
@@ -1921,7 +1937,8 @@ class Engine {
   int slot_of_[2] = {0, 0};
   int copy_mode_ = 0;
   hsa_agent_t gpu_agent_{}, cpu_agent_{};
-  hsa_amd_sdma_engine_id_t sdma_engine_{};
+  hsa_amd_sdma_engine_id_t sdma_engine_{}, sdma_engine2_{};
+  int sdma_split_ = 2;
   hsa_signal_t sdma_sig_[EGRESS_SLOTS] = {};
   bool sdma_pending_[EGRESS_SLOTS] = {};
   u32 copy_wgs_ = 16;
