@@ -174,7 +174,7 @@ def main():
                          "overlap at ~47 GB/s each, bench/pcie_probe.hip), the runtime blit kernel (holds CUs "
                          "for the whole transfer), the runtime's NoCU request, or our copy kernel")
     ap.add_argument("--copy-wgs", type=int, default=16)
-    ap.add_argument("--sdma-split", type=int, default=2,
+    ap.add_argument("--sdma-split", type=int, default=1,
                     help="--copy-engine sdma: egress D2H of >= 2 MB split over this many SDMA engines (1 or 2)")
     ap.add_argument("--sdma-engine", type=int, default=-1,
                     help="--copy-engine sdma: SDMA engine for the egress D2H (-1 = highest available)")

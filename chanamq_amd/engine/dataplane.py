@@ -667,10 +667,12 @@ class GpuDataPlane(ControlState):
         self._mark_dirty(s)
 
     def unpause(self, conn):
+        """The connection's bytes are processed again from the next submitted step (k_stage
+        clears the device flag): safe from any thread while steps are in flight."""
         c = self.conns.get(conn)
         if c is not None:
             c.paused = False
-        self._up_at("conn_paused", 0, conn, np.uint32)
+        self.eng.stage_unpause(int(conn))
 
     # ================================================================== steps
     def _pinned(self, n, parity):

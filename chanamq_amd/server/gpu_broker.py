@@ -352,7 +352,7 @@ class GpuBroker:
         while self._running:
             evs = fe.poll_events(5 if tiers else 20)
             persist = [e for e in evs if e[0] == FE_PERSIST]
-            dev = [e for e in evs if e[0] != FE_PERSIST]
+            dev = self._fast_events([e for e in evs if e[0] != FE_PERSIST])
             if dev or self._tx_pending:
                 with self.lock:
                     while dev or (self._tx_pending and self.node is None):
@@ -375,6 +375,45 @@ class GpuBroker:
                 self._sync_fe_stats()
                 self._watermarks()
                 self._flush_all()
+
+    def _fast_events(self, dev):
+        """Basic.Get traffic without pausing the stepper: a Get on a local queue is staged
+        for the next step (fe.queue_get) and its answer (FE_GET) replied to right away --
+        neither touches device state (the getting connection's unpause rides the next
+        step, GpuDataPlane.unpause).  Returns the events left for the locked path."""
+        if self.node is not None or not hasattr(self.plane, "eng"):
+            return dev
+        rest = []
+        for e in dev:
+            kind, conn = e[0], e[1]
+            if kind == FE_GET and (e[2] & 0xFFFFFFFF) in (GS_OK, GS_EMPTY, GS_RETRY):
+                self._get_answer(conn, e[2], e[3])
+                continue
+            if kind == FE_CTRL and self._fast_get(conn, e[4]):
+                continue
+            rest.append(e)
+        return rest
+
+    def _fast_get(self, conn, raw):
+        c = self.conns.get(conn)
+        if c is None or c.state != "open" or len(raw) < 11:
+            return False
+        t, ch, size = struct.unpack_from(">BHI", raw, 0)
+        if t != C.FRAME_METHOD or struct.unpack_from(">HH", raw, 7) != (60, 70) or ch in c.closing_channels:
+            return False
+        p = self.plane
+        pc = p.conns.get(c.id)
+        if pc is None or ch not in pc.channels:
+            return False
+        m = decode_method(bytes(raw[7:7 + size]))
+        q = p.queues.get((pc.vhost, m.queue or c.last_queue.get(ch, "")))
+        if q is None or q.exclusive_owner not in (-1, c.id) or q.owner != p.rank:
+            return False   # errors and remote queues: the locked path
+        gid = self._next_get = getattr(self, "_next_get", 0) + 1
+        self._dev_gets[gid] = (c.id, ch, q.slot, bool(m.no_ack))
+        self.fe.queue_get(c.id, p.chslot(c.id, ch), q.slot, int(bool(m.no_ack)), gid)
+        self.stats["device_gets"] = self.stats.get("device_gets", 0) + 1
+        return True
 
     def _handle_fe(self, evs):
         ctrl, events, seg_status, txbuf = [], [], [], []

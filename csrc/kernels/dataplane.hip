@@ -354,6 +354,13 @@ __global__ __launch_bounds__(1024) void k_stage(DS d) {
       d.ctr->n_grow = 0; d.tot[TS_NMOVE] = 0; d.tot[TS_NDEFER] = 0; d.tot[TS_TTL_BUDGET] = 0;
       *d.egress_budget = 0;
     }
+    // connections whose control command the host has answered resume with this step (the
+    // frame scan, the only reader and writer of the flag, runs after this kernel)
+    const u32 nunp = d.in->nunp;
+    for (u32 k = tid; k < nunp; k += 1024) {
+      const u32 c = d.unpause_req[k];
+      if (c < d.c_max) d.conn_paused[c] = 0;
+    }
   }
   u32 total = 0;
   for (u32 k = tid; k < nseg; k += 1024) total += align16(d.carry_len[d.segs[k].conn] + d.segs[k].len + 32);

@@ -51,7 +51,9 @@ struct StepIn {         // host -> device per step (64 B)
   u32 worker;           // snowflake worker id (rank)
   u32 nget;             // Basic.Get requests of this step (DS.get_req, <= GET_STEP_MAX)
   u64 egress;           // device pointer: this step's egress slot (engine rotates slots)
-  u64 pad[2];
+  u32 nunp;             // connections to unpause before this step's frame scan (DS.unpause_req)
+  u32 pad1;
+  u64 pad2;
 };
 
 

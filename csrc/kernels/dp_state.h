@@ -197,6 +197,7 @@ struct DS {
   u32* dirty_list;
   u32* n_dirty;
   u32* def_list;            // [nch] channels left dirty by k_chan_advance (record budget hit)
+  const u32* unpause_req;   // per parity [UNPAUSE_STEP_MAX]: connections k_stage unpauses
   const GetReq* get_req;    // per parity [GET_STEP_MAX]: Basic.Get requests of the step
   GetOut* get_out_h;        // per parity, host-mapped [GET_STEP_MAX]: their answers
   USlot* uwin;              // [chslots][ucap]

@@ -12,6 +12,7 @@
 #include <functional>
 #include <map>
 #include <memory>
+#include <mutex>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -193,7 +194,7 @@ class Engine {
     sdma_ = copy_mode_ == 1;
     copy_wgs_ = (u32)get("copy_wgs", 16);
     sdma_pref_ = cfg.contains("sdma_engine") ? cfg["sdma_engine"].cast<int>() : -1;
-    sdma_split_ = cfg.contains("sdma_split") ? std::max(1, std::min(2, cfg["sdma_split"].cast<int>())) : 2;
+    sdma_split_ = cfg.contains("sdma_split") ? std::max(1, std::min(2, cfg["sdma_split"].cast<int>())) : 1;
 
     // ---- allocations
     auto dev = [&](const char* name, size_t bytes) { return alloc(name, bytes, false); };
@@ -230,6 +231,8 @@ class Engine {
       io.get_req = (const GetReq*)dev(("get_req" + sfx).c_str(), sizeof(GetReq) * GET_STEP_MAX);
       io.get_out_h = (GetOut*)hst(("get_out" + sfx).c_str(), sizeof(GetOut) * GET_STEP_MAX);
       stage_gets_[p] = (GetReq*)pinned(("stage_gets" + sfx).c_str(), sizeof(GetReq) * GET_STEP_MAX);
+      io.unpause_req = (const u32*)dev(("unpause_req" + sfx).c_str(), 4ull * UNPAUSE_STEP_MAX);
+      stage_unp_[p] = (u32*)pinned(("stage_unp" + sfx).c_str(), 4ull * UNPAUSE_STEP_MAX);
     }
 
     // egress slots rotate per step independently of the IO parity: step t renders into
@@ -498,7 +501,7 @@ class Engine {
       io.seg_out_h = io_[p].seg_out_h; io.conn_out_h = io_[p].conn_out_h; io.ctrl_h = io_[p].ctrl_h;
       io.ctrl_rec_h = io_[p].ctrl_rec_h; io.grow_h = io_[p].grow_h; io.conn_conf_h = io_[p].conn_conf_h;
       io.persist_h = io_[p].persist_h; io.crec_h = io_[p].crec_h;
-      io.get_req = io_[p].get_req; io.get_out_h = io_[p].get_out_h;
+      io.get_req = io_[p].get_req; io.get_out_h = io_[p].get_out_h; io.unpause_req = io_[p].unpause_req;
       static_cast<DS&>(io_[p]) = io;
     }
     // native exchange (sharded steps driven by the native front end, csrc/core/frontend.cpp):
@@ -777,6 +780,16 @@ class Engine {
       pend_gets_.clear();
     }
     nget_[p] = in->nget;
+    {   // connections the host unpaused since the last step (any thread may stage them)
+      std::lock_guard<std::mutex> g(unp_mu_);
+      in->nunp = (u32)std::min<size_t>(pend_unp_.size(), UNPAUSE_STEP_MAX);
+      if (in->nunp) {
+        memcpy(stage_unp_[p], pend_unp_.data(), 4ull * in->nunp);
+        pend_unp_.erase(pend_unp_.begin(), pend_unp_.begin() + in->nunp);
+      }
+    }
+    if (in->nunp)
+      HIPCHECK(hipMemcpyAsync((void*)io_[p].unpause_req, stage_unp_[p], 4ull * in->nunp, hipMemcpyHostToDevice, s_h2d_));
     // the payload may already be on its way (prefetch): then only the step's descriptors
     // follow it on the H2D stream
     const bool pre = pre_[p];
@@ -813,6 +826,17 @@ class Engine {
     pre_ptr_[p] = payload_ptr;
     pre_len_[p] = payload_len;
     return true;
+  }
+
+  // a paused connection (its control command answered) resumes with the next submitted
+  // step: k_stage clears its flag before the frame scan reads it, so the host never writes
+  // device state while steps are in flight.  Any thread.
+  void stage_unpause(u32 conn) {
+    if (conn >= d_.c_max) throw std::runtime_error("stage_unpause: bad connection");
+    std::lock_guard<std::mutex> g(unp_mu_);
+    for (u32 c : pend_unp_)
+      if (c == conn) return;
+    pend_unp_.push_back(conn);
   }
 
   // Basic.Get requests for the next submitted step (validated by the caller: a local queue
@@ -1512,8 +1536,9 @@ class Engine {
     HIPCHECK(hipStreamWaitEvent(s_d2h_, ev_done_[p], 0));
     if (n && copy_mode_ == 3) {
       HIPCHECK(hipEventSynchronize(ev_done_[p]));
-      // large egress split over two SDMA engines (one engine tops out below the link's
-      // device -> host rate); each part decrements the slot's signal once
+      // sdma_split 2: large egress split over two SDMA engines, each part decrementing the
+      // slot's signal once (measured slower on MI355X: 28.9 vs 38.6 M msgs/s, p99 6.6 ms,
+      // profiles/r4_sdma_split.md -- off by default)
       const int k = (n >= (2u << 20) && sdma_engine2_) ? 2 : 1;
       hsa_signal_store_screlease(sdma_sig_[e], k);
       const u64 half = k == 2 ? ((n / 2) & ~(u64)4095) : n;
@@ -1927,6 +1952,9 @@ class Engine {
     par1_.push_back([m, p1](DS& io) { io.*m = p1; });
   }
   GetReq* stage_gets_[2] = {nullptr, nullptr};
+  u32* stage_unp_[2] = {nullptr, nullptr};
+  std::mutex unp_mu_;
+  std::vector<u32> pend_unp_;
   u32 nget_[2] = {0, 0};
   HostIO io_[2];
   CmqEngineApi api_{};
@@ -1938,7 +1966,7 @@ class Engine {
   int copy_mode_ = 0;
   hsa_agent_t gpu_agent_{}, cpu_agent_{};
   hsa_amd_sdma_engine_id_t sdma_engine_{}, sdma_engine2_{};
-  int sdma_split_ = 2;
+  int sdma_split_ = 1;
   hsa_signal_t sdma_sig_[EGRESS_SLOTS] = {};
   bool sdma_pending_[EGRESS_SLOTS] = {};
   u32 copy_wgs_ = 16;
@@ -1998,6 +2026,7 @@ PYBIND11_MODULE(_dataplane, m) {
            py::arg("flags") = 0)
       .def("launch", &Engine::launch)
       .def("prefetch", &Engine::prefetch, py::arg("payload_ptr"), py::arg("payload_len"))
+      .def("stage_unpause", &Engine::stage_unpause)
       .def("stage_gets", [](Engine& e, py::buffer b) {
              py::buffer_info bi = b.request();
              const size_t nb = (size_t)bi.size * bi.itemsize;
