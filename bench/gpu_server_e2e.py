@@ -54,6 +54,7 @@ def plane_for(spec):
     return GpuDataPlane(c_max=512, chpc=8, q_max=256, cons_max=1024, seg_max=512, cmd_max=1 << 17,
                         deliv_max=1 << 17, msg_max=1 << 21, ucap=8192, deliver_cap=8192,
                         ingress_cap=64 << 20, egress_cap=160 << 20, log_bytes=8 << 30, ring_pool=1 << 25,
+                        spill_bytes=8 << 30,   # (the broker's default tiering: old bodies leave HBM)
                         tb_max=256, default_queue_capacity=1 << 20, persist=int(persist),
                         persist_max=1 << 16, persist_bytes=512 << 20, carry_cap=SIZING["carry_cap"])
 
@@ -196,7 +197,9 @@ def run_one(core, name, spec, io, io_threads, seconds, rate=0.0, lg_threads=12, 
         except Exception as e:   # diagnostics only
             after = {"error": repr(e)}
         b.stop()
+        body_log = None
         if store is not None:
+            body_log = store.body_stats() if hasattr(store, "body_stats") else None
             store.close()
     lc = getattr(plane, "last_counters", {}) or {}
     r["engine_host_s"] = {k: round(v, 4) for k, v in plane.eng.host_times(False).items()}
@@ -220,7 +223,7 @@ def run_one(core, name, spec, io, io_threads, seconds, rate=0.0, lg_threads=12, 
                            gets_per_s=sum(g[0] + g[1] for g in gout) / max(1e-9, max((g[2] for g in gout), default=1)),
                            device_gets=st.get("device_gets", 0)) if n_getters else None),
              last_step={k: lc.get(k) for k in ("n_ring_full", "n_dropped_nomem")},
-             store=getattr(b, "_pw_stats", None))
+             store=getattr(b, "_pw_stats", None), body_log=body_log)
     del plane
     return r
 

@@ -253,6 +253,7 @@ def test_sharded_rank_config_and_large_message_to_owner(tmp_path):
     conf.write_text(open(SMALL_CONF).read() + """
 chana.mq.gpu {
   body-log-bytes = 68719476736
+  spill-bytes = 1073741824
   ingress-bytes = 100663296
   egress-bytes = 167772160
   message-table = 4194304
