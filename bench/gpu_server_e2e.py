@@ -78,6 +78,7 @@ def thread_cpu():
 
 
 FE_CFG = {}
+BROKER_CFG = {}
 # per-connection bytes per step (the front end reads at most this, and at most the room
 # left in the connection's device carry, so two steps in flight need carry >= 2x): the
 # batch a step can take from one producer, so the ceiling of throughput per step period
@@ -121,6 +122,8 @@ def run_one(core, name, spec, io, io_threads, seconds, rate=0.0, lg_threads=12, 
         store = core.Store()
         store.open(store_dir or tempfile.mkdtemp(prefix="cmq-gpu-store-"), True)
     bkw = dict(spec.get("_broker", {}))
+    if persist and BROKER_CFG.get("persist_group_ms"):
+        bkw["persist_group_ms"] = BROKER_CFG["persist_group_ms"]
     spec = {k: v for k, v in spec.items() if not k.startswith("_")}
     b = GpuBroker(plane, idle_step_ms=0.5, store=store, io=io, io_threads=io_threads,
                   per_conn_read=SIZING["per_conn_read"], fe_cfg=FE_CFG, **bkw).start()
@@ -344,10 +347,13 @@ def main():
     ap.add_argument("--sharded", type=int, default=0,
                     help="N > 1: the pipelined sharded server with N ranks on this GPU (producers on rank 1, "
                          "consumers on rank 0 and then on rank 1 through device links)")
+    ap.add_argument("--persist-group-ms", type=float, default=0.0,
+                    help="durable specs: a group commit waits until its oldest batch is this old")
     ap.add_argument("--getters", type=int, default=0,
                     help="also run each spec with this many Basic.Get pollers on pre-filled queues (the load's "
                          "throughput with and without them, and the gets/s)")
     args = ap.parse_args()
+    BROKER_CFG["persist_group_ms"] = args.persist_group_ms
     SIZING.update(per_conn_read=args.per_conn_read, carry_cap=max(args.carry_cap, 2 * args.per_conn_read))
     if args.wblock_high:
         FE_CFG.update(wblock_high=args.wblock_high, wblock_low=args.wblock_high // 4)

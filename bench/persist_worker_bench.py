@@ -49,12 +49,15 @@ def main():
     ap.add_argument("--window", type=int, default=1,
                     help="steps in flight before the producer waits for commits (1 = commit every step "
                          "before the next; the pipelined front end keeps stepping while a commit runs)")
+    ap.add_argument("--group-ms", type=float, default=0.0, help="PersistWorker.set_group_delay")
     a = ap.parse_args()
     core = load()
     d = a.dir or tempfile.mkdtemp()
     st = core.Store()
     st.open(os.path.join(d, "store"), a.fsync)
     w = core.PersistWorker(st)
+    if a.group_ms:
+        w.set_group_delay(a.group_ms)
     for q in range(a.queues):
         w.set_queue(q, f"AMQ.DEFAULT-_.cfg4.q{q}")
     w.start()

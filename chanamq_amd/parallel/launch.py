@@ -66,11 +66,11 @@ class Launcher:
             p.wait(None if end is None else max(0.1, end - time.time()))
         return [p.returncode for p in self.procs]
 
-    def stop(self, sig=None):
+    def stop(self, sig=None, timeout=30):
         for p in self.procs:
             if p.poll() is None:
                 p.terminate() if sig is None else p.send_signal(sig)
-        return self.wait(30)
+        return self.wait(timeout)
 
 
 def main(argv=None):

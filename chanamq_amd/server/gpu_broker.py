@@ -117,7 +117,8 @@ class GpuBroker:
                  idle_step_ms=2.0, product="chanamq-amd", version="0.1.0", io="native",
                  ingress_bytes=64 << 20, per_conn_read=256 << 10, mem_high_watermark=None, mem_low_watermark=None,
                  store=None, node=None, reuseport=False, io_threads=4, fe_cfg=None, spill_at=None, spill_hot=1024,
-                 confirm_read=128 << 10, cold_dir=None, cold=True, cold_hot=1 << 16, cold_window=1 << 15):
+                 confirm_read=128 << 10, cold_dir=None, cold=True, cold_hot=1 << 16, cold_window=1 << 15,
+                 persist_group_ms=0.0):
         """``io``: "pipeline" = native pipelined front end (csrc/core/frontend.cpp: IO
         threads + a stepper thread keeping two steps in flight, no Python per step),
         "native" = C++ batched gateway polled by a Python step loop (csrc/core/
@@ -131,7 +132,8 @@ class GpuBroker:
             raise ValueError("io='pipeline' needs a GPU data plane (sharded: built with native_xchg=1)")
         self.io = io
         self.io_threads = io_threads
-        self.fe_cfg = dict(fe_cfg or {})    # extra native front-end settings (frontend.hpp FrontendCfg)
+        self.fe_cfg = dict(fe_cfg or {})
+        self.persist_group_ms = persist_group_ms    # extra native front-end settings (frontend.hpp FrontendCfg)
         self.gw = None
         self.fe = None
         self._fe_stats = None
@@ -240,6 +242,8 @@ class GpuBroker:
             self.port = self.fe.port
             if self.persistence is not None:   # native write-behind: records never touch Python
                 self._pw = load().PersistWorker(self.persistence.store)
+                if self.persist_group_ms > 0:   # see PersistWorker::set_group_delay
+                    self._pw.set_group_delay(float(self.persist_group_ms))
                 self.fe.attach_persist(self._pw)
                 self.persistence.attach_native(self._pw)
             if self.node is not None:

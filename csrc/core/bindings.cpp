@@ -308,6 +308,7 @@ PYBIND11_MODULE(_core, m) {
              w.submit(step, std::string(persist), std::string(consumed));
            })
       .def("drain", &PersistWorker::drain, py::call_guard<py::gil_scoped_release>())
+      .def("set_group_delay", &PersistWorker::set_group_delay)
       .def("stats", [](PersistWorker& w) {
              py::dict o;
              o["rows"] = w.rows(); o["commits"] = w.commits(); o["body_bytes"] = w.bytes(); o["busy_s"] = w.busy_s();

@@ -56,7 +56,7 @@ void PersistWorker::seed_row(const std::string& qid, i64 msgid, i64 offset, i32 
 void PersistWorker::submit(u64 step, std::string persist, std::string consumed) {
   {
     std::lock_guard<std::mutex> g(mu_);
-    q_.push_back(Batch{step, std::move(persist), std::move(consumed)});
+    q_.push_back(Batch{step, std::move(persist), std::move(consumed), std::chrono::steady_clock::now()});
     ++submitted_;
   }
   cv_.notify_one();
@@ -73,6 +73,11 @@ void PersistWorker::loop() {
   while (true) {
     cv_.wait(g, [&] { return !q_.empty() || !running_; });
     if (q_.empty() && !running_) break;
+    const i64 delay = delay_us_.load();
+    if (delay > 0 && running_) {   // let the group gather (a deep queue goes at once)
+      const auto until = q_.front().t + std::chrono::microseconds(delay);
+      cv_.wait_until(g, until, [&] { return !running_ || q_.size() >= 256; });
+    }
     std::deque<Batch> work;
     work.swap(q_);
     g.unlock();

@@ -20,6 +20,7 @@
 // WAL (nothing to recover), so the store's work falls as the load rises.
 #pragma once
 #include <atomic>
+#include <chrono>
 #include <condition_variable>
 #include <deque>
 #include <functional>
@@ -49,6 +50,9 @@ class PersistWorker {
   // records of step `step` (0 = a host-run step / Basic.Get: no egress held)
   void submit(u64 step, std::string persist, std::string consumed);
   void drain();                                       // every submitted batch committed
+  // a group commit starts once its oldest batch is this old (0 = at once): messages
+  // consumed within the window never reach the disk, at the price of later confirms
+  void set_group_delay(double ms) { delay_us_ = (i64)(ms * 1000.0); }
   u64 rows() const { return rows_; }
   u64 commits() const { return commits_; }
   u64 bytes() const { return bytes_; }
@@ -59,7 +63,7 @@ class PersistWorker {
   double sync_s() const { return sync_s_; }
 
  private:
-  struct Batch { u64 step; std::string persist, consumed; };
+  struct Batch { u64 step; std::string persist, consumed; std::chrono::steady_clock::time_point t; };
   struct Row { i64 offset; i32 size; bool unack; };
   struct RowKey {
     u32 q; i64 id;
@@ -102,6 +106,7 @@ class PersistWorker {
   std::vector<BodyLog::Loc> locs_;
   std::atomic<u64> rows_{0}, commits_{0}, bytes_{0};
   double busy_s_ = 0, apply_s_ = 0, flush_s_ = 0, sync_s_ = 0;
+  std::atomic<i64> delay_us_{0};
 };
 
 }  // namespace cmq

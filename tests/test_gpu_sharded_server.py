@@ -261,7 +261,7 @@ chana.mq.gpu {
 """)
     env = dict(os.environ, PYTHONPATH=os.path.dirname(HERE))
     ln = Launcher(2, ["-m", "chanamq_amd.server.sharded", "--config", str(conf), "--plane", "gpu", "--port", "0",
-                      "--backend", "gloo", "--info-dir", str(tmp_path), "--xchg-timeout-ms", "30000"], env=env).start()
+                      "--backend", "gloo", "--info-dir", str(tmp_path), "--xchg-timeout-ms", "10000"], env=env).start()
     try:
         deadline = time.time() + 240
         while time.time() < deadline and not all((tmp_path / f"rank{r}.json").exists() for r in range(2)):
@@ -298,4 +298,4 @@ chana.mq.gpu {
         c1.close()
         assert not ln.poll()
     finally:
-        ln.stop()
+        ln.stop(timeout=90)   # a rank outliving its peer waits out the exchange timeout
