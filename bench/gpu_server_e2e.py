@@ -122,7 +122,7 @@ def run_one(core, name, spec, io, io_threads, seconds, rate=0.0, lg_threads=12, 
         store = core.Store()
         store.open(store_dir or tempfile.mkdtemp(prefix="cmq-gpu-store-"), True)
     bkw = dict(spec.get("_broker", {}))
-    if persist and BROKER_CFG.get("persist_group_ms"):
+    if persist and "persist_group_ms" in BROKER_CFG:
         bkw["persist_group_ms"] = BROKER_CFG["persist_group_ms"]
     spec = {k: v for k, v in spec.items() if not k.startswith("_")}
     b = GpuBroker(plane, idle_step_ms=0.5, store=store, io=io, io_threads=io_threads,
@@ -347,7 +347,7 @@ def main():
     ap.add_argument("--sharded", type=int, default=0,
                     help="N > 1: the pipelined sharded server with N ranks on this GPU (producers on rank 1, "
                          "consumers on rank 0 and then on rank 1 through device links)")
-    ap.add_argument("--persist-group-ms", type=float, default=0.0,
+    ap.add_argument("--persist-group-ms", type=float, default=3.0,
                     help="durable specs: a group commit waits until its oldest batch is this old")
     ap.add_argument("--getters", type=int, default=0,
                     help="also run each spec with this many Basic.Get pollers on pre-filled queues (the load's "
