@@ -187,8 +187,9 @@ def main():
     ap.add_argument("--mode", choices=["sharded", "independent"], default="sharded",
                     help="N>1: one sharded broker (cross-GPU routing over RCCL) or N unconnected shards")
     ap.add_argument("--prefetch", type=int, default=1,
-                    help="1: queue step t+1's ingress H2D right after submitting step t (the copy engine never "
-                         "idles between steps; the step's latency clock starts there); 0: H2D at submit")
+                    help="N: keep the ingress H2D of the next N steps queued (submitted step t -> t+1..t+N; "
+                         "the copy engine never idles between steps; a step's latency clock starts when its "
+                         "bytes are queued); 0: H2D at submit")
     ap.add_argument("--xchg", choices=["native", "torch"], default="native",
                     help="N>1 sharded: the engine's own exchange -- grouped RCCL send/recv on its exchange "
                          "stream, counts through host shared memory (the code the sharded server runs; "
@@ -301,6 +302,7 @@ def main():
                     if t0 is not None:
                         lat_w.append((t - t0, int(lh[k])))
 
+        end = step_i + n
         for i in range(n):
             b = step_i % args.blocks
             if step_i not in pre:   # (a prefetched step's clock started when its bytes were queued)
@@ -317,11 +319,16 @@ def main():
             else:
                 pending.append((submit(segs[b], base + offs[b], blens[b]), step_i))
             step_i += 1
-            if args.prefetch and i < n - 1:
-                nb = step_i % args.blocks
-                sub_t[step_i] = time.perf_counter()
-                if dp.prefetch(base + offs[nb], blens[nb]):
-                    pre.add(step_i)
+            # the next steps of this run whose bytes are not queued yet (in order: the engine
+            # queues each call's payload for the next such step)
+            nxt = max(step_i, max(pre) + 1 if pre else step_i)
+            while args.prefetch and nxt < min(step_i + args.prefetch, end):
+                nb = nxt % args.blocks
+                sub_t[nxt] = time.perf_counter()
+                if not dp.prefetch(base + offs[nb], blens[nb]):
+                    break
+                pre.add(nxt)
+                nxt += 1
             if len(pending) > 1:
                 t, s = pending.pop(0)
                 account(dp.finish(t, collect=False, wait_egress=False), s)

@@ -562,6 +562,7 @@ class Engine {
     if (copy_mode_ == 3) init_sdma();
     HIPCHECK(hipStreamCreateWithFlags(&s_comp_, hipStreamNonBlocking));
     HIPCHECK(hipStreamCreateWithFlags(&s_h2d_, hipStreamNonBlocking));
+    HIPCHECK(hipStreamCreateWithFlags(&s_pre_, hipStreamNonBlocking));   // ingress payloads (overlap)
     HIPCHECK(hipStreamCreateWithFlags(&s_d2h_, hipStreamNonBlocking));
     {   // the ingest half gets its own (high-priority) hardware queue: next to the routing
         // half of the previous step, not queued behind it
@@ -571,6 +572,7 @@ class Engine {
     }
     for (int p = 0; p < 2; ++p) {
       HIPCHECK(hipEventCreateWithFlags(&ev_ing_[p], hipEventDisableTiming));
+      HIPCHECK(hipEventCreateWithFlags(&ev_pre_[p], hipEventDisableTiming));
       HIPCHECK(hipEventCreateWithFlags(&ev_rest_[p], hipEventDisableTiming));
     }
     // overlap (world 1): the step's ingest half runs on its own stream, next to the
@@ -600,6 +602,7 @@ class Engine {
   ~Engine() {
     (void)hipStreamSynchronize(s_comp_);
     (void)hipStreamSynchronize(s_h2d_);
+    (void)hipStreamSynchronize(s_pre_);
     (void)hipStreamSynchronize(s_d2h_);
     for (int p = 0; p < 2; ++p) {
       if (graph_exec_[p]) (void)hipGraphExecDestroy(graph_exec_[p]);
@@ -793,14 +796,18 @@ class Engine {
     // the payload may already be on its way (prefetch): then only the step's descriptors
     // follow it on the H2D stream
     const bool pre = pre_[p];
-    if (pre && (pre_ptr_[p] != payload_ptr || pre_len_[p] != payload_len))
+    if (pre && (pre_seq_[p] != step || pre_ptr_[p] != payload_ptr || pre_len_[p] != payload_len))
       throw std::runtime_error("submit: payload differs from the one prefetched for this step");
     pre_[p] = false;
     HIPCHECK(hipMemcpyAsync((void*)io_[p].in, in, sizeof(StepIn), hipMemcpyHostToDevice, s_h2d_));
     if (sb) HIPCHECK(hipMemcpyAsync((void*)io_[p].segs, stage_segs_[p], sb, hipMemcpyHostToDevice, s_h2d_));
+    // overlapped engines move payloads on their own stream (prefetches run ahead of the
+    // small per-step copies there; the ingest half waits for both)
+    hipStream_t ps = overlap_ ? s_pre_ : s_h2d_;
     if (payload_len && !pre)
       HIPCHECK(hipMemcpyAsync((void*)io_[p].ingress, (const void*)payload_ptr, payload_len,
-                              sdma_ ? hipMemcpyDeviceToDeviceNoCU : hipMemcpyHostToDevice, s_h2d_));
+                              sdma_ ? hipMemcpyDeviceToDeviceNoCU : hipMemcpyHostToDevice, ps));
+    if (overlap_) HIPCHECK(hipEventRecord(ev_pre_[p], s_pre_));
     HIPCHECK(hipEventRecord(ev_h2d_[p], s_h2d_));
     inflight_[p] = true;
     staged_[p] = true;
@@ -814,15 +821,25 @@ class Engine {
   // half of the step two back, the last reader of this parity's ingress buffer -- so the
   // copy engine never idles between steps.  The step is then submit()ed with the same
   // payload.  false: not applicable (no overlap), nothing queued.
+  // Up to two steps ahead: each call queues the payload of the next step not yet queued
+  // (the next submit, then the one after it).
   bool prefetch(u64 payload_ptr, u64 payload_len) {
     if (!overlap_ || !payload_len) return false;
-    const int p = (int)(seq_ & 1);
-    if (pre_[p] || staged_[p]) throw std::runtime_error("prefetch: this step's payload is already queued");
+    u64 tgt = seq_;
+    int p = (int)(tgt & 1);
+    if (pre_[p]) {   // the next submit's payload is queued already: the one after it
+      tgt = seq_ + 1;
+      p = (int)(tgt & 1);
+      if (pre_[p]) return false;
+    }
+    if (staged_[p]) throw std::runtime_error("prefetch: this step's payload is already queued");
     if (payload_len > d_.ingress_cap) throw std::runtime_error("ingress payload exceeds ingress_cap");
-    if (ing_issued_[p]) HIPCHECK(hipStreamWaitEvent(s_h2d_, ev_ing_[p], 0));
+    // the buffer's last reader: the ingest half of step tgt - 2 (launched by now)
+    if (ing_issued_[p]) HIPCHECK(hipStreamWaitEvent(s_pre_, ev_ing_[p], 0));
     HIPCHECK(hipMemcpyAsync((void*)io_[p].ingress, (const void*)payload_ptr, payload_len,
-                            sdma_ ? hipMemcpyDeviceToDeviceNoCU : hipMemcpyHostToDevice, s_h2d_));
+                            sdma_ ? hipMemcpyDeviceToDeviceNoCU : hipMemcpyHostToDevice, s_pre_));
     pre_[p] = true;
+    pre_seq_[p] = tgt;
     pre_ptr_[p] = payload_ptr;
     pre_len_[p] = payload_len;
     return true;
@@ -869,6 +886,7 @@ class Engine {
       // (the routing half of step t-2); the routing half on s_comp_ behind it and behind
       // the previous step's routing half (stream order), as a single step would run
       HIPCHECK(hipStreamWaitEvent(s_ing_, ev_h2d_[p], 0));
+      HIPCHECK(hipStreamWaitEvent(s_ing_, ev_pre_[p], 0));
       if (rest_issued_[p]) HIPCHECK(hipStreamWaitEvent(s_ing_, ev_rest_[p], 0));
       {
         HostTimer t(&ht_[2]);
@@ -1624,6 +1642,7 @@ class Engine {
 
   void sync() {
     HIPCHECK(hipStreamSynchronize(s_h2d_));
+    HIPCHECK(hipStreamSynchronize(s_pre_));
     HIPCHECK(hipStreamSynchronize(s_ing_));
     HIPCHECK(hipStreamSynchronize(s_comp_));
     HIPCHECK(hipStreamSynchronize(s_d2h_));
@@ -1939,7 +1958,9 @@ class Engine {
   hipEvent_t ev_ing_[2], ev_rest_[2];
   bool rest_issued_[2] = {false, false}, ing_issued_[2] = {false, false};
   bool pre_[2] = {false, false};        // the next step's payload H2D already queued (prefetch)
-  u64 pre_ptr_[2] = {0, 0}, pre_len_[2] = {0, 0};
+  u64 pre_ptr_[2] = {0, 0}, pre_len_[2] = {0, 0}, pre_seq_[2] = {0, 0};
+  hipEvent_t ev_pre_[2];
+  hipStream_t s_pre_ = nullptr;
   hipGraphExec_t graph_ing_[2] = {nullptr, nullptr};
   hipGraphExec_t graph_rest_[2] = {nullptr, nullptr};
   u64* scan_status_ing_ = nullptr;
