@@ -3855,6 +3855,17 @@ __global__ __launch_bounds__(256) void k_copy_out(u8* dst, const u8* src, u64 n)
   for (u64 i = (nv << 4) + gtid; i < n; i += gsz) dst[i] = src[i];
 }
 
+// the same, sized on the device (the step's egress byte count): launched right behind the
+// step's kernels, with no host round trip between render and copy (copy_engine=2, overlap)
+__global__ __launch_bounds__(256) void k_copy_out_dev(u8* dst, const u8* src, const Counters* c) {
+  const u64 n = c->egress_bytes;
+  const u64 gtid = blockIdx.x * blockDim.x + threadIdx.x, gsz = (u64)gridDim.x * blockDim.x;
+  const u64 nv = n >> 4;
+  typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+  for (u64 i = gtid; i < nv; i += gsz) ((v4u*)dst)[i] = __builtin_nontemporal_load(((const v4u*)src) + i);
+  for (u64 i = (nv << 4) + gtid; i < n; i += gsz) dst[i] = src[i];
+}
+
 // copy the step's small host-visible results to their host-mapped mirrors in one pass
 // (16-B stores, grid-stride) once the whole step has run
 DEV void copy16(u8* dst, const u8* src, u64 n, u64 gtid, u64 gsz) {

@@ -905,6 +905,14 @@ class Engine {
       HIPCHECK(hipEventRecord(ev_rest_[p], s_comp_));
       rest_issued_[p] = true;
       HIPCHECK(hipEventRecord(ev_done_[p], s_comp_));
+      if (copy_mode_ == 2) {   // egress D2H right behind the step, sized on the device
+        HIPCHECK(hipStreamWaitEvent(s_d2h_, ev_rest_[p], 0));
+        hipLaunchKernelGGL(k_copy_out_dev, dim3(copy_wgs_), dim3(256), 0, s_d2h_, egress_host_dev_[e],
+                           (const u8*)egress_dev_[e], (const Counters*)io_[p].ctr);
+        HIPCHECK(hipEventRecord(ev_d2h_[e], s_d2h_));
+        d2h_issued_[e] = true;
+        eager_d2h_[p] = true;
+      }
       return;
     }
     HIPCHECK(hipStreamWaitEvent(s_comp_, ev_h2d_[p], 0));
@@ -1551,6 +1559,10 @@ class Engine {
     const Counters* c = (const Counters*)buf("ctr_host" + std::to_string(p)).ptr;
     u64 n = c->egress_bytes;
     const int e = slot_of_[p];
+    if (eager_d2h_[p]) {   // already queued behind the step (launch)
+      eager_d2h_[p] = false;
+      return n;
+    }
     HIPCHECK(hipStreamWaitEvent(s_d2h_, ev_done_[p], 0));
     if (n && copy_mode_ == 3) {
       HIPCHECK(hipEventSynchronize(ev_done_[p]));
@@ -1957,6 +1969,7 @@ class Engine {
   hipStream_t s_ing_ = nullptr;
   hipEvent_t ev_ing_[2], ev_rest_[2];
   bool rest_issued_[2] = {false, false}, ing_issued_[2] = {false, false};
+  bool eager_d2h_[2] = {false, false};   // the step's egress copy was queued at launch (copy_mode 2)
   bool pre_[2] = {false, false};        // the next step's payload H2D already queued (prefetch)
   u64 pre_ptr_[2] = {0, 0}, pre_len_[2] = {0, 0}, pre_seq_[2] = {0, 0};
   hipEvent_t ev_pre_[2];

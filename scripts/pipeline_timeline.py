@@ -32,8 +32,10 @@ ks = sorted(rows("*kernel_trace.csv"), key=lambda r: int(r["Start_Timestamp"]))
 cs = rows("*memory_copy_trace.csv")
 h2d, d2h = [], []
 for r in cs:
-    size = int(r.get("Bytes") or r.get("Size") or 0)
-    if size < min_bytes:
+    size = r.get("Bytes") or r.get("Size")
+    span_ns = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+    # (no size column in this rocprofv3 version: a payload copy is one longer than 20 us)
+    if (int(size) < min_bytes) if size else span_ns < 20000:
         continue
     kind = (r.get("Direction") or r.get("Kind") or "").upper()
     span = (int(r["Start_Timestamp"]), int(r["End_Timestamp"]))
