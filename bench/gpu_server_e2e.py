@@ -251,7 +251,7 @@ def wal_soak(core, seconds, io_threads=4, lg_threads=12, cons_threads=8, rate=0.
     def sample():
         while not done[0]:
             samples.append((round(time.time() - t0, 1), store.wal_bytes(), store.live_estimate(),
-                            store.compact_stats()["runs"]))
+                            store.compact_stats()["runs"], store.body_stats()["disk_bytes"]))
             time.sleep(1.0)
     import threading
     th = threading.Thread(target=sample, daemon=True)
@@ -266,6 +266,7 @@ def wal_soak(core, seconds, io_threads=4, lg_threads=12, cons_threads=8, rate=0.
     cs = store.compact_stats()
     wal_end = store.wal_bytes()
     rows = {t: store.row_count(t) for t in ("msgs", "queues", "queue_unacks")}
+    body_log = store.body_stats()
     store.close()
     del plane
     t1 = time.perf_counter()
@@ -280,7 +281,7 @@ def wal_soak(core, seconds, io_threads=4, lg_threads=12, cons_threads=8, rate=0.
     return dict(name="config4_wal_soak", seconds=seconds, recv_msgs_per_s=r["received"] / r["elapsed"],
                 confirmed_per_s=r["confirmed"] / r["elapsed"], error=r["error"], wal_samples=samples,
                 wal_end_bytes=wal_end, rows_at_end=rows, compactions=cs, reopen_replay_s=replay_s,
-                recover_s=recover_s, recovered_msgs=recovered,
+                recover_s=recover_s, recovered_msgs=recovered, body_log=body_log,
                 body_bytes_written=getattr(b, "_pw_stats", {}).get("body_bytes"))
 
 

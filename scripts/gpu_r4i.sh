@@ -17,4 +17,6 @@ for cfg in ${BENCH:-"32768 sdma 16" "32768 kernel 16" "32768 kernel 32" "49152 k
 done
 timeout -k 10 600 python -u -m pytest tests/test_gpu_dataplane.py -x -q --timeout 400 --timeout-method thread -p no:cacheprovider -k "copykernel or graph" > $O/pytest.log 2>&1
 rc=$?; echo "pytest exit $rc" >> $O/pytest.log; tail -3 $O/pytest.log | grep -E "passed|failed"; fatal $rc pytest
+timeout -k 10 300 python -u bench/gpu_server_e2e.py --io-threads 8 --wal-soak 30 --out $O/e2e_config4_soak30.json > $O/e2e_config4_soak.log 2>&1
+rc=$?; fatal $rc soak; grep "^{" $O/e2e_config4_soak.log | cut -c1-600 | tail -1
 exit 0
