@@ -2059,7 +2059,10 @@ DEV void route_one(const DS& d, u32 p, u32 lane) {
 // 1024-thread block: the group's topic prefilter tiles on MFMA (fused k_topic_mfma), then
 // one wave per publish.  Pass 1 runs fused with the store (k_route_store) after
 // k_scan_route reserved the phase's log region.  The imports' pass 0 is k_import_route.
-__global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void k_route(DS d) {
+#ifndef ROUTE_WPE   // k_route occupancy target: 8 (two blocks per CU, 64 VGPRs, 12 VGPRs spilled)
+#define ROUTE_WPE 8     // or 4 (one block per CU, no spill): A/B through CHANAMQ_DP_SO
+#endif
+__global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(ROUTE_WPE))) void k_route(DS d) {
   const u32 lane = lane_id(), w = threadIdx.x >> 6;
   const u32 lo = d.tot[TS_RANGE_LO];
   u32 n = d.tot[TS_RANGE_HI];
