@@ -906,6 +906,8 @@ class Engine {
       rest_issued_[p] = true;
       HIPCHECK(hipEventRecord(ev_done_[p], s_comp_));
       if (copy_mode_ == 2) {   // egress D2H right behind the step, sized on the device
+        // (measured slower than the host-issued SDMA copy -- CU stores over PCIe stall
+        // behind the next step's kernels: 8.7 vs 32.9 M msgs/s, profiles/r4_bench/pre_*)
         HIPCHECK(hipStreamWaitEvent(s_d2h_, ev_rest_[p], 0));
         hipLaunchKernelGGL(k_copy_out_dev, dim3(copy_wgs_), dim3(256), 0, s_d2h_, egress_host_dev_[e],
                            (const u8*)egress_dev_[e], (const Counters*)io_[p].ctr);

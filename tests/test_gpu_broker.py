@@ -309,6 +309,10 @@ def test_durable_persistent_messages_survive_restart(kind, tmp_path):
     assert [d.body for d in got] == [b"p0", b"p1", b"p2", b"p3"]
     cc.basic_ack(got[1].delivery_tag, multiple=True)     # p0, p1 consumed; p2, p3 stay unacked
     assert [d.body for d in cc.consume_n(2)] == [b"p4", b"p5"]   # the freed credit: unacked too
+    import time
+    end = time.time() + 5   # the acked rows go with the next group commit (persist-group-ms)
+    while st.row_count("msgs") != 8 and time.time() < end:
+        cc.connection.process(0.02) if hasattr(cc, "connection") else time.sleep(0.02)
     assert st.row_count("msgs") == 8
     b.stop()
     st.close()
