@@ -18,4 +18,9 @@ for v in base wpe4; do
   f=$(find $O/t_$v -name "*kernel_stats.csv" | head -1); [ -n "$f" ] && cp $f $O/kernel_stats_$v.csv && grep -E "k_route\b|k_route\"|Name" $O/kernel_stats_$v.csv | cut -c1-200
   rm -rf $O/t_$v
 done
+unset CHANAMQ_DP_SO
+timeout -k 10 900 python -u -m pytest tests/test_gpu_dataplane.py tests/test_gpu_broker.py -q --timeout 400 --timeout-method thread -p no:cacheprovider > $O/pytest.log 2>&1
+rc=$?; echo "pytest exit $rc" >> $O/pytest.log; tail -3 $O/pytest.log | grep -E "passed|failed"; fatal $rc pytest
+timeout -k 10 300 python -u bench/gpu_server_e2e.py --io-threads 8 --wal-soak 30 --out $O/e2e_config4_soak30.json > $O/e2e_config4_soak.log 2>&1
+rc=$?; fatal $rc soak; grep "^{" $O/e2e_config4_soak.log | cut -c1-700 | tail -1
 exit 0
