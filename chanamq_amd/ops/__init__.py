@@ -76,11 +76,11 @@ def load():
     (raises ImportError with a build hint if it cannot be built)."""
     alt = os.environ.get("CHANAMQ_DP_SO")
     if alt:   # an A/B variant (build_variant)
-        import importlib.util
+        from importlib import util as ilu
         mod = sys.modules.get("chanamq_amd.ops._dataplane")
         if mod is None:
-            spec = importlib.util.spec_from_file_location("chanamq_amd.ops._dataplane", alt)
-            mod = importlib.util.module_from_spec(spec)
+            spec = ilu.spec_from_file_location("chanamq_amd.ops._dataplane", alt)
+            mod = ilu.module_from_spec(spec)
             spec.loader.exec_module(mod)
             sys.modules["chanamq_amd.ops._dataplane"] = mod
         return mod
