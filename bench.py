@@ -163,7 +163,10 @@ def main():
     ap.add_argument("--producers", type=int, default=256)
     ap.add_argument("--queues", type=int, default=16)
     ap.add_argument("--body", type=int, default=1024)
-    ap.add_argument("--chunk", type=int, default=65536, help="bytes per producer per step (TCP read)")
+    ap.add_argument("--chunk", type=int, default=49152,
+                    help="bytes per producer per step (TCP read); 49152 holds >= 36 M msgs/s at p50 ~0.9 ms at K=20 "
+                         "(65536: ~38 M at p50 1.08 ms, but box-to-box outliers; 32768: ~30 M at 0.73 ms; "
+                         "profiles/r4_summary.md)")
     ap.add_argument("--blocks", type=int, default=8)
     ap.add_argument("--soak-s", type=float, default=2.0,
                     help="after the timed steps (and the result line), keep stepping untimed for this long so "
