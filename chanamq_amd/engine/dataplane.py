@@ -360,7 +360,7 @@ class GpuDataPlane(ControlState):
         n = min(c["n_persist"], self.info["persist_max"])
         if not n:
             return []
-        raw = self.eng.host_view(f"persist{self._last_parity}")[:c["persist_used"]]
+        raw = self.eng.host_view(f"persist{self.eng.persist_slot(self._last_parity)}")[:c["persist_used"]]
         return parse_persist(raw)
 
     def _check_records(self, c):
@@ -378,7 +378,7 @@ class GpuDataPlane(ControlState):
         n = min(c["n_consumed"], self.info["persist_max"])
         if not n:
             return out
-        return out + parse_consumed(self.eng.host_view(f"consumed{self._last_parity}")[:n * CONSUMED_REC.itemsize])
+        return out + parse_consumed(self.eng.host_view(f"consumed{self.eng.persist_slot(self._last_parity)}")[:n * CONSUMED_REC.itemsize])
 
     def take_link_consumed(self, slots):
         """The last finished step's consumed records of the shadow queues ``slots``
@@ -387,7 +387,7 @@ class GpuDataPlane(ControlState):
         n = min(c["n_consumed"], self.info["persist_max"]) if c and self.info.get("persist") else 0
         if not n:
             return []
-        recs = parse_consumed(self.eng.host_view(f"consumed{self._last_parity}")[:n * CONSUMED_REC.itemsize])
+        recs = parse_consumed(self.eng.host_view(f"consumed{self.eng.persist_slot(self._last_parity)}")[:n * CONSUMED_REC.itemsize])
         return [r for r in recs if r[1] in slots]
 
     def take_persist_raw(self):
@@ -398,9 +398,9 @@ class GpuDataPlane(ControlState):
             return b"", b""
         self._check_records(c)
         p = self._last_parity
-        persist = bytes(self.eng.host_view(f"persist{p}")[:c["persist_used"]]) if c["n_persist"] else b""
+        persist = bytes(self.eng.host_view(f"persist{self.eng.persist_slot(p)}")[:c["persist_used"]]) if c["n_persist"] else b""
         n = min(c["n_consumed"], self.info["persist_max"])
-        consumed = bytes(self.eng.host_view(f"consumed{p}")[:n * CONSUMED_REC.itemsize]) if n else b""
+        consumed = bytes(self.eng.host_view(f"consumed{self.eng.persist_slot(p)}")[:n * CONSUMED_REC.itemsize]) if n else b""
         return persist, consumed
 
     def take_get_consumed(self):

@@ -187,6 +187,12 @@ void Frontend::stop() {
     if (io->th.joinable()) io->th.join();
   }
   ev_cv_.notify_all();
+  {
+    std::lock_guard<std::mutex> g(pc_mu_);
+    pc_stop_ = true;
+  }
+  pc_cv_.notify_all();
+  if (pc_th_.joinable()) pc_th_.join();   // (drains the queued copies first)
   // the engine is alive until the front end is stopped (and no step is in flight now)
   for (int k = 0; k < 3; ++k)
     if (arena_pinned_[k]) { api_->host_unregister(api_->eng, arena_[k]); arena_pinned_[k] = false; }
@@ -464,6 +470,42 @@ void Frontend::release(u64 step) {
 void Frontend::attach_persist(PersistWorker* w) {
   persist_ = w;
   w->on_commit([this](u64 step) { release(step); });
+  if (!pc_th_.joinable()) pc_th_ = std::thread([this] { copier(); });
+}
+
+void Frontend::copier() {
+  pthread_setname_np(pthread_self(), "cmq-pcopy");
+  std::unique_lock<std::mutex> g(pc_mu_);
+  while (true) {
+    pc_cv_.wait(g, [&] { return !pc_q_.empty() || pc_stop_; });
+    if (pc_q_.empty()) break;
+    PCopy c = pc_q_.front();
+    pc_q_.pop_front();
+    ++pc_active_;
+    g.unlock();
+    std::string a, b;
+    if (c.plen) a.assign((const char*)c.persist, c.plen);
+    if (c.clen) b.assign((const char*)c.consumed, c.clen);
+    persist_->submit(c.step, std::move(a), std::move(b));
+    g.lock();
+    --pc_active_;
+    pc_done_cv_.notify_all();
+  }
+}
+
+void Frontend::post_copy(const PCopy& c) {
+  {
+    std::lock_guard<std::mutex> g(pc_mu_);
+    pc_q_.push_back(c);
+  }
+  pc_cv_.notify_one();
+}
+
+// before the engine reuses a record slot: at most `max_pending` copies still to run
+void Frontend::wait_copies(size_t max_pending) {
+  if (!pc_th_.joinable()) return;
+  std::unique_lock<std::mutex> g(pc_mu_);
+  pc_done_cv_.wait(g, [&] { return pc_q_.size() + pc_active_ <= max_pending; });
 }
 
 FeStats Frontend::stats() {
@@ -974,15 +1016,21 @@ void Frontend::finish_oldest(std::deque<Inflight>& inflight) {
       post(std::move(e));
       return;
     }
-    FeEvent e;
-    e.kind = FE_PERSIST;
-    e.a = f.step;
-    e.b = 0;
-    if (c.n_persist) e.data.assign((const char*)api_->persist_host(api_->eng, p), c.persist_used);
-    if (c.n_consumed)
-      e.data2.assign((const char*)api_->consumed_host(api_->eng, p), (size_t)c.n_consumed * sizeof(ConsumedRec));
-    if (persist_) persist_->submit(f.step, std::move(e.data), std::move(e.data2));
-    else post(std::move(e));
+    if (persist_) {   // copied off the stepper (the slot outlives this step by PSLOTS - 1)
+      post_copy(PCopy{f.step, c.n_persist ? api_->persist_host(api_->eng, p) : nullptr,
+                      c.n_persist ? (size_t)c.persist_used : 0,
+                      c.n_consumed ? (const u8*)api_->consumed_host(api_->eng, p) : nullptr,
+                      c.n_consumed ? (size_t)c.n_consumed * sizeof(ConsumedRec) : 0});
+    } else {
+      FeEvent e;
+      e.kind = FE_PERSIST;
+      e.a = f.step;
+      e.b = 0;
+      if (c.n_persist) e.data.assign((const char*)api_->persist_host(api_->eng, p), c.persist_used);
+      if (c.n_consumed)
+        e.data2.assign((const char*)api_->consumed_host(api_->eng, p), (size_t)c.n_consumed * sizeof(ConsumedRec));
+      post(std::move(e));
+    }
     needs_commit = true;
   }
   const int slot = api_->egress_slot(api_->eng, p);
@@ -1041,6 +1089,7 @@ void Frontend::stepper() {
     }
     if (want_pause) {
       while (!inflight.empty() && !failed_) finish_oldest(inflight);
+      wait_copies(0);   // a host-run step may reuse any record slot
       flush_pending(false);
       std::unique_lock<std::mutex> g(st_mu_);
       paused_ = true;
@@ -1105,6 +1154,7 @@ void Frontend::stepper() {
       i64 t1 = now_ns();
       Inflight f;
       stage_gets(f);
+      wait_copies(PSLOTS - 3);   // the slot this submit takes was last used PSLOTS steps back
       int p = api_->submit(api_->eng, segs.data(), (u32)segs.size(), arena_[arena_i_], used, wall_ms(), cfg_.worker);
       if (!check(p)) break;
       {
@@ -1281,6 +1331,7 @@ void Frontend::stepper_sharded() {
     stage_gets(f);
     {
       GpuWait gw(gpu_wait_since_);
+      wait_copies(PSLOTS - 3);
       p = api_->submit(api_->eng, segs.data(), (u32)segs.size(), arena_[arena_i_], ph_used_.load(), wall_ms(),
                        cfg_.worker);
     }
@@ -1334,6 +1385,7 @@ void Frontend::stepper_sharded() {
         int p2;
         {
           GpuWait gw(gpu_wait_since_);
+          wait_copies(PSLOTS - 3);
           p2 = api_->flush_submit ? api_->flush_submit(api_->eng, wall_ms(), cfg_.worker)
                                   : api_->submit(api_->eng, nullptr, 0, arena_[arena_i_], 0, wall_ms(), cfg_.worker);
         }

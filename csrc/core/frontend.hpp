@@ -270,6 +270,19 @@ class Frontend {
   std::vector<u32> held_cnt_;   // per connection: held entries carrying its bytes (keeps its order)
   u64 held_total_ = 0;
   PersistWorker* persist_ = nullptr;
+  // store records handed to the write-behind off the stepper thread: the engine keeps a
+  // step's records for PSLOTS - 1 further steps (rotating slots), a copier thread moves
+  // them into the worker's batches meanwhile; the stepper only waits when it falls behind
+  struct PCopy { u64 step; const u8* persist; size_t plen; const u8* consumed; size_t clen; };
+  void copier();
+  void post_copy(const PCopy& c);
+  void wait_copies(size_t max_pending);
+  std::thread pc_th_;
+  std::mutex pc_mu_;
+  std::condition_variable pc_cv_, pc_done_cv_;
+  std::deque<PCopy> pc_q_;
+  size_t pc_active_ = 0;
+  bool pc_stop_ = false;
   std::atomic<u64> released_{0};
   bool have_released_ = false;
 

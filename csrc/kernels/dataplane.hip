@@ -3832,7 +3832,7 @@ __global__ __launch_bounds__(256) void k_persist_pack(DS d) {
       if (lane == 0) atomicAdd(&d.ctr->n_persist_overflow, 1u);
       continue;
     }
-    u8* o = d.persist_h + off;
+    u8* o = d.ps_persist[d.in->pslot] + off;
     const u8* slot = msg_slot(d, m.log_off);
     if (lane == 0) {
       PersistHdr h;
@@ -3897,7 +3897,7 @@ DEV void host_out_copies(const DS& d, u64 gtid, u64 gsz) {
   if (d.persist) {
     u32 nr = d.ctr->n_consumed;
     if (nr > d.persist_max) nr = d.persist_max;
-    copy16((u8*)d.crec_h, (const u8*)d.crec, (u64)nr * sizeof(ConsumedRec), gtid, gsz);
+    copy16((u8*)d.ps_crec[d.in->pslot], (const u8*)d.crec, (u64)nr * sizeof(ConsumedRec), gtid, gsz);
   }
 }
 

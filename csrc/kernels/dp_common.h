@@ -52,7 +52,7 @@ struct StepIn {         // host -> device per step (64 B)
   u32 nget;             // Basic.Get requests of this step (DS.get_req, <= GET_STEP_MAX)
   u64 egress;           // device pointer: this step's egress slot (engine rotates slots)
   u32 nunp;             // connections to unpause before this step's frame scan (DS.unpause_req)
-  u32 pad1;
+  u32 pslot;            // host persist slot of this step (DS.ps_persist / ps_crec, rotating)
   u64 pad2;
 };
 

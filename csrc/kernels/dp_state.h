@@ -283,6 +283,11 @@ struct DS {
   ConsumedRec* crec;        // [persist_max]
   u32* ps_size;             // [persist_max]
   u32* ps_off;
+  // host-mapped store records of a step, in PSLOTS slots rotating per step (StepIn.pslot):
+  // a step's records stay valid for PSLOTS - 1 further steps, so the front end can hand
+  // them to the store without copying them on its stepper thread
+  u8* ps_persist[PSLOTS];      // [persist_bytes]
+  ConsumedRec* ps_crec[PSLOTS];  // [persist_max]
   u8* persist_h;            // host-mapped [persist_bytes]
   ConsumedRec* crec_h;      // host-mapped [persist_max]
 

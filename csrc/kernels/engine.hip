@@ -221,10 +221,12 @@ class Engine {
       io.grow_h = (RingMove*)hst(("grow" + sfx).c_str(), sizeof(RingMove) * GROW_MAX);
       io.conn_conf_h = (u32*)hst(("conn_conf" + sfx).c_str(), 4ull * d_.c_max);
       io.xchg = (u32*)hst(("xchg" + sfx).c_str(), 4ull * XC_WORDS);
-      if (d_.persist) {
-        io.persist_h = (u8*)hst(("persist" + sfx).c_str(), d_.persist_bytes + 64);
-        io.crec_h = (ConsumedRec*)hst(("consumed" + sfx).c_str(), sizeof(ConsumedRec) * (u64)d_.persist_max + 64);
-      }
+      if (d_.persist && p == 0)
+        for (int k = 0; k < PSLOTS; ++k) {   // shared by both parities (rotating per step)
+          const std::string ks = std::to_string(k);
+          d_.ps_persist[k] = (u8*)hst(("persist" + ks).c_str(), d_.persist_bytes + 64);
+          d_.ps_crec[k] = (ConsumedRec*)hst(("consumed" + ks).c_str(), sizeof(ConsumedRec) * (u64)d_.persist_max + 64);
+        }
       stage_in_[p] = (StepIn*)pinned(("stage_in" + sfx).c_str(), sizeof(StepIn));
       stage_segs_[p] = (SegIn*)pinned(("stage_segs" + sfx).c_str(), sizeof(SegIn) * d_.seg_max);
       // Basic.Get on the step: the requests (H2D with the step) and their answers
@@ -500,7 +502,6 @@ class Engine {
       io.ctrl = io_[p].ctrl; io.ctrl_rec = io_[p].ctrl_rec; io.xchg = io_[p].xchg;
       io.seg_out_h = io_[p].seg_out_h; io.conn_out_h = io_[p].conn_out_h; io.ctrl_h = io_[p].ctrl_h;
       io.ctrl_rec_h = io_[p].ctrl_rec_h; io.grow_h = io_[p].grow_h; io.conn_conf_h = io_[p].conn_conf_h;
-      io.persist_h = io_[p].persist_h; io.crec_h = io_[p].crec_h;
       io.get_req = io_[p].get_req; io.get_out_h = io_[p].get_out_h; io.unpause_req = io_[p].unpause_req;
       static_cast<DS&>(io_[p]) = io;
     }
@@ -769,6 +770,8 @@ class Engine {
     in->worker = worker;
     const int e = (int)(seq_ % EGRESS_SLOTS);
     in->egress = (u64)egress_dev_[e];
+    in->pslot = (u32)(seq_ % PSLOTS);
+    pslot_of_[p] = (int)in->pslot;
     slot_of_[p] = e;
     if (sb) memcpy(stage_segs_[p], segp, sb);
     // staged Basic.Get requests ride this step; their answers start out RETRY (a queue the
@@ -1462,8 +1465,8 @@ class Engine {
     a.ctrl_rec = [](void* e, int p) -> const CtrlRec* { return ((Engine*)e)->io_[p].ctrl_rec_hh; };
     a.ctrl = [](void* e, int p) -> const u8* { return ((Engine*)e)->io_[p].ctrl_hh; };
     a.egress_host = [](void* e, int slot) -> const u8* { return ((Engine*)e)->egress_host_[slot]; };
-    a.persist_host = [](void* e, int p) -> const u8* { return ((Engine*)e)->io_[p].persist_hh; };
-    a.consumed_host = [](void* e, int p) -> const ConsumedRec* { return ((Engine*)e)->io_[p].crec_hh; };
+    a.persist_host = [](void* e, int p) -> const u8* { return ((Engine*)e)->pslot_host(p); };
+    a.consumed_host = [](void* e, int p) -> const ConsumedRec* { return ((Engine*)e)->cslot_host(p); };
     a.wblock = (u32*)buf("conn_wblock").ptr;
     a.grow_host = [](void* e, int p) -> const RingMove* { return ((Engine*)e)->io_[p].grow_hh; };
     a.conn_conf = [](void* e, int p) -> const u32* { return ((Engine*)e)->io_[p].conn_conf_hh; };
@@ -1509,8 +1512,6 @@ class Engine {
       h.conn_out_hh = (const ConnOut*)buf("conn_out" + sfx).ptr;
       h.ctrl_rec_hh = (const CtrlRec*)buf("ctrl_rec" + sfx).ptr;
       h.ctrl_hh = (const u8*)buf("ctrl" + sfx).ptr;
-      h.persist_hh = d_.persist ? (const u8*)buf("persist" + sfx).ptr : nullptr;
-      h.crec_hh = d_.persist ? (const ConsumedRec*)buf("consumed" + sfx).ptr : nullptr;
       h.grow_hh = (const RingMove*)buf("grow" + sfx).ptr;
       h.conn_conf_hh = (const u32*)buf("conn_conf" + sfx).ptr;
       h.get_out_hh = (const GetOut*)buf("get_out" + sfx).ptr;
@@ -1609,6 +1610,14 @@ class Engine {
 
   // egress slot (host view "egress_host<slot>") of the step last submitted with parity p
   int egress_slot(int p) const { return slot_of_[p]; }
+  // store-record slot (host views "persist<slot>" / "consumed<slot>") of that step
+  int persist_slot(int p) const { return pslot_of_[p]; }
+  const u8* pslot_host(int p) {
+    return d_.persist ? (const u8*)buf("persist" + std::to_string(pslot_of_[p])).ptr : nullptr;
+  }
+  const ConsumedRec* cslot_host(int p) {
+    return d_.persist ? (const ConsumedRec*)buf("consumed" + std::to_string(pslot_of_[p])).ptr : nullptr;
+  }
 
   // HSA agents of this device and of the host, an SDMA engine for GPU -> host copies
   void init_sdma() {
@@ -1999,6 +2008,7 @@ class Engine {
   u8* egress_host_[EGRESS_SLOTS] = {};
   u8* egress_host_dev_[EGRESS_SLOTS] = {};
   int slot_of_[2] = {0, 0};
+  int pslot_of_[2] = {0, 0};
   int copy_mode_ = 0;
   hsa_agent_t gpu_agent_{}, cpu_agent_{};
   hsa_amd_sdma_engine_id_t sdma_engine_{}, sdma_engine2_{};
@@ -2062,6 +2072,7 @@ PYBIND11_MODULE(_dataplane, m) {
            py::arg("flags") = 0)
       .def("launch", &Engine::launch)
       .def("prefetch", &Engine::prefetch, py::arg("payload_ptr"), py::arg("payload_len"))
+      .def("persist_slot", &Engine::persist_slot)
       .def("stage_unpause", &Engine::stage_unpause)
       .def("stage_gets", [](Engine& e, py::buffer b) {
              py::buffer_info bi = b.request();

@@ -100,6 +100,7 @@ struct GetOut { u32 status; u32 msg_count; };
 // success and -1 on error (message: error()).  Parity p = the double-buffered step IO set
 // of a submitted step; its host-mapped outputs stay valid until the next submit of p.
 #define CMQ_STEP_ABI 6
+#define PSLOTS 4                // rotating host store-record slots (a step's records live PSLOTS - 1 more steps)
 #define UNPAUSE_STEP_MAX 1024   // connections unpaused per step (StepIn.nunp)
 struct CmqEngineApi {
   u32 abi;
