@@ -124,6 +124,8 @@ def run_one(core, name, spec, io, io_threads, seconds, rate=0.0, lg_threads=12, 
     bkw = dict(spec.get("_broker", {}))
     if persist and "persist_group_ms" in BROKER_CFG:
         bkw["persist_group_ms"] = BROKER_CFG["persist_group_ms"]
+    if BROKER_CFG.get("confirm_read"):
+        bkw["confirm_read"] = BROKER_CFG["confirm_read"]
     spec = {k: v for k, v in spec.items() if not k.startswith("_")}
     b = GpuBroker(plane, idle_step_ms=0.5, store=store, io=io, io_threads=io_threads,
                   per_conn_read=SIZING["per_conn_read"], fe_cfg=FE_CFG, **bkw).start()
@@ -348,6 +350,8 @@ def main():
     ap.add_argument("--sharded", type=int, default=0,
                     help="N > 1: the pipelined sharded server with N ranks on this GPU (producers on rank 1, "
                          "consumers on rank 0 and then on rank 1 through device links)")
+    ap.add_argument("--confirm-read", type=int, default=0,
+                    help="bytes per confirm-mode connection per step (0 = the broker default, 128 KiB)")
     ap.add_argument("--persist-group-ms", type=float, default=3.0,
                     help="durable specs: a group commit waits until its oldest batch is this old")
     ap.add_argument("--getters", type=int, default=0,
@@ -355,6 +359,7 @@ def main():
                          "throughput with and without them, and the gets/s)")
     args = ap.parse_args()
     BROKER_CFG["persist_group_ms"] = args.persist_group_ms
+    BROKER_CFG["confirm_read"] = args.confirm_read
     SIZING.update(per_conn_read=args.per_conn_read, carry_cap=max(args.carry_cap, 2 * args.per_conn_read))
     if args.wblock_high:
         FE_CFG.update(wblock_high=args.wblock_high, wblock_low=args.wblock_high // 4)
