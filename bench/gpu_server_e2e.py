@@ -352,7 +352,7 @@ def main():
                          "consumers on rank 0 and then on rank 1 through device links)")
     ap.add_argument("--confirm-read", type=int, default=0,
                     help="bytes per confirm-mode connection per step (0 = the broker default, 128 KiB)")
-    ap.add_argument("--persist-group-ms", type=float, default=3.0,
+    ap.add_argument("--persist-group-ms", type=float, default=2.0,
                     help="durable specs: a group commit waits until its oldest batch is this old")
     ap.add_argument("--getters", type=int, default=0,
                     help="also run each spec with this many Basic.Get pollers on pre-filled queues (the load's "

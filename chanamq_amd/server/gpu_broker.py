@@ -118,7 +118,7 @@ class GpuBroker:
                  ingress_bytes=64 << 20, per_conn_read=256 << 10, mem_high_watermark=None, mem_low_watermark=None,
                  store=None, node=None, reuseport=False, io_threads=4, fe_cfg=None, spill_at=None, spill_hot=1024,
                  confirm_read=128 << 10, cold_dir=None, cold=True, cold_hot=1 << 16, cold_window=1 << 15,
-                 persist_group_ms=3.0):
+                 persist_group_ms=2.0):
         """``io``: "pipeline" = native pipelined front end (csrc/core/frontend.cpp: IO
         threads + a stepper thread keeping two steps in flight, no Python per step),
         "native" = C++ batched gateway polled by a Python step loop (csrc/core/

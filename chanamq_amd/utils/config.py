@@ -276,7 +276,7 @@ class Config:
         broker = dict(io=str(g(k + "front-end", "pipeline")), io_threads=int(g(k + "io-threads", 4)),
                       idle_step_ms=float(g(k + "idle-step-ms", 1.0)), per_conn_read=int(g(k + "per-conn-read", 512 << 10)),
                       confirm_read=int(g(k + "confirm-read", 128 << 10)),
-                      persist_group_ms=float(g(k + "persist-group-ms", 3.0)),
+                      persist_group_ms=float(g(k + "persist-group-ms", 2.0)),
                       mem_high_watermark=hi, mem_low_watermark=lo)
         return plane, broker
 
