@@ -357,10 +357,14 @@ def main():
     if shards > 1 and not native:
         dp.exchanger.bytes_sent = 0
     dp.eng.host_times(True)
+    import gc
+    gc.collect()
+    gc.disable()   # the host loop is the pipeline's driver: no collector pause inside the window
     t0 = time.perf_counter()
     dl, pb, hist, eg = run(args.steps, measure=True)
     dp.eng.sync()
     torch.cuda.synchronize()
+    gc.enable()
     if dist:
         dist.barrier()
     t = time.perf_counter() - t0
