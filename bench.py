@@ -267,6 +267,7 @@ def main():
     submit = dp.submit_lockstep if native else dp.submit_raw
 
     sub_t = {}      # step index -> host time its ingress was handed to the GPU (submit / prefetch)
+    slow = {"ms": 0.0}   # the timed window's slowest loop iteration: submit / prefetch / finish / egress
     pre = set()     # steps whose payload H2D is already queued (prefetch)
     lat_w = []      # (publish->deliver seconds, deliveries) of the timed steps
 
@@ -308,6 +309,7 @@ def main():
 
         end = step_i + n
         for i in range(n):
+            tp = [time.perf_counter()]   # host time per phase of this iteration (slowest kept)
             b = step_i % args.blocks
             if step_i not in pre:   # (a prefetched step's clock started when its bytes were queued)
                 sub_t[step_i] = time.perf_counter()
@@ -322,6 +324,7 @@ def main():
                 pending.append((submit(sg, base + offs[b], blens[b]), step_i))
             else:
                 pending.append((submit(segs[b], base + offs[b], blens[b]), step_i))
+            tp.append(time.perf_counter())
             step_i += 1
             # the next steps of this run whose bytes are not queued yet (in order: the engine
             # queues each call's payload for the next such step)
@@ -333,14 +336,21 @@ def main():
                     break
                 pre.add(nxt)
                 nxt += 1
+            tp.append(time.perf_counter())
             if len(pending) > 1:
                 t, s = pending.pop(0)
                 account(dp.finish(t, collect=False, wait_egress=False), s)
+                tp.append(time.perf_counter())
                 if done:
                     t2, s2 = done.pop(0)
                     dp.egress_wait(t2)
                     ready(s2)
                 done.append((t, s))
+            tp.append(time.perf_counter())
+            if measure:
+                ph = [round((b2 - a2) * 1e3, 3) for a2, b2 in zip(tp, tp[1:])]
+                if sum(ph) > slow["ms"]:
+                    slow.update(ms=round(sum(ph), 3), step=i, phases_ms=ph)
         for t, s in done:
             dp.egress_wait(t)
             ready(s)
@@ -443,6 +453,7 @@ def main():
                             "bytes of the delivering step in host memory (no TCP; bench/gpu_server_e2e.py "
                             "measures client-to-client over TCP)",
             "diag": errs,
+            "slowest_iteration": slow,
             "host_us_per_step": {k: round(v * 1e6 / args.steps, 1) for k, v in dp.eng.host_times(False).items()},
             "storm": ({"requeued_msgs": flow["requeued"], "flow_paused_steps": flow["paused_steps"]}
                       if storm else None),
