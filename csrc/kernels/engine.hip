@@ -563,7 +563,9 @@ class Engine {
     if (copy_mode_ == 3) init_sdma();
     HIPCHECK(hipStreamCreateWithFlags(&s_comp_, hipStreamNonBlocking));
     HIPCHECK(hipStreamCreateWithFlags(&s_h2d_, hipStreamNonBlocking));
-    HIPCHECK(hipStreamCreateWithFlags(&s_pre_, hipStreamNonBlocking));   // ingress payloads (overlap)
+    // ingress payloads share the H2D stream: a stream of their own stalled the host for ~6 ms
+    // in an early prefetch on some boxes (12+ MB copies; profiles/r4_summary.md)
+    s_pre_ = s_h2d_;
     HIPCHECK(hipStreamCreateWithFlags(&s_d2h_, hipStreamNonBlocking));
     {   // the ingest half gets its own (high-priority) hardware queue: next to the routing
         // half of the previous step, not queued behind it
