@@ -518,7 +518,7 @@ DEV void frame_scan_seg(const DS& d, const u32 s) {
     const u32 len = d.segs[s].len, cl = L - len;
     u8* const dst = d.work + wbase;
     if (cl) block_copy(dst, d.carry + (u64)conn * d.carry_cap, cl, tid, FS_NT);
-    if (len) block_copy(dst + cl, d.ingress + d.segs[s].src, len, tid, FS_NT);
+    if (len) block_copy(dst + cl, (const u8*)d.in->ingress + d.segs[s].src, len, tid, FS_NT);
   }
   __threadfence_block();
   __syncthreads();

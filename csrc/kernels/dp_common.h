@@ -53,7 +53,7 @@ struct StepIn {         // host -> device per step (64 B)
   u64 egress;           // device pointer: this step's egress slot (engine rotates slots)
   u32 nunp;             // connections to unpause before this step's frame scan (DS.unpause_req)
   u32 pslot;            // host persist slot of this step (DS.ps_persist / ps_crec, rotating)
-  u64 pad2;
+  u64 ingress;          // device pointer: this step's ingress slot (engine rotates INGRESS_SLOTS)
 };
 
 

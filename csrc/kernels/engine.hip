@@ -208,7 +208,13 @@ class Engine {
       DS& io = io_[p];
       io.in = (StepIn*)dev(("in" + sfx).c_str(), sizeof(StepIn));
       io.segs = (const SegIn*)dev(("segs" + sfx).c_str(), sizeof(SegIn) * d_.seg_max);
-      io.ingress = (const u8*)dev(("ingress" + sfx).c_str(), d_.ingress_cap + 64);
+      // ingress payloads rotate over INGRESS_SLOTS buffers by step (StepIn.ingress): the
+      // next step's payload goes into a slot whose last reader (three steps back) is known
+      // done, so an early H2D never waits on the GPU
+      if (p == 0)
+        for (int k = 0; k < INGRESS_SLOTS; ++k)
+          ingress_slot_[k] = (u8*)dev(("ingress_s" + std::to_string(k)).c_str(), d_.ingress_cap + 64);
+      io.ingress = ingress_slot_[p];
       io.seg_out = (SegOut*)dev(("seg_out_d" + sfx).c_str(), sizeof(SegOut) * d_.seg_max);
       io.seg_out_h = (SegOut*)hst(("seg_out" + sfx).c_str(), sizeof(SegOut) * d_.seg_max);
       io.ctr_host = (Counters*)hst(("ctr_host" + sfx).c_str(), sizeof(Counters));
@@ -578,6 +584,8 @@ class Engine {
       HIPCHECK(hipEventCreateWithFlags(&ev_pre_[p], hipEventDisableTiming));
       HIPCHECK(hipEventCreateWithFlags(&ev_rest_[p], hipEventDisableTiming));
     }
+    for (int k = 0; k < INGRESS_SLOTS; ++k)
+      HIPCHECK(hipEventCreateWithFlags(&ev_ing_slot_[k], hipEventDisableTiming));
     // overlap (world 1): the step's ingest half runs on its own stream, next to the
     // previous step's routing / delivery half
     overlap_ = d_.world == 1 && get("overlap", 1) != 0;
@@ -772,9 +780,12 @@ class Engine {
     in->worker = worker;
     const int e = (int)(seq_ % EGRESS_SLOTS);
     in->egress = (u64)egress_dev_[e];
+    const int is = (int)(seq_ % INGRESS_SLOTS);
+    in->ingress = (u64)ingress_slot_[is];
     in->pslot = (u32)(seq_ % PSLOTS);
     pslot_of_[p] = (int)in->pslot;
     slot_of_[p] = e;
+    launch_seq_[p] = step;
     if (sb) memcpy(stage_segs_[p], segp, sb);
     // staged Basic.Get requests ride this step; their answers start out RETRY (a queue the
     // device cannot serve now leaves it so)
@@ -810,7 +821,7 @@ class Engine {
     // small per-step copies there; the ingest half waits for both)
     hipStream_t ps = overlap_ ? s_pre_ : s_h2d_;
     if (payload_len && !pre)
-      HIPCHECK(hipMemcpyAsync((void*)io_[p].ingress, (const void*)payload_ptr, payload_len,
+      HIPCHECK(hipMemcpyAsync((void*)ingress_slot_[is], (const void*)payload_ptr, payload_len,
                               sdma_ ? hipMemcpyDeviceToDeviceNoCU : hipMemcpyHostToDevice, ps));
     if (overlap_) HIPCHECK(hipEventRecord(ev_pre_[p], s_pre_));
     HIPCHECK(hipEventRecord(ev_h2d_[p], s_h2d_));
@@ -839,9 +850,13 @@ class Engine {
     }
     if (staged_[p]) throw std::runtime_error("prefetch: this step's payload is already queued");
     if (payload_len > d_.ingress_cap) throw std::runtime_error("ingress payload exceeds ingress_cap");
-    // the buffer's last reader: the ingest half of step tgt - 2 (launched by now)
-    if (ing_issued_[p]) HIPCHECK(hipStreamWaitEvent(s_pre_, ev_ing_[p], 0));
-    HIPCHECK(hipMemcpyAsync((void*)io_[p].ingress, (const void*)payload_ptr, payload_len,
+    // the slot's last reader: the ingest of step tgt - INGRESS_SLOTS, collected by now in
+    // the drivers' order (bench / front end prefetch t+1 once t-2 is finished); if not,
+    // the copy waits for it on the GPU
+    const int is = (int)(tgt % INGRESS_SLOTS);
+    if (tgt >= INGRESS_SLOTS && ing_slot_issued_[is] && hipEventQuery(ev_ing_slot_[is]) != hipSuccess)
+      HIPCHECK(hipStreamWaitEvent(s_pre_, ev_ing_slot_[is], 0));
+    HIPCHECK(hipMemcpyAsync((void*)ingress_slot_[is], (const void*)payload_ptr, payload_len,
                             sdma_ ? hipMemcpyDeviceToDeviceNoCU : hipMemcpyHostToDevice, s_pre_));
     pre_[p] = true;
     pre_seq_[p] = tgt;
@@ -900,6 +915,11 @@ class Engine {
       }
       HIPCHECK(hipEventRecord(ev_ing_[p], s_ing_));
       ing_issued_[p] = true;
+      {
+        const int is = (int)(launch_seq_[p] % INGRESS_SLOTS);
+        HIPCHECK(hipEventRecord(ev_ing_slot_[is], s_ing_));
+        ing_slot_issued_[is] = true;
+      }
       HIPCHECK(hipStreamWaitEvent(s_comp_, ev_ing_[p], 0));
       if (d2h_issued_[e]) HIPCHECK(hipStreamWaitEvent(s_comp_, ev_d2h_[e], 0));
       {
@@ -1983,7 +2003,11 @@ class Engine {
   hipEvent_t ev_ing_[2], ev_rest_[2];
   bool rest_issued_[2] = {false, false}, ing_issued_[2] = {false, false};
   bool eager_d2h_[2] = {false, false};   // the step's egress copy was queued at launch (copy_mode 2)
-  bool pre_[2] = {false, false};        // the next step's payload H2D already queued (prefetch)
+  bool pre_[2] = {false, false};
+  u8* ingress_slot_[INGRESS_SLOTS] = {};
+  hipEvent_t ev_ing_slot_[INGRESS_SLOTS];
+  bool ing_slot_issued_[INGRESS_SLOTS] = {};
+  u64 launch_seq_[2] = {0, 0};          // the step number staged in each parity
   u64 pre_ptr_[2] = {0, 0}, pre_len_[2] = {0, 0}, pre_seq_[2] = {0, 0};
   hipEvent_t ev_pre_[2];
   hipStream_t s_pre_ = nullptr;
