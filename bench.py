@@ -164,7 +164,7 @@ def main():
     ap.add_argument("--queues", type=int, default=16)
     ap.add_argument("--body", type=int, default=1024)
     ap.add_argument("--chunk", type=int, default=49152,
-                    help="bytes per producer per step (TCP read); 49152 holds >= 36 M msgs/s at p50 ~0.9 ms at K=20 "
+                    help="bytes per producer per step (TCP read); 49152: 35-37.5 M msgs/s at p50 0.82-0.94 ms at K=20 "
                          "(65536: ~38 M at p50 1.08 ms, but box-to-box outliers; 32768: ~30 M at 0.73 ms; "
                          "profiles/r4_summary.md)")
     ap.add_argument("--blocks", type=int, default=8)
