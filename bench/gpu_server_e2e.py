@@ -54,7 +54,7 @@ def plane_for(spec):
     return GpuDataPlane(c_max=512, chpc=8, q_max=256, cons_max=1024, seg_max=512, cmd_max=1 << 17,
                         deliv_max=1 << 17, msg_max=1 << 21, ucap=8192, deliver_cap=8192,
                         ingress_cap=64 << 20, egress_cap=160 << 20, log_bytes=8 << 30, ring_pool=1 << 25,
-                        spill_bytes=8 << 30,   # (the broker's default tiering: old bodies leave HBM)
+                        spill_bytes=SIZING.get("spill_bytes", 8 << 30),   # (default tiering: old bodies leave HBM)
                         tb_max=256, default_queue_capacity=1 << 20, persist=int(persist),
                         persist_max=1 << 16, persist_bytes=512 << 20, carry_cap=SIZING["carry_cap"])
 
@@ -350,6 +350,7 @@ def main():
     ap.add_argument("--sharded", type=int, default=0,
                     help="N > 1: the pipelined sharded server with N ranks on this GPU (producers on rank 1, "
                          "consumers on rank 0 and then on rank 1 through device links)")
+    ap.add_argument("--spill-bytes", type=int, default=8 << 30, help="host spill ring of the bench plane (0 = off)")
     ap.add_argument("--confirm-read", type=int, default=0,
                     help="bytes per confirm-mode connection per step (0 = the broker default, 128 KiB)")
     ap.add_argument("--persist-group-ms", type=float, default=2.0,
@@ -360,6 +361,7 @@ def main():
     args = ap.parse_args()
     BROKER_CFG["persist_group_ms"] = args.persist_group_ms
     BROKER_CFG["confirm_read"] = args.confirm_read
+    SIZING["spill_bytes"] = args.spill_bytes
     SIZING.update(per_conn_read=args.per_conn_read, carry_cap=max(args.carry_cap, 2 * args.per_conn_read))
     if args.wblock_high:
         FE_CFG.update(wblock_high=args.wblock_high, wblock_low=args.wblock_high // 4)
