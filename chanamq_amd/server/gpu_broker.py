@@ -13,7 +13,9 @@ scala/chana/mq/amqp/server/engine/FrameStage.scala:319-500).
 The plane can be a ``GpuDataPlane`` (HIP) or a ``GoldenDataPlane`` (CPU executable
 spec, used by the CPU tests of this server).
 
-Basic.Get runs on the device between steps (k_basic_get).  Transactions: on a Tx
+Basic.Get: with the pipelined front end it is served inside the next step (k_dequeue,
+staged by the front end; the broker handles Get and its answer without pausing the
+stepper); the other front ends run it between steps (k_basic_get).  Transactions: on a Tx
 channel the device hands publishes / acks to the host instead of applying them
 (CK_TXBUF); Tx.Commit applies the acks between steps and injects the publishes through a
 pseudo-connection in the next step, Tx.Rollback drops them.  Not on the GPU path yet
