@@ -153,6 +153,12 @@ Frontend::Frontend(const FrontendCfg& cfg, const CmqEngineApi* api) : cfg_(cfg),
 
 Frontend::~Frontend() {
   stop();
+  {   // (a front end that was attached to a store but never started has its copier only)
+    std::lock_guard<std::mutex> g(pc_mu_);
+    pc_stop_ = true;
+  }
+  pc_cv_.notify_all();
+  if (pc_th_.joinable()) pc_th_.join();
   for (auto& c : conns_)
     if (c->fd >= 0) ::close(c->fd);
   for (auto& io : io_) {
