@@ -15,7 +15,7 @@ EXT_PATH = os.path.join(_HERE, "_core" + _EXT)
 SOURCES = ["codec.cpp", "store.cpp", "broker.cpp", "loadgen.cpp", "gateway.cpp", "frontend.cpp", "persist.cpp",
            "bodylog.cpp", "tls_proxy.cpp",            "bindings.cpp"]
 HEADERS = ["codec.hpp", "store.hpp", "broker.hpp", "loadgen.hpp", "gateway.hpp", "frontend.hpp", "persist.hpp", "bodylog.hpp", "flatmap.hpp", "tls_proxy.hpp",
-           "../kernels/step_abi.h"]
+           "../kernels/step_abi.h", "../kernels/xchg_host.h"]
 
 
 def _src_hash():

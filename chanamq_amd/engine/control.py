@@ -320,7 +320,9 @@ class ControlState:
         for x in self.exchanges.values():   # QueueDeleted broadcast (ExchangeEntity.scala:191-193)
             x.bindings = [(s, k) for s, k in x.bindings if s != q.slot]
         del self.queue_by_slot[q.slot]
-        self._free_q.append(q.slot)
+        # a freed slot is reused last (FIFO), not next: a request still naming the old slot
+        # (a Basic.Get staged for a step) must not land on a queue declared right after
+        self._free_q.insert(0, q.slot)
         self._ring_free.setdefault(q.capacity, []).append(q.ring_off)
         self.queue_deleted(q)
         self.routing_changed()

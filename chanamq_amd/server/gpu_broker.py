@@ -67,7 +67,7 @@ class _Conn:
 
 FE_OPEN, FE_CLOSED, FE_HOST, FE_CTRL, FE_TXBUF, FE_EVENT, FE_STATUS, FE_PERSIST, FE_ERROR, FE_GROW, FE_SYNC, \
     FE_XFAIL, FE_INJECTED, FE_GET = range(1, 15)
-GS_EMPTY, GS_OK, GS_RETRY, GS_NO_SPACE, GS_WINDOW_FULL = range(5)   # step_abi.h GetOut.status
+GS_EMPTY, GS_OK, GS_RETRY, GS_NO_SPACE, GS_WINDOW_FULL, GS_GONE = range(6)   # step_abi.h GetOut.status
 
 
 class _PlaneLock:
@@ -214,7 +214,7 @@ class GpuBroker:
         self._links = {}        # (conn, channel, consumer tag) -> link id (remote consumers)
         self._get_links = {}    # (vhost, queue) -> get link id (Basic.Get of remote queues)
         self._get_wait = {}     # pull id -> (conn, channel, no_ack, link id)
-        self._dev_gets = {}     # Basic.Gets queued on the device: id -> (conn, channel, queue slot, no_ack)
+        self._dev_gets = {}     # Basic.Gets queued on the device: id -> (conn, channel, queue slot, no_ack, vhost, queue)
         self._get_holders = {}  # get link id -> {(conn, channel)} holding unacked Get messages
         self._get_used = {}     # get link id -> monotonic time of its last Get
         self._pull_seq = 0
@@ -392,7 +392,7 @@ class GpuBroker:
         rest = []
         for e in dev:
             kind, conn = e[0], e[1]
-            if kind == FE_GET and (e[2] & 0xFFFFFFFF) in (GS_OK, GS_EMPTY, GS_RETRY):
+            if kind == FE_GET and (e[2] & 0xFFFFFFFF) in (GS_OK, GS_EMPTY, GS_RETRY, GS_GONE):
                 self._get_answer(conn, e[2], e[3])
                 continue
             if kind == FE_CTRL and self._fast_get(conn, e[4]):
@@ -416,7 +416,7 @@ class GpuBroker:
         if q is None or q.exclusive_owner not in (-1, c.id) or q.owner != p.rank:
             return False   # errors and remote queues: the locked path
         gid = self._next_get = getattr(self, "_next_get", 0) + 1
-        self._dev_gets[gid] = (c.id, ch, q.slot, bool(m.no_ack))
+        self._dev_gets[gid] = (c.id, ch, q.slot, bool(m.no_ack), pc.vhost, q.name)
         self.fe.queue_get(c.id, p.chslot(c.id, ch), q.slot, int(bool(m.no_ack)), gid)
         self.stats["device_gets"] = self.stats.get("device_gets", 0) + 1
         return True
@@ -551,6 +551,14 @@ class GpuBroker:
         st = self.fe.stats()
         self.stats.update(steps=st["steps"], published=st["published"], delivered=st["delivered"])
         self._fe_stats = st
+        pw = getattr(self, "_pw", None)
+        if pw is not None and "store_failed" not in self.stats:
+            ps = pw.stats()
+            if ps["failed"]:   # confirms stay held; fe.healthy() is False (a sharded node fails over)
+                self.stats["store_failed"] = ps["error"]
+                import logging
+                logging.getLogger("chanamq.gpu").error("persistent store failed, confirms are held from now on: %s",
+                                                       ps["error"])
 
     def _host_step(self, inputs):
         """A synchronous step run by the control plane while the front end is paused
@@ -1423,7 +1431,7 @@ class GpuBroker:
                 # served inside the next step (k_dequeue, ahead of the queue's consumers): no
                 # pipeline drain; the connection stays paused until FE_GET answers it
                 gid = self._next_get = getattr(self, "_next_get", 0) + 1
-                self._dev_gets[gid] = (c.id, ch, q.slot, bool(m.no_ack))
+                self._dev_gets[gid] = (c.id, ch, q.slot, bool(m.no_ack), vh, q.name)
                 self.fe.queue_get(c.id, p.chslot(c.id, ch), q.slot, int(bool(m.no_ack)), gid)
                 self.stats["device_gets"] = self.stats.get("device_gets", 0) + 1
                 return "deferred"
@@ -1550,12 +1558,17 @@ class GpuBroker:
         if req is None or c is None or c.state != "open":
             return
         st, cnt = a & 0xFFFFFFFF, a >> 32
-        _, ch, slot, no_ack = req
+        _, ch, slot, no_ack, vh, qname = req
+        q = self.plane.queues.get((vh, qname))
+        if st == GS_RETRY and (q is None or q.slot != slot or q.owner != self.plane.rank):
+            st = GS_GONE   # deleted (or moved) while the Get waited: never resubmitted
         if st == GS_RETRY:
             self._dev_gets[gid] = req
             self.fe.queue_get(conn, self.plane.chslot(conn, ch), slot, int(no_ack), gid)
             return
-        if st == GS_EMPTY:
+        if st == GS_GONE:   # the reference's Pull on a missing queue entity: 404
+            self._chan_close(c, ch, C.NOT_FOUND, f"no queue '{qname}' in vhost '{vh}'", 60, 70)
+        elif st == GS_EMPTY:
             self._send(c, ch, Method("basic.get_empty"))
         elif st != GS_OK:
             self._chan_close(c, ch, C.RESOURCE_ERROR, "basic.get: " + (

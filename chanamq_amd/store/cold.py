@@ -24,14 +24,16 @@ import numpy as np
 
 SEG_SHIFT = 30
 SEG = 1 << SEG_SHIFT
+SLOTS = 16384      # dp_common.h COLD_SEGS: the device counts segment s's live bytes at [s % SLOTS]
 COLD_REC = np.dtype([("msg", "<u4"), ("q", "<u4"), ("qpos", "<u8"), ("pos", "<u8"), ("cold", "<u8"),
                      ("bytes", "<u4"), ("pad", "<u4")])
 assert COLD_REC.itemsize == 40
 
 
 class ColdStore:
-    def __init__(self, path=None):
+    def __init__(self, path=None, slots=SLOTS):
         self.own = path is None
+        self.slots = slots
         self.path = path or tempfile.mkdtemp(prefix="cmq-cold-")
         if os.path.isdir(self.path):
             for f in os.listdir(self.path):
@@ -57,7 +59,7 @@ class ColdStore:
             if (self.head & (SEG - 1)) + n > SEG:        # never across a segment
                 self._flush(batch, bstart)
                 batch, bstart = [], None
-                self.head = ((self.head >> SEG_SHIFT) + 1) << SEG_SHIFT
+                self.head = self._next_seg(self.head >> SEG_SHIFT) << SEG_SHIFT
             if bstart is None:
                 bstart = self.head
             offs.append(self.head)
@@ -68,6 +70,18 @@ class ColdStore:
                 batch, bstart = [], None
         self._flush(batch, bstart)
         return offs
+
+    def _next_seg(self, cur):
+        """The segment after ``cur`` whose live-byte slot (seg % slots) no open segment
+        uses: offsets grow without bound, slots wrap, and two live segments must never
+        share one (the device's count would mix them and gc could unlink a live one)."""
+        used = {seg % self.slots for seg in self.fds}
+        seg = cur + 1
+        for _ in range(self.slots):
+            if seg % self.slots not in used:
+                return seg
+            seg += 1
+        raise OSError("cold store: every segment slot holds live bodies")
 
     def _flush(self, batch, start):
         if not batch:
@@ -91,8 +105,8 @@ class ColdStore:
         segment), except the one being appended to."""
         cur = self.head >> SEG_SHIFT
         n = 0
-        for seg in list(self.fds):
-            if seg != cur and seg < len(live) and live[seg % len(live)] <= 0:
+        for seg in list(self.fds):   # (slots never alias: _next_seg)
+            if seg != cur and live[seg % len(live)] <= 0:
                 os.close(self.fds.pop(seg))
                 os.unlink(os.path.join(self.path, f"cold-{seg}.seg"))
                 n += 1

@@ -313,6 +313,7 @@ PYBIND11_MODULE(_core, m) {
              py::dict o;
              o["rows"] = w.rows(); o["commits"] = w.commits(); o["body_bytes"] = w.bytes(); o["busy_s"] = w.busy_s();
              o["apply_s"] = w.apply_s(); o["flush_s"] = w.flush_s(); o["sync_s"] = w.sync_s();
+             o["failed"] = w.failed(); o["error"] = w.error();
              return o;
            });
   py::class_<TlsProxy>(m, "TlsProxy")

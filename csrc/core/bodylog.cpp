@@ -70,9 +70,22 @@ std::string BodyLog::path(uint32_t seg) const {
   return dir_ + b;
 }
 
+// the directory entry of a new segment file is durable before a row names it: fsync of
+// the bodies directory after its mkdir and after each segment creation (rare: one per
+// seg_bytes of a stripe), ahead of the group commit that references the segment
+void BodyLog::sync_dir_locked() {
+  if (!fsync_) return;
+  if (dfd_ < 0) dfd_ = ::open(dir_.c_str(), O_RDONLY | O_DIRECTORY);
+  if (dfd_ >= 0) ::fsync(dfd_);
+}
+
 void BodyLog::start_locked() {
   if (started_) return;
-  ::mkdir(dir_.c_str(), 0755);
+  if (::mkdir(dir_.c_str(), 0755) == 0 && fsync_) {   // a new directory: its parent's entry too
+    const size_t sl = dir_.find_last_of('/');
+    const int pfd = ::open(sl == std::string::npos ? "." : dir_.substr(0, sl ? sl : 1).c_str(), O_RDONLY | O_DIRECTORY);
+    if (pfd >= 0) { ::fsync(pfd); ::close(pfd); }
+  }
   st_ = std::vector<Stripe>(nstripes_);
   for (int k = 0; k < nstripes_; ++k) st_[k].th = std::thread([this, k] { run(k); });
   started_ = true;
@@ -82,6 +95,7 @@ void BodyLog::roll_locked(Stripe& s) {
   const uint32_t seg = next_seg_++;
   const int fd = ::open(path(seg).c_str(), O_WRONLY | O_CREAT | O_TRUNC, 0644);
   if (fd < 0) throw std::runtime_error("body log: cannot create " + path(seg));
+  sync_dir_locked();
   std::lock_guard<std::mutex> a(amu_);
   if (s.fd >= 0) {
     s.retired.push_back(s.fd);
@@ -323,6 +337,7 @@ void BodyLog::close() {
       for (int fd : s.retired) ::close(fd);
     }
   }
+  if (dfd_ >= 0) { ::close(dfd_); dfd_ = -1; }
   std::lock_guard<std::mutex> g(mu_);
   std::lock_guard<std::mutex> a(amu_);
   st_.clear();

@@ -65,11 +65,13 @@ class BodyLog {
   };
   void start_locked();
   void roll_locked(Stripe& s);
+  void sync_dir_locked();
   void run(int k);
   std::string path(uint32_t seg) const;
 
   std::string dir_;
   bool fsync_;
+  int dfd_ = -1;                     // the bodies directory (fsync after segment creation)
   int nstripes_ = 4;
   uint64_t seg_bytes_ = 1ull << 30;
   std::mutex mu_;                        // stripes, jobs

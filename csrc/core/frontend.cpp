@@ -1219,6 +1219,7 @@ void Frontend::sync_done() {
 
 bool Frontend::healthy(double stuck_s) const {
   if (failed_) return false;
+  if (persist_ && persist_->failed()) return false;   // the store cannot commit: fail over
   const i64 t = gpu_wait_since_.load();
   return !t || (now_ns() - t) < (i64)(stuck_s * 1e9);
 }

@@ -65,7 +65,7 @@ void PersistWorker::submit(u64 step, std::string persist, std::string consumed) 
 void PersistWorker::drain() {
   std::unique_lock<std::mutex> g(mu_);
   const u64 want = submitted_;
-  done_cv_.wait(g, [&] { return committed_ >= want || !running_; });
+  done_cv_.wait(g, [&] { return committed_ >= want || !running_ || failed_.load(); });
 }
 
 void PersistWorker::loop() {
@@ -80,20 +80,37 @@ void PersistWorker::loop() {
     }
     std::deque<Batch> work;
     work.swap(q_);
-    g.unlock();
-    auto t0 = std::chrono::steady_clock::now(), t1 = t0;
-    u64 top = 0;
-    {
-      std::lock_guard<std::mutex> qg(qid_mu_);
-      for (auto& b : work) {
-        apply(b);
-        if (b.step > top) top = b.step;
-      }
-      t1 = std::chrono::steady_clock::now();
-      flush_born();   // rows that outlived the group (their batches are still alive here)
+    if (failed_) {   // a group already failed: later ones are never reported committed
+      committed_ += work.size();
+      done_cv_.notify_all();
+      continue;
     }
-    auto t2 = std::chrono::steady_clock::now();
-    st_->sync();   // group commit: one fsync for every batch that was waiting (+ the body log's)
+    g.unlock();
+    auto t0 = std::chrono::steady_clock::now(), t1 = t0, t2 = t0;
+    u64 top = 0;
+    try {
+      {
+        std::lock_guard<std::mutex> qg(qid_mu_);
+        for (auto& b : work) {
+          apply(b);
+          if (b.step > top) top = b.step;
+        }
+        t1 = std::chrono::steady_clock::now();
+        flush_born();   // rows that outlived the group (their batches are still alive here)
+      }
+      t2 = std::chrono::steady_clock::now();
+      st_->sync();   // group commit: one fsync for every batch that was waiting (+ the body log's)
+    } catch (std::exception& e) {
+      // ENOSPC / EIO (sticky in the body log) or a segment that could not be created: the
+      // group is not durable.  Its steps' confirms stay held (no commit callback), the
+      // worker reports failed() and the broker fails over instead of std::terminate
+      g.lock();
+      if (!failed_) err_ = e.what();
+      failed_ = true;
+      committed_ += work.size();
+      done_cv_.notify_all();
+      continue;
+    }
     ++commits_;
     auto t3 = std::chrono::steady_clock::now();
     apply_s_ += std::chrono::duration<double>(t1 - t0).count();

@@ -61,6 +61,14 @@ class PersistWorker {
   double apply_s() const { return apply_s_; }
   double flush_s() const { return flush_s_; }
   double sync_s() const { return sync_s_; }
+  // a group commit failed (ENOSPC / EIO on the WAL or the body log, a segment that could
+  // not be created): nothing of that group or later is reported committed, so their
+  // publisher confirms are never released; the broker reads this through stats / healthy
+  bool failed() const { return failed_.load(); }
+  std::string error() const {
+    std::lock_guard<std::mutex> g(mu_);
+    return err_;
+  }
 
  private:
   struct Batch { u64 step; std::string persist, consumed; std::chrono::steady_clock::time_point t; };
@@ -82,7 +90,7 @@ class PersistWorker {
 
   Store* st_;
   std::function<void(u64)> commit_cb_;
-  std::mutex mu_;
+  mutable std::mutex mu_;
   std::condition_variable cv_, done_cv_;
   std::deque<Batch> q_;
   u64 submitted_ = 0, committed_ = 0;
@@ -107,6 +115,8 @@ class PersistWorker {
   std::atomic<u64> rows_{0}, commits_{0}, bytes_{0};
   double busy_s_ = 0, apply_s_ = 0, flush_s_ = 0, sync_s_ = 0;
   std::atomic<i64> delay_us_{0};
+  std::atomic<bool> failed_{false};
+  std::string err_;                                   // (mu_) what failed first
 };
 
 }  // namespace cmq

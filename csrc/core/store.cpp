@@ -222,7 +222,13 @@ void Store::close() {
   compact_stop_ = false;
   std::lock_guard<std::recursive_mutex> g(mu_);
   if (fd_ >= 0) {
-    sync();
+    // the fds close even when the last sync fails (a sticky body-log error): close() runs
+    // from the destructor too, where an exception would terminate the process
+    try {
+      sync();
+    } catch (std::exception& e) {
+      close_error_ = e.what();
+    }
     ::close(fd_);
     fd_ = -1;
   }

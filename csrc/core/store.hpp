@@ -191,6 +191,7 @@ class Store {
   uint64_t auto_backoff_ = 0;         // after a failed background run: retry once the WAL passes this
   std::thread compact_th_;
   std::atomic<bool> compacting_{false}, compact_stop_{false};
+  std::string close_error_;          // what the final sync of close() reported (it never throws)
   CompactStats cstats_;
 
   std::recursive_mutex mu_;

@@ -2960,7 +2960,14 @@ __global__ __launch_bounds__(256) void k_dequeue(DS d) {
   }
   if (q >= d.q_max) return;
   if (!d.q_active[q]) {
-    if (tid == 0) d.q_nruns[q] = 0;
+    if (tid == 0) {
+      d.q_nruns[q] = 0;
+      // a Basic.Get staged for a queue deleted since: answered GONE (never left RETRY, which
+      // the host would resubmit forever -- or serve from whatever queue reuses the slot)
+      const u32 ng = d.in->nget < GET_STEP_MAX ? d.in->nget : GET_STEP_MAX;
+      for (u32 i = 0; i < ng; ++i)
+        if (d.get_req[i].q == q) d.get_out_h[i] = GetOut{GS_GONE, 0u};
+    }
     return;
   }
   const bool nodisp = (d.in->flags & SF_NODISPATCH) != 0;

@@ -93,7 +93,9 @@ struct ConnOut { u32 off; u32 len; };
 // Reference: FrameStage.scala:1199-1229, QueueEntity.scala:318-393
 #define GET_STEP_MAX 256
 struct GetReq { u32 conn; u32 chslot; u32 q; u32 noack; };
-enum : u32 { GS_EMPTY = 0, GS_OK = 1, GS_RETRY = 2, GS_NO_SPACE = 3, GS_WINDOW_FULL = 4 };
+// GONE: the request's queue slot is no longer active (deleted since the request was
+// staged): the host answers it from its own view of the queue, never retries it
+enum : u32 { GS_EMPTY = 0, GS_OK = 1, GS_RETRY = 2, GS_NO_SPACE = 3, GS_WINDOW_FULL = 4, GS_GONE = 5 };
 struct GetOut { u32 status; u32 msg_count; };
 
 // C entry points of one Engine (engine.hip: Engine::c_api).  All return 0 / a parity on

@@ -36,11 +36,18 @@ constexpr int XH_WORDS = 16;       // u32 header words per (source, destination)
 constexpr int XMAX = 16;           // ranks (dp_state.h WORLD_MAX)
 
 struct ShmCtl {                    // first 4 KB of the segment
-  std::atomic<uint32_t> arrive;
-  std::atomic<uint32_t> gen;
+  // the barrier: generation << 32 | arrivals in it, one word, so an arrival, a withdrawal,
+  // the completion (the last arrival moves it to (gen + 1, 0) in the same CAS) and the
+  // abort of a generation nobody can complete any more are each one atomic step
+  std::atomic<uint64_t> state;
   uint32_t n;                      // ranks in this group
   uint32_t magic;
+  // how generation g ended, at [g % OUTCOMES]: g << 1 | aborted.  Written by the member
+  // that completed g (after its CAS) or aborted it (before its CAS; an aborted generation
+  // can never complete); a member that finds the state past its generation reads it here
+  std::atomic<uint64_t> outcome[64];
 };
+constexpr uint64_t OUTCOMES = 64;
 
 class ShmXchg {
  public:
@@ -65,7 +72,7 @@ class ShmXchg {
     base_ = (uint8_t*)::mmap(nullptr, total_, PROT_READ | PROT_WRITE, MAP_SHARED, fd_, 0);
     if (base_ == MAP_FAILED) throw std::runtime_error("shm xchg: mmap failed");
     ctl_ = (ShmCtl*)base_;
-    gen_seen_ = ctl_->gen.load();
+    gen_ = 0;   // a group's segment is new (fresh name): every member starts at generation 0
   }
   ~ShmXchg() {
     if (base_ && base_ != MAP_FAILED) ::munmap(base_, total_);
@@ -93,43 +100,76 @@ class ShmXchg {
     return (uint64_t*)(base_ + 4096 + per_ * (size_t)i + 2 * (size_t)XMAX * XMAX * XH_WORDS * 4);
   }
 
-  // all members arrive; 0, or -2 after timeout_ms (a peer is gone)
+  // all members arrive; 0, or -2 after timeout_ms (a peer is gone).  Every member reports
+  // the same outcome for a generation: it completes only by the n-th arrival, and a member
+  // that timed out first takes its arrival back (withdraw), so the generation can no longer
+  // complete -- the others time out too.  Arrivals carry the generation they are for
+  // (gen_), so a member that failed generation g and comes back for g + 1 never counts
+  // towards g: it aborts g instead, and a peer still waiting in g fails it.
   int barrier() {
-    const uint32_t n = (uint32_t)members_.size();
-    const uint32_t g = ctl_->gen.load(std::memory_order_acquire);
-    if (ctl_->arrive.fetch_add(1, std::memory_order_acq_rel) + 1 == n) {
-      ctl_->arrive.store(0, std::memory_order_relaxed);
-      ctl_->gen.store(g + 1, std::memory_order_release);
-      return 0;
+    const uint64_t n = members_.size();
+    const uint64_t b = gen_;
+    uint64_t s = ctl_->state.load(std::memory_order_acquire);
+    while (true) {
+      const uint64_t g = s >> 32, c = s & 0xffffffffull;
+      if (g > b) return settle(b);   // the group left b without this member (aborted)
+      uint64_t nxt;
+      if (g < b) {
+        // generation g is still open but this member already failed it (it only moves
+        // past g by failing it): nobody can complete g any more -- abort it, arrive in b
+        for (uint64_t k = g; k < b; ++k) ctl_->outcome[k % OUTCOMES].store(k << 1 | 1, std::memory_order_release);
+        nxt = n == 1 ? ((b + 1) << 32) : ((b << 32) | 1);
+      } else {
+        nxt = c + 1 == n ? ((b + 1) << 32) : s + 1;
+      }
+      if (ctl_->state.compare_exchange_weak(s, nxt, std::memory_order_acq_rel, std::memory_order_acquire)) {
+        if ((nxt >> 32) == b + 1) {   // this arrival completed b
+          ctl_->outcome[b % OUTCOMES].store(b << 1, std::memory_order_release);
+          gen_ = b + 1;
+          return 0;
+        }
+        break;
+      }
     }
     const auto t0 = std::chrono::steady_clock::now();
     for (uint32_t spin = 0;; ++spin) {
-      if (ctl_->gen.load(std::memory_order_acquire) != g) return 0;
+      if ((ctl_->state.load(std::memory_order_acquire) >> 32) != b) return settle(b);
       if (spin < 2000) { sched_yield(); continue; }
       timespec ts{0, 20000};
       nanosleep(&ts, nullptr);
       if ((spin & 63) == 0 &&
           std::chrono::duration_cast<std::chrono::milliseconds>(std::chrono::steady_clock::now() - t0).count() >
               timeout_ms_)
-        return withdraw(g);
+        return withdraw(b);
     }
   }
 
-  // Timed out: take this rank's arrival back, so the generation cannot complete without
-  // it and every member reports the same outcome (all pass, or all time out and drop the
-  // step's exchange together).  If the last member arrived meanwhile, the generation did
-  // complete and this rank passes too.
-  int withdraw(uint32_t g) {
-    uint32_t a = ctl_->arrive.load(std::memory_order_acquire);
-    while (true) {
-      if (ctl_->gen.load(std::memory_order_acquire) != g) return 0;
-      if (a == 0) {   // the completing member reset the count: its gen store follows
-        sched_yield();
-        a = ctl_->arrive.load(std::memory_order_acquire);
-        continue;
+  // Timed out in generation b: take this rank's arrival back, so b cannot complete without
+  // it.  If b completed (or was aborted) meanwhile, that outcome stands for this rank too.
+  int withdraw(uint64_t b) {
+    uint64_t s = ctl_->state.load(std::memory_order_acquire);
+    while ((s >> 32) == b) {
+      if (ctl_->state.compare_exchange_weak(s, s - 1, std::memory_order_acq_rel, std::memory_order_acquire)) {
+        gen_ = b + 1;
+        return -2;
       }
-      if (ctl_->arrive.compare_exchange_weak(a, a - 1, std::memory_order_acq_rel, std::memory_order_acquire))
-        return ctl_->gen.load(std::memory_order_acquire) != g ? 0 : -2;
+    }
+    return settle(b);
+  }
+
+  // the state left generation b: completed (0) or aborted (-2), as recorded in the outcome
+  // ring (its writer may still be between its CAS and that store: wait for it, bounded)
+  int settle(uint64_t b) {
+    gen_ = b + 1;
+    const auto t0 = std::chrono::steady_clock::now();
+    for (uint32_t spin = 0;; ++spin) {
+      const uint64_t o = ctl_->outcome[b % OUTCOMES].load(std::memory_order_acquire);
+      if ((o >> 1) == b) return (o & 1) ? -2 : 0;
+      sched_yield();
+      if ((spin & 63) == 0 &&
+          std::chrono::duration_cast<std::chrono::milliseconds>(std::chrono::steady_clock::now() - t0).count() >
+              timeout_ms_)
+        return -2;
     }
   }
 
@@ -157,7 +197,7 @@ class ShmXchg {
   int fd_ = -1;
   uint8_t* base_ = nullptr;
   ShmCtl* ctl_ = nullptr;
-  uint32_t gen_seen_ = 0;
+  uint64_t gen_ = 0;                 // the barrier generation this member's next call is for
   uint64_t seq_ = 0;
   bool unlinked_ = false;
 };

@@ -144,3 +144,28 @@ def test_memory_only_store_keeps_bodies_in_rows():
     w.drain()
     w.stop()
     assert st.select_message(9)[3] == b"hello"
+
+
+def test_store_failure_is_reported_not_fatal(tmp_path):
+    """a group commit whose body-log segment cannot be created (or whose pwritev /
+    fdatasync failed: the error is sticky) throws on the PersistWorker thread.  The worker
+    catches it: the process lives, drain() returns, nothing of the group (or later) is
+    reported committed -- so no publisher confirm is released -- and stats() says why.
+    Store.close() still closes its files."""
+    core = load()
+    st = _open(core, tmp_path / "s")
+    st.insert_queue_meta("v-_.dq0", -1, set(), True, 0)
+    # the bodies directory is a regular file: the first segment cannot be created
+    (tmp_path / "s" / "bodies").write_bytes(b"not a directory")
+    w = core.PersistWorker(st)
+    w.set_queue(0, "v-_.dq0")
+    w.start()
+    w.submit(1, b"".join(_rec(100 + i, 0, i, _body(i)) for i in range(8)), b"")
+    w.drain()
+    w.submit(2, _rec(200, 0, 8, _body(1)), b"")   # after the failure: dropped, drain returns
+    w.drain()
+    s = w.stats()
+    assert s["failed"] and "cannot create" in s["error"], s
+    assert s["commits"] == 0
+    w.stop()
+    st.close()   # must not throw

@@ -186,6 +186,50 @@ def test_basic_get_ack_nack_and_empty(broker):
     c.close()
 
 
+def test_basic_get_races_queue_delete(broker):
+    """Basic.Gets racing a Queue.Delete on another connection: every Get is
+    answered (GetOk / GetEmpty, or the channel closed 404 once the queue is gone) -- never
+    resubmitted forever against the deleted slot -- and a queue declared right after the
+    delete does not take over the deleted queue's slot (a Get staged for it cannot land
+    there)."""
+    import threading
+    from chanamq_amd.client import ChannelClosed as CC
+    a, b = conn(broker), conn(broker)
+    ca, cb = a.channel(), b.channel()
+    for r in range(3):
+        name = f"race{r}"
+        cb.queue_declare(name)
+        for i in range(20):
+            cb.basic_publish("", name, b"x%d" % i)
+        b.process(0.1)
+        answers, errs = [], []
+
+        def getter():
+            ch = ca
+            try:
+                for _ in range(60):
+                    answers.append(ch.basic_get(name, no_ack=True))
+            except CC as e:
+                errs.append(e.code)
+        old_slot = next(q.slot for k, q in broker.plane.queues.items() if k[1] == name)
+        t = threading.Thread(target=getter)
+        t.start()
+        b.process(0.02)
+        cb.queue_delete(name)
+        cb.queue_declare(name + "-next")   # may not reuse the deleted slot
+        assert next(q.slot for k, q in broker.plane.queues.items() if k[1] == name + "-next") != old_slot
+        t.join(30)
+        assert not t.is_alive(), "a Basic.Get was never answered"
+        assert errs in ([], [404])
+        if errs:
+            ca = a.channel()
+    with pytest.raises(ChannelClosed) as e:
+        ca.basic_get("race0")
+    assert e.value.code == 404
+    a.close()
+    b.close()
+
+
 def test_transactions_commit_and_rollback(broker):
     """Tx on the data path: publishes and acks of a Tx channel take effect at Tx.Commit
     only (in order), Tx.Rollback drops them; a mandatory unroutable publish is returned
