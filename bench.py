@@ -172,6 +172,9 @@ def main():
                     help="after the timed steps (and the result line), keep stepping untimed for this long so "
                          "an external GPU-utilisation sampler sees the workload (0 = off)")
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--egress-gate", type=int, default=1, choices=[0, 1],
+                    help="1: each step's egress D2H is queued on the SDMA engine at launch and started by the "
+                         "step's last kernel (no host round trip); 0: issued by the host once it saw the step finish")
     ap.add_argument("--copy-engine", choices=["kernel", "nocu", "blit", "sdma"], default="sdma",
                     help="egress D2H: an SDMA engine other than the ingress H2D's (default: H2D and D2H "
                          "overlap at ~47 GB/s each, bench/pcie_probe.hip), the runtime blit kernel (holds CUs "
@@ -244,7 +247,7 @@ def main():
                log_bytes=16 << 30, ring_pool=Q * qcap + qtot + 1024, tb_max=max(64, qtot) if not fan else 64,
                fan_max=max(1 << 20, qtot * 2), carry_cap=256 << 10, graph=0 if args.no_graph else 1,
                copy_engine={"blit": 0, "nocu": 1, "kernel": 2, "sdma": 3}[args.copy_engine], copy_wgs=args.copy_wgs, sdma_engine=args.sdma_engine,
-               sdma_split=args.sdma_split)
+               sdma_split=args.sdma_split, egress_gate=args.egress_gate)
     native = shards > 1 and args.xchg == "native"
     if native:
         dp = setup_native_exchange(args, cfg, GpuDataPlane, dist, backend, local, rank, world)
@@ -337,14 +340,18 @@ def main():
                 pre.add(nxt)
                 nxt += 1
             tp.append(time.perf_counter())
+            # the egress of step i-2 first (its D2H started when that step's last kernel
+            # opened the gate, about when step i-1's routing half began): it is in host
+            # memory by the time its wait returns; then step i-1's results (the host's
+            # only per-step wait on the kernels), which frees its parity for step i+1
+            if done:
+                t2, s2 = done.pop(0)
+                dp.egress_wait(t2)
+                ready(s2)
+            tp.append(time.perf_counter())
             if len(pending) > 1:
                 t, s = pending.pop(0)
                 account(dp.finish(t, collect=False, wait_egress=False), s)
-                tp.append(time.perf_counter())
-                if done:
-                    t2, s2 = done.pop(0)
-                    dp.egress_wait(t2)
-                    ready(s2)
                 done.append((t, s))
             tp.append(time.perf_counter())
             if measure:
@@ -455,6 +462,7 @@ def main():
             "diag": errs,
             "slowest_iteration": slow,
             "host_us_per_step": {k: round(v * 1e6 / args.steps, 1) for k, v in dp.eng.host_times(False).items()},
+            "egress": dp.eng.egress_stats(),
             "storm": ({"requeued_msgs": flow["requeued"], "flow_paused_steps": flow["paused_steps"]}
                       if storm else None),
             "cross_gpu_bytes_per_s": (dp.exchanger.bytes_sent * world / t) if shards > 1 and not native else None,

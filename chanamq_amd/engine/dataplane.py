@@ -801,7 +801,7 @@ class GpuDataPlane(ControlState):
             self.step_no += 1
             self.eng.drop_exchange(p)
             self.eng.launch_b(p)
-            return (p, len(segs), t0)
+            return (p, len(segs), t0, self.eng.egress_slot(p))
         if self.world > 1 and self.lag and self.exchanger is not None:
             # one process per rank, pipelined exchange: queue H2D(t), then run step t-1's
             # all-to-all while those bytes cross PCIe, then launch step t (whose phase B
@@ -813,7 +813,7 @@ class GpuDataPlane(ControlState):
                 self._exchange_parity(self._xprev)
             self.eng.launch(p)
             self._pending = self._xprev = p
-            return (p, len(segs), t0)
+            return (p, len(segs), t0, self.eng.egress_slot(p))
         p = self.eng.submit(segs, int(payload_ptr), int(payload_len), now, self.step_no, now, self.worker)
         self.step_no += 1
         if self.world > 1:
@@ -829,7 +829,7 @@ class GpuDataPlane(ControlState):
                     self.set_import(recv)
                 else:
                     self.submit_b(recv)
-        return (p, len(segs), t0)
+        return (p, len(segs), t0, self.eng.egress_slot(p))
 
     def prefetch(self, payload_ptr, payload_len):
         """Queue the NEXT step's ingress payload H2D now (overlapped single-GPU engine): it
@@ -858,7 +858,7 @@ class GpuDataPlane(ControlState):
                 raise RuntimeError(f"rank {self.rank}: native exchange failed (rc {rc}: a peer did not answer)")
         self.eng.launch_b(p)
         self._xprev = p
-        return (p, len(segs), t0)
+        return (p, len(segs), t0, self.eng.egress_slot(p))
 
     def _exchange_parity(self, q):
         """All-to-all of the launched step of parity ``q`` (its phase A packed S[q]; the
@@ -905,7 +905,7 @@ class GpuDataPlane(ControlState):
         self._pending = None
 
     def finish(self, ticket, collect=True, wait_egress=True, collect_egress=True):
-        p, nseg, t0 = ticket
+        p, nseg, t0, slot = ticket
         self.eng.wait_results(p)
         self._last_parity = p
         res = StepResult()
@@ -938,10 +938,10 @@ class GpuDataPlane(ControlState):
                         res.ctrl.append((int(rec["conn"]), bytes(io["ctrl"][o:o + n])))
             res.txbuf.sort()
         if wait_egress or collect:
-            self.eng.egress_wait(p)
+            self.eng.egress_wait_slot(slot)
         if collect and collect_egress:
             co = io["conn_out"]
-            eg = self._egress[self.eng.egress_slot(p)]
+            eg = self._egress[slot]
             for conn in np.nonzero(co["len"])[0]:
                 o, n = int(co["off"][conn]), int(co["len"][conn])
                 res.egress[int(conn)] = bytes(eg[o:o + n])
@@ -951,7 +951,9 @@ class GpuDataPlane(ControlState):
     def host_egress(self, ticket):
         """(egress bytes view, ConnOut view) of a finished step, for zero-copy socket writes."""
         io = self._io[ticket[0]]
-        return self._egress[self.eng.egress_slot(ticket[0])], io["conn_out"]
+        return self._egress[ticket[3]], io["conn_out"]
 
     def egress_wait(self, ticket):
-        self.eng.egress_wait(ticket[0])
+        # by the slot the step rendered into (recorded at submit): a later step of the same
+        # parity has its own slot, so waiting "by parity" would wait for the wrong copy
+        self.eng.egress_wait_slot(ticket[3])

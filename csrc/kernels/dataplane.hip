@@ -3802,6 +3802,15 @@ DEV void final_step(const DS& d) {
   if (d.links)
     for (u32 r = 0; r < d.world; ++r) d.xchg[XC_ACK_N + r] = d.lk_cnt[r] < d.lk_cap ? d.lk_cnt[r] : d.lk_cap;
   *d.ctr_host = *c;
+  // open the step's egress gate: the SDMA engine, polling it, starts the D2H of this
+  // step's egress now.  The rendered bytes left their L2s at the earlier kernels' ends;
+  // the system-scope release covers this kernel's own stores (vector store, system scope)
+  const u64 gate = d.in->gate;
+  if (gate) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __hip_atomic_store((i64*)gate, (i64)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
 }
 
 // persistence: size + pack the step's persist records (header + message bytes) into the

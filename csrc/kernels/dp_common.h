@@ -42,7 +42,7 @@ enum : u32 {
 enum : u32 { US_FREE = 0, US_PENDING = 1, US_ACKED = 2, US_REQUEUE = 3, US_DONE = 4 };
 
 
-struct StepIn {         // host -> device per step (64 B)
+struct StepIn {         // host -> device per step (72 B)
   u32 nseg;
   u32 flags;
   i64 now_ms;
@@ -54,6 +54,11 @@ struct StepIn {         // host -> device per step (64 B)
   u32 nunp;             // connections to unpause before this step's frame scan (DS.unpause_req)
   u32 pslot;            // host persist slot of this step (DS.ps_persist / ps_crec, rotating)
   u64 ingress;          // device pointer: this step's ingress slot (engine rotates INGRESS_SLOTS)
+  // the value word of this step's egress gate (an HSA signal, 1 while armed; 0 = none): the
+  // step's last kernel stores 0 once every byte is rendered, which releases the egress D2H
+  // the host queued on the SDMA engine at launch -- no host round trip between render and
+  // copy
+  u64 gate;
 };
 
 

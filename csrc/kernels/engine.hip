@@ -17,6 +17,7 @@
 #include <string>
 #include <vector>
 
+#include <hsa/amd_hsa_signal.h>
 #include <hsa/hsa.h>
 #include <hsa/hsa_ext_amd.h>
 #include <rocprofiler-sdk-roctx/roctx.h>
@@ -589,6 +590,12 @@ class Engine {
     // overlap (world 1): the step's ingest half runs on its own stream, next to the
     // previous step's routing / delivery half
     overlap_ = d_.world == 1 && get("overlap", 1) != 0;
+    // egress_gate (HSA SDMA egress, overlapped steps): the step's D2H is queued on the SDMA
+    // engine at launch, behind a gate signal the step's last kernel opens (final_step), sized
+    // from the recent steps' egress (a host-issued tail copies the rest when a step renders
+    // more) -- the host is off the render -> D2H path.  0: the D2H is issued by the host
+    // after it saw the step finish (egress_copy)
+    gated_ = copy_mode_ == 3 && overlap_ && get("egress_gate", 1) != 0;
     for (int p = 0; p < 2; ++p) {
       HIPCHECK(hipEventCreateWithFlags(&ev_h2d_[p], hipEventDisableTiming));
       HIPCHECK(hipEventCreateWithFlags(&ev_done_[p], hipEventDisableTiming));
@@ -611,6 +618,13 @@ class Engine {
   }
 
   ~Engine() {
+    // a gated copy never outlives its gate: open every gate, so no SDMA queue waits forever
+    // (a step that faulted before its last kernel), then let the copies finish
+    if (copy_mode_ == 3)
+      for (int e = 0; e < EGRESS_SLOTS; ++e) {
+        if (gate_sig_[e].handle) hsa_signal_store_screlease(gate_sig_[e], 0);
+        if (sdma_pending_[e] || tail_pending_[e]) sdma_wait(e);
+      }
     (void)hipStreamSynchronize(s_comp_);
     (void)hipStreamSynchronize(s_h2d_);
     (void)hipStreamSynchronize(s_pre_);
@@ -725,6 +739,7 @@ class Engine {
     o["world"] = d_.world; o["rank"] = d_.my_rank; o["import_max"] = d_.import_max; o["pub_cap"] = d_.pub_cap;
     o["copy_engine"] = copy_mode_ == 3 ? "hsa-sdma" : copy_mode_ == 2 ? "kernel" : (sdma_ ? "nocu" : "blit");
     o["copy_wgs"] = copy_wgs_;
+    o["egress_gate"] = gated_ ? 1 : 0;
     o["egress_slots"] = EGRESS_SLOTS;
     { u32 e = 0; while (copy_mode_ == 3 && e < 32 && !(((u32)sdma_engine_ >> e) & 1u)) ++e; o["sdma_engine"] = copy_mode_ == 3 ? (int)e : -1; }
     { u32 e = 0; while (sdma_engine2_ && e < 32 && !(((u32)sdma_engine2_ >> e) & 1u)) ++e; o["sdma_engine2"] = sdma_engine2_ ? (int)e : -1; }
@@ -780,6 +795,15 @@ class Engine {
     in->worker = worker;
     const int e = (int)(seq_ % EGRESS_SLOTS);
     in->egress = (u64)egress_dev_[e];
+    // the slot's previous D2H (step t - EGRESS_SLOTS, long finished) must be complete before
+    // its gate is re-armed and its buffer rendered into again
+    if (copy_mode_ == 3 && (sdma_pending_[e] || tail_pending_[e])) { HostTimer t(&ht_[1]); sdma_wait(e); }
+    spec_[e] = gated_ ? spec_bytes() : 0;
+    in->gate = 0;
+    if (spec_[e]) {
+      hsa_signal_store_screlease(gate_sig_[e], 1);
+      in->gate = (u64)&((amd_signal_t*)gate_sig_[e].handle)->value;
+    }
     const int is = (int)(seq_ % INGRESS_SLOTS);
     in->ingress = (u64)ingress_slot_[is];
     in->pslot = (u32)(seq_ % PSLOTS);
@@ -930,6 +954,19 @@ class Engine {
       HIPCHECK(hipEventRecord(ev_rest_[p], s_comp_));
       rest_issued_[p] = true;
       HIPCHECK(hipEventRecord(ev_done_[p], s_comp_));
+      if (spec_[e]) {   // the egress D2H, queued now, starts when the step's last kernel opens the gate
+        Range rg("chanamq.K5.egress_gated");
+        hsa_signal_store_screlease(sdma_sig_[e], 1);
+        hsa_status_t st = hsa_amd_memory_async_copy_on_engine(egress_host_[e], cpu_agent_, egress_dev_[e], gpu_agent_,
+                                                              spec_[e], 1, &gate_sig_[e], sdma_sig_[e], sdma_engine_, true);
+        if (st != HSA_STATUS_SUCCESS) {
+          hsa_signal_store_screlease(sdma_sig_[e], 0);
+          throw std::runtime_error("hsa_amd_memory_async_copy_on_engine (gated egress) failed");
+        }
+        sdma_pending_[e] = true;
+        ++eg_stats_[0];
+        eg_stats_[2] += spec_[e];
+      }
       if (copy_mode_ == 2) {   // egress D2H right behind the step, sized on the device
         // (measured slower than the host-issued SDMA copy -- CU stores over PCIe stall
         // behind the next step's kernels: 8.7 vs 32.9 M msgs/s, profiles/r4_bench/pre_*)
@@ -1558,6 +1595,8 @@ class Engine {
     if (copy_mode_ == 3) {
       if (sdma_pending_[e])
         hsa_signal_wait_scacquire(sdma_sig_[e], HSA_SIGNAL_CONDITION_EQ, 0, UINT64_MAX, HSA_WAIT_STATE_ACTIVE);
+      if (tail_pending_[e])
+        hsa_signal_wait_scacquire(tail_sig_[e], HSA_SIGNAL_CONDITION_EQ, 0, UINT64_MAX, HSA_WAIT_STATE_ACTIVE);
       return;
     }
     if (d2h_issued_[e]) HIPCHECK(hipEventSynchronize(ev_d2h_[e]));
@@ -1565,7 +1604,7 @@ class Engine {
 
   void egress_wait_slot(int e) {
     HostTimer ht(&ht_[5]);
-    if (copy_mode_ == 3) { if (sdma_pending_[e]) sdma_wait(e); return; }
+    if (copy_mode_ == 3) { sdma_wait(e); return; }
     if (d2h_issued_[e]) HIPCHECK(hipEventSynchronize(ev_d2h_[e]));
   }
 
@@ -1576,6 +1615,10 @@ class Engine {
     if (staged_[p]) throw std::runtime_error("wait_results: step staged but never launched");
     HIPCHECK(hipEventSynchronize(ev_done_[p]));
     inflight_[p] = false;
+    // egress history of the gated copies' sizing (every finished step, idle ones too)
+    const u64 n = ((const Counters*)buf("ctr_host" + std::to_string(p)).ptr)->egress_bytes;
+    eg_hist_[eg_hist_i_++ & 3] = n;
+    eg_stats_[3] += n;
   }
 
   u64 egress_copy(int p) {
@@ -1584,6 +1627,22 @@ class Engine {
     const Counters* c = (const Counters*)buf("ctr_host" + std::to_string(p)).ptr;
     u64 n = c->egress_bytes;
     const int e = slot_of_[p];
+    if (spec_[e]) {   // gated: the bulk is on its way already; the host only adds a tail
+      if (n > spec_[e]) {
+        const u64 off = spec_[e];
+        hsa_signal_store_screlease(tail_sig_[e], 1);
+        hsa_status_t st = hsa_amd_memory_async_copy_on_engine((u8*)egress_host_[e] + off, cpu_agent_,
+                                                              (u8*)egress_dev_[e] + off, gpu_agent_, n - off, 0, nullptr,
+                                                              tail_sig_[e], tail_engine_, true);
+        if (st != HSA_STATUS_SUCCESS) {
+          hsa_signal_store_screlease(tail_sig_[e], 0);
+          throw std::runtime_error("hsa_amd_memory_async_copy_on_engine (egress tail) failed");
+        }
+        tail_pending_[e] = true;
+        ++eg_stats_[1];
+      }
+      return n;
+    }
     if (eager_d2h_[p]) {   // already queued behind the step (launch)
       eager_d2h_[p] = false;
       return n;
@@ -1621,13 +1680,38 @@ class Engine {
   void egress_wait(int p) {
     HostTimer ht(&ht_[5]);
     const int e = slot_of_[p];
-    if (copy_mode_ == 3) { if (sdma_pending_[e]) sdma_wait(e); return; }
+    if (copy_mode_ == 3) { sdma_wait(e); return; }
     HIPCHECK(hipEventSynchronize(ev_d2h_[e]));
   }
 
+  // the slot's D2H (+ its tail) complete
   void sdma_wait(int e) {
-    hsa_signal_wait_scacquire(sdma_sig_[e], HSA_SIGNAL_CONDITION_EQ, 0, UINT64_MAX, HSA_WAIT_STATE_ACTIVE);
+    if (sdma_pending_[e])
+      hsa_signal_wait_scacquire(sdma_sig_[e], HSA_SIGNAL_CONDITION_EQ, 0, UINT64_MAX, HSA_WAIT_STATE_ACTIVE);
+    if (tail_pending_[e])
+      hsa_signal_wait_scacquire(tail_sig_[e], HSA_SIGNAL_CONDITION_EQ, 0, UINT64_MAX, HSA_WAIT_STATE_ACTIVE);
     sdma_pending_[e] = false;
+    tail_pending_[e] = false;
+  }
+
+  // gated egress: bytes to copy speculatively for the next step -- the largest of the last
+  // four steps' egress + 1/16 + 64 KB, in 64 KB units (0 after four steps without egress)
+  u64 spec_bytes() const {
+    u64 mx = 0;
+    for (u64 v : eg_hist_) mx = v > mx ? v : mx;
+    if (!mx) return 0;
+    const u64 sz = (mx + mx / 16 + (64u << 10) + 65535) & ~(u64)65535;
+    return sz < egress_alloc_ ? sz : egress_alloc_;
+  }
+  // gated egress counters: [gated copies, tail copies, bytes copied speculatively, bytes rendered]
+  py::dict egress_stats() const {
+    py::dict o;
+    o["gated"] = gated_;
+    o["gated_copies"] = eg_stats_[0];
+    o["tail_copies"] = eg_stats_[1];
+    o["spec_bytes"] = eg_stats_[2];
+    o["egress_bytes"] = eg_stats_[3];
+    return o;
   }
 
   // egress slot (host view "egress_host<slot>") of the step last submitted with parity p
@@ -1673,14 +1757,21 @@ class Engine {
     if (sdma_split_ > 1)
       for (u32 c : {2u, 3u, 0u})
         if (c != pick && ((mask >> c) & 1u)) { sdma_engine2_ = (hsa_amd_sdma_engine_id_t)(1u << c); break; }
+    // the tail engine (gated egress): another full-rate engine than the gated copies' --
+    // which can sit behind the next step's gate -- and than the runtime's H2D engine 0
+    tail_engine_ = sdma_engine_;
+    for (u32 c : {2u, 3u, 0u})
+      if (c != pick && ((mask >> c) & 1u)) { tail_engine_ = (hsa_amd_sdma_engine_id_t)(1u << c); break; }
     for (int e = 0; e < EGRESS_SLOTS; ++e)
-      if (hsa_signal_create(0, 0, nullptr, &sdma_sig_[e]) != HSA_STATUS_SUCCESS)
+      if (hsa_signal_create(0, 0, nullptr, &sdma_sig_[e]) != HSA_STATUS_SUCCESS ||
+          hsa_signal_create(0, 0, nullptr, &tail_sig_[e]) != HSA_STATUS_SUCCESS ||
+          hsa_signal_create(0, 0, nullptr, &gate_sig_[e]) != HSA_STATUS_SUCCESS)
         throw std::runtime_error("hsa_signal_create failed");
   }
 
   void drain_egress() {
     for (int e = 0; e < EGRESS_SLOTS; ++e) {
-      if (sdma_pending_[e]) sdma_wait(e);
+      sdma_wait(e);
       if (d2h_issued_[e]) HIPCHECK(hipEventSynchronize(ev_d2h_[e]));
     }
   }
@@ -2041,6 +2132,17 @@ class Engine {
   int sdma_split_ = 1;
   hsa_signal_t sdma_sig_[EGRESS_SLOTS] = {};
   bool sdma_pending_[EGRESS_SLOTS] = {};
+  // gated egress: per slot the gate the step's last kernel opens, the host tail's signal,
+  // whether a tail is in flight and the bytes copied speculatively for the slot's step
+  bool gated_ = false;
+  hsa_signal_t gate_sig_[EGRESS_SLOTS] = {};
+  hsa_signal_t tail_sig_[EGRESS_SLOTS] = {};
+  bool tail_pending_[EGRESS_SLOTS] = {};
+  u64 spec_[EGRESS_SLOTS] = {};
+  hsa_amd_sdma_engine_id_t tail_engine_{};
+  u64 eg_hist_[4] = {0, 0, 0, 0};
+  u32 eg_hist_i_ = 0;
+  u64 eg_stats_[4] = {0, 0, 0, 0};
   u32 copy_wgs_ = 16;
   int sdma_pref_ = -1;
   double ht_[8] = {0, 0, 0, 0, 0, 0, 0, 0};   // host_times() phases
@@ -2123,6 +2225,7 @@ PYBIND11_MODULE(_dataplane, m) {
       .def("egress_copy", &Engine::egress_copy)
       .def("egress_wait", &Engine::egress_wait)
       .def("egress_slot", &Engine::egress_slot)
+      .def("egress_wait_slot", &Engine::egress_wait_slot)
       .def("sync", &Engine::sync)
       .def("c_api", &Engine::c_api)
       .def("xchg_setup", &Engine::xchg_setup, py::arg("kind"), py::arg("arg"), py::arg("members"),
@@ -2141,5 +2244,6 @@ PYBIND11_MODULE(_dataplane, m) {
       .def("drop_exchange", &Engine::drop_exchange)
       .def("launch_b", &Engine::launch_b)
       .def("counters", &Engine::counters)
-      .def("host_times", &Engine::host_times, py::arg("reset") = false);
+      .def("host_times", &Engine::host_times, py::arg("reset") = false)
+      .def("egress_stats", &Engine::egress_stats);
 }

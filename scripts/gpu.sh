@@ -14,6 +14,7 @@
 #   bench       bench.py at the driver's K=20 / W=5, once per CHUNKS entry (default: the
 #               bench's default step), REPEAT times each (default 1)
 #   bench200    the same at K=200 (steady state)
+#   sweep       bench.py once per SWEEP entry ("label=--args;label=--args"), REPEAT times, K=${K:-20}
 #   trace       rocprofv3 kernel + memory-copy trace of bench.py (CHUNK, default 32768),
 #               then the step timeline / overlap / gap summaries
 #   stats       rocprofv3 --kernel-trace --stats of bench.py (per-kernel time table)
@@ -62,6 +63,16 @@ for T in "$@"; do
         CA=""; [ "$ch" != default ] && CA="--chunk $ch"
         timeout -k 10 150 python bench.py --gpus 1 --steps $K --warmup 5 --soak-s 0 $CA $BENCH_ARGS > $f 2> ${f%.json}.err
         ok $? bench; line $f
+      done
+    done ;;
+  sweep)   # SWEEP="label1=--args ...;label2=--args ..." -> bench.py K=${K:-20} once per entry, REPEAT times
+    IFS=';' read -ra ENTRIES <<< "$SWEEP"
+    for ent in "${ENTRIES[@]}"; do
+      lab=${ent%%=*}; args=${ent#*=}
+      for r in $(seq 1 "${REPEAT:-1}"); do
+        f=$O/sweep_${lab}_r$r.json
+        timeout -k 10 150 python bench.py --gpus 1 --steps ${K:-20} --warmup 5 --soak-s 0 $args > $f 2> ${f%.json}.err
+        ok $? "sweep $lab"; line $f
       done
     done ;;
   trace)
