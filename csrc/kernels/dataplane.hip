@@ -343,8 +343,16 @@ DEV bool topic_match(const u8* pat, u32 plen, const u8* key, u32 klen, bool hash
 // step, whose output the frame scan then read back)
 __global__ __launch_bounds__(1024) void k_stage(DS d) {
   __shared__ u32 lds[1024 / 64 + 1];
+  __shared__ StepIn s_in;
   const u32 tid = threadIdx.x;
-  const u32 nseg = d.in->nseg;
+  // the step's descriptors from the host's mapped staging (one PCIe round), written to
+  // their device copies for every later kernel of the step
+  if (tid == 0) {
+    s_in = *d.in_h;
+    *d.in = s_in;
+  }
+  __syncthreads();
+  const u32 nseg = s_in.nseg;
   {
     u32* c = (u32*)d.ctr;
     for (u32 k = tid; k < sizeof(Counters) / 4; k += 1024)
@@ -356,14 +364,18 @@ __global__ __launch_bounds__(1024) void k_stage(DS d) {
     }
     // connections whose control command the host has answered resume with this step (the
     // frame scan, the only reader and writer of the flag, runs after this kernel)
-    const u32 nunp = d.in->nunp;
+    const u32 nunp = s_in.nunp;
     for (u32 k = tid; k < nunp; k += 1024) {
       const u32 c = d.unpause_req[k];
       if (c < d.c_max) d.conn_paused[c] = 0;
     }
   }
   u32 total = 0;
-  for (u32 k = tid; k < nseg; k += 1024) total += align16(d.carry_len[d.segs[k].conn] + d.segs[k].len + 32);
+  for (u32 k = tid; k < nseg; k += 1024) {
+    const SegIn sg = d.segs_h[k];
+    ((SegIn*)d.segs)[k] = sg;
+    total += align16(d.carry_len[sg.conn] + sg.len + 32);
+  }
   u32 all_t;
   block_scan<1024>(total, lds, all_t);
   if (tid == 0) d.tot[15] = all_t;  // work bytes used
@@ -373,8 +385,9 @@ __global__ __launch_bounds__(1024) void k_stage(DS d) {
     const u32 k = b0 + tid;
     u32 cl = 0, len = 0, v = 0;
     if (k < nseg) {
-      cl = d.carry_len[d.segs[k].conn];
-      len = d.segs[k].len;
+      const SegIn sg = d.segs_h[k];   // (the device copy of this block's own stores: not re-read)
+      cl = d.carry_len[sg.conn];
+      len = sg.len;
       v = align16(cl + len + 32);
     }
     u32 all;
@@ -1394,23 +1407,22 @@ __global__ __launch_bounds__(256) void k_decode(DS d) {
 // routing half.  k_decode only records acks and publishes, so the ingest half never
 // touches delivery-side state and can run next to the previous step's k_chan_advance /
 // k_render (engine overlap).  Also the routing half's per-step resets.
-__global__ __launch_bounds__(256) void k_marks(DS d) {
-  const u32 i = blockIdx.x * 256 + threadIdx.x;
-  if (i == 0) {
-    if (d.links)
-      for (u32 r = 0; r < WORLD_MAX; ++r) d.lk_cnt[r] = 0;
-    // snowflake virtual position base for this step (ID_SLOT_BITS slots per wall-clock ms)
-    const u64 floor_pos = d.in->id_ms << ID_SLOT_BITS;
-    const u64 cur = *d.id_next;
-    *d.id_next = cur > floor_pos ? cur : floor_pos;
-  }
+// (fused into k_route_store, phase 0: the marks only have to precede k_chan_advance, and
+// the snowflake id floor moved into log_reserve, its one reader -- a launch less per step)
+DEV void marks_range(const DS& d, u32 i0, u32 stride) {
+  if (i0 == 0 && d.links)
+    for (u32 r = 0; r < WORLD_MAX; ++r) d.lk_cnt[r] = 0;
   const u32 na = d.ctr->n_acks, np = d.ctr->n_pubs;
-  if (i < na) apply_ack(d, d.acks[i], i);
-  if (i < np) {
-    const u32 ch = d.pubs[i].chslot;
-    if (ch != INVALID && d.ch_confirm[ch]) atomicAdd(&d.ch_pub_cnt[ch], 1u);
+  const u32 n = na > np ? na : np;
+  for (u32 i = i0; i < n; i += stride) {
+    if (i < na) apply_ack(d, d.acks[i], i);
+    if (i < np) {
+      const u32 ch = d.pubs[i].chslot;
+      if (ch != INVALID && d.ch_confirm[ch]) atomicAdd(&d.ch_pub_cnt[ch], 1u);
+    }
   }
 }
+__global__ __launch_bounds__(256) void k_marks(DS d) { marks_range(d, blockIdx.x * 256 + threadIdx.x, gridDim.x * 256); }
 
 // ============================================================================ scans
 // single-block multi-array exclusive scan; n read from device; totals -> tot[slot+k]
@@ -2087,8 +2099,12 @@ DEV void log_reserve(const DS& d) {
   u32 np = d.tot[TS_PAIR_BASE] + d.tot[0];
   d.tot[TS_PAIR_N] = np < d.pair_max ? np : d.pair_max;
   d.ctr->n_pairs = d.tot[TS_PAIR_N];
-  *d.id_base = *d.id_next;
-  *d.id_next = *d.id_next + routed;
+  // snowflake virtual position base for this step (ID_SLOT_BITS slots per wall-clock ms):
+  // never below the step's clock (was k_marks; idempotent for a second routing phase)
+  const u64 floor_pos = d.in->id_ms << ID_SLOT_BITS;
+  const u64 cur = *d.id_next > floor_pos ? *d.id_next : floor_pos;
+  *d.id_base = cur;
+  *d.id_next = cur + routed;
   u64 head = *d.log_head, tail = *d.log_tail;
   u64 phys = head % d.log_bytes;
   if (phys + total > d.log_bytes) head += d.log_bytes - phys;
@@ -2141,9 +2157,11 @@ DEV void live_add_blocks(const DS& d, u32 lane) {
 // k_store: one pass over the phase's publishes)
 DEV void store_one_pre(const DS& d, u32 p, u32 lane, const Pub& pb, u32 nq, u32 rr, u32 soff, u32 wbase);
 DEV void live_add_blocks(const DS& d, u32 lane);
-__global__ __launch_bounds__(256) void k_route_store(DS d) {
+__global__ __launch_bounds__(256) void k_route_store(DS d, u32 marks) {
   u32 lane = lane_id();
   if (blockIdx.x == 0 && threadIdx.x < 64) live_add_blocks(d, lane);
+  // phase 0 (the step's own commands): K9 ack marks + K10 confirm counts (fused k_marks)
+  if (marks) marks_range(d, blockIdx.x * blockDim.x + threadIdx.x, gridDim.x * blockDim.x);
   u32 n = d.tot[TS_RANGE_HI];
   if (n > d.pub_cap) n = d.pub_cap;
   const u32 nw = (gridDim.x * blockDim.x) >> 6;
@@ -2536,16 +2554,9 @@ __global__ void k_qfirst(DS d, u32 src) {
   if (i == 0 || (k[i - 1] >> rb) != (k[i] >> rb)) d.q_first[k[i] >> rb] = i;
 }
 
-DEV u32 enqueue_one(const DS& d, u32 src, u32 i, u32 n, PersistRec* pr, u32 hs_ntiles) {
-  const u32* kk = d.pair_k[src];
-  const u32 rb = d.rank_bits;
-  u32 q = kk[i] >> rb;
-  u32 p = d.pair_v[src][i];
-  // single-pass sort (queue|rank key <= 8 bits): the queue's first pair is where digit
-  // (q << rank_bits) starts; otherwise k_qfirst recorded it
-  u32 first = hs_ntiles ? d.hist_scan[q << rb] : d.q_first[q];
-  u32 rank = i - first;
-  bool last = (i + 1 == n) || (kk[i + 1] >> rb) != q;
+// publish p's entry at position `rank` of this step's entries for queue q (`last`: the
+// queue's last pair, which moves q_tail); returns the message to release if the ring is full
+DEV u32 enqueue_at(const DS& d, u32 q, u32 p, u32 rank, bool last, PersistRec* pr) {
   const Pub& pb = d.pubs[p];
   // the queue's last pair moves q_tail in this kernel: every pair reads the tail that
   // k_ring_plan recorded before the enqueue, never q_tail itself
@@ -2578,6 +2589,16 @@ DEV u32 enqueue_one(const DS& d, u32 src, u32 i, u32 n, PersistRec* pr, u32 hs_n
   }
   return drop;
 }
+DEV u32 enqueue_one(const DS& d, u32 src, u32 i, u32 n, PersistRec* pr, u32 hs_ntiles) {
+  const u32* kk = d.pair_k[src];
+  const u32 rb = d.rank_bits;
+  u32 q = kk[i] >> rb;
+  u32 p = d.pair_v[src][i];
+  // single-pass sort (queue|rank key <= 8 bits): the queue's first pair is where digit
+  // (q << rank_bits) starts; otherwise k_qfirst recorded it
+  u32 first = hs_ntiles ? d.hist_scan[q << rb] : d.q_first[q];
+  return enqueue_at(d, q, p, i - first, (i + 1 == n) || (kk[i + 1] >> rb) != q, pr);
+}
 
 // ---- unbounded queues (QueueEntity.scala:271-316 keeps a growing Vector): before the
 // step's enqueue, the last pair of every queue checks that the queue's ring holds this
@@ -2585,13 +2606,17 @@ DEV u32 enqueue_one(const DS& d, u32 src, u32 i, u32 n, PersistRec* pr, u32 hs_n
 // ring pool (one bump pointer shared with the host's allocator), within the queue's
 // max_capacity.  Positions stay absolute (entry pos lives at off + (pos & mask)), so
 // unacked windows, requeues and store rows keep their queue offsets.
+DEV void plan_queue(const DS& d, u32 q, u64 cnt);
 DEV void ring_plan_one(const DS& d, u32 src, u32 hs_ntiles, u32 i, u32 n) {
   const u32* kk = d.pair_k[src];
   const u32 rb = d.rank_bits;
   const u32 q = kk[i] >> rb;
   if (i + 1 < n && (kk[i + 1] >> rb) == q) return;   // not the queue's last pair
   const u32 first = hs_ntiles ? d.hist_scan[q << rb] : d.q_first[q];
-  const u64 cnt = (u64)(i - first) + 1;
+  plan_queue(d, q, (u64)(i - first) + 1);
+}
+// queue q takes cnt entries this step: record its tail before the enqueue, grow its ring
+DEV void plan_queue(const DS& d, u32 q, u64 cnt) {
   const u64 head = d.q_head[q], tail = d.q_tail[q];
   d.q_enq_tail[q] = tail;
   const u64 mask = d.q_ring_mask[q], cap = mask + 1;
@@ -2666,6 +2691,142 @@ __global__ void k_enqueue(DS d, u32 src, u32 hs_ntiles) {
       bool want = pr.msg != INVALID;
       u32 k = wave_reserve(&d.ctr->n_persist, want);
       if (want && k < d.persist_max) d.prec[k] = pr;
+    }
+  }
+}
+
+// ---- single-pass sort (queue | rank key <= 11 bits) with the enqueue fused: k_ring_plan
+// and k_enqueue fold into the sort's two kernels.  The histogram's last block knows every
+// queue's pair count (its digit range) and plans the rings; the scatter knows every pair's
+// sorted position -- its rank in its queue -- and writes the ring entry itself, so the
+// sorted pair arrays are never materialised.  Two launches a step instead of four.
+DEV void plan_rings_block(const DS& d, const u32* hscan, u32 n, u32 D, u32 tid, u32 nt) {
+  const u32 rb = d.rank_bits;
+  for (u32 q = tid; q < d.q_max && (q << rb) < D; q += nt) {
+    // the digit starts (row 0 of hscan) were stored by this block: agent-scope loads
+    const u32 first = __hip_atomic_load(&hscan[q << rb], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const u32 nx = ((q + 1) << rb) < D
+                       ? __hip_atomic_load(&hscan[(q + 1) << rb], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                       : n;
+    if (nx > first) plan_queue(d, q, nx - first);
+  }
+  __syncthreads();
+  const u32 nm = __hip_atomic_load(&d.tot[TS_NMOVE], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (!nm) return;   // (block-uniform) rings that grew: copy their live entries over
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  for (u32 m = 0; m < nm; ++m) {
+    const RingMove mv = d.moves[m];
+    for (u64 pos = mv.head + tid; pos < mv.tail; pos += nt)
+      d.ring[mv.new_off + (pos & mv.new_mask)] = d.ring[mv.old_off + (pos & mv.old_mask)];
+  }
+}
+
+template <int DB>
+__global__ __launch_bounds__(RsNt<DB>::v) void k_rs_hist_plan(DS d, const u32* keys, const u32* np, u32* hist,
+                                                             u32* hscan, u32* ticket, u32 ntiles) {
+  constexpr u32 NT = RsNt<DB>::v, D = 1u << DB;
+  __shared__ u32 cnt[D];
+  __shared__ u32 lds[NT / 64 + 1];
+  __shared__ u32 s_last;
+  u32 tid = threadIdx.x, t = blockIdx.x;
+  const u32 n = *np;
+  u32 T = (n + SORT_TILE - 1) / SORT_TILE;
+  if (T > ntiles) T = ntiles;
+  if (T == 0) {   // no pairs: nothing to plan (the queues' tails stay)
+    return;
+  }
+  if (t >= T) return;
+  bool last = false;
+  for (; t < T; t += gridDim.x) {
+    for (u32 k = tid; k < D; k += NT) cnt[k] = 0;
+    __syncthreads();
+    const u32 base = t * SORT_TILE;
+    for (u32 j = 0; j < SORT_TILE / NT; ++j) {
+      const u32 i = base + j * NT + tid;
+      if (i < n) atomicAdd(&cnt[keys[i] & (D - 1)], 1u);
+    }
+    __syncthreads();
+    for (u32 k = tid; k < D; k += NT)
+      __hip_atomic_store(&hist[t * D + k], cnt[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __syncthreads();
+    if (tid == 0) s_last = atomicAdd(ticket, 1u) == T - 1;
+    __syncthreads();
+    last = last || s_last;
+  }
+  if (!last) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  if (tid == 0) *ticket = 0;
+  rs_offsets<DB>(hist, hscan, T, lds);
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __syncthreads();
+  plan_rings_block(d, hscan, n, D, tid, NT);
+}
+
+template <int DB>
+__global__ __launch_bounds__(256) void k_rs_scatter_enq(DS d, const u32* kin, const u32* vin, const u32* np,
+                                                       const u32* hscan) {
+  constexpr u32 D = 1u << DB;
+  __shared__ u32 wc[4][D];
+  const u32 tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+  const u32 n = *np, rb = d.rank_bits;
+  for (u32 t = blockIdx.x; t * SORT_TILE < n; t += gridDim.x) {   // tile-stride (capped grid)
+    const u32 base = t * SORT_TILE;
+    __syncthreads();
+    for (u32 i = tid; i < 4 * D; i += 256) ((u32*)wc)[i] = 0;
+    __syncthreads();
+    const u32 wbase = base + w * (SORT_TILE / 4);
+    for (u32 c = 0; c < SORT_TILE / 256; ++c) {   // per-wave digit counts
+      const u32 i = wbase + c * 64 + lane;
+      const bool valid = i < n;
+      const u32 dg = valid ? kin[i] & (D - 1) : 0;
+      u64 peers = __ballot(valid);
+#pragma unroll
+      for (u32 bb = 0; bb < DB; ++bb) {
+        const u64 m = __ballot((dg >> bb) & 1);
+        peers &= ((dg >> bb) & 1) ? m : ~m;
+      }
+      if (valid && ((peers & lanemask_lt()) == 0)) wc[w][dg] += __popcll(peers);
+      __builtin_amdgcn_wave_barrier();
+    }
+    __syncthreads();
+    for (u32 dg = tid; dg < D; dg += 256) {
+      u32 run = hscan[t * D + dg];
+      for (u32 ww = 0; ww < 4; ++ww) { const u32 x = wc[ww][dg]; wc[ww][dg] = run; run += x; }
+    }
+    __syncthreads();
+    for (u32 c = 0; c < SORT_TILE / 256; ++c) {
+      const u32 i = wbase + c * 64 + lane;
+      const bool valid = i < n;
+      const u32 key = valid ? kin[i] : 0;
+      const u32 dg = key & (D - 1);
+      u64 peers = __ballot(valid);
+#pragma unroll
+      for (u32 bb = 0; bb < DB; ++bb) {
+        const u64 m = __ballot((dg >> bb) & 1);
+        peers &= ((dg >> bb) & 1) ? m : ~m;
+      }
+      const u32 basepos = ((volatile u32*)wc[w])[dg];
+      const u32 pos = basepos + __popcll(peers & lanemask_lt());
+      PersistRec pr;
+      pr.msg = INVALID;
+      u32 drop = INVALID;
+      if (valid) {
+        const u32 q = key >> rb;
+        const u32 first = hscan[q << rb];
+        const u32 nx = ((q + 1) << rb) < D ? hscan[(q + 1) << rb] : n;
+        drop = enqueue_at(d, q, vin[i], pos - first, pos + 1 == nx, &pr);
+      }
+      wave_release(d, drop, drop != INVALID);
+      if (drop != INVALID) atomicAdd(&d.ctr->n_ring_full, 1u);
+      if (d.persist) {
+        const bool want = pr.msg != INVALID;
+        const u32 k = wave_reserve(&d.ctr->n_persist, want);
+        if (want && k < d.persist_max) d.prec[k] = pr;
+      }
+      __builtin_amdgcn_wave_barrier();
+      if (valid && ((peers & lanemask_lt()) == 0)) ((volatile u32*)wc[w])[dg] = basepos + __popcll(peers);
+      __builtin_amdgcn_wave_barrier();
     }
   }
 }

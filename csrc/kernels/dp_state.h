@@ -71,8 +71,10 @@ struct DS {
   u64 log_bytes, log_block, n_log_blocks, work_cap, ingress_cap, egress_cap, ctrl_cap, ring_pool;
 
   // ---------------- step io
-  StepIn* in;
-  const SegIn* segs;
+  StepIn* in;               // device copy of the step's StepIn (k_stage writes it)
+  const SegIn* segs;        // device copy of the step's segments (k_stage writes them)
+  const StepIn* in_h;       // host-mapped: the host's staging of them (read once, by k_stage)
+  const SegIn* segs_h;
   const u8* ingress;
   SegOut* seg_out;          // device; published to seg_out_h at the end of the step
   Counters* ctr;            // device

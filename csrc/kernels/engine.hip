@@ -234,8 +234,14 @@ class Engine {
           d_.ps_persist[k] = (u8*)hst(("persist" + ks).c_str(), d_.persist_bytes + 64);
           d_.ps_crec[k] = (ConsumedRec*)hst(("consumed" + ks).c_str(), sizeof(ConsumedRec) * (u64)d_.persist_max + 64);
         }
-      stage_in_[p] = (StepIn*)pinned(("stage_in" + sfx).c_str(), sizeof(StepIn));
-      stage_segs_[p] = (SegIn*)pinned(("stage_segs" + sfx).c_str(), sizeof(SegIn) * d_.seg_max);
+      // the step's descriptors stay in host-mapped memory: k_stage reads them over PCIe
+      // and writes the device copies (io.in / io.segs) the later kernels read.  Two H2D
+      // copies per step were runtime blit kernels on a third hardware queue, ordered behind
+      // the prefetched payload: ~50 us between the payload's arrival and the ingest
+      io.in_h = (const StepIn*)hst(("stage_in" + sfx).c_str(), sizeof(StepIn));
+      io.segs_h = (const SegIn*)hst(("stage_segs" + sfx).c_str(), sizeof(SegIn) * d_.seg_max + 64);
+      stage_in_[p] = (StepIn*)buf("stage_in" + sfx).ptr;
+      stage_segs_[p] = (SegIn*)buf("stage_segs" + sfx).ptr;
       // Basic.Get on the step: the requests (H2D with the step) and their answers
       io.get_req = (const GetReq*)dev(("get_req" + sfx).c_str(), sizeof(GetReq) * GET_STEP_MAX);
       io.get_out_h = (GetOut*)hst(("get_out" + sfx).c_str(), sizeof(GetOut) * GET_STEP_MAX);
@@ -510,6 +516,7 @@ class Engine {
       io.seg_out_h = io_[p].seg_out_h; io.conn_out_h = io_[p].conn_out_h; io.ctrl_h = io_[p].ctrl_h;
       io.ctrl_rec_h = io_[p].ctrl_rec_h; io.grow_h = io_[p].grow_h; io.conn_conf_h = io_[p].conn_conf_h;
       io.get_req = io_[p].get_req; io.get_out_h = io_[p].get_out_h; io.unpause_req = io_[p].unpause_req;
+      io.in_h = io_[p].in_h; io.segs_h = io_[p].segs_h;
       static_cast<DS&>(io_[p]) = io;
     }
     // native exchange (sharded steps driven by the native front end, csrc/core/frontend.cpp):
@@ -839,8 +846,6 @@ class Engine {
     if (pre && (pre_seq_[p] != step || pre_ptr_[p] != payload_ptr || pre_len_[p] != payload_len))
       throw std::runtime_error("submit: payload differs from the one prefetched for this step");
     pre_[p] = false;
-    HIPCHECK(hipMemcpyAsync((void*)io_[p].in, in, sizeof(StepIn), hipMemcpyHostToDevice, s_h2d_));
-    if (sb) HIPCHECK(hipMemcpyAsync((void*)io_[p].segs, stage_segs_[p], sb, hipMemcpyHostToDevice, s_h2d_));
     // overlapped engines move payloads on their own stream (prefetches run ahead of the
     // small per-step copies there; the ingest half waits for both)
     hipStream_t ps = overlap_ ? s_pre_ : s_h2d_;
@@ -1160,21 +1165,21 @@ class Engine {
     if (db) HIPCHECK(hipMemcpy((void*)rdesc, di.ptr, db, hipMemcpyHostToDevice));
     if (pb) HIPCHECK(hipMemcpy((void*)rpay, pi.ptr, pb, hipMemcpyHostToDevice));
     DS& io = io_[0];
-    StepIn in{};
+    StepIn& in = *stage_in_[0];   // (k_stage copies it to the device; no step in flight)
+    in = StepIn{};
     in.nseg = 0;
     in.now_ms = now_ms;
     in.step = seq_;
     in.id_ms = now_ms;
     in.worker = 0;
     in.egress = (u64)egress_dev_[0];
-    HIPCHECK(hipMemcpy((void*)io.in, &in, sizeof(StepIn), hipMemcpyHostToDevice));
+    in.ingress = (u64)ingress_slot_[0];
     u32* x = (u32*)buf("xchg0").ptr;
     for (u32 r = 0; r < 2 * WORLD_MAX; ++r) x[2 * WORLD_MAX + r] = x[XC_RECV_AN + r] = 0;
     for (u32 r = 0; r < WORLD_MAX; ++r) x[XC_RACK_N + r] = 0;
     x[2 * WORLD_MAX + d_.my_rank] = x[XC_RECV_AN + d_.my_rank] = n;
     x[3 * WORLD_MAX + d_.my_rank] = x[XC_RECV_AB + d_.my_rank] = (u32)pb;
     launch_ingest(s_comp_, io);
-    launch_marks(s_comp_, io);   // (no commands: the routing half's id floor / link-ack resets)
     launch_route(s_comp_, io, d_.pub_max);
     launch_phase_b(s_comp_, io, /*dispatch=*/false);
     HIPCHECK(hipStreamSynchronize(s_comp_));
@@ -1902,7 +1907,7 @@ class Engine {
                                  &d.tot[TS_RANGE_HI], d.pub_cap, 0, &d.tot[TS_RANGE_LO]);
     hipLaunchKernelGGL(k_scan_route, dim3(ceil_div(d.pub_cap ? d.pub_cap : 1, SCAN_TILE)), dim3(1024), 0, s, a, d.tot,
                        scan_status_, scan_ctl_, scan_smax_, d);
-    hipLaunchKernelGGL(k_route_store, wave_blocks(nmax), dim3(256), 0, s, d);
+    hipLaunchKernelGGL(k_route_store, wave_blocks(nmax), dim3(256), 0, s, d, imports ? 0u : 1u);
   }
 
   // serialise publishes with remote owners into the per-destination send buffers
@@ -1920,15 +1925,34 @@ class Engine {
   void launch_tail(hipStream_t s, const DS& d, bool dispatch = true) {
     Range rg("chanamq.K7-K11.tail");
     u32 nch = d.c_max * d.chpc;
-    u32* pk[2] = {d.pair_k[0], d.pair_k[1]};
-    u32* pv[2] = {d.pair_v[0], d.pair_v[1]};
-    u32 psrc = radix_sort(s, d, pk, pv, &d.tot[TS_PAIR_N], d.pair_max, d.q_bits + d.rank_bits);
     const u32 pbits = d.q_bits + d.rank_bits;
-    // single pass (<= 11 key bits): queue starts straight from the digit offsets
-    const u32 hs_ntiles = pbits <= 11 ? ceil_div(d.pair_max, SORT_TILE) : 0;
-    if (!hs_ntiles) hipLaunchKernelGGL(k_qfirst, blocks(d.pair_max, 256), dim3(256), 0, s, d, psrc);
-    hipLaunchKernelGGL(k_ring_plan, capped(ceil_div(d.pair_max, 256), 1024), dim3(256), 0, s, d, psrc, hs_ntiles);
-    hipLaunchKernelGGL(k_enqueue, capped(ceil_div(d.pair_max, 256), 1024), dim3(256), 0, s, d, psrc, hs_ntiles);
+    if (pbits <= 11) {
+      // single-pass sort with the ring plan folded into the histogram's last block and the
+      // enqueue into the scatter (k_rs_hist_plan / k_rs_scatter_enq): two launches
+      const u32 nt = ceil_div(d.pair_max, SORT_TILE);
+      const u32* n = &d.tot[TS_PAIR_N];
+      u32* tk = &d.tot[TS_RS_TICKET];
+      if (pbits <= 8) {
+        hipLaunchKernelGGL(k_rs_hist_plan<8>, capped(nt, 256), dim3(RsNt<8>::v), 0, s, d, d.pair_k[0], n, d_.hist, d_.hist_scan, tk, nt);
+        hipLaunchKernelGGL(k_rs_scatter_enq<8>, capped(nt, 256), dim3(256), 0, s, d, d.pair_k[0], d.pair_v[0], n, d_.hist_scan);
+      } else if (pbits == 9) {
+        hipLaunchKernelGGL(k_rs_hist_plan<9>, capped(nt, 256), dim3(RsNt<9>::v), 0, s, d, d.pair_k[0], n, d_.hist, d_.hist_scan, tk, nt);
+        hipLaunchKernelGGL(k_rs_scatter_enq<9>, capped(nt, 256), dim3(256), 0, s, d, d.pair_k[0], d.pair_v[0], n, d_.hist_scan);
+      } else if (pbits == 10) {
+        hipLaunchKernelGGL(k_rs_hist_plan<10>, capped(nt, 256), dim3(RsNt<10>::v), 0, s, d, d.pair_k[0], n, d_.hist, d_.hist_scan, tk, nt);
+        hipLaunchKernelGGL(k_rs_scatter_enq<10>, capped(nt, 256), dim3(256), 0, s, d, d.pair_k[0], d.pair_v[0], n, d_.hist_scan);
+      } else {
+        hipLaunchKernelGGL(k_rs_hist_plan<11>, capped(nt, 256), dim3(RsNt<11>::v), 0, s, d, d.pair_k[0], n, d_.hist, d_.hist_scan, tk, nt);
+        hipLaunchKernelGGL(k_rs_scatter_enq<11>, capped(nt, 256), dim3(256), 0, s, d, d.pair_k[0], d.pair_v[0], n, d_.hist_scan);
+      }
+    } else {
+      u32* pk[2] = {d.pair_k[0], d.pair_k[1]};
+      u32* pv[2] = {d.pair_v[0], d.pair_v[1]};
+      const u32 psrc = radix_sort(s, d, pk, pv, &d.tot[TS_PAIR_N], d.pair_max, pbits);
+      hipLaunchKernelGGL(k_qfirst, blocks(d.pair_max, 256), dim3(256), 0, s, d, psrc);
+      hipLaunchKernelGGL(k_ring_plan, capped(ceil_div(d.pair_max, 256), 1024), dim3(256), 0, s, d, psrc, 0u);
+      hipLaunchKernelGGL(k_enqueue, capped(ceil_div(d.pair_max, 256), 1024), dim3(256), 0, s, d, psrc, 0u);
+    }
     // without persistence nothing runs after k_post: it also writes the host-visible
     // outputs and its last block the counters (fused k_host_out)
     const u32 fin = d.persist ? 0u : 1u;
@@ -1970,22 +1994,15 @@ class Engine {
   // world == 1: the whole step; world > 1: phase A (ingest, local route, pack)
   void launch_main(hipStream_t s, const DS& d) {
     launch_ingest(s, d);
-    launch_marks(s, d);
-    launch_route(s, d, d.pub_max);
+    launch_route(s, d, d.pub_max);   // (+ the K9 marks / K10 confirm counts: k_route_store)
     if (d.world > 1) launch_pack(s, d);
     else launch_tail(s, d);
   }
 
-  // the step's acks / nacks / rejects marked in the channel windows and its publishes
-  // counted for their channels' confirms: the first kernel of the routing half (k_decode
-  // only records them), so an overlapped ingest never touches delivery-side state
-  void launch_marks(hipStream_t s, const DS& d) {
-    const u64 n = d.ack_max > d.pub_max ? d.ack_max : d.pub_max;
-    hipLaunchKernelGGL(k_marks, blocks(n, 256), dim3(256), 0, s, d);
-  }
-  // world == 1 with overlap: the routing / delivery half of the step
+  // world == 1 with overlap: the routing / delivery half of the step (the step's acks /
+  // nacks / rejects are marked and its confirms counted in it -- k_route_store, phase 0 --
+  // never in the ingest half, so an overlapped ingest never touches delivery-side state)
   void launch_rest(hipStream_t s, const DS& d) {
-    launch_marks(s, d);
     launch_route(s, d, d.pub_max);
     launch_tail(s, d);
   }
