@@ -270,7 +270,8 @@ def main():
     submit = dp.submit_lockstep if native else dp.submit_raw
 
     sub_t = {}      # step index -> host time its ingress was handed to the GPU (submit / prefetch)
-    slow = {"ms": 0.0}   # the timed window's slowest loop iteration: submit / prefetch / finish / egress
+    slow = {"ms": 0.0}   # the timed window's slowest loop iteration: submit / prefetch / egress / finish
+    phases = []          # every timed iteration's phases (ms): submit, prefetch, egress wait, finish
     pre = set()     # steps whose payload H2D is already queued (prefetch)
     lat_w = []      # (publish->deliver seconds, deliveries) of the timed steps
 
@@ -356,6 +357,7 @@ def main():
             tp.append(time.perf_counter())
             if measure:
                 ph = [round((b2 - a2) * 1e3, 3) for a2, b2 in zip(tp, tp[1:])]
+                phases.append(ph)
                 if sum(ph) > slow["ms"]:
                     slow.update(ms=round(sum(ph), 3), step=i, phases_ms=ph)
         for t, s in done:
@@ -461,6 +463,8 @@ def main():
                             "measures client-to-client over TCP)",
             "diag": errs,
             "slowest_iteration": slow,
+            "iteration_phases_ms_median": ([round(float(np.median([p[k] for p in phases if len(p) > k])), 4)
+                                            for k in range(max(len(p) for p in phases))] if phases else None),
             "host_us_per_step": {k: round(v * 1e6 / args.steps, 1) for k, v in dp.eng.host_times(False).items()},
             "egress": dp.eng.egress_stats(),
             "storm": ({"requeued_msgs": flow["requeued"], "flow_paused_steps": flow["paused_steps"]}

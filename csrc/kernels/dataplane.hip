@@ -549,11 +549,14 @@ DEV void frame_scan_seg(const DS& d, const u32 s) {
       d.seg_out[s] = so;
       d.seg_cmd_base[s] = INVALID;
       d.seg_npub[s] = 0;
+      d.seg_nack[s] = 0;
     }
     return;
   }
   if (L == 0) {
-    if (tid == 0) { d.carry_len[conn] = 0; d.seg_out[s] = so; d.seg_cmd_base[s] = INVALID; d.seg_npub[s] = 0; }
+    if (tid == 0) {
+      d.carry_len[conn] = 0; d.seg_out[s] = so; d.seg_cmd_base[s] = INVALID; d.seg_npub[s] = 0; d.seg_nack[s] = 0;
+    }
     return;
   }
   if (tid == 0) { sh_m = 0; sh_over = 0; }
@@ -939,11 +942,17 @@ DEV void frame_scan_seg(const DS& d, const u32 s) {
   }
   FS_MARK(6);
   const i64 now = d.in->now_ms;
-  u32 my_pubs = 0;
+  u32 npub_run = 0, nack_run = 0;   // the segment's publishes / acks so far (their ordinals)
   for (u32 f0 = 0; f0 < kf; f0 += FS_NT) {
     u32 f = f0 + tid;
     u32 is_cmd = 0, nfr = 0;
     u32 p = 0;
+    // every command's kind first: the publish / ack ordinals within the segment come out of
+    // the same block scan as the command index (no grid-wide rank scan over the commands)
+    Cmd c;
+    FInfo fi;
+    u32 cls = 0, mid = 0, hp = 0;
+    FInfo hi;
     if (f < kf) {
       p = CPOS(f);
       if (b[p] == 1) {
@@ -954,24 +963,12 @@ DEV void frame_scan_seg(const DS& d, const u32 s) {
         }
       }
     }
-    u32 tcnt, tf;
-    u32 r = block_scan<FS_NT>(is_cmd, sc, tcnt);
-    u32 fr = block_scan<FS_NT>(nfr, sc, tf);
     if (is_cmd) {
-      Cmd c;
-      FInfo fi = frame_at(b, p, L, fmax);
-      u32 cls = be16(b + p + 7), mid = be16(b + p + 9);
-      c.conn = conn;
-      c.ch = fi.ch;
-      c.m_off = wbase + p + 7;
-      c.m_len = fi.size;
-      c.h_off = 0; c.h_len = 0; c.frag0 = 0; c.nfrag = 0; c.body_size = 0;
-      c.seg = s;
-      c.raw_off = wbase + p;
-      i32 chs = fi.ch ? chan_lookup(d, conn, fi.ch) : -1;
+      fi = frame_at(b, p, L, fmax);
+      cls = be16(b + p + 7);
+      mid = be16(b + p + 9);
+      const i32 chs = fi.ch ? chan_lookup(d, conn, fi.ch) : -1;
       c.pad[0] = (u32)chs;
-      c.pad[1] = 0; c.pad[2] = 0;
-      u32 endp = p + 8 + fi.size;
       if (cls == 60 && mid == 40 && chs >= 0) c.kind = CK_PUBLISH;
       else if (cls == 60 && mid == 80 && chs >= 0) c.kind = CK_ACK;
       else if (cls == 60 && mid == 90 && chs >= 0) c.kind = CK_REJECT;
@@ -979,14 +976,36 @@ DEV void frame_scan_seg(const DS& d, const u32 s) {
       else c.kind = CK_CONTROL;
       if (c.kind != CK_CONTROL && d.ch_tx[chs]) c.kind = CK_TXBUF;   // held by the host until Tx.Commit
       if (cls == 60 && mid == 40) {
-        u32 hp = CPOS(f + 1);
-        FInfo hi = frame_at(b, hp, L, fmax);
-        c.h_off = wbase + hp + 7;
-        c.h_len = hi.size;
-        c.body_size = (u32)be64(b + hp + 7 + 4);
+        hp = CPOS(f + 1);
+        hi = frame_at(b, hp, L, fmax);
         // a publish too large for the carry is a control command: the host assembles it
         if ((c.kind == CK_PUBLISH || c.kind == CK_TXBUF) && big_publish(d, fi.size, hi.size, be64(b + hp + 7 + 4), fmax))
           c.kind = CK_CONTROL;
+      }
+    }
+    const u32 is_pub = is_cmd && c.kind == CK_PUBLISH;
+    const u32 is_ack = is_cmd && (c.kind == CK_ACK || c.kind == CK_NACK || c.kind == CK_REJECT);
+    // one scan of three 11-bit counters (<= FS_NT each per chunk): commands | pubs | acks
+    u32 tpk, tf;
+    const u32 rpk = block_scan<FS_NT>(is_cmd | (is_pub << 11) | (is_ack << 22), sc, tpk);
+    u32 fr = block_scan<FS_NT>(nfr, sc, tf);
+    const u32 r = rpk & 0x7ffu, tcnt = tpk & 0x7ffu;
+    if (is_cmd) {
+      c.conn = conn;
+      c.ch = fi.ch;
+      c.m_off = wbase + p + 7;
+      c.m_len = fi.size;
+      c.h_off = 0; c.h_len = 0; c.frag0 = 0; c.nfrag = 0; c.body_size = 0;
+      c.seg = s;
+      c.raw_off = wbase + p;
+      // ordinals within the segment: k_decode numbers publishes / acks segment-major
+      c.pad[1] = npub_run + ((rpk >> 11) & 0x7ffu);
+      c.pad[2] = nack_run + (rpk >> 22);
+      u32 endp = p + 8 + fi.size;
+      if (cls == 60 && mid == 40) {
+        c.h_off = wbase + hp + 7;
+        c.h_len = hi.size;
+        c.body_size = (u32)be64(b + hp + 7 + 4);
         c.frag0 = sh_frag_base + frun + fr;
         c.nfrag = nfr;
         endp = hp + 8 + hi.size;
@@ -1003,10 +1022,9 @@ DEV void frame_scan_seg(const DS& d, const u32 s) {
       c.raw_len = endp - p;
       const u32 ci = sh_cmd_base + run + r;
       d.cmds[ci] = c;
-      // classification for the publish / ack rank scans (fused k_classify)
-      d.cmd_is_pub[ci] = c.kind == CK_PUBLISH;
-      my_pubs += c.kind == CK_PUBLISH;
-      d.cmd_is_ack[ci] = c.kind == CK_ACK || c.kind == CK_NACK || c.kind == CK_REJECT;
+      // classification for the rank scan of the large-segment-count path (k_decode)
+      d.cmd_is_pub[ci] = is_pub;
+      d.cmd_is_ack[ci] = is_ack;
       if (c.kind == CK_CONTROL || c.kind == CK_TXBUF) {
         u32 cbase;
         u32 g = reserve_sat(&d.ctr->ctrl_bytes, c.raw_len, (u32)d.ctrl_cap, &cbase);
@@ -1025,16 +1043,15 @@ DEV void frame_scan_seg(const DS& d, const u32 s) {
     }
     run += tcnt;
     frun += tf;
+    npub_run += (tpk >> 11) & 0x7ffu;
+    nack_run += tpk >> 22;
   }
   if (tid == 0 && kf > 0) d.conn_last_rx[conn] = now;
   if (reason == 0) so.status |= SS_CTRL;
-  {   // the segment's publish count: k_decode numbers publishes in segment order
-    u32 np;
-    block_scan<FS_NT>(my_pubs, sc, np);
-    if (tid == 0) {
-      d.seg_cmd_base[s] = (run && sh_cmd_base != INVALID) ? sh_cmd_base : INVALID;
-      d.seg_npub[s] = d.seg_cmd_base[s] == INVALID ? 0u : np;
-    }
+  if (tid == 0) {   // the segment's publish / ack counts: k_decode numbers them segment-major
+    d.seg_cmd_base[s] = (run && sh_cmd_base != INVALID) ? sh_cmd_base : INVALID;
+    d.seg_npub[s] = d.seg_cmd_base[s] == INVALID ? 0u : npub_run;
+    d.seg_nack[s] = d.seg_cmd_base[s] == INVALID ? 0u : nack_run;
   }
 
   FS_MARK(7);
@@ -1065,8 +1082,7 @@ __global__ __launch_bounds__(FS_NT) void k_frame_scan(DS d) {
 }
 
 // ============================================================================ K3 classify / decode
-DEV void set_counts(const DS& d) {
-  u32 np = d.tot[4], na = d.tot[5];
+DEV void set_counts(const DS& d, u32 np, u32 na) {
   d.ctr->n_pubs = np < d.pub_max ? np : d.pub_max;
   d.ctr->n_acks = na < d.ack_max ? na : d.ack_max;
   // routing phase 0: the step's own publishes
@@ -1246,28 +1262,47 @@ DEV void apply_ack(const DS& d, Ack a, u32 ai) {
 // publishes are numbered in segment order (segment s's publishes follow those of the
 // segments before it), not in the order the frame-scan blocks reserved their commands:
 // queue order across connections is then deterministic (the golden model's order)
-#define DEC_SEG_LDS 4096
 __global__ __launch_bounds__(256) void k_decode(DS d) {
   __shared__ u32 spref[DEC_SEG_LDS];
+  __shared__ u32 sprefa[DEC_SEG_LDS];
   __shared__ u32 lds[256 / 64 + 1];
-  if (blockIdx.x == 0 && threadIdx.x == 0) set_counts(d);  // fused: counts + phase-0 range
-  {
-    u32 n0 = d.ctr->n_cmds;
-    if (blockIdx.x * 256 >= (n0 < d.cmd_max ? n0 : d.cmd_max)) return;   // whole block idle
-  }
   const u32 nseg = d.in->nseg;
   const bool seg_order = nseg <= DEC_SEG_LDS;
-  if (seg_order) {
-    u32 run = 0;
+  u32 n0 = d.ctr->n_cmds;
+  n0 = n0 < d.cmd_max ? n0 : d.cmd_max;
+  if (!d.rank_scan) {
+    // segment-major numbering from the frame scan's per-segment ordinals: every busy block
+    // (and block 0, which sets the step's counts) scans the segments' publish / ack counts
+    if (blockIdx.x != 0 && blockIdx.x * 256 >= n0) return;   // whole block idle
+    u32 run = 0, runa = 0;
     for (u32 b0 = 0; b0 < nseg; b0 += 256) {
       const u32 k = b0 + threadIdx.x;
-      const u32 v = k < nseg ? d.seg_npub[k] : 0;
-      u32 all;
+      const u32 v = k < nseg ? d.seg_npub[k] : 0, va = k < nseg ? d.seg_nack[k] : 0;
+      u32 all, alla;
       const u32 o = block_scan<256>(v, lds, all);
-      if (k < nseg) spref[k] = run + o;
+      const u32 oa = block_scan<256>(va, lds, alla);
+      if (k < nseg) { spref[k] = run + o; sprefa[k] = runa + oa; }
       run += all;
+      runa += alla;
     }
+    if (blockIdx.x == 0 && threadIdx.x == 0) set_counts(d, run, runa);   // fused: counts + phase-0 range
     __syncthreads();
+    if (blockIdx.x * 256 >= n0) return;
+  } else {
+    if (blockIdx.x == 0 && threadIdx.x == 0) set_counts(d, d.tot[4], d.tot[5]);
+    if (blockIdx.x * 256 >= n0) return;   // whole block idle
+    if (seg_order) {
+      u32 run = 0;
+      for (u32 b0 = 0; b0 < nseg; b0 += 256) {
+        const u32 k = b0 + threadIdx.x;
+        const u32 v = k < nseg ? d.seg_npub[k] : 0;
+        u32 all;
+        const u32 o = block_scan<256>(v, lds, all);
+        if (k < nseg) spref[k] = run + o;
+        run += all;
+      }
+      __syncthreads();
+    }
   }
   u32 i = blockIdx.x * blockDim.x + threadIdx.x;
   u32 n = d.ctr->n_cmds;
@@ -1276,9 +1311,14 @@ __global__ __launch_bounds__(256) void k_decode(DS d) {
   const Cmd c = d.cmds[i];
   const u8* w = d.work;
   if (c.kind == CK_PUBLISH) {
-    u32 pi = d.cmd_pub_rank[i];
-    if (seg_order && c.seg < nseg && d.seg_cmd_base[c.seg] != INVALID)
-      pi = spref[c.seg] + (pi - d.cmd_pub_rank[d.seg_cmd_base[c.seg]]);
+    u32 pi;
+    if (!d.rank_scan) {
+      pi = spref[c.seg] + c.pad[1];
+    } else {
+      pi = d.cmd_pub_rank[i];
+      if (seg_order && c.seg < nseg && d.seg_cmd_base[c.seg] != INVALID)
+        pi = spref[c.seg] + (pi - d.cmd_pub_rank[d.seg_cmd_base[c.seg]]);
+    }
     if (pi >= d.pub_max) return;
     Pub pb;
     pb.conn = c.conn;
@@ -1387,7 +1427,7 @@ __global__ __launch_bounds__(256) void k_decode(DS d) {
     pb.nwords = pb.rk_len <= 32 ? build_keyvec_win(d, rkw, pb.rk_len, pi) : build_keyvec(d, w + pb.rk_off, pb.rk_len, pi);
     d.pubs[pi] = pb;   // (its channel's confirm count: k_marks)
   } else if (c.kind == CK_ACK || c.kind == CK_NACK || c.kind == CK_REJECT) {
-    u32 ai = d.cmd_ack_rank[i];
+    const u32 ai = d.rank_scan ? d.cmd_ack_rank[i] : sprefa[c.seg] + c.pad[2];
     if (ai >= d.ack_max) return;
     Ack a;
     a.chslot = c.pad[0];

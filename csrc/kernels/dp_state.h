@@ -7,6 +7,7 @@
 #define CAND_MAX 8192         // frame candidates per segment held in LDS
 #define ID_WORKERS 64         // snowflake worker ids per GPU (K13)
 #define ID_SLOT_BITS 18       // log2(ID_WORKERS * 4096): id slots per millisecond
+#define DEC_SEG_LDS 4096      // k_decode: segment prefixes in LDS up to this many segments
 #define SORT_TILE 1024        // radix-sort tile (256 threads x 4): more tiles, more blocks in flight
 #define TOPIC_K 256           // topic key vector: 8 words x 32 hash bits (int8 +-1)
 #define TOPIC_WORDS 8
@@ -117,6 +118,8 @@ struct DS {
   u32* seg_total;
   u32* seg_cmd_base;        // first command of each segment (INVALID: none / overflowed)
   u32* seg_npub;            // publishes of each segment: publishes get segment-ordered indices
+  u32* seg_nack;            // acks / nacks / rejects of each segment (segment-ordered indices)
+  u32 rank_scan;            // 1: publish / ack indices from a grid-wide rank scan (seg_max > DEC_SEG_LDS)
   u8* work;
 
   // ---------------- commands

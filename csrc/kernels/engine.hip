@@ -282,6 +282,10 @@ class Engine {
     d_.seg_total = (u32*)dev("seg_total", 4ull * d_.seg_max);
     d_.seg_cmd_base = (u32*)dev("seg_cmd_base", 4ull * d_.seg_max);
     d_.seg_npub = (u32*)dev("seg_npub", 4ull * d_.seg_max);
+    d_.seg_nack = (u32*)dev("seg_nack", 4ull * d_.seg_max);
+    // up to DEC_SEG_LDS segments k_decode numbers publishes / acks from the frame scan's
+    // per-segment ordinals (segment prefix in LDS): no rank scan over the commands
+    d_.rank_scan = d_.seg_max > DEC_SEG_LDS ? 1u : 0u;
     d_.work = (u8*)dev("work", d_.work_cap + 4096);   // imports are read in place (k_import_route)
 
     d_.cmds = (Cmd*)dev("cmds", sizeof(Cmd) * (u64)d_.cmd_max);
@@ -495,6 +499,7 @@ class Engine {
     dup(&DS::seg_total, "seg_total", 4ull * d_.seg_max);
     dup(&DS::seg_cmd_base, "seg_cmd_base", 4ull * d_.seg_max);
     dup(&DS::seg_npub, "seg_npub", 4ull * d_.seg_max);
+    dup(&DS::seg_nack, "seg_nack", 4ull * d_.seg_max);
     dup(&DS::work, "work", d_.work_cap + 4096);
     dup(&DS::cmds, "cmds", sizeof(Cmd) * (u64)d_.cmd_max);
     dup(&DS::frags, "frags", sizeof(Frag) * ((u64)d_.frag_max + d_.import_max));
@@ -870,6 +875,7 @@ class Engine {
   // (the next submit, then the one after it).
   bool prefetch(u64 payload_ptr, u64 payload_len) {
     if (!overlap_ || !payload_len) return false;
+    Range rg("chanamq.step.prefetch");
     u64 tgt = seq_;
     int p = (int)(tgt & 1);
     if (pre_[p]) {   // the next submit's payload is queued already: the one after it
@@ -1886,8 +1892,9 @@ class Engine {
     // busy ones, and blocks past the step's segments would still be dispatched one by one
     // after them (the grid is sized for capacity at capture)
     hipLaunchKernelGGL(k_frame_scan, capped(d.seg_max, n_cu_), dim3(FS_NT), 0, s, d);
-    launch_scan(s, d, {{d.cmd_is_pub, d.cmd_pub_rank}, {d.cmd_is_ack, d.cmd_ack_rank}}, &d.ctr->n_cmds,
-                d.cmd_max, 4, nullptr, /*ingest=*/true);
+    if (d.rank_scan)
+      launch_scan(s, d, {{d.cmd_is_pub, d.cmd_pub_rank}, {d.cmd_is_ack, d.cmd_ack_rank}}, &d.ctr->n_cmds,
+                  d.cmd_max, 4, nullptr, /*ingest=*/true);
     hipLaunchKernelGGL(k_decode, blocks(d.cmd_max, 256), dim3(256), 0, s, d);
   }
 

@@ -86,6 +86,14 @@ for T in "$@"; do
     mkdir -p $O/trace_c$ch
     for f in $(find $O/t -name "*kernel_trace.csv" -o -name "*memory_copy_trace.csv"); do gzip -c $f > $O/trace_c$ch/$(basename $f).gz; done
     rm -rf $O/t ;;
+  trace_host)   # the trace above plus the host's roctx ranges (submit / prefetch / waits)
+    ch=${CHUNK:-32768}
+    timeout -k 10 240 rocprofv3 --kernel-trace --memory-copy-trace --marker-trace --output-format csv -d $O/th -o run -- \
+      python3 bench.py --steps 40 --warmup 5 --soak-s 0 --chunk $ch $BENCH_ARGS > $O/trace_host.log 2>&1
+    ok $? trace_host
+    mkdir -p $O/trace_host_c$ch
+    for f in $(find $O/th -name "*kernel_trace.csv" -o -name "*memory_copy_trace.csv" -o -name "*marker_api_trace.csv"); do gzip -c $f > $O/trace_host_c$ch/$(basename $f).gz; done
+    rm -rf $O/th ;;
   stats)
     timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $O/s -o run -- \
       python3 bench.py --steps 20 --warmup 5 --soak-s 0 $BENCH_ARGS > $O/stats.log 2>&1
