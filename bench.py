@@ -172,6 +172,9 @@ def main():
                     help="after the timed steps (and the result line), keep stepping untimed for this long so "
                          "an external GPU-utilisation sampler sees the workload (0 = off)")
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--loop", choices=["poll", "block"], default="poll",
+                    help="host loop: poll = submit as soon as a parity frees and stamp each egress when it "
+                         "lands (non-blocking queries); block = submit / prefetch / wait egress t-2 / finish t-1")
     ap.add_argument("--egress-gate", type=int, default=1, choices=[0, 1],
                     help="1: each step's egress D2H is queued on the SDMA engine at launch and started by the "
                          "step's last kernel (no host round trip); 0: issued by the host once it saw the step finish")
@@ -206,6 +209,8 @@ def main():
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world > 1:   # lockstep exchange steps: the blocking loop (every rank submits in step)
+        args.loop = "block"
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     import torch
@@ -312,6 +317,68 @@ def main():
                         lat_w.append((t - t0, int(lh[k])))
 
         end = step_i + n
+
+        def submit_next():
+            nonlocal step_i
+            b = step_i % args.blocks
+            if step_i not in pre:   # (a prefetched step's clock started when its bytes were queued)
+                sub_t[step_i] = time.perf_counter()
+            pre.discard(step_i)
+            if storm:   # ack-all each step, nack-all-requeue every 4th: a redelivery storm
+                cs = extra["nack" if step_i % 4 == 3 else "ack"][b]
+                if flow["paused"]:
+                    flow["paused_steps"] += 1
+                    sg = cs
+                else:
+                    sg = np.concatenate([segs[b], cs])
+            else:
+                sg = segs[b]
+            t = submit(sg, base + offs[b], blens[b])
+            s = step_i
+            step_i += 1
+            nxt = max(step_i, max(pre) + 1 if pre else step_i)
+            while args.prefetch and nxt < min(step_i + args.prefetch, end):
+                nb = nxt % args.blocks
+                sub_t[nxt] = time.perf_counter()
+                if not dp.prefetch(base + offs[nb], blens[nb]):
+                    break
+                pre.add(nxt)
+                nxt += 1
+            return t, s
+
+        if args.loop == "poll":
+            # the host never blocks on one thing while another is due: a parity frees ->
+            # submit the next step at once (its ingest overlaps the routing half in flight);
+            # an egress lands -> its deliveries are stamped when it does
+            from collections import deque
+            pq, dq = deque(), deque()
+            issued = 0
+            last = time.perf_counter()
+            while issued < n or pq or dq:
+                prog = False
+                if issued < n and len(pq) < 2:
+                    pq.append(submit_next())
+                    issued += 1
+                    prog = True
+                    if measure:
+                        now = time.perf_counter()
+                        phases.append([round((now - last) * 1e3, 4)])
+                        last = now
+                if pq and dp.step_done(pq[0][0]):
+                    t, s = pq.popleft()
+                    account(dp.finish(t, collect=False, wait_egress=False), s)
+                    dq.append((t, s))
+                    prog = True
+                while dq and dp.egress_done(dq[0][0]):
+                    t, s = dq.popleft()
+                    ready(s)
+                    prog = True
+                if not prog and issued == n and not pq:   # draining: block on the last egress
+                    t, s = dq.popleft()
+                    dp.egress_wait(t)
+                    ready(s)
+            return dl, pb, hist, eg
+
         for i in range(n):
             tp = [time.perf_counter()]   # host time per phase of this iteration (slowest kept)
             b = step_i % args.blocks

@@ -953,6 +953,14 @@ class GpuDataPlane(ControlState):
         io = self._io[ticket[0]]
         return self._egress[ticket[3]], io["conn_out"]
 
+    def step_done(self, ticket):
+        """Non-blocking: the step's kernels have finished (``finish`` will not wait)."""
+        return bool(self.eng.step_done(ticket[0]))
+
+    def egress_done(self, ticket):
+        """Non-blocking: the finished step's egress bytes are in host memory."""
+        return bool(self.eng.egress_done_slot(ticket[3]))
+
     def egress_wait(self, ticket):
         # by the slot the step rendered into (recorded at submit): a later step of the same
         # parity has its own slot, so waiting "by parity" would wait for the wrong copy

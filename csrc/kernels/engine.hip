@@ -1619,6 +1619,22 @@ class Engine {
     if (d2h_issued_[e]) HIPCHECK(hipEventSynchronize(ev_d2h_[e]));
   }
 
+  // non-blocking: the launched step of parity p has finished (its results are readable)
+  bool step_done(int p) {
+    if (!inflight_[p] || staged_[p] || phase_a_[p] || b_due_[p]) return !inflight_[p];
+    return hipEventQuery(ev_done_[p]) == hipSuccess;
+  }
+  // non-blocking: egress slot e's D2H (and tail) landed in host memory
+  bool egress_done_slot(int e) {
+    if (copy_mode_ == 3) {
+      if (sdma_pending_[e] && hsa_signal_load_scacquire(sdma_sig_[e]) != 0) return false;
+      if (tail_pending_[e] && hsa_signal_load_scacquire(tail_sig_[e]) != 0) return false;
+      sdma_pending_[e] = tail_pending_[e] = false;
+      return true;
+    }
+    return !d2h_issued_[e] || hipEventQuery(ev_d2h_[e]) == hipSuccess;
+  }
+
   void wait_results(int p) {
     HostTimer ht(&ht_[3]);
     Range rg("chanamq.step.wait_results");
@@ -2250,6 +2266,8 @@ PYBIND11_MODULE(_dataplane, m) {
       .def("egress_wait", &Engine::egress_wait)
       .def("egress_slot", &Engine::egress_slot)
       .def("egress_wait_slot", &Engine::egress_wait_slot)
+      .def("egress_done_slot", &Engine::egress_done_slot)
+      .def("step_done", &Engine::step_done)
       .def("sync", &Engine::sync)
       .def("c_api", &Engine::c_api)
       .def("xchg_setup", &Engine::xchg_setup, py::arg("kind"), py::arg("arg"), py::arg("members"),
