@@ -172,7 +172,11 @@ def main():
                     help="after the timed steps (and the result line), keep stepping untimed for this long so "
                          "an external GPU-utilisation sampler sees the workload (0 = off)")
     ap.add_argument("--no-graph", action="store_true")
-    ap.add_argument("--loop", choices=["poll", "block"], default="poll",
+    ap.add_argument("--overlap", type=int, default=1, choices=[0, 1],
+                    help="1: a step's ingest half on its own high-priority stream (it may run beside the "
+                         "previous step's routing half); 0: the whole step as one graph on one stream (no "
+                         "cross-queue hand-off between the halves)")
+    ap.add_argument("--loop", choices=["poll", "block"], default="block",
                     help="host loop: poll = submit as soon as a parity frees and stamp each egress when it "
                          "lands (non-blocking queries); block = submit / prefetch / wait egress t-2 / finish t-1")
     ap.add_argument("--egress-gate", type=int, default=1, choices=[0, 1],
@@ -252,7 +256,7 @@ def main():
                log_bytes=16 << 30, ring_pool=Q * qcap + qtot + 1024, tb_max=max(64, qtot) if not fan else 64,
                fan_max=max(1 << 20, qtot * 2), carry_cap=256 << 10, graph=0 if args.no_graph else 1,
                copy_engine={"blit": 0, "nocu": 1, "kernel": 2, "sdma": 3}[args.copy_engine], copy_wgs=args.copy_wgs, sdma_engine=args.sdma_engine,
-               sdma_split=args.sdma_split, egress_gate=args.egress_gate)
+               sdma_split=args.sdma_split, egress_gate=args.egress_gate, overlap=args.overlap)
     native = shards > 1 and args.xchg == "native"
     if native:
         dp = setup_native_exchange(args, cfg, GpuDataPlane, dist, backend, local, rank, world)

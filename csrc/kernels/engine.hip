@@ -607,7 +607,7 @@ class Engine {
     // from the recent steps' egress (a host-issued tail copies the rest when a step renders
     // more) -- the host is off the render -> D2H path.  0: the D2H is issued by the host
     // after it saw the step finish (egress_copy)
-    gated_ = copy_mode_ == 3 && overlap_ && get("egress_gate", 1) != 0;
+    gated_ = copy_mode_ == 3 && d_.world == 1 && get("egress_gate", 1) != 0;
     for (int p = 0; p < 2; ++p) {
       HIPCHECK(hipEventCreateWithFlags(&ev_h2d_[p], hipEventDisableTiming));
       HIPCHECK(hipEventCreateWithFlags(&ev_done_[p], hipEventDisableTiming));
@@ -874,7 +874,7 @@ class Engine {
   // Up to two steps ahead: each call queues the payload of the next step not yet queued
   // (the next submit, then the one after it).
   bool prefetch(u64 payload_ptr, u64 payload_len) {
-    if (!overlap_ || !payload_len) return false;
+    if (d_.world != 1 || !payload_len) return false;   // (s_pre_ is s_h2d_: the step waits for it)
     Range rg("chanamq.step.prefetch");
     u64 tgt = seq_;
     int p = (int)(tgt & 1);
@@ -965,19 +965,7 @@ class Engine {
       HIPCHECK(hipEventRecord(ev_rest_[p], s_comp_));
       rest_issued_[p] = true;
       HIPCHECK(hipEventRecord(ev_done_[p], s_comp_));
-      if (spec_[e]) {   // the egress D2H, queued now, starts when the step's last kernel opens the gate
-        Range rg("chanamq.K5.egress_gated");
-        hsa_signal_store_screlease(sdma_sig_[e], 1);
-        hsa_status_t st = hsa_amd_memory_async_copy_on_engine(egress_host_[e], cpu_agent_, egress_dev_[e], gpu_agent_,
-                                                              spec_[e], 1, &gate_sig_[e], sdma_sig_[e], sdma_engine_, true);
-        if (st != HSA_STATUS_SUCCESS) {
-          hsa_signal_store_screlease(sdma_sig_[e], 0);
-          throw std::runtime_error("hsa_amd_memory_async_copy_on_engine (gated egress) failed");
-        }
-        sdma_pending_[e] = true;
-        ++eg_stats_[0];
-        eg_stats_[2] += spec_[e];
-      }
+      gated_copy(e);
       if (copy_mode_ == 2) {   // egress D2H right behind the step, sized on the device
         // (measured slower than the host-issued SDMA copy -- CU stores over PCIe stall
         // behind the next step's kernels: 8.7 vs 32.9 M msgs/s, profiles/r4_bench/pre_*)
@@ -999,6 +987,11 @@ class Engine {
       HIPCHECK(hipGraphLaunch(graph_exec_[p], s_comp_));
     } else {
       launch_main(s_comp_, io_[p]);
+    }
+    if (d_.world == 1) {   // the ingress slot's last reader (a later prefetch into it waits for it)
+      const int is = (int)(launch_seq_[p] % INGRESS_SLOTS);
+      HIPCHECK(hipEventRecord(ev_ing_slot_[is], s_comp_));
+      ing_slot_issued_[is] = true;
     }
     if (d_.world > 1 && lag_) {
       HIPCHECK(hipEventRecord(ev_a_[p], s_comp_));
@@ -1032,6 +1025,7 @@ class Engine {
       counts_ready_[p] = true;
     } else {
       HIPCHECK(hipEventRecord(ev_done_[p], s_comp_));
+      gated_copy(e);   // (world 1, one stream: the whole step is one graph)
     }
   }
 
@@ -1617,6 +1611,22 @@ class Engine {
     HostTimer ht(&ht_[5]);
     if (copy_mode_ == 3) { sdma_wait(e); return; }
     if (d2h_issued_[e]) HIPCHECK(hipEventSynchronize(ev_d2h_[e]));
+  }
+
+  // the egress D2H of slot e, queued now: starts when the step's last kernel opens the gate
+  void gated_copy(int e) {
+    if (!spec_[e]) return;
+    Range rg("chanamq.K5.egress_gated");
+    hsa_signal_store_screlease(sdma_sig_[e], 1);
+    hsa_status_t st = hsa_amd_memory_async_copy_on_engine(egress_host_[e], cpu_agent_, egress_dev_[e], gpu_agent_,
+                                                          spec_[e], 1, &gate_sig_[e], sdma_sig_[e], sdma_engine_, true);
+    if (st != HSA_STATUS_SUCCESS) {
+      hsa_signal_store_screlease(sdma_sig_[e], 0);
+      throw std::runtime_error("hsa_amd_memory_async_copy_on_engine (gated egress) failed");
+    }
+    sdma_pending_[e] = true;
+    ++eg_stats_[0];
+    eg_stats_[2] += spec_[e];
   }
 
   // non-blocking: the launched step of parity p has finished (its results are readable)
