@@ -493,6 +493,40 @@ DEV bool big_publish(const DS& d, u32 msize, u32 hsize, u64 bsz, u32 fmax) {
   return (u64)msize + 8 + hsize + 8 + bsz + 8 * nb > d.carry_cap;
 }
 
+// bytes [sh, sh + 16) of the 32 bytes a:b (sh 0..15): four dword funnel shifts
+DEV uint4 shift_pair(uint4 a, uint4 b, u32 sh) {
+  const u32 w[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+  const u32 q = sh >> 2, r = sh & 3;
+  u32 o[4];
+#pragma unroll
+  for (u32 i = 0; i < 4; ++i) {
+    // (selects over the eight words: q is wave-uniform only per segment)
+    const u32 lo = q == 0 ? w[i] : q == 1 ? w[i + 1] : q == 2 ? w[i + 2] : w[i + 3];
+    const u32 hi = q == 0 ? w[i + 1] : q == 1 ? w[i + 2] : q == 2 ? w[i + 3] : w[i + 4];
+    o[i] = r ? __builtin_amdgcn_alignbyte(hi, lo, r) : lo;
+  }
+  return make_uint4(o[0], o[1], o[2], o[3]);
+}
+// word c (bytes [16c, 16c + 16)) of a segment = the connection's carry (cl bytes, C
+// 16-aligned) then its new ingress bytes (N 16-aligned; reading up to 32 bytes past them
+// stays inside the ingress slot's slack); bytes past the segment are don't-care
+DEV uint4 seg_word(const u8* C, u32 cl, const u8* N, u32 c) {
+  const u32 b0 = c * 16;
+  if (b0 + 16 <= cl) return *(const uint4*)(C + b0);
+  if (b0 >= cl) {
+    const u32 o = b0 - cl, k = o >> 4, sh = o & 15;
+    const uint4 a = ((const uint4*)N)[k];
+    return sh ? shift_pair(a, ((const uint4*)N)[k + 1], sh) : a;
+  }
+  u32 v[4] = {0, 0, 0, 0};   // the word holding the carry's end and the new bytes' start
+  for (u32 j = 0; j < 16; ++j) {
+    const u32 i = b0 + j;
+    const u32 x = i < cl ? C[i] : N[i - cl];
+    v[j >> 2] |= x << (8 * (j & 3));
+  }
+  return make_uint4(v[0], v[1], v[2], v[3]);
+}
+
 DEV void frame_scan_seg(const DS& d, const u32 s) {
   __shared__ uint4 fs_pool[FS_POOL / 16];
   __shared__ u32 sc[FS_NT / 64 + 1];
@@ -524,14 +558,20 @@ DEV void frame_scan_seg(const DS& d, const u32 s) {
   const u32 fmax = d.conn_frame_max[conn];
   const u32 wbase = d.seg_start[s];
   FS_MARK(15);
-  if (d.tot[15] <= d.work_cap) {
+  const u32 seg_len = d.segs[s].len, seg_cl = L - seg_len;
+  const u8* const seg_C = d.carry + (u64)conn * d.carry_cap;
+  const u8* const seg_N = (const u8*)d.in->ingress + d.segs[s].src;
+  // the common segment is copied into the work buffer by the screen pass itself: one read
+  // of the sources, the work copy, the LDS stage and the candidate mask from the same
+  // registers (was: a copy pass, then the screen re-reading the copy)
+  const bool fit = d.tot[15] <= d.work_cap;
+  const bool fuse = fit && L > 0 && ((L + 15) >> 4) <= FS_AM_MAX && !d.conn_paused[conn];
+  if (fit && !fuse) {
     // the segment into the work buffer (fused k_stage copy): the connection's carry, then
-    // its new ingress bytes.  k_decode / k_route_store read publishes from there; the
-    // screen below reads it back while it is hot in L2 and stages it in LDS
-    const u32 len = d.segs[s].len, cl = L - len;
+    // its new ingress bytes.  k_decode / k_route_store read publishes from there
     u8* const dst = d.work + wbase;
-    if (cl) block_copy(dst, d.carry + (u64)conn * d.carry_cap, cl, tid, FS_NT);
-    if (len) block_copy(dst + cl, (const u8*)d.in->ingress + d.segs[s].src, len, tid, FS_NT);
+    if (seg_cl) block_copy(dst, seg_C, seg_cl, tid, FS_NT);
+    if (seg_len) block_copy(dst + seg_cl, seg_N, seg_len, tid, FS_NT);
   }
   __threadfence_block();
   __syncthreads();
@@ -577,12 +617,16 @@ DEV void frame_scan_seg(const DS& d, const u32 s) {
     const u32 fmg = d.frame_max_global;
     if (use_am) {   // candidate screen of the segment into LDS (fused k_cand), coalesced reads
       const uint4* W = (const uint4*)bg;   // 16-aligned; >= 32 bytes of padding after the segment
+      uint4* const WD = (uint4*)(d.work + wbase);
       for (u32 cc = tid; cc < nm; cc += FS_NT * 4) {
         uint4 x[4], y[4];
 #pragma unroll
         for (int k = 0; k < 4; ++k) {   // every load of the batch in flight before any use
           const u32 c = cc + k * FS_NT;
-          if (c < nm) { x[k] = W[c]; y[k] = W[c + 1]; }
+          if (c < nm) {
+            if (fuse) { x[k] = seg_word(seg_C, seg_cl, seg_N, c); y[k] = seg_word(seg_C, seg_cl, seg_N, c + 1); }
+            else { x[k] = W[c]; y[k] = W[c + 1]; }
+          }
         }
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
@@ -590,9 +634,11 @@ DEV void frame_scan_seg(const DS& d, const u32 s) {
           if (c < nm) {
             amask[c] = (u16)cand_bits(x[k], y[k], fmg);
             if (staged) fs_stage[c] = x[k];
+            if (fuse) WD[c] = x[k];
           }
         }
       }
+      if (fuse && !staged) __threadfence_block();   // the later phases read the work copy
       if (staged && tid < 2) fs_stage[nm + tid] = make_uint4(0, 0, 0, 0);   // the screen's read-ahead
       __syncthreads();
       if (staged) b = (const u8*)fs_stage;
