@@ -112,8 +112,32 @@ def stop_pollers(p):
     return [tuple(x) for x in json.loads(lines[-1])] if lines else []
 
 
+def churn_start(port, conn_threads=4, cons_threads=4):
+    """Connection open/close and consume/cancel churn in its own process (bench/churn_client.py)."""
+    import subprocess
+    p = subprocess.Popen([sys.executable, os.path.join(os.path.dirname(os.path.abspath(__file__)), "churn_client.py"),
+                          "--port", str(port), "--conn-threads", str(conn_threads), "--cons-threads", str(cons_threads)],
+                         stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True)
+    line = p.stdout.readline()
+    if line.strip() != "ready":
+        p.kill()
+        raise RuntimeError(f"churn client failed to start: {line!r}")
+    return p
+
+
+def churn_stop(p):
+    import subprocess
+    try:
+        out, _ = p.communicate("", timeout=60)
+    except subprocess.TimeoutExpired:
+        p.kill()
+        return {"error": "churn client did not stop"}
+    lines = [x for x in out.splitlines() if x.startswith("{")]
+    return json.loads(lines[-1]) if lines else {"error": "no churn result"}
+
+
 def run_one(core, name, spec, io, io_threads, seconds, rate=0.0, lg_threads=12, store_dir=None, cons_threads=8,
-            n_getters=0):
+            n_getters=0, churn=None):
     from chanamq_amd.server.gpu_broker import GpuBroker
     persist = bool(spec.get("persistent"))
     plane = plane_for(spec)
@@ -145,7 +169,14 @@ def run_one(core, name, spec, io, io_threads, seconds, rate=0.0, lg_threads=12, 
     gout, gproc = [], None
     if n_getters:
         gproc = get_pollers(b.port, n_getters)
+    cproc, cout = None, None
+    if churn:
+        cproc = churn_start(b.port, *churn)
+    st0 = dict(b.stats)
     try:
+        if cproc is not None:
+            cproc.stdin.write("go\n")
+            cproc.stdin.flush()
         r = core.run_load(dict(port=b.port, seconds=seconds, warmup=1.0, queue=f"e2e.{name}",
                                exchange=f"e2e.x.{name}", threads=lg_threads, consumer_threads=cons_threads,
                                rate=rate, **spec))
@@ -153,6 +184,9 @@ def run_one(core, name, spec, io, io_threads, seconds, rate=0.0, lg_threads=12, 
         done[0] = True
         if gproc is not None:
             gout = stop_pollers(gproc)
+        if cproc is not None:
+            cout = churn_stop(cproc)
+        st1 = dict(b.stats)
         smp.join()
         cpu1 = thread_cpu()
         after = {}
@@ -228,6 +262,8 @@ def run_one(core, name, spec, io, io_threads, seconds, rate=0.0, lg_threads=12, 
                            gets_per_s=sum(g[0] + g[1] for g in gout) / max(1e-9, max((g[2] for g in gout), default=1)),
                            device_gets=st.get("device_gets", 0)) if n_getters else None),
              last_step={k: lc.get(k) for k in ("n_ring_full", "n_dropped_nomem")},
+             churn=cout,
+             control_sections={k: st1.get(k, 0) - st0.get(k, 0) for k in ("pauses", "light_sections")},
              store=getattr(b, "_pw_stats", None), body_log=body_log)
     del plane
     return r
@@ -355,6 +391,10 @@ def main():
                     help="bytes per confirm-mode connection per step (0 = the broker default, 128 KiB)")
     ap.add_argument("--persist-group-ms", type=float, default=2.0,
                     help="durable specs: a group commit waits until its oldest batch is this old")
+    ap.add_argument("--churn", action="store_true",
+                    help="paced runs again next to connection open/close and consume/cancel churn "
+                         "(bench/churn_client.py): delivered rate and latency with and without it")
+    ap.add_argument("--churn-threads", default="4,4", help="connection,consumer churn threads")
     ap.add_argument("--getters", type=int, default=0,
                     help="also run each spec with this many Basic.Get pollers on pre-filled queues (the load's "
                          "throughput with and without them, and the gets/s)")
@@ -440,7 +480,17 @@ def main():
                     results.append(rp)
                     print(json.dumps({k: rp[k] for k in ("name", "io", "io_threads", "rate_per_producer",
                                                          "recv_msgs_per_s", "p50_us", "p95_us", "p99_us",
-                                                         "error")}), flush=True)
+                                                         "error", "control_sections")}), flush=True)
+                    if args.churn:
+                        ct = tuple(int(x) for x in args.churn_threads.split(","))
+                        rc = run_one(core, name, spec, io, nt, args.seconds, rate=rate, lg_threads=args.loadgen_threads,
+                                     cons_threads=args.consumer_threads, churn=ct)
+                        rc["paced_fraction"] = args.paced
+                        rc["delivered_vs_no_churn"] = rc["recv_msgs_per_s"] / max(1e-9, rp["recv_msgs_per_s"])
+                        results.append(rc)
+                        print(json.dumps({k: rc[k] for k in ("name", "io_threads", "rate_per_producer", "recv_msgs_per_s",
+                                                             "delivered_vs_no_churn", "p50_us", "p95_us", "p99_us",
+                                                             "error", "churn", "control_sections")}), flush=True)
     if args.out:
         import platform
         with open(args.out, "w") as f:

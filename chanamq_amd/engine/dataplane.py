@@ -123,13 +123,38 @@ class GpuDataPlane(ControlState):
                          shard_map=shard_map)
 
     # ================================================================== uploads
+    # ``defer`` (set by the broker around control work done while steps keep running): table
+    # writes are staged in the engine and ridden by the next submitted step -- applied by
+    # its first kernel before it reads anything -- instead of synchronous copies that need
+    # the pipeline drained.  Device reads are refused meanwhile (the state they would see
+    # is neither before nor after the staged writes).
+    defer = False
+
+    def _write(self, name, a, offset):
+        if self.defer:
+            self.eng.stage_write(name, a, offset)
+        else:
+            self.eng.upload(name, a, offset)
+
+    def _quiet(self, what):
+        if self.defer:
+            raise RuntimeError(f"{what}: a device read while control writes are deferred")
+
+    def flush_deltas(self):
+        """Apply the staged control writes now (the caller holds the engine: no step in flight)."""
+        self.eng.flush_deltas()
+
+    def deltas_pending(self):
+        """(records, bytes, channels to mark) staged and not yet taken by a step."""
+        return tuple(self.eng.deltas_pending())
+
     def _up(self, name, arr, index=0):
         a = np.ascontiguousarray(arr)
-        self.eng.upload(name, a, index * a.itemsize if a.ndim else index * a.itemsize)
+        self._write(name, a, index * a.itemsize if a.ndim else index * a.itemsize)
 
     def _up_at(self, name, value, index, dtype):
         a = np.array([value], dtype=dtype)
-        self.eng.upload(name, a, index * a.itemsize)
+        self._write(name, a, index * a.itemsize)
 
     def routing_changed(self):
         i = self.info
@@ -238,7 +263,7 @@ class GpuDataPlane(ControlState):
                     if row[s] == 0:
                         row[s] = (ch << 16) | 0x8000 | chan.local
                         break
-        self.eng.upload("chmap", row, conn * size * 4)
+        self._write("chmap", row, conn * size * 4)
 
     def connection_changed(self, conn):
         c = self.conns.get(conn)
@@ -285,6 +310,9 @@ class GpuDataPlane(ControlState):
         c.channels[chan.ch] = saved
 
     def _mark_dirty(self, chslot):
+        if self.defer:   # the step's first kernel puts it on the dirty list (device atomics)
+            self.eng.stage_mark_dirty(int(chslot))
+            return
         flag = np.frombuffer(self.eng.download("ch_dirty", chslot * 4, 4), np.uint32)[0]
         if flag:
             return
@@ -329,7 +357,7 @@ class GpuDataPlane(ControlState):
             self._up_at("cons_tag_off", cid * 256, cid, np.uint32)
             self._up_at("cons_tag_len", len(tag), cid, np.uint32)
             if tag:
-                self.eng.upload("tpool", np.frombuffer(tag, np.uint8), cid * 256)
+                self._write("tpool", np.frombuffer(tag, np.uint8), cid * 256)
         else:
             self._up_at("cons_active", 0, cid, np.uint32)
         self._sync_consumers()
@@ -349,6 +377,7 @@ class GpuDataPlane(ControlState):
 
     # ---- host-side queue/channel ops between steps (the plane is idle: step() is synchronous)
     def _u64(self, name, idx):
+        self._quiet(name)
         return int(np.frombuffer(self.eng.download(name, idx * 8, 8), np.uint64)[0])
 
     # ---- persistence (engine built with persist=1)
@@ -473,6 +502,7 @@ class GpuDataPlane(ControlState):
     def take_carry(self, conn):
         """The bytes the device holds for a paused connection (its carry: the frames after
         a command the host took over), removed from the device."""
+        self._quiet("carry")
         n = int(np.frombuffer(self.eng.download("carry_len", 4 * conn, 4), np.uint32)[0])
         data = bytes(self.eng.download("carry", conn * self.info["carry_cap"], n)) if n else b""
         self._up_at("carry_len", 0, conn, np.uint32)

@@ -33,7 +33,7 @@ USLOT = np.dtype([("state", "<u4"), ("msg", "<u4"), ("q", "<u4"), ("cons", "<u4"
 US_FREE, US_PENDING, US_ACKED, US_REQUEUE, US_DONE = 0, 1, 2, 3, 4
 CTRL_TXBUF = 0x80000000     # CtrlRec.seg: data command of a transactional channel (low bits = position)
 
-STRUCT_SIZES = {"SegIn": 16, "SegOut": 32, "CtrlRec": 16, "ConnOut": 8, "StepIn": 72, "RDesc": 64, "USlot": 32}
+STRUCT_SIZES = {"SegIn": 16, "SegOut": 32, "CtrlRec": 16, "ConnOut": 8, "StepIn": 80, "RDesc": 64, "USlot": 32}
 assert RDESC.itemsize == 64
 
 # SegOut.status bits

@@ -72,24 +72,83 @@ GS_EMPTY, GS_OK, GS_RETRY, GS_NO_SPACE, GS_WINDOW_FULL, GS_GONE = range(6)   # s
 
 class _PlaneLock:
     """Exclusive access to the data plane's device tables.  With the pipelined front end
-    the outermost acquisition pauses its stepper (steps in flight finished, their egress
-    written) and the release resumes it."""
+    the outermost full acquisition pauses its stepper (steps in flight finished, their
+    egress written) and the release resumes it.
+
+    ``light`` sections (``_LightLock``) share the lock but do not pause: the control work
+    inside them only writes connection / channel / consumer tables, which the plane stages
+    (``GpuDataPlane.defer``) for the next step's first kernel; their replies go out behind
+    the egress of the steps that were in flight (``Frontend.send_after``).  A full section
+    nested in a light one pauses then, and first applies what the light one staged."""
 
     def __init__(self, broker):
         self.b, self.rl, self.depth = broker, threading.RLock(), 0
+        self.paused_at = 0   # depth of the acquisition that paused the stepper (0: running)
+        self.light = 0       # open light sections
+
+    def _defer(self, on):
+        if hasattr(self.b.plane, "eng"):
+            self.b.plane.defer = on
+
+    @property
+    def deferring(self):
+        return self.light > 0 and not self.paused_at
 
     def __enter__(self):
         self.rl.acquire()
         self.depth += 1
-        if self.depth == 1 and self.b.fe is not None:
+        if not self.paused_at and self.b.fe is not None:
+            self.b.stats["pauses"] = self.b.stats.get("pauses", 0) + 1
             self.b.fe.pause()
+            self.paused_at = self.depth
+            self._defer(False)
+            if hasattr(self.b.plane, "flush_deltas"):   # what light sections staged, applied now
+                self.b.plane.flush_deltas()
+            if hasattr(self.b.fe, "flush_ctl"):          # and the replies held behind it written
+                self.b.fe.flush_ctl()
         return self
 
     def __exit__(self, *exc):
-        self.depth -= 1
-        if self.depth == 0 and self.b.fe is not None:
+        if self.paused_at == self.depth:
             self.b.fe.resume()
+            self.paused_at = 0
+            if self.light:
+                self._defer(True)
+        self.depth -= 1
         self.rl.release()
+
+
+class _LightLock:
+    """A control section that leaves the steps running (see ``_PlaneLock``)."""
+
+    def __init__(self, lock):
+        self.l = lock
+
+    def __enter__(self):
+        lk = self.l
+        lk.rl.acquire()
+        lk.depth += 1
+        lk.light += 1
+        if not lk.paused_at:
+            lk._defer(True)
+            lk.b.stats["light_sections"] = lk.b.stats.get("light_sections", 0) + 1
+        return self
+
+    def __exit__(self, *exc):
+        lk = self.l
+        lk.light -= 1
+        if not lk.light and not lk.paused_at:
+            lk._defer(False)
+            if lk.b.fe is not None:
+                lk.b.fe.wake()   # the staged writes ride the next step
+        lk.depth -= 1
+        lk.rl.release()
+
+
+# control commands that only touch connection / channel / consumer tables: handled while
+# the steps keep running (their table writes ride the next step)
+_LIGHT_METHODS = {(10, 50), (10, 51), (20, 10), (20, 20), (20, 21), (20, 40), (20, 41), (30, 10), (60, 10),
+                  (60, 20), (60, 30), (85, 10)}
 
 
 class _Hard(Exception):
@@ -232,6 +291,7 @@ class GpuBroker:
         self._wake_r, self._wake_w = os.pipe()
         self.stats = dict(steps=0, published=0, delivered=0, connections=0)
         self.lock = _PlaneLock(self)
+        self.light = _LightLock(self.lock)
 
     # ------------------------------------------------------------------ lifecycle
     def start(self):
@@ -360,9 +420,14 @@ class GpuBroker:
             persist = [e for e in evs if e[0] == FE_PERSIST]
             dev = self._fast_events([e for e in evs if e[0] != FE_PERSIST])
             if dev or self._tx_pending:
-                with self.lock:
+                light = not self._tx_pending and self._light_ok(dev)
+                with (self.light if light else self.lock):
                     while dev or (self._tx_pending and self.node is None):
-                        self._handle_fe(dev)
+                        if light and not self._light_ok(dev):
+                            with self.lock:   # a command that needs the device drained
+                                self._handle_fe(dev)
+                        else:
+                            self._handle_fe(dev)
                         if self.node is not None:   # sharded: injected into the lockstep steps
                             self._tx_inject()
                         while self._tx_pending and self.node is None:   # committed transactions:
@@ -381,6 +446,53 @@ class GpuBroker:
                 self._sync_fe_stats()
                 self._watermarks()
                 self._flush_all()
+
+    # ------------------------------------------------------------------ light control sections
+    def _light_capable(self):
+        return (self.fe is not None and self.node is None and self.persistence is None
+                and hasattr(self.plane, "eng") and hasattr(self.fe, "send_after") and not self._links)
+
+    def _close_light(self, c):
+        """A connection whose close only releases connection / channel / consumer rows."""
+        return not any(q.exclusive_owner == c.id for q in self.plane.queues.values())
+
+    def _plock(self):
+        """The lock for a light-safe operation: light inside a light section, else full."""
+        return self.light if self.lock.deferring else self.lock
+
+    def _light_ok(self, evs):
+        """Whether this batch of front-end events can be handled with the steps running:
+        handshakes, channel / consumer / QoS / confirm commands and plain closes; anything
+        that reads device state or changes queues, exchanges or bindings needs the drain."""
+        if not self._light_capable():
+            return False
+        n, nb, nd = self.plane.deltas_pending()
+        if n > 256 or nb > (1 << 20) or nd > 1024:   # a change set must fit one step's delta buffer
+            return False
+        for kind, conn, a, b, data, data2 in evs:
+            if kind in (FE_OPEN, FE_GET, FE_EVENT, FE_STATUS, FE_TXBUF):
+                continue
+            c = self.conns.get(conn)
+            if kind == FE_CLOSED:
+                if c is not None and c.state == "open" and not self._close_light(c):
+                    return False
+            elif kind == FE_HOST:
+                if c is not None and (c.state not in ("header", "start", "tune", "closing") or c.big is not None):
+                    return False
+            elif kind == FE_CTRL:
+                if c is None or c.state != "open" or len(data) < 11:
+                    continue
+                ch = struct.unpack_from(">H", data, 1)[0]
+                if ch in c.closing_channels:
+                    continue
+                key = struct.unpack_from(">HH", data, 7)
+                if data[0] != C.FRAME_METHOD or key not in _LIGHT_METHODS:
+                    return False
+                if key == (10, 50) and not self._close_light(c):
+                    return False
+            else:
+                return False
+        return True
 
     def _fast_events(self, dev):
         """Basic.Get traffic without pausing the stepper: a Get on a local queue is staged
@@ -453,7 +565,7 @@ class GpuBroker:
                 was_open = c.state == "open"
                 rest = self._host_bytes(c, data)
                 if c.state == "open" and not was_open:
-                    self._flush(c)
+                    self._flush(c, direct=True)   # Connection.OpenOk: no device traffic yet
                     self.fe.set_heartbeat(conn, c.heartbeat)
                     self.fe.set_data_mode(conn, rest)
             elif kind == FE_CTRL:
@@ -827,7 +939,7 @@ class GpuBroker:
                 vh = normalize_vhost(m.virtual_host)
                 if vh not in self.plane.vhosts:
                     raise _Hard(C.NOT_FOUND, f"no vhost '{vh}'", 10, 40)
-                with self.lock:
+                with self._plock():
                     self.plane.open_connection(c.id, vh, c.frame_max)
                 self._send(c, 0, Method("connection.open_ok"))
                 c.state = "open"
@@ -961,7 +1073,8 @@ class GpuBroker:
             ch = struct.unpack_from(">H", raw, 1)[0]
             if (conn, ch) in self._txbuf:
                 self._txbuf[(conn, ch)].append(raw)
-        self._watermarks()
+        if not self.lock.deferring:   # (tier upkeep reads the device: outside light sections)
+            self._watermarks()
         self.stats["steps"] += 1
         self.stats["published"] += cnt.get("n_pubs", 0)
         self.stats["delivered"] += cnt.get("n_deliv", 0)
@@ -1285,7 +1398,7 @@ class GpuBroker:
     def _connection_method(self, c, m):
         if m.name == "connection.close":
             self._send(c, 0, Method("connection.close_ok"))
-            self._flush(c)
+            self._flush(c, direct=True)   # the connection's last bytes (fe.close follows)
             self._drop(c)
         elif m.name == "connection.close_ok":
             self._drop(c)
@@ -1746,11 +1859,16 @@ class GpuBroker:
                 self.fe.set_host_mode(c.id)
         c.state = "closing"
 
-    def _flush(self, c):
+    def _flush(self, c, direct=False):
         if not c.out or c.state == "closed":
             return
         if self.fe is not None:
-            self.fe.send(c.id, bytes(c.out))
+            if self.lock.deferring and c.state == "open" and not direct:
+                # behind the deliveries of the steps in flight and the step carrying this
+                # command's table writes
+                self.fe.send_after(c.id, bytes(c.out))
+            else:
+                self.fe.send(c.id, bytes(c.out))
             c.out.clear()
             c.last_tx = time.monotonic()
             return
@@ -1880,7 +1998,8 @@ class GpuBroker:
             if prev != "gone":
                 self._flush(c)
             if prev == "open" or c.id in self.plane.conns:
-                with self.lock:
+                light = self.lock.deferring or (self._light_capable() and self._close_light(c))
+                with (self.light if light and self._close_light(c) else self.lock):
                     self.plane.close_connection(c.id)
             self.conns.pop(c.id, None)
             self.fe.close(c.id)

@@ -249,6 +249,13 @@ PYBIND11_MODULE(_core, m) {
              py::gil_scoped_release nogil;
              f.send(conn, s.data(), s.size());
            })
+      .def("send_after", [](Frontend& f, uint32_t conn, py::bytes b) {
+             std::string s = b;
+             py::gil_scoped_release nogil;
+             f.send_after(conn, s.data(), s.size());
+           })
+      .def("wake", &Frontend::wake)
+      .def("flush_ctl", &Frontend::flush_ctl, py::call_guard<py::gil_scoped_release>())
       .def("send_egress", [](Frontend& f, py::buffer egress, py::buffer conn_out, uint32_t n_slots) {
              py::buffer_info e = egress.request(), c = conn_out.request();
              if ((uint64_t)c.size * c.itemsize < 8ull * n_slots) throw std::runtime_error("conn_out too small");

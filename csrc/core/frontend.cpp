@@ -317,6 +317,73 @@ void Frontend::send(u32 conn, const char* data, size_t n) {
   write_some(c);
 }
 
+void Frontend::send_after(u32 conn, const char* data, size_t n) {
+  if (conn >= c_max_ || !n) return;
+  {
+    std::lock_guard<std::mutex> g(ctl_mu_);
+    // behind the steps in flight and the next one, which carries the control writes the
+    // command staged (Engine::pack_deltas): the reply never overtakes its own table changes
+    ctl_out_.push_back(CtlOut{sub_step_.load() + 1, conn, conns_[conn]->gen.load(), std::string(data, n)});
+  }
+  wake_stepper();
+}
+
+// (control plane, stepper paused, staged writes applied) every held reply goes out now,
+// in order, behind the egress the pause already wrote
+void Frontend::flush_ctl() {
+  std::deque<CtlOut> go;
+  {
+    std::lock_guard<std::mutex> g(ctl_mu_);
+    go.swap(ctl_out_);
+  }
+  for (auto& o : go)
+    if (o.gen == conns_[o.conn]->gen.load()) send(o.conn, o.data.data(), o.data.size());
+}
+
+// a held reply waits for a step not submitted yet: the stepper must submit one
+bool Frontend::ctl_needs_step() {
+  std::lock_guard<std::mutex> g(ctl_mu_);
+  return !ctl_out_.empty() && ctl_out_.back().after > sub_step_.load();
+}
+
+void Frontend::wake() { wake_stepper(); }
+
+bool Frontend::ctl_pending() {
+  std::lock_guard<std::mutex> g(ctl_mu_);
+  return !ctl_out_.empty();
+}
+
+// (stepper) control replies whose steps have all finished go out behind those steps'
+// egress: one Scatter at the end of this IO phase's list, in reply order per connection
+void Frontend::release_ctl() {
+  std::vector<CtlOut> go;
+  {
+    std::lock_guard<std::mutex> g(ctl_mu_);
+    const u64 fin = fin_step_.load();
+    // held (write-behind) steps not yet released keep every reply behind them
+    while (!ctl_out_.empty() && ctl_out_.front().after <= fin && held_.empty()) {
+      go.push_back(std::move(ctl_out_.front()));
+      ctl_out_.pop_front();
+    }
+  }
+  if (go.empty()) return;
+  Scatter sc;
+  sc.co.assign(c_max_, ConnOut{0, 0});
+  sc.gen.assign(c_max_, 0);
+  for (u32 c = 0; c < c_max_; ++c) sc.gen[c] = conns_[c]->gen.load();
+  // per connection contiguous (its replies keep their order)
+  std::vector<std::vector<size_t>> by(c_max_);
+  for (size_t k = 0; k < go.size(); ++k) by[go[k].conn].push_back(k);
+  for (u32 c = 0; c < c_max_; ++c) {
+    if (by[c].empty()) continue;
+    const u32 off = (u32)sc.own.size();
+    for (size_t k : by[c])
+      if (go[k].gen == sc.gen[c]) sc.own += go[k].data;   // (a closed connection's: dropped)
+    sc.co[c] = ConnOut{off, (u32)sc.own.size() - off};
+  }
+  if (!sc.own.empty()) out_.push_back(std::move(sc));
+}
+
 void Frontend::send_egress(const u8* egress, const ConnOut* co, u32 n_slots) {
   for (u32 i = 0; i < n_slots && i < c_max_; ++i)
     if (co[i].len) send(i, (const char*)egress + co[i].off, co[i].len);
@@ -541,6 +608,11 @@ void Frontend::accept_all(FeIo& io0) {
     u32 id = 0;
     {
       std::lock_guard<std::mutex> g(free_mu_);
+      const u64 fin = fin_step_.load();
+      while (!quarantine_.empty() && quarantine_.front().first <= fin) {
+        free_.push_back(quarantine_.front().second);
+        quarantine_.pop_front();
+      }
       if (!free_.empty()) { id = free_.back(); free_.pop_back(); }
     }
     if (!id) { ::close(fd); continue; }
@@ -688,8 +760,9 @@ void Frontend::io_loop(int i) {
       c.in_ready = false;
       io.owned.erase(std::remove(io.owned.begin(), io.owned.end(), id), io.owned.end());
       io.ready.erase(std::remove(io.ready.begin(), io.ready.end(), id), io.ready.end());
+      // reusable once the steps in flight now have finished (their results name this slot)
       std::lock_guard<std::mutex> g(free_mu_);
-      free_.push_back(id);
+      quarantine_.emplace_back(sub_step_.load(), id);
     }
     // ---- socket events
     bool data_ready = false;
@@ -1080,6 +1153,7 @@ void Frontend::finish_oldest(std::deque<Inflight>& inflight) {
   pend_bytes_ = c.egress_bytes;
   pend_ = std::move(h);
   last_busy_ = busy;
+  fin_step_.store(f.step);
 }
 
 void Frontend::stepper() {
@@ -1106,7 +1180,9 @@ void Frontend::stepper() {
       continue;
     }
     // ---- idle: nothing in flight, nothing to write, nothing readable
-    if (inflight.empty() && !pend_valid_ && out_.empty() && !last_busy_ && !releasable() && !gets_pending()) {
+    const bool host_work = api_->host_work && api_->host_work(api_->eng) > 0;   // staged control writes
+    if (inflight.empty() && !pend_valid_ && out_.empty() && !last_busy_ && !releasable() && !gets_pending() &&
+        !host_work && !ctl_pending()) {
       std::unique_lock<std::mutex> g(st_mu_);
       const double idle = cfg_.idle_step_ms > 0 ? cfg_.idle_step_ms : 1000.0;
       st_cv_.wait_for(g, std::chrono::microseconds((i64)(idle * 1000)),
@@ -1146,7 +1222,8 @@ void Frontend::stepper() {
       }
     }
     const u64 used = ph_used_.load();
-    const bool submit = !segs.empty() || last_busy_ || idle_tick_ || gets_pending();
+    const bool submit = !segs.empty() || last_busy_ || idle_tick_ || gets_pending() ||
+                        (api_->host_work && api_->host_work(api_->eng) > 0) || ctl_needs_step();
     idle_tick_ = false;
     bool submitted = false;
     if (submit) {
@@ -1182,6 +1259,7 @@ void Frontend::stepper() {
       }
       f.p = p;
       f.step = ++step_no_;
+      sub_step_.store(step_no_);
       f.segs = std::move(seglens);
       f.gen.resize(c_max_);
       for (u32 k = 0; k < c_max_; ++k) f.gen[k] = conns_[k]->gen.load();
@@ -1346,6 +1424,7 @@ void Frontend::stepper_sharded() {
     arena_i_ = (arena_i_ + 1) % 3;
     f.p = p;
     f.step = ++step_no_;
+    sub_step_.store(step_no_);
     f.segs = std::move(seglens);
     f.gen.resize(c_max_);
     for (u32 k = 0; k < c_max_; ++k) f.gen[k] = conns_[k]->gen.load();
@@ -1521,6 +1600,7 @@ bool Frontend::collect_scatter(std::vector<Scatter*>& scat) {
     out_.push_back(std::move(sc));
     held_.pop_front();
   }
+  release_ctl();
   for (auto& sc : out_) scat.push_back(&sc);
   return true;
 }
@@ -1734,6 +1814,7 @@ EchoEngine::EchoEngine(u32 c_max, u32 seg_max, u64 ingress_cap, u32 carry_cap, u
   api_.host_register = nullptr;
   api_.host_unregister = nullptr;
   api_.egress_ready = nullptr;
+  api_.host_work = nullptr;
 }
 
 void EchoEngine::unpause(u32 conn) {

@@ -133,6 +133,12 @@ class Frontend {
   void set_read_cap(u32 conn, u64 bytes);                // per-step read budget (0: per_conn_read)
   void close(u32 conn);                                  // flush, close the socket, free the slot
   void kick(u32 conn);                                   // unpaused: re-present its device carry
+  // control reply of a command handled while steps keep running (no pause): written after
+  // the egress of every step submitted so far, so a Basic.CancelOk / Channel.CloseOk never
+  // overtakes a delivery rendered before it.  Any thread.
+  void send_after(u32 conn, const char* data, size_t n);
+  void wake();                                           // the stepper looks for work (staged control writes)
+  void flush_ctl();                                      // (paused) write every held control reply now
   // bytes for a socketless pseudo-connection (committed transactions): stepped with the
   // next step like a client's, FE_INJECTED once that step finished; egress is dropped
   void inject(u32 conn, const std::string& bytes);
@@ -290,6 +296,17 @@ class Frontend {
   FeStats stats_;
   std::atomic<u64> rx_bytes_{0}, tx_bytes_{0};
   u64 step_no_ = 0;
+  // steps submitted / finished so far (control replies and freed connection slots wait
+  // for the steps that were in flight when they were produced)
+  std::atomic<u64> sub_step_{0}, fin_step_{0};
+  struct CtlOut { u64 after; u32 conn; u32 gen; std::string data; };
+  std::mutex ctl_mu_;
+  std::deque<CtlOut> ctl_out_;
+  bool ctl_pending();
+  bool ctl_needs_step();
+  void release_ctl();
+  // closed connection slots: reusable once the steps in flight at their close finished
+  std::deque<std::pair<u64, u32>> quarantine_;   // (sub_step_ at close, slot), free_mu_
   i64 last_submit_ = 0;   // (stats: the stepper's period between submits)
   std::atomic<bool> failed_{false};   // read by healthy() (heartbeat thread)
 

@@ -335,6 +335,56 @@ DEV bool topic_match(const u8* pat, u32 plen, const u8* key, u32 klen, bool hash
   return true;
 }
 
+// ============================================================================ deferred control writes
+// The control plane's table writes (connection / channel / consumer state) staged while
+// steps run, packed per step by the host (Engine::pack_deltas): applied by k_stage before
+// the step reads anything, so no pipeline drain is needed for them.  Layout:
+//   DeltaHead | DeltaRec[nrec] | u32 dirty channel slots[ndirty] (16-B padded) | data chunks
+// Records never overlap (the host keeps the last write of every byte), so they are applied
+// in parallel: 16-byte chunk i belongs to record r with chunk0[r] <= i < chunk0[r + 1].
+struct DeltaHead { u32 nrec, ndirty, nchunk, pad; };
+struct DeltaRec { u64 dst; u32 len; u32 chunk0; };
+#define DELTA_REC_MAX 1024   // records per step (the host keeps the rest for later steps)
+DEV void apply_deltas(const DS& d, const u8* buf, u32 tid, u32 nt, DeltaRec* lrec) {
+  const DeltaHead h = *(const DeltaHead*)buf;
+  const DeltaRec* recs = (const DeltaRec*)(buf + sizeof(DeltaHead));
+  const u32* dirty = (const u32*)(recs + h.nrec);
+  const uint4* data = (const uint4*)((const u8*)dirty + ((4u * h.ndirty + 15u) & ~15u));
+  for (u32 r = tid; r < h.nrec; r += nt) lrec[r] = recs[r];
+  __syncthreads();
+  for (u32 i = tid; i < h.nchunk; i += nt) {
+    u32 lo = 0, hi = h.nrec;   // last record with chunk0 <= i
+    while (hi - lo > 1) {
+      const u32 mid = (lo + hi) >> 1;
+      if (lrec[mid].chunk0 <= i) lo = mid; else hi = mid;
+    }
+    const DeltaRec r = lrec[lo];
+    const u32 off = (i - r.chunk0) * 16u;
+    const u32 n = r.len - off < 16u ? r.len - off : 16u;
+    const uint4 v = data[i];
+    u8* dst = (u8*)(uintptr_t)(r.dst + off);
+    const u32 w[4] = {v.x, v.y, v.z, v.w};
+    if (((uintptr_t)dst & 3) == 0 && (n & 3) == 0) {
+      for (u32 k = 0; k < n / 4; ++k) ((u32*)dst)[k] = w[k];
+    } else {
+      for (u32 k = 0; k < n; ++k) dst[k] = (u8)(w[k >> 2] >> (8 * (k & 3)));
+    }
+  }
+  __syncthreads();
+  // closing channels: on the dirty list (k_chan_advance requeues their unacked deliveries)
+  for (u32 k = tid; k < h.ndirty; k += nt) {
+    const u32 ch = dirty[k];
+    if (atomicExch(&d.ch_dirty[ch], 1u) == 0) d.dirty_list[atomicAdd(d.n_dirty, 1u)] = ch;
+  }
+  __threadfence();   // (rare: steps with control writes) every later read of the block sees them
+  __syncthreads();
+}
+// between steps (the control plane holds the engine): the staged writes now
+__global__ __launch_bounds__(1024) void k_apply_deltas(DS d, const u8* buf) {
+  __shared__ DeltaRec lrec[DELTA_REC_MAX];
+  apply_deltas(d, buf, threadIdx.x, 1024, lrec);
+}
+
 // ============================================================================ K0 step init
 // one block: resets the step counters and lays the step's segments out in the work buffer
 // (segment k at the prefix of the 16-aligned sizes carry + new bytes + 32 of the segments
@@ -344,6 +394,7 @@ DEV bool topic_match(const u8* pat, u32 plen, const u8* key, u32 klen, bool hash
 __global__ __launch_bounds__(1024) void k_stage(DS d) {
   __shared__ u32 lds[1024 / 64 + 1];
   __shared__ StepIn s_in;
+  __shared__ DeltaRec lrec[DELTA_REC_MAX];
   const u32 tid = threadIdx.x;
   // the step's descriptors from the host's mapped staging (one PCIe round), written to
   // their device copies for every later kernel of the step
@@ -352,6 +403,7 @@ __global__ __launch_bounds__(1024) void k_stage(DS d) {
     *d.in = s_in;
   }
   __syncthreads();
+  if (s_in.delta_bytes) apply_deltas(d, d.delta_h, tid, 1024, lrec);   // control writes first
   const u32 nseg = s_in.nseg;
   {
     u32* c = (u32*)d.ctr;

@@ -42,7 +42,7 @@ enum : u32 {
 enum : u32 { US_FREE = 0, US_PENDING = 1, US_ACKED = 2, US_REQUEUE = 3, US_DONE = 4 };
 
 
-struct StepIn {         // host -> device per step (72 B)
+struct StepIn {         // host -> device per step (80 B)
   u32 nseg;
   u32 flags;
   i64 now_ms;
@@ -59,6 +59,10 @@ struct StepIn {         // host -> device per step (72 B)
   // the host queued on the SDMA engine at launch -- no host round trip between render and
   // copy
   u64 gate;
+  // deferred control writes (DS.delta_h of this parity, packed by the host): bytes, 0 = none.
+  // k_stage applies them first, before the step reads any table
+  u32 delta_bytes;
+  u32 pad_;
 };
 
 

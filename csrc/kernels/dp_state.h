@@ -76,6 +76,7 @@ struct DS {
   const SegIn* segs;        // device copy of the step's segments (k_stage writes them)
   const StepIn* in_h;       // host-mapped: the host's staging of them (read once, by k_stage)
   const SegIn* segs_h;
+  const u8* delta_h;        // host-mapped: this parity's deferred control writes (StepIn.delta_bytes)
   const u8* ingress;
   SegOut* seg_out;          // device; published to seg_out_h at the end of the step
   Counters* ctr;            // device

@@ -9,6 +9,7 @@
 
 #include <chrono>
 #include <algorithm>
+#include <deque>
 #include <functional>
 #include <map>
 #include <memory>
@@ -242,6 +243,9 @@ class Engine {
       io.segs_h = (const SegIn*)hst(("stage_segs" + sfx).c_str(), sizeof(SegIn) * d_.seg_max + 64);
       stage_in_[p] = (StepIn*)buf("stage_in" + sfx).ptr;
       stage_segs_[p] = (SegIn*)buf("stage_segs" + sfx).ptr;
+      // deferred control writes ridden by this parity's steps (pack_deltas)
+      io.delta_h = (const u8*)hst(("delta" + sfx).c_str(), DELTA_CAP);
+      dl_h_[p] = (u8*)buf("delta" + sfx).ptr;
       // Basic.Get on the step: the requests (H2D with the step) and their answers
       io.get_req = (const GetReq*)dev(("get_req" + sfx).c_str(), sizeof(GetReq) * GET_STEP_MAX);
       io.get_out_h = (GetOut*)hst(("get_out" + sfx).c_str(), sizeof(GetOut) * GET_STEP_MAX);
@@ -521,7 +525,7 @@ class Engine {
       io.seg_out_h = io_[p].seg_out_h; io.conn_out_h = io_[p].conn_out_h; io.ctrl_h = io_[p].ctrl_h;
       io.ctrl_rec_h = io_[p].ctrl_rec_h; io.grow_h = io_[p].grow_h; io.conn_conf_h = io_[p].conn_conf_h;
       io.get_req = io_[p].get_req; io.get_out_h = io_[p].get_out_h; io.unpause_req = io_[p].unpause_req;
-      io.in_h = io_[p].in_h; io.segs_h = io_[p].segs_h;
+      io.in_h = io_[p].in_h; io.segs_h = io_[p].segs_h; io.delta_h = io_[p].delta_h;
       static_cast<DS&>(io_[p]) = io;
     }
     // native exchange (sharded steps driven by the native front end, csrc/core/frontend.cpp):
@@ -835,16 +839,15 @@ class Engine {
       pend_gets_.clear();
     }
     nget_[p] = in->nget;
-    {   // connections the host unpaused since the last step (any thread may stage them)
-      std::lock_guard<std::mutex> g(unp_mu_);
-      in->nunp = (u32)std::min<size_t>(pend_unp_.size(), UNPAUSE_STEP_MAX);
-      if (in->nunp) {
-        memcpy(stage_unp_[p], pend_unp_.data(), 4ull * in->nunp);
-        pend_unp_.erase(pend_unp_.begin(), pend_unp_.begin() + in->nunp);
-      }
-    }
+    // the control writes staged so far (what fits one step) and the connections
+    // unpaused with them: a connection resumed in this step finds every write staged
+    // before its unpause applied (k_stage applies the writes first)
+    u32 nunp = 0;
+    in->delta_bytes = pack_deltas(p, stage_unp_[p], &nunp);
+    in->nunp = nunp;
     if (in->nunp)
       HIPCHECK(hipMemcpyAsync((void*)io_[p].unpause_req, stage_unp_[p], 4ull * in->nunp, hipMemcpyHostToDevice, s_h2d_));
+    dl_step_[p] = in->delta_bytes;
     // the payload may already be on its way (prefetch): then only the step's descriptors
     // follow it on the H2D stream
     const bool pre = pre_[p];
@@ -900,15 +903,162 @@ class Engine {
     return true;
   }
 
+  // ---- deferred control writes (no pipeline drain): the control plane stages table writes
+  // while steps run; the next submitted step carries them (k_stage applies them first).
+  // Any thread.  Writes to the same bytes: the last one wins (records never overlap).
+  void stage_write(u64 dst, const u8* data, u64 n) {
+    if (!n) return;
+    std::lock_guard<std::mutex> g(dl_mu_);
+    if (dl_.empty()) dl_.emplace_back();
+    DlBatch& bt = dl_.back();
+    const u64 a = dst, e = dst + n;
+    auto it = bt.w.lower_bound(a);
+    if (it != bt.w.begin()) --it;
+    std::vector<std::pair<u64, std::string>> keep;
+    while (it != bt.w.end() && it->first < e) {
+      const u64 s0 = it->first, s1 = s0 + it->second.size();
+      if (s1 <= a) { ++it; continue; }
+      if (s0 < a) keep.emplace_back(s0, it->second.substr(0, a - s0));
+      if (s1 > e) keep.emplace_back(e, it->second.substr(e - s0));
+      bt.bytes -= it->second.size();
+      dl_bytes_ -= it->second.size();
+      it = bt.w.erase(it);
+    }
+    for (auto& kv : keep) {
+      bt.bytes += kv.second.size();
+      dl_bytes_ += kv.second.size();
+      bt.w.emplace(kv.first, std::move(kv.second));
+    }
+    bt.w.emplace(a, std::string((const char*)data, n));
+    bt.bytes += n;
+    dl_bytes_ += n;
+  }
+  void stage_write_buf(const std::string& name, py::buffer data, size_t offset) {
+    py::buffer_info info = data.request();
+    const size_t n = (size_t)info.size * info.itemsize;
+    const Buf& b = buf(name);
+    if (offset + n > b.bytes) throw std::runtime_error("stage_write overflows " + name);
+    if (b.host) { memcpy((u8*)b.ptr + offset, info.ptr, n); return; }   // host-mapped: direct
+    stage_write((u64)b.ptr + offset, (const u8*)info.ptr, n);
+  }
+  void stage_mark_dirty(u32 ch) {
+    if (ch >= d_.c_max * d_.chpc) throw std::runtime_error("stage_mark_dirty: bad channel slot");
+    std::lock_guard<std::mutex> g(dl_mu_);
+    if (dl_.empty()) dl_.emplace_back();
+    auto& dv = dl_.back().dirty;
+    for (u32 c : dv)
+      if (c == ch) return;
+    dv.push_back(ch);
+  }
+  // (records, data bytes, channels to mark) staged and not yet taken by a step
+  py::tuple deltas_pending() {
+    std::lock_guard<std::mutex> g(dl_mu_);
+    size_t nrec = 0, nd = 0;
+    for (auto& bt : dl_) { nrec += bt.w.size(); nd += bt.dirty.size(); }
+    return py::make_tuple(nrec, dl_bytes_, nd);
+  }
+  bool host_work() {
+    std::lock_guard<std::mutex> g(dl_mu_);
+    if (!unp_ready_.empty()) return true;
+    for (auto& bt : dl_)
+      if (!bt.w.empty() || !bt.dirty.empty() || !bt.unp.empty()) return true;
+    return false;
+  }
+  bool has_deltas() {
+    std::lock_guard<std::mutex> g(dl_mu_);
+    for (auto& bt : dl_)
+      if (!bt.w.empty() || !bt.dirty.empty()) return true;
+    return false;
+  }
+  // the oldest staged batch into parity p's host-mapped delta buffer: bytes used (0 = none).
+  // What does not fit (records or bytes) stays for a later step: records are independent
+  // bytes, and the control plane keeps a change set within one step by staging it whole
+  // under its lock before any unpause (it checks deltas_pending() against the limits)
+  // The batch's unpauses go to unp (at most UNPAUSE_STEP_MAX, *nunp) or, with unp null
+  // (flush_deltas: no step), to unp_ready_ for the next submitted step.
+  u32 pack_deltas(int p, u32* unp, u32* nunp) {
+    std::lock_guard<std::mutex> g(dl_mu_);
+    u32 nu = 0;
+    auto take_unp = [&](std::vector<u32>& v) {
+      size_t k = 0;
+      for (; k < v.size(); ++k) {
+        if (!unp) { unp_ready_.push_back(v[k]); continue; }
+        if (nu == UNPAUSE_STEP_MAX) break;
+        unp[nu++] = v[k];
+      }
+      v.erase(v.begin(), v.begin() + k);
+    };
+    if (unp) take_unp(unp_ready_);
+    while (!dl_.empty() && dl_.front().w.empty() && dl_.front().dirty.empty()) {
+      take_unp(dl_.front().unp);   // a batch of unpauses only (no writes)
+      if (!dl_.front().unp.empty()) break;
+      if (dl_.size() == 1) { dl_.pop_front(); break; }
+      dl_.pop_front();
+    }
+    if (nunp) *nunp = nu;
+    if (dl_.empty() || (dl_.front().w.empty() && dl_.front().dirty.empty())) return 0;
+    DlBatch& bt = dl_.front();
+    u8* o = dl_h_[p];
+    const u32 ndirty = (u32)std::min<size_t>(bt.dirty.size(), 4096);
+    u64 nrec = 0, nchunk = 0;
+    for (auto& kv : bt.w) {
+      const u64 ch = (kv.second.size() + 15) / 16;
+      const u64 need = 16 + 16 * (nrec + 1) + ((4ull * ndirty + 15) & ~15ull) + 16 * (nchunk + ch);
+      if (nrec == DELTA_REC_MAX || need > DELTA_CAP) break;
+      ++nrec;
+      nchunk += ch;
+    }
+    DeltaHead* h = (DeltaHead*)o;
+    h->nrec = (u32)nrec; h->ndirty = ndirty; h->nchunk = (u32)nchunk; h->pad = 0;
+    DeltaRec* recs = (DeltaRec*)(o + sizeof(DeltaHead));
+    u32* dirty = (u32*)(recs + nrec);
+    u8* data = (u8*)dirty + ((4ull * ndirty + 15) & ~15ull);
+    u64 r = 0, c = 0;
+    for (auto it = bt.w.begin(); it != bt.w.end() && r < nrec;) {
+      recs[r].dst = it->first;
+      recs[r].len = (u32)it->second.size();
+      recs[r].chunk0 = (u32)c;
+      memcpy(data + 16 * c, it->second.data(), it->second.size());
+      c += (it->second.size() + 15) / 16;
+      bt.bytes -= it->second.size();
+      dl_bytes_ -= it->second.size();
+      it = bt.w.erase(it);
+      ++r;
+    }
+    for (u32 k = 0; k < ndirty; ++k) dirty[k] = bt.dirty[k];
+    bt.dirty.erase(bt.dirty.begin(), bt.dirty.begin() + ndirty);
+    if (bt.w.empty() && bt.dirty.empty()) {   // the whole batch went: its unpauses ride along
+      take_unp(bt.unp);
+      if (bt.unp.empty()) dl_.pop_front();
+      if (nunp) *nunp = nu;
+    }
+    ++dl_steps_;
+    return (u32)((data - o) + 16 * c);
+  }
+  // between steps (the control plane holds the engine): apply what is staged now
+  void flush_deltas() {
+    if (!has_deltas()) return;
+    if (inflight_[0] || inflight_[1]) throw std::runtime_error("flush_deltas() between steps only");
+    sync();
+    while (has_deltas()) {
+      if (!pack_deltas(0, nullptr, nullptr)) break;
+      hipLaunchKernelGGL(k_apply_deltas, dim3(1), dim3(1024), 0, s_comp_, io_[0], io_[0].delta_h);
+      HIPCHECK(hipGetLastError());
+      HIPCHECK(hipStreamSynchronize(s_comp_));
+    }
+  }
+
   // a paused connection (its control command answered) resumes with the next submitted
   // step: k_stage clears its flag before the frame scan reads it, so the host never writes
   // device state while steps are in flight.  Any thread.
   void stage_unpause(u32 conn) {
     if (conn >= d_.c_max) throw std::runtime_error("stage_unpause: bad connection");
-    std::lock_guard<std::mutex> g(unp_mu_);
-    for (u32 c : pend_unp_)
+    std::lock_guard<std::mutex> g(dl_mu_);
+    if (dl_.empty()) dl_.emplace_back();
+    auto& v = dl_.back().unp;   // with the writes staged before it
+    for (u32 c : v)
       if (c == conn) return;
-    pend_unp_.push_back(conn);
+    v.push_back(conn);
   }
 
   // Basic.Get requests for the next submitted step (validated by the caller: a local queue
@@ -943,6 +1093,8 @@ class Engine {
       HIPCHECK(hipStreamWaitEvent(s_ing_, ev_h2d_[p], 0));
       HIPCHECK(hipStreamWaitEvent(s_ing_, ev_pre_[p], 0));
       if (rest_issued_[p]) HIPCHECK(hipStreamWaitEvent(s_ing_, ev_rest_[p], 0));
+      // control writes: applied between steps -- after the previous step's routing half
+      if (dl_step_[p] && rest_issued_[p ^ 1]) HIPCHECK(hipStreamWaitEvent(s_ing_, ev_rest_[p ^ 1], 0));
       {
         HostTimer t(&ht_[2]);
         if (!graph_ing_[p]) capture_on(s_ing_, &graph_ing_[p], [&] { launch_ingest(s_ing_, io_[p]); });
@@ -1568,6 +1720,7 @@ class Engine {
       return ((Engine*)e)->guard([&] { ((Engine*)e)->stage_gets(r, n); return 0; });
     };
     a.get_out = [](void* e, int p) -> const GetOut* { return ((Engine*)e)->io_[p].get_out_hh; };
+    a.host_work = [](void* e) -> int { return ((Engine*)e)->host_work() ? 1 : 0; };
     for (int p = 0; p < 2; ++p) {
       std::string sfx = std::to_string(p);
       HostIO& h = io_[p];
@@ -2133,6 +2286,18 @@ class Engine {
     const GetOut* get_out_hh = nullptr;
   };
   std::vector<GetReq> pend_gets_;   // Basic.Get requests for the next submit
+  // deferred control writes: device address -> bytes (non-overlapping), channels to mark
+  static constexpr u64 DELTA_CAP = 4ull << 20;
+  std::mutex dl_mu_;
+  struct DlBatch { std::map<u64, std::string> w; std::vector<u32> dirty, unp; u64 bytes = 0; };
+  std::vector<u32> unp_ready_;   // unpauses of batches flush_deltas applied (next step)
+  // staged writes with the unpauses staged after them; a batch that overflows one step's
+  // delta buffer keeps its unpauses until its last write is packed
+  std::deque<DlBatch> dl_;
+  u64 dl_bytes_ = 0;
+  u8* dl_h_[2] = {nullptr, nullptr};
+  u32 dl_step_[2] = {0, 0};
+  u64 dl_steps_ = 0;
   static constexpr u32 COLD_BATCH = 1u << 16;   // cold records per pick / scan call
   ColdRec* cold_recs_ = nullptr;
   u32* cold_cnt_ = nullptr;
@@ -2165,8 +2330,6 @@ class Engine {
   }
   GetReq* stage_gets_[2] = {nullptr, nullptr};
   u32* stage_unp_[2] = {nullptr, nullptr};
-  std::mutex unp_mu_;
-  std::vector<u32> pend_unp_;
   u32 nget_[2] = {0, 0};
   HostIO io_[2];
   CmqEngineApi api_{};
@@ -2297,5 +2460,9 @@ PYBIND11_MODULE(_dataplane, m) {
       .def("launch_b", &Engine::launch_b)
       .def("counters", &Engine::counters)
       .def("host_times", &Engine::host_times, py::arg("reset") = false)
-      .def("egress_stats", &Engine::egress_stats);
+      .def("egress_stats", &Engine::egress_stats)
+      .def("stage_write", &Engine::stage_write_buf, py::arg("name"), py::arg("data"), py::arg("offset") = 0)
+      .def("stage_mark_dirty", &Engine::stage_mark_dirty)
+      .def("deltas_pending", &Engine::deltas_pending)
+      .def("flush_deltas", &Engine::flush_deltas, py::call_guard<py::gil_scoped_release>());
 }

@@ -101,7 +101,7 @@ struct GetOut { u32 status; u32 msg_count; };
 // C entry points of one Engine (engine.hip: Engine::c_api).  All return 0 / a parity on
 // success and -1 on error (message: error()).  Parity p = the double-buffered step IO set
 // of a submitted step; its host-mapped outputs stay valid until the next submit of p.
-#define CMQ_STEP_ABI 6
+#define CMQ_STEP_ABI 7
 #define PSLOTS 4                // rotating host store-record slots (a step's records live PSLOTS - 1 more steps)
 #define UNPAUSE_STEP_MAX 1024   // connections unpaused per step (StepIn.nunp)
 struct CmqEngineApi {
@@ -156,5 +156,8 @@ struct CmqEngineApi {
   // the NEXT submit's payload H2D queued now (overlapped single-GPU engine): 1 queued, 0 not
   // applicable, -1 error; that submit must pass the same payload
   int (*prefetch)(void* eng, const u8* payload, u64 len);
+  // control writes (or unpauses) staged for the next step: 1 = the stepper should step even
+  // without client bytes (null: never)
+  int (*host_work)(void* eng);
 };
 #define GROW_MAX 4096   // grow requests reported per step

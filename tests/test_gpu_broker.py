@@ -754,3 +754,78 @@ def test_backlog_past_hbm_and_host_tiers_goes_to_the_cold_store(gpu, io, tmp_pat
         c.close()
     finally:
         b.stop()
+
+
+@pytest.mark.gpu
+def test_control_churn_rides_the_steps_without_a_drain(gpu):
+    """Connection open/close, channel open/close and consume/cancel while a publisher
+    streams: handled in light control sections (their table writes staged and applied by
+    the next step's first kernel, replies sent behind the deliveries in flight), so the
+    stepper is never paused for them; a closed channel's unacked deliveries are still
+    requeued before its slot is reused (its CloseOk waits for the step carrying the close,
+    so the reopen rides a later one), and no delivery is lost."""
+    import threading
+    import time
+    from chanamq_amd.engine.dataplane import GpuDataPlane
+    from chanamq_amd.server.gpu_broker import GpuBroker
+    b = GpuBroker(GpuDataPlane(default_queue_capacity=1 << 12, **GPU_CFG), idle_step_ms=1.0, io="pipeline",
+                  ingress_bytes=8 << 20).start()
+    try:
+        s = conn(b)
+        sch = s.channel()
+        for q in ("load", "cq", "rq"):
+            sch.queue_declare(q)
+        for k in range(10):
+            sch.basic_publish("", "rq", f"r{k}".encode())
+        sink = conn(b)
+        kch = sink.channel()
+        kch.basic_consume("load", "sink", no_ack=True)
+        stop = threading.Event()
+        sent = [0]
+
+        def pump():
+            pc = conn(b)
+            pch = pc.channel()
+            while not stop.is_set():
+                for _ in range(50):
+                    pch.basic_publish("", "load", sent[0].to_bytes(4, "big") * 64)
+                    sent[0] += 1
+                pc.process(0.002)
+            pc.close()
+        th = threading.Thread(target=pump, daemon=True)
+        th.start()
+        time.sleep(0.3)
+        pauses0, light0 = b.stats.get("pauses", 0), b.stats.get("light_sections", 0)
+        # manual-ack consumer takes the 10, its channel closes with them unacked
+        rc = conn(b)
+        r1 = rc.channel(5)
+        r1.basic_consume("rq", "r", no_ack=False)
+        assert sorted(d.body for d in r1.consume_n(10)) == sorted(f"r{k}".encode() for k in range(10))
+        r1.close()
+        r2 = rc.channel(5)   # same channel number (same device slot): gets them again, redelivered
+        r2.basic_consume("rq", "r2", no_ack=False)
+        again = r2.consume_n(10, timeout=20)
+        assert sorted(d.body for d in again) == sorted(f"r{k}".encode() for k in range(10))
+        assert all(d.method.redelivered for d in again)
+        # consume / cancel and connection churn
+        cc = conn(b)
+        cch = cc.channel()
+        for k in range(100):
+            cch.basic_consume("cq", f"c{k}", no_ack=True)
+            cch.basic_cancel(f"c{k}")
+        for _ in range(20):
+            x = conn(b)
+            x.channel()
+            x.close()
+        pauses1, light1 = b.stats.get("pauses", 0), b.stats.get("light_sections", 0)
+        stop.set()
+        th.join(20)
+        # every publish arrives, in order
+        got = kch.consume_n(sent[0], timeout=60)
+        assert [int.from_bytes(d.body[:4], "big") for d in got] == list(range(sent[0]))
+        assert light1 - light0 >= 150, (light0, light1)
+        assert pauses1 == pauses0, (pauses0, pauses1, b.stats)
+        for c_ in (s, sink, rc, cc):
+            c_.close()
+    finally:
+        b.stop()
