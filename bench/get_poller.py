@@ -1,7 +1,8 @@
 """Basic.Get pollers for bench/gpu_server_e2e.py --getters, in their own process (the
 broker's control plane runs in the bench process: pollers there would compete with it for
 the GIL).  Pre-fills one queue per poller, prints "ready", polls Basic.Get (no-ack) until
-stdin closes, then prints one JSON line: [[gets ok, gets empty, seconds], ...]."""
+stdin closes -- ``--pipeline`` Gets in flight per poller, answered inside the steps that
+decode them -- then prints one JSON line: [[gets ok, gets empty, seconds], ...]."""
 import argparse
 import json
 import os
@@ -18,6 +19,7 @@ def main():
     ap.add_argument("--port", type=int, required=True)
     ap.add_argument("--n", type=int, default=4)
     ap.add_argument("--prefill", type=int, default=200000)
+    ap.add_argument("--pipeline", type=int, default=16, help="Basic.Gets in flight per poller")
     a = ap.parse_args()
     c = Connection(port=a.port, vhost="/", timeout=60)
     ch = c.channel()
@@ -35,7 +37,11 @@ def main():
         ok = empty = 0
         t0 = time.time()
         while not stop.is_set():
-            if pch.basic_get(f"e2e.getq{i}", no_ack=True) is None:
+            if a.pipeline > 1:
+                got, e = pch.basic_get_many(f"e2e.getq{i}", a.pipeline, no_ack=True)
+                ok += len(got)
+                empty += e
+            elif pch.basic_get(f"e2e.getq{i}", no_ack=True) is None:
                 empty += 1
             else:
                 ok += 1

@@ -147,6 +147,28 @@ class Channel:
             return None
         return self.conn._wait(pred, self)[0]
 
+    def basic_get_many(self, queue, n, no_ack=True):
+        """``n`` pipelined Basic.Gets in one write (the server answers them in order): the
+        GetOk deliveries, and how many came back GetEmpty."""
+        self.conn._send_raw(encode_method_frame(self.number, Method("basic.get", queue=queue, no_ack=no_ack)) * n)
+        state = {"ok": [], "empty": 0}
+
+        def pred():
+            if self.closed:
+                raise self.closed
+            for i in range(len(self.inbox) - 1, -1, -1):
+                if self.inbox[i].name == "basic.get_empty":
+                    del self.inbox[i]
+                    state["empty"] += 1
+            keep = collections.deque()
+            while self.deliveries:
+                d = self.deliveries.popleft()
+                (state["ok"] if d.method.name == "basic.get_ok" else keep).append(d)
+            self.deliveries.extend(keep)
+            return True if len(state["ok"]) + state["empty"] >= n else None
+        self.conn._wait(pred, self)
+        return state["ok"], state["empty"]
+
     def basic_ack(self, delivery_tag, multiple=False):
         self._send("basic.ack", delivery_tag=delivery_tag, multiple=multiple)
 

@@ -15,7 +15,7 @@ import numpy as np
 from .. import ops
 from ..protocol import constants as C
 from .control import ControlError, ControlState
-from .layout import (CONN_OUT, CONSUMED_REC, RING_MOVE, CTRL_REC, CTRL_TXBUF, INVALID, MF_HAS_TS, MF_HOSTPUB, MF_PERSIST,
+from .layout import (CONN_OUT, CONSUMED_REC, RING_MOVE, CTRL_REC, CTRL_DGET, CTRL_TXBUF, INVALID, MF_HAS_TS, MF_HOSTPUB, MF_PERSIST,
                      MF_ONEQ, MF_REDELIVERED, MF_RESTORE,
                      PERSIST_HDR, RDESC, SEG_IN, SEG_OUT, SS_CTRL, US_ACKED, US_PENDING, US_REQUEUE, USLOT,
                      chan_hash, direct_key, exch_hash, fnv1a64, topic_pattern_row, topic_word_offsets)
@@ -323,6 +323,7 @@ class GpuDataPlane(ControlState):
 
     def queue_declared(self, q):
         self._up_at("q_owner", q.owner, q.slot, np.uint32)
+        self._up_at("q_excl", q.exclusive_owner + 1 if q.exclusive_owner >= 0 else 0, q.slot, np.uint32)
         self._up_at("q_durable", int(q.durable), q.slot, np.uint32)
         self._up_at("q_ring_off", q.ring_off, q.slot, np.uint64)
         self._up_at("q_ring_mask", q.capacity - 1, q.slot, np.uint64)
@@ -964,6 +965,8 @@ class GpuDataPlane(ControlState):
                     o, n, sg = int(rec["off"]), int(rec["len"]), int(rec["seg"])
                     if sg & CTRL_TXBUF:
                         res.txbuf.append((int(rec["conn"]), sg & ~CTRL_TXBUF, bytes(io["ctrl"][o:o + n])))
+                    elif sg & CTRL_DGET:   # (the connection was not paused)
+                        res.ctrl.append((int(rec["conn"]), bytes(io["ctrl"][o:o + n]), True))
                     else:
                         res.ctrl.append((int(rec["conn"]), bytes(io["ctrl"][o:o + n])))
             res.txbuf.sort()

@@ -229,6 +229,28 @@ class GoldenDataPlane(ControlState):
             return None
         return conn * self.chpc + c.channels[ch].local
 
+    def _dget_resolve(self, conn, data, p, size):
+        """Basic.Get the step serves itself (spec of dget_resolve, dataplane.hip): a named
+        queue bound to the vhost's default exchange, owned here, not another connection's
+        exclusive queue.  -> (queue slot, no_ack) or None (the host serves it)."""
+        if size < 8:
+            return None
+        a, end = p + 7 + 6, p + 7 + size
+        n = data[a]
+        if n == 0 or a + 1 + n + 1 > end:
+            return None
+        name = bytes(data[a + 1:a + 1 + n])
+        x = self.exchanges.get((self.conns[conn].vhost, ""))
+        if x is None or x.type != "direct":
+            return None
+        qs = self._route(x, name)
+        if len(qs) != 1:
+            return None
+        q = self.queue_by_slot.get(qs[0])
+        if q is None or q.owner != self.rank or q.exclusive_owner not in (-1, conn):
+            return None
+        return q.slot, data[a + 1 + n] & 1
+
     # ------------------------------------------------------------------ frame scan (K1)
     def _scan(self, conn, data):
         c = self.conns[conn]
@@ -258,6 +280,7 @@ class GoldenDataPlane(ControlState):
         stop = None  # (frame index, reason)
         f = 0
         nf = len(frames)
+        gkey = None   # (channel, queue, no_ack) of the segment's first step-served Basic.Get
         while f < nf:
             p, fi = frames[f]
             if fi is None:
@@ -275,6 +298,15 @@ class GoldenDataPlane(ControlState):
                 break
             cls, mid = struct.unpack_from(">HH", data, p + 7)
             chs = self._chan_of(conn, ch)
+            g = self._dget_resolve(conn, data, p, size) if (cls, mid) == (60, 70) and chs is not None else None
+            if gkey is not None and (g is None or (ch,) + g != gkey):
+                stop = (f, 4)   # only the same Basic.Get may follow the first in one step
+                break
+            if g is not None:
+                gkey = (ch,) + g
+                cmds.append(dict(kind="get", ch=ch, chslot=chs, q=g[0], noack=bool(g[1]), raw=data[p:p + 8 + size]))
+                f += 1
+                continue
             data_cmd = cls == 60 and mid in (40, 80, 90, 120) and chs is not None
             if cls == 60 and mid == 40:
                 if f + 1 >= nf or frames[f + 1][1] is None:
@@ -338,6 +370,8 @@ class GoldenDataPlane(ControlState):
             status |= SS_FRAME_ERROR if reason == 3 else SS_UNEXPECTED
         if reason == 0:
             status |= SS_CTRL
+        if reason == 4:
+            status |= SS_OVERFLOW
         return cmds, consumed, status
 
     # ------------------------------------------------------------------ one step
@@ -455,7 +489,7 @@ class GoldenDataPlane(ControlState):
         for c, cl in self.carry.items():
             if cl and c in self.conns and not self.conns[c].paused:
                 conns.add(c)
-        pubs, acks = [], []
+        pubs, acks, gets = [], [], []
         for conn in sorted(conns):
             data = self.carry[conn] + inputs.get(conn, b"")
             if self.conns[conn].paused:
@@ -466,7 +500,9 @@ class GoldenDataPlane(ControlState):
             chans = self.conns[conn].channels
             for cmd in cmds:
                 cmd["conn"] = conn
-                if cmd["kind"] != "control" and chans[cmd["ch"]].tx:   # held until Tx.Commit
+                if cmd["kind"] == "get":
+                    gets.append(cmd)
+                elif cmd["kind"] != "control" and chans[cmd["ch"]].tx:   # held until Tx.Commit
                     out["txbuf"].append((conn, cmd["m"][0] - 7, cmd["raw"]))
                 elif cmd["kind"] == "publish":
                     pubs.append((cmd, data))
@@ -486,12 +522,13 @@ class GoldenDataPlane(ControlState):
         returns = defaultdict(list)
         for cmd, data in pubs:
             self._publish(cmd, data, now_ms, returns, out)
-        self._pend = dict(out=out, returns=returns, acks=acks, now_ms=now_ms,
+        self._pend = dict(out=out, returns=returns, acks=acks, gets=gets, now_ms=now_ms,
                           send_counts=self._pack() if self.world > 1 else None)
 
     def step_b(self, recv=None):
         st, self._pend = self._pend, None
         out, returns, acks, now_ms = st["out"], st["returns"], st["acks"], st["now_ms"]
+        dgets = st.get("gets", ())
         cnt = self.counters
         if recv is not None:
             records = self._parse_recv(recv)
@@ -579,8 +616,12 @@ class GoldenDataPlane(ControlState):
         delivs = []
         budget = [0]
         self._ttl_budget = 0
+        gets = defaultdict(list)
+        for g in dgets:
+            gets[g["q"]].append(g)
+        gempty = defaultdict(list)
         for q in sorted(self.queue_by_slot):
-            delivs.extend(self._dequeue(q, now_ms, budget))
+            delivs.extend(self._dequeue(q, now_ms, budget, gets.get(q, ()), gempty, out))
         # ---- tags: stable sort by chslot
         delivs.sort(key=lambda d: d["chslot"])
         for d in delivs:
@@ -597,7 +638,7 @@ class GoldenDataPlane(ControlState):
         by_conn = defaultdict(list)
         for d in delivs:
             by_conn[d["chslot"] // self.chpc].append(d)
-        conns_out = set(by_conn) | set(returns)
+        conns_out = set(by_conn) | set(returns) | set(gempty)
         for s, st in self.ch.items():
             if st["pub_cnt"]:
                 conns_out.add(s // self.chpc)
@@ -617,6 +658,8 @@ class GoldenDataPlane(ControlState):
             fm = self.conns[conn].frame_max if conn in self.conns else 131072
             for d in by_conn.get(conn, []):
                 parts.append(self._render_deliver(d, fm))
+            for chno in gempty.get(conn, ()):   # Basic.GetEmpty frames close the region
+                parts.append(_frame(1, chno, struct.pack(">HHB", 60, 72, 0)))
             if parts:
                 out["egress"][conn] = b"".join(parts)
         for d in delivs:
@@ -760,7 +803,7 @@ class GoldenDataPlane(ControlState):
             return now_ms + int(e)
         return 0
 
-    def _dequeue(self, q, now_ms, budget):
+    def _dequeue(self, q, now_ms, budget, gets=(), gempty=None, step_out=None):
         qq = self.queue_by_slot[q]
         ring = self.ring[q]
         cnt = self.counters
@@ -777,10 +820,31 @@ class GoldenDataPlane(ControlState):
             self._release(ring.pop(0)[0])
             self.qpos_head[q] += 1
             cnt["n_expired"] += 1
+        # the step's Basic.Gets of this queue, in wire order, ahead of its consumers (spec of
+        # k_dequeue's request loop): GetOk as a delivery on the getter's channel, GetEmpty at
+        # the end of its connection's egress, a full delivery window -> the host serves it
+        got = []
+        for g in gets:
+            s = g["chslot"]
+            st = self.ch[s]
+            if not ring:
+                gempty[g["conn"]].append(st["num"])
+                continue
+            if st["win"] >= self.ucap or len(got) >= 32:   # (RUNS_PER_Q / 2 Get runs per queue)
+                step_out["ctrl"].append((g["conn"], g["raw"], True))
+                continue
+            msg, red, exp = ring.pop(0)
+            st["win"] += 1
+            if not g["noack"]:
+                st["unacked"] += 1
+                self.cons_unacked[-1] += 1
+            got.append(dict(chslot=s, cons=-1, msg=msg, q=q, qpos=self.qpos_head[q], expire=exp, redelivered=red,
+                            noack=g["noack"], get_left=len(ring)))
+            self.qpos_head[q] += 1
         mall = len(qq.consumers)
         if not mall or not ring:
-            return []
-        m = min(mall, 64)
+            return got
+        m = min(mall, 64 - len(got))
         r = self.qrr[q] % mall
         remaining = len(ring)
         grants = []
@@ -825,14 +889,18 @@ class GoldenDataPlane(ControlState):
         self.qrr[q] = (r + 1) % mall
         del ring[:pos]
         self.qpos_head[q] += pos
-        return out
+        return got + out
 
     def _render_deliver(self, d, fm):
         m = d["msg"]
         ch = self.ch[d["chslot"]]["num"]
-        tag = d["tag_str"][:255]
-        mp = (struct.pack(">HHB", 60, 60, len(tag)) + tag + struct.pack(">QB", d["tag"], 1 if d["redelivered"] else 0)
-              + bytes([len(m.ex)]) + m.ex + bytes([len(m.rk)]) + m.rk)
+        if "get_left" in d:   # Basic.GetOk (message-count: what the queue held after it)
+            mp = (struct.pack(">HHQB", 60, 71, d["tag"], 1 if d["redelivered"] else 0) + bytes([len(m.ex)]) + m.ex
+                  + bytes([len(m.rk)]) + m.rk + struct.pack(">I", d["get_left"]))
+        else:
+            tag = d["tag_str"][:255]
+            mp = (struct.pack(">HHB", 60, 60, len(tag)) + tag + struct.pack(">QB", d["tag"], 1 if d["redelivered"] else 0)
+                  + bytes([len(m.ex)]) + m.ex + bytes([len(m.rk)]) + m.rk)
         parts = [_frame(1, ch, mp), _frame(2, ch, struct.pack(">HHQ", 60, 0, len(m.body)) + m.props)]
         step = fm - 8 if fm else len(m.body)
         for i in range(0, len(m.body), max(step, 1)):

@@ -273,7 +273,9 @@ class GpuBroker:
         self._links = {}        # (conn, channel, consumer tag) -> link id (remote consumers)
         self._get_links = {}    # (vhost, queue) -> get link id (Basic.Get of remote queues)
         self._get_wait = {}     # pull id -> (conn, channel, no_ack, link id)
-        self._dev_gets = {}     # Basic.Gets queued on the device: id -> (conn, channel, queue slot, no_ack, vhost, queue)
+        self._dev_gets = {}     # Basic.Gets queued on the device: id -> (conn, channel, queue slot, no_ack, vhost,
+        #                         queue, resume: the answer unpauses the connection)
+        self._dget_ctx = False  # handling a step-decoded Basic.Get (its connection is not paused)
         self._get_holders = {}  # get link id -> {(conn, channel)} holding unacked Get messages
         self._get_used = {}     # get link id -> monotonic time of its last Get
         self._pull_seq = 0
@@ -507,12 +509,12 @@ class GpuBroker:
             if kind == FE_GET and (e[2] & 0xFFFFFFFF) in (GS_OK, GS_EMPTY, GS_RETRY, GS_GONE):
                 self._get_answer(conn, e[2], e[3])
                 continue
-            if kind == FE_CTRL and self._fast_get(conn, e[4]):
+            if kind == FE_CTRL and self._fast_get(conn, e[4], resume=e[2] != 1):
                 continue
             rest.append(e)
         return rest
 
-    def _fast_get(self, conn, raw):
+    def _fast_get(self, conn, raw, resume=True):
         c = self.conns.get(conn)
         if c is None or c.state != "open" or len(raw) < 11:
             return False
@@ -528,7 +530,7 @@ class GpuBroker:
         if q is None or q.exclusive_owner not in (-1, c.id) or q.owner != p.rank:
             return False   # errors and remote queues: the locked path
         gid = self._next_get = getattr(self, "_next_get", 0) + 1
-        self._dev_gets[gid] = (c.id, ch, q.slot, bool(m.no_ack), pc.vhost, q.name)
+        self._dev_gets[gid] = (c.id, ch, q.slot, bool(m.no_ack), pc.vhost, q.name, resume)
         self.fe.queue_get(c.id, p.chslot(c.id, ch), q.slot, int(bool(m.no_ack)), gid)
         self.stats["device_gets"] = self.stats.get("device_gets", 0) + 1
         return True
@@ -568,8 +570,8 @@ class GpuBroker:
                     self._flush(c, direct=True)   # Connection.OpenOk: no device traffic yet
                     self.fe.set_heartbeat(conn, c.heartbeat)
                     self.fe.set_data_mode(conn, rest)
-            elif kind == FE_CTRL:
-                ctrl.append((conn, data))
+            elif kind == FE_CTRL:   # (a == 1: a Basic.Get its step decoded but could not serve)
+                ctrl.append((conn, data, a == 1))
             elif kind == FE_TXBUF:
                 txbuf.append((conn, a, data))
             elif kind == FE_EVENT:
@@ -1099,17 +1101,24 @@ class GpuBroker:
             elif status & SS_TOO_LARGE:
                 self._conn_close(c, C.FRAME_ERROR, "command exceeds the server's limits")
             # SS_OVERFLOW is a per-step capacity limit: the rest stays in the carry
-        for conn, raw in ctrl:
+        for item in ctrl:
+            conn, raw = item[0], item[1]
+            # a step-decoded Basic.Get handed to the host did not pause its connection: its
+            # answer must not resume one another command paused meanwhile
+            dget = len(item) > 2 and item[2]
             c = self.conns.get(conn)
             if c is None:
                 continue
             deferred = False
             if c.state == "open":
+                self._dget_ctx = dget
                 try:
                     deferred = self._control(c, raw) == "deferred"
                 except _Hard as e:
                     self._conn_close(c, e.code, e.text, e.cls, e.mid)
-            if c.state == "open" and not deferred:
+                finally:
+                    self._dget_ctx = False
+            if c.state == "open" and not deferred and not dget:
                 self._unpause(conn)
         return had_input or had_egress or bool(ctrl) or cnt.get("n_deliv", 0) > 0
 
@@ -1544,7 +1553,7 @@ class GpuBroker:
                 # served inside the next step (k_dequeue, ahead of the queue's consumers): no
                 # pipeline drain; the connection stays paused until FE_GET answers it
                 gid = self._next_get = getattr(self, "_next_get", 0) + 1
-                self._dev_gets[gid] = (c.id, ch, q.slot, bool(m.no_ack), vh, q.name)
+                self._dev_gets[gid] = (c.id, ch, q.slot, bool(m.no_ack), vh, q.name, not self._dget_ctx)
                 self.fe.queue_get(c.id, p.chslot(c.id, ch), q.slot, int(bool(m.no_ack)), gid)
                 self.stats["device_gets"] = self.stats.get("device_gets", 0) + 1
                 return "deferred"
@@ -1671,7 +1680,7 @@ class GpuBroker:
         if req is None or c is None or c.state != "open":
             return
         st, cnt = a & 0xFFFFFFFF, a >> 32
-        _, ch, slot, no_ack, vh, qname = req
+        _, ch, slot, no_ack, vh, qname, resume = req
         q = self.plane.queues.get((vh, qname))
         if st == GS_RETRY and (q is None or q.slot != slot or q.owner != self.plane.rank):
             st = GS_GONE   # deleted (or moved) while the Get waited: never resubmitted
@@ -1687,7 +1696,7 @@ class GpuBroker:
             self._chan_close(c, ch, C.RESOURCE_ERROR, "basic.get: " + (
                 "message exceeds the egress buffer" if st == GS_NO_SPACE else "channel delivery window full"), 60, 70)
         self._flush(c)
-        if c.state == "open":
+        if c.state == "open" and resume:
             self._unpause(conn)
 
     def _remote_get(self, c, ch, vh, q, m):

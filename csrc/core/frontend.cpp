@@ -1069,6 +1069,7 @@ void Frontend::finish_oldest(std::deque<Inflight>& inflight) {
         e.data.assign((const char*)cb + cr[k].off, cr[k].len);
       } else {
         e.kind = FE_CTRL;
+        e.a = (cr[k].seg & CTRL_DGET) ? 1 : 0;   // a step-decoded Basic.Get: connection not paused
         e.data.assign((const char*)cb + cr[k].off, cr[k].len);
       }
       post(std::move(e));

@@ -412,6 +412,7 @@ __global__ __launch_bounds__(1024) void k_stage(DS d) {
     if (tid == 0) {   // (per-parity scratch only: the link-ack counts and the id floor are
                       // reset by k_marks, in the step's routing half)
       d.ctr->n_grow = 0; d.tot[TS_NMOVE] = 0; d.tot[TS_NDEFER] = 0; d.tot[TS_TTL_BUDGET] = 0;
+      d.tot[TS_NDGET] = 0;
       *d.egress_budget = 0;
     }
     // connections whose control command the host has answered resume with this step (the
@@ -579,11 +580,49 @@ DEV uint4 seg_word(const u8* C, u32 cl, const u8* N, u32 c) {
   return make_uint4(v[0], v[1], v[2], v[3]);
 }
 
+// Basic.Get the step can serve itself: a named queue of the connection's vhost (the default
+// exchange's direct binding of that name), owned by this rank, not another connection's
+// exclusive queue.  An empty name (the channel's last declared queue) and every error case
+// go to the host.  Method args at b + p + 7: class, method, ticket, queue shortstr, bits.
+DEV bool dget_resolve(const DS& d, u32 conn, const u8* b, u32 p, u32 size, u32& q, u32& noack) {
+  if (size < 8) return false;
+  const u32 a = p + 7 + 6, n = b[a], end = p + 7 + size;
+  if (n == 0 || a + 1 + n + 1 > end) return false;
+  const u8* name = b + a + 1;
+  const u32 vh = d.conn_vhost[conn];
+  const u64 hk = exch_hash(vh, name, 0);   // the vhost's default exchange ("")
+  i32 xs = -1;
+  for (u32 j = 0; j <= d.xhash_mask; ++j) {
+    const u32 slot = (u32)(hk + j) & d.xhash_mask;
+    const i32 v = d.x_hval[slot];
+    if (v < 0) break;
+    if (d.x_hkey[slot] == hk) { xs = v; break; }
+  }
+  if (xs < 0 || d.x_type[xs] != EX_DIRECT) return false;
+  const u64 k = fnv1a64_dev(name, n) ^ (u64(xs) * 0x9E3779B97F4A7C15ULL);
+  for (u32 j = 0; j <= d.dhash_mask; ++j) {
+    const u32 s = (u32)(k + j) & d.dhash_mask;
+    const i32 ex = d.d_exch[s];
+    if (ex < 0) return false;
+    if (ex == xs && d.d_key[s] == k && word_eq(d.kpool + d.d_kb_off[s], d.d_kb_len[s], name, n)) {
+      if (d.d_q_n[s] != 1) return false;
+      const u32 qq = d.d_q[d.d_q_off[s]];
+      const u32 ex_owner = d.q_excl[qq];
+      if (!d.q_active[qq] || d.q_owner[qq] != d.my_rank || (ex_owner && ex_owner != conn + 1)) return false;
+      q = qq;
+      noack = b[a + 1 + n] & 1u;
+      return true;
+    }
+  }
+  return false;
+}
+
 DEV void frame_scan_seg(const DS& d, const u32 s) {
   __shared__ uint4 fs_pool[FS_POOL / 16];
   __shared__ u32 sc[FS_NT / 64 + 1];
   __shared__ u32 sh_m, sh_over, sh_ok, sh_nf, sh_stop, sh_brk;
   __shared__ u32 sh_cmd_base, sh_frag_base, sh_ncmd;
+  __shared__ u32 sh_get0, sh_gch, sh_gq, sh_gna, sh_gbase;   // Basic.Get: the segment's first, its key
 
   const u32 tid = threadIdx.x;
   const u32 conn = d.segs[s].conn;
@@ -909,9 +948,10 @@ DEV void frame_scan_seg(const DS& d, const u32 s) {
 
   // ---- (d) commands: each method frame walks its content frames
   for (u32 f = tid; f < nf; f += FS_NT) claim[f] = 0;
-  if (tid == 0) sh_stop = (nf << 3) | 7;  // (frame << 3) | reason; 7 = none
+  if (tid == 0) { sh_stop = (nf << 3) | 7; sh_get0 = INVALID; }  // (frame << 3) | reason; 7 = none
   __syncthreads();
-  // stop reasons: 0 = after control, 1 = incomplete, 2 = unexpected frame, 3 = frame error
+  // stop reasons: 0 = after control, 1 = incomplete, 2 = unexpected frame, 3 = frame error,
+  // 4 = before a command that may not follow the segment's Basic.Gets in one step
   for (u32 f = tid; f < nf; f += FS_NT) {
     u32 p = CPOS(f);
     FInfo fi = frame_at(b, p, L, fmax);
@@ -927,6 +967,10 @@ DEV void frame_scan_seg(const DS& d, const u32 s) {
     bool content = (cls == 60 && mid == 40);
     bool data = (cls == 60 && (mid == 40 || mid == 80 || mid == 90 || mid == 120)) && fi.ch != 0 &&
                 chan_lookup(d, conn, fi.ch) >= 0;
+    if (cls == 60 && mid == 70 && fi.ch != 0 && chan_lookup(d, conn, fi.ch) >= 0) {
+      u32 gq, gna;
+      if (dget_resolve(d, conn, b, p, fi.size, gq, gna)) { atomicMin(&sh_get0, f); continue; }
+    }
     if (!content) {
       if (!data) atomicMin(&sh_stop, ((f + 1) << 3) | 0);
       continue;
@@ -969,6 +1013,33 @@ DEV void frame_scan_seg(const DS& d, const u32 s) {
     if (fi.complete) atomicMin(&sh_stop, (f << 3) | 2);
   }
   __syncthreads();
+  if (sh_get0 != INVALID) {   // (block-uniform) the segment serves Basic.Gets in this step
+    // they all ask the same (channel, queue, no-ack) -- any two then answer alike, whichever
+    // is served first -- and nothing but such Gets follows the first in this step (an ack
+    // after a Get may name its delivery tag, which the step assigns later); the rest of the
+    // segment waits in the carry for the next step
+    const u32 g0 = sh_get0;
+    if (tid == g0 % FS_NT) {
+      const u32 p = CPOS(g0);
+      FInfo fi = frame_at(b, p, L, fmax);
+      u32 gq = 0, gna = 0;
+      dget_resolve(d, conn, b, p, fi.size, gq, gna);
+      sh_gch = fi.ch; sh_gq = gq; sh_gna = gna;
+    }
+    __syncthreads();
+    for (u32 f = g0 + 1 + tid; f < nf; f += FS_NT) {
+      const u32 p = CPOS(f);
+      if (b[p] != 1) continue;   // content and heartbeat frames go with their method / nothing
+      FInfo fi = frame_at(b, p, L, fmax);
+      bool same = false;
+      if (fi.complete && fi.size >= 4 && be16(b + p + 7) == 60 && be16(b + p + 9) == 70 && fi.ch == sh_gch) {
+        u32 gq, gna;
+        same = dget_resolve(d, conn, b, p, fi.size, gq, gna) && gq == sh_gq && gna == sh_gna;
+      }
+      if (!same) atomicMin(&sh_stop, (f << 3) | 4);
+    }
+    __syncthreads();
+  }
   FS_MARK(4);
   u32 stop = sh_stop;
   u32 kf = stop >> 3, reason = stop & 7;
@@ -989,6 +1060,7 @@ DEV void frame_scan_seg(const DS& d, const u32 s) {
     so.err_off = consumed;
   }
   if (over && reason != 0 && kf == nf) so.status |= SS_OVERFLOW;
+  if (reason == 4) so.status |= SS_OVERFLOW;   // the carry is re-presented to the next step
 
   FS_MARK(5);
   // ---- (e) emit commands for method frames < kf
@@ -1049,7 +1121,7 @@ DEV void frame_scan_seg(const DS& d, const u32 s) {
     // the same block scan as the command index (no grid-wide rank scan over the commands)
     Cmd c;
     FInfo fi;
-    u32 cls = 0, mid = 0, hp = 0;
+    u32 cls = 0, mid = 0, hp = 0, gq = 0, gna = 0;
     FInfo hi;
     if (f < kf) {
       p = CPOS(f);
@@ -1068,11 +1140,12 @@ DEV void frame_scan_seg(const DS& d, const u32 s) {
       const i32 chs = fi.ch ? chan_lookup(d, conn, fi.ch) : -1;
       c.pad[0] = (u32)chs;
       if (cls == 60 && mid == 40 && chs >= 0) c.kind = CK_PUBLISH;
+      else if (cls == 60 && mid == 70 && chs >= 0 && dget_resolve(d, conn, b, p, fi.size, gq, gna)) c.kind = CK_GET;
       else if (cls == 60 && mid == 80 && chs >= 0) c.kind = CK_ACK;
       else if (cls == 60 && mid == 90 && chs >= 0) c.kind = CK_REJECT;
       else if (cls == 60 && mid == 120 && chs >= 0) c.kind = CK_NACK;
       else c.kind = CK_CONTROL;
-      if (c.kind != CK_CONTROL && d.ch_tx[chs]) c.kind = CK_TXBUF;   // held by the host until Tx.Commit
+      if (c.kind != CK_CONTROL && c.kind != CK_GET && d.ch_tx[chs]) c.kind = CK_TXBUF;   // held until Tx.Commit
       if (cls == 60 && mid == 40) {
         hp = CPOS(f + 1);
         hi = frame_at(b, hp, L, fmax);
@@ -1088,6 +1161,16 @@ DEV void frame_scan_seg(const DS& d, const u32 s) {
     const u32 rpk = block_scan<FS_NT>(is_cmd | (is_pub << 11) | (is_ack << 22), sc, tpk);
     u32 fr = block_scan<FS_NT>(nfr, sc, tf);
     const u32 r = rpk & 0x7ffu, tcnt = tpk & 0x7ffu;
+    // the segment's Basic.Gets: a contiguous DGet range per chunk, in wire order
+    u32 gi = INVALID;
+    if (sh_get0 != INVALID) {   // (block-uniform)
+      const u32 is_get = is_cmd && c.kind == CK_GET;
+      u32 tg;
+      const u32 rg = block_scan<FS_NT>(is_get, sc, tg);
+      if (tid == 0) sh_gbase = tg ? atomicAdd(&d.tot[TS_NDGET], tg) : 0;
+      __syncthreads();
+      if (is_get) gi = sh_gbase + rg;
+    }
     if (is_cmd) {
       c.conn = conn;
       c.ch = fi.ch;
@@ -1119,6 +1202,16 @@ DEV void frame_scan_seg(const DS& d, const u32 s) {
       }
       c.raw_len = endp - p;
       const u32 ci = sh_cmd_base + run + r;
+      if (gi != INVALID) {
+        if (gi < DGET_MAX) {
+          DGet g;
+          g.conn = conn; g.chslot = c.pad[0]; g.q = gq; g.noack = gna;
+          g.raw_off = c.raw_off; g.raw_len = c.raw_len; g.seg = s; g.pad = 0;
+          d.dget[gi] = g;
+        } else {
+          c.kind = CK_CONTROL;   // the step's DGet list is full: the host serves it (not paused)
+        }
+      }
       d.cmds[ci] = c;
       // classification for the rank scan of the large-segment-count path (k_decode)
       d.cmd_is_pub[ci] = is_pub;
@@ -1132,7 +1225,7 @@ DEV void frame_scan_seg(const DS& d, const u32 s) {
         if (g == c.raw_len) {
           for (u32 k = 0; k < c.raw_len; ++k) d.ctrl[cbase + k] = b[p + k];
           rec.off = cbase; rec.len = c.raw_len;
-          rec.seg = c.kind == CK_TXBUF ? (CTRL_TXBUF | p) : s;
+          rec.seg = c.kind == CK_TXBUF ? (CTRL_TXBUF | p) : gi != INVALID ? (CTRL_DGET | s) : s;
         } else {   // control buffer full: an event, the host closes the connection (506)
           rec.off = INVALID; rec.len = 506; rec.seg = 0;
         }
@@ -1177,6 +1270,24 @@ __global__ __launch_bounds__(FS_NT) void k_frame_scan(DS d) {
     frame_scan_seg(d, s);
     __syncthreads();   // the next segment reuses the LDS
   }
+}
+
+// a Basic.Get the frame scan decoded that its step cannot serve (delivery window full, cold
+// queue head, step full, queue gone): its bytes go to the host as a control record flagged
+// CTRL_DGET -- the connection is not paused -- and the host serves it with a later step
+DEV void dget_to_host(const DS& d, const DGet& g) {
+  u32 cbase;
+  const u32 got = reserve_sat(&d.ctr->ctrl_bytes, g.raw_len, (u32)d.ctrl_cap, &cbase);
+  const u32 ri = atomicAdd(&d.ctr->n_ctrl, 1u);
+  CtrlRec rec;
+  rec.conn = g.conn;
+  if (got == g.raw_len) {
+    for (u32 k = 0; k < g.raw_len; ++k) d.ctrl[cbase + k] = d.work[g.raw_off + k];
+    rec.off = cbase; rec.len = g.raw_len; rec.seg = CTRL_DGET | g.seg;
+  } else {   // control buffer full: an event, the host closes the connection (506)
+    rec.off = INVALID; rec.len = 506; rec.seg = 0;
+  }
+  if (ri < d.seg_max * 2) d.ctrl_rec[ri] = rec;
 }
 
 // ============================================================================ K3 classify / decode
@@ -3258,6 +3369,7 @@ __global__ __launch_bounds__(256) void k_dequeue(DS d) {
     }
   }
   if (q >= d.q_max) return;
+  const u32 ndg = d.tot[TS_NDGET] < DGET_MAX ? d.tot[TS_NDGET] : DGET_MAX;   // Basic.Gets decoded this step
   if (!d.q_active[q]) {
     if (tid == 0) {
       d.q_nruns[q] = 0;
@@ -3266,12 +3378,18 @@ __global__ __launch_bounds__(256) void k_dequeue(DS d) {
       const u32 ng = d.in->nget < GET_STEP_MAX ? d.in->nget : GET_STEP_MAX;
       for (u32 i = 0; i < ng; ++i)
         if (d.get_req[i].q == q) d.get_out_h[i] = GetOut{GS_GONE, 0u};
+      for (u32 k = 0; k < ndg; ++k)
+        if (d.dget[k].q == q) dget_to_host(d, d.dget[k]);
     }
     return;
   }
   const bool nodisp = (d.in->flags & SF_NODISPATCH) != 0;
   if (nodisp && d.links && d.q_link_owner[q]) {   // a live link shadow: its acks could not travel
-    if (tid == 0) d.q_nruns[q] = 0;
+    if (tid == 0) {
+      d.q_nruns[q] = 0;
+      for (u32 k = 0; k < ndg; ++k)
+        if (d.dget[k].q == q) dget_to_host(d, d.dget[k]);
+    }
     return;
   }
   // agent-scope load: the requeue above (this block's thread 0) may have moved the head
@@ -3317,13 +3435,23 @@ __global__ __launch_bounds__(256) void k_dequeue(DS d) {
   // rendered as GetOk + header + body by k_render; EMPTY / RETRY / WINDOW_FULL go back
   // to the host through the step's host-mapped GetOut (the host initialised them RETRY)
   u32 ngr = 0;
-  if (d.in->nget) {   // kernel-uniform
+  if (d.in->nget || ndg) {   // kernel-uniform
     if (tid == 0) {
       const u32 ng = d.in->nget < GET_STEP_MAX ? d.in->nget : GET_STEP_MAX;
       const u64 clim = d.q_cold_lim[q];   // a cold head waits for the host's page-in (RETRY)
       u64 h = head;
-      for (u32 i = 0; i < ng; ++i) {
-        const GetReq rq = d.get_req[i];
+      // the host-staged requests (their connections were paused: nothing of theirs was
+      // decoded this step), then the step's own Basic.Gets in wire order
+      for (u32 i = 0; i < ng + ndg; ++i) {
+        const bool dev = i >= ng;
+        DGet dg;
+        GetReq rq;
+        if (dev) {
+          dg = d.dget[i - ng];
+          rq.conn = dg.conn; rq.chslot = dg.chslot; rq.q = dg.q; rq.noack = dg.noack;
+        } else {
+          rq = d.get_req[i];
+        }
         if (rq.q != q) continue;
         GetOut o;
         o.status = GS_RETRY;
@@ -3359,7 +3487,14 @@ __global__ __launch_bounds__(256) void k_dequeue(DS d) {
             o.msg_count = rn.cons;
           }
         }
-        d.get_out_h[i] = o;
+        if (!dev) {
+          d.get_out_h[i] = o;
+        } else if (o.status == GS_EMPTY && reserve_sat64(d.egress_budget, 13, d.egress_cap) == 13) {
+          atomicAdd(&d.conn_gempty[dg.conn], 1u);   // Basic.GetEmpty, rendered by render_confirms
+          d.conn_gempty_ch[dg.conn] = d.ch_num[dg.chslot];
+        } else if (o.status != GS_OK) {
+          dget_to_host(d, dg);
+        }
       }
       s_head = h;
       s_ngr = ngr;
@@ -3658,7 +3793,7 @@ __global__ void k_conn_sizes(DS d) {
     u32 l = d.conn_dlast[c];
     dl = d.dv_off[l] + d.dv_size[l] - d.dv_off[f];
   }
-  d.conn_total[c] = d.conn_ret_bytes[c] + conf + dl;
+  d.conn_total[c] = d.conn_ret_bytes[c] + conf + dl + 13u * d.conn_gempty[c];
 }
 
 // single block (c_max <= CONN_LAYOUT_MAX): k_conn_sizes + scan of conn_total + k_conn_out
@@ -3733,7 +3868,7 @@ __global__ __launch_bounds__(1024) void k_conn_layout(DS d) {
         u32 l = d.conn_dlast[c];
         dl = d.dv_off[l] + d.dv_size[l] - d.dv_off[f];
       }
-      total = d.conn_ret_bytes[c] + conf + dl;
+      total = d.conn_ret_bytes[c] + conf + dl + 13u * d.conn_gempty[c];
       d.conn_total[c] = total;
     }
     u32 all;
@@ -3913,6 +4048,17 @@ DEV void render_deliv(const DS& d, u32 i) {
 // may resend a nacked message, it never loses an acked one (FrameStage.scala:571-596
 // confirms everything it asked the entities to store; drops are ours: ring full, no memory)
 DEV void render_confirms(const DS& d, u32 c) {
+  const u32 ng = d.conn_gempty[c];
+  if (ng) {   // Basic.GetEmpty (60/72, empty cluster-id) frames close the connection's region
+    u8* e = (u8*)d.in->egress + (u64)d.conn_base[c] + d.conn_total[c] - 13u * ng;
+    const u32 chno = d.conn_gempty_ch[c];
+    for (u32 k = 0; k < ng; ++k, e += 13) {
+      put_frame_hdr(e, 1, chno, 5);
+      wr16(e + 7, 60); wr16(e + 9, 72);
+      e[11] = 0;
+      e[12] = 0xCE;
+    }
+  }
   u32 conf = d.conn_conf_bytes[c];
   u8* o = (u8*)d.in->egress + (u64)d.conn_base[c] + d.conn_ret_bytes[c];
   u32 p = 0;
@@ -4053,6 +4199,7 @@ __global__ __launch_bounds__(256) void k_post(DS d, u32 fin) {
     d.conn_dlast[i] = INVALID;
     d.conn_ret_bytes[i] = 0;
     d.conn_ret_min[i] = INVALID;
+    d.conn_gempty[i] = 0;
   }
   if (!fin) return;
   host_out_copies(d, i, (u64)gridDim.x * blockDim.x);
@@ -4098,6 +4245,7 @@ DEV void final_step(const DS& d) {
   c->msg_free_top = *d.msg_free_top;
   c->n_live_msgs = d.msg_max - *d.msg_free_top;
   c->live_bytes = *d.live_bytes;
+  c->n_dget = d.tot[TS_NDGET];
   if (d.links)
     for (u32 r = 0; r < d.world; ++r) d.xchg[XC_ACK_N + r] = d.lk_cnt[r] < d.lk_cap ? d.lk_cnt[r] : d.lk_cap;
   *d.ctr_host = *c;

@@ -20,6 +20,8 @@ enum : u32 {
   CK_CONTROL = 5,   // everything else: bytes go to the host control plane
   CK_TXBUF = 6,     // publish / ack / nack / reject on a transactional channel: raw bytes
                     // to the host (buffered until Tx.Commit), connection not paused
+  CK_GET = 7,       // Basic.Get (60/70) of a local queue named in the command: served in the
+                    // step (DGet list), connection not paused
 };
 
 // ---- exchange types (constants.py EX_*)

@@ -50,8 +50,16 @@ enum : u32 {
   TS_NRACK = 65,                        // link acks received this step (k_import_route -> link_ack_one)
   TS_PK_TICKET = 66,                    // k_pack_scan finished-tile ticket (last tile: prefixes)
   TS_POST_TICKET = 67,                  // k_post finished-block ticket (last block: final_step)
-  TS_NCADEF = 68                        // channels k_chan_advance deferred (store-record budget)
+  TS_NCADEF = 68,                       // channels k_chan_advance deferred (store-record budget)
+  TS_NDGET = 69                         // Basic.Get commands the frame scan decoded (DGet list)
 };
+
+// Basic.Get decoded from a connection's bytes by the frame scan (no host round trip): served
+// by k_dequeue with the host-staged requests; GetOk rendered like a delivery, GetEmpty
+// rendered at the end of the connection's egress; a Get the step cannot serve (window full,
+// cold head, step full) goes to the host as a control record (CTRL_DGET) and is served there
+#define DGET_MAX 4096
+struct DGet { u32 conn, chslot, q, noack, raw_off, raw_len, seg, pad; };
 
 // remote-consumer link ack (X3): the connection side consumed message `xid` (owner's
 // epoch << 40 | owner's delivery tag) of shadow queue `tq`
@@ -267,6 +275,10 @@ struct DS {
   u32 xfer_desc_max;        // records per step, all destinations
   u64 xfer_bytes;           // payload bytes per step, all destinations
   u32* q_owner;             // [q_max] owning rank
+  u32* q_excl;              // [q_max] exclusive owner connection + 1 (0: not exclusive)
+  DGet* dget;               // per parity [DGET_MAX]: Basic.Get commands of the step (tot[TS_NDGET])
+  u32* conn_gempty;         // per connection: Basic.GetEmpty frames to render this step
+  u32* conn_gempty_ch;      // per connection: their channel number
   u32* pub_rmask;           // [pub_cap] remote ranks owning >= 1 routed queue
   u32* xp_cnt;              // [world][pub_cap] record for rank r?
   u32* xp_cnt_off;

@@ -317,6 +317,10 @@ class Engine {
     d_.conn_ret_min = (u32*)dev("conn_ret_min", 4ull * d_.c_max);
     u64 xw = d_.world > 1 ? (u64)d_.world * d_.pub_cap : 64;
     d_.q_owner = (u32*)dev("q_owner", 4ull * d_.q_max);
+    d_.q_excl = (u32*)dev("q_excl", 4ull * d_.q_max);
+    d_.dget = (DGet*)dev("dget", sizeof(DGet) * (u64)DGET_MAX);
+    d_.conn_gempty = (u32*)dev("conn_gempty", 4ull * d_.c_max);
+    d_.conn_gempty_ch = (u32*)dev("conn_gempty_ch", 4ull * d_.c_max);
     d_.pub_rmask = (u32*)dev("pub_rmask", 4ull * d_.pub_cap);
     d_.xp_cnt = nullptr;   // (per-rank count arrays: k_pack_scan counts in registers)
     d_.xp_cnt_off = (u32*)dev("xp_cnt_off", 4 * xw);
@@ -515,6 +519,7 @@ class Engine {
     dup(&DS::pub_keyvec, "pub_keyvec", (u64)d_.pub_cap * TOPIC_K + 64);
     dup(&DS::pub_kwoff, "pub_kwoff", 2ull * TOPIC_WORDS * d_.pub_cap + 64);
     dup(&DS::acks, "acks", sizeof(Ack) * (u64)d_.ack_max);
+    dup(&DS::dget, "dget", sizeof(DGet) * (u64)DGET_MAX);
     for (int p = 0; p < 2; ++p) {
       DS io = d_;
       if (p == 1)
@@ -1992,7 +1997,7 @@ class Engine {
     F(n_dropped_nomem); F(n_expired); F(n_routed_msgs); F(n_unknown_exchange); F(n_ring_full);
     F(n_acked); F(log_head); F(log_tail); F(msg_free_top); F(n_live_msgs);
     F(n_persist); F(n_consumed); F(persist_used); F(n_persist_overflow);
-    F(live_bytes); F(n_grow);
+    F(live_bytes); F(n_grow); F(n_dget);
 #undef F
     std::vector<u32> lat(c.lat_hist, c.lat_hist + LAT_BINS);
     o["lat_hist"] = lat;

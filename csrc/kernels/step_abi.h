@@ -27,6 +27,8 @@ enum : u32 {
 };
 
 #define CTRL_TXBUF 0x80000000u   // CtrlRec.seg flag: CK_TXBUF record, low bits = wire position
+#define CTRL_DGET 0x40000000u    // CtrlRec.seg flag: a Basic.Get the step decoded but could not
+                                 // serve (the connection is not paused: the host serves it)
 
 struct SegIn {          // host -> device, one per connection with bytes this step
   u32 conn;
@@ -75,7 +77,8 @@ struct Counters {       // per-step counters (device -> host)
   u32 msg_free_top, n_live_msgs;
   i64 live_bytes;       // body-log slot bytes of live messages (exact, unlike head - tail)
   u32 n_grow;           // rings grown this step (grow_host list of RingMove)
-  u32 pad[3];
+  u32 n_dget;           // Basic.Gets decoded (and served or handed to the host) this step
+  u32 pad[2];
 };
 
 struct CtrlRec { u32 conn; u32 off; u32 len; u32 seg; };

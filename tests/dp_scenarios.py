@@ -161,6 +161,32 @@ def sc_basic_get(dp):
             {2: ack_frame(1, 0, multiple=True)}, {}]
 
 
+def get_cmd(ch, queue, no_ack):
+    return render_command(ch, Method("basic.get", ticket=0, queue=queue, no_ack=no_ack))
+
+
+def sc_wire_get(dp):
+    """Basic.Get from the connection's bytes, served by the step itself: pipelined Gets of
+    one (channel, queue, no-ack) in one step; a different Get or an ack after them waits
+    for the next step (carry); GetEmpty on a drained queue; an unnamed queue, another
+    connection's exclusive queue and a full delivery window go to the host."""
+    dp.declare_queue(VH, "wg", ttl_ms=0)
+    dp.declare_queue(VH, "wx", exclusive_owner=1)
+    dp.open_connection(1, VH)
+    dp.open_channel(1, 1)
+    dp.open_connection(2, VH)
+    dp.open_channel(2, 1)
+    dp.open_channel(2, 2)
+    pubs = publish_stream(7, "", lambda i: "wg", 700, seed=21)
+    burst = (get_cmd(1, "wg", True) * 3 + get_cmd(1, "wg", False) * 2 + ack_frame(1, 5, multiple=True)
+             + get_cmd(2, "wg", True))
+    return [{1: pubs}, {2: burst}, {}, {}, {},
+            {2: get_cmd(1, "wg", True) * 2},                        # 1 left: GetOk then GetEmpty
+            {2: get_cmd(2, "wx", True)},                            # another connection's exclusive queue
+            {"__unpause__": [2], 2: get_cmd(1, "", True)},          # unnamed: the host's
+            {"__unpause__": [2]}]
+
+
 def sc_tx_hold(dp):
     dp.declare_queue(VH, "txh")
     dp.open_connection(1, VH)
@@ -266,6 +292,7 @@ SCENARIOS = {
     "window_wrap": sc_window_wrap,
     "tx_hold": sc_tx_hold,
     "basic_get": sc_basic_get,
+    "wire_get": sc_wire_get,
     "direct_split": sc_direct_split,
     "default_exchange": sc_default_exchange,
     "topic": sc_topic,

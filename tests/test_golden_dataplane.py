@@ -2,7 +2,7 @@
 
 from collections import defaultdict
 
-from dp_scenarios import SCENARIOS, run
+from dp_scenarios import SCENARIOS, VH, run
 
 from chanamq_amd.engine.golden import GoldenDataPlane
 from chanamq_amd.engine.layout import SS_CTRL, SS_FRAME_ERROR
@@ -170,3 +170,23 @@ def test_mixed_multiple_settles_first_cover_wins():
     assert [c.body for c in red[:7]] == [first[t] for t in (1, 2, 3, 4, 11, 13, 14)]
     assert not any(c.body in (first[9], first[10]) for c in d[16:])
     assert g.memory_in_use() == 0
+
+
+def test_wire_basic_get_served_by_the_step():
+    """Basic.Get decoded from the connection's bytes (no host round trip): pipelined Gets of
+    one key in one step, the next key / an ack wait a step, GetEmpty rendered in egress,
+    the host gets only what the step cannot decide (unnamed / exclusive queue)."""
+    from chanamq_amd.protocol.codec import CommandAssembler, FrameParser
+    g, outs, pc = run_sc("wire_get")
+
+    def names(o):
+        fp, ca = FrameParser(), CommandAssembler()
+        cmds = [ca.feed(f) for f in fp.feed(o["egress"].get(2, b""))]
+        return [(c.channel, c.method.name, getattr(c.method, "delivery_tag", None)) for c in cmds if c and c.method]
+    assert names(outs[1]) == [(1, "basic.get_ok", 1), (1, "basic.get_ok", 2), (1, "basic.get_ok", 3)]
+    assert names(outs[2]) == [(1, "basic.get_ok", 4), (1, "basic.get_ok", 5)]   # (the ack waits a step)
+    assert names(outs[3]) == [(2, "basic.get_ok", 1)]
+    assert names(outs[5]) == [(1, "basic.get_ok", 6), (1, "basic.get_empty", None)]
+    assert outs[1]["ctrl"] == [] and outs[5]["ctrl"] == []
+    assert [len(c) for c in outs[6]["ctrl"]] == [2] and [len(c) for c in outs[7]["ctrl"]] == [2]
+    assert g.message_count(g.queues[(VH, "wg")].slot) == 0

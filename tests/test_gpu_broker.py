@@ -186,6 +186,33 @@ def test_basic_get_ack_nack_and_empty(broker):
     c.close()
 
 
+def test_pipelined_basic_gets_answered_in_order(broker):
+    """Many Basic.Gets in flight on one channel (served by the steps that decode them on
+    the device planes): every message once, in queue order, then GetEmpty; a Get of an
+    unnamed queue (the channel's last declared one) still works through the host."""
+    p = conn(broker)
+    ch = p.channel()
+    ch.queue_declare("pg")
+    for i in range(100):
+        ch.basic_publish("", "pg", f"m{i:03d}".encode())
+    ch.queue_declare("pg2")
+    g = conn(broker)
+    gch = g.channel()
+    got, empty = [], 0
+    for _ in range(3):
+        ok, e = gch.basic_get_many("pg", 40, no_ack=True)
+        got += ok
+        empty += e
+    assert [d.body for d in got] == [f"m{i:03d}".encode() for i in range(100)] and empty == 20
+    assert [d.method.message_count for d in got[:3]] == [99, 98, 97]
+    gch.queue_declare("pg2")
+    ch.basic_publish("", "pg2", b"last")
+    d = gch.basic_get("", no_ack=True)
+    assert d is not None and d.body == b"last"
+    p.close()
+    g.close()
+
+
 def test_basic_get_races_queue_delete(broker):
     """Basic.Gets racing a Queue.Delete on another connection: every Get is
     answered (GetOk / GetEmpty, or the channel closed 404 once the queue is gone) -- never
