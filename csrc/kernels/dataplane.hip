@@ -546,19 +546,18 @@ DEV bool big_publish(const DS& d, u32 msize, u32 hsize, u64 bsz, u32 fmax) {
   return (u64)msize + 8 + hsize + 8 + bsz + 8 * nb > d.carry_cap;
 }
 
-// bytes [sh, sh + 16) of the 32 bytes a:b (sh 0..15): four dword funnel shifts
+// bytes [sh, sh + 16) of the 32 bytes a:b (sh 0..15): a two-level word barrel shift (by 2
+// words, then 1 -- named registers and selects: an indexed word array here was lowered to
+// a scratch-memory table, 48 bytes per lane), then four dword funnel shifts
 DEV uint4 shift_pair(uint4 a, uint4 b, u32 sh) {
-  const u32 w[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
   const u32 q = sh >> 2, r = sh & 3;
-  u32 o[4];
-#pragma unroll
-  for (u32 i = 0; i < 4; ++i) {
-    // (selects over the eight words: q is wave-uniform only per segment)
-    const u32 lo = q == 0 ? w[i] : q == 1 ? w[i + 1] : q == 2 ? w[i + 2] : w[i + 3];
-    const u32 hi = q == 0 ? w[i + 1] : q == 1 ? w[i + 2] : q == 2 ? w[i + 3] : w[i + 4];
-    o[i] = r ? __builtin_amdgcn_alignbyte(hi, lo, r) : lo;
-  }
-  return make_uint4(o[0], o[1], o[2], o[3]);
+  const bool q2 = (q & 2) != 0, q1 = (q & 1) != 0;
+  const u32 s0 = q2 ? a.z : a.x, s1 = q2 ? a.w : a.y, s2 = q2 ? b.x : a.z;
+  const u32 s3 = q2 ? b.y : a.w, s4 = q2 ? b.z : b.x, s5 = q2 ? b.w : b.y;
+  const u32 w0 = q1 ? s1 : s0, w1 = q1 ? s2 : s1, w2 = q1 ? s3 : s2, w3 = q1 ? s4 : s3, w4 = q1 ? s5 : s4;
+  if (!r) return make_uint4(w0, w1, w2, w3);
+  return make_uint4(__builtin_amdgcn_alignbyte(w1, w0, r), __builtin_amdgcn_alignbyte(w2, w1, r),
+                    __builtin_amdgcn_alignbyte(w3, w2, r), __builtin_amdgcn_alignbyte(w4, w3, r));
 }
 // word c (bytes [16c, 16c + 16)) of a segment = the connection's carry (cl bytes, C
 // 16-aligned) then its new ingress bytes (N 16-aligned; reading up to 32 bytes past them
@@ -572,6 +571,7 @@ DEV uint4 seg_word(const u8* C, u32 cl, const u8* N, u32 c) {
     return sh ? shift_pair(a, ((const uint4*)N)[k + 1], sh) : a;
   }
   u32 v[4] = {0, 0, 0, 0};   // the word holding the carry's end and the new bytes' start
+#pragma unroll
   for (u32 j = 0; j < 16; ++j) {
     const u32 i = b0 + j;
     const u32 x = i < cl ? C[i] : N[i - cl];
@@ -1275,7 +1275,8 @@ __global__ __launch_bounds__(FS_NT) void k_frame_scan(DS d) {
 // a Basic.Get the frame scan decoded that its step cannot serve (delivery window full, cold
 // queue head, step full, queue gone): its bytes go to the host as a control record flagged
 // CTRL_DGET -- the connection is not paused -- and the host serves it with a later step
-DEV void dget_to_host(const DS& d, const DGet& g) {
+DEV void dget_to_host(const DS& d, u32 k) {
+  const DGet g = d.dget[k];
   u32 cbase;
   const u32 got = reserve_sat(&d.ctr->ctrl_bytes, g.raw_len, (u32)d.ctrl_cap, &cbase);
   const u32 ri = atomicAdd(&d.ctr->n_ctrl, 1u);
@@ -2324,7 +2325,10 @@ DEV void route_one(const DS& d, u32 p, u32 lane) {
 #define ROUTE_WPE 8     // or 4 (one block per CU, no spill): A/B through CHANAMQ_DP_SO
 #endif
 __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(ROUTE_WPE))) void k_route(DS d) {
-  const u32 lane = lane_id(), w = threadIdx.x >> 6;
+  // the wave index as a scalar: each wave's publish index, and every pointer derived from
+  // it, then lives in SGPRs (as a VGPR value it pushed the wave router past 64 VGPRs and
+  // into scratch)
+  const u32 lane = lane_id(), w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const u32 lo = d.tot[TS_RANGE_LO];
   u32 n = d.tot[TS_RANGE_HI];
   if (n > d.pub_cap) n = d.pub_cap;
@@ -2414,7 +2418,9 @@ __global__ __launch_bounds__(256) void k_route_store(DS d, u32 marks) {
   u32 n = d.tot[TS_RANGE_HI];
   if (n > d.pub_cap) n = d.pub_cap;
   const u32 nw = (gridDim.x * blockDim.x) >> 6;
-  for (u32 p = d.tot[TS_RANGE_LO] + ((blockIdx.x * blockDim.x + threadIdx.x) >> 6); p < n; p += nw) {
+  // (wave-uniform, made scalar: the publish's loads and pointers stay in SGPRs)
+  const u32 wave = __builtin_amdgcn_readfirstlane((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+  for (u32 p = d.tot[TS_RANGE_LO] + wave; p < n; p += nw) {
     // the store's loads go out before pass 1's pair stores (which the compiler cannot
     // move them past: every table is a global pointer of DS), one round instead of two
     const Pub pb = d.pubs[p];
@@ -3379,7 +3385,7 @@ __global__ __launch_bounds__(256) void k_dequeue(DS d) {
       for (u32 i = 0; i < ng; ++i)
         if (d.get_req[i].q == q) d.get_out_h[i] = GetOut{GS_GONE, 0u};
       for (u32 k = 0; k < ndg; ++k)
-        if (d.dget[k].q == q) dget_to_host(d, d.dget[k]);
+        if (d.dget[k].q == q) dget_to_host(d, k);
     }
     return;
   }
@@ -3388,7 +3394,7 @@ __global__ __launch_bounds__(256) void k_dequeue(DS d) {
     if (tid == 0) {
       d.q_nruns[q] = 0;
       for (u32 k = 0; k < ndg; ++k)
-        if (d.dget[k].q == q) dget_to_host(d, d.dget[k]);
+        if (d.dget[k].q == q) dget_to_host(d, k);
     }
     return;
   }
@@ -3444,11 +3450,10 @@ __global__ __launch_bounds__(256) void k_dequeue(DS d) {
       // decoded this step), then the step's own Basic.Gets in wire order
       for (u32 i = 0; i < ng + ndg; ++i) {
         const bool dev = i >= ng;
-        DGet dg;
+        const u32 dk = dev ? i - ng : 0u;
         GetReq rq;
         if (dev) {
-          dg = d.dget[i - ng];
-          rq.conn = dg.conn; rq.chslot = dg.chslot; rq.q = dg.q; rq.noack = dg.noack;
+          rq.conn = d.dget[dk].conn; rq.chslot = d.dget[dk].chslot; rq.q = d.dget[dk].q; rq.noack = d.dget[dk].noack;
         } else {
           rq = d.get_req[i];
         }
@@ -3490,10 +3495,10 @@ __global__ __launch_bounds__(256) void k_dequeue(DS d) {
         if (!dev) {
           d.get_out_h[i] = o;
         } else if (o.status == GS_EMPTY && reserve_sat64(d.egress_budget, 13, d.egress_cap) == 13) {
-          atomicAdd(&d.conn_gempty[dg.conn], 1u);   // Basic.GetEmpty, rendered by render_confirms
-          d.conn_gempty_ch[dg.conn] = d.ch_num[dg.chslot];
+          atomicAdd(&d.conn_gempty[rq.conn], 1u);   // Basic.GetEmpty, rendered by render_confirms
+          d.conn_gempty_ch[rq.conn] = d.ch_num[rq.chslot];
         } else if (o.status != GS_OK) {
-          dget_to_host(d, dg);
+          dget_to_host(d, dk);
         }
       }
       s_head = h;
@@ -4151,7 +4156,8 @@ __global__ __launch_bounds__(256) void k_render(DS d, u32 n_rc) {
   if (blockIdx.x < n_rc) { render_rc(d, blockIdx.x); return; }
   const u32 n = d.ctr->n_deliv;
   const u32 nw = ((gridDim.x - n_rc) * blockDim.x) >> 6;
-  for (u32 i = ((blockIdx.x - n_rc) * blockDim.x + threadIdx.x) >> 6; i < n; i += nw) render_deliv(d, i);
+  const u32 wave = __builtin_amdgcn_readfirstlane(((blockIdx.x - n_rc) * blockDim.x + threadIdx.x) >> 6);
+  for (u32 i = wave; i < n; i += nw) render_deliv(d, i);
 }
 DEV void render_rc(const DS& d, u32 blk) {
   if (blk >= RC_RET_BLOCKS) {
