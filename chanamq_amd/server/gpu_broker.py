@@ -557,8 +557,8 @@ class GpuBroker:
                 if c is not None:
                     c.state = "gone"
                     self._drop(c)
-                else:
-                    self.fe.close(conn)
+                else:   # (a: the slot's generation -- it may have been freed and reused since)
+                    self.fe.close(conn, a)
             elif kind == FE_HOST:
                 c = self.conns.get(conn)
                 data = self.fe.take(conn)

@@ -269,7 +269,7 @@ PYBIND11_MODULE(_core, m) {
       .def("set_host_mode", &Frontend::set_host_mode)
       .def("set_heartbeat", &Frontend::set_heartbeat)
       .def("set_read_cap", &Frontend::set_read_cap)
-      .def("close", &Frontend::close)
+      .def("close", &Frontend::close, py::arg("conn"), py::arg("gen") = -1)
       .def("kick", &Frontend::kick)
       .def("pause", &Frontend::pause, py::call_guard<py::gil_scoped_release>())
       .def("resume", &Frontend::resume, py::call_guard<py::gil_scoped_release>())

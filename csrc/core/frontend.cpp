@@ -432,8 +432,9 @@ void Frontend::set_read_cap(u32 conn, u64 bytes) {
   if (conn < c_max_) conns_[conn]->read_cap = bytes;
 }
 
-void Frontend::close(u32 conn) {
+void Frontend::close(u32 conn, i64 gen) {
   if (conn == 0 || conn >= c_max_) return;
+  if (gen >= 0 && conns_[conn]->gen.load() != (u32)gen) return;   // a stale close: slot freed since
   FeIo& io = *io_[conns_[conn]->io];
   {
     std::lock_guard<std::mutex> g(io.qmu);
@@ -667,7 +668,7 @@ void Frontend::drop(FeConn& c, bool notify) {
   ::close(c.fd);
   c.fd = -1;
   c.mode = M_DEAD;
-  c.gen.fetch_add(1);
+  const u32 g2 = c.gen.fetch_add(1) + 1;
   c.read_cap = 0;
   c.out.clear();
   c.out_pos = 0;
@@ -678,6 +679,7 @@ void Frontend::drop(FeConn& c, bool notify) {
     FeEvent e;
     e.kind = FE_CLOSED;
     e.conn = c.id;
+    e.a = g2;   // the control plane's close(conn, gen) of this slot is stale once it moved on
     post(std::move(e));
   }
 }
@@ -741,6 +743,7 @@ void Frontend::io_loop(int i) {
       FeConn& c = *conns_[id];
       {
         std::lock_guard<std::mutex> g(c.mu);
+        if (c.mode == M_FREE) continue;   // closed twice: the slot is freed (or reused) once
         if (c.fd >= 0) {
           write_some(c);
           epoll_ctl(io.epfd, EPOLL_CTL_DEL, c.fd, nullptr);

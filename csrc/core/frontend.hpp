@@ -131,7 +131,9 @@ class Frontend {
   void set_host_mode(u32 conn);                          // bytes go to the control plane again
   void set_heartbeat(u32 conn, u32 seconds);
   void set_read_cap(u32 conn, u64 bytes);                // per-step read budget (0: per_conn_read)
-  void close(u32 conn);                                  // flush, close the socket, free the slot
+  // flush, close the socket, free the slot; gen >= 0: only if the slot's generation is
+  // still gen (an FE_CLOSED event's a: the slot may have been freed and reused since)
+  void close(u32 conn, i64 gen = -1);
   void kick(u32 conn);                                   // unpaused: re-present its device carry
   // control reply of a command handled while steps keep running (no pause): written after
   // the egress of every step submitted so far, so a Basic.CancelOk / Channel.CloseOk never
