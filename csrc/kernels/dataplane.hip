@@ -709,18 +709,27 @@ DEV void frame_scan_seg(const DS& d, const u32 s) {
     if (use_am) {   // candidate screen of the segment into LDS (fused k_cand), coalesced reads
       const uint4* W = (const uint4*)bg;   // 16-aligned; >= 32 bytes of padding after the segment
       uint4* const WD = (uint4*)(d.work + wbase);
-      for (u32 cc = tid; cc < nm; cc += FS_NT * 4) {
+      // every word is read from memory once: a lane's next word (the screen looks 16 bytes
+      // ahead) is its neighbour lane's word, the wave's last lane reads it itself -- all 256
+      // segment blocks screen at once, so the double read made this phase HBM-bound
+      const u32 ln = lane_id();
+      // (wave-uniform trip count: every lane of a wave takes part in the shuffles)
+      for (u32 cb = tid - ln; cb < nm; cb += FS_NT * 4) {
+        const u32 cc = cb + ln;
         uint4 x[4], y[4];
 #pragma unroll
         for (int k = 0; k < 4; ++k) {   // every load of the batch in flight before any use
-          const u32 c = cc + k * FS_NT;
-          if (c < nm) {
-            if (fuse) { x[k] = seg_word(seg_C, seg_cl, seg_N, c); y[k] = seg_word(seg_C, seg_cl, seg_N, c + 1); }
-            else { x[k] = W[c]; y[k] = W[c + 1]; }
-          }
+          const u32 c = cc + k * FS_NT;   // (c == nm: the word after the segment, read as slack)
+          x[k] = make_uint4(0, 0, 0, 0);
+          y[k] = make_uint4(0, 0, 0, 0);
+          if (c <= nm) x[k] = fuse ? seg_word(seg_C, seg_cl, seg_N, c) : W[c];
+          if (ln == 63 && c < nm) y[k] = fuse ? seg_word(seg_C, seg_cl, seg_N, c + 1) : W[c + 1];
         }
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
+          const uint4 nx = make_uint4(__shfl_down(x[k].x, 1), __shfl_down(x[k].y, 1), __shfl_down(x[k].z, 1),
+                                      __shfl_down(x[k].w, 1));
+          if (ln != 63) y[k] = nx;
           const u32 c = cc + k * FS_NT;
           if (c < nm) {
             amask[c] = (u16)cand_bits(x[k], y[k], fmg);
