@@ -1076,9 +1076,11 @@ DEV void frame_scan_seg(const DS& d, const u32 s) {
   u32 run = 0, frun = 0;
   if (tid == 0) { sh_cmd_base = INVALID; sh_ncmd = 0; }
   __syncthreads();
-  // count first
+  // count first -- unless the commands fit one emit chunk (the common case): then the emit
+  // pass reserves them itself, from the scans it runs anyway
+  const bool one = kf <= FS_NT;   // (block-uniform)
   u32 my_cmds = 0, my_frags = 0;
-  for (u32 f = tid; f < kf; f += FS_NT) {
+  for (u32 f = tid; f < kf && !one; f += FS_NT) {
     u32 p = CPOS(f);
     if (b[p] != 1) continue;
     ++my_cmds;
@@ -1088,13 +1090,15 @@ DEV void frame_scan_seg(const DS& d, const u32 s) {
       while (e < kf && b[CPOS(e)] == 3) { ++my_frags; ++e; }
     }
   }
-  u32 tc, tfr;
-  block_scan<FS_NT>(my_cmds, sc, tc);
-  block_scan<FS_NT>(my_frags, sc, tfr);
+  u32 tc = 0, tfr = 0;
+  if (!one) {
+    block_scan<FS_NT>(my_cmds, sc, tc);
+    block_scan<FS_NT>(my_frags, sc, tfr);
+  }
   // one uncontended atomicAdd per block (a CAS loop here serialises all blocks);
   // on overflow the reserved in-range slots are filled with CK_NONE and the whole
   // segment is carried to the next step
-  if (tid == 0) {
+  if (!one && tid == 0) {
     u32 cb = tc ? atomicAdd(&d.ctr->n_cmds, tc) : 0;
     u32 fb = tfr ? atomicAdd(&d.ctr->n_frags, tfr) : 0;
     sh_frag_base = fb;
@@ -1170,6 +1174,33 @@ DEV void frame_scan_seg(const DS& d, const u32 s) {
     const u32 rpk = block_scan<FS_NT>(is_cmd | (is_pub << 11) | (is_ack << 22), sc, tpk);
     u32 fr = block_scan<FS_NT>(nfr, sc, tf);
     const u32 r = rpk & 0x7ffu, tcnt = tpk & 0x7ffu;
+    if (one) {   // the segment's only chunk: reserve its commands / fragments now (as above)
+      if (tid == 0) {
+        const u32 cb = tcnt ? atomicAdd(&d.ctr->n_cmds, tcnt) : 0;
+        const u32 fb = tf ? atomicAdd(&d.ctr->n_frags, tf) : 0;
+        sh_frag_base = fb;
+        sh_cmd_base = cb;
+        sh_ncmd = (cb + tcnt > d.cmd_max || fb + tf > d.frag_max) ? 1u : 0u;
+      }
+      __syncthreads();
+      if (sh_ncmd && tcnt > 0) {   // (block-uniform) overflow: nothing is emitted, all carried
+        const u32 cb = sh_cmd_base;
+        for (u32 i = cb + tid; i < cb + tcnt && i < d.cmd_max; i += FS_NT) {
+          d.cmds[i].kind = CK_NONE;
+          d.cmd_is_pub[i] = 0;
+          d.cmd_is_ack[i] = 0;
+        }
+        __syncthreads();
+        if (tid == 0) sh_cmd_base = INVALID;
+        so.status |= SS_OVERFLOW;
+        so.status &= ~(SS_FRAME_ERROR | SS_UNEXPECTED);
+        consumed = 0;
+        kf = 0;
+        reason = 7;
+        break;
+      }
+      if (tcnt == 0 && tid == 0) sh_cmd_base = INVALID;
+    }
     // the segment's Basic.Gets: a contiguous DGet range per chunk, in wire order
     u32 gi = INVALID;
     if (sh_get0 != INVALID) {   // (block-uniform)
