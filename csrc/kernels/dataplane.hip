@@ -1615,15 +1615,18 @@ __global__ __launch_bounds__(256) void k_decode(DS d) {
     }
     pb.exch = ok ? xs : -2;
     pb.keyhash = pb.rk_len <= 32 ? win_fnv64<0>(rkw, pb.rk_len, FNV64_BASIS) : fnv1a64_dev(w + pb.rk_off, pb.rk_len);
-    // properties (flags chain then values)
+    // properties (flags chain then values), read through a 32-byte register window of the
+    // header payload (one pair of loads instead of one dependent load per field)
     u32 ho = c.h_off + 12, hend = c.h_off + c.h_len;
     pb.props_off = ho;
     pb.props_len = hend > ho ? hend - ho : 0;
+    const Win32 pw = load_win(w + ho);
+    auto pbyte = [&](u32 q) -> u32 { const u32 o = q - ho; return o < 32 ? win_byte(pw, o) : (u32)w[q]; };
     u32 fl = 0;   // the first property-flags word (continuation words are skipped)
     u32 nfl = 0;
     u32 q = ho;
     while (q + 2 <= hend) {
-      u32 fw = be16(w + q);
+      u32 fw = (pbyte(q) << 8) | pbyte(q + 1);
       q += 2;
       if (nfl == 0) fl = fw;
       ++nfl;
@@ -1638,25 +1641,25 @@ __global__ __launch_bounds__(256) void k_decode(DS d) {
       switch (bit) {
         case 13: {
           if (q + 4 > hend) { pok = false; break; }
-          u32 tl = be32(w + q);
+          u32 tl = (pbyte(q) << 24) | (pbyte(q + 1) << 16) | (pbyte(q + 2) << 8) | pbyte(q + 3);
           q += 4 + tl;
           pok = q <= hend;
           break;
         }
         case 12:
           if (q + 1 > hend) { pok = false; break; }
-          if (w[q] == 2) pb.flags |= MF_PERSIST;
+          if (pbyte(q) == 2) pb.flags |= MF_PERSIST;
           q += 1;
           break;
         case 11: q += 1; pok = q <= hend; break;
         case 8: {
           if (q + 1 > hend) { pok = false; break; }
-          u32 sl = w[q];
+          u32 sl = pbyte(q);
           if (q + 1 + sl > hend) { pok = false; break; }
           i64 v = 0;
           bool digits = sl > 0 && sl <= 18;
           for (u32 k = 0; k < sl && digits; ++k) {
-            u8 ch = w[q + 1 + k];
+            u32 ch = pbyte(q + 1 + k);
             if (ch < '0' || ch > '9') digits = false;
             else v = v * 10 + (ch - '0');
           }
@@ -1664,14 +1667,20 @@ __global__ __launch_bounds__(256) void k_decode(DS d) {
           q += 1 + sl;
           break;
         }
-        case 6:
+        case 6: {
           if (q + 8 > hend) { pok = false; break; }
-          pb.ts_ms = (i64)be64(w + q) * 1000;
+          u64 ts = 0;
+#pragma unroll
+          for (u32 k = 0; k < 8; ++k) ts = (ts << 8) | pbyte(q + k);
+          pb.ts_ms = (i64)ts * 1000;
           pb.flags |= MF_HAS_TS;
           q += 8;
           break;
+        }
         default:
-          pok = skip_shortstr(w, q, hend);
+          if (q + 1 > hend) { pok = false; break; }
+          q += 1 + pbyte(q);
+          pok = q <= hend;
       }
     }
     pb.nwords = pb.rk_len <= 32 ? build_keyvec_win(d, rkw, pb.rk_len, pi) : build_keyvec(d, w + pb.rk_off, pb.rk_len, pi);
