@@ -34,7 +34,7 @@ US_FREE, US_PENDING, US_ACKED, US_REQUEUE, US_DONE = 0, 1, 2, 3, 4
 CTRL_TXBUF = 0x80000000     # CtrlRec.seg: data command of a transactional channel (low bits = position)
 CTRL_DGET = 0x40000000      # CtrlRec.seg: a Basic.Get its step decoded but could not serve (not paused)
 
-STRUCT_SIZES = {"SegIn": 16, "SegOut": 32, "CtrlRec": 16, "ConnOut": 8, "StepIn": 80, "RDesc": 64, "USlot": 32}
+STRUCT_SIZES = {"SegIn": 16, "SegOut": 32, "CtrlRec": 16, "ConnOut": 8, "StepIn": 96, "RDesc": 64, "USlot": 32}
 assert RDESC.itemsize == 64
 
 # SegOut.status bits

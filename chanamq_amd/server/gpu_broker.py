@@ -664,6 +664,8 @@ class GpuBroker:
             return
         st = self.fe.stats()
         self.stats.update(steps=st["steps"], published=st["published"], delivered=st["delivered"])
+        if st.get("spill_moved"):
+            self.stats["spilled_bytes"] = st["spill_moved"]
         self._fe_stats = st
         pw = getattr(self, "_pw", None)
         if pw is not None and "store_failed" not in self.stats:
@@ -1932,6 +1934,17 @@ class GpuBroker:
         else:
             lc = getattr(self.plane, "last_counters", None) or {}
             logu = lc.get("log_head", 0) - lc.get("log_tail", 0)
+        if self.fe is not None and hasattr(self.plane, "eng") and self.node is None:
+            # pipelined single-GPU engine: above the watermark every step moves its share
+            # (k_dequeue, at most 2 MiB a step so the egress D2H keeps most of the link) --
+            # no pipeline drain; _sync_fe_stats counts the bytes
+            on = logu >= self.spill_at
+            if on != getattr(self, "_spill_on", False):
+                self._spill_on = on
+                self.plane.eng.stage_spill(1 << 15 if on else 0, self.spill_hot, 2 << 20)
+                if on:
+                    self.fe.wake()
+            return
         now = time.monotonic()
         if logu < self.spill_at or now - self._last_spill < 0.01:
             return

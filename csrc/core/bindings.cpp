@@ -288,6 +288,7 @@ PYBIND11_MODULE(_core, m) {
              FeStats s = f.stats();
              py::dict o;
              o["steps"] = s.steps; o["published"] = s.published; o["delivered"] = s.delivered;
+             o["spill_moved"] = s.spill_moved;
              o["rx_bytes"] = s.rx_bytes; o["tx_bytes"] = s.tx_bytes; o["egress_bytes"] = s.egress_bytes;
              o["held_steps"] = s.held_steps; o["idle_steps"] = s.idle_steps; o["gather_segs"] = s.gather_segs;
              o["live_bytes"] = s.live_bytes; o["live_msgs"] = s.live_msgs; o["io_phase_s"] = s.io_phase_s;

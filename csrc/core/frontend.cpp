@@ -1133,6 +1133,7 @@ void Frontend::finish_oldest(std::deque<Inflight>& inflight) {
     std::lock_guard<std::mutex> g(stats_mu_);
     stats_.steps++;
     stats_.published += c.n_pubs;
+    stats_.spill_moved += c.spill_moved;
     stats_.delivered += c.n_deliv;
     stats_.egress_bytes += c.egress_bytes;
     stats_.live_bytes = c.live_bytes;

@@ -94,6 +94,7 @@ struct FrontendCfg {
 
 struct FeStats {
   u64 steps = 0, published = 0, delivered = 0, rx_bytes = 0, tx_bytes = 0, egress_bytes = 0;
+  u64 spill_moved = 0;   // body bytes moved to the host spill ring by steps (StepIn.spill_*)
   u64 held_steps = 0, idle_steps = 0, gather_segs = 0;
   u64 dropped_nomem = 0, ring_full = 0, unroutable = 0, routed = 0, expired = 0, ctrl = 0;
   i64 live_bytes = 0;

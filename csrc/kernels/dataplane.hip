@@ -413,6 +413,8 @@ __global__ __launch_bounds__(1024) void k_stage(DS d) {
                       // reset by k_marks, in the step's routing half)
       d.ctr->n_grow = 0; d.tot[TS_NMOVE] = 0; d.tot[TS_NDEFER] = 0; d.tot[TS_TTL_BUDGET] = 0;
       d.tot[TS_NDGET] = 0;
+      d.tot[TS_SPILL_USED] = 0;
+      d.ctr->spill_moved = 0;
       *d.egress_budget = 0;
     }
     // connections whose control command the host has answered resume with this step (the
@@ -3389,6 +3391,47 @@ DEV void unreserve(const DS& d, u32 c, u32 take) {
 #define REQ_BLK 1024
 DEV void requeue_compact(const DS& d);
 DEV void requeue_queue(const DS& d, u32 q, u64* kpos, u32* kidx, u32* cnt_p);
+// one queue's share of a spill (4 waves): every queued message past the first `hot` entries
+// (of a queue with consumers) whose slot lies below log position `lim` -- its body to the
+// host spill ring, the message switched to it; at most `budget` bytes per launch across
+// all queues (budget 0: no limit)
+DEV bool spill_reserve(const DS& d, u32 sz, u64* pos);
+DEV void spill_queue(const DS& d, u32 q, u64 lim, u32 hot, u32 budget, u64* moved) {
+  const u32 lane = lane_id(), w = threadIdx.x >> 6;
+  if (!d.q_active[q]) return;
+  // (agent scope: in k_dequeue this block's requeue may just have moved the head)
+  const u64 head = __hip_atomic_load(&d.q_head[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const u64 tail = d.q_tail[q], mask = d.q_ring_mask[q];
+  const Desc* ring = d.ring + d.q_ring_off[q];
+  const u64 skip = d.q_cons_n[q] ? hot : 0;
+  for (u64 i = head + skip + w; i < tail; i += 4) {
+    const u32 msg = ring[i & mask].msg;
+    if (msg == INVALID || msg >= d.msg_max) continue;
+    MsgEnt& m = d.msgs[msg];
+    const u64 lo = __hip_atomic_load(&m.log_off, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if ((lo & SPILL_BIT) || lo >= lim) continue;
+    const u32 sz = m.slot_bytes;
+    u64 pos = 0;
+    u32 ok = 0;
+    if (lane == 0) {
+      ok = (!budget || atomicAdd(&d.tot[TS_SPILL_USED], sz) + sz <= budget) ? 1u : 0u;
+      if (ok) ok = spill_reserve(d, sz, &pos) ? 1u : 0u;
+    }
+    ok = (u32)__shfl((int)ok, 0);
+    if (!ok) break;   // the spill ring is full, or this step's budget is spent
+    pos = shfl64(pos, 0);
+    wave_copy(d.spill + (pos % d.spill_bytes), d.log + (lo % d.log_bytes), sz);
+    __threadfence_system();   // the copy reached host memory before the slot is switched
+    if (lane == 0 &&
+        atomicCAS((unsigned long long*)&m.log_off, (unsigned long long)lo, (unsigned long long)(SPILL_BIT | pos)) == lo) {
+      atomicAdd((unsigned long long*)&d.log_live[(lo / d.log_block) % d.n_log_blocks], (unsigned long long)(-(i64)sz));
+      atomicAdd((unsigned long long*)&d.spill_live[(pos / d.log_block) % d.n_spill_blocks], (unsigned long long)sz);
+      atomicAdd((unsigned long long*)d.live_bytes, (unsigned long long)(-(i64)sz));
+      atomicAdd((unsigned long long*)moved, (unsigned long long)sz);
+    }
+  }
+}
+
 __global__ __launch_bounds__(256) void k_dequeue(DS d) {
   __shared__ u32 g_cons[RUNS_PER_Q];
   __shared__ u32 g_n[RUNS_PER_Q];
@@ -3439,6 +3482,11 @@ __global__ __launch_bounds__(256) void k_dequeue(DS d) {
     return;
   }
   const bool nodisp = (d.in->flags & SF_NODISPATCH) != 0;
+  if (d.in->spill_frac && d.spill_bytes) {   // (kernel-uniform) the step's share of body tiering
+    const u64 lim = *d.log_tail + (((u64)d.log_bytes * d.in->spill_frac) >> 16);
+    spill_queue(d, q, lim, d.in->spill_hot, d.in->spill_budget, &d.ctr->spill_moved);
+    __syncthreads();
+  }
   if (nodisp && d.links && d.q_link_owner[q]) {   // a live link shadow: its acks could not travel
     if (tid == 0) {
       d.q_nruns[q] = 0;
@@ -4592,34 +4640,9 @@ DEV bool spill_reserve(const DS& d, u32 sz, u64* pos) {
 // never-live gap the spill tail passes).  Its log block loses the bytes, so the next
 // step's final_step can advance the log tail.  Unacked deliveries stay in the log.
 __global__ __launch_bounds__(256) void k_spill(DS d, u64 lim, u32 hot, unsigned long long* moved) {
-  const u32 q = blockIdx.x, lane = lane_id(), w = threadIdx.x >> 6;
-  if (q >= d.q_max || !d.q_active[q] || d.spill_bytes == 0) return;
-  const u64 head = d.q_head[q], tail = d.q_tail[q], mask = d.q_ring_mask[q];
-  const Desc* ring = d.ring + d.q_ring_off[q];
-  const u64 skip = d.q_cons_n[q] ? hot : 0;
-  for (u64 i = head + skip + w; i < tail; i += 4) {
-    const u32 msg = ring[i & mask].msg;
-    if (msg == INVALID || msg >= d.msg_max) continue;
-    MsgEnt& m = d.msgs[msg];
-    const u64 lo = __hip_atomic_load(&m.log_off, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if ((lo & SPILL_BIT) || lo >= lim) continue;
-    const u32 sz = m.slot_bytes;
-    u64 pos = 0;
-    u32 ok = 0;
-    if (lane == 0) ok = spill_reserve(d, sz, &pos) ? 1u : 0u;
-    ok = (u32)__shfl((int)ok, 0);
-    if (!ok) break;   // the spill ring is full
-    pos = shfl64(pos, 0);
-    wave_copy(d.spill + (pos % d.spill_bytes), d.log + (lo % d.log_bytes), sz);
-    __threadfence_system();   // the copy reached host memory before the slot is switched
-    if (lane == 0 &&
-        atomicCAS((unsigned long long*)&m.log_off, (unsigned long long)lo, (unsigned long long)(SPILL_BIT | pos)) == lo) {
-      atomicAdd((unsigned long long*)&d.log_live[(lo / d.log_block) % d.n_log_blocks], (unsigned long long)(-(i64)sz));
-      atomicAdd((unsigned long long*)&d.spill_live[(pos / d.log_block) % d.n_spill_blocks], (unsigned long long)sz);
-      atomicAdd((unsigned long long*)d.live_bytes, (unsigned long long)(-(i64)sz));
-      atomicAdd(moved, (unsigned long long)sz);
-    }
-  }
+  const u32 q = blockIdx.x;
+  if (q >= d.q_max || d.spill_bytes == 0) return;
+  spill_queue(d, q, lim, hot, 0, (u64*)moved);
 }
 
 // ============================================================================ cold store (between steps)

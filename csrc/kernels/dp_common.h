@@ -44,7 +44,7 @@ enum : u32 {
 enum : u32 { US_FREE = 0, US_PENDING = 1, US_ACKED = 2, US_REQUEUE = 3, US_DONE = 4 };
 
 
-struct StepIn {         // host -> device per step (80 B)
+struct StepIn {         // host -> device per step (96 B)
   u32 nseg;
   u32 flags;
   i64 now_ms;
@@ -64,7 +64,13 @@ struct StepIn {         // host -> device per step (80 B)
   // deferred control writes (DS.delta_h of this parity, packed by the host): bytes, 0 = none.
   // k_stage applies them first, before the step reads any table
   u32 delta_bytes;
-  u32 pad_;
+  // body tier upkeep riding the step (k_dequeue, no pipeline drain): queued bodies in the
+  // oldest spill_frac / 65536 of the HBM log, past the first spill_hot entries of a queue
+  // with consumers, move to the host spill ring, at most spill_budget bytes this step
+  u32 spill_frac;
+  u32 spill_hot;
+  u32 spill_budget;
+  u32 pad_[2];
 };
 
 

@@ -51,7 +51,8 @@ enum : u32 {
   TS_PK_TICKET = 66,                    // k_pack_scan finished-tile ticket (last tile: prefixes)
   TS_POST_TICKET = 67,                  // k_post finished-block ticket (last block: final_step)
   TS_NCADEF = 68,                       // channels k_chan_advance deferred (store-record budget)
-  TS_NDGET = 69                         // Basic.Get commands the frame scan decoded (DGet list)
+  TS_NDGET = 69,                        // Basic.Get commands the frame scan decoded (DGet list)
+  TS_SPILL_USED = 70                    // bytes of StepIn.spill_budget reserved this step (k_dequeue)
 };
 
 // Basic.Get decoded from a connection's bytes by the frame scan (no host round trip): served

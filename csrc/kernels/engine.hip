@@ -844,6 +844,12 @@ class Engine {
       pend_gets_.clear();
     }
     nget_[p] = in->nget;
+    {   // body tiering asked for by the control plane rides this step (k_dequeue)
+      std::lock_guard<std::mutex> g(dl_mu_);
+      in->spill_frac = spill_req_[0];
+      in->spill_hot = spill_req_[1];
+      in->spill_budget = spill_req_[2];
+    }
     // the control writes staged so far (what fits one step) and the connections
     // unpaused with them: a connection resumed in this step finds every write staged
     // before its unpause applied (k_stage applies the writes first)
@@ -954,6 +960,15 @@ class Engine {
     for (u32 c : dv)
       if (c == ch) return;
     dv.push_back(ch);
+  }
+  // from the next submitted step on, every step moves queued bodies in the oldest frac/65536
+  // of the HBM log (past the first `hot` entries of a queue with consumers) to the host
+  // spill ring, at most `budget` bytes a step -- spill() without the pipeline drain; frac 0
+  // stops it.  Any thread.
+  void stage_spill(u32 frac, u32 hot, u32 budget) {
+    if (!d_.spill_bytes) return;
+    std::lock_guard<std::mutex> g(dl_mu_);
+    spill_req_[0] = frac; spill_req_[1] = hot; spill_req_[2] = budget;
   }
   // (records, data bytes, channels to mark) staged and not yet taken by a step
   py::tuple deltas_pending() {
@@ -1997,7 +2012,7 @@ class Engine {
     F(n_dropped_nomem); F(n_expired); F(n_routed_msgs); F(n_unknown_exchange); F(n_ring_full);
     F(n_acked); F(log_head); F(log_tail); F(msg_free_top); F(n_live_msgs);
     F(n_persist); F(n_consumed); F(persist_used); F(n_persist_overflow);
-    F(live_bytes); F(n_grow); F(n_dget);
+    F(live_bytes); F(n_grow); F(n_dget); F(spill_moved);
 #undef F
     std::vector<u32> lat(c.lat_hist, c.lat_hist + LAT_BINS);
     o["lat_hist"] = lat;
@@ -2296,6 +2311,7 @@ class Engine {
   std::mutex dl_mu_;
   struct DlBatch { std::map<u64, std::string> w; std::vector<u32> dirty, unp; u64 bytes = 0; };
   std::vector<u32> unp_ready_;   // unpauses of batches flush_deltas applied (next step)
+  u32 spill_req_[3] = {0, 0, 0};   // stage_spill for the next submitted step (dl_mu_)
   // staged writes with the unpauses staged after them; a batch that overflows one step's
   // delta buffer keeps its unpauses until its last write is packed
   std::deque<DlBatch> dl_;
@@ -2468,6 +2484,7 @@ PYBIND11_MODULE(_dataplane, m) {
       .def("egress_stats", &Engine::egress_stats)
       .def("stage_write", &Engine::stage_write_buf, py::arg("name"), py::arg("data"), py::arg("offset") = 0)
       .def("stage_mark_dirty", &Engine::stage_mark_dirty)
+      .def("stage_spill", &Engine::stage_spill)
       .def("deltas_pending", &Engine::deltas_pending)
       .def("flush_deltas", &Engine::flush_deltas, py::call_guard<py::gil_scoped_release>());
 }

@@ -78,7 +78,7 @@ struct Counters {       // per-step counters (device -> host)
   i64 live_bytes;       // body-log slot bytes of live messages (exact, unlike head - tail)
   u32 n_grow;           // rings grown this step (grow_host list of RingMove)
   u32 n_dget;           // Basic.Gets decoded (and served or handed to the host) this step
-  u32 pad[2];
+  u64 spill_moved;      // body bytes this step moved to the host spill ring (StepIn.spill_*)
 };
 
 struct CtrlRec { u32 conn; u32 off; u32 len; u32 seg; };
