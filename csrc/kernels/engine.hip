@@ -1790,12 +1790,22 @@ class Engine {
   void gated_copy(int e) {
     if (!spec_[e]) return;
     Range rg("chanamq.K5.egress_gated");
-    hsa_signal_store_screlease(sdma_sig_[e], 1);
-    hsa_status_t st = hsa_amd_memory_async_copy_on_engine(egress_host_[e], cpu_agent_, egress_dev_[e], gpu_agent_,
-                                                          spec_[e], 1, &gate_sig_[e], sdma_sig_[e], sdma_engine_, true);
-    if (st != HSA_STATUS_SUCCESS) {
-      hsa_signal_store_screlease(sdma_sig_[e], 0);
-      throw std::runtime_error("hsa_amd_memory_async_copy_on_engine (gated egress) failed");
+    // sdma_split 2: the speculative copy in two halves on two SDMA engines, both released by
+    // the same gate, each decrementing the slot's completion signal once
+    const u64 n = spec_[e];
+    const int k = (sdma_split_ > 1 && sdma_engine2_ && n >= (4u << 20)) ? 2 : 1;
+    const u64 half = k == 2 ? ((n / 2) & ~(u64)4095) : n;
+    hsa_signal_store_screlease(sdma_sig_[e], k);
+    for (int i = 0; i < k; ++i) {
+      const u64 off = i ? half : 0, len = i ? n - half : half;
+      hsa_status_t st = hsa_amd_memory_async_copy_on_engine((u8*)egress_host_[e] + off, cpu_agent_,
+                                                            (u8*)egress_dev_[e] + off, gpu_agent_, len, 1,
+                                                            &gate_sig_[e], sdma_sig_[e],
+                                                            i ? sdma_engine2_ : sdma_engine_, true);
+      if (st != HSA_STATUS_SUCCESS) {
+        hsa_signal_store_screlease(sdma_sig_[e], 0);
+        throw std::runtime_error("hsa_amd_memory_async_copy_on_engine (gated egress) failed");
+      }
     }
     sdma_pending_[e] = true;
     ++eg_stats_[0];
@@ -1969,9 +1979,14 @@ class Engine {
         if (c != pick && ((mask >> c) & 1u)) { sdma_engine2_ = (hsa_amd_sdma_engine_id_t)(1u << c); break; }
     // the tail engine (gated egress): another full-rate engine than the gated copies' --
     // which can sit behind the next step's gate -- and than the runtime's H2D engine 0
+    // (nor the split copies' second engine: an engine's queue is in order, and a gated copy
+    // waiting there for the next step's gate would hold the tail back by a step)
     tail_engine_ = sdma_engine_;
     for (u32 c : {2u, 3u, 0u})
-      if (c != pick && ((mask >> c) & 1u)) { tail_engine_ = (hsa_amd_sdma_engine_id_t)(1u << c); break; }
+      if (c != pick && ((mask >> c) & 1u) && (1u << c) != (u32)sdma_engine2_) {
+        tail_engine_ = (hsa_amd_sdma_engine_id_t)(1u << c);
+        break;
+      }
     for (int e = 0; e < EGRESS_SLOTS; ++e)
       if (hsa_signal_create(0, 0, nullptr, &sdma_sig_[e]) != HSA_STATUS_SUCCESS ||
           hsa_signal_create(0, 0, nullptr, &tail_sig_[e]) != HSA_STATUS_SUCCESS ||
