@@ -172,10 +172,11 @@ def main():
                     help="after the timed steps (and the result line), keep stepping untimed for this long so "
                          "an external GPU-utilisation sampler sees the workload (0 = off)")
     ap.add_argument("--no-graph", action="store_true")
-    ap.add_argument("--overlap", type=int, default=1, choices=[0, 1],
+    ap.add_argument("--overlap", type=int, default=0, choices=[0, 1],
                     help="1: a step's ingest half on its own high-priority stream (it may run beside the "
-                         "previous step's routing half); 0: the whole step as one graph on one stream (no "
-                         "cross-queue hand-off between the halves)")
+                         "previous step's routing half); 0 (default): the whole step as one graph on one "
+                         "stream (no cross-queue hand-off between the halves; measured equal throughput, "
+                         "p50 0.85 vs 1.10 ms at 49152, profiles/r5_fs1, r5_split)")
     ap.add_argument("--loop", choices=["poll", "block"], default="block",
                     help="host loop: poll = submit as soon as a parity frees and stamp each egress when it "
                          "lands (non-blocking queries); block = submit / prefetch / wait egress t-2 / finish t-1")
@@ -199,11 +200,12 @@ def main():
                          "the collective overlaps the next step); 0 = synchronous")
     ap.add_argument("--mode", choices=["sharded", "independent"], default="sharded",
                     help="N>1: one sharded broker (cross-GPU routing over RCCL) or N unconnected shards")
-    ap.add_argument("--prefetch", type=int, default=1, choices=[0, 1, 2],
+    ap.add_argument("--prefetch", type=int, default=0, choices=[0, 1, 2],
                     help="N: keep the ingress H2D of the next N steps queued (submitted step t -> t+1..t+N; "
                          "the copy engine never idles between steps; a step's latency clock starts when its "
-                         "bytes are queued); 0: H2D at submit.  Measured: 1 is best (32768: 32.9 M msgs/s at "
-                         "K=20 vs 12.9 M at 2, profiles/r4_bench/pre_*.json)")
+                         "bytes are queued); 0 (default): H2D at submit.  With the whole step on one stream "
+                         "0 is best at the default step: K=200 38.8 M msgs/s at p50 0.85 ms vs 37.5 M at "
+                         "1.12 ms with 1 (profiles/r5_split); at 32768 B 1 is faster (31 vs 27 M)")
     ap.add_argument("--xchg", choices=["native", "torch"], default="native",
                     help="N>1 sharded: the engine's own exchange -- grouped RCCL send/recv on its exchange "
                          "stream, counts through host shared memory (the code the sharded server runs; "
