@@ -19,7 +19,7 @@ def main():
     ap.add_argument("--port", type=int, required=True)
     ap.add_argument("--n", type=int, default=4)
     ap.add_argument("--prefill", type=int, default=200000)
-    ap.add_argument("--pipeline", type=int, default=16, help="Basic.Gets in flight per poller")
+    ap.add_argument("--pipeline", type=int, default=64, help="Basic.Gets in flight per poller")
     a = ap.parse_args()
     c = Connection(port=a.port, vhost="/", timeout=60)
     ch = c.channel()
