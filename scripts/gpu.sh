@@ -22,7 +22,8 @@
 #               per counter group (PMC_GROUPS overrides), each under its own time limit
 #   xchg        the single-rank RCCL exchange test, then the 2- and 4-rank native / torch
 #               exchange rehearsal on this one GPU (gloo launcher => shared-memory backend)
-#   e2e         bench/gpu_server_e2e.py, every spec, paced at 50 % (E2E_ARGS appended)
+#   e2e         bench/gpu_server_e2e.py, every spec, paced at 50 % (E2E_ARGS appended; IOT io
+#               threads, LG load-generator threads, TAG output-name suffix)
 #   e2e_c2      config 2 only over TCP, paced at 50 % (E2E_ARGS appended)
 #   churn       config 2 paced at 50 % next to connection / consumer churn (E2E_ARGS appended)
 #   sharded     the sharded-server GPU tests
@@ -126,12 +127,12 @@ for T in "$@"; do
     done ;;
   e2e)
     timeout -k 10 900 python -u bench/gpu_server_e2e.py --seconds 4 --io-threads ${IOT:-8} --paced 0.5 \
-      --out $O/e2e_all_specs.json $E2E_ARGS > $O/e2e.log 2>&1
-    rc=$?; tail -12 $O/e2e.log | cut -c1-600; ok $rc e2e ;;
+      --loadgen-threads ${LG:-12} --out $O/e2e_all_specs${TAG:-}.json $E2E_ARGS > $O/e2e${TAG:-}.log 2>&1
+    rc=$?; tail -12 $O/e2e${TAG:-}.log | cut -c1-600; ok $rc e2e ;;
   e2e_c2)
     timeout -k 10 400 python -u bench/gpu_server_e2e.py --seconds 4 --io-threads ${IOT:-8} --only config2 --paced 0.5 \
-      --out $O/e2e_c2.json $E2E_ARGS > $O/e2e_c2.log 2>&1
-    rc=$?; tail -4 $O/e2e_c2.log | cut -c1-600; ok $rc e2e_c2 ;;
+      --loadgen-threads ${LG:-12} --out $O/e2e_c2${TAG:-}.json $E2E_ARGS > $O/e2e_c2${TAG:-}.log 2>&1
+    rc=$?; tail -4 $O/e2e_c2${TAG:-}.log | cut -c1-600; ok $rc e2e_c2 ;;
   churn)
     timeout -k 10 400 python -u bench/gpu_server_e2e.py --seconds 5 --io-threads ${IOT:-8} --only config2 --paced 0.5 \
       --churn --out $O/e2e_churn.json $E2E_ARGS > $O/e2e_churn.log 2>&1
