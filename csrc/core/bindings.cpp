@@ -256,6 +256,7 @@ PYBIND11_MODULE(_core, m) {
            })
       .def("wake", &Frontend::wake)
       .def("flush_ctl", &Frontend::flush_ctl, py::call_guard<py::gil_scoped_release>())
+      .def("ctl_state", &Frontend::ctl_state)
       .def("send_egress", [](Frontend& f, py::buffer egress, py::buffer conn_out, uint32_t n_slots) {
              py::buffer_info e = egress.request(), c = conn_out.request();
              if ((uint64_t)c.size * c.itemsize < 8ull * n_slots) throw std::runtime_error("conn_out too small");

@@ -340,6 +340,11 @@ void Frontend::flush_ctl() {
     if (o.gen == conns_[o.conn]->gen.load()) send(o.conn, o.data.data(), o.data.size());
 }
 
+std::vector<u64> Frontend::ctl_state() {
+  std::lock_guard<std::mutex> g(ctl_mu_);
+  return {(u64)ctl_out_.size(), ctl_out_.empty() ? 0 : ctl_out_.front().after, sub_step_.load(), fin_step_.load()};
+}
+
 // a held reply waits for a step not submitted yet: the stepper must submit one
 bool Frontend::ctl_needs_step() {
   std::lock_guard<std::mutex> g(ctl_mu_);

@@ -142,6 +142,8 @@ class Frontend {
   void send_after(u32 conn, const char* data, size_t n);
   void wake();                                           // the stepper looks for work (staged control writes)
   void flush_ctl();                                      // (paused) write every held control reply now
+  // (held control replies, the first one's step, steps submitted, steps finished)
+  std::vector<u64> ctl_state();
   // bytes for a socketless pseudo-connection (committed transactions): stepped with the
   // next step like a client's, FE_INJECTED once that step finished; egress is dropped
   void inject(u32 conn, const std::string& bytes);

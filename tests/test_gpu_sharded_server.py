@@ -133,6 +133,13 @@ def test_pipelined_remote_consumers_and_gets(cluster):
     assert g.basic_get("lqa", no_ack=True).body == b"g2"
     assert g.basic_get("lqa") is None
     c1.process(1.5)   # the idle get link closes; acks reached the owner: nothing comes back
+    # pipelined Basic.Gets on the owner's rank: decoded and answered inside its steps
+    for i in range(3):
+        p.basic_publish("lx", "a.h", b"h%d" % i)
+    c0.process(0.3)
+    lg = c0.channel()
+    ok, empty = lg.basic_get_many("lqa", 5, no_ack=True)
+    assert [d.body for d in ok] == [b"h0", b"h1", b"h2"] and empty == 2
     a.basic_consume("lqa", "ca3", no_ack=True)
     p.basic_publish("lx", "a.end", b"end2")
     assert a.consume_n(1)[0].body == b"end2"
