@@ -43,6 +43,20 @@ def conn(b, **kw):
     return Connection(port=b.port, vhost="/", **kw)
 
 
+def channel_or_dump(b, c):
+    """c.channel(); on a timeout, the pipelined server's control / stepper state first."""
+    try:
+        return c.channel()
+    except TimeoutError:
+        fe, lk = getattr(b, "fe", None), b.lock
+        if fe is not None and hasattr(fe, "ctl_state"):
+            print("ctl_state (held, first after, submitted, finished):", fe.ctl_state(), "steps", fe.stats()["steps"],
+                  "lock depth", lk.depth, "paused_at", lk.paused_at, "light", lk.light,
+                  "deltas", b.plane.eng.deltas_pending() if hasattr(b.plane, "eng") else None,
+                  "conns", {k: v.state for k, v in b.conns.items()})
+        raise
+
+
 def test_publish_consume_topic(broker):
     p = conn(broker)
     ch = p.channel()
@@ -450,7 +464,7 @@ def test_confirmed_publishes_into_a_small_queue_are_never_lost(broker):
     assert ch.wait_for_confirms(timeout=60)
     assert ch.queue_declare("deep", passive=True).message_count == n
     c = conn(broker)
-    cc = c.channel()
+    cc = channel_or_dump(broker, c)
     cc.basic_consume("deep", "deepc", no_ack=True)
     got = cc.consume_n(n, timeout=120)
     assert [int.from_bytes(d.body, "big") for d in got] == list(range(n))
@@ -842,7 +856,7 @@ def test_control_churn_rides_the_steps_without_a_drain(gpu):
             cch.basic_cancel(f"c{k}")
         for _ in range(20):
             x = conn(b)
-            x.channel()
+            channel_or_dump(b, x)
             x.close()
         pauses1, light1 = b.stats.get("pauses", 0), b.stats.get("light_sections", 0)
         stop.set()
