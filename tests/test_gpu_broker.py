@@ -43,17 +43,27 @@ def conn(b, **kw):
     return Connection(port=b.port, vhost="/", **kw)
 
 
+def dump_state(b):
+    """The pipelined server's control / stepper state (printed into a failing test's log)."""
+    import time
+    fe, lk = getattr(b, "fe", None), b.lock
+    if fe is None or not hasattr(fe, "ctl_state"):
+        return
+    for k in range(2):
+        print("ctl_state (held, first after, submitted, finished):", fe.ctl_state(), "steps", fe.stats()["steps"],
+              "lock depth", lk.depth, "paused_at", lk.paused_at, "light", lk.light,
+              "deltas", b.plane.eng.deltas_pending() if hasattr(b.plane, "eng") else None,
+              "running", b._running, "ctl thread", [t.name for t in __import__("threading").enumerate()],
+              "conns", {k2: v.state for k2, v in b.conns.items()})
+        time.sleep(0.5)
+
+
 def channel_or_dump(b, c):
     """c.channel(); on a timeout, the pipelined server's control / stepper state first."""
     try:
         return c.channel()
     except TimeoutError:
-        fe, lk = getattr(b, "fe", None), b.lock
-        if fe is not None and hasattr(fe, "ctl_state"):
-            print("ctl_state (held, first after, submitted, finished):", fe.ctl_state(), "steps", fe.stats()["steps"],
-                  "lock depth", lk.depth, "paused_at", lk.paused_at, "light", lk.light,
-                  "deltas", b.plane.eng.deltas_pending() if hasattr(b.plane, "eng") else None,
-                  "conns", {k: v.state for k, v in b.conns.items()})
+        dump_state(b)
         raise
 
 
@@ -813,13 +823,13 @@ def test_control_churn_rides_the_steps_without_a_drain(gpu):
                   ingress_bytes=8 << 20).start()
     try:
         s = conn(b)
-        sch = s.channel()
+        sch = channel_or_dump(b, s)
         for q in ("load", "cq", "rq"):
             sch.queue_declare(q)
         for k in range(10):
             sch.basic_publish("", "rq", f"r{k}".encode())
         sink = conn(b)
-        kch = sink.channel()
+        kch = channel_or_dump(b, sink)
         kch.basic_consume("load", "sink", no_ack=True)
         stop = threading.Event()
         sent = [0]
@@ -839,7 +849,7 @@ def test_control_churn_rides_the_steps_without_a_drain(gpu):
         pauses0, light0 = b.stats.get("pauses", 0), b.stats.get("light_sections", 0)
         # manual-ack consumer takes the 10, its channel closes with them unacked
         rc = conn(b)
-        r1 = rc.channel(5)
+        r1 = rc.channel(5)   # (a fixed number: the reopen below reuses its device slot)
         r1.basic_consume("rq", "r", no_ack=False)
         assert sorted(d.body for d in r1.consume_n(10)) == sorted(f"r{k}".encode() for k in range(10))
         r1.close()
