@@ -58,6 +58,19 @@ def dump_state(b):
         time.sleep(0.5)
 
 
+def dump_on_channel_timeout(monkeypatch, b):
+    """Every Connection.channel() of the test dumps the server state before it times out."""
+    orig = Connection.channel
+
+    def channel(self, *a, **kw):
+        try:
+            return orig(self, *a, **kw)
+        except TimeoutError:
+            dump_state(b)
+            raise
+    monkeypatch.setattr(Connection, "channel", channel)
+
+
 def channel_or_dump(b, c):
     """c.channel(); on a timeout, the pipelined server's control / stepper state first."""
     try:
@@ -808,7 +821,7 @@ def test_backlog_past_hbm_and_host_tiers_goes_to_the_cold_store(gpu, io, tmp_pat
 
 
 @pytest.mark.gpu
-def test_control_churn_rides_the_steps_without_a_drain(gpu):
+def test_control_churn_rides_the_steps_without_a_drain(gpu, monkeypatch):
     """Connection open/close, channel open/close and consume/cancel while a publisher
     streams: handled in light control sections (their table writes staged and applied by
     the next step's first kernel, replies sent behind the deliveries in flight), so the
@@ -821,6 +834,7 @@ def test_control_churn_rides_the_steps_without_a_drain(gpu):
     from chanamq_amd.server.gpu_broker import GpuBroker
     b = GpuBroker(GpuDataPlane(default_queue_capacity=1 << 12, **GPU_CFG), idle_step_ms=1.0, io="pipeline",
                   ingress_bytes=8 << 20).start()
+    dump_on_channel_timeout(monkeypatch, b)
     try:
         s = conn(b)
         sch = channel_or_dump(b, s)
