@@ -466,21 +466,30 @@ class GpuBroker:
         """Whether this batch of front-end events can be handled with the steps running:
         handshakes, channel / consumer / QoS / confirm commands and plain closes; anything
         that reads device state or changes queues, exchanges or bindings needs the drain."""
+        why = self._light_why(evs)
+        if why is not None:   # (why the stepper pauses: stats["pause_why"], by cause)
+            pw = self.stats.setdefault("pause_why", {})
+            pw[why] = pw.get(why, 0) + 1
+        return why is None
+
+    def _light_why(self, evs):
         if not self._light_capable():
-            return False
+            return "not light-capable"
         n, nb, nd = self.plane.deltas_pending()
         if n > 256 or nb > (1 << 20) or nd > 1024:   # a change set must fit one step's delta buffer
-            return False
+            return "staged writes"
         for kind, conn, a, b, data, data2 in evs:
             if kind in (FE_OPEN, FE_GET, FE_EVENT, FE_STATUS, FE_TXBUF):
                 continue
             c = self.conns.get(conn)
             if kind == FE_CLOSED:
                 if c is not None and c.state == "open" and not self._close_light(c):
-                    return False
+                    return "close with exclusive queues"
             elif kind == FE_HOST:
-                if c is not None and (c.state not in ("header", "start", "tune", "closing") or c.big is not None):
-                    return False
+                # handshakes and the close handshake; on an open connection a stale event (its
+                # bytes went to the data plane with set_data_mode) -- nothing reads the device
+                if c is not None and (c.state not in ("header", "start", "tune", "closing", "open") or c.big is not None):
+                    return "host bytes " + c.state
             elif kind == FE_CTRL:
                 if c is None or c.state != "open" or len(data) < 11:
                     continue
@@ -489,12 +498,12 @@ class GpuBroker:
                     continue
                 key = struct.unpack_from(">HH", data, 7)
                 if data[0] != C.FRAME_METHOD or key not in _LIGHT_METHODS:
-                    return False
+                    return "method %d.%d" % key if data[0] == C.FRAME_METHOD else "content"
                 if key == (10, 50) and not self._close_light(c):
-                    return False
+                    return "close with exclusive queues"
             else:
-                return False
-        return True
+                return "event %d" % kind
+        return None
 
     def _fast_events(self, dev):
         """Basic.Get traffic without pausing the stepper: a Get on a local queue is staged

@@ -689,13 +689,22 @@ void Frontend::drop(FeConn& c, bool notify) {
   }
 }
 
-static void host_read(Frontend* fe, FeConn& c, std::atomic<u64>& rx, bool& eof, bool& notify) {
+// bytes of a host-mode connection to its host buffer.  The control plane may switch the
+// connection to the data plane meanwhile (set_data_mode moves the host buffer to the
+// inject queue under c.mu): bytes read after that go to the inject queue too (to_data: the
+// caller marks the connection ready), never to a host buffer nobody reads any more
+static void host_read(Frontend* fe, FeConn& c, std::atomic<u64>& rx, bool& eof, bool& notify, bool& to_data) {
   char buf[1 << 16];
   for (;;) {
     ssize_t k = ::recv(c.fd, buf, sizeof buf, 0);
     if (k > 0) {
       rx += (u64)k;
       std::lock_guard<std::mutex> g(c.mu);
+      if (c.mode == M_DATA) {
+        c.inject.append(buf, (size_t)k);
+        to_data = true;
+        continue;
+      }
       c.hostbuf.append(buf, (size_t)k);
       if (!c.host_notified) { c.host_notified = true; notify = true; }
       continue;
@@ -738,9 +747,10 @@ void Frontend::io_loop(int i) {
       if (c.mode == M_DATA) {
         if (!c.in_ready) { c.in_ready = true; io.ready.push_back(id); }
       } else if (c.mode == M_HOST && c.fd >= 0) {
-        bool eof = false, notify = false;
-        host_read(this, c, rx_bytes_, eof, notify);
+        bool eof = false, notify = false, to_data = false;
+        host_read(this, c, rx_bytes_, eof, notify, to_data);
         if (notify) { FeEvent e; e.kind = FE_HOST; e.conn = id; post(std::move(e)); }
+        if (to_data && !c.in_ready) { c.in_ready = true; io.ready.push_back(id); }
         if (eof) drop(c, true);
       }
     }
@@ -798,9 +808,13 @@ void Frontend::io_loop(int i) {
         if (!c.in_ready) { c.in_ready = true; io.ready.push_back((u32)id); }
         data_ready = true;
       } else if (m == M_HOST) {
-        bool eof = false, notify = false;
-        host_read(this, c, rx_bytes_, eof, notify);
+        bool eof = false, notify = false, to_data = false;
+        host_read(this, c, rx_bytes_, eof, notify, to_data);
         if (notify) { FeEvent ev; ev.kind = FE_HOST; ev.conn = (u32)id; post(std::move(ev)); }
+        if (to_data) {   // switched to the data plane while reading: its next step takes them
+          if (!c.in_ready) { c.in_ready = true; io.ready.push_back((u32)id); }
+          data_ready = true;
+        }
         if (eof) drop(c, true);
       }
     }
