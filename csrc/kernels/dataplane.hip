@@ -3432,7 +3432,7 @@ DEV void spill_queue(const DS& d, u32 q, u64 lim, u32 hot, u32 budget, u64* move
   }
 }
 
-__global__ __launch_bounds__(256) void k_dequeue(DS d) {
+DEV void dequeue_queue(const DS& d) {
   __shared__ u32 g_cons[RUNS_PER_Q];
   __shared__ u32 g_n[RUNS_PER_Q];
   __shared__ u64 s_head;
@@ -3733,6 +3733,26 @@ __global__ __launch_bounds__(256) void k_dequeue(DS d) {
   }
 }
 
+// K8 dequeue, one block per queue; the last block to finish (ticket) then lays out the
+// step's delivery runs (fused k_runs: a launch less per step)
+template <u32 NT> DEV void runs_body(const DS& d, u64* key_lds, u32 key_cap, u32* lds);
+#define DQ_RUN_LDS 2048   // runs sorted in the fused k_runs' LDS (more: the global-memory sort)
+__global__ __launch_bounds__(256) void k_dequeue(DS d) {
+  __shared__ u64 key_lds[DQ_RUN_LDS];
+  __shared__ u32 lds[256 / 64 + 1];
+  __shared__ u32 s_last;
+  dequeue_queue(d);
+  // every block's runs and counts are written (their stores returned) before its ticket
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __syncthreads();
+  if (threadIdx.x == 0) s_last = atomicAdd(&d.tot[TS_DQ_TICKET], 1u) == gridDim.x - 1;
+  __syncthreads();
+  if (!s_last) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  if (threadIdx.x == 0) d.tot[TS_DQ_TICKET] = 0;
+  runs_body<256>(d, key_lds, DQ_RUN_LDS, lds);
+}
+
 // ============================================================================ runs -> deliveries
 // One block: gather the step's runs (queue order, then round-robin order), sort them by
 // channel (bitonic on (channel << 32 | run slot): ties keep queue order, the stable order
@@ -3754,22 +3774,21 @@ DEV void bitonic_sort_u64(u64* k, u32 np2, u32 tid, u32 nt) {
   }
 }
 
-__global__ __launch_bounds__(1024) void k_runs(DS d) {
-  __shared__ u64 key_lds[RUN_SORT_LDS];
-  __shared__ u32 lds[1024 / 64 + 1];
+template <u32 NT>
+DEV void runs_body(const DS& d, u64* key_lds, u32 key_cap, u32* lds) {
   const u32 tid = threadIdx.x;
   // pass 1: total runs
   u32 R = 0;
-  for (u32 b0 = 0; b0 < d.q_max; b0 += 1024) {
+  for (u32 b0 = 0; b0 < d.q_max; b0 += NT) {
     u32 qq = b0 + tid;
     u32 v = qq < d.q_max ? d.q_nruns[qq] : 0;
     u32 all;
-    u32 off = block_scan<1024>(v, lds, all);
+    u32 off = block_scan<NT>(v, lds, all);
     for (u32 j = 0; j < v; ++j) {
       const u32 slot = qq * RUNS_PER_Q + j;
       const u32 pos = R + off + j;
       const u64 k = ((u64)d.runs[slot].ch << 32) | slot;
-      if (pos < RUN_SORT_LDS) key_lds[pos] = k;
+      if (pos < key_cap) key_lds[pos] = k;
       d.run_key[pos] = k;
     }
     R += all;
@@ -3777,19 +3796,19 @@ __global__ __launch_bounds__(1024) void k_runs(DS d) {
   __syncthreads();
   u32 np2 = 1;
   while (np2 < R) np2 <<= 1;
-  const bool in_lds = np2 <= RUN_SORT_LDS;
+  const bool in_lds = np2 <= key_cap;
   u64* key = in_lds ? key_lds : d.run_key;
-  for (u32 i = R + tid; i < np2; i += 1024) key[i] = ~0ull;
+  for (u32 i = R + tid; i < np2; i += NT) key[i] = ~0ull;
   __syncthreads();
-  if (R > 1) bitonic_sort_u64(key, np2, tid, 1024);
+  if (R > 1) bitonic_sort_u64(key, np2, tid, NT);
   // pass 2: delivery offsets in run order
   u32 run = 0;
-  for (u32 b0 = 0; b0 < R; b0 += 1024) {
+  for (u32 b0 = 0; b0 < R; b0 += NT) {
     const u32 s = b0 + tid;
     u32 cnt = 0, slot = 0;
     if (s < R) { slot = (u32)key[s]; cnt = d.runs[slot].cnt; }
     u32 all;
-    u32 off = block_scan<1024>(cnt, lds, all);
+    u32 off = block_scan<NT>(cnt, lds, all);
     if (s < R) {
       const u32 start = run + off;
       d.run_order[s] = slot;
@@ -3808,6 +3827,11 @@ __global__ __launch_bounds__(1024) void k_runs(DS d) {
     d.tot[TS_NRUNS] = R;
     d.ctr->n_deliv = run;   // the saturating slot counter may have ended above deliv_max
   }
+}
+__global__ __launch_bounds__(1024) void k_runs(DS d) {
+  __shared__ u64 key_lds[RUN_SORT_LDS];
+  __shared__ u32 lds[1024 / 64 + 1];
+  runs_body<1024>(d, key_lds, RUN_SORT_LDS, lds);
 }
 
 DEV void wave_consumed(const DS& d, u32 msg, u32 q, u64 qpos, u32 kind, bool valid);
@@ -4847,14 +4871,19 @@ DEV void requeue_compact(const DS& d) {
   u32 run = 0;
   for (u32 b0 = 0; b0 < n; b0 += 256) {
     u32 i = b0 + threadIdx.x;
-    ReqItem r;
-    r.q = INVALID;
-    if (i < n) r = d.req[i];
-    u32 keep = (i < n && r.q != INVALID) ? 1 : 0;
+    // (fields as scalars: an aggregate copy across the scan's barriers was lowered to scratch)
+    u32 rq = INVALID, rm = 0;
+    u64 rp = 0;
+    i64 re = 0;
+    if (i < n) { rq = d.req[i].q; rm = d.req[i].msg; rp = d.req[i].qpos; re = d.req[i].expire_ms; }
+    u32 keep = (i < n && rq != INVALID) ? 1 : 0;
     u32 all;
     u32 off = block_scan<256>(keep, lds, all);
     __syncthreads();
-    if (keep) d.req[run + off] = r;  // run + off <= i: safe forward compaction
+    if (keep) {   // run + off <= i: safe forward compaction
+      ReqItem& o = d.req[run + off];
+      o.q = rq; o.msg = rm; o.qpos = rp; o.expire_ms = re;
+    }
     __syncthreads();
     run += all;
   }

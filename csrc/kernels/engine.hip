@@ -2186,8 +2186,7 @@ class Engine {
     hipLaunchKernelGGL(k_chan_advance, capped(nch, 1024), dim3(256), 0, s, d);
     // k_dequeue first puts requeued deliveries back in front of their queues' heads, in
     // queue-offset order (QueueEntity.scala:415-446), then dispatches
-    hipLaunchKernelGGL(k_dequeue, dim3(d.q_max), dim3(256), 0, s, d);
-    hipLaunchKernelGGL(k_runs, dim3(1), dim3(1024), 0, s, d);
+    hipLaunchKernelGGL(k_dequeue, dim3(d.q_max), dim3(256), 0, s, d);   // (its last block: k_runs)
     hipLaunchKernelGGL(k_dv_write, blocks(d.deliv_max, 256), dim3(256), 0, s, d);
     if (d.c_max <= CONN_LAYOUT_MAX) {
       hipLaunchKernelGGL(k_conn_layout, dim3(1), dim3(1024), 0, s, d);   // + the delivery-size scan
