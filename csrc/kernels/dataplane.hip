@@ -3742,8 +3742,9 @@ __global__ __launch_bounds__(256) void k_dequeue(DS d) {
   __shared__ u32 lds[256 / 64 + 1];
   __shared__ u32 s_last;
   dequeue_queue(d);
-  // every block's runs and counts are written (their stores returned) before its ticket
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  // every block's runs and counts reach the device-wide coherence point before its ticket
+  // (agent scope: the last block may run on another XCD, whose L2 does not see this one's)
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
   __syncthreads();
   if (threadIdx.x == 0) s_last = atomicAdd(&d.tot[TS_DQ_TICKET], 1u) == gridDim.x - 1;
   __syncthreads();
