@@ -578,16 +578,60 @@ class GpuDataPlane(ControlState):
         from ..store.cold import COLD_REC
         if not self.info.get("spill_bytes"):
             return 0
-        lim = self._u64("spill_tail", 0) + int(frac * self.info["spill_bytes"])
-        recs = np.frombuffer(self.eng.cold_pick(int(hot), int(lim), 1 << 16, int(max_bytes)), COLD_REC).copy()
+        lim = int(frac * self.info["spill_bytes"])   # (from the ring's tail)
+        recs = np.frombuffer(self.eng.cold_pick(int(hot), lim, 1 << 16, int(max_bytes)), COLD_REC).copy()
+        recs = self._cold_store(store, recs)
+        if recs is None:
+            return 0
+        self.eng.cold_commit(recs)
+        return int(recs["bytes"].sum())
+
+    def _cold_store(self, store, recs):
         recs = recs[recs["bytes"] > 0]
         if not len(recs):
-            return 0
+            return None
         ring, sb = self._spill_view(), self.info["spill_bytes"]
         views = [memoryview(ring[int(p) % sb:int(p) % sb + int(n)]) for p, n in zip(recs["pos"], recs["bytes"])]
         recs["cold"] = store.put_many(views)
-        self.eng.cold_commit(recs)
+        return recs
+
+    def _cold_load(self, store, recs):
+        ring, sb = self._spill_view(), self.info["spill_bytes"]
+        for p, n, c in zip(recs["pos"], recs["bytes"], recs["cold"]):
+            if n:
+                store.get_into(int(c), memoryview(ring[int(p) % sb:int(p) % sb + int(n)]))
+
+    # ---- the cold tier beside the steps (single GPU, pipelined front end): ``run(post)``
+    # posts one engine side operation, gets a step to carry it and returns its result
+    # (GpuBroker._side).  No pipeline drain: the steps keep running while the store is
+    # written or read.
+    def cold_out_side(self, store, run, hot=1 << 16, max_bytes=256 << 20, frac=0.5, min_used=0.6):
+        """cold_out with the pick and the commit as side operations; nothing moves while
+        the spill ring is less than ``min_used`` full (checked on the device)."""
+        from ..store.cold import COLD_REC
+        sb = self.info.get("spill_bytes")
+        if not sb:
+            return 0
+        raw = run(lambda: self.eng.side_cold_pick(int(hot), int(frac * sb), int(min_used * sb), 1 << 16,
+                                                  int(max_bytes)))
+        recs = self._cold_store(store, np.frombuffer(raw, COLD_REC).copy())
+        if recs is None:
+            return 0
+        run(lambda: self.eng.side_cold_commit(recs))
         return int(recs["bytes"].sum())
+
+    def cold_in_side(self, store, run, window=1 << 15):
+        """cold_in with the scan and the switch-back as side operations."""
+        from ..store.cold import COLD_REC
+        if not self.info.get("spill_bytes"):
+            return 0
+        recs = np.frombuffer(run(lambda: self.eng.side_cold_scan(int(window), 1 << 16)), COLD_REC).copy()
+        self._cold_load(store, recs)
+        run(lambda: self.eng.side_cold_in(recs))
+        return int(recs["bytes"].sum())
+
+    def cold_live_side(self, run):
+        return np.frombuffer(run(self.eng.side_cold_live), np.int64).copy()
 
     def cold_in(self, store, window=1 << 15):
         """Bodies of cold entries within ``window`` positions of their queue's head read
@@ -596,10 +640,7 @@ class GpuDataPlane(ControlState):
         if not self.info.get("spill_bytes"):
             return 0
         recs = np.frombuffer(self.eng.cold_scan(int(window), 1 << 16), COLD_REC).copy()
-        ring, sb = self._spill_view(), self.info["spill_bytes"]
-        for p, n, c in zip(recs["pos"], recs["bytes"], recs["cold"]):
-            if n:
-                store.get_into(int(c), memoryview(ring[int(p) % sb:int(p) % sb + int(n)]))
+        self._cold_load(store, recs)
         self.eng.cold_in(recs)
         return int(recs["bytes"].sum())
 

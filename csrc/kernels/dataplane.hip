@@ -4679,10 +4679,14 @@ __global__ __launch_bounds__(256) void k_spill(DS d, u64 lim, u32 hot, unsigned 
 // Candidates are taken from the oldest part of the ring (slot position below `lim`, like
 // k_spill's log limit): the ring is a FIFO, so only freeing its tail end makes room; a
 // queue with consumers keeps its first `hot` entries resident.
-__global__ __launch_bounds__(256) void k_cold_pick(DS d, u32 hot, u64 lim, ColdRec* out, u32 max_n, u32* n_out,
-                                                   unsigned long long* bytes, u64 max_bytes) {
+// `lim` counts from the ring's tail; nothing is picked while the ring holds less than
+// `min_used` bytes (the cold thread asks every 10 ms without reading the ring state)
+__global__ __launch_bounds__(256) void k_cold_pick(DS d, u32 hot, u64 lim_rel, u64 min_used, ColdRec* out, u32 max_n,
+                                                   u32* n_out, unsigned long long* bytes, u64 max_bytes) {
   const u32 q = blockIdx.x, lane = lane_id(), w = threadIdx.x >> 6;
   if (q >= d.q_max || !d.q_active[q] || d.spill_bytes == 0) return;
+  if (*d.spill_head - *d.spill_tail < min_used) return;
+  const u64 lim = *d.spill_tail + lim_rel;
   const u64 head = d.q_head[q], tail = d.q_tail[q], mask = d.q_ring_mask[q];
   const Desc* ring = d.ring + d.q_ring_off[q];
   const u64 skip = d.q_cons_n[q] ? hot : 0;
@@ -4719,6 +4723,8 @@ __global__ void k_cold_commit(DS d, const ColdRec* recs, u32 n) {
   if (i >= n) return;
   const ColdRec r = recs[i];
   if (!r.bytes || r.msg >= d.msg_max) return;
+  // (picked a few steps ago by the cold thread: an entry delivered since then stays spilled)
+  if (d.q_head[r.q] > r.qpos) return;
   MsgEnt& m = d.msgs[r.msg];
   const u64 expect = SPILL_BIT | r.pos;
   if (atomicCAS((unsigned long long*)&m.log_off, (unsigned long long)expect, (unsigned long long)(COLD_BIT | r.cold)) !=
@@ -4778,6 +4784,10 @@ __global__ __launch_bounds__(64) void k_cold_scan(DS d, u32 window, ColdRec* out
     pos = shfl64(pos, 0);
     k0 = (u32)__shfl((int)k0, 0);
     const u32 k = k0 + (u32)__popcll(cm & lanemask_lt());
+    // the reserved bytes count as live from here: steps that run before k_cold_in (the
+    // cold thread reads the store meanwhile) must not move the ring's tail over them
+    if (cold && ok) atomicAdd((unsigned long long*)&d.spill_live[((pos + off) / d.log_block) % d.n_spill_blocks],
+                              (unsigned long long)sz);
     if (cold && k < max_n) {   // (not ok: a record of bytes 0, skipped by the host)
       ColdRec r;
       r.msg = ok ? msg : INVALID; r.q = q; r.qpos = i; r.pos = pos + off; r.cold = lo & ~COLD_BIT;
@@ -4795,13 +4805,28 @@ __global__ void k_cold_in(DS d, const ColdRec* recs, u32 n, const u64* scan_end)
   if (i < n) {
     const ColdRec r = recs[i];
     if (r.bytes && r.msg < d.msg_max) {
-      d.msgs[r.msg].log_off = SPILL_BIT | r.pos;
-      atomicAdd((unsigned long long*)&d.spill_live[(r.pos / d.log_block) % d.n_spill_blocks], (unsigned long long)r.bytes);
-      atomicAdd((unsigned long long*)&d.cold_live[(r.cold >> COLD_SEG_SHIFT) % COLD_SEGS],
-                (unsigned long long)(-(i64)r.bytes));
+      // still the cold message the scan listed (not purged since): back to its ring slot;
+      // else the slot's reservation is returned
+      const unsigned long long expect = COLD_BIT | r.cold;
+      if (atomicCAS((unsigned long long*)&d.msgs[r.msg].log_off, expect, (unsigned long long)(SPILL_BIT | r.pos)) ==
+          expect)
+        atomicAdd((unsigned long long*)&d.cold_live[(r.cold >> COLD_SEG_SHIFT) % COLD_SEGS],
+                  (unsigned long long)(-(i64)r.bytes));
+      else
+        spill_free(d, SPILL_BIT | r.pos, r.bytes);
     }
   }
   if (i < d.q_max && scan_end[i] != 0) d.q_cold_lim[i] = scan_end[i];   // (0: not scanned)
+}
+
+// the cold thread's copy of a pick / scan: the listed records into host-mapped memory
+__global__ void k_side_out(const ColdRec* recs, const u32* cnt, u32 max_n, u32* out, u32* out_cnt) {
+  u32 n = *cnt;
+  if (n > max_n) n = max_n;
+  const u32 words = n * (u32)(sizeof(ColdRec) / 4);
+  const u32* src = (const u32*)recs;
+  for (u32 i = blockIdx.x * blockDim.x + threadIdx.x; i < words; i += gridDim.x * blockDim.x) out[i] = src[i];
+  if (blockIdx.x == 0 && threadIdx.x == 0) out_cnt[0] = n;
 }
 
 // ============================================================================ requeue (pre-step)

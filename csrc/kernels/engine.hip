@@ -14,6 +14,8 @@
 #include <map>
 #include <memory>
 #include <mutex>
+#include <condition_variable>
+#include <thread>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -447,6 +449,12 @@ class Engine {
     cold_cnt_ = (u32*)dev("cold_cnt", 16);
     cold_bytes_ = (unsigned long long*)dev("cold_bytes", 8);
     cold_end_ = (u64*)dev("cold_end", 8ull * d_.q_max);
+    if (d_.spill_bytes && d_.world == 1) {   // (side operations)
+      side_d_ = alloc("cold_side", sizeof(ColdRec) * COLD_BATCH + 64, true);
+      side_h_ = buf("cold_side").ptr;
+      side_live_h_ = (i64*)pinned("cold_side_live", 8ull * COLD_SEGS);
+      HIPCHECK(hipEventCreateWithFlags(&ev_side_, hipEventDisableTiming));
+    }
     d_.q_cold_lim = (u64*)dev("q_cold_lim", 8ull * d_.q_max);
     HIPCHECK(hipMemset(d_.q_cold_lim, 0xff, 8ull * d_.q_max));
 
@@ -659,6 +667,7 @@ class Engine {
       (void)hipEventDestroy(ev_done_[p]);
     }
     for (int e = 0; e < EGRESS_SLOTS; ++e) (void)hipEventDestroy(ev_d2h_[e]);
+    if (ev_side_) (void)hipEventDestroy(ev_side_);
     (void)hipStreamDestroy(s_comp_);
     (void)hipStreamDestroy(s_h2d_);
     (void)hipStreamDestroy(s_d2h_);
@@ -979,7 +988,7 @@ class Engine {
   }
   bool host_work() {
     std::lock_guard<std::mutex> g(dl_mu_);
-    if (!unp_ready_.empty()) return true;
+    if (!unp_ready_.empty() || side_queued()) return true;
     for (auto& bt : dl_)
       if (!bt.w.empty() || !bt.dirty.empty() || !bt.unp.empty()) return true;
     return false;
@@ -1110,6 +1119,11 @@ class Engine {
       // ingest half on s_ing_: after this step's H2D and once parity p's buffers are free
       // (the routing half of step t-2); the routing half on s_comp_ behind it and behind
       // the previous step's routing half (stream order), as a single step would run
+      // a side operation between the previous step's routing half and this step's ingest
+      if (side_queued()) {
+        run_side(s_comp_);
+        HIPCHECK(hipStreamWaitEvent(s_ing_, ev_side_, 0));
+      }
       HIPCHECK(hipStreamWaitEvent(s_ing_, ev_h2d_[p], 0));
       HIPCHECK(hipStreamWaitEvent(s_ing_, ev_pre_[p], 0));
       if (rest_issued_[p]) HIPCHECK(hipStreamWaitEvent(s_ing_, ev_rest_[p], 0));
@@ -1150,6 +1164,7 @@ class Engine {
       }
       return;
     }
+    if (side_h_) run_side(s_comp_);
     HIPCHECK(hipStreamWaitEvent(s_comp_, ev_h2d_[p], 0));
     if (d2h_issued_[e]) HIPCHECK(hipStreamWaitEvent(s_comp_, ev_d2h_[e], 0));
     if (d_.world > 1 && !xfer_set_) throw std::runtime_error("set_xfer_buffers() before the first sharded step");
@@ -1261,14 +1276,15 @@ class Engine {
 
   // ---- cold store (third body tier), between steps; the host moves the bytes
   // out: candidate records (ColdRec[], bytes 0 = skip) for the host to write to the store
+  // (slots below spill tail + lim)
   py::bytes cold_pick(u32 hot, u64 lim, u32 max_n, u64 max_bytes) {
     if (!d_.spill_bytes) return py::bytes("");
     cold_guard("cold_pick");
     if (max_n > COLD_BATCH) max_n = COLD_BATCH;
     HIPCHECK(hipMemsetAsync(cold_cnt_, 0, 16, s_comp_));
     HIPCHECK(hipMemsetAsync(cold_bytes_, 0, 8, s_comp_));
-    hipLaunchKernelGGL(k_cold_pick, dim3(d_.q_max), dim3(256), 0, s_comp_, io_[0], hot, lim, cold_recs_, max_n,
-                       cold_cnt_, cold_bytes_, max_bytes);
+    hipLaunchKernelGGL(k_cold_pick, dim3(d_.q_max), dim3(256), 0, s_comp_, io_[0], hot, lim, (u64)0, cold_recs_,
+                       max_n, cold_cnt_, cold_bytes_, max_bytes);
     return cold_fetch(max_n);
   }
   // ... the host stored them (ColdRec.cold = store offsets): switch the messages over
@@ -1295,6 +1311,111 @@ class Engine {
     hipLaunchKernelGGL(k_cold_in, blocks(g, 256), dim3(256), 0, s_comp_, io_[0], cold_recs_, n, cold_end_);
     HIPCHECK(hipStreamSynchronize(s_comp_));
   }
+  // ---- the same four operations beside the steps (no pipeline drain, single GPU): the
+  // cold thread posts one (side_*), the next launch() runs it on the compute stream between
+  // two steps, side_wait() hands back its records; the steps keep flowing while the host
+  // moves bodies between the ring and the store.  A pick is picked up again by the commit
+  // only where its entry is still queued (k_cold_commit); k_cold_scan's ring slots count as
+  // live until k_cold_in.  SIDE_LIVE copies cold_live (store segment GC).
+  enum : int { SIDE_NONE = 0, SIDE_PICK, SIDE_COMMIT, SIDE_SCAN, SIDE_IN, SIDE_LIVE };
+  void side_post(int kind, u32 a, u64 b, u64 c, u32 max_n, u64 max_bytes, const ColdRec* recs, u32 n) {
+    if (d_.world != 1) throw std::runtime_error("side operations: single-GPU engines only");
+    if (!side_h_) throw std::runtime_error("side operations: no spill ring");
+    std::lock_guard<std::mutex> g(side_mu_);
+    if (side_.kind) throw std::runtime_error("side operation pending (side_wait first)");
+    if (n) memcpy((u8*)side_h_ + 64, recs, sizeof(ColdRec) * n);
+    side_ = Side{kind, a, b, c, max_n > COLD_BATCH ? COLD_BATCH : max_n, max_bytes, n, false};
+  }
+  void side_cold_pick(u32 hot, u64 lim_rel, u64 min_used, u32 max_n, u64 max_bytes) {
+    side_post(SIDE_PICK, hot, lim_rel, min_used, max_n, max_bytes, nullptr, 0);
+  }
+  void side_cold_scan(u32 window, u32 max_n) { side_post(SIDE_SCAN, window, 0, 0, max_n, 0, nullptr, 0); }
+  void side_cold_commit(py::buffer recs) { side_recs(SIDE_COMMIT, recs); }
+  void side_cold_in(py::buffer recs) { side_recs(SIDE_IN, recs); }
+  void side_cold_live() { side_post(SIDE_LIVE, 0, 0, 0, 0, 0, nullptr, 0); }
+  void side_recs(int kind, py::buffer recs) {
+    py::buffer_info bi = recs.request();
+    const size_t nb = (size_t)bi.size * bi.itemsize;
+    if (nb % sizeof(ColdRec) || nb / sizeof(ColdRec) > COLD_BATCH) throw std::runtime_error("cold: bad ColdRec batch");
+    side_post(kind, 0, 0, 0, 0, 0, (const ColdRec*)bi.ptr, (u32)(nb / sizeof(ColdRec)));
+  }
+  bool side_queued() {
+    std::lock_guard<std::mutex> g(side_mu_);
+    return side_.kind && !side_.launched;
+  }
+  // launch(): the posted operation on stream s, ahead of the step's kernels
+  void run_side(hipStream_t s) {
+    std::lock_guard<std::mutex> g(side_mu_);
+    if (!side_.kind || side_.launched) return;
+    ColdRec* hrecs = (ColdRec*)((u8*)side_h_ + 64);
+    ColdRec* drecs = (ColdRec*)((u8*)side_d_ + 64);
+    switch (side_.kind) {
+      case SIDE_PICK:
+      case SIDE_SCAN:
+        HIPCHECK(hipMemsetAsync(cold_cnt_, 0, 16, s));
+        if (side_.kind == SIDE_PICK) {
+          HIPCHECK(hipMemsetAsync(cold_bytes_, 0, 8, s));
+          hipLaunchKernelGGL(k_cold_pick, dim3(d_.q_max), dim3(256), 0, s, io_[0], side_.a, side_.b, side_.c,
+                             cold_recs_, side_.max_n, cold_cnt_, cold_bytes_, side_.max_bytes);
+        } else {
+          HIPCHECK(hipMemsetAsync(cold_end_, 0, 8ull * d_.q_max, s));
+          hipLaunchKernelGGL(k_cold_scan, dim3(d_.q_max), dim3(64), 0, s, io_[0], side_.a, cold_recs_, side_.max_n,
+                             cold_cnt_, cold_end_);
+        }
+        hipLaunchKernelGGL(k_side_out, dim3(64), dim3(256), 0, s, (const ColdRec*)cold_recs_, (const u32*)cold_cnt_,
+                           side_.max_n, (u32*)drecs, (u32*)side_d_);
+        break;
+      case SIDE_COMMIT:
+      case SIDE_IN:
+        if (side_.n)
+          HIPCHECK(hipMemcpyAsync(cold_recs_, hrecs, sizeof(ColdRec) * side_.n, hipMemcpyHostToDevice, s));
+        if (side_.kind == SIDE_COMMIT) {
+          if (side_.n)
+            hipLaunchKernelGGL(k_cold_commit, blocks(side_.n, 256), dim3(256), 0, s, io_[0], cold_recs_, side_.n);
+        } else {
+          const u64 g2 = side_.n > d_.q_max ? side_.n : d_.q_max;
+          hipLaunchKernelGGL(k_cold_in, blocks(g2, 256), dim3(256), 0, s, io_[0], cold_recs_, side_.n, cold_end_);
+        }
+        break;
+      case SIDE_LIVE:
+        HIPCHECK(hipMemcpyAsync(side_live_h_, d_.cold_live, 8ull * COLD_SEGS, hipMemcpyDeviceToHost, s));
+        break;
+    }
+    HIPCHECK(hipGetLastError());
+    HIPCHECK(hipEventRecord(ev_side_, s));
+    side_.launched = true;
+    side_cv_.notify_all();
+  }
+  // the posted operation's result once it ran: ColdRec[] (pick / scan), cold_live bytes
+  // (live), b"" (commit / in); None while it has not finished within timeout_s
+  py::object side_wait(double timeout_s) {
+    int kind;
+    {
+      py::gil_scoped_release nogil;
+      std::unique_lock<std::mutex> g(side_mu_);
+      if (!side_.kind) throw std::runtime_error("side_wait: nothing posted");
+      const auto until = std::chrono::steady_clock::now() + std::chrono::microseconds((i64)(timeout_s * 1e6));
+      if (!side_cv_.wait_until(g, until, [&] { return side_.launched; })) return py::none();
+      kind = side_.kind;
+      g.unlock();
+      while (true) {
+        const hipError_t e = hipEventQuery(ev_side_);
+        if (e == hipSuccess) break;
+        if (e != hipErrorNotReady) HIPCHECK(e);
+        if (std::chrono::steady_clock::now() > until) return py::none();
+        std::this_thread::sleep_for(std::chrono::microseconds(50));
+      }
+    }
+    std::lock_guard<std::mutex> g(side_mu_);
+    side_.kind = SIDE_NONE;
+    if (kind == SIDE_PICK || kind == SIDE_SCAN) {
+      const u32 n = *(volatile u32*)side_h_;
+      return py::bytes((const char*)side_h_ + 64, sizeof(ColdRec) * (size_t)n);
+    }
+    if (kind == SIDE_LIVE) return py::bytes((const char*)side_live_h_, 8ull * COLD_SEGS);
+    return py::bytes("");
+  }
+
   void cold_guard(const char* what) {
     if (inflight_[0] || inflight_[1]) throw std::runtime_error(std::string(what) + "() between steps only");
     if (native_x_ && (counts_ready_[0] || counts_ready_[1]))
@@ -2334,6 +2455,14 @@ class Engine {
   u32 dl_step_[2] = {0, 0};
   u64 dl_steps_ = 0;
   static constexpr u32 COLD_BATCH = 1u << 16;   // cold records per pick / scan call
+  struct Side { int kind; u32 a; u64 b, c; u32 max_n; u64 max_bytes; u32 n; bool launched; };
+  Side side_{SIDE_NONE, 0, 0, 0, 0, 0, 0, false};
+  std::mutex side_mu_;
+  std::condition_variable side_cv_;
+  hipEvent_t ev_side_ = nullptr;
+  void* side_h_ = nullptr;      // host-mapped: [count @0][ColdRec[] @64]
+  void* side_d_ = nullptr;
+  i64* side_live_h_ = nullptr;
   ColdRec* cold_recs_ = nullptr;
   u32* cold_cnt_ = nullptr;
   unsigned long long* cold_bytes_ = nullptr;
@@ -2468,6 +2597,13 @@ PYBIND11_MODULE(_dataplane, m) {
       .def("cold_commit", &Engine::cold_commit)
       .def("cold_scan", &Engine::cold_scan, py::arg("window"), py::arg("max_n"))
       .def("cold_in", &Engine::cold_in)
+      .def("side_cold_pick", &Engine::side_cold_pick, py::arg("hot"), py::arg("lim"), py::arg("min_used"),
+           py::arg("max_n"), py::arg("max_bytes"))
+      .def("side_cold_commit", &Engine::side_cold_commit)
+      .def("side_cold_scan", &Engine::side_cold_scan, py::arg("window"), py::arg("max_n"))
+      .def("side_cold_in", &Engine::side_cold_in)
+      .def("side_cold_live", &Engine::side_cold_live)
+      .def("side_wait", &Engine::side_wait, py::arg("timeout_s"))
       .def("basic_get", &Engine::basic_get, py::arg("q"), py::arg("chslot"), py::arg("noack"), py::arg("now_ms"))
       .def("wait_results", &Engine::wait_results)
       .def("egress_copy", &Engine::egress_copy)

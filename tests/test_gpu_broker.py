@@ -783,7 +783,8 @@ def test_backlog_past_hbm_and_host_tiers_goes_to_the_cold_store(gpu, io, tmp_pat
     host memory, the full ring moves cold bodies to the cold store on disk (third tier,
     MessageEntity.scala:174-186), publishers are never paused or nacked; the consumer then
     gets every message in order and intact -- each cold body read back into the ring
-    just before its queue position is delivered."""
+    just before its queue position is delivered.  With the native front end both tiers
+    ride the steps: the stepper never pauses for them."""
     import time
     from chanamq_amd.engine.dataplane import GpuDataPlane
     from chanamq_amd.server.gpu_broker import GpuBroker
@@ -796,6 +797,7 @@ def test_backlog_past_hbm_and_host_tiers_goes_to_the_cold_store(gpu, io, tmp_pat
         ch = p.channel()
         ch.queue_declare("deep")
         ch.confirm_select()
+        pauses0 = b.stats.get("pauses", 0)
         n, size = 36864, 16 << 10   # 576 MB of bodies: 6x (log + ring)
         for k in range(n):
             ch.basic_publish("", "deep", k.to_bytes(4, "big") * (size // 4))
@@ -814,6 +816,9 @@ def test_backlog_past_hbm_and_host_tiers_goes_to_the_cold_store(gpu, io, tmp_pat
         assert [int.from_bytes(d.body[:4], "big") for d in got] == list(range(n))
         assert all(d.body == d.body[:4] * (size // 4) for d in got[::101])
         assert b.stats.get("cold_in_bytes", 0) > (256 << 20)
+        if io == "pipeline":   # (the consumer's own declare / consume are light sections)
+            assert b.stats.get("cold_side_ops", 0) > 0 and b.stats.get("cold_errors", 0) == 0, b.stats
+            assert b.stats.get("pauses", 0) - pauses0 <= 2, b.stats
         p.close()
         c.close()
     finally:
