@@ -283,7 +283,6 @@ def main():
     sub_t = {}      # step index -> host time its ingress was handed to the GPU (submit / prefetch)
     slow = {"ms": 0.0}   # the timed window's slowest loop iteration: submit / prefetch / egress / finish
     phases = []          # every timed iteration's phases (ms): submit, prefetch, egress wait, finish
-    diag_first = [None] if os.environ.get("CHANAMQ_BENCH_DIAG_FIRST") else []
     pre = set()     # steps whose payload H2D is already queued (prefetch)
     lat_w = []      # (publish->deliver seconds, deliveries) of the timed steps
 
@@ -432,8 +431,6 @@ def main():
             if measure:
                 ph = [round((b2 - a2) * 1e3, 3) for a2, b2 in zip(tp, tp[1:])]
                 phases.append(ph)
-                if diag_first and i < 3:   # (diagnostics only: the engine's host phase sums so far)
-                    diag_first.append({k: round(v * 1e6, 1) for k, v in dp.eng.host_times(False).items() if v})
                 if sum(ph) > slow["ms"]:
                     slow.update(ms=round(sum(ph), 3), step=i, phases_ms=ph)
         for t, s in done:
@@ -444,6 +441,12 @@ def main():
             ready(s)
         return dl, pb, hist, eg
 
+    # the host loop is the pipeline's driver: no collector pause inside the window.  Collected
+    # before the warm-up steps, which then re-warm the allocator (a collection right before
+    # the window made the first timed submit 0.6 ms slower: profiles/r5_first/)
+    import gc
+    gc.collect()
+    gc.disable()
     run(args.warmup)
     if dist:
         dist.barrier()
@@ -452,9 +455,6 @@ def main():
     if shards > 1 and not native:
         dp.exchanger.bytes_sent = 0
     dp.eng.host_times(True)
-    import gc
-    gc.collect()
-    gc.disable()   # the host loop is the pipeline's driver: no collector pause inside the window
     t0 = time.perf_counter()
     dl, pb, hist, eg = run(args.steps, measure=True)
     dp.eng.sync()
@@ -540,7 +540,6 @@ def main():
             "diag": errs,
             "slowest_iteration": slow,
             "first_iterations_ms": phases[:3],
-            **({"diag_first_host_us": diag_first[1:]} if diag_first else {}),
             "iteration_phases_ms_median": ([round(float(np.median([p[k] for p in phases if len(p) > k])), 4)
                                             for k in range(max(len(p) for p in phases))] if phases else None),
             "host_us_per_step": {k: round(v * 1e6 / args.steps, 1) for k, v in dp.eng.host_times(False).items()},
