@@ -2050,6 +2050,11 @@ class GpuBroker:
             except Exception as e:   # (kept running: a store error must not end the tier)
                 self.stats["cold_errors"] = self.stats.get("cold_errors", 0) + 1
                 logging.getLogger("chanamq.gpu").warning("cold tier: %s", e)
+                try:   # an operation posted before the error still completes first
+                    while self._running and self.plane.eng.side_pending():
+                        self.plane.eng.side_wait(0.05)
+                except Exception:
+                    pass
                 time.sleep(0.1)
 
     def _set_flow(self, active):

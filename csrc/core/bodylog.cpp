@@ -242,16 +242,40 @@ void BodyLog::unref(const Loc& l) {
 }
 
 void BodyLog::reap() {
-  std::lock_guard<std::mutex> a(amu_);
-  for (uint32_t seg : dead_) {
-    auto it = segs_.find(seg);
-    if (it == segs_.end() || it->second.live_n || it->second.current) continue;
-    if (it->second.rfd >= 0) ::close(it->second.rfd);
-    ::unlink(path(seg).c_str());
-    stats_.reclaimed += it->second.size;
-    segs_.erase(it);
+  std::vector<std::pair<int, std::string>> out;
+  {
+    std::lock_guard<std::mutex> a(amu_);
+    for (uint32_t seg : dead_) {
+      auto it = segs_.find(seg);
+      if (it == segs_.end() || it->second.live_n || it->second.current) continue;
+      out.emplace_back(it->second.rfd, path(seg));
+      stats_.reclaimed += it->second.size;
+      segs_.erase(it);
+    }
+    dead_.clear();
   }
-  dead_.clear();
+  if (out.empty()) return;
+  std::lock_guard<std::mutex> r(rmu_);
+  if (!reap_th_.joinable()) {
+    reap_stop_ = false;
+    reap_th_ = std::thread([this] { reaper(); });
+  }
+  for (auto& e : out) reap_q_.push_back(std::move(e));
+  rcv_.notify_one();
+}
+
+void BodyLog::reaper() {
+  std::unique_lock<std::mutex> r(rmu_);
+  while (true) {
+    rcv_.wait(r, [&] { return reap_stop_ || !reap_q_.empty(); });
+    if (reap_q_.empty()) return;   // (stop: after the queue drained)
+    auto e = std::move(reap_q_.front());
+    reap_q_.pop_front();
+    r.unlock();
+    if (e.first >= 0) ::close(e.first);
+    ::unlink(e.second.c_str());
+    r.lock();
+  }
 }
 
 bool BodyLog::read(const Loc& l, std::string* rec) {
@@ -338,6 +362,13 @@ void BodyLog::close() {
     }
   }
   if (dfd_ >= 0) { ::close(dfd_); dfd_ = -1; }
+  {
+    std::unique_lock<std::mutex> r(rmu_);
+    reap_stop_ = true;
+    rcv_.notify_all();
+    r.unlock();
+    if (reap_th_.joinable()) reap_th_.join();
+  }
   std::lock_guard<std::mutex> g(mu_);
   std::lock_guard<std::mutex> a(amu_);
   st_.clear();

@@ -1339,6 +1339,10 @@ class Engine {
     if (nb % sizeof(ColdRec) || nb / sizeof(ColdRec) > COLD_BATCH) throw std::runtime_error("cold: bad ColdRec batch");
     side_post(kind, 0, 0, 0, 0, 0, (const ColdRec*)bi.ptr, (u32)(nb / sizeof(ColdRec)));
   }
+  bool side_pending() {
+    std::lock_guard<std::mutex> g(side_mu_);
+    return side_.kind != SIDE_NONE;
+  }
   bool side_queued() {
     std::lock_guard<std::mutex> g(side_mu_);
     return side_.kind && !side_.launched;
@@ -1389,23 +1393,27 @@ class Engine {
   // the posted operation's result once it ran: ColdRec[] (pick / scan), cold_live bytes
   // (live), b"" (commit / in); None while it has not finished within timeout_s
   py::object side_wait(double timeout_s) {
-    int kind;
+    int kind = SIDE_NONE;
+    hipError_t err = hipSuccess;
+    bool done = false;
     {
-      py::gil_scoped_release nogil;
+      py::gil_scoped_release nogil;   // (no Python objects in here)
       std::unique_lock<std::mutex> g(side_mu_);
-      if (!side_.kind) throw std::runtime_error("side_wait: nothing posted");
-      const auto until = std::chrono::steady_clock::now() + std::chrono::microseconds((i64)(timeout_s * 1e6));
-      if (!side_cv_.wait_until(g, until, [&] { return side_.launched; })) return py::none();
       kind = side_.kind;
-      g.unlock();
-      while (true) {
-        const hipError_t e = hipEventQuery(ev_side_);
-        if (e == hipSuccess) break;
-        if (e != hipErrorNotReady) HIPCHECK(e);
-        if (std::chrono::steady_clock::now() > until) return py::none();
-        std::this_thread::sleep_for(std::chrono::microseconds(50));
+      const auto until = std::chrono::steady_clock::now() + std::chrono::microseconds((i64)(timeout_s * 1e6));
+      if (kind && side_cv_.wait_until(g, until, [&] { return side_.launched; })) {
+        g.unlock();
+        while (true) {
+          err = hipEventQuery(ev_side_);
+          if (err == hipSuccess) { done = true; break; }
+          if (err != hipErrorNotReady || std::chrono::steady_clock::now() > until) break;
+          std::this_thread::sleep_for(std::chrono::microseconds(50));
+        }
       }
     }
+    if (!kind) throw std::runtime_error("side_wait: nothing posted");
+    if (err != hipSuccess && err != hipErrorNotReady) HIPCHECK(err);
+    if (!done) return py::none();
     std::lock_guard<std::mutex> g(side_mu_);
     side_.kind = SIDE_NONE;
     if (kind == SIDE_PICK || kind == SIDE_SCAN) {
@@ -2604,6 +2612,7 @@ PYBIND11_MODULE(_dataplane, m) {
       .def("side_cold_in", &Engine::side_cold_in)
       .def("side_cold_live", &Engine::side_cold_live)
       .def("side_wait", &Engine::side_wait, py::arg("timeout_s"))
+      .def("side_pending", &Engine::side_pending)
       .def("basic_get", &Engine::basic_get, py::arg("q"), py::arg("chslot"), py::arg("noack"), py::arg("now_ms"))
       .def("wait_results", &Engine::wait_results)
       .def("egress_copy", &Engine::egress_copy)
