@@ -183,7 +183,7 @@ class GpuBroker:
                  idle_step_ms=2.0, product="chanamq-amd", version="0.1.0", io="native",
                  ingress_bytes=64 << 20, per_conn_read=256 << 10, mem_high_watermark=None, mem_low_watermark=None,
                  store=None, node=None, reuseport=False, io_threads=4, fe_cfg=None, spill_at=None, spill_hot=1024,
-                 confirm_read=128 << 10, cold_dir=None, cold=True, cold_hot=1 << 16, cold_window=1 << 15,
+                 confirm_read=128 << 10, cold_dir=None, cold=True, cold_hot=1 << 16, cold_window=1 << 15, cold_beside=True,
                  persist_group_ms=2.0):
         """``io``: "pipeline" = native pipelined front end (csrc/core/frontend.cpp: IO
         threads + a stepper thread keeping two steps in flight, no Python per step),
@@ -247,6 +247,7 @@ class GpuBroker:
             self.cold = ColdStore(cold_dir)
             plane.cold_store = self.cold
         self.cold_hot, self.cold_window = cold_hot, cold_window
+        self.cold_beside = cold_beside
         self._last_cold = self._last_cold_gc = 0.0
         self._cold_pending = False
         # durable queues x persistent messages -> store (write-behind, confirm gating)
@@ -2004,7 +2005,7 @@ class GpuBroker:
     def _cold_beside(self):
         """The cold tier runs beside the steps (its own thread, engine side operations)
         on a single-GPU engine driven by the native front end."""
-        return (self.cold is not None and self.fe is not None and self.node is None
+        return (self.cold_beside and self.cold is not None and self.fe is not None and self.node is None
                 and hasattr(getattr(self.plane, "eng", None), "side_cold_pick"))
 
     def _side(self, post):

@@ -26,6 +26,8 @@
 #               threads, LG load-generator threads, TAG output-name suffix)
 #   e2e_c2      config 2 only over TCP, paced at 50 % (E2E_ARGS appended)
 #   churn       config 2 paced at 50 % next to connection / consumer churn (E2E_ARGS appended)
+#   cold        bench/cold_paging.py: a backlog through all three body tiers, drained under live
+#               traffic (COLD_ARGS appended)
 #   sharded     the sharded-server GPU tests
 #   tests:PAT   pytest -m gpu -x -k PAT
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
@@ -137,6 +139,9 @@ for T in "$@"; do
     timeout -k 10 400 python -u bench/gpu_server_e2e.py --seconds 5 --io-threads ${IOT:-8} --only config2 --paced 0.5 \
       --churn --out $O/e2e_churn.json $E2E_ARGS > $O/e2e_churn.log 2>&1
     rc=$?; tail -4 $O/e2e_churn.log | cut -c1-800; ok $rc churn ;;
+  cold)   # timed cold paging: backlog through HBM log -> host ring -> disk, drained under live traffic
+    timeout -k 10 300 python -u bench/cold_paging.py --out $O/cold_paging.json $COLD_ARGS > $O/cold_paging.log 2>&1
+    rc=$?; tail -3 $O/cold_paging.log | cut -c1-600; ok $rc cold ;;
   sharded)
     timeout -k 10 700 $PYT tests/test_gpu_sharded_server.py tests/test_gpu_sharded.py -m gpu -x -v > $O/pytest_sharded.log 2>&1
     rc=$?; tail -4 $O/pytest_sharded.log; ok $rc sharded ;;
