@@ -140,9 +140,10 @@ def setup_native_exchange(args, cfg, GpuDataPlane, dist, backend, local, rank, w
         dist.broadcast_object_list(names, src=0)
         nm = names[0]
         if kind == "rccl":
-            dp.xchg_setup("rccl", nm["uid"], list(range(world)), args.xchg_timeout_ms, counts_shm=nm["shm"] + "-c")
+            dp.xchg_setup("rccl", nm["uid"], list(range(world)), args.xchg_timeout_ms, counts_shm=nm["shm"] + "-c",
+                          async_x=bool(args.async_x))
         else:
-            dp.xchg_setup("shm", nm["shm"], list(range(world)), args.xchg_timeout_ms)
+            dp.xchg_setup("shm", nm["shm"], list(range(world)), args.xchg_timeout_ms, async_x=bool(args.async_x))
     except Exception as e:   # noqa: BLE001 - reported, then agreed on below
         err = e
     bad = torch.tensor([1.0 if err is not None else 0.0], device="cuda" if backend == "nccl" else "cpu")
@@ -212,6 +213,9 @@ def main():
                          "CHANAMQ_BENCH_BACKEND=gloo: the shared-memory backend) -- or torch.distributed "
                          "all_to_all_single (parallel/exchange.py)")
     ap.add_argument("--xchg-timeout-ms", type=int, default=30000)
+    ap.add_argument("--async-x", type=int, default=1,
+                    help="native exchange on the engine's exchange thread, phase B waiting on the device (0: "
+                         "the stepper runs each exchange itself)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))

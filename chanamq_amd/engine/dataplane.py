@@ -786,13 +786,15 @@ class GpuDataPlane(ControlState):
         t = self.submit_raw(segs, payload_ptr, payload_len, now_ms)
         return self.finish(t, collect=collect)
 
-    def xchg_setup(self, kind, arg, members, timeout_ms=10000, failover=False, counts_shm=""):
+    def xchg_setup(self, kind, arg, members, timeout_ms=10000, failover=False, counts_shm="", async_x=False):
         """Native exchange backend over the live ranks ``members``: "rccl" (arg = the
         128-byte unique id from ``xchg_unique_id()``) or "shm" (arg = a shared-memory name
         common to the group, for ranks sharing one host).  ``counts_shm`` (rccl): move the
-        per-step counts through host shared memory (ranks of one node), the bulk on RCCL."""
+        per-step counts through host shared memory (ranks of one node), the bulk on RCCL.
+        ``async_x``: each step's exchange runs on the engine's exchange thread and phase B
+        waits for it on the device; ``exchange()`` returns the previous step's result."""
         self.eng.xchg_setup(kind, arg, sorted(int(m) for m in members), int(timeout_ms), bool(failover),
-                            counts_shm)
+                            counts_shm, bool(async_x))
 
     def xchg_unique_id(self):
         return self.mod.Engine.xchg_unique_id()

@@ -66,6 +66,8 @@ def main(argv=None):
     ap.add_argument("--no-fsync", action="store_true")
     ap.add_argument("--backend", default="", help="default: nccl (RCCL) for --plane gpu, gloo for golden; "
                                                   "gloo + gpu rehearses several ranks on one GPU")
+    ap.add_argument("--async-x", type=int, default=1,
+                    help="each step's exchange on the engine's exchange thread (phase B waits on the device)")
     ap.add_argument("--xchg-timeout-ms", type=int, default=15000,
                     help="pipeline: a peer silent this long in an exchange is failed over")
     ap.add_argument("--hb-timeout-s", type=float, default=3.0)
@@ -121,7 +123,7 @@ def main(argv=None):
                 if rank == min(live):
                     store.set(key, plane.xchg_unique_id())
                 uid = store.get(key)
-                plane.xchg_setup("rccl", uid, live, args.xchg_timeout_ms, failover=True)
+                plane.xchg_setup("rccl", uid, live, args.xchg_timeout_ms, failover=True, async_x=bool(args.async_x))
             else:
                 # a fresh segment name per launch and epoch, chosen by the lowest live rank: a
                 # segment left by a killed earlier run (same store address) is never reused
@@ -129,7 +131,7 @@ def main(argv=None):
                 if rank == min(live):
                     store.set(key, f"{shm_base}-{os.getpid()}-{uuid.uuid4().hex[:12]}-e{epoch}")
                 name = store.get(key).decode()
-                plane.xchg_setup("shm", name, live, args.xchg_timeout_ms, failover=True)
+                plane.xchg_setup("shm", name, live, args.xchg_timeout_ms, failover=True, async_x=bool(args.async_x))
         rebuild_xchg(list(range(world)), 0)
         node.rebuild_xchg = rebuild_xchg
     st = None

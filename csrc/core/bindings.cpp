@@ -343,7 +343,8 @@ PYBIND11_MODULE(_core, m) {
            py::arg("carry_cap"), py::arg("world") = 1, py::arg("rank") = 0)
       .def("c_api", &EchoEngine::c_api)
       .def("unpause", &EchoEngine::unpause)
-      .def("xchg_setup", &EchoEngine::xchg_setup, py::arg("name"), py::arg("members"), py::arg("timeout_ms") = 5000)
+      .def("xchg_setup", &EchoEngine::xchg_setup, py::arg("name"), py::arg("members"), py::arg("timeout_ms") = 5000,
+           py::arg("async_x") = false)
       .def_readonly("imported", &EchoEngine::imported)
       .def_readonly("steps", &EchoEngine::steps);
 

@@ -1385,6 +1385,13 @@ void Frontend::park_sync(int kind, u64 step) {
 void Frontend::stepper_sharded() {
   pthread_setname_np(pthread_self(), "cmq-stepper");
   std::deque<Inflight> inflight;
+  // drop the pending exchange of parity q: 0, -1 error (reported), -2 the asynchronous
+  // exchange still in flight failed (its phase B imported nothing): a failover
+  auto dropx = [&](int q) -> int {
+    const int r = api_->drop_exchange(api_->eng, q);
+    if (r == -1) check(-1);
+    return r;
+  };
   while (running_ && !failed_) {
     bool want_pause;
     {
@@ -1464,7 +1471,7 @@ void Frontend::stepper_sharded() {
       if (rc == -1) { check(-1); break; }
       if (rc == -2) {
         xfail = true;
-        if (!check(api_->drop_exchange(api_->eng, xpend_))) break;
+        if (dropx(xpend_) == -1) break;
       } else if (orf & XF_SYNC) {
         sync_req_ = false;   // served by this sync (later requests join its control batch)
       }
@@ -1503,7 +1510,7 @@ void Frontend::stepper_sharded() {
         u32 dummy = 0;
         int rc = api_->exchange(api_->eng, xpend_, 0, &dummy);
         if (rc == -1) { check(-1); bad = true; break; }
-        if (rc == -2) { xfail = true; if (!check(api_->drop_exchange(api_->eng, xpend_))) { bad = true; break; } }
+        if (rc == -2) { xfail = true; if (dropx(xpend_) == -1) { bad = true; break; } }
         if (!check(api_->launch_b(api_->eng, p2))) { bad = true; break; }
         Inflight f2;
         f2.p = p2;
@@ -1514,7 +1521,11 @@ void Frontend::stepper_sharded() {
         xpend_ = p2;
       }
       if (bad) break;
-      if (xpend_ >= 0 && !check(api_->drop_exchange(api_->eng, xpend_))) break;   // packed nothing
+      if (xpend_ >= 0) {   // packed nothing (asynchronous: the last flush exchange lands first)
+        const int r = dropx(xpend_);
+        if (r == -1) break;
+        if (r == -2) xfail = true;
+      }
       xpend_ = -1;
       {
         std::lock_guard<std::mutex> g(stats_mu_);
@@ -1530,7 +1541,7 @@ void Frontend::stepper_sharded() {
       }
     }
     if (xfail) {   // a peer is gone: nothing of the failed exchange was imported anywhere
-      if (xpend_ >= 0 && !check(api_->drop_exchange(api_->eng, xpend_))) break;
+      if (xpend_ >= 0 && dropx(xpend_) == -1) break;
       xpend_ = -1;
       drain(inflight);
       flush_pending(false);
@@ -1654,34 +1665,117 @@ void Frontend::flush_pending(bool final) {
 }
 
 // ============================================================================ EchoEngine
-EchoEngine::~EchoEngine() = default;
+EchoEngine::~EchoEngine() { x_stop(); }
 
-void EchoEngine::xchg_setup(const std::string& name, const std::vector<int>& members, int timeout_ms) {
+void EchoEngine::xchg_setup(const std::string& name, const std::vector<int>& members, int timeout_ms, bool async) {
+  x_stop();
   shm_.reset();
   members_ = members;
   std::sort(members_.begin(), members_.end());
   shm_.reset(new cmqx::ShmXchg(name, members_, (int)rank_, 1 << 20, timeout_ms));
   xseq_ = 0;
   imports_.clear();
+  async_ = async;
+  if (async_) xth_ = std::thread([this] { x_loop(); });
 }
 
-// the shared-memory exchange of the step of parity q: forwarded segments travel as
-// [u32 conn][u32 len][bytes] records
-int EchoEngine::exchange(int q, u32 flags, u32* orf) {
+void EchoEngine::x_stop() {
+  {
+    std::lock_guard<std::mutex> g(xmu_);
+    xstop_ = true;
+    xcv_.notify_all();
+  }
+  if (xth_.joinable()) xth_.join();
+  std::lock_guard<std::mutex> g(xmu_);
+  xstop_ = xjob_ = xbusy_ = xres_ = false;
+  b_wait_[0] = b_wait_[1] = b_due_[0] = b_due_[1] = false;
+}
+
+// forwarded segments of the step of parity q, per member: [u32 conn][u32 len][bytes] records
+std::vector<std::string> EchoEngine::pack_fwd(int q) {
   Io& io = io_[q];
-  if (!io.ready) { err_ = "exchange: no phase-A step of this parity"; return -1; }
   const int n = (int)members_.size();
-  int me = 0;
-  for (int i = 0; i < n; ++i) if (members_[i] == (int)rank_) me = i;
   std::vector<std::string> blocks(n);
   for (int i = 0; i < n; ++i) {
-    if (i == me) continue;
+    if (members_[i] == (int)rank_) continue;
     for (auto& rec : io.fwd[members_[i]]) {
       u32 h[2] = {rec.first, (u32)rec.second.size()};
       blocks[i].append((const char*)h, 8);
       blocks[i] += rec.second;
     }
   }
+  return blocks;
+}
+
+// the last job's result (waits for it); 0 / flags 0 when none is uncollected
+int EchoEngine::collect(u32* orf) {
+  std::unique_lock<std::mutex> g(xmu_);
+  xcv_.wait(g, [&] { return !xjob_ && !xbusy_; });
+  *orf = 0;
+  if (!xres_) return 0;
+  xres_ = false;
+  *orf = xres_orf_;
+  return xres_rc_;
+}
+
+void EchoEngine::x_loop() {
+  std::unique_lock<std::mutex> g(xmu_);
+  while (true) {
+    xcv_.wait(g, [&] { return xstop_ || xjob_; });
+    if (!xjob_) return;
+    std::vector<std::string> blocks = std::move(xblocks_);
+    const u32 fl = xflags_;
+    const int dst = xdst_;
+    xjob_ = false;
+    xbusy_ = true;
+    g.unlock();
+    u32 orf = 0;
+    std::vector<std::pair<u32, std::string>> im;
+    const int rc = exchange_blocks(blocks, fl, &orf, &im);
+    if (rc) im.clear();   // phase B imports nothing
+    g.lock();
+    ximports_ = std::move(im);
+    b_wait_[dst] = false;
+    if (b_due_[dst]) {   // launched before its exchange finished: it runs now
+      b_due_[dst] = false;
+      run_b(dst, ximports_);
+    }
+    xbusy_ = false;
+    xres_ = true;
+    xres_rc_ = rc;
+    xres_orf_ = orf;
+    xcv_.notify_all();
+  }
+}
+
+// the shared-memory exchange of the step of parity q
+int EchoEngine::exchange(int q, u32 flags, u32* orf) {
+  Io& io = io_[q];
+  if (!io.ready) { err_ = "exchange: no phase-A step of this parity"; return -1; }
+  std::vector<std::string> blocks = pack_fwd(q);
+  if (!async_) {
+    const int rc = exchange_blocks(blocks, flags, orf, &imports_);
+    if (rc == 0) io.ready = false;
+    return rc;
+  }
+  const int rc = collect(orf);
+  if (rc) return rc;
+  io.ready = false;
+  std::lock_guard<std::mutex> g(xmu_);
+  xblocks_ = std::move(blocks);
+  xflags_ = flags;
+  xdst_ = q ^ 1;
+  b_wait_[q ^ 1] = true;
+  xjob_ = true;
+  xcv_.notify_all();
+  return 0;
+}
+
+int EchoEngine::exchange_blocks(std::vector<std::string>& blocks, u32 flags, u32* orf,
+                                std::vector<std::pair<u32, std::string>>* imports) {
+  const int n = (int)members_.size();
+  int me = 0;
+  for (int i = 0; i < n; ++i) if (members_[i] == (int)rank_) me = i;
   std::vector<u32> hs((size_t)n * cmqx::XH_WORDS, 0), hr((size_t)n * cmqx::XH_WORDS, 0);
   for (int i = 0; i < n; ++i) {
     hs[(size_t)i * cmqx::XH_WORDS + 1] = (u32)blocks[i].size();
@@ -1706,7 +1800,7 @@ int EchoEngine::exchange(int q, u32 flags, u32* orf) {
   }
   rc = shm_->barrier();
   if (rc) return rc;
-  imports_.clear();
+  imports->clear();
   for (int i = 0; i < n; ++i) {
     if (i == me) continue;
     const u8* src = shm_->box(i) + shm_->dir(i)[me];
@@ -1714,20 +1808,29 @@ int EchoEngine::exchange(int q, u32 flags, u32* orf) {
     for (u32 k = 0; k + 8 <= len;) {
       u32 h[2];
       memcpy(h, src + k, 8);
-      imports_.emplace_back(h[0], std::string((const char*)src + k + 8, h[1]));
+      imports->emplace_back(h[0], std::string((const char*)src + k + 8, h[1]));
       k += 8 + h[1];
     }
   }
-  io.ready = false;
   ++xseq_;
   return 0;
 }
 
 // phase B: imported records become egress of their connection slot in this step
 void EchoEngine::launch_b(int p) {
+  if (async_) {
+    std::lock_guard<std::mutex> g(xmu_);
+    if (b_wait_[p]) { b_due_[p] = true; return; }   // after its exchange (x_loop)
+    run_b(p, ximports_);   // (its exchange finished first, or none: nothing to import)
+    return;
+  }
+  run_b(p, imports_);
+}
+
+void EchoEngine::run_b(int p, std::vector<std::pair<u32, std::string>>& imports) {
   Io& io = io_[p];
   std::string& eg = slot_[slot_of_[p]];
-  for (auto& im : imports_) {
+  for (auto& im : imports) {
     if (im.first >= io.co.size()) continue;
     ConnOut& c = io.co[im.first];
     std::string prev = c.len ? eg.substr(c.off, c.len) : std::string();
@@ -1738,7 +1841,7 @@ void EchoEngine::launch_b(int p) {
     io.ctr.n_deliv++;
     ++imported;
   }
-  imports_.clear();
+  imports.clear();
   io.ctr.egress_bytes = (u32)eg.size();
 }
 
@@ -1811,7 +1914,13 @@ EchoEngine::EchoEngine(u32 c_max, u32 seg_max, u64 ingress_cap, u32 carry_cap, u
     io.ctr.egress_bytes = (u32)eg.size();
     return p;
   };
-  api_.wait_results = [](void*, int) -> int { return 0; };
+  api_.wait_results = [](void* e, int p) -> int {   // (asynchronous: phase B ran)
+    EchoEngine& E = *(EchoEngine*)e;
+    if (!E.async_) return 0;
+    std::unique_lock<std::mutex> g(E.xmu_);
+    E.xcv_.wait(g, [&] { return !E.b_due_[p]; });
+    return 0;
+  };
   api_.egress_slot = [](void* e, int p) -> int { return ((EchoEngine*)e)->slot_of_[p]; };
   api_.egress_copy = [](void*, int) -> int { return 0; };
   api_.egress_wait_slot = [](void*, int) -> int { return 0; };
@@ -1828,9 +1937,12 @@ EchoEngine::EchoEngine(u32 c_max, u32 seg_max, u64 ingress_cap, u32 carry_cap, u
   api_.consumed_host = [](void*, int) -> const ConsumedRec* { return nullptr; };
   api_.exchange = [](void* e, int q, u32 flags, u32* orf) -> int { return ((EchoEngine*)e)->exchange(q, flags, orf); };
   api_.drop_exchange = [](void* e, int q) -> int {
-    ((EchoEngine*)e)->io_[q].ready = false;
-    ((EchoEngine*)e)->imports_.clear();
-    return 0;
+    EchoEngine& E = *(EchoEngine*)e;
+    E.io_[q].ready = false;
+    E.imports_.clear();
+    if (!E.async_) return 0;
+    u32 orf = 0;
+    return E.collect(&orf);   // the job in flight (its phase B has run)
   };
   api_.launch_b = [](void* e, int p) -> int { ((EchoEngine*)e)->launch_b(p); return 0; };
   api_.links = 0;

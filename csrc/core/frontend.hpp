@@ -338,7 +338,11 @@ class EchoEngine {
   ~EchoEngine();
   u64 c_api() { return (u64)&api_; }
   void unpause(u32 conn);
-  void xchg_setup(const std::string& name, const std::vector<int>& members, int timeout_ms);
+  // async: the Engine's asynchronous exchange, emulated -- exchange() hands the step's
+  // records to an exchange thread and returns the previous exchange's result; phase B runs
+  // once its exchange finished (on that thread when launch_b came first); wait_results
+  // waits for it
+  void xchg_setup(const std::string& name, const std::vector<int>& members, int timeout_ms, bool async = false);
   u64 steps = 0, imported = 0;
 
  private:
@@ -353,7 +357,25 @@ class EchoEngine {
     bool ready = false;                                  // phase A done, exchange due
   };
   int exchange(int q, u32 flags, u32* orf);
+  int exchange_blocks(std::vector<std::string>& blocks, u32 flags, u32* orf,
+                      std::vector<std::pair<u32, std::string>>* imports);
+  std::vector<std::string> pack_fwd(int q);
   void launch_b(int p);
+  void run_b(int p, std::vector<std::pair<u32, std::string>>& imports);
+  int collect(u32* orf);
+  void x_loop();
+  void x_stop();
+  bool async_ = false;
+  std::thread xth_;
+  std::mutex xmu_;
+  std::condition_variable xcv_;
+  bool xstop_ = false, xjob_ = false, xbusy_ = false, xres_ = false;
+  int xres_rc_ = 0, xdst_ = -1;
+  u32 xflags_ = 0, xres_orf_ = 0;
+  std::vector<std::string> xblocks_;
+  std::vector<std::pair<u32, std::string>> ximports_;   // the finished job's records
+  bool b_wait_[2] = {false, false};                     // phase B of parity p waits for the job
+  bool b_due_[2] = {false, false};                      // ... and was launched (runs after it)
   std::unique_ptr<cmqx::ShmXchg> shm_;
   std::vector<int> members_;
   std::vector<std::pair<u32, std::string>> imports_;

@@ -4819,6 +4819,25 @@ __global__ void k_cold_in(DS d, const ColdRec* recs, u32 n, const u64* scan_end)
   if (i < d.q_max && scan_end[i] != 0) d.q_cold_lim[i] = scan_end[i];   // (0: not scanned)
 }
 
+// ============================================================================ asynchronous exchange
+// Phase B of a sharded step waits here (one wave, ahead of its graph) until the exchange
+// thread finished the exchange it imports: the thread writes the received counts, then the
+// job's sequence number into host-mapped flag[0].  Bounded: after ~20 s the wave gives up
+// and sets flag[1] (the exchange thread always releases its job, so only a lost thread
+// would get there; the host reports it), so a stuck host can never wedge the queue.
+__global__ __launch_bounds__(64) void k_xwait(const u32* flag, u32 seq, u32* gave_up) {
+  const u64 t0 = __builtin_amdgcn_s_memrealtime();   // 100 MHz
+  while (true) {
+    const u32 v = __hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+    if ((int)(v - seq) >= 0) return;
+    if (__builtin_amdgcn_s_memrealtime() - t0 > 2000000000ull) {
+      if (threadIdx.x == 0) __hip_atomic_store(gave_up, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      return;
+    }
+    __builtin_amdgcn_s_sleep(32);
+  }
+}
+
 // the cold thread's copy of a pick / scan: the listed records into host-mapped memory
 __global__ void k_side_out(const ColdRec* recs, const u32* cnt, u32 max_n, u32* out, u32* out_cnt) {
   u32 n = *cnt;

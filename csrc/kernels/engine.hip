@@ -647,6 +647,7 @@ class Engine {
   }
 
   ~Engine() {
+    x_stop();
     // a gated copy never outlives its gate: open every gate, so no SDMA queue waits forever
     // (a step that faulted before its last kernel), then let the copies finish
     if (copy_mode_ == 3)
@@ -1552,11 +1553,12 @@ class Engine {
   // RCCL round trip with two PCIe copies; the bulk records stay on RCCL over xGMI.  All
   // ranks of one node (the bench, the sharded server on one host) can use it.
   void xchg_setup(const std::string& kind, const std::string& arg, std::vector<int> members, int timeout_ms,
-                  bool failover, const std::string& counts_shm) {
+                  bool failover, const std::string& counts_shm, bool async) {
     if (!native_x_) throw std::runtime_error("xchg_setup: engine built without native_xchg");
     for (int& m : members)
       if (m < 0 || m >= (int)d_.world) throw std::runtime_error("xchg_setup: bad member");
     std::sort(members.begin(), members.end());
+    x_stop();   // (a job of the old group finished or failed: its phase B was released)
     rccl_.reset();
     shm_.reset();
     cshm_.reset();
@@ -1579,6 +1581,15 @@ class Engine {
     xseq_ = 0;
     x_wait_ = false;
     lag_recv_.clear();
+    async_x_ = async;
+    if (async_x_) {
+      if (!xflag_h_) {
+        xflag_d_ = (u32*)alloc("xflag", 64, true);
+        xflag_h_ = (u32*)buf("xflag").ptr;
+      }
+      __atomic_store_n(&xflag_h_[0], xjob_seq_, __ATOMIC_RELEASE);
+      xth_ = std::thread([this] { x_loop(); });
+    }
   }
 
   static py::bytes xchg_unique_id() { return py::bytes(cmqx::rccl_unique_id()); }
@@ -1586,11 +1597,119 @@ class Engine {
   // the exchange of the launched step of parity q.  0: done (launch_b imports it);
   // -2: a peer did not answer within the timeout (nothing imported, retry impossible:
   // the caller drops it and fails over).  or_flags: OR of every member's flags.
+  //
+  // Asynchronous (xchg_setup async=true): the step's exchange is handed
+  // to the exchange thread and the call returns the PREVIOUS exchange's result (rc, flags
+  // OR) -- one step later, the same on every rank, so lockstep decisions stay identical --
+  // after waiting for that job, which normally finished while the last step ran.  launch_b
+  // queues phase B behind a device-side wait for its job (k_xwait), so the stepper submits
+  // step t+1 while step t's counts and bulk transfer are in flight.  -2 from a finished job:
+  // this step is not exchanged (the caller drops it); a failed job releases its phase B
+  // with nothing to import.
   int exchange(int q, u32 flags, u32* or_flags) {
-    Range rg("chanamq.X1.exchange");
-    HostTimer ht(&ht_[6]);
     if (!native_x_ || (!rccl_ && !shm_)) throw std::runtime_error("exchange: no native exchange set up");
     if (!counts_ready_[q]) throw std::runtime_error("exchange: no phase-A step of this parity");
+    if (!async_x_) {
+      const int rc = exchange_now(q, flags, or_flags, -1);
+      if (rc == 0) counts_ready_[q] = false;
+      return rc;
+    }
+    HostTimer ht(&ht_[6]);
+    int rc = 0;
+    u32 orf = 0;
+    x_collect(&rc, &orf);
+    *or_flags = orf;
+    if (rc) return rc;
+    counts_ready_[q] = false;
+    std::lock_guard<std::mutex> g(xmu_);
+    xq_ = q;
+    xflags_ = flags;
+    xseq_job_ = ++xjob_seq_;
+    if (xseq_job_ == 0) xseq_job_ = ++xjob_seq_;   // (0: no wait)
+    b_wait_[q ^ 1] = xseq_job_;
+    xjob_ = true;
+    xcv_.notify_all();
+    return 0;
+  }
+
+  // the last job's result (waits for it); (0, 0) when none is uncollected
+  void x_collect(int* rc, u32* orf) {
+    std::unique_lock<std::mutex> g(xmu_);
+    xcv_.wait(g, [&] { return !xjob_ && !xbusy_; });
+    *rc = 0;
+    *orf = 0;
+    if (xflag_h_ && __atomic_load_n(&xflag_h_[1], __ATOMIC_ACQUIRE))
+      throw std::runtime_error("a phase B gave up waiting for its exchange (exchange thread lost)");
+    if (xres_) {
+      *rc = xres_rc_;
+      *orf = xres_orf_;
+      xres_ = false;
+      if (xres_rc_ == -1) throw std::runtime_error("exchange thread: " + xerr_);
+    }
+  }
+
+  void x_loop() {
+    HIPCHECK(hipSetDevice(device_));
+    std::unique_lock<std::mutex> g(xmu_);
+    while (true) {
+      xcv_.wait(g, [&] { return xstop_ || xjob_; });
+      if (!xjob_) return;
+      const int q = xq_;
+      const u32 fl = xflags_, seq = xseq_job_;
+      xjob_ = false;
+      xbusy_ = true;
+      g.unlock();
+      u32 orf = 0;
+      int rc;
+      std::string err;
+      try {
+        rc = exchange_now(q, fl, &orf, q ^ 1);
+      } catch (const std::exception& e) {
+        rc = -1;
+        err = e.what();
+      }
+      if (rc) x_recv_counts(q ^ 1, nullptr);   // phase B imports nothing
+      __atomic_store_n(&xflag_h_[0], seq, __ATOMIC_RELEASE);
+      g.lock();
+      xbusy_ = false;
+      xres_ = true;
+      xres_rc_ = rc;
+      xres_orf_ = orf;
+      xerr_ = err;
+      xcv_.notify_all();
+    }
+  }
+
+  void x_stop() {
+    {
+      std::lock_guard<std::mutex> g(xmu_);
+      xstop_ = true;
+      xcv_.notify_all();
+    }
+    if (xth_.joinable()) xth_.join();
+    std::lock_guard<std::mutex> g(xmu_);
+    xstop_ = xjob_ = xbusy_ = xres_ = false;
+    b_wait_[0] = b_wait_[1] = 0;
+  }
+
+  // what phase B of parity p imports: per rank [records, bytes, publish records, publish
+  // bytes, link acks]; v null: nothing
+  void x_recv_counts(int p, const u32* v) {
+    u32* x = (u32*)buf("xchg" + std::to_string(p)).ptr;
+    for (u32 r = 0; r < d_.world; ++r) {
+      x[XC_RECV_N + r] = v ? v[r] : 0;
+      x[XC_RECV_B + r] = v ? v[d_.world + r] : 0;
+      x[XC_RECV_AN + r] = v ? v[2 * d_.world + r] : 0;
+      x[XC_RECV_AB + r] = v ? v[3 * d_.world + r] : 0;
+      x[XC_RACK_N + r] = v ? v[4 * d_.world + r] : 0;
+    }
+  }
+
+  // dst >= 0 (exchange thread): the received counts go straight into parity dst's xchg
+  // words and the RCCL bulk transfer is waited for here, not by phase B's stream
+  int exchange_now(int q, u32 flags, u32* or_flags, int dst) {
+    Range rg("chanamq.X1.exchange");
+    HostTimer ht(&ht_[dst >= 0 ? 8 : 6]);   // (async: the exchange thread's time)
     HIPCHECK(hipEventSynchronize(ev_a_[q]));
     const u32* x = (const u32*)buf("xchg" + std::to_string(q)).ptr;
     if (x[XC_OVF]) throw std::runtime_error("cross-rank send buffers overflowed (xfer_desc_max / xfer_bytes)");
@@ -1697,8 +1816,8 @@ class Engine {
         rc = rccl_->bulk(snd, rcv);
       }
       if (rc) return rc;
-      x_wait_ = true;
-      if (xfailover_) {   // bounded: a peer lost mid-transfer must not wedge the compute stream
+      x_wait_ = dst < 0;
+      if (xfailover_ || dst >= 0) {   // bounded: a peer lost mid-transfer must not wedge the compute stream
         rc = rccl_->wait(rccl_->event());
         if (rc) return rc;
       }
@@ -1757,31 +1876,40 @@ class Engine {
       lag_recv_[3 * d_.world + r] = h[1];
       lag_recv_[4 * d_.world + r] = h[4];
     }
-    counts_ready_[q] = false;
+    if (dst >= 0) {
+      x_recv_counts(dst, lag_recv_.data());
+      lag_recv_.clear();
+    }
     ++xseq_;
     return 0;
   }
 
   // the launched step of parity q will not be exchanged (it packed nothing, or a peer
   // failed): the next phase B imports nothing
-  void drop_exchange(int q) {
+  // Asynchronous: also waits for the job in flight; -2 when it failed (its phase B imported
+  // nothing), which the caller handles like a failed exchange.
+  int drop_exchange(int q) {
     counts_ready_[q] = false;
     lag_recv_.clear();
     x_wait_ = false;
+    if (!async_x_) return 0;
+    int rc = 0;
+    u32 orf = 0;
+    x_collect(&rc, &orf);
+    return rc;
   }
 
   // phase B of the launched step of parity p, importing the last exchange (if any)
   void launch_b(int p) {
     if (!b_due_[p]) throw std::runtime_error("launch_b: no phase-A step of this parity");
     b_due_[p] = false;
-    u32* x = (u32*)buf("xchg" + std::to_string(p)).ptr;
-    const bool have = lag_recv_.size() == 5 * d_.world;
-    for (u32 r = 0; r < d_.world; ++r) {
-      x[XC_RECV_N + r] = have ? lag_recv_[r] : 0;
-      x[XC_RECV_B + r] = have ? lag_recv_[d_.world + r] : 0;
-      x[XC_RECV_AN + r] = have ? lag_recv_[2 * d_.world + r] : 0;
-      x[XC_RECV_AB + r] = have ? lag_recv_[3 * d_.world + r] : 0;
-      x[XC_RACK_N + r] = have ? lag_recv_[4 * d_.world + r] : 0;
+    if (async_x_) {   // behind its exchange job (the exchange thread writes the counts)
+      const u32 w = b_wait_[p];
+      b_wait_[p] = 0;
+      if (w) hipLaunchKernelGGL(k_xwait, dim3(1), dim3(64), 0, s_comp_, (const u32*)xflag_d_, w, xflag_d_ + 1);
+      else x_recv_counts(p, nullptr);
+    } else {
+      x_recv_counts(p, lag_recv_.size() == 5 * d_.world ? lag_recv_.data() : nullptr);
     }
     lag_recv_.clear();
     if (x_wait_ && rccl_) HIPCHECK(hipStreamWaitEvent(s_comp_, rccl_->event(), 0));
@@ -1845,7 +1973,10 @@ class Engine {
       return g < 0 ? -1 : rc;
     };
     a.drop_exchange = [](void* e, int q) -> int {
-      return ((Engine*)e)->guard([&] { ((Engine*)e)->drop_exchange(q); return 0; });
+      Engine* E = (Engine*)e;
+      int rc = 0;
+      int g = E->guard([&] { rc = E->drop_exchange(q); return 0; });
+      return g < 0 ? -1 : rc;
     };
     a.launch_b = [](void* e, int p) -> int {
       return ((Engine*)e)->guard([&] { ((Engine*)e)->launch_b(p); return 0; });
@@ -2140,10 +2271,12 @@ class Engine {
 
   // seconds spent in each host phase since the last reset
   py::dict host_times(bool reset) {
-    static const char* names[8] = {"submit", "submit_sdma_wait", "submit_graph_launch", "wait_results",
-                                   "egress_copy", "egress_wait", "exchange", "exchange_counts"};
+    // (asynchronous exchange: "exchange" is the stepper's wait for the previous job,
+    // "exchange_thread" and "exchange_counts" the exchange thread's time)
+    static const char* names[9] = {"submit", "submit_sdma_wait", "submit_graph_launch", "wait_results",
+                                   "egress_copy", "egress_wait", "exchange", "exchange_counts", "exchange_thread"};
     py::dict o;
-    for (int i = 0; i < 8; ++i) { o[names[i]] = ht_[i]; if (reset) ht_[i] = 0; }
+    for (int i = 0; i < 9; ++i) { o[names[i]] = ht_[i]; if (reset) ht_[i] = 0; }
     return o;
   }
 
@@ -2427,6 +2560,18 @@ class Engine {
   bool xfailover_ = false;
   bool x_wait_ = false;              // phase B waits on the RCCL bulk transfer
   u64 xseq_ = 0;
+  // asynchronous exchange (xchg_setup async=true): one job at a time on the exchange thread
+  bool async_x_ = false;
+  std::thread xth_;
+  std::mutex xmu_;
+  std::condition_variable xcv_;
+  bool xstop_ = false, xjob_ = false, xbusy_ = false, xres_ = false;
+  int xq_ = 0, xres_rc_ = 0;
+  u32 xflags_ = 0, xres_orf_ = 0, xjob_seq_ = 0, xseq_job_ = 0;
+  std::string xerr_;
+  u32 b_wait_[2] = {0, 0};           // launch_b(p): the job phase B of parity p waits for (0: none)
+  u32* xflag_h_ = nullptr;           // host-mapped [0] last finished job, [1] a device wait gave up
+  u32* xflag_d_ = nullptr;
   u8* xs_desc_[2] = {nullptr, nullptr};
   u8* xs_pay_[2] = {nullptr, nullptr};
   u8* xr_desc_[2] = {nullptr, nullptr};
@@ -2530,7 +2675,7 @@ class Engine {
   u64 eg_stats_[4] = {0, 0, 0, 0};
   u32 copy_wgs_ = 16;
   int sdma_pref_ = -1;
-  double ht_[8] = {0, 0, 0, 0, 0, 0, 0, 0};   // host_times() phases
+  double ht_[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};   // host_times() phases
   StepIn* stage_in_[2] = {nullptr, nullptr};
   SegIn* stage_segs_[2] = {nullptr, nullptr};
   hipStream_t s_comp_ = nullptr, s_h2d_ = nullptr, s_d2h_ = nullptr;
@@ -2625,6 +2770,7 @@ PYBIND11_MODULE(_dataplane, m) {
       .def("c_api", &Engine::c_api)
       .def("xchg_setup", &Engine::xchg_setup, py::arg("kind"), py::arg("arg"), py::arg("members"),
            py::arg("timeout_ms") = 10000, py::arg("failover") = false, py::arg("counts_shm") = "",
+           py::arg("async_x") = false,
            py::call_guard<py::gil_scoped_release>())
       .def_static("xchg_unique_id", &Engine::xchg_unique_id)
       .def("exchange", [](Engine& e, int q, u32 flags) {

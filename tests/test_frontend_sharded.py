@@ -34,15 +34,14 @@ def _read_until(s, token, timeout=10.0):
     return buf
 
 
-@pytest.fixture
-def ranks(tmp_path):
+def _start(tmp_path, world, mode):
     name = "cmq-test-" + uuid.uuid4().hex[:12]
     procs, ports = [], []
-    for r in range(2):
+    for r in range(world):
         out = str(tmp_path / f"rank{r}.port")
-        procs.append(subprocess.Popen([sys.executable, os.path.join(HERE, "frontend_sharded_worker.py"), str(r), "2",
-                                       name, out], stdout=subprocess.PIPE, stderr=subprocess.STDOUT))
-    for r in range(2):
+        procs.append(subprocess.Popen([sys.executable, os.path.join(HERE, "frontend_sharded_worker.py"), str(r),
+                                       str(world), name, out, mode], stdout=subprocess.PIPE, stderr=subprocess.STDOUT))
+    for r in range(world):
         out = tmp_path / f"rank{r}.port"
         end = time.time() + 60
         while not out.exists():
@@ -50,14 +49,24 @@ def ranks(tmp_path):
             assert time.time() < end
             time.sleep(0.05)
         ports.append(int(out.read_text()))
-    yield procs, ports, tmp_path
-    for r in range(2):
+    return procs, ports
+
+
+def _stop(tmp_path, procs):
+    for r in range(len(procs)):
         (tmp_path / f"rank{r}.port.stop").write_text("")
     for p in procs:
         try:
             p.wait(20)
         except subprocess.TimeoutExpired:
             p.kill()
+
+
+@pytest.fixture(params=["sync", "async"])
+def ranks(tmp_path, request):
+    procs, ports = _start(tmp_path, 2, request.param)
+    yield procs, ports, tmp_path
+    _stop(tmp_path, procs)
 
 
 def _conn(port):
@@ -106,3 +115,45 @@ def test_lockstep_exchange_sync_and_failover(ranks):
     assert procs[0].poll() is None
     c0.close()
     c1.close()
+
+
+@pytest.mark.timeout(180)
+def test_eight_ranks_async_exchange_sync_and_three_killed(tmp_path):
+    """Eight ranks on the asynchronous exchange (each step's exchange on the engine's
+    exchange thread, phase B behind it, results one step later): records cross a ring of
+    ranks, a control sync parks all eight at the same step, then ranks 2, 5 and 7 die --
+    every survivor's exchange fails, it fails over and keeps serving."""
+    world = 8
+    procs, ports = _start(tmp_path, world, "async")
+    try:
+        cs = [_conn(p) for p in ports]
+        time.sleep(0.3)
+        for r in range(world):   # r -> r+1
+            cs[r].sendall(b"r%dXR%dfrom%d." % (r, (r + 1) % world, r))
+        for r in range(world):
+            _read_until(cs[(r + 1) % world], b"from%d." % r)
+        cs[3].sendall(b"CTRL")
+        got = [_read_until(c, b";", timeout=15) for c in cs]
+        steps = [re.findall(rb"SYNC(\d+);", g)[0] for g in got]
+        assert len(set(steps)) == 1, steps
+        for r in (2, 5, 7):
+            procs[r].kill()
+            procs[r].wait(10)
+        live = [r for r in range(world) if r not in (2, 5, 7)]
+        for r in live:
+            cs[r].sendall(b"ping")
+        for r in live:
+            _read_until(cs[r], b"FAILOVER", timeout=30)
+            cs[r].sendall(b"alone%d" % r)
+            _read_until(cs[r], b"alone%d" % r)
+            assert procs[r].poll() is None
+        for c in cs:
+            c.close()
+    finally:
+        _stop(tmp_path, procs)
+    per_step = []
+    for r in live:
+        xs, xn, _, xf = (tmp_path / f"rank{r}.port.stats").read_text().split()
+        per_step.append(1e6 * float(xs) / max(1, int(xn)))
+        assert int(xf) >= 1
+    print("stepper exchange us/step per surviving rank:", [round(v, 1) for v in per_step])
