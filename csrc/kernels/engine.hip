@@ -669,6 +669,8 @@ class Engine {
     }
     for (int e = 0; e < EGRESS_SLOTS; ++e) (void)hipEventDestroy(ev_d2h_[e]);
     if (ev_side_) (void)hipEventDestroy(ev_side_);
+    if (s_x_) (void)hipStreamDestroy(s_x_);
+    if (s_io_) (void)hipStreamDestroy(s_io_);
     (void)hipStreamDestroy(s_comp_);
     (void)hipStreamDestroy(s_h2d_);
     (void)hipStreamDestroy(s_d2h_);
@@ -730,7 +732,16 @@ class Engine {
     const Buf& b = buf(name);
     if (offset + n > b.bytes) throw std::runtime_error("upload overflows " + name);
     if (b.host) memcpy((u8*)b.ptr + offset, info.ptr, n);
-    else HIPCHECK(hipMemcpy((u8*)b.ptr + offset, info.ptr, n, hipMemcpyHostToDevice));
+    else io_copy((u8*)b.ptr + offset, info.ptr, n, hipMemcpyHostToDevice);
+  }
+
+  // table reads / writes from any host thread: on their own non-blocking stream (a
+  // legacy-stream copy would conflict with a graph capture running on the stepper thread)
+  void io_copy(void* dst, const void* src, size_t n, hipMemcpyKind k) {
+    std::lock_guard<std::mutex> g(io_mu_);
+    if (!s_io_) HIPCHECK(hipStreamCreateWithFlags(&s_io_, hipStreamNonBlocking));
+    HIPCHECK(hipMemcpyAsync(dst, src, n, k, s_io_));
+    HIPCHECK(hipStreamSynchronize(s_io_));
   }
 
   py::bytes download(const std::string& name, size_t offset, size_t n) {
@@ -739,7 +750,7 @@ class Engine {
     if (offset + n > b.bytes) throw std::runtime_error("download overflows " + name);
     std::string out(n, '\0');
     if (b.host) memcpy(&out[0], (u8*)b.ptr + offset, n);
-    else HIPCHECK(hipMemcpy(&out[0], (u8*)b.ptr + offset, n, hipMemcpyDeviceToHost));
+    else io_copy(&out[0], (u8*)b.ptr + offset, n, hipMemcpyDeviceToHost);
     return py::bytes(out);
   }
 
@@ -1559,6 +1570,7 @@ class Engine {
       if (m < 0 || m >= (int)d_.world) throw std::runtime_error("xchg_setup: bad member");
     std::sort(members.begin(), members.end());
     x_stop();   // (a job of the old group finished or failed: its phase B was released)
+    if (!s_x_) HIPCHECK(hipStreamCreateWithFlags(&s_x_, hipStreamNonBlocking));
     rccl_.reset();
     shm_.reset();
     cshm_.reset();
@@ -1663,6 +1675,7 @@ class Engine {
       int rc;
       std::string err;
       try {
+        std::lock_guard<std::mutex> cg(cap_mu_);
         rc = exchange_now(q, fl, &orf, q ^ 1);
       } catch (const std::exception& e) {
         rc = -1;
@@ -1836,17 +1849,18 @@ class Engine {
         const u64 ld = 64ull * lnn[r], lb = lnb[r], kb = 16ull * lnk[r];
         if (off + nd + ld + nb + 16 + lb + kb > shm_->box_bytes())
           throw std::runtime_error("exchange: shm mailbox too small");
-        if (nd) HIPCHECK(hipMemcpy(box + off, S_d + 64 * sbn[r], nd, hipMemcpyDeviceToHost));
+        if (nd) HIPCHECK(hipMemcpyAsync(box + off, S_d + 64 * sbn[r], nd, hipMemcpyDeviceToHost, s_x_));
         off += nd;
-        if (ld) HIPCHECK(hipMemcpy(box + off, L_d + 64 * lbn[r], ld, hipMemcpyDeviceToHost));
+        if (ld) HIPCHECK(hipMemcpyAsync(box + off, L_d + 64 * lbn[r], ld, hipMemcpyDeviceToHost, s_x_));
         off += ld;
-        if (nb) HIPCHECK(hipMemcpy(box + off, S_p + sbb[r], nb, hipMemcpyDeviceToHost));
+        if (nb) HIPCHECK(hipMemcpyAsync(box + off, S_p + sbb[r], nb, hipMemcpyDeviceToHost, s_x_));
         off += (nb + 15) & ~15ull;
-        if (lb) HIPCHECK(hipMemcpy(box + off, L_p + lbb[r], lb, hipMemcpyDeviceToHost));
+        if (lb) HIPCHECK(hipMemcpyAsync(box + off, L_p + lbb[r], lb, hipMemcpyDeviceToHost, s_x_));
         off += (lb + 15) & ~15ull;
-        if (kb) HIPCHECK(hipMemcpy(box + off, K_s + 16ull * d_.lk_cap * r, kb, hipMemcpyDeviceToHost));
+        if (kb) HIPCHECK(hipMemcpyAsync(box + off, K_s + 16ull * d_.lk_cap * r, kb, hipMemcpyDeviceToHost, s_x_));
         off += kb;
       }
+      HIPCHECK(hipStreamSynchronize(s_x_));
       rc = shm_->barrier();
       if (rc) return rc;
       for (int i = 0; i < n; ++i) {
@@ -1854,14 +1868,15 @@ class Engine {
         const u32* h = &hr[(size_t)i * cmqx::XH_WORDS];
         const u8* src = shm_->box(i) + shm_->dir(i)[me];
         const u64 nd = 64ull * h[0], nb = h[1], ld = 64ull * h[2], lb = h[3], kb = 16ull * h[4];
-        if (nd + ld) HIPCHECK(hipMemcpy(R_d + 64 * rbn[i], src, nd + ld, hipMemcpyHostToDevice));
+        if (nd + ld) HIPCHECK(hipMemcpyAsync(R_d + 64 * rbn[i], src, nd + ld, hipMemcpyHostToDevice, s_x_));
         src += nd + ld;
-        if (nb) HIPCHECK(hipMemcpy(R_p + rbb[i], src, nb, hipMemcpyHostToDevice));
+        if (nb) HIPCHECK(hipMemcpyAsync(R_p + rbb[i], src, nb, hipMemcpyHostToDevice, s_x_));
         src += (nb + 15) & ~15ull;
-        if (lb) HIPCHECK(hipMemcpy(R_p + rbb[i] + nb, src, lb, hipMemcpyHostToDevice));
+        if (lb) HIPCHECK(hipMemcpyAsync(R_p + rbb[i] + nb, src, lb, hipMemcpyHostToDevice, s_x_));
         src += (lb + 15) & ~15ull;
-        if (kb) HIPCHECK(hipMemcpy(RK + 16 * rbk[i], src, kb, hipMemcpyHostToDevice));
+        if (kb) HIPCHECK(hipMemcpyAsync(RK + 16 * rbk[i], src, kb, hipMemcpyHostToDevice, s_x_));
       }
+      HIPCHECK(hipStreamSynchronize(s_x_));
     }
     // what launch_b writes into the importing step's xchg: per rank [records, bytes,
     // publish records, publish bytes]
@@ -2490,6 +2505,7 @@ class Engine {
   }
   void capture_on(hipStream_t st, hipGraphExec_t* ge, const std::function<void()>& f) {
     hipGraph_t g;
+    std::lock_guard<std::mutex> cg(cap_mu_);   // (no exchange-thread HIP call inside a capture)
     HIPCHECK(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
     f();
     HIPCHECK(hipStreamEndCapture(st, &g));
@@ -2506,6 +2522,7 @@ class Engine {
 
   void capture_main(int p) {
     hipGraph_t g;
+    std::lock_guard<std::mutex> cg(cap_mu_);   // (no exchange-thread HIP call inside a capture)
     HIPCHECK(hipStreamBeginCapture(s_comp_, hipStreamCaptureModeThreadLocal));
     launch_main(s_comp_, io_[p]);
     HIPCHECK(hipStreamEndCapture(s_comp_, &g));
@@ -2515,6 +2532,7 @@ class Engine {
 
   void capture_b(int p) {
     hipGraph_t g;
+    std::lock_guard<std::mutex> cg(cap_mu_);   // (no exchange-thread HIP call inside a capture)
     HIPCHECK(hipStreamBeginCapture(s_comp_, hipStreamCaptureModeThreadLocal));
     launch_phase_b(s_comp_, io_[p]);
     HIPCHECK(hipStreamEndCapture(s_comp_, &g));
@@ -2571,6 +2589,10 @@ class Engine {
   std::string xerr_;
   u32 b_wait_[2] = {0, 0};           // launch_b(p): the job phase B of parity p waits for (0: none)
   u32* xflag_h_ = nullptr;           // host-mapped [0] last finished job, [1] a device wait gave up
+  std::mutex cap_mu_;                // graph captures vs the exchange thread's HIP calls
+  hipStream_t s_x_ = nullptr;        // the shared-memory exchange's copies
+  std::mutex io_mu_;
+  hipStream_t s_io_ = nullptr;       // upload / download
   u32* xflag_d_ = nullptr;
   u8* xs_desc_[2] = {nullptr, nullptr};
   u8* xs_pay_[2] = {nullptr, nullptr};

@@ -22,6 +22,8 @@
 #               per counter group (PMC_GROUPS overrides), each under its own time limit
 #   xchg        the single-rank RCCL exchange test, then the 2- and 4-rank native / torch
 #               exchange rehearsal on this one GPU (gloo launcher => shared-memory backend)
+#   xchg8       the 8-rank shared-memory rehearsal on this one GPU (asynchronous and synchronous
+#               exchange; the stepper's exchange wait per step is host_us_per_step.exchange)
 #   e2e         bench/gpu_server_e2e.py, every spec, paced at 50 % (E2E_ARGS appended; IOT io
 #               threads, LG load-generator threads, TAG output-name suffix)
 #   e2e_c2      config 2 only over TCP, paced at 50 % (E2E_ARGS appended)
@@ -127,6 +129,14 @@ for T in "$@"; do
         ok $? "xchg ${n}r $x"; line $f
       done
     done ;;
+  xchg8)   # the 8-rank shared-memory rehearsal on this one GPU, asynchronous exchange then synchronous
+    for ax in 1 0; do
+      f=$O/bench_8r_shm_async$ax.json
+      CHANAMQ_BENCH_BACKEND=gloo timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 \
+        --master-addr 127.0.0.1 --master-port $((29610 + ax)) bench.py --gpus 8 --steps 30 --warmup 5 --soak-s 0 \
+        --xchg native --async-x $ax > $f 2> ${f%.json}.err
+      ok $? "xchg8 async $ax"; line $f
+    done ;;
   e2e)
     timeout -k 10 900 python -u bench/gpu_server_e2e.py --seconds 4 --io-threads ${IOT:-8} --paced 0.5 \
       --loadgen-threads ${LG:-12} --out $O/e2e_all_specs${TAG:-}.json $E2E_ARGS > $O/e2e${TAG:-}.log 2>&1
@@ -143,7 +153,7 @@ for T in "$@"; do
     timeout -k 10 300 python -u bench/cold_paging.py --out $O/cold_paging.json $COLD_ARGS > $O/cold_paging.log 2>&1
     rc=$?; tail -3 $O/cold_paging.log | cut -c1-600; ok $rc cold ;;
   sharded)
-    timeout -k 10 700 $PYT tests/test_gpu_sharded_server.py tests/test_gpu_sharded.py -m gpu -x -v > $O/pytest_sharded.log 2>&1
+    timeout -k 10 700 $PYT tests/test_gpu_sharded.py tests/test_gpu_sharded_server.py -m gpu -x -v > $O/pytest_sharded.log 2>&1
     rc=$?; tail -4 $O/pytest_sharded.log; ok $rc sharded ;;
   tests:*)
     timeout -k 10 900 $PYT tests -m gpu -x -v -k "${T#tests:}" > $O/pytest_k.log 2>&1

@@ -11,16 +11,23 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "slow: long-running test")
 
 
+_GPU_WHY = []
+
+
 def gpu_available():
     try:
         from chanamq_amd import ops
-        return ops.load().device_count() > 0
-    except Exception:
+        n = ops.load().device_count()
+        if n <= 0:
+            _GPU_WHY.append(f"device_count() = {n}")
+        return n > 0
+    except Exception as e:   # (reported by the fixture)
+        _GPU_WHY.append(repr(e))
         return False
 
 
 @pytest.fixture(scope="session")
 def gpu():
     if not gpu_available():
-        pytest.fail("GPU test requested but no GPU / data-plane extension available")
+        pytest.fail("GPU test requested but no GPU / data-plane extension available: " + "; ".join(_GPU_WHY))
     return True
