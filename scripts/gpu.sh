@@ -131,10 +131,10 @@ for T in "$@"; do
     done ;;
   xchg8)   # the 8-rank shared-memory rehearsal on this one GPU, asynchronous exchange then synchronous
     for ax in 1 0; do
-      f=$O/bench_8r_shm_async$ax.json
+      f=$O/bench_8r_shm_async$ax${TAG:-}.json
       CHANAMQ_BENCH_BACKEND=gloo timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 \
         --master-addr 127.0.0.1 --master-port $((29610 + ax)) bench.py --gpus 8 --steps 30 --warmup 5 --soak-s 0 \
-        --xchg native --async-x $ax > $f 2> ${f%.json}.err
+        --xchg native --async-x $ax $XCHG8_ARGS > $f 2> ${f%.json}.err
       ok $? "xchg8 async $ax"; line $f
     done ;;
   e2e)
