@@ -31,6 +31,7 @@
 #   cold        bench/cold_paging.py: a backlog through all three body tiers, drained under live
 #               traffic (COLD_ARGS appended)
 #   sharded     the sharded-server GPU tests
+#   sharded_e2e config 2 on the 2-rank sharded server over TCP, local vs remote consumers
 #   tests:PAT   pytest -m gpu -x -k PAT
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 O=gpurun_out/${RUN:-gpu}
@@ -152,6 +153,10 @@ for T in "$@"; do
   cold)   # timed cold paging: backlog through HBM log -> host ring -> disk, drained under live traffic
     timeout -k 10 300 python -u bench/cold_paging.py --out $O/cold_paging.json $COLD_ARGS > $O/cold_paging.log 2>&1
     rc=$?; tail -3 $O/cold_paging.log | cut -c1-600; ok $rc cold ;;
+  sharded_e2e)   # config 2 on the 2-rank sharded server, consumers on the owner rank vs remote
+    timeout -k 10 600 python -u bench/gpu_server_e2e.py --sharded 2 --only config2 --seconds 4 --io-threads 2 \
+      --out $O/sharded2_config2_local_remote${TAG:-}.json $E2E_ARGS > $O/sharded_e2e${TAG:-}.log 2>&1
+    rc=$?; tail -6 $O/sharded_e2e${TAG:-}.log | cut -c1-400; ok $rc sharded_e2e ;;
   sharded)
     timeout -k 10 700 $PYT tests/test_gpu_sharded.py tests/test_gpu_sharded_server.py -m gpu -x -v > $O/pytest_sharded.log 2>&1
     rc=$?; tail -4 $O/pytest_sharded.log; ok $rc sharded ;;
