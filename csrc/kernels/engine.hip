@@ -1901,13 +1901,15 @@ class Engine {
 
   // the launched step of parity q will not be exchanged (it packed nothing, or a peer
   // failed): the next phase B imports nothing
-  // Asynchronous: also waits for the job in flight; -2 when it failed (its phase B imported
-  // nothing), which the caller handles like a failed exchange.
-  int drop_exchange(int q) {
+  // Asynchronous, collect (the stepper): also waits for the job in flight; -2 when it
+  // failed (its phase B imported nothing), which the caller handles like a failed exchange.
+  // A host-run step of the control plane (collect false) leaves the stepper's uncollected
+  // result alone: it carries the flags every rank acts on at the same step.
+  int drop_exchange(int q, bool collect = true) {
     counts_ready_[q] = false;
     lag_recv_.clear();
     x_wait_ = false;
-    if (!async_x_) return 0;
+    if (!async_x_ || !collect) return 0;
     int rc = 0;
     u32 orf = 0;
     x_collect(&rc, &orf);
@@ -2804,7 +2806,7 @@ PYBIND11_MODULE(_dataplane, m) {
              }
              return py::make_tuple(rc, orf);
            }, py::arg("parity"), py::arg("flags") = 0)
-      .def("drop_exchange", &Engine::drop_exchange)
+      .def("drop_exchange", &Engine::drop_exchange, py::arg("q"), py::arg("collect") = false)
       .def("launch_b", &Engine::launch_b)
       .def("counters", &Engine::counters)
       .def("host_times", &Engine::host_times, py::arg("reset") = false)
