@@ -3836,11 +3836,9 @@ __global__ __launch_bounds__(1024) void k_runs(DS d) {
 }
 
 DEV void wave_consumed(const DS& d, u32 msg, u32 q, u64 qpos, u32 kind, bool valid);
-DEV void conn_layout_body(const DS& d, u32* lds);
 // thread per delivery: expand its run (binary search), assign the channel's next delivery
-// tag, fill the unacked window slot, size the rendered frames.  layout: the last block to
-// finish then lays out the connections' egress (k_conn_layout, one launch less per step)
-__global__ __launch_bounds__(1024) void k_dv_write(DS d, u32 layout) {
+// tag, fill the unacked window slot, size the rendered frames
+__global__ void k_dv_write(DS d) {
   const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
   const u32 n = d.ctr->n_deliv;
   const bool valid = i < n;
@@ -3904,19 +3902,6 @@ __global__ __launch_bounds__(1024) void k_dv_write(DS d, u32 layout) {
   if (d.persist)   // manual-ack delivery of a persistent message: its row becomes an unack
     wave_consumed(d, dv.msg, dv.q, dv.qpos, 3u, valid && !(dv.flags & 2));
   wave_add_u32(d.ctr->lat_hist, lat < LAT_BINS ? lat : LAT_BINS - 1, 1u, valid);
-  if (!layout) return;
-  __shared__ u32 s_last;
-  __shared__ u32 lds[1024 / 64 + 1];
-  // every block's sizes reach the device-wide coherence point before its ticket (agent
-  // scope: the last block may run on another XCD)
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-  __syncthreads();
-  if (threadIdx.x == 0) s_last = atomicAdd(&d.tot[TS_DV_TICKET], 1u) == gridDim.x - 1;
-  __syncthreads();
-  if (!s_last) return;
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  if (threadIdx.x == 0) d.tot[TS_DV_TICKET] = 0;
-  conn_layout_body(d, lds);
 }
 
 // per connection: egress size = returns + confirms + deliveries
@@ -3938,10 +3923,10 @@ __global__ void k_conn_sizes(DS d) {
   d.conn_total[c] = d.conn_ret_bytes[c] + conf + dl + 13u * d.conn_gempty[c];
 }
 
-// single block of 1024 threads (c_max <= CONN_LAYOUT_MAX): k_conn_sizes + scan of
-// conn_total + k_conn_out -- run by k_dv_write's last block (fused k_conn_layout)
+// single block (c_max <= CONN_LAYOUT_MAX): k_conn_sizes + scan of conn_total + k_conn_out
 #define CONN_LAYOUT_MAX 8192
-DEV void conn_layout_body(const DS& d, u32* lds) {
+__global__ __launch_bounds__(1024) void k_conn_layout(DS d) {
+  __shared__ u32 lds[1024 / 64 + 1];
   // exclusive scan of the deliveries' rendered sizes (fused k_scan: one block walks the
   // step's deliveries 16K at a time -- 16 per thread, all loads of a pass in flight at
   // once, one block scan per pass: a step's deliveries usually take one pass)

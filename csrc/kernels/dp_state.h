@@ -53,8 +53,7 @@ enum : u32 {
   TS_NCADEF = 68,                       // channels k_chan_advance deferred (store-record budget)
   TS_NDGET = 69,                        // Basic.Get commands the frame scan decoded (DGet list)
   TS_SPILL_USED = 70,                   // bytes of StepIn.spill_budget reserved this step (k_dequeue)
-  TS_DQ_TICKET = 71,                    // k_dequeue finished-block ticket (last block: the step's runs)
-  TS_DV_TICKET = 72                     // k_dv_write finished-block ticket (last block: k_conn_layout)
+  TS_DQ_TICKET = 71                     // k_dequeue finished-block ticket (last block: the step's runs)
 };
 
 // Basic.Get decoded from a connection's bytes by the frame scan (no host round trip): served

@@ -2466,10 +2466,10 @@ class Engine {
     // k_dequeue first puts requeued deliveries back in front of their queues' heads, in
     // queue-offset order (QueueEntity.scala:415-446), then dispatches
     hipLaunchKernelGGL(k_dequeue, dim3(d.q_max), dim3(256), 0, s, d);   // (its last block: k_runs)
-    if (d.c_max <= CONN_LAYOUT_MAX) {   // (its last block: k_conn_layout + the delivery-size scan)
-      hipLaunchKernelGGL(k_dv_write, blocks(d.deliv_max, 1024), dim3(1024), 0, s, d, 1u);
+    hipLaunchKernelGGL(k_dv_write, blocks(d.deliv_max, 256), dim3(256), 0, s, d);
+    if (d.c_max <= CONN_LAYOUT_MAX) {
+      hipLaunchKernelGGL(k_conn_layout, dim3(1), dim3(1024), 0, s, d);   // + the delivery-size scan
     } else {
-      hipLaunchKernelGGL(k_dv_write, blocks(d.deliv_max, 1024), dim3(1024), 0, s, d, 0u);
       launch_scan(s, d, {{d.dv_size, d.dv_off}}, &d.ctr->n_deliv, d.deliv_max, 6);
       hipLaunchKernelGGL(k_conn_sizes, blocks(d.c_max, 256), dim3(256), 0, s, d);
       launch_scan(s, d, {{d.conn_total, d.conn_base}}, nullptr, d.c_max, 7);
