@@ -213,9 +213,9 @@ def main():
                          "CHANAMQ_BENCH_BACKEND=gloo: the shared-memory backend) -- or torch.distributed "
                          "all_to_all_single (parallel/exchange.py)")
     ap.add_argument("--xchg-timeout-ms", type=int, default=30000)
-    ap.add_argument("--async-x", type=int, default=1,
-                    help="native exchange on the engine's exchange thread, phase B waiting on the device (0: "
-                         "the stepper runs each exchange itself)")
+    ap.add_argument("--async-x", type=int, default=0,
+                    help="1: native exchange on the engine's exchange thread, phase B waiting on the device "
+                         "(default 0: the stepper runs each exchange itself; profiles/r5_summary.md)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))

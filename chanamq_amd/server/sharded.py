@@ -66,8 +66,8 @@ def main(argv=None):
     ap.add_argument("--no-fsync", action="store_true")
     ap.add_argument("--backend", default="", help="default: nccl (RCCL) for --plane gpu, gloo for golden; "
                                                   "gloo + gpu rehearses several ranks on one GPU")
-    ap.add_argument("--async-x", type=int, default=1,
-                    help="each step's exchange on the engine's exchange thread (phase B waits on the device)")
+    ap.add_argument("--async-x", type=int, default=0,
+                    help="1: each step's exchange on the engine's exchange thread (phase B waits on the device)")
     ap.add_argument("--xchg-timeout-ms", type=int, default=15000,
                     help="pipeline: a peer silent this long in an exchange is failed over")
     ap.add_argument("--hb-timeout-s", type=float, default=3.0)
