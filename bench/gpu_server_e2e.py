@@ -334,7 +334,8 @@ def run_sharded(core, name, spec, world, mode, seconds, rate=0.0, io_threads=2, 
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     env = dict(os.environ, PYTHONPATH=root)
     ln = Launcher(world, ["-m", "chanamq_amd.server.sharded", "--config", SMALL_CONF, "--plane", "gpu", "--port", "0", "--backend", "gloo",
-                          "--info-dir", tmp, "--io-threads", str(io_threads), "--idle-step-ms", "0.5"],
+                          "--info-dir", tmp, "--io-threads", str(io_threads), "--idle-step-ms", "0.5"]
+                  + os.environ.get("CHANAMQ_SHARDED_ARGS", "").split(),
                   env=env).start()
     try:
         deadline = time.time() + 180
