@@ -647,7 +647,7 @@ class Engine {
   }
 
   ~Engine() {
-    x_stop();
+    x_stop(true);
     // a gated copy never outlives its gate: open every gate, so no SDMA queue waits forever
     // (a step that faulted before its last kernel), then let the copies finish
     if (copy_mode_ == 3)
@@ -1693,11 +1693,16 @@ class Engine {
     }
   }
 
-  void x_stop() {
+  // shutdown (abort true): a job still waiting for a peer gives up at once
+  void x_stop(bool abort = false) {
     {
       std::lock_guard<std::mutex> g(xmu_);
       xstop_ = true;
       xcv_.notify_all();
+      if (abort && (xjob_ || xbusy_)) {
+        if (shm_) shm_->abort();
+        if (cshm_) cshm_->abort();
+      }
     }
     if (xth_.joinable()) xth_.join();
     std::lock_guard<std::mutex> g(xmu_);

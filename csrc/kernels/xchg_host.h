@@ -138,8 +138,9 @@ class ShmXchg {
       timespec ts{0, 20000};
       nanosleep(&ts, nullptr);
       if ((spin & 63) == 0 &&
-          std::chrono::duration_cast<std::chrono::milliseconds>(std::chrono::steady_clock::now() - t0).count() >
-              timeout_ms_)
+          (abort_.load(std::memory_order_relaxed) ||
+           std::chrono::duration_cast<std::chrono::milliseconds>(std::chrono::steady_clock::now() - t0).count() >
+               timeout_ms_))
         return withdraw(b);
     }
   }
@@ -173,6 +174,9 @@ class ShmXchg {
     }
   }
 
+  // a waiting barrier gives up now (as after its timeout): the owner is shutting down
+  void abort() { abort_.store(true, std::memory_order_relaxed); }
+
   // count exchange: send[dest member][XH_WORDS] -> recv[src member][XH_WORDS]
   int counts(const uint32_t* send, uint32_t* recv) {
     const int k = (int)(seq_++ & 1);
@@ -193,6 +197,7 @@ class ShmXchg {
   std::string name_;
   std::vector<int> members_;
   int me_ = 0, idx_ = 0, timeout_ms_ = 10000;
+  std::atomic<bool> abort_{false};
   size_t box_ = 0, hdr_ = 0, per_ = 0, total_ = 0;
   int fd_ = -1;
   uint8_t* base_ = nullptr;
