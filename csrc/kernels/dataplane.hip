@@ -426,10 +426,14 @@ __global__ __launch_bounds__(1024) void k_stage(DS d) {
     }
   }
   u32 total = 0;
+  u32 cl0 = 0, len0 = 0;   // this thread's first segment (the usual step has <= 1024): the
+                           // layout pass below reuses it instead of a second PCIe read
   for (u32 k = tid; k < nseg; k += 1024) {
     const SegIn sg = d.segs_h[k];
     ((SegIn*)d.segs)[k] = sg;
-    total += align16(d.carry_len[sg.conn] + sg.len + 32);
+    const u32 cl = d.carry_len[sg.conn];
+    if (k == tid) { cl0 = cl; len0 = sg.len; }
+    total += align16(cl + sg.len + 32);
   }
   u32 all_t;
   block_scan<1024>(total, lds, all_t);
@@ -440,9 +444,14 @@ __global__ __launch_bounds__(1024) void k_stage(DS d) {
     const u32 k = b0 + tid;
     u32 cl = 0, len = 0, v = 0;
     if (k < nseg) {
-      const SegIn sg = d.segs_h[k];   // (the device copy of this block's own stores: not re-read)
-      cl = d.carry_len[sg.conn];
-      len = sg.len;
+      if (b0 == 0) {
+        cl = cl0;
+        len = len0;
+      } else {
+        const SegIn sg = d.segs_h[k];
+        cl = d.carry_len[sg.conn];
+        len = sg.len;
+      }
       v = align16(cl + len + 32);
     }
     u32 all;
@@ -3432,7 +3441,9 @@ DEV void spill_queue(const DS& d, u32 q, u64 lim, u32 hot, u32 budget, u64* move
   }
 }
 
-DEV void dequeue_queue(const DS& d) {
+// true: the block wrote runs with plain stores (the fused k_runs' ticket needs an
+// agent-scope release); false: at most q_nruns[q] = 0, stored agent-coherent
+DEV bool dequeue_queue(const DS& d) {
   __shared__ u32 g_cons[RUNS_PER_Q];
   __shared__ u32 g_n[RUNS_PER_Q];
   __shared__ u64 s_head;
@@ -3466,11 +3477,11 @@ DEV void dequeue_queue(const DS& d) {
       __syncthreads();
     }
   }
-  if (q >= d.q_max) return;
+  if (q >= d.q_max) return false;
   const u32 ndg = d.tot[TS_NDGET] < DGET_MAX ? d.tot[TS_NDGET] : DGET_MAX;   // Basic.Gets decoded this step
   if (!d.q_active[q]) {
     if (tid == 0) {
-      d.q_nruns[q] = 0;
+      __hip_atomic_store(&d.q_nruns[q], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       // a Basic.Get staged for a queue deleted since: answered GONE (never left RETRY, which
       // the host would resubmit forever -- or serve from whatever queue reuses the slot)
       const u32 ng = d.in->nget < GET_STEP_MAX ? d.in->nget : GET_STEP_MAX;
@@ -3479,7 +3490,7 @@ DEV void dequeue_queue(const DS& d) {
       for (u32 k = 0; k < ndg; ++k)
         if (d.dget[k].q == q) dget_to_host(d, k);
     }
-    return;
+    return false;
   }
   const bool nodisp = (d.in->flags & SF_NODISPATCH) != 0;
   if (d.in->spill_frac && d.spill_bytes) {   // (kernel-uniform) the step's share of body tiering
@@ -3489,11 +3500,11 @@ DEV void dequeue_queue(const DS& d) {
   }
   if (nodisp && d.links && d.q_link_owner[q]) {   // a live link shadow: its acks could not travel
     if (tid == 0) {
-      d.q_nruns[q] = 0;
+      __hip_atomic_store(&d.q_nruns[q], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       for (u32 k = 0; k < ndg; ++k)
         if (d.dget[k].q == q) dget_to_host(d, k);
     }
-    return;
+    return false;
   }
   // agent-scope load: the requeue above (this block's thread 0) may have moved the head
   // after this wave read the line
@@ -3611,7 +3622,7 @@ DEV void dequeue_queue(const DS& d) {
   const u64 avail = dlim > head ? dlim - head : 0;
   if (mall == 0 || avail == 0 || nodisp) {
     if (tid == 0) { d.q_head[q] = head; d.q_nruns[q] = ngr; }
-    return;
+    return true;
   }
   const u32 m = mall > RUNS_PER_Q - ngr ? RUNS_PER_Q - ngr : mall;
   const u32 r = d.q_rr[q] % mall;
@@ -3731,6 +3742,7 @@ DEV void dequeue_queue(const DS& d) {
     d.q_head[q] = qp;
     d.q_rr[q] = (r + 1) % mall;
   }
+  return true;
 }
 
 // K8 dequeue, one block per queue; the last block to finish (ticket) then lays out the
@@ -3741,10 +3753,13 @@ __global__ __launch_bounds__(256) void k_dequeue(DS d) {
   __shared__ u64 key_lds[DQ_RUN_LDS];
   __shared__ u32 lds[256 / 64 + 1];
   __shared__ u32 s_last;
-  dequeue_queue(d);
+  const bool wrote = dequeue_queue(d);
   // every block's runs and counts reach the device-wide coherence point before its ticket
-  // (agent scope: the last block may run on another XCD, whose L2 does not see this one's)
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  // (agent scope: the last block may run on another XCD, whose L2 does not see this one's);
+  // a block that wrote no runs stored its zero count agent-coherent and skips the L2
+  // write-back that release costs
+  if (wrote) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  else __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
   __syncthreads();
   if (threadIdx.x == 0) s_last = atomicAdd(&d.tot[TS_DQ_TICKET], 1u) == gridDim.x - 1;
   __syncthreads();
