@@ -82,3 +82,47 @@ def test_deleted_tables_ddl_export_and_round_trip(tmp_path):
     st3 = open_store(str(tmp_path / "b"), fsync=False)   # replayed from its WAL
     assert summary(st3)["queues_deleted"] == 5 and summary(st3)["queue_metas_deleted"] == 1
     st3.close()
+
+
+def test_live_push_and_pull_over_the_native_protocol(tmp_path):
+    """store -> (CQL native protocol v4: STARTUP + PasswordAuthenticator, DDL, batched
+    prepared INSERTs) -> a CQL server -> SELECT back into a fresh store: every row of every
+    table survives.  The server is tests/cql_fake_server.py (no Cassandra here; it decodes
+    the values with its own codec from the reference schema), so parity with a real
+    cluster stays unpinned."""
+    import os
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from cql_fake_server import FakeCql
+
+    from chanamq_amd.store.cql_native import CqlClient, CqlError, pull, push
+    srv = FakeCql(user="cassandra", password="secret")
+    try:
+        try:
+            CqlClient(port=srv.port, user="cassandra", password="wrong")
+            raise AssertionError("bad credentials accepted")
+        except CqlError:
+            pass
+        st = open_store(str(tmp_path / "a"), fsync=False)
+        _fill(st)
+        st.pending_delete_queue("AMQ.DEFAULT-_.q")
+        st.insert_queue_meta("AMQ.DEFAULT-_.q2", 3, set(), False, 0)
+        st.sync()
+        before = rows(st)
+        with CqlClient(port=srv.port, user="cassandra", password="secret") as cl:
+            n = push(st, cl, keyspace="cmq", batch=4)
+        st.close()
+        assert n["msgs"] == 5 and n["queues_deleted"] == 5 and n["queue_metas"] == 1
+        assert any(s.startswith("CREATE KEYSPACE IF NOT EXISTS cmq") for s in srv.statements)
+        assert len(srv.tables[("cmq", "msgs")]) == 5
+        st2 = open_store(str(tmp_path / "b"), fsync=False)
+        with CqlClient(port=srv.port, user="cassandra", password="secret") as cl:
+            got = pull(cl, st2, keyspace="cmq")
+        assert got == n
+        after = rows(st2)
+        for t in before:
+            key = lambda r: sorted((k, repr(sorted(v) if isinstance(v, (set, frozenset)) else v)) for k, v in r.items())
+            assert sorted(map(key, before[t])) == sorted(map(key, after[t])), t
+        st2.close()
+    finally:
+        srv.close()
