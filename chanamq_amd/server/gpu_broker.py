@@ -2031,6 +2031,8 @@ class GpuBroker:
         last_gc = 0.0
         while self._running:
             time.sleep(0.01)
+            if not self._cold_pending and not self.stats.get("spilled_bytes", 0):
+                continue   # nothing ever left HBM: no side operation (each costs a step launch)
             try:
                 if self._cold_pending:
                     got = p.cold_in_side(self.cold, self._side, self.cold_window)
