@@ -9,7 +9,8 @@ paged back from disk during the drain, the live stream's publish->deliver latenc
 native load generator's.
 
 Both tiers ride the steps (k_dequeue's in-step spill, the cold thread's engine side
-operations), so the stepper pause count must not move during the run.  Bodies of a
+operations), so the stepper pause count must not move during the run.  Before the drain a
+``--hold-s`` phase runs the same live stream next to the resting backlog.  Bodies of a
 sample of the drained messages are checked against the load generator's fill pattern.
 Reference: MessageEntity.scala:82-102,174-186 (bodies leave memory, come back on demand).
 
@@ -42,6 +43,7 @@ def main():
     ap.add_argument("--live-rate", type=float, default=10000.0, help="live msgs/s (1 KB, 1P1C)")
     ap.add_argument("--io-threads", type=int, default=4)
     ap.add_argument("--cold-sync", action="store_true", help="cold tier between paused steps (the old path)")
+    ap.add_argument("--hold-s", type=float, default=6.0, help="live stream next to the resting backlog first")
     ap.add_argument("--out", default="")
     args = ap.parse_args()
 
@@ -85,6 +87,15 @@ def main():
                               cold_out_bytes=st1.get("cold_out_bytes", 0), spilled_bytes=st1.get("spilled_bytes", 0),
                               on_disk=b.cold.bytes_on_disk(), nacked=int(r1.get("nacked", 0)), error=r1["error"])
         print("backlog", json.dumps(out["backlog"]), flush=True)
+        # ---- the live stream next to the resting backlog (tiers full, nothing drained)
+        if args.hold_s > 0:
+            st_h = dict(b.stats)
+            h = core.run_load(dict(port=b.port, seconds=args.hold_s, warmup=1.0, queue="cold.hold", exchange="",
+                                   producers=1, consumers=1, msg_size=1024, rate=args.live_rate, threads=2,
+                                   prefetch=1000))
+            out["hold"] = {k: h.get(k) for k in ("sent", "received", "elapsed", "p50_us", "p95_us", "p99_us", "error")}
+            out["hold"]["pauses"] = b.stats.get("pauses", 0) - st_h.get("pauses", 0)
+            print("hold", json.dumps(out["hold"]), flush=True)
         # ---- phase 2: drain under live traffic
         got = [0] * args.drainers
         bad = [0]
