@@ -266,13 +266,13 @@ static bool read_until(int fd, const std::string& token) {
   return true;
 }
 
-static void frontend_sharded() {
-  const std::string name = "cmq-sanitize-" + std::to_string(::getpid());
+static void frontend_sharded(bool async_x) {
+  const std::string name = "cmq-sanitize-" + std::to_string(::getpid()) + (async_x ? "-a" : "-s");
   std::unique_ptr<EchoEngine> eng[2];
   for (u32 r = 0; r < 2; ++r) eng[r] = std::make_unique<EchoEngine>(64, 64, 1 << 20, 1 << 16, 2, r);
   {
-    std::thread t0([&] { eng[0]->xchg_setup(name, {0, 1}, 2000); });
-    std::thread t1([&] { eng[1]->xchg_setup(name, {0, 1}, 2000); });
+    std::thread t0([&] { eng[0]->xchg_setup(name, {0, 1}, 2000, async_x); });
+    std::thread t1([&] { eng[1]->xchg_setup(name, {0, 1}, 2000, async_x); });
     t0.join();
     t1.join();
   }
@@ -317,8 +317,9 @@ static void frontend_sharded() {
     t0.join();
     t1.join();
   }
-  fprintf(stderr, "sharded front end: %llu steps, %llu exchanges, imported %llu\n", (unsigned long long)s0.steps,
-          (unsigned long long)s0.xchg_steps, (unsigned long long)eng[1]->imported);
+  fprintf(stderr, "sharded front end (%s exchange): %llu steps, %llu exchanges, imported %llu\n",
+          async_x ? "asynchronous" : "synchronous", (unsigned long long)s0.steps, (unsigned long long)s0.xchg_steps,
+          (unsigned long long)eng[1]->imported);
 }
 
 int main(int argc, char** argv) {
@@ -329,7 +330,8 @@ int main(int argc, char** argv) {
   codec_fuzz();
   broker_and_loadgen(dir + "/broker");
   frontend_echo();
-  frontend_sharded();
+  frontend_sharded(false);
+  frontend_sharded(true);
   fprintf(stderr, "host sanitizer run: ok\n");
   return 0;
 }
