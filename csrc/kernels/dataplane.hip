@@ -4720,21 +4720,34 @@ __global__ __launch_bounds__(256) void k_cold_pick(DS d, u32 hot, u64 lim_rel, u
   const u64 head = d.q_head[q], tail = d.q_tail[q], mask = d.q_ring_mask[q];
   const Desc* ring = d.ring + d.q_ring_off[q];
   const u64 skip = d.q_cons_n[q] ? hot : 0;
-  for (u64 b = head + skip + (u64)w * 64; b < tail; b += 256) {
+  // resume past the queue's cold prefix (cursor): a deep cold backlog is not walked again
+  // at every call (it was: up to ~370 us between two steps, profiles/r5_coldprof/)
+  __shared__ unsigned long long s_open;
+  if (threadIdx.x == 0) s_open = ~0ull;
+  __syncthreads();
+  const u64 start0 = head + skip;
+  u64 cur = d.q_cold_cur[q];
+  if (cur < start0 || cur > tail) cur = start0;   // (the head passed it, or the slot was reset)
+  u64 open = ~0ull;   // this wave's first entry that is not cold (or where it stopped)
+  for (u64 b = cur + (u64)w * 64; b < tail; b += 256) {
     const u64 i = b + lane;
-    bool want = false;
+    bool want = false, cold = false;
     u32 msg = INVALID, sz = 0;
     u64 lo = 0;
     if (i < tail) {
       msg = ring[i & mask].msg;
-      if (msg != INVALID && msg < d.msg_max) {
+      cold = msg == INVALID || msg >= d.msg_max;
+      if (!cold) {
         const MsgEnt& m = d.msgs[msg];
         lo = m.log_off;
         sz = m.slot_bytes;
+        cold = (lo & COLD_BIT) != 0;
         want = (lo & SPILL_BIT) && !(lo & COLD_BIT) && (lo & ~SPILL_BIT) < lim && m.refcnt == 1 &&
                !(m.flags & MF_PERSIST);
       }
     }
+    const u64 nc = __ballot(i < tail && !cold);
+    if (nc && open == ~0ull) open = b + (u64)(__ffsll((unsigned long long)nc) - 1);
     const u32 k = wave_reserve(n_out, want);
     bool ok = want && k < max_n;
     if (ok) ok = atomicAdd(bytes, (unsigned long long)sz) + sz <= max_bytes;
@@ -4744,8 +4757,14 @@ __global__ __launch_bounds__(256) void k_cold_pick(DS d, u32 hot, u64 lim_rel, u
       r.bytes = ok ? sz : 0; r.pad = 0;
       out[k] = r;
     }
-    if (__ballot(want && !ok)) break;   // the batch is full
+    if (__ballot(want && !ok)) {   // the batch is full
+      if (b < open) open = b;
+      break;
+    }
   }
+  if (lane == 0 && open != ~0ull) atomicMin(&s_open, (unsigned long long)open);
+  __syncthreads();
+  if (threadIdx.x == 0) d.q_cold_cur[q] = s_open == ~0ull ? tail : (u64)s_open;
 }
 
 __global__ void k_cold_commit(DS d, const ColdRec* recs, u32 n) {

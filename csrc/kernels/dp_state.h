@@ -245,6 +245,7 @@ struct DS {
   i64* cold_live;           // [COLD_SEGS] live bytes per cold-store segment (host unlinks freed ones)
   u64* q_cold_lim;          // [q_max] deliveries stop here (~0: nothing of the queue is cold)
   u64* q_spill_cur;         // [q_max] spill_queue resumes here: entries before it are tiered
+  u64* q_cold_cur;          // [q_max] k_cold_pick resumes here: entries before it are cold
   u64* id_next;             // snowflake virtual sequence position
 
   // ---------------- deliveries

@@ -458,6 +458,7 @@ class Engine {
     d_.q_cold_lim = (u64*)dev("q_cold_lim", 8ull * d_.q_max);
     HIPCHECK(hipMemset(d_.q_cold_lim, 0xff, 8ull * d_.q_max));
     d_.q_spill_cur = (u64*)dev("q_spill_cur", 8ull * d_.q_max);
+    d_.q_cold_cur = (u64*)dev("q_cold_cur", 8ull * d_.q_max);
 
     d_.deliv = (Deliv*)dev("deliv", sizeof(Deliv) * (u64)d_.deliv_max);
     {
