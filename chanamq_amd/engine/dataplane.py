@@ -242,7 +242,8 @@ class GpuDataPlane(ControlState):
                           ("d_kb_len", d_kb_len), ("d_q_off", d_q_off), ("d_q_n", d_q_n),
                           ("t_queue", t_queue), ("t_exch", t_exch), ("t_kb_off", t_kb_off),
                           ("t_kb_len", t_kb_len), ("t_flags", t_flags), ("t_expect", t_expect),
-                          ("t_mat", t_mat), ("t_woff", t_woff)):
+                          ("t_mat", t_mat), ("t_woff", t_woff),
+                          ("t_count", np.array([len(tb), 0, 0, 0], np.uint32))):
             self._up(name, arr)
         if fan_q:
             self._up("fan_q", np.array(fan_q, np.uint32))

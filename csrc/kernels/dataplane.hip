@@ -2120,12 +2120,16 @@ DEV void topic_tile(const DS& d, u32 i0, u32 j0, u32 jt, u32 ntb, u32 npub, u32 
 // pub_match (global: k_route_store re-reads them for publishes with > 8 queues) and made
 // visible to the block's waves before they route.
 DEV void topic_group(const DS& d, u32 g0, u32 n, u32 w, u32 lane) {
-  const u32 ntb = d.tb_max ? d.tb_pad >> 4 : 0u;
-  if (ntb == 0) return;
+  // the prefilter tiles of the bindings in use only (the tables are packed from row 0): a
+  // step of a few publishes on a 4096-row table cost ~68 us here (profiles/r5_coldprof/)
+  const u32 nused = d.t_count[0] < d.tb_pad ? d.t_count[0] : d.tb_pad;
+  const u32 ntb = d.tb_max ? d.tb_pad >> 4 : 0u;   // (pub_match row stride: every tile)
+  const u32 nt = d.tb_max ? (nused + 15) >> 4 : 0u;
+  if (nt == 0) return;
   const u32 pi = g0 + lane;
   const bool need = lane < 16 && pi < n && !(d.pubs[pi].flags & (MF_ONEQ | MF_RESTORE));
   if (!__ballot(need)) return;
-  for (u32 jt = w; jt < ntb; jt += 16) topic_tile(d, g0, jt * 16, jt, ntb, n, lane);
+  for (u32 jt = w; jt < nt; jt += 16) topic_tile(d, g0, jt * 16, jt, ntb, n, lane);
 }
 
 

@@ -179,6 +179,7 @@ struct DS {
   u32* d_q;                 // direct queue lists
   u8* kpool;                // key/pattern bytes
   u32* t_queue; u32* t_exch; u32* t_kb_off; u32* t_kb_len; u32* t_flags; i32* t_expect;
+  u32* t_count;             // [4] topic bindings in use ([0]; rows 0..n-1 of the tables above)
   i8* t_mat;                // [tb_pad][TOPIC_K]
   u16* t_woff;              // [tb_pad][TOPIC_WORDS] pattern words: offset << 8 | length
 

@@ -373,6 +373,11 @@ class Engine {
     d_.t_kb_off = (u32*)dev("t_kb_off", 4ull * d_.tb_pad);
     d_.t_kb_len = (u32*)dev("t_kb_len", 4ull * d_.tb_pad);
     d_.t_flags = (u32*)dev("t_flags", 4ull * d_.tb_pad);
+    d_.t_count = (u32*)dev("t_count", 16);
+    {   // (until the first topology upload: every row, as before the count existed)
+      const u32 all[4] = {d_.tb_pad, 0, 0, 0};
+      HIPCHECK(hipMemcpy(d_.t_count, all, 16, hipMemcpyHostToDevice));
+    }
     d_.t_expect = (i32*)dev("t_expect", 4ull * d_.tb_pad);
     d_.t_mat = (i8*)dev("t_mat", (u64)d_.tb_pad * TOPIC_K + 64);
     d_.t_woff = (u16*)dev("t_woff", 2ull * TOPIC_WORDS * d_.tb_pad + 64);
