@@ -123,10 +123,10 @@ for T in "$@"; do
     rc=$?; tail -3 $O/pytest_rccl.log; ok $rc rccl_single
     for n in 2 4; do
       for x in native torch; do
-        f=$O/bench_${n}r_$x.json
+        f=$O/bench_${n}r_$x${TAG:-}.json
         CHANAMQ_BENCH_BACKEND=gloo timeout -k 10 240 python -m torch.distributed.run --nnodes=1 --nproc-per-node $n \
           --master-addr 127.0.0.1 --master-port $((29600 + n)) bench.py --gpus $n --steps 30 --warmup 5 --soak-s 0 \
-          --xchg $x > $f 2> ${f%.json}.err
+          --xchg $x $BENCH_ARGS > $f 2> ${f%.json}.err
         ok $? "xchg ${n}r $x"; line $f
       done
     done ;;
