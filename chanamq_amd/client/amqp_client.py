@@ -55,6 +55,7 @@ class Channel:
         self.published = 0
         self.confirmed_upto = 0   # highest confirmed publish sequence seen (across waits)
         self.confirm_mode = False
+        self.consumer_tags = set()   # tags whose Basic.ConsumeOk arrived (strict ordering check)
 
     # ---------------------------------------------------------------- plumbing
     def _send(self, name, **args):
@@ -231,7 +232,7 @@ class Channel:
 
 class Connection:
     def __init__(self, host="127.0.0.1", port=5672, vhost="/", user="guest", password="guest", heartbeat=0,
-                 frame_max=131072, tls=False, timeout=10.0, capabilities=None):
+                 frame_max=131072, tls=False, timeout=10.0, capabilities=None, strict=False):
         self.sock = socket.create_connection((host, port), timeout=timeout)
         self.sock.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
         if tls:
@@ -249,6 +250,10 @@ class Connection:
         self.server_properties = None
         self.frame_max = frame_max
         self.heartbeats_received = 0
+        # strict: record what a strict client (the Java client's "Unsolicited delivery")
+        # rejects -- a Basic.Deliver for a consumer tag whose ConsumeOk has not arrived yet
+        self.strict = strict
+        self.violations = []
         self._next_ch = 1
         self._wbuf = bytearray()
         self._send_raw(C.PROTOCOL_HEADER)
@@ -328,6 +333,10 @@ class Connection:
         ch = self.channels.get(cmd.channel)
         if ch is None:
             return
+        if m.name == "basic.consume_ok":
+            ch.consumer_tags.add(m.consumer_tag)
+        elif m.name == "basic.deliver" and self.strict and m.consumer_tag not in ch.consumer_tags:
+            self.violations.append(f"unsolicited delivery: tag {m.consumer_tag!r} before its consume_ok")
         if m.name in ("basic.deliver", "basic.get_ok"):
             ch.deliveries.append(Delivery(cmd.channel, m, cmd.props, cmd.body))
         elif m.name == "basic.return":

@@ -354,7 +354,9 @@ class GpuDataPlane(ControlState):
             self._up_at("cons_q", c.queue, cid, np.uint32)
             self._up_at("cons_ch", self.chslot(c.conn, c.ch), cid, np.uint32)
             self._up_at("cons_noack", int(c.no_ack), cid, np.uint32)
-            self._up_at("cons_active", 1, cid, np.uint32)
+            # deferred (light control section, steps running): 2 = active from the step after
+            # the one applying it, so no Basic.Deliver overtakes the ConsumeOk (k_stage)
+            self._up_at("cons_active", 2 if self.defer else 1, cid, np.uint32)
             self._up_at("cons_unacked", 0, cid, np.uint32)
             self._up_at("cons_tag_off", cid * 256, cid, np.uint32)
             self._up_at("cons_tag_len", len(tag), cid, np.uint32)

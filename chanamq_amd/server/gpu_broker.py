@@ -125,11 +125,17 @@ class _LightLock:
     def __init__(self, lock):
         self.l = lock
 
+    def _eng(self):
+        return getattr(self.l.b.plane, "eng", None)
+
     def __enter__(self):
         lk = self.l
         lk.rl.acquire()
         lk.depth += 1
         lk.light += 1
+        eng = self._eng()
+        if eng is not None and hasattr(eng, "stage_begin"):
+            eng.stage_begin()   # one batch per section: no step takes it before __exit__
         if not lk.paused_at:
             lk._defer(True)
             lk.b.stats["light_sections"] = lk.b.stats.get("light_sections", 0) + 1
@@ -138,12 +144,25 @@ class _LightLock:
     def __exit__(self, *exc):
         lk = self.l
         lk.light -= 1
+        eng = self._eng()
+        if eng is not None and hasattr(eng, "stage_end"):
+            eng.stage_end()
         if not lk.light and not lk.paused_at:
             lk._defer(False)
             if lk.b.fe is not None:
                 lk.b.fe.wake()   # the staged writes ride the next step
         lk.depth -= 1
         lk.rl.release()
+
+    def cut(self):
+        """Close the section's staged batch here (it rides the next step) and go on
+        staging into a new one: a change set never outgrows one step's delta buffer."""
+        eng = self._eng()
+        if eng is not None and hasattr(eng, "stage_end"):
+            eng.stage_end()
+            eng.stage_begin()
+            if self.l.b.fe is not None:
+                self.l.b.fe.wake()
 
 
 # control commands that only touch connection / channel / consumer tables: handled while
@@ -439,6 +458,15 @@ class GpuBroker:
                         if light and not self._light_ok(dev):
                             with self.lock:   # a command that needs the device drained
                                 self._handle_fe(dev)
+                        elif light:
+                            # a few commands at a time: once the staged set nears what one
+                            # step applies, the batch is cut there (each command's writes stay
+                            # in one step's batch: ADVICE r5)
+                            for k in range(0, len(dev), 16):
+                                n, nb, _ = self.plane.deltas_pending()
+                                if k and (n > 256 or nb > (1 << 20)):
+                                    self.light.cut()
+                                self._handle_fe(dev[k:k + 16])
                         else:
                             self._handle_fe(dev)
                         if self.node is not None:   # sharded: injected into the lockstep steps

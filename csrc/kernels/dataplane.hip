@@ -402,6 +402,13 @@ __global__ __launch_bounds__(1024) void k_stage(DS d) {
     s_in = *d.in_h;
     *d.in = s_in;
   }
+  // consumers a light control section activated (cons_active 2, applied by an earlier
+  // step's k_stage) take deliveries from this step on: the step that applied them rendered
+  // none, so its egress -- behind which the front end released the Basic.ConsumeOk
+  // (Frontend::send_after) -- never holds a Basic.Deliver that overtakes the ConsumeOk.
+  // Flipped before this step's own writes are applied (theirs wait one more step)
+  for (u32 c = tid; c < d.cons_max; c += 1024)
+    if (d.cons_active[c] == 2u) d.cons_active[c] = 1u;
   __syncthreads();
   if (s_in.delta_bytes) apply_deltas(d, d.delta_h, tid, 1024, lrec);   // control writes first
   const u32 nseg = s_in.nseg;
@@ -3656,7 +3663,9 @@ DEV bool dequeue_queue(const DS& d) {
       u32 ch = d.cons_ch[c];
       // wblock: the front end's socket backlog for this connection is above its high
       // watermark (host-mapped, written by the IO threads): its messages stay queued in HBM
-      if (!d.cons_active[c] || !d.ch_flow[ch] || d.conn_wblock[ch / d.chpc]) continue;
+      // (cons_active 2: staged by a light control section this step -- it takes deliveries
+      // from the next step on, behind its Basic.ConsumeOk)
+      if (d.cons_active[c] != 1u || !d.ch_flow[ch] || d.conn_wblock[ch / d.chpc]) continue;
       u64 share = (remaining + (m - j) - 1) / (m - j);
       u32 want = (u32)(share < d.deliver_cap ? share : d.deliver_cap);
       bool noack = d.cons_noack[c];

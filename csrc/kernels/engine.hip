@@ -947,8 +947,11 @@ class Engine {
   // Any thread.  Writes to the same bytes: the last one wins (records never overlap).
   void stage_write(u64 dst, const u8* data, u64 n) {
     if (!n) return;
+    // one record must fit a step's delta buffer with its header (a larger one
+    // was never packed and kept the stepper spinning on host_work)
+    if (n + 64 > DELTA_CAP) throw std::runtime_error("stage_write: a write larger than one step's delta buffer");
     std::lock_guard<std::mutex> g(dl_mu_);
-    if (dl_.empty()) dl_.emplace_back();
+    if (dl_.empty()) new_batch();
     DlBatch& bt = dl_.back();
     const u64 a = dst, e = dst + n;
     auto it = bt.w.lower_bound(a);
@@ -983,11 +986,29 @@ class Engine {
   void stage_mark_dirty(u32 ch) {
     if (ch >= d_.c_max * d_.chpc) throw std::runtime_error("stage_mark_dirty: bad channel slot");
     std::lock_guard<std::mutex> g(dl_mu_);
-    if (dl_.empty()) dl_.emplace_back();
+    if (dl_.empty()) new_batch();
     auto& dv = dl_.back().dirty;
     for (u32 c : dv)
       if (c == ch) return;
     dv.push_back(ch);
+  }
+  // a light control section's staging: everything staged until stage_end() forms one batch
+  // that no step takes before the section closed it (a step packing in the middle of a
+  // section split a command's consumer rows and q_cons lists over two steps)
+  void stage_begin() {
+    std::lock_guard<std::mutex> g(dl_mu_);
+    ++dl_open_;
+    if (dl_.empty() || !dl_.back().open) new_batch();
+  }
+  void stage_end() {
+    std::lock_guard<std::mutex> g(dl_mu_);
+    if (dl_open_) --dl_open_;
+    if (!dl_open_)
+      for (auto& bt : dl_) bt.open = false;
+  }
+  void new_batch() {   // (dl_mu_ held)
+    dl_.emplace_back();
+    dl_.back().open = dl_open_ > 0;
   }
   // from the next submitted step on, every step moves queued bodies in the oldest frac/65536
   // of the HBM log (past the first `hot` entries of a queue with consumers) to the host
@@ -1008,8 +1029,10 @@ class Engine {
   bool host_work() {
     std::lock_guard<std::mutex> g(dl_mu_);
     if (!unp_ready_.empty() || side_queued()) return true;
-    for (auto& bt : dl_)
+    for (auto& bt : dl_) {
+      if (bt.open) break;   // (staged by a section still running: stage_end wakes the stepper)
       if (!bt.w.empty() || !bt.dirty.empty() || !bt.unp.empty()) return true;
+    }
     return false;
   }
   bool has_deltas() {
@@ -1037,14 +1060,21 @@ class Engine {
       v.erase(v.begin(), v.begin() + k);
     };
     if (unp) take_unp(unp_ready_);
+    // a step (unp set) never takes a batch a light section is still staging into;
+    // flush_deltas (between steps, the control plane holds the engine) takes everything
+    if (unp && !dl_.empty() && dl_.front().open) { if (nunp) *nunp = nu; return 0; }
     while (!dl_.empty() && dl_.front().w.empty() && dl_.front().dirty.empty()) {
+      if (unp && dl_.front().open) break;
       take_unp(dl_.front().unp);   // a batch of unpauses only (no writes)
       if (!dl_.front().unp.empty()) break;
       if (dl_.size() == 1) { dl_.pop_front(); break; }
       dl_.pop_front();
     }
     if (nunp) *nunp = nu;
-    if (dl_.empty() || (dl_.front().w.empty() && dl_.front().dirty.empty())) return 0;
+    if (dl_.empty() || (dl_.front().w.empty() && dl_.front().dirty.empty()) || (unp && dl_.front().open)) {
+      if (nunp) *nunp = nu;
+      return 0;
+    }
     DlBatch& bt = dl_.front();
     u8* o = dl_h_[p];
     const u32 ndirty = (u32)std::min<size_t>(bt.dirty.size(), 4096);
@@ -1102,7 +1132,7 @@ class Engine {
   void stage_unpause(u32 conn) {
     if (conn >= d_.c_max) throw std::runtime_error("stage_unpause: bad connection");
     std::lock_guard<std::mutex> g(dl_mu_);
-    if (dl_.empty()) dl_.emplace_back();
+    if (dl_.empty()) new_batch();
     auto& v = dl_.back().unp;   // with the writes staged before it
     for (u32 c : v)
       if (c == conn) return;
@@ -2633,12 +2663,15 @@ class Engine {
   // deferred control writes: device address -> bytes (non-overlapping), channels to mark
   static constexpr u64 DELTA_CAP = 4ull << 20;
   std::mutex dl_mu_;
-  struct DlBatch { std::map<u64, std::string> w; std::vector<u32> dirty, unp; u64 bytes = 0; };
+  // open: a light control section is still staging into it (stage_begin .. stage_end); a
+  // step never takes an open batch, so one section's change set rides one step whole
+  struct DlBatch { std::map<u64, std::string> w; std::vector<u32> dirty, unp; u64 bytes = 0; bool open = false; };
   std::vector<u32> unp_ready_;   // unpauses of batches flush_deltas applied (next step)
   u32 spill_req_[3] = {0, 0, 0};   // stage_spill for the next submitted step (dl_mu_)
   // staged writes with the unpauses staged after them; a batch that overflows one step's
   // delta buffer keeps its unpauses until its last write is packed
   std::deque<DlBatch> dl_;
+  u32 dl_open_ = 0;   // light sections staging now (stage_begin / stage_end)
   u64 dl_bytes_ = 0;
   u8* dl_h_[2] = {nullptr, nullptr};
   u32 dl_step_[2] = {0, 0};
@@ -2825,6 +2858,8 @@ PYBIND11_MODULE(_dataplane, m) {
       .def("egress_stats", &Engine::egress_stats)
       .def("stage_write", &Engine::stage_write_buf, py::arg("name"), py::arg("data"), py::arg("offset") = 0)
       .def("stage_mark_dirty", &Engine::stage_mark_dirty)
+      .def("stage_begin", &Engine::stage_begin)
+      .def("stage_end", &Engine::stage_end)
       .def("stage_spill", &Engine::stage_spill)
       .def("deltas_pending", &Engine::deltas_pending)
       .def("flush_deltas", &Engine::flush_deltas, py::call_guard<py::gil_scoped_release>());

@@ -870,7 +870,13 @@ def test_control_churn_rides_the_steps_without_a_drain(gpu, monkeypatch):
         rc = conn(b)
         r1 = rc.channel(5)   # (a fixed number: the reopen below reuses its device slot)
         r1.basic_consume("rq", "r", no_ack=False)
-        assert sorted(d.body for d in r1.consume_n(10)) == sorted(f"r{k}".encode() for k in range(10))
+        try:
+            first = r1.consume_n(10, timeout=20)
+        except TimeoutError:
+            print("r1 got", len(r1.deliveries), "stats", b.stats, "fe", b.fe.stats() if b.fe else None)
+            dump_state(b)
+            raise
+        assert sorted(d.body for d in first) == sorted(f"r{k}".encode() for k in range(10))
         r1.close()
         r2 = rc.channel(5)   # same channel number (same device slot): gets them again, redelivered
         r2.basic_consume("rq", "r2", no_ack=False)
@@ -896,6 +902,63 @@ def test_control_churn_rides_the_steps_without_a_drain(gpu, monkeypatch):
         assert light1 - light0 >= 150, (light0, light1)
         assert pauses1 == pauses0, (pauses0, pauses1, b.stats.get("pause_why"))
         for c_ in (s, sink, rc, cc):
+            c_.close()
+    finally:
+        b.stop()
+
+
+@pytest.mark.gpu
+def test_consume_ok_precedes_first_delivery_in_light_sections(gpu):
+    """Basic.Consume on a queue with a backlog while the steps keep running (a light control
+    section): the consumer's rows ride a step, and the Basic.ConsumeOk is released behind
+    that step's egress -- so the device must not dispatch to the new consumer in that same
+    step (cons_active 2 -> 1 at the next step's k_stage), or a strict client (Java:
+    "Unsolicited delivery") sees a Basic.Deliver for a tag it does not know yet."""
+    import threading
+    import time
+    from chanamq_amd.engine.dataplane import GpuDataPlane
+    from chanamq_amd.server.gpu_broker import GpuBroker
+    b = GpuBroker(GpuDataPlane(default_queue_capacity=1 << 12, **GPU_CFG), idle_step_ms=1.0, io="pipeline",
+                  ingress_bytes=8 << 20).start()
+    try:
+        s = conn(b)
+        sch = s.channel()
+        sch.queue_declare("load")
+        names = [f"bq{k}" for k in range(12)]
+        for q in names:
+            sch.queue_declare(q)
+            for i in range(40):
+                sch.basic_publish("", q, f"{q}-{i}".encode())
+        s.process(0.2)
+        sink = conn(b)
+        kch = sink.channel()
+        kch.basic_consume("load", "sink", no_ack=True)
+        stop = threading.Event()
+
+        def pump():   # keeps the stepper busy: every consume below is handled beside the steps
+            pc = conn(b)
+            pch = pc.channel()
+            while not stop.is_set():
+                for _ in range(20):
+                    pch.basic_publish("", "load", b"x" * 256)
+                pc.process(0.002)
+            pc.close()
+        th = threading.Thread(target=pump, daemon=True)
+        th.start()
+        time.sleep(0.2)
+        light0, pauses0 = b.stats.get("light_sections", 0), b.stats.get("pauses", 0)
+        strict = conn(b, strict=True)
+        for k, q in enumerate(names):
+            ch = strict.channel()
+            ch.basic_consume(q, f"t{k}", no_ack=(k % 2 == 0))
+            got = ch.consume_n(40, timeout=20)
+            assert sorted(d.body for d in got) == sorted(f"{q}-{i}".encode() for i in range(40))
+        assert strict.violations == [], strict.violations[:3]
+        assert b.stats.get("light_sections", 0) - light0 >= len(names)
+        assert b.stats.get("pauses", 0) == pauses0, b.stats.get("pause_why")
+        stop.set()
+        th.join(20)
+        for c_ in (s, sink, strict):
             c_.close()
     finally:
         b.stop()
