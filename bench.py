@@ -121,6 +121,34 @@ def build_workload(dp, rank, producers, queues, body, chunk, blocks, cons_base, 
     return pool, segs, offs, block_len, msgs_per_step, len(probe), extra
 
 
+def verify_egress(dp, base, pool_len, tickets):
+    """Egress by reference, checked outside the timed window on finished steps: every
+    gather entry points into the retained ingress pool, and the spliced wire bytes of every
+    connection parse as complete AMQP frames and commands (a missing or misplaced body breaks
+    the frame-end markers).  Returns the number of Basic.Deliver commands checked."""
+    from chanamq_amd.engine.layout import EGRESS_REF
+    from chanamq_amd.protocol.codec import CommandAssembler, FrameParser
+    checked = 0
+    if True:
+        for t in tickets:
+            c = dp.eng.counters(t[0])
+            eg, co = dp.host_egress(t)
+            if c["n_ref"]:
+                raw = dp._egress[t[3]]
+                tab = raw[c["gath_off"]:c["gath_off"] + 16 * c["n_deliv"]].view(EGRESS_REF)
+                r = tab[tab["len"] > 0]
+                assert ((r["src"] >= base) & (r["src"] + r["len"] <= base + pool_len)).all(), "gather outside pool"
+                assert (np.diff(tab["dst"].astype(np.int64)) >= 0).all(), "gather table not monotone"
+            for conn in np.nonzero(co["len"])[0]:
+                o, n = int(co["off"][conn]), int(co["len"][conn])
+                fp, ca = FrameParser(), CommandAssembler()
+                for f in fp.feed(bytes(eg[o:o + n])):
+                    cmd = ca.feed(f)
+                    if cmd is not None and cmd.method.name == "basic.deliver":
+                        checked += 1
+    return checked
+
+
 def setup_native_exchange(args, cfg, GpuDataPlane, dist, backend, local, rank, world):
     """The sharded plane on the engine's native exchange, as the sharded server builds it
     (server/sharded.py): rank 0 draws the RCCL unique id and names the shared-memory
@@ -213,6 +241,12 @@ def main():
                          "CHANAMQ_BENCH_BACKEND=gloo: the shared-memory backend) -- or torch.distributed "
                          "all_to_all_single (parallel/exchange.py)")
     ap.add_argument("--xchg-timeout-ms", type=int, default=30000)
+    ap.add_argument("--egress-ref", type=int, default=1, choices=[0, 1],
+                    help="1 (default): egress by reference -- a delivery whose body arrived in the same step's "
+                         "ingress payload is rendered without it and the host sends the body from that payload "
+                         "(the pinned pool block, unchanged until the block is submitted again 8 steps later), so "
+                         "bodies cross PCIe once; the D2H carries the frames + a gather table.  0: every body "
+                         "rendered into HBM egress and copied D2H")
     ap.add_argument("--async-x", type=int, default=0,
                     help="1: native exchange on the engine's exchange thread, phase B waiting on the device "
                          "(default 0: the stepper runs each exchange itself; profiles/r5_summary.md)")
@@ -262,7 +296,8 @@ def main():
                log_bytes=16 << 30, ring_pool=Q * qcap + qtot + 1024, tb_max=max(64, qtot) if not fan else 64,
                fan_max=max(1 << 20, qtot * 2), carry_cap=256 << 10, graph=0 if args.no_graph else 1,
                copy_engine={"blit": 0, "nocu": 1, "kernel": 2, "sdma": 3}[args.copy_engine], copy_wgs=args.copy_wgs, sdma_engine=args.sdma_engine,
-               sdma_split=args.sdma_split, egress_gate=args.egress_gate, overlap=args.overlap)
+               sdma_split=args.sdma_split, egress_gate=args.egress_gate, overlap=args.overlap,
+               egress_ref=0 if args.egress_ref else -1)
     native = shards > 1 and args.xchg == "native"
     if native:
         dp = setup_native_exchange(args, cfg, GpuDataPlane, dist, backend, local, rank, world)
@@ -289,6 +324,7 @@ def main():
     phases = []          # every timed iteration's phases (ms): submit, prefetch, egress wait, finish
     pre = set()     # steps whose payload H2D is already queued (prefetch)
     lat_w = []      # (publish->deliver seconds, deliveries) of the timed steps
+    wire, nref = [0], [0]
 
     def run(n, measure=False):
         # software pipeline, 3 steps in flight: H2D(t+1) || kernels(t) || D2H(t-1);
@@ -297,6 +333,7 @@ def main():
         dl = pb = 0
         hist = np.zeros(32, np.int64)
         eg = 0
+        wire[0] = 0
         pending = []    # (ticket, step index)
         done = []
         lat_of = {}     # step index -> its lat_hist (deliveries by publish-step lag)
@@ -307,6 +344,10 @@ def main():
             dl += c["n_deliv"]
             pb += c["n_pubs"]
             eg += c["egress_bytes"]
+            # bytes on the wire: the rendered frames + the referenced bodies (not the table)
+            tab = 16 * c["n_deliv"] if c["n_ref"] else 0
+            wire[0] += c["egress_bytes"] - tab + c["ref_bytes"]
+            nref[0] += c["n_ref"]
             lh = np.array(c["lat_hist"], np.int64)
             hist[:] += lh
             lat_of[s] = lh
@@ -467,6 +508,16 @@ def main():
     if dist:
         dist.barrier()
     t = time.perf_counter() - t0
+    n_ref_timed, wire_timed = nref[0], wire[0]
+    verified = None
+    if args.egress_ref:   # two more steps, each finished and checked on its own (every rank)
+        verified = 0
+        for _ in range(2):
+            b = step_i % args.blocks
+            tk = submit(segs[b], base + offs[b], blens[b])
+            step_i += 1
+            dp.finish(tk, collect=False, wait_egress=True)
+            verified += verify_egress(dp, base, sum(blens) + 64, [tk])
     c = dp.eng.counters((step_i - 1) & 1)
     errs = {k: c[k] for k in ("n_dropped_nomem", "n_ring_full", "n_unknown_exchange", "n_unroutable",
                               "n_routed_msgs", "n_pairs", "n_deliv", "n_live_msgs") if c[k]}
@@ -538,6 +589,12 @@ def main():
             "p99_latency_ms": p99_ms,
             "published_msgs_per_s": pb / t,
             "egress_GBps": eg / t / 1e9,
+            "d2h_bytes_per_step": eg / max(1, args.steps * world),
+            "wire_bytes_per_step": wire_timed / max(1, args.steps),
+            "egress_ref": ({"referenced_deliveries": n_ref_timed, "verified": verified,
+                            "note": "bodies of deliveries referenced in the ingress pool block of their own step "
+                                    "(never rewritten; resubmitted 8 steps later); the D2H carries frames + "
+                                    "gather table"} if args.egress_ref else None),
             "latency_note": "measured per delivery on the host clock: submit of the publishing step -> egress "
                             "bytes of the delivering step in host memory (no TCP; bench/gpu_server_e2e.py "
                             "measures client-to-client over TCP)",

@@ -203,7 +203,7 @@ def run_one(core, name, spec, io, io_threads, seconds, rate=0.0, lg_threads=12, 
                         ent = np.dtype([("log_off", "<u8"), ("msg_id", "<u8"), ("ts", "<i8"), ("slot_bytes", "<u4"),
                                         ("body_len", "<u4"), ("body_off", "<u4"), ("props_len", "<u2"), ("ex_len", "u1"),
                                         ("rk_len", "u1"), ("refcnt", "<i4"), ("flags", "<u4"), ("pub_step", "<u4"),
-                                        ("pad", "<u4")])
+                                        ("pad", "<u4"), ("href", "<u8")])
                         m = np.frombuffer(plane.eng.download("msgs"), ent)
                         free_top = plane.info["msg_max"] - after["live_msgs"]
                         fl = set(np.frombuffer(plane.eng.download("msg_free", 0, 4 * free_top), np.uint32).tolist())

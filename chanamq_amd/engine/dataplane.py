@@ -7,6 +7,7 @@ hipGraph and returns per-connection egress bytes plus the control commands the
 device routed back to the host.
 """
 
+import ctypes
 import time
 from collections import defaultdict
 
@@ -15,7 +16,8 @@ import numpy as np
 from .. import ops
 from ..protocol import constants as C
 from .control import ControlError, ControlState
-from .layout import (CONN_OUT, CONSUMED_REC, RING_MOVE, CTRL_REC, CTRL_DGET, CTRL_TXBUF, INVALID, MF_HAS_TS, MF_HOSTPUB, MF_PERSIST,
+from .layout import (CONN_OUT, CONSUMED_REC, EGRESS_REF, RING_MOVE, CTRL_REC, CTRL_DGET, CTRL_TXBUF, INVALID, MF_HAS_TS,
+                     MF_HOSTPUB, MF_PERSIST,
                      MF_ONEQ, MF_REDELIVERED, MF_RESTORE,
                      PERSIST_HDR, RDESC, SEG_IN, SEG_OUT, SS_CTRL, US_ACKED, US_PENDING, US_REQUEUE, USLOT,
                      chan_hash, direct_key, exch_hash, fnv1a64, topic_pattern_row, topic_word_offsets)
@@ -67,9 +69,16 @@ class StepResult:
 
 class GpuDataPlane(ControlState):
     def __init__(self, device=0, hash_wildcard=True, graph=True, worker=0, default_queue_capacity=1 << 16,
-                 world=1, rank=0, shard_map=None, exchanger=None, exchange_lag=0, **cfg):
+                 world=1, rank=0, shard_map=None, exchanger=None, exchange_lag=0, egress_ref=0, **cfg):
+        """``egress_ref``: egress by reference -- a delivery whose body arrived in the
+        ingress payload of the same step (or up to ``egress_ref`` steps earlier) is rendered
+        without the body, which the host takes from that payload (``finish`` / ``host_egress``
+        splice it back in; the native front end sends it with sendmsg iovecs).  The caller
+        keeps each payload unchanged until the delivering step's egress is collected
+        (``step()`` does: a payload buffer is reused two steps later).  None / -1: off."""
         self.mod = ops.load()
         full = dict(cfg)
+        full.setdefault("egress_ref_back", -1 if egress_ref is None else int(egress_ref))
         full.update(device=device, hash_wildcard=int(hash_wildcard), graph=int(graph), world=world, rank=rank,
                     exchange_lag=int(exchange_lag))
         self.eng = self.mod.Engine(full)
@@ -1019,18 +1028,46 @@ class GpuDataPlane(ControlState):
         if wait_egress or collect:
             self.eng.egress_wait_slot(slot)
         if collect and collect_egress:
-            co = io["conn_out"]
-            eg = self._egress[slot]
+            eg, co = self._wire(self._egress[slot], io["conn_out"], c)
             for conn in np.nonzero(co["len"])[0]:
                 o, n = int(co["off"][conn]), int(co["len"][conn])
                 res.egress[int(conn)] = bytes(eg[o:o + n])
         res.elapsed = time.perf_counter() - t0
         return res
 
+    def _wire(self, eg, co, c):
+        """The step's egress as sent on the wire: with referenced bodies (Counters.n_ref)
+        the rendered bytes with every body spliced in from its host ingress payload at its
+        gather entry (EgressRef), and the connections' (offset, length) in that buffer."""
+        if not c["n_ref"]:
+            return eg, co
+        n = min(int(c["n_deliv"]), int(self.info["deliv_max"]))
+        go = int(c["gath_off"])
+        tab = eg[go:go + 16 * n].view(EGRESS_REF)
+        refs = tab[tab["len"] > 0].copy()
+        dst, ln = refs["dst"].astype(np.int64), refs["len"].astype(np.int64)
+        out = np.empty(go + int(ln.sum()), np.uint8)
+        prev = w = 0
+        for d, src, k in zip(dst.tolist(), refs["src"].tolist(), ln.tolist()):
+            out[w:w + d - prev] = eg[prev:d]
+            w += d - prev
+            ctypes.memmove(out.ctypes.data + w, src, k)
+            w += k
+            prev = d
+        out[w:w + go - prev] = eg[prev:go]
+        cum = np.concatenate([[0], np.cumsum(ln)])
+        off, cl = co["off"].astype(np.int64), co["len"].astype(np.int64)
+        s0 = cum[np.searchsorted(dst, off, side="left")]
+        s1 = cum[np.searchsorted(dst, off + cl, side="left")]
+        wco = np.zeros(len(co), CONN_OUT)
+        wco["off"], wco["len"] = off + s0, cl + (s1 - s0)
+        return out, wco
+
     def host_egress(self, ticket):
-        """(egress bytes view, ConnOut view) of a finished step, for zero-copy socket writes."""
+        """(egress bytes, ConnOut) of a finished step as sent on the wire: zero-copy views
+        when no delivery referenced a host body, else a spliced copy (``_wire``)."""
         io = self._io[ticket[0]]
-        return self._egress[ticket[3]], io["conn_out"]
+        return self._wire(self._egress[ticket[3]], io["conn_out"], self.eng.counters(ticket[0]))
 
     def step_done(self, ticket):
         """Non-blocking: the step's kernels have finished (``finish`` will not wait)."""

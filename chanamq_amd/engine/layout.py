@@ -34,7 +34,11 @@ US_FREE, US_PENDING, US_ACKED, US_REQUEUE, US_DONE = 0, 1, 2, 3, 4
 CTRL_TXBUF = 0x80000000     # CtrlRec.seg: data command of a transactional channel (low bits = position)
 CTRL_DGET = 0x40000000      # CtrlRec.seg: a Basic.Get its step decoded but could not serve (not paused)
 
-STRUCT_SIZES = {"SegIn": 16, "SegOut": 32, "CtrlRec": 16, "ConnOut": 8, "StepIn": 96, "RDesc": 64, "USlot": 32}
+# egress by reference: one gather entry per delivery of a step with Counters.n_ref > 0
+# (dp_common.h EgressRef): the len body bytes at host address src go before egress byte dst
+EGRESS_REF = np.dtype([("src", "<u8"), ("dst", "<u4"), ("len", "<u4")])
+
+STRUCT_SIZES = {"SegIn": 16, "SegOut": 32, "CtrlRec": 16, "ConnOut": 8, "StepIn": 112, "RDesc": 64, "USlot": 32}
 assert RDESC.itemsize == 64
 
 # SegOut.status bits

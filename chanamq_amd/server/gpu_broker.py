@@ -107,6 +107,11 @@ class _PlaneLock:
                 self.b.plane.flush_deltas()
             if hasattr(self.b.fe, "flush_ctl"):          # and the replies held behind it written
                 self.b.fe.flush_ctl()
+            if self.light:
+                # replies a light section produced but has not queued yet: written now,
+                # while paused (its staged writes were just applied; once the steps resume,
+                # a consumer it activated gets deliveries, which must follow its ConsumeOk)
+                self.b._flush_all()
         return self
 
     def __exit__(self, *exc):

@@ -12,6 +12,7 @@
 #include <sys/eventfd.h>
 #include <sys/ioctl.h>
 #include <sys/socket.h>
+#include <sys/uio.h>
 #include <unistd.h>
 
 #include <algorithm>
@@ -110,7 +111,13 @@ Frontend::Frontend(const FrontendCfg& cfg, const CmqEngineApi* api) : cfg_(cfg),
   }
   for (u32 i = cfg_.max_slot; i >= 1; --i) free_.push_back(i);
   const u64 arena_bytes = ((api_->ingress_cap + 64 + 4095) / 4096) * 4096;
-  for (int k = 0; k < 3; ++k) {
+  // egress by reference: deliveries of the same step's bodies (back 0) are sent from the
+  // arena they arrived in (NARENA arenas keep it unchanged until that egress is written)
+  if (cfg_.egress_ref && api_->set_egress_ref && api_->set_egress_ref(api_->eng, 0, cfg_.egress_ref_min) == 0)
+    narena_ = NARENA;
+  else if (api_->set_egress_ref)
+    api_->set_egress_ref(api_->eng, -1, 0);
+  for (int k = 0; k < narena_; ++k) {
     arena_[k] = (u8*)aligned_alloc(4096, arena_bytes);
     if (!arena_[k]) throw std::runtime_error("frontend: arena allocation failed");
     // page-locked: the step's H2D is a DMA straight from the arena (a pageable source is
@@ -166,7 +173,7 @@ Frontend::~Frontend() {
     if (io->evfd >= 0) ::close(io->evfd);
   }
   if (lfd_ >= 0) ::close(lfd_);
-  for (auto* a : arena_) free(a);
+  for (auto* a : arena_) free(a);   // (free(nullptr) for unused ones)
 }
 
 void Frontend::start() {
@@ -200,7 +207,7 @@ void Frontend::stop() {
   pc_cv_.notify_all();
   if (pc_th_.joinable()) pc_th_.join();   // (drains the queued copies first)
   // the engine is alive until the front end is stopped (and no step is in flight now)
-  for (int k = 0; k < 3; ++k)
+  for (int k = 0; k < narena_; ++k)
     if (arena_pinned_[k]) { api_->host_unregister(api_->eng, arena_[k]); arena_pinned_[k] = false; }
 }
 
@@ -308,6 +315,83 @@ void Frontend::scatter_conn(FeConn& c, const u8* data, u32 n) {
   wblock_update(c);
 }
 
+// first gather entry whose insertion point is at or after `off` (dst never decreases)
+static u32 gath_lower(const EgressRef* g, u32 n, u32 off) {
+  u32 lo = 0, hi = n;
+  while (lo < hi) {
+    const u32 mid = (lo + hi) >> 1;
+    if (g[mid].dst < off) lo = mid + 1; else hi = mid;
+  }
+  return lo;
+}
+
+void Frontend::scatter_ref(FeConn& c, const u8* base, const ConnOut& o, const Scatter& sc) {
+  const EgressRef* g = (const EgressRef*)(base + sc.gath_off);
+  const u32 end = o.off + o.len;
+  std::vector<iovec> v;
+  u32 pos = o.off;
+  for (u32 k = gath_lower(g, sc.gath_n, o.off); k < sc.gath_n && g[k].dst < end; ++k) {
+    if (!g[k].len) continue;
+    if (g[k].dst > pos) v.push_back(iovec{(void*)(base + pos), (size_t)(g[k].dst - pos)});
+    v.push_back(iovec{(void*)(uintptr_t)g[k].src, (size_t)g[k].len});
+    pos = g[k].dst;
+  }
+  if (end > pos) v.push_back(iovec{(void*)(base + pos), (size_t)(end - pos)});
+  std::lock_guard<std::mutex> gd(c.mu);
+  if (c.fd < 0) return;
+  size_t i = 0;
+  if (c.out_pos >= c.out.size()) {   // nothing queued: straight from the slot and the arena
+    c.out.clear();
+    c.out_pos = 0;
+    u64 sent = 0;
+    while (i < v.size()) {
+      msghdr m{};
+      m.msg_iov = &v[i];
+      m.msg_iovlen = std::min<size_t>(v.size() - i, 1024);   // (IOV_MAX)
+      ssize_t k = ::sendmsg(c.fd, &m, MSG_NOSIGNAL);
+      if (k < 0 && errno == EINTR) continue;
+      if (k <= 0) break;
+      sent += (u64)k;
+      size_t left = (size_t)k;
+      while (i < v.size() && left >= v[i].iov_len) { left -= v[i].iov_len; ++i; }
+      if (left) { v[i].iov_base = (u8*)v[i].iov_base + left; v[i].iov_len -= left; }
+    }
+    tx_bytes_ += sent;
+    c.last_tx = now_ns();
+  }
+  for (; i < v.size(); ++i) c.out.append((const char*)v[i].iov_base, v[i].iov_len);   // the rest waits
+  wblock_update(c);
+}
+
+void Frontend::materialize(Scatter& sc, const u8* egress, u64 bytes) {
+  if (!sc.gath_n) {
+    sc.own.assign((const char*)egress, bytes);
+    sc.egress = nullptr;
+    return;
+  }
+  const EgressRef* g = (const EgressRef*)(egress + sc.gath_off);
+  std::string own;
+  u32 k = 0;
+  for (auto& o : sc.co) {   // (connection regions lie in ascending offset order)
+    if (!o.len) continue;
+    const u32 start = (u32)own.size(), end = o.off + o.len;
+    u32 pos = o.off;
+    k = gath_lower(g, sc.gath_n, o.off);
+    for (; k < sc.gath_n && g[k].dst < end; ++k) {
+      if (!g[k].len) continue;
+      own.append((const char*)egress + pos, g[k].dst - pos);
+      own.append((const char*)(uintptr_t)g[k].src, g[k].len);
+      pos = g[k].dst;
+    }
+    own.append((const char*)egress + pos, end - pos);
+    o = ConnOut{start, (u32)own.size() - start};
+  }
+  sc.own.swap(own);
+  sc.egress = nullptr;
+  sc.gath_n = 0;
+  sc.gath_off = 0;
+}
+
 void Frontend::send(u32 conn, const char* data, size_t n) {
   if (conn >= c_max_ || !n) return;
   FeConn& c = *conns_[conn];
@@ -322,8 +406,12 @@ void Frontend::send_after(u32 conn, const char* data, size_t n) {
   {
     std::lock_guard<std::mutex> g(ctl_mu_);
     // behind the steps in flight and the next one, which carries the control writes the
-    // command staged (Engine::pack_deltas): the reply never overtakes its own table changes
-    ctl_out_.push_back(CtlOut{sub_step_.load() + 1, conn, conns_[conn]->gen.load(), std::string(data, n)});
+    // command staged (Engine::pack_deltas): the reply never overtakes its own table changes.
+    // With batch ids: exactly behind the egress of the step that applied the command's
+    // write batch -- before the next step's, where a consumer it activated first gets
+    // deliveries (k_stage flips cons_active 2 -> 1): no Basic.Deliver before its ConsumeOk
+    const u64 batch = api_->dl_state ? api_->dl_state(api_->eng, 0) : 0;
+    ctl_out_.push_back(CtlOut{sub_step_.load() + 1, conn, conns_[conn]->gen.load(), std::string(data, n), batch});
   }
   wake_stepper();
 }
@@ -364,9 +452,10 @@ void Frontend::release_ctl() {
   std::vector<CtlOut> go;
   {
     std::lock_guard<std::mutex> g(ctl_mu_);
-    const u64 fin = fin_step_.load();
+    // the egress queued so far covers steps <= out_step_ and write batches <= out_batch_;
     // held (write-behind) steps not yet released keep every reply behind them
-    while (!ctl_out_.empty() && ctl_out_.front().after <= fin && held_.empty()) {
+    while (!ctl_out_.empty() && ctl_out_.front().after <= out_step_ && ctl_out_.front().batch <= out_batch_ &&
+           held_.empty()) {
       go.push_back(std::move(ctl_out_.front()));
       ctl_out_.pop_front();
     }
@@ -839,7 +928,9 @@ void Frontend::io_loop(int i) {
             if (o.len) {
               FeConn& c = *conns_[id];
               if (!sc->gen.empty() && sc->gen[id] != c.gen.load()) continue;   // closed since: stale
-              if (c.mode == M_DATA || c.mode == M_HOST) scatter_conn(c, base + o.off, o.len);
+              if (c.mode != M_DATA && c.mode != M_HOST) continue;
+              if (sc->gath_n) scatter_ref(c, base, o, *sc);
+              else scatter_conn(c, base + o.off, o.len);
             }
           }
         }
@@ -1139,10 +1230,15 @@ void Frontend::finish_oldest(std::deque<Inflight>& inflight) {
   const ConnOut* co = api_->conn_out(api_->eng, p);
   Held h;
   h.step = f.step;
+  h.batch_hi = f.batch_hi;
   h.needs_commit = needs_commit;
   h.sc.co.assign(co, co + c_max_);
   h.sc.gen = std::move(f.gen);
   h.sc.egress = api_->egress_host(api_->eng, slot);
+  if (c.n_ref && c.egress_bytes > c.gath_off) {   // deliveries referencing arena bodies
+    h.sc.gath_off = c.gath_off;
+    h.sc.gath_n = (u32)((c.egress_bytes - c.gath_off) / sizeof(EgressRef));
+  }
   if (needs_commit && api_->conn_conf) {
     const u32* cf = api_->conn_conf(api_->eng, p);
     h.conf.assign(cf, cf + c_max_);
@@ -1283,12 +1379,13 @@ void Frontend::stepper() {
       }
       f.p = p;
       f.step = ++step_no_;
+      f.batch_hi = api_->dl_state ? api_->dl_state(api_->eng, 1) : 0;
       sub_step_.store(step_no_);
       f.segs = std::move(seglens);
       f.gen.resize(c_max_);
       for (u32 k = 0; k < c_max_; ++k) f.gen[k] = conns_[k]->gen.load();
       inflight.push_back(std::move(f));
-      arena_i_ = (arena_i_ + 1) % 3;
+      arena_i_ = (arena_i_ + 1) % narena_;
       last_step = now_ns();
       submitted = true;
       last_busy_ = false;
@@ -1452,9 +1549,10 @@ void Frontend::stepper_sharded() {
                        cfg_.worker);
     }
     if (!check(p)) break;
-    arena_i_ = (arena_i_ + 1) % 3;
+    arena_i_ = (arena_i_ + 1) % narena_;
     f.p = p;
     f.step = ++step_no_;
+    f.batch_hi = api_->dl_state ? api_->dl_state(api_->eng, 1) : 0;
     sub_step_.store(step_no_);
     f.segs = std::move(seglens);
     f.gen.resize(c_max_);
@@ -1515,6 +1613,7 @@ void Frontend::stepper_sharded() {
         Inflight f2;
         f2.p = p2;
         f2.step = ++step_no_;
+        f2.batch_hi = api_->dl_state ? api_->dl_state(api_->eng, 1) : 0;
         f2.gen.resize(c_max_);
         for (u32 j = 0; j < c_max_; ++j) f2.gen[j] = conns_[j]->gen.load();
         inflight.push_back(std::move(f2));
@@ -1572,6 +1671,11 @@ void Frontend::stepper_sharded() {
 bool Frontend::stash_pend(bool copy) {
   if (!pend_valid_) return true;
   pend_valid_ = false;
+  // replies due behind the egress already queued go first: this step's egress may hold
+  // deliveries a reply must precede (a ConsumeOk before its consumer's first delivery)
+  release_ctl();
+  out_step_ = std::max(out_step_, pend_.step);
+  out_batch_ = std::max(out_batch_, pend_.batch_hi);
   // the common case (no copy, nothing held): the IO threads wait for the D2H themselves
   // before writing the slot out, so the stepper goes on to gather and submit meanwhile
   const bool defer = !copy && !pend_.needs_commit && held_total_ == 0 && api_->egress_ready != nullptr;
@@ -1581,8 +1685,7 @@ bool Frontend::stash_pend(bool copy) {
   }
   if (!pend_.needs_commit && held_total_ == 0) {
     if (copy) {   // the slot may be reused before it is written: copy
-      pend_.sc.own.assign((const char*)pend_.sc.egress, pend_bytes_);
-      pend_.sc.egress = nullptr;
+      materialize(pend_.sc, pend_.sc.egress, pend_bytes_);
     } else if (pend_bytes_ && defer) {
       pend_.sc.wait_slot = pend_slot_;
     }
@@ -1611,15 +1714,13 @@ bool Frontend::stash_pend(bool copy) {
   }
   if (now_any) {
     now.egress = pend_.sc.egress;
-    if (copy) {
-      now.own.assign((const char*)pend_.sc.egress, pend_bytes_);
-      now.egress = nullptr;
-    }
+    now.gath_n = pend_.sc.gath_n;
+    now.gath_off = pend_.sc.gath_off;
+    if (copy) materialize(now, pend_.sc.egress, pend_bytes_);
     out_.push_back(std::move(now));
   }
   if (held_any) {
-    pend_.sc.own.assign((const char*)pend_.sc.egress, pend_bytes_);
-    pend_.sc.egress = nullptr;
+    materialize(pend_.sc, pend_.sc.egress, pend_bytes_);
     held_.push_back(std::move(pend_));
   }
   return true;

@@ -90,6 +90,12 @@ struct FrontendCfg {
   // connections are gathered and writes the finished step's egress after that, while the
   // step is submitted (the sockets' send path no longer sits on the step's critical path)
   bool async_scatter = true;
+  // egress by reference (step_abi.h set_egress_ref): a delivery of a body that arrived in
+  // the same step is rendered without it and sent from the ingress arena with sendmsg
+  // iovecs -- the body crosses PCIe once.  Needs NARENA arenas (an arena is gathered into
+  // again only after every egress that may reference it is written)
+  bool egress_ref = true;
+  u32 egress_ref_min = 256;
 };
 
 struct FeStats {
@@ -180,6 +186,7 @@ class Frontend {
     std::vector<std::pair<u32, u32>> segs;
     std::vector<u32> gen;
     std::vector<std::pair<u32, u64>> gets;   // (conn, id) of the Basic.Gets it serves
+    u64 batch_hi = 0;   // staged control-write batches taken by this step and earlier (dl_state 1)
   };
   struct PendGet { GetReq r; u64 id; };
   std::mutex get_mu_;
@@ -194,10 +201,13 @@ class Frontend {
     // closed since (its slot possibly reused by a new client) are dropped, never written
     std::vector<u32> gen;
     int wait_slot = -1;      // egress slot whose D2H the writer waits for first (-1: ready)
+    // egress by reference: gath_n EgressRef entries at gath_off of the egress bytes (0: the
+    // bytes are the wire bytes)
+    u32 gath_n = 0, gath_off = 0;
   };
   // needs_commit: the step's store records must commit before the confirm-gated part of
   // its egress leaves; conf = that step's confirm bytes per connection (empty = all gated)
-  struct Held { u64 step; bool needs_commit; Scatter sc; std::vector<u32> conf; };
+  struct Held { u64 step; bool needs_commit; Scatter sc; std::vector<u32> conf; u64 batch_hi = 0; };
 
   void stepper();
   void stepper_sharded();
@@ -219,6 +229,11 @@ class Frontend {
   bool write_some(FeConn& c);   // mu held
   void wblock_update(FeConn& c);   // mu held
   void scatter_conn(FeConn& c, const u8* data, u32 n);
+  // one connection's part of a step's egress, its referenced bodies spliced in (sendmsg)
+  void scatter_ref(FeConn& c, const u8* base, const ConnOut& o, const Scatter& sc);
+  // the scatter's wire bytes into sc.own (its egress slot / arena may be reused before it
+  // is written): bodies spliced in, offsets rewritten
+  static void materialize(Scatter& sc, const u8* egress, u64 bytes);
   void gather_conn(FeIo& io, FeConn& c, u8* arena, u64 cap);
   bool check(int rc);
 
@@ -233,9 +248,14 @@ class Frontend {
   std::thread stepper_;
   std::atomic<bool> running_{false};
 
-  // pinned ingress arenas (3: the H2D of step t is done before step t+3 gathers)
-  u8* arena_[3] = {nullptr, nullptr, nullptr};
-  bool arena_pinned_[3] = {false, false, false};
+  // pinned ingress arenas, gathered into in turn.  3 suffice for the H2D (step t's copy is
+  // done before step t+3 gathers); egress by reference needs 4: step t's egress is written
+  // by the IO threads after their gather of step t+2 and may still be in progress while
+  // step t+3 gathers, and it may reference step t's arena.  One more for margin
+  static constexpr int NARENA = 5;
+  u8* arena_[NARENA] = {};
+  bool arena_pinned_[NARENA] = {};
+  int narena_ = 3;
   int arena_i_ = 0;
 
   // IO phase
@@ -304,12 +324,18 @@ class Frontend {
   // steps submitted / finished so far (control replies and freed connection slots wait
   // for the steps that were in flight when they were produced)
   std::atomic<u64> sub_step_{0}, fin_step_{0};
-  struct CtlOut { u64 after; u32 conn; u32 gen; std::string data; };
+  // after: released behind the egress of step `after`; batch (light sections, 0: none):
+  // and not before the egress of the step that applied that staged-write batch, and never
+  // after the egress of any later step (stash_pend releases first)
+  struct CtlOut { u64 after; u32 conn; u32 gen; std::string data; u64 batch = 0; };
   std::mutex ctl_mu_;
   std::deque<CtlOut> ctl_out_;
   bool ctl_pending();
   bool ctl_needs_step();
   void release_ctl();
+  // step / write batch of the last egress queued for writing (out_ or held_): a reply is
+  // released only once the egress of the step it waits for was queued, and before the next
+  u64 out_step_ = 0, out_batch_ = 0;
   // closed connection slots: reusable once the steps in flight at their close finished
   std::deque<std::pair<u64, u32>> quarantine_;   // (sub_step_ at close, slot), free_mu_
   i64 last_submit_ = 0;   // (stats: the stepper's period between submits)

@@ -136,6 +136,9 @@ DEV u32 block_scan(u32 v, u32* lds, u32& total) {
   return res;
 }
 
+DEV u64 shfl_xor64(u64 v, int m) {
+  return ((u64)(u32)__shfl_xor((int)(v >> 32), m, 64) << 32) | (u32)__shfl_xor((int)(u32)v, m, 64);
+}
 DEV u64 shfl64(u64 v, u32 src) {
   u32 lo = __shfl((u32)v, src, 64), hi = __shfl((u32)(v >> 32), src, 64);
   return (u64(hi) << 32) | lo;
@@ -422,6 +425,7 @@ __global__ __launch_bounds__(1024) void k_stage(DS d) {
       d.tot[TS_NDGET] = 0;
       d.tot[TS_SPILL_USED] = 0;
       d.ctr->spill_moved = 0;
+      d.ctr->n_ref = 0; d.ctr->gath_off = 0; d.ctr->ref_bytes = 0;
       *d.egress_budget = 0;
     }
     // connections whose control command the host has answered resume with this step (the
@@ -1702,6 +1706,18 @@ __global__ __launch_bounds__(256) void k_decode(DS d) {
       }
     }
     pb.nwords = pb.rk_len <= 32 ? build_keyvec_win(d, rkw, pb.rk_len, pi) : build_keyvec(d, w + pb.rk_off, pb.rk_len, pi);
+    // egress by reference: a body that is one run of this step's new ingress bytes (not in
+    // the connection's carry) keeps its host address -- its deliveries can be sent from
+    // there instead of crossing PCIe back (render_deliv)
+    if (c.nfrag == 1 && d.in->ingress_host && d.in->ref_back != 0xffffffffu && c.body_size >= d.in->ref_min &&
+        c.seg < nseg) {
+      const Frag fg = d.frags[c.frag0];
+      const u32 w0 = d.seg_start[c.seg], cl = d.seg_total[c.seg] - d.segs[c.seg].len;
+      if (fg.len == c.body_size && fg.off >= w0 + cl) {
+        pb.flags |= MF_HREF;
+        pb.pad = (u32)(d.segs[c.seg].src + (fg.off - w0 - cl));
+      }
+    }
     d.pubs[pi] = pb;   // (its channel's confirm count: k_marks)
   } else if (c.kind == CK_ACK || c.kind == CK_NACK || c.kind == CK_REJECT) {
     const u32 ai = d.rank_scan ? d.cmd_ack_rank[i] : sprefa[c.seg] + c.pad[2];
@@ -2555,6 +2571,7 @@ DEV void store_one_pre(const DS& d, u32 p, u32 lane, const Pub& pb, u32 nq, u32 
     m.flags = pb.flags;
     m.pub_step = (u32)d.in->step;
     m.pad = 0;
+    m.href = (pb.flags & (MF_HREF | MF_IMPORTED)) == MF_HREF ? d.in->ingress_host + pb.pad : 0ull;
     d.msgs[msg] = m;
     u32 pmsg = msg;
     if (fit < pb.nq) {
@@ -3396,6 +3413,19 @@ DEV u32 deliver_size(const DS& d, u32 cons, const MsgEnt& m, u32 conn) {
   return sz + m.body_len + 8 * nb;
 }
 
+// egress by reference: the delivery of message m to connection conn is rendered without its
+// body (the host sends those bytes from the publishing step's ingress payload): a body the
+// publish decode marked (MsgEnt.href), published at most ref_back steps ago, no shorter than
+// ref_min and within one body frame of the connection.  Link pseudo-connections ship
+// restore records, never references.  k_dv_write and render_deliv must agree: same inputs
+DEV bool deliv_ref(const DS& d, const MsgEnt& m, u32 conn) {
+  if (!m.href || d.in->ref_back == 0xffffffffu || m.body_len < d.in->ref_min) return false;
+  if ((u32)d.in->step - m.pub_step > d.in->ref_back) return false;
+  if (d.links && d.conn_link[conn]) return false;
+  const u32 fm = d.conn_frame_max[conn];
+  return fm == 0 || m.body_len <= fm - 8;
+}
+
 // give back channel reservations for `take` messages not delivered after all
 DEV void unreserve(const DS& d, u32 c, u32 take) {
   u32 ch = d.cons_ch[c];
@@ -3885,7 +3915,7 @@ __global__ void k_dv_write(DS d) {
   const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
   const u32 n = d.ctr->n_deliv;
   const bool valid = i < n;
-  u32 lat = 0;
+  u32 lat = 0, nref = 0, rbytes = 0;
   Deliv dv;
   dv.msg = INVALID; dv.q = 0; dv.qpos = 0; dv.flags = 2;
   if (valid) {
@@ -3919,9 +3949,11 @@ __global__ void k_dv_write(DS d) {
     u.expire_ms = ds.expire_ms;
     d.uwin[(u64)ch * (d.ucap_mask + 1) + ((tag - 1) & d.ucap_mask)] = u;
     const MsgEnt& m = d.msgs[ds.msg];
-    const u32 sz = deliver_size(d, cons, m, ch / d.chpc);
+    const bool ref = deliv_ref(d, m, ch / d.chpc);
+    const u32 sz = deliver_size(d, cons, m, ch / d.chpc) - (ref ? m.body_len : 0u);
     dv.size = sz;
     d.dv_size[i] = sz;
+    if (ref) { nref = 1; rbytes = m.body_len; }
     d.deliv[i] = dv;
     lat = (u32)d.in->step - m.pub_step;
     // the channel's last delivery this step: the window needs a k_chan_advance pass
@@ -3945,6 +3977,15 @@ __global__ void k_dv_write(DS d) {
   if (d.persist)   // manual-ack delivery of a persistent message: its row becomes an unack
     wave_consumed(d, dv.msg, dv.q, dv.qpos, 3u, valid && !(dv.flags & 2));
   wave_add_u32(d.ctr->lat_hist, lat < LAT_BINS ? lat : LAT_BINS - 1, 1u, valid);
+  {   // referenced deliveries / body bytes of the step (one atomic per wave)
+    u32 nr = nref;
+    u64 rb = rbytes;
+    for (int o = 32; o > 0; o >>= 1) { nr += __shfl_xor(nr, o, 64); rb += shfl_xor64(rb, o); }
+    if (lane_id() == 0 && nr) {
+      atomicAdd(&d.ctr->n_ref, nr);
+      atomicAdd((unsigned long long*)&d.ctr->ref_bytes, (unsigned long long)rb);
+    }
+  }
 }
 
 // per connection: egress size = returns + confirms + deliveries
@@ -3964,6 +4005,19 @@ __global__ void k_conn_sizes(DS d) {
     dl = d.dv_off[l] + d.dv_size[l] - d.dv_off[f];
   }
   d.conn_total[c] = d.conn_ret_bytes[c] + conf + dl + 13u * d.conn_gempty[c];
+}
+
+// the step's D2H size: its rendered bytes, then -- when any delivery references a host
+// body -- the gather table (one EgressRef per delivery), so one copy carries both
+DEV void set_egress_bytes(const DS& d, u32 eb) {
+  if (d.ctr->n_ref) {
+    u32 nd = d.ctr->n_deliv;
+    if (nd > d.deliv_max) nd = d.deliv_max;
+    const u32 go = align16(eb);
+    d.ctr->gath_off = go;
+    eb = go + 16u * nd;
+  }
+  d.ctr->egress_bytes = eb;
 }
 
 // single block (c_max <= CONN_LAYOUT_MAX): k_conn_sizes + scan of conn_total + k_conn_out
@@ -4049,7 +4103,7 @@ __global__ __launch_bounds__(1024) void k_conn_layout(DS d) {
       o.len = d.links && d.conn_link[c] ? 0u : total;   // links: their bytes go to lsend_*
       d.conn_base[c] = o.off;
       d.conn_out[c] = o;
-      if (c == d.c_max - 1) d.ctr->egress_bytes = o.off + total;
+      if (c == d.c_max - 1) set_egress_bytes(d, o.off + total);
     }
     run += all;
   }
@@ -4062,7 +4116,7 @@ __global__ void k_conn_out(DS d) {
   o.off = d.conn_base[c];
   o.len = d.links && d.conn_link[c] ? 0u : d.conn_total[c];
   d.conn_out[c] = o;
-  if (c == d.c_max - 1) d.ctr->egress_bytes = o.off + d.conn_total[c];
+  if (c == d.c_max - 1) set_egress_bytes(d, o.off + d.conn_total[c]);
 }
 
 // ============================================================================ links (X2/X3)
@@ -4140,7 +4194,12 @@ DEV void render_deliv(const DS& d, u32 i) {
   u32 conn = ch / d.chpc;
   u32 f = d.conn_dfirst[conn];
   const u8* slot = msg_slot(d, m.log_off);
+  // gather entry of this delivery (the table exists when some delivery of the step
+  // references its body; dst of an unreferenced one = its end, so dst never decreases)
+  const bool ref = deliv_ref(d, m, conn);
+  EgressRef* gt = d.ctr->n_ref ? (EgressRef*)((u8*)d.in->egress + d.ctr->gath_off) : nullptr;
   if (d.links && d.conn_link[conn]) {   // X2: a restore record for the shadow queue
+    if (gt && lane == 0) gt[i] = EgressRef{0ull, d.conn_base[conn], 0u};
     const u32 dest = d.conn_link[conn] - 1;
     const u32 po = d.link_bbase[conn] + (d.dv_off[i] - d.dv_off[f]);
     u8* lo = d.lsend_pay + (u64)d.link_dbase[dest] + po;
@@ -4166,6 +4225,8 @@ DEV void render_deliv(const DS& d, u32 i) {
   }
   u64 off = (u64)d.conn_base[conn] + d.conn_ret_bytes[conn] + d.conn_conf_bytes[conn] + d.dv_off[i] -
             d.dv_off[f];
+  if (gt && lane == 0)   // (a referenced body goes after its body frame's 7-byte header)
+    gt[i] = ref ? EgressRef{m.href, (u32)(off + dv.size - 1u), m.body_len} : EgressRef{0ull, (u32)(off + dv.size), 0u};
   if (off + dv.size > d.egress_cap) return;  // never: dequeue reserves an egress byte budget
   u8* o = (u8*)d.in->egress + off;
   u32 chno = d.ch_num[ch];
@@ -4202,6 +4263,13 @@ DEV void render_deliv(const DS& d, u32 i) {
   u32 bp = hp + m.props_len + 1;
   u32 fm = d.conn_frame_max[conn];
   u32 fmb = fm ? fm - 8 : 0xffffffffu;
+  if (ref) {   // one body frame whose payload the host inserts: header, then the frame end
+    if (lane == 0) {
+      put_frame_hdr(o + bp, 3, chno, m.body_len);
+      o[bp + 7] = 0xCE;
+    }
+    return;
+  }
   const u8* body = slot + m.body_off;
   for (u32 b0 = 0; b0 < m.body_len; b0 += fmb) {
     u32 bl = m.body_len - b0 < fmb ? m.body_len - b0 : fmb;
@@ -4887,13 +4955,26 @@ __global__ void k_cold_in(DS d, const ColdRec* recs, u32 n, const u64* scan_end)
 // job's sequence number into host-mapped flag[0].  Bounded: after ~20 s the wave gives up
 // and sets flag[1] (the exchange thread always releases its job, so only a lost thread
 // would get there; the host reports it), so a stuck host can never wedge the queue.
-__global__ __launch_bounds__(64) void k_xwait(const u32* flag, u32 seq, u32* gave_up) {
+// lim: s_memrealtime ticks (100 MHz) after which the job counts as lost (the host derives
+// it from the exchange timeout); phase B then imports nothing -- its receive counts are
+// zeroed here too (the host zeroed them before handing the job over; a job that finishes
+// after the give-up must not have them imported), and the next exchange() call throws
+__global__ __launch_bounds__(64) void k_xwait(const u32* flag, u32 seq, u32* gave_up, u64 lim, u32* xchg, u32 world) {
   const u64 t0 = __builtin_amdgcn_s_memrealtime();   // 100 MHz
   while (true) {
     const u32 v = __hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
     if ((int)(v - seq) >= 0) return;
-    if (__builtin_amdgcn_s_memrealtime() - t0 > 2000000000ull) {
+    if (__builtin_amdgcn_s_memrealtime() - t0 > lim) {
+      const u32 r = threadIdx.x;
+      if (r < world && r < WORLD_MAX) {
+        __hip_atomic_store(&xchg[XC_RECV_N + r], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(&xchg[XC_RECV_B + r], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(&xchg[XC_RECV_AN + r], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(&xchg[XC_RECV_AB + r], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(&xchg[XC_RACK_N + r], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
       if (threadIdx.x == 0) __hip_atomic_store(gave_up, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __threadfence_system();
       return;
     }
     __builtin_amdgcn_s_sleep(32);

@@ -36,8 +36,10 @@ enum : u32 {
   MF_ONEQ = 128,        // cross-rank record routed at its origin to exactly one queue: RDesc.tq
   MF_SLOTFMT = 256,     // cross-rank record laid out as a body-log slot ([ex][rk][props] padded
                         // to 16, then the body): the owner stores it with one aligned copy
-  MF_HOSTPUB = 512      // a publish assembled by the host (larger than the connection carry):
+  MF_HOSTPUB = 512,     // a publish assembled by the host (larger than the connection carry):
                         // routed by its exchange, publisher channel in RDesc.pad[0], conn pad[1]
+  MF_HREF = 1024        // (Pub only) the body is one contiguous run of this step's new ingress
+                        // bytes, at payload offset Pub.pad: MsgEnt.href = StepIn.ingress_host + it
 };
 
 // ---- unacked slot states
@@ -70,8 +72,18 @@ struct StepIn {         // host -> device per step (96 B)
   u32 spill_frac;
   u32 spill_hot;
   u32 spill_budget;
-  u32 pad_[2];
+  // egress by reference (bodies are not sent back over PCIe): a delivery whose
+  // body is a run of the host ingress payload of a step no more than ref_back steps back
+  // (0xffffffff: off) and at least ref_min bytes long is rendered without its body bytes --
+  // the step's gather table (EgressRef, after the rendered bytes) tells the host where they
+  // go.  ingress_host = this step's payload in host memory (0: its bodies are not referable)
+  u32 ref_back;
+  u32 ref_min;
+  u64 ingress_host;
+  u64 pad_;
 };
+static_assert(sizeof(StepIn) == 112, "StepIn layout");
+
 
 
 struct Cmd {            // one assembled command (device internal)
@@ -165,7 +177,9 @@ struct MsgEnt {         // message table (one per stored message; body stored on
   u32 flags;
   u32 pub_step;         // step the message was published (latency histogram)
   u32 pad;
+  u64 href;             // host address of the body in its step's ingress payload (0: none)
 };
+static_assert(sizeof(MsgEnt) == 64, "MsgEnt layout");
 
 struct Desc {           // queue ring entry
   u32 msg;

@@ -198,13 +198,15 @@ class Engine {
     sdma_ = copy_mode_ == 1;
     copy_wgs_ = (u32)get("copy_wgs", 16);
     sdma_pref_ = cfg.contains("sdma_engine") ? cfg["sdma_engine"].cast<int>() : -1;
+    wait_ms_ = (u32)get("wait_timeout_ms", 10000);
     sdma_split_ = cfg.contains("sdma_split") ? std::max(1, std::min(2, cfg["sdma_split"].cast<int>())) : 1;
 
     // ---- allocations
     auto dev = [&](const char* name, size_t bytes) { return alloc(name, bytes, false); };
     auto hst = [&](const char* name, size_t bytes) { return alloc(name, bytes, true); };
     d_.ctr = (Counters*)dev("ctr", sizeof(Counters));
-    egress_alloc_ = d_.egress_cap + d_.work_cap + (u64)nch * 21 + 4096;
+    // (+ the gather table of egress by reference: one EgressRef per delivery)
+    egress_alloc_ = d_.egress_cap + d_.work_cap + (u64)nch * 21 + 4096 + 16ull * d_.deliv_max;
     // per-parity step IO: step t uses set t&1, so step t+1's H2D and step t-1's D2H
     // overlap step t's kernels (double buffering; the graph of each parity is captured once)
     for (int p = 0; p < 2; ++p) {
@@ -503,6 +505,7 @@ class Engine {
     }
     d_.tot = (u32*)dev("tot", 4ull * 128);
     d_.egress_budget = (u64*)dev("egress_budget", 8);
+    gate_dummy_ = dev("gate_dummy", 64);
     // Basic.Get: rendered frames + result, host-mapped (a stored body never exceeds the
     // carry, which bounds an assembled command)
     get_cap_ = (u64)d_.carry_cap + d_.carry_cap / 64 + 4096;
@@ -626,6 +629,11 @@ class Engine {
     // overlap (world 1): the step's ingest half runs on its own stream, next to the
     // previous step's routing / delivery half
     overlap_ = d_.world == 1 && get("overlap", 1) != 0;
+    // egress by reference (StepIn.ref_back / ref_min): off unless the driver keeps its
+    // ingress payloads for it (set_egress_ref)
+    ref_back_ = cfg.contains("egress_ref_back") ? cfg["egress_ref_back"].cast<int>() : -1;
+    if (ref_back_ > 64) throw std::runtime_error("egress_ref_back: at most 64 steps back");
+    ref_min_ = (u32)get("egress_ref_min", 256);
     // egress_gate (HSA SDMA egress, overlapped steps): the step's D2H is queued on the SDMA
     // engine at launch, behind a gate signal the step's last kernel opens (final_step), sized
     // from the recent steps' egress (a host-issued tail copies the rest when a step renders
@@ -660,7 +668,9 @@ class Engine {
     if (copy_mode_ == 3)
       for (int e = 0; e < EGRESS_SLOTS; ++e) {
         if (gate_sig_[e].handle) hsa_signal_store_screlease(gate_sig_[e], 0);
-        if (sdma_pending_[e] || tail_pending_[e]) sdma_wait(e);
+        if (sdma_pending_[e] || tail_pending_[e]) {
+          try { sdma_wait(e); } catch (const std::exception&) {}   // (reported already)
+        }
       }
     (void)hipStreamSynchronize(s_comp_);
     (void)hipStreamSynchronize(s_h2d_);
@@ -789,6 +799,8 @@ class Engine {
     o["copy_engine"] = copy_mode_ == 3 ? "hsa-sdma" : copy_mode_ == 2 ? "kernel" : (sdma_ ? "nocu" : "blit");
     o["copy_wgs"] = copy_wgs_;
     o["egress_gate"] = gated_ ? 1 : 0;
+    o["egress_ref_back"] = ref_back_;
+    o["egress_ref_min"] = ref_min_;
     o["egress_slots"] = EGRESS_SLOTS;
     { u32 e = 0; while (copy_mode_ == 3 && e < 32 && !(((u32)sdma_engine_ >> e) & 1u)) ++e; o["sdma_engine"] = copy_mode_ == 3 ? (int)e : -1; }
     { u32 e = 0; while (sdma_engine2_ && e < 32 && !(((u32)sdma_engine2_ >> e) & 1u)) ++e; o["sdma_engine2"] = sdma_engine2_ ? (int)e : -1; }
@@ -837,6 +849,9 @@ class Engine {
     StepIn* in = stage_in_[p];
     *in = StepIn{};
     in->nseg = nseg;
+    in->ref_back = ref_back_ >= 0 ? (u32)ref_back_ : 0xffffffffu;
+    in->ref_min = ref_min_;
+    in->ingress_host = ref_back_ >= 0 && payload_len ? payload_ptr : 0;
     in->flags = sflags;
     in->now_ms = now_ms;
     in->step = step;
@@ -852,6 +867,10 @@ class Engine {
     if (spec_[e]) {
       hsa_signal_store_screlease(gate_sig_[e], 1);
       in->gate = (u64)&((amd_signal_t*)gate_sig_[e].handle)->value;
+      if (gate_fault_) {   // (tests) the last kernel opens a scratch word instead: the copy never starts
+        gate_fault_ = false;
+        in->gate = (u64)gate_dummy_;
+      }
     }
     const int is = (int)(seq_ % INGRESS_SLOTS);
     in->ingress = (u64)ingress_slot_[is];
@@ -1009,6 +1028,15 @@ class Engine {
   void new_batch() {   // (dl_mu_ held)
     dl_.emplace_back();
     dl_.back().open = dl_open_ > 0;
+    dl_.back().id = dl_next_id_++;
+  }
+  // batch ids (light sections tie their replies to them, Frontend::send_after): 0 = the
+  // batch staging goes into now (the next one to be created when none is open), 1 = every
+  // batch up to this id was taken by a submitted step (or applied by flush_deltas)
+  u64 dl_state(int which) {
+    std::lock_guard<std::mutex> g(dl_mu_);
+    if (which == 1) return dl_.empty() ? dl_next_id_ - 1 : dl_.front().id - 1;
+    return (!dl_.empty() && dl_.back().open) ? dl_.back().id : dl_next_id_;
   }
   // from the next submitted step on, every step moves queued bodies in the oldest frac/65536
   // of the HBM log (past the first `hot` entries of a queue with consumers) to the host
@@ -1517,6 +1545,7 @@ class Engine {
     DS& io = io_[0];
     StepIn& in = *stage_in_[0];   // (k_stage copies it to the device; no step in flight)
     in = StepIn{};
+    in.ref_back = 0xffffffffu;   // (no dispatch: nothing rendered)
     in.nseg = 0;
     in.now_ms = now_ms;
     in.step = seq_;
@@ -1670,6 +1699,11 @@ class Engine {
     *or_flags = orf;
     if (rc) return rc;
     counts_ready_[q] = false;
+    // what the next phase B (parity q^1) imports starts out as nothing: the job writes the
+    // counts when it succeeds; a phase B whose wait gives up imports nothing instead of the
+    // counts parity q^1 held two steps ago.  (Its last reader, step t-2, has
+    // finished: its results were collected before this step's submit)
+    x_recv_counts(q ^ 1, nullptr);
     std::lock_guard<std::mutex> g(xmu_);
     xq_ = q;
     xflags_ = flags;
@@ -1871,7 +1905,7 @@ class Engine {
         rc = rccl_->bulk(snd, rcv);
       }
       if (rc) return rc;
-      x_wait_ = dst < 0;
+      if (dst < 0) x_wait_ = true;   // (stepper thread only: the exchange thread never touches it)
       if (xfailover_ || dst >= 0) {   // bounded: a peer lost mid-transfer must not wedge the compute stream
         rc = rccl_->wait(rccl_->event());
         if (rc) return rc;
@@ -1921,22 +1955,21 @@ class Engine {
       HIPCHECK(hipStreamSynchronize(s_x_));
     }
     // what launch_b writes into the importing step's xchg: per rank [records, bytes,
-    // publish records, publish bytes]
-    lag_recv_.assign(5 * d_.world, 0);
+    // publish records, publish bytes].  A local vector: on the exchange thread (dst >= 0)
+    // the stepper's lag_recv_ must not be touched (unsynchronised vector writes)
+    std::vector<u32> recv(5 * d_.world, 0);
     for (int i = 0; i < n; ++i) {
       if (i == me) continue;
       const int r = xmembers_[i];
       const u32* h = &hr[(size_t)i * cmqx::XH_WORDS];
-      lag_recv_[r] = h[0] + h[2];
-      lag_recv_[d_.world + r] = h[1] + h[3];
-      lag_recv_[2 * d_.world + r] = h[0];
-      lag_recv_[3 * d_.world + r] = h[1];
-      lag_recv_[4 * d_.world + r] = h[4];
+      recv[r] = h[0] + h[2];
+      recv[d_.world + r] = h[1] + h[3];
+      recv[2 * d_.world + r] = h[0];
+      recv[3 * d_.world + r] = h[1];
+      recv[4 * d_.world + r] = h[4];
     }
-    if (dst >= 0) {
-      x_recv_counts(dst, lag_recv_.data());
-      lag_recv_.clear();
-    }
+    if (dst >= 0) x_recv_counts(dst, recv.data());
+    else lag_recv_.swap(recv);
     ++xseq_;
     return 0;
   }
@@ -1949,8 +1982,10 @@ class Engine {
   // result alone: it carries the flags every rank acts on at the same step.
   int drop_exchange(int q, bool collect = true) {
     counts_ready_[q] = false;
-    lag_recv_.clear();
-    x_wait_ = false;
+    if (!async_x_) {   // (asynchronous: the exchange thread's job owns no stepper state)
+      lag_recv_.clear();
+      x_wait_ = false;
+    }
     if (!async_x_ || !collect) return 0;
     int rc = 0;
     u32 orf = 0;
@@ -1965,14 +2000,18 @@ class Engine {
     if (async_x_) {   // behind its exchange job (the exchange thread writes the counts)
       const u32 w = b_wait_[p];
       b_wait_[p] = 0;
-      if (w) hipLaunchKernelGGL(k_xwait, dim3(1), dim3(64), 0, s_comp_, (const u32*)xflag_d_, w, xflag_d_ + 1);
+      // give up only well past every bound the job itself has (counts barrier + bulk
+      // barrier + the bulk's own wait, each xtimeout_ms) plus settle: then the job is lost
+      const u64 lim = ((u64)xtimeout_ms_ * 3 + 5000) * 100000ull;   // s_memrealtime: 100 MHz
+      if (w) hipLaunchKernelGGL(k_xwait, dim3(1), dim3(64), 0, s_comp_, (const u32*)xflag_d_, w, xflag_d_ + 1, lim,
+                                io_[p].xchg, d_.world);
       else x_recv_counts(p, nullptr);
     } else {
       x_recv_counts(p, lag_recv_.size() == 5 * d_.world ? lag_recv_.data() : nullptr);
+      lag_recv_.clear();
+      if (x_wait_ && rccl_) HIPCHECK(hipStreamWaitEvent(s_comp_, rccl_->event(), 0));
+      x_wait_ = false;
     }
-    lag_recv_.clear();
-    if (x_wait_ && rccl_) HIPCHECK(hipStreamWaitEvent(s_comp_, rccl_->event(), 0));
-    x_wait_ = false;
     if (graph_enabled_) {
       if (!graph_b_[p]) capture_b(p);
       HIPCHECK(hipGraphLaunch(graph_b_[p], s_comp_));
@@ -2060,6 +2099,10 @@ class Engine {
     };
     a.get_out = [](void* e, int p) -> const GetOut* { return ((Engine*)e)->io_[p].get_out_hh; };
     a.host_work = [](void* e) -> int { return ((Engine*)e)->host_work() ? 1 : 0; };
+    a.dl_state = [](void* e, int which) -> u64 { return ((Engine*)e)->dl_state(which); };
+    a.set_egress_ref = [](void* e, int back, u32 min_bytes) -> int {
+      return ((Engine*)e)->guard([&] { ((Engine*)e)->set_egress_ref(back, min_bytes); return 0; });
+    };
     for (int p = 0; p < 2; ++p) {
       std::string sfx = std::to_string(p);
       HostIO& h = io_[p];
@@ -2090,10 +2133,8 @@ class Engine {
   // issued before the caller learnt of the slot)
   void egress_ready(int e) {
     if (copy_mode_ == 3) {
-      if (sdma_pending_[e])
-        hsa_signal_wait_scacquire(sdma_sig_[e], HSA_SIGNAL_CONDITION_EQ, 0, UINT64_MAX, HSA_WAIT_STATE_ACTIVE);
-      if (tail_pending_[e])
-        hsa_signal_wait_scacquire(tail_sig_[e], HSA_SIGNAL_CONDITION_EQ, 0, UINT64_MAX, HSA_WAIT_STATE_ACTIVE);
+      if (sdma_pending_[e]) bounded_wait(sdma_sig_[e], e, "egress D2H");
+      if (tail_pending_[e]) bounded_wait(tail_sig_[e], e, "egress tail D2H");
       return;
     }
     if (d2h_issued_[e]) HIPCHECK(hipEventSynchronize(ev_d2h_[e]));
@@ -2225,13 +2266,35 @@ class Engine {
 
   // the slot's D2H (+ its tail) complete
   void sdma_wait(int e) {
-    if (sdma_pending_[e])
-      hsa_signal_wait_scacquire(sdma_sig_[e], HSA_SIGNAL_CONDITION_EQ, 0, UINT64_MAX, HSA_WAIT_STATE_ACTIVE);
-    if (tail_pending_[e])
-      hsa_signal_wait_scacquire(tail_sig_[e], HSA_SIGNAL_CONDITION_EQ, 0, UINT64_MAX, HSA_WAIT_STATE_ACTIVE);
+    if (sdma_pending_[e]) bounded_wait(sdma_sig_[e], e, "egress D2H");
+    if (tail_pending_[e]) bounded_wait(tail_sig_[e], e, "egress tail D2H");
     sdma_pending_[e] = false;
     tail_pending_[e] = false;
   }
+
+  // a copy's completion signal reaching 0: an active spin first (a step's egress lands
+  // within its period; a blocked wait would add the interrupt wake-up to every delivery's
+  // latency), then blocked waits up to the engine's wait deadline -- past it the copy is
+  // declared lost: the slot's gate is opened (a gated copy that never saw its step's last
+  // kernel would otherwise hold its SDMA queue forever) and the engine reports an error
+  // (the front end's healthy() turns false, a sharded node fails over).  Was: an unbounded
+  // active wait, a core spinning forever on a lost gate
+  void bounded_wait(hsa_signal_t sig, int e, const char* what) {
+    if (hsa_signal_wait_scacquire(sig, HSA_SIGNAL_CONDITION_EQ, 0, spin_ticks_, HSA_WAIT_STATE_ACTIVE) == 0) return;
+    const auto t0 = std::chrono::steady_clock::now();
+    while (hsa_signal_wait_scacquire(sig, HSA_SIGNAL_CONDITION_EQ, 0, block_ticks_, HSA_WAIT_STATE_BLOCKED) != 0) {
+      if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(wait_ms_)) {
+        if (gate_sig_[e].handle) hsa_signal_store_screlease(gate_sig_[e], 0);
+        wait_failed_ = true;
+        throw std::runtime_error(std::string(what) + " of egress slot " + std::to_string(e) + " did not complete within " +
+                                 std::to_string(wait_ms_) + " ms (gate never opened / copy lost)");
+      }
+    }
+  }
+  // fault injection (tests): the next submitted step's egress gate is never opened by its
+  // last kernel (it stores to a scratch word instead), as after a step that died before it
+  void inject_gate_fault() { gate_fault_ = true; }
+  bool wait_failed() const { return wait_failed_; }
 
   // gated egress: bytes to copy speculatively for the next step -- the largest of the last
   // four steps' egress + 1/16 + 64 KB, in 64 KB units (0 after four steps without egress)
@@ -2255,6 +2318,14 @@ class Engine {
 
   // egress slot (host view "egress_host<slot>") of the step last submitted with parity p
   int egress_slot(int p) const { return slot_of_[p]; }
+  // egress by reference from the next submitted step on (StepIn.ref_back): bodies of the
+  // last `back` steps' ingress payloads (-1: off) of at least min_bytes are not rendered;
+  // the caller keeps those payloads unchanged until the delivering step's egress is sent
+  void set_egress_ref(int back, u32 min_bytes) {
+    if (back > 64) throw std::runtime_error("set_egress_ref: at most 64 steps back");
+    ref_back_ = back < 0 ? -1 : back;
+    ref_min_ = min_bytes < 16 ? 16 : min_bytes;
+  }
   // store-record slot (host views "persist<slot>" / "consumed<slot>") of that step
   int persist_slot(int p) const { return pslot_of_[p]; }
   const u8* pslot_host(int p) {
@@ -2277,6 +2348,12 @@ class Engine {
       return HSA_STATUS_SUCCESS;
     }, &ctx);
     if ((int)ctx.gpus.size() <= device_ || ctx.cpus.empty()) throw std::runtime_error("HSA agents not found");
+    {   // bounded_wait: spin 2 ms actively, then block in 1 ms slices
+      u64 f = 0;
+      if (hsa_system_get_info(HSA_SYSTEM_INFO_TIMESTAMP_FREQUENCY, &f) != HSA_STATUS_SUCCESS || !f) f = 100000000ull;
+      spin_ticks_ = f / 500;
+      block_ticks_ = f / 1000;
+    }
     gpu_agent_ = ctx.gpus[device_];
     cpu_agent_ = ctx.cpus[0];
     uint32_t mask = 0;
@@ -2348,7 +2425,7 @@ class Engine {
     F(n_dropped_nomem); F(n_expired); F(n_routed_msgs); F(n_unknown_exchange); F(n_ring_full);
     F(n_acked); F(log_head); F(log_tail); F(msg_free_top); F(n_live_msgs);
     F(n_persist); F(n_consumed); F(persist_used); F(n_persist_overflow);
-    F(live_bytes); F(n_grow); F(n_dget); F(spill_moved);
+    F(live_bytes); F(n_grow); F(n_dget); F(spill_moved); F(n_ref); F(gath_off); F(ref_bytes);
 #undef F
     std::vector<u32> lat(c.lat_hist, c.lat_hist + LAT_BINS);
     o["lat_hist"] = lat;
@@ -2590,6 +2667,8 @@ class Engine {
   std::map<std::string, Buf> bufs_;
   u64 total_bytes_ = 0;
   u64 egress_alloc_ = 0;
+  int ref_back_ = -1;    // egress by reference: steps back a body may be referenced (-1 off)
+  u32 ref_min_ = 256;    // smallest referenced body (smaller ones are cheaper inline)
   u32 ntiles_max_ = 0;
   u32 restore_max_ = 0;
   u64 carry_budget_ = 0;
@@ -2665,13 +2744,14 @@ class Engine {
   std::mutex dl_mu_;
   // open: a light control section is still staging into it (stage_begin .. stage_end); a
   // step never takes an open batch, so one section's change set rides one step whole
-  struct DlBatch { std::map<u64, std::string> w; std::vector<u32> dirty, unp; u64 bytes = 0; bool open = false; };
+  struct DlBatch { std::map<u64, std::string> w; std::vector<u32> dirty, unp; u64 bytes = 0; bool open = false; u64 id = 0; };
   std::vector<u32> unp_ready_;   // unpauses of batches flush_deltas applied (next step)
   u32 spill_req_[3] = {0, 0, 0};   // stage_spill for the next submitted step (dl_mu_)
   // staged writes with the unpauses staged after them; a batch that overflows one step's
   // delta buffer keeps its unpauses until its last write is packed
   std::deque<DlBatch> dl_;
   u32 dl_open_ = 0;   // light sections staging now (stage_begin / stage_end)
+  u64 dl_next_id_ = 1;   // id of the next batch (DlBatch.id)
   u64 dl_bytes_ = 0;
   u8* dl_h_[2] = {nullptr, nullptr};
   u32 dl_step_[2] = {0, 0};
@@ -2735,6 +2815,10 @@ class Engine {
   // whether a tail is in flight and the bytes copied speculatively for the slot's step
   bool gated_ = false;
   hsa_signal_t gate_sig_[EGRESS_SLOTS] = {};
+  u64 spin_ticks_ = 0, block_ticks_ = 0;   // bounded_wait: active spin / blocked slice (timestamp ticks)
+  u32 wait_ms_ = 10000;                    // bounded_wait deadline
+  bool wait_failed_ = false, gate_fault_ = false;
+  void* gate_dummy_ = nullptr;             // device word a faulted step's gate store lands in
   hsa_signal_t tail_sig_[EGRESS_SLOTS] = {};
   bool tail_pending_[EGRESS_SLOTS] = {};
   u64 spec_[EGRESS_SLOTS] = {};
@@ -2832,6 +2916,7 @@ PYBIND11_MODULE(_dataplane, m) {
       .def("egress_copy", &Engine::egress_copy)
       .def("egress_wait", &Engine::egress_wait)
       .def("egress_slot", &Engine::egress_slot)
+      .def("set_egress_ref", &Engine::set_egress_ref)
       .def("egress_wait_slot", &Engine::egress_wait_slot)
       .def("egress_done_slot", &Engine::egress_done_slot)
       .def("step_done", &Engine::step_done)
@@ -2856,9 +2941,12 @@ PYBIND11_MODULE(_dataplane, m) {
       .def("counters", &Engine::counters)
       .def("host_times", &Engine::host_times, py::arg("reset") = false)
       .def("egress_stats", &Engine::egress_stats)
+      .def("inject_gate_fault", &Engine::inject_gate_fault)
+      .def("wait_failed", &Engine::wait_failed)
       .def("stage_write", &Engine::stage_write_buf, py::arg("name"), py::arg("data"), py::arg("offset") = 0)
       .def("stage_mark_dirty", &Engine::stage_mark_dirty)
       .def("stage_begin", &Engine::stage_begin)
+      .def("dl_state", &Engine::dl_state)
       .def("stage_end", &Engine::stage_end)
       .def("stage_spill", &Engine::stage_spill)
       .def("deltas_pending", &Engine::deltas_pending)

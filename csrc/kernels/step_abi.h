@@ -79,6 +79,12 @@ struct Counters {       // per-step counters (device -> host)
   u32 n_grow;           // rings grown this step (grow_host list of RingMove)
   u32 n_dget;           // Basic.Gets decoded (and served or handed to the host) this step
   u64 spill_moved;      // body bytes this step moved to the host spill ring (StepIn.spill_*)
+  // egress by reference: deliveries rendered without their body bytes (0: no gather table),
+  // those bodies' bytes, and where the gather table (EgressRef[n_deliv]) starts in the
+  // step's egress.  egress_bytes = bytes to copy D2H (rendered bytes + table); the wire
+  // bytes are egress_bytes - table + ref_bytes
+  u32 n_ref, gath_off;
+  u64 ref_bytes;
 };
 
 struct CtrlRec { u32 conn; u32 off; u32 len; u32 seg; };
@@ -88,6 +94,12 @@ struct CtrlRec { u32 conn; u32 off; u32 len; u32 seg; };
 struct RingMove { u32 q, pad; u64 old_off, old_mask, new_off, new_mask, head, tail; };
 
 struct ConnOut { u32 off; u32 len; };
+// one gather entry per delivery of a step whose deliveries reference host bodies
+// (Counters.n_ref > 0): the `len` body bytes at host address `src` go at offset `dst` of the
+// step's rendered egress (before the byte there); len 0 = the delivery is rendered whole.
+// dst never decreases along the table (deliveries are in egress order)
+struct EgressRef { u64 src; u32 dst; u32 len; };
+static_assert(sizeof(EgressRef) == 16, "EgressRef layout");
 
 // Basic.Get served inside a step (k_dequeue, before the queue's consumers): the front end
 // stages up to GET_STEP_MAX requests with a submit; the device answers each in the step's
@@ -104,7 +116,7 @@ struct GetOut { u32 status; u32 msg_count; };
 // C entry points of one Engine (engine.hip: Engine::c_api).  All return 0 / a parity on
 // success and -1 on error (message: error()).  Parity p = the double-buffered step IO set
 // of a submitted step; its host-mapped outputs stay valid until the next submit of p.
-#define CMQ_STEP_ABI 7
+#define CMQ_STEP_ABI 8
 #define PSLOTS 4                // rotating host store-record slots (a step's records live PSLOTS - 1 more steps)
 #define UNPAUSE_STEP_MAX 1024   // connections unpaused per step (StepIn.nunp)
 struct CmqEngineApi {
@@ -162,5 +174,14 @@ struct CmqEngineApi {
   // control writes (or unpauses) staged for the next step: 1 = the stepper should step even
   // without client bytes (null: never)
   int (*host_work)(void* eng);
+  // egress by reference: deliveries of bodies from the ingress payload of the last `back`
+  // steps (0 = the same step; -1 = off), at least min_bytes long, are rendered without them
+  // (Counters.n_ref / EgressRef).  The caller keeps those payloads unchanged until the
+  // delivering step's egress is written out
+  int (*set_egress_ref)(void* eng, int back, u32 min_bytes);
+  // staged control-write batches (light control sections): which 0 = the id of the batch
+  // staging goes into now, 1 = the highest id every batch up to which a submitted step has
+  // taken (a reply tied to batch b may leave once the step that took b has finished)
+  u64 (*dl_state)(void* eng, int which);
 };
 #define GROW_MAX 4096   // grow requests reported per step

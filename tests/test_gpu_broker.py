@@ -947,18 +947,19 @@ def test_consume_ok_precedes_first_delivery_in_light_sections(gpu):
         th.start()
         time.sleep(0.2)
         light0, pauses0 = b.stats.get("light_sections", 0), b.stats.get("pauses", 0)
-        strict = conn(b, strict=True)
+        stricts = [conn(b, strict=True) for _ in range(3)]   # (chpc 8: channels per connection)
         for k, q in enumerate(names):
-            ch = strict.channel()
+            ch = stricts[k % 3].channel()
             ch.basic_consume(q, f"t{k}", no_ack=(k % 2 == 0))
             got = ch.consume_n(40, timeout=20)
             assert sorted(d.body for d in got) == sorted(f"{q}-{i}".encode() for i in range(40))
-        assert strict.violations == [], strict.violations[:3]
+        for sc in stricts:
+            assert sc.violations == [], sc.violations[:3]
         assert b.stats.get("light_sections", 0) - light0 >= len(names)
         assert b.stats.get("pauses", 0) == pauses0, b.stats.get("pause_why")
         stop.set()
         th.join(20)
-        for c_ in (s, sink, strict):
+        for c_ in [s, sink] + stricts:
             c_.close()
     finally:
         b.stop()

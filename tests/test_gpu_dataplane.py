@@ -142,3 +142,83 @@ def test_decode_windows_name_and_key_lengths(gpu):
             if cm is not None and cm.method is not None:
                 got.append(cm.method.routing_key)
         assert got == w, (c, w)
+
+
+def _deliveries(raw):
+    from chanamq_amd.protocol.codec import CommandAssembler, FrameParser
+    fp, ca = FrameParser(), CommandAssembler()
+    return [c for c in (ca.feed(f) for f in fp.feed(raw)) if c is not None and c.method.name == "basic.deliver"]
+
+
+def test_egress_by_reference_window(gpu):
+    """Egress by reference: deliveries of bodies that arrived in the same step are rendered
+    without them (Counters.n_ref; the D2H is the frames + gather table) and spliced back on
+    the host; a body whose ingress payload may have been recycled since (published earlier,
+    delivered from the backlog) is rendered from HBM.  Both byte-exact after the gather."""
+    from chanamq_amd.engine.dataplane import GpuDataPlane
+    from chanamq_amd.engine.traffic import publish_stream
+
+    d = GpuDataPlane(egress_ref=0, **CFG)
+    vh = "AMQ.DEFAULT"
+    d.declare_exchange(vh, "rx", "direct")
+    d.declare_queue(vh, "rq", capacity=1024)
+    d.bind(vh, "rq", "rx", "k")
+    for c in (0, 1):
+        d.open_connection(c, vh)
+        d.open_channel(c, 1)
+    # step 1: no consumer yet -- the bodies wait in HBM; the payload buffer is reused later
+    r = d.step({0: publish_stream(6, "rx", lambda i: "k", 704, seed=1)})
+    assert r.counters["n_deliv"] == 0
+    d.step({0: b""})
+    d.step({0: b""})   # (both payload buffers rewritten since step 1)
+    d.consume(1, 1, vh, "rq", "c", no_ack=True)
+    r = d.step({})
+    got = _deliveries(r.egress.get(1, b""))
+    assert len(got) == 6 and r.counters["n_ref"] == 0       # from HBM
+    stream = publish_stream(6, "rx", lambda i: "k", 704, seed=2)
+    r = d.step({0: stream})
+    got2 = _deliveries(r.egress.get(1, b""))
+    c = r.counters
+    assert len(got2) == 6 and c["n_ref"] == 6 and c["ref_bytes"] == 6 * 704
+    # the same step's bodies, byte-exact after the splice, and the D2H holds none of them
+    from chanamq_amd.protocol.codec import CommandAssembler, FrameParser
+    fp, ca = FrameParser(), CommandAssembler()
+    pubs = [x for x in (ca.feed(f) for f in fp.feed(stream)) if x is not None]
+    assert [g.body for g in got2] == [p.body for p in pubs]
+    assert c["egress_bytes"] - 16 * c["n_deliv"] + c["ref_bytes"] >= 6 * 704
+    assert c["egress_bytes"] < 6 * 704
+    # off: every body rendered into HBM egress again
+    d.eng.set_egress_ref(-1, 256)
+    r = d.step({0: publish_stream(3, "rx", lambda i: "k", 704, seed=3)})
+    assert r.counters["n_ref"] == 0 and len(_deliveries(r.egress.get(1, b""))) == 3
+
+
+def test_lost_egress_gate_fails_within_deadline(gpu):
+    """A gated egress copy whose gate is never opened (a step that died before its last
+    kernel) surfaces as an engine error within the wait deadline instead of a host thread
+    spinning forever; the engine still tears down."""
+    import time
+
+    from chanamq_amd.engine.dataplane import GpuDataPlane
+    from chanamq_amd.engine.traffic import publish_stream
+
+    d = GpuDataPlane(copy_engine=3, egress_gate=1, wait_timeout_ms=400, overlap=0, **CFG)
+    if not d.info.get("egress_gate"):
+        pytest.skip("engine built without gated egress")
+    vh = "AMQ.DEFAULT"
+    d.declare_exchange(vh, "gx", "fanout")
+    d.declare_queue(vh, "gq", capacity=4096)
+    d.bind(vh, "gq", "gx", "")
+    for c in (0, 1):
+        d.open_connection(c, vh)
+        d.open_channel(c, 1)
+    d.consume(1, 1, vh, "gq", "c", no_ack=True)
+    for k in range(6):   # egress history: the next steps' D2H is queued at launch, gated
+        assert d.step({0: publish_stream(20, "gx", lambda i: "", 512, seed=k)}).counters["n_deliv"] == 20
+    d.eng.inject_gate_fault()
+    t0 = time.monotonic()
+    with pytest.raises(RuntimeError, match="did not complete"):
+        d.step({0: publish_stream(20, "gx", lambda i: "", 512, seed=99)})
+    assert time.monotonic() - t0 < 5.0
+    assert d.eng.wait_failed()
+    del d
