@@ -158,7 +158,9 @@ def setup_native_exchange(args, cfg, GpuDataPlane, dist, backend, local, rank, w
 
     import torch
     dp, err = None, None
-    kind = "rccl" if backend == "nccl" else "shm"
+    # (CHANAMQ_BENCH_XCHG=rccl under gloo: the RCCL code path through CHANAMQ_RCCL_LIB, the
+    # tests' one-GPU stand-in -- a rehearsal, not a scaling number)
+    kind = os.environ.get("CHANAMQ_BENCH_XCHG") or ("rccl" if backend == "nccl" else "shm")
     try:
         dp = GpuDataPlane(device=local, worker=rank, world=world, rank=rank, native_xchg=1, **cfg)
         names = [None]
@@ -575,7 +577,11 @@ def main():
                 "seq_len": args.body,
                 "parallelism": (f"queue-sharded x{world}: one broker, cross-GPU routing by "
                                 + (("engine-native grouped RCCL send/recv over xGMI, counts via host shared memory"
-                                    if backend == "nccl" else "engine-native shared-memory exchange (host-staged)")
+                                    if backend == "nccl" else
+                                    "engine-native RCCL code path through the TEST STAND-IN library (one-GPU "
+                                    "rehearsal: shared memory + hipMemcpy, not xGMI; no scaling number)"
+                                    if dp.info.get("rccl_standin") else
+                                    "engine-native shared-memory exchange (host-staged)")
                                    if native else
                                    "RCCL all-to-all" if backend == "nccl" else f"{backend} all-to-all staged through the host")
                                 + (" (pipelined, +1 step for cross-GPU messages)" if args.exchange_lag else "")

@@ -126,6 +126,7 @@ class GpuDataPlane(ControlState):
             else:
                 self.eng.set_xfer_buffers(self._xs[0][0].data_ptr(), self._xs[0][1].data_ptr(),
                                           self._xr[0][0].data_ptr(), self._xr[0][1].data_ptr())
+        self._deleted_rings = {}
         super().__init__(c_max=i["c_max"], chpc=i["chpc"], q_max=i["q_max"], x_max=i["x_max"],
                          cons_max=i["cons_max"], hash_wildcard=hash_wildcard, ring_pool=i["ring_pool"],
                          default_queue_capacity=default_queue_capacity, world=world, rank=rank,
@@ -348,6 +349,13 @@ class GpuDataPlane(ControlState):
 
     def queue_deleted(self, q):
         self._up_at("q_active", 0, q.slot, np.uint32)
+        if self.defer:
+            # a light control section (steps running): no device read.  The host's view of
+            # the ring is current up to the ring moves it has seen (FE_GROW); a move still in
+            # flight reports the range it abandoned, which rings_moved then frees
+            self._deleted_rings[q.slot] = (q.ring_off, q.capacity)
+            self._sync_consumers()
+            return
         # if the device grew the ring since the host last looked, ControlState just freed the
         # abandoned range (free anyway); the live one goes back to the pool too
         off = self._u64("q_ring_off", q.slot)
@@ -837,17 +845,52 @@ class GpuDataPlane(ControlState):
         self._up_at("n_link_conns", len(conns), 0, np.uint32)
 
     # ---- unbounded queues: the device grows rings (k_ring_plan); the host mirrors it
+    _deleted_rings = None
+    _ring_chunk = (0, 0)
+
     def _ring_alloc(self, cap):
         """Rings come from one pool whose bump pointer lives on the device (k_ring_plan
-        allocates from it mid-step); ranges returned by deletes / growth are reused first."""
+        allocates from it mid-step); ranges returned by deletes / growth are reused first.
+        In a light control section (steps running, no device reads) a new ring comes from
+        the host's reserved chunk (``reserve_ring_chunk``)."""
         lst = self._ring_free.get(cap)
         if lst:
             return lst.pop()
+        off, left = self._ring_chunk
+        if left >= cap:
+            self._ring_chunk = (off + cap, left - cap)
+            return off
+        if self.defer:
+            raise ControlError(C.RESOURCE_ERROR, "ring chunk exhausted in a light section")
         top = self._u64("ring_top", 0)
         if top + cap > self.ring_pool:
             raise ControlError(C.RESOURCE_ERROR, "ring pool exhausted")
         self._up_at("ring_top", top + cap, 0, np.uint64)
         return top
+
+    def reserve_ring_chunk(self, entries):
+        """(Steps paused / between steps) take ``entries`` ring entries from the device's bump
+        pointer for queues declared in light sections (what is left of the last chunk goes
+        back to the free lists).  Returns the entries now reserved."""
+        off, left = self._ring_chunk
+        if left >= entries // 2:
+            return left
+        top = self._u64("ring_top", 0)
+        take = min(int(entries), self.ring_pool - top)
+        if take <= 0:
+            return left
+        self._up_at("ring_top", top + take, 0, np.uint64)
+        if left:   # (power-of-two pieces of the old remainder to the free lists)
+            while left:
+                k = 1 << (left.bit_length() - 1)
+                self._ring_free.setdefault(k, []).append(off)
+                off, left = off + k, left - k
+        self._ring_chunk = (top, take)
+        return take
+
+    def ring_light_ok(self, cap):
+        """A ring of ``cap`` entries can be allocated without a device read."""
+        return bool(self._ring_free.get(cap)) or self._ring_chunk[1] >= cap
 
     def _refresh_ring(self, q):
         """The device may have moved the queue's ring: adopt its current one and return the
@@ -861,6 +904,13 @@ class GpuDataPlane(ControlState):
     def rings_moved(self, raw):
         """RingMove records of a finished step (or the front end's FE_GROW event)."""
         for mv in np.frombuffer(raw, RING_MOVE):
+            dr = (self._deleted_rings or {}).get(int(mv["q"]))
+            if dr is not None and dr == (int(mv["old_off"]), int(mv["old_mask"]) + 1):
+                # the queue was deleted in a light section while this move was in flight: its
+                # old range went back with the delete, the new one goes now
+                del self._deleted_rings[int(mv["q"])]
+                self._ring_free.setdefault(int(mv["new_mask"]) + 1, []).append(int(mv["new_off"]))
+                continue
             q = self.queue_by_slot.get(int(mv["q"]))
             if q is not None and q.owner == self.rank and q.ring_off == int(mv["old_off"]):
                 self._ring_free.setdefault(q.capacity, []).append(q.ring_off)

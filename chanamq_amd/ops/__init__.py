@@ -71,9 +71,37 @@ def build_variant(path, defines):
     return path
 
 
+STANDIN_DIR = os.path.join(os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))),
+                           "tests", "rccl_standin")
+STANDIN_SO = os.path.join(STANDIN_DIR, "librccl_standin.so")
+
+
+def build_rccl_standin(verbose=False):
+    """The tests' shared-memory stand-in for librccl (tests/rccl_standin): lets several
+    ranks of the engine's RCCL exchange share one GPU.  Test-only (see ``load``)."""
+    src = os.path.join(STANDIN_DIR, "rccl_standin.cpp")
+    if not os.path.exists(src):
+        return None
+    if os.path.exists(STANDIN_SO) and os.path.getmtime(STANDIN_SO) >= os.path.getmtime(src):
+        return STANDIN_SO
+    hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+    cmd = [hipcc, "--offload-arch=gfx950", "-O2", "-std=c++17", "-shared", "-fPIC", src, "-o", STANDIN_SO + ".tmp",
+           "-lrt"]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    subprocess.run(cmd, check=True)
+    os.replace(STANDIN_SO + ".tmp", STANDIN_SO)
+    return STANDIN_SO
+
+
 def load():
     """Import the compiled extension, rebuilding it first if the sources changed
-    (raises ImportError with a build hint if it cannot be built)."""
+    (raises ImportError with a build hint if it cannot be built).  Refuses a librccl
+    override (CHANAMQ_RCCL_LIB: the tests' stand-in) unless CHANAMQ_RCCL_STANDIN_OK=1 says
+    this is a test or a labelled rehearsal."""
+    if os.environ.get("CHANAMQ_RCCL_LIB") and os.environ.get("CHANAMQ_RCCL_STANDIN_OK") != "1":
+        raise RuntimeError("CHANAMQ_RCCL_LIB names a librccl stand-in: test-only (set CHANAMQ_RCCL_STANDIN_OK=1 "
+                           "in tests / labelled rehearsals)")
     alt = os.environ.get("CHANAMQ_DP_SO")
     if alt:   # an A/B variant (build_variant)
         from importlib import util as ilu

@@ -107,6 +107,9 @@ class _PlaneLock:
                 self.b.plane.flush_deltas()
             if hasattr(self.b.fe, "flush_ctl"):          # and the replies held behind it written
                 self.b.fe.flush_ctl()
+            if hasattr(self.b.plane, "reserve_ring_chunk") and self.b.node is None:
+                # rings for queues declared in light sections (no device read there)
+                self.b.plane.reserve_ring_chunk(64 * self.b.plane.default_queue_capacity)
             if self.light:
                 # replies a light section produced but has not queued yet: written now,
                 # while paused (its staged writes were just applied; once the steps resume,
@@ -174,6 +177,10 @@ class _LightLock:
 # the steps keep running (their table writes ride the next step)
 _LIGHT_METHODS = {(10, 50), (10, 51), (20, 10), (20, 20), (20, 21), (20, 40), (20, 41), (30, 10), (60, 10),
                   (60, 20), (60, 30), (85, 10)}
+# single node only (a sharded node replicates them through the control log): topology
+# changes that only rewrite routing tables (staged whole, applied by one step's k_stage),
+# and the declare of a new queue whose ring comes from the host's reserved chunk
+_LIGHT_TOPOLOGY = {(40, 10), (40, 20), (50, 10), (50, 20), (50, 50)}
 
 
 class _ColdStopped(Exception):
@@ -329,6 +336,8 @@ class GpuBroker:
     def start(self):
         if self.io == "pipeline":
             from ..broker import load
+            if hasattr(self.plane, "reserve_ring_chunk") and self.node is None:
+                self.plane.reserve_ring_chunk(64 * self.plane.default_queue_capacity)
             self.fe = load().Frontend(self.plane.eng.c_api(), dict(
                 host=self.host, port=self.port, io_threads=self.io_threads, per_conn_read=self.per_conn_read,
                 idle_step_ms=self.idle_step_s * 1000.0, worker=self.plane.worker, max_slot=self._top_slot,
@@ -495,12 +504,54 @@ class GpuBroker:
 
     # ------------------------------------------------------------------ light control sections
     def _light_capable(self):
-        return (self.fe is not None and self.node is None and self.persistence is None
-                and hasattr(self.plane, "eng") and hasattr(self.fe, "send_after") and not self._links)
+        # (a store is no obstacle: the light commands write no store rows -- consumer sets are
+        # not persisted -- and their replies wait only for the held steps carrying bytes of
+        # their own connection, Frontend::release_ctl)
+        return (self.fe is not None and hasattr(self.plane, "eng") and hasattr(self.fe, "send_after")
+                and (self.node is None or getattr(self.plane, "native_xchg", False)))
 
     def _close_light(self, c):
-        """A connection whose close only releases connection / channel / consumer rows."""
-        return not any(q.exclusive_owner == c.id for q in self.plane.queues.values())
+        """A connection whose close only releases connection / channel / consumer rows --
+        and, on a single node, its exclusive queues (deleted without device reads,
+        GpuDataPlane.queue_deleted) -- with no remote-consumer link to close through the
+        control log."""
+        if any(k[0] == c.id for k in self._links):
+            return False
+        return self.node is None or not any(q.exclusive_owner == c.id for q in self.plane.queues.values())
+
+    def _topology_light(self, c, key, data):
+        """Exchange / queue / binding commands handled beside the steps (single node)."""
+        if self.node is not None or key not in _LIGHT_TOPOLOGY:
+            return False
+        if key != (50, 10):
+            return True
+        try:
+            m = decode_method(bytes(data[7:]))
+        except Exception:   # noqa: BLE001 - malformed: the full path reports it
+            return False
+        pc = self.plane.conns.get(c.id)
+        if m.passive or pc is None or (m.queue and (pc.vhost, m.queue) in self.plane.queues):
+            return False   # (an existing queue's DeclareOk needs its message count: a device read)
+        cap = 1
+        while cap < self.plane.default_queue_capacity:
+            cap <<= 1
+        return hasattr(self.plane, "ring_light_ok") and self.plane.ring_light_ok(cap)
+
+    def _consume_light(self, c, data):
+        """Basic.Consume / Cancel in a light section: on a sharded node only for a queue this
+        rank owns (a remote queue is a link through the control log) / a local consumer."""
+        if self.node is None:
+            return True
+        try:
+            m = decode_method(bytes(data[7:]))
+        except Exception:   # noqa: BLE001 - malformed: the full path reports it
+            return False
+        ch = struct.unpack_from(">H", data, 1)[0]
+        if m.name == "basic.cancel":
+            return (c.id, ch, m.consumer_tag) not in self._links
+        pc = self.plane.conns.get(c.id)
+        q = self.plane.queues.get((pc.vhost if pc else "", m.queue or c.last_queue.get(ch, "")))
+        return q is not None and q.owner == self.plane.rank
 
     def _plock(self):
         """The lock for a light-safe operation: light inside a light section, else full."""
@@ -541,10 +592,16 @@ class GpuBroker:
                 if ch in c.closing_channels:
                     continue
                 key = struct.unpack_from(">HH", data, 7)
+                if data[0] == C.FRAME_METHOD and key in _LIGHT_TOPOLOGY and self._topology_light(c, key, data):
+                    continue
                 if data[0] != C.FRAME_METHOD or key not in _LIGHT_METHODS:
                     return "method %d.%d" % key if data[0] == C.FRAME_METHOD else "content"
                 if key == (10, 50) and not self._close_light(c):
                     return "close with exclusive queues"
+                if key == (20, 40) and any(k[0] == c.id and k[1] == ch for k in self._links):
+                    return "channel close with remote consumers"
+                if key in ((60, 20), (60, 30)) and not self._consume_light(c, data):
+                    return "remote consumer"
             else:
                 return "event %d" % kind
         return None
@@ -723,11 +780,14 @@ class GpuBroker:
         pw = getattr(self, "_pw", None)
         if pw is not None and "store_failed" not in self.stats:
             ps = pw.stats()
-            if ps["failed"]:   # confirms stay held; fe.healthy() is False (a sharded node fails over)
+            if ps["failed"]:   # held confirms -> Nack, publishers blocked; fe.healthy() False (sharded: fail over)
                 self.stats["store_failed"] = ps["error"]
                 import logging
-                logging.getLogger("chanamq.gpu").error("persistent store failed, confirms are held from now on: %s",
-                                                       ps["error"])
+                logging.getLogger("chanamq.gpu").error("persistent store failed: unconfirmed publishes are nacked, "
+                                                       "publishers blocked: %s", ps["error"])
+                self._watermarks()
+        if st.get("store_fail_nacks"):
+            self.stats["store_fail_nacks"] = st["store_fail_nacks"]
 
     def _host_step(self, inputs):
         """A synchronous step run by the control plane while the front end is paused
@@ -1520,7 +1580,8 @@ class GpuBroker:
                 self.persistence.queue(p.queue_by_slot[slot])
             if not m.nowait:
                 qq = p.queue_by_slot[slot]
-                self._send(c, ch, Method("queue.declare_ok", queue=name, message_count=p.message_count(slot),
+                cnt = 0 if q is None else p.message_count(slot)   # (a new queue: no device read)
+                self._send(c, ch, Method("queue.declare_ok", queue=name, message_count=cnt,
                                          consumer_count=len(qq.consumers)))
         elif n == "queue.bind":
             qn = m.queue or c.last_queue.get(ch, "")
@@ -1957,6 +2018,15 @@ class GpuBroker:
                 self._flush(c)
 
     def _watermarks(self):
+        # a failed store never accepts another persistent publish: publishers are blocked for
+        # good (Connection.Blocked / Channel.Flow off) and the front end turns every confirm it
+        # still held into Basic.Nack (frontend.cpp collect_scatter); /admin/stats reports it
+        if "store_failed" in self.stats:
+            if not self.blocked:
+                self.blocked = True
+                self.stats["flow_off"] = self.stats.get("flow_off", 0) + 1
+                self._set_flow(False)
+            return
         if self.spill_at:
             self._maybe_spill()
         if self.cold is not None and getattr(self, "_cold_thread", None) is None:
@@ -2101,7 +2171,8 @@ class GpuBroker:
                 if active:
                     self._send(c, 0, Method("connection.unblocked"))
                 else:
-                    self._send(c, 0, Method("connection.blocked", reason="low on memory"))
+                    self._send(c, 0, Method("connection.blocked", reason="persistent store failed"
+                                            if "store_failed" in self.stats else "low on memory"))
             else:
                 pc = self.plane.conns.get(c.id)
                 for ch in (list(pc.channels) if pc else []):

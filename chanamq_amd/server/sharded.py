@@ -66,6 +66,9 @@ def main(argv=None):
     ap.add_argument("--no-fsync", action="store_true")
     ap.add_argument("--backend", default="", help="default: nccl (RCCL) for --plane gpu, gloo for golden; "
                                                   "gloo + gpu rehearses several ranks on one GPU")
+    ap.add_argument("--xchg", choices=["auto", "rccl", "shm"], default="auto",
+                    help="pipeline: the engine's exchange backend (auto: rccl with --backend nccl, else shm); rccl "
+                         "under gloo runs the RCCL code path through CHANAMQ_RCCL_LIB (the tests' stand-in)")
     ap.add_argument("--async-x", type=int, default=0,
                     help="1: each step's exchange on the engine's exchange thread (phase B waits on the device)")
     ap.add_argument("--xchg-timeout-ms", type=int, default=15000,
@@ -112,7 +115,7 @@ def main(argv=None):
     comm = Comm(store=store, backend="gloo" if pipeline else backend, timeout_s=60, wait_s=20)
     node = ShardedNode(plane, comm, membership=Membership(store, rank, world, timeout_s=args.hb_timeout_s))
     if pipeline:
-        xkind = "rccl" if backend == "nccl" else "shm"
+        xkind = args.xchg if args.xchg != "auto" else ("rccl" if backend == "nccl" else "shm")
         shm_base = "cmq-x-" + os.environ.get(ENV_STORE, "local").replace(":", "-").replace(".", "-")
 
         def rebuild_xchg(live, epoch):

@@ -78,6 +78,7 @@ PYBIND11_MODULE(_core, m) {
       .def("sync", &Store::sync, py::call_guard<py::gil_scoped_release>())
       .def("compact", &Store::compact, py::call_guard<py::gil_scoped_release>())
       .def("set_auto_compact", &Store::set_auto_compact, py::arg("ratio"), py::arg("min_bytes"))
+      .def("set_quota", &Store::set_quota, py::arg("bytes"))
       .def("wait_compaction", &Store::wait_compaction, py::call_guard<py::gil_scoped_release>())
       .def("wal_bytes", &Store::walBytes)
       .def("live_estimate", &Store::liveEstimate)
@@ -291,6 +292,7 @@ PYBIND11_MODULE(_core, m) {
              o["steps"] = s.steps; o["published"] = s.published; o["delivered"] = s.delivered;
              o["spill_moved"] = s.spill_moved;
              o["rx_bytes"] = s.rx_bytes; o["tx_bytes"] = s.tx_bytes; o["egress_bytes"] = s.egress_bytes;
+             o["store_fail_nacks"] = s.store_fail_nacks;
              o["held_steps"] = s.held_steps; o["idle_steps"] = s.idle_steps; o["gather_segs"] = s.gather_segs;
              o["live_bytes"] = s.live_bytes; o["live_msgs"] = s.live_msgs; o["io_phase_s"] = s.io_phase_s;
              o["dropped_nomem"] = s.dropped_nomem; o["ring_full"] = s.ring_full; o["unroutable"] = s.unroutable;

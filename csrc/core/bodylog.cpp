@@ -114,6 +114,11 @@ void BodyLog::put(const char* const* recs, const uint32_t* lens, size_t n, Loc* 
   uint64_t total = 0;
   for (size_t i = 0; i < n; ++i) total += FRAME + lens[i];
   std::lock_guard<std::mutex> g(mu_);
+  if (q_lim_ && (!err_.empty() || q_used_->fetch_add(total) + total > q_lim_)) {
+    if (err_.empty()) err_ = "body log write: No space left on device (store quota of " + std::to_string(q_lim_) + " bytes)";
+    for (size_t i = 0; i < n; ++i) out[i] = Loc{};
+    return;
+  }
   start_locked();
   // contiguous chunks of about equal bytes, one per stripe (small groups use fewer)
   const int k = (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)nstripes_, total / (256u << 10)));

@@ -13,6 +13,7 @@
 // insertMessage), which spreads the writes over its memtables / commitlog; here the
 // spreading is the stripes, and a segment file is unlinked once no live row refers to it.
 #pragma once
+#include <atomic>
 #include <condition_variable>
 #include <cstdint>
 #include <deque>
@@ -39,6 +40,9 @@ class BodyLog {
   BodyLog(std::string dir, bool fsync);
   ~BodyLog();
   void configure(int stripes, uint64_t seg_bytes);
+  // a byte budget shared with the WAL (Store::set_quota): a put() past it fails like a full
+  // disk (the sticky error wait() reports), nothing of it is written
+  void set_quota(std::atomic<uint64_t>* used, uint64_t limit) { q_used_ = used; q_lim_ = limit; }
   // place n records (locations returned now) and start writing them; the pointers must stay
   // valid until wait() returns
   void put(const char* const* recs, const uint32_t* lens, size_t n, Loc* out);
@@ -80,6 +84,8 @@ class BodyLog {
   bool started_ = false, stop_ = false;
   uint64_t pending_ = 0;
   std::string err_;
+  std::atomic<uint64_t>* q_used_ = nullptr;
+  uint64_t q_lim_ = 0;
   int rr_ = 0;
   uint32_t next_seg_ = 1;
   std::mutex amu_;                       // segment accounting, read fds

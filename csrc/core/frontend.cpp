@@ -452,12 +452,22 @@ void Frontend::release_ctl() {
   std::vector<CtlOut> go;
   {
     std::lock_guard<std::mutex> g(ctl_mu_);
-    // the egress queued so far covers steps <= out_step_ and write batches <= out_batch_;
-    // held (write-behind) steps not yet released keep every reply behind them
-    while (!ctl_out_.empty() && ctl_out_.front().after <= out_step_ && ctl_out_.front().batch <= out_batch_ &&
-           held_.empty()) {
-      go.push_back(std::move(ctl_out_.front()));
-      ctl_out_.pop_front();
+    // the egress queued so far covers steps <= out_step_ and write batches <= out_batch_; a
+    // connection with bytes in held (write-behind) steps keeps its replies behind them --
+    // per connection, so a durable broker whose steps are nearly always held still answers
+    // the other connections' control commands (replies keep their order per connection)
+    std::vector<u32> blocked;
+    for (auto it = ctl_out_.begin(); it != ctl_out_.end();) {
+      const u32 c = it->conn;
+      const bool ok = it->after <= out_step_ && it->batch <= out_batch_ && (c >= c_max_ || held_cnt_[c] == 0) &&
+                      std::find(blocked.begin(), blocked.end(), c) == blocked.end();
+      if (!ok) {
+        blocked.push_back(c);
+        ++it;
+        continue;
+      }
+      go.push_back(std::move(*it));
+      it = ctl_out_.erase(it);
     }
   }
   if (go.empty()) return;
@@ -1726,11 +1736,41 @@ bool Frontend::stash_pend(bool copy) {
   return true;
 }
 
+u64 Frontend::nack_confirms(Scatter& sc) {
+  if (sc.own.empty()) return 0;
+  u8* b = (u8*)&sc.own[0];
+  u64 n = 0;
+  for (auto& o : sc.co) {
+    u64 p = o.off;
+    const u64 end = (u64)o.off + o.len;
+    while (p + 8 <= end) {
+      const u32 size = ((u32)b[p + 3] << 24) | ((u32)b[p + 4] << 16) | ((u32)b[p + 5] << 8) | b[p + 6];
+      if (p + 8 + size > end) break;
+      // a method frame Basic.Ack (60/80, 13 argument bytes): only publisher confirms
+      if (b[p] == 1 && size == 13 && b[p + 7] == 0 && b[p + 8] == 60 && b[p + 9] == 0 && b[p + 10] == 80) {
+        b[p + 10] = 120;
+        b[p + 19] &= 1;   // multiple kept, requeue 0
+        ++n;
+      }
+      p += 8 + size;
+    }
+  }
+  return n;
+}
+
 bool Frontend::collect_scatter(std::vector<Scatter*>& scat) {
   if (!stash_pend(false)) return false;
   const u64 rel = released_.load();
-  while (!held_.empty() && (!held_.front().needs_commit || held_.front().step <= rel)) {
+  // a failed store never commits again: the held steps it did not commit go out now, their
+  // confirms as Basic.Nack (they were held forever)
+  const bool pfail = persist_ && persist_->failed();
+  while (!held_.empty() && (pfail || !held_.front().needs_commit || held_.front().step <= rel)) {
     Scatter& sc = held_.front().sc;
+    if (pfail && held_.front().needs_commit && held_.front().step > rel) {
+      const u64 k = nack_confirms(sc);
+      std::lock_guard<std::mutex> g(stats_mu_);
+      stats_.store_fail_nacks += k;
+    }
     for (u32 c = 0; c < c_max_; ++c)
       if (sc.co[c].len) { --held_cnt_[c]; --held_total_; }
     out_.push_back(std::move(sc));
@@ -1742,7 +1782,8 @@ bool Frontend::collect_scatter(std::vector<Scatter*>& scat) {
 }
 
 bool Frontend::releasable() const {
-  return !held_.empty() && (!held_.front().needs_commit || held_.front().step <= released_.load());
+  return !held_.empty() && (!held_.front().needs_commit || held_.front().step <= released_.load() ||
+                            (persist_ && persist_->failed()));
 }
 
 bool Frontend::any_data_conn() const {

@@ -102,6 +102,7 @@ struct FeStats {
   u64 steps = 0, published = 0, delivered = 0, rx_bytes = 0, tx_bytes = 0, egress_bytes = 0;
   u64 spill_moved = 0;   // body bytes moved to the host spill ring by steps (StepIn.spill_*)
   u64 held_steps = 0, idle_steps = 0, gather_segs = 0;
+  u64 store_fail_nacks = 0;   // publisher confirms turned into Basic.Nack: their store commit failed
   u64 dropped_nomem = 0, ring_full = 0, unroutable = 0, routed = 0, expired = 0, ctrl = 0;
   i64 live_bytes = 0;
   u64 live_msgs = 0;
@@ -234,6 +235,10 @@ class Frontend {
   // the scatter's wire bytes into sc.own (its egress slot / arena may be reused before it
   // is written): bodies spliced in, offsets rewritten
   static void materialize(Scatter& sc, const u8* egress, u64 bytes);
+  // the store failed: every publisher confirm (Basic.Ack) in a held step's egress becomes a
+  // Basic.Nack -- same frame size, method 80 -> 120, requeue 0 -- so no publish whose rows
+  // never reached the disk is acknowledged; returns the frames changed
+  static u64 nack_confirms(Scatter& sc);
   void gather_conn(FeIo& io, FeConn& c, u8* arena, u64 cap);
   bool check(int rc);
 

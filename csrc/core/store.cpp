@@ -212,6 +212,7 @@ void Store::open(const std::string& dir, bool fsync_enabled) {
   fd_ = ::open(path_.c_str(), O_RDWR | O_CREAT | O_APPEND, 0644);
   if (fd_ < 0) throw std::runtime_error("store: cannot open " + path_);
   body_.reset(new BodyLog(dir + "/bodies", fsync_enabled));
+  if (quota_) body_->set_quota(&quota_used_, quota_);
   replay();
   body_->open_existing();
 }
@@ -235,7 +236,17 @@ void Store::close() {
   if (body_) body_->close();
 }
 
+void Store::set_quota(uint64_t bytes) {
+  std::lock_guard<std::recursive_mutex> g(mu_);
+  quota_ = bytes;
+  quota_used_ = wal_bytes_;
+  if (body_) body_->set_quota(&quota_used_, bytes);
+}
+
 void Store::write_all(const std::string& rec) {
+  if (quota_ && quota_used_.fetch_add(rec.size()) + rec.size() > quota_)
+    throw std::runtime_error("store: WAL write failed: No space left on device (store quota of " +
+                             std::to_string(quota_) + " bytes)");
   write_fd(fd_, rec.data(), rec.size());
   wal_bytes_ += rec.size();
 }

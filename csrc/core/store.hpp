@@ -107,6 +107,10 @@ class Store {
   void compact();          // rewrite the WAL from live rows now (waits for it)
   // background compaction policy: WAL > ratio x live estimate and > min_bytes (ratio 0 = off)
   void set_auto_compact(double ratio, uint64_t min_bytes) { auto_ratio_ = ratio; auto_min_ = min_bytes; }
+  // a byte budget for the store on disk (WAL appends + body log), 0 = none: writes past it
+  // fail like a full disk (ENOSPC), which the write-behind reports as a store failure --
+  // operators cap a store this way; tests use it to fill a store deterministically
+  void set_quota(uint64_t bytes);
   void wait_compaction();
   CompactStats compactStats();
   uint64_t liveEstimate();
@@ -201,6 +205,8 @@ class Store {
   bool dirty_ = false;
   bool replaying_ = false;
   uint64_t wal_bytes_ = 0;
+  uint64_t quota_ = 0;
+  std::atomic<uint64_t> quota_used_{0};
 
   std::unique_ptr<BodyLog> body_;     // with a store on disk
   std::map<int64_t, MsgRow> msgs_;

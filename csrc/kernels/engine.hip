@@ -793,6 +793,7 @@ class Engine {
     o["carry_budget"] = carry_budget_;
     o["exchange_lag"] = lag_ ? 1 : 0;
     o["native_xchg"] = native_x_ ? 1 : 0;
+    o["rccl_standin"] = (rccl_ && cmqx::RcclLib::get().standin) ? 1 : 0;   // (tests/rccl_standin: not RCCL)
     o["links"] = links_ ? 1 : 0;
     o["import_bytes"] = d_.import_bytes;
     o["world"] = d_.world; o["rank"] = d_.my_rank; o["import_max"] = d_.import_max; o["pub_cap"] = d_.pub_cap;

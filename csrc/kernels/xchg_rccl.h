@@ -36,6 +36,7 @@ struct RcclLib {
   ncclResult_t (*CommDestroy)(ncclComm_t) = nullptr;
   ncclResult_t (*CommGetAsyncError)(ncclComm_t, ncclResult_t*) = nullptr;
   const char* (*GetErrorString)(ncclResult_t) = nullptr;
+  bool standin = false;   // the test-only stand-in (tests/rccl_standin), not RCCL
 
   static RcclLib& get() {
     static RcclLib lib;
@@ -48,10 +49,20 @@ struct RcclLib {
     if (!f) throw std::runtime_error(std::string("librccl: missing symbol ") + n);
   }
   void open() {
-    const char* names[] = {"librccl.so.1", "librccl.so", "/opt/rocm/lib/librccl.so"};
-    for (const char* n : names)
-      if ((h = dlopen(n, RTLD_NOW | RTLD_GLOBAL))) break;
+    // CHANAMQ_RCCL_LIB: another library with the same entry points first -- the tests'
+    // shared-memory stand-in that lets several ranks share one GPU (RCCL refuses that).
+    // chanamq_amd.ops.load() refuses the override unless CHANAMQ_RCCL_STANDIN_OK=1
+    const char* over = getenv("CHANAMQ_RCCL_LIB");
+    if (over && *over) {
+      if (!(h = dlopen(over, RTLD_NOW | RTLD_LOCAL)))
+        throw std::runtime_error(std::string("CHANAMQ_RCCL_LIB: dlopen failed: ") + dlerror());
+    } else {
+      const char* names[] = {"librccl.so.1", "librccl.so", "/opt/rocm/lib/librccl.so"};
+      for (const char* n : names)
+        if ((h = dlopen(n, RTLD_NOW | RTLD_GLOBAL))) break;
+    }
     if (!h) throw std::runtime_error("librccl not found (dlopen)");
+    standin = dlsym(h, "cmq_rccl_standin") != nullptr;
     sym(GetUniqueId, "ncclGetUniqueId");
     sym(CommInitRank, "ncclCommInitRank");
     sym(Send, "ncclSend");
@@ -123,12 +134,13 @@ class RcclXchg {
     if (hipMemcpyAsync(dh_send_, hs, row * n, hipMemcpyHostToDevice, s_) != hipSuccess) return -1;
     RcclLib& L = RcclLib::get();
     if (L.GroupStart()) return -1;
+    int bad = 0;   // a failed enqueue inside the group: the group still ends, then fails
     for (int i = 0; i < n; ++i) {
       if (i == idx_) continue;
-      L.Send((const char*)dh_send_ + row * i, row, nccl_int8, i, comm_, s_);
-      L.Recv((char*)dh_recv_ + row * i, row, nccl_int8, i, comm_, s_);
+      bad |= L.Send((const char*)dh_send_ + row * i, row, nccl_int8, i, comm_, s_) != 0;
+      bad |= L.Recv((char*)dh_recv_ + row * i, row, nccl_int8, i, comm_, s_) != 0;
     }
-    if (L.GroupEnd()) return -2;
+    if (L.GroupEnd() || bad) { abort(); return -2; }
     if (hipMemcpyAsync(hr, dh_recv_, row * n, hipMemcpyDeviceToHost, s_) != hipSuccess) return -1;
     if (hipEventRecord(ev_, s_) != hipSuccess) return -1;
     int rc = wait(ev_);
@@ -144,14 +156,15 @@ class RcclXchg {
     RcclLib& L = RcclLib::get();
     if (L.GroupStart()) return -1;
     const int n = (int)members_.size();
+    int bad = 0;
     for (int i = 0; i < n; ++i) {
       if (i == idx_) continue;
       for (const XPart& p : sends[i])
-        if (p.bytes) L.Send(p.ptr, p.bytes, nccl_int8, i, comm_, s_);
+        if (p.bytes) bad |= L.Send(p.ptr, p.bytes, nccl_int8, i, comm_, s_) != 0;
       for (const XPart& p : recvs[i])
-        if (p.bytes) L.Recv(p.ptr, p.bytes, nccl_int8, i, comm_, s_);
+        if (p.bytes) bad |= L.Recv(p.ptr, p.bytes, nccl_int8, i, comm_, s_) != 0;
     }
-    if (L.GroupEnd()) return -2;
+    if (L.GroupEnd() || bad) { abort(); return -2; }
     if (hipEventRecord(ev_, s_) != hipSuccess) return -1;
     return 0;
   }

@@ -963,3 +963,67 @@ def test_consume_ok_precedes_first_delivery_in_light_sections(gpu):
             c_.close()
     finally:
         b.stop()
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(180)
+def test_store_failure_nacks_unconfirmed_publishes(gpu, tmp_path):
+    """Config 4 into a store that fills up (a store quota: its writes then fail like a full
+    disk): the write-behind reports the failure, every publish whose rows did not reach the
+    disk gets Basic.Nack within about a second (they were held forever before), publishers
+    are blocked, /admin/stats names the failure -- and every acked message is in the store."""
+    import json
+    import time
+
+    from chanamq_amd.broker import load
+    from chanamq_amd.server.gpu_broker import GpuBroker
+    core = load()
+    path = str(tmp_path / "store")
+    st = core.Store()
+    st.open(path, True)
+    st.set_quota(3 << 20)
+    b = GpuBroker(make_persist_plane("gpu"), idle_step_ms=1.0, ingress_bytes=8 << 20, store=st, io="pipeline").start()
+    try:
+        p = conn(b)
+        ch = p.channel()
+        ch.queue_declare("sq", durable=True)
+        ch.confirm_select()
+        body = b"s" * 4096
+        sent, t_fail = 0, None
+        while sent < 6000 and ch.flow_active and not p.blocked:
+            for _ in range(25):
+                ch.basic_publish("", "sq", body, {"delivery_mode": 2})
+                sent += 1
+            p.process(0.002)
+            if t_fail is None and "store_failed" in b.stats:
+                t_fail = time.monotonic()
+        end = time.monotonic() + 20
+        fate = {}
+
+        def resolve():
+            while ch.confirms:
+                tag, multiple, ack = ch.confirms.popleft()
+                for t in (range(1, tag + 1) if multiple else (tag,)):
+                    fate.setdefault(t, ack)
+            return len(fate) >= sent
+        while not resolve() and time.monotonic() < end:
+            p.process(0.01)
+        t_done = time.monotonic()
+        if t_fail is None:
+            t_fail = t_done
+        assert "store_failed" in b.stats, b.stats
+        assert len(fate) >= sent, (len(fate), sent)
+        acked = sorted(t for t in range(1, sent + 1) if fate[t])
+        nacked = [t for t in range(1, sent + 1) if not fate[t]]
+        assert nacked and acked, (len(acked), len(nacked))
+        assert t_done - t_fail < 2.0, t_done - t_fail    # (stats are polled every 50 ms)
+        assert b.stats.get("store_fail_nacks", 0) > 0 and b.blocked
+        assert "No space left" in json.loads(b.stats_json())["store_failed"]
+        p.close()
+    finally:
+        b.stop()
+        st.close()
+    st2 = core.Store()
+    st2.open(path, True)   # every acked message is on disk
+    assert st2.row_count("msgs") >= len(acked), (st2.row_count("msgs"), len(acked))
+    st2.close()

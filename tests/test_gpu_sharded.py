@@ -124,3 +124,91 @@ def test_rccl_single_rank_paths(gpu):
     p = subprocess.run([sys.executable, os.path.join(HERE, "rccl_single_worker.py")], env=env,
                        capture_output=True, text=True, timeout=170)
     assert p.returncode == 0 and "RCCL ok" in p.stdout, (p.returncode, p.stdout[-2000:], p.stderr[-3000:])
+
+
+def _standin_env():
+    from chanamq_amd import ops
+    so = ops.build_rccl_standin()
+    assert so and os.path.exists(so), "tests/rccl_standin/librccl_standin.so not built"
+    return {"CHANAMQ_RCCL_LIB": so, "CHANAMQ_RCCL_STANDIN_OK": "1"}
+
+
+def _native_procs(spec_name, world, kind, steps, extra=()):
+    with tempfile.TemporaryDirectory() as d:
+        env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()), WORLD_SIZE=str(world),
+                   PYTHONPATH=os.pathsep.join([os.path.dirname(HERE), HERE]), **_standin_env())
+        procs = [subprocess.Popen([sys.executable, os.path.join(HERE, "native_xchg_worker.py"), spec_name, d, kind]
+                                  + list(extra), env=dict(env, RANK=str(r))) for r in range(world)]
+        for p in procs:
+            assert p.wait(timeout=300) == 0
+        got = [dict() for _ in range(steps)]
+        for r in range(world):
+            with open(os.path.join(d, f"rank{r}.json")) as f:
+                for k, eg in enumerate(json.load(f)):
+                    for c, hx in eg.items():
+                        got[k][int(c)] = bytes.fromhex(hx)
+    return got
+
+
+@pytest.mark.timeout(400)
+@pytest.mark.parametrize("world,name,extra", [(2, "topic", ()), (2, "fanout_confirm", ("counts_shm",)),
+                                              (3, "direct_manual_ack", ()), (4, "fanout_confirm", ())])
+def test_engine_rccl_exchange_multi_rank_matches_golden(gpu, world, name, extra):
+    """The engine's RCCL exchange (xchg_rccl.h RcclXchg: count exchange and bulk as grouped
+    ncclSend / ncclRecv, bounded event waits) with 2-4 ranks, one process each, all on the
+    one test GPU through the tests' librccl stand-in (real RCCL refuses two ranks on one
+    device): byte-identical to the golden cluster with the pipelined exchange."""
+    want = run_cluster_lag(SHARDED[name](), world, extra_steps=2)
+    got = _native_procs(name, world, "rccl", len(want), extra)
+    for k, (a, b) in enumerate(zip(want, got)):
+        assert set(a) == set(b), (k, sorted(a), sorted(b))
+        for c in a:
+            assert a[c] == b[c], (k, c)
+
+
+_MISMATCH = r'''
+import ctypes, os, sys
+L = ctypes.CDLL(os.environ["CHANAMQ_RCCL_LIB"])
+rank, uid_hex = int(sys.argv[1]), sys.argv[2]
+class Uid(ctypes.Structure):
+    _fields_ = [("internal", ctypes.c_char * 128)]
+uid = Uid.from_buffer_copy(bytes.fromhex(uid_hex))
+comm = ctypes.c_void_p()
+assert L.ncclCommInitRank(ctypes.byref(comm), 2, uid, rank) == 0
+bufs = [ctypes.create_string_buffer(512) for _ in range(4)]
+def group(ops):
+    L.ncclGroupStart()
+    bad = 0
+    for send, i, n in ops:
+        f = L.ncclSend if send else L.ncclRecv
+        bad |= f(bufs[i], ctypes.c_size_t(n), 0, 1 - rank, comm, None)
+    return L.ncclGroupEnd() or bad
+ctypes.memmove(bufs[0], b"x" * 100, 100)
+# a matched group first: both sides agree
+r1 = group([(True, 0, 100), (False, 1, 100)])
+# then the receiver posts its second part one byte longer than the sender sent
+r2 = group([(True, 0, 100), (True, 2, 200)] if rank == 0 else [(False, 1, 100), (False, 3, 201)])
+print("RESULT", rank, r1, r2, flush=True)
+L.ncclCommDestroy(comm)
+'''
+
+
+@pytest.mark.timeout(120)
+def test_rccl_standin_fails_loudly_on_mismatched_parts(gpu):
+    """The stand-in is stricter than NCCL: a peer's group whose part sizes differ from the
+    receives this rank posted fails the group (ncclInvalidUsage) and aborts the
+    communicator, so an exchange whose two sides disagree cannot pass a test."""
+    env = dict(os.environ, **_standin_env())
+    uid = (b"CMQSTND\0" + f"/cmq-rccl-standin-mm-{os.getpid()}".encode()).ljust(128, b"\0").hex()
+    procs = [subprocess.Popen([sys.executable, "-c", _MISMATCH, str(r), uid], env=env, stdout=subprocess.PIPE,
+                              stderr=subprocess.PIPE, text=True) for r in range(2)]
+    outs = [p.communicate(timeout=100) for p in procs]
+    res = {}
+    for out, err in outs:
+        for line in out.splitlines():
+            if line.startswith("RESULT"):
+                _, r, r1, r2 = line.split()
+                res[int(r)] = (int(r1), int(r2))
+    assert res.get(0, (None,))[0] == 0 and res.get(1, (None,))[0] == 0, (res, outs)
+    assert res[1][1] == 5, (res, outs)            # ncclInvalidUsage on the receiving side
+    assert "mismatch" in outs[1][1], outs[1][1][-500:]

@@ -18,12 +18,23 @@ pytestmark = pytest.mark.gpu
 HERE = os.path.dirname(os.path.abspath(__file__))
 
 
-@pytest.fixture
-def cluster(tmp_path):
-    from chanamq_amd.parallel.launch import Launcher
+def _xchg_env(xchg):
+    """--xchg rccl: the engine's RCCL exchange through the tests' librccl stand-in (RCCL
+    itself refuses several ranks on one GPU)."""
     env = dict(os.environ, PYTHONPATH=os.path.dirname(HERE))
+    if xchg == "rccl":
+        from chanamq_amd import ops
+        env.update(CHANAMQ_RCCL_LIB=ops.build_rccl_standin(), CHANAMQ_RCCL_STANDIN_OK="1")
+    return env
+
+
+@pytest.fixture
+def cluster(tmp_path, request):
+    from chanamq_amd.parallel.launch import Launcher
+    xchg = getattr(request, "param", "shm")
+    env = _xchg_env(xchg)
     ln = Launcher(2, ["-m", "chanamq_amd.server.sharded", "--config", SMALL_CONF, "--plane", "gpu", "--port", "0", "--backend", "gloo",
-                      "--info-dir", str(tmp_path), "--xchg-timeout-ms", "20000"], env=env).start()
+                      "--info-dir", str(tmp_path), "--xchg-timeout-ms", "20000", "--xchg", xchg], env=env).start()
     deadline = time.time() + 180
     while time.time() < deadline and not all((tmp_path / f"rank{r}.json").exists() for r in range(2)):
         assert not ln.poll(), f"rank exited early: {ln.poll()}"
@@ -37,6 +48,7 @@ def cluster(tmp_path):
 
 
 @pytest.mark.timeout(300)
+@pytest.mark.parametrize("cluster", ["shm", "rccl"], indirect=True)
 def test_pipelined_cross_rank_routing_and_topology(cluster):
     ports, ln = cluster
     c0 = Connection(port=ports[0], vhost="/")
@@ -179,7 +191,8 @@ def test_pipelined_transactions_and_durable_topology(cluster):
 
 
 @pytest.mark.timeout(400)
-def test_pipelined_rank_death_durable_redelivery(tmp_path):
+@pytest.mark.parametrize("xchg", ["shm", "rccl"])
+def test_pipelined_rank_death_durable_redelivery(tmp_path, xchg):
     """HA on GPU planes: 3 pipelined ranks on the one GPU.  A client on rank 2 declares a
     durable queue there, publishes persistent messages with confirms and holds 5 of them
     unacked; rank 2 is killed.  The survivors' next exchange times out (bounded wait),
@@ -188,10 +201,10 @@ def test_pipelined_rank_death_durable_redelivery(tmp_path):
     back, the 5 it held flagged redelivered (README.md:50, QueueEntity.scala:107-135)."""
     from chanamq_amd.client import ChannelClosed
     from chanamq_amd.parallel.launch import Launcher
-    env = dict(os.environ, PYTHONPATH=os.path.dirname(HERE))
+    env = _xchg_env(xchg)   # rccl: the survivors rebuild the communicator (CommAbort, new uid, CommInitRank)
     ln = Launcher(3, ["-m", "chanamq_amd.server.sharded", "--config", SMALL_CONF, "--plane", "gpu", "--port", "0", "--backend", "gloo",
                       "--info-dir", str(tmp_path), "--store-dir", str(tmp_path / "store"), "--no-fsync",
-                      "--xchg-timeout-ms", "4000", "--hb-timeout-s", "2"], env=env).start()
+                      "--xchg-timeout-ms", "4000", "--hb-timeout-s", "2", "--xchg", xchg], env=env).start()
     try:
         deadline = time.time() + 180
         while time.time() < deadline and not all((tmp_path / f"rank{r}.json").exists() for r in range(3)):
