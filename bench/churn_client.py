@@ -5,6 +5,9 @@ Two kinds of worker threads run until stdin closes:
   conn  open a connection (handshake + Channel.Open), then Connection.Close -- one cycle
   cons  on a long-lived channel: Basic.Consume (wait for ConsumeOk), Basic.Cancel (wait for
         CancelOk) on a queue of their own that no publisher feeds
+  rpc   the RPC client pattern: open a connection, declare a server-named exclusive reply
+        queue, bind it, consume it, publish a request routed to it, wait for the reply,
+        close (the close deletes the exclusive queue) -- one cycle
 
 Prints "ready" once the queues are declared, then one JSON object at the end: cycles and
 seconds per kind, and the latency percentiles (ms) of each cycle.  With the broker's light
@@ -32,15 +35,18 @@ def main():
     ap.add_argument("--port", type=int, required=True)
     ap.add_argument("--conn-threads", type=int, default=4)
     ap.add_argument("--cons-threads", type=int, default=4)
+    ap.add_argument("--rpc-threads", type=int, default=0)
     a = ap.parse_args()
     setup = Connection(port=a.port, vhost="/", timeout=60)
     sch = setup.channel()
     for i in range(a.cons_threads):
         sch.queue_declare(f"churn.q{i}")
+    if a.rpc_threads:
+        sch.exchange_declare("churn.rpcx", "direct")
     setup.close()
     stop = threading.Event()
-    lat = {"conn": [], "cons": [], "cancel": []}
-    cnt = {"conn": 0, "cons": 0}
+    lat = {"conn": [], "cons": [], "cancel": [], "rpc": []}
+    cnt = {"conn": 0, "cons": 0, "rpc": 0}
     errs = []
     t_start = [0.0]
 
@@ -82,7 +88,32 @@ def main():
         except Exception:
             pass
 
+    def rpc_worker(i):
+        k = 0
+        while not stop.is_set():
+            t0 = time.perf_counter()
+            try:
+                c = Connection(port=a.port, vhost="/", timeout=30)
+                ch = c.channel()
+                q = ch.queue_declare("", exclusive=True).queue
+                ch.queue_bind(q, "churn.rpcx", q)
+                ch.basic_consume(q, consumer_tag="rpc", no_ack=True)
+                body = b"req-%d-%d" % (i, k)
+                ch.basic_publish("churn.rpcx", q, body)
+                got = ch.consume_n(1, timeout=30)
+                c.close()
+                if got[0].body != body:
+                    raise RuntimeError("rpc reply mismatch")
+            except Exception as e:
+                errs.append(repr(e))
+                time.sleep(0.01)
+                continue
+            k += 1
+            lat["rpc"].append(time.perf_counter() - t0)
+            cnt["rpc"] += 1
+
     ths = [threading.Thread(target=conn_worker, daemon=True) for _ in range(a.conn_threads)]
+    ths += [threading.Thread(target=rpc_worker, args=(i,), daemon=True) for i in range(a.rpc_threads)]
     ths += [threading.Thread(target=cons_worker, args=(i,), daemon=True) for i in range(a.cons_threads)]
     print("ready", flush=True)
     sys.stdin.readline()       # "go": the load's measured window starts
@@ -100,6 +131,8 @@ def main():
                conn_cycle_ms=dict(p50=pct(lat["conn"], 50), p99=pct(lat["conn"], 99), max=pct(lat["conn"], 100)),
                consume_ok_ms=dict(p50=pct(lat["cons"], 50), p99=pct(lat["cons"], 99), max=pct(lat["cons"], 100)),
                cancel_ok_ms=dict(p50=pct(lat["cancel"], 50), p99=pct(lat["cancel"], 99), max=pct(lat["cancel"], 100)),
+               rpc_cycles=cnt["rpc"], rpc_per_s=round(cnt["rpc"] / el, 1),
+               rpc_cycle_ms=dict(p50=pct(lat["rpc"], 50), p99=pct(lat["rpc"], 99), max=pct(lat["rpc"], 100)),
                errors=len(errs), error_sample=errs[:3])
     print(json.dumps(out), flush=True)
 

@@ -112,11 +112,13 @@ def stop_pollers(p):
     return [tuple(x) for x in json.loads(lines[-1])] if lines else []
 
 
-def churn_start(port, conn_threads=4, cons_threads=4):
-    """Connection open/close and consume/cancel churn in its own process (bench/churn_client.py)."""
+def churn_start(port, conn_threads=4, cons_threads=4, rpc_threads=0):
+    """Connection open/close, consume/cancel and RPC-pattern churn in its own process
+    (bench/churn_client.py)."""
     import subprocess
     p = subprocess.Popen([sys.executable, os.path.join(os.path.dirname(os.path.abspath(__file__)), "churn_client.py"),
-                          "--port", str(port), "--conn-threads", str(conn_threads), "--cons-threads", str(cons_threads)],
+                          "--port", str(port), "--conn-threads", str(conn_threads), "--cons-threads", str(cons_threads),
+                          "--rpc-threads", str(rpc_threads)],
                          stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True)
     line = p.stdout.readline()
     if line.strip() != "ready":
@@ -137,10 +139,12 @@ def churn_stop(p):
 
 
 def run_one(core, name, spec, io, io_threads, seconds, rate=0.0, lg_threads=12, store_dir=None, cons_threads=8,
-            n_getters=0, churn=None):
+            n_getters=0, churn=None, with_store=False):
+    """with_store: a store (on disk, fsync on) attached even when the spec publishes nothing
+    persistent: the broker then runs as a durable one (write-behind, held steps)."""
     from chanamq_amd.server.gpu_broker import GpuBroker
-    persist = bool(spec.get("persistent"))
-    plane = plane_for(spec)
+    persist = bool(spec.get("persistent")) or with_store
+    plane = plane_for(dict(spec, persistent=persist))
     store = None
     if persist:
         store = core.Store()
@@ -323,7 +327,8 @@ def wal_soak(core, seconds, io_threads=4, lg_threads=12, cons_threads=8, rate=0.
                 body_bytes_written=getattr(b, "_pw_stats", {}).get("body_bytes"))
 
 
-def run_sharded(core, name, spec, world, mode, seconds, rate=0.0, io_threads=2, lg_threads=12, cons_threads=8):
+def run_sharded(core, name, spec, world, mode, seconds, rate=0.0, io_threads=2, lg_threads=12, cons_threads=8,
+                churn=None):
     """The pipelined sharded server (server/sharded.py, ``world`` rank processes on this
     one GPU, shared-memory exchange): the topology is declared on rank 0 (its queues live
     there), producers attach to rank 1 (every publish crosses the per-step exchange) and
@@ -346,14 +351,24 @@ def run_sharded(core, name, spec, world, mode, seconds, rate=0.0, io_threads=2, 
         ports = [json.load(open(os.path.join(tmp, f"rank{r}.json")))["port"] for r in range(world)]
         spec = {k: v for k, v in spec.items() if not k.startswith("_")}
         t0 = time.time()
-        r = core.run_load(dict(port=ports[0], consumer_port=ports[0] if mode == "local" else ports[1 % world],
-                               producer_port=ports[1 % world], seconds=seconds, warmup=1.0,
-                               queue=f"e2e.{name}", exchange=f"e2e.x.{name}", threads=lg_threads,
-                               consumer_threads=cons_threads, rate=rate, **spec))
+        cproc, cout = None, None
+        if churn:   # on the consumers' rank: its queues live there, its control ops stay local
+            cproc = churn_start(ports[0], *churn)
+            cproc.stdin.write("go\n")
+            cproc.stdin.flush()
+        try:
+            r = core.run_load(dict(port=ports[0], consumer_port=ports[0] if mode == "local" else ports[1 % world],
+                                   producer_port=ports[1 % world], seconds=seconds, warmup=1.0,
+                                   queue=f"e2e.{name}", exchange=f"e2e.x.{name}", threads=lg_threads,
+                                   consumer_threads=cons_threads, rate=rate, **spec))
+        finally:
+            if cproc is not None:
+                cout = churn_stop(cproc)
         time.sleep(0.7)
         ranks = [json.load(open(os.path.join(tmp, f"rank{k}.json"))) for k in range(world)]
     finally:
         ln.stop()
+    r["churn"] = cout
     r.update(name=name, io="pipeline-sharded", world=world, consumers_on=mode, io_threads=io_threads,
              rate_per_producer=rate, recv_msgs_per_s=r["received"] / r["elapsed"],
              sent_msgs_per_s=r["sent"] / r["elapsed"], confirmed_per_s=r["confirmed"] / r["elapsed"],
@@ -361,7 +376,8 @@ def run_sharded(core, name, spec, world, mode, seconds, rate=0.0, io_threads=2, 
              ranks=[{"rank": k["rank"], "front_end": {x: k["front_end"].get(x) for x in
                                                       ("steps", "idle_steps", "xchg_steps", "syncs", "xfails",
                                                        "flush_steps", "xchg_s", "submit_s", "io_phase_s", "wait_s",
-                                                       "published", "delivered", "held_steps")}}
+                                                       "published", "delivered", "held_steps")},
+                     "control_sections": {x: k["stats"].get(x) for x in ("pauses", "light_sections", "pause_why")}}
                     for k in ranks])
     return r
 
@@ -395,7 +411,9 @@ def main():
     ap.add_argument("--churn", action="store_true",
                     help="paced runs again next to connection open/close and consume/cancel churn "
                          "(bench/churn_client.py): delivered rate and latency with and without it")
-    ap.add_argument("--churn-threads", default="4,4", help="connection,consumer churn threads")
+    ap.add_argument("--churn-threads", default="4,4,0", help="connection,consumer,rpc churn threads")
+    ap.add_argument("--churn-store", action="store_true",
+                    help="--churn: the broker runs with a store on disk (fsync on), i.e. as a durable broker")
     ap.add_argument("--getters", type=int, default=0,
                     help="also run each spec with this many Basic.Get pollers on pre-filled queues (the load's "
                          "throughput with and without them, and the gets/s)")
@@ -435,6 +453,16 @@ def main():
                     rp["paced_fraction"] = args.paced
                     results.append(rp)
                     print(json.dumps({k: rp.get(k) for k in keys + ("rate_per_producer", "p95_us")}), flush=True)
+                    if args.churn and mode == "local":
+                        ct = tuple(int(x) for x in args.churn_threads.split(","))
+                        rc = run_sharded(core, name, spec, args.sharded, mode, args.seconds, rate=rate,
+                                         io_threads=int(args.io_threads.split(",")[0]), lg_threads=args.loadgen_threads,
+                                         cons_threads=args.consumer_threads, churn=ct)
+                        rc["paced_fraction"] = args.paced
+                        rc["delivered_vs_no_churn"] = rc["recv_msgs_per_s"] / max(1e-9, rp["recv_msgs_per_s"])
+                        results.append(rc)
+                        print(json.dumps({k: rc.get(k) for k in keys + ("rate_per_producer", "p95_us",
+                                                                        "delivered_vs_no_churn", "churn")}), flush=True)
         if args.out:
             with open(args.out, "w") as f:
                 json.dump({"meta": {"transport": "loopback TCP", "data_plane": f"HIP gfx950, {args.sharded} ranks on 1 GPU",
@@ -484,8 +512,18 @@ def main():
                                                          "error", "control_sections")}), flush=True)
                     if args.churn:
                         ct = tuple(int(x) for x in args.churn_threads.split(","))
+                        if args.churn_store:   # the no-churn reference with the same store attached
+                            rp = run_one(core, name, spec, io, nt, args.seconds, rate=rate,
+                                         lg_threads=args.loadgen_threads, cons_threads=args.consumer_threads,
+                                         with_store=True)
+                            rp["paced_fraction"] = args.paced
+                            rp["with_store"] = True
+                            results.append(rp)
+                            print(json.dumps({k: rp[k] for k in ("name", "io_threads", "recv_msgs_per_s", "p50_us",
+                                                                 "p99_us", "error", "control_sections")}), flush=True)
                         rc = run_one(core, name, spec, io, nt, args.seconds, rate=rate, lg_threads=args.loadgen_threads,
-                                     cons_threads=args.consumer_threads, churn=ct)
+                                     cons_threads=args.consumer_threads, churn=ct, with_store=args.churn_store)
+                        rc["with_store"] = args.churn_store
                         rc["paced_fraction"] = args.paced
                         rc["delivered_vs_no_churn"] = rc["recv_msgs_per_s"] / max(1e-9, rp["recv_msgs_per_s"])
                         results.append(rc)

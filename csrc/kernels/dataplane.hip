@@ -405,13 +405,6 @@ __global__ __launch_bounds__(1024) void k_stage(DS d) {
     s_in = *d.in_h;
     *d.in = s_in;
   }
-  // consumers a light control section activated (cons_active 2, applied by an earlier
-  // step's k_stage) take deliveries from this step on: the step that applied them rendered
-  // none, so its egress -- behind which the front end released the Basic.ConsumeOk
-  // (Frontend::send_after) -- never holds a Basic.Deliver that overtakes the ConsumeOk.
-  // Flipped before this step's own writes are applied (theirs wait one more step)
-  for (u32 c = tid; c < d.cons_max; c += 1024)
-    if (d.cons_active[c] == 2u) d.cons_active[c] = 1u;
   __syncthreads();
   if (s_in.delta_bytes) apply_deltas(d, d.delta_h, tid, 1024, lrec);   // control writes first
   const u32 nseg = s_in.nseg;
@@ -4432,6 +4425,16 @@ __global__ __launch_bounds__(256) void k_post(DS d, u32 fin) {
   const u32 nd = d.tot[TS_NDEFER], gs = gridDim.x * blockDim.x;
   for (u32 b = 0; b < nd; b += gs)   // grid-uniform trip count (wave_release ballots)
     wave_release(d, b + i < nd ? d.defer_free[b + i] : INVALID, b + i < nd);
+  // consumers a light control section activated (cons_active 2, applied by this or an
+  // earlier step's k_stage) take deliveries from the next step on: this step's dequeue (it
+  // ran before this kernel) rendered none for them, so its egress -- behind which the front
+  // end releases the Basic.ConsumeOk (Frontend::send_after) -- never holds a Basic.Deliver
+  // that overtakes the ConsumeOk.  (Here and not in the next step's k_stage: with the
+  // overlapped engine that k_stage may run beside this step's k_dequeue; a step that stages
+  // writes waits for the previous step's routing half, so no 2 written after this point is
+  // flipped by it)
+  for (u32 c = i; c < d.cons_max; c += gridDim.x * blockDim.x)
+    if (d.cons_active[c] == 2u) d.cons_active[c] = 1u;
   // reset per-connection scratch (fused k_post2)
   if (i < d.c_max) {
     d.conn_dfirst[i] = INVALID;
