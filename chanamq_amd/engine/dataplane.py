@@ -876,7 +876,8 @@ class GpuDataPlane(ControlState):
         if left >= entries // 2:
             return left
         top = self._u64("ring_top", 0)
-        take = min(int(entries), self.ring_pool - top)
+        # (at most an eighth of what is left: the device grows rings from the same pool mid-step)
+        take = min(int(entries), (self.ring_pool - top) // 8)
         if take <= 0:
             return left
         self._up_at("ring_top", top + take, 0, np.uint64)

@@ -3411,12 +3411,18 @@ DEV u32 deliver_size(const DS& d, u32 cons, const MsgEnt& m, u32 conn) {
 // publish decode marked (MsgEnt.href), published at most ref_back steps ago, no shorter than
 // ref_min and within one body frame of the connection.  Link pseudo-connections ship
 // restore records, never references.  k_dv_write and render_deliv must agree: same inputs
-DEV bool deliv_ref(const DS& d, const MsgEnt& m, u32 conn) {
-  if (!m.href || d.in->ref_back == 0xffffffffu || m.body_len < d.in->ref_min) return false;
-  if ((u32)d.in->step - m.pub_step > d.in->ref_back) return false;
-  if (d.links && d.conn_link[conn]) return false;
+// Returns the body's host address, or 0 (rendered whole).  A body in the host spill ring
+// is referenced there whatever its age: a freed ring byte is reused only SPILL_LAG steps
+// later (spill_reserve), after every egress that can reference it was written out
+DEV u64 deliv_href(const DS& d, const MsgEnt& m, u32 conn) {
+  if (d.in->ref_back == 0xffffffffu || m.body_len < d.in->ref_min) return 0;
+  if (d.links && d.conn_link[conn]) return 0;
   const u32 fm = d.conn_frame_max[conn];
-  return fm == 0 || m.body_len <= fm - 8;
+  if (fm != 0 && m.body_len > fm - 8) return 0;
+  if ((m.log_off & (SPILL_BIT | COLD_BIT)) == SPILL_BIT && d.spill_host)
+    return d.spill_host + ((m.log_off & ~SPILL_BIT) % d.spill_bytes) + m.body_off;
+  if (!m.href || (u32)d.in->step - m.pub_step > d.in->ref_back) return 0;
+  return m.href;
 }
 
 // give back channel reservations for `take` messages not delivered after all
@@ -3942,7 +3948,7 @@ __global__ void k_dv_write(DS d) {
     u.expire_ms = ds.expire_ms;
     d.uwin[(u64)ch * (d.ucap_mask + 1) + ((tag - 1) & d.ucap_mask)] = u;
     const MsgEnt& m = d.msgs[ds.msg];
-    const bool ref = deliv_ref(d, m, ch / d.chpc);
+    const bool ref = deliv_href(d, m, ch / d.chpc) != 0;
     const u32 sz = deliver_size(d, cons, m, ch / d.chpc) - (ref ? m.body_len : 0u);
     dv.size = sz;
     d.dv_size[i] = sz;
@@ -4189,7 +4195,8 @@ DEV void render_deliv(const DS& d, u32 i) {
   const u8* slot = msg_slot(d, m.log_off);
   // gather entry of this delivery (the table exists when some delivery of the step
   // references its body; dst of an unreferenced one = its end, so dst never decreases)
-  const bool ref = deliv_ref(d, m, conn);
+  const u64 href = deliv_href(d, m, conn);
+  const bool ref = href != 0;
   EgressRef* gt = d.ctr->n_ref ? (EgressRef*)((u8*)d.in->egress + d.ctr->gath_off) : nullptr;
   if (d.links && d.conn_link[conn]) {   // X2: a restore record for the shadow queue
     if (gt && lane == 0) gt[i] = EgressRef{0ull, d.conn_base[conn], 0u};
@@ -4219,7 +4226,7 @@ DEV void render_deliv(const DS& d, u32 i) {
   u64 off = (u64)d.conn_base[conn] + d.conn_ret_bytes[conn] + d.conn_conf_bytes[conn] + d.dv_off[i] -
             d.dv_off[f];
   if (gt && lane == 0)   // (a referenced body goes after its body frame's 7-byte header)
-    gt[i] = ref ? EgressRef{m.href, (u32)(off + dv.size - 1u), m.body_len} : EgressRef{0ull, (u32)(off + dv.size), 0u};
+    gt[i] = ref ? EgressRef{href, (u32)(off + dv.size - 1u), m.body_len} : EgressRef{0ull, (u32)(off + dv.size), 0u};
   if (off + dv.size > d.egress_cap) return;  // never: dequeue reserves an egress byte budget
   u8* o = (u8*)d.in->egress + off;
   u32 chno = d.ch_num[ch];
@@ -4480,6 +4487,7 @@ DEV void final_step(const DS& d) {
       st = (bi + 1) * d.log_block;
     }
     *d.spill_tail = st > sh ? sh : st;
+    d.spill_tail_lag[d.in->step % SPILL_LAG] = *d.spill_tail;
   }
   Counters* c = d.ctr;
   c->log_head = head;
@@ -4757,7 +4765,10 @@ __global__ __launch_bounds__(64) void k_basic_get(DS d, u32 q, u32 ch, u32 noack
 // reserve `sz` bytes in the spill ring (never across its wrap), false when it is full
 DEV bool spill_reserve(const DS& d, u32 sz, u64* pos) {
   unsigned long long cur = __hip_atomic_load(d.spill_head, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  const u64 tail = *d.spill_tail;
+  // the tail of SPILL_LAG steps ago (the oldest of the history): bytes freed since may still
+  // be referenced by an egress not yet written out (spilled bodies are sent from the ring)
+  u64 tail = *d.spill_tail;
+  for (u32 k = 0; k < SPILL_LAG; ++k) tail = d.spill_tail_lag[k] < tail ? d.spill_tail_lag[k] : tail;
   while (true) {
     u64 h = cur;
     const u64 phys = h % d.spill_bytes;

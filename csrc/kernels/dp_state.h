@@ -17,6 +17,7 @@
 #define EGRESS_SLOTS 3        // rotating egress buffers (render of step t || D2H of t-1, t-2)
 #define RUNS_PER_Q 64         // consumers served per queue per step (dequeue round-robin window)
 #define RUN_SORT_LDS 8192     // runs sorted in LDS by k_runs (more: global-memory sort)
+#define SPILL_LAG 6           // steps a freed spill-ring byte stays untouched (egress by reference)
 
 // host-mapped xchg[] words (one array per IO parity).  [XC_SEND_N + r] / [XC_SEND_B + r]:
 // records / payload bytes phase A packed for rank r; [XC_RECV_N + r] / [XC_RECV_B + r]:
@@ -242,6 +243,11 @@ struct DS {
   u64 spill_bytes, n_spill_blocks;
   u64* spill_head;
   u64* spill_tail;
+  // egress by reference of spilled bodies: the ring's host address, and its tail over the
+  // last SPILL_LAG steps -- space freed by a step is reused only SPILL_LAG steps later, after
+  // the egress that may still reference it has been written out (spill_reserve)
+  u64 spill_host;
+  u64* spill_tail_lag;      // [SPILL_LAG]
   i64* spill_live;          // live bytes per spill block
   i64* cold_live;           // [COLD_SEGS] live bytes per cold-store segment (host unlinks freed ones)
   u64* q_cold_lim;          // [q_max] deliveries stop here (~0: nothing of the queue is cold)

@@ -450,6 +450,8 @@ class Engine {
     d_.spill_tail = (u64*)dev("spill_tail", 8);
     d_.spill_live = (i64*)dev("spill_live", 8ull * (d_.n_spill_blocks ? d_.n_spill_blocks : 1));
     d_.spill = d_.spill_bytes ? (u8*)hst("spill", d_.spill_bytes + 4096) : nullptr;
+    d_.spill_host = d_.spill_bytes ? (u64)buf("spill").ptr : 0;
+    d_.spill_tail_lag = (u64*)dev("spill_tail_lag", 8ull * SPILL_LAG);
     spill_moved_ = (unsigned long long*)dev("spill_moved", 8);
     d_.cold_live = (i64*)dev("cold_live", 8ull * COLD_SEGS);
     cold_recs_ = (ColdRec*)dev("cold_recs", sizeof(ColdRec) * COLD_BATCH);
@@ -1036,8 +1038,13 @@ class Engine {
   // batch up to this id was taken by a submitted step (or applied by flush_deltas)
   u64 dl_state(int which) {
     std::lock_guard<std::mutex> g(dl_mu_);
-    if (which == 1) return dl_.empty() ? dl_next_id_ - 1 : dl_.front().id - 1;
-    return (!dl_.empty() && dl_.back().open) ? dl_.back().id : dl_next_id_;
+    if (which == 1) {   // (closed batches with nothing in them count as taken: no step needs to carry them)
+      for (auto& bt : dl_)
+        if (bt.open || !bt.w.empty() || !bt.dirty.empty() || !bt.unp.empty()) return bt.id - 1;
+      return dl_next_id_ - 1;
+    }
+    // outside a light section nothing is staged for the caller: no batch to wait for
+    return (!dl_.empty() && dl_.back().open) ? dl_.back().id : 0;
   }
   // from the next submitted step on, every step moves queued bodies in the oldest frac/65536
   // of the HBM log (past the first `hot` entries of a queue with consumers) to the host

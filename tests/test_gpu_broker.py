@@ -802,7 +802,11 @@ def test_backlog_past_hbm_and_host_tiers_goes_to_the_cold_store(gpu, io, tmp_pat
         for k in range(n):
             ch.basic_publish("", "deep", k.to_bytes(4, "big") * (size // 4))
             if k % 64 == 63:
-                assert ch.wait_for_confirms(timeout=60), f"publish {k} nacked"
+                if not ch.wait_for_confirms(timeout=60):
+                    b._sync_fe_stats()
+                    fs = {x: (b._fe_stats or {}).get(x) for x in ("dropped_nomem", "ring_full", "log_used", "live_bytes",
+                                                                  "spill_moved", "live_msgs")}
+                    raise AssertionError(f"publish {k} nacked: {fs} {b.stats}")
                 time.sleep(0.001)
         assert ch.wait_for_confirms(timeout=60)
         assert not b.blocked and b.stats.get("flow_off", 0) == 0
