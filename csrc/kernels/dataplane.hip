@@ -69,6 +69,17 @@ DEV void wave_copy(u8* dst, const u8* src, u32 n) {
   for (u32 i = (nv << 4) + lane; i < n; i += 64) dst[i] = src[i];
 }
 
+// same, by the G lanes (lane = 0..G-1) of a lane group
+template <u32 G>
+DEV void group_copy(u8* dst, const u8* src, u32 n, u32 lane) {
+  u32 nv = n >> 4;
+  for (u32 i = lane; i < nv; i += G) {
+    U4 v = *(const U4*)(src + (u64)i * 16);
+    *(U4*)(dst + (u64)i * 16) = v;
+  }
+  for (u32 i = (nv << 4) + lane; i < n; i += G) dst[i] = src[i];
+}
+
 // same, by all threads of a block
 DEV void block_copy(u8* dst, const u8* src, u32 n, u32 tid, u32 nt) {
   u32 nv = n >> 4;
@@ -4182,11 +4193,11 @@ DEV u32 put_frame_hdr(u8* o, u32 type, u32 ch, u32 size) {
   return 7;
 }
 
-// one wave per delivery
-DEV void render_deliv(const DS& d, u32 i);
-// one wave per delivery i (< n_deliv)
-DEV void render_deliv(const DS& d, u32 i) {
-  u32 lane = lane_id();
+// one group of RD_G lanes per delivery i (< n_deliv), lane = 0..RD_G-1: with egress by
+// reference a delivery is ~100 bytes of frames, so a whole wave per delivery left 3/4 of
+// its lanes idle (four deliveries per wave now)
+#define RD_G 16
+DEV void render_deliv(const DS& d, u32 i, u32 lane) {
   const Deliv dv = d.deliv[i];
   const u32 ch = dv.chslot;
   const MsgEnt m = d.msgs[dv.msg];
@@ -4204,8 +4215,8 @@ DEV void render_deliv(const DS& d, u32 i) {
     const u32 po = d.link_bbase[conn] + (d.dv_off[i] - d.dv_off[f]);
     u8* lo = d.lsend_pay + (u64)d.link_dbase[dest] + po;
     const u32 meta = m.ex_len + m.rk_len + m.props_len;
-    wave_copy(lo, slot, meta);
-    wave_copy(lo + meta, slot + m.body_off, m.body_len);
+    group_copy<RD_G>(lo, slot, meta, lane);
+    group_copy<RD_G>(lo + meta, slot + m.body_off, m.body_len, lane);
     if (lane == 0) {
       RDesc rd{};
       rd.pay_off = po;
@@ -4253,12 +4264,12 @@ DEV void render_deliv(const DS& d, u32 i) {
   }
   if (!get) {
     const u8* tg = d.tpool + d.cons_tag_off[dv.cons];
-    for (u32 k = lane; k < taglen; k += 64) o[p_tag + k] = tg[k];
+    for (u32 k = lane; k < taglen; k += RD_G) o[p_tag + k] = tg[k];
   }
-  for (u32 k = lane; k < m.ex_len; k += 64) o[p_ex + k] = slot[k];
-  for (u32 k = lane; k < m.rk_len; k += 64) o[p_rk + k] = slot[m.ex_len + k];
+  for (u32 k = lane; k < m.ex_len; k += RD_G) o[p_ex + k] = slot[k];
+  for (u32 k = lane; k < m.rk_len; k += RD_G) o[p_rk + k] = slot[m.ex_len + k];
   u32 hp = 8 + mp + 7 + 12;
-  wave_copy(o + hp, slot + m.ex_len + m.rk_len, m.props_len);
+  group_copy<RD_G>(o + hp, slot + m.ex_len + m.rk_len, m.props_len, lane);
   if (lane == 0) o[hp + m.props_len] = 0xCE;
   u32 bp = hp + m.props_len + 1;
   u32 fm = d.conn_frame_max[conn];
@@ -4274,7 +4285,7 @@ DEV void render_deliv(const DS& d, u32 i) {
   for (u32 b0 = 0; b0 < m.body_len; b0 += fmb) {
     u32 bl = m.body_len - b0 < fmb ? m.body_len - b0 : fmb;
     if (lane == 0) put_frame_hdr(o + bp, 3, chno, bl);
-    wave_copy(o + bp + 7, body + b0, bl);
+    group_copy<RD_G>(o + bp + 7, body + b0, bl, lane);
     if (lane == 0) o[bp + 7 + bl] = 0xCE;
     bp += bl + 8;
   }
@@ -4388,9 +4399,10 @@ DEV void render_rc(const DS& d, u32 blk);
 __global__ __launch_bounds__(256) void k_render(DS d, u32 n_rc) {
   if (blockIdx.x < n_rc) { render_rc(d, blockIdx.x); return; }
   const u32 n = d.ctr->n_deliv;
-  const u32 nw = ((gridDim.x - n_rc) * blockDim.x) >> 6;
-  const u32 wave = __builtin_amdgcn_readfirstlane(((blockIdx.x - n_rc) * blockDim.x + threadIdx.x) >> 6);
-  for (u32 i = wave; i < n; i += nw) render_deliv(d, i);
+  const u32 ng = ((gridDim.x - n_rc) * blockDim.x) / RD_G;
+  const u32 g = ((blockIdx.x - n_rc) * blockDim.x + threadIdx.x) / RD_G;
+  const u32 lane = threadIdx.x % RD_G;
+  for (u32 i = g; i < n; i += ng) render_deliv(d, i, lane);
 }
 DEV void render_rc(const DS& d, u32 blk) {
   if (blk >= RC_RET_BLOCKS) {

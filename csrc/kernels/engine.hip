@@ -641,7 +641,8 @@ class Engine {
     // from the recent steps' egress (a host-issued tail copies the rest when a step renders
     // more) -- the host is off the render -> D2H path.  0: the D2H is issued by the host
     // after it saw the step finish (egress_copy)
-    gated_ = copy_mode_ == 3 && d_.world == 1 && get("egress_gate", 1) != 0;
+    // (sharded ranks too: the step's last kernel -- phase B's -- opens the gate the same way)
+    gated_ = copy_mode_ == 3 && get("egress_gate", 1) != 0;
     for (int p = 0; p < 2; ++p) {
       HIPCHECK(hipEventCreateWithFlags(&ev_h2d_[p], hipEventDisableTiming));
       HIPCHECK(hipEventCreateWithFlags(&ev_done_[p], hipEventDisableTiming));
@@ -849,6 +850,22 @@ class Engine {
     int p = (int)(seq_ & 1);
     if (inflight_[p]) throw std::runtime_error("submit: results of the previous step of this parity not collected");
     HIPCHECK(hipEventSynchronize(ev_h2d_[p]));  // staging buffers of step t-2 are free
+    // the payload first: the H2D is the step's longest stage and nothing below changes what
+    // it copies (the slot's last reader, step t - INGRESS_SLOTS, is finished: its results were
+    // collected before step t-2's).  It may already be on its way (prefetch): then only the
+    // step's descriptors follow it on the H2D stream
+    const int is = (int)(seq_ % INGRESS_SLOTS);
+    const bool pre = pre_[p];
+    if (pre && (pre_seq_[p] != step || pre_ptr_[p] != payload_ptr || pre_len_[p] != payload_len))
+      throw std::runtime_error("submit: payload differs from the one prefetched for this step");
+    pre_[p] = false;
+    {   // overlapped engines move payloads on their own stream (prefetches run ahead of the
+        // small per-step copies there; the ingest half waits for both)
+      hipStream_t ps = overlap_ ? s_pre_ : s_h2d_;
+      if (payload_len && !pre)
+        HIPCHECK(hipMemcpyAsync((void*)ingress_slot_[is], (const void*)payload_ptr, payload_len,
+                                sdma_ ? hipMemcpyDeviceToDeviceNoCU : hipMemcpyHostToDevice, ps));
+    }
     StepIn* in = stage_in_[p];
     *in = StepIn{};
     in->nseg = nseg;
@@ -875,7 +892,6 @@ class Engine {
         in->gate = (u64)gate_dummy_;
       }
     }
-    const int is = (int)(seq_ % INGRESS_SLOTS);
     in->ingress = (u64)ingress_slot_[is];
     in->pslot = (u32)(seq_ % PSLOTS);
     pslot_of_[p] = (int)in->pslot;
@@ -909,18 +925,6 @@ class Engine {
     if (in->nunp)
       HIPCHECK(hipMemcpyAsync((void*)io_[p].unpause_req, stage_unp_[p], 4ull * in->nunp, hipMemcpyHostToDevice, s_h2d_));
     dl_step_[p] = in->delta_bytes;
-    // the payload may already be on its way (prefetch): then only the step's descriptors
-    // follow it on the H2D stream
-    const bool pre = pre_[p];
-    if (pre && (pre_seq_[p] != step || pre_ptr_[p] != payload_ptr || pre_len_[p] != payload_len))
-      throw std::runtime_error("submit: payload differs from the one prefetched for this step");
-    pre_[p] = false;
-    // overlapped engines move payloads on their own stream (prefetches run ahead of the
-    // small per-step copies there; the ingest half waits for both)
-    hipStream_t ps = overlap_ ? s_pre_ : s_h2d_;
-    if (payload_len && !pre)
-      HIPCHECK(hipMemcpyAsync((void*)ingress_slot_[is], (const void*)payload_ptr, payload_len,
-                              sdma_ ? hipMemcpyDeviceToDeviceNoCU : hipMemcpyHostToDevice, ps));
     if (overlap_) HIPCHECK(hipEventRecord(ev_pre_[p], s_pre_));
     HIPCHECK(hipEventRecord(ev_h2d_[p], s_h2d_));
     inflight_[p] = true;
@@ -1291,6 +1295,7 @@ class Engine {
         launch_phase_b(s_comp_, io_[p]);
       }
       HIPCHECK(hipEventRecord(ev_done_[p], s_comp_));
+      gated_copy(e);
     } else if (d_.world > 1) {
       HIPCHECK(hipEventRecord(ev_a_[p], s_comp_));
       phase_a_[p] = true;
@@ -1336,6 +1341,7 @@ class Engine {
       launch_phase_b(s_comp_, io_[p]);
     }
     HIPCHECK(hipEventRecord(ev_done_[p], s_comp_));
+    gated_copy(slot_of_[p]);   // (the phase-B render opens the gate)
     phase_a_[p] = false;
   }
 
@@ -2027,6 +2033,7 @@ class Engine {
       launch_phase_b(s_comp_, io_[p]);
     }
     HIPCHECK(hipEventRecord(ev_done_[p], s_comp_));
+    gated_copy(slot_of_[p]);   // (phase B's last kernel opens the gate: sharded ranks gate too)
   }
 
   // ------------------------------------------------------------- native front end
