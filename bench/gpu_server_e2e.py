@@ -417,7 +417,11 @@ def main():
     ap.add_argument("--getters", type=int, default=0,
                     help="also run each spec with this many Basic.Get pollers on pre-filled queues (the load's "
                          "throughput with and without them, and the gets/s)")
+    ap.add_argument("--egress-ref", type=int, default=1,
+                    help="1: the front end sends delivered bodies from the host ingress arenas (egress by "
+                         "reference); 0: every delivered body comes back over PCIe in the egress bytes")
     args = ap.parse_args()
+    FE_CFG["egress_ref"] = bool(args.egress_ref)
     BROKER_CFG["persist_group_ms"] = args.persist_group_ms
     BROKER_CFG["confirm_read"] = args.confirm_read
     SIZING["spill_bytes"] = args.spill_bytes
