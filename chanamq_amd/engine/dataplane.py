@@ -863,6 +863,8 @@ class GpuDataPlane(ControlState):
         if self.defer:
             raise ControlError(C.RESOURCE_ERROR, "ring chunk exhausted in a light section")
         top = self._u64("ring_top", 0)
+        if top + cap > self.ring_pool and left and off + left == top:
+            top, self._ring_chunk = off, (0, 0)   # the unused light-section chunk goes back first
         if top + cap > self.ring_pool:
             raise ControlError(C.RESOURCE_ERROR, "ring pool exhausted")
         self._up_at("ring_top", top + cap, 0, np.uint64)
@@ -876,10 +878,12 @@ class GpuDataPlane(ControlState):
         if left >= entries // 2:
             return left
         top = self._u64("ring_top", 0)
+        if left and off + left == top:   # the old remainder is the pool's top: extend it in place
+            top, left = off, 0
         # (at most an eighth of what is left: the device grows rings from the same pool mid-step)
         take = min(int(entries), (self.ring_pool - top) // 8)
         if take <= 0:
-            return left
+            return self._ring_chunk[1]   # (nothing changed)
         self._up_at("ring_top", top + take, 0, np.uint64)
         if left:   # (power-of-two pieces of the old remainder to the free lists)
             while left:

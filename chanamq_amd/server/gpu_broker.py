@@ -109,7 +109,7 @@ class _PlaneLock:
                 self.b.fe.flush_ctl()
             if hasattr(self.b.plane, "reserve_ring_chunk") and self.b.node is None:
                 # rings for queues declared in light sections (no device read there)
-                self.b.plane.reserve_ring_chunk(64 * self.b.plane.default_queue_capacity)
+                self.b.plane.reserve_ring_chunk(16 * self.b.plane.default_queue_capacity)
             if self.light:
                 # replies a light section produced but has not queued yet: written now,
                 # while paused (its staged writes were just applied; once the steps resume,
@@ -337,7 +337,7 @@ class GpuBroker:
         if self.io == "pipeline":
             from ..broker import load
             if hasattr(self.plane, "reserve_ring_chunk") and self.node is None:
-                self.plane.reserve_ring_chunk(64 * self.plane.default_queue_capacity)
+                self.plane.reserve_ring_chunk(16 * self.plane.default_queue_capacity)
             self.fe = load().Frontend(self.plane.eng.c_api(), dict(
                 host=self.host, port=self.port, io_threads=self.io_threads, per_conn_read=self.per_conn_read,
                 idle_step_ms=self.idle_step_s * 1000.0, worker=self.plane.worker, max_slot=self._top_slot,
