@@ -184,6 +184,19 @@ def run_one(core, name, spec, io, io_threads, seconds, rate=0.0, lg_threads=12, 
         r = core.run_load(dict(port=b.port, seconds=seconds, warmup=1.0, queue=f"e2e.{name}",
                                exchange=f"e2e.x.{name}", threads=lg_threads, consumer_threads=cons_threads,
                                rate=rate, **spec))
+    except Exception:   # what the broker still holds back when a client gives up on a reply
+        try:
+            b._sync_fe_stats()
+            fs = getattr(b, "_fe_stats", None) or {}
+            eng = getattr(plane, "eng", None)
+            print(json.dumps({"diag": "load failed", "ctl_state": list(b.fe.ctl_state()) if b.fe else None,
+                              "dl_state": [eng.dl_state(0), eng.dl_state(1)] if eng is not None else None,
+                              "held_steps": fs.get("held_steps"), "steps": fs.get("steps"),
+                              "stats": {k: v for k, v in b.stats.items() if isinstance(v, (int, float, str))}}),
+                  file=sys.stderr, flush=True)
+        except Exception as e:   # noqa: BLE001
+            print("diag failed:", e, file=sys.stderr, flush=True)
+        raise
     finally:
         done[0] = True
         if gproc is not None:
@@ -420,6 +433,8 @@ def main():
     ap.add_argument("--egress-ref", type=int, default=1,
                     help="1: the front end sends delivered bodies from the host ingress arenas (egress by "
                          "reference); 0: every delivered body comes back over PCIe in the egress bytes")
+    ap.add_argument("--with-store", action="store_true",
+                    help="every run with a store on disk attached (a durable broker)")
     args = ap.parse_args()
     FE_CFG["egress_ref"] = bool(args.egress_ref)
     BROKER_CFG["persist_group_ms"] = args.persist_group_ms
@@ -480,7 +495,7 @@ def main():
         for io in args.io.split(","):
             for nt in ([int(x) for x in args.io_threads.split(",")] if io == "pipeline" else [1]):
                 r = run_one(core, name, spec, io, nt, args.seconds, lg_threads=args.loadgen_threads,
-                               cons_threads=args.consumer_threads)
+                               cons_threads=args.consumer_threads, with_store=args.with_store)
                 results.append(r)
                 print(json.dumps({k: r[k] for k in ("name", "io", "io_threads", "recv_msgs_per_s", "sent_msgs_per_s",
                                                     "confirmed_per_s", "p50_us", "p99_us", "error", "redelivered",
@@ -508,7 +523,7 @@ def main():
                     if spec.get("exchange_type") == "fanout":   # deliveries = publishes x queues
                         rate /= max(1, spec.get("queues", 1))
                     rp = run_one(core, name, spec, io, nt, args.seconds, rate=rate, lg_threads=args.loadgen_threads,
-                               cons_threads=args.consumer_threads)
+                               cons_threads=args.consumer_threads, with_store=args.with_store)
                     rp["paced_fraction"] = args.paced
                     results.append(rp)
                     print(json.dumps({k: rp[k] for k in ("name", "io", "io_threads", "rate_per_producer",

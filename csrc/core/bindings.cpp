@@ -226,7 +226,7 @@ PYBIND11_MODULE(_core, m) {
              S("host", host); S("port", port); S("io_threads", io_threads); S("per_conn_read", per_conn_read);
              S("idle_step_ms", idle_step_ms); S("sweep_ms", sweep_ms); S("worker", worker); S("max_slot", max_slot); S("reuseport", reuseport);
              S("sndbuf", sndbuf); S("rcvbuf", rcvbuf); S("wblock_high", wblock_high); S("wblock_low", wblock_low);
-             S("async_scatter", async_scatter); S("egress_ref", egress_ref); S("egress_ref_min", egress_ref_min);
+             S("async_scatter", async_scatter); S("egress_ref", egress_ref); S("egress_ref_min", egress_ref_min); S("egress_ref_step_min", egress_ref_step_min);
 #undef S
              return new Frontend(c, (const CmqEngineApi*)api);
            }), py::arg("engine_api"), py::arg("cfg") = py::dict())

@@ -113,8 +113,10 @@ Frontend::Frontend(const FrontendCfg& cfg, const CmqEngineApi* api) : cfg_(cfg),
   const u64 arena_bytes = ((api_->ingress_cap + 64 + 4095) / 4096) * 4096;
   // egress by reference: deliveries of the same step's bodies (back 0) are sent from the
   // arena they arrived in (NARENA arenas keep it unchanged until that egress is written)
-  if (cfg_.egress_ref && api_->set_egress_ref && api_->set_egress_ref(api_->eng, 0, cfg_.egress_ref_min) == 0)
+  if (cfg_.egress_ref && api_->set_egress_ref && api_->set_egress_ref(api_->eng, 0, cfg_.egress_ref_min) == 0) {
     narena_ = NARENA;
+    ref_on_ = true;
+  }
   else if (api_->set_egress_ref)
     api_->set_egress_ref(api_->eng, -1, 0);
   for (int k = 0; k < narena_; ++k) {
@@ -390,6 +392,15 @@ void Frontend::materialize(Scatter& sc, const u8* egress, u64 bytes) {
   sc.egress = nullptr;
   sc.gath_n = 0;
   sc.gath_off = 0;
+}
+
+// egress by reference for the next submitted step only when it gathered enough bytes
+void Frontend::ref_for_step(u64 used) {
+  if (narena_ != NARENA) return;
+  const bool on = used >= cfg_.egress_ref_step_min;
+  if (on == ref_on_) return;
+  api_->set_egress_ref(api_->eng, on ? 0 : -1, cfg_.egress_ref_min);
+  ref_on_ = on;
 }
 
 void Frontend::send(u32 conn, const char* data, size_t n) {
@@ -1368,6 +1379,7 @@ void Frontend::stepper() {
       Inflight f;
       stage_gets(f);
       wait_copies(PSLOTS - 3);   // the slot this submit takes was last used PSLOTS steps back
+      ref_for_step(used);
       int p = api_->submit(api_->eng, segs.data(), (u32)segs.size(), arena_[arena_i_], used, wall_ms(), cfg_.worker);
       if (!check(p)) break;
       {
@@ -1555,6 +1567,7 @@ void Frontend::stepper_sharded() {
     {
       GpuWait gw(gpu_wait_since_);
       wait_copies(PSLOTS - 3);
+      ref_for_step(ph_used_.load());
       p = api_->submit(api_->eng, segs.data(), (u32)segs.size(), arena_[arena_i_], ph_used_.load(), wall_ms(),
                        cfg_.worker);
     }

@@ -95,7 +95,7 @@ struct Client {
       if (m.cls() == 10 && m.mid() == 50) throw std::runtime_error("loadgen: connection closed: " + m.s(1));
       if (m.cls() == 20 && m.mid() == 40) throw std::runtime_error("loadgen: channel closed: " + m.s(1));
     }
-    throw std::runtime_error("loadgen: timeout waiting for reply");
+    throw std::runtime_error("loadgen: timeout waiting for reply " + std::to_string(cls) + "." + std::to_string(mid));
   }
   void open(const std::string& host, int port, const std::string& vhost) {
     if (!connect_to(host, port)) throw std::runtime_error("loadgen: cannot connect");

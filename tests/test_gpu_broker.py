@@ -34,7 +34,10 @@ def make_plane(kind):
 def broker(request):
     from chanamq_amd.server.gpu_broker import GpuBroker
     kind, io = request.param.split("-")
-    b = GpuBroker(make_plane(kind), idle_step_ms=1.0, io=io, ingress_bytes=8 << 20).start()
+    # (the pipeline front end sends every step's bodies by reference here, however small the
+    # step: the production threshold, egress_ref_step_min, would leave these steps inline)
+    b = GpuBroker(make_plane(kind), idle_step_ms=1.0, io=io, ingress_bytes=8 << 20,
+                  fe_cfg={"egress_ref_step_min": 0} if io == "pipeline" else None).start()
     yield b
     b.stop()
 
