@@ -190,7 +190,11 @@ def run_one(core, name, spec, io, io_threads, seconds, rate=0.0, lg_threads=12, 
             fs = getattr(b, "_fe_stats", None) or {}
             eng = getattr(plane, "eng", None)
             print(json.dumps({"diag": "load failed", "ctl_state": list(b.fe.ctl_state()) if b.fe else None,
-                              "dl_state": [eng.dl_state(0), eng.dl_state(1)] if eng is not None else None,
+                              "dl_state": [eng.dl_state(k) for k in range(4)] if eng is not None else None,
+                              "lock": [b.lock.depth, b.lock.light, b.lock.paused_at],
+                              "conns": [(c.id, c.state, len(c.out)) for c in list(b.conns.values())],
+                              "conn_paused": [int(np.frombuffer(eng.download("conn_paused", 4 * c.id, 4), np.uint32)[0])
+                                              for c in list(b.conns.values())] if eng is not None else None,
                               "held_steps": fs.get("held_steps"), "steps": fs.get("steps"),
                               "stats": {k: v for k, v in b.stats.items() if isinstance(v, (int, float, str))}}),
                   file=sys.stderr, flush=True)

@@ -1042,6 +1042,8 @@ class Engine {
   // batch up to this id was taken by a submitted step (or applied by flush_deltas)
   u64 dl_state(int which) {
     std::lock_guard<std::mutex> g(dl_mu_);
+    if (which == 2) return dl_open_;      // (diagnostics: open light sections, batches queued)
+    if (which == 3) return dl_.size();
     if (which == 1) {   // (closed batches with nothing in them count as taken: no step needs to carry them)
       for (auto& bt : dl_)
         if (bt.open || !bt.w.empty() || !bt.dirty.empty() || !bt.unp.empty()) return bt.id - 1;
