@@ -198,6 +198,11 @@ def run_one(core, name, spec, io, io_threads, seconds, rate=0.0, lg_threads=12, 
                               "held_steps": fs.get("held_steps"), "steps": fs.get("steps"),
                               "stats": {k: v for k, v in b.stats.items() if isinstance(v, (int, float, str))}}),
                   file=sys.stderr, flush=True)
+            import traceback
+            for tid, fr in sys._current_frames().items():   # where the control thread is
+                st = traceback.format_stack(fr)
+                if any("gpu_broker.py" in x for x in st):
+                    print(f"--- thread {tid}\n" + "".join(st[-14:]), file=sys.stderr, flush=True)
         except Exception as e:   # noqa: BLE001
             print("diag failed:", e, file=sys.stderr, flush=True)
         raise
