@@ -86,16 +86,20 @@ struct Client {
     }
     return true;
   }
+  std::string skipped_;
   Method expect(u16 cls, u16 mid) {
     Frame f;
+    std::string& skipped = skipped_;   // (every method skipped on this connection so far)
     while (frame(f)) {
       if (f.type != FRAME_METHOD) continue;
       Method m = decode_method((const u8*)f.payload.data(), f.payload.size());
       if (m.cls() == cls && m.mid() == mid) return m;
+      skipped += " " + std::to_string(m.cls()) + "." + std::to_string(m.mid());
       if (m.cls() == 10 && m.mid() == 50) throw std::runtime_error("loadgen: connection closed: " + m.s(1));
       if (m.cls() == 20 && m.mid() == 40) throw std::runtime_error("loadgen: channel closed: " + m.s(1));
     }
-    throw std::runtime_error("loadgen: timeout waiting for reply " + std::to_string(cls) + "." + std::to_string(mid));
+    throw std::runtime_error("loadgen: timeout waiting for reply " + std::to_string(cls) + "." + std::to_string(mid) +
+                             " (skipped:" + skipped + ")");
   }
   void open(const std::string& host, int port, const std::string& vhost) {
     if (!connect_to(host, port)) throw std::runtime_error("loadgen: cannot connect");
