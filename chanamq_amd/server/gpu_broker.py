@@ -23,6 +23,7 @@ pseudo-connection in the next step, Tx.Rollback drops them.  Not on the GPU path
 Sharded: consumers and Basic.Get may name a queue another rank owns (parallel/links.py).
 """
 
+import collections
 import logging
 import os
 import selectors
@@ -230,6 +231,7 @@ class GpuBroker:
         self.io = io
         self.io_threads = io_threads
         self.fe_cfg = dict(fe_cfg or {})
+        self.ctl_trace = collections.deque(maxlen=4000) if os.environ.get("CHANAMQ_CTL_TRACE") else None
         self.persist_group_ms = persist_group_ms    # extra native front-end settings (frontend.hpp FrontendCfg)
         self.gw = None
         self.fe = None
@@ -1282,6 +1284,8 @@ class GpuBroker:
         if t != C.FRAME_METHOD:
             raise _Hard(C.UNEXPECTED_FRAME, "content frame without a method")
         m = decode_method(raw[7:7 + size])
+        if self.ctl_trace is not None:   # (diagnostics: CHANAMQ_CTL_TRACE=1)
+            self.ctl_trace.append((round(time.monotonic(), 4), c.id, ch, m.name, self.lock.deferring, self.lock.paused_at))
         if ch in c.closing_channels:
             if m.name == "channel.close_ok":
                 c.closing_channels.discard(ch)
@@ -1988,6 +1992,9 @@ class GpuBroker:
         if not c.out or c.state == "closed":
             return
         if self.fe is not None:
+            if self.ctl_trace is not None:
+                self.ctl_trace.append((round(time.monotonic(), 4), c.id, "flush", len(c.out),
+                                       self.lock.deferring and c.state == "open" and not direct))
             if self.lock.deferring and c.state == "open" and not direct:
                 # behind the deliveries of the steps in flight and the step carrying this
                 # command's table writes
