@@ -200,11 +200,9 @@ def run_one(core, name, spec, io, io_threads, seconds, rate=0.0, lg_threads=12, 
                   file=sys.stderr, flush=True)
             tr = list(b.ctl_trace or [])
             if tr:   # the connections whose last queue.declare has no queue.purge after it
-                last = {}
-                for e in tr:
-                    if e[2] != "flush" and e[3] in ("queue.declare", "queue.purge"):
-                        last[e[1]] = e[3]
-                for cid in [k for k, v in last.items() if v == "queue.declare"]:
+                admin = sorted({e[1] for e in tr if e[2] != "flush" and e[3] == "queue.declare"
+                                and str(e[6] or "").startswith("e2e.")})
+                for cid in admin:
                     print(f"--- trace conn {cid}:", [e for e in tr if e[1] == cid][-40:], file=sys.stderr, flush=True)
             import traceback
             for tid, fr in sys._current_frames().items():   # where the control thread is

@@ -231,7 +231,7 @@ class GpuBroker:
         self.io = io
         self.io_threads = io_threads
         self.fe_cfg = dict(fe_cfg or {})
-        self.ctl_trace = collections.deque(maxlen=4000) if os.environ.get("CHANAMQ_CTL_TRACE") else None
+        self.ctl_trace = collections.deque(maxlen=400000) if os.environ.get("CHANAMQ_CTL_TRACE") else None
         self.persist_group_ms = persist_group_ms    # extra native front-end settings (frontend.hpp FrontendCfg)
         self.gw = None
         self.fe = None
@@ -1285,7 +1285,8 @@ class GpuBroker:
             raise _Hard(C.UNEXPECTED_FRAME, "content frame without a method")
         m = decode_method(raw[7:7 + size])
         if self.ctl_trace is not None:   # (diagnostics: CHANAMQ_CTL_TRACE=1)
-            self.ctl_trace.append((round(time.monotonic(), 4), c.id, ch, m.name, self.lock.deferring, self.lock.paused_at))
+            self.ctl_trace.append((round(time.monotonic(), 4), c.id, ch, m.name, self.lock.deferring, self.lock.paused_at,
+                                   getattr(m, "queue", None)))
         if ch in c.closing_channels:
             if m.name == "channel.close_ok":
                 c.closing_channels.discard(ch)
