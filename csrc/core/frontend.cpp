@@ -394,6 +394,17 @@ void Frontend::materialize(Scatter& sc, const u8* egress, u64 bytes) {
   sc.gath_off = 0;
 }
 
+// the connections a submitted step unpauses get their carries re-presented by the next
+// gather (Python kicks them when it stages the unpause, but inside a light section that
+// kick can be spent on a step submitted before the batch carrying the unpause closed --
+// the connection would then sit paused-free with its next command stuck in the carry)
+void Frontend::kick_unpaused(int p) {
+  if (!api_->unpaused) return;
+  const u32* l = nullptr;
+  const u32 n = api_->unpaused(api_->eng, p, &l);
+  for (u32 k = 0; k < n && l; ++k) kick(l[k]);
+}
+
 // egress by reference for the next submitted step only when it gathered enough bytes
 void Frontend::ref_for_step(u64 used) {
   if (narena_ != NARENA) return;
@@ -1399,6 +1410,7 @@ void Frontend::stepper() {
         }
         last_submit_ = t1;
       }
+      kick_unpaused(p);
       f.p = p;
       f.step = ++step_no_;
       f.batch_hi = api_->dl_state ? api_->dl_state(api_->eng, 1) : 0;
@@ -1573,6 +1585,7 @@ void Frontend::stepper_sharded() {
     }
     if (!check(p)) break;
     arena_i_ = (arena_i_ + 1) % narena_;
+    kick_unpaused(p);
     f.p = p;
     f.step = ++step_no_;
     f.batch_hi = api_->dl_state ? api_->dl_state(api_->eng, 1) : 0;
@@ -1634,6 +1647,7 @@ void Frontend::stepper_sharded() {
         if (rc == -2) { xfail = true; if (dropx(xpend_) == -1) { bad = true; break; } }
         if (!check(api_->launch_b(api_->eng, p2))) { bad = true; break; }
         Inflight f2;
+        kick_unpaused(p2);
         f2.p = p2;
         f2.step = ++step_no_;
         f2.batch_hi = api_->dl_state ? api_->dl_state(api_->eng, 1) : 0;

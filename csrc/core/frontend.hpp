@@ -138,6 +138,7 @@ class Frontend {
   std::vector<FeEvent> poll_events(int timeout_ms);
   std::string take(u32 conn);                           // host-mode bytes received so far
   void ref_for_step(u64 used);
+  void kick_unpaused(int p);
   void send(u32 conn, const char* data, size_t n);      // append to the connection's output
   void send_egress(const u8* egress, const ConnOut* co, u32 n_slots);   // a host-run step's egress
   void set_data_mode(u32 conn, const std::string& leftover);   // bytes now go to the GPU

@@ -922,6 +922,7 @@ class Engine {
     u32 nunp = 0;
     in->delta_bytes = pack_deltas(p, stage_unp_[p], &nunp);
     in->nunp = nunp;
+    nunp_[p] = nunp;
     if (in->nunp)
       HIPCHECK(hipMemcpyAsync((void*)io_[p].unpause_req, stage_unp_[p], 4ull * in->nunp, hipMemcpyHostToDevice, s_h2d_));
     dl_step_[p] = in->delta_bytes;
@@ -2117,6 +2118,12 @@ class Engine {
     a.get_out = [](void* e, int p) -> const GetOut* { return ((Engine*)e)->io_[p].get_out_hh; };
     a.host_work = [](void* e) -> int { return ((Engine*)e)->host_work() ? 1 : 0; };
     a.dl_state = [](void* e, int which) -> u64 { return ((Engine*)e)->dl_state(which); };
+    a.unpaused = [](void* e, int p, const u32** out) -> u32 {
+      Engine* en = (Engine*)e;
+      if (p < 0 || p > 1) return 0;
+      *out = en->stage_unp_[p];
+      return en->nunp_[p];
+    };
     a.set_egress_ref = [](void* e, int back, u32 min_bytes) -> int {
       return ((Engine*)e)->guard([&] { ((Engine*)e)->set_egress_ref(back, min_bytes); return 0; });
     };
@@ -2813,6 +2820,7 @@ class Engine {
   }
   GetReq* stage_gets_[2] = {nullptr, nullptr};
   u32* stage_unp_[2] = {nullptr, nullptr};
+  u32 nunp_[2] = {0, 0};   // unpauses the last submit on each parity carried
   u32 nget_[2] = {0, 0};
   HostIO io_[2];
   CmqEngineApi api_{};

@@ -116,7 +116,7 @@ struct GetOut { u32 status; u32 msg_count; };
 // C entry points of one Engine (engine.hip: Engine::c_api).  All return 0 / a parity on
 // success and -1 on error (message: error()).  Parity p = the double-buffered step IO set
 // of a submitted step; its host-mapped outputs stay valid until the next submit of p.
-#define CMQ_STEP_ABI 8
+#define CMQ_STEP_ABI 9
 #define PSLOTS 4                // rotating host store-record slots (a step's records live PSLOTS - 1 more steps)
 #define UNPAUSE_STEP_MAX 1024   // connections unpaused per step (StepIn.nunp)
 struct CmqEngineApi {
@@ -183,5 +183,9 @@ struct CmqEngineApi {
   // staging goes into now, 1 = the highest id every batch up to which a submitted step has
   // taken (a reply tied to batch b may leave once the step that took b has finished)
   u64 (*dl_state)(void* eng, int which);
+  // the connections whose unpause the last submit on parity p carried (k_stage clears their
+  // flag): the caller re-presents their carries from the next step on -- a light section's
+  // kick may have been spent on a step submitted before its batch closed
+  u32 (*unpaused)(void* eng, int p, const u32** conns);
 };
 #define GROW_MAX 4096   // grow requests reported per step
