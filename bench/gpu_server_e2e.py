@@ -53,7 +53,7 @@ def plane_for(spec):
     persist = bool(spec.get("persistent"))
     return GpuDataPlane(c_max=512, chpc=8, q_max=256, cons_max=1024, seg_max=512, cmd_max=1 << 17,
                         deliv_max=1 << 17, msg_max=1 << 21, ucap=8192, deliver_cap=8192,
-                        ingress_cap=64 << 20, egress_cap=160 << 20, log_bytes=8 << 30, ring_pool=1 << 25,
+                        ingress_cap=64 << 20, egress_cap=160 << 20, log_bytes=8 << 30, ring_pool=1 << 27,
                         spill_bytes=SIZING.get("spill_bytes", 8 << 30),   # (default tiering: old bodies leave HBM)
                         tb_max=256, default_queue_capacity=1 << 20, persist=int(persist),
                         persist_max=1 << 16, persist_bytes=512 << 20, carry_cap=SIZING["carry_cap"])
@@ -176,7 +176,7 @@ def run_one(core, name, spec, io, io_threads, seconds, rate=0.0, lg_threads=12, 
     cproc, cout = None, None
     if churn:
         cproc = churn_start(b.port, *churn)
-    st0 = dict(b.stats)
+    st0 = {k: (dict(v) if isinstance(v, dict) else v) for k, v in b.stats.items()}
     try:
         if cproc is not None:
             cproc.stdin.write("go\n")
@@ -218,7 +218,7 @@ def run_one(core, name, spec, io, io_threads, seconds, rate=0.0, lg_threads=12, 
             gout = stop_pollers(gproc)
         if cproc is not None:
             cout = churn_stop(cproc)
-        st1 = dict(b.stats)
+        st1 = {k: (dict(v) if isinstance(v, dict) else v) for k, v in b.stats.items()}
         smp.join()
         cpu1 = thread_cpu()
         after = {}
@@ -295,7 +295,9 @@ def run_one(core, name, spec, io, io_threads, seconds, rate=0.0, lg_threads=12, 
                            device_gets=st.get("device_gets", 0)) if n_getters else None),
              last_step={k: lc.get(k) for k in ("n_ring_full", "n_dropped_nomem")},
              churn=cout,
-             control_sections={k: st1.get(k, 0) - st0.get(k, 0) for k in ("pauses", "light_sections")},
+             control_sections=dict({k: st1.get(k, 0) - st0.get(k, 0) for k in ("pauses", "light_sections")},
+                                   pause_why={k: v - (st0.get("pause_why") or {}).get(k, 0)
+                                              for k, v in (st1.get("pause_why") or {}).items()}),
              store=getattr(b, "_pw_stats", None), body_log=body_log)
     del plane
     return r
