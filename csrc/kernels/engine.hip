@@ -1084,12 +1084,16 @@ class Engine {
       if (!bt.w.empty() || !bt.dirty.empty()) return true;
     return false;
   }
-  // the oldest staged batch into parity p's host-mapped delta buffer: bytes used (0 = none).
-  // What does not fit (records or bytes) stays for a later step: records are independent
-  // bytes, and the control plane keeps a change set within one step by staging it whole
-  // under its lock before any unpause (it checks deltas_pending() against the limits)
-  // The batch's unpauses go to unp (at most UNPAUSE_STEP_MAX, *nunp) or, with unp null
-  // (flush_deltas: no step), to unp_ready_ for the next submitted step.
+  // staged batches, oldest first, into parity p's host-mapped delta buffer: bytes used (0 =
+  // none).  The oldest batch may go in part (what does not fit -- records or bytes -- stays
+  // for a later step; records are independent bytes, and the control plane keeps a change
+  // set within one step by cutting its batches at deltas_pending() limits); later closed
+  // batches ride the same step whole, as long as they fit and write no byte an earlier
+  // record of the step writes (k_apply_deltas applies a step's records in parallel).  One
+  // batch per step capped the light sections at the step rate: under connection / RPC
+  // churn on a slower (durable) broker they queued up until a full pause flushed them.
+  // A batch's unpauses go with its last records to unp (at most UNPAUSE_STEP_MAX, *nunp) or,
+  // with unp null (flush_deltas: no step), to unp_ready_ for the next submitted step.
   u32 pack_deltas(int p, u32* unp, u32* nunp) {
     std::lock_guard<std::mutex> g(dl_mu_);
     u32 nu = 0;
@@ -1102,59 +1106,102 @@ class Engine {
       }
       v.erase(v.begin(), v.begin() + k);
     };
+    auto done = [&](u32 r) { if (nunp) *nunp = nu; return r; };
     if (unp) take_unp(unp_ready_);
     // a step (unp set) never takes a batch a light section is still staging into;
     // flush_deltas (between steps, the control plane holds the engine) takes everything
-    if (unp && !dl_.empty() && dl_.front().open) { if (nunp) *nunp = nu; return 0; }
-    while (!dl_.empty() && dl_.front().w.empty() && dl_.front().dirty.empty()) {
-      if (unp && dl_.front().open) break;
-      take_unp(dl_.front().unp);   // a batch of unpauses only (no writes)
-      if (!dl_.front().unp.empty()) break;
-      if (dl_.size() == 1) { dl_.pop_front(); break; }
+    auto usable = [&](const DlBatch& bt) { return !(unp && bt.open); };
+    // leading batches with no writes: their unpauses only
+    while (!dl_.empty() && usable(dl_.front()) && dl_.front().w.empty() && dl_.front().dirty.empty()) {
+      take_unp(dl_.front().unp);
+      if (!dl_.front().unp.empty()) return done(0);   // (the step's unpause list is full)
+      if (dl_.size() == 1 && dl_.front().open) { dl_.pop_front(); break; }
       dl_.pop_front();
     }
-    if (nunp) *nunp = nu;
-    if (dl_.empty() || (dl_.front().w.empty() && dl_.front().dirty.empty()) || (unp && dl_.front().open)) {
-      if (nunp) *nunp = nu;
-      return 0;
-    }
-    DlBatch& bt = dl_.front();
-    u8* o = dl_h_[p];
-    const u32 ndirty = (u32)std::min<size_t>(bt.dirty.size(), 4096);
-    u64 nrec = 0, nchunk = 0;
-    for (auto& kv : bt.w) {
+    if (dl_.empty() || !usable(dl_.front()) || (dl_.front().w.empty() && dl_.front().dirty.empty())) return done(0);
+    // ---- plan: how many records of the first batch, then which whole batches follow
+    u64 nrec = 0, nchunk = 0, ndirty = 0;
+    std::map<u64, u64> iv;   // byte ranges [dst, end) written by the records planned so far
+    auto overlaps = [&](u64 d0, u64 d1) {
+      auto it = iv.lower_bound(d0);
+      if (it != iv.end() && it->first < d1) return true;
+      if (it != iv.begin() && std::prev(it)->second > d0) return true;
+      return false;
+    };
+    auto need = [&](u64 r, u64 dn, u64 ch) { return 16 + 16 * r + ((4 * dn + 15) & ~15ull) + 16 * ch; };
+    DlBatch& b0 = dl_.front();
+    const u64 nd0 = std::min<u64>(b0.dirty.size(), 4096);
+    u64 n0 = 0;
+    for (auto& kv : b0.w) {
       const u64 ch = (kv.second.size() + 15) / 16;
-      const u64 need = 16 + 16 * (nrec + 1) + ((4ull * ndirty + 15) & ~15ull) + 16 * (nchunk + ch);
-      if (nrec == DELTA_REC_MAX || need > DELTA_CAP) break;
+      if (nrec == DELTA_REC_MAX || need(nrec + 1, nd0, nchunk + ch) > DELTA_CAP) break;
       ++nrec;
       nchunk += ch;
+      iv[kv.first] = kv.first + kv.second.size();
+      ++n0;
     }
+    ndirty = nd0;
+    size_t nwhole = 0;   // later batches taken whole
+    if (n0 == b0.w.size() && nd0 == b0.dirty.size() && b0.unp.size() + nu <= UNPAUSE_STEP_MAX) {
+      u32 nu_plan = nu + (u32)b0.unp.size();
+      for (size_t k = 1; k < dl_.size(); ++k) {
+        DlBatch& bt = dl_[k];
+        if (!usable(bt)) break;
+        u64 r = nrec, ch = nchunk;
+        const u64 dn = ndirty + bt.dirty.size();
+        bool ok = dn <= 4096 && nu_plan + bt.unp.size() <= UNPAUSE_STEP_MAX;
+        for (auto it = bt.w.begin(); ok && it != bt.w.end(); ++it) {
+          ++r;
+          ch += (it->second.size() + 15) / 16;
+          ok = r <= DELTA_REC_MAX && need(r, dn, ch) <= DELTA_CAP &&
+               !overlaps(it->first, it->first + it->second.size());
+        }
+        if (!ok) break;
+        for (auto& kv : bt.w) iv[kv.first] = kv.first + kv.second.size();
+        nrec = r;
+        nchunk = ch;
+        ndirty = dn;
+        nu_plan += (u32)bt.unp.size();
+        ++nwhole;
+      }
+    }
+    // ---- write: head, records, dirty channels, data
+    u8* o = dl_h_[p];
     DeltaHead* h = (DeltaHead*)o;
-    h->nrec = (u32)nrec; h->ndirty = ndirty; h->nchunk = (u32)nchunk; h->pad = 0;
+    h->nrec = (u32)nrec; h->ndirty = (u32)ndirty; h->nchunk = (u32)nchunk; h->pad = 0;
     DeltaRec* recs = (DeltaRec*)(o + sizeof(DeltaHead));
     u32* dirty = (u32*)(recs + nrec);
     u8* data = (u8*)dirty + ((4ull * ndirty + 15) & ~15ull);
-    u64 r = 0, c = 0;
-    for (auto it = bt.w.begin(); it != bt.w.end() && r < nrec;) {
-      recs[r].dst = it->first;
-      recs[r].len = (u32)it->second.size();
-      recs[r].chunk0 = (u32)c;
-      memcpy(data + 16 * c, it->second.data(), it->second.size());
-      c += (it->second.size() + 15) / 16;
-      bt.bytes -= it->second.size();
-      dl_bytes_ -= it->second.size();
-      it = bt.w.erase(it);
-      ++r;
+    u64 r = 0, c = 0, di = 0;
+    auto put = [&](DlBatch& bt, u64 nr, u64 ndr) {
+      u64 k = 0;
+      for (auto it = bt.w.begin(); it != bt.w.end() && k < nr; ++k) {
+        recs[r].dst = it->first;
+        recs[r].len = (u32)it->second.size();
+        recs[r].chunk0 = (u32)c;
+        memcpy(data + 16 * c, it->second.data(), it->second.size());
+        c += (it->second.size() + 15) / 16;
+        bt.bytes -= it->second.size();
+        dl_bytes_ -= it->second.size();
+        it = bt.w.erase(it);
+        ++r;
+      }
+      for (u64 k2 = 0; k2 < ndr; ++k2) dirty[di++] = bt.dirty[k2];
+      bt.dirty.erase(bt.dirty.begin(), bt.dirty.begin() + ndr);
+    };
+    put(b0, n0, nd0);
+    size_t gone = 0;   // leading batches fully taken (unpauses included)
+    for (size_t k = 0; k <= nwhole; ++k) {
+      DlBatch& bt = dl_[k];
+      if (k) put(bt, bt.w.size(), bt.dirty.size());
+      if (!bt.w.empty() || !bt.dirty.empty()) break;   // (the first batch went in part)
+      take_unp(bt.unp);   // the whole batch went: its unpauses ride along
+      if (!bt.unp.empty()) break;
+      ++gone;
     }
-    for (u32 k = 0; k < ndirty; ++k) dirty[k] = bt.dirty[k];
-    bt.dirty.erase(bt.dirty.begin(), bt.dirty.begin() + ndirty);
-    if (bt.w.empty() && bt.dirty.empty()) {   // the whole batch went: its unpauses ride along
-      take_unp(bt.unp);
-      if (bt.unp.empty()) dl_.pop_front();
-      if (nunp) *nunp = nu;
-    }
+    for (size_t k = 0; k < gone; ++k) dl_.pop_front();
     ++dl_steps_;
-    return (u32)((data - o) + 16 * c);
+    return done((u32)((data - o) + 16 * c));
   }
   // between steps (the control plane holds the engine): apply what is staged now
   void flush_deltas() {
