@@ -254,13 +254,39 @@ class GpuDataPlane(ControlState):
                           ("t_kb_len", t_kb_len), ("t_flags", t_flags), ("t_expect", t_expect),
                           ("t_mat", t_mat), ("t_woff", t_woff),
                           ("t_count", np.array([len(tb), 0, 0, 0], np.uint32))):
-            self._up(name, arr)
+            self._up_diff(name, arr)
         if fan_q:
-            self._up("fan_q", np.array(fan_q, np.uint32))
+            self._up_diff("fan_q", np.array(fan_q, np.uint32))
         if d_q:
-            self._up("d_q", np.array(d_q, np.uint32))
+            self._up_diff("d_q", np.array(d_q, np.uint32))
         if kpool:
-            self._up("kpool", np.frombuffer(bytes(kpool), np.uint8))
+            self._up_diff("kpool", np.frombuffer(bytes(kpool), np.uint8))
+
+    _route_cache = None
+
+    def _up_diff(self, name, arr):
+        """A routing table: only the byte runs that differ from its last upload are written.
+        A declare / bind rebuilds every table on the host; staging them whole (MBs with a
+        large direct hash) in a light section overflowed the step's delta budget at once, so
+        RPC-style churn paused the stepper on every cycle."""
+        raw = np.ascontiguousarray(arr).view(np.uint8).reshape(-1)
+        if self._route_cache is None:
+            self._route_cache = {}
+        old = self._route_cache.get(name)
+        self._route_cache[name] = raw.copy()
+        if old is None or len(old) != len(raw):
+            self._write(name, raw, 0)
+            return
+        diff = np.flatnonzero(old != raw)
+        if not len(diff):
+            return
+        cut = np.flatnonzero(np.diff(diff) > 64)   # runs closer than 64 B are written as one
+        starts = np.concatenate((diff[:1], diff[cut + 1]))
+        ends = np.concatenate((diff[cut], diff[-1:])) + 1
+        if len(starts) > 16:   # scattered (e.g. key offsets shifted): one record, first to last
+            starts, ends = starts[:1], ends[-1:]
+        for a, b in zip(starts.tolist(), ends.tolist()):
+            self._write(name, raw[a:b], a)
 
     def _chmap_row(self, conn):
         size = self.info["chmap_size"]
