@@ -410,7 +410,9 @@ void Frontend::ref_for_step(u64 used) {
   if (narena_ != NARENA) return;
   const bool on = used >= cfg_.egress_ref_step_min;
   if (on == ref_on_) return;
-  api_->set_egress_ref(api_->eng, on ? 0 : -1, cfg_.egress_ref_min);
+  // (below the threshold spilled bodies still go from the host spill ring: large, and not
+  // in HBM -- rendering them would read them across PCIe and send them back again)
+  api_->set_egress_ref(api_->eng, on ? 0 : -2, cfg_.egress_ref_min);
   ref_on_ = on;
 }
 

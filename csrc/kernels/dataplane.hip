@@ -3432,6 +3432,7 @@ DEV u64 deliv_href(const DS& d, const MsgEnt& m, u32 conn) {
   if (fm != 0 && m.body_len > fm - 8) return 0;
   if ((m.log_off & (SPILL_BIT | COLD_BIT)) == SPILL_BIT && d.spill_host)
     return d.spill_host + ((m.log_off & ~SPILL_BIT) % d.spill_bytes) + m.body_off;
+  if (d.in->ref_back & REF_SPILL_ONLY) return 0;   // (ingress bodies inline this step)
   if (!m.href || (u32)d.in->step - m.pub_step > d.in->ref_back) return 0;
   return m.href;
 }

@@ -46,6 +46,8 @@ enum : u32 {
 enum : u32 { US_FREE = 0, US_PENDING = 1, US_ACKED = 2, US_REQUEUE = 3, US_DONE = 4 };
 
 
+// StepIn.ref_back flag: only bodies in the host spill ring go by reference this step
+#define REF_SPILL_ONLY 0x80000000u
 struct StepIn {         // host -> device per step (96 B)
   u32 nseg;
   u32 flags;

@@ -869,7 +869,7 @@ class Engine {
     StepIn* in = stage_in_[p];
     *in = StepIn{};
     in->nseg = nseg;
-    in->ref_back = ref_back_ >= 0 ? (u32)ref_back_ : 0xffffffffu;
+    in->ref_back = ref_back_ >= 0 ? (u32)ref_back_ : ref_back_ == -2 ? REF_SPILL_ONLY : 0xffffffffu;
     in->ref_min = ref_min_;
     in->ingress_host = ref_back_ >= 0 && payload_len ? payload_ptr : 0;
     in->flags = sflags;
@@ -2390,11 +2390,12 @@ class Engine {
   // egress slot (host view "egress_host<slot>") of the step last submitted with parity p
   int egress_slot(int p) const { return slot_of_[p]; }
   // egress by reference from the next submitted step on (StepIn.ref_back): bodies of the
-  // last `back` steps' ingress payloads (-1: off) of at least min_bytes are not rendered;
+  // last `back` steps' ingress payloads (-1: off; -2: only bodies in the host spill ring) of
+  // at least min_bytes are not rendered;
   // the caller keeps those payloads unchanged until the delivering step's egress is sent
   void set_egress_ref(int back, u32 min_bytes) {
     if (back > 64) throw std::runtime_error("set_egress_ref: at most 64 steps back");
-    ref_back_ = back < 0 ? -1 : back;
+    ref_back_ = back == -2 ? -2 : back < 0 ? -1 : back;
     ref_min_ = min_bytes < 16 ? 16 : min_bytes;
   }
   // store-record slot (host views "persist<slot>" / "consumed<slot>") of that step

@@ -175,7 +175,8 @@ struct CmqEngineApi {
   // without client bytes (null: never)
   int (*host_work)(void* eng);
   // egress by reference: deliveries of bodies from the ingress payload of the last `back`
-  // steps (0 = the same step; -1 = off), at least min_bytes long, are rendered without them
+  // steps (0 = the same step; -1 = off; -2 = only bodies spilled to the host ring), at least
+  // min_bytes long, are rendered without them
   // (Counters.n_ref / EgressRef).  The caller keeps those payloads unchanged until the
   // delivering step's egress is written out
   int (*set_egress_ref)(void* eng, int back, u32 min_bytes);
