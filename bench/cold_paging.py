@@ -148,6 +148,8 @@ def main():
         lt.start()
         time.sleep(1.0)   # the live stream's topology and warm-up
         st_a = dict(b.stats)
+        b._sync_fe_stats()
+        fe_a = dict(b._fe_stats)
         td = time.time()
         ths = [threading.Thread(target=drain, args=(k,)) for k in range(args.drainers)]
         for t in ths:
@@ -159,6 +161,8 @@ def main():
         for t in ths:
             t.join(timeout=10)
         st_b = dict(b.stats)
+        b._sync_fe_stats()
+        fe_b = dict(b._fe_stats)
         lt.join()
         stop[0] = True
         n = sum(got)
@@ -169,7 +173,12 @@ def main():
                             bodies_checked=checked[0], bodies_bad=bad[0], bad_examples=bad_ex,
                             pauses=st_b.get("pauses", 0) - st_a.get("pauses", 0),
                             cold_side_ops=st_b.get("cold_side_ops", 0) - st_a.get("cold_side_ops", 0),
-                            cold_errors=st_b.get("cold_errors", 0))
+                            cold_errors=st_b.get("cold_errors", 0),
+                            # the front end during the drain: step period / IO phase / result wait
+                            # (log2 us bins) and the IO threads' busiest phase
+                            front_end={k: [x - y for x, y in zip(fe_b[k], fe_a[k])] for k in
+                                       ("h_period_us_log2", "h_io_us_log2", "h_wait_us_log2", "h_submit_us_log2")
+                                       if k in fe_b and k in fe_a})
         out["live"] = {k: live.get(k) for k in ("sent", "received", "elapsed", "p50_us", "p95_us", "p99_us", "error")}
         print("drain", json.dumps(out["drain"]), flush=True)
         print("live", json.dumps(out["live"]), flush=True)

@@ -284,7 +284,16 @@ bool Frontend::write_some(FeConn& c) {
       continue;
     }
     if (k < 0 && errno == EINTR) continue;
-    if (k < 0 && (errno == EAGAIN || errno == EWOULDBLOCK)) return false;   // EPOLLOUT edge resumes
+    if (k < 0 && (errno == EAGAIN || errno == EWOULDBLOCK)) {   // EPOLLOUT edge resumes
+      // a consumer that never catches up never empties its queue: drop the sent prefix once
+      // it is half the buffer (else the string keeps every byte ever sent to it, and each
+      // growth copies them all -- multi-ms stalls of this IO thread in a cold drain)
+      if (c.out_pos >= (256u << 10) && 2 * c.out_pos >= c.out.size()) {
+        c.out.erase(0, c.out_pos);
+        c.out_pos = 0;
+      }
+      return false;
+    }
     c.out.clear();
     c.out_pos = 0;
     return false;   // broken: the IO thread sees EPOLLERR/HUP and drops it
