@@ -653,8 +653,18 @@ DEV void frame_scan_seg(const DS& d, const u32 s) {
   const u32 tid = threadIdx.x;
   const u32 conn = d.segs[s].conn;
   const u32 L = d.seg_total[s];
-  const u8* const bg = d.work + d.seg_start[s];   // the segment in the work buffer (HBM)
-  const u8* b = bg;                              // switched to the LDS stage after the screen
+  const u32 seg_len = d.segs[s].len, seg_cl = L - seg_len;
+  // a segment with no carry is scanned where its H2D put it: the ingress slots follow the
+  // work buffers in one allocation, so a u32 offset from d.work reaches them and every
+  // later reader (decode, route-store, returns, gets) takes the bytes from there -- one HBM
+  // copy of the step's bytes less.  (seg_start then records that offset: k_decode's
+  // body-reference arithmetic.)  Single GPU: sharded steps read imports beside the work.
+  const u64 ing_rel = (u64)d.in->ingress - (u64)d.work;
+  const bool inplace = d.world == 1 && seg_cl == 0 && L > 0 && (u64)d.in->ingress > (u64)d.work &&
+                       ing_rel + d.segs[s].src + L + 64 < (1ull << 32) && d.tot[15] <= d.work_cap;
+  const u32 wbase = inplace ? (u32)(ing_rel + d.segs[s].src) : d.seg_start[s];
+  const u8* const bg = d.work + wbase;   // the segment in HBM: the work buffer or its ingress slot
+  const u8* b = bg;                      // switched to the LDS stage after the screen
   // the pool for this segment: [stage] wend cpos chain/amask csucc claim
   const u32 nm16 = (L + 15) >> 4;
   const bool staged = nm16 * 16 + 32 <= FS_STAGE;
@@ -673,17 +683,16 @@ DEV void frame_scan_seg(const DS& d, const u32 s) {
   int16_t* const csucc = (int16_t*)(chain_am + (staged ? FS_CAND_STAGED : (CAND_MAX > FS_AM_MAX ? CAND_MAX : FS_AM_MAX)));
   u8* const claim = (u8*)(csucc + cmax);
   const u32 fmax = d.conn_frame_max[conn];
-  const u32 wbase = d.seg_start[s];
   FS_MARK(15);
-  const u32 seg_len = d.segs[s].len, seg_cl = L - seg_len;
   const u8* const seg_C = d.carry + (u64)conn * d.carry_cap;
   const u8* const seg_N = (const u8*)d.in->ingress + d.segs[s].src;
   // the common segment is copied into the work buffer by the screen pass itself: one read
   // of the sources, the work copy, the LDS stage and the candidate mask from the same
   // registers (was: a copy pass, then the screen re-reading the copy)
   const bool fit = d.tot[15] <= d.work_cap;
-  const bool fuse = fit && L > 0 && ((L + 15) >> 4) <= FS_AM_MAX && !d.conn_paused[conn];
-  if (fit && !fuse) {
+  const bool fuse = fit && !inplace && L > 0 && ((L + 15) >> 4) <= FS_AM_MAX && !d.conn_paused[conn];
+  if (inplace && tid == 0) d.seg_start[s] = wbase;
+  if (fit && !fuse && !inplace) {
     // the segment into the work buffer (fused k_stage copy): the connection's carry, then
     // its new ingress bytes.  k_decode / k_route_store read publishes from there
     u8* const dst = d.work + wbase;

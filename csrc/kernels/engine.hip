@@ -60,6 +60,7 @@ struct Buf {
   void* ptr = nullptr;
   size_t bytes = 0;
   bool host = false;
+  bool view = false;   // a named range of another allocation (not freed on its own)
 };
 
 class Engine {
@@ -207,6 +208,17 @@ class Engine {
     d_.ctr = (Counters*)dev("ctr", sizeof(Counters));
     // (+ the gather table of egress by reference: one EgressRef per delivery)
     egress_alloc_ = d_.egress_cap + d_.work_cap + (u64)nch * 21 + 4096 + 16ull * d_.deliv_max;
+    // the two parities' work buffers and the ingress slots in one allocation, the slots
+    // last: a u32 offset from either work buffer reaches them, so a segment without a
+    // carry is scanned and read where its H2D put it (k_frame_scan in place: no work copy)
+    {
+      const u64 wb = (d_.work_cap + 4096 + 255) & ~255ull, ib = (d_.ingress_cap + 64 + 255) & ~255ull;
+      u8* base = (u8*)dev("work_all", 2 * wb + INGRESS_SLOTS * ib);
+      d_.work = (u8*)view("work", base, d_.work_cap + 4096);   // imports are read in place (k_import_route)
+      work_p1_ = (u8*)view("work_p1", base + wb, d_.work_cap + 4096);
+      for (int k = 0; k < INGRESS_SLOTS; ++k)
+        ingress_slot_[k] = (u8*)view(("ingress_s" + std::to_string(k)).c_str(), base + 2 * wb + k * ib, d_.ingress_cap + 64);
+    }
     // per-parity step IO: step t uses set t&1, so step t+1's H2D and step t-1's D2H
     // overlap step t's kernels (double buffering; the graph of each parity is captured once)
     for (int p = 0; p < 2; ++p) {
@@ -217,9 +229,6 @@ class Engine {
       // ingress payloads rotate over INGRESS_SLOTS buffers by step (StepIn.ingress): the
       // next step's payload goes into a slot whose last reader (three steps back) is known
       // done, so an early H2D never waits on the GPU
-      if (p == 0)
-        for (int k = 0; k < INGRESS_SLOTS; ++k)
-          ingress_slot_[k] = (u8*)dev(("ingress_s" + std::to_string(k)).c_str(), d_.ingress_cap + 64);
       io.ingress = ingress_slot_[p];
       io.seg_out = (SegOut*)dev(("seg_out_d" + sfx).c_str(), sizeof(SegOut) * d_.seg_max);
       io.seg_out_h = (SegOut*)hst(("seg_out" + sfx).c_str(), sizeof(SegOut) * d_.seg_max);
@@ -294,7 +303,6 @@ class Engine {
     // up to DEC_SEG_LDS segments k_decode numbers publishes / acks from the frame scan's
     // per-segment ordinals (segment prefix in LDS): no rank scan over the commands
     d_.rank_scan = d_.seg_max > DEC_SEG_LDS ? 1u : 0u;
-    d_.work = (u8*)dev("work", d_.work_cap + 4096);   // imports are read in place (k_import_route)
 
     d_.cmds = (Cmd*)dev("cmds", sizeof(Cmd) * (u64)d_.cmd_max);
     d_.frags = (Frag*)dev("frags", sizeof(Frag) * ((u64)d_.frag_max + d_.import_max));
@@ -528,7 +536,7 @@ class Engine {
     dup(&DS::seg_cmd_base, "seg_cmd_base", 4ull * d_.seg_max);
     dup(&DS::seg_npub, "seg_npub", 4ull * d_.seg_max);
     dup(&DS::seg_nack, "seg_nack", 4ull * d_.seg_max);
-    dup(&DS::work, "work", d_.work_cap + 4096);
+    par1_.push_back([this](DS& io) { io.work = work_p1_; });   // (allocated with the ingress slots)
     dup(&DS::cmds, "cmds", sizeof(Cmd) * (u64)d_.cmd_max);
     dup(&DS::frags, "frags", sizeof(Frag) * ((u64)d_.frag_max + d_.import_max));
     dup(&DS::cmd_is_pub, "cmd_is_pub", 4ull * d_.cmd_max);
@@ -695,6 +703,7 @@ class Engine {
     (void)hipStreamDestroy(s_h2d_);
     (void)hipStreamDestroy(s_d2h_);
     for (auto& kv : bufs_) {
+      if (kv.second.view) continue;
       if (kv.second.host) (void)hipHostFree(kv.second.ptr);
       else (void)hipFree(kv.second.ptr);
     }
@@ -732,6 +741,16 @@ class Engine {
       return dp;
     }
     return b.ptr;
+  }
+
+  // a named device range inside an allocation made with alloc()
+  void* view(const char* name, void* ptr, size_t bytes) {
+    Buf b;
+    b.ptr = ptr;
+    b.bytes = bytes;
+    b.view = true;
+    bufs_[name] = b;
+    return ptr;
   }
 
   const Buf& buf(const std::string& name) const {
@@ -1275,11 +1294,6 @@ class Engine {
       }
       HIPCHECK(hipEventRecord(ev_ing_[p], s_ing_));
       ing_issued_[p] = true;
-      {
-        const int is = (int)(launch_seq_[p] % INGRESS_SLOTS);
-        HIPCHECK(hipEventRecord(ev_ing_slot_[is], s_ing_));
-        ing_slot_issued_[is] = true;
-      }
       HIPCHECK(hipStreamWaitEvent(s_comp_, ev_ing_[p], 0));
       if (d2h_issued_[e]) HIPCHECK(hipStreamWaitEvent(s_comp_, ev_d2h_[e], 0));
       {
@@ -1289,6 +1303,11 @@ class Engine {
       }
       HIPCHECK(hipEventRecord(ev_rest_[p], s_comp_));
       rest_issued_[p] = true;
+      {   // the ingress slot's last reader: the routing half (segments scanned in place)
+        const int is = (int)(launch_seq_[p] % INGRESS_SLOTS);
+        HIPCHECK(hipEventRecord(ev_ing_slot_[is], s_comp_));
+        ing_slot_issued_[is] = true;
+      }
       HIPCHECK(hipEventRecord(ev_done_[p], s_comp_));
       gated_copy(e);
       if (copy_mode_ == 2) {   // egress D2H right behind the step, sized on the device
@@ -2849,6 +2868,7 @@ class Engine {
   bool eager_d2h_[2] = {false, false};   // the step's egress copy was queued at launch (copy_mode 2)
   bool pre_[2] = {false, false};
   u8* ingress_slot_[INGRESS_SLOTS] = {};
+  u8* work_p1_ = nullptr;
   hipEvent_t ev_ing_slot_[INGRESS_SLOTS];
   bool ing_slot_issued_[INGRESS_SLOTS] = {};
   u64 launch_seq_[2] = {0, 0};          // the step number staged in each parity
