@@ -649,20 +649,25 @@ DEV void frame_scan_seg(const DS& d, const u32 s) {
   __shared__ u32 sh_m, sh_over, sh_ok, sh_nf, sh_stop, sh_brk;
   __shared__ u32 sh_cmd_base, sh_frag_base, sh_ncmd;
   __shared__ u32 sh_get0, sh_gch, sh_gq, sh_gna, sh_gbase;   // Basic.Get: the segment's first, its key
+  __shared__ u32 sh_split;   // split mode: bytes [0, sh_split) are in the work buffer
 
   const u32 tid = threadIdx.x;
   const u32 conn = d.segs[s].conn;
   const u32 L = d.seg_total[s];
-  const u32 seg_len = d.segs[s].len, seg_cl = L - seg_len;
-  // a segment with no carry is scanned where its H2D put it: the ingress slots follow the
-  // work buffers in one allocation, so a u32 offset from d.work reaches them and every
-  // later reader (decode, route-store, returns, gets) takes the bytes from there -- one HBM
-  // copy of the step's bytes less.  (seg_start then records that offset: k_decode's
-  // body-reference arithmetic.)  Single GPU: sharded steps read imports beside the work.
+  const u32 seg_len = d.segs[s].len, seg_cl = L - seg_len, src = d.segs[s].src;
+  // the step's new bytes are read where their H2D put them: the ingress slots follow the
+  // work buffers in one allocation, so a u32 offset from d.work reaches them, and every
+  // later reader (decode, route-store, returns, gets) takes a frame's bytes from there.  A
+  // segment with no carry is scanned in place (nothing goes to the work buffer); one with a
+  // carry is staged in LDS by the screen and only its head -- the carry and the frame that
+  // straddles into the new bytes -- is written to the work buffer (split mode, OFF below):
+  // the work copy of the step's bytes is gone.  Single GPU (sharded steps read imports
+  // beside the work buffer).
   const u64 ing_rel = (u64)d.in->ingress - (u64)d.work;
-  const bool inplace = d.world == 1 && seg_cl == 0 && L > 0 && (u64)d.in->ingress > (u64)d.work &&
-                       ing_rel + d.segs[s].src + L + 64 < (1ull << 32) && d.tot[15] <= d.work_cap;
-  const u32 wbase = inplace ? (u32)(ing_rel + d.segs[s].src) : d.seg_start[s];
+  const bool ing_ok = d.world == 1 && (u64)d.in->ingress > (u64)d.work && ing_rel + src + L + 64 < (1ull << 32) &&
+                      d.tot[15] <= d.work_cap;
+  const bool inplace = ing_ok && seg_cl == 0 && L > 0;
+  const u32 wbase = inplace ? (u32)(ing_rel + src) : d.seg_start[s];
   const u8* const bg = d.work + wbase;   // the segment in HBM: the work buffer or its ingress slot
   const u8* b = bg;                      // switched to the LDS stage after the screen
   // the pool for this segment: [stage] wend cpos chain/amask csucc claim
@@ -691,7 +696,7 @@ DEV void frame_scan_seg(const DS& d, const u32 s) {
   // registers (was: a copy pass, then the screen re-reading the copy)
   const bool fit = d.tot[15] <= d.work_cap;
   const bool fuse = fit && !inplace && L > 0 && ((L + 15) >> 4) <= FS_AM_MAX && !d.conn_paused[conn];
-  if (inplace && tid == 0) d.seg_start[s] = wbase;
+  const bool split = fuse && staged && ing_ok;   // (the screen then leaves the work buffer alone)
   if (fit && !fuse && !inplace) {
     // the segment into the work buffer (fused k_stage copy): the connection's carry, then
     // its new ingress bytes.  k_decode / k_route_store read publishes from there
@@ -769,7 +774,7 @@ DEV void frame_scan_seg(const DS& d, const u32 s) {
           if (c < nm) {
             amask[c] = (u16)cand_bits(x[k], y[k], fmg);
             if (staged) fs_stage[c] = x[k];
-            if (fuse) WD[c] = x[k];
+            if (fuse && !split) WD[c] = x[k];
           }
         }
       }
@@ -1106,6 +1111,28 @@ DEV void frame_scan_seg(const DS& d, const u32 s) {
   if (over && reason != 0 && kf == nf) so.status |= SS_OVERFLOW;
   if (reason == 4) so.status |= SS_OVERFLOW;   // the carry is re-presented to the next step
 
+  // split mode: the work buffer gets the carry and the frame that runs from it into the new
+  // bytes (frames start inside the carry only before that point); later frames are read from
+  // the ingress slot
+  if (split) {
+    if (tid == 0) sh_split = seg_cl;
+    __syncthreads();
+    for (u32 f = tid; f < nf; f += FS_NT) {
+      const u32 p = CPOS(f);
+      if (p >= seg_cl) continue;
+      const FInfo fi = frame_at(b, p, L, fmax);
+      const u64 e = fi.complete ? (u64)p + 8 + fi.size : (u64)L;
+      atomicMax(&sh_split, (u32)(e < L ? e : L));
+    }
+    __syncthreads();
+    uint4* const WD = (uint4*)(d.work + wbase);
+    const u32 nw = (sh_split + 15) >> 4;
+    for (u32 w = tid; w < nw; w += FS_NT) WD[w] = fs_stage[w];
+    __syncthreads();
+  }
+  const u32 sp = split ? sh_split : inplace ? 0u : L + 1u;
+  // a frame's offset from d.work (frames lie wholly below sp or at / above it)
+  auto OFF = [&](u32 pos) -> u32 { return pos < sp ? wbase + pos : (u32)(ing_rel + src + pos - seg_cl); };
   FS_MARK(5);
   // ---- (e) emit commands for method frames < kf
   u32 run = 0, frun = 0;
@@ -1249,17 +1276,17 @@ DEV void frame_scan_seg(const DS& d, const u32 s) {
     if (is_cmd) {
       c.conn = conn;
       c.ch = fi.ch;
-      c.m_off = wbase + p + 7;
+      c.m_off = OFF(p) + 7;
       c.m_len = fi.size;
       c.h_off = 0; c.h_len = 0; c.frag0 = 0; c.nfrag = 0; c.body_size = 0;
       c.seg = s;
-      c.raw_off = wbase + p;
+      c.raw_off = OFF(p);
       // ordinals within the segment: k_decode numbers publishes / acks segment-major
       c.pad[1] = npub_run + ((rpk >> 11) & 0x7ffu);
       c.pad[2] = nack_run + (rpk >> 22);
       u32 endp = p + 8 + fi.size;
       if (cls == 60 && mid == 40) {
-        c.h_off = wbase + hp + 7;
+        c.h_off = OFF(hp) + 7;
         c.h_len = hi.size;
         c.body_size = (u32)be64(b + hp + 7 + 4);
         c.frag0 = sh_frag_base + frun + fr;
@@ -1269,7 +1296,7 @@ DEV void frame_scan_seg(const DS& d, const u32 s) {
           u32 bp = CPOS(f + 2 + k);
           FInfo bi = frame_at(b, bp, L, fmax);
           Frag fg;
-          fg.off = wbase + bp + 7;
+          fg.off = OFF(bp) + 7;
           fg.len = bi.size;
           d.frags[c.frag0 + k] = fg;
           endp = bp + 8 + bi.size;
@@ -1324,7 +1351,12 @@ DEV void frame_scan_seg(const DS& d, const u32 s) {
   // ---- (f) carry out: bytes [consumed, L)
   u32 rest = L - consumed;
   if (rest > d.carry_cap) { so.status |= SS_TOO_LARGE; rest = 0; }
-  else block_copy(d.carry + (u64)conn * d.carry_cap, bg + consumed, rest, tid, FS_NT);   // 16-B moves from HBM
+  else if (split) {   // [consumed, sp) from the work copy, the rest from the ingress slot (sp >= carry)
+    u8* const cd = d.carry + (u64)conn * d.carry_cap;
+    if (consumed < sp) block_copy(cd, d.work + wbase + consumed, sp - consumed, tid, FS_NT);
+    const u32 from = consumed > sp ? consumed : sp;
+    if (from < L) block_copy(cd + (from - consumed), seg_N + (from - seg_cl), L - from, tid, FS_NT);
+  } else block_copy(d.carry + (u64)conn * d.carry_cap, bg + consumed, rest, tid, FS_NT);   // 16-B moves from HBM
   FS_MARK(8);
   if (tid == 0) {
     so.consumed = consumed;
@@ -1726,7 +1758,11 @@ __global__ __launch_bounds__(256) void k_decode(DS d) {
         c.seg < nseg) {
       const Frag fg = d.frags[c.frag0];
       const u32 w0 = d.seg_start[c.seg], cl = d.seg_total[c.seg] - d.segs[c.seg].len;
-      if (fg.len == c.body_size && fg.off >= w0 + cl) {
+      const u64 ing_rel = (u64)d.in->ingress - (u64)d.work;
+      if (fg.len == c.body_size && (u64)d.in->ingress > (u64)d.work && fg.off >= ing_rel) {
+        pb.flags |= MF_HREF;   // (read in place from the ingress slot: its payload offset)
+        pb.pad = (u32)(fg.off - ing_rel);
+      } else if (fg.len == c.body_size && fg.off >= w0 + cl && fg.off < w0 + d.seg_total[c.seg]) {
         pb.flags |= MF_HREF;
         pb.pad = (u32)(d.segs[c.seg].src + (fg.off - w0 - cl));
       }
