@@ -335,7 +335,13 @@ class GpuBroker:
         self.light = _LightLock(self.lock)
 
     # ------------------------------------------------------------------ lifecycle
+    _live = None   # started, not yet stopped (tests stop what a failed test left running)
+
     def start(self):
+        import weakref
+        if GpuBroker._live is None:
+            GpuBroker._live = weakref.WeakSet()
+        GpuBroker._live.add(self)
         if self.io == "pipeline":
             from ..broker import load
             if hasattr(self.plane, "reserve_ring_chunk") and self.node is None:
@@ -398,6 +404,8 @@ class GpuBroker:
         return self
 
     def stop(self):
+        if GpuBroker._live is not None:
+            GpuBroker._live.discard(self)
         self._running = False
         os.write(self._wake_w, b"x")
         if self._thread:

@@ -31,3 +31,18 @@ def gpu():
     if not gpu_available():
         pytest.fail("GPU test requested but no GPU / data-plane extension available: " + "; ".join(_GPU_WHY))
     return True
+
+
+@pytest.fixture(autouse=True)
+def _stop_leftover_brokers():
+    """A GPU broker a failed test left running is stopped at its teardown: its native
+    threads would otherwise end the process with std::terminate at exit (abort, and the
+    GPU run stops there instead of reporting the failure)."""
+    yield
+    mod = sys.modules.get("chanamq_amd.server.gpu_broker")
+    live = getattr(getattr(mod, "GpuBroker", None), "_live", None) if mod else None
+    for b in list(live or []):
+        try:
+            b.stop()
+        except Exception:   # noqa: BLE001 - best effort
+            pass
