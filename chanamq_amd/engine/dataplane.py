@@ -11,6 +11,8 @@ import ctypes
 import time
 from collections import defaultdict
 
+import os
+
 import numpy as np
 
 from .. import ops
@@ -79,6 +81,8 @@ class GpuDataPlane(ControlState):
         self.mod = ops.load()
         full = dict(cfg)
         full.setdefault("egress_ref_back", -1 if egress_ref is None else int(egress_ref))
+        # (k_frame_scan reads new bytes in place; CHANAMQ_SCAN_IN_PLACE=0 for the copy path)
+        full.setdefault("scan_in_place", int(os.environ.get("CHANAMQ_SCAN_IN_PLACE", "1")))
         full.update(device=device, hash_wildcard=int(hash_wildcard), graph=int(graph), world=world, rank=rank,
                     exchange_lag=int(exchange_lag))
         self.eng = self.mod.Engine(full)

@@ -664,7 +664,7 @@ DEV void frame_scan_seg(const DS& d, const u32 s) {
   // the work copy of the step's bytes is gone.  Single GPU (sharded steps read imports
   // beside the work buffer).
   const u64 ing_rel = (u64)d.in->ingress - (u64)d.work;
-  const bool ing_ok = d.world == 1 && (u64)d.in->ingress > (u64)d.work && ing_rel + src + L + 64 < (1ull << 32) &&
+  const bool ing_ok = d.scan_inplace && d.world == 1 && (u64)d.in->ingress > (u64)d.work && ing_rel + src + L + 64 < (1ull << 32) &&
                       d.tot[15] <= d.work_cap;
   const bool inplace = ing_ok && seg_cl == 0 && L > 0;
   const u32 wbase = inplace ? (u32)(ing_rel + src) : d.seg_start[s];
@@ -1759,7 +1759,7 @@ __global__ __launch_bounds__(256) void k_decode(DS d) {
       const Frag fg = d.frags[c.frag0];
       const u32 w0 = d.seg_start[c.seg], cl = d.seg_total[c.seg] - d.segs[c.seg].len;
       const u64 ing_rel = (u64)d.in->ingress - (u64)d.work;
-      if (fg.len == c.body_size && (u64)d.in->ingress > (u64)d.work && fg.off >= ing_rel) {
+      if (fg.len == c.body_size && d.scan_inplace && (u64)d.in->ingress > (u64)d.work && fg.off >= ing_rel) {
         pb.flags |= MF_HREF;   // (read in place from the ingress slot: its payload offset)
         pb.pad = (u32)(fg.off - ing_rel);
       } else if (fg.len == c.body_size && fg.off >= w0 + cl && fg.off < w0 + d.seg_total[c.seg]) {

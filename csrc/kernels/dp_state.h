@@ -283,6 +283,7 @@ struct DS {
 
   // ---------------- sharding (cross-rank publish exchange; world == 1: unused)
   u32 world, my_rank, rank_bits, pub_cap, import_max;
+  u32 scan_inplace;         // k_frame_scan reads the step's new bytes from the ingress slot (cfg scan_in_place)
   u32 xfer_desc_max;        // records per step, all destinations
   u64 xfer_bytes;           // payload bytes per step, all destinations
   u32* q_owner;             // [q_max] owning rank

@@ -303,6 +303,7 @@ class Engine {
     // up to DEC_SEG_LDS segments k_decode numbers publishes / acks from the frame scan's
     // per-segment ordinals (segment prefix in LDS): no rank scan over the commands
     d_.rank_scan = d_.seg_max > DEC_SEG_LDS ? 1u : 0u;
+    d_.scan_inplace = get("scan_in_place", 1) ? 1u : 0u;
 
     d_.cmds = (Cmd*)dev("cmds", sizeof(Cmd) * (u64)d_.cmd_max);
     d_.frags = (Frag*)dev("frags", sizeof(Frag) * ((u64)d_.frag_max + d_.import_max));
