@@ -39,6 +39,8 @@ def _stop_leftover_brokers():
     threads would otherwise end the process with std::terminate at exit (abort, and the
     GPU run stops there instead of reporting the failure)."""
     yield
+    if os.environ.get("CHANAMQ_KEEP_LEFTOVER_BROKERS"):
+        return
     mod = sys.modules.get("chanamq_amd.server.gpu_broker")
     live = getattr(getattr(mod, "GpuBroker", None), "_live", None) if mod else None
     for b in list(live or []):
