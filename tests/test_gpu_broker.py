@@ -430,6 +430,13 @@ def test_durable_persistent_messages_survive_restart(kind, tmp_path):
 
     st2 = core.Store()
     st2.open(str(tmp_path / "store"), True)
+    try:   # (what the store holds for the queue: in the failure message)
+        from chanamq_amd.engine.control import normalize_vhost
+        from chanamq_amd.engine.persistence import entity_id
+        sel = st2.select_queue(entity_id(normalize_vhost("/"), "dur.q"))
+        held = (sel[0], sorted(sel[1]), sorted(sel[2])) if sel is not None else None
+    except Exception as e:   # noqa: BLE001
+        held = repr(e)
     b2 = GpuBroker(make_persist_plane(kind), idle_step_ms=1.0, ingress_bytes=8 << 20, store=st2, io=io).start()
     assert b2.recovered == 8
     c2 = conn(b2)
@@ -437,7 +444,7 @@ def test_durable_persistent_messages_survive_restart(kind, tmp_path):
     ch2.basic_consume("dur.q", "dc2", no_ack=True)
     got2 = ch2.consume_n(8)
     assert [d.body for d in got2] == [b"p2", b"p3", b"p4", b"p5", b"p6", b"p7", b"p8", b"p9"]
-    assert [bool(d.method.redelivered) for d in got2] == [True] * 4 + [False] * 4
+    assert [bool(d.method.redelivered) for d in got2] == [True] * 4 + [False] * 4, held
     c2.process(0.3)
     assert st2.row_count("msgs") == 0                     # auto-acked: rows deleted
     # the durable topology came back too: publishing through the exchange still routes
