@@ -412,6 +412,12 @@ class GpuBroker:
             self._thread.join(timeout=10)
         if getattr(self, "_cold_thread", None) is not None:
             self._cold_thread.join(timeout=10)
+        if getattr(self, "_pw", None) is not None:
+            # shutdown is not a client close: what the open connections hold unacked stays in
+            # queue_unacks (redelivered first on restart), so the requeue records the drops
+            # below produce on the still-running stepper are not committed
+            self._pw.drain()
+            self._pw.stop()
         for c in list(self.conns.values()):
             self._drop(c)
         if self.fe is not None:

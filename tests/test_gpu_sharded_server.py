@@ -31,10 +31,13 @@ def _xchg_env(xchg):
 @pytest.fixture
 def cluster(tmp_path, request):
     from chanamq_amd.parallel.launch import Launcher
-    xchg = getattr(request, "param", "shm")
+    # param: "<shm|rccl>[-async]" -- the exchange backend, and -async for the exchange thread
+    # (--async-x 1: phase A's exchange overlaps the next step's ingest, k_xwait gates phase B)
+    xchg, _, mode = getattr(request, "param", "shm").partition("-")
     env = _xchg_env(xchg)
     ln = Launcher(2, ["-m", "chanamq_amd.server.sharded", "--config", SMALL_CONF, "--plane", "gpu", "--port", "0", "--backend", "gloo",
-                      "--info-dir", str(tmp_path), "--xchg-timeout-ms", "20000", "--xchg", xchg], env=env).start()
+                      "--info-dir", str(tmp_path), "--xchg-timeout-ms", "20000", "--xchg", xchg,
+                      "--async-x", "1" if mode == "async" else "0"], env=env).start()
     deadline = time.time() + 180
     while time.time() < deadline and not all((tmp_path / f"rank{r}.json").exists() for r in range(2)):
         assert not ln.poll(), f"rank exited early: {ln.poll()}"
@@ -48,7 +51,7 @@ def cluster(tmp_path, request):
 
 
 @pytest.mark.timeout(300)
-@pytest.mark.parametrize("cluster", ["shm", "rccl"], indirect=True)
+@pytest.mark.parametrize("cluster", ["shm", "rccl", "shm-async", "rccl-async"], indirect=True)
 def test_pipelined_cross_rank_routing_and_topology(cluster):
     ports, ln = cluster
     c0 = Connection(port=ports[0], vhost="/")
@@ -88,6 +91,7 @@ def test_pipelined_cross_rank_routing_and_topology(cluster):
 
 
 @pytest.mark.timeout(300)
+@pytest.mark.parametrize("cluster", ["shm", "shm-async", "rccl-async"], indirect=True)
 def test_pipelined_remote_consumers_and_gets(cluster):
     """X2/X3 on the device: a consumer on rank 1 of rank 0's queue (deliveries shipped as
     restore records in the exchange, acks back as ack records), manual ack with prefetch,
