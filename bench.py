@@ -337,6 +337,7 @@ def main():
         eg = 0
         wire[0] = 0
         pending = []    # (ticket, step index)
+        waited = []     # the step whose kernels were waited for, not collected yet
         done = []
         lat_of = {}     # step index -> its lat_hist (deliveries by publish-step lag)
 
@@ -461,25 +462,33 @@ def main():
                 pre.add(nxt)
                 nxt += 1
             tp.append(time.perf_counter())
-            # the egress of step i-2 first (its D2H started when that step's last kernel
-            # opened the gate, about when step i-1's routing half began): it is in host
-            # memory by the time its wait returns; then step i-1's results (the host's
-            # only per-step wait on the kernels), which frees its parity for step i+1
-            if done:
+            # step i-2, waited on at the end of the previous iteration: collected only now,
+            # behind step i's submit (its bookkeeping is off the wait -> next-H2D path); then
+            # its egress (the D2H its last kernel started a step ago: in host memory by now)
+            if waited:
+                t2, s2 = waited.pop()
+                account(dp.finish(t2, collect=False, wait_egress=False, waited=True), s2)
+                done.append((t2, s2))
+            while done:
                 t2, s2 = done.pop(0)
                 dp.egress_wait(t2)
                 ready(s2)
             tp.append(time.perf_counter())
+            # step i-1's kernels (the host's only per-step wait on them): frees its parity, so
+            # the next iteration's submit -- step i+1's ingress H2D -- follows the wait at once
             if len(pending) > 1:
                 t, s = pending.pop(0)
-                account(dp.finish(t, collect=False, wait_egress=False), s)
-                done.append((t, s))
+                dp.wait(t)
+                waited.append((t, s))
             tp.append(time.perf_counter())
             if measure:
                 ph = [round((b2 - a2) * 1e3, 3) for a2, b2 in zip(tp, tp[1:])]
                 phases.append(ph)
                 if sum(ph) > slow["ms"]:
                     slow.update(ms=round(sum(ph), 3), step=i, phases_ms=ph)
+        for t, s in waited:
+            account(dp.finish(t, collect=False, wait_egress=False, waited=True), s)
+            done.append((t, s))
         for t, s in done:
             dp.egress_wait(t)
             ready(s)
@@ -614,7 +623,10 @@ def main():
             "storm": ({"requeued_msgs": flow["requeued"], "flow_paused_steps": flow["paused_steps"]}
                       if storm else None),
             "cross_gpu_bytes_per_s": (dp.exchanger.bytes_sent * world / t) if shards > 1 and not native else None,
-            "exchange": args.xchg if shards > 1 else None,
+            "exchange": ((args.xchg + " (" + (os.environ.get("CHANAMQ_BENCH_XCHG") or ("rccl" if backend == "nccl" else "shm"))
+                          + (", librccl stand-in" if os.environ.get("CHANAMQ_RCCL_LIB") else "") + ")") if native else args.xchg)
+                         if shards > 1 else None,
+            "async_exchange": bool(args.async_x) if shards > 1 else None,
             "prefetch": bool(args.prefetch), "chunk_bytes_per_producer": args.chunk,
             "post_soak_s": args.soak_s,
         }

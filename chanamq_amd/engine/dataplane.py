@@ -1075,9 +1075,17 @@ class GpuDataPlane(ControlState):
         self.eng.submit_b(self._pending, [int(x) for x in recv], int(stream))
         self._pending = None
 
-    def finish(self, ticket, collect=True, wait_egress=True, collect_egress=True):
+    def wait(self, ticket):
+        """The blocking half of ``finish``: returns once the step's kernels are done and its
+        parity is free for the next submit; ``finish(ticket, waited=True)`` then collects.  A
+        driver that submits between the two puts the next step's ingress H2D right behind
+        the wait instead of behind the previous step's bookkeeping."""
+        self.eng.wait_results(ticket[0])
+
+    def finish(self, ticket, collect=True, wait_egress=True, collect_egress=True, waited=False):
         p, nseg, t0, slot = ticket
-        self.eng.wait_results(p)
+        if not waited:
+            self.eng.wait_results(p)
         self._last_parity = p
         res = StepResult()
         res.counters = c = self.eng.counters(p)

@@ -130,6 +130,19 @@ for T in "$@"; do
         ok $? "xchg ${n}r $x"; line $f
       done
     done ;;
+  xchg_rccl)   # bench.py's RCCL exchange (RcclXchg) at 2 / 4 / 8 ranks on this one GPU through the tests'
+               # librccl stand-in (real RCCL refuses several ranks on one device): a rehearsal, not scaling
+    SO=$(python3 -c "from chanamq_amd import ops; print(ops.build_rccl_standin())") || { echo "no stand-in"; exit 1; }
+    for n in ${RANKS:-2 4 8}; do
+      for ax in ${ASYNC:-0 1}; do
+        f=$O/bench_${n}r_rccl_async$ax${TAG:-}.json
+        CHANAMQ_BENCH_BACKEND=gloo CHANAMQ_BENCH_XCHG=rccl CHANAMQ_RCCL_LIB=$SO CHANAMQ_RCCL_STANDIN_OK=1 \
+          timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node $n \
+          --master-addr 127.0.0.1 --master-port $((29620 + n + 10 * ax)) bench.py --gpus $n --steps 30 --warmup 5 \
+          --soak-s 0 --xchg native --async-x $ax $XCHG8_ARGS > $f 2> ${f%.json}.err
+        ok $? "xchg_rccl ${n}r async $ax"; line $f
+      done
+    done ;;
   xchg8)   # the 8-rank shared-memory rehearsal on this one GPU, asynchronous exchange then synchronous
     for ax in 1 0; do
       f=$O/bench_8r_shm_async$ax${TAG:-}.json
