@@ -70,9 +70,11 @@ def _main_gpu(args, bc, cfg, log):
         plane_kw["device"] = args.device
     core = load()
     store = None
+    mirror = None
     if bc["data_dir"]:
         from ..store import open_store
         store = open_store(bc["data_dir"], bc["fsync"])
+        mirror = _cassandra_live(cfg, store, log)
     plane = GpuDataPlane(**plane_kw)
     broker = GpuBroker(plane, host=bc["host"], port=bc["port"], heartbeat=bc["heartbeat"], frame_max=bc["frame_max"],
                        channel_max=bc["channel_max"] or 2047, store=store, **broker_kw).start()
@@ -104,9 +106,35 @@ def _main_gpu(args, bc, cfg, log):
     if tls is not None:
         tls.stop()
     broker.stop()
+    if mirror is not None:
+        mirror.stop()
     if store is not None:
         store.close()
     return 0
+
+
+def _cassandra_live(cfg, store, log):
+    """``chana.mq.store.cassandra-live``: the store's rows written through to the
+    ``chana.mq.cassandra.pass-through`` keyspace while the broker runs (the reference's
+    CassandraOpService); ``cassandra-recover`` first fills an empty store from it."""
+    if not bool(cfg.get("chana.mq.store.cassandra-live", False)):
+        return None
+    from ..store.cassandra_live import CassandraMirror
+    from ..store.cql_native import CqlClient, pull
+    hosts = cfg.get("chana.mq.cassandra.pass-through.hosts", ["localhost"])
+    host = hosts[0] if isinstance(hosts, (list, tuple)) else str(hosts)
+    port = int(cfg.get("chana.mq.cassandra.pass-through.port", 9042))
+    ks = str(cfg.get("chana.mq.cassandra.pass-through.keyspace", "chanamq"))
+    user = cfg.get("chana.mq.cassandra.pass-through.user", None)
+    password = cfg.get("chana.mq.cassandra.pass-through.password", None)
+    if bool(cfg.get("chana.mq.store.cassandra-recover", False)) and not store.queue_ids() and not store.message_ids():
+        with CqlClient(host, port, user, password) as cl:
+            n = pull(cl, store, keyspace=ks)
+        log.info("store filled from Cassandra %s:%d/%s: %s", host, port, ks, n)
+    m = CassandraMirror(store, host, port, ks, user, password,
+                        interval_s=float(cfg.get("chana.mq.store.cassandra-interval-ms", 50)) / 1000.0).start()
+    log.info("store rows written through to Cassandra %s:%d/%s", host, port, ks)
+    return m
 
 
 if __name__ == "__main__":

@@ -180,6 +180,31 @@ PYBIND11_MODULE(_core, m) {
              bool a;
              if (!s.selectVhost(id, &a)) return py::none();
              return py::bool_(a);
+           })
+      // change feed of the live Cassandra mirror (store/cassandra_live.py)
+      .def("set_mirror", &Store::setMirror)
+      .def("mirror_pending", &Store::mirrorPending)
+      .def("mirror_take", [](Store& s, size_t max_keys) {
+             Store::MirrorKeys k = s.mirrorTake(max_keys);
+             py::dict d;
+             d["msgs"] = k.msgs; d["qmsgs"] = k.qmsgs; d["qunacks"] = k.qunacks; d["qmetas"] = k.qmetas;
+             d["qparts"] = k.qparts; d["xs"] = k.xs; d["vhosts"] = k.vhosts; d["deleted"] = k.deleted;
+             return d;
+           }, py::arg("max_keys") = 4096)
+      .def("select_queue_msg", [](Store& s, std::string q, int64_t off) -> py::object {
+             QueueMsgRow r;
+             if (!s.selectQueueMsg(q, off, &r)) return py::none();
+             return py::make_tuple(r.offset, r.msgid, r.size);
+           })
+      .def("select_queue_unack", [](Store& s, std::string q, int64_t mid) -> py::object {
+             QueueMsgRow r;
+             if (!s.selectQueueUnack(q, mid, &r)) return py::none();
+             return py::make_tuple(r.offset, r.msgid, r.size);
+           })
+      .def("select_queue_meta", [](Store& s, std::string q) -> py::object {
+             QueueMetaRow m;
+             if (!s.selectQueueMeta(q, &m)) return py::none();
+             return py::make_tuple(m.lconsumed, m.consumers, m.durable, m.ttl);
            });
 
   py::class_<Gateway>(m, "Gateway")

@@ -539,7 +539,9 @@ void Store::apply(uint8_t op, const std::string& pl) {
       break;
     }
     case OP_MSG_REFER: { int64_t id = (int64_t)r.llng(); int32_t ref = (int32_t)r.lng();
-      auto it = msgs_.find(id); if (it != msgs_.end()) it->second.refer = ref; break; }
+      auto it = msgs_.find(id); if (it != msgs_.end()) it->second.refer = ref;
+      if (marking()) md_msgs_.insert(id);
+      break; }
     case OP_MSG_DEL: {
       auto it = msgs_.find((int64_t)r.llng());
       if (it != msgs_.end()) drop_msg(it);
@@ -553,6 +555,7 @@ void Store::apply(uint8_t op, const std::string& pl) {
       for (u32 i = 0; i < n; ++i) m.consumers.insert(r.longstr());
       m.durable = r.octet(); m.ttl = (int64_t)r.llng();
       queue_metas_[q] = m;
+      if (marking()) md_qmetas_.insert(q);
       break;
     }
     case OP_QMSG_INS: {
@@ -562,10 +565,22 @@ void Store::apply(uint8_t op, const std::string& pl) {
       int64_t ttl = (int64_t)r.llng(), at = (int64_t)r.llng();
       m.expire_at = ttl > 0 ? at + ttl : 0;
       queues_[q][m.offset] = m;
+      if (marking()) md_qmsgs_.emplace(q, m.offset);
       break;
     }
-    case OP_QMSG_DEL: { std::string q = r.longstr(); queues_[q].erase((int64_t)r.llng()); break; }
-    case OP_QLAST: { std::string q = r.longstr(); queue_metas_[q].lconsumed = (int64_t)r.llng(); break; }
+    case OP_QMSG_DEL: {
+      std::string q = r.longstr();
+      const int64_t off = (int64_t)r.llng();
+      queues_[q].erase(off);
+      if (marking()) md_qmsgs_.emplace(q, off);
+      break;
+    }
+    case OP_QLAST: {
+      std::string q = r.longstr();
+      queue_metas_[q].lconsumed = (int64_t)r.llng();
+      if (marking()) md_qmetas_.insert(q);
+      break;
+    }
     case OP_QCONSUMED: {
       // lconsumed := L; rows with offset <= L removed; unacks inserted (correct columns: A.Q21)
       std::string q = r.longstr();
@@ -579,11 +594,13 @@ void Store::apply(uint8_t op, const std::string& pl) {
         u.offset = (int64_t)r.llng(); u.msgid = (int64_t)r.llng(); u.size = (int32_t)r.lng();
         queue_unacks_[q][u.msgid] = u;
       }
+      if (marking()) { md_qmetas_.insert(q); md_qparts_.insert(q); }
       break;
     }
     case OP_QFORCE_DEL: {
       std::string q = r.longstr();
       queues_.erase(q); queue_metas_.erase(q); queue_unacks_.erase(q);
+      if (marking()) { md_qmetas_.insert(q); md_qparts_.insert(q); }
       break;
     }
     case OP_QPENDING_DEL: {  // copy to *_deleted tables, then delete (CassandraOpService.scala:561-604)
@@ -598,6 +615,7 @@ void Store::apply(uint8_t op, const std::string& pl) {
       for (auto& kv : queues_[q]) queues_deleted_[q][kv.first] = kv.second;
       for (auto& kv : queue_unacks_[q]) queue_unacks_deleted_[q][kv.first] = kv.second;
       queues_.erase(q); queue_metas_.erase(q); queue_unacks_.erase(q);
+      if (marking()) { md_qmetas_.insert(q); md_qparts_.insert(q); md_deleted_.insert(q); }
       break;
     }
     case OP_QDEL_CONSUMED: {
@@ -605,6 +623,7 @@ void Store::apply(uint8_t op, const std::string& pl) {
       int64_t L = (int64_t)r.llng();
       auto& rows = queues_[q];
       rows.erase(rows.begin(), rows.upper_bound(L));
+      if (marking()) md_qparts_.insert(q);
       break;
     }
     case OP_QUNACK_INS: {
@@ -612,15 +631,23 @@ void Store::apply(uint8_t op, const std::string& pl) {
       QueueMsgRow u;
       u.offset = (int64_t)r.llng(); u.msgid = (int64_t)r.llng(); u.size = (int32_t)r.lng();
       queue_unacks_[q][u.msgid] = u;
+      if (marking()) md_qunacks_.emplace(q, u.msgid);
       break;
     }
-    case OP_QUNACK_DEL: { std::string q = r.longstr(); queue_unacks_[q].erase((int64_t)r.llng()); break; }
+    case OP_QUNACK_DEL: {
+      std::string q = r.longstr();
+      const int64_t mid = (int64_t)r.llng();
+      queue_unacks_[q].erase(mid);
+      if (marking()) md_qunacks_.emplace(q, mid);
+      break;
+    }
     case OP_X_INS: {
       std::string id = r.longstr();
       ExchangeRow x;
       x.tpe = r.longstr(); x.durable = r.octet(); x.autodel = r.octet(); x.internal = r.octet();
       x.args = r_map(r);
       exchanges_[id] = x;
+      if (marking()) md_xs_.insert(id);
       break;
     }
     case OP_BIND_INS: {
@@ -628,26 +655,40 @@ void Store::apply(uint8_t op, const std::string& pl) {
       BindRow b;
       b.queue = r.longstr(); b.key = r.longstr(); b.args = r_map(r);
       binds_[id][{b.queue, b.key}] = b;
+      if (marking()) md_xs_.insert(id);
       break;
     }
     case OP_BIND_DEL: {
       std::string id = r.longstr(), q = r.longstr(), k = r.longstr();
       binds_[id].erase({q, k});
+      if (marking()) md_xs_.insert(id);
       break;
     }
     case OP_BIND_DEL_Q: {
       std::string q = r.longstr();
       for (auto& kv : binds_)
-        for (auto it = kv.second.begin(); it != kv.second.end();)
-          it = it->first.first == q ? kv.second.erase(it) : std::next(it);
+        for (auto it = kv.second.begin(); it != kv.second.end();) {
+          if (it->first.first == q) {
+            if (marking()) md_xs_.insert(kv.first);
+            it = kv.second.erase(it);
+          } else {
+            ++it;
+          }
+        }
       break;
     }
-    case OP_X_DEL: { std::string id = r.longstr(); exchanges_.erase(id); binds_.erase(id); break; }
+    case OP_X_DEL: {
+      std::string id = r.longstr();
+      exchanges_.erase(id); binds_.erase(id);
+      if (marking()) md_xs_.insert(id);
+      break;
+    }
     case OP_QDMETA_INS: {
       std::string q = r.longstr();
       QueueMetaDeletedRow d;
       d.lconsumed = (int64_t)r.llng(); d.nconsumer = (int32_t)r.lng(); d.durable = r.octet();
       queue_metas_deleted_[q] = d;
+      if (marking()) md_deleted_.insert(q);
       break;
     }
     case OP_QDMSG_INS:
@@ -657,6 +698,7 @@ void Store::apply(uint8_t op, const std::string& pl) {
       u.offset = (int64_t)r.llng(); u.msgid = (int64_t)r.llng(); u.size = (int32_t)r.lng();
       if (op == OP_QDMSG_INS) queues_deleted_[q][u.offset] = u;
       else queue_unacks_deleted_[q][u.msgid] = u;
+      if (marking()) md_deleted_.insert(q);
       break;
     }
     case OP_ROWS: {
@@ -681,8 +723,18 @@ void Store::apply(uint8_t op, const std::string& pl) {
       apply_rows(qids, ops.data(), nops);
       break;
     }
-    case OP_VH_INS: { std::string id = r.longstr(); vhosts_[id] = r.octet(); break; }
-    case OP_VH_DEL: vhosts_.erase(r.longstr()); break;
+    case OP_VH_INS: {
+      std::string id = r.longstr();
+      vhosts_[id] = r.octet();
+      if (marking()) md_vhosts_.insert(id);
+      break;
+    }
+    case OP_VH_DEL: {
+      std::string id = r.longstr();
+      vhosts_.erase(id);
+      if (marking()) md_vhosts_.insert(id);
+      break;
+    }
     default: break;
   }
   (void)now;
@@ -713,11 +765,13 @@ void Store::put_msg(MsgRow&& m) {
   if (m.bseg >= 0 && body_) body_->ref(BodyLog::Loc{(uint32_t)m.bseg, m.blen, m.boff});
   const int64_t id = m.id;
   msgs_.emplace(id, std::move(m));
+  if (marking()) md_msgs_.insert(id);
 }
 
 void Store::drop_msg(std::map<int64_t, MsgRow>::iterator it) {
   msg_bytes_ -= msg_size(it->second);
   if (it->second.bseg >= 0 && body_) body_->unref(BodyLog::Loc{(uint32_t)it->second.bseg, it->second.blen, it->second.boff});
+  if (marking()) md_msgs_.insert(it->first);
   msgs_.erase(it);
 }
 
@@ -739,13 +793,27 @@ void Store::apply_rows(const std::vector<const std::string*>& qids, const RowOp*
         if (qok) {
           auto& t = rows(o.q);
           t.insert_or_assign(t.end(), o.offset, QueueMsgRow{o.offset, o.msgid, o.size, 0});
+          if (marking()) md_qmsgs_.emplace(*qids[o.q], o.offset);
         }
         break;
-      case ROW_QMSG_DEL: if (qok) rows(o.q).erase(o.offset); break;
-      case ROW_QUNACK_INS:
-        if (qok) unacks(o.q)[o.msgid] = QueueMsgRow{o.offset, o.msgid, o.size, 0};
+      case ROW_QMSG_DEL:
+        if (qok) {
+          rows(o.q).erase(o.offset);
+          if (marking()) md_qmsgs_.emplace(*qids[o.q], o.offset);
+        }
         break;
-      case ROW_QUNACK_DEL: if (qok) unacks(o.q).erase(o.msgid); break;
+      case ROW_QUNACK_INS:
+        if (qok) {
+          unacks(o.q)[o.msgid] = QueueMsgRow{o.offset, o.msgid, o.size, 0};
+          if (marking()) md_qunacks_.emplace(*qids[o.q], o.msgid);
+        }
+        break;
+      case ROW_QUNACK_DEL:
+        if (qok) {
+          unacks(o.q).erase(o.msgid);
+          if (marking()) md_qunacks_.emplace(*qids[o.q], o.msgid);
+        }
+        break;
       case ROW_MSG_DEL: {
         auto it = msgs_.find(o.msgid);
         if (it != msgs_.end()) drop_msg(it);
@@ -754,6 +822,7 @@ void Store::apply_rows(const std::vector<const std::string*>& qids, const RowOp*
       case ROW_MSG_REFER: {
         auto it = msgs_.find(o.msgid);
         if (it != msgs_.end()) it->second.refer = o.size;
+        if (marking()) md_msgs_.insert(o.msgid);
         break;
       }
       case ROW_MSG_REF: {
@@ -911,6 +980,78 @@ void Store::insertQueueUnack(const std::string& q, int64_t offset, int64_t msgid
 void Store::deleteQueueUnack(const std::string& q, int64_t msgid) {
   LOCK; Writer w; w.longstr(q); w.llng((u64)msgid); append(OP_QUNACK_DEL, w.done());
 }
+// ---- change feed
+void Store::setMirror(bool on) {
+  LOCK;
+  mirror_ = on;
+  if (!on) {
+    md_msgs_.clear(); md_qmsgs_.clear(); md_qunacks_.clear(); md_qmetas_.clear(); md_qparts_.clear();
+    md_xs_.clear(); md_vhosts_.clear(); md_deleted_.clear();
+  }
+}
+
+size_t Store::mirrorPending() {
+  LOCK;
+  return md_msgs_.size() + md_qmsgs_.size() + md_qunacks_.size() + md_qmetas_.size() + md_qparts_.size() +
+         md_xs_.size() + md_vhosts_.size() + md_deleted_.size();
+}
+
+Store::MirrorKeys Store::mirrorTake(size_t max_keys) {
+  LOCK;
+  MirrorKeys k;
+  auto take = [&](auto& set, auto& out) {
+    auto it = set.begin();
+    for (size_t n = 0; it != set.end() && n < max_keys; ++n) out.push_back(*it++);
+    set.erase(set.begin(), it);
+  };
+  // a whole partition rewritten covers that queue's single-row keys (taken with it)
+  take(md_qparts_, k.qparts);
+  std::set<std::string> parts(k.qparts.begin(), k.qparts.end());
+  auto take_rows = [&](std::set<std::pair<std::string, int64_t>>& set, std::vector<std::pair<std::string, int64_t>>& out) {
+    size_t n = 0;
+    for (auto it = set.begin(); it != set.end() && n < max_keys;) {
+      if (!parts.count(it->first)) { out.push_back(*it); ++n; }
+      it = set.erase(it);
+    }
+  };
+  take_rows(md_qmsgs_, k.qmsgs);
+  take_rows(md_qunacks_, k.qunacks);
+  take(md_msgs_, k.msgs);
+  take(md_qmetas_, k.qmetas);
+  take(md_xs_, k.xs);
+  take(md_vhosts_, k.vhosts);
+  take(md_deleted_, k.deleted);
+  return k;
+}
+
+bool Store::selectQueueMsg(const std::string& q, int64_t offset, QueueMsgRow* out) {
+  LOCK;
+  auto qi = queues_.find(q);
+  if (qi == queues_.end()) return false;
+  auto it = qi->second.find(offset);
+  if (it == qi->second.end() || (it->second.expire_at && it->second.expire_at <= now_ms())) return false;
+  *out = it->second;
+  return true;
+}
+
+bool Store::selectQueueUnack(const std::string& q, int64_t msgid, QueueMsgRow* out) {
+  LOCK;
+  auto qi = queue_unacks_.find(q);
+  if (qi == queue_unacks_.end()) return false;
+  auto it = qi->second.find(msgid);
+  if (it == qi->second.end()) return false;
+  *out = it->second;
+  return true;
+}
+
+bool Store::selectQueueMeta(const std::string& q, QueueMetaRow* out) {
+  LOCK;
+  auto it = queue_metas_.find(q);
+  if (it == queue_metas_.end()) return false;
+  *out = it->second;
+  return true;
+}
+
 void Store::insertExchange(const std::string& id, const ExchangeRow& x) {
   LOCK; Writer w; w.longstr(id); w.longstr(x.tpe); w.octet(x.durable); w.octet(x.autodel); w.octet(x.internal);
   w_map(w, x.args); append(OP_X_INS, w.done());

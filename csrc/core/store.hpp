@@ -167,6 +167,24 @@ class Store {
   void insertDeletedQueueMsg(const std::string& q, int64_t offset, int64_t msgid, int32_t size);
   void insertDeletedQueueUnack(const std::string& q, int64_t offset, int64_t msgid, int32_t size);
 
+  // ---- change feed (store/cassandra_live.py, the live Cassandra mirror): with it on, every
+  // change marks the key of the row (or the partition, for range / whole-queue changes) it
+  // touched; mirrorTake hands over up to max_keys marked keys of each kind and clears them,
+  // and the mirror reads those rows' current state back (select*) and writes it -- repeated
+  // changes to one row between two takes cost one write (a publish acked before the take:
+  // none).  Replay and compaction mark nothing.
+  struct MirrorKeys {
+    std::vector<int64_t> msgs;
+    std::vector<std::pair<std::string, int64_t>> qmsgs, qunacks;   // (queue, offset) / (queue, msgid)
+    std::vector<std::string> qmetas, qparts, xs, vhosts, deleted;
+  };
+  void setMirror(bool on);
+  MirrorKeys mirrorTake(size_t max_keys);
+  size_t mirrorPending();
+  bool selectQueueMsg(const std::string& q, int64_t offset, QueueMsgRow* out);
+  bool selectQueueUnack(const std::string& q, int64_t msgid, QueueMsgRow* out);
+  bool selectQueueMeta(const std::string& q, QueueMetaRow* out);
+
   // ---- recovery / inspection
   std::vector<std::string> vhostIds();
   std::vector<std::string> exchangeIds();
@@ -217,6 +235,13 @@ class Store {
   std::map<std::string, ExchangeRow> exchanges_;
   std::map<std::string, std::map<std::pair<std::string, std::string>, BindRow>> binds_;
   std::map<std::string, bool> vhosts_;
+
+  // change feed (setMirror)
+  bool mirror_ = false;
+  std::set<int64_t> md_msgs_;
+  std::set<std::pair<std::string, int64_t>> md_qmsgs_, md_qunacks_;
+  std::set<std::string> md_qmetas_, md_qparts_, md_xs_, md_vhosts_, md_deleted_;
+  bool marking() const { return mirror_ && !replaying_; }
 };
 
 }  // namespace cmq

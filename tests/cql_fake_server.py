@@ -158,6 +158,20 @@ class FakeCql:
             with self.lock:
                 self.tables.setdefault((ks, t), {})[pk] = row
             return struct.pack(">i", 1)
+        m = re.match(r"DELETE FROM (\w+)\.(\w+) WHERE (.+)$", s)
+        if m:   # a row (every key column given) or a whole partition (a key prefix)
+            ks, t = m.group(1), m.group(2)
+            conds = [x.strip() for x in m.group(3).split(" AND ")]
+            cols = [c.split("=")[0].strip() for c in conds]
+            types = dict(SCHEMA[t][0])
+            want = {col: _dec(v, types[col]) for col, v in zip(cols, vals)}
+            keys = SCHEMA[t][1] + SCHEMA[t][2]
+            assert cols == keys[:len(cols)] and len(cols) >= len(SCHEMA[t][1]), ("not a key prefix", cols)
+            with self.lock:
+                tab = self.tables.setdefault((ks, t), {})
+                for pk in [pk for pk in tab if pk[:len(cols)] == tuple(want[c] for c in cols)]:
+                    del tab[pk]
+            return struct.pack(">i", 1)
         m = re.match(r"SELECT \* FROM (\w+)\.(\w+)$", s)
         if m:
             ks, t = m.group(1), m.group(2)
