@@ -2948,38 +2948,61 @@ __global__ void k_qfirst(DS d, u32 src) {
 
 // publish p's entry at position `rank` of this step's entries for queue q (`last`: the
 // queue's last pair, which moves q_tail); returns the message to release if the ring is full
-DEV u32 enqueue_at(const DS& d, u32 q, u32 p, u32 rank, bool last, PersistRec* pr) {
+// a pair's enqueue in two halves: every load (the publish, the queue's ring state), then
+// the stores -- so a kernel can have the loads of several pairs in flight at once
+struct EnqLoad {
+  u32 msg = INVALID, flags = 0, chslot = INVALID;
+  u64 head = 0, tail = 0, mask = 0, ring_off = 0;
+  i64 expire_ms = 0, ttl = 0;
+  bool durable = false;
+};
+DEV EnqLoad enq_load(const DS& d, u32 q, u32 p) {
   const Pub& pb = d.pubs[p];
+  EnqLoad e;
+  e.msg = pb.msg;
+  e.flags = pb.flags;
+  e.chslot = pb.chslot;
+  e.expire_ms = pb.expire_ms;
   // the queue's last pair moves q_tail in this kernel: every pair reads the tail that
   // k_ring_plan recorded before the enqueue, never q_tail itself
-  u64 head = d.q_head[q], tail = d.q_enq_tail[q];
-  u64 cap = d.q_ring_mask[q] + 1;
-  u64 freec = cap - (tail - head);
+  e.head = d.q_head[q];
+  e.tail = d.q_enq_tail[q];
+  e.mask = d.q_ring_mask[q];
+  e.ring_off = d.q_ring_off[q];
+  e.ttl = d.q_ttl[q];
+  e.durable = d.persist && d.q_durable[q];
+  return e;
+}
+DEV u32 enq_store(const DS& d, const EnqLoad& l, u32 q, u32 rank, bool last, PersistRec* pr) {
+  const u64 cap = l.mask + 1;
+  const u64 freec = cap - (l.tail - l.head);
   u32 drop = INVALID;
-  if (pb.msg == INVALID) return INVALID;
+  if (l.msg == INVALID) return INVALID;
   if (rank < freec) {
-    u64 pos = tail + rank;
+    u64 pos = l.tail + rank;
     Desc ds;
-    ds.msg = pb.msg;
-    ds.flags = (pb.flags & MF_REDELIVERED) ? 1u : 0u;
-    i64 e = pb.expire_ms;
-    i64 qt = d.q_ttl[q];
-    if (qt > 0) { i64 qe = d.in->now_ms + qt; e = (e == 0 || qe < e) ? qe : e; }
+    ds.msg = l.msg;
+    ds.flags = (l.flags & MF_REDELIVERED) ? 1u : 0u;
+    i64 e = l.expire_ms;
+    if (l.ttl > 0) { i64 qe = d.in->now_ms + l.ttl; e = (e == 0 || qe < e) ? qe : e; }
     ds.expire_ms = e;
-    d.ring[d.q_ring_off[q] + (pos & d.q_ring_mask[q])] = ds;
-    if (d.persist && d.q_durable[q] && (pb.flags & MF_PERSIST) && !(pb.flags & MF_RESTORE)) {
-      pr->msg = pb.msg; pr->q = q; pr->qpos = pos; pr->expire_ms = e;
+    d.ring[l.ring_off + (pos & l.mask)] = ds;
+    if (l.durable && (l.flags & MF_PERSIST) && !(l.flags & MF_RESTORE)) {
+      pr->msg = l.msg; pr->q = q; pr->qpos = pos; pr->expire_ms = e;
     }
   } else {
-    drop = pb.msg;
-    if (pb.chslot != INVALID) d.ch_pub_fail[pb.chslot] = 1u;   // confirmed with Basic.Nack
+    drop = l.msg;
+    if (l.chslot != INVALID) d.ch_pub_fail[l.chslot] = 1u;   // confirmed with Basic.Nack
   }
   if (last) {
     u64 cnt = rank + 1;
-    u64 nt = tail + (cnt < freec ? cnt : freec);
+    u64 nt = l.tail + (cnt < freec ? cnt : freec);
     d.q_tail[q] = nt;
   }
   return drop;
+}
+DEV u32 enqueue_at(const DS& d, u32 q, u32 p, u32 rank, bool last, PersistRec* pr) {
+  return enq_store(d, enq_load(d, q, p), q, rank, last, pr);
 }
 DEV u32 enqueue_one(const DS& d, u32 src, u32 i, u32 n, PersistRec* pr, u32 hs_ntiles) {
   const u32* kk = d.pair_k[src];
@@ -3158,27 +3181,40 @@ __global__ __launch_bounds__(RsNt<DB>::v) void k_rs_hist_plan(DS d, const u32* k
 template <int DB>
 __global__ __launch_bounds__(256) void k_rs_scatter_enq(DS d, const u32* kin, const u32* vin, const u32* np,
                                                        const u32* hscan) {
-  constexpr u32 D = 1u << DB;
+  constexpr u32 D = 1u << DB, CH = SORT_TILE / 256;   // CH items per lane
   __shared__ u32 wc[4][D];
   const u32 tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
   const u32 n = *np, rb = d.rank_bits;
+  const u64 lt = lanemask_lt();
   for (u32 t = blockIdx.x; t * SORT_TILE < n; t += gridDim.x) {   // tile-stride (capped grid)
     const u32 base = t * SORT_TILE;
     __syncthreads();
     for (u32 i = tid; i < 4 * D; i += 256) ((u32*)wc)[i] = 0;
     __syncthreads();
     const u32 wbase = base + w * (SORT_TILE / 4);
-    for (u32 c = 0; c < SORT_TILE / 256; ++c) {   // per-wave digit counts
+    // the lane's CH pairs loaded at once, and kept: the rank pass and the enqueue reuse them
+    // (was: each of the CH rounds re-read its pair, then walked its queue's state -- ~3
+    // dependent memory trips a round, CH rounds in series: the kernel's 12-13 us floor)
+    u32 key[CH], val[CH];
+    u64 pe[CH];
+#pragma unroll
+    for (u32 c = 0; c < CH; ++c) {
       const u32 i = wbase + c * 64 + lane;
-      const bool valid = i < n;
-      const u32 dg = valid ? kin[i] & (D - 1) : 0;
+      key[c] = i < n ? kin[i] : 0u;
+      val[c] = i < n ? vin[i] : 0u;
+    }
+#pragma unroll
+    for (u32 c = 0; c < CH; ++c) {   // per-wave digit counts
+      const bool valid = wbase + c * 64 + lane < n;
+      const u32 dg = key[c] & (D - 1);
       u64 peers = __ballot(valid);
 #pragma unroll
       for (u32 bb = 0; bb < DB; ++bb) {
         const u64 m = __ballot((dg >> bb) & 1);
         peers &= ((dg >> bb) & 1) ? m : ~m;
       }
-      if (valid && ((peers & lanemask_lt()) == 0)) wc[w][dg] += __popcll(peers);
+      pe[c] = peers;
+      if (valid && ((peers & lt) == 0)) wc[w][dg] += __popcll(peers);
       __builtin_amdgcn_wave_barrier();
     }
     __syncthreads();
@@ -3187,28 +3223,37 @@ __global__ __launch_bounds__(256) void k_rs_scatter_enq(DS d, const u32* kin, co
       for (u32 ww = 0; ww < 4; ++ww) { const u32 x = wc[ww][dg]; wc[ww][dg] = run; run += x; }
     }
     __syncthreads();
-    for (u32 c = 0; c < SORT_TILE / 256; ++c) {
-      const u32 i = wbase + c * 64 + lane;
-      const bool valid = i < n;
-      const u32 key = valid ? kin[i] : 0;
-      const u32 dg = key & (D - 1);
-      u64 peers = __ballot(valid);
+    // every pair's position in digit order (LDS only), then every load the enqueue needs --
+    // its queue's first pair / next digit start, the publish, the queue's ring state -- issued
+    // together for the lane's CH pairs, then the ring stores
+    u32 pos[CH];
 #pragma unroll
-      for (u32 bb = 0; bb < DB; ++bb) {
-        const u64 m = __ballot((dg >> bb) & 1);
-        peers &= ((dg >> bb) & 1) ? m : ~m;
-      }
+    for (u32 c = 0; c < CH; ++c) {
+      const bool valid = wbase + c * 64 + lane < n;
+      const u32 dg = key[c] & (D - 1);
       const u32 basepos = ((volatile u32*)wc[w])[dg];
-      const u32 pos = basepos + __popcll(peers & lanemask_lt());
+      pos[c] = basepos + __popcll(pe[c] & lt);
+      __builtin_amdgcn_wave_barrier();
+      if (valid && ((pe[c] & lt) == 0)) ((volatile u32*)wc[w])[dg] = basepos + __popcll(pe[c]);
+      __builtin_amdgcn_wave_barrier();
+    }
+    EnqLoad el[CH];
+    u32 first[CH], nx[CH];
+#pragma unroll
+    for (u32 c = 0; c < CH; ++c) {
+      const bool valid = wbase + c * 64 + lane < n;
+      const u32 q = key[c] >> rb;
+      first[c] = valid ? hscan[q << rb] : 0u;
+      nx[c] = valid ? (((q + 1) << rb) < D ? hscan[(q + 1) << rb] : n) : 0u;
+      el[c] = valid ? enq_load(d, q, val[c]) : EnqLoad{};
+    }
+#pragma unroll
+    for (u32 c = 0; c < CH; ++c) {
+      const bool valid = wbase + c * 64 + lane < n;
       PersistRec pr;
       pr.msg = INVALID;
       u32 drop = INVALID;
-      if (valid) {
-        const u32 q = key >> rb;
-        const u32 first = hscan[q << rb];
-        const u32 nx = ((q + 1) << rb) < D ? hscan[(q + 1) << rb] : n;
-        drop = enqueue_at(d, q, vin[i], pos - first, pos + 1 == nx, &pr);
-      }
+      if (valid) drop = enq_store(d, el[c], key[c] >> rb, pos[c] - first[c], pos[c] + 1 == nx[c], &pr);
       wave_release(d, drop, drop != INVALID);
       if (drop != INVALID) atomicAdd(&d.ctr->n_ring_full, 1u);
       if (d.persist) {
@@ -3216,9 +3261,6 @@ __global__ __launch_bounds__(256) void k_rs_scatter_enq(DS d, const u32* kin, co
         const u32 k = wave_reserve(&d.ctr->n_persist, want);
         if (want && k < d.persist_max) d.prec[k] = pr;
       }
-      __builtin_amdgcn_wave_barrier();
-      if (valid && ((peers & lanemask_lt()) == 0)) ((volatile u32*)wc[w])[dg] = basepos + __popcll(peers);
-      __builtin_amdgcn_wave_barrier();
     }
   }
 }
@@ -3967,22 +4009,36 @@ __global__ __launch_bounds__(1024) void k_runs(DS d) {
 DEV void wave_consumed(const DS& d, u32 msg, u32 q, u64 qpos, u32 kind, bool valid);
 // thread per delivery: expand its run (binary search), assign the channel's next delivery
 // tag, fill the unacked window slot, size the rendered frames
-__global__ void k_dv_write(DS d) {
+#define DVW_LDS 512   // runs staged in LDS per block (more: searched in global memory)
+__global__ __launch_bounds__(256) void k_dv_write(DS d) {
+  __shared__ u32 s_start[DVW_LDS];
+  __shared__ Run s_run[DVW_LDS];
   const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
   const u32 n = d.ctr->n_deliv;
   const bool valid = i < n;
   u32 lat = 0, nref = 0, rbytes = 0;
   Deliv dv;
   dv.msg = INVALID; dv.q = 0; dv.qpos = 0; dv.flags = 2;
+  const u32 R = d.tot[TS_NRUNS];
+  // the step's runs (run order) staged in LDS by the block: one coalesced load of the
+  // starts and the runs instead of a chain of dependent global loads per delivery (the
+  // binary search's probes, then run_order -> runs)
+  const bool lds_runs = R <= DVW_LDS;
+  if (lds_runs && blockIdx.x * blockDim.x < n) {   // (block-uniform)
+    for (u32 s = threadIdx.x; s < R; s += blockDim.x) {
+      s_start[s] = d.run_start[s];
+      s_run[s] = d.runs[d.run_order[s]];
+    }
+    __syncthreads();
+  }
   if (valid) {
-    const u32 R = d.tot[TS_NRUNS];
     u32 lo = 0, hi = R;   // last s with run_start[s] <= i
     while (hi - lo > 1) {
       u32 mid = (lo + hi) >> 1;
-      if (d.run_start[mid] <= i) lo = mid; else hi = mid;
+      if ((lds_runs ? s_start[mid] : d.run_start[mid]) <= i) lo = mid; else hi = mid;
     }
-    const Run rn = d.runs[d.run_order[lo]];
-    const u32 k = i - d.run_start[lo];
+    const Run rn = lds_runs ? s_run[lo] : d.runs[d.run_order[lo]];
+    const u32 k = i - (lds_runs ? s_start[lo] : d.run_start[lo]);
     const Desc ds = d.ring[d.q_ring_off[rn.q] + ((rn.qpos + k) & d.q_ring_mask[rn.q])];
     const u32 ch = rn.ch;
     const u64 tag = d.ch_next_tag[ch] + (i - d.ch_first[ch]);
@@ -4013,7 +4069,8 @@ __global__ void k_dv_write(DS d) {
     d.deliv[i] = dv;
     lat = (u32)d.in->step - m.pub_step;
     // the channel's last delivery this step: the window needs a k_chan_advance pass
-    bool last = i + 1 == n || (k + 1 == rn.cnt && (lo + 1 >= R || d.runs[d.run_order[lo + 1]].ch != ch));
+    bool last = i + 1 == n ||
+                (k + 1 == rn.cnt && (lo + 1 >= R || (lds_runs ? s_run[lo + 1].ch : d.runs[d.run_order[lo + 1]].ch) != ch));
     if (last) {
       // auto-ack channel with nothing pending (no manual delivery awaiting a settle, no
       // deferred marks): every slot up to this tag is done, so the window head moves here

@@ -1720,7 +1720,15 @@ class Engine {
       if (m < 0 || m >= (int)d_.world) throw std::runtime_error("xchg_setup: bad member");
     std::sort(members.begin(), members.end());
     x_stop();   // (a job of the old group finished or failed: its phase B was released)
-    if (!s_x_) HIPCHECK(hipStreamCreateWithFlags(&s_x_, hipStreamNonBlocking));
+    if (!s_x_) {
+      // high priority: the runtime takes a high-priority stream's hardware queue from a pool
+      // of its own, so the exchange never shares a queue with s_comp_ -- where, with the
+      // asynchronous exchange, phase B's k_xwait spins until this stream's transfer is done
+      // (4 hardware queues per process: a sixth normal stream wraps onto s_comp_'s queue)
+      int lo = 0, hi = 0;
+      HIPCHECK(hipDeviceGetStreamPriorityRange(&lo, &hi));
+      HIPCHECK(hipStreamCreateWithPriority(&s_x_, hipStreamNonBlocking, hi));
+    }
     rccl_.reset();
     shm_.reset();
     cshm_.reset();

@@ -99,7 +99,12 @@ class RcclXchg {
     ncclUniqueId id;
     memcpy(id.internal, uid.data(), sizeof id.internal);
     RcclLib& L = RcclLib::get();
-    if (hipStreamCreateWithFlags(&s_, hipStreamNonBlocking) != hipSuccess) throw std::runtime_error("rccl xchg: stream");
+    // high priority: a hardware queue of its own, never s_comp_'s (the asynchronous exchange
+    // parks phase B there in k_xwait until this stream's counts and bulk are done)
+    int plo = 0, phi = 0;
+    if (hipDeviceGetStreamPriorityRange(&plo, &phi) != hipSuccess ||
+        hipStreamCreateWithPriority(&s_, hipStreamNonBlocking, phi) != hipSuccess)
+      throw std::runtime_error("rccl xchg: stream");
     if (hipEventCreateWithFlags(&ev_, hipEventDisableTiming) != hipSuccess) throw std::runtime_error("rccl xchg: event");
     ncclResult_t r = L.CommInitRank(&comm_, (int)members_.size(), id, idx_);
     if (r) throw std::runtime_error(std::string("ncclCommInitRank: ") + L.GetErrorString(r));

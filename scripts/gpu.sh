@@ -32,7 +32,7 @@
 #               traffic (COLD_ARGS appended)
 #   sharded     the sharded-server GPU tests
 #   sharded_e2e config 2 on the 2-rank sharded server over TCP, local vs remote consumers
-#   tests:PAT   pytest -m gpu -x -k PAT
+#   tests:PAT   pytest -m gpu -x -k PAT ('+' = or)
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 O=gpurun_out/${RUN:-gpu}
 mkdir -p "$O"
@@ -173,8 +173,9 @@ for T in "$@"; do
   sharded)
     timeout -k 10 700 $PYT tests/test_gpu_sharded.py tests/test_gpu_sharded_server.py -m gpu -x -v > $O/pytest_sharded.log 2>&1
     rc=$?; tail -4 $O/pytest_sharded.log; ok $rc sharded ;;
-  tests:*)
-    timeout -k 10 900 $PYT tests -m gpu -x -v -k "${T#tests:}" > $O/pytest_k.log 2>&1
+  tests:*)   # PAT: a -k expression, '+' between alternatives (tests:dataplane+scale = -k "dataplane or scale")
+    K_EXPR=${T#tests:}; K_EXPR=${K_EXPR//+/ or }
+    timeout -k 10 900 $PYT tests -m gpu -x -v -k "$K_EXPR" > $O/pytest_k.log 2>&1
     rc=$?; grep -E "PASSED|FAILED|ERROR" $O/pytest_k.log | tail -30; tail -2 $O/pytest_k.log; ok $rc "tests ${T#tests:}" ;;
   *) echo "unknown task $T"; exit 2 ;;
   esac

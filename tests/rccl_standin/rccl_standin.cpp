@@ -134,8 +134,11 @@ ncclResult_t run_group(std::vector<Op>& ops) {
                 (unsigned long long)c->h->box_bytes);
         return c->err = ncclInvalidUsage;
       }
-      if (mine[k]->bytes &&
-          hipMemcpy(c->box(c->rank, p) + off, mine[k]->ptr, mine[k]->bytes, hipMemcpyDefault) != hipSuccess)
+      // (on the op's own stream, as RCCL's kernels would run: never the null stream, whose
+      // hardware queue may be the one a spinning kernel of the engine holds)
+      if (mine[k]->bytes && (hipMemcpyAsync(c->box(c->rank, p) + off, mine[k]->ptr, mine[k]->bytes, hipMemcpyDefault,
+                                            mine[k]->s) != hipSuccess ||
+                             hipStreamSynchronize(mine[k]->s) != hipSuccess))
         return c->err = ncclUnhandledCudaError;
       ch.sizes[k] = mine[k]->bytes;
       off += (mine[k]->bytes + 63) & ~63ull;
@@ -168,8 +171,9 @@ ncclResult_t run_group(std::vector<Op>& ops) {
     }
     uint64_t off = 0;
     for (size_t k = 0; k < mine.size(); ++k) {
-      if (mine[k]->bytes &&
-          hipMemcpy(mine[k]->ptr, c->box(p, c->rank) + off, mine[k]->bytes, hipMemcpyDefault) != hipSuccess)
+      if (mine[k]->bytes && (hipMemcpyAsync(mine[k]->ptr, c->box(p, c->rank) + off, mine[k]->bytes, hipMemcpyDefault,
+                                            mine[k]->s) != hipSuccess ||
+                             hipStreamSynchronize(mine[k]->s) != hipSuccess))
         return c->err = ncclUnhandledCudaError;
       off += (mine[k]->bytes + 63) & ~63ull;
     }
