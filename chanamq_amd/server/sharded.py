@@ -173,7 +173,12 @@ def main(argv=None):
                        "plane": {k: plane.info[k] for k in ("log_bytes", "msg_max", "c_max", "q_max", "ingress_cap",
                                                             "egress_cap", "spill_bytes")
                                  if hasattr(plane, "info") and k in plane.info},
-                       "front_end": {k: v for k, v in fes.items() if k != "lat_hist"}}, f)
+                       "front_end": {k: v for k, v in fes.items() if k != "lat_hist"},
+                       # (diagnostics) control ops not yet synced, deferred replies, and with
+                       # CHANAMQ_CTL_TRACE=1 the tail of the control trace
+                       "control": {"outbox": len(node.log.outbox), "applied": node.log.applied,
+                                   "deferred": len(getattr(broker, "_deferred", {}) or {}),
+                                   "trace": [repr(t) for t in list(broker.ctl_trace or [])[-40:]]}}, f)
         os.replace(path + ".tmp", path)
     write_info()
     stop = threading.Event()

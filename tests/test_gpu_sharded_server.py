@@ -21,7 +21,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 def _xchg_env(xchg):
     """--xchg rccl: the engine's RCCL exchange through the tests' librccl stand-in (RCCL
     itself refuses several ranks on one GPU)."""
-    env = dict(os.environ, PYTHONPATH=os.path.dirname(HERE))
+    env = dict(os.environ, PYTHONPATH=os.path.dirname(HERE), CHANAMQ_CTL_TRACE="1")   # (trace: in rank*.json)
     if xchg == "rccl":
         from chanamq_amd import ops
         env.update(CHANAMQ_RCCL_LIB=ops.build_rccl_standin(), CHANAMQ_RCCL_STANDIN_OK="1")
@@ -283,7 +283,7 @@ chana.mq.gpu {
   message-table = 4194304
 }
 """)
-    env = dict(os.environ, PYTHONPATH=os.path.dirname(HERE))
+    env = dict(os.environ, PYTHONPATH=os.path.dirname(HERE), CHANAMQ_CTL_TRACE="1")   # (trace: in rank*.json)
     ln = Launcher(2, ["-m", "chanamq_amd.server.sharded", "--config", str(conf), "--plane", "gpu", "--port", "0",
                       "--backend", "gloo", "--info-dir", str(tmp_path), "--xchg-timeout-ms", "10000"], env=env).start()
     try:
