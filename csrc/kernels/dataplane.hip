@@ -3597,9 +3597,13 @@ DEV void spill_queue(const DS& d, u32 q, u64 lim, u32 hot, u32 budget, u64* move
 
 // true: the block wrote runs with plain stores (the fused k_runs' ticket needs an
 // agent-scope release); false: at most q_nruns[q] = 0, stored agent-coherent
+// a consumer's dispatch inputs, loaded by the block's other waves while wave 0 walks the
+// TTL head (thread 0's credit loop then reads them from LDS: only its atomics stay serial)
+struct DqCons { u32 c, ch, ok, noack, pc, glob, unacked; };
 DEV bool dequeue_queue(const DS& d) {
   __shared__ u32 g_cons[RUNS_PER_Q];
   __shared__ u32 g_n[RUNS_PER_Q];
+  __shared__ DqCons g_ci[RUNS_PER_Q];
   __shared__ u64 s_head;
   __shared__ u32 s_ngr;
   __shared__ unsigned long long s_bytes;
@@ -3694,6 +3698,25 @@ DEV bool dequeue_queue(const DS& d) {
       if (live) break;
     }
     if (lane == 0) { s_head = head; s_bytes = 0; }
+  } else if (!nodisp && tid - 64 < RUNS_PER_Q) {   // the consumers' inputs, beside the TTL walk
+    const u32 j = tid - 64, mall0 = d.q_cons_n[q];
+    if (j < mall0) {
+      const u32 c = d.q_cons[d.q_cons_off[q] + (d.q_rr[q] % mall0 + j) % mall0];
+      const u32 ch = d.cons_ch[c];
+      DqCons ci;
+      ci.c = c;
+      ci.ch = ch;
+      // wblock: the front end's socket backlog for this connection is above its high
+      // watermark (host-mapped, written by the IO threads): its messages stay queued in HBM
+      // (cons_active 2: staged by a light control section this step -- it takes deliveries
+      // from the next step on, behind its Basic.ConsumeOk)
+      ci.ok = d.cons_active[c] == 1u && d.ch_flow[ch] && !d.conn_wblock[ch / d.chpc];
+      ci.noack = d.cons_noack[c];
+      ci.pc = d.ch_prefetch[ch];
+      ci.glob = d.ch_global[ch];
+      ci.unacked = d.cons_unacked[c];
+      g_ci[j] = ci;
+    }
   }
   __syncthreads();
   head = s_head;
@@ -3780,32 +3803,29 @@ DEV bool dequeue_queue(const DS& d) {
   }
   const u32 m = mall > RUNS_PER_Q - ngr ? RUNS_PER_Q - ngr : mall;
   const u32 r = d.q_rr[q] % mall;
-  // (1) counts by credit
+  // (1) counts by credit (the consumers' inputs came in beside the TTL walk: g_ci)
   if (tid == 0) {
     u64 remaining = avail;
     for (u32 j = 0; j < m; ++j) {
-      u32 c = d.q_cons[d.q_cons_off[q] + (r + j) % mall];
+      const DqCons ci = g_ci[j];
+      u32 c = ci.c;
       g_cons[j] = c;
       g_n[j] = 0;
       if (remaining == 0) continue;
-      u32 ch = d.cons_ch[c];
-      // wblock: the front end's socket backlog for this connection is above its high
-      // watermark (host-mapped, written by the IO threads): its messages stay queued in HBM
-      // (cons_active 2: staged by a light control section this step -- it takes deliveries
-      // from the next step on, behind its Basic.ConsumeOk)
-      if (d.cons_active[c] != 1u || !d.ch_flow[ch] || d.conn_wblock[ch / d.chpc]) continue;
+      u32 ch = ci.ch;
+      if (!ci.ok) continue;
       u64 share = (remaining + (m - j) - 1) / (m - j);
       u32 want = (u32)(share < d.deliver_cap ? share : d.deliver_cap);
-      bool noack = d.cons_noack[c];
-      u32 pc = d.ch_prefetch[ch];
-      if (!noack && pc && !d.ch_global[ch]) {
-        u32 used = d.cons_unacked[c];
+      bool noack = ci.noack;
+      u32 pc = ci.pc;
+      if (!noack && pc && !ci.glob) {
+        u32 used = ci.unacked;
         u32 cr = used < pc ? pc - used : 0;
         want = want < cr ? want : cr;
       }
       u32 wb;
       u32 g = reserve_upto(&d.ch_win[ch], want, d.ucap_mask + 1, &wb);
-      if (!noack && pc && d.ch_global[ch] && g) {
+      if (!noack && pc && ci.glob && g) {
         u32 ub;
         u32 g2 = reserve_upto(&d.ch_unacked[ch], g, pc, &ub);
         if (g2 < g) atomicSub(&d.ch_win[ch], g - g2);
@@ -3827,8 +3847,21 @@ DEV bool dequeue_queue(const DS& d) {
       const u32 cnt = g_n[j];
       if (!cnt) continue;
       const u32 c = g_cons[j];
-      const u32 conn = d.cons_ch[c] / d.chpc;
-      for (u32 k = tid; k < cnt; k += 256) mine += deliver_size(d, c, d.msgs[ring[(qp + k) & mask].msg], conn);
+      const u32 conn = g_ci[j].ch / d.chpc;
+      // four entries a thread per round, their ring loads then their message loads in flight
+      // together (a round trip each per entry in series before)
+      constexpr u32 U = 4;
+      for (u32 k0 = tid; k0 < cnt; k0 += 256 * U) {
+        u32 mg[U];
+#pragma unroll
+        for (u32 u = 0; u < U; ++u) {
+          const u32 k = k0 + u * 256;
+          mg[u] = k < cnt ? ring[(qp + k) & mask].msg : INVALID;
+        }
+#pragma unroll
+        for (u32 u = 0; u < U; ++u)
+          if (mg[u] != INVALID) mine += deliver_size(d, c, d.msgs[mg[u]], conn);
+      }
       qp += cnt;
     }
     for (int o = 32; o > 0; o >>= 1) mine += __shfl_xor(mine, o, 64);

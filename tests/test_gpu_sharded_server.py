@@ -91,7 +91,6 @@ def test_pipelined_cross_rank_routing_and_topology(cluster):
 
 
 @pytest.mark.timeout(300)
-@pytest.mark.parametrize("cluster", ["shm", "shm-async", "rccl-async"], indirect=True)
 def test_pipelined_remote_consumers_and_gets(cluster):
     """X2/X3 on the device: a consumer on rank 1 of rank 0's queue (deliveries shipped as
     restore records in the exchange, acks back as ack records), manual ack with prefetch,
