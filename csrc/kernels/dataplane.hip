@@ -650,7 +650,6 @@ DEV void frame_scan_seg(const DS& d, const u32 s) {
   __shared__ u32 sh_cmd_base, sh_frag_base, sh_ncmd;
   __shared__ u32 sh_get0, sh_gch, sh_gq, sh_gna, sh_gbase;   // Basic.Get: the segment's first, its key
   __shared__ u32 sh_split;   // split mode: bytes [0, sh_split) are in the work buffer
-  __shared__ u32 sh_c0ch, sh_c0chs, sh_c0tx;   // the segment's first frame: channel, slot, tx
 
   const u32 tid = threadIdx.x;
   const u32 conn = d.segs[s].conn;
@@ -732,20 +731,6 @@ DEV void frame_scan_seg(const DS& d, const u32 s) {
     return;
   }
   if (tid == 0) { sh_m = 0; sh_over = 0; }
-  if (tid == FS_NT - 1) {
-    // the channel of the segment's first frame, looked up beside the screen: a connection
-    // publishes on one channel, so phase (e) finds most frames' channel slot and tx flag here
-    // (two dependent global round trips less there)
-    u32 c0 = 0xffffffffu, s0 = 0, t0 = 0;
-    const u8* h0 = seg_cl ? seg_C : seg_N;   // (the work copy of a carry segment is not written yet)
-    if (L >= 8 && seg_cl != 1 && seg_cl != 2 && h0[0] >= 1 && h0[0] <= 3) {
-      c0 = be16(h0 + 1);
-      const i32 cs = c0 ? chan_lookup(d, conn, c0) : -1;
-      s0 = (u32)cs;
-      t0 = cs >= 0 ? d.ch_tx[cs] : 0u;
-    }
-    sh_c0ch = c0; sh_c0chs = s0; sh_c0tx = t0;
-  }
   __syncthreads();
 
   FS_MARK(0);
@@ -1227,8 +1212,7 @@ DEV void frame_scan_seg(const DS& d, const u32 s) {
       fi = frame_at(b, p, L, fmax);
       cls = be16(b + p + 7);
       mid = be16(b + p + 9);
-      const bool c0 = fi.ch == sh_c0ch;
-      const i32 chs = fi.ch ? (c0 ? (i32)sh_c0chs : chan_lookup(d, conn, fi.ch)) : -1;
+      const i32 chs = fi.ch ? chan_lookup(d, conn, fi.ch) : -1;
       c.pad[0] = (u32)chs;
       if (cls == 60 && mid == 40 && chs >= 0) c.kind = CK_PUBLISH;
       else if (cls == 60 && mid == 70 && chs >= 0 && dget_resolve(d, conn, b, p, fi.size, gq, gna)) c.kind = CK_GET;
@@ -1236,7 +1220,7 @@ DEV void frame_scan_seg(const DS& d, const u32 s) {
       else if (cls == 60 && mid == 90 && chs >= 0) c.kind = CK_REJECT;
       else if (cls == 60 && mid == 120 && chs >= 0) c.kind = CK_NACK;
       else c.kind = CK_CONTROL;
-      if (c.kind != CK_CONTROL && c.kind != CK_GET && (c0 ? sh_c0tx : d.ch_tx[chs])) c.kind = CK_TXBUF;   // held until Tx.Commit
+      if (c.kind != CK_CONTROL && c.kind != CK_GET && d.ch_tx[chs]) c.kind = CK_TXBUF;   // held until Tx.Commit
       if (cls == 60 && mid == 40) {
         hp = CPOS(f + 1);
         hi = frame_at(b, hp, L, fmax);
