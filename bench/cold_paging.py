@@ -42,6 +42,8 @@ def main():
     ap.add_argument("--drainers", type=int, default=4)
     ap.add_argument("--live-rate", type=float, default=10000.0, help="live msgs/s (1 KB, 1P1C)")
     ap.add_argument("--io-threads", type=int, default=4)
+    ap.add_argument("--deliver-cap-bytes", type=int, default=1 << 20,
+                    help="per-consumer egress per step (the server's chana.mq.gpu.deliver-cap-bytes; 0 = off)")
     ap.add_argument("--cold-sync", action="store_true", help="cold tier between paused steps (the old path)")
     ap.add_argument("--hold-s", type=float, default=6.0, help="live stream next to the resting backlog first")
     ap.add_argument("--out", default="")
@@ -56,7 +58,8 @@ def main():
     plane = GpuDataPlane(c_max=64, chpc=8, q_max=64, cons_max=256, seg_max=64, cmd_max=1 << 16, deliv_max=1 << 16,
                          msg_max=1 << 20, ucap=4096, deliver_cap=4096, ingress_cap=32 << 20, egress_cap=64 << 20,
                          log_bytes=args.log_mb << 20, log_block=1 << 20, spill_bytes=args.ring_mb << 20,
-                         ring_pool=1 << 23, default_queue_capacity=1 << 20, carry_cap=1 << 20)
+                         ring_pool=1 << 23, default_queue_capacity=1 << 20, carry_cap=1 << 20,
+                         deliver_cap_bytes=args.deliver_cap_bytes)
     b = GpuBroker(plane, idle_step_ms=0.5, io="pipeline", io_threads=args.io_threads, mem_high_watermark=0,
                   cold_dir=cold_dir, cold_hot=4096, cold_window=4096, cold_beside=not args.cold_sync).start()
     out = dict(config=vars(args), cold_dir=cold_dir)

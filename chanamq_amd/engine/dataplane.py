@@ -158,6 +158,10 @@ class GpuDataPlane(ControlState):
         """Apply the staged control writes now (the caller holds the engine: no step in flight)."""
         self.eng.flush_deltas()
 
+    def set_deliver_cap_bytes(self, n):
+        """Per-step byte cap of one consumer's deliveries (StepIn.dcap_bytes; 0 = off)."""
+        self.eng.set_deliver_cap_bytes(int(n))
+
     def deltas_pending(self):
         """(records, bytes, channels to mark) staged and not yet taken by a step."""
         return tuple(self.eng.deltas_pending())

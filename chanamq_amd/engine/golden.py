@@ -41,7 +41,7 @@ class _Msg:
 class GoldenDataPlane(ControlState):
     def __init__(self, hash_wildcard=True, ucap=8192, deliver_cap=4096, carry_cap=1 << 20,
                  egress_cap=96 << 20, deliv_max=65536, exchanger=None, xfer_desc_max=1 << 15,
-                 xfer_bytes=1 << 24, persist=False, exchange_lag=0, persist_max=1 << 16, **kw):
+                 xfer_bytes=1 << 24, persist=False, exchange_lag=0, persist_max=1 << 16, deliver_cap_bytes=0, **kw):
         super().__init__(hash_wildcard=hash_wildcard, **kw)
         self.persist = persist
         # k_dequeue: durable TTL skips <= persist_max / 4 a step; the engine raises
@@ -63,6 +63,7 @@ class GoldenDataPlane(ControlState):
             self._xr_desc = torch.zeros(xfer_desc_max * RDESC.itemsize, dtype=torch.uint8)
             self._xr_pay = torch.zeros(xfer_bytes, dtype=torch.uint8)
         self.ucap, self.deliver_cap, self.carry_cap = ucap, deliver_cap, carry_cap
+        self.deliver_cap_bytes = int(deliver_cap_bytes)
         self.egress_cap, self.deliv_max = egress_cap, deliv_max
         self.carry = defaultdict(bytes)
         self.step_no = 0
@@ -846,7 +847,7 @@ class GoldenDataPlane(ControlState):
             return got
         m = min(mall, 64 - len(got))
         r = self.qrr[q] % mall
-        remaining = len(ring)
+        remaining = n_ring = len(ring)
         grants = []
         for j in range(m):
             cid = qq.consumers[(r + j) % mall]
@@ -858,6 +859,10 @@ class GoldenDataPlane(ControlState):
             if remaining and c.active and chan.flow:
                 share = -(-remaining // (m - j))
                 want = min(share, self.deliver_cap)
+                cap = self.deliver_cap_bytes
+                if cap and want > 1:   # byte cap: max(1, cap / size of the consumer's first delivery)
+                    s0 = self._deliver_size(c, ring[n_ring - remaining][0])
+                    want = min(want, 1 if s0 >= cap else cap // s0)
                 pc = chan.prefetch_count
                 if not c.no_ack and pc and not chan.global_:
                     want = min(want, max(pc - self.cons_unacked[cid], 0))
@@ -890,6 +895,17 @@ class GoldenDataPlane(ControlState):
         del ring[:pos]
         self.qpos_head[q] += pos
         return got + out
+
+    def set_deliver_cap_bytes(self, n):
+        self.deliver_cap_bytes = int(n)
+
+    def _deliver_size(self, c, m):
+        """Rendered size of a Basic.Deliver of m to consumer c (k_dequeue's deliver_size)."""
+        fm = self.conns[c.conn].frame_max
+        mp = 4 + 1 + len(c.tag.encode()[:255]) + 8 + 1 + 1 + len(m.ex) + 1 + len(m.rk)
+        fmb = fm - 8 if fm else None
+        nb = (-(-len(m.body) // fmb) if fmb else 1) if m.body else 0
+        return 8 + mp + 8 + 12 + len(m.props) + len(m.body) + 8 * nb
 
     def _render_deliver(self, d, fm):
         m = d["msg"]

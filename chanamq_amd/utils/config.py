@@ -254,6 +254,7 @@ class Config:
             x_max=int(g(k + "max-exchanges", 1024)), cons_max=int(g(k + "max-consumers", 16384)),
             seg_max=int(g(k + "max-segments-per-step", 1024)), cmd_max=int(g(k + "max-commands-per-step", 131072)),
             deliv_max=int(g(k + "max-deliveries-per-step", 65536)), deliver_cap=int(g(k + "deliver-cap", 8192)),
+            deliver_cap_bytes=int(g(k + "deliver-cap-bytes", 1 << 20)),
             msg_max=int(g(k + "message-table", 1 << 24)), log_bytes=int(g(k + "body-log-bytes", 64 << 30)),
             ring_pool=int(g(k + "queue-ring-pool", 1 << 28)),
             default_queue_capacity=int(g(k + "queue-capacity", 1 << 16)), ucap=int(g(k + "unacked-window", 8192)),

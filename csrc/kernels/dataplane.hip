@@ -3816,6 +3816,12 @@ DEV bool dequeue_queue(const DS& d) {
       if (!ci.ok) continue;
       u64 share = (remaining + (m - j) - 1) / (m - j);
       u32 want = (u32)(share < d.deliver_cap ? share : d.deliver_cap);
+      const u32 dcb = d.in->dcap_bytes;
+      if (dcb && want > 1 && !(d.links && d.conn_link[ch / d.chpc])) {   // byte cap (StepIn.dcap_bytes)
+        const u32 s0 = deliver_size(d, c, d.msgs[ring[(head + (avail - remaining)) & mask].msg], ch / d.chpc);
+        const u32 lim = s0 >= dcb ? 1u : dcb / s0;
+        want = want < lim ? want : lim;
+      }
       bool noack = ci.noack;
       u32 pc = ci.pc;
       if (!noack && pc && !ci.glob) {

@@ -82,7 +82,11 @@ struct StepIn {         // host -> device per step (96 B)
   u32 ref_back;
   u32 ref_min;
   u64 ingress_host;
-  u64 pad_;
+  // a consumer takes at most max(1, dcap_bytes / s) deliveries this step, s = the rendered
+  // size of the first one (0: no byte cap): bounds one connection's egress per step, so a
+  // deep-backlog drain does not stretch the front end's IO phase for everyone else
+  u32 dcap_bytes;
+  u32 pad_;
 };
 static_assert(sizeof(StepIn) == 112, "StepIn layout");
 

@@ -133,6 +133,7 @@ class Engine {
     u32 ucap = next_pow2((u32)get("ucap", 8192));
     d_.ucap_mask = ucap - 1;
     d_.deliver_cap = (u32)get("deliver_cap", 4096);
+    dcap_bytes_ = (u32)get("deliver_cap_bytes", 0);
     d_.chmap_size = next_pow2(d_.chpc * 2);
     u32 xhash = next_pow2(d_.x_max * 2);
     d_.xhash_mask = xhash - 1;
@@ -892,6 +893,7 @@ class Engine {
     in->ref_back = ref_back_ >= 0 ? (u32)ref_back_ : ref_back_ == -2 ? REF_SPILL_ONLY : 0xffffffffu;
     in->ref_min = ref_min_;
     in->ingress_host = ref_back_ >= 0 && payload_len ? payload_ptr : 0;
+    in->dcap_bytes = dcap_bytes_;
     in->flags = sflags;
     in->now_ms = now_ms;
     in->step = step;
@@ -2871,6 +2873,9 @@ class Engine {
   u64* cold_end_ = nullptr;
   // overlapped steps (world 1)
   bool overlap_ = false;
+ public:
+  u32 dcap_bytes_ = 0;   // StepIn.dcap_bytes of the next submitted steps (deliver_cap_bytes)
+ private:
   hipStream_t s_ing_ = nullptr;
   hipEvent_t ev_ing_[2], ev_rest_[2];
   bool rest_issued_[2] = {false, false}, ing_issued_[2] = {false, false};
@@ -3019,6 +3024,7 @@ PYBIND11_MODULE(_dataplane, m) {
       .def("egress_wait", &Engine::egress_wait)
       .def("egress_slot", &Engine::egress_slot)
       .def("set_egress_ref", &Engine::set_egress_ref)
+      .def("set_deliver_cap_bytes", [](Engine& e, u32 n) { e.dcap_bytes_ = n; })
       .def("egress_wait_slot", &Engine::egress_wait_slot)
       .def("egress_done_slot", &Engine::egress_done_slot)
       .def("step_done", &Engine::step_done)

@@ -284,7 +284,26 @@ def sc_mixed_multiple_settles(dp):
     return [{1: s}, {2: mixed}, {}, {2: rev}, {}, {2: ack_frame(1, 0)}, {}]
 
 
+def sc_deliver_cap_bytes(dp):
+    """A backlog of large then small bodies drained by an auto-ack and a manual-ack consumer
+    under a per-step byte cap: each consumer takes max(1, cap / size of its first delivery)
+    a step (StepIn.dcap_bytes), so the drain spreads over steps with ~cap bytes each."""
+    dp.set_deliver_cap_bytes(2500)
+    dp.declare_queue(VH, "big")
+    dp.open_connection(1, VH)
+    dp.open_channel(1, 1)
+    dp.open_connection(2, VH)
+    dp.open_channel(2, 1)
+    dp.open_connection(3, VH)
+    dp.open_channel(3, 1)
+    dp.consume(2, 1, VH, "big", "auto", no_ack=True)
+    dp.consume(3, 1, VH, "big", "man", no_ack=False)
+    s = publish_stream(14, "", lambda i: "big", 900, seed=11) + publish_stream(30, "", lambda i: "big", 40, seed=12)
+    return [{1: s}, {}, {3: ack_frame(1, 0, multiple=True)}, {}, {3: ack_frame(1, 0, multiple=True)}, {}, {}, {}]
+
+
 SCENARIOS = {
+    "deliver_cap_bytes": sc_deliver_cap_bytes,
     "mixed_multiple_settles": sc_mixed_multiple_settles,
     "ring_growth": sc_ring_growth,
     "confirm_ring_full": sc_confirm_ring_full,
