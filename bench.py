@@ -208,6 +208,9 @@ def main():
                          "previous step's routing half); 0 (default): the whole step as one graph on one "
                          "stream (no cross-queue hand-off between the halves; measured equal throughput, "
                          "p50 0.85 vs 1.10 ms at 49152, profiles/r5_fs1, r5_split)")
+    ap.add_argument("--h2d-at-wait", type=int, default=1, choices=[0, 1],
+                    help="1: queue the next step's payload H2D right after the wait on step t-1's kernels "
+                         "(its latency clock starts there); 0: at its submit")
     ap.add_argument("--loop", choices=["poll", "block"], default="block",
                     help="host loop: poll = submit as soon as a parity frees and stamp each egress when it "
                          "lands (non-blocking queries); block = submit / prefetch / wait egress t-2 / finish t-1")
@@ -480,6 +483,15 @@ def main():
                 t, s = pending.pop(0)
                 dp.wait(t)
                 waited.append((t, s))
+                # the next step's payload H2D right behind the wait (its parity is free now):
+                # the copy engine restarts without waiting for the loop's bookkeeping and
+                # submit; the step's latency clock starts here, where its bytes are queued
+                if args.h2d_at_wait and not args.prefetch and not storm and world == 1 and step_i < end \
+                        and step_i not in pre:
+                    nb = step_i % args.blocks
+                    sub_t[step_i] = time.perf_counter()
+                    if dp.prefetch(base + offs[nb], blens[nb]):
+                        pre.add(step_i)
             tp.append(time.perf_counter())
             if measure:
                 ph = [round((b2 - a2) * 1e3, 3) for a2, b2 in zip(tp, tp[1:])]
