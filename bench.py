@@ -208,6 +208,10 @@ def main():
                          "previous step's routing half); 0 (default): the whole step as one graph on one "
                          "stream (no cross-queue hand-off between the halves; measured equal throughput, "
                          "p50 0.85 vs 1.10 ms at 49152, profiles/r5_fs1, r5_split)")
+    ap.add_argument("--parities", type=int, default=3, choices=[2, 3],
+                    help="per-step IO sets of the engine (single GPU, --overlap 0): 3 = the next step is submitted once "
+                         "step t-2 is collected, so its ingress H2D never waits for the host to see step t-1 end; "
+                         "2 = double buffering")
     ap.add_argument("--h2d-at-wait", type=int, default=1, choices=[0, 1],
                     help="1: queue the next step's payload H2D right after the wait on step t-1's kernels "
                          "(its latency clock starts there); 0: at its submit")
@@ -301,7 +305,7 @@ def main():
                log_bytes=16 << 30, ring_pool=Q * qcap + qtot + 1024, tb_max=max(64, qtot) if not fan else 64,
                fan_max=max(1 << 20, qtot * 2), carry_cap=256 << 10, graph=0 if args.no_graph else 1,
                copy_engine={"blit": 0, "nocu": 1, "kernel": 2, "sdma": 3}[args.copy_engine], copy_wgs=args.copy_wgs, sdma_engine=args.sdma_engine,
-               sdma_split=args.sdma_split, egress_gate=args.egress_gate, overlap=args.overlap,
+               sdma_split=args.sdma_split, egress_gate=args.egress_gate, overlap=args.overlap, parities=args.parities,
                egress_ref=0 if args.egress_ref else -1)
     native = shards > 1 and args.xchg == "native"
     if native:
@@ -318,6 +322,7 @@ def main():
     pool, segs, offs, blens, mps, msg_bytes, extra = build_workload(dp, rank, P, Q, args.body, args.chunk,
                                                                     args.blocks, cons_base=P, shards=shards,
                                                                     kind=args.workload)
+    npar = dp.info.get("parities", 2)   # steps in flight before the host waits for the oldest
     flow_high = 1 << 30      # storm: producers pause (Channel.Flow) above 1 GiB of stored bodies
     flow = {"paused": False, "paused_steps": 0, "requeued": 0}
     base = pool.ctypes.data
@@ -479,7 +484,7 @@ def main():
             tp.append(time.perf_counter())
             # step i-1's kernels (the host's only per-step wait on them): frees its parity, so
             # the next iteration's submit -- step i+1's ingress H2D -- follows the wait at once
-            if len(pending) > 1:
+            if len(pending) > npar - 1:
                 t, s = pending.pop(0)
                 dp.wait(t)
                 waited.append((t, s))
@@ -541,7 +546,7 @@ def main():
             step_i += 1
             dp.finish(tk, collect=False, wait_egress=True)
             verified += verify_egress(dp, base, sum(blens) + 64, [tk])
-    c = dp.eng.counters((step_i - 1) & 1)
+    c = dp.eng.counters((step_i - 1) % npar)
     errs = {k: c[k] for k in ("n_dropped_nomem", "n_ring_full", "n_unknown_exchange", "n_unroutable",
                               "n_routed_msgs", "n_pairs", "n_deliv", "n_live_msgs") if c[k]}
 
@@ -639,7 +644,8 @@ def main():
                           + (", librccl stand-in" if os.environ.get("CHANAMQ_RCCL_LIB") else "") + ")") if native else args.xchg)
                          if shards > 1 else None,
             "async_exchange": bool(args.async_x) if shards > 1 else None,
-            "prefetch": bool(args.prefetch), "chunk_bytes_per_producer": args.chunk,
+            "prefetch": bool(args.prefetch), "parities": npar, "h2d_at_wait": bool(args.h2d_at_wait),
+            "chunk_bytes_per_producer": args.chunk,
             "post_soak_s": args.soak_s,
         }
         print(json.dumps(out), flush=True)

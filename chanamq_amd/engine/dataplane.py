@@ -83,6 +83,11 @@ class GpuDataPlane(ControlState):
         full.setdefault("egress_ref_back", -1 if egress_ref is None else int(egress_ref))
         # (k_frame_scan reads new bytes in place; CHANAMQ_SCAN_IN_PLACE=0 for the copy path)
         full.setdefault("scan_in_place", int(os.environ.get("CHANAMQ_SCAN_IN_PLACE", "1")))
+        # per-step IO sets: 3 on a single-GPU engine without the overlapped ingest (the engine
+        # keeps 2 otherwise); CHANAMQ_PARITIES=3 selects it (and that engine mode) for tests
+        if int(os.environ.get("CHANAMQ_PARITIES", "0")) >= 3 and world == 1:
+            full.setdefault("parities", 3)
+            full.setdefault("overlap", 0)
         full.update(device=device, hash_wildcard=int(hash_wildcard), graph=int(graph), world=world, rank=rank,
                     exchange_lag=int(exchange_lag))
         self.eng = self.mod.Engine(full)
@@ -98,10 +103,11 @@ class GpuDataPlane(ControlState):
         self._io = [dict(seg_out=self.eng.host_view(f"seg_out{p}").view(SEG_OUT),
                          ctrl_rec=self.eng.host_view(f"ctrl_rec{p}").view(CTRL_REC),
                          conn_out=self.eng.host_view(f"conn_out{p}").view(CONN_OUT),
-                         ctrl=self.eng.host_view(f"ctrl{p}")) for p in (0, 1)]
+                         ctrl=self.eng.host_view(f"ctrl{p}")) for p in range(i.get("parities", 2))]
+        self.parities = i.get("parities", 2)
         # rendered egress: the engine rotates i["egress_slots"] buffers over the steps
         self._egress = [self.eng.host_view(f"egress_host{e}") for e in range(i["egress_slots"])]
-        self._pin = [None, None]
+        self._pin = [None] * self.parities
         self.exchanger = exchanger
         self._get_consumed = []   # store records of Basic.Get, emitted with the next step's
         self._pending = None
@@ -825,7 +831,7 @@ class GpuDataPlane(ControlState):
         order = sorted(conns)
         segs = np.zeros(len(order), SEG_IN)
         total = sum((len(inputs.get(c, b"")) + 15) & ~15 for c in order)
-        pin = self._pinned(total + 16, self.step_no & 1)
+        pin = self._pinned(total + 16, self.step_no % self.parities)
         off = 0
         for k, c in enumerate(order):
             data = inputs.get(c, b"")

@@ -14,7 +14,7 @@
 #define LAT_BINS 32
 #define WORLD_MAX 16          // ranks of one sharded broker (one node: 8 GPUs)
 #define INGRESS_SLOTS 3       // rotating ingress payload buffers (StepIn.ingress)
-#define EGRESS_SLOTS 3        // rotating egress buffers (render of step t || D2H of t-1, t-2)
+#define EGRESS_SLOTS 4        // rotating egress buffers (render of step t || D2H of t-1 .. t-3)
 #define RUNS_PER_Q 64         // consumers served per queue per step (dequeue round-robin window)
 #define RUN_SORT_LDS 8192     // runs sorted in LDS by k_runs (more: global-memory sort)
 #define SPILL_LAG 6           // steps a freed spill-ring byte stays untouched (egress by reference)

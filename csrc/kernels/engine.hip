@@ -63,6 +63,12 @@ struct Buf {
   bool view = false;   // a named range of another allocation (not freed on its own)
 };
 
+// per-step IO sets ("parities"): step t uses set t % npar_.  Two (double buffering) by
+// default; three for a single-GPU engine without the overlapped ingest (cfg "parities"): the
+// host then submits step t+1 once step t-2 -- not t-1 -- is collected, so the next step's
+// ingress H2D never waits for the host to notice the previous step's kernels ending
+static constexpr int NPAR_MAX = 3;
+
 class Engine {
  public:
   explicit Engine(py::dict cfg) {
@@ -220,9 +226,10 @@ class Engine {
       for (int k = 0; k < INGRESS_SLOTS; ++k)
         ingress_slot_[k] = (u8*)view(("ingress_s" + std::to_string(k)).c_str(), base + 2 * wb + k * ib, d_.ingress_cap + 64);
     }
-    // per-parity step IO: step t uses set t&1, so step t+1's H2D and step t-1's D2H
-    // overlap step t's kernels (double buffering; the graph of each parity is captured once)
-    for (int p = 0; p < 2; ++p) {
+    // per-parity step IO: step t uses set t % npar_, so step t+1's H2D and step t-1's D2H
+    // overlap step t's kernels (the graph of each parity is captured once)
+    npar_ = (d_.world == 1 && get("overlap", 1) == 0 && get("parities", 2) >= 3) ? 3 : 2;
+    for (int p = 0; p < npar_; ++p) {
       std::string sfx = std::to_string(p);
       DS& io = io_[p];
       io.in = (StepIn*)dev(("in" + sfx).c_str(), sizeof(StepIn));
@@ -550,7 +557,7 @@ class Engine {
     dup(&DS::pub_kwoff, "pub_kwoff", 2ull * TOPIC_WORDS * d_.pub_cap + 64);
     dup(&DS::acks, "acks", sizeof(Ack) * (u64)d_.ack_max);
     dup(&DS::dget, "dget", sizeof(DGet) * (u64)DGET_MAX);
-    for (int p = 0; p < 2; ++p) {
+    for (int p = 0; p < npar_; ++p) {
       DS io = d_;
       if (p == 1)
         for (auto& f : par1_) f(io);
@@ -631,7 +638,7 @@ class Engine {
       HIPCHECK(hipDeviceGetStreamPriorityRange(&lo, &hi));
       HIPCHECK(hipStreamCreateWithPriority(&s_ing_, hipStreamNonBlocking, hi));
     }
-    for (int p = 0; p < 2; ++p) {
+    for (int p = 0; p < npar_; ++p) {
       HIPCHECK(hipEventCreateWithFlags(&ev_ing_[p], hipEventDisableTiming));
       HIPCHECK(hipEventCreateWithFlags(&ev_pre_[p], hipEventDisableTiming));
       HIPCHECK(hipEventCreateWithFlags(&ev_rest_[p], hipEventDisableTiming));
@@ -653,7 +660,7 @@ class Engine {
     // after it saw the step finish (egress_copy)
     // (sharded ranks too: the step's last kernel -- phase B's -- opens the gate the same way)
     gated_ = copy_mode_ == 3 && get("egress_gate", 1) != 0;
-    for (int p = 0; p < 2; ++p) {
+    for (int p = 0; p < npar_; ++p) {
       HIPCHECK(hipEventCreateWithFlags(&ev_h2d_[p], hipEventDisableTiming));
       HIPCHECK(hipEventCreateWithFlags(&ev_done_[p], hipEventDisableTiming));
       HIPCHECK(hipEventCreateWithFlags(&ev_a_[p], hipEventDisableTiming));
@@ -689,7 +696,7 @@ class Engine {
     (void)hipStreamSynchronize(s_h2d_);
     (void)hipStreamSynchronize(s_pre_);
     (void)hipStreamSynchronize(s_d2h_);
-    for (int p = 0; p < 2; ++p) {
+    for (int p = 0; p < npar_; ++p) {
       if (graph_exec_[p]) (void)hipGraphExecDestroy(graph_exec_[p]);
       if (graph_b_[p]) (void)hipGraphExecDestroy(graph_b_[p]);
       (void)hipEventDestroy(ev_a_[p]);
@@ -827,6 +834,7 @@ class Engine {
     o["egress_ref_back"] = ref_back_;
     o["egress_ref_min"] = ref_min_;
     o["egress_slots"] = EGRESS_SLOTS;
+    o["parities"] = npar_;
     { u32 e = 0; while (copy_mode_ == 3 && e < 32 && !(((u32)sdma_engine_ >> e) & 1u)) ++e; o["sdma_engine"] = copy_mode_ == 3 ? (int)e : -1; }
     { u32 e = 0; while (sdma_engine2_ && e < 32 && !(((u32)sdma_engine2_ >> e) & 1u)) ++e; o["sdma_engine2"] = sdma_engine2_ ? (int)e : -1; }
     o["persist"] = d_.persist; o["persist_max"] = d_.persist_max; o["persist_bytes"] = d_.persist_bytes;
@@ -868,7 +876,7 @@ class Engine {
     const u64 step = seq_;
     if (nseg > d_.seg_max) throw std::runtime_error("too many segments");
     if (payload_len > d_.ingress_cap) throw std::runtime_error("ingress payload exceeds ingress_cap");
-    int p = (int)(seq_ & 1);
+    int p = (int)(seq_ % (u64)npar_);
     if (inflight_[p]) throw std::runtime_error("submit: results of the previous step of this parity not collected");
     HIPCHECK(hipEventSynchronize(ev_h2d_[p]));  // staging buffers of step t-2 are free
     // the payload first: the H2D is the step's longest stage and nothing below changes what
@@ -968,10 +976,10 @@ class Engine {
     if (d_.world != 1 || !payload_len) return false;   // (s_pre_ is s_h2d_: the step waits for it)
     Range rg("chanamq.step.prefetch");
     u64 tgt = seq_;
-    int p = (int)(tgt & 1);
+    int p = (int)(tgt % (u64)npar_);
     if (pre_[p]) {   // the next submit's payload is queued already: the one after it
       tgt = seq_ + 1;
-      p = (int)(tgt & 1);
+      p = (int)(tgt % (u64)npar_);
       if (pre_[p]) return false;
     }
     if (staged_[p]) throw std::runtime_error("prefetch: this step's payload is already queued");
@@ -1692,7 +1700,7 @@ class Engine {
   void set_xfer_buffers(u64 send_desc, u64 send_pay, u64 recv_desc, u64 recv_pay) {
     d_.send_desc = (RDesc*)send_desc; d_.send_pay = (u8*)send_pay;
     d_.recv_desc = (const RDesc*)recv_desc; d_.recv_pay = (const u8*)recv_pay;
-    for (int p = 0; p < 2; ++p) {
+    for (int p = 0; p < npar_; ++p) {
       io_[p].send_desc = d_.send_desc; io_[p].send_pay = d_.send_pay;
       io_[p].recv_desc = d_.recv_desc; io_[p].recv_pay = d_.recv_pay;
       if (graph_exec_[p]) { HIPCHECK(hipGraphExecDestroy(graph_exec_[p])); graph_exec_[p] = nullptr; }
@@ -2204,7 +2212,7 @@ class Engine {
     a.set_egress_ref = [](void* e, int back, u32 min_bytes) -> int {
       return ((Engine*)e)->guard([&] { ((Engine*)e)->set_egress_ref(back, min_bytes); return 0; });
     };
-    for (int p = 0; p < 2; ++p) {
+    for (int p = 0; p < npar_; ++p) {
       std::string sfx = std::to_string(p);
       HostIO& h = io_[p];
       h.ctr_host_h = (const Counters*)buf("ctr_host" + sfx).ptr;
@@ -2783,18 +2791,18 @@ class Engine {
   u32 scan_smax_ = 0;
   bool graph_enabled_ = true;
   bool sdma_ = true;
-  hipGraphExec_t graph_exec_[2] = {nullptr, nullptr};
-  hipGraphExec_t graph_b_[2] = {nullptr, nullptr};
-  hipEvent_t ev_a_[2], ev_ext_[2];
-  bool phase_a_[2] = {false, false};
-  bool counts_ready_[2] = {false, false};
+  hipGraphExec_t graph_exec_[NPAR_MAX] = {};
+  hipGraphExec_t graph_b_[NPAR_MAX] = {};
+  hipEvent_t ev_a_[NPAR_MAX], ev_ext_[NPAR_MAX];
+  bool phase_a_[NPAR_MAX] = {};
+  bool counts_ready_[NPAR_MAX] = {};
   bool lag_ = false;
   std::vector<u32> lag_recv_;
   u64 lag_stream_ = 0;
   bool xfer_set_ = false;
   // native exchange
   bool native_x_ = false;
-  bool b_due_[2] = {false, false};   // phase A launched, phase B not yet (native exchange)
+  bool b_due_[NPAR_MAX] = {};   // phase A launched, phase B not yet (native exchange)
   std::unique_ptr<cmqx::RcclXchg> rccl_;
   std::unique_ptr<cmqx::ShmXchg> shm_;
   std::unique_ptr<cmqx::ShmXchg> cshm_;   // rccl + host shared-memory count exchange
@@ -2812,7 +2820,7 @@ class Engine {
   int xq_ = 0, xres_rc_ = 0;
   u32 xflags_ = 0, xres_orf_ = 0, xjob_seq_ = 0, xseq_job_ = 0;
   std::string xerr_;
-  u32 b_wait_[2] = {0, 0};           // launch_b(p): the job phase B of parity p waits for (0: none)
+  u32 b_wait_[NPAR_MAX] = {};           // launch_b(p): the job phase B of parity p waits for (0: none)
   u32* xflag_h_ = nullptr;           // host-mapped [0] last finished job, [1] a device wait gave up
   std::mutex cap_mu_;                // graph captures vs the exchange thread's HIP calls
   hipStream_t s_x_ = nullptr;        // the shared-memory exchange's copies
@@ -2855,8 +2863,8 @@ class Engine {
   u32 dl_open_ = 0;   // light sections staging now (stage_begin / stage_end)
   u64 dl_next_id_ = 1;   // id of the next batch (DlBatch.id)
   u64 dl_bytes_ = 0;
-  u8* dl_h_[2] = {nullptr, nullptr};
-  u32 dl_step_[2] = {0, 0};
+  u8* dl_h_[NPAR_MAX] = {};
+  u32 dl_step_[NPAR_MAX] = {};
   u64 dl_steps_ = 0;
   static constexpr u32 COLD_BATCH = 1u << 16;   // cold records per pick / scan call
   struct Side { int kind; u32 a; u64 b, c; u32 max_n; u64 max_bytes; u32 n; bool launched; };
@@ -2873,24 +2881,25 @@ class Engine {
   u64* cold_end_ = nullptr;
   // overlapped steps (world 1)
   bool overlap_ = false;
+  int npar_ = 2;   // per-step IO sets in use (NPAR_MAX arrays)
  public:
   u32 dcap_bytes_ = 0;   // StepIn.dcap_bytes of the next submitted steps (deliver_cap_bytes)
  private:
   hipStream_t s_ing_ = nullptr;
-  hipEvent_t ev_ing_[2], ev_rest_[2];
-  bool rest_issued_[2] = {false, false}, ing_issued_[2] = {false, false};
-  bool eager_d2h_[2] = {false, false};   // the step's egress copy was queued at launch (copy_mode 2)
-  bool pre_[2] = {false, false};
+  hipEvent_t ev_ing_[NPAR_MAX], ev_rest_[NPAR_MAX];
+  bool rest_issued_[NPAR_MAX] = {}, ing_issued_[NPAR_MAX] = {};
+  bool eager_d2h_[NPAR_MAX] = {};   // the step's egress copy was queued at launch (copy_mode 2)
+  bool pre_[NPAR_MAX] = {};
   u8* ingress_slot_[INGRESS_SLOTS] = {};
   u8* work_p1_ = nullptr;
   hipEvent_t ev_ing_slot_[INGRESS_SLOTS];
   bool ing_slot_issued_[INGRESS_SLOTS] = {};
-  u64 launch_seq_[2] = {0, 0};          // the step number staged in each parity
-  u64 pre_ptr_[2] = {0, 0}, pre_len_[2] = {0, 0}, pre_seq_[2] = {0, 0};
-  hipEvent_t ev_pre_[2];
+  u64 launch_seq_[NPAR_MAX] = {};          // the step number staged in each parity
+  u64 pre_ptr_[NPAR_MAX] = {}, pre_len_[NPAR_MAX] = {}, pre_seq_[NPAR_MAX] = {};
+  hipEvent_t ev_pre_[NPAR_MAX];
   hipStream_t s_pre_ = nullptr;
-  hipGraphExec_t graph_ing_[2] = {nullptr, nullptr};
-  hipGraphExec_t graph_rest_[2] = {nullptr, nullptr};
+  hipGraphExec_t graph_ing_[NPAR_MAX] = {};
+  hipGraphExec_t graph_rest_[NPAR_MAX] = {};
   u64* scan_status_ing_ = nullptr;
   u32* scan_ctl_ing_ = nullptr;
   // parity 1's copies of the per-step buffers (parity 0 keeps d_'s)
@@ -2900,18 +2909,18 @@ class Engine {
     T* p1 = (T*)alloc((std::string(name) + "_p1").c_str(), bytes, false);
     par1_.push_back([m, p1](DS& io) { io.*m = p1; });
   }
-  GetReq* stage_gets_[2] = {nullptr, nullptr};
-  u32* stage_unp_[2] = {nullptr, nullptr};
-  u32 nunp_[2] = {0, 0};   // unpauses the last submit on each parity carried
-  u32 nget_[2] = {0, 0};
-  HostIO io_[2];
+  GetReq* stage_gets_[NPAR_MAX] = {};
+  u32* stage_unp_[NPAR_MAX] = {};
+  u32 nunp_[NPAR_MAX] = {};   // unpauses the last submit on each parity carried
+  u32 nget_[NPAR_MAX] = {};
+  HostIO io_[NPAR_MAX];
   CmqEngineApi api_{};
   std::string err_;
   u8* egress_dev_[EGRESS_SLOTS] = {};
   u8* egress_host_[EGRESS_SLOTS] = {};
   u8* egress_host_dev_[EGRESS_SLOTS] = {};
-  int slot_of_[2] = {0, 0};
-  int pslot_of_[2] = {0, 0};
+  int slot_of_[NPAR_MAX] = {};
+  int pslot_of_[NPAR_MAX] = {};
   int copy_mode_ = 0;
   hsa_agent_t gpu_agent_{}, cpu_agent_{};
   hsa_amd_sdma_engine_id_t sdma_engine_{}, sdma_engine2_{};
@@ -2936,12 +2945,12 @@ class Engine {
   u32 copy_wgs_ = 16;
   int sdma_pref_ = -1;
   double ht_[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};   // host_times() phases
-  StepIn* stage_in_[2] = {nullptr, nullptr};
-  SegIn* stage_segs_[2] = {nullptr, nullptr};
+  StepIn* stage_in_[NPAR_MAX] = {};
+  SegIn* stage_segs_[NPAR_MAX] = {};
   hipStream_t s_comp_ = nullptr, s_h2d_ = nullptr, s_d2h_ = nullptr;
-  hipEvent_t ev_h2d_[2], ev_done_[2], ev_d2h_[EGRESS_SLOTS];
-  bool inflight_[2] = {false, false};
-  bool staged_[2] = {false, false};   // submitted with defer, kernels not launched yet
+  hipEvent_t ev_h2d_[NPAR_MAX], ev_done_[NPAR_MAX], ev_d2h_[EGRESS_SLOTS];
+  bool inflight_[NPAR_MAX] = {};
+  bool staged_[NPAR_MAX] = {};   // submitted with defer, kernels not launched yet
   bool d2h_issued_[EGRESS_SLOTS] = {};
   u64 seq_ = 0;
 };
