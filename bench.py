@@ -208,10 +208,10 @@ def main():
                          "previous step's routing half); 0 (default): the whole step as one graph on one "
                          "stream (no cross-queue hand-off between the halves; measured equal throughput, "
                          "p50 0.85 vs 1.10 ms at 49152, profiles/r5_fs1, r5_split)")
-    ap.add_argument("--parities", type=int, default=3, choices=[2, 3],
-                    help="per-step IO sets of the engine (single GPU, --overlap 0): 3 = the next step is submitted once "
-                         "step t-2 is collected, so its ingress H2D never waits for the host to see step t-1 end; "
-                         "2 = double buffering")
+    ap.add_argument("--parities", type=int, default=2, choices=[2, 3],
+                    help="per-step IO sets of the engine (single GPU, --overlap 0): 2 (default) = double buffering; "
+                         "3 = the next step is submitted once step t-2 is collected -- measured the same step period "
+                         "at p50 0.79 vs 0.54 ms (profiles/r6_u): the period is the GPU's, not the host's")
     ap.add_argument("--h2d-at-wait", type=int, default=1, choices=[0, 1],
                     help="1: queue the next step's payload H2D right after the wait on step t-1's kernels "
                          "(its latency clock starts there); 0: at its submit")
