@@ -628,6 +628,10 @@ class Engine {
     if (copy_mode_ == 3) init_sdma();
     HIPCHECK(hipStreamCreateWithFlags(&s_comp_, hipStreamNonBlocking));
     HIPCHECK(hipStreamCreateWithFlags(&s_h2d_, hipStreamNonBlocking));
+    // (non-overlapped single GPU, cfg h2d_alt) odd steps' ingress copies on a second stream:
+    // consecutive steps' payloads need not wait for one stream's previous copy to retire
+    if (d_.world == 1 && get("overlap", 1) == 0 && get("h2d_alt", 0) != 0)
+      HIPCHECK(hipStreamCreateWithFlags(&s_h2d_alt_, hipStreamNonBlocking));
     // ingress payloads share the H2D stream: a stream of their own stalled the host for ~6 ms
     // in an early prefetch on some boxes (12+ MB copies; profiles/r4_summary.md)
     s_pre_ = s_h2d_;
@@ -694,6 +698,7 @@ class Engine {
       }
     (void)hipStreamSynchronize(s_comp_);
     (void)hipStreamSynchronize(s_h2d_);
+    if (s_h2d_alt_) (void)hipStreamSynchronize(s_h2d_alt_);
     (void)hipStreamSynchronize(s_pre_);
     (void)hipStreamSynchronize(s_d2h_);
     for (int p = 0; p < npar_; ++p) {
@@ -710,6 +715,7 @@ class Engine {
     if (s_io_) (void)hipStreamDestroy(s_io_);
     (void)hipStreamDestroy(s_comp_);
     (void)hipStreamDestroy(s_h2d_);
+    if (s_h2d_alt_) (void)hipStreamDestroy(s_h2d_alt_);
     (void)hipStreamDestroy(s_d2h_);
     for (auto& kv : bufs_) {
       if (kv.second.view) continue;
@@ -890,7 +896,7 @@ class Engine {
     pre_[p] = false;
     {   // overlapped engines move payloads on their own stream (prefetches run ahead of the
         // small per-step copies there; the ingest half waits for both)
-      hipStream_t ps = overlap_ ? s_pre_ : s_h2d_;
+      hipStream_t ps = overlap_ ? s_pre_ : h2d_of(step);
       if (payload_len && !pre)
         HIPCHECK(hipMemcpyAsync((void*)ingress_slot_[is], (const void*)payload_ptr, payload_len,
                                 sdma_ ? hipMemcpyDeviceToDeviceNoCU : hipMemcpyHostToDevice, ps));
@@ -936,7 +942,7 @@ class Engine {
       GetOut* go = (GetOut*)buf("get_out" + std::to_string(p)).ptr;
       for (u32 i = 0; i < in->nget; ++i) go[i] = GetOut{GS_RETRY, 0};
       HIPCHECK(hipMemcpyAsync((void*)io_[p].get_req, stage_gets_[p], sizeof(GetReq) * in->nget,
-                              hipMemcpyHostToDevice, s_h2d_));
+                              hipMemcpyHostToDevice, h2d_of(step)));
       pend_gets_.clear();
     }
     nget_[p] = in->nget;
@@ -954,10 +960,11 @@ class Engine {
     in->nunp = nunp;
     nunp_[p] = nunp;
     if (in->nunp)
-      HIPCHECK(hipMemcpyAsync((void*)io_[p].unpause_req, stage_unp_[p], 4ull * in->nunp, hipMemcpyHostToDevice, s_h2d_));
+      HIPCHECK(hipMemcpyAsync((void*)io_[p].unpause_req, stage_unp_[p], 4ull * in->nunp, hipMemcpyHostToDevice,
+                              h2d_of(step)));
     dl_step_[p] = in->delta_bytes;
     if (overlap_) HIPCHECK(hipEventRecord(ev_pre_[p], s_pre_));
-    HIPCHECK(hipEventRecord(ev_h2d_[p], s_h2d_));
+    HIPCHECK(hipEventRecord(ev_h2d_[p], overlap_ ? s_h2d_ : h2d_of(step)));
     inflight_[p] = true;
     staged_[p] = true;
     ++seq_;
@@ -988,10 +995,11 @@ class Engine {
     // the drivers' order (bench / front end prefetch t+1 once t-2 is finished); if not,
     // the copy waits for it on the GPU
     const int is = (int)(tgt % INGRESS_SLOTS);
+    hipStream_t ps = overlap_ ? s_pre_ : h2d_of(tgt);
     if (tgt >= INGRESS_SLOTS && ing_slot_issued_[is] && hipEventQuery(ev_ing_slot_[is]) != hipSuccess)
-      HIPCHECK(hipStreamWaitEvent(s_pre_, ev_ing_slot_[is], 0));
+      HIPCHECK(hipStreamWaitEvent(ps, ev_ing_slot_[is], 0));
     HIPCHECK(hipMemcpyAsync((void*)ingress_slot_[is], (const void*)payload_ptr, payload_len,
-                            sdma_ ? hipMemcpyDeviceToDeviceNoCU : hipMemcpyHostToDevice, s_pre_));
+                            sdma_ ? hipMemcpyDeviceToDeviceNoCU : hipMemcpyHostToDevice, ps));
     pre_[p] = true;
     pre_seq_[p] = tgt;
     pre_ptr_[p] = payload_ptr;
@@ -2509,6 +2517,7 @@ class Engine {
 
   void sync() {
     HIPCHECK(hipStreamSynchronize(s_h2d_));
+    if (s_h2d_alt_) HIPCHECK(hipStreamSynchronize(s_h2d_alt_));
     HIPCHECK(hipStreamSynchronize(s_pre_));
     HIPCHECK(hipStreamSynchronize(s_ing_));
     HIPCHECK(hipStreamSynchronize(s_comp_));
@@ -2948,6 +2957,8 @@ class Engine {
   StepIn* stage_in_[NPAR_MAX] = {};
   SegIn* stage_segs_[NPAR_MAX] = {};
   hipStream_t s_comp_ = nullptr, s_h2d_ = nullptr, s_d2h_ = nullptr;
+  hipStream_t s_h2d_alt_ = nullptr;   // odd steps' H2D (cfg h2d_alt)
+  hipStream_t h2d_of(u64 step) const { return (s_h2d_alt_ && (step & 1)) ? s_h2d_alt_ : s_h2d_; }
   hipEvent_t ev_h2d_[NPAR_MAX], ev_done_[NPAR_MAX], ev_d2h_[EGRESS_SLOTS];
   bool inflight_[NPAR_MAX] = {};
   bool staged_[NPAR_MAX] = {};   // submitted with defer, kernels not launched yet
