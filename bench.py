@@ -519,7 +519,7 @@ def main():
 
     # the host loop is the pipeline's driver: no collector pause inside the window.  Collected
     # before the warm-up steps, which then re-warm the allocator (a collection right before
-    # the window made the first timed submit 0.6 ms slower: profiles/r5_first/)
+    # the window made the first timed submit 0.6 ms slower, round 5: profiles/r5_summary.md)
     import gc
     gc.collect()
     gc.disable()
