@@ -88,6 +88,12 @@ class GpuDataPlane(ControlState):
         if int(os.environ.get("CHANAMQ_PARITIES", "0")) >= 3 and world == 1:
             full.setdefault("parities", 3)
             full.setdefault("overlap", 0)
+        # CHANAMQ_H2D_HSA=1: ingress payloads through HSA, waited for on the device (engine cfg
+        # h2d_hsa; single GPU without the overlapped ingest, HSA egress)
+        if int(os.environ.get("CHANAMQ_H2D_HSA", "0")) and world == 1:
+            full.setdefault("h2d_hsa", 1)
+            full.setdefault("overlap", 0)
+            full.setdefault("copy_engine", 3)
         full.update(device=device, hash_wildcard=int(hash_wildcard), graph=int(graph), world=world, rank=rank,
                     exchange_lag=int(exchange_lag))
         self.eng = self.mod.Engine(full)

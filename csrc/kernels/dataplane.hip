@@ -399,6 +399,28 @@ __global__ __launch_bounds__(1024) void k_apply_deltas(DS d, const u8* buf) {
   apply_deltas(d, buf, threadIdx.x, 1024, lrec);
 }
 
+// ============================================================================ K0' ingress wait
+// the step's ingress payload copy, queued by the host on an SDMA engine through HSA (Engine
+// h2d_hsa): waited for here, on the device, between k_stage and the frame scan.  No marker
+// on a HIP stream and no cross-queue barrier sits between two steps' copies, so they run back
+// to back on their engine (12.7 MB each: 237.7 us per copy this way vs 262 us with
+// hipMemcpyAsync + event + stream wait, bench/micro/h2d_chain_probe.hip, profiles/r6_z).
+// The SDMA engine writes HBM behind the L2s: every block (16 of them, two per XCD) ends with
+// a system-scope acquire, dropping its XCD's stale lines before any kernel reads the slot.
+// Bounded: a copy that never completes lets the step run on and the host's check of the
+// signal at collection (Engine::wait_results) reports it
+__global__ __launch_bounds__(64) void k_h2d_wait(DS d) {
+  const u64 sig = d.in->h2d_sig;
+  if (!sig) return;
+  if (threadIdx.x == 0)
+    for (u32 it = 0; it < (1u << 24); ++it) {
+      if (__hip_atomic_load((const i64*)sig, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == 0) break;
+      __builtin_amdgcn_s_sleep(4);
+    }
+  __syncthreads();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+}
+
 // ============================================================================ K0 step init
 // one block: resets the step counters and lays the step's segments out in the work buffer
 // (segment k at the prefix of the 16-aligned sizes carry + new bytes + 32 of the segments

@@ -87,8 +87,12 @@ struct StepIn {         // host -> device per step (96 B)
   // deep-backlog drain does not stretch the front end's IO phase for everyone else
   u32 dcap_bytes;
   u32 pad_;
+  // the value word of the HSA completion signal of this step's ingress copy when the host
+  // queued it on an SDMA engine itself (0: a runtime copy the step's stream waits for):
+  // k_h2d_wait holds the step's frame scan until it reads 0
+  u64 h2d_sig;
 };
-static_assert(sizeof(StepIn) == 112, "StepIn layout");
+static_assert(sizeof(StepIn) == 120, "StepIn layout");
 
 
 

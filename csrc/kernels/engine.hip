@@ -632,6 +632,14 @@ class Engine {
     // consecutive steps' payloads need not wait for one stream's previous copy to retire
     if (d_.world == 1 && get("overlap", 1) == 0 && get("h2d_alt", 0) != 0)
       HIPCHECK(hipStreamCreateWithFlags(&s_h2d_alt_, hipStreamNonBlocking));
+    // (non-overlapped single GPU, HSA egress, cfg h2d_hsa) ingress payloads queued on an SDMA
+    // engine through HSA and waited for on the device (k_h2d_wait): consecutive steps' copies
+    // run back to back, with no HIP marker / cross-queue barrier between them
+    h2d_hsa_ = copy_mode_ == 3 && !sdma_ && d_.world == 1 && get("overlap", 1) == 0 && get("h2d_hsa", 0) != 0;
+    if (h2d_hsa_)
+      for (int k = 0; k < INGRESS_SLOTS; ++k)
+        if (hsa_signal_create(0, 0, nullptr, &ing_sig_[k]) != HSA_STATUS_SUCCESS)
+          throw std::runtime_error("hsa_signal_create failed");
     // ingress payloads share the H2D stream: a stream of their own stalled the host for ~6 ms
     // in an early prefetch on some boxes (12+ MB copies; profiles/r4_summary.md)
     s_pre_ = s_h2d_;
@@ -696,10 +704,17 @@ class Engine {
           try { sdma_wait(e); } catch (const std::exception&) {}   // (reported already)
         }
       }
+    for (int k = 0; k < INGRESS_SLOTS; ++k)
+      if (ing_sig_[k].handle) {
+        if (ing_hsa_[k]) (void)hsa_signal_wait_scacquire(ing_sig_[k], HSA_SIGNAL_CONDITION_EQ, 0, 2000 * block_ticks_,
+                                                          HSA_WAIT_STATE_BLOCKED);
+      }
     (void)hipStreamSynchronize(s_comp_);
     (void)hipStreamSynchronize(s_h2d_);
     if (s_h2d_alt_) (void)hipStreamSynchronize(s_h2d_alt_);
     (void)hipStreamSynchronize(s_pre_);
+    for (int k = 0; k < INGRESS_SLOTS; ++k)
+      if (ing_sig_[k].handle) hsa_signal_destroy(ing_sig_[k]);
     (void)hipStreamSynchronize(s_d2h_);
     for (int p = 0; p < npar_; ++p) {
       if (graph_exec_[p]) (void)hipGraphExecDestroy(graph_exec_[p]);
@@ -843,6 +858,7 @@ class Engine {
     o["parities"] = npar_;
     { u32 e = 0; while (copy_mode_ == 3 && e < 32 && !(((u32)sdma_engine_ >> e) & 1u)) ++e; o["sdma_engine"] = copy_mode_ == 3 ? (int)e : -1; }
     { u32 e = 0; while (sdma_engine2_ && e < 32 && !(((u32)sdma_engine2_ >> e) & 1u)) ++e; o["sdma_engine2"] = sdma_engine2_ ? (int)e : -1; }
+    { u32 e = 0; while (h2d_hsa_ && e < 32 && !(((u32)ing_engine_ >> e) & 1u)) ++e; o["h2d_hsa_engine"] = h2d_hsa_ ? (int)e : -1; }
     o["persist"] = d_.persist; o["persist_max"] = d_.persist_max; o["persist_bytes"] = d_.persist_bytes;
     o["restore_max"] = restore_max_;
     o["xfer_desc_max"] = d_.xfer_desc_max; o["xfer_bytes"] = d_.xfer_bytes; o["world_max"] = WORLD_MAX;
@@ -897,12 +913,14 @@ class Engine {
     {   // overlapped engines move payloads on their own stream (prefetches run ahead of the
         // small per-step copies there; the ingest half waits for both)
       hipStream_t ps = overlap_ ? s_pre_ : h2d_of(step);
-      if (payload_len && !pre)
-        HIPCHECK(hipMemcpyAsync((void*)ingress_slot_[is], (const void*)payload_ptr, payload_len,
-                                sdma_ ? hipMemcpyDeviceToDeviceNoCU : hipMemcpyHostToDevice, ps));
+      if (payload_len && !pre) ingress_copy(step, is, payload_ptr, payload_len, ps);
+      else if (!payload_len) ing_hsa_[is] = false;
     }
     StepIn* in = stage_in_[p];
     *in = StepIn{};
+    in->h2d_sig = ing_hsa_[is] ? (u64)&((amd_signal_t*)ing_sig_[is].handle)->value : 0;
+    // the step's stream waits for the H2D stream only when a runtime copy of this step is on it
+    h2d_hip_[p] = !h2d_hsa_ || (payload_len && !ing_hsa_[is]) || !pend_gets_.empty();
     in->nseg = nseg;
     in->ref_back = ref_back_ >= 0 ? (u32)ref_back_ : ref_back_ == -2 ? REF_SPILL_ONLY : 0xffffffffu;
     in->ref_min = ref_min_;
@@ -963,6 +981,7 @@ class Engine {
       HIPCHECK(hipMemcpyAsync((void*)io_[p].unpause_req, stage_unp_[p], 4ull * in->nunp, hipMemcpyHostToDevice,
                               h2d_of(step)));
     dl_step_[p] = in->delta_bytes;
+    if (in->nunp) h2d_hip_[p] = true;
     if (overlap_) HIPCHECK(hipEventRecord(ev_pre_[p], s_pre_));
     HIPCHECK(hipEventRecord(ev_h2d_[p], overlap_ ? s_h2d_ : h2d_of(step)));
     inflight_[p] = true;
@@ -996,10 +1015,7 @@ class Engine {
     // the copy waits for it on the GPU
     const int is = (int)(tgt % INGRESS_SLOTS);
     hipStream_t ps = overlap_ ? s_pre_ : h2d_of(tgt);
-    if (tgt >= INGRESS_SLOTS && ing_slot_issued_[is] && hipEventQuery(ev_ing_slot_[is]) != hipSuccess)
-      HIPCHECK(hipStreamWaitEvent(ps, ev_ing_slot_[is], 0));
-    HIPCHECK(hipMemcpyAsync((void*)ingress_slot_[is], (const void*)payload_ptr, payload_len,
-                            sdma_ ? hipMemcpyDeviceToDeviceNoCU : hipMemcpyHostToDevice, ps));
+    ingress_copy(tgt, is, payload_ptr, payload_len, ps);
     pre_[p] = true;
     pre_seq_[p] = tgt;
     pre_ptr_[p] = payload_ptr;
@@ -1342,7 +1358,7 @@ class Engine {
       return;
     }
     if (side_h_) run_side(s_comp_);
-    HIPCHECK(hipStreamWaitEvent(s_comp_, ev_h2d_[p], 0));
+    if (h2d_hip_[p]) HIPCHECK(hipStreamWaitEvent(s_comp_, ev_h2d_[p], 0));
     if (d2h_issued_[e]) HIPCHECK(hipStreamWaitEvent(s_comp_, ev_d2h_[e], 0));
     if (d_.world > 1 && !xfer_set_) throw std::runtime_error("set_xfer_buffers() before the first sharded step");
     if (graph_enabled_) {
@@ -2312,6 +2328,14 @@ class Engine {
     if (staged_[p]) throw std::runtime_error("wait_results: step staged but never launched");
     HIPCHECK(hipEventSynchronize(ev_done_[p]));
     inflight_[p] = false;
+    if (h2d_hsa_) {   // (k_h2d_wait gives up after ~2^24 polls: the step then ran on a stale slot)
+      const int is = (int)(launch_seq_[p] % INGRESS_SLOTS);
+      if (ing_hsa_[is] && hsa_signal_load_scacquire(ing_sig_[is]) != 0) {
+        wait_failed_ = true;
+        throw std::runtime_error("ingress copy of step " + std::to_string(launch_seq_[p]) +
+                                 " did not complete before its step ran (HSA SDMA copy lost)");
+      }
+    }
     // egress history of the gated copies' sizing (every finished step, idle ones too)
     const u64 n = ((const Counters*)buf("ctr_host" + std::to_string(p)).ptr)->egress_bytes;
     eg_hist_[eg_hist_i_++ & 3] = n;
@@ -2401,7 +2425,7 @@ class Engine {
     const auto t0 = std::chrono::steady_clock::now();
     while (hsa_signal_wait_scacquire(sig, HSA_SIGNAL_CONDITION_EQ, 0, block_ticks_, HSA_WAIT_STATE_BLOCKED) != 0) {
       if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(wait_ms_)) {
-        if (gate_sig_[e].handle) hsa_signal_store_screlease(gate_sig_[e], 0);
+        if (e >= 0 && gate_sig_[e].handle) hsa_signal_store_screlease(gate_sig_[e], 0);
         wait_failed_ = true;
         throw std::runtime_error(std::string(what) + " of egress slot " + std::to_string(e) + " did not complete within " +
                                  std::to_string(wait_ms_) + " ms (gate never opened / copy lost)");
@@ -2501,6 +2525,17 @@ class Engine {
         tail_engine_ = (hsa_amd_sdma_engine_id_t)(1u << c);
         break;
       }
+    // the ingress engine (cfg h2d_hsa): engine 0, the runtime's own H2D engine -- the egress
+    // engines stay free of it (measured: egress on engine 0 next to the ingress copies halves
+    // the throughput, profiles/r6_x); else any full-rate engine the egress does not use
+    ing_engine_ = (hsa_amd_sdma_engine_id_t)0;
+    for (u32 c : {0u, 3u, 2u, 1u})
+      if (((mask >> c) & 1u) && (1u << c) != (u32)sdma_engine_ && (1u << c) != (u32)sdma_engine2_ &&
+          (1u << c) != (u32)tail_engine_) {
+        ing_engine_ = (hsa_amd_sdma_engine_id_t)(1u << c);
+        break;
+      }
+    if (!ing_engine_) ing_engine_ = tail_engine_;
     for (int e = 0; e < EGRESS_SLOTS; ++e)
       if (hsa_signal_create(0, 0, nullptr, &sdma_sig_[e]) != HSA_STATUS_SUCCESS ||
           hsa_signal_create(0, 0, nullptr, &tail_sig_[e]) != HSA_STATUS_SUCCESS ||
@@ -2619,6 +2654,7 @@ class Engine {
   void launch_ingest(hipStream_t s, const DS& d) {
     Range rg("chanamq.K1-K4.ingest");
     hipLaunchKernelGGL(k_stage, dim3(1), dim3(1024), 0, s, d);
+    if (h2d_hsa_) hipLaunchKernelGGL(k_h2d_wait, dim3(16), dim3(64), 0, s, d);
     // one block per CU fits (154 KB of LDS): more blocks than CUs only queue behind the
     // busy ones, and blocks past the step's segments would still be dispatched one by one
     // after them (the grid is sized for capacity at capture)
@@ -2959,6 +2995,47 @@ class Engine {
   hipStream_t s_comp_ = nullptr, s_h2d_ = nullptr, s_d2h_ = nullptr;
   hipStream_t s_h2d_alt_ = nullptr;   // odd steps' H2D (cfg h2d_alt)
   hipStream_t h2d_of(u64 step) const { return (s_h2d_alt_ && (step & 1)) ? s_h2d_alt_ : s_h2d_; }
+  // cfg h2d_hsa: ingress payloads in GPU-mapped host memory go to the SDMA engine through HSA
+  bool h2d_hsa_ = false;
+  hsa_amd_sdma_engine_id_t ing_engine_{};
+  hsa_signal_t ing_sig_[INGRESS_SLOTS] = {};
+  bool ing_hsa_[INGRESS_SLOTS] = {};   // the slot's last payload went through HSA (ing_sig_)
+  bool h2d_hip_[NPAR_MAX] = {true, true, true};   // the step's stream waits for ev_h2d_
+
+  // the agent address of a payload in page-locked host memory (hipHostMalloc /
+  // hipHostRegister), 0 for pageable memory (the runtime's copy stages that)
+  static u64 ingress_src(u64 ptr) {
+    hipPointerAttribute_t a{};
+    if (hipPointerGetAttributes(&a, (const void*)ptr) != hipSuccess) {
+      (void)hipGetLastError();
+      return 0;
+    }
+    return a.type == hipMemoryTypeHost && a.devicePointer ? (u64)a.devicePointer : 0;
+  }
+
+  // a step's payload into ingress slot is: on the HSA path (k_h2d_wait waits for it on the
+  // device) or as a runtime copy on stream ps (the step's stream waits for ev_h2d_)
+  void ingress_copy(u64 step, int is, u64 ptr, u64 len, hipStream_t ps) {
+    const u64 src = h2d_hsa_ ? ingress_src(ptr) : 0;
+    if (src) {
+      // the slot's last reader (step - INGRESS_SLOTS, collected long ago in the drivers'
+      // order) and its copy are done before the signal is re-armed
+      if (step >= INGRESS_SLOTS && ing_slot_issued_[is] && hipEventQuery(ev_ing_slot_[is]) != hipSuccess)
+        HIPCHECK(hipEventSynchronize(ev_ing_slot_[is]));
+      if (ing_hsa_[is]) bounded_wait(ing_sig_[is], -1, "ingress H2D");
+      hsa_signal_store_relaxed(ing_sig_[is], 1);
+      if (hsa_amd_memory_async_copy_on_engine(ingress_slot_[is], gpu_agent_, (const void*)src, cpu_agent_, len, 0,
+                                              nullptr, ing_sig_[is], ing_engine_, true) != HSA_STATUS_SUCCESS)
+        throw std::runtime_error("hsa_amd_memory_async_copy_on_engine (ingress) failed");
+      ing_hsa_[is] = true;
+      return;
+    }
+    if (step >= INGRESS_SLOTS && ing_slot_issued_[is] && hipEventQuery(ev_ing_slot_[is]) != hipSuccess)
+      HIPCHECK(hipStreamWaitEvent(ps, ev_ing_slot_[is], 0));
+    HIPCHECK(hipMemcpyAsync((void*)ingress_slot_[is], (const void*)ptr, len,
+                            sdma_ ? hipMemcpyDeviceToDeviceNoCU : hipMemcpyHostToDevice, ps));
+    ing_hsa_[is] = false;
+  }
   hipEvent_t ev_h2d_[NPAR_MAX], ev_done_[NPAR_MAX], ev_d2h_[EGRESS_SLOTS];
   bool inflight_[NPAR_MAX] = {};
   bool staged_[NPAR_MAX] = {};   // submitted with defer, kernels not launched yet

@@ -9,7 +9,10 @@ pytestmark = pytest.mark.gpu
 from gpu_cfg import CFG  # noqa: E402
 
 
-@pytest.fixture(params=[(True, 0), (False, 0), (True, 2), (True, 3)], ids=["graph", "eager", "copykernel", "hsa-sdma"])
+# h2d-hsa: the ingress payload copies on an SDMA engine through HSA, waited for on the
+# device by k_h2d_wait (single GPU without the overlapped ingest; bench --h2d-hsa)
+@pytest.fixture(params=[(True, 0), (False, 0), (True, 2), (True, 3), (True, 3, {"h2d_hsa": 1, "overlap": 0})],
+                ids=["graph", "eager", "copykernel", "hsa-sdma", "h2d-hsa"])
 def graph(request):
     return request.param
 
@@ -22,7 +25,10 @@ def test_gpu_matches_golden(gpu, name, graph):
     g = GoldenDataPlane(c_max=CFG["c_max"], chpc=CFG["chpc"], q_max=CFG["q_max"], x_max=CFG["x_max"],
                         cons_max=CFG["cons_max"], ucap=CFG["ucap"], carry_cap=CFG["carry_cap"],
                         default_queue_capacity=CFG["default_queue_capacity"])
-    d = GpuDataPlane(graph=graph[0], copy_engine=graph[1], **CFG)
+    extra = graph[2] if len(graph) > 2 else {}
+    d = GpuDataPlane(graph=graph[0], copy_engine=graph[1], **extra, **CFG)
+    if extra.get("h2d_hsa"):
+        assert d.info["h2d_hsa_engine"] >= 0
     steps_g = SCENARIOS[name](g)
     steps_d = SCENARIOS[name](d)
     og = run(g, steps_g, now_step_ms=3000)
