@@ -265,6 +265,16 @@ class Config:
             # cold message bodies spill to this much pinned host memory once the HBM log fills
             # (-1 = auto: an eighth of the host's RAM, at most 64 GiB)
             spill_bytes=_auto_spill(int(g(k + "spill-bytes", -1))))
+        # step pipeline (engine defaults unless set): the egress D2H engine (blit | sdma), the
+        # overlapped ingest half, and the ingress H2D through HSA with a device-side wait
+        # (h2d-hsa: single GPU, overlap off, sdma egress; bench.py's default step pipeline)
+        ce = g(k + "copy-engine", None)
+        if ce is not None:
+            plane["copy_engine"] = {"blit": 0, "nocu": 1, "kernel": 2, "sdma": 3}[str(ce)]
+        for key, name in (("overlap", "overlap"), ("h2d-hsa", "h2d_hsa")):
+            v = g(k + key, None)
+            if v is not None:
+                plane[name] = int(bool(v))
         if store_dir:
             plane.update(persist=1, persist_max=int(g(k + "persist-records", 1 << 16)),
                          persist_bytes=int(g(k + "persist-bytes", 256 << 20)))

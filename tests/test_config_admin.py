@@ -116,3 +116,15 @@ def test_sharded_rank_reads_gpu_config(tmp_path):
     args = argparse.Namespace(c_max=64, idle_step_ms=0.5, io_threads=2)
     plane, broker = sharded_plane_config(cfg, args, world=2, rank=0, pipeline=False)
     assert plane["c_max"] == 64 and plane["native_xchg"] == 0 and broker["idle_step_ms"] == 0.5
+
+
+def test_gpu_step_pipeline_keys(tmp_path):
+    """chana.mq.gpu.copy-engine / overlap / h2d-hsa reach the engine config only when set
+    (the engine's defaults otherwise)."""
+    from chanamq_amd.utils.config import Config
+    plane, _ = Config.load([], {}).gpu_config()
+    assert not {"copy_engine", "overlap", "h2d_hsa"} & set(plane)
+    f = tmp_path / "p.conf"
+    f.write_text("chana.mq.gpu { copy-engine = sdma, overlap = false, h2d-hsa = true }\n")
+    plane, _ = Config.load([str(f)], {}).gpu_config()
+    assert plane["copy_engine"] == 3 and plane["overlap"] == 0 and plane["h2d_hsa"] == 1
