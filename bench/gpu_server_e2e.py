@@ -56,7 +56,8 @@ def plane_for(spec):
                         ingress_cap=64 << 20, egress_cap=160 << 20, log_bytes=8 << 30, ring_pool=1 << 27,
                         spill_bytes=SIZING.get("spill_bytes", 8 << 30),   # (default tiering: old bodies leave HBM)
                         tb_max=256, default_queue_capacity=1 << 20, persist=int(persist),
-                        persist_max=1 << 16, persist_bytes=512 << 20, carry_cap=SIZING["carry_cap"])
+                        persist_max=1 << 16, persist_bytes=512 << 20, carry_cap=SIZING["carry_cap"],
+                        **SIZING.get("plane_cfg", {}))
 
 
 def thread_cpu():
@@ -450,6 +451,9 @@ def main():
     ap.add_argument("--egress-ref", type=int, default=1,
                     help="1: the front end sends delivered bodies from the host ingress arenas (egress by "
                          "reference); 0: every delivered body comes back over PCIe in the egress bytes")
+    ap.add_argument("--plane-cfg", default="",
+                    help='JSON engine settings for the server plane, e.g. {"copy_engine": 3, "overlap": 0, '
+                         '"h2d_hsa": 1} (the step pipeline of bench.py; chana.mq.gpu.copy-engine / overlap / h2d-hsa)')
     ap.add_argument("--with-store", action="store_true",
                     help="every run with a store on disk attached (a durable broker)")
     args = ap.parse_args()
@@ -457,6 +461,8 @@ def main():
     BROKER_CFG["persist_group_ms"] = args.persist_group_ms
     BROKER_CFG["confirm_read"] = args.confirm_read
     SIZING["spill_bytes"] = args.spill_bytes
+    if args.plane_cfg:
+        SIZING["plane_cfg"] = json.loads(args.plane_cfg)
     SIZING.update(per_conn_read=args.per_conn_read, carry_cap=max(args.carry_cap, 2 * args.per_conn_read))
     if args.wblock_high:
         FE_CFG.update(wblock_high=args.wblock_high, wblock_low=args.wblock_high // 4)
