@@ -31,7 +31,7 @@ def sharded_plane_config(cfg, args, world, rank, pipeline):
     same keys and defaults as the single-GPU launcher (AMQPServer.scala:52-70: every node
     boots from the same HOCON) -- plus the rank's place in the group.  Command-line flags
     override their keys.  Every rank keeps store rows (persist) for failover adoption."""
-    plane, broker = cfg.gpu_config()
+    plane, broker = cfg.gpu_config(single=False)
     plane.pop("device", None)   # each rank drives its own LOCAL_RANK GPU
     if args.c_max:
         plane["c_max"] = args.c_max

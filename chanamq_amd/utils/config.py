@@ -243,8 +243,12 @@ class Config:
             "hash_wildcard": bool(g("chana.mq.routing.topic-hash-wildcard", True)),
         }
 
-    def gpu_config(self):
-        """``chana.mq.gpu.*`` -> (GpuDataPlane keyword arguments, GpuBroker keyword arguments)."""
+    def gpu_config(self, single=True):
+        """``chana.mq.gpu.*`` -> (GpuDataPlane keyword arguments, GpuBroker keyword arguments).
+        ``single``: the single-GPU server, whose step pipeline defaults to bench.py's (SDMA
+        egress, whole step one graph, ingress through HSA: TCP config 2 at 5 M msgs/s p50 0.56
+        vs 0.86 ms, p99 1.6 vs 6.3 ms, profiles/r6_fe2/); sharded ranks keep the engine's
+        defaults unless the keys are set."""
         g = self.get
         k = "chana.mq.gpu."
         store_dir = g("chana.mq.store.dir", "")
@@ -268,11 +272,11 @@ class Config:
         # step pipeline (engine defaults unless set): the egress D2H engine (blit | sdma), the
         # overlapped ingest half, and the ingress H2D through HSA with a device-side wait
         # (h2d-hsa: single GPU, overlap off, sdma egress; bench.py's default step pipeline)
-        ce = g(k + "copy-engine", None)
+        ce = g(k + "copy-engine", "sdma" if single else None)
         if ce is not None:
             plane["copy_engine"] = {"blit": 0, "nocu": 1, "kernel": 2, "sdma": 3}[str(ce)]
-        for key, name in (("overlap", "overlap"), ("h2d-hsa", "h2d_hsa")):
-            v = g(k + key, None)
+        for key, name, dflt in (("overlap", "overlap", False), ("h2d-hsa", "h2d_hsa", True)):
+            v = g(k + key, dflt if single else None)
             if v is not None:
                 plane[name] = int(bool(v))
         if store_dir:

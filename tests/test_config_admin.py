@@ -119,12 +119,14 @@ def test_sharded_rank_reads_gpu_config(tmp_path):
 
 
 def test_gpu_step_pipeline_keys(tmp_path):
-    """chana.mq.gpu.copy-engine / overlap / h2d-hsa reach the engine config only when set
-    (the engine's defaults otherwise)."""
+    """chana.mq.gpu.copy-engine / overlap / h2d-hsa: the single-GPU server defaults to
+    bench.py's step pipeline, sharded ranks to the engine's; set keys win."""
     from chanamq_amd.utils.config import Config
-    plane, _ = Config.load([], {}).gpu_config()
+    plane, _ = Config.load([], {}).gpu_config()   # the single-GPU server: bench.py's pipeline
+    assert plane["copy_engine"] == 3 and plane["overlap"] == 0 and plane["h2d_hsa"] == 1
+    plane, _ = Config.load([], {}).gpu_config(single=False)   # sharded ranks: the engine's
     assert not {"copy_engine", "overlap", "h2d_hsa"} & set(plane)
     f = tmp_path / "p.conf"
-    f.write_text("chana.mq.gpu { copy-engine = sdma, overlap = false, h2d-hsa = true }\n")
+    f.write_text("chana.mq.gpu { copy-engine = blit, overlap = true, h2d-hsa = false }\n")
     plane, _ = Config.load([str(f)], {}).gpu_config()
-    assert plane["copy_engine"] == 3 and plane["overlap"] == 0 and plane["h2d_hsa"] == 1
+    assert plane["copy_engine"] == 0 and plane["overlap"] == 1 and plane["h2d_hsa"] == 0
