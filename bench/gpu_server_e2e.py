@@ -451,9 +451,10 @@ def main():
     ap.add_argument("--egress-ref", type=int, default=1,
                     help="1: the front end sends delivered bodies from the host ingress arenas (egress by "
                          "reference); 0: every delivered body comes back over PCIe in the egress bytes")
-    ap.add_argument("--plane-cfg", default="",
-                    help='JSON engine settings for the server plane, e.g. {"copy_engine": 3, "overlap": 0, '
-                         '"h2d_hsa": 1} (the step pipeline of bench.py; chana.mq.gpu.copy-engine / overlap / h2d-hsa)')
+    ap.add_argument("--plane-cfg", default='{"copy_engine": 3, "overlap": 0, "h2d_hsa": 1}',
+                    help="JSON engine settings for the server plane; default: the single-GPU server's step "
+                         "pipeline (SDMA egress, one graph, ingress through HSA -- chana.mq.gpu.copy-engine / "
+                         "overlap / h2d-hsa); '{}': the engine's defaults (blit egress, overlapped ingest)")
     ap.add_argument("--with-store", action="store_true",
                     help="every run with a store on disk attached (a durable broker)")
     args = ap.parse_args()
