@@ -412,8 +412,9 @@ __global__ __launch_bounds__(1024) void k_apply_deltas(DS d, const u8* buf) {
 __global__ __launch_bounds__(64) void k_h2d_wait(DS d) {
   const u64 sig = d.in->h2d_sig;
   if (!sig) return;
+  const u32 lim = d.in->h2d_polls ? d.in->h2d_polls : (1u << 24);
   if (threadIdx.x == 0)
-    for (u32 it = 0; it < (1u << 24); ++it) {
+    for (u32 it = 0; it < lim; ++it) {
       if (__hip_atomic_load((const i64*)sig, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == 0) break;
       __builtin_amdgcn_s_sleep(4);
     }

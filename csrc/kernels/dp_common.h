@@ -86,7 +86,7 @@ struct StepIn {         // host -> device per step (96 B)
   // size of the first one (0: no byte cap): bounds one connection's egress per step, so a
   // deep-backlog drain does not stretch the front end's IO phase for everyone else
   u32 dcap_bytes;
-  u32 pad_;
+  u32 h2d_polls;        // k_h2d_wait's poll budget (0: 2^24, ~20 s; tests lower it)
   // the value word of the HSA completion signal of this step's ingress copy when the host
   // queued it on an SDMA engine itself (0: a runtime copy the step's stream waits for):
   // k_h2d_wait holds the step's frame scan until it reads 0

@@ -525,6 +525,7 @@ class Engine {
     d_.tot = (u32*)dev("tot", 4ull * 128);
     d_.egress_budget = (u64*)dev("egress_budget", 8);
     gate_dummy_ = dev("gate_dummy", 64);
+    h2d_dummy_ = pinned("h2d_dummy", 64);
     // Basic.Get: rendered frames + result, host-mapped (a stored body never exceeds the
     // carry, which bounds an assembled command)
     get_cap_ = (u64)d_.carry_cap + d_.carry_cap / 64 + 4096;
@@ -919,6 +920,13 @@ class Engine {
     StepIn* in = stage_in_[p];
     *in = StepIn{};
     in->h2d_sig = ing_hsa_[is] ? (u64)&((amd_signal_t*)ing_sig_[is].handle)->value : 0;
+    if (in->h2d_sig && h2d_fault_) {   // (tests) the step waits on a word no copy completes
+      h2d_fault_ = false;
+      *(volatile i64*)h2d_dummy_ = 1;
+      in->h2d_sig = (u64)h2d_dummy_;
+      in->h2d_polls = 4096;
+    }
+    h2d_addr_[p] = in->h2d_sig;
     // the step's stream waits for the H2D stream only when a runtime copy of this step is on it
     h2d_hip_[p] = !h2d_hsa_ || (payload_len && !ing_hsa_[is]) || !pend_gets_.empty();
     in->nseg = nseg;
@@ -2328,9 +2336,8 @@ class Engine {
     if (staged_[p]) throw std::runtime_error("wait_results: step staged but never launched");
     HIPCHECK(hipEventSynchronize(ev_done_[p]));
     inflight_[p] = false;
-    if (h2d_hsa_) {   // (k_h2d_wait gives up after ~2^24 polls: the step then ran on a stale slot)
-      const int is = (int)(launch_seq_[p] % INGRESS_SLOTS);
-      if (ing_hsa_[is] && hsa_signal_load_scacquire(ing_sig_[is]) != 0) {
+    if (h2d_addr_[p]) {   // (k_h2d_wait gives up after its poll budget: the step then ran on a stale slot)
+      if (*(volatile const i64*)h2d_addr_[p] != 0) {
         wait_failed_ = true;
         throw std::runtime_error("ingress copy of step " + std::to_string(launch_seq_[p]) +
                                  " did not complete before its step ran (HSA SDMA copy lost)");
@@ -2435,6 +2442,8 @@ class Engine {
   // fault injection (tests): the next submitted step's egress gate is never opened by its
   // last kernel (it stores to a scratch word instead), as after a step that died before it
   void inject_gate_fault() { gate_fault_ = true; }
+  // (tests) the next step's ingress wait polls a word that never reaches 0 (HSA ingress only)
+  void inject_h2d_fault() { h2d_fault_ = true; }
   bool wait_failed() const { return wait_failed_; }
 
   // gated egress: bytes to copy speculatively for the next step -- the largest of the last
@@ -3001,6 +3010,9 @@ class Engine {
   hsa_signal_t ing_sig_[INGRESS_SLOTS] = {};
   bool ing_hsa_[INGRESS_SLOTS] = {};   // the slot's last payload went through HSA (ing_sig_)
   bool h2d_hip_[NPAR_MAX] = {true, true, true};   // the step's stream waits for ev_h2d_
+  u64 h2d_addr_[NPAR_MAX] = {};   // the word the step's k_h2d_wait polled (0: none)
+  bool h2d_fault_ = false;
+  void* h2d_dummy_ = nullptr;     // pinned host word of inject_h2d_fault
 
   // the agent address of a payload in page-locked host memory (hipHostMalloc /
   // hipHostRegister), 0 for pageable memory (the runtime's copy stages that)
@@ -3147,6 +3159,7 @@ PYBIND11_MODULE(_dataplane, m) {
       .def("host_times", &Engine::host_times, py::arg("reset") = false)
       .def("egress_stats", &Engine::egress_stats)
       .def("inject_gate_fault", &Engine::inject_gate_fault)
+      .def("inject_h2d_fault", &Engine::inject_h2d_fault)
       .def("wait_failed", &Engine::wait_failed)
       .def("stage_write", &Engine::stage_write_buf, py::arg("name"), py::arg("data"), py::arg("offset") = 0)
       .def("stage_mark_dirty", &Engine::stage_mark_dirty)

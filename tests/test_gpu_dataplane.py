@@ -228,3 +228,30 @@ def test_lost_egress_gate_fails_within_deadline(gpu):
     assert time.monotonic() - t0 < 5.0
     assert d.eng.wait_failed()
     del d
+
+
+def test_lost_ingress_copy_fails_loudly(gpu):
+    """An HSA ingress copy the step's k_h2d_wait never sees complete (injected: the step
+    polls a word no copy clears, with a short poll budget) fails that step's collection with
+    an engine error instead of passing a stale ingress slot off as the step's bytes; the
+    engine still tears down."""
+    from chanamq_amd.engine.dataplane import GpuDataPlane
+    from chanamq_amd.engine.traffic import publish_stream
+
+    d = GpuDataPlane(copy_engine=3, overlap=0, h2d_hsa=1, **CFG)
+    assert d.info["h2d_hsa_engine"] >= 0
+    vh = "AMQ.DEFAULT"
+    d.declare_exchange(vh, "hx", "fanout")
+    d.declare_queue(vh, "hq", capacity=4096)
+    d.bind(vh, "hq", "hx", "")
+    for c in (0, 1):
+        d.open_connection(c, vh)
+        d.open_channel(c, 1)
+    d.consume(1, 1, vh, "hq", "c", no_ack=True)
+    for k in range(4):
+        assert d.step({0: publish_stream(20, "hx", lambda i: "", 512, seed=k)}).counters["n_deliv"] == 20
+    d.eng.inject_h2d_fault()
+    with pytest.raises(RuntimeError, match="ingress copy of step"):
+        d.step({0: publish_stream(20, "hx", lambda i: "", 512, seed=99)})
+    assert d.eng.wait_failed()
+    del d
