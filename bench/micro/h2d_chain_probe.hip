@@ -150,5 +150,27 @@ int main(int argc, char** argv) {
            per3 * 1e6, n / per3 / 1e9);
     for (auto& x : sg) hsa_signal_destroy(x);
   }
+  // one payload split in halves over two engines at once (0 and 2): is the H2D bound by one
+  // engine or by the link?
+  {
+    std::vector<hsa_signal_t> sg(2 * K);
+    for (auto& x : sg) hsa_signal_create(1, 0, nullptr, &x);
+    const size_t h1 = (n / 2 + 4095) & ~size_t(4095);
+    t0 = now_s();
+    for (int k = 0; k < K; ++k)
+      for (int half = 0; half < 2; ++half) {
+        const size_t off = half ? h1 : 0, len = half ? n - h1 : h1;
+        if (hsa_amd_memory_async_copy_on_engine((char*)d[k] + off, ag.gpus[0], (char*)h + off, ag.cpus[0], len, 0,
+                                                nullptr, sg[2 * k + half],
+                                                (hsa_amd_sdma_engine_id_t)(1u << (half ? 2 : 0)), true) !=
+            HSA_STATUS_SUCCESS)
+          return 1;
+      }
+    for (auto& x : sg)
+      hsa_signal_wait_scacquire(x, HSA_SIGNAL_CONDITION_EQ, 0, UINT64_MAX, HSA_WAIT_STATE_ACTIVE);
+    const double per = (now_s() - t0) / K;
+    printf("split engines 0+2, %zu KB x %d: %.1f us per payload, %.1f GB/s\n", n >> 10, K, per * 1e6, n / per / 1e9);
+    for (auto& x : sg) hsa_signal_destroy(x);
+  }
   return 0;
 }
