@@ -38,7 +38,7 @@ CTRL_DGET = 0x40000000      # CtrlRec.seg: a Basic.Get its step decoded but coul
 # (dp_common.h EgressRef): the len body bytes at host address src go before egress byte dst
 EGRESS_REF = np.dtype([("src", "<u8"), ("dst", "<u4"), ("len", "<u4")])
 
-STRUCT_SIZES = {"SegIn": 16, "SegOut": 32, "CtrlRec": 16, "ConnOut": 8, "StepIn": 120, "RDesc": 64, "USlot": 32}
+STRUCT_SIZES = {"SegIn": 16, "SegOut": 32, "CtrlRec": 16, "ConnOut": 8, "StepIn": 128, "RDesc": 64, "USlot": 32}
 assert RDESC.itemsize == 64
 
 # SegOut.status bits

@@ -410,12 +410,14 @@ __global__ __launch_bounds__(1024) void k_apply_deltas(DS d, const u8* buf) {
 // Bounded: a copy that never completes lets the step run on and the host's check of the
 // signal at collection (Engine::wait_results) reports it
 __global__ __launch_bounds__(64) void k_h2d_wait(DS d) {
-  const u64 sig = d.in->h2d_sig;
+  const u64 sig = d.in->h2d_sig, sig2 = d.in->h2d_sig2;   // (sig2: a payload split over two engines)
   if (!sig) return;
   const u32 lim = d.in->h2d_polls ? d.in->h2d_polls : (1u << 24);
   if (threadIdx.x == 0)
     for (u32 it = 0; it < lim; ++it) {
-      if (__hip_atomic_load((const i64*)sig, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == 0) break;
+      if (__hip_atomic_load((const i64*)sig, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == 0 &&
+          (!sig2 || __hip_atomic_load((const i64*)sig2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == 0))
+        break;
       __builtin_amdgcn_s_sleep(4);
     }
   __syncthreads();

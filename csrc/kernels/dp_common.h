@@ -91,8 +91,9 @@ struct StepIn {         // host -> device per step (96 B)
   // queued it on an SDMA engine itself (0: a runtime copy the step's stream waits for):
   // k_h2d_wait holds the step's frame scan until it reads 0
   u64 h2d_sig;
+  u64 h2d_sig2;         // the second half's copy of a payload split over two engines (0: none)
 };
-static_assert(sizeof(StepIn) == 120, "StepIn layout");
+static_assert(sizeof(StepIn) == 128, "StepIn layout");
 
 
 

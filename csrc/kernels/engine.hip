@@ -206,6 +206,10 @@ class Engine {
     sdma_ = copy_mode_ == 1;
     copy_wgs_ = (u32)get("copy_wgs", 16);
     sdma_pref_ = cfg.contains("sdma_engine") ? cfg["sdma_engine"].cast<int>() : -1;
+    // (measured: no step-period gain in bench.py, 45.9 / 46.4 vs 45.9 / 46.3 M msgs/s,
+    // profiles/r6_sp/ -- the egress D2H shares the link; opt-in)
+    h2d_split_cfg_ = get("h2d_split", 0) != 0;
+    h2d_split_min_ = get("h2d_split_min", 4u << 20);   // (tests lower it: every payload splits)
     wait_ms_ = (u32)get("wait_timeout_ms", 10000);
     sdma_split_ = cfg.contains("sdma_split") ? std::max(1, std::min(2, cfg["sdma_split"].cast<int>())) : 1;
 
@@ -639,7 +643,8 @@ class Engine {
     h2d_hsa_ = copy_mode_ == 3 && !sdma_ && d_.world == 1 && get("overlap", 1) == 0 && get("h2d_hsa", 0) != 0;
     if (h2d_hsa_)
       for (int k = 0; k < INGRESS_SLOTS; ++k)
-        if (hsa_signal_create(0, 0, nullptr, &ing_sig_[k]) != HSA_STATUS_SUCCESS)
+        if (hsa_signal_create(0, 0, nullptr, &ing_sig_[k]) != HSA_STATUS_SUCCESS ||
+            hsa_signal_create(0, 0, nullptr, &ing_sig2_[k]) != HSA_STATUS_SUCCESS)
           throw std::runtime_error("hsa_signal_create failed");
     // ingress payloads share the H2D stream: a stream of their own stalled the host for ~6 ms
     // in an early prefetch on some boxes (12+ MB copies; profiles/r4_summary.md)
@@ -709,13 +714,15 @@ class Engine {
       if (ing_sig_[k].handle) {
         if (ing_hsa_[k]) (void)hsa_signal_wait_scacquire(ing_sig_[k], HSA_SIGNAL_CONDITION_EQ, 0, 2000 * block_ticks_,
                                                           HSA_WAIT_STATE_BLOCKED);
+        if (ing_split_[k]) (void)hsa_signal_wait_scacquire(ing_sig2_[k], HSA_SIGNAL_CONDITION_EQ, 0, 2000 * block_ticks_,
+                                                            HSA_WAIT_STATE_BLOCKED);
       }
     (void)hipStreamSynchronize(s_comp_);
     (void)hipStreamSynchronize(s_h2d_);
     if (s_h2d_alt_) (void)hipStreamSynchronize(s_h2d_alt_);
     (void)hipStreamSynchronize(s_pre_);
     for (int k = 0; k < INGRESS_SLOTS; ++k)
-      if (ing_sig_[k].handle) hsa_signal_destroy(ing_sig_[k]);
+      if (ing_sig_[k].handle) { hsa_signal_destroy(ing_sig_[k]); hsa_signal_destroy(ing_sig2_[k]); }
     (void)hipStreamSynchronize(s_d2h_);
     for (int p = 0; p < npar_; ++p) {
       if (graph_exec_[p]) (void)hipGraphExecDestroy(graph_exec_[p]);
@@ -860,6 +867,8 @@ class Engine {
     { u32 e = 0; while (copy_mode_ == 3 && e < 32 && !(((u32)sdma_engine_ >> e) & 1u)) ++e; o["sdma_engine"] = copy_mode_ == 3 ? (int)e : -1; }
     { u32 e = 0; while (sdma_engine2_ && e < 32 && !(((u32)sdma_engine2_ >> e) & 1u)) ++e; o["sdma_engine2"] = sdma_engine2_ ? (int)e : -1; }
     { u32 e = 0; while (h2d_hsa_ && e < 32 && !(((u32)ing_engine_ >> e) & 1u)) ++e; o["h2d_hsa_engine"] = h2d_hsa_ ? (int)e : -1; }
+    { u32 e = 0; while (h2d_hsa_ && ing_engine2_ && e < 32 && !(((u32)ing_engine2_ >> e) & 1u)) ++e;
+      o["h2d_hsa_engine2"] = h2d_hsa_ && ing_engine2_ ? (int)e : -1; }
     o["persist"] = d_.persist; o["persist_max"] = d_.persist_max; o["persist_bytes"] = d_.persist_bytes;
     o["restore_max"] = restore_max_;
     o["xfer_desc_max"] = d_.xfer_desc_max; o["xfer_bytes"] = d_.xfer_bytes; o["world_max"] = WORLD_MAX;
@@ -920,13 +929,16 @@ class Engine {
     StepIn* in = stage_in_[p];
     *in = StepIn{};
     in->h2d_sig = ing_hsa_[is] ? (u64)&((amd_signal_t*)ing_sig_[is].handle)->value : 0;
+    in->h2d_sig2 = ing_hsa_[is] && ing_split_[is] ? (u64)&((amd_signal_t*)ing_sig2_[is].handle)->value : 0;
     if (in->h2d_sig && h2d_fault_) {   // (tests) the step waits on a word no copy completes
       h2d_fault_ = false;
       *(volatile i64*)h2d_dummy_ = 1;
       in->h2d_sig = (u64)h2d_dummy_;
+      in->h2d_sig2 = 0;
       in->h2d_polls = 4096;
     }
     h2d_addr_[p] = in->h2d_sig;
+    h2d_addr2_[p] = in->h2d_sig2;
     // the step's stream waits for the H2D stream only when a runtime copy of this step is on it
     h2d_hip_[p] = !h2d_hsa_ || (payload_len && !ing_hsa_[is]) || !pend_gets_.empty();
     in->nseg = nseg;
@@ -2337,7 +2349,7 @@ class Engine {
     HIPCHECK(hipEventSynchronize(ev_done_[p]));
     inflight_[p] = false;
     if (h2d_addr_[p]) {   // (k_h2d_wait gives up after its poll budget: the step then ran on a stale slot)
-      if (*(volatile const i64*)h2d_addr_[p] != 0) {
+      if (*(volatile const i64*)h2d_addr_[p] != 0 || (h2d_addr2_[p] && *(volatile const i64*)h2d_addr2_[p] != 0)) {
         wait_failed_ = true;
         throw std::runtime_error("ingress copy of step " + std::to_string(launch_seq_[p]) +
                                  " did not complete before its step ran (HSA SDMA copy lost)");
@@ -2545,6 +2557,16 @@ class Engine {
         break;
       }
     if (!ing_engine_) ing_engine_ = tail_engine_;
+    // a split payload's second engine (cfg h2d_split, default off): another full-rate one the
+    // egress does not use
+    ing_engine2_ = (hsa_amd_sdma_engine_id_t)0;
+    if (h2d_split_cfg_)
+      for (u32 c : {3u, 2u})
+        if (((mask >> c) & 1u) && (1u << c) != (u32)ing_engine_ && (1u << c) != (u32)sdma_engine_ &&
+            (1u << c) != (u32)sdma_engine2_ && (1u << c) != (u32)tail_engine_) {
+          ing_engine2_ = (hsa_amd_sdma_engine_id_t)(1u << c);
+          break;
+        }
     for (int e = 0; e < EGRESS_SLOTS; ++e)
       if (hsa_signal_create(0, 0, nullptr, &sdma_sig_[e]) != HSA_STATUS_SUCCESS ||
           hsa_signal_create(0, 0, nullptr, &tail_sig_[e]) != HSA_STATUS_SUCCESS ||
@@ -3011,7 +3033,13 @@ class Engine {
   bool ing_hsa_[INGRESS_SLOTS] = {};   // the slot's last payload went through HSA (ing_sig_)
   bool h2d_hip_[NPAR_MAX] = {true, true, true};   // the step's stream waits for ev_h2d_
   u64 h2d_addr_[NPAR_MAX] = {};   // the word the step's k_h2d_wait polled (0: none)
+  u64 h2d_addr2_[NPAR_MAX] = {};  // (and its second half's, a split payload)
+  hsa_amd_sdma_engine_id_t ing_engine2_{};   // a split payload's second engine (0: no split)
+  hsa_signal_t ing_sig2_[INGRESS_SLOTS] = {};
+  bool ing_split_[INGRESS_SLOTS] = {};
   bool h2d_fault_ = false;
+  bool h2d_split_cfg_ = false;
+  u64 h2d_split_min_ = 4u << 20;
   void* h2d_dummy_ = nullptr;     // pinned host word of inject_h2d_fault
 
   // the agent address of a payload in page-locked host memory (hipHostMalloc /
@@ -3035,11 +3063,24 @@ class Engine {
       if (step >= INGRESS_SLOTS && ing_slot_issued_[is] && hipEventQuery(ev_ing_slot_[is]) != hipSuccess)
         HIPCHECK(hipEventSynchronize(ev_ing_slot_[is]));
       if (ing_hsa_[is]) bounded_wait(ing_sig_[is], -1, "ingress H2D");
+      if (ing_split_[is]) bounded_wait(ing_sig2_[is], -1, "ingress H2D");
+      // a large payload in two halves on two engines at once: 56.8 vs 54.9 GB/s on one (the
+      // PCIe link is the bound, bench/micro/h2d_chain_probe.hip, profiles/r6_z/h2d_chain3.txt)
+      const bool split = ing_engine2_ && len >= h2d_split_min_ && len > 8192;
+      const u64 h1 = split ? ((len / 2 + 4095) & ~u64(4095)) : len;
       hsa_signal_store_relaxed(ing_sig_[is], 1);
-      if (hsa_amd_memory_async_copy_on_engine(ingress_slot_[is], gpu_agent_, (const void*)src, cpu_agent_, len, 0,
+      if (hsa_amd_memory_async_copy_on_engine(ingress_slot_[is], gpu_agent_, (const void*)src, cpu_agent_, h1, 0,
                                               nullptr, ing_sig_[is], ing_engine_, true) != HSA_STATUS_SUCCESS)
         throw std::runtime_error("hsa_amd_memory_async_copy_on_engine (ingress) failed");
+      if (split) {
+        hsa_signal_store_relaxed(ing_sig2_[is], 1);
+        if (hsa_amd_memory_async_copy_on_engine(ingress_slot_[is] + h1, gpu_agent_, (const void*)(src + h1), cpu_agent_,
+                                                len - h1, 0, nullptr, ing_sig2_[is], ing_engine2_,
+                                                true) != HSA_STATUS_SUCCESS)
+          throw std::runtime_error("hsa_amd_memory_async_copy_on_engine (ingress, second half) failed");
+      }
       ing_hsa_[is] = true;
+      ing_split_[is] = split;
       return;
     }
     if (step >= INGRESS_SLOTS && ing_slot_issued_[is] && hipEventQuery(ev_ing_slot_[is]) != hipSuccess)
@@ -3047,6 +3088,7 @@ class Engine {
     HIPCHECK(hipMemcpyAsync((void*)ingress_slot_[is], (const void*)ptr, len,
                             sdma_ ? hipMemcpyDeviceToDeviceNoCU : hipMemcpyHostToDevice, ps));
     ing_hsa_[is] = false;
+    ing_split_[is] = false;
   }
   hipEvent_t ev_h2d_[NPAR_MAX], ev_done_[NPAR_MAX], ev_d2h_[EGRESS_SLOTS];
   bool inflight_[NPAR_MAX] = {};

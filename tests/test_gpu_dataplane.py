@@ -10,8 +10,9 @@ from gpu_cfg import CFG  # noqa: E402
 
 
 # h2d-hsa: the ingress payload copies on an SDMA engine through HSA, waited for on the
-# device by k_h2d_wait (single GPU without the overlapped ingest; bench --h2d-hsa)
-@pytest.fixture(params=[(True, 0), (False, 0), (True, 2), (True, 3), (True, 3, {"h2d_hsa": 1, "overlap": 0})],
+# device by k_h2d_wait (single GPU without the overlapped ingest; bench --h2d-hsa), every
+# payload over 8 KB split in halves over two SDMA engines (h2d_split_min lowered from 4 MB)
+@pytest.fixture(params=[(True, 0), (False, 0), (True, 2), (True, 3), (True, 3, {"h2d_hsa": 1, "overlap": 0, "h2d_split": 1, "h2d_split_min": 4096})],
                 ids=["graph", "eager", "copykernel", "hsa-sdma", "h2d-hsa"])
 def graph(request):
     return request.param
